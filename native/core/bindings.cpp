@@ -1,0 +1,253 @@
+// pybind11 bindings of the native scheduling engine (module yoda_scheduler_amd._native._yoda_core).
+#include <array>
+
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "engine.hpp"
+
+namespace py = pybind11;
+using namespace yoda;
+
+namespace {
+
+int8_t effect_of(const std::string& e) {
+  if (e == "NoSchedule") return kNoSchedule;
+  if (e == "PreferNoSchedule") return kPreferNoSchedule;
+  if (e == "NoExecute") return kNoExecute;
+  return kEffectAny;
+}
+
+int8_t selop_of(const std::string& op) {
+  if (op == "In") return kIn;
+  if (op == "NotIn") return kNotIn;
+  if (op == "Exists") return kExists;
+  if (op == "DoesNotExist") return kDoesNotExist;
+  if (op == "Gt") return kGt;
+  if (op == "Lt") return kLt;
+  throw std::invalid_argument("unknown node selector operator: " + op);
+}
+
+SelTerm make_term(Engine& e, const py::list& reqs) {
+  SelTerm t;
+  for (auto item : reqs) {
+    auto tup = item.cast<py::tuple>();   // (key, op, [values])
+    SelReq r;
+    r.key = e.intern(tup[0].cast<std::string>());
+    r.op = selop_of(tup[1].cast<std::string>());
+    r.num = 0;
+    for (auto v : tup[2].cast<py::list>()) {
+      std::string s = v.cast<std::string>();
+      r.values.push_back(e.intern(s));
+      if (r.op == kGt || r.op == kLt) r.num = std::stoll(s);
+    }
+    t.reqs.push_back(std::move(r));
+  }
+  return t;
+}
+
+py::tuple cycle_tuple(const CycleResult& r) {
+  return py::make_tuple(r.node, r.feasible, r.evaluated, r.cards, r.score, r.reason_counts, r.gang_quality);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_yoda_core, m) {
+  m.doc() = "Native placement / scheduling-cycle engine (C++17)";
+  m.attr("F_NODE_UNSCHEDULABLE") = (uint32_t)F_NODE_UNSCHEDULABLE;
+  m.attr("F_NODE_NAME") = (uint32_t)F_NODE_NAME;
+  m.attr("F_TAINT_TOLERATION") = (uint32_t)F_TAINT_TOLERATION;
+  m.attr("F_NODE_AFFINITY") = (uint32_t)F_NODE_AFFINITY;
+  m.attr("F_NODE_RESOURCES_FIT") = (uint32_t)F_NODE_RESOURCES_FIT;
+  m.attr("F_YODA") = (uint32_t)F_YODA;
+  m.attr("S_YODA") = (int)S_YODA;
+  m.attr("S_LEAST_ALLOCATED") = (int)S_LEAST_ALLOCATED;
+  m.attr("S_BALANCED_ALLOCATION") = (int)S_BALANCED_ALLOCATION;
+  m.attr("S_TAINT_TOLERATION") = (int)S_TAINT_TOLERATION;
+  m.attr("S_NODE_AFFINITY") = (int)S_NODE_AFFINITY;
+  m.attr("S_MOST_ALLOCATED") = (int)S_MOST_ALLOCATED;
+  m.attr("REASONS") = py::make_tuple("OK", "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity",
+                                     "NodeResourcesFit", "NoScv", "ScvStale", "GpuNumber", "GpuMemory",
+                                     "GpuClock", "GpuFit", "NodeGone");
+
+  py::class_<PodReq>(m, "PodReq")
+      .def_readonly("has_number", &PodReq::has_number)
+      .def_readonly("number", &PodReq::number)
+      .def_readonly("has_memory", &PodReq::has_memory)
+      .def_readonly("memory", &PodReq::memory)
+      .def_readonly("has_clock", &PodReq::has_clock)
+      .def_readonly("clock", &PodReq::clock)
+      .def_readonly("cpu_m", &PodReq::cpu_m)
+      .def_readonly("mem", &PodReq::mem);
+
+  py::class_<Engine>(m, "Engine")
+      .def(py::init<bool, int>(), py::arg("compat") = false, py::arg("threads") = 1)
+      .def_property("compat", &Engine::compat, &Engine::set_compat)
+      .def_property("filters", &Engine::filters, &Engine::set_filters)
+      .def("set_score_weight", &Engine::set_score_weight)
+      .def("score_weight", &Engine::score_weight)
+      .def("set_gang_weights",
+           [](Engine& e, int64_t link, int64_t numa, int64_t fit, int64_t occ, bool binpack, int64_t gang_score,
+              int64_t enum_limit) {
+             auto& w = e.weights();
+             w.w_link = link; w.w_numa = numa; w.w_fit = fit; w.w_occ = occ;
+             w.gpu_binpack = binpack; w.w_gang_score = gang_score; w.enum_limit = enum_limit;
+           },
+           py::arg("link") = 4, py::arg("numa") = 2, py::arg("fit") = 1, py::arg("occ") = 1,
+           py::arg("binpack") = true, py::arg("gang_score") = 3, py::arg("enum_limit") = 5000)
+      .def("set_percentage_of_nodes_to_score", &Engine::set_percentage_of_nodes_to_score)
+      .def("seed", &Engine::seed)
+      .def("intern", &Engine::intern)
+      .def("upsert_node", &Engine::upsert_node)
+      .def("node_index", &Engine::node_index)
+      .def("remove_node", &Engine::remove_node)
+      .def_property_readonly("num_nodes", &Engine::num_nodes)
+      .def_property_readonly("live_nodes", &Engine::live_nodes)
+      .def_property_readonly("cycles", &Engine::cycles)
+      .def_property_readonly("ledger_size", &Engine::ledger_size)
+      .def("node_name", [](Engine& e, int32_t i) { return e.node(i).name; })
+      .def("set_node_meta",
+           [](Engine& e, int32_t idx, bool unsched, const std::vector<std::pair<std::string, std::string>>& labels,
+              const std::vector<std::tuple<std::string, std::string, std::string>>& taints, int64_t cpu_m,
+              int64_t mem, int64_t pods) {
+             Node& n = e.node(idx);
+             n.unschedulable = unsched;
+             n.labels.clear();
+             for (auto& kv : labels) n.labels[e.intern(kv.first)] = e.intern(kv.second);
+             n.taints.clear();
+             for (auto& t : taints)
+               n.taints.push_back(Taint{e.intern(std::get<0>(t)), e.intern(std::get<1>(t)), effect_of(std::get<2>(t))});
+             n.alloc_cpu_m = cpu_m;
+             n.alloc_mem = mem;
+             n.alloc_pods = pods;
+           })
+      // cards: list of (total, free, clock, bandwidth, core, power, healthy, phys, numa, occ_q)
+      .def("set_cards",
+           [](Engine& e, int32_t idx,
+              const std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, bool, int32_t,
+                                           int32_t, int32_t>>& cs,
+              uint64_t card_number, uint64_t free_sum, uint64_t total_sum, bool stale) {
+             std::vector<Card> cards;
+             cards.reserve(cs.size());
+             for (auto& t : cs) {
+               Card c;
+               std::tie(c.total_mb, c.free_mb, c.clock, c.bandwidth, c.core, c.power, c.healthy, c.phys, c.numa,
+                        c.occ_q) = t;
+               if (c.phys < 0 || c.phys >= kMaxPhys) throw std::invalid_argument("physical id out of range");
+               cards.push_back(c);
+             }
+             e.set_cards(idx, std::move(cards), card_number, free_sum, total_sum, stale);
+           })
+      .def("clear_scv", &Engine::clear_scv)
+      .def("set_links", &Engine::set_links)
+      .def("node_cards",
+           [](Engine& e, int32_t idx) {
+             py::list out;
+             for (auto& c : e.node(idx).cards)
+               out.append(py::make_tuple(c.total_mb, c.free_mb, c.reserved_mb, c.pods, c.clock, c.healthy, c.phys));
+             return out;
+           })
+      .def("node_usage",
+           [](Engine& e, int32_t idx) {
+             const Node& n = e.node(idx);
+             return py::make_tuple(n.req_cpu_m, n.req_mem, n.pod_count, n.label_mem_sum);
+           })
+      .def("make_req",
+           [](Engine& e, bool has_number, uint64_t number, bool has_memory, uint64_t memory, bool has_clock,
+              uint64_t clock, uint64_t clock_min, int64_t priority, const std::string& node_name, int64_t cpu_m,
+              int64_t mem, const std::vector<std::pair<std::string, std::string>>& node_selector,
+              const py::list& required, const py::list& preferred, const py::list& tolerations) {
+             PodReq r;
+             r.has_number = has_number;
+             r.number = has_number ? number : 1;
+             r.has_memory = has_memory;
+             r.memory = memory;
+             r.has_clock = has_clock;
+             r.clock = clock;
+             r.clock_min = clock_min;
+             r.priority = priority;
+             r.node_name = node_name.empty() ? -1 : e.intern(node_name);
+             r.cpu_m = cpu_m;
+             r.mem = mem;
+             for (auto& kv : node_selector) r.node_selector.emplace_back(e.intern(kv.first), e.intern(kv.second));
+             for (auto t : required) r.required_terms.push_back(make_term(e, t.cast<py::list>()));
+             for (auto p : preferred) {
+               auto tup = p.cast<py::tuple>();
+               r.preferred_terms.push_back(PrefTerm{tup[0].cast<int32_t>(), make_term(e, tup[1].cast<py::list>())});
+             }
+             for (auto t : tolerations) {
+               auto tup = t.cast<py::tuple>();   // (key|None, value, op, effect)
+               Toleration x;
+               x.key = tup[0].is_none() ? -1 : e.intern(tup[0].cast<std::string>());
+               if (x.key == 0) x.key = -1;   // empty key
+               x.value = e.intern(tup[1].cast<std::string>());
+               x.op = tup[2].cast<std::string>() == "Exists" ? kTolExists : kTolEqual;
+               x.effect = effect_of(tup[3].cast<std::string>());
+               r.tolerations.push_back(x);
+             }
+             return r;
+           },
+           py::arg("has_number"), py::arg("number"), py::arg("has_memory"), py::arg("memory"), py::arg("has_clock"),
+           py::arg("clock"), py::arg("clock_min") = 0, py::arg("priority") = 0, py::arg("node_name") = "",
+           py::arg("cpu_m") = 0, py::arg("mem") = 0,
+           py::arg("node_selector") = std::vector<std::pair<std::string, std::string>>{},
+           py::arg("required") = py::list(), py::arg("preferred") = py::list(), py::arg("tolerations") = py::list())
+      .def("reserve", &Engine::reserve)
+      .def("release", &Engine::release)
+      .def("has_pod", &Engine::has_pod)
+      .def("assignment",
+           [](Engine& e, uint64_t pod) -> py::object {
+             const Assignment* a = e.assignment(pod);
+             if (!a) return py::none();
+             return py::make_tuple(a->node, a->cards, a->mb);
+           })
+      .def("filter_node",
+           [](Engine& e, const PodReq& r, int32_t idx) { return (int)e.filter_node(r, idx, nullptr, nullptr, nullptr); })
+      .def("collect_max",
+           [](Engine& e, const PodReq& r, const std::vector<int32_t>& idxs) {
+             uint64_t mx[6];
+             e.collect_max(r, idxs, mx);
+             return py::make_tuple(mx[0], mx[1], mx[2], mx[3], mx[4], mx[5]);
+           })
+      .def("yoda_raw_score",
+           [](Engine& e, const PodReq& r, int32_t idx, const std::array<uint64_t, 6>& mx) {
+             return e.yoda_raw_score(r, idx, mx.data());
+           })
+      .def_static("normalize_yoda",
+                  [](std::vector<int64_t> s) {
+                    Engine::normalize_yoda(s);
+                    return s;
+                  })
+      .def("select_gpus",
+           [](Engine& e, const PodReq& r, int32_t idx) {
+             std::vector<int32_t> out;
+             int32_t q = 0;
+             bool ok = e.select_gpus(r, idx, &out, &q);
+             return py::make_tuple(ok, out, q);
+           })
+      .def("feasible_nodes",
+           [](Engine& e, const PodReq& r, const std::vector<int32_t>& cand) {
+             std::vector<int32_t> reasons;
+             auto f = e.feasible_nodes(r, cand, &reasons);
+             return py::make_tuple(f, reasons);
+           })
+      .def("score_nodes", &Engine::score_nodes)
+      .def("schedule",
+           [](Engine& e, uint64_t pod, const PodReq& r, bool assume, const std::vector<int32_t>& cand,
+              const std::vector<int64_t>& extra) { return cycle_tuple(e.schedule(pod, r, assume, cand, extra)); },
+           py::arg("pod"), py::arg("req"), py::arg("assume") = true,
+           py::arg("candidates") = std::vector<int32_t>{}, py::arg("extra") = std::vector<int64_t>{})
+      .def("schedule_batch",
+           [](Engine& e, const std::vector<uint64_t>& pods, const std::vector<PodReq*>& reqs) {
+             if (pods.size() != reqs.size()) throw std::invalid_argument("pods/reqs length mismatch");
+             std::vector<const PodReq*> rr(reqs.begin(), reqs.end());
+             std::vector<CycleResult> res;
+             {
+               py::gil_scoped_release nogil;
+               res = e.schedule_batch(pods, rr);
+             }
+             py::list out;
+             for (auto& r : res) out.append(cycle_tuple(r));
+             return out;
+           });
+}

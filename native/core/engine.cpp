@@ -1,0 +1,767 @@
+// Native scheduling engine: see engine.hpp for the design notes.
+#include "engine.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+#include <stdexcept>
+
+namespace yoda {
+
+// ============================================================== ThreadPool
+ThreadPool::ThreadPool(int n) {
+  for (int i = 0; i < n - 1; ++i) workers_.emplace_back([this] { worker(); });
+}
+
+ThreadPool::~ThreadPool() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : workers_) t.join();
+}
+
+void ThreadPool::worker() {
+  uint64_t seen = 0;
+  for (;;) {
+    const std::function<void(int, int)>* job;
+    int n, grain;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      job = job_;
+      n = job_n_;
+      grain = job_grain_;
+      ++active_;
+    }
+    for (;;) {
+      int b = next_.fetch_add(grain);
+      if (b >= n) break;
+      (*job)(b, std::min(n, b + grain));
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (--active_ == 0) done_cv_.notify_all();
+    }
+  }
+}
+
+void ThreadPool::parallel_for(int n, int grain, const std::function<void(int, int)>& fn) {
+  if (workers_.empty() || n <= grain) {
+    fn(0, n);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    job_ = &fn;
+    job_n_ = n;
+    job_grain_ = grain;
+    next_.store(0);
+    ++gen_;
+  }
+  cv_.notify_all();
+  for (;;) {
+    int b = next_.fetch_add(grain);
+    if (b >= n) break;
+    fn(b, std::min(n, b + grain));
+  }
+  std::unique_lock<std::mutex> lk(mu_);
+  done_cv_.wait(lk, [&] { return active_ == 0 && next_.load() >= n; });
+  job_ = nullptr;
+}
+
+// ============================================================== Engine basics
+Engine::Engine(bool compat, int threads) : compat_(compat) {
+  if (threads > 1) pool_ = new ThreadPool(threads);
+  intern("");
+  unsched_key_ = intern("node.kubernetes.io/unschedulable");
+}
+
+Engine::~Engine() { delete pool_; }
+
+int32_t Engine::intern(const std::string& s) {
+  auto it = string_idx_.find(s);
+  if (it != string_idx_.end()) return it->second;
+  int32_t id = (int32_t)strings_.size();
+  strings_.push_back(s);
+  string_idx_.emplace(s, id);
+  return id;
+}
+
+int32_t Engine::upsert_node(const std::string& name) {
+  auto it = node_idx_.find(name);
+  if (it != node_idx_.end()) return it->second;
+  int32_t idx;
+  if (!free_slots_.empty()) {
+    idx = free_slots_.back();
+    free_slots_.pop_back();
+    nodes_[idx] = Node();
+  } else {
+    idx = (int32_t)nodes_.size();
+    nodes_.emplace_back();
+  }
+  nodes_[idx].name = name;
+  nodes_[idx].alive = true;
+  node_idx_[name] = idx;
+  ++live_;
+  return idx;
+}
+
+int32_t Engine::node_index(const std::string& name) const {
+  auto it = node_idx_.find(name);
+  return it == node_idx_.end() ? -1 : it->second;
+}
+
+void Engine::remove_node(int32_t idx) {
+  if (idx < 0 || idx >= (int32_t)nodes_.size() || !nodes_[idx].alive) return;
+  // drop reservations that point at this node
+  for (auto it = ledger_.begin(); it != ledger_.end();) {
+    if (it->second.node == idx) it = ledger_.erase(it);
+    else ++it;
+  }
+  node_idx_.erase(nodes_[idx].name);
+  nodes_[idx] = Node();
+  nodes_[idx].alive = false;
+  free_slots_.push_back(idx);
+  --live_;
+}
+
+void Engine::set_cards(int32_t idx, std::vector<Card> cards, uint64_t card_number, uint64_t free_sum,
+                       uint64_t total_sum, bool stale) {
+  Node& n = nodes_.at(idx);
+  // keep the ledger: reservations are per card index
+  std::vector<uint64_t> res(cards.size(), 0);
+  std::vector<int32_t> pods(cards.size(), 0);
+  for (size_t i = 0; i < cards.size() && i < n.cards.size(); ++i) {
+    res[i] = n.cards[i].reserved_mb;
+    pods[i] = n.cards[i].pods;
+  }
+  n.cards = std::move(cards);
+  for (size_t i = 0; i < n.cards.size(); ++i) {
+    n.cards[i].reserved_mb = res[i];
+    n.cards[i].pods = pods[i];
+  }
+  n.card_number = card_number;
+  n.free_sum = free_sum;
+  n.total_sum = total_sum;
+  n.has_scv = true;
+  n.stale = stale;
+  int32_t np = 0;
+  for (auto& c : n.cards) np = std::max(np, c.phys + 1);
+  if (np != n.nphys) {
+    n.nphys = np;
+    n.link_q.assign((size_t)np * np, 10000);
+  }
+}
+
+void Engine::clear_scv(int32_t idx) {
+  Node& n = nodes_.at(idx);
+  n.has_scv = false;
+  n.cards.clear();
+  n.card_number = n.free_sum = n.total_sum = 0;
+  n.nphys = 0;
+  n.link_q.clear();
+}
+
+void Engine::set_links(int32_t idx, int32_t nphys, std::vector<int32_t> q) {
+  Node& n = nodes_.at(idx);
+  if ((int64_t)q.size() != (int64_t)nphys * nphys) throw std::invalid_argument("link matrix size");
+  n.nphys = nphys;
+  n.link_q = std::move(q);
+}
+
+const Assignment* Engine::assignment(uint64_t pod) const {
+  auto it = ledger_.find(pod);
+  return it == ledger_.end() ? nullptr : &it->second;
+}
+
+// ============================================================== ledger
+bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::vector<int32_t>& cards) {
+  if (ledger_.count(pod)) return false;
+  if (idx < 0 || idx >= (int32_t)nodes_.size() || !nodes_[idx].alive) return false;
+  Node& n = nodes_[idx];
+  Assignment a;
+  a.node = idx;
+  a.mb = req.has_memory ? req.memory : 0;
+  for (int32_t c : cards) {
+    if (c < 0 || c >= (int32_t)n.cards.size()) return false;
+  }
+  a.cards = cards;
+  if (!compat_) {
+    for (int32_t c : cards) {
+      n.cards[c].reserved_mb += a.mb;
+      n.cards[c].pods += 1;
+    }
+  }
+  a.cpu_m = req.cpu_m;
+  a.mem = req.mem;
+  a.has_label_mem = req.has_memory;
+  a.label_mem = req.memory;
+  n.req_cpu_m += a.cpu_m;
+  n.req_mem += a.mem;
+  n.pod_count += 1;
+  if (a.has_label_mem) n.label_mem_sum += a.label_mem;
+  ledger_.emplace(pod, std::move(a));
+  return true;
+}
+
+bool Engine::release(uint64_t pod) {
+  auto it = ledger_.find(pod);
+  if (it == ledger_.end()) return false;
+  const Assignment& a = it->second;
+  if (a.node >= 0 && a.node < (int32_t)nodes_.size() && nodes_[a.node].alive) {
+    Node& n = nodes_[a.node];
+    if (!compat_) {
+      for (int32_t c : a.cards) {
+        if (c < (int32_t)n.cards.size()) {
+          n.cards[c].reserved_mb -= std::min(n.cards[c].reserved_mb, a.mb);
+          n.cards[c].pods = std::max(0, n.cards[c].pods - 1);
+        }
+      }
+    }
+    n.req_cpu_m -= a.cpu_m;
+    n.req_mem -= a.mem;
+    n.pod_count -= 1;
+    if (a.has_label_mem) n.label_mem_sum -= a.label_mem;
+  }
+  ledger_.erase(it);
+  return true;
+}
+
+// ============================================================== default filters
+static bool tolerates(const Toleration& t, const Taint& x) {
+  if (t.effect != kEffectAny && t.effect != x.effect) return false;
+  if (t.key >= 0 && t.key != x.key) return false;
+  if (t.key < 0 && t.op != kTolExists) return false;   // empty key requires Exists
+  if (t.op == kTolExists) return true;
+  return t.value == x.value;
+}
+
+bool Engine::taints_ok(const PodReq& req, const Node& n) const {
+  for (const Taint& x : n.taints) {
+    if (x.effect == kPreferNoSchedule) continue;
+    bool ok = false;
+    for (const Toleration& t : req.tolerations)
+      if (tolerates(t, x)) { ok = true; break; }
+    if (!ok) return false;
+  }
+  return true;
+}
+
+bool Engine::term_matches(const SelTerm& t, const Node& n) const {
+  if (t.reqs.empty()) return false;   // empty term matches no objects (upstream)
+  for (const SelReq& r : t.reqs) {
+    auto it = n.labels.find(r.key);
+    bool has = it != n.labels.end();
+    switch (r.op) {
+      case kIn:
+        if (!has || std::find(r.values.begin(), r.values.end(), it->second) == r.values.end()) return false;
+        break;
+      case kNotIn:
+        if (has && std::find(r.values.begin(), r.values.end(), it->second) != r.values.end()) return false;
+        break;
+      case kExists:
+        if (!has) return false;
+        break;
+      case kDoesNotExist:
+        if (has) return false;
+        break;
+      case kGt:
+      case kLt: {
+        if (!has) return false;
+        const std::string& s = strings_[it->second];
+        char* end = nullptr;
+        long long v = std::strtoll(s.c_str(), &end, 10);
+        if (s.empty() || *end != '\0') return false;
+        if (r.op == kGt ? !(v > r.num) : !(v < r.num)) return false;
+        break;
+      }
+    }
+  }
+  return true;
+}
+
+bool Engine::affinity_ok(const PodReq& req, const Node& n) const {
+  for (auto& kv : req.node_selector) {
+    auto it = n.labels.find(kv.first);
+    if (it == n.labels.end() || it->second != kv.second) return false;
+  }
+  if (req.required_terms.empty()) return true;
+  for (const SelTerm& t : req.required_terms)
+    if (term_matches(t, n)) return true;
+  return false;
+}
+
+// ============================================================== yoda policy
+uint64_t Engine::eff_free(const Card& c) const {
+  if (compat_) return c.free_mb;
+  uint64_t cap = c.total_mb > c.reserved_mb ? c.total_mb - c.reserved_mb : 0;
+  return std::min(c.free_mb, cap);
+}
+
+bool Engine::yoda_card_eligible(const PodReq& req, const Card& c, uint64_t m, uint64_t cl) const {
+  if (!c.healthy) return false;
+  if (eff_free(c) < m) return false;
+  if (req.has_clock && c.clock != cl) return false;
+  if (req.clock_min && c.clock < req.clock_min) return false;
+  return true;
+}
+
+Reason Engine::filter_node(const PodReq& req, int32_t idx, uint64_t* pn, uint64_t* pm, uint64_t* pc) const {
+  const Node& n = nodes_[idx];
+  if (!n.alive) return RS_DEAD;
+  if (filters_ & F_NODE_UNSCHEDULABLE) {
+    if (n.unschedulable) {
+      // tolerated only by node.kubernetes.io/unschedulable:NoSchedule
+      bool tol = false;
+      Taint t{unsched_key_, 0, kNoSchedule};
+      for (const Toleration& x : req.tolerations)
+        if (tolerates(x, t)) { tol = true; break; }
+      if (!tol) return RS_UNSCHEDULABLE;
+    }
+  }
+  if (filters_ & F_NODE_RESOURCES_FIT) {
+    if (n.pod_count + 1 > n.alloc_pods) return RS_RESOURCES;
+    if (req.cpu_m > 0 && n.alloc_cpu_m < req.cpu_m + n.req_cpu_m) return RS_RESOURCES;
+    if (req.mem > 0 && n.alloc_mem < req.mem + n.req_mem) return RS_RESOURCES;
+  }
+  if ((filters_ & F_NODE_NAME) && req.node_name > 0 && strings_[req.node_name] != n.name) return RS_NODE_NAME;
+  if ((filters_ & F_NODE_AFFINITY) && !affinity_ok(req, n)) return RS_AFFINITY;
+  if ((filters_ & F_TAINT_TOLERATION) && !taints_ok(req, n)) return RS_TAINT;
+  if (!(filters_ & F_YODA)) return RS_OK;
+  return yoda_filter(req, idx, pn, pm, pc);
+}
+
+Reason Engine::yoda_filter(const PodReq& req, int32_t idx, uint64_t* pn, uint64_t* pm, uint64_t* pc) const {
+  // (*Yoda).Filter: scheduler.go:76-93
+  const Node& n = nodes_[idx];
+  if (!n.has_scv) return RS_NO_SCV;
+  uint64_t num = req.has_number ? req.number : 1;
+  uint64_t m = req.has_memory ? req.memory : 0;
+  uint64_t cl = req.has_clock ? req.clock : 0;
+  if (pn) *pn = num;
+  if (pm) *pm = m;
+  if (pc) *pc = cl;
+  // PodFitsNumber (filter.go:11-16)
+  if (req.has_number ? !(req.number <= n.card_number) : !(n.card_number > 0)) return RS_GPU_NUMBER;
+  if (compat_) {
+    if (req.has_memory) {
+      uint64_t cnt = 0;
+      for (const Card& c : n.cards)
+        if (c.healthy && c.free_mb >= m) ++cnt;
+      if (cnt < num) return RS_GPU_MEMORY;
+    }
+    if (req.has_clock) {
+      uint64_t cnt = 0;
+      for (const Card& c : n.cards)
+        if (c.healthy && c.clock == cl) ++cnt;
+      if (cnt < num) return RS_GPU_CLOCK;
+    }
+    return RS_OK;
+  }
+  if (n.stale) return RS_STALE;
+  uint64_t cnt = 0;
+  for (const Card& c : n.cards)
+    if (yoda_card_eligible(req, c, m, cl)) ++cnt;
+  return cnt >= num ? RS_OK : RS_GPU_FIT;
+}
+
+void Engine::collect_max(const PodReq& req, const std::vector<int32_t>& idxs, uint64_t mx[6]) const {
+  // order: bandwidth, clock, core, free, power, total; all seeded 1 (collection.go:31-38)
+  for (int i = 0; i < 6; ++i) mx[i] = 1;
+  for (int32_t idx : idxs) {
+    uint64_t num, m, cl;
+    if (!nodes_[idx].alive || !nodes_[idx].has_scv) continue;
+    if (yoda_filter(req, idx, &num, &m, &cl) != RS_OK) continue;
+    for (const Card& c : nodes_[idx].cards) {
+      bool take = compat_ ? (c.free_mb >= m && c.clock >= cl) : yoda_card_eligible(req, c, m, cl);
+      if (!take) continue;
+      uint64_t f = eff_free(c);
+      mx[0] = std::max(mx[0], c.bandwidth);
+      mx[1] = std::max(mx[1], c.clock);
+      mx[2] = std::max(mx[2], c.core);
+      mx[3] = std::max(mx[3], f);
+      mx[4] = std::max(mx[4], c.power);
+      mx[5] = std::max(mx[5], c.total_mb);
+    }
+  }
+}
+
+uint64_t Engine::yoda_raw_score(const PodReq& req, int32_t idx, const uint64_t mx[6]) const {
+  const Node& n = nodes_[idx];
+  uint64_t num, m, cl;
+  uint64_t basic = 0;
+  if (yoda_filter(req, idx, &num, &m, &cl) == RS_OK) {
+    for (const Card& c : n.cards) {
+      bool take = compat_ ? (c.free_mb >= m && c.clock >= cl) : yoda_card_eligible(req, c, m, cl);
+      if (!take) continue;
+      uint64_t f = eff_free(c);
+      uint64_t bw = c.bandwidth * 100 / mx[0];
+      uint64_t clk = c.clock * 100 / (compat_ ? mx[0] : mx[1]);   // Q2: algorithm.go:60
+      uint64_t core = c.core * 100 / mx[2];
+      uint64_t pw = c.power * 100 / mx[4];
+      uint64_t fm = f * 100 / mx[3];
+      uint64_t tm = c.total_mb * 100 / mx[5];
+      basic += (bw + clk + core + pw) + fm * 2 + tm * 1;
+    }
+  }
+  uint64_t total, free, alloc;
+  if (compat_) {
+    total = n.total_sum;
+    free = n.free_sum;
+    alloc = n.label_mem_sum;
+  } else {
+    total = free = alloc = 0;
+    for (const Card& c : n.cards) {
+      total += c.total_mb;
+      free += eff_free(c);
+      alloc += c.reserved_mb;
+    }
+  }
+  uint64_t actual = total ? (free * 100 / total) * 2 : 0;                        // Q4 guard
+  uint64_t allocate = (total == 0 || total < alloc) ? 0 : (total - alloc) * 100 / total * 3;
+  uint64_t s = basic + allocate + actual;
+  if (!compat_ && req.has_number && req.number > 1 && req.number <= n.cards.size()) {
+    std::vector<int32_t> sel;
+    int32_t q = 0;
+    if (select_gpus(req, idx, &sel, &q)) s += (uint64_t)(q / 100) * (uint64_t)wt_.w_gang_score;
+  }
+  return s > (uint64_t)INT64_MAX ? 0 : s;   // filter.Uint64ToInt64 (filter.go:84)
+}
+
+void Engine::normalize_yoda(std::vector<int64_t>& s) {
+  if (s.empty()) return;
+  int64_t highest = 0, lowest = s[0];
+  for (int64_t v : s) {
+    lowest = std::min(lowest, v);
+    highest = std::max(highest, v);
+  }
+  if (highest == lowest) --lowest;
+  int64_t den = (int64_t)((uint64_t)highest - (uint64_t)lowest);
+  for (auto& v : s) {
+    int64_t num = (int64_t)(((uint64_t)v - (uint64_t)lowest) * (uint64_t)kMaxNodeScore);
+    v = num / den;
+  }
+}
+
+// ============================================================== gang selection
+int64_t Engine::gang_objective(const Node& n, const std::vector<int32_t>& set, uint64_t m,
+                               int64_t* link_bad_out) const {
+  const int64_t k = (int64_t)set.size();
+  int64_t P = k * (k - 1) / 2;
+  int64_t qsum = 0;
+  uint64_t numa_mask = 0;
+  int64_t free_after = 0, total = 0, occ = 0;
+  for (int64_t a = 0; a < k; ++a) {
+    const Card& ca = n.cards[set[a]];
+    numa_mask |= 1ull << (ca.numa & 63);
+    free_after += (int64_t)(eff_free(ca) - m);
+    total += (int64_t)ca.total_mb;
+    occ += ca.occ_q;
+    for (int64_t b = a + 1; b < k; ++b) {
+      const Card& cb = n.cards[set[b]];
+      int32_t q = 10000;
+      if (ca.phys != cb.phys && ca.phys < n.nphys && cb.phys < n.nphys)
+        q = n.link_q[(size_t)ca.phys * n.nphys + cb.phys];
+      qsum += q;
+    }
+  }
+  int64_t link_bad = P ? (P * 10000 - qsum) * 100 / P : 0;
+  int64_t d = __builtin_popcountll(numa_mask);
+  int64_t numa_bad = k > 1 ? (d - 1) * 1000000 / (k - 1) : 0;
+  int64_t leftover = total ? free_after * 1000000 / total : 0;
+  int64_t fit = wt_.gpu_binpack ? leftover : 1000000 - leftover;
+  int64_t occ_bad = k ? occ * 100 / k : 0;
+  if (link_bad_out) *link_bad_out = link_bad;
+  return wt_.w_link * link_bad + wt_.w_numa * numa_bad + wt_.w_fit * fit + wt_.w_occ * occ_bad;
+}
+
+static uint64_t n_choose_k(uint64_t n, uint64_t k, uint64_t cap) {
+  if (k > n) return 0;
+  k = std::min(k, n - k);
+  uint64_t r = 1;
+  for (uint64_t i = 1; i <= k; ++i) {
+    r = r * (n - k + i) / i;
+    if (r > cap) return cap + 1;
+  }
+  return r;
+}
+
+bool Engine::select_gpus(const PodReq& req, int32_t idx, std::vector<int32_t>* out, int32_t* quality) const {
+  const Node& n = nodes_[idx];
+  out->clear();
+  if (quality) *quality = 10000;
+  uint64_t k = req.has_number ? req.number : 1;
+  uint64_t m = req.has_memory ? req.memory : 0;
+  uint64_t cl = req.has_clock ? req.clock : 0;
+  if (k == 0) return true;
+  std::vector<int32_t> E;
+  for (int32_t i = 0; i < (int32_t)n.cards.size(); ++i) {
+    const Card& c = n.cards[i];
+    bool ok = compat_ ? (c.healthy && c.free_mb >= m && (!req.has_clock || c.clock == cl))
+                      : yoda_card_eligible(req, c, m, cl);
+    if (ok) E.push_back(i);
+  }
+  if (compat_) {
+    // the reference never assigns GPUs; report the first k candidates (informational)
+    for (uint64_t i = 0; i < k && i < E.size(); ++i) out->push_back(E[i]);
+    return out->size() == k;
+  }
+  if (E.size() < k) return false;
+  int64_t best = INT64_MAX, best_link = 0, lb = 0;
+  std::vector<int32_t> cur;
+  uint64_t total = n_choose_k(E.size(), k, (uint64_t)wt_.enum_limit);
+  if (total <= (uint64_t)wt_.enum_limit) {
+    // exhaustive lexicographic k-subset enumeration
+    std::vector<int32_t> pos(k);
+    for (uint64_t i = 0; i < k; ++i) pos[i] = (int32_t)i;
+    cur.resize(k);
+    for (;;) {
+      for (uint64_t i = 0; i < k; ++i) cur[i] = E[pos[i]];
+      int64_t obj = gang_objective(n, cur, m, &lb);
+      if (obj < best) {
+        best = obj;
+        best_link = lb;
+        *out = cur;
+      }
+      int64_t i = (int64_t)k - 1;
+      while (i >= 0 && pos[i] == (int32_t)(E.size() - k + i)) --i;
+      if (i < 0) break;
+      ++pos[i];
+      for (uint64_t j = i + 1; j < k; ++j) pos[j] = pos[j - 1] + 1;
+    }
+  } else {
+    // greedy growth: add the card that minimises the objective of the partial set
+    std::vector<char> used(n.cards.size(), 0);
+    for (uint64_t step = 0; step < k; ++step) {
+      int64_t bo = INT64_MAX;
+      int32_t bi = -1;
+      for (int32_t e : E) {
+        if (used[e]) continue;
+        cur.push_back(e);
+        int64_t obj = gang_objective(n, cur, m, &lb);
+        cur.pop_back();
+        if (obj < bo) {
+          bo = obj;
+          bi = e;
+        }
+      }
+      used[bi] = 1;
+      cur.push_back(bi);
+    }
+    std::sort(cur.begin(), cur.end());
+    best = gang_objective(n, cur, m, &best_link);
+    *out = cur;
+  }
+  if (quality) *quality = (int32_t)(10000 - best_link / 100);
+  return true;
+}
+
+// ============================================================== cycle
+int32_t Engine::num_feasible_to_find(int32_t all) const {
+  const int32_t kMin = 100;
+  if (all < kMin || pct_nodes_ >= 100) return all;
+  int32_t pct = pct_nodes_;
+  if (pct <= 0) {
+    pct = 50 - all / 125;
+    if (pct < 5) pct = 5;
+  }
+  int32_t num = (int32_t)((int64_t)all * pct / 100);
+  return num < kMin ? kMin : num;
+}
+
+std::vector<int32_t> Engine::feasible_nodes(const PodReq& req, const std::vector<int32_t>& candidates,
+                                            std::vector<int32_t>* reasons) {
+  std::vector<int32_t> all;
+  if (candidates.empty()) {
+    all.reserve(live_);
+    for (int32_t i = 0; i < (int32_t)nodes_.size(); ++i)
+      if (nodes_[i].alive) all.push_back(i);
+  } else {
+    all = candidates;
+  }
+  const int32_t N = (int32_t)all.size();
+  std::vector<int32_t> feasible;
+  if (reasons) reasons->assign(RS_NUM, 0);
+  if (N == 0) return feasible;
+  const int32_t want = num_feasible_to_find(N);
+  const int32_t start = next_start_ % N;
+  std::vector<int8_t> res;
+  int32_t processed = 0;
+  const int32_t chunk = pool_ ? std::max(256, pool_->size() * 64) : N;
+  for (int32_t base = 0; base < N && (int32_t)feasible.size() < want; base += chunk) {
+    int32_t len = std::min(chunk, N - base);
+    res.assign(len, 0);
+    auto body = [&](int b, int e) {
+      for (int j = b; j < e; ++j) {
+        int32_t idx = all[(start + base + j) % N];
+        res[j] = (int8_t)filter_node(req, idx, nullptr, nullptr, nullptr);
+      }
+    };
+    if (pool_ && len >= 512) pool_->parallel_for(len, 64, body);
+    else body(0, len);
+    for (int32_t j = 0; j < len; ++j) {
+      ++processed;
+      if (res[j] == RS_OK) {
+        feasible.push_back(all[(start + base + j) % N]);
+        if ((int32_t)feasible.size() >= want) break;
+      } else if (reasons) {
+        (*reasons)[res[j]]++;
+      }
+    }
+  }
+  next_start_ = (start + processed) % N;
+  return feasible;
+}
+
+static void default_normalize(std::vector<int64_t>& s, bool reverse) {
+  int64_t mx = 0;
+  for (int64_t v : s) mx = std::max(mx, v);
+  if (mx == 0) {
+    if (reverse)
+      for (auto& v : s) v = kMaxNodeScore;
+    return;
+  }
+  for (auto& v : s) {
+    v = kMaxNodeScore * v / mx;
+    if (reverse) v = kMaxNodeScore - v;
+  }
+}
+
+std::vector<int64_t> Engine::score_nodes(const PodReq& req, const std::vector<int32_t>& feas) {
+  const size_t F = feas.size();
+  std::vector<int64_t> total(F, 0);
+  std::vector<int64_t> s(F);
+  if (score_w_[S_YODA] && (filters_ & F_YODA)) {
+    uint64_t mx[6];
+    if (compat_) {
+      // reference: maxima over every Scv in the cluster (collection.go:39)
+      std::vector<int32_t> all;
+      for (int32_t i = 0; i < (int32_t)nodes_.size(); ++i)
+        if (nodes_[i].alive && nodes_[i].has_scv) all.push_back(i);
+      collect_max(req, all, mx);
+    } else {
+      collect_max(req, feas, mx);
+    }
+    auto body = [&](int b, int e) {
+      for (int i = b; i < e; ++i) s[i] = (int64_t)yoda_raw_score(req, feas[i], mx);
+    };
+    if (pool_ && F >= 512) pool_->parallel_for((int)F, 64, body);
+    else body(0, (int)F);
+    normalize_yoda(s);
+    for (size_t i = 0; i < F; ++i) total[i] += s[i] * score_w_[S_YODA];
+  }
+  const int64_t nz_cpu = req.cpu_m > 0 ? req.cpu_m : 100;               // upstream non-zero defaults
+  const int64_t nz_mem = req.mem > 0 ? req.mem : 200LL * 1024 * 1024;
+  if (score_w_[S_LEAST_ALLOCATED] || score_w_[S_MOST_ALLOCATED] || score_w_[S_BALANCED_ALLOCATION]) {
+    for (size_t i = 0; i < F; ++i) {
+      const Node& n = nodes_[feas[i]];
+      int64_t rc = n.req_cpu_m + nz_cpu, rm = n.req_mem + nz_mem;
+      int64_t least = 0, most = 0;
+      if (n.alloc_cpu_m > 0 && rc <= n.alloc_cpu_m) least += (n.alloc_cpu_m - rc) * 100 / n.alloc_cpu_m;
+      if (n.alloc_mem > 0 && rm <= n.alloc_mem) least += (int64_t)((__int128)(n.alloc_mem - rm) * 100 / n.alloc_mem);
+      if (n.alloc_cpu_m > 0) most += std::min<int64_t>(rc, n.alloc_cpu_m) * 100 / n.alloc_cpu_m;
+      if (n.alloc_mem > 0) most += (int64_t)((__int128)std::min<int64_t>(rm, n.alloc_mem) * 100 / n.alloc_mem);
+      total[i] += score_w_[S_LEAST_ALLOCATED] * (least / 2) + score_w_[S_MOST_ALLOCATED] * (most / 2);
+      if (score_w_[S_BALANCED_ALLOCATION]) {
+        double cf = n.alloc_cpu_m > 0 ? (double)rc / (double)n.alloc_cpu_m : 1.0;
+        double mf = n.alloc_mem > 0 ? (double)rm / (double)n.alloc_mem : 1.0;
+        int64_t b = (cf >= 1 || mf >= 1) ? 0 : (int64_t)((1.0 - std::abs(cf - mf)) * 100);
+        total[i] += score_w_[S_BALANCED_ALLOCATION] * b;
+      }
+    }
+  }
+  if (score_w_[S_TAINT_TOLERATION]) {
+    for (size_t i = 0; i < F; ++i) {
+      int64_t cnt = 0;
+      for (const Taint& x : nodes_[feas[i]].taints) {
+        if (x.effect != kPreferNoSchedule) continue;
+        bool ok = false;
+        for (const Toleration& t : req.tolerations)
+          if ((t.effect == kEffectAny || t.effect == kPreferNoSchedule) && tolerates(t, x)) { ok = true; break; }
+        if (!ok) ++cnt;
+      }
+      s[i] = cnt;
+    }
+    default_normalize(s, true);
+    for (size_t i = 0; i < F; ++i) total[i] += s[i] * score_w_[S_TAINT_TOLERATION];
+  }
+  if (score_w_[S_NODE_AFFINITY] && !req.preferred_terms.empty()) {
+    for (size_t i = 0; i < F; ++i) {
+      int64_t w = 0;
+      for (const PrefTerm& p : req.preferred_terms)
+        if (term_matches(p.term, nodes_[feas[i]])) w += p.weight;
+      s[i] = w;
+    }
+    default_normalize(s, false);
+    for (size_t i = 0; i < F; ++i) total[i] += s[i] * score_w_[S_NODE_AFFINITY];
+  }
+  return total;
+}
+
+CycleResult Engine::schedule(uint64_t pod, const PodReq& req, bool assume, const std::vector<int32_t>& candidates,
+                             const std::vector<int64_t>& extra) {
+  ++cycles_;
+  CycleResult r;
+  std::vector<int32_t> feas = feasible_nodes(req, candidates, &r.reason_counts);
+  r.feasible = (int32_t)feas.size();
+  r.evaluated = candidates.empty() ? live_ : (int32_t)candidates.size();
+  if (feas.empty()) return r;
+  int32_t chosen;
+  if (feas.size() == 1) {
+    chosen = feas[0];   // upstream: exactly one feasible node → no scoring
+  } else {
+    std::vector<int64_t> sc = score_nodes(req, feas);
+    if (!extra.empty()) {
+      std::unordered_map<int32_t, int64_t> ex;
+      for (size_t i = 0; i < candidates.size() && i < extra.size(); ++i) ex[candidates[i]] = extra[i];
+      for (size_t i = 0; i < feas.size(); ++i) {
+        auto it = ex.find(feas[i]);
+        if (it != ex.end()) sc[i] += it->second;
+      }
+    }
+    // selectHost: max score, reservoir-sampled tie break
+    int64_t best = sc[0];
+    chosen = feas[0];
+    uint64_t cnt = 1;
+    for (size_t i = 1; i < feas.size(); ++i) {
+      if (sc[i] > best) {
+        best = sc[i];
+        chosen = feas[i];
+        cnt = 1;
+      } else if (sc[i] == best) {
+        ++cnt;
+        if (rng_() % cnt == 0) chosen = feas[i];
+      }
+    }
+    r.score = best;
+  }
+  r.node = chosen;
+  if (filters_ & F_YODA) {
+    int32_t q = 10000;
+    if (!select_gpus(req, chosen, &r.cards, &q) && !compat_) {
+      // cannot happen in fixed mode (filter guarantees eligibility); be defensive
+      r.node = -1;
+      r.reason_counts.assign(RS_NUM, 0);
+      r.reason_counts[RS_GPU_FIT] = 1;
+      return r;
+    }
+    r.gang_quality = q;
+  }
+  if (assume) reserve(pod, req, chosen, r.cards);
+  return r;
+}
+
+std::vector<CycleResult> Engine::schedule_batch(const std::vector<uint64_t>& pods,
+                                                const std::vector<const PodReq*>& reqs) {
+  std::vector<CycleResult> out;
+  out.reserve(pods.size());
+  static const std::vector<int32_t> none;
+  static const std::vector<int64_t> nox;
+  for (size_t i = 0; i < pods.size(); ++i) out.push_back(schedule(pods[i], *reqs[i], true, none, nox));
+  return out;
+}
+
+}  // namespace yoda

@@ -1,0 +1,254 @@
+// Native placement + scheduling-cycle engine for the yoda scheduler.
+//
+// Holds the cluster as struct-of-arrays-ish node records (k8s node facts + sniffed
+// MI355X cards + the scheduler's per-GPU HBM reservation ledger) and runs the whole
+// hot loop of a scheduling cycle natively: Filter (yoda + the upstream default
+// filters that matter for GPU pods) → PreScore (cluster maxima, SURVEY Q1 fix) →
+// Score (yoda formula, compat or fixed) → NormalizeScore → weighted sum →
+// selectHost → Reserve (k-subset xGMI-aware gang selection on the chosen node).
+//
+// Reference parity: pkg/yoda/filter/filter.go:11-58, pkg/yoda/score/algorithm.go:28-87,
+// pkg/yoda/collection/collection.go:30-78, pkg/yoda/scheduler.go:76-157 (see
+// yoda_scheduler_amd/plugins/yoda_policy.py for the executable Python spec).
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace yoda {
+
+constexpr int64_t kMaxNodeScore = 100;
+constexpr int kMaxPhys = 64;
+
+enum TaintEffect : int8_t { kNoSchedule = 0, kPreferNoSchedule = 1, kNoExecute = 2, kEffectAny = 3 };
+enum TolOp : int8_t { kTolEqual = 0, kTolExists = 1 };
+enum SelOp : int8_t { kIn = 0, kNotIn = 1, kExists = 2, kDoesNotExist = 3, kGt = 4, kLt = 5 };
+
+// Plugin bits for the native filter / score sets.
+enum FilterBit : uint32_t {
+  F_NODE_UNSCHEDULABLE = 1u << 0,
+  F_NODE_NAME = 1u << 1,
+  F_TAINT_TOLERATION = 1u << 2,
+  F_NODE_AFFINITY = 1u << 3,
+  F_NODE_RESOURCES_FIT = 1u << 4,
+  F_YODA = 1u << 5,
+};
+enum ScoreIdx : int {
+  S_YODA = 0,
+  S_LEAST_ALLOCATED = 1,
+  S_BALANCED_ALLOCATION = 2,
+  S_TAINT_TOLERATION = 3,
+  S_NODE_AFFINITY = 4,
+  S_MOST_ALLOCATED = 5,
+  S_NUM = 6,
+};
+
+// Why a node was rejected (first failing plugin), reported for FitError diagnosis.
+enum Reason : int8_t {
+  RS_OK = 0, RS_UNSCHEDULABLE, RS_NODE_NAME, RS_TAINT, RS_AFFINITY, RS_RESOURCES, RS_NO_SCV,
+  RS_STALE, RS_GPU_NUMBER, RS_GPU_MEMORY, RS_GPU_CLOCK, RS_GPU_FIT, RS_DEAD, RS_NUM
+};
+
+struct Card {
+  uint64_t total_mb = 0, free_mb = 0;
+  uint64_t clock = 0, bandwidth = 0, core = 0, power = 0;
+  bool healthy = true;
+  int32_t phys = 0;
+  int32_t numa = 0;
+  int32_t occ_q = 0;          // CU occupancy in 1e-4 units (0..10000)
+  uint64_t reserved_mb = 0;   // ledger: HBM reserved by assumed/bound pods
+  int32_t pods = 0;           // pods holding a reservation on this card
+};
+
+struct Taint { int32_t key, value; int8_t effect; };
+struct Toleration { int32_t key; int32_t value; int8_t op; int8_t effect; };  // key -1 = any
+struct SelReq { int32_t key; int8_t op; std::vector<int32_t> values; int64_t num; };
+struct SelTerm { std::vector<SelReq> reqs; };
+struct PrefTerm { int32_t weight; SelTerm term; };
+
+struct Node {
+  std::string name;
+  bool alive = true;
+  bool unschedulable = false;
+  bool has_scv = false;
+  bool stale = false;
+  std::vector<Card> cards;
+  uint64_t card_number = 0, free_sum = 0, total_sum = 0;   // Scv.Status (sniffed)
+  int32_t nphys = 0;
+  std::vector<int32_t> link_q;        // nphys*nphys pair quality, 10000 = idle healthy link
+  std::unordered_map<int32_t, int32_t> labels;   // interned key → interned value
+  std::vector<Taint> taints;
+  int64_t alloc_cpu_m = 0, alloc_mem = 0, alloc_pods = 0;
+  int64_t req_cpu_m = 0, req_mem = 0, pod_count = 0;
+  uint64_t label_mem_sum = 0;         // Σ scv/memory labels of pods on node (compat Allocate)
+};
+
+struct PodReq {
+  // scv labels (Go semantics already applied by the caller's parser)
+  bool has_number = false, has_memory = false, has_clock = false;
+  uint64_t number = 1, memory = 0, clock = 0, clock_min = 0;
+  int64_t priority = 0;
+  // k8s spec
+  int32_t node_name = -1;                // interned spec.nodeName, -1 = none
+  int64_t cpu_m = 0, mem = 0;
+  std::vector<std::pair<int32_t, int32_t>> node_selector;
+  std::vector<SelTerm> required_terms;   // ORed
+  std::vector<PrefTerm> preferred_terms;
+  std::vector<Toleration> tolerations;
+};
+
+struct Weights {
+  // gang / GPU-level selection objective (lower is better), see gang_objective()
+  int64_t w_link = 4, w_numa = 2, w_fit = 1, w_occ = 1;
+  bool gpu_binpack = true;      // best-fit within node (keeps whole GPUs free for gangs)
+  int64_t w_gang_score = 3;     // node score bonus × xGMI quality for multi-GPU pods (fixed mode)
+  int64_t enum_limit = 5000;    // exhaustive k-subset search up to this many subsets
+};
+
+struct Assignment {
+  int32_t node = -1;
+  std::vector<int32_t> cards;
+  uint64_t mb = 0;              // per card
+  int64_t cpu_m = 0, mem = 0;
+  uint64_t label_mem = 0;
+  bool has_label_mem = false;
+};
+
+struct CycleResult {
+  int32_t node = -1;                 // selected node, -1 = unschedulable
+  int32_t feasible = 0;
+  int32_t evaluated = 0;
+  std::vector<int32_t> cards;        // GPU assignment on the selected node
+  int64_t score = 0;
+  std::vector<int32_t> reason_counts;  // RS_NUM histogram over rejected nodes
+  int32_t gang_quality = 0;          // 0..10000
+};
+
+class ThreadPool {
+ public:
+  explicit ThreadPool(int n);
+  ~ThreadPool();
+  // Runs fn(begin, end) over [0, n) in chunks across workers (+ the caller).
+  void parallel_for(int n, int grain, const std::function<void(int, int)>& fn);
+  int size() const { return (int)workers_.size() + 1; }
+
+ private:
+  void worker();
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int, int)>* job_ = nullptr;
+  int job_n_ = 0, job_grain_ = 1;
+  std::atomic<int> next_{0};
+  int active_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+class Engine {
+ public:
+  Engine(bool compat, int threads);
+  ~Engine();
+
+  // ---- configuration
+  bool compat() const { return compat_; }
+  void set_compat(bool c) { compat_ = c; }
+  void set_filters(uint32_t mask) { filters_ = mask; }
+  uint32_t filters() const { return filters_; }
+  void set_score_weight(int idx, int64_t w) { score_w_[idx] = w; }
+  int64_t score_weight(int idx) const { return score_w_[idx]; }
+  Weights& weights() { return wt_; }
+  void set_percentage_of_nodes_to_score(int p) { pct_nodes_ = p; }
+  void seed(uint64_t s) { rng_.seed(s); }
+  int32_t intern(const std::string& s);
+  const std::string& str(int32_t id) const { return strings_[id]; }
+
+  // ---- cluster state
+  int32_t upsert_node(const std::string& name);      // returns index (stable)
+  int32_t node_index(const std::string& name) const;
+  void remove_node(int32_t idx);
+  Node& node(int32_t idx) { return nodes_[idx]; }
+  const Node& node(int32_t idx) const { return nodes_[idx]; }
+  int32_t num_nodes() const { return (int32_t)nodes_.size(); }
+  int32_t live_nodes() const { return live_; }
+  void set_cards(int32_t idx, std::vector<Card> cards, uint64_t card_number, uint64_t free_sum,
+                 uint64_t total_sum, bool stale);
+  void clear_scv(int32_t idx);
+  void set_links(int32_t idx, int32_t nphys, std::vector<int32_t> q);
+
+  // ---- ledger
+  bool reserve(uint64_t pod, const PodReq& req, int32_t node, const std::vector<int32_t>& cards);
+  bool release(uint64_t pod);
+  bool has_pod(uint64_t pod) const { return ledger_.count(pod) != 0; }
+  const Assignment* assignment(uint64_t pod) const;
+  size_t ledger_size() const { return ledger_.size(); }
+
+  // ---- policy pieces (exposed for parity tests and for the Python runner)
+  Reason filter_node(const PodReq& req, int32_t idx, uint64_t* n, uint64_t* m, uint64_t* c) const;
+  Reason yoda_filter(const PodReq& req, int32_t idx, uint64_t* n, uint64_t* m, uint64_t* c) const;
+  void collect_max(const PodReq& req, const std::vector<int32_t>& nodes, uint64_t mx[6]) const;
+  uint64_t yoda_raw_score(const PodReq& req, int32_t idx, const uint64_t mx[6]) const;
+  static void normalize_yoda(std::vector<int64_t>& s);
+  // GPU set on node (empty + false if none)
+  bool select_gpus(const PodReq& req, int32_t idx, std::vector<int32_t>* out, int32_t* quality) const;
+
+  // ---- full native cycle
+  // candidates: node indices to consider (empty = all). Python filter/score plugins can
+  // pre-restrict candidates and add extra per-node scores (extra_scores aligned with
+  // candidates, already weighted), so the native fast path and the hybrid runner share
+  // one implementation.
+  CycleResult schedule(uint64_t pod, const PodReq& req, bool assume,
+                       const std::vector<int32_t>& candidates,
+                       const std::vector<int64_t>& extra_scores);
+
+  // Batch: schedule pods in order, each seeing the previous ones' reservations.
+  std::vector<CycleResult> schedule_batch(const std::vector<uint64_t>& pods,
+                                          const std::vector<const PodReq*>& reqs);
+
+  // Filter only → feasible node indices (for the hybrid runner)
+  std::vector<int32_t> feasible_nodes(const PodReq& req, const std::vector<int32_t>& candidates,
+                                      std::vector<int32_t>* reasons);
+  // Native weighted score of the given feasible nodes (normalized per plugin, summed).
+  std::vector<int64_t> score_nodes(const PodReq& req, const std::vector<int32_t>& feasible);
+
+  uint64_t cycles() const { return cycles_; }
+
+ private:
+  bool taints_ok(const PodReq& req, const Node& n) const;
+  bool affinity_ok(const PodReq& req, const Node& n) const;
+  bool term_matches(const SelTerm& t, const Node& n) const;
+  bool yoda_card_eligible(const PodReq& req, const Card& c, uint64_t m, uint64_t cl) const;
+  uint64_t eff_free(const Card& c) const;
+  int64_t gang_objective(const Node& n, const std::vector<int32_t>& set, uint64_t m,
+                         int64_t* link_bad) const;
+  int32_t num_feasible_to_find(int32_t all) const;
+
+  bool compat_;
+  uint32_t filters_ = F_NODE_UNSCHEDULABLE | F_NODE_NAME | F_TAINT_TOLERATION | F_NODE_AFFINITY |
+                      F_NODE_RESOURCES_FIT | F_YODA;
+  int64_t score_w_[S_NUM] = {300, 1, 1, 1, 1, 0};
+  Weights wt_;
+  int pct_nodes_ = 0;
+  int32_t unsched_key_ = 0;
+  std::vector<Node> nodes_;
+  std::vector<int32_t> free_slots_;
+  int32_t live_ = 0;
+  std::unordered_map<std::string, int32_t> node_idx_;
+  std::vector<std::string> strings_;
+  std::unordered_map<std::string, int32_t> string_idx_;
+  std::unordered_map<uint64_t, Assignment> ledger_;
+  std::mt19937_64 rng_{0x59d4};
+  int32_t next_start_ = 0;
+  uint64_t cycles_ = 0;
+  ThreadPool* pool_ = nullptr;
+};
+
+}  // namespace yoda

@@ -1,0 +1,217 @@
+"""Scheduler cache: nodes, Scv telemetry, bound + assumed pods — backed by the native
+engine's node table and per-GPU HBM reservation ledger.
+
+Upstream semantics kept: a selected pod is *assumed* into the cache
+before its asynchronous bind, so the very next cycle already sees it (the reference's
+Allocate score depends on this, ``pkg/yoda/score/algorithm.go:74-80``); an assumed pod
+is confirmed when the informer reports it bound, forgotten on bind failure, and
+expires if the confirmation never arrives.
+
+MI355X additions: assumed/bound pods reserve ``scv/memory`` MB on each assigned GPU
+(quirk Q10 fixed), the assignment travels as the ``scv.amd.com/gpus`` annotation and
+is rebuilt from it on restart (SURVEY §5 checkpoint/resume), and an ``Scv`` whose
+sample is older than ``staleFactor × updateInterval`` makes its node unschedulable for
+GPU pods.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+from typing import Callable, Optional
+
+from ..models.labels import ANNOTATION_GPUS
+from ..models.pod import NodeInfo, PodInfo
+from ..models.scv import Scv
+from ..ops.native import pod_req, push_node, push_scv
+
+
+@dataclass
+class PodState:
+    info: PodInfo
+    node: str
+    cards: list[int]
+    assumed: bool
+    deadline: Optional[float] = None      # assumed + binding finished → expiry
+
+
+class SchedulerCache:
+    def __init__(self, engine, compat: bool = False, stale_factor: float = 3.0,
+                 assume_ttl: float = 30.0, clock: Callable[[], float] = time.monotonic,
+                 wall: Callable[[], float] = time.time) -> None:
+        self.engine = engine
+        self.compat = compat
+        self.stale_factor = stale_factor
+        self.assume_ttl = assume_ttl
+        self.clock = clock
+        self.wall = wall
+        self.nodes: dict[str, NodeInfo] = {}
+        self.scvs: dict[str, Scv] = {}
+        self._stale: dict[str, bool] = {}
+        self.pods: dict[str, PodState] = {}
+        self.node_pods: dict[str, set[str]] = {}
+        self.generation = 0
+
+    # ------------------------------------------------------------------ nodes
+    def add_node(self, obj: dict) -> None:
+        info = NodeInfo.from_obj(obj)
+        self.nodes[info.name] = info
+        idx = push_node(self.engine, info)
+        self.node_pods.setdefault(info.name, set())
+        scv = self.scvs.get(info.name)
+        if scv is not None:
+            push_scv(self.engine, idx, scv, self.compat, self._stale.get(info.name, False))
+        self.generation += 1
+
+    update_node = add_node
+
+    def remove_node(self, name: str) -> None:
+        self.nodes.pop(name, None)
+        idx = self.engine.node_index(name)
+        if idx >= 0:
+            self.engine.remove_node(idx)
+        for uid in list(self.node_pods.pop(name, ())):
+            self.pods.pop(uid, None)
+        self.generation += 1
+
+    # ------------------------------------------------------------------ telemetry
+    def set_scv(self, scv: Scv) -> None:
+        self.scvs[scv.name] = scv
+        stale = (not self.compat) and scv.is_stale(self.wall(), self.stale_factor)
+        self._stale[scv.name] = stale
+        idx = self.engine.node_index(scv.name)
+        if idx >= 0:
+            push_scv(self.engine, idx, scv, self.compat, stale)
+        self.generation += 1
+
+    def add_scv(self, obj: dict) -> None:
+        self.set_scv(Scv.from_json(obj))
+
+    update_scv = add_scv
+
+    def remove_scv(self, name: str) -> None:
+        self.scvs.pop(name, None)
+        self._stale.pop(name, None)
+        idx = self.engine.node_index(name)
+        if idx >= 0:
+            self.engine.clear_scv(idx)
+        self.generation += 1
+
+    def refresh_staleness(self) -> list[str]:
+        """Re-evaluate sample freshness; returns nodes whose state flipped."""
+        if self.compat:
+            return []
+        now, flipped = self.wall(), []
+        for name, scv in self.scvs.items():
+            st = scv.is_stale(now, self.stale_factor)
+            if st != self._stale.get(name):
+                self._stale[name] = st
+                idx = self.engine.node_index(name)
+                if idx >= 0:
+                    push_scv(self.engine, idx, scv, self.compat, st)
+                flipped.append(name)
+        return flipped
+
+    # ------------------------------------------------------------------ pods
+    def _track(self, ps: PodState) -> None:
+        self.pods[ps.info.uid] = ps
+        self.node_pods.setdefault(ps.node, set()).add(ps.info.uid)
+
+    def assumed(self, pi: PodInfo, node: str, cards: list[int]) -> None:
+        """Record a pod the engine reserved during ``schedule(assume=True)``."""
+        self._track(PodState(pi, node, list(cards), True))
+
+    def assume(self, pi: PodInfo, node: str, cards: list[int]) -> bool:
+        idx = self.engine.node_index(node)
+        if idx < 0 or not self.engine.reserve(pi.num_id, pod_req(self.engine, pi), idx, list(cards)):
+            return False
+        self.assumed(pi, node, cards)
+        return True
+
+    def finish_binding(self, pi: PodInfo) -> None:
+        ps = self.pods.get(pi.uid)
+        if ps is not None and ps.assumed:
+            ps.deadline = self.clock() + self.assume_ttl
+
+    def forget(self, pi: PodInfo) -> None:
+        ps = self.pods.pop(pi.uid, None)
+        if ps is not None:
+            self.node_pods.get(ps.node, set()).discard(pi.uid)
+        self.engine.release(pi.num_id)
+
+    def add_pod(self, obj: dict) -> None:
+        """A bound pod observed by the informer (confirms an assumed pod)."""
+        meta = obj.get("metadata") or {}
+        ps = self.pods.get(meta.get("uid"))
+        if ps is not None and ps.assumed and ps.node == (obj.get("spec") or {}).get("nodeName"):
+            ps.assumed, ps.deadline = False, None      # fast confirm: no re-parse
+            ps.info.obj = obj
+            return
+        pi = PodInfo.from_obj(obj)
+        node = pi.node_name
+        ps = self.pods.get(pi.uid)
+        if ps is not None:
+            if ps.assumed and ps.node == node:
+                ps.assumed, ps.deadline = False, None
+                ps.info = pi
+                return
+            self.forget(ps.info)
+        idx = self.engine.node_index(node)
+        cards = parse_gpu_annotation(pi.annotations.get(ANNOTATION_GPUS))
+        if idx >= 0:
+            req = pod_req(self.engine, pi)
+            if cards is None:
+                ok, sel, _ = self.engine.select_gpus(req, idx)
+                cards = sel if ok else []
+            if not self.engine.reserve(pi.num_id, req, idx, cards):
+                self.engine.reserve(pi.num_id, req, idx, [])
+        self._track(PodState(pi, node, cards or [], False))
+
+    def update_pod(self, obj: dict) -> None:
+        pi = PodInfo.from_obj(obj)
+        ps = self.pods.get(pi.uid)
+        if ps is None or ps.node != pi.node_name:
+            self.add_pod(obj)
+        else:
+            ps.info = pi
+
+    def remove_pod(self, uid: str) -> None:
+        ps = self.pods.pop(uid, None)
+        if ps is not None:
+            self.node_pods.get(ps.node, set()).discard(uid)
+            self.engine.release(ps.info.num_id)
+
+    def cleanup_expired(self) -> list[PodInfo]:
+        now, out = self.clock(), []
+        for uid, ps in list(self.pods.items()):
+            if ps.assumed and ps.deadline is not None and now > ps.deadline:
+                self.forget(ps.info)
+                out.append(ps.info)
+        return out
+
+    def is_assumed(self, uid: str) -> bool:
+        ps = self.pods.get(uid)
+        return ps is not None and ps.assumed
+
+    # ------------------------------------------------------------------ views
+    def node_gpu_state(self, name: str) -> list[dict]:
+        idx = self.engine.node_index(name)
+        if idx < 0:
+            return []
+        return [{"total": t, "free": f, "reserved": r, "pods": p, "clock": c, "healthy": h, "phys": ph}
+                for (t, f, r, p, c, h, ph) in self.engine.node_cards(idx)]
+
+    def snapshot_counts(self) -> dict:
+        return {"nodes": len(self.nodes), "scvs": len(self.scvs), "pods": len(self.pods),
+                "assumed": sum(1 for p in self.pods.values() if p.assumed)}
+
+
+def parse_gpu_annotation(v: Optional[str]) -> Optional[list[int]]:
+    if v is None:
+        return None
+    v = v.strip()
+    if not v:
+        return []
+    try:
+        return [int(x) for x in v.split(",") if x.strip()]
+    except ValueError:
+        return None

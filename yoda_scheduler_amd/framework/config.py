@@ -1,0 +1,255 @@
+"""``KubeSchedulerConfiguration`` loader (v1beta1 as shipped by the reference, plus
+v1beta2/v1beta3/v1), with upstream default-plugin merging.
+
+The reference ships a v1beta1 config enabling ``yoda`` at filter (weight 0) and score
+(weight 300) under ``schedulerName: yoda-scheduler2``, with leader election on lease
+``kube-system/yoda-scheduler`` 15s/10s/2s, ``percentageOfNodesToScore: 0`` and pod
+backoff 1s→10s (``deploy/yoda-scheduler.yaml:8-31``). Profiles only list yoda, so the
+upstream defaults stay enabled; ``merge_plugins`` reproduces that.
+"""
+from __future__ import annotations
+
+import copy
+import re
+from dataclasses import dataclass, field
+from typing import Any, Optional
+
+import yaml
+
+from .interfaces import EXTENSION_POINTS
+
+SUPPORTED_API_VERSIONS = (
+    "kubescheduler.config.k8s.io/v1beta1",
+    "kubescheduler.config.k8s.io/v1beta2",
+    "kubescheduler.config.k8s.io/v1beta3",
+    "kubescheduler.config.k8s.io/v1",
+)
+
+
+@dataclass
+class PluginRef:
+    name: str
+    weight: int = 0
+
+
+# kube-scheduler v1.20 (v1beta1) default plugin set, in upstream order.
+DEFAULT_PLUGINS: dict[str, list[PluginRef]] = {
+    "queueSort": [PluginRef("PrioritySort")],
+    "preFilter": [PluginRef("NodeResourcesFit"), PluginRef("NodePorts"), PluginRef("PodTopologySpread"),
+                  PluginRef("InterPodAffinity"), PluginRef("VolumeBinding")],
+    "filter": [PluginRef("NodeUnschedulable"), PluginRef("NodeResourcesFit"), PluginRef("NodeName"),
+               PluginRef("NodePorts"), PluginRef("NodeAffinity"), PluginRef("VolumeRestrictions"),
+               PluginRef("TaintToleration"), PluginRef("EBSLimits"), PluginRef("GCEPDLimits"),
+               PluginRef("NodeVolumeLimits"), PluginRef("AzureDiskLimits"), PluginRef("VolumeBinding"),
+               PluginRef("VolumeZone"), PluginRef("PodTopologySpread"), PluginRef("InterPodAffinity")],
+    "postFilter": [PluginRef("DefaultPreemption")],
+    "preScore": [PluginRef("InterPodAffinity"), PluginRef("PodTopologySpread"), PluginRef("TaintToleration")],
+    "score": [PluginRef("NodeResourcesBalancedAllocation", 1), PluginRef("ImageLocality", 1),
+              PluginRef("InterPodAffinity", 1), PluginRef("NodeResourcesLeastAllocated", 1),
+              PluginRef("NodeAffinity", 1), PluginRef("NodePreferAvoidPods", 10000),
+              PluginRef("PodTopologySpread", 2), PluginRef("TaintToleration", 1)],
+    "reserve": [PluginRef("VolumeBinding")],
+    "permit": [],
+    "preBind": [PluginRef("VolumeBinding")],
+    "bind": [PluginRef("DefaultBinder")],
+    "postBind": [],
+}
+
+
+@dataclass
+class LeaderElectionConfig:
+    leader_elect: bool = True
+    lease_duration: float = 15.0
+    renew_deadline: float = 10.0
+    retry_period: float = 2.0
+    resource_lock: str = "leases"
+    resource_name: str = "kube-scheduler"
+    resource_namespace: str = "kube-system"
+
+
+@dataclass
+class ClientConnection:
+    kubeconfig: str = ""
+    qps: float = 50.0
+    burst: int = 100
+    content_type: str = "application/json"
+
+
+@dataclass
+class Profile:
+    scheduler_name: str = "default-scheduler"
+    plugins: dict[str, list[PluginRef]] = field(default_factory=dict)
+    plugin_config: dict[str, dict] = field(default_factory=dict)
+
+
+@dataclass
+class SchedulerConfig:
+    api_version: str = SUPPORTED_API_VERSIONS[0]
+    leader_election: LeaderElectionConfig = field(default_factory=LeaderElectionConfig)
+    client_connection: ClientConnection = field(default_factory=ClientConnection)
+    percentage_of_nodes_to_score: int = 0
+    pod_initial_backoff_seconds: float = 1.0
+    pod_max_backoff_seconds: float = 10.0
+    parallelism: int = 16
+    health_bind_address: str = "0.0.0.0:10251"
+    metrics_bind_address: str = "0.0.0.0:10251"
+    enable_profiling: bool = True
+    profiles: list[Profile] = field(default_factory=list)
+    # yoda-mi355x extensions (top-level key ``yodaRuntime``): binding pipeline + batching
+    bind_concurrency: int = 256
+    batch_size: int = 256
+    unschedulable_flush_seconds: float = 60.0
+
+    def profile(self, name: str) -> Optional[Profile]:
+        for p in self.profiles:
+            if p.scheduler_name == name:
+                return p
+        return None
+
+
+_DUR = re.compile(r"(\d+(?:\.\d+)?)(ns|us|µs|ms|s|m|h)")
+_UNIT = {"ns": 1e-9, "us": 1e-6, "µs": 1e-6, "ms": 1e-3, "s": 1.0, "m": 60.0, "h": 3600.0}
+
+
+def parse_duration(v: Any) -> float:
+    """Go ``time.Duration`` string ("15s", "1m30s", "100ms") or a number of seconds."""
+    if v is None:
+        return 0.0
+    if isinstance(v, (int, float)):
+        return float(v)
+    s = str(v).strip()
+    if not s:
+        return 0.0
+    total, pos = 0.0, 0
+    for m in _DUR.finditer(s):
+        if m.start() != pos:
+            raise ValueError(f"invalid duration {v!r}")
+        total += float(m.group(1)) * _UNIT[m.group(2)]
+        pos = m.end()
+    if pos != len(s):
+        raise ValueError(f"invalid duration {v!r}")
+    return total
+
+
+def _plugin_set(d: Optional[dict]) -> tuple[list[PluginRef], list[str]]:
+    d = d or {}
+    enabled = [PluginRef(p["name"], int(p.get("weight", 0) or 0)) for p in d.get("enabled") or []]
+    disabled = [p["name"] for p in d.get("disabled") or []]
+    return enabled, disabled
+
+
+def merge_plugins(custom: dict[str, Any] | None) -> dict[str, list[PluginRef]]:
+    """Upstream ``mergePlugins``: defaults minus ``disabled`` (``*`` = all); enabled
+    plugins that are also defaults override the default in place; the rest append."""
+    custom = custom or {}
+    out: dict[str, list[PluginRef]] = {}
+    for point in EXTENSION_POINTS:
+        enabled, disabled = _plugin_set(custom.get(point))
+        dis = set(disabled)
+        en = {p.name: p for p in enabled}
+        merged: list[PluginRef] = []
+        used = set()
+        if "*" not in dis:
+            for p in DEFAULT_PLUGINS[point]:
+                if p.name in dis:
+                    continue
+                if p.name in en:
+                    merged.append(copy.copy(en[p.name]))
+                    used.add(p.name)
+                else:
+                    merged.append(copy.copy(p))
+        for p in enabled:
+            if p.name not in used:
+                merged.append(copy.copy(p))
+                used.add(p.name)
+        if point == "score":
+            for p in merged:
+                if p.weight == 0:
+                    p.weight = 1
+        out[point] = merged
+    # multiPoint (v1beta3+): enable at every point the plugin implements; resolved later
+    mp_enabled, _ = _plugin_set(custom.get("multiPoint"))
+    if mp_enabled:
+        out["multiPoint"] = mp_enabled
+    return out
+
+
+def _f(d: dict, key: str, default):
+    v = d.get(key)
+    return default if v is None else v
+
+
+def parse_config(doc: dict) -> SchedulerConfig:
+    av = doc.get("apiVersion", SUPPORTED_API_VERSIONS[0])
+    if av not in SUPPORTED_API_VERSIONS:
+        raise ValueError(f"unsupported apiVersion {av!r}")
+    if doc.get("kind", "KubeSchedulerConfiguration") != "KubeSchedulerConfiguration":
+        raise ValueError("kind must be KubeSchedulerConfiguration")
+    le = doc.get("leaderElection") or {}
+    cc = doc.get("clientConnection") or {}
+    cfg = SchedulerConfig(
+        api_version=av,
+        leader_election=LeaderElectionConfig(
+            leader_elect=bool(_f(le, "leaderElect", True)),
+            lease_duration=parse_duration(_f(le, "leaseDuration", "15s")),
+            renew_deadline=parse_duration(_f(le, "renewDeadline", "10s")),
+            retry_period=parse_duration(_f(le, "retryPeriod", "2s")),
+            resource_lock=_f(le, "resourceLock", "leases"),
+            resource_name=_f(le, "resourceName", "kube-scheduler"),
+            resource_namespace=_f(le, "resourceNamespace", "kube-system"),
+        ),
+        client_connection=ClientConnection(
+            kubeconfig=_f(cc, "kubeconfig", ""), qps=float(_f(cc, "qps", 50)), burst=int(_f(cc, "burst", 100)),
+            content_type=_f(cc, "contentType", "application/json")),
+        percentage_of_nodes_to_score=int(_f(doc, "percentageOfNodesToScore", 0)),
+        pod_initial_backoff_seconds=float(_f(doc, "podInitialBackoffSeconds", 1)),
+        pod_max_backoff_seconds=float(_f(doc, "podMaxBackoffSeconds", 10)),
+        parallelism=int(_f(doc, "parallelism", 16)),
+        health_bind_address=_f(doc, "healthzBindAddress", "0.0.0.0:10251"),
+        metrics_bind_address=_f(doc, "metricsBindAddress", "0.0.0.0:10251"),
+        enable_profiling=bool(_f(doc, "enableProfiling", True)),
+    )
+    rt = doc.get("yodaRuntime") or {}
+    cfg.bind_concurrency = int(_f(rt, "bindConcurrency", cfg.bind_concurrency))
+    cfg.batch_size = int(_f(rt, "batchSize", cfg.batch_size))
+    cfg.unschedulable_flush_seconds = float(_f(rt, "unschedulableFlushSeconds", cfg.unschedulable_flush_seconds))
+    if not 0 <= cfg.percentage_of_nodes_to_score <= 100:
+        raise ValueError("percentageOfNodesToScore must be in [0, 100]")
+    if cfg.pod_initial_backoff_seconds <= 0 or cfg.pod_max_backoff_seconds < cfg.pod_initial_backoff_seconds:
+        raise ValueError("invalid pod backoff")
+    profiles = doc.get("profiles") or [{}]
+    names = set()
+    for pd in profiles:
+        name = pd.get("schedulerName") or "default-scheduler"
+        if name in names:
+            raise ValueError(f"duplicate profile {name!r}")
+        names.add(name)
+        pc = {}
+        for item in pd.get("pluginConfig") or []:
+            pc[item["name"]] = dict(item.get("args") or {})
+        cfg.profiles.append(Profile(scheduler_name=name, plugins=merge_plugins(pd.get("plugins")), plugin_config=pc))
+    qs = {tuple(p.name for p in pr.plugins["queueSort"]) for pr in cfg.profiles}
+    if len(qs) > 1:
+        raise ValueError("all profiles must use the same queueSort plugin")
+    return cfg
+
+
+def load_config(path: str) -> SchedulerConfig:
+    with open(path) as f:
+        docs = [d for d in yaml.safe_load_all(f) if d]
+    for d in docs:
+        if d.get("kind") == "KubeSchedulerConfiguration":
+            return parse_config(d)
+    # allow the ConfigMap manifest itself (deploy/yoda-scheduler.yaml)
+    for d in docs:
+        if d.get("kind") == "ConfigMap":
+            for v in (d.get("data") or {}).values():
+                inner = yaml.safe_load(v)
+                if isinstance(inner, dict) and inner.get("kind") == "KubeSchedulerConfiguration":
+                    return parse_config(inner)
+    raise ValueError(f"{path}: no KubeSchedulerConfiguration found")
+
+
+def default_config(scheduler_name: str = "default-scheduler") -> SchedulerConfig:
+    return parse_config({"apiVersion": SUPPORTED_API_VERSIONS[0], "kind": "KubeSchedulerConfiguration",
+                         "profiles": [{"schedulerName": scheduler_name}]})

@@ -1,0 +1,212 @@
+"""Scheduling queue: activeQ heap + podBackoffQ + unschedulableQ.
+
+* activeQ is ordered by the profile's QueueSort plugin. The reference's ``Less`` has no
+  tie-break (``pkg/yoda/sort/sort.go:8-10``, quirk Q7); here every key ends with a
+  monotonically increasing enqueue sequence number, so equal priorities are FIFO.
+* Failed pods go to backoffQ with ``initial × 2^(attempts−1)`` capped at ``max``
+  (``podInitialBackoffSeconds``/``podMaxBackoffSeconds``, ``deploy:19-20``), or to the
+  unschedulableQ when the failure was "unschedulable"; cluster events move them back,
+  and a periodic flush re-activates pods parked longer than the flush interval.
+"""
+from __future__ import annotations
+
+import asyncio
+import heapq
+import itertools
+import time
+from typing import Callable, Optional
+
+from ..models.pod import PodInfo
+
+
+class SchedulingQueue:
+    def __init__(self, sort_key: Callable[[PodInfo], tuple], initial_backoff: float = 1.0,
+                 max_backoff: float = 10.0, unschedulable_flush: float = 60.0,
+                 clock: Callable[[], float] = time.monotonic) -> None:
+        self._sort_key = sort_key
+        self._seq = itertools.count()
+        self._active: list[tuple] = []           # (key..., seq, uid)
+        self._active_entries: dict[str, tuple] = {}
+        self._backoff: list[tuple[float, int, str]] = []
+        self._backoff_pods: dict[str, PodInfo] = {}
+        self._unsched: dict[str, tuple[PodInfo, float]] = {}
+        self._pods: dict[str, PodInfo] = {}       # uid → info for everything queued
+        self.initial_backoff = initial_backoff
+        self.max_backoff = max_backoff
+        self.unschedulable_flush = unschedulable_flush
+        self.clock = clock
+        self._cond: Optional[asyncio.Event] = None
+        self.scheduling_cycle = 0
+        self._move_request_cycle = -1
+        self.closed = False
+
+    # ------------------------------------------------------------------ helpers
+    def _event(self) -> asyncio.Event:
+        if self._cond is None:
+            self._cond = asyncio.Event()
+        return self._cond
+
+    def _push_active(self, pi: PodInfo) -> None:
+        pi.enqueued = self.clock()
+        if not pi.initial_attempt:
+            pi.initial_attempt = pi.enqueued
+        entry = (*self._sort_key(pi), next(self._seq), pi.uid)
+        self._active_entries[pi.uid] = entry
+        self._pods[pi.uid] = pi
+        heapq.heappush(self._active, entry)
+        if self._cond is not None:
+            self._cond.set()
+
+    def backoff_duration(self, pi: PodInfo) -> float:
+        d = self.initial_backoff * (2 ** max(pi.attempts - 1, 0))
+        return min(d, self.max_backoff)
+
+    # ------------------------------------------------------------------ API
+    def __len__(self) -> int:
+        return len(self._active_entries) + len(self._backoff_pods) + len(self._unsched)
+
+    def pending(self) -> dict[str, int]:
+        return {"active": len(self._active_entries), "backoff": len(self._backoff_pods),
+                "unschedulable": len(self._unsched)}
+
+    def contains(self, uid: str) -> bool:
+        return uid in self._pods
+
+    def add(self, pi: PodInfo) -> None:
+        """New pending pod (informer add)."""
+        if pi.uid in self._pods:
+            self.update(pi)
+            return
+        self._push_active(pi)
+
+    def update(self, pi: PodInfo) -> None:
+        old = self._pods.get(pi.uid)
+        if old is None:
+            self._push_active(pi)
+            return
+        pi.attempts, pi.initial_attempt = old.attempts, old.initial_attempt
+        if pi.uid in self._active_entries:
+            self._pods[pi.uid] = pi      # heap entry stays; the info is refreshed
+            return
+        # an update may make an unschedulable pod schedulable: retry now
+        self._remove_parked(pi.uid)
+        self._push_active(pi)
+
+    def _remove_parked(self, uid: str) -> None:
+        self._backoff_pods.pop(uid, None)
+        self._unsched.pop(uid, None)
+
+    def delete(self, uid: str) -> None:
+        self._pods.pop(uid, None)
+        self._active_entries.pop(uid, None)   # lazy heap deletion
+        self._remove_parked(uid)
+
+    def pop_nowait(self) -> Optional[PodInfo]:
+        while self._active:
+            entry = heapq.heappop(self._active)
+            uid = entry[-1]
+            if self._active_entries.get(uid) is not entry:
+                continue
+            del self._active_entries[uid]
+            pi = self._pods.pop(uid)
+            pi.attempts += 1
+            self.scheduling_cycle += 1
+            return pi
+        return None
+
+    def pop_batch(self, n: int) -> list[PodInfo]:
+        out = []
+        while len(out) < n:
+            pi = self.pop_nowait()
+            if pi is None:
+                break
+            out.append(pi)
+        return out
+
+    async def pop(self, timeout: Optional[float] = None) -> Optional[PodInfo]:
+        while True:
+            self.flush_backoff_completed()
+            pi = self.pop_nowait()
+            if pi is not None or self.closed:
+                return pi
+            ev = self._event()
+            ev.clear()
+            wait = self._next_backoff_wait()
+            if timeout is not None:
+                wait = timeout if wait is None else min(wait, timeout)
+            try:
+                if wait is None:
+                    await ev.wait()
+                else:
+                    await asyncio.wait_for(ev.wait(), wait)
+            except asyncio.TimeoutError:
+                if timeout is not None and self._next_backoff_wait() is None and not self._active_entries:
+                    return None
+
+    def _next_backoff_wait(self) -> Optional[float]:
+        while self._backoff and self._backoff[0][2] not in self._backoff_pods:
+            heapq.heappop(self._backoff)
+        if not self._backoff:
+            return None
+        return max(0.0, self._backoff[0][0] - self.clock())
+
+    def add_unschedulable(self, pi: PodInfo, cycle: int, unschedulable: bool = True) -> None:
+        """Re-queue a pod whose cycle failed. If a move request happened since the pod
+        was popped, go straight to backoff (upstream ``moveRequestCycle`` rule)."""
+        if pi.uid in self._pods:
+            return
+        self._pods[pi.uid] = pi
+        pi.enqueued = self.clock()          # backoff counts from the failed attempt
+        if not unschedulable or self._move_request_cycle >= cycle:
+            self._to_backoff(pi)
+        else:
+            self._unsched[pi.uid] = (pi, self.clock())
+
+    def _to_backoff(self, pi: PodInfo) -> None:
+        t = self.clock() + self.backoff_duration(pi)
+        self._backoff_pods[pi.uid] = pi
+        heapq.heappush(self._backoff, (t, next(self._seq), pi.uid))
+        if self._cond is not None:
+            self._cond.set()
+
+    def flush_backoff_completed(self) -> int:
+        now, n = self.clock(), 0
+        while self._backoff and self._backoff[0][0] <= now:
+            _, _, uid = heapq.heappop(self._backoff)
+            pi = self._backoff_pods.pop(uid, None)
+            if pi is not None:
+                self._pods.pop(uid, None)
+                self._push_active(pi)
+                n += 1
+        return n
+
+    def flush_unschedulable_leftover(self) -> int:
+        now = self.clock()
+        old = [pi for pi, t in self._unsched.values() if now - t > self.unschedulable_flush]
+        for pi in old:
+            del self._unsched[pi.uid]
+            self._pods.pop(pi.uid, None)
+            self._route(pi)
+        return len(old)
+
+    def _route(self, pi: PodInfo) -> None:
+        if self.clock() - pi.enqueued < self.backoff_duration(pi):
+            self._to_backoff(pi)
+        else:
+            self._push_active(pi)
+
+    def move_all_to_active_or_backoff(self, event: str = "") -> int:
+        """A cluster event (node add, Scv update, pod delete...) may make parked pods
+        schedulable."""
+        pods = [pi for pi, _ in self._unsched.values()]
+        self._unsched.clear()
+        for pi in pods:
+            self._pods.pop(pi.uid, None)
+            self._route(pi)
+        self._move_request_cycle = self.scheduling_cycle
+        return len(pods)
+
+    def close(self) -> None:
+        self.closed = True
+        if self._cond is not None:
+            self._cond.set()

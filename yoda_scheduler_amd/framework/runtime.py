@@ -1,0 +1,195 @@
+"""Per-profile framework: instantiates the profile's plugins and splits every extension
+point into a *native* part (one engine call evaluates all nodes) and a *Python* part
+(out-of-tree plugins written against :mod:`interfaces`).
+
+A profile whose non-inert plugins are all native (the shipped yoda profile + upstream
+defaults) takes the fully native cycle: one C++ call per pod — or per batch of pods —
+does Filter → PreScore → Score → Normalize → selectHost → Reserve. Otherwise the
+hybrid runner interleaves native node sets with the Python plugins.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Optional
+
+from .config import Profile
+from .interfaces import (EXTENSION_POINTS, POINT_TYPES, BindPlugin, CycleState, FilterPlugin, NodeScore,
+                         PermitPlugin, PostBindPlugin, PostFilterPlugin, PreBindPlugin, PreFilterPlugin,
+                         PreScorePlugin, QueueSortPlugin, ReservePlugin, ScorePlugin, Status, MAX_NODE_SCORE)
+from .registry import Registry
+
+log = logging.getLogger("yoda.framework")
+
+S_SLOTS = 6
+
+
+class Framework:
+    def __init__(self, profile: Profile, registry: Registry, handle) -> None:
+        self.profile = profile
+        self.name = profile.scheduler_name
+        self.handle = handle
+        self.plugins: dict[str, object] = {}
+        self.points: dict[str, list[tuple[object, int]]] = {p: [] for p in EXTENSION_POINTS}
+        plugins = dict(profile.plugins)
+        multi = plugins.pop("multiPoint", [])
+        for point in EXTENSION_POINTS:
+            refs = list(plugins.get(point, []))
+            for ref in multi:
+                inst = self._get(ref.name, registry)
+                if isinstance(inst, POINT_TYPES[point]) and all(r.name != ref.name for r in refs):
+                    refs.append(ref)
+            for ref in refs:
+                inst = self._get(ref.name, registry)
+                if getattr(inst, "inert", False):
+                    continue
+                if point in ("preFilter", "preScore", "reserve") and not isinstance(inst, POINT_TYPES[point]):
+                    continue   # pre-work folded into the plugin's filter/score (or the native cycle)
+
+                if not isinstance(inst, POINT_TYPES[point]):
+                    raise ValueError(f"profile {self.name}: plugin {ref.name} does not implement {point}")
+                self.points[point].append((inst, ref.weight))
+        qs = self.points["queueSort"]
+        if len(qs) != 1:
+            raise ValueError(f"profile {self.name}: exactly one queueSort plugin required, got {len(qs)}")
+        self.queue_sort: QueueSortPlugin = qs[0][0]
+        self.bind_plugins: list[BindPlugin] = [p for p, _ in self.points["bind"]]
+        if not self.bind_plugins:
+            raise ValueError(f"profile {self.name}: at least one bind plugin required")
+
+        # native split
+        self.filter_mask = 0
+        self.score_w = [0] * S_SLOTS
+        self.filter_py: list[FilterPlugin] = []
+        self.score_py: list[tuple[ScorePlugin, int]] = []
+        for p, _ in self.points["filter"]:
+            nb = p.native()
+            if nb is not None and nb.filter_bit:
+                self.filter_mask |= nb.filter_bit
+            else:
+                self.filter_py.append(p)
+        for p, w in self.points["score"]:
+            nb = p.native()
+            if nb is not None and nb.score_index >= 0:
+                self.score_w[nb.score_index] += w
+            else:
+                self.score_py.append((p, w))
+        self.pre_filter: list[PreFilterPlugin] = [p for p, _ in self.points["preFilter"] if p.native() is None]
+        self.pre_score: list[PreScorePlugin] = [p for p, _ in self.points["preScore"] if p.native() is None]
+        self.post_filter: list[PostFilterPlugin] = [p for p, _ in self.points["postFilter"]]
+        self.reserve: list[ReservePlugin] = [p for p, _ in self.points["reserve"] if p.native() is None]
+        self.permit: list[PermitPlugin] = [p for p, _ in self.points["permit"]]
+        self.pre_bind: list[PreBindPlugin] = [p for p, _ in self.points["preBind"]]
+        self.post_bind: list[PostBindPlugin] = [p for p, _ in self.points["postBind"]]
+        self.yoda = self.plugins.get("yoda")
+        # Python filters that are no-ops for most pods (e.g. NodePorts without hostPorts)
+        # keep a pod on the native path unless they actually apply to it.
+        self.filter_py_conditional = [p for p in self.filter_py if hasattr(p, "is_noop_for")]
+        static = [p for p in self.filter_py if not hasattr(p, "is_noop_for")]
+        self.fully_native_static = not (static or self.score_py or self.pre_filter or self.pre_score
+                                        or self.reserve or self.permit)
+        self.fully_native = self.fully_native_static and not self.filter_py_conditional
+
+    def native_for(self, pod) -> bool:
+        if not self.fully_native_static:
+            return False
+        return all(p.is_noop_for(pod) for p in self.filter_py_conditional)
+
+    def _get(self, name: str, registry: Registry):
+        inst = self.plugins.get(name)
+        if inst is None:
+            inst = registry.create(name, self.profile.plugin_config.get(name, {}), self.handle)
+            self.plugins[name] = inst
+        return inst
+
+    # ------------------------------------------------------------------ engine config
+    def apply(self, engine) -> None:
+        engine.filters = self.filter_mask
+        for i, w in enumerate(self.score_w):
+            engine.set_score_weight(i, w)
+        if self.yoda is not None:
+            self.yoda.configure_engine(engine)
+
+    # ------------------------------------------------------------------ Python points
+    def run_pre_filter(self, state: CycleState, pod) -> Status:
+        for p in self.pre_filter:
+            st = p.pre_filter(state, pod)
+            if not st.is_success():
+                st.plugin = st.plugin or p.name
+                return st
+        return Status.ok()
+
+    def run_filter_py(self, state: CycleState, pod, nodes: list[str]) -> tuple[list[str], dict]:
+        if not self.filter_py:
+            return nodes, {}
+        out, failed = [], {}
+        active = [p for p in self.filter_py if not getattr(p, "is_noop_for", lambda _p: False)(pod)]
+        for n in nodes:
+            for p in active:
+                st = p.filter(state, pod, n)
+                if not st.is_success():
+                    failed[n] = st
+                    break
+            else:
+                out.append(n)
+        return out, failed
+
+    def run_score_py(self, state: CycleState, pod, nodes: list[str]) -> list[int]:
+        total = [0] * len(nodes)
+        for p in self.pre_score:
+            st = p.pre_score(state, pod, nodes)
+            if not st.is_success():
+                raise RuntimeError(f"preScore {p.name}: {st.message()}")
+        for p, w in self.score_py:
+            scores = []
+            for n in nodes:
+                s, st = p.score(state, pod, n)
+                if not st.is_success():
+                    raise RuntimeError(f"score {p.name}: {st.message()}")
+                scores.append(NodeScore(n, s))
+            if p.has_normalize():
+                st = p.normalize_score(state, pod, scores)
+                if not st.is_success():
+                    raise RuntimeError(f"normalize {p.name}: {st.message()}")
+            for i, ns in enumerate(scores):
+                if not 0 <= ns.score <= MAX_NODE_SCORE:
+                    raise RuntimeError(f"plugin {p.name} returned out-of-range score {ns.score}")
+                total[i] += ns.score * w
+        return total
+
+    def run_reserve(self, state: CycleState, pod, node: str) -> Status:
+        for i, p in enumerate(self.reserve):
+            st = p.reserve(state, pod, node)
+            if not st.is_success():
+                for q in reversed(self.reserve[:i]):
+                    q.unreserve(state, pod, node)
+                return st
+        return Status.ok()
+
+    def run_unreserve(self, state: CycleState, pod, node: str) -> None:
+        for p in reversed(self.reserve):
+            p.unreserve(state, pod, node)
+
+    def run_permit(self, state: CycleState, pod, node: str) -> tuple[Status, float]:
+        wait = 0.0
+        for p in self.permit:
+            st, t = p.permit(state, pod, node)
+            if not st.is_success() and st.code.name != "WAIT":
+                return st, 0.0
+            wait = max(wait, t)
+        return Status.ok(), wait
+
+    async def run_bind(self, state: CycleState, pod, node: str) -> Status:
+        for p in self.pre_bind:
+            st = await p.pre_bind(state, pod, node)
+            if not st.is_success():
+                return st
+        for p in self.bind_plugins:
+            st = await p.bind(state, pod, node)
+            if st.code.name == "SKIP":
+                continue
+            return st
+        return Status.error("no bind plugin bound the pod")
+
+    def run_post_bind(self, state: CycleState, pod, node: str) -> None:
+        for p in self.post_bind:
+            p.post_bind(state, pod, node)

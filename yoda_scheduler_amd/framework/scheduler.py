@@ -1,0 +1,467 @@
+"""The scheduler: informers → queue → (native) scheduling cycle → assume → async bind.
+
+Re-provides the upstream runtime the reference links against:
+``scheduleOne`` semantics, 1-feasible-node shortcut, score × weight summation,
+selectHost with random tie-break, assume-before-bind, bind failure → forget + requeue
+with backoff, ``FailedScheduling`` diagnosis, leader election gating.
+
+Performance design (SURVEY §7.3 hard part 2): the per-pod cycle for an all-native
+profile is a single C++ call; when several pods are waiting, up to ``batchSize`` of
+them are scheduled in one GIL-free ``schedule_batch`` call (each pod still sees the
+reservations of the pods before it, so the outcome equals sequential cycles). Binds
+run through a bounded worker pool behind the client QPS limiter.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import time
+from typing import Callable, Optional
+
+from ..kube.informer import Informer
+from ..models.pod import PodInfo, forget_num_id
+from ..ops.native import core, pod_req
+from ..utils import klog
+from ..utils.metrics import SchedulerMetrics
+from ..utils.ratelimit import TokenBucket
+from .cache import SchedulerCache
+from .config import SchedulerConfig
+from .events import EventRecorder
+from .interfaces import CycleState, Status
+from .queue import SchedulingQueue
+from .registry import Registry, default_registry
+from .runtime import Framework
+
+log = logging.getLogger("yoda.scheduler")
+
+
+class Handle:
+    """``framework.Handle`` analogue handed to plugin factories."""
+
+    def __init__(self, sched: "Scheduler") -> None:
+        self._s = sched
+
+    @property
+    def client(self):
+        return self._s.client
+
+    @property
+    def cache(self) -> SchedulerCache:
+        return self._s.cache
+
+    @property
+    def engine(self):
+        return self._s.engine
+
+    @property
+    def recorder(self) -> EventRecorder:
+        return self._s.recorder
+
+    def preempt(self, pod: PodInfo, node: str, victims: list[PodInfo]) -> None:
+        self._s._preempt(pod, node, victims)
+
+
+class Scheduler:
+    def __init__(self, client, config: SchedulerConfig, registry: Optional[Registry] = None, *,
+                 engine_threads: int = 1, metrics=None, record_events: bool = True,
+                 seed: Optional[int] = None, clock: Callable[[], float] = time.monotonic,
+                 bind_limiter: Optional[TokenBucket] = None) -> None:
+        self.client = client
+        self.config = config
+        self.registry = registry or default_registry()
+        self.metrics = metrics if metrics is not None else SchedulerMetrics()
+        cc = config.client_connection
+        self.limiter = bind_limiter or TokenBucket(cc.qps, cc.burst)
+        self.recorder = EventRecorder(client, enabled=record_events)
+        self.handle = Handle(self)
+        # the engine must exist before plugins are created (they may query it)
+        compat = any(((p.plugin_config.get("yoda") or {}).get("compat", False)) for p in config.profiles)
+        stale_factor = float(next(((p.plugin_config.get("yoda") or {}).get("staleFactor", 3.0)
+                                   for p in config.profiles if "yoda" in p.plugin_config), 3.0))
+        self.engine = core().Engine(bool(compat), max(1, int(engine_threads)))
+        if seed is not None:
+            self.engine.seed(seed)
+        self.engine.set_percentage_of_nodes_to_score(config.percentage_of_nodes_to_score)
+        self.cache = SchedulerCache(self.engine, compat=bool(compat), stale_factor=stale_factor, clock=clock)
+        self.frameworks: dict[str, Framework] = {p.scheduler_name: Framework(p, self.registry, self.handle)
+                                                 for p in config.profiles}
+        qs = next(iter(self.frameworks.values())).queue_sort
+        self.queue = SchedulingQueue(qs.sort_key, config.pod_initial_backoff_seconds, config.pod_max_backoff_seconds,
+                                     config.unschedulable_flush_seconds, clock=clock)
+        self._active_fw: Optional[Framework] = None
+        self._bind_q: asyncio.Queue = asyncio.Queue()
+        self._tasks: list[asyncio.Task] = []
+        self.informers: dict[str, Informer] = {}
+        self.scheduled = 0
+        self.failed = 0
+        self.bind_errors = 0
+        self._stop = asyncio.Event()
+        self.leading = asyncio.Event()
+        self.pending_binds = 0
+        self.batching = config.batch_size > 1
+
+    # ================================================================== informers
+    def _responsible(self, obj: dict) -> bool:
+        return ((obj.get("spec") or {}).get("schedulerName") or "default-scheduler") in self.frameworks
+
+    @staticmethod
+    def _assigned(obj: dict) -> bool:
+        return bool((obj.get("spec") or {}).get("nodeName"))
+
+    @staticmethod
+    def _terminal(obj: dict) -> bool:
+        return (obj.get("status") or {}).get("phase") in ("Succeeded", "Failed")
+
+    def on_pod_add(self, obj: dict) -> None:
+        if self._assigned(obj):
+            if not self._terminal(obj):
+                self.cache.add_pod(obj)
+        elif self._responsible(obj) and not self._terminal(obj):
+            self.queue.add(PodInfo.from_obj(obj))
+
+    def on_pod_update(self, old: dict, new: dict) -> None:
+        if self._assigned(new):
+            uid = new["metadata"].get("uid")
+            if self._terminal(new):
+                self.cache.remove_pod(uid)
+                self.queue.move_all_to_active_or_backoff("AssignedPodCompleted")
+                return
+            if not self._assigned(old):
+                self.queue.delete(uid)
+                if self.cache.is_assumed(uid):
+                    ps = self.cache.pods[uid]
+                    self.metrics.pod_scheduling.observe(max(0.0, time.monotonic() - ps.info.initial_attempt))
+                    self.metrics.pod_attempts.observe(ps.info.attempts)
+                self.cache.add_pod(new)
+            else:
+                self.cache.update_pod(new)
+        elif self._responsible(new) and not self._terminal(new):
+            if self.cache.is_assumed(new["metadata"].get("uid")):
+                return   # upstream skipPodUpdate: assumed pods only get status noise
+            self.queue.update(PodInfo.from_obj(new))
+
+    def on_pod_delete(self, obj: dict) -> None:
+        uid = (obj.get("metadata") or {}).get("uid")
+        if self._assigned(obj) or self.cache.is_assumed(uid):
+            self.cache.remove_pod(uid)
+            self.queue.move_all_to_active_or_backoff("AssignedPodDelete")
+        else:
+            self.queue.delete(uid)
+        forget_num_id(uid)
+
+    def on_node_add(self, obj: dict) -> None:
+        self.cache.add_node(obj)
+        self.queue.move_all_to_active_or_backoff("NodeAdd")
+
+    def on_node_update(self, old: dict, new: dict) -> None:
+        self.cache.update_node(new)
+        if old.get("spec") != new.get("spec") or (old.get("metadata") or {}).get("labels") != \
+                (new.get("metadata") or {}).get("labels") or (old.get("status") or {}).get("allocatable") != \
+                (new.get("status") or {}).get("allocatable"):
+            self.queue.move_all_to_active_or_backoff("NodeUpdate")
+
+    def on_node_delete(self, obj: dict) -> None:
+        self.cache.remove_node(obj["metadata"]["name"])
+
+    def on_scv(self, obj: dict) -> None:
+        self.cache.add_scv(obj)
+        self.queue.move_all_to_active_or_backoff("ScvUpdate")
+
+    def on_scv_update(self, old: dict, new: dict) -> None:
+        self.on_scv(new)
+
+    def on_scv_delete(self, obj: dict) -> None:
+        self.cache.remove_scv(obj["metadata"]["name"])
+
+    def make_informers(self) -> dict[str, Informer]:
+        self.informers = {
+            "nodes": Informer(self.client, "nodes", self.on_node_add, self.on_node_update, self.on_node_delete),
+            "scvs": Informer(self.client, "scvs", self.on_scv, self.on_scv_update, self.on_scv_delete),
+            "pods": Informer(self.client, "pods", self.on_pod_add, self.on_pod_update, self.on_pod_delete),
+        }
+        return self.informers
+
+    # ================================================================== cycle
+    def _activate(self, fw: Framework) -> None:
+        if self._active_fw is not fw:
+            fw.apply(self.engine)
+            self._active_fw = fw
+
+    def _pod_gone(self, pi: PodInfo) -> bool:
+        inf = self.informers.get("pods")
+        if inf is None:
+            return False
+        cur = inf.store.get(pi.key)
+        return cur is None or cur["metadata"].get("uid") != pi.uid or self._assigned(cur)
+
+    def schedule_one(self, pi: PodInfo) -> None:
+        fw = self.frameworks.get(pi.scheduler_name)
+        if fw is None or self._pod_gone(pi):
+            return
+        self._activate(fw)
+        cycle = self.queue.scheduling_cycle
+        t0 = time.perf_counter()
+        state = CycleState()
+        if fw.native_for(pi):
+            res = self.engine.schedule(pi.num_id, pod_req(self.engine, pi), True)
+        else:
+            res = self._hybrid_cycle(fw, state, pi)
+            if res is None:
+                return
+        self._finish_cycle(fw, state, pi, res, cycle, t0)
+
+    def _hybrid_cycle(self, fw: Framework, state: CycleState, pi: PodInfo):
+        st = fw.run_pre_filter(state, pi)
+        if not st.is_success():
+            self._fail(fw, state, pi, self.queue.scheduling_cycle, f"0/{self.engine.live_nodes} nodes are available: "
+                       f"{st.message()}", time.perf_counter())
+            return None
+        req = pod_req(self.engine, pi)
+        feas_idx, reasons = self.engine.feasible_nodes(req, [])
+        names = [self.engine.node_name(i) for i in feas_idx]
+        names2, failed = fw.run_filter_py(state, pi, names)
+        if len(names2) != len(names):
+            keep = set(names2)
+            feas_idx = [i for i, n in zip(feas_idx, names) if n in keep]
+        extra = fw.run_score_py(state, pi, names2) if (len(names2) > 1 and fw.score_py) else []
+        if not feas_idx:
+            py_fail = len(failed)
+            reasons = list(reasons)
+            return (-1, 0, self.engine.live_nodes, [], 0, reasons, 0, failed, py_fail)
+        return self.engine.schedule(pi.num_id, req, True, feas_idx, extra)
+
+    def _finish_cycle(self, fw: Framework, state: CycleState, pi: PodInfo, res, cycle: int, t0: float) -> None:
+        node_idx = res[0]
+        m = self.metrics
+        if node_idx < 0:
+            msg = self._fit_error(res)
+            self._fail(fw, state, pi, cycle, msg, t0)
+            return
+        node = self.engine.node_name(node_idx)
+        cards = res[3]
+        self.cache.assumed(pi, node, cards)
+        pi.assigned_cards = cards if (fw.filter_mask & core().F_YODA) else None
+        if fw.reserve:
+            st = fw.run_reserve(state, pi, node)
+            if not st.is_success():
+                self.cache.forget(pi)
+                self._fail(fw, state, pi, cycle, st.message(), t0, unschedulable=False)
+                return
+        if fw.permit:
+            st, _wait = fw.run_permit(state, pi, node)
+            if not st.is_success():
+                fw.run_unreserve(state, pi, node)
+                self.cache.forget(pi)
+                self._fail(fw, state, pi, cycle, st.message(), t0, unschedulable=st.is_unschedulable())
+                return
+        m.algorithm.observe(time.perf_counter() - t0)
+        m.child(m.attempts, "scheduled", fw.name).inc()
+        if klog.V(3):
+            log.info("pod %s → node %s gpus=%s score=%d feasible=%d", pi.key, node, cards, res[4], res[1])
+        self.pending_binds += 1
+        self._bind_q.put_nowait((fw, state, pi, node, cycle, t0))
+
+    def _fit_error(self, res) -> str:
+        reasons = res[5]
+        names = core().REASONS
+        text = {"NodeUnschedulable": "node(s) were unschedulable", "NodeName": "node(s) didn't match the requested node name",
+                "TaintToleration": "node(s) had taints that the pod didn't tolerate",
+                "NodeAffinity": "node(s) didn't match node selector", "NodeResourcesFit": "Insufficient cpu/memory/pods",
+                "NoScv": "node(s) have no Scv telemetry", "ScvStale": "node(s) have stale Scv telemetry",
+                "GpuNumber": "node(s) have too few GPUs", "GpuMemory": "node(s) have too few GPUs with enough free HBM",
+                "GpuClock": "node(s) have too few GPUs with the requested clock",
+                "GpuFit": "node(s) have too few healthy GPUs matching scv/memory+scv/clock"}
+        parts = [f"{c} {text.get(names[i], names[i])}" for i, c in enumerate(reasons) if c and i]
+        if len(res) > 8 and res[8]:
+            parts.append(f"{res[8]} node(s) rejected by out-of-tree filters")
+        return f"0/{res[2]} nodes are available: " + ", ".join(sorted(parts)) + "."
+
+    def _fail(self, fw: Framework, state: CycleState, pi: PodInfo, cycle: int, msg: str, t0: float,
+              unschedulable: bool = True) -> None:
+        m = self.metrics
+        self.failed += 1
+        nominated = ""
+        if unschedulable and fw.post_filter:
+            for p in fw.post_filter:
+                try:
+                    r, st = p.post_filter(state, pi, {})
+                except Exception as e:  # noqa: BLE001
+                    log.warning("postFilter %s failed: %r", getattr(p, "name", p), e)
+                    continue
+                if st.is_success() and r is not None and r.nominated_node:
+                    nominated = r.nominated_node
+                    break
+        m.child(m.attempts, "unschedulable" if unschedulable else "error", fw.name).inc()
+        m.algorithm.observe(time.perf_counter() - t0)
+        self.recorder.pod_event(pi, "Warning", "FailedScheduling", msg)
+        if klog.V(2):
+            log.info("unable to schedule %s: %s", pi.key, msg)
+        self.queue.add_unschedulable(pi, cycle, unschedulable)
+        asyncio.get_event_loop().create_task(self._update_condition(pi, msg, nominated))
+
+    async def _update_condition(self, pi: PodInfo, msg: str, nominated: str) -> None:
+        patch = {"status": {"conditions": [{"type": "PodScheduled", "status": "False", "reason": "Unschedulable",
+                                            "message": msg}]}}
+        if nominated:
+            patch["status"]["nominatedNodeName"] = nominated
+        try:
+            await self.limiter.acquire()
+            await self.client.patch("pods", pi.name, patch, pi.namespace)
+        except Exception as e:  # noqa: BLE001 - best effort like upstream
+            log.debug("condition update for %s failed: %r", pi.key, e)
+
+    def _preempt(self, pod: PodInfo, node: str, victims: list[PodInfo]) -> None:
+        self.metrics.preemption_attempts.inc()
+        self.metrics.preemption_victims.observe(len(victims))
+        for v in victims:
+            self.recorder.pod_event(v, "Normal", "Preempted", f"Preempted by {pod.key} on node {node}")
+            asyncio.get_event_loop().create_task(self._delete_victim(v))
+
+    async def _delete_victim(self, v: PodInfo) -> None:
+        try:
+            await self.limiter.acquire()
+            await self.client.delete("pods", v.name, v.namespace)
+        except Exception as e:  # noqa: BLE001
+            log.warning("preemption: deleting %s failed: %r", v.key, e)
+
+    # ================================================================== batch cycle
+    def schedule_batch(self, pods: list[PodInfo]) -> None:
+        """Schedule a run of popped pods; consecutive pods of an all-native profile go
+        through one GIL-free engine call."""
+        i = 0
+        while i < len(pods):
+            fw = self.frameworks.get(pods[i].scheduler_name)
+            if fw is None or not fw.native_for(pods[i]):
+                self.schedule_one(pods[i])
+                i += 1
+                continue
+            j = i
+            run = []
+            while j < len(pods) and pods[j].scheduler_name == fw.name and fw.native_for(pods[j]):
+                if not self._pod_gone(pods[j]):
+                    run.append(pods[j])
+                j += 1
+            i = j
+            if not run:
+                continue
+            self._activate(fw)
+            cycle = self.queue.scheduling_cycle
+            t0 = time.perf_counter()
+            eng = self.engine
+            results = eng.schedule_batch([p.num_id for p in run], [pod_req(eng, p) for p in run])
+            self.metrics.batch_size.observe(len(run))
+            for p, res in zip(run, results):
+                self._finish_cycle(fw, CycleState(), p, res, cycle, t0)
+
+    # ================================================================== binding
+    async def _bind_worker(self) -> None:
+        q, m = self._bind_q, self.metrics
+        while True:
+            fw, state, pi, node, cycle, t0 = await q.get()
+            try:
+                await self.limiter.acquire()
+                tb = time.perf_counter()
+                try:
+                    st = await fw.run_bind(state, pi, node)
+                except Exception as e:  # noqa: BLE001
+                    st = Status.error(repr(e))
+                m.binding.observe(time.perf_counter() - tb)
+                if st.is_success():
+                    self.cache.finish_binding(pi)
+                    fw.run_post_bind(state, pi, node)
+                    self.scheduled += 1
+                    m.child(m.e2e, "scheduled", fw.name).observe(time.perf_counter() - t0)
+                    self.recorder.pod_event(pi, "Normal", "Scheduled",
+                                            f"Successfully assigned {pi.key} to {node}")
+                else:
+                    self.bind_errors += 1
+                    fw.run_unreserve(state, pi, node)
+                    self.cache.forget(pi)
+                    m.child(m.e2e, "error", fw.name).observe(time.perf_counter() - t0)
+                    self.recorder.pod_event(pi, "Warning", "FailedScheduling", f"Binding rejected: {st.message()}")
+                    log.info("bind %s → %s failed: %s", pi.key, node, st.message())
+                    self.queue.add_unschedulable(pi, cycle, unschedulable=False)
+            finally:
+                self.pending_binds -= 1
+
+    # ================================================================== loops
+    async def _housekeeping(self, period: float = 0.5) -> None:
+        m = self.metrics
+        while True:
+            await asyncio.sleep(period)
+            self.queue.flush_backoff_completed()
+            self.queue.flush_unschedulable_leftover()
+            self.cache.cleanup_expired()
+            flipped = self.cache.refresh_staleness()
+            if flipped:
+                self.queue.move_all_to_active_or_backoff("ScvStale")
+            for q, n in self.queue.pending().items():
+                m.child(m.pending, q).set(n)
+
+    async def scheduling_loop(self) -> None:
+        q = self.queue
+        bs = max(1, self.config.batch_size)
+        while not self._stop.is_set():
+            pi = await q.pop()
+            if pi is None:
+                if q.closed:
+                    return
+                continue
+            if self.batching and q._active_entries:
+                batch = [pi] + q.pop_batch(bs - 1)
+                self.schedule_batch(batch)
+            else:
+                self.schedule_one(pi)
+            # let informers / binders run between cycles
+            await asyncio.sleep(0)
+
+    async def start(self, wait_sync: bool = True) -> None:
+        """Start informers, binders, recorder and housekeeping (not the scheduling loop)."""
+        loop = asyncio.get_event_loop()
+        if not self.informers:
+            self.make_informers()
+        for inf in self.informers.values():
+            self._tasks.append(loop.create_task(inf.run()))
+        n_workers = max(1, self.config.bind_concurrency)
+        for _ in range(n_workers):
+            self._tasks.append(loop.create_task(self._bind_worker()))
+        self._tasks.append(loop.create_task(self.recorder.run()))
+        self._tasks.append(loop.create_task(self._housekeeping()))
+        if wait_sync:
+            await self.wait_synced()
+
+    async def wait_synced(self) -> None:
+        for inf in self.informers.values():
+            await inf.synced.wait()
+
+    async def run(self, elector=None) -> None:
+        await self.start()
+        if elector is not None:
+            await elector.acquire()
+            self.leading.set()
+            self._tasks.append(asyncio.get_event_loop().create_task(self._watch_leadership(elector)))
+        else:
+            self.leading.set()
+        await self.scheduling_loop()
+
+    async def _watch_leadership(self, elector) -> None:
+        await elector.lost.wait()
+        log.error("leader election lost; stopping scheduling")
+        self.stop()
+
+    def stop(self) -> None:
+        self._stop.set()
+        self.queue.close()
+        for inf in self.informers.values():
+            inf.stop()
+
+    async def shutdown(self) -> None:
+        self.stop()
+        for t in self._tasks:
+            t.cancel()
+        await asyncio.gather(*self._tasks, return_exceptions=True)
+        self._tasks.clear()
+
+    async def drain_binds(self) -> None:
+        while self.pending_binds:
+            await asyncio.sleep(0)

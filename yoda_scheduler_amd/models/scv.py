@@ -1,0 +1,260 @@
+"""``Scv`` node-telemetry CRD (``scvs.core.run-linux.com/v1``), wire-compatible.
+
+The reference consumes ``github.com/NJUPT-ISL/SCV/api/v1`` (``go.mod:6``); only the
+fields it touches are load-bearing: ``Status.CardNumber``,
+``CardList``, ``FreeMemorySum``, ``TotalMemorySum`` and per card ``Health``,
+``FreeMemory``, ``TotalMemory``, ``Clock``, ``Bandwidth``, ``Core``, ``Power``.
+Field names live in ONE place (``_CARD_FIELDS`` / ``_STATUS_FIELDS``) so the CRD
+schema, the sniffer publisher and the scheduler cache agree.
+
+MI355X additions are an additive ``status.amd`` block: per-GPU physical id, PCI BDF,
+NUMA node, compute/memory partition, CU occupancy, sclk and per-peer xGMI link load,
+plus the sample timestamp used for staleness-based health.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import time
+from dataclasses import dataclass, field
+from typing import Any
+
+GROUP = "core.run-linux.com"
+VERSION = "v1"
+API_VERSION = f"{GROUP}/{VERSION}"
+KIND = "Scv"
+PLURAL = "scvs"
+HEALTHY = "Healthy"
+
+_CARD_FIELDS = {
+    # python attr : json key
+    "id": "id",
+    "health": "health",
+    "model": "model",
+    "power": "power",
+    "total_memory": "totalMemory",
+    "clock": "clock",
+    "free_memory": "freeMemory",
+    "core": "core",
+    "bandwidth": "bandwidth",
+}
+
+_AMD_CARD_FIELDS = {
+    "physical_id": "physicalId",
+    "bdf": "bdf",
+    "numa_node": "numaNode",
+    "compute_partition": "computePartition",
+    "memory_partition": "memoryPartition",
+    "cu_occupancy": "cuOccupancy",
+    "sclk_mhz": "sclkMhz",
+    "ecc_uncorrectable": "eccUncorrectable",
+    "xgmi_links_up": "xgmiLinksUp",
+}
+
+
+@dataclass
+class XgmiLink:
+    peer: int                 # physical id of the peer GPU
+    load: float = 0.0         # 0..1 utilisation estimated from counter deltas
+    read_kbps: float = 0.0
+    write_kbps: float = 0.0
+    max_bandwidth_gbps: float = 0.0
+    up: bool = True
+
+    def to_json(self) -> dict:
+        return {"peer": self.peer, "load": round(self.load, 6), "readKBps": self.read_kbps,
+                "writeKBps": self.write_kbps, "maxBandwidthGBps": self.max_bandwidth_gbps,
+                "up": self.up}
+
+    @classmethod
+    def from_json(cls, d: dict) -> "XgmiLink":
+        return cls(peer=int(d.get("peer", 0)), load=float(d.get("load", 0.0)),
+                   read_kbps=float(d.get("readKBps", 0.0)), write_kbps=float(d.get("writeKBps", 0.0)),
+                   max_bandwidth_gbps=float(d.get("maxBandwidthGBps", 0.0)), up=bool(d.get("up", True)))
+
+
+@dataclass
+class Card:
+    id: int = 0
+    health: str = HEALTHY
+    model: str = ""
+    power: int = 0            # W
+    total_memory: int = 0     # MB
+    clock: int = 0            # MHz
+    free_memory: int = 0      # MB
+    core: int = 0             # compute units
+    bandwidth: int = 0        # GB/s (HBM)
+    # --- amd extension (status.amd.cards[i]) ---
+    physical_id: int | None = None
+    bdf: str = ""
+    numa_node: int = 0
+    compute_partition: str = "SPX"
+    memory_partition: str = "NPS1"
+    cu_occupancy: float = 0.0   # 0..100 (gfx activity %)
+    sclk_mhz: int = 0           # current sclk
+    ecc_uncorrectable: int = 0
+    xgmi_links_up: bool = True
+    xgmi: list[XgmiLink] = field(default_factory=list)
+
+    @property
+    def phys(self) -> int:
+        return self.id if self.physical_id is None else self.physical_id
+
+    def base_json(self) -> dict:
+        return {j: getattr(self, a) for a, j in _CARD_FIELDS.items()}
+
+    def amd_json(self) -> dict:
+        d = {j: getattr(self, a) for a, j in _AMD_CARD_FIELDS.items()}
+        d["physicalId"] = self.phys
+        d["id"] = self.id
+        d["xgmi"] = [l.to_json() for l in self.xgmi]
+        return d
+
+
+@dataclass
+class ScvStatus:
+    card_list: list[Card] = field(default_factory=list)
+    total_memory_sum: int = 0
+    free_memory_sum: int = 0
+    card_number: int = 0
+    update_time: float | None = None     # unix seconds (serialised RFC3339)
+    sniffer: str = ""                    # producer id (amd-smi / fake / nvml)
+
+    def recompute_sums(self) -> None:
+        self.card_number = len(self.card_list)
+        self.total_memory_sum = sum(c.total_memory for c in self.card_list)
+        self.free_memory_sum = sum(c.free_memory for c in self.card_list)
+
+
+@dataclass
+class Scv:
+    name: str
+    status: ScvStatus = field(default_factory=ScvStatus)
+    update_interval_ms: int = 1000
+    resource_version: str = ""
+    labels: dict = field(default_factory=dict)
+
+    # ------------------------------------------------------------------ JSON
+    def to_json(self) -> dict:
+        st = self.status
+        status: dict[str, Any] = {
+            "cardList": [c.base_json() for c in st.card_list],
+            "totalMemorySum": st.total_memory_sum,
+            "freeMemorySum": st.free_memory_sum,
+            "cardNumber": st.card_number,
+        }
+        if st.update_time is not None:
+            status["updateTime"] = rfc3339(st.update_time)
+        status["amd"] = {
+            "sniffer": st.sniffer,
+            "cards": [c.amd_json() for c in st.card_list],
+        }
+        meta: dict[str, Any] = {"name": self.name}
+        if self.resource_version:
+            meta["resourceVersion"] = self.resource_version
+        if self.labels:
+            meta["labels"] = dict(self.labels)
+        return {"apiVersion": API_VERSION, "kind": KIND, "metadata": meta,
+                "spec": {"updateInterval": self.update_interval_ms}, "status": status}
+
+    @classmethod
+    def from_json(cls, obj: dict) -> "Scv":
+        meta = obj.get("metadata") or {}
+        status = obj.get("status") or {}
+        amd = status.get("amd") or {}
+        amd_cards = {int(c.get("id", i)): c for i, c in enumerate(amd.get("cards") or [])}
+        cards: list[Card] = []
+        for i, cj in enumerate(status.get("cardList") or []):
+            c = Card()
+            for a, j in _CARD_FIELDS.items():
+                if j in cj and cj[j] is not None:
+                    v = cj[j]
+                    setattr(c, a, v if a in ("health", "model") else int(v))
+            ext = amd_cards.get(c.id) or amd_cards.get(i)
+            if ext:
+                for a, j in _AMD_CARD_FIELDS.items():
+                    if j in ext and ext[j] is not None:
+                        setattr(c, a, ext[j])
+                c.physical_id = int(ext.get("physicalId", c.id))
+                c.xgmi = [XgmiLink.from_json(l) for l in ext.get("xgmi") or []]
+            cards.append(c)
+        st = ScvStatus(
+            card_list=cards,
+            total_memory_sum=int(status.get("totalMemorySum", 0) or 0),
+            free_memory_sum=int(status.get("freeMemorySum", 0) or 0),
+            card_number=int(status.get("cardNumber", 0) or 0),
+            update_time=parse_rfc3339(status.get("updateTime")),
+            sniffer=str(amd.get("sniffer", "")),
+        )
+        spec = obj.get("spec") or {}
+        return cls(name=meta.get("name", ""), status=st,
+                   update_interval_ms=int(spec.get("updateInterval", 1000) or 1000),
+                   resource_version=str(meta.get("resourceVersion", "")),
+                   labels=dict(meta.get("labels") or {}))
+
+    def is_stale(self, now: float | None = None, factor: float = 3.0) -> bool:
+        """Fresh iff sampled within ``factor`` × update interval (SURVEY §5 health)."""
+        t = self.status.update_time
+        if t is None:
+            return False   # producers that do not stamp (reference SCV) are never stale
+        now = time.time() if now is None else now
+        return (now - t) * 1000.0 > factor * max(self.update_interval_ms, 1)
+
+
+def rfc3339(t: float) -> str:
+    frac = f"{t % 1:.6f}"[1:]
+    return time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(t)) + frac + "Z"
+
+
+def parse_rfc3339(s: Any) -> float | None:
+    if s is None or s == "":
+        return None
+    if isinstance(s, (int, float)):
+        return float(s)
+    s = str(s)
+    try:   # C fast path (py3.10 fromisoformat needs an explicit offset)
+        return _dt.datetime.fromisoformat(s[:-1] + "+00:00" if s.endswith("Z") else s).timestamp()
+    except ValueError:
+        pass
+    import calendar
+    base, frac = s.rstrip("Z"), 0.0
+    if "." in base:
+        base, f = base.split(".", 1)
+        frac = float("0." + f) if f else 0.0
+    return calendar.timegm(time.strptime(base, "%Y-%m-%dT%H:%M:%S")) + frac
+
+
+def crd_manifest() -> dict:
+    """CustomResourceDefinition for scvs.core.run-linux.com (cluster-scoped, status subresource)."""
+    int_t = {"type": "integer", "format": "int64", "minimum": 0}
+    card_props = {j: ({"type": "string"} if a in ("health", "model") else dict(int_t))
+                  for a, j in _CARD_FIELDS.items()}
+    schema = {
+        "type": "object",
+        "properties": {
+            "spec": {"type": "object", "properties": {"updateInterval": {"type": "integer"}}},
+            "status": {
+                "type": "object",
+                "properties": {
+                    "cardList": {"type": "array", "items": {"type": "object", "properties": card_props}},
+                    "totalMemorySum": dict(int_t),
+                    "freeMemorySum": dict(int_t),
+                    "cardNumber": dict(int_t),
+                    "updateTime": {"type": "string", "format": "date-time"},
+                    "amd": {"type": "object", "x-kubernetes-preserve-unknown-fields": True},
+                },
+            },
+        },
+    }
+    return {
+        "apiVersion": "apiextensions.k8s.io/v1",
+        "kind": "CustomResourceDefinition",
+        "metadata": {"name": f"{PLURAL}.{GROUP}"},
+        "spec": {
+            "group": GROUP,
+            "scope": "Cluster",
+            "names": {"plural": PLURAL, "singular": "scv", "kind": KIND, "listKind": "ScvList"},
+            "versions": [{"name": VERSION, "served": True, "storage": True,
+                          "subresources": {"status": {}},
+                          "schema": {"openAPIV3Schema": schema}}],
+        },
+    }

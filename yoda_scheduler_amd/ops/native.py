@@ -1,0 +1,100 @@
+"""Loader + marshalling for the native scheduling engine (``_yoda_core``).
+
+The engine is mandatory: there is no silent Python fallback on the hot path. If the
+extension is missing it is built in-tree on first import (hipcc/g++ are in the image);
+if that fails the import raises.
+"""
+from __future__ import annotations
+
+import importlib
+import threading
+
+from ..models.pod import NodeInfo, PodInfo
+from ..models.scv import HEALTHY, Scv
+
+_lock = threading.Lock()
+_core = None
+
+
+def core():
+    """Return the ``_yoda_core`` extension module, building it in-tree if needed."""
+    global _core
+    if _core is not None:
+        return _core
+    with _lock:
+        if _core is None:
+            try:
+                _core = importlib.import_module("yoda_scheduler_amd._native._yoda_core")
+            except ImportError:
+                from .build import build_core, OUT
+                OUT.mkdir(parents=True, exist_ok=True)
+                (OUT / "__init__.py").touch()
+                build_core()
+                importlib.invalidate_caches()
+                _core = importlib.import_module("yoda_scheduler_amd._native._yoda_core")
+    return _core
+
+
+def card_tuples(scv: Scv) -> list[tuple]:
+    out = []
+    for c in scv.status.card_list:
+        out.append((int(c.total_memory) & 0xFFFFFFFFFFFFFFFF, int(c.free_memory) & 0xFFFFFFFFFFFFFFFF,
+                    int(c.clock) & 0xFFFFFFFFFFFFFFFF, int(c.bandwidth) & 0xFFFFFFFFFFFFFFFF,
+                    int(c.core) & 0xFFFFFFFFFFFFFFFF, int(c.power) & 0xFFFFFFFFFFFFFFFF,
+                    c.health == HEALTHY and c.ecc_uncorrectable == 0 and c.xgmi_links_up,
+                    int(c.phys), int(c.numa_node), int(round(float(c.cu_occupancy) * 100))))
+    return out
+
+
+def compat_card_tuples(scv: Scv) -> list[tuple]:
+    """Reference semantics: health is exactly ``Health == "Healthy"``."""
+    return [t[:6] + (c.health == HEALTHY,) + t[7:] for t, c in zip(card_tuples(scv), scv.status.card_list)]
+
+
+def link_matrix(scv: Scv) -> tuple[int, list[int]]:
+    """Pair quality in 1e-4 units: 10000 × (1 − load) for an up link, 0 for a down one."""
+    cards = scv.status.card_list
+    nphys = max((c.phys for c in cards), default=-1) + 1
+    q = [10000] * (nphys * nphys)
+    for c in cards:
+        for l in c.xgmi:
+            if 0 <= l.peer < nphys:
+                v = 0 if not l.up else int(round(10000 * (1.0 - min(max(l.load, 0.0), 1.0))))
+                q[c.phys * nphys + l.peer] = v
+    # symmetrise with the worse direction (a ring uses both)
+    for a in range(nphys):
+        for b in range(a + 1, nphys):
+            v = min(q[a * nphys + b], q[b * nphys + a])
+            q[a * nphys + b] = q[b * nphys + a] = v
+    return nphys, q
+
+
+def push_scv(engine, idx: int, scv: Scv, compat: bool, stale: bool = False) -> None:
+    st = scv.status
+    cards = compat_card_tuples(scv) if compat else card_tuples(scv)
+    engine.set_cards(idx, cards, int(st.card_number) & 0xFFFFFFFFFFFFFFFF,
+                     int(st.free_memory_sum) & 0xFFFFFFFFFFFFFFFF,
+                     int(st.total_memory_sum) & 0xFFFFFFFFFFFFFFFF, stale)
+    nphys, q = link_matrix(scv)
+    if nphys:
+        engine.set_links(idx, nphys, q)
+
+
+def push_node(engine, info: NodeInfo) -> int:
+    idx = engine.upsert_node(info.name)
+    engine.set_node_meta(idx, info.unschedulable, list(info.labels.items()), list(info.taints),
+                         info.cpu_m, info.mem, info.pods)
+    return idx
+
+
+def pod_req(engine, pi: PodInfo):
+    """Build (and cache on the PodInfo) the engine's PodReq."""
+    if pi.native_owner is engine and pi.native_req is not None:
+        return pi.native_req
+    g = pi.gpu
+    r = engine.make_req(g.has_number, g.number, g.has_memory, g.memory, g.has_clock, g.clock,
+                        g.clock_min, g.priority, pi.node_name, pi.cpu_m, pi.mem,
+                        list(pi.node_selector.items()), pi.required_terms, pi.preferred_terms,
+                        pi.tolerations)
+    pi.native_req, pi.native_owner = r, engine
+    return r

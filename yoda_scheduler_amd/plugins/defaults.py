@@ -1,0 +1,198 @@
+"""In-tree default plugins (the upstream v1.20 set the reference's profile keeps).
+
+Hot filters/scores are *native*: they declare an engine binding and run inside the
+C++ cycle (``native/core/engine.cpp``). Plugins whose upstream behaviour depends on
+objects this scheduler does not model yet (volumes, inter-pod affinity, topology
+spread, images) are registered as inert so reference configs load unchanged; they
+are listed in ``INERT_PLUGINS`` and documented in README as not yet implemented.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+from ..framework.interfaces import (BindPlugin, CycleState, FilterPlugin, NativeBinding, Plugin,
+                                    PostFilterPlugin, PostFilterResult, QueueSortPlugin, ScorePlugin, Status)
+from ..models.labels import ANNOTATION_GPUS, ANNOTATION_RESERVED
+from ..ops.native import core
+
+
+def _c():
+    return core()
+
+
+class PrioritySort(QueueSortPlugin):
+    """``.spec.priority`` desc, then enqueue order (upstream PrioritySort)."""
+    name = "PrioritySort"
+
+    def sort_key(self, pi) -> tuple:
+        return (-pi.priority,)
+
+
+class NodeUnschedulable(FilterPlugin):
+    name = "NodeUnschedulable"
+
+    def native(self):
+        return NativeBinding(filter_bit=_c().F_NODE_UNSCHEDULABLE)
+
+
+class NodeName(FilterPlugin):
+    name = "NodeName"
+
+    def native(self):
+        return NativeBinding(filter_bit=_c().F_NODE_NAME)
+
+
+class NodeResourcesFit(FilterPlugin):
+    name = "NodeResourcesFit"
+
+    def native(self):
+        return NativeBinding(filter_bit=_c().F_NODE_RESOURCES_FIT)
+
+
+class NodeAffinity(FilterPlugin, ScorePlugin):
+    name = "NodeAffinity"
+
+    def native(self):
+        return NativeBinding(filter_bit=_c().F_NODE_AFFINITY, score_index=_c().S_NODE_AFFINITY)
+
+
+class TaintToleration(FilterPlugin, ScorePlugin):
+    name = "TaintToleration"
+
+    def native(self):
+        return NativeBinding(filter_bit=_c().F_TAINT_TOLERATION, score_index=_c().S_TAINT_TOLERATION)
+
+
+class NodeResourcesLeastAllocated(ScorePlugin):
+    name = "NodeResourcesLeastAllocated"
+
+    def native(self):
+        return NativeBinding(score_index=_c().S_LEAST_ALLOCATED)
+
+
+class NodeResourcesMostAllocated(ScorePlugin):
+    name = "NodeResourcesMostAllocated"
+
+    def native(self):
+        return NativeBinding(score_index=_c().S_MOST_ALLOCATED)
+
+
+class NodeResourcesBalancedAllocation(ScorePlugin):
+    name = "NodeResourcesBalancedAllocation"
+
+    def native(self):
+        return NativeBinding(score_index=_c().S_BALANCED_ALLOCATION)
+
+
+class NodePorts(FilterPlugin):
+    """Host-port conflicts against pods already on the node (Python; rare on GPU nodes)."""
+    name = "NodePorts"
+
+    def filter(self, state: CycleState, pod, node_name: str) -> Status:
+        if not pod.host_ports:
+            return Status.ok()
+        cache = self.handle.cache
+        used = set()
+        for uid in cache.node_pods.get(node_name, ()):
+            ps = cache.pods.get(uid)
+            if ps is not None:
+                for port, proto, ip in ps.info.host_ports:
+                    used.add((port, proto))
+        for port, proto, _ip in pod.host_ports:
+            if (port, proto) in used:
+                return Status.unschedulable("node(s) didn't have free ports for the requested pod ports",
+                                            plugin=self.name)
+        return Status.ok()
+
+    def is_noop_for(self, pod) -> bool:
+        return not pod.host_ports
+
+
+class _Inert(Plugin):
+    inert = True
+
+
+def _inert(name: str):
+    return type(name, (_Inert,), {"name": name})
+
+
+INERT_PLUGINS = ["VolumeRestrictions", "EBSLimits", "GCEPDLimits", "NodeVolumeLimits", "AzureDiskLimits",
+                 "VolumeBinding", "VolumeZone", "PodTopologySpread", "InterPodAffinity", "ImageLocality",
+                 "NodePreferAvoidPods", "NodeLabel", "ServiceAffinity", "SelectorSpread", "CSILimits"]
+
+
+class DefaultBinder(BindPlugin):
+    """POST pods/{name}/binding; the GPU assignment rides on the Binding's annotations,
+    which the apiserver copies onto the pod (one round trip, no extra patch)."""
+    name = "DefaultBinder"
+
+    async def bind(self, state: CycleState, pod, node_name: str) -> Status:
+        ann = {}
+        cards = getattr(pod, "assigned_cards", None)
+        if cards is not None:
+            ann[ANNOTATION_GPUS] = ",".join(str(c) for c in cards)
+            if pod.gpu.has_memory:
+                ann[ANNOTATION_RESERVED] = str(pod.gpu.memory)
+        try:
+            await self.handle.client.bind(pod.namespace, pod.name, pod.uid, node_name, ann)
+        except Exception as e:  # noqa: BLE001 - surfaced as a bind failure
+            return Status.error(f"binding rejected: {e}", plugin=self.name)
+        return Status.ok()
+
+
+class DefaultPreemption(PostFilterPlugin):
+    """Evict lower-priority pods so a high-priority pod fits (GPU-aware).
+
+    For every node that failed for a resolvable reason, remove that node's
+    lower-priority pods lowest-priority first from the native ledger (a what-if), and
+    stop as soon as the engine's filter passes. The node with the fewest victims — then
+    the lowest highest-victim priority — wins; victims are deleted through the API and
+    the preemptor is nominated to the node. The ledger is restored before returning.
+    """
+    name = "DefaultPreemption"
+
+    def post_filter(self, state: CycleState, pod, statuses: dict) -> tuple[Optional[PostFilterResult], Status]:
+        h = self.handle
+        if pod.priority <= 0 and not self.args.get("preemptZeroPriority", False):
+            return None, Status.unschedulable("preemption: pod has no priority", plugin=self.name)
+        eng, cache = h.engine, h.cache
+        from ..ops.native import pod_req
+        req = pod_req(eng, pod)
+        best = None
+        for node, ps_uids in cache.node_pods.items():
+            idx = eng.node_index(node)
+            if idx < 0:
+                continue
+            cands = sorted((cache.pods[u] for u in ps_uids if u in cache.pods and cache.pods[u].info.priority < pod.priority),
+                           key=lambda ps: ps.info.priority)
+            if not cands:
+                continue
+            removed = []
+            fit = False
+            for ps in cands:
+                eng.release(ps.info.num_id)
+                removed.append(ps)
+                if eng.filter_node(req, idx) == 0:
+                    fit = True
+                    break
+            # restore the ledger exactly
+            for ps in removed:
+                eng.reserve(ps.info.num_id, pod_req(eng, ps.info), idx, list(ps.cards))
+            if fit:
+                key = (len(removed), max(p.info.priority for p in removed))
+                if best is None or key < best[0]:
+                    best = (key, node, removed)
+        if best is None:
+            return None, Status.unschedulable("preemption: no node can be freed", plugin=self.name)
+        _, node, victims = best
+        h.preempt(pod, node, [v.info for v in victims])
+        return PostFilterResult(node), Status.ok()
+
+
+def register_defaults(registry) -> None:
+    for cls in (PrioritySort, NodeUnschedulable, NodeName, NodeResourcesFit, NodeAffinity, TaintToleration,
+                NodeResourcesLeastAllocated, NodeResourcesMostAllocated, NodeResourcesBalancedAllocation,
+                NodePorts, DefaultBinder, DefaultPreemption):
+        registry.register(cls.name, cls)
+    for n in INERT_PLUGINS:
+        registry.register(n, _inert(n))
