@@ -1,0 +1,163 @@
+#!/usr/bin/env python3
+"""Headline benchmark: pods scheduled/s + p99 scheduling latency on a 1000-pod burst onto
+an 8×MI355X node (BASELINE.json config 3; other configs via ``--config``).
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 launched
+by ``torch.distributed.run`` with one rank per GPU. Scaling is **weak**: every rank runs
+one scheduler shard (its own apiserver, 8×MI355X node, scheduler) on its own GPU and
+schedules its own burst each step, i.e. N independent scheduling domains. ``value`` is
+the whole-job aggregate (pods bound on all ranks ÷ the slowest rank's time), latency
+percentiles are over every pod of every rank.
+
+Each rank samples its GPU with the C++ amd-smi collector (when the driver is present)
+and uses the real HBM size / max sclk / CU count / power cap / HBM bandwidth as the
+card template of its synthetic node — pods and node layout are synthetic, the per-GPU
+telemetry is real (reported in ``telemetry``).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import sys
+import time
+
+REFERENCE_DERIVED_PODS_PER_S = 55.0   # derived (unmeasured) ceiling at client QPS 50 / burst 100
+METRIC = "pods scheduled/sec + p99 scheduling latency, 1000-pod burst on 8×MI355X node"
+
+
+def _telemetry_template(local_rank: int) -> tuple[dict | None, dict]:
+    info: dict = {"source": "synthetic MI355X spec"}
+    try:
+        from yoda_scheduler_amd.sniffer.collector import AmdSmiBackend
+        be = AmdSmiBackend()
+        samples = be.sample()
+        be.close()
+        if not samples:
+            return None, info
+        s = samples[min(local_rank, len(samples) - 1)]
+        tmpl = {"total_memory": int(s["vramTotalMB"]), "clock": int(s["sclkMaxMHz"]),
+                "core": int(s["computeUnits"]), "power": int(s["powerLimitW"]),
+                "bandwidth": int(s["hbmBandwidthGBps"]), "model": s.get("model", "")}
+        tmpl = {k: v for k, v in tmpl.items() if v}
+        info = {"source": "amd-smi (C++ collector)", "gpu_index": s["index"], "bdf": s["bdf"], **tmpl}
+        return tmpl, info
+    except Exception as e:  # noqa: BLE001 - CPU box / no driver
+        info["amd_smi_error"] = str(e)[:200]
+        return None, info
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
+    ap.add_argument("--qps", type=float, default=5000.0, help="client QPS (deploy default 5000; reference 50)")
+    ap.add_argument("--burst", type=int, default=10000, help="client burst (deploy default 10000; reference 100)")
+    ap.add_argument("--reference-qps", action="store_true", help="use the reference's client limits 50/100")
+    ap.add_argument("--batch", type=int, default=256, help="native batch size (1 = strictly one pod per cycle)")
+    ap.add_argument("--compat", action="store_true", help="reference-compatible yoda scoring (no HBM ledger)")
+    ap.add_argument("--no-events", action="store_true")
+    a = ap.parse_args(argv)
+    if a.reference_qps:
+        a.qps, a.burst = 50.0, 100
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+
+    import torch
+    import torch.distributed as dist
+    cuda = torch.cuda.is_available()
+    if cuda:
+        torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
+    if world > 1:
+        dist.init_process_group("nccl" if cuda else "gloo")
+    dev = torch.device("cuda", torch.cuda.current_device()) if cuda else torch.device("cpu")
+
+    def sync() -> None:
+        if world > 1:
+            dist.barrier()
+        if cuda:
+            torch.cuda.synchronize()
+
+    tmpl, tel = _telemetry_template(local_rank)
+
+    from yoda_scheduler_amd.bench.harness import Shard, percentile
+    from yoda_scheduler_amd.bench.workloads import make_workload
+    w = make_workload(a.config, seed=rank)
+    loop = asyncio.new_event_loop()
+    asyncio.set_event_loop(loop)
+    shards = [Shard(w, qps=a.qps, burst=a.burst, batch=a.batch, template=tmpl, events=not a.no_events,
+                    compat=a.compat, seed=rank * 1000 + i) for i in range(a.warmup + a.steps)]
+    for s in shards:
+        loop.run_until_complete(s.start())
+    for i in range(a.warmup):
+        loop.run_until_complete(shards[i].burst(f"w{i}"))
+
+    sync()
+    t0 = time.perf_counter()
+    results = [loop.run_until_complete(shards[a.warmup + i].burst(f"s{i}")) for i in range(a.steps)]
+    sync()
+    elapsed = time.perf_counter() - t0
+
+    bound = sum(r.bound for r in results)
+    unsched = sum(r.unschedulable for r in results)
+    lats = [x for r in results for x in r.latencies_s]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([bound, unsched], dtype=torch.float64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        bound, unsched = int(c[0].item()), int(c[1].item())
+        gathered: list = [None] * world
+        dist.all_gather_object(gathered, lats)
+        lats = [x for g in gathered for x in g]
+        tels: list = [None] * world
+        dist.all_gather_object(tels, tel)
+    else:
+        tels = [tel]
+    for s in shards:
+        loop.run_until_complete(s.stop())
+
+    if rank == 0:
+        value = bound / elapsed if elapsed > 0 else 0.0
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "pods/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1000.0, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / REFERENCE_DERIVED_PODS_PER_S, 2),
+            "dtype": "int64",
+            "data": "synthetic pods + node layout; per-GPU telemetry from amd-smi when available",
+            "config": {"model": f"yoda-scheduler config{a.config}: {w.name}",
+                       "global_batch": w.n_pods * world, "seq_len": None,
+                       "parallelism": f"shard{world}" if world > 1 else "shard1"},
+            "p50_latency_ms": round(percentile(lats, 50) * 1000.0, 3),
+            "p99_latency_ms": round(percentile(lats, 99) * 1000.0, 3),
+            "max_latency_ms": round(max(lats) * 1000.0, 3) if lats else None,
+            "pods_bound": bound,
+            "pods_unschedulable": unsched,
+            "client_qps": a.qps, "client_burst": a.burst, "native_batch": a.batch, "compat": a.compat,
+            "baseline_note": "vs_baseline against BASELINE.md's derived (unmeasured) ~55 pods/s reference ceiling "
+                             "(kube-scheduler v1.20 client QPS 50 / burst 100)",
+            "telemetry": tels[0],
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    loop.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,228 @@
+// gfx950 device probes backing the Scv card fields with measured values (SURVEY §7 phase 6):
+//   * HBM read / copy bandwidth        → Card.Bandwidth (GB/s actually achievable)
+//   * HBM pattern write/verify          → Card.Health (uncorrectable data errors)
+//   * xGMI peer-write bandwidth          → per-link quality for gang placement
+//
+// Wave64 / CDNA4 notes: 16 B per lane per access (float4), 4 independent loads in flight
+// per lane, grid = 8 blocks per CU × 256 CUs with grid-stride loops (cdna guide G11/G13);
+// the pattern check reduces mismatches per wave with a 64-bit ballot and issues ONE
+// atomic per wave (G12).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#define YODA_CHECK(x)                                   \
+  do {                                                  \
+    hipError_t e__ = (x);                               \
+    if (e__ != hipSuccess) return (int)e__;             \
+  } while (0)
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ uint32_t mix32(uint64_t i, uint32_t seed) {
+  // splitmix-style avalanche of the element index: every word of the buffer gets a
+  // distinct, address-dependent value (catches stuck bits and aliasing)
+  uint64_t z = i * 0x9E3779B97F4A7C15ull + seed;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (uint32_t)(z ^ (z >> 31));
+}
+
+__global__ __launch_bounds__(kBlock) void k_read(const float4* __restrict__ src, size_t n4, float* __restrict__ sink) {
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  // 4 independent 16-B loads in flight per lane
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    acc.x += a.x + b.x + c.x + d.x;
+    acc.y += a.y + b.y + c.y + d.y;
+    acc.z += a.z + b.z + c.z + d.z;
+    acc.w += a.w + b.w + c.w + d.w;
+  }
+  for (; i < n4; i += stride) {
+    float4 a = src[i];
+    acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+  }
+  float s = acc.x + acc.y + acc.z + acc.w;
+  if (s == 1234.5f) sink[blockIdx.x] = s;   // practically never: keeps the loads alive
+}
+
+__global__ __launch_bounds__(kBlock) void k_copy(const float4* __restrict__ src, float4* __restrict__ dst, size_t n4) {
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a; dst[i + stride] = b; dst[i + 2 * stride] = c; dst[i + 3 * stride] = d;
+  }
+  for (; i < n4; i += stride) dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill(uint4* __restrict__ buf, size_t n16, uint32_t seed) {
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n16; i += stride) {
+    const uint64_t w = i * 4;
+    buf[i] = make_uint4(mix32(w, seed), mix32(w + 1, seed), mix32(w + 2, seed), mix32(w + 3, seed));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_verify(const uint4* __restrict__ buf, size_t n16, uint32_t seed,
+                                                   unsigned long long* __restrict__ errors) {
+  const size_t stride = (size_t)gridDim.x * kBlock;
+  uint32_t bad = 0;
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n16; i += stride) {
+    const uint64_t w = i * 4;
+    uint4 v = buf[i];
+    bad += (v.x != mix32(w, seed)) + (v.y != mix32(w + 1, seed)) + (v.z != mix32(w + 2, seed)) +
+           (v.w != mix32(w + 3, seed));
+  }
+  // wave-level reduction (64 lanes), one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) bad += __shfl_xor(bad, off, 64);
+  if ((threadIdx.x & 63) == 0 && bad) atomicAdd(errors, (unsigned long long)bad);
+}
+
+int grid_for(int device) {
+  int cus = 256;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  return cus * 8;
+}
+
+}  // namespace
+
+extern "C" {
+
+int yoda_hip_device_count(int* n) {
+  YODA_CHECK(hipGetDeviceCount(n));
+  return 0;
+}
+
+// name: out buffer (>= 64 bytes); returns gcnArchName, CUs, HBM bytes
+int yoda_hip_device_info(int device, char* arch, int arch_len, int* cus, unsigned long long* hbm_bytes,
+                         int* clock_khz) {
+  hipDeviceProp_t p;
+  YODA_CHECK(hipGetDeviceProperties(&p, device));
+  snprintf(arch, arch_len, "%s", p.gcnArchName);
+  *cus = p.multiProcessorCount;
+  *hbm_bytes = (unsigned long long)p.totalGlobalMem;
+  *clock_khz = p.clockRate;
+  return 0;
+}
+
+// HBM read and copy bandwidth (GB/s, 1e9 bytes) over a `bytes` working set; copy counts
+// read + write bytes. Buffers are allocated and freed here (probe, not hot path).
+int yoda_hbm_bandwidth(int device, unsigned long long bytes, int iters, double* read_gbps, double* copy_gbps) {
+  YODA_CHECK(hipSetDevice(device));
+  const size_t n4 = (size_t)(bytes / 16);
+  float4 *a = nullptr, *b = nullptr;
+  float* sink = nullptr;
+  hipEvent_t e0, e1;
+  YODA_CHECK(hipMalloc(&a, n4 * 16));
+  YODA_CHECK(hipMalloc(&b, n4 * 16));
+  const int grid = grid_for(device);
+  YODA_CHECK(hipMalloc(&sink, grid * sizeof(float)));
+  YODA_CHECK(hipMemset(a, 0, n4 * 16));
+  YODA_CHECK(hipMemset(b, 0, n4 * 16));
+  YODA_CHECK(hipEventCreate(&e0));
+  YODA_CHECK(hipEventCreate(&e1));
+  // warm-up
+  hipLaunchKernelGGL(k_read, dim3(grid), dim3(kBlock), 0, 0, a, n4, sink);
+  hipLaunchKernelGGL(k_copy, dim3(grid), dim3(kBlock), 0, 0, a, b, n4);
+  YODA_CHECK(hipDeviceSynchronize());
+  float ms = 0.f;
+  YODA_CHECK(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(k_read, dim3(grid), dim3(kBlock), 0, 0, a, n4, sink);
+  YODA_CHECK(hipEventRecord(e1, 0));
+  YODA_CHECK(hipEventSynchronize(e1));
+  YODA_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  *read_gbps = (double)n4 * 16.0 * iters / (ms * 1e-3) / 1e9;
+  YODA_CHECK(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(k_copy, dim3(grid), dim3(kBlock), 0, 0, a, b, n4);
+  YODA_CHECK(hipEventRecord(e1, 0));
+  YODA_CHECK(hipEventSynchronize(e1));
+  YODA_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  *copy_gbps = (double)n4 * 32.0 * iters / (ms * 1e-3) / 1e9;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(a);
+  hipFree(b);
+  hipFree(sink);
+  return (int)hipGetLastError();
+}
+
+// Write an address-dependent pattern over `bytes` of HBM and verify it; returns the
+// number of mismatching 32-bit words in *errors.
+int yoda_hbm_pattern_check(int device, unsigned long long bytes, unsigned seed, unsigned long long* errors,
+                           float* ms_out) {
+  YODA_CHECK(hipSetDevice(device));
+  const size_t n16 = (size_t)(bytes / 16);
+  uint4* buf = nullptr;
+  unsigned long long* d_err = nullptr;
+  YODA_CHECK(hipMalloc(&buf, n16 * 16));
+  YODA_CHECK(hipMalloc(&d_err, sizeof(unsigned long long)));
+  YODA_CHECK(hipMemset(d_err, 0, sizeof(unsigned long long)));
+  hipEvent_t e0, e1;
+  YODA_CHECK(hipEventCreate(&e0));
+  YODA_CHECK(hipEventCreate(&e1));
+  const int grid = grid_for(device);
+  YODA_CHECK(hipEventRecord(e0, 0));
+  hipLaunchKernelGGL(k_fill, dim3(grid), dim3(kBlock), 0, 0, buf, n16, seed);
+  hipLaunchKernelGGL(k_verify, dim3(grid), dim3(kBlock), 0, 0, buf, n16, seed, d_err);
+  YODA_CHECK(hipEventRecord(e1, 0));
+  YODA_CHECK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  YODA_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  if (ms_out) *ms_out = ms;
+  YODA_CHECK(hipMemcpy(errors, d_err, sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(buf);
+  hipFree(d_err);
+  return (int)hipGetLastError();
+}
+
+// xGMI peer-write bandwidth: a copy kernel running on `src` streams a local buffer into
+// a buffer resident on `dst` (remote stores over the point-to-point xGMI link).
+// Returns 1 in *supported if peer access is not possible (no xGMI path).
+int yoda_peer_write_bandwidth(int src, int dst, unsigned long long bytes, int iters, double* gbps, int* supported) {
+  int can = 0;
+  *gbps = 0.0;
+  YODA_CHECK(hipDeviceCanAccessPeer(&can, src, dst));
+  *supported = can;
+  if (!can || src == dst) return 0;
+  YODA_CHECK(hipSetDevice(src));
+  hipError_t pe = hipDeviceEnablePeerAccess(dst, 0);
+  if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) return (int)pe;
+  (void)hipGetLastError();
+  const size_t n4 = (size_t)(bytes / 16);
+  float4 *local = nullptr, *remote = nullptr;
+  YODA_CHECK(hipMalloc(&local, n4 * 16));
+  YODA_CHECK(hipMemset(local, 0, n4 * 16));
+  YODA_CHECK(hipSetDevice(dst));
+  YODA_CHECK(hipMalloc(&remote, n4 * 16));
+  YODA_CHECK(hipSetDevice(src));
+  const int grid = grid_for(src);
+  hipEvent_t e0, e1;
+  YODA_CHECK(hipEventCreate(&e0));
+  YODA_CHECK(hipEventCreate(&e1));
+  hipLaunchKernelGGL(k_copy, dim3(grid), dim3(kBlock), 0, 0, local, remote, n4);
+  YODA_CHECK(hipDeviceSynchronize());
+  YODA_CHECK(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(k_copy, dim3(grid), dim3(kBlock), 0, 0, local, remote, n4);
+  YODA_CHECK(hipEventRecord(e1, 0));
+  YODA_CHECK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  YODA_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  *gbps = (double)n4 * 16.0 * iters / (ms * 1e-3) / 1e9;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(local);
+  YODA_CHECK(hipSetDevice(dst));
+  hipFree(remote);
+  YODA_CHECK(hipSetDevice(src));
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

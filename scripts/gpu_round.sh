@@ -1,0 +1,28 @@
+#!/usr/bin/env bash
+# One GPU-box session: GPU tests, smoke, bench, rocprofv3 kernel stats.
+# Each GPU step has its own time limit; the script stops after any crash-like exit
+# (timeout 124/137, abort 134, segfault 139) and keeps going after plain failures (1).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -5 "gpurun_out/$name.log"
+  case $rc in 0|1|2|5) return 0 ;; *) echo "stopping after crash-like exit $rc"; exit $rc ;; esac
+}
+STEPS=${STEPS:-"tests smoke bench"}
+for s in $STEPS; do
+  case $s in
+    tests) step gpu_tests 600 python -m pytest tests -m gpu -q -x ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py ;;
+    bench5) step bench5 600 python bench.py --config 5 ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+  esac
+done
+echo "=== done"

@@ -1,0 +1,95 @@
+"""GPU tests: gfx950 HIP probes, the C++ amd-smi collector against the real driver, and a
+real-telemetry → Scv → schedule round trip."""
+import asyncio
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_device_is_gfx950(require_gpu):
+    from yoda_scheduler_amd.ops import hip
+    assert hip.device_count() >= 1
+    info = hip.device_info(0)
+    assert info["arch"].startswith("gfx950"), info
+    assert info["cus"] >= 200
+    assert info["hbm_bytes"] > 200 * 2**30
+
+
+def test_hbm_pattern_probe_clean(require_gpu):
+    from yoda_scheduler_amd.ops import hip
+    r = hip.hbm_pattern_check(0, 256 << 20, seed=1234)
+    assert r["errors"] == 0, r
+
+
+def test_hbm_pattern_probe_detects_mismatch_semantics(require_gpu):
+    # different seeds produce different patterns: verify a fresh fill under seed B is clean
+    from yoda_scheduler_amd.ops import hip
+    a = hip.hbm_pattern_check(0, 64 << 20, seed=1)
+    b = hip.hbm_pattern_check(0, 64 << 20, seed=2)
+    assert a["errors"] == 0 and b["errors"] == 0
+
+
+def test_hbm_bandwidth_probe(require_gpu):
+    from yoda_scheduler_amd.ops import hip
+    r = hip.hbm_bandwidth(0, 1 << 30, 10)
+    # MI355X: 8 TB/s peak, ~6.3 TB/s achievable; anything below 2 TB/s means a broken probe
+    assert r["read_gbps"] > 2000, r
+    assert r["copy_gbps"] > 2000, r
+
+
+def test_amdsmi_collector_real(require_gpu):
+    from yoda_scheduler_amd.sniffer.collector import AmdSmiBackend, samples_to_scv
+    be = AmdSmiBackend()
+    s = be.sample()
+    s2 = be.sample()   # second sample exercises the link-rate differencing path
+    be.close()
+    assert len(s) >= 1 and len(s2) == len(s)
+    g = s[0]
+    assert g["vramTotalMB"] > 200_000, g
+    assert g["computeUnits"] >= 200, g
+    assert g["sclkMaxMHz"] >= 2000, g
+    scv = samples_to_scv("gpu-node", s2)
+    assert scv.status.card_number == len(s)
+    assert scv.status.total_memory_sum == sum(x["vramTotalMB"] for x in s)
+
+
+def test_real_telemetry_schedules_pod(require_gpu):
+    """amd-smi (C++) → Scv publish → scheduler Filter/Score/bind with GPU assignment."""
+    from yoda_scheduler_amd.fakeapi.client import InProcessClient
+    from yoda_scheduler_amd.fakeapi.server import FakeApiServer
+    from yoda_scheduler_amd.framework.config import default_config
+    from yoda_scheduler_amd.framework.scheduler import Scheduler
+    from yoda_scheduler_amd.models.device import make_node
+    from yoda_scheduler_amd.sniffer.collector import AmdSmiBackend
+    from yoda_scheduler_amd.sniffer.publisher import SnifferAgent
+    from yoda_scheduler_amd.utils.metrics import NullMetrics
+
+    async def run():
+        srv = FakeApiServer()
+        cl = InProcessClient(srv)
+        srv.create("nodes", make_node("gpu-node"))
+        agent = SnifferAgent(cl, "gpu-node", AmdSmiBackend(), interval=60.0)
+        await agent.publish_once()
+        cfg = default_config("yoda-scheduler")
+        from yoda_scheduler_amd.framework.config import PluginRef
+        prof = cfg.profiles[0]
+        prof.plugins["filter"].append(PluginRef("yoda"))
+        prof.plugins["score"].append(PluginRef("yoda", 300))
+        s = Scheduler(cl, cfg, metrics=NullMetrics(), record_events=False)
+        await s.start()
+        loop_task = asyncio.get_event_loop().create_task(s.scheduling_loop())
+        srv.create("pods", {"metadata": {"name": "p", "namespace": "default", "labels": {"scv/memory": "1000"}},
+                            "spec": {"schedulerName": "yoda-scheduler", "containers": [{"name": "c", "image": "x"}]}})
+        for _ in range(2000):
+            if srv.bind_log:
+                break
+            await asyncio.sleep(0.001)
+        pod = srv.get("pods", "p", "default")
+        await s.shutdown()
+        loop_task.cancel()
+        return pod
+
+    pod = asyncio.run(run())
+    assert pod["spec"]["nodeName"] == "gpu-node"
+    assert pod["metadata"]["annotations"]["scv.amd.com/gpus"] != ""

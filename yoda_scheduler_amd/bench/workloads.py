@@ -1,0 +1,108 @@
+"""The five BASELINE.json burst configurations as synthetic, seeded workloads.
+
+| # | BASELINE config                                                         | cluster                        |
+|---|-------------------------------------------------------------------------|--------------------------------|
+| 1 | 1 pod, scv/memory=1000, 1-node cluster with fake-GPU CRD                | 1 node × 8 MI355X              |
+| 2 | 100-pod burst, scv/memory, single 1×MI355X node                         | 1 node × 1 MI355X              |
+| 3 | 1000-pod burst, mixed scv/memory + scv/number, single 8×MI355X node     | 1 node × 8 MI355X (headline)   |
+| 4 | 1000-pod burst, scv/clock high-perf labels, 4 nodes × 8×MI355X          | 2×MI355X(2400) + 2×MI350X(2200)|
+| 5 | 5000-pod burst, mixed + multi-GPU pods, 4 nodes × 8×MI355X              | 4 nodes × 8 MI355X             |
+
+Config 4 mixes MI355X (2400 MHz max sclk) and MI350X (2200 MHz) nodes so the exact-match
+``scv/clock`` selector has something to select. Demand is sized
+so every pod fits with per-GPU HBM reservation (≈60-75 % of HBM), i.e. the burst
+measures scheduling, not capacity exhaustion.
+"""
+from __future__ import annotations
+
+import random
+import time
+from dataclasses import dataclass, field
+from typing import Optional
+
+from ..models.device import MI350X, MI355X, GpuSpec, make_node, make_scv
+from ..models.scv import Card, Scv
+
+
+@dataclass
+class Workload:
+    id: int
+    name: str
+    nodes: list[tuple[str, GpuSpec, int]]            # (name, spec, gpus)
+    pods: list[dict] = field(default_factory=list)   # label dicts
+    scheduler_name: str = "yoda-scheduler"
+
+    @property
+    def n_pods(self) -> int:
+        return len(self.pods)
+
+
+def _mixed_labels(rng: random.Random) -> dict:
+    r = rng.random()
+    if r < 0.60:
+        return {"scv/memory": str(rng.choice([256, 512, 1024, 2048]))}
+    if r < 0.70:
+        return {"scv/number": "1"}
+    if r < 0.88:
+        return {"scv/number": "2", "scv/memory": str(rng.choice([512, 1024]))}
+    if r < 0.97:
+        return {"scv/number": "4", "scv/memory": "1024"}
+    return {"scv/number": "8", "scv/memory": "1024"}
+
+
+def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None) -> Workload:
+    rng = random.Random(seed * 7919 + cfg)
+    if cfg == 1:
+        w = Workload(1, "1 pod scv/memory=1000, 1 node x 8 MI355X (fake CRD)", [("node-0", MI355X, 8)])
+        w.pods = [{"scv/memory": "1000"}]
+    elif cfg == 2:
+        w = Workload(2, "100-pod burst scv/memory, 1 node x 1 MI355X", [("node-0", MI355X, 1)])
+        w.pods = [{"scv/memory": str(rng.choice([512, 1024, 2048]))} for _ in range(100)]
+    elif cfg == 3:
+        w = Workload(3, "1000-pod burst mixed scv/memory+scv/number, 1 node x 8 MI355X", [("node-0", MI355X, 8)])
+        w.pods = [_mixed_labels(rng) for _ in range(1000)]
+    elif cfg == 4:
+        w = Workload(4, "1000-pod burst scv/clock, 4 nodes x 8 GPUs (2x MI355X@2400, 2x MI350X@2200)",
+                     [("node-0", MI355X, 8), ("node-1", MI355X, 8), ("node-2", MI350X, 8), ("node-3", MI350X, 8)])
+        w.pods = []
+        for _ in range(1000):
+            lab = {"scv/clock": "2400" if rng.random() < 0.7 else "2200",
+                   "scv/memory": str(rng.choice([1024, 2048, 4096]))}
+            if rng.random() < 0.1:
+                lab["scv/number"] = "2"
+            w.pods.append(lab)
+    elif cfg == 5:
+        w = Workload(5, "5000-pod burst mixed + multi-GPU, 4 nodes x 8 MI355X (xGMI gang scoring)",
+                     [(f"node-{i}", MI355X, 8) for i in range(4)])
+        w.pods = [_mixed_labels(rng) for _ in range(5000)]
+    else:
+        raise ValueError(f"unknown config {cfg}")
+    return w
+
+
+def pod_object(i: int, labels: dict, scheduler_name: str, namespace: str = "default",
+               prefix: str = "burst") -> dict:
+    return {"apiVersion": "v1", "kind": "Pod",
+            "metadata": {"name": f"{prefix}-{i}", "namespace": namespace, "labels": dict(labels)},
+            "spec": {"schedulerName": scheduler_name,
+                     "containers": [{"name": "main", "image": "rocm/pytorch:latest",
+                                     "resources": {"requests": {"cpu": "100m", "memory": "128Mi"}}}]}}
+
+
+def populate(server, w: Workload, template: Optional[dict] = None, link_load: float = 0.0,
+             seed: int = 0) -> None:
+    """Create the workload's nodes and their Scv telemetry in a fake apiserver.
+    ``template`` (from a real amd-smi sample) overrides the per-card static fields."""
+    rng = random.Random(seed)
+    for name, spec, gpus in w.nodes:
+        server.create("nodes", make_node(name))
+        scv = make_scv(name, spec, gpus, update_time=time.time(), link_load=link_load, rng=rng,
+                       jitter=link_load > 0)
+        scv.update_interval_ms = 60_000     # one sample stays fresh for the whole burst
+        if template:
+            for c in scv.status.card_list:
+                for k, v in template.items():
+                    setattr(c, k, v)
+                c.free_memory = min(c.free_memory, c.total_memory)
+            scv.status.recompute_sums()
+        server.create("scvs", scv.to_json())

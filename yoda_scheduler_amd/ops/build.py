@@ -92,7 +92,7 @@ def build_hip(force: bool = False) -> Path:
     out = OUT / "libyoda_hip.so"
     if force or _stale(out, deps):
         _run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-Wall", f"-I{src}", *map(str, srcs), "-o", str(out)], "hip kernels")
+              "-Wall", "-Wno-unused-result", "-Wno-unused-value", f"-I{src}", *map(str, srcs), "-o", str(out)], "hip kernels")
     return out
 
 

@@ -1,0 +1,108 @@
+"""ctypes binding of ``libyoda_hip.so`` (gfx950 kernels, C ABI).
+
+Runtime note: PyTorch-ROCm wheels bundle their own ``libamdhip64.so`` with SONAME
+``libamdhip64.so.7`` — the same SONAME as ``/opt/rocm``'s. Whichever is loaded first
+serves both, so when torch is importable it is imported *before* this library:
+kernels launched here and tensors allocated by torch then share one HIP runtime and
+device context (required to pass ``tensor.data_ptr()`` / torch streams to our
+kernels). Processes without torch (sniffer, scheduler) use ``/opt/rocm`` directly.
+
+There is no silent fallback: if the library is missing it is built in-tree, and if
+it cannot be loaded the call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from pathlib import Path
+from typing import Optional
+
+_LIB: Optional[ctypes.CDLL] = None
+_lock = threading.Lock()
+PATH = Path(__file__).resolve().parents[1] / "_native" / "libyoda_hip.so"
+
+c_int, c_uint, c_ull, c_double, c_float, c_char_p, c_void_p = (
+    ctypes.c_int, ctypes.c_uint, ctypes.c_ulonglong, ctypes.c_double, ctypes.c_float, ctypes.c_char_p,
+    ctypes.c_void_p)
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    P = ctypes.POINTER
+    sigs = {
+        "yoda_hip_device_count": [P(c_int)],
+        "yoda_hip_device_info": [c_int, c_char_p, c_int, P(c_int), P(c_ull), P(c_int)],
+        "yoda_hbm_bandwidth": [c_int, c_ull, c_int, P(c_double), P(c_double)],
+        "yoda_hbm_pattern_check": [c_int, c_ull, c_uint, P(c_ull), P(c_float)],
+        "yoda_peer_write_bandwidth": [c_int, c_int, c_ull, c_int, P(c_double), P(c_int)],
+    }
+    for name, args in sigs.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = c_int
+    try:
+        from . import device_scorer as _ds
+        _ds.declare(lib)
+    except AttributeError:
+        pass
+
+
+def lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _lock:
+        if _LIB is None:
+            try:   # share torch's HIP runtime when torch is present (see module doc)
+                import torch  # noqa: F401
+            except ImportError:
+                pass
+            if not PATH.exists():
+                from .build import build_hip, OUT
+                OUT.mkdir(parents=True, exist_ok=True)
+                build_hip()
+            l = ctypes.CDLL(str(PATH), mode=ctypes.RTLD_GLOBAL)
+            _declare(l)
+            _LIB = l
+    return _LIB
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise HipError(f"{what} failed with hipError {rc}")
+
+
+def device_count() -> int:
+    n = c_int(0)
+    rc = lib().yoda_hip_device_count(ctypes.byref(n))
+    return 0 if rc else n.value
+
+
+def device_info(device: int = 0) -> dict:
+    arch = ctypes.create_string_buffer(64)
+    cus, hbm, clk = c_int(0), c_ull(0), c_int(0)
+    _check(lib().yoda_hip_device_info(device, arch, 64, ctypes.byref(cus), ctypes.byref(hbm), ctypes.byref(clk)),
+           "hipGetDeviceProperties")
+    return {"arch": arch.value.decode(), "cus": cus.value, "hbm_bytes": hbm.value, "clock_khz": clk.value}
+
+
+def hbm_bandwidth(device: int = 0, nbytes: int = 1 << 30, iters: int = 10) -> dict:
+    r, c = c_double(0), c_double(0)
+    _check(lib().yoda_hbm_bandwidth(device, nbytes, iters, ctypes.byref(r), ctypes.byref(c)), "hbm_bandwidth")
+    return {"read_gbps": r.value, "copy_gbps": c.value, "bytes": nbytes, "iters": iters}
+
+
+def hbm_pattern_check(device: int = 0, nbytes: int = 1 << 30, seed: int = 0x5eed) -> dict:
+    err, ms = c_ull(0), c_float(0)
+    _check(lib().yoda_hbm_pattern_check(device, nbytes, seed, ctypes.byref(err), ctypes.byref(ms)), "hbm_pattern")
+    return {"errors": err.value, "ms": ms.value, "bytes": nbytes}
+
+
+def peer_write_bandwidth(src: int, dst: int, nbytes: int = 256 << 20, iters: int = 10) -> dict:
+    g, sup = c_double(0), c_int(0)
+    _check(lib().yoda_peer_write_bandwidth(src, dst, nbytes, iters, ctypes.byref(g), ctypes.byref(sup)),
+           "peer_write_bandwidth")
+    return {"gbps": g.value, "supported": bool(sup.value)}

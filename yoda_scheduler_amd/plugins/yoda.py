@@ -9,7 +9,7 @@ this class carries the configuration and the Python-visible pieces.
 Plugin args (``pluginConfig[].args`` for ``yoda``):
   compat: false        reproduce the reference bit-exactly (quirks Q2/Q3, no HBM ledger)
   staleFactor: 3.0     Scv older than factor × updateInterval → node unschedulable
-  gpuStrategy: binpack|spread     GPU choice inside a node (best-fit vs worst-fit)
+  gpuStrategy: spread|binpack     GPU choice inside a node (worst-fit vs best-fit)
   gangWeights: {link: 4, numa: 2, fit: 1, occupancy: 1, score: 3, enumLimit: 5000}
 
 Unlike the reference there is one shared Scv informer per process (Q8), scheduling is
@@ -35,7 +35,11 @@ class Yoda(QueueSortPlugin, FilterPlugin, PostFilterPlugin, ScorePlugin):
         a = self.args
         self.compat = bool(a.get("compat", False))
         self.stale_factor = float(a.get("staleFactor", 3.0))
-        self.gpu_strategy = str(a.get("gpuStrategy", "binpack")).lower()
+        # "spread" (default) fills a node's GPUs evenly (worst-fit): with HBM-sharing pods
+        # it keeps the per-GPU free HBM level, so multi-GPU gangs stay placeable until the
+        # node is nearly full. "binpack" (best-fit) keeps whole GPUs empty instead — the
+        # better choice when most pods want dedicated GPUs.
+        self.gpu_strategy = str(a.get("gpuStrategy", "spread")).lower()
         if self.gpu_strategy not in ("binpack", "spread"):
             raise ValueError(f"yoda: gpuStrategy must be binpack|spread, got {self.gpu_strategy!r}")
         gw = a.get("gangWeights") or {}
