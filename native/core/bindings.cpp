@@ -94,7 +94,7 @@ PYBIND11_MODULE(_yoda_core, m) {
              w.gpu_binpack = binpack; w.w_gang_score = gang_score; w.enum_limit = enum_limit;
            },
            py::arg("link") = 4, py::arg("numa") = 2, py::arg("fit") = 1, py::arg("occ") = 1,
-           py::arg("binpack") = true, py::arg("gang_score") = 3, py::arg("enum_limit") = 5000)
+           py::arg("binpack") = false, py::arg("gang_score") = 3, py::arg("enum_limit") = 5000)
       .def("set_percentage_of_nodes_to_score", &Engine::set_percentage_of_nodes_to_score)
       .def("seed", &Engine::seed)
       .def("intern", &Engine::intern)

@@ -127,7 +127,11 @@ std::vector<GpuSample> Collector::sample() {
     else g.errors.push_back("vram_info");
     amdsmi_power_info_t pi{};
     if (amdsmi_get_power_info(h, &pi) == AMDSMI_STATUS_SUCCESS) {
-      g.power_limit_w = pi.power_limit;
+      // ROCm 7.2 reports power_limit in µW on MI355X (1.4e9 for a 1400 W cap) although the
+      // header says W; normalise anything implausibly large for watts.
+      uint64_t lim = pi.power_limit;
+      while (lim > 100000) lim /= 1000;
+      g.power_limit_w = (uint32_t)lim;
       g.power_w = pi.current_socket_power ? pi.current_socket_power : pi.average_socket_power;
     } else {
       g.errors.push_back("power_info");

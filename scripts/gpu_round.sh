@@ -22,7 +22,7 @@ for s in $STEPS; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     bench5) step bench5 600 python bench.py --config 5 ;;
-    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
 done
 echo "=== done"

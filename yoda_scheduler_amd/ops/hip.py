@@ -45,9 +45,9 @@ def _declare(lib: ctypes.CDLL) -> None:
         f.restype = c_int
     try:
         from . import device_scorer as _ds
-        _ds.declare(lib)
-    except AttributeError:
-        pass
+    except ImportError:
+        return
+    _ds.declare(lib)
 
 
 def lib() -> ctypes.CDLL:
