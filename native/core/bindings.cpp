@@ -126,7 +126,7 @@ PYBIND11_MODULE(_yoda_core, m) {
            [](Engine& e, int32_t idx,
               const std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, bool, int32_t,
                                            int32_t, int32_t>>& cs,
-              uint64_t card_number, uint64_t free_sum, uint64_t total_sum, bool stale) {
+              uint64_t card_number, uint64_t free_sum, uint64_t total_sum, bool stale, double sample_ts) {
              std::vector<Card> cards;
              cards.reserve(cs.size());
              for (auto& t : cs) {
@@ -136,15 +136,20 @@ PYBIND11_MODULE(_yoda_core, m) {
                if (c.phys < 0 || c.phys >= kMaxPhys) throw std::invalid_argument("physical id out of range");
                cards.push_back(c);
              }
-             e.set_cards(idx, std::move(cards), card_number, free_sum, total_sum, stale);
-           })
+             e.set_cards(idx, std::move(cards), card_number, free_sum, total_sum, stale, sample_ts);
+           },
+           py::arg("idx"), py::arg("cards"), py::arg("card_number"), py::arg("free_sum"), py::arg("total_sum"),
+           py::arg("stale"), py::arg("sample_ts") = 0.0)
+      .def_property("settle_seconds", &Engine::settle_seconds, &Engine::set_settle_seconds)
+      .def("set_fixed_now", &Engine::set_fixed_now)
       .def("clear_scv", &Engine::clear_scv)
       .def("set_links", &Engine::set_links)
       .def("node_cards",
            [](Engine& e, int32_t idx) {
              py::list out;
              for (auto& c : e.node(idx).cards)
-               out.append(py::make_tuple(c.total_mb, c.free_mb, c.reserved_mb, c.pods, c.clock, c.healthy, c.phys));
+               out.append(py::make_tuple(c.total_mb, c.free_mb, c.reserved_mb, c.pods, c.clock, c.healthy, c.phys,
+                                         c.pending_mb));
              return out;
            })
       .def("node_usage",

@@ -2,6 +2,7 @@
 #include "engine.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <stdexcept>
 
@@ -128,8 +129,14 @@ void Engine::remove_node(int32_t idx) {
   --live_;
 }
 
+double Engine::now() const {
+  if (fixed_now_ >= 0) return fixed_now_;
+  using namespace std::chrono;
+  return duration<double>(system_clock::now().time_since_epoch()).count();
+}
+
 void Engine::set_cards(int32_t idx, std::vector<Card> cards, uint64_t card_number, uint64_t free_sum,
-                       uint64_t total_sum, bool stale) {
+                       uint64_t total_sum, bool stale, double sample_ts) {
   Node& n = nodes_.at(idx);
   // keep the ledger: reservations are per card index
   std::vector<uint64_t> res(cards.size(), 0);
@@ -141,7 +148,16 @@ void Engine::set_cards(int32_t idx, std::vector<Card> cards, uint64_t card_numbe
   n.cards = std::move(cards);
   for (size_t i = 0; i < n.cards.size(); ++i) {
     n.cards[i].reserved_mb = res[i];
+    n.cards[i].pending_mb = 0;
     n.cards[i].pods = pods[i];
+  }
+  // recompute which reservations the new sample cannot reflect yet
+  n.sample_ts = sample_ts;
+  for (uint64_t pod : n.pods) {
+    const Assignment& a = ledger_.at(pod);
+    if (!is_pending(n, a)) continue;
+    for (int32_t c : a.cards)
+      if (c < (int32_t)n.cards.size()) n.cards[c].pending_mb += a.mb;
   }
   n.card_number = card_number;
   n.free_sum = free_sum;
@@ -189,12 +205,17 @@ bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::ve
     if (c < 0 || c >= (int32_t)n.cards.size()) return false;
   }
   a.cards = cards;
+  a.t_res = now();
   if (!compat_) {
+    const bool pend = is_pending(n, a);
     for (int32_t c : cards) {
       n.cards[c].reserved_mb += a.mb;
+      if (pend) n.cards[c].pending_mb += a.mb;
       n.cards[c].pods += 1;
     }
   }
+  a.slot = (int32_t)n.pods.size();
+  n.pods.push_back(pod);
   a.cpu_m = req.cpu_m;
   a.mem = req.mem;
   a.has_label_mem = req.has_memory;
@@ -214,12 +235,20 @@ bool Engine::release(uint64_t pod) {
   if (a.node >= 0 && a.node < (int32_t)nodes_.size() && nodes_[a.node].alive) {
     Node& n = nodes_[a.node];
     if (!compat_) {
+      const bool pend = is_pending(n, a);
       for (int32_t c : a.cards) {
         if (c < (int32_t)n.cards.size()) {
           n.cards[c].reserved_mb -= std::min(n.cards[c].reserved_mb, a.mb);
+          if (pend) n.cards[c].pending_mb -= std::min(n.cards[c].pending_mb, a.mb);
           n.cards[c].pods = std::max(0, n.cards[c].pods - 1);
         }
       }
+    }
+    if (a.slot >= 0 && a.slot < (int32_t)n.pods.size()) {
+      uint64_t last = n.pods.back();
+      n.pods[a.slot] = last;
+      n.pods.pop_back();
+      if (last != pod) ledger_.at(last).slot = a.slot;
     }
     n.req_cpu_m -= a.cpu_m;
     n.req_mem -= a.mem;
@@ -296,9 +325,12 @@ bool Engine::affinity_ok(const PodReq& req, const Node& n) const {
 
 // ============================================================== yoda policy
 uint64_t Engine::eff_free(const Card& c) const {
+  // Sampled free HBM minus reservations the sample cannot contain yet, capped by the
+  // ledger view (total − all reservations, for pods that have not allocated yet).
   if (compat_) return c.free_mb;
   uint64_t cap = c.total_mb > c.reserved_mb ? c.total_mb - c.reserved_mb : 0;
-  return std::min(c.free_mb, cap);
+  uint64_t sampled = c.free_mb > c.pending_mb ? c.free_mb - c.pending_mb : 0;
+  return std::min(sampled, cap);
 }
 
 bool Engine::yoda_card_eligible(const PodReq& req, const Card& c, uint64_t m, uint64_t cl) const {

@@ -65,6 +65,7 @@ struct Card {
   int32_t numa = 0;
   int32_t occ_q = 0;          // CU occupancy in 1e-4 units (0..10000)
   uint64_t reserved_mb = 0;   // ledger: HBM reserved by assumed/bound pods
+  uint64_t pending_mb = 0;    // part of reserved_mb the last sample cannot reflect yet
   int32_t pods = 0;           // pods holding a reservation on this card
 };
 
@@ -89,6 +90,8 @@ struct Node {
   int64_t alloc_cpu_m = 0, alloc_mem = 0, alloc_pods = 0;
   int64_t req_cpu_m = 0, req_mem = 0, pod_count = 0;
   uint64_t label_mem_sum = 0;         // Σ scv/memory labels of pods on node (compat Allocate)
+  double sample_ts = 0;               // unix time of the Scv sample the cards came from
+  std::vector<uint64_t> pods;         // ledger entries on this node (for pending recompute)
 };
 
 struct PodReq {
@@ -120,6 +123,8 @@ struct Assignment {
   int64_t cpu_m = 0, mem = 0;
   uint64_t label_mem = 0;
   bool has_label_mem = false;
+  double t_res = 0;             // unix time of the reservation
+  int32_t slot = -1;            // index in Node::pods
 };
 
 struct CycleResult {
@@ -179,8 +184,15 @@ class Engine {
   const Node& node(int32_t idx) const { return nodes_[idx]; }
   int32_t num_nodes() const { return (int32_t)nodes_.size(); }
   int32_t live_nodes() const { return live_; }
+  // sample_ts: when the Scv sample was taken (unix s). Reservations younger than
+  // sample_ts − settle are "pending": the sample cannot contain their HBM use yet, so
+  // they are subtracted from the sampled free memory (never double-counted: see eff_free).
   void set_cards(int32_t idx, std::vector<Card> cards, uint64_t card_number, uint64_t free_sum,
-                 uint64_t total_sum, bool stale);
+                 uint64_t total_sum, bool stale, double sample_ts = 0);
+  void set_settle_seconds(double s) { settle_s_ = s; }
+  double settle_seconds() const { return settle_s_; }
+  // test hook: pin the reservation clock (unix s); <0 = use the system clock
+  void set_fixed_now(double t) { fixed_now_ = t; }
   void clear_scv(int32_t idx);
   void set_links(int32_t idx, int32_t nphys, std::vector<int32_t> q);
 
@@ -246,6 +258,10 @@ class Engine {
   std::unordered_map<std::string, int32_t> string_idx_;
   std::unordered_map<uint64_t, Assignment> ledger_;
   std::mt19937_64 rng_{0x59d4};
+  double settle_s_ = 30.0;
+  double fixed_now_ = -1.0;
+  double now() const;
+  bool is_pending(const Node& n, const Assignment& a) const { return a.t_res > n.sample_ts - settle_s_; }
   int32_t next_start_ = 0;
   uint64_t cycles_ = 0;
   ThreadPool* pool_ = nullptr;

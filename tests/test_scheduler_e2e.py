@@ -1,0 +1,311 @@
+"""End-to-end scheduling against the in-process fake apiserver:
+BASELINE config 1, HBM reservation (Q10), multi-node scoring (Q1), staleness, bind
+failures, preemption, restart/resume from annotations, compat mode, hybrid plugins."""
+import asyncio
+import time
+
+from yoda_scheduler_amd.fakeapi.server import Faults
+from yoda_scheduler_amd.framework.interfaces import FilterPlugin, ScorePlugin, Status
+from yoda_scheduler_amd.framework.registry import default_registry
+from yoda_scheduler_amd.models.device import MI350X
+from yoda_scheduler_amd.testing import FakeCluster, yoda_config
+
+
+def run(coro):
+    return asyncio.run(coro)
+
+
+def test_config1_single_pod_memory_1000():
+    async def go():
+        c = FakeCluster()
+        c.add_node("node-0")
+        await c.start()
+        c.add_pod("test", {"scv/memory": "1000"})
+        assert await c.wait_bound(1)
+        pod = c.pod("test")
+        assert pod["spec"]["nodeName"] == "node-0"
+        ann = pod["metadata"]["annotations"]
+        assert len(ann["scv.amd.com/gpus"].split(",")) == 1 and ann["scv.amd.com/reserved-mb"] == "1000"
+        conds = {x["type"]: x["status"] for x in pod["status"]["conditions"]}
+        assert conds["PodScheduled"] == "True"
+        await asyncio.sleep(0.05)
+        reasons = c.sched.recorder.recorded
+        await c.stop()
+        return reasons
+    reasons = run(go())
+    assert reasons["Scheduled"] == 1
+
+
+def test_multinode_scores_and_spreads_q1_fixed():
+    """The reference errors in Score with >=2 feasible nodes (Q1); here every pod binds and
+    yoda's Actual/Allocate terms spread load across equal nodes."""
+    async def go():
+        c = FakeCluster()
+        for i in range(4):
+            c.add_node(f"n{i}")
+        await c.start()
+        for i in range(40):
+            c.add_pod(f"p{i}", {"scv/memory": "20000"})
+        assert await c.wait_bound(40)
+        per = {}
+        for i in range(40):
+            per[c.node_of(f"p{i}")] = per.get(c.node_of(f"p{i}"), 0) + 1
+        await c.stop()
+        return per
+    per = run(go())
+    assert len(per) == 4 and max(per.values()) - min(per.values()) <= 2
+
+
+def test_hbm_reservation_prevents_oversubscription():
+    async def go():
+        c = FakeCluster()
+        c.add_node("small", gpus=1, used_mb=[294912 - 10000])     # 10 GB free on one GPU
+        await c.start()
+        for i in range(3):
+            c.add_pod(f"p{i}", {"scv/memory": "4000"})
+        await c.wait(lambda: len(c.server.bind_log) >= 2 and c.sched.failed >= 1, 3)
+        bound = sorted(c.server.bind_log)
+        pend = c.pod("p2") if "default/p2" not in c.server.bind_log else None
+        await asyncio.sleep(0.05)
+        await c.stop()
+        return bound, c.sched.failed
+    bound, failed = run(go())
+    assert len(bound) == 2 and failed >= 1
+
+
+def test_pod_delete_frees_reservation_and_requeues():
+    async def go():
+        c = FakeCluster()
+        c.add_node("one", gpus=1, used_mb=[294912 - 5000])
+        await c.start()
+        c.add_pod("a", {"scv/memory": "4000"})
+        assert await c.wait_bound(1)
+        c.add_pod("b", {"scv/memory": "4000"})
+        await c.wait(lambda: c.sched.failed >= 1, 2)
+        assert "default/b" not in c.server.bind_log
+        c.server.delete("pods", "a", "default")
+        ok = await c.wait(lambda: "default/b" in c.server.bind_log, 3)
+        await c.stop()
+        return ok
+    assert run(go())
+
+
+def test_stale_and_missing_scv_make_node_unschedulable():
+    async def go():
+        c = FakeCluster()
+        c.add_node("fresh")
+        c.add_node("noscv", scv=False)
+        c.add_node("stale", interval_ms=10)        # 3 × 10 ms freshness window
+        await asyncio.sleep(0.05)
+        await c.start()
+        for i in range(10):
+            c.add_pod(f"p{i}", {"scv/memory": "1000"})
+        assert await c.wait_bound(10)
+        nodes = {c.node_of(f"p{i}") for i in range(10)}
+        await c.stop()
+        return nodes
+    assert run(go()) == {"fresh"}
+
+
+def test_scv_update_revives_stale_node():
+    async def go():
+        c = FakeCluster()
+        c.add_node("n", interval_ms=10)
+        await asyncio.sleep(0.05)
+        await c.start()
+        c.add_pod("p", {"scv/memory": "1000"})
+        await c.wait(lambda: c.sched.failed >= 1, 2)
+        assert not c.server.bind_log
+        obj = dict(c.scv_obj("n"))
+        st = dict(obj["status"])
+        from yoda_scheduler_amd.models.scv import rfc3339
+        st["updateTime"] = rfc3339(time.time() + 5)
+        obj["status"] = st
+        c.server.update("scvs", obj)
+        ok = await c.wait_bound(1, 3)
+        await c.stop()
+        return ok
+    assert run(go())
+
+
+def test_bind_failures_are_retried():
+    async def go():
+        c = FakeCluster(faults=Faults(bind_fail_ratio=0.5, seed=3))
+        c.add_node("n")
+        await c.start()
+        for i in range(20):
+            c.add_pod(f"p{i}", {"scv/memory": "100"})
+        ok = await c.wait_bound(20, 10)
+        errs = c.sched.bind_errors
+        ledger = c.sched.engine.ledger_size
+        await c.stop()
+        return ok, errs, ledger
+    ok, errs, ledger = run(go())
+    assert ok and errs > 0 and ledger == 20
+
+
+def test_priority_queue_order():
+    async def go():
+        c = FakeCluster()
+        c.add_node("n", gpus=1, used_mb=[294912 - 3000])        # room for exactly one 2000 MB pod
+        for i, prio in enumerate([1, 5, 3]):
+            c.add_pod(f"p{prio}", {"scv/memory": "2000", "scv/priority": str(prio)})
+        await c.start()
+        await c.wait_bound(1)
+        await asyncio.sleep(0.05)
+        winners = list(c.server.bind_log)
+        await c.stop()
+        return winners
+    assert run(go()) == ["default/p5"]
+
+
+def test_multi_gpu_gang_gets_distinct_gpus_and_idle_links():
+    async def go():
+        c = FakeCluster()
+        c.add_node("n", gpus=8)
+        # make GPU 0's links busy: a 2-GPU gang should avoid GPU 0
+        obj = dict(c.scv_obj("n"))
+        st = dict(obj["status"])
+        amd = dict(st["amd"])
+        cards = []
+        for card in amd["cards"]:
+            card = dict(card)
+            card["xgmi"] = [dict(l, load=0.95 if card["physicalId"] == 0 or l["peer"] == 0 else 0.0)
+                            for l in card["xgmi"]]
+            cards.append(card)
+        amd["cards"] = cards
+        st["amd"] = amd
+        obj["status"] = st
+        c.server.update("scvs", obj)
+        await c.start()
+        c.add_pod("g4", {"scv/number": "4", "scv/memory": "1000"})
+        c.add_pod("g8", {"scv/number": "8", "scv/memory": "1000"})
+        assert await c.wait_bound(2)
+        out = c.gpus_of("g4"), c.gpus_of("g8")
+        await c.stop()
+        return out
+    g4, g8 = run(go())
+    assert len(set(g4)) == 4 and 0 not in g4
+    assert sorted(g8) == list(range(8))
+
+
+def test_clock_selector_picks_matching_model():
+    async def go():
+        c = FakeCluster()
+        c.add_node("mi355x")
+        c.add_node("mi350x", spec=MI350X)
+        await c.start()
+        c.add_pod("fast", {"scv/clock": "2400", "scv/memory": "1000"})
+        c.add_pod("slow", {"scv/clock": "2200", "scv/memory": "1000"})
+        c.add_pod("none", {"scv/clock": "1000"})
+        await c.wait_bound(2)
+        await c.wait(lambda: c.sched.failed >= 1, 2)
+        r = c.node_of("fast"), c.node_of("slow"), c.node_of("none")
+        await c.stop()
+        return r
+    assert run(go()) == ("mi355x", "mi350x", "")
+
+
+def test_preemption_evicts_lower_priority():
+    async def go():
+        c = FakeCluster()
+        c.add_node("n", gpus=1, used_mb=[294912 - 10000])
+        await c.start()
+        c.add_pod("low", {"scv/memory": "8000"}, priority=1)
+        assert await c.wait_bound(1)
+        c.add_pod("high", {"scv/memory": "8000"}, priority=100)
+        ok = await c.wait(lambda: "default/high" in c.server.bind_log, 5)
+        try:
+            c.pod("low")
+            low_exists = True
+        except Exception:
+            low_exists = False
+        await c.stop()
+        return ok, low_exists
+    ok, low_exists = run(go())
+    assert ok and not low_exists
+
+
+def test_restart_rebuilds_ledger_from_annotations():
+    async def go():
+        c = FakeCluster()
+        c.add_node("n", gpus=2)
+        await c.start()
+        for i in range(6):
+            c.add_pod(f"p{i}", {"scv/memory": "100000"})
+        await c.wait_bound(4, 3)
+        await asyncio.sleep(0.05)
+        before = c.sched.cache.node_gpu_state("n")
+        await c.stop()
+        c2 = FakeCluster(server=c.server)
+        await c2.start()
+        await asyncio.sleep(0.1)
+        after = c2.sched.cache.node_gpu_state("n")
+        await c2.stop()
+        return before, after, len(c.server.bind_log)
+    before, after, nbound = run(go())
+    assert nbound == 4                      # 2 GPUs × 2 pods of 100 GB (288 GB each)
+    assert [g["reserved"] for g in before] == [g["reserved"] for g in after] == [200000, 200000]
+
+
+def test_compat_mode_reproduces_q3_and_oversubscription():
+    async def go():
+        c = FakeCluster(yoda_config(compat=True))
+        c.add_node("n", gpus=1, used_mb=[294912 - 5000])
+        await c.start()
+        for i in range(3):
+            c.add_pod(f"p{i}", {"scv/memory": "4000"})
+        ok = await c.wait_bound(3, 3)        # no HBM ledger in compat: all three "fit"
+        await c.stop()
+        return ok
+    assert run(go())
+
+
+def test_native_default_filters_taints_and_selector():
+    async def go():
+        c = FakeCluster()
+        c.add_node("tainted", taints=[{"key": "gpu", "value": "reserved", "effect": "NoSchedule"}])
+        c.add_node("labeled", labels={"pool": "train"})
+        await c.start()
+        c.add_pod("sel", {"scv/memory": "1"}, nodeSelector={"pool": "train"})
+        c.add_pod("tol", {"scv/memory": "1"}, nodeSelector={"kubernetes.io/hostname": "tainted"},
+                  tolerations=[{"key": "gpu", "operator": "Equal", "value": "reserved", "effect": "NoSchedule"}])
+        c.add_pod("blocked", {"scv/memory": "1"}, nodeSelector={"kubernetes.io/hostname": "tainted"})
+        await c.wait_bound(2)
+        await c.wait(lambda: c.sched.failed >= 1, 2)
+        r = c.node_of("sel"), c.node_of("tol"), c.node_of("blocked")
+        await c.stop()
+        return r
+    assert run(go()) == ("labeled", "tainted", "")
+
+
+def test_hybrid_python_plugins():
+    class OnlyEven(FilterPlugin):
+        name = "OnlyEven"
+
+        def filter(self, state, pod, node_name):
+            return Status.ok() if int(node_name[1:]) % 2 == 0 else Status.unschedulable("odd")
+
+    class PreferHigh(ScorePlugin):
+        name = "PreferHigh"
+
+        def score(self, state, pod, node_name):
+            return int(node_name[1:]) * 10, Status.ok()
+
+    reg = default_registry().with_plugin("OnlyEven", lambda a, h: OnlyEven(a, h)) \
+                            .with_plugin("PreferHigh", lambda a, h: PreferHigh(a, h))
+
+    async def go():
+        cfg = yoda_config(extra_filter=["OnlyEven"], extra_score=["PreferHigh"])
+        cfg["profiles"][0]["plugins"]["score"]["enabled"][-1]["weight"] = 100000
+        c = FakeCluster(cfg, registry=reg)
+        for i in range(6):
+            c.add_node(f"n{i}")
+        await c.start()
+        assert not c.sched.frameworks["yoda-scheduler"].fully_native
+        c.add_pod("p", {"scv/memory": "1"})
+        await c.wait_bound(1)
+        n = c.node_of("p")
+        await c.stop()
+        return n
+    assert run(go()) == "n4"

@@ -197,8 +197,9 @@ class SchedulerCache:
         idx = self.engine.node_index(name)
         if idx < 0:
             return []
-        return [{"total": t, "free": f, "reserved": r, "pods": p, "clock": c, "healthy": h, "phys": ph}
-                for (t, f, r, p, c, h, ph) in self.engine.node_cards(idx)]
+        return [{"total": t, "free": f, "reserved": r, "pods": p, "clock": c, "healthy": h, "phys": ph,
+                 "pending": pe}
+                for (t, f, r, p, c, h, ph, pe) in self.engine.node_cards(idx)]
 
     def snapshot_counts(self) -> dict:
         return {"nodes": len(self.nodes), "scvs": len(self.scvs), "pods": len(self.pods),

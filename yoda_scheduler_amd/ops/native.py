@@ -74,7 +74,7 @@ def push_scv(engine, idx: int, scv: Scv, compat: bool, stale: bool = False) -> N
     cards = compat_card_tuples(scv) if compat else card_tuples(scv)
     engine.set_cards(idx, cards, int(st.card_number) & 0xFFFFFFFFFFFFFFFF,
                      int(st.free_memory_sum) & 0xFFFFFFFFFFFFFFFF,
-                     int(st.total_memory_sum) & 0xFFFFFFFFFFFFFFFF, stale)
+                     int(st.total_memory_sum) & 0xFFFFFFFFFFFFFFFF, stale, float(st.update_time or 0.0))
     nphys, q = link_matrix(scv)
     if nphys:
         engine.set_links(idx, nphys, q)

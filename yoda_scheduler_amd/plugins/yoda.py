@@ -35,6 +35,9 @@ class Yoda(QueueSortPlugin, FilterPlugin, PostFilterPlugin, ScorePlugin):
         a = self.args
         self.compat = bool(a.get("compat", False))
         self.stale_factor = float(a.get("staleFactor", 3.0))
+        # a reservation counts against the sniffed free HBM until a sample taken this long
+        # after it (container start + allocation) is expected to show its usage
+        self.settle_seconds = float(a.get("sampleSettleSeconds", 30.0))
         # "spread" (default) fills a node's GPUs evenly (worst-fit): with HBM-sharing pods
         # it keeps the per-GPU free HBM level, so multi-GPU gangs stay placeable until the
         # node is nearly full. "binpack" (best-fit) keeps whole GPUs empty instead — the
@@ -53,6 +56,7 @@ class Yoda(QueueSortPlugin, FilterPlugin, PostFilterPlugin, ScorePlugin):
 
     def configure_engine(self, engine) -> None:
         engine.set_gang_weights(binpack=self.gpu_strategy == "binpack", **self.gang)
+        engine.settle_seconds = self.settle_seconds
 
     # QueueSort: sort.Less (sort.go:8-10) + FIFO tie-break (Q7)
     def sort_key(self, pi) -> tuple:

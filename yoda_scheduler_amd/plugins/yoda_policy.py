@@ -65,14 +65,17 @@ class NodeView:
     free_memory_sum: int
     total_memory_sum: int
     reserved_mb: Sequence[int] = ()      # per card, from assumed/bound pods (fixed mode)
+    pending_mb: Sequence[int] = ()       # part of reserved the last sample cannot reflect yet
     label_memory_sum: int = 0            # Σ scv/memory label of pods on node (compat Allocate)
     stale: bool = False
 
     def eff_free(self, i: int) -> int:
+        """min(sampled free − pending, total − reserved), floored at 0."""
         c = self.cards[i]
         if not self.reserved_mb:
             return c.free_memory
-        return max(0, min(c.free_memory, c.total_memory - self.reserved_mb[i]))
+        pend = self.pending_mb[i] if self.pending_mb else 0
+        return max(0, min(c.free_memory - pend, c.total_memory - self.reserved_mb[i]))
 
 
 # ------------------------------------------------------------------ predicates
@@ -188,6 +191,22 @@ def calculate_score(mv: MaxValue, req: GpuRequest, node: NodeView, compat: bool 
     """score.CalculateScore → Uint64ToInt64 (scheduler.go:124-128)."""
     s = u64(basic_score(mv, req, node, compat) + allocate_score(node, compat) + actual_score(node, compat))
     return uint64_to_int64(s)
+
+
+def gang_bonus(req: GpuRequest, node: NodeView, link_q: Sequence[int], nphys: int, w=None) -> int:
+    """Fixed-mode node-score bonus for multi-GPU pods: best achievable xGMI quality of a
+    k-GPU set on the node (``parallel/gang.py``), × ``gangWeights.score``."""
+    from ..parallel.gang import GangWeights, GpuView, select
+    w = w or GangWeights()
+    if not (req.has_number and 1 < req.number <= len(node.cards)):
+        return 0
+    m = req.memory if req.has_memory else 0
+    c = req.clock if req.has_clock else 0
+    views = [GpuView(node.eff_free(i), cd.total_memory, cd.phys, cd.numa_node, int(round(cd.cu_occupancy * 100)))
+             for i, cd in enumerate(node.cards)]
+    elig = [i for i in range(len(node.cards)) if card_eligible(req, node, i, m, c)]
+    ok, _sel, q = select(views, elig, req.number, m, link_q, nphys, w)
+    return (q // 100) * w.gang_score if ok else 0
 
 
 def normalize_scores(scores: list[int]) -> list[int]:
