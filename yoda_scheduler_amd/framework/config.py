@@ -99,6 +99,7 @@ class SchedulerConfig:
     bind_concurrency: int = 256
     batch_size: int = 256
     unschedulable_flush_seconds: float = 60.0
+    gc_threshold: tuple = (50_000, 50, 1000)
 
     def profile(self, name: str) -> Optional[Profile]:
         for p in self.profiles:
@@ -213,6 +214,7 @@ def parse_config(doc: dict) -> SchedulerConfig:
     cfg.bind_concurrency = int(_f(rt, "bindConcurrency", cfg.bind_concurrency))
     cfg.batch_size = int(_f(rt, "batchSize", cfg.batch_size))
     cfg.unschedulable_flush_seconds = float(_f(rt, "unschedulableFlushSeconds", cfg.unschedulable_flush_seconds))
+    cfg.gc_threshold = tuple(int(x) for x in _f(rt, "gcThreshold", cfg.gc_threshold))
     if not 0 <= cfg.percentage_of_nodes_to_score <= 100:
         raise ValueError("percentageOfNodesToScore must be in [0, 100]")
     if cfg.pod_initial_backoff_seconds <= 0 or cfg.pod_max_backoff_seconds < cfg.pod_initial_backoff_seconds:

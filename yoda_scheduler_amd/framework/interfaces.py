@@ -68,14 +68,12 @@ class CycleState:
     """Per-cycle scratch map. ``write`` under ``lock`` like upstream v1.20 (the
     reference takes the lock explicitly, ``pkg/yoda/collection/collection.go:53-55``)."""
 
-    __slots__ = ("_data", "_lock", "record_metrics", "skip_filter", "skip_score")
+    __slots__ = ("_data", "_lock", "record_metrics")
 
     def __init__(self) -> None:
         self._data: dict[str, StateData] = {}
-        self._lock = threading.RLock()
+        self._lock = None        # created on first use: most cycles never lock
         self.record_metrics = False
-        self.skip_filter: set[str] = set()
-        self.skip_score: set[str] = set()
 
     def read(self, key: str) -> StateData:
         try:
@@ -90,6 +88,8 @@ class CycleState:
         self._data.pop(key, None)
 
     def lock(self):
+        if self._lock is None:
+            self._lock = threading.RLock()
         return self._lock
 
     def clone(self) -> "CycleState":

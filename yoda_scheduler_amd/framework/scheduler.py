@@ -14,6 +14,8 @@ run through a bounded worker pool behind the client QPS limiter.
 from __future__ import annotations
 
 import asyncio
+import collections
+import gc
 import logging
 import time
 from typing import Callable, Optional
@@ -21,7 +23,7 @@ from typing import Callable, Optional
 from ..kube.informer import Informer
 from ..models.pod import PodInfo, forget_num_id
 from ..ops.native import core, pod_req
-from ..utils import klog
+from ..utils import gctune, klog
 from ..utils.metrics import SchedulerMetrics
 from ..utils.ratelimit import TokenBucket
 from .cache import SchedulerCache
@@ -33,6 +35,8 @@ from .registry import Registry, default_registry
 from .runtime import Framework
 
 log = logging.getLogger("yoda.scheduler")
+
+_EMPTY_STATE = CycleState()      # shared read-only state for all-native cycles
 
 
 class Handle:
@@ -89,7 +93,8 @@ class Scheduler:
         self.queue = SchedulingQueue(qs.sort_key, config.pod_initial_backoff_seconds, config.pod_max_backoff_seconds,
                                      config.unschedulable_flush_seconds, clock=clock)
         self._active_fw: Optional[Framework] = None
-        self._bind_q: asyncio.Queue = asyncio.Queue()
+        self._bind_dq: collections.deque = collections.deque()
+        self._bind_ev = asyncio.Event()
         self._tasks: list[asyncio.Task] = []
         self.informers: dict[str, Informer] = {}
         self.scheduled = 0
@@ -259,7 +264,7 @@ class Scheduler:
         if klog.V(3):
             log.info("pod %s → node %s gpus=%s score=%d feasible=%d", pi.key, node, cards, res[4], res[1])
         self.pending_binds += 1
-        self._bind_q.put_nowait((fw, state, pi, node, cycle, t0))
+        self._enqueue_bind((fw, state, pi, node, cycle, t0))
 
     def _fit_error(self, res) -> str:
         reasons = res[5]
@@ -281,6 +286,8 @@ class Scheduler:
         m = self.metrics
         self.failed += 1
         nominated = ""
+        if state is None:
+            state = CycleState()
         if unschedulable and fw.post_filter:
             for p in fw.post_filter:
                 try:
@@ -351,13 +358,27 @@ class Scheduler:
             results = eng.schedule_batch([p.num_id for p in run], [pod_req(eng, p) for p in run])
             self.metrics.batch_size.observe(len(run))
             for p, res in zip(run, results):
-                self._finish_cycle(fw, CycleState(), p, res, cycle, t0)
+                self._finish_cycle(fw, None, p, res, cycle, t0)   # all-native: no Python state
 
     # ================================================================== binding
+    def _enqueue_bind(self, item: tuple) -> None:
+        self._bind_dq.append(item)
+        if not self._bind_ev.is_set():
+            self._bind_ev.set()
+
     async def _bind_worker(self) -> None:
-        q, m = self._bind_q, self.metrics
+        """Bind workers drain a shared deque and only park when it is empty, so a burst
+        costs one wake-up per worker instead of one per pod; ``bindConcurrency`` workers
+        keep that many binds in flight against a remote apiserver."""
+        dq, ev, m = self._bind_dq, self._bind_ev, self.metrics
         while True:
-            fw, state, pi, node, cycle, t0 = await q.get()
+            if not dq:
+                ev.clear()
+                await ev.wait()
+                continue
+            fw, state, pi, node, cycle, t0 = dq.popleft()
+            if state is None:
+                state = _EMPTY_STATE
             try:
                 await self.limiter.acquire()
                 tb = time.perf_counter()
@@ -429,6 +450,7 @@ class Scheduler:
         self._tasks.append(loop.create_task(self._housekeeping()))
         if wait_sync:
             await self.wait_synced()
+        gctune.tune(self.config.gc_threshold)
 
     async def wait_synced(self) -> None:
         for inf in self.informers.values():

@@ -9,7 +9,7 @@ from __future__ import annotations
 import itertools
 import time
 from dataclasses import dataclass, field
-from typing import Any
+from typing import Any, Optional
 
 from ..utils.quantity import bytes_of, cpu_millis
 from .labels import GpuRequest, parse_gpu_request
@@ -66,63 +66,92 @@ def _terms(terms: list | None) -> list[list[tuple[str, str, list[str]]]]:
     return out
 
 
-@dataclass
 class PodInfo:
-    obj: dict
-    uid: str
-    namespace: str
-    name: str
-    num_id: int
-    labels: dict
-    gpu: GpuRequest
-    scheduler_name: str
-    node_name: str
-    cpu_m: int
-    mem: int
-    priority: int
-    node_selector: dict
-    required_terms: list
-    preferred_terms: list
-    tolerations: list
-    creation: float
-    annotations: dict
-    host_ports: list = field(default_factory=list)
-    # cycle bookkeeping (queue)
-    attempts: int = 0
-    initial_attempt: float = 0.0
-    enqueued: float = 0.0
-    native_req: Any = None          # engine-specific PodReq cache
-    native_owner: Any = None
+    """Parsed pod. ``__slots__`` + a hand-written constructor: one of these is built per
+    pod per informer event on the scheduling hot path."""
+
+    __slots__ = ("obj", "uid", "namespace", "name", "num_id", "labels", "gpu", "scheduler_name", "node_name",
+                 "cpu_m", "mem", "priority", "node_selector", "required_terms", "preferred_terms", "tolerations",
+                 "annotations", "host_ports", "attempts", "initial_attempt", "enqueued", "native_req",
+                 "native_owner", "assigned_cards", "_creation")
+
+    def __init__(self, obj: dict, uid: str, namespace: str, name: str, num_id: int, labels: dict, gpu: GpuRequest,
+                 scheduler_name: str = "default-scheduler", node_name: str = "", cpu_m: int = 0, mem: int = 0,
+                 priority: int = 0, node_selector: Optional[dict] = None, required_terms: Optional[list] = None,
+                 preferred_terms: Optional[list] = None, tolerations: Optional[list] = None,
+                 annotations: Optional[dict] = None, host_ports: Optional[list] = None) -> None:
+        self.obj = obj
+        self.uid = uid
+        self.namespace = namespace
+        self.name = name
+        self.num_id = num_id
+        self.labels = labels
+        self.gpu = gpu
+        self.scheduler_name = scheduler_name
+        self.node_name = node_name
+        self.cpu_m = cpu_m
+        self.mem = mem
+        self.priority = priority
+        self.node_selector = node_selector if node_selector is not None else {}
+        self.required_terms = required_terms if required_terms is not None else []
+        self.preferred_terms = preferred_terms if preferred_terms is not None else []
+        self.tolerations = tolerations if tolerations is not None else []
+        self.annotations = annotations if annotations is not None else {}
+        self.host_ports = host_ports if host_ports is not None else []
+        self.attempts = 0
+        self.initial_attempt = 0.0
+        self.enqueued = 0.0
+        self.native_req: Any = None          # engine-specific PodReq cache
+        self.native_owner: Any = None
+        self.assigned_cards: Optional[list] = None
+        self._creation: Optional[float] = None
 
     @property
     def key(self) -> str:
         return f"{self.namespace}/{self.name}"
 
+    @property
+    def creation(self) -> float:
+        """creationTimestamp (parsed lazily: the hot path never needs it)."""
+        if self._creation is None:
+            self._creation = parse_rfc3339((self.obj.get("metadata") or {}).get("creationTimestamp")) or time.time()
+        return self._creation
+
+    def __repr__(self) -> str:
+        return f"PodInfo({self.key}, gpu={self.gpu}, node={self.node_name!r})"
+
     @classmethod
     def from_obj(cls, obj: dict) -> "PodInfo":
-        meta = obj.get("metadata") or {}
-        spec = obj.get("spec") or {}
+        meta = obj.get("metadata") or _EMPTY
+        spec = obj.get("spec") or _EMPTY
         labels = meta.get("labels") or {}
+        uid = meta.get("uid") or pod_key(obj)
         cpu, mem = _requests(spec)
-        aff = (spec.get("affinity") or {}).get("nodeAffinity") or {}
-        req = (aff.get("requiredDuringSchedulingIgnoredDuringExecution") or {}).get("nodeSelectorTerms")
-        pref = [(int(p.get("weight", 0)), _terms([p.get("preference") or {}])[0])
-                for p in aff.get("preferredDuringSchedulingIgnoredDuringExecution") or []]
-        tols = [(t.get("key") or None, str(t.get("value", "") or ""), t.get("operator", "Equal") or "Equal",
-                 t.get("effect", "") or "") for t in spec.get("tolerations") or []]
-        ports = [(p.get("hostPort"), p.get("protocol", "TCP"), p.get("hostIP", ""))
-                 for c in spec.get("containers") or [] for p in c.get("ports") or [] if p.get("hostPort")]
-        created = parse_rfc3339(meta.get("creationTimestamp")) or time.time()
-        return cls(
-            obj=obj, uid=meta.get("uid") or pod_key(obj), namespace=meta.get("namespace", "default"),
-            name=meta.get("name", ""), num_id=pod_num_id(meta.get("uid") or pod_key(obj)), labels=labels, gpu=parse_gpu_request(labels),
-            scheduler_name=spec.get("schedulerName") or "default-scheduler",
-            node_name=spec.get("nodeName") or "", cpu_m=cpu, mem=mem,
-            priority=int(spec.get("priority") or 0),
-            node_selector=dict(spec.get("nodeSelector") or {}),
-            required_terms=_terms(req), preferred_terms=pref, tolerations=tols, creation=created,
-            annotations=dict(meta.get("annotations") or {}), host_ports=ports,
-        )
+        aff = spec.get("affinity")
+        req = pref = None
+        if aff:
+            na = aff.get("nodeAffinity") or _EMPTY
+            req = _terms((na.get("requiredDuringSchedulingIgnoredDuringExecution") or _EMPTY).get("nodeSelectorTerms"))
+            pref = [(int(p.get("weight", 0)), _terms([p.get("preference") or {}])[0])
+                    for p in na.get("preferredDuringSchedulingIgnoredDuringExecution") or ()]
+        tols = spec.get("tolerations")
+        if tols:
+            tols = [(t.get("key") or None, str(t.get("value", "") or ""), t.get("operator", "Equal") or "Equal",
+                     t.get("effect", "") or "") for t in tols]
+        ports = None
+        for c in spec.get("containers") or ():
+            for p in c.get("ports") or ():
+                if p.get("hostPort"):
+                    (ports := ports or []).append((p.get("hostPort"), p.get("protocol", "TCP"), p.get("hostIP", "")))
+        ns = spec.get("nodeSelector")
+        ann = meta.get("annotations")
+        return cls(obj, uid, meta.get("namespace", "default"), meta.get("name", ""), pod_num_id(uid), labels,
+                   parse_gpu_request(labels), spec.get("schedulerName") or "default-scheduler",
+                   spec.get("nodeName") or "", cpu, mem, int(spec.get("priority") or 0),
+                   dict(ns) if ns else None, req, pref, tols or None, dict(ann) if ann else None, ports)
+
+
+_EMPTY: dict = {}
 
 
 @dataclass
