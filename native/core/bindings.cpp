@@ -110,16 +110,31 @@ PYBIND11_MODULE(_yoda_core, m) {
            [](Engine& e, int32_t idx, bool unsched, const std::vector<std::pair<std::string, std::string>>& labels,
               const std::vector<std::tuple<std::string, std::string, std::string>>& taints, int64_t cpu_m,
               int64_t mem, int64_t pods) {
-             Node& n = e.node(idx);
-             n.unschedulable = unsched;
-             n.labels.clear();
-             for (auto& kv : labels) n.labels[e.intern(kv.first)] = e.intern(kv.second);
-             n.taints.clear();
+             std::vector<std::pair<int32_t, int32_t>> lab;
+             for (auto& kv : labels) lab.emplace_back(e.intern(kv.first), e.intern(kv.second));
+             std::vector<Taint> ts;
              for (auto& t : taints)
-               n.taints.push_back(Taint{e.intern(std::get<0>(t)), e.intern(std::get<1>(t)), effect_of(std::get<2>(t))});
-             n.alloc_cpu_m = cpu_m;
-             n.alloc_mem = mem;
-             n.alloc_pods = pods;
+               ts.push_back(Taint{e.intern(std::get<0>(t)), e.intern(std::get<1>(t)), effect_of(std::get<2>(t))});
+             e.set_node_meta(idx, unsched, lab, ts, cpu_m, mem, pods);
+           })
+      .def("enable_device",
+           [](Engine& e, const std::string& path, int device, int capacity, int min_nodes) {
+             std::string err;
+             bool ok = e.enable_device(path, device, capacity, min_nodes, &err);
+             return py::make_tuple(ok, err);
+           },
+           py::arg("lib_path"), py::arg("device") = 0, py::arg("capacity") = 65536, py::arg("min_nodes") = 256)
+      .def("disable_device", &Engine::disable_device)
+      .def_property_readonly("device_enabled", &Engine::device_enabled)
+      .def_property_readonly("device_cycles", &Engine::device_cycles)
+      .def_property_readonly("device_fallbacks", &Engine::device_fallbacks)
+      .def("device_last_us", &Engine::device_last_us)
+      .def("device_eligible", &Engine::device_eligible)
+      .def("device_cycle",
+           [](Engine& e, const PodReq& r) -> py::object {
+             CycleResult c;
+             if (!e.device_cycle(r, &c)) return py::none();
+             return cycle_tuple(c);
            })
       // cards: list of (total, free, clock, bandwidth, core, power, healthy, phys, numa, occ_q)
       .def("set_cards",

@@ -1,8 +1,14 @@
 // Native scheduling engine: see engine.hpp for the design notes.
 #include "engine.hpp"
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <chrono>
+#include <climits>
+#include <cstring>
+
+#include "yoda_dev_abi.h"
 #include <cstdlib>
 #include <stdexcept>
 
@@ -80,7 +86,10 @@ Engine::Engine(bool compat, int threads) : compat_(compat) {
   unsched_key_ = intern("node.kubernetes.io/unschedulable");
 }
 
-Engine::~Engine() { delete pool_; }
+Engine::~Engine() {
+  disable_device();
+  delete pool_;
+}
 
 int32_t Engine::intern(const std::string& s) {
   auto it = string_idx_.find(s);
@@ -107,6 +116,7 @@ int32_t Engine::upsert_node(const std::string& name) {
   nodes_[idx].alive = true;
   node_idx_[name] = idx;
   ++live_;
+  mark_dirty(idx);
   return idx;
 }
 
@@ -123,10 +133,35 @@ void Engine::remove_node(int32_t idx) {
     else ++it;
   }
   node_idx_.erase(nodes_[idx].name);
+  hard_taint_nodes_ -= nodes_[idx].hard_taint;
+  prefer_taint_nodes_ -= nodes_[idx].prefer_taint;
   nodes_[idx] = Node();
   nodes_[idx].alive = false;
   free_slots_.push_back(idx);
   --live_;
+  mark_dirty(idx);
+}
+
+void Engine::set_node_meta(int32_t idx, bool unschedulable, const std::vector<std::pair<int32_t, int32_t>>& labels,
+                           const std::vector<Taint>& taints, int64_t cpu_m, int64_t mem, int64_t pods) {
+  Node& n = nodes_.at(idx);
+  n.unschedulable = unschedulable;
+  n.labels.clear();
+  for (auto& kv : labels) n.labels[kv.first] = kv.second;
+  n.taints = taints;
+  hard_taint_nodes_ -= n.hard_taint;
+  prefer_taint_nodes_ -= n.prefer_taint;
+  n.hard_taint = n.prefer_taint = false;
+  for (const Taint& t : taints) {
+    if (t.effect == kPreferNoSchedule) n.prefer_taint = true;
+    else n.hard_taint = true;
+  }
+  hard_taint_nodes_ += n.hard_taint;
+  prefer_taint_nodes_ += n.prefer_taint;
+  n.alloc_cpu_m = cpu_m;
+  n.alloc_mem = mem;
+  n.alloc_pods = pods;
+  mark_dirty(idx);
 }
 
 double Engine::now() const {
@@ -170,6 +205,7 @@ void Engine::set_cards(int32_t idx, std::vector<Card> cards, uint64_t card_numbe
     n.nphys = np;
     n.link_q.assign((size_t)np * np, 10000);
   }
+  mark_dirty(idx);
 }
 
 void Engine::clear_scv(int32_t idx) {
@@ -179,6 +215,7 @@ void Engine::clear_scv(int32_t idx) {
   n.card_number = n.free_sum = n.total_sum = 0;
   n.nphys = 0;
   n.link_q.clear();
+  mark_dirty(idx);
 }
 
 void Engine::set_links(int32_t idx, int32_t nphys, std::vector<int32_t> q) {
@@ -186,6 +223,7 @@ void Engine::set_links(int32_t idx, int32_t nphys, std::vector<int32_t> q) {
   if ((int64_t)q.size() != (int64_t)nphys * nphys) throw std::invalid_argument("link matrix size");
   n.nphys = nphys;
   n.link_q = std::move(q);
+  mark_dirty(idx);
 }
 
 const Assignment* Engine::assignment(uint64_t pod) const {
@@ -225,6 +263,7 @@ bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::ve
   n.pod_count += 1;
   if (a.has_label_mem) n.label_mem_sum += a.label_mem;
   ledger_.emplace(pod, std::move(a));
+  mark_dirty(idx);
   return true;
 }
 
@@ -254,6 +293,7 @@ bool Engine::release(uint64_t pod) {
     n.req_mem -= a.mem;
     n.pod_count -= 1;
     if (a.has_label_mem) n.label_mem_sum -= a.label_mem;
+    mark_dirty(a.node);
   }
   ledger_.erase(it);
   return true;
@@ -737,6 +777,13 @@ CycleResult Engine::schedule(uint64_t pod, const PodReq& req, bool assume, const
                              const std::vector<int64_t>& extra) {
   ++cycles_;
   CycleResult r;
+  if (dev_ctx_ && candidates.empty() && extra.empty() && live_ >= dev_min_nodes_ && device_eligible(req)) {
+    if (schedule_device(req, &r)) {
+      if (assume && r.node >= 0) reserve(pod, req, r.node, r.cards);
+      return r;
+    }
+    r = CycleResult();
+  }
   std::vector<int32_t> feas = feasible_nodes(req, candidates, &r.reason_counts);
   r.feasible = (int32_t)feas.size();
   r.evaluated = candidates.empty() ? live_ : (int32_t)candidates.size();
@@ -794,6 +841,215 @@ std::vector<CycleResult> Engine::schedule_batch(const std::vector<uint64_t>& pod
   static const std::vector<int64_t> nox;
   for (size_t i = 0; i < pods.size(); ++i) out.push_back(schedule(pods[i], *reqs[i], true, none, nox));
   return out;
+}
+
+// ============================================================== device scorer (dlopen)
+using dev_create_t = void* (*)(int, int, char*, int);
+using dev_destroy_t = void (*)(void*);
+using dev_upload_t = int (*)(void*, int, const int32_t*, const yoda_dev_node_t*);
+using dev_schedule_t = int (*)(void*, int, const yoda_dev_req_t*, const uint8_t*, yoda_dev_result_t*);
+using dev_last_us_t = float (*)(void*);
+
+void Engine::mark_dirty(int32_t idx) {
+  if (!dev_ctx_ || idx < 0) return;
+  if ((int32_t)dirty_.size() <= idx) dirty_.resize(idx + 1, 0);
+  if (!dirty_[idx]) {
+    dirty_[idx] = 1;
+    dirty_list_.push_back(idx);
+  }
+}
+
+bool Engine::enable_device(const std::string& lib_path, int device, int capacity, int min_nodes, std::string* err) {
+  disable_device();
+  void* lib = dlopen(lib_path.c_str(), RTLD_NOW | RTLD_GLOBAL);
+  if (!lib) {
+    if (err) *err = std::string("dlopen: ") + dlerror();
+    return false;
+  }
+  auto create = (dev_create_t)dlsym(lib, "yoda_dev_create");
+  fn_destroy_ = dlsym(lib, "yoda_dev_destroy");
+  fn_upload_ = dlsym(lib, "yoda_dev_upload");
+  fn_schedule_ = dlsym(lib, "yoda_dev_schedule");
+  fn_last_us_ = dlsym(lib, "yoda_dev_last_us");
+  if (!create || !fn_destroy_ || !fn_upload_ || !fn_schedule_ || !fn_last_us_) {
+    if (err) *err = "libyoda_hip.so lacks the yoda_dev_* entry points";
+    dlclose(lib);
+    return false;
+  }
+  char buf[256] = {0};
+  void* ctx = create(device, capacity, buf, sizeof buf);
+  if (!ctx) {
+    if (err) *err = buf;
+    dlclose(lib);
+    return false;
+  }
+  dev_lib_ = lib;
+  dev_ctx_ = ctx;
+  dev_cap_ = capacity;
+  dev_min_nodes_ = min_nodes;
+  // everything is dirty for the first device cycle
+  dirty_.assign(nodes_.size(), 0);
+  dirty_list_.clear();
+  for (int32_t i = 0; i < (int32_t)nodes_.size(); ++i) mark_dirty(i);
+  return true;
+}
+
+void Engine::disable_device() {
+  if (dev_ctx_) ((dev_destroy_t)fn_destroy_)(dev_ctx_);
+  if (dev_lib_) dlclose(dev_lib_);
+  dev_ctx_ = dev_lib_ = nullptr;
+  dirty_.clear();
+  dirty_list_.clear();
+}
+
+float Engine::device_last_us() const { return dev_ctx_ ? ((dev_last_us_t)fn_last_us_)(dev_ctx_) : 0.f; }
+
+bool Engine::pack_node(int32_t idx, void* out) const {
+  yoda_dev_node_t* row = (yoda_dev_node_t*)out;
+  std::memset(row, 0, sizeof(*row));
+  const Node& n = nodes_[idx];
+  if (!n.alive) return true;   // flags 0 = dead slot
+  if (n.cards.size() > YODA_DEV_CARDS || n.nphys > YODA_DEV_CARDS || n.card_number > UINT32_MAX) return false;
+  row->flags = YODA_DEV_ALIVE | (n.has_scv ? YODA_DEV_HAS_SCV : 0) | (n.stale ? YODA_DEV_STALE : 0) |
+               (n.unschedulable ? YODA_DEV_UNSCHEDULABLE : 0);
+  row->ncards = (uint8_t)n.cards.size();
+  row->nphys = (uint8_t)n.nphys;
+  row->card_number = (uint32_t)n.card_number;
+  row->alloc_cpu = n.alloc_cpu_m;
+  row->alloc_mem = n.alloc_mem;
+  row->alloc_pods = n.alloc_pods;
+  row->req_cpu = n.req_cpu_m;
+  row->req_mem = n.req_mem;
+  row->pod_count = n.pod_count;
+  if (n.alloc_mem > (int64_t)1 << 56 || n.alloc_cpu_m > (int64_t)1 << 56) return false;
+  for (size_t c = 0; c < n.cards.size(); ++c) {
+    const Card& x = n.cards[c];
+    const uint64_t vals[8] = {x.total_mb, x.free_mb, x.reserved_mb, x.pending_mb, x.clock, x.bandwidth, x.core, x.power};
+    for (uint64_t v : vals)
+      if (v > UINT32_MAX) return false;
+    if (x.phys < 0 || x.phys >= YODA_DEV_CARDS) return false;
+    row->cards[c] = yoda_dev_card_t{(uint32_t)x.total_mb, (uint32_t)x.free_mb, (uint32_t)x.reserved_mb,
+                                    (uint32_t)x.pending_mb, (uint32_t)x.clock, (uint32_t)x.bandwidth,
+                                    (uint32_t)x.core, (uint32_t)x.power};
+    row->healthy[c] = x.healthy;
+    row->phys[c] = (uint8_t)x.phys;
+    row->numa[c] = (uint8_t)(x.numa & 63);
+    row->occ[c] = (uint16_t)std::min(std::max(x.occ_q, 0), 65535);
+  }
+  for (int a = 0; a < n.nphys; ++a)
+    for (int b = 0; b < n.nphys; ++b)
+      row->linkq[a][b] = (uint16_t)std::min(std::max(n.link_q[(size_t)a * n.nphys + b], 0), 65535);
+  return true;
+}
+
+bool Engine::flush_dirty() {
+  if (dirty_list_.empty()) return true;
+  std::vector<yoda_dev_node_t> rows(dirty_list_.size());
+  for (size_t i = 0; i < dirty_list_.size(); ++i)
+    if (!pack_node(dirty_list_[i], &rows[i])) return false;   // stays dirty; CPU path this cycle
+  if (((dev_upload_t)fn_upload_)(dev_ctx_, (int)dirty_list_.size(), dirty_list_.data(), rows.data()) != 0)
+    return false;
+  for (int32_t i : dirty_list_) dirty_[i] = 0;
+  dirty_list_.clear();
+  return true;
+}
+
+bool Engine::device_eligible(const PodReq& req) const {
+  if (!dev_ctx_ || compat_) return false;
+  if ((int32_t)nodes_.size() > dev_cap_) return false;
+  if (wt_.enum_limit < 70) return false;                       // device search is always exhaustive
+  if (score_w_[S_NODE_AFFINITY] && !req.preferred_terms.empty()) return false;
+  if (score_w_[S_TAINT_TOLERATION] && prefer_taint_nodes_ > 0) return false;
+  int64_t wsum = 0;
+  for (int i = 0; i < S_NUM; ++i) wsum += score_w_[i] < 0 ? -score_w_[i] : score_w_[i];
+  if (wsum * 200 >= ((int64_t)1 << 38)) return false;          // key = (final << 24) | perm
+  if (wt_.w_link < 0 || wt_.w_link > 1000000 || wt_.w_numa > 1000000 || wt_.w_fit > 1000000 || wt_.w_occ > 1000000)
+    return false;
+  return true;
+}
+
+Reason Engine::candidate_reason(const PodReq& req, const Node& n) const {
+  if ((filters_ & F_NODE_NAME) && req.node_name > 0 && strings_[req.node_name] != n.name) return RS_NODE_NAME;
+  if ((filters_ & F_NODE_AFFINITY) && !affinity_ok(req, n)) return RS_AFFINITY;
+  if ((filters_ & F_TAINT_TOLERATION) && !taints_ok(req, n)) return RS_TAINT;
+  return RS_OK;
+}
+
+bool Engine::schedule_device(const PodReq& req, CycleResult* r) {
+  if (!flush_dirty()) {
+    ++dev_fallbacks_;
+    return false;
+  }
+  yoda_dev_req_t d{};
+  d.number = req.has_number ? req.number : 1;
+  d.memory = req.has_memory ? req.memory : 0;
+  d.clock = req.has_clock ? req.clock : 0;
+  d.clock_min = req.clock_min;
+  d.cpu_m = req.cpu_m;
+  d.mem = req.mem;
+  d.has_number = req.has_number;
+  d.has_memory = req.has_memory;
+  d.has_clock = req.has_clock;
+  d.binpack = wt_.gpu_binpack;
+  d.filters = filters_;
+  d.w_yoda = score_w_[S_YODA];
+  d.w_least = score_w_[S_LEAST_ALLOCATED];
+  d.w_balanced = score_w_[S_BALANCED_ALLOCATION];
+  d.w_most = score_w_[S_MOST_ALLOCATED];
+  // no PreferNoSchedule taints anywhere: TaintToleration normalises every node to 100
+  d.w_const = score_w_[S_TAINT_TOLERATION] * kMaxNodeScore;
+  d.w_link = wt_.w_link;
+  d.w_numa = wt_.w_numa;
+  d.w_fit = wt_.w_fit;
+  d.w_occ = wt_.w_occ;
+  d.w_gang_score = wt_.w_gang_score;
+  Taint ut{unsched_key_, 0, kNoSchedule};
+  for (const Toleration& x : req.tolerations)
+    if (tolerates(x, ut)) d.tolerates_unschedulable = 1;
+  // random tie-break: bijective p(i) = (i*mul + add) mod 2^24 and its inverse
+  uint32_t mul = (uint32_t)(rng_() | 1u) & 0xFFFFFFu, add = (uint32_t)rng_() & 0xFFFFFFu;
+  uint32_t inv = mul;   // Newton: inv = inv * (2 - mul*inv), 5 steps reach 2^24
+  for (int i = 0; i < 5; ++i) inv *= 2u - mul * inv;
+  d.perm_mul = mul;
+  d.perm_add = add;
+  d.perm_inv = inv & 0xFFFFFFu;
+  std::vector<uint8_t> cand;
+  const bool need_cand = ((filters_ & F_NODE_NAME) && req.node_name > 0) ||
+                         ((filters_ & F_NODE_AFFINITY) && (!req.node_selector.empty() || !req.required_terms.empty())) ||
+                         ((filters_ & F_TAINT_TOLERATION) && hard_taint_nodes_ > 0);
+  if (need_cand) {
+    cand.assign(nodes_.size(), 0);
+    for (int32_t i = 0; i < (int32_t)nodes_.size(); ++i)
+      if (nodes_[i].alive) cand[i] = (uint8_t)candidate_reason(req, nodes_[i]);
+    d.use_candidates = 1;
+  }
+  yoda_dev_result_t res{};
+  int rc = ((dev_schedule_t)fn_schedule_)(dev_ctx_, (int)nodes_.size(), &d, need_cand ? cand.data() : nullptr, &res);
+  if (rc != 0) {
+    ++dev_fallbacks_;
+    return false;
+  }
+  ++dev_cycles_;
+  r->node = res.node;
+  r->feasible = res.feasible;
+  r->evaluated = live_;
+  r->score = res.score;
+  r->reason_counts.assign(RS_NUM, 0);
+  for (int i = 1; i < RS_NUM && i < YODA_DEV_REASONS; ++i)
+    if (i != RS_DEAD) r->reason_counts[i] = res.reasons[i];
+  r->cards.clear();
+  r->gang_quality = 10000;
+  if (r->node >= 0 && (filters_ & F_YODA)) {
+    for (int c = 0; c < YODA_DEV_CARDS; ++c)
+      if ((res.mask >> c) & 1u) r->cards.push_back(c);
+    r->gang_quality = res.quality;
+  }
+  return true;
+}
+
+bool Engine::device_cycle(const PodReq& req, CycleResult* out) {
+  if (!device_eligible(req)) return false;
+  return schedule_device(req, out);
 }
 
 }  // namespace yoda

@@ -90,6 +90,7 @@ struct Node {
   int64_t alloc_cpu_m = 0, alloc_mem = 0, alloc_pods = 0;
   int64_t req_cpu_m = 0, req_mem = 0, pod_count = 0;
   uint64_t label_mem_sum = 0;         // Σ scv/memory labels of pods on node (compat Allocate)
+  bool hard_taint = false, prefer_taint = false;   // has NoSchedule/NoExecute, PreferNoSchedule taints
   double sample_ts = 0;               // unix time of the Scv sample the cards came from
   std::vector<uint64_t> pods;         // ledger entries on this node (for pending recompute)
 };
@@ -233,7 +234,31 @@ class Engine {
 
   uint64_t cycles() const { return cycles_; }
 
+  // ---- k8s node facts (keeps the taint census the device path needs)
+  void set_node_meta(int32_t idx, bool unschedulable, const std::vector<std::pair<int32_t, int32_t>>& labels,
+                     const std::vector<Taint>& taints, int64_t cpu_m, int64_t mem, int64_t pods);
+
+  // ---- gfx950 device scorer (libyoda_hip.so, loaded with dlopen; see native/hip/scorer.hip)
+  // Offloads whole cycles for clusters of >= min_nodes nodes when the pod/profile is
+  // representable on the device (fixed mode, <= 8 GPUs per node, ...); otherwise, or on
+  // any device error, the CPU path runs. Device cycles score every feasible node (the
+  // adaptive percentageOfNodesToScore sampling exists to bound CPU cost).
+  bool enable_device(const std::string& lib_path, int device, int capacity, int min_nodes, std::string* err);
+  void disable_device();
+  bool device_enabled() const { return dev_ctx_ != nullptr; }
+  uint64_t device_cycles() const { return dev_cycles_; }
+  uint64_t device_fallbacks() const { return dev_fallbacks_; }
+  float device_last_us() const;
+  bool device_eligible(const PodReq& req) const;
+  // parity hook: run one device cycle without reserving; false if not eligible/failed
+  bool device_cycle(const PodReq& req, CycleResult* out);
+
  private:
+  void mark_dirty(int32_t idx);
+  bool pack_node(int32_t idx, void* row) const;   // row: yoda_dev_node_t*
+  bool flush_dirty();
+  bool schedule_device(const PodReq& req, CycleResult* r);
+  Reason candidate_reason(const PodReq& req, const Node& n) const;
   bool taints_ok(const PodReq& req, const Node& n) const;
   bool affinity_ok(const PodReq& req, const Node& n) const;
   bool term_matches(const SelTerm& t, const Node& n) const;
@@ -260,6 +285,19 @@ class Engine {
   std::mt19937_64 rng_{0x59d4};
   double settle_s_ = 30.0;
   double fixed_now_ = -1.0;
+  // device scorer state
+  void* dev_lib_ = nullptr;
+  void* dev_ctx_ = nullptr;
+  int dev_cap_ = 0;
+  int dev_min_nodes_ = 256;
+  uint64_t dev_cycles_ = 0, dev_fallbacks_ = 0;
+  std::vector<char> dirty_;
+  std::vector<int32_t> dirty_list_;
+  int32_t hard_taint_nodes_ = 0, prefer_taint_nodes_ = 0;
+  void* fn_destroy_ = nullptr;
+  void* fn_upload_ = nullptr;
+  void* fn_schedule_ = nullptr;
+  void* fn_last_us_ = nullptr;
   double now() const;
   bool is_pending(const Node& n, const Assignment& a) const { return a.t_res > n.sample_ts - settle_s_; }
   int32_t next_start_ = 0;

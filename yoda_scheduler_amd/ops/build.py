@@ -49,13 +49,13 @@ def _run(cmd: list[str], what: str) -> None:
 
 def build_core(force: bool = False) -> Path:
     srcs = [NATIVE / "core" / "engine.cpp", NATIVE / "core" / "bindings.cpp"]
-    deps = srcs + [NATIVE / "core" / "engine.hpp"]
+    deps = srcs + [NATIVE / "core" / "engine.hpp", NATIVE / "hip" / "yoda_dev_abi.h"]
     out = OUT / f"_yoda_core{EXT}"
     if force or _stale(out, deps):
         cxx = os.environ.get("CXX", "g++")
         _run([cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-Wall",
-              "-Wno-unused-function", *_pybind_includes(), f"-I{NATIVE / 'core'}",
-              *map(str, srcs), "-o", str(out), "-lpthread"], "core")
+              "-Wno-unused-function", *_pybind_includes(), f"-I{NATIVE / 'core'}", f"-I{NATIVE / 'hip'}",
+              *map(str, srcs), "-o", str(out), "-lpthread", "-ldl"], "core")
     return out
 
 

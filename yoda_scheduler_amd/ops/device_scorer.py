@@ -1,0 +1,127 @@
+"""gfx950 device placement scorer — enabling it on an engine, and the smoke/parity helpers.
+
+The native engine ``dlopen``s ``libyoda_hip.so`` itself and calls ``yoda_dev_schedule`` from
+C++ inside ``Engine::schedule`` whenever the cluster has at least ``min_nodes`` nodes and
+the pod is representable on the device (see ``Engine::device_eligible``), so the Python
+control plane never touches the device on the hot path. Node records are mirrored
+incrementally: every engine mutation marks its node dirty and dirty rows are scattered
+into the device table before the next device cycle.
+"""
+from __future__ import annotations
+
+import ctypes
+import random
+
+from .hip import PATH, lib as hip_lib
+
+
+def declare(lib: ctypes.CDLL) -> None:
+    lib.yoda_dev_last_us.argtypes = [ctypes.c_void_p]
+    lib.yoda_dev_last_us.restype = ctypes.c_float
+
+
+def enable(engine, device: int = 0, capacity: int = 65536, min_nodes: int = 256) -> None:
+    """Attach the device scorer to ``engine``; raises if the GPU path cannot start."""
+    hip_lib()          # builds the library if needed; shares torch's HIP runtime if loaded
+    ok, err = engine.enable_device(str(PATH), device, capacity, min_nodes)
+    if not ok:
+        raise RuntimeError(f"device scorer unavailable: {err}")
+
+
+def synthetic_cluster(engine, n_nodes: int, seed: int = 0, compat: bool = False, busy: float = 0.5):
+    """Populate ``engine`` with ``n_nodes`` random MI355X/MI350X nodes (8 GPUs each)."""
+    from ..models.device import MI350X, MI355X, make_node
+    from ..models.pod import NodeInfo
+    from ..models.scv import Card, Scv, ScvStatus, XgmiLink
+    from .native import push_node, push_scv
+    rng = random.Random(seed)
+    for i in range(n_nodes):
+        spec = MI355X if rng.random() < 0.75 else MI350X
+        info = NodeInfo.from_obj(make_node(f"node-{i}", cpu=str(rng.choice([96, 192])),
+                                           memory=rng.choice(["1Ti", "2Ti"])))
+        idx = push_node(engine, info)
+        cards = []
+        for g in range(8):
+            used = rng.randint(0, int(spec.hbm_mb * busy))
+            cards.append(Card(id=g, health="Healthy" if rng.random() > 0.02 else "Unhealthy",
+                              total_memory=spec.hbm_mb, free_memory=spec.hbm_mb - used, clock=spec.max_sclk_mhz,
+                              bandwidth=spec.hbm_bw_gbps, core=spec.cus, power=spec.power_w, physical_id=g,
+                              numa_node=int(g >= 4), cu_occupancy=rng.randint(0, 100)))
+        for c in cards:
+            c.xgmi = [XgmiLink(peer=d.phys, load=rng.choice([0.0, 0.0, 0.1, 0.5, 0.9])) for d in cards if d is not c]
+        st = ScvStatus(card_list=cards, update_time=0.0)
+        st.recompute_sums()
+        push_scv(engine, idx, Scv(name=f"node-{i}", status=st), compat,
+                 stale=rng.random() < 0.01)
+
+
+def random_request(engine, rng: random.Random, uid: str):
+    from ..models.pod import PodInfo
+    from .native import pod_req
+    lab = {}
+    r = rng.random()
+    if r < 0.5:
+        lab["scv/memory"] = str(rng.choice([1024, 4096, 65536, 200000]))
+    elif r < 0.8:
+        lab.update({"scv/number": str(rng.choice([2, 4, 8])), "scv/memory": str(rng.choice([1024, 16384]))})
+    elif r < 0.9:
+        lab.update({"scv/clock": str(rng.choice([2400, 2200])), "scv/memory": "2048"})
+    else:
+        lab["scv/number"] = str(rng.choice([1, 3, 9]))
+    pi = PodInfo.from_obj({"metadata": {"name": uid, "uid": uid, "labels": lab},
+                           "spec": {"containers": [{"name": "c", "resources": {"requests": {
+                               "cpu": rng.choice(["1", "8"]), "memory": "16Gi"}}}]}})
+    return pi, pod_req(engine, pi)
+
+
+def compare_cycle(engine, req) -> dict:
+    """Run one device cycle and the CPU reference on the same state; return a diff dict
+    (empty = bit-exact). Ties may pick different nodes; the device's node must be one of
+    the CPU's argmax set, and its GPU set must equal the CPU's choice on that node."""
+    dev = engine.device_cycle(req)
+    if dev is None:
+        return {"skipped": True}
+    feas, reasons = engine.feasible_nodes(req, [])
+    diffs = {}
+    if dev[1] != len(feas):
+        diffs["feasible"] = (dev[1], len(feas))
+    if list(dev[5]) != list(reasons):
+        diffs["reasons"] = (list(dev[5]), list(reasons))
+    if feas:
+        if len(feas) == 1:
+            best, arg = 0, {feas[0]}
+        else:
+            sc = engine.score_nodes(req, feas)
+            best = max(sc)
+            arg = {n for n, s in zip(feas, sc) if s == best}
+        if dev[4] != best:
+            diffs["score"] = (dev[4], best)
+        if dev[0] not in arg:
+            diffs["node"] = (dev[0], sorted(arg)[:5])
+        ok, cards, q = engine.select_gpus(req, dev[0])
+        if list(dev[3]) != list(cards) or (ok and dev[6] != q):
+            diffs["cards"] = (list(dev[3]), list(cards), dev[6], q)
+    elif dev[0] != -1:
+        diffs["node"] = (dev[0], -1)
+    return diffs
+
+
+def smoke(device: int = 0, n_nodes: int = 512, pods: int = 32) -> dict:
+    """Device vs CPU parity on a synthetic cluster (used by ``__graft_entry__.smoke``)."""
+    from .native import core
+    eng = core().Engine(False, 1)
+    eng.set_percentage_of_nodes_to_score(100)
+    synthetic_cluster(eng, n_nodes, seed=1)
+    enable(eng, device, capacity=max(1024, n_nodes), min_nodes=1)
+    rng = random.Random(7)
+    bad = []
+    for k in range(pods):
+        pi, req = random_request(eng, rng, f"smoke-{k}")
+        d = compare_cycle(eng, req)
+        if d:
+            bad.append(d)
+        res = eng.schedule(pi.num_id, req, True)      # device path + reserve → next pod sees it
+    if bad:
+        raise AssertionError(f"device scorer mismatch: {bad[:3]}")
+    return {"device_cycles": eng.device_cycles, "fallbacks": eng.device_fallbacks,
+            "last_us": round(eng.device_last_us(), 1)}
