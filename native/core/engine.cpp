@@ -936,9 +936,16 @@ bool Engine::pack_node(int32_t idx, void* out) const {
     row->numa[c] = (uint8_t)(x.numa & 63);
     row->occ[c] = (uint16_t)std::min(std::max(x.occ_q, 0), 65535);
   }
-  for (int a = 0; a < n.nphys; ++a)
-    for (int b = 0; b < n.nphys; ++b)
-      row->linkq[a][b] = (uint16_t)std::min(std::max(n.link_q[(size_t)a * n.nphys + b], 0), 65535);
+  // card-pair link quality, resolved here so the device needs no phys indirection
+  // (same rule as gang_objective: same physical GPU or unknown link → 10000)
+  for (size_t a = 0; a < n.cards.size(); ++a)
+    for (size_t b = 0; b < n.cards.size(); ++b) {
+      const int32_t pa = n.cards[a].phys, pb = n.cards[b].phys;
+      int32_t q = 10000;
+      if (pa != pb && pa < n.nphys && pb < n.nphys) q = n.link_q[(size_t)pa * n.nphys + pb];
+      if (q < 0 || q > 65535) return false;   // not representable: CPU path
+      row->linkq[a][b] = (uint16_t)q;
+    }
   return true;
 }
 

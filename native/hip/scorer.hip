@@ -3,16 +3,26 @@
 // mode) — Filter → PreScore maxima → yoda Score + xGMI gang search → NormalizeScore →
 // weighted sum → selectHost.
 //
-// Mapping to CDNA4: a 64-lane wave owns one node; lanes 0..7 own its GPU slots (card
-// eligibility via one 64-bit __ballot), and for the gang search all 64 lanes enumerate
-// the 256 GPU subsets of the node (4 per lane) and reduce the best one with __shfl_xor.
-// Blocks are 4 waves and grid-stride over nodes; per-block LDS reductions cut the
-// cross-workgroup atomics to a few per block (maxima, min/max raw score, argmax key),
-// keeping them off the single-address serialisation cliff (cdna guide G12).
-// Four launches per pod; cluster-global accumulators are re-armed by the last kernel so no
-// memset sits between pods. No MFMA: the work is integer compare/reduce, not matmul-shaped.
+// CDNA4 mapping
+//  * a 64-lane wave scores 8 nodes at once: lane group g (8 lanes) owns node base+g and
+//    lane s of the group owns GPU slot s, so eligibility is one 64-bit __ballot split in
+//    8-bit fields and every per-node reduction is a 3-step __shfl_xor inside the group;
+//  * the k-GPU gang search walks a constant table of the C(8,k) subsets with k set bits
+//    (≤ 70), 8 lanes per node, skipping subsets with ineligible GPUs; the objective uses
+//    per-lane register tables (effective free HBM, total, occupancy, NUMA, the 28
+//    card-pair xGMI qualities resolved by the host) — integer math mirrors the CPU;
+//  * 64-bit divisions (the scoring is full of them) go through an exact double-estimate
+//    + integer-correction path instead of the ~100-instruction software divide;
+//  * blocks of 4 waves grid-stride over nodes; per-block LDS reductions, XCD-sharded
+//    counters and check-before-atomic max/min keep cross-workgroup atomics to a handful;
+//  * the select kernel's last block (agent-scope ticket, release/acquire per the CDNA
+//    visibility rules) decodes the winner, writes the result straight into mapped pinned
+//    host memory and re-arms the accumulators — 3 launches and no memcpy per pod in the
+//    steady state (dirty node rows ride in a patch kernel's arguments).
+// No MFMA: the work is integer compare/reduce, not matmul-shaped.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <climits>
 #include <cstdint>
 #include <cstdio>
@@ -31,156 +41,231 @@ constexpr int RS_UNSCHEDULABLE = 1, RS_RESOURCES = 5, RS_NO_SCV = 6, RS_STALE = 
 
 constexpr int kWaves = 4;
 constexpr int kBlock = 64 * kWaves;
+constexpr int kGroup = 8;                 // lanes per node
+constexpr int kNodesPerWave = 64 / kGroup;
+constexpr int kPatchRows = 6;             // dirty rows passed by value (6 × 512 B + idx < 4 KiB of kernarg)
+constexpr int kShards = 8;
 
 struct Globals {
   unsigned long long maxima[6];   // seeded 1 (collection.go:31-38)
   unsigned long long raw_lo;      // seeded ULLONG_MAX
   unsigned long long raw_hi;      // seeded 0 (scheduler.go:134 `highest := 0`)
   unsigned long long best_key;    // (final << 24) | perm(node)
-  int reasons[YODA_DEV_REASONS];
-  int feasible;
+  // counters sharded 8 ways (blockIdx % 8 ≈ one XCD under round-robin dispatch; speed
+  // only) so 2k blocks do not serialise on one address; the select kernel sums shards
+  int reasons[kShards][YODA_DEV_REASONS];
+  int feasible[kShards];
+  unsigned int ticket;
   int pad[3];
 };
+
+struct PatchArgs {
+  int n;
+  int32_t idx[kPatchRows];
+  yoda_dev_node_t rows[kPatchRows];
+};
+
+// subsets of {0..7} grouped by popcount, ascending (lexicographic order is irrelevant:
+// ties are broken explicitly by `better`)
+struct SubsetTable {
+  uint8_t masks[256];
+  uint16_t start[10];
+};
+
+__constant__ SubsetTable c_subsets;
+
+SubsetTable make_subsets() {
+  SubsetTable t{};
+  int p = 0;
+  for (int k = 0; k <= 8; ++k) {
+    t.start[k] = (uint16_t)p;
+    for (int m = 0; m < 256; ++m)
+      if (__builtin_popcount(m) == k) t.masks[p++] = (uint8_t)m;
+  }
+  t.start[9] = (uint16_t)p;
+  return t;
+}
 
 __host__ __device__ inline void globals_reset(Globals* g) {
   for (int k = 0; k < 6; ++k) g->maxima[k] = 1;
   g->raw_lo = ULLONG_MAX;
   g->raw_hi = 0;
   g->best_key = 0;
-  for (int k = 0; k < YODA_DEV_REASONS; ++k) g->reasons[k] = 0;
-  g->feasible = 0;
+  for (int s = 0; s < kShards; ++s) {
+    for (int k = 0; k < YODA_DEV_REASONS; ++k) g->reasons[s][k] = 0;
+    g->feasible[s] = 0;
+  }
+  g->ticket = 0;
 }
 
-__device__ __forceinline__ uint64_t eff_free(const yoda_dev_card_t& c) {
-  uint64_t sampled = c.free > c.pending ? (uint64_t)(c.free - c.pending) : 0;
-  uint64_t cap = c.total > c.reserved ? (uint64_t)(c.total - c.reserved) : 0;
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// relaxed agent-scope read of an accumulator (memory-side value, any XCD)
+__device__ __forceinline__ unsigned long long peek(unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// atomics only when this block can still change the accumulator
+__device__ __forceinline__ void max_if(unsigned long long* p, unsigned long long v) {
+  if (v > peek(p)) atomicMax(p, v);
+}
+__device__ __forceinline__ void min_if(unsigned long long* p, unsigned long long v) {
+  if (v < peek(p)) atomicMin(p, v);
+}
+
+// Exact floor(n / d) for d > 0: a correctly rounded double quotient is within 1 of the
+// truth while n < 2^53; one integer multiply-subtract fixes it. Larger n (not produced
+// by realistic clusters) take the software divide.
+__device__ __forceinline__ uint64_t udiv(uint64_t n, uint64_t d) {
+  if (n < (1ull << 53) && d < (1ull << 53)) {
+    uint64_t q = (uint64_t)((double)n / (double)d);
+    const uint64_t qd = q * d;
+    if (qd > n) --q;
+    else if (n - qd >= d) ++q;
+    return q;
+  }
+  return n / d;
+}
+// truncating int division by a tiny divisor (≤ 28): every non-integer quotient is at least
+// 1/28 away from an integer, far beyond the double rounding error → exact
+__device__ __forceinline__ int32_t sdiv_small(int32_t n, int32_t d) { return (int32_t)((double)n / (double)d); }
+
+__device__ __forceinline__ uint64_t eff_free(uint32_t free, uint32_t pending, uint32_t total, uint32_t reserved) {
+  const uint64_t sampled = free > pending ? (uint64_t)(free - pending) : 0;
+  const uint64_t cap = total > reserved ? (uint64_t)(total - reserved) : 0;
   return sampled < cap ? sampled : cap;
 }
 
-__device__ __forceinline__ bool card_ok(const yoda_dev_req_t& r, const yoda_dev_node_t* nd, int c) {
-  const yoda_dev_card_t& cd = nd->cards[c];
-  if (!nd->healthy[c]) return false;
-  if (eff_free(cd) < r.memory) return false;
-  if (r.has_clock && (uint64_t)cd.clock != r.clock) return false;
-  if (r.clock_min && (uint64_t)cd.clock < r.clock_min) return false;
-  return true;
-}
-
-__device__ __forceinline__ unsigned long long wave_max8(unsigned long long v) {
-  // lanes 0..7 hold the values of one node (others 0); reduce within each 8-lane group
+template <typename T>
+__device__ __forceinline__ T gmax(T v) {   // max over the 8 lanes of a group
+#pragma unroll
   for (int off = 4; off > 0; off >>= 1) {
-    unsigned long long o = __shfl_xor(v, off, 64);
+    const T o = __shfl_xor(v, off, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T gsum(T v) {
+#pragma unroll
+  for (int off = 4; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wmax_across_groups(T v) {   // max over the 8 groups of a wave
+#pragma unroll
+  for (int off = 8; off < 64; off <<= 1) {
+    const T o = __shfl_xor(v, off, 64);
     v = o > v ? o : v;
   }
   return v;
 }
 
-__device__ __forceinline__ unsigned long long wave_sum8(unsigned long long v) {
-  for (int off = 4; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
+// ------------------------------------------------------------------ dirty-row patch
+__global__ void k_patch(PatchArgs a, yoda_dev_node_t* __restrict__ nodes) {
+  const int rec = threadIdx.x >> 5, part = threadIdx.x & 31;
+  if (rec >= a.n) return;
+  const uint4* src = reinterpret_cast<const uint4*>(&a.rows[rec]);
+  reinterpret_cast<uint4*>(nodes + a.idx[rec])[part] = src[part];
+}
+
+__global__ void k_scatter(const yoda_dev_node_t* __restrict__ stage, const int32_t* __restrict__ idx, int n,
+                          yoda_dev_node_t* __restrict__ nodes) {
+  const int rec = blockIdx.x * (blockDim.x / 32) + (threadIdx.x >> 5);
+  if (rec >= n) return;
+  const uint4* src = reinterpret_cast<const uint4*>(stage + rec);
+  reinterpret_cast<uint4*>(nodes + idx[rec])[threadIdx.x & 31] = src[threadIdx.x & 31];
 }
 
 // ------------------------------------------------------------------ K1: filter + maxima
 __global__ __launch_bounds__(kBlock) void k_filter(const yoda_dev_node_t* __restrict__ nodes, int n,
-                                                   const yoda_dev_req_t* __restrict__ req_p,
-                                                   const uint8_t* __restrict__ cand, uint8_t* __restrict__ feas,
-                                                   uint8_t* __restrict__ elig, Globals* __restrict__ g) {
+                                                   const yoda_dev_req_t r, const uint8_t* __restrict__ cand,
+                                                   uint8_t* __restrict__ feas, uint8_t* __restrict__ elig,
+                                                   Globals* __restrict__ g) {
   __shared__ unsigned long long s_max[kWaves][6];
   __shared__ int s_reason[YODA_DEV_REASONS];
   __shared__ int s_feas;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = uniform(threadIdx.x >> 6);
+  const int grp = lane >> 3, sub = lane & 7;
   if (threadIdx.x < YODA_DEV_REASONS) s_reason[threadIdx.x] = 0;
   if (threadIdx.x == 0) s_feas = 0;
-  if (lane < 6) s_max[wave][lane] = 1;
   __syncthreads();
-  const yoda_dev_req_t r = *req_p;
   const bool yoda = (r.filters & F_YODA) != 0;
-  for (int i = blockIdx.x * kWaves + wave; i < n; i += gridDim.x * kWaves) {
-    const yoda_dev_node_t* nd = nodes + i;
-    const uint8_t flags = nd->flags;
+  unsigned long long wmx[6] = {1, 1, 1, 1, 1, 1};
+  int nfeas = 0;
+  const int stride = gridDim.x * kWaves * kNodesPerWave;
+  for (int base = uniform((blockIdx.x * kWaves + wave) * kNodesPerWave); base < n; base += stride) {
+    const int i = base + grp;
+    const bool valid = i < n;
+    const yoda_dev_node_t* nd = nodes + (valid ? i : n - 1);
+    // every load of the node issued up front: one memory round trip per node
+    const uint8_t flags = valid ? nd->flags : 0, ncards = nd->ncards;
+    const uint32_t card_number = nd->card_number;
+    const int64_t pod_count = nd->pod_count, alloc_pods = nd->alloc_pods, alloc_cpu = nd->alloc_cpu,
+                  req_cpu = nd->req_cpu, alloc_mem = nd->alloc_mem, req_mem = nd->req_mem;
+    const yoda_dev_card_t cd = nd->cards[sub];
+    const uint8_t healthy = nd->healthy[sub];
+    const uint8_t cnd = (r.use_candidates && valid) ? cand[i] : 0;
     int reason = 0;
     if (!(flags & YODA_DEV_ALIVE)) {
       reason = RS_DEAD;
     } else if ((r.filters & F_NODE_UNSCHEDULABLE) && (flags & YODA_DEV_UNSCHEDULABLE) && !r.tolerates_unschedulable) {
       reason = RS_UNSCHEDULABLE;
     } else if (r.filters & F_NODE_RESOURCES_FIT) {
-      if (nd->pod_count + 1 > nd->alloc_pods) reason = RS_RESOURCES;
-      else if (r.cpu_m > 0 && nd->alloc_cpu < r.cpu_m + nd->req_cpu) reason = RS_RESOURCES;
-      else if (r.mem > 0 && nd->alloc_mem < r.mem + nd->req_mem) reason = RS_RESOURCES;
+      if (pod_count + 1 > alloc_pods) reason = RS_RESOURCES;
+      else if (r.cpu_m > 0 && alloc_cpu < r.cpu_m + req_cpu) reason = RS_RESOURCES;
+      else if (r.mem > 0 && alloc_mem < r.mem + req_mem) reason = RS_RESOURCES;
     }
-    if (!reason && r.use_candidates && cand[i]) reason = cand[i];
-    uint32_t emask = 0;
+    if (!reason && cnd) reason = cnd;
+    bool yoda_stage = false;
     if (!reason && yoda) {
-      if (!(flags & YODA_DEV_HAS_SCV)) {
-        reason = RS_NO_SCV;
-      } else if (r.has_number ? !(r.number <= (uint64_t)nd->card_number) : !(nd->card_number > 0)) {
-        reason = RS_GPU_NUMBER;
-      } else if (flags & YODA_DEV_STALE) {
-        reason = RS_STALE;
-      } else {
-        const bool e = lane < nd->ncards && card_ok(r, nd, lane);
-        emask = (uint32_t)(__ballot(e) & 0xFFu);
-        if ((uint64_t)__popc(emask) < r.number) reason = RS_GPU_FIT;
-      }
+      if (!(flags & YODA_DEV_HAS_SCV)) reason = RS_NO_SCV;
+      else if (r.has_number ? !(r.number <= (uint64_t)card_number) : !(card_number > 0)) reason = RS_GPU_NUMBER;
+      else if (flags & YODA_DEV_STALE) reason = RS_STALE;
+      else yoda_stage = true;
     }
-    if (lane == 0) {
-      feas[i] = reason == 0;
+    const uint64_t ef = eff_free(cd.free, cd.pending, cd.total, cd.reserved);
+    const bool e = yoda_stage && sub < ncards && healthy && ef >= r.memory &&
+                   (!r.has_clock || (uint64_t)cd.clock == r.clock) && (!r.clock_min || (uint64_t)cd.clock >= r.clock_min);
+    const uint32_t emask = (uint32_t)((__ballot(e) >> (grp * kGroup)) & 0xFFu);
+    if (yoda_stage && (uint64_t)__popc(emask) < r.number) reason = RS_GPU_FIT;
+    const bool ok = valid && reason == 0;
+    if (valid && sub == 0) {
+      feas[i] = ok;
       elig[i] = (uint8_t)emask;
-      if (reason) atomicAdd(&s_reason[reason], 1);
-      else atomicAdd(&s_feas, 1);
+      if (reason && reason != RS_DEAD) atomicAdd(&s_reason[reason], 1);
+      else if (reason == RS_DEAD) atomicAdd(&s_reason[RS_DEAD], 1);
     }
-    if (!reason && yoda) {
-      unsigned long long v[6] = {0, 0, 0, 0, 0, 0};
-      if (lane < 8 && ((emask >> lane) & 1u)) {
-        const yoda_dev_card_t& cd = nd->cards[lane];
-        v[0] = cd.bandwidth; v[1] = cd.clock; v[2] = cd.core; v[3] = eff_free(cd); v[4] = cd.power; v[5] = cd.total;
-      }
+    if (sub == 0 && ok) ++nfeas;
+    if (yoda) {
+      const bool take = ok && ((emask >> sub) & 1u);
+      unsigned long long v[6];
+      v[0] = take ? cd.bandwidth : 0; v[1] = take ? cd.clock : 0; v[2] = take ? cd.core : 0;
+      v[3] = take ? ef : 0; v[4] = take ? cd.power : 0; v[5] = take ? cd.total : 0;
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
-        unsigned long long m = wave_max8(v[k]);
-        if (lane == 0 && m > s_max[wave][k]) s_max[wave][k] = m;
+        const unsigned long long m = wmax_across_groups(gmax(v[k]));
+        wmx[k] = m > wmx[k] ? m : wmx[k];
       }
     }
+  }
+  nfeas = gsum(nfeas);
+  nfeas += __shfl_xor(nfeas, 8, 64);
+  nfeas += __shfl_xor(nfeas, 16, 64);
+  nfeas += __shfl_xor(nfeas, 32, 64);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s_max[wave][k] = wmx[k];
+    if (nfeas) atomicAdd(&s_feas, nfeas);
   }
   __syncthreads();
   if (threadIdx.x < 6) {
     unsigned long long m = 1;
     for (int w = 0; w < kWaves; ++w) m = s_max[w][threadIdx.x] > m ? s_max[w][threadIdx.x] : m;
-    if (m > 1) atomicMax(&g->maxima[threadIdx.x], m);
+    if (m > 1) max_if(&g->maxima[threadIdx.x], m);
   }
-  if (threadIdx.x < YODA_DEV_REASONS && s_reason[threadIdx.x]) atomicAdd(&g->reasons[threadIdx.x], s_reason[threadIdx.x]);
-  if (threadIdx.x == 0 && s_feas) atomicAdd(&g->feasible, s_feas);
-}
-
-// gang objective of subset `m` (bit i = card i) — engine.cpp Engine::gang_objective
-__device__ __forceinline__ int64_t gang_obj(const yoda_dev_req_t& r, const yoda_dev_node_t* nd, uint32_t m,
-                                            const uint64_t* ef, int64_t* link_bad_out) {
-  const int64_t k = __popc(m);
-  const int64_t P = k * (k - 1) / 2;
-  int64_t qsum = 0, free_after = 0, total = 0, occ = 0;
-  uint64_t numa_mask = 0;
-  for (int a = 0; a < YODA_DEV_CARDS; ++a) {
-    if (!((m >> a) & 1u)) continue;
-    numa_mask |= 1ull << (nd->numa[a] & 63);
-    free_after += (int64_t)(ef[a] - r.memory);
-    total += (int64_t)nd->cards[a].total;
-    occ += nd->occ[a];
-    for (int b = a + 1; b < YODA_DEV_CARDS; ++b) {
-      if (!((m >> b) & 1u)) continue;
-      int32_t q = 10000;
-      const int pa = nd->phys[a], pb = nd->phys[b];
-      if (pa != pb && pa < nd->nphys && pb < nd->nphys) q = nd->linkq[pa][pb];
-      qsum += q;
-    }
-  }
-  const int64_t link_bad = P ? (P * 10000 - qsum) * 100 / P : 0;
-  const int64_t d = __popcll(numa_mask);
-  const int64_t numa_bad = k > 1 ? (d - 1) * 1000000 / (k - 1) : 0;
-  const int64_t leftover = total ? free_after * 1000000 / total : 0;
-  const int64_t fit = r.binpack ? leftover : 1000000 - leftover;
-  const int64_t occ_bad = k ? occ * 100 / k : 0;
-  *link_bad_out = link_bad;
-  return r.w_link * link_bad + r.w_numa * numa_bad + r.w_fit * fit + r.w_occ * occ_bad;
+  const int sh = blockIdx.x % kShards;
+  if (threadIdx.x < YODA_DEV_REASONS && s_reason[threadIdx.x]) atomicAdd(&g->reasons[sh][threadIdx.x], s_reason[threadIdx.x]);
+  if (threadIdx.x == 0 && s_feas) atomicAdd(&g->feasible[sh], s_feas);
 }
 
 // (obj, mask) a better than b: smaller objective, then lexicographically smaller subset
@@ -192,103 +277,155 @@ __device__ __forceinline__ bool better(int64_t oa, uint32_t ma, int64_t ob, uint
 
 // ------------------------------------------------------------------ K2: scores + gang search
 __global__ __launch_bounds__(kBlock) void k_score(const yoda_dev_node_t* __restrict__ nodes, int n,
-                                                  const yoda_dev_req_t* __restrict__ req_p,
-                                                  const uint8_t* __restrict__ feas, const uint8_t* __restrict__ elig,
-                                                  int64_t* __restrict__ raw, int64_t* __restrict__ total_out,
-                                                  uint32_t* __restrict__ mask_out, int32_t* __restrict__ quality_out,
-                                                  Globals* __restrict__ g) {
+                                                  const yoda_dev_req_t r, const uint8_t* __restrict__ feas,
+                                                  const uint8_t* __restrict__ elig, int64_t* __restrict__ raw,
+                                                  int64_t* __restrict__ total_out, uint32_t* __restrict__ mask_out,
+                                                  int32_t* __restrict__ quality_out, Globals* __restrict__ g) {
   __shared__ unsigned long long s_lo[kWaves], s_hi[kWaves];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
-    s_lo[wave] = ULLONG_MAX;
-    s_hi[wave] = 0;
-  }
-  const yoda_dev_req_t r = *req_p;
+  const int lane = threadIdx.x & 63, wave = uniform(threadIdx.x >> 6);
+  const int grp = lane >> 3, sub = lane & 7;
   const bool yoda_f = (r.filters & F_YODA) != 0;
   const bool yoda_s = yoda_f && r.w_yoda != 0;
-  const unsigned long long* mx = g->maxima;
-  const unsigned long long mx0 = mx[0], mx1 = mx[1], mx2 = mx[2], mx3 = mx[3], mx4 = mx[4], mx5 = mx[5];
-  const uint64_t k = r.has_number ? r.number : 1;
-  for (int i = blockIdx.x * kWaves + wave; i < n; i += gridDim.x * kWaves) {
-    if (!feas[i]) continue;     // wave-uniform
-    const yoda_dev_node_t* nd = nodes + i;
-    const uint32_t emask = elig[i];
-    // ---- per-GPU data every lane needs for the subset search
+  const uint64_t mx0 = g->maxima[0], mx1 = g->maxima[1], mx2 = g->maxima[2], mx3 = g->maxima[3], mx4 = g->maxima[4],
+                 mx5 = g->maxima[5];
+  const int k = (int)(r.has_number ? (r.number > 64 ? 64 : r.number) : 1);
+  const bool search = yoda_f && k >= 1 && k <= YODA_DEV_CARDS;
+  const int32_t P = k * (k - 1) / 2;
+  const int s_begin = search ? c_subsets.start[k] : 0, s_end = search ? c_subsets.start[k + 1] : 0;
+  const int64_t nz_cpu = r.cpu_m > 0 ? r.cpu_m : 100;
+  const int64_t nz_mem = r.mem > 0 ? r.mem : 200LL * 1024 * 1024;
+  unsigned long long lo = ULLONG_MAX, hi = 0;
+  const int stride = gridDim.x * kWaves * kNodesPerWave;
+  for (int base = uniform((blockIdx.x * kWaves + wave) * kNodesPerWave); base < n; base += stride) {
+    const int i = base + grp;
+    const bool act = i < n && feas[i];
+    if (!__any(act)) continue;
+    const yoda_dev_node_t* nd = nodes + (i < n ? i : n - 1);
+    const uint32_t emask = act ? elig[i] : 0u;
+    const uint8_t ncards = nd->ncards;
+    // ---- per-node register tables (every lane of the group holds the whole node)
     uint64_t ef[YODA_DEV_CARDS];
+    uint32_t tot[YODA_DEV_CARDS], occ[YODA_DEV_CARDS], numa[YODA_DEV_CARDS];
 #pragma unroll
-    for (int c = 0; c < YODA_DEV_CARDS; ++c) ef[c] = eff_free(nd->cards[c]);
-    // ---- gang / GPU-set selection (also the Reserve choice for the winning node)
+    for (int a = 0; a < YODA_DEV_CARDS; ++a) {
+      const uint4 lo4 = reinterpret_cast<const uint4*>(&nd->cards[a])[0];   // total, free, reserved, pending
+      ef[a] = eff_free(lo4.y, lo4.w, lo4.x, lo4.z);
+      tot[a] = lo4.x;
+      occ[a] = nd->occ[a];
+      numa[a] = nd->numa[a] & 63u;
+    }
+    uint32_t lq[32];   // 64 u16 card-pair qualities, packed 2 per dword
+    {
+      const uint4* q4 = reinterpret_cast<const uint4*>(&nd->linkq[0][0]);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const uint4 v = q4[t];
+        lq[4 * t] = v.x; lq[4 * t + 1] = v.y; lq[4 * t + 2] = v.z; lq[4 * t + 3] = v.w;
+      }
+    }
+    // ---- gang / GPU-set selection (the Reserve choice if this node wins)
     uint32_t best_m = 0;
-    int64_t best_o = LLONG_MAX, best_lb = 0;
+    int64_t best_o = LLONG_MAX;
+    int32_t best_lb = 0;
     bool found = false;
-    if (yoda_f && k >= 1 && k <= YODA_DEV_CARDS) {
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t m = (uint32_t)(lane + 64 * j);
-        if ((uint64_t)__popc(m) != k || (m & ~emask)) continue;
-        int64_t lb;
-        const int64_t o = gang_obj(r, nd, m, ef, &lb);
+    if (search && act) {
+      for (int t = s_begin + sub; t < s_end; t += kGroup) {
+        const uint32_t m = c_subsets.masks[t];
+        if (m & ~emask) continue;
+        int32_t qsum = 0;
+        uint64_t nmask = 0;
+        uint64_t fa = 0, tt = 0;
+        uint32_t oc = 0;
+#pragma unroll
+        for (int a = 0; a < YODA_DEV_CARDS; ++a) {
+          const bool ia = (m >> a) & 1u;
+          nmask |= ia ? (1ull << numa[a]) : 0ull;
+          fa += ia ? ef[a] - r.memory : 0;
+          tt += ia ? tot[a] : 0;
+          oc += ia ? occ[a] : 0u;
+#pragma unroll
+          for (int b = a + 1; b < YODA_DEV_CARDS; ++b) {
+            const int idx = a * YODA_DEV_CARDS + b;
+            const int32_t q = (int32_t)((lq[idx >> 1] >> ((idx & 1) * 16)) & 0xFFFFu);
+            qsum += (ia && ((m >> b) & 1u)) ? q : 0;
+          }
+        }
+        const int32_t lb = P ? sdiv_small((P * 10000 - qsum) * 100, P) : 0;
+        const int32_t d = __popcll(nmask);
+        const int64_t numa_bad = k > 1 ? (int64_t)sdiv_small((d - 1) * 1000000, k - 1) : 0;
+        const int64_t leftover = tt ? (int64_t)udiv(fa * 1000000ull, tt) : 0;
+        const int64_t fit = r.binpack ? leftover : 1000000 - leftover;
+        const int64_t occ_bad = (int64_t)sdiv_small((int32_t)(oc * 100u), k);
+        const int64_t o = r.w_link * (int64_t)lb + r.w_numa * numa_bad + r.w_fit * fit + r.w_occ * occ_bad;
         if (!found || better(o, m, best_o, best_m)) {
           best_o = o; best_m = m; best_lb = lb; found = true;
         }
       }
-      for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+      for (int off = 4; off > 0; off >>= 1) {
         const int64_t oo = __shfl_xor(best_o, off, 64);
         const uint32_t om = __shfl_xor(best_m, off, 64);
-        const int64_t ol = __shfl_xor(best_lb, off, 64);
+        const int32_t ol = __shfl_xor(best_lb, off, 64);
         const int of = __shfl_xor((int)found, off, 64);
         if (of && (!found || better(oo, om, best_o, best_m))) {
           best_o = oo; best_m = om; best_lb = ol; found = true;
         }
       }
-    }
-    const int32_t quality = found ? (int32_t)(10000 - best_lb / 100) : 10000;
-    // ---- yoda raw score (algorithm.go:28-87 with the Q1/Q2/Q3/Q4 fixes)
-    unsigned long long basic = 0, tot = 0, fre = 0, alloc = 0;
-    if (lane < nd->ncards) {
-      const yoda_dev_card_t& cd = nd->cards[lane];
-      tot = cd.total;
-      fre = ef[lane];
-      alloc = cd.reserved;
-      if ((emask >> lane) & 1u) {
-        const uint64_t bw = (uint64_t)cd.bandwidth * 100 / mx0;
-        const uint64_t clk = (uint64_t)cd.clock * 100 / mx1;
-        const uint64_t core = (uint64_t)cd.core * 100 / mx2;
-        const uint64_t pw = (uint64_t)cd.power * 100 / mx4;
-        const uint64_t fm = ef[lane] * 100 / mx3;
-        const uint64_t tm = (uint64_t)cd.total * 100 / mx5;
-        basic = (bw + clk + core + pw) + fm * 2 + tm;
+    } else {
+      // keep the shuffles wave-uniform for inactive groups
+#pragma unroll
+      for (int off = 4; off > 0; off >>= 1) {
+        (void)__shfl_xor(best_o, off, 64);
+        (void)__shfl_xor(best_m, off, 64);
+        (void)__shfl_xor(best_lb, off, 64);
+        (void)__shfl_xor((int)found, off, 64);
       }
     }
-    basic = wave_sum8(basic);
-    tot = wave_sum8(tot);
-    fre = wave_sum8(fre);
-    alloc = wave_sum8(alloc);
-    if (lane == 0) {
+    const int32_t quality = found ? 10000 - sdiv_small(best_lb, 100) : 10000;
+    // ---- yoda raw score (algorithm.go:28-87 with the Q1/Q2/Q3/Q4 fixes); lane sub = card sub
+    uint64_t basic = 0, tsum = 0, fsum = 0, asum = 0;
+    if (act && sub < ncards) {
+      const yoda_dev_card_t cd = nd->cards[sub];
+      tsum = cd.total;
+      fsum = ef[0];
+#pragma unroll
+      for (int a = 1; a < YODA_DEV_CARDS; ++a) fsum = sub == a ? ef[a] : fsum;
+      asum = cd.reserved;
+      if ((emask >> sub) & 1u) {
+        basic = udiv((uint64_t)cd.bandwidth * 100, mx0) + udiv((uint64_t)cd.clock * 100, mx1) +
+                udiv((uint64_t)cd.core * 100, mx2) + udiv((uint64_t)cd.power * 100, mx4) +
+                udiv(fsum * 100, mx3) * 2 + udiv((uint64_t)cd.total * 100, mx5);
+      }
+    }
+    basic = gsum(basic);
+    tsum = gsum(tsum);
+    fsum = gsum(fsum);
+    asum = gsum(asum);
+    if (act && sub == 0) {
       int64_t s_out = 0;
       if (yoda_s) {
-        const uint64_t actual = tot ? (fre * 100 / tot) * 2 : 0;
-        const uint64_t allocate = (tot == 0 || tot < alloc) ? 0 : (tot - alloc) * 100 / tot * 3;
+        const uint64_t actual = tsum ? udiv(fsum * 100, tsum) * 2 : 0;
+        const uint64_t allocate = (tsum == 0 || tsum < asum) ? 0 : udiv((tsum - asum) * 100, tsum) * 3;
         uint64_t s = basic + allocate + actual;
-        if (r.has_number && r.number > 1 && r.number <= nd->ncards && found)
+        if (r.has_number && r.number > 1 && r.number <= ncards && found)
           s += (uint64_t)(quality / 100) * (uint64_t)r.w_gang_score;
         s_out = s > (uint64_t)LLONG_MAX ? 0 : (int64_t)s;
         const unsigned long long us = (unsigned long long)s_out;
-        if (us < s_lo[wave]) s_lo[wave] = us;
-        if (us > s_hi[wave]) s_hi[wave] = us;
+        lo = us < lo ? us : lo;
+        hi = us > hi ? us : hi;
       }
       // upstream default scores (engine.cpp Engine::score_nodes)
-      const int64_t nz_cpu = r.cpu_m > 0 ? r.cpu_m : 100;
-      const int64_t nz_mem = r.mem > 0 ? r.mem : 200LL * 1024 * 1024;
       const int64_t rc = nd->req_cpu + nz_cpu, rm = nd->req_mem + nz_mem;
+      const int64_t ac = nd->alloc_cpu, am = nd->alloc_mem;
       int64_t least = 0, most = 0, extra = r.w_const;
-      if (nd->alloc_cpu > 0 && rc <= nd->alloc_cpu) least += (nd->alloc_cpu - rc) * 100 / nd->alloc_cpu;
-      if (nd->alloc_mem > 0 && rm <= nd->alloc_mem) least += (nd->alloc_mem - rm) * 100 / nd->alloc_mem;
-      if (nd->alloc_cpu > 0) most += (rc < nd->alloc_cpu ? rc : nd->alloc_cpu) * 100 / nd->alloc_cpu;
-      if (nd->alloc_mem > 0) most += (rm < nd->alloc_mem ? rm : nd->alloc_mem) * 100 / nd->alloc_mem;
+      if (ac > 0 && rc <= ac) least += (int64_t)udiv((uint64_t)(ac - rc) * 100, (uint64_t)ac);
+      if (am > 0 && rm <= am) least += (int64_t)udiv((uint64_t)(am - rm) * 100, (uint64_t)am);
+      if (ac > 0) most += (int64_t)udiv((uint64_t)(rc < ac ? rc : ac) * 100, (uint64_t)ac);
+      if (am > 0) most += (int64_t)udiv((uint64_t)(rm < am ? rm : am) * 100, (uint64_t)am);
       extra += r.w_least * (least / 2) + r.w_most * (most / 2);
       if (r.w_balanced) {
-        const double cf = nd->alloc_cpu > 0 ? (double)rc / (double)nd->alloc_cpu : 1.0;
-        const double mf = nd->alloc_mem > 0 ? (double)rm / (double)nd->alloc_mem : 1.0;
+        const double cf = ac > 0 ? (double)rc / (double)ac : 1.0;
+        const double mf = am > 0 ? (double)rm / (double)am : 1.0;
         const int64_t b = (cf >= 1 || mf >= 1) ? 0 : (int64_t)((1.0 - fabs(cf - mf)) * 100);
         extra += r.w_balanced * b;
       }
@@ -298,43 +435,53 @@ __global__ __launch_bounds__(kBlock) void k_score(const yoda_dev_node_t* __restr
       quality_out[i] = quality;
     }
   }
+  // wave-level min/max of the raw score (lanes that scored nothing hold the identities)
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long ol = __shfl_xor(lo, off, 64), oh = __shfl_xor(hi, off, 64);
+    lo = ol < lo ? ol : lo;
+    hi = oh > hi ? oh : hi;
+  }
+  if (lane == 0) {
+    s_lo[wave] = lo;
+    s_hi[wave] = hi;
+  }
   __syncthreads();
   if (threadIdx.x == 0 && yoda_s) {
-    unsigned long long lo = ULLONG_MAX, hi = 0;
+    unsigned long long blo = ULLONG_MAX, bhi = 0;
     for (int w = 0; w < kWaves; ++w) {
-      lo = s_lo[w] < lo ? s_lo[w] : lo;
-      hi = s_hi[w] > hi ? s_hi[w] : hi;
+      blo = s_lo[w] < blo ? s_lo[w] : blo;
+      bhi = s_hi[w] > bhi ? s_hi[w] : bhi;
     }
-    if (lo != ULLONG_MAX) atomicMin(&g->raw_lo, lo);
-    if (hi) atomicMax(&g->raw_hi, hi);
+    if (blo != ULLONG_MAX) min_if(&g->raw_lo, blo);
+    if (bhi) max_if(&g->raw_hi, bhi);
   }
 }
 
-// ------------------------------------------------------------------ K3: normalize + argmax
-__global__ __launch_bounds__(kBlock) void k_select(int n, const yoda_dev_req_t* __restrict__ req_p,
-                                                   const uint8_t* __restrict__ feas, const int64_t* __restrict__ raw,
-                                                   const int64_t* __restrict__ total, Globals* __restrict__ g) {
-  __shared__ unsigned long long s_key[kBlock / 64];
+// ------------------------------------------------------------------ K3: normalize + argmax + result
+__global__ __launch_bounds__(kBlock) void k_select(int n, const yoda_dev_req_t r, const uint8_t* __restrict__ feas,
+                                                   const int64_t* __restrict__ raw, const int64_t* __restrict__ total,
+                                                   const uint32_t* __restrict__ mask, const int32_t* __restrict__ quality,
+                                                   Globals* __restrict__ g, yoda_dev_result_t* __restrict__ out) {
+  __shared__ unsigned long long s_key[kWaves];
+  __shared__ bool s_last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const yoda_dev_req_t r = *req_p;
   const bool yoda_s = (r.filters & F_YODA) && r.w_yoda != 0;
   // scheduler.go:132-157: highest seeded 0, lowest = min; equal → lowest − 1
   const int64_t hi = (int64_t)g->raw_hi;
   int64_t lo = (int64_t)g->raw_lo;
   if (hi == lo) --lo;
-  const int64_t den = (int64_t)((uint64_t)hi - (uint64_t)lo);
+  const uint64_t den = (uint64_t)hi - (uint64_t)lo;
   unsigned long long best = 0;
   for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     if (!feas[i]) continue;
     int64_t f = total[i];
-    if (yoda_s) {
-      const int64_t num = (int64_t)(((uint64_t)raw[i] - (uint64_t)lo) * 100ull);
-      f += (num / den) * r.w_yoda;
-    }
+    if (yoda_s) f += (int64_t)udiv(((uint64_t)raw[i] - (uint64_t)lo) * 100ull, den) * r.w_yoda;
     const uint32_t p = ((uint32_t)i * r.perm_mul + r.perm_add) & 0xFFFFFFu;
     const unsigned long long key = ((unsigned long long)f << 24) | p;
     best = key > best ? key : best;
   }
+#pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const unsigned long long o = __shfl_xor(best, off, 64);
     best = o > best ? o : best;
@@ -343,47 +490,45 @@ __global__ __launch_bounds__(kBlock) void k_select(int n, const yoda_dev_req_t* 
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long b = 0;
-    for (int w = 0; w < kBlock / 64; ++w) b = s_key[w] > b ? s_key[w] : b;
-    if (b) atomicMax(&g->best_key, b);
+    for (int w = 0; w < kWaves; ++w) b = s_key[w] > b ? s_key[w] : b;
+    if (b) max_if(&g->best_key, b);
+    // release this block's contribution, then take a ticket (agent scope: other XCDs)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned t = __hip_atomic_fetch_add(&g->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == gridDim.x - 1);
   }
-}
-
-// ------------------------------------------------------------------ K4: result + re-arm
-__global__ void k_finish(const yoda_dev_req_t* __restrict__ req_p, const uint32_t* __restrict__ mask,
-                         const int32_t* __restrict__ quality, Globals* __restrict__ g,
-                         yoda_dev_result_t* __restrict__ out) {
-  if (threadIdx.x != 0) return;
-  const yoda_dev_req_t r = *req_p;
-  out->feasible = g->feasible;
-  if (g->feasible == 0) {
-    out->node = -1;
-    out->score = 0;
-    out->mask = 0;
-    out->quality = 0;
+  __syncthreads();
+  if (!s_last || threadIdx.x != 0) return;
+  // last block: every other block's atomicMax has landed
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const unsigned long long key = __hip_atomic_load(&g->best_key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int nf = 0;
+  for (int s = 0; s < kShards; ++s) nf += g->feasible[s];
+  yoda_dev_result_t res;
+  res.feasible = nf;
+  if (nf == 0) {
+    res.node = -1;
+    res.score = 0;
+    res.mask = 0;
+    res.quality = 0;
   } else {
-    const unsigned long long key = g->best_key;
     const uint32_t p = (uint32_t)(key & 0xFFFFFFull);
     const int32_t node = (int32_t)(((p - r.perm_add) * r.perm_inv) & 0xFFFFFFu);
-    out->node = node;
-    out->score = g->feasible == 1 ? 0 : (int64_t)(key >> 24);
-    out->mask = mask[node];
-    out->quality = quality[node];
+    res.node = node;
+    res.score = nf == 1 ? 0 : (int64_t)(key >> 24);
+    res.mask = mask[node];
+    res.quality = quality[node];
   }
-  for (int k = 0; k < YODA_DEV_REASONS; ++k) out->reasons[k] = g->reasons[k];
-  for (int k = 0; k < 6; ++k) out->maxima[k] = g->maxima[k];
-  out->raw_lo = (int64_t)g->raw_lo;
-  out->raw_hi = (int64_t)g->raw_hi;
-  globals_reset(g);
-}
-
-__global__ void k_scatter(const yoda_dev_node_t* __restrict__ stage, const int32_t* __restrict__ idx, int n,
-                          yoda_dev_node_t* __restrict__ nodes) {
-  // one 512-byte record per 32 lanes (16 B each)
-  const int rec = blockIdx.x * (blockDim.x / 32) + (threadIdx.x >> 5);
-  if (rec >= n) return;
-  const uint4* src = reinterpret_cast<const uint4*>(stage + rec);
-  uint4* dst = reinterpret_cast<uint4*>(nodes + idx[rec]);
-  dst[threadIdx.x & 31] = src[threadIdx.x & 31];
+  for (int k = 0; k < YODA_DEV_REASONS; ++k) {
+    int s = 0;
+    for (int h = 0; h < kShards; ++h) s += g->reasons[h][k];
+    res.reasons[k] = s;
+  }
+  for (int k = 0; k < 6; ++k) res.maxima[k] = g->maxima[k];
+  res.raw_lo = (int64_t)g->raw_lo;
+  res.raw_hi = (int64_t)g->raw_hi;
+  *out = res;                 // mapped pinned host memory
+  globals_reset(g);           // re-arm for the next pod; the kernel boundary publishes it
 }
 
 struct Ctx {
@@ -396,23 +541,18 @@ struct Ctx {
   int64_t *d_raw = nullptr, *d_total = nullptr;
   uint32_t* d_mask = nullptr;
   int32_t* d_quality = nullptr;
-  yoda_dev_req_t *d_req = nullptr, *h_req = nullptr;
-  yoda_dev_result_t *d_res = nullptr, *h_res = nullptr;
+  yoda_dev_result_t *h_res = nullptr, *d_res_map = nullptr;
   Globals* d_g = nullptr;
   float last_us = 0;
   int grid = 1024;
+  bool timing = true;
 };
 
-#define CK(x)                            \
-  do {                                   \
-    hipError_t e__ = (x);                \
+#define CK(x)                               \
+  do {                                      \
+    hipError_t e__ = (x);                   \
     if (e__ != hipSuccess) return (int)e__; \
   } while (0)
-
-int grid_for(const Ctx* c, int n) {
-  int g = (n + kWaves - 1) / kWaves;
-  return g < c->grid ? (g > 0 ? g : 1) : c->grid;
-}
 
 }  // namespace
 
@@ -431,6 +571,8 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
   if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
   int cus = 256;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess) c->grid = cus * 4;
+  const SubsetTable st = make_subsets();
+  if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_subsets), &st, sizeof st)) != hipSuccess) return fail("subsets", e);
   if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
   if ((e = hipEventCreate(&c->e0)) != hipSuccess) return fail("event", e);
   if ((e = hipEventCreate(&c->e1)) != hipSuccess) return fail("event", e);
@@ -450,11 +592,11 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
   if ((e = hipMalloc(&c->d_total, N * sizeof(int64_t))) != hipSuccess) return fail("total", e);
   if ((e = hipMalloc(&c->d_mask, N * sizeof(uint32_t))) != hipSuccess) return fail("mask", e);
   if ((e = hipMalloc(&c->d_quality, N * sizeof(int32_t))) != hipSuccess) return fail("quality", e);
-  if ((e = hipMalloc(&c->d_req, sizeof(yoda_dev_req_t))) != hipSuccess) return fail("req", e);
-  if ((e = hipHostMalloc(&c->h_req, sizeof(yoda_dev_req_t), hipHostMallocDefault)) != hipSuccess) return fail("req", e);
-  if ((e = hipMalloc(&c->d_res, sizeof(yoda_dev_result_t))) != hipSuccess) return fail("res", e);
-  if ((e = hipHostMalloc(&c->h_res, sizeof(yoda_dev_result_t), hipHostMallocDefault)) != hipSuccess)
-    return fail("res", e);
+  // result: mapped, coherent pinned host memory written by the select kernel's last block
+  if ((e = hipHostMalloc(&c->h_res, sizeof(yoda_dev_result_t), hipHostMallocMapped | hipHostMallocCoherent)) !=
+      hipSuccess)
+    return fail("result", e);
+  if ((e = hipHostGetDevicePointer((void**)&c->d_res_map, c->h_res, 0)) != hipSuccess) return fail("result map", e);
   if ((e = hipMalloc(&c->d_g, sizeof(Globals))) != hipSuccess) return fail("globals", e);
   Globals init;
   globals_reset(&init);
@@ -469,8 +611,7 @@ void yoda_dev_destroy(void* p) {
   hipStreamSynchronize(c->stream);
   hipFree(c->d_nodes); hipFree(c->d_stage); hipHostFree(c->h_stage); hipFree(c->d_idx); hipHostFree(c->h_idx);
   hipFree(c->d_feas); hipFree(c->d_elig); hipFree(c->d_cand); hipHostFree(c->h_cand); hipFree(c->d_raw);
-  hipFree(c->d_total); hipFree(c->d_mask); hipFree(c->d_quality); hipFree(c->d_req); hipHostFree(c->h_req);
-  hipFree(c->d_res); hipHostFree(c->h_res); hipFree(c->d_g);
+  hipFree(c->d_total); hipFree(c->d_mask); hipFree(c->d_quality); hipHostFree(c->h_res); hipFree(c->d_g);
   hipEventDestroy(c->e0); hipEventDestroy(c->e1);
   hipStreamDestroy(c->stream);
   delete c;
@@ -485,16 +626,27 @@ int yoda_dev_upload(void* p, int n, const int32_t* idx, const yoda_dev_node_t* r
   for (int i = 0; i < n; ++i)
     if (idx[i] < 0 || idx[i] >= c->cap) return -2;   // never scatter outside the node table
   CK(hipSetDevice(c->device));
+  if (n <= kPatchRows) {
+    // steady state (a reservation dirtied one node): rows travel in the kernel arguments
+    PatchArgs a;
+    a.n = n;
+    for (int i = 0; i < n; ++i) {
+      a.idx[i] = idx[i];
+      a.rows[i] = rows[i];
+    }
+    hipLaunchKernelGGL(k_patch, dim3(1), dim3(32 * kPatchRows), 0, c->stream, a, c->d_nodes);
+    CK(hipGetLastError());
+    return 0;      // stream-ordered before the next schedule; nothing host-side to protect
+  }
   memcpy(c->h_stage, rows, (size_t)n * sizeof(yoda_dev_node_t));
   memcpy(c->h_idx, idx, (size_t)n * sizeof(int32_t));
   CK(hipMemcpyAsync(c->d_stage, c->h_stage, (size_t)n * sizeof(yoda_dev_node_t), hipMemcpyHostToDevice, c->stream));
   CK(hipMemcpyAsync(c->d_idx, c->h_idx, (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
   const int per_block = 8;   // 8 records × 32 lanes = 256 threads
-  hipLaunchKernelGGL(k_scatter, dim3((n + per_block - 1) / per_block), dim3(256), 0, c->stream, c->d_stage, c->d_idx, n,
-                     c->d_nodes);
+  hipLaunchKernelGGL(k_scatter, dim3((n + per_block - 1) / per_block), dim3(256), 0, c->stream, c->d_stage, c->d_idx,
+                     n, c->d_nodes);
   CK(hipGetLastError());
-  // the staging buffers are reused by the next upload: wait for the copies
-  CK(hipStreamSynchronize(c->stream));
+  CK(hipStreamSynchronize(c->stream));   // staging buffers are reused by the next upload
   return 0;
 }
 
@@ -503,29 +655,34 @@ int yoda_dev_schedule(void* p, int n, const yoda_dev_req_t* req, const uint8_t* 
   if (n <= 0 || n > c->cap) return -1;
   if (req->use_candidates && !cand) return -3;
   CK(hipSetDevice(c->device));
-  *c->h_req = *req;
-  CK(hipMemcpyAsync(c->d_req, c->h_req, sizeof(yoda_dev_req_t), hipMemcpyHostToDevice, c->stream));
-  if (req->use_candidates) {
+  const yoda_dev_req_t r = *req;
+  if (r.use_candidates) {
     memcpy(c->h_cand, cand, (size_t)n);
     CK(hipMemcpyAsync(c->d_cand, c->h_cand, (size_t)n, hipMemcpyHostToDevice, c->stream));
   }
-  const int grid = grid_for(c, n);
-  const int grid_sel = (n + kBlock - 1) / kBlock < c->grid ? (n + kBlock - 1) / kBlock : c->grid;
-  CK(hipEventRecord(c->e0, c->stream));
-  hipLaunchKernelGGL(k_filter, dim3(grid), dim3(kBlock), 0, c->stream, c->d_nodes, n, c->d_req, c->d_cand, c->d_feas,
+  const int per_block = kWaves * kNodesPerWave;
+  int grid = (n + per_block - 1) / per_block;
+  grid = grid < c->grid ? grid : c->grid;
+  int grid_sel = (n + kBlock - 1) / kBlock;
+  grid_sel = grid_sel < c->grid ? grid_sel : c->grid;
+  c->h_res->feasible = -1;   // sentinel: overwritten by the device
+  if (c->timing) CK(hipEventRecord(c->e0, c->stream));
+  hipLaunchKernelGGL(k_filter, dim3(grid), dim3(kBlock), 0, c->stream, c->d_nodes, n, r, c->d_cand, c->d_feas,
                      c->d_elig, c->d_g);
-  hipLaunchKernelGGL(k_score, dim3(grid), dim3(kBlock), 0, c->stream, c->d_nodes, n, c->d_req, c->d_feas, c->d_elig,
+  hipLaunchKernelGGL(k_score, dim3(grid), dim3(kBlock), 0, c->stream, c->d_nodes, n, r, c->d_feas, c->d_elig,
                      c->d_raw, c->d_total, c->d_mask, c->d_quality, c->d_g);
-  hipLaunchKernelGGL(k_select, dim3(grid_sel > 0 ? grid_sel : 1), dim3(kBlock), 0, c->stream, n, c->d_req, c->d_feas,
-                     c->d_raw, c->d_total, c->d_g);
-  hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, c->stream, c->d_req, c->d_mask, c->d_quality, c->d_g, c->d_res);
+  hipLaunchKernelGGL(k_select, dim3(grid_sel), dim3(kBlock), 0, c->stream, n, r, c->d_feas, c->d_raw, c->d_total,
+                     c->d_mask, c->d_quality, c->d_g, c->d_res_map);
   CK(hipGetLastError());
-  CK(hipEventRecord(c->e1, c->stream));
-  CK(hipMemcpyAsync(c->h_res, c->d_res, sizeof(yoda_dev_result_t), hipMemcpyDeviceToHost, c->stream));
+  if (c->timing) CK(hipEventRecord(c->e1, c->stream));
   CK(hipStreamSynchronize(c->stream));
-  float ms = 0;
-  if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) c->last_us = ms * 1000.0f;
-  *out = *c->h_res;
+  if (c->timing) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) c->last_us = ms * 1000.0f;
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  memcpy(out, c->h_res, sizeof(*out));
+  if (out->feasible < 0) return -4;    // the result never arrived
   return 0;
 }
 
@@ -533,6 +690,7 @@ int yoda_dev_debug(void* p, int n, uint8_t* feas, int64_t* raw, int64_t* total, 
   Ctx* c = (Ctx*)p;
   if (n <= 0 || n > c->cap) return -1;
   CK(hipSetDevice(c->device));
+  CK(hipStreamSynchronize(c->stream));
   if (feas) CK(hipMemcpy(feas, c->d_feas, (size_t)n, hipMemcpyDeviceToHost));
   if (raw) CK(hipMemcpy(raw, c->d_raw, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost));
   if (total) CK(hipMemcpy(total, c->d_total, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost));

@@ -28,7 +28,7 @@ typedef struct {
 
 typedef struct {
   yoda_dev_card_t cards[YODA_DEV_CARDS];     // 256
-  uint16_t linkq[YODA_DEV_CARDS][YODA_DEV_CARDS];   // 128, phys-indexed pair quality (1e-4)
+  uint16_t linkq[YODA_DEV_CARDS][YODA_DEV_CARDS];   // 128, card-pair xGMI quality (1e-4), host-resolved
   uint16_t occ[YODA_DEV_CARDS];              // 16, CU occupancy (1e-4)
   uint8_t healthy[YODA_DEV_CARDS];           // 8
   uint8_t phys[YODA_DEV_CARDS];              // 8
