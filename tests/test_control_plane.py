@@ -1,0 +1,298 @@
+"""HTTP Kubernetes client ↔ fake apiserver HTTP front, scheduling over HTTP, Lease leader
+election (single leader, failover, release), sniffer publishing, CLI entry points."""
+import asyncio
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+from yoda_scheduler_amd.fakeapi.http import FakeApiHttp
+from yoda_scheduler_amd.fakeapi.server import FakeApiServer
+from yoda_scheduler_amd.kube.client import KubeClient, KubeConfig
+from yoda_scheduler_amd.kube.errors import ApiError
+from yoda_scheduler_amd.models.device import make_node, make_scv
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run(coro):
+    return asyncio.run(coro)
+
+
+def test_http_client_crud_watch_bind():
+    async def go():
+        api = FakeApiHttp()
+        url = await api.start()
+        cl = KubeClient(KubeConfig(url))
+        try:
+            n = await cl.create("nodes", make_node("n1"))
+            assert n["metadata"]["resourceVersion"]
+            items, rv = await cl.list("nodes")
+            assert [i["metadata"]["name"] for i in items] == ["n1"]
+            got = []
+
+            async def watcher():
+                async for typ, obj in cl.watch("pods", rv):
+                    got.append((typ, obj["metadata"]["name"], (obj.get("spec") or {}).get("nodeName")))
+                    if len(got) == 3:
+                        return
+
+            t = asyncio.get_event_loop().create_task(watcher())
+            await asyncio.sleep(0.05)
+            p = await cl.create("pods", {"metadata": {"name": "p", "namespace": "default"}, "spec": {}})
+            await cl.bind("default", "p", p["metadata"]["uid"], "n1", {"scv.amd.com/gpus": "0,1"})
+            with pytest.raises(ApiError) as ei:
+                await cl.bind("default", "p", p["metadata"]["uid"], "n1")
+            assert ei.value.code == 409
+            await cl.patch("pods", "p", {"metadata": {"labels": {"a": "b"}}}, "default")
+            await asyncio.wait_for(t, 3)
+            pod = await cl.get("pods", "p", "default")
+            assert pod["spec"]["nodeName"] == "n1" and pod["metadata"]["annotations"]["scv.amd.com/gpus"] == "0,1"
+            assert pod["metadata"]["labels"] == {"a": "b"}
+            stale = dict(pod)
+            stale["metadata"] = dict(pod["metadata"], resourceVersion="1")
+            with pytest.raises(ApiError) as ei:
+                await cl.update("pods", stale, "default")
+            assert ei.value.code == 409
+            await cl.delete("pods", "p", "default")
+            with pytest.raises(ApiError) as ei:
+                await cl.get("pods", "p", "default")
+            assert ei.value.code == 404
+            return got
+        finally:
+            await cl.close()
+            await api.stop()
+    got = run(go())
+    assert got[0] == ("ADDED", "p", None) and got[1] == ("MODIFIED", "p", "n1")
+
+
+def test_watch_too_old_resource_version_is_gone():
+    async def go():
+        srv = FakeApiServer(history=4)
+        api = FakeApiHttp(srv)
+        url = await api.start()
+        cl = KubeClient(KubeConfig(url))
+        for i in range(10):
+            srv.create("nodes", make_node(f"n{i}"))
+        try:
+            with pytest.raises(ApiError) as ei:
+                async for _ in cl.watch("nodes", "1"):
+                    pass
+            return ei.value.code
+        finally:
+            await cl.close()
+            await api.stop()
+    assert run(go()) == 410
+
+
+def test_schedule_over_http_with_informer_relist():
+    from yoda_scheduler_amd.framework.config import parse_config
+    from yoda_scheduler_amd.framework.scheduler import Scheduler
+    from yoda_scheduler_amd.testing import yoda_config
+
+    async def go():
+        srv = FakeApiServer()
+        srv.create("nodes", make_node("n1"))
+        s = make_scv("n1", update_time=time.time())
+        s.update_interval_ms = 600_000
+        srv.create("scvs", s.to_json())
+        api = FakeApiHttp(srv)
+        url = await api.start()
+        cl = KubeClient(KubeConfig(url))
+        sched = Scheduler(cl, parse_config(yoda_config()))
+        await sched.start()
+        loop_t = asyncio.get_event_loop().create_task(sched.scheduling_loop())
+        for i in range(20):
+            srv.create("pods", {"metadata": {"name": f"p{i}", "namespace": "default", "labels": {"scv/memory": "100"}},
+                                "spec": {"schedulerName": "yoda-scheduler"}})
+            if i == 10:
+                srv.close_watches()          # informers must resume from their resourceVersion
+        t0 = time.time()
+        while len(srv.bind_log) < 20 and time.time() - t0 < 10:
+            await asyncio.sleep(0.01)
+        n = len(srv.bind_log)
+        await sched.shutdown()
+        loop_t.cancel()
+        await cl.close()
+        await api.stop()
+        return n
+    assert run(go()) == 20
+
+
+def test_leader_election_single_leader_and_failover():
+    from yoda_scheduler_amd.fakeapi.client import InProcessClient
+    from yoda_scheduler_amd.framework.leader import LeaderElector
+
+    async def go():
+        srv = FakeApiServer()
+        cl = InProcessClient(srv)
+        a = LeaderElector(cl, identity="a", lease_duration=0.6, renew_deadline=0.4, retry_period=0.1)
+        b = LeaderElector(cl, identity="b", lease_duration=0.6, renew_deadline=0.4, retry_period=0.1)
+        await a.acquire()
+        tb = asyncio.get_event_loop().create_task(b.acquire())
+        await asyncio.sleep(0.8)
+        assert a.is_leader and not b.is_leader and not tb.done()
+        # a stops renewing (crash): b takes over after the lease expires
+        a._task.cancel()
+        await asyncio.wait_for(tb, 3)
+        assert b.is_leader
+        lease = srv.get("leases", "yoda-scheduler", "kube-system")
+        assert lease["spec"]["holderIdentity"] == "b" and lease["spec"]["leaseTransitions"] == 1
+        # clean release lets a standby in immediately
+        await b.release()
+        c = LeaderElector(cl, identity="c", lease_duration=5, renew_deadline=4, retry_period=0.1)
+        await asyncio.wait_for(c.acquire(), 2)
+        await c.release()
+        return True
+    assert run(go())
+
+
+def test_leader_loses_lease_when_apiserver_unreachable():
+    from yoda_scheduler_amd.framework.leader import LeaderElector
+
+    class Flaky:
+        def __init__(self, inner):
+            self.inner, self.down = inner, False
+
+        def __getattr__(self, n):
+            f = getattr(self.inner, n)
+
+            async def w(*a, **k):
+                if self.down:
+                    raise ApiError(503, "ServiceUnavailable", "down")
+                return await f(*a, **k)
+            return w
+
+    from yoda_scheduler_amd.fakeapi.client import InProcessClient
+
+    async def go():
+        cl = Flaky(InProcessClient(FakeApiServer()))
+        a = LeaderElector(cl, identity="a", lease_duration=0.5, renew_deadline=0.3, retry_period=0.05)
+        await a.acquire()
+        cl.down = True
+        await asyncio.wait_for(a.lost.wait(), 3)
+        return a.is_leader
+    assert run(go()) is False
+
+
+def test_sniffer_agent_publishes_and_updates():
+    from yoda_scheduler_amd.fakeapi.client import InProcessClient
+    from yoda_scheduler_amd.sniffer.collector import FakeBackend
+    from yoda_scheduler_amd.sniffer.publisher import SnifferAgent
+
+    async def go():
+        srv = FakeApiServer()
+        be = FakeBackend(8)
+        agent = SnifferAgent(InProcessClient(srv), "node-x", be, interval=0.01)
+        await agent.run(count=3)
+        be.state[3].ecc_uncorrectable = 2          # fault injection: ECC error on GPU 3
+        be.state[0].used_mb = 100_000
+        be.state[1].link_load = {2: 0.8}
+        await agent.publish_once()
+        return srv.get("scvs", "node-x")
+    obj = run(go())
+    from yoda_scheduler_amd.models.scv import Scv
+    s = Scv.from_json(obj)
+    assert s.status.card_number == 8 and s.status.card_list[3].health == "Unhealthy"
+    assert s.status.card_list[0].free_memory == 294912 - 100_000
+    assert any(l.peer == 2 and l.load == pytest.approx(0.8) for l in s.status.card_list[1].xgmi)
+    assert int(obj["metadata"]["resourceVersion"]) > 1
+
+
+def test_cli_write_config_and_sniffer_print():
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    out = subprocess.run([sys.executable, "-m", "yoda_scheduler_amd.cmd.scheduler", "--config",
+                          os.path.join(ROOT, "deploy", "yoda-scheduler.yaml"), "--v=3", "--write-config-to", "-",
+                          "--authentication-kubeconfig=/x"],
+                         capture_output=True, text=True, env=env, timeout=60)
+    assert out.returncode == 0, out.stderr
+    cfg = json.loads(out.stdout)
+    assert [p["scheduler_name"] for p in cfg["profiles"]] == ["yoda-scheduler2", "yoda-scheduler"]
+    out = subprocess.run([sys.executable, "-m", "yoda_scheduler_amd.cmd.sniffer", "--print", "--backend", "fake",
+                          "--node", "n0", "--fake-gpus", "4"], capture_output=True, text=True, env=env, timeout=60)
+    assert out.returncode == 0, out.stderr
+    scv = json.loads(out.stdout)
+    assert scv["metadata"]["name"] == "n0" and scv["status"]["cardNumber"] == 4
+
+
+def test_cli_fake_cluster_serves_health_and_schedules():
+    """End-to-end process test: yoda-scheduler --fake-cluster with its fake apiserver on
+    HTTP; a pod posted over HTTP gets bound; /healthz and /metrics answer."""
+    import socket
+
+    def free_port():
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        return p
+
+    api_port, status_port = free_port(), free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    proc = subprocess.Popen([sys.executable, "-m", "yoda_scheduler_amd.cmd.scheduler", "--fake-cluster", "2",
+                             "--fake-apiserver-port", str(api_port), "--port", str(status_port),
+                             "--bind-address", "127.0.0.1", "--device-scorer", "off"],
+                            env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+
+    async def go():
+        cl = KubeClient(KubeConfig(f"http://127.0.0.1:{api_port}"))
+        try:
+            for _ in range(200):
+                try:
+                    await cl.list("nodes")
+                    break
+                except Exception:
+                    await asyncio.sleep(0.05)
+            await cl.create("pods", {"metadata": {"name": "cli", "namespace": "default",
+                                                  "labels": {"scv/memory": "1000"}},
+                                     "spec": {"schedulerName": "yoda-scheduler"}})
+            for _ in range(200):
+                pod = await cl.get("pods", "cli", "default")
+                if pod["spec"].get("nodeName"):
+                    break
+                await asyncio.sleep(0.05)
+            import aiohttp
+            async with aiohttp.ClientSession() as s:
+                async with s.get(f"http://127.0.0.1:{status_port}/healthz") as r:
+                    health = await r.text()
+                async with s.get(f"http://127.0.0.1:{status_port}/metrics") as r:
+                    metrics = await r.text()
+            return pod, health, metrics
+        finally:
+            await cl.close()
+
+    try:
+        pod, health, metrics = run(go())
+    finally:
+        proc.terminate()
+        try:
+            proc.wait(10)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+    assert pod["spec"]["nodeName"].startswith("mi355x-")
+    assert health == "ok"
+    assert "scheduler_schedule_attempts_total" in metrics
+
+
+def test_tracer_chrome_trace():
+    from yoda_scheduler_amd.testing import FakeCluster, yoda_config
+
+    async def go():
+        cfg = yoda_config()
+        cfg["yodaRuntime"]["trace"] = True
+        c = FakeCluster(cfg)
+        c.add_node("n")
+        await c.start()
+        for i in range(5):
+            c.add_pod(f"p{i}", {"scv/memory": "1"})
+        await c.wait_bound(5)
+        await asyncio.sleep(0.02)
+        tr = c.sched.tracer.chrome_trace()
+        await c.stop()
+        return tr
+    tr = run(go())
+    names = {e["name"] for e in tr["traceEvents"]}
+    assert "bind" in names and ({"cycle", "native_batch"} & names)

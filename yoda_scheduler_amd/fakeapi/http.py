@@ -1,0 +1,139 @@
+"""HTTP front of the fake apiserver: the subset of the Kubernetes REST API the scheduler,
+sniffer and leader election use, served by aiohttp so the real :class:`KubeClient` (and
+``kubectl``-style tools) can be exercised end to end without a cluster, including from
+other processes (multi-process / HA tests).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import re
+from typing import Optional
+
+from aiohttp import web
+
+from ..kube.errors import ApiError
+from ..kube.resources import RESOURCES
+from .server import FakeApiServer
+
+_PATH = re.compile(
+    r"^/(?:api/v1|apis/(?P<group>[^/]+)/(?P<version>[^/]+))"
+    r"(?:/namespaces/(?P<ns>[^/]+))?/(?P<res>[^/]+)(?:/(?P<name>[^/]+))?(?:/(?P<sub>[^/]+))?$")
+
+
+def _resolve(path: str):
+    m = _PATH.match(path)
+    if not m:
+        return None
+    res = m.group("res")
+    if res not in RESOURCES:
+        return None
+    return res, m.group("ns"), m.group("name"), m.group("sub")
+
+
+def _status(e: ApiError) -> web.Response:
+    return web.json_response(e.status_obj(), status=e.code)
+
+
+class FakeApiHttp:
+    def __init__(self, server: Optional[FakeApiServer] = None, host: str = "127.0.0.1", port: int = 0) -> None:
+        self.server = server or FakeApiServer()
+        self.host = host
+        self.port = port
+        self._runner: Optional[web.AppRunner] = None
+        self.app = web.Application()
+        async def healthz(_r):
+            return web.Response(text="ok")
+
+        async def version(_r):
+            return web.json_response({"major": "1", "minor": "20", "gitVersion": "v1.20.0-yoda-fake"})
+
+        self.app.router.add_get("/healthz", healthz)
+        self.app.router.add_get("/version", version)
+        self.app.router.add_route("*", "/{tail:.*}", self.dispatch)
+
+    @property
+    def url(self) -> str:
+        return f"http://{self.host}:{self.port}"
+
+    async def start(self) -> str:
+        self._runner = web.AppRunner(self.app)
+        await self._runner.setup()
+        site = web.TCPSite(self._runner, self.host, self.port)
+        await site.start()
+        self.port = site._server.sockets[0].getsockname()[1]   # type: ignore[union-attr]
+        return self.url
+
+    async def stop(self) -> None:
+        self.server.close_watches()
+        if self._runner is not None:
+            await self._runner.cleanup()
+
+    async def dispatch(self, req: web.Request) -> web.StreamResponse:
+        r = _resolve(req.path)
+        if r is None:
+            return _status(ApiError(404, "NotFound", f"no route for {req.path}"))
+        res, ns, name, sub = r
+        s = self.server
+        try:
+            if req.method == "GET":
+                if name is None:
+                    if req.query.get("watch") in ("1", "true"):
+                        return await self._watch(req, res, req.query.get("resourceVersion", "0"))
+                    items, rv = s.list(res, ns)
+                    return web.json_response({"kind": RESOURCES[res].kind + "List", "apiVersion": RESOURCES[res].api_version,
+                                              "metadata": {"resourceVersion": rv}, "items": items})
+                return web.json_response(s.get(res, name, ns))
+            body = await req.json() if req.can_read_body else {}
+            if req.method == "POST":
+                if sub == "binding" and res == "pods":
+                    meta = body.get("metadata") or {}
+                    s.bind(ns or "default", name, meta.get("uid", ""), (body.get("target") or {}).get("name", ""),
+                           meta.get("annotations"))
+                    return web.json_response({"kind": "Status", "status": "Success", "code": 201}, status=201)
+                return web.json_response(s.create(res, body, ns), status=201)
+            if req.method == "PUT":
+                return web.json_response(s.update(res, body, ns, status_only=(sub == "status")))
+            if req.method == "PATCH":
+                return web.json_response(s.patch(res, name, body, ns))
+            if req.method == "DELETE":
+                return web.json_response(s.delete(res, name, ns))
+        except ApiError as e:
+            return _status(e)
+        return _status(ApiError(405, "MethodNotAllowed", req.method))
+
+    async def _watch(self, req: web.Request, res: str, rv: str) -> web.StreamResponse:
+        try:
+            w = self.server.watch(res, rv)
+        except ApiError as e:
+            resp = web.StreamResponse(status=200, headers={"Content-Type": "application/json"})
+            await resp.prepare(req)
+            await resp.write((json.dumps({"type": "ERROR", "object": e.status_obj()}) + "\n").encode())
+            return resp
+        resp = web.StreamResponse(status=200, headers={"Content-Type": "application/json",
+                                                       "Transfer-Encoding": "chunked"})
+        await resp.prepare(req)
+        timeout = float(req.query.get("timeoutSeconds", "300"))
+        try:
+            while True:
+                try:
+                    ev = await asyncio.wait_for(w.queue.get(), timeout)
+                except asyncio.TimeoutError:
+                    break
+                if ev is None:
+                    break
+                typ, obj = ev
+                await resp.write((json.dumps({"type": typ, "object": obj}) + "\n").encode())
+        except (ConnectionResetError, asyncio.CancelledError):
+            pass
+        finally:
+            w.close()
+        return resp
+
+
+async def serve_forever(host: str = "127.0.0.1", port: int = 8001, server: Optional[FakeApiServer] = None) -> None:
+    api = FakeApiHttp(server, host, port)
+    url = await api.start()
+    print(f"fake apiserver listening on {url}", flush=True)
+    while True:
+        await asyncio.sleep(3600)

@@ -100,6 +100,13 @@ class SchedulerConfig:
     batch_size: int = 256
     unschedulable_flush_seconds: float = 60.0
     gc_threshold: tuple = (50_000, 50, 1000)
+    # gfx950 device scorer (yodaRuntime.deviceScorer): auto = use it when a GPU is visible
+    device_scorer: str = "auto"
+    device_index: int = 0
+    device_min_nodes: int = 256
+    device_capacity: int = 65536
+    engine_threads: int = 1
+    trace: bool = False
 
     def profile(self, name: str) -> Optional[Profile]:
         for p in self.profiles:
@@ -215,6 +222,16 @@ def parse_config(doc: dict) -> SchedulerConfig:
     cfg.batch_size = int(_f(rt, "batchSize", cfg.batch_size))
     cfg.unschedulable_flush_seconds = float(_f(rt, "unschedulableFlushSeconds", cfg.unschedulable_flush_seconds))
     cfg.gc_threshold = tuple(int(x) for x in _f(rt, "gcThreshold", cfg.gc_threshold))
+    ds = rt.get("deviceScorer") or {}
+    en = _f(ds, "enabled", "auto")
+    cfg.device_scorer = {True: "on", False: "off"}.get(en, str(en).lower()) if isinstance(en, bool) else str(en).lower()
+    if cfg.device_scorer not in ("auto", "on", "off"):
+        raise ValueError("yodaRuntime.deviceScorer.enabled must be auto|on|off")
+    cfg.device_index = int(_f(ds, "device", 0))
+    cfg.device_min_nodes = int(_f(ds, "minNodes", 256))
+    cfg.device_capacity = int(_f(ds, "capacity", 65536))
+    cfg.engine_threads = int(_f(rt, "engineThreads", 1))
+    cfg.trace = bool(_f(rt, "trace", False))
     if not 0 <= cfg.percentage_of_nodes_to_score <= 100:
         raise ValueError("percentageOfNodesToScore must be in [0, 100]")
     if cfg.pod_initial_backoff_seconds <= 0 or cfg.pod_max_backoff_seconds < cfg.pod_initial_backoff_seconds:

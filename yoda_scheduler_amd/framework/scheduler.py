@@ -26,6 +26,7 @@ from ..ops.native import core, pod_req
 from ..utils import gctune, klog
 from ..utils.metrics import SchedulerMetrics
 from ..utils.ratelimit import TokenBucket
+from ..utils.tracing import Tracer
 from .cache import SchedulerCache
 from .config import SchedulerConfig
 from .events import EventRecorder
@@ -82,9 +83,11 @@ class Scheduler:
         compat = any(((p.plugin_config.get("yoda") or {}).get("compat", False)) for p in config.profiles)
         stale_factor = float(next(((p.plugin_config.get("yoda") or {}).get("staleFactor", 3.0)
                                    for p in config.profiles if "yoda" in p.plugin_config), 3.0))
-        self.engine = core().Engine(bool(compat), max(1, int(engine_threads)))
+        self.engine = core().Engine(bool(compat), max(1, int(engine_threads), config.engine_threads))
         if seed is not None:
             self.engine.seed(seed)
+        self.device_error = ""
+        self._maybe_enable_device(bool(compat))
         self.engine.set_percentage_of_nodes_to_score(config.percentage_of_nodes_to_score)
         self.cache = SchedulerCache(self.engine, compat=bool(compat), stale_factor=stale_factor, clock=clock)
         self.frameworks: dict[str, Framework] = {p.scheduler_name: Framework(p, self.registry, self.handle)
@@ -104,6 +107,27 @@ class Scheduler:
         self.leading = asyncio.Event()
         self.pending_binds = 0
         self.batching = config.batch_size > 1
+        self.tracer = Tracer() if config.trace else None
+
+    def _maybe_enable_device(self, compat: bool) -> None:
+        """Attach the gfx950 device scorer (large clusters): ``auto`` uses it only when a
+        GPU is visible and the library loads; ``on`` makes any failure fatal."""
+        mode = self.config.device_scorer
+        if mode == "off" or compat:
+            return
+        try:
+            from ..ops import device_scorer, hip
+            if mode == "auto" and hip.device_count() <= 0:
+                return
+            device_scorer.enable(self.engine, self.config.device_index, self.config.device_capacity,
+                                 self.config.device_min_nodes)
+            log.info("device scorer enabled on GPU %d (>= %d nodes)", self.config.device_index,
+                     self.config.device_min_nodes)
+        except Exception as e:  # noqa: BLE001
+            self.device_error = str(e)
+            if mode == "on":
+                raise
+            log.info("device scorer not used: %s", e)
 
     # ================================================================== informers
     def _responsible(self, obj: dict) -> bool:
@@ -214,6 +238,10 @@ class Scheduler:
             if res is None:
                 return
         self._finish_cycle(fw, state, pi, res, cycle, t0)
+        if self.tracer is not None:
+            tr = self.tracer
+            tr.span("cycle", tr.now_us() - (time.perf_counter() - t0) * 1e6, pod=pi.key, node=res[0],
+                    feasible=res[1], native=fw.native_for(pi))
 
     def _hybrid_cycle(self, fw: Framework, state: CycleState, pi: PodInfo):
         st = fw.run_pre_filter(state, pi)
@@ -357,6 +385,10 @@ class Scheduler:
             eng = self.engine
             results = eng.schedule_batch([p.num_id for p in run], [pod_req(eng, p) for p in run])
             self.metrics.batch_size.observe(len(run))
+            if self.tracer is not None:
+                tr = self.tracer
+                tr.span("native_batch", tr.now_us() - (time.perf_counter() - t0) * 1e6, pods=len(run),
+                        device_cycles=eng.device_cycles)
             for p, res in zip(run, results):
                 self._finish_cycle(fw, None, p, res, cycle, t0)   # all-native: no Python state
 
@@ -387,6 +419,9 @@ class Scheduler:
                 except Exception as e:  # noqa: BLE001
                     st = Status.error(repr(e))
                 m.binding.observe(time.perf_counter() - tb)
+                if self.tracer is not None:
+                    self.tracer.span("bind", self.tracer.now_us() - (time.perf_counter() - tb) * 1e6, cat="bind",
+                                     pod=pi.key, node=node, ok=st.is_success())
                 if st.is_success():
                     self.cache.finish_binding(pi)
                     fw.run_post_bind(state, pi, node)

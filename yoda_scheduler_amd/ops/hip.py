@@ -2,10 +2,9 @@
 
 Runtime note: PyTorch-ROCm wheels bundle their own ``libamdhip64.so`` with SONAME
 ``libamdhip64.so.7`` — the same SONAME as ``/opt/rocm``'s. Whichever is loaded first
-serves both, so when torch is importable it is imported *before* this library:
-kernels launched here and tensors allocated by torch then share one HIP runtime and
-device context (required to pass ``tensor.data_ptr()`` / torch streams to our
-kernels). Processes without torch (sniffer, scheduler) use ``/opt/rocm`` directly.
+serves both, so processes that use torch import it *before* this library: kernels
+launched here and tensors allocated by torch then share one HIP runtime and device
+context. Processes without torch (sniffer, scheduler) use ``/opt/rocm`` directly.
 
 There is no silent fallback: if the library is missing it is built in-tree, and if
 it cannot be loaded the call raises.
@@ -56,10 +55,9 @@ def lib() -> ctypes.CDLL:
         return _LIB
     with _lock:
         if _LIB is None:
-            try:   # share torch's HIP runtime when torch is present (see module doc)
-                import torch  # noqa: F401
-            except ImportError:
-                pass
+            # No torch import here: a scheduler process should not pay for torch. Processes
+            # that use torch (bench, smoke, GPU tests) import it first, so the shared SONAME
+            # resolves our NEEDED entry to torch's already-loaded runtime.
             if not PATH.exists():
                 from .build import build_hip, OUT
                 OUT.mkdir(parents=True, exist_ok=True)

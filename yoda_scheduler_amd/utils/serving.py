@@ -1,0 +1,55 @@
+"""Health / metrics / configz / debug HTTP endpoints of the scheduler process (the
+kube-scheduler serving surface the reference inherits)."""
+from __future__ import annotations
+
+import json
+from typing import Callable, Optional
+
+from aiohttp import web
+
+
+class StatusServer:
+    def __init__(self, host: str, port: int, metrics_render: Callable[[], bytes],
+                 healthy: Callable[[], bool] = lambda: True, configz: Optional[Callable[[], dict]] = None,
+                 debug: Optional[Callable[[], dict]] = None, trace: Optional[Callable[[], dict]] = None) -> None:
+        self.host, self.port = host, port
+        self.app = web.Application()
+        self.app.router.add_get("/healthz", self._health(healthy))
+        self.app.router.add_get("/livez", self._health(healthy))
+        self.app.router.add_get("/readyz", self._health(healthy))
+        async def metrics(_r):
+            return web.Response(body=metrics_render(), content_type="text/plain", charset="utf-8")
+
+        self.app.router.add_get("/metrics", metrics)
+        for path, fn in (("/configz", configz), ("/debug/yoda", debug), ("/debug/trace", trace)):
+            if fn is not None:
+                self.app.router.add_get(path, self._json(fn))
+        self._runner: Optional[web.AppRunner] = None
+
+    @staticmethod
+    def _json(fn):
+        async def h(_r):
+            return web.json_response(fn(), dumps=_dumps)
+        return h
+
+    @staticmethod
+    def _health(fn):
+        async def h(_r):
+            return web.Response(text="ok") if fn() else web.Response(text="unhealthy", status=500)
+        return h
+
+    async def start(self) -> int:
+        self._runner = web.AppRunner(self.app)
+        await self._runner.setup()
+        site = web.TCPSite(self._runner, self.host, self.port)
+        await site.start()
+        self.port = site._server.sockets[0].getsockname()[1]   # type: ignore[union-attr]
+        return self.port
+
+    async def stop(self) -> None:
+        if self._runner is not None:
+            await self._runner.cleanup()
+
+
+def _dumps(o) -> str:
+    return json.dumps(o, default=lambda x: getattr(x, "__dict__", str(x)))
