@@ -662,7 +662,9 @@ std::vector<int32_t> Engine::feasible_nodes(const PodReq& req, const std::vector
   const int32_t start = next_start_ % N;
   std::vector<int8_t> res;
   int32_t processed = 0;
-  const int32_t chunk = pool_ ? std::max(256, pool_->size() * 64) : N;
+  // chunks big enough to amortise a parallel_for (>= 512 nodes) yet small enough that the
+  // adaptive percentageOfNodesToScore early exit still saves work on huge clusters
+  const int32_t chunk = pool_ ? std::max(1024, pool_->size() * 256) : N;
   for (int32_t base = 0; base < N && (int32_t)feasible.size() < want; base += chunk) {
     int32_t len = std::min(chunk, N - base);
     res.assign(len, 0);

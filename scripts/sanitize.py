@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Build and run the native engine stress driver under sanitizers:
+ASan+UBSan (memory errors, UB) and TSan (the ThreadPool used by the parallel filter).
+Host code only — GPU sanitizers are not part of this pool."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CORE = os.path.join(ROOT, "native", "core")
+HIP = os.path.join(ROOT, "native", "hip")
+
+VARIANTS = {
+    "asan-ubsan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer"],
+    "tsan": ["-fsanitize=thread"],
+}
+
+
+def run(variant: str, nodes: int = 700, steps: int = 2000, threads: int = 4) -> int:
+    # > 512 nodes so the ThreadPool parallel filter/score paths run under TSan
+    flags = VARIANTS[variant]
+    out = os.path.join(tempfile.gettempdir(), f"yoda_stress_{variant}")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", *flags, f"-I{CORE}", f"-I{HIP}",
+           os.path.join(CORE, "engine.cpp"), os.path.join(CORE, "stress_main.cpp"), "-o", out, "-lpthread", "-ldl"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stderr)
+        return r.returncode
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1",
+               TSAN_OPTIONS="halt_on_error=1")
+    env.pop("LD_PRELOAD", None)
+    r = subprocess.run([out, str(nodes), str(steps), str(threads)], capture_output=True, text=True, env=env,
+                       timeout=600)
+    sys.stdout.write(f"[{variant}] {r.stdout}")
+    if r.returncode != 0:
+        sys.stderr.write(r.stderr[-4000:])
+    return r.returncode
+
+
+def main() -> int:
+    rc = 0
+    for v in VARIANTS:
+        rc |= run(v)
+    return rc
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,17 @@
+"""Host-side race/memory checks of the native engine: the randomised stress
+driver built with ASan+UBSan and with TSan (ThreadPool parallel filter/score)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("variant", ["asan-ubsan", "tsan"])
+def test_engine_stress_under_sanitizers(variant):
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import sanitize
+    assert sanitize.run(variant) == 0

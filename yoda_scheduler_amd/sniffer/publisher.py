@@ -62,6 +62,9 @@ class SnifferAgent:
                     if e.code != 404:
                         raise
                     out = await self.client.create("scvs", obj)
+                    # with the status subresource a real apiserver drops .status on create
+                    obj["metadata"]["resourceVersion"] = out["metadata"]["resourceVersion"]
+                    out = await self.client.update_status("scvs", obj)
                     self.published += 1
                     return out
                 obj["metadata"]["resourceVersion"] = cur["metadata"]["resourceVersion"]
