@@ -1,0 +1,45 @@
+"""Multi-process paths on CPU (gloo, world_size 2): the bench.py weak-scaling contract
+(one scheduler shard per rank, max-over-ranks timing, aggregate value) and the all-reduce
+probe used to validate gang placements."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _torchrun(args, nproc=2, timeout=240):
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), *args]
+    return subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT, env=env, timeout=timeout)
+
+
+def test_bench_two_ranks_weak_scaling_contract():
+    r = _torchrun(["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout          # exactly one JSON line, from rank 0
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
+    assert d["pods_bound"] == 2 * 2 * 1000 and d["config"]["global_batch"] == 2000
+    assert abs(d["value"] - d["pods_bound"] / (d["ms_per_step"] * d["steps"] / 1000.0)) / d["value"] < 0.01
+    assert d["higher_is_better"] is True and d["p99_latency_ms"] > 0
+
+
+def test_allreduce_probe_gloo():
+    r = _torchrun(["-m", "yoda_scheduler_amd.parallel.rccl_probe", "--sizes", "64K,1M", "--iters", "3"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    rows = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert [x["bytes"] for x in rows] == [65536, 1 << 20]
+    assert all(x["world"] == 2 and x["busbw_gbps"] > 0 for x in rows)
