@@ -90,6 +90,24 @@ def test_pod_delete_frees_reservation_and_requeues():
     assert run(go())
 
 
+def test_unschedulable_pod_does_not_spin():
+    """Our own PodScheduled=False status write must not pull the pod back into activeQ
+    (upstream isPodUpdated); it stays parked until a cluster event or the flush."""
+    async def go():
+        c = FakeCluster()
+        c.add_node("n", gpus=1, used_mb=[294912 - 1000])
+        await c.start()
+        c.add_pod("big", {"scv/memory": "5000"})
+        await asyncio.sleep(0.6)
+        failed = c.sched.failed
+        cond = {x["type"]: x for x in (c.pod("big").get("status") or {}).get("conditions") or []}
+        await c.stop()
+        return failed, cond
+    failed, cond = run(go())
+    assert 1 <= failed <= 3
+    assert cond["PodScheduled"]["status"] == "False" and "GPU" in cond["PodScheduled"]["message"]
+
+
 def test_stale_and_missing_scv_make_node_unschedulable():
     async def go():
         c = FakeCluster()

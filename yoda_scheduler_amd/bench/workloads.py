@@ -95,7 +95,8 @@ def populate(server, w: Workload, template: Optional[dict] = None, link_load: fl
     ``template`` (from a real amd-smi sample) overrides the per-card static fields."""
     rng = random.Random(seed)
     for name, spec, gpus in w.nodes:
-        server.create("nodes", make_node(name))
+        # kubelet --max-pods 2048: config 5 packs 5000 HBM-sharing pods onto 4 nodes
+        server.create("nodes", make_node(name, pods=2048))
         scv = make_scv(name, spec, gpus, update_time=time.time(), link_load=link_load, rng=rng,
                        jitter=link_load > 0)
         scv.update_interval_ms = 60_000     # one sample stays fresh for the whole burst

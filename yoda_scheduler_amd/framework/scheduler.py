@@ -38,6 +38,18 @@ from .runtime import Framework
 log = logging.getLogger("yoda.scheduler")
 
 _EMPTY_STATE = CycleState()      # shared read-only state for all-native cycles
+_VOLATILE_META = ("resourceVersion", "generation", "managedFields")
+
+
+def _pod_updated(old: dict, new: dict) -> bool:
+    """Upstream ``isPodUpdated``: ignore changes to status and volatile metadata, so the
+    scheduler's own unschedulable-condition writes do not pull a parked pod back into
+    activeQ (that would spin failing pods in a hot loop)."""
+    if old.get("spec") != new.get("spec"):
+        return True
+    om = {k: v for k, v in (old.get("metadata") or {}).items() if k not in _VOLATILE_META}
+    nm = {k: v for k, v in (new.get("metadata") or {}).items() if k not in _VOLATILE_META}
+    return om != nm
 
 
 class Handle:
@@ -167,6 +179,8 @@ class Scheduler:
         elif self._responsible(new) and not self._terminal(new):
             if self.cache.is_assumed(new["metadata"].get("uid")):
                 return   # upstream skipPodUpdate: assumed pods only get status noise
+            if not _pod_updated(old, new):
+                return   # status/resourceVersion-only change (e.g. our own PodScheduled=False)
             self.queue.update(PodInfo.from_obj(new))
 
     def on_pod_delete(self, obj: dict) -> None:
