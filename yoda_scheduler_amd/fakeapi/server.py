@@ -85,6 +85,10 @@ class FakeApiServer:
                  clock=time.perf_counter) -> None:
         self._rv = itertools.count(1)
         self._last_rv = 0
+        # uids: unique per server (random prefix) and per object (counter) — uuid4 per
+        # object costs more than the rest of a create
+        self._uid_prefix = uuid.uuid4().hex[:20]
+        self._uids = itertools.count(1)
         self._objs: dict[str, dict[str, dict]] = {r: {} for r in RESOURCES}
         self._watchers: dict[str, set[Watch]] = {r: set() for r in RESOURCES}
         self._history: dict[str, collections.deque] = {r: collections.deque(maxlen=history) for r in RESOURCES}
@@ -133,7 +137,7 @@ class FakeApiServer:
         new = dict(obj)
         new.setdefault("apiVersion", r.api_version)
         new.setdefault("kind", r.kind)
-        meta["uid"] = meta.get("uid") or str(uuid.uuid4())
+        meta["uid"] = meta.get("uid") or f"{self._uid_prefix}-{next(self._uids):012x}"
         meta["resourceVersion"] = self._next_rv()
         meta.setdefault("creationTimestamp", rfc3339(time.time()))
         new["metadata"] = meta

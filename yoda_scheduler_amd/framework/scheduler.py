@@ -109,7 +109,7 @@ class Scheduler:
                                      config.unschedulable_flush_seconds, clock=clock)
         self._active_fw: Optional[Framework] = None
         self._bind_dq: collections.deque = collections.deque()
-        self._bind_ev = asyncio.Event()
+        self._bind_idle: collections.deque = collections.deque()
         self._tasks: list[asyncio.Task] = []
         self.informers: dict[str, Informer] = {}
         self.scheduled = 0
@@ -409,18 +409,26 @@ class Scheduler:
     # ================================================================== binding
     def _enqueue_bind(self, item: tuple) -> None:
         self._bind_dq.append(item)
-        if not self._bind_ev.is_set():
-            self._bind_ev.set()
+        idle = self._bind_idle
+        while idle:                       # wake exactly one parked worker
+            fut = idle.popleft()
+            if not fut.done():
+                fut.set_result(None)
+                break
 
     async def _bind_worker(self) -> None:
-        """Bind workers drain a shared deque and only park when it is empty, so a burst
-        costs one wake-up per worker instead of one per pod; ``bindConcurrency`` workers
-        keep that many binds in flight against a remote apiserver."""
-        dq, ev, m = self._bind_dq, self._bind_ev, self.metrics
+        """Bind workers drain a shared deque and park (one future each) only when it is
+        empty; an enqueue wakes at most one parked worker. A burst therefore costs a
+        handful of task switches instead of one (or, with a broadcast event, one per
+        worker) per pod, and ``bindConcurrency`` workers keep that many binds in flight
+        against a remote apiserver."""
+        dq, m = self._bind_dq, self.metrics
+        loop = asyncio.get_event_loop()
         while True:
             if not dq:
-                ev.clear()
-                await ev.wait()
+                fut = loop.create_future()
+                self._bind_idle.append(fut)
+                await fut
                 continue
             fw, state, pi, node, cycle, t0 = dq.popleft()
             if state is None:

@@ -200,9 +200,16 @@ class Scv:
         return (now - t) * 1000.0 > factor * max(self.update_interval_ms, 1)
 
 
+_rfc_sec = [-1, ""]
+
+
 def rfc3339(t: float) -> str:
-    frac = f"{t % 1:.6f}"[1:]
-    return time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(t)) + frac + "Z"
+    """RFC 3339 with microseconds (k8s MicroTime). The whole-second prefix is cached:
+    bursts stamp thousands of objects within the same second."""
+    sec = int(t)
+    if sec != _rfc_sec[0]:
+        _rfc_sec[0], _rfc_sec[1] = sec, time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(sec))
+    return f"{_rfc_sec[1]}.{int((t - sec) * 1e6):06d}Z"
 
 
 def parse_rfc3339(s: Any) -> float | None:
