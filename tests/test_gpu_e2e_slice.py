@@ -1,0 +1,68 @@
+"""GPU: SURVEY §7.2 minimum end-to-end slice on a real MI355X.
+
+C++ amd-smi sniffer → Scv published → scheduler (native engine) binds a ``scv/memory``
+pod with a GPU assignment annotation → executor starts a ROCm process pinned with
+HIP_VISIBLE_DEVICES that allocates the pod's HBM → the next amd-smi sample shows the drop,
+and the new Scv makes the scheduler see it (ledger pending → sampled)."""
+import asyncio
+import time
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_minimum_end_to_end_slice(require_gpu):
+    from yoda_scheduler_amd.fakeapi.client import InProcessClient
+    from yoda_scheduler_amd.fakeapi.server import FakeApiServer
+    from yoda_scheduler_amd.framework.config import parse_config
+    from yoda_scheduler_amd.framework.scheduler import Scheduler
+    from yoda_scheduler_amd.models.device import make_node
+    from yoda_scheduler_amd.models.scv import Scv
+    from yoda_scheduler_amd.sniffer.collector import AmdSmiBackend
+    from yoda_scheduler_amd.sniffer.executor import PodExecutor
+    from yoda_scheduler_amd.sniffer.publisher import SnifferAgent
+    from yoda_scheduler_amd.testing import yoda_config
+
+    MB = 4096
+
+    async def go():
+        srv = FakeApiServer()
+        cl = InProcessClient(srv)
+        srv.create("nodes", make_node("mi355x-0"))
+        agent = SnifferAgent(cl, "mi355x-0", AmdSmiBackend(), interval=60.0)
+        await agent.publish_once()
+        before = Scv.from_json(srv.get("scvs", "mi355x-0"))
+        sched = Scheduler(cl, parse_config(yoda_config(yoda_args={"sampleSettleSeconds": 0.0})))
+        await sched.start()
+        loop_t = asyncio.get_event_loop().create_task(sched.scheduling_loop())
+        srv.create("pods", {"metadata": {"name": "slice", "namespace": "default", "labels": {"scv/memory": str(MB)}},
+                            "spec": {"schedulerName": "yoda-scheduler"}})
+        for _ in range(2000):
+            if srv.bind_log:
+                break
+            await asyncio.sleep(0.005)
+        pod = srv.get("pods", "slice", "default")
+        ex = PodExecutor(cl, "mi355x-0", hold_seconds=120)
+        r = ex.launch(pod)
+        ok = await ex.wait_allocated(r)
+        try:
+            await asyncio.sleep(0.5)
+            await agent.publish_once()
+            after = Scv.from_json(srv.get("scvs", "mi355x-0"))
+            await asyncio.sleep(0.05)
+            gpu_state = sched.cache.node_gpu_state("mi355x-0")
+        finally:
+            ex.stop_all()
+            await sched.shutdown()
+            loop_t.cancel()
+        return pod, ok, r.log, before, after, gpu_state
+
+    pod, ok, log, before, after, gpu_state = asyncio.run(go())
+    gpus = [int(x) for x in pod["metadata"]["annotations"]["scv.amd.com/gpus"].split(",")]
+    assert len(gpus) == 1
+    assert ok, log
+    g = gpus[0]
+    drop = before.status.card_list[g].free_memory - after.status.card_list[g].free_memory
+    assert drop >= MB, (drop, log)                        # the sniffer saw the pod's HBM
+    assert gpu_state[g]["reserved"] == MB and gpu_state[g]["pending"] == 0   # sample now reflects it

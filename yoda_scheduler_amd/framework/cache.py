@@ -49,6 +49,7 @@ class SchedulerCache:
         self._stale: dict[str, bool] = {}
         self.pods: dict[str, PodState] = {}
         self.node_pods: dict[str, set[str]] = {}
+        self._anti: set[str] = set()
         self.generation = 0
 
     # ------------------------------------------------------------------ nodes
@@ -115,6 +116,17 @@ class SchedulerCache:
     def _track(self, ps: PodState) -> None:
         self.pods[ps.info.uid] = ps
         self.node_pods.setdefault(ps.node, set()).add(ps.info.uid)
+        aff = ((ps.info.obj.get("spec") or {}).get("affinity") or {}).get("podAntiAffinity") or {}
+        if aff.get("requiredDuringSchedulingIgnoredDuringExecution"):
+            self._anti.add(ps.info.uid)
+        else:
+            self._anti.discard(ps.info.uid)
+
+    def pods_with_required_anti_affinity(self) -> int:
+        """Bound/assumed pods whose required anti-affinity can reject new pods (symmetry)."""
+        if self._anti:
+            self._anti &= self.pods.keys()
+        return len(self._anti)
 
     def assumed(self, pi: PodInfo, node: str, cards: list[int]) -> None:
         """Record a pod the engine reserved during ``schedule(assume=True)``."""

@@ -81,18 +81,24 @@ class Framework:
         self.pre_bind: list[PreBindPlugin] = [p for p, _ in self.points["preBind"]]
         self.post_bind: list[PostBindPlugin] = [p for p, _ in self.points["postBind"]]
         self.yoda = self.plugins.get("yoda")
-        # Python filters that are no-ops for most pods (e.g. NodePorts without hostPorts)
-        # keep a pod on the native path unless they actually apply to it.
-        self.filter_py_conditional = [p for p in self.filter_py if hasattr(p, "is_noop_for")]
-        static = [p for p in self.filter_py if not hasattr(p, "is_noop_for")]
-        self.fully_native_static = not (static or self.score_py or self.pre_filter or self.pre_score
-                                        or self.reserve or self.permit)
-        self.fully_native = self.fully_native_static and not self.filter_py_conditional
+        # Python plugins that are no-ops for most pods (NodePorts without hostPorts,
+        # PodTopologySpread without constraints, InterPodAffinity without terms) keep a
+        # pod on the native path unless they actually apply to it.
+        py_plugins = self.filter_py + [p for p, _ in self.score_py] + self.pre_filter + self.pre_score
+        self.conditional = list({id(p): p for p in py_plugins if hasattr(p, "is_noop_for")}.values())
+        static = [p for p in py_plugins if not hasattr(p, "is_noop_for")]
+        self.fully_native_static = not (static or self.reserve or self.permit)
+        self.fully_native = self.fully_native_static and not self.conditional
 
     def native_for(self, pod) -> bool:
         if not self.fully_native_static:
             return False
-        return all(p.is_noop_for(pod) for p in self.filter_py_conditional)
+        return all(p.is_noop_for(pod) for p in self.conditional)
+
+    @staticmethod
+    def _applies(p, pod) -> bool:
+        f = getattr(p, "is_noop_for", None)
+        return f is None or not f(pod)
 
     def _get(self, name: str, registry: Registry):
         inst = self.plugins.get(name)
@@ -112,6 +118,8 @@ class Framework:
     # ------------------------------------------------------------------ Python points
     def run_pre_filter(self, state: CycleState, pod) -> Status:
         for p in self.pre_filter:
+            if not self._applies(p, pod):
+                continue
             st = p.pre_filter(state, pod)
             if not st.is_success():
                 st.plugin = st.plugin or p.name
@@ -122,7 +130,7 @@ class Framework:
         if not self.filter_py:
             return nodes, {}
         out, failed = [], {}
-        active = [p for p in self.filter_py if not getattr(p, "is_noop_for", lambda _p: False)(pod)]
+        active = [p for p in self.filter_py if self._applies(p, pod)]
         for n in nodes:
             for p in active:
                 st = p.filter(state, pod, n)
@@ -136,10 +144,14 @@ class Framework:
     def run_score_py(self, state: CycleState, pod, nodes: list[str]) -> list[int]:
         total = [0] * len(nodes)
         for p in self.pre_score:
+            if not self._applies(p, pod):
+                continue
             st = p.pre_score(state, pod, nodes)
             if not st.is_success():
                 raise RuntimeError(f"preScore {p.name}: {st.message()}")
         for p, w in self.score_py:
+            if not self._applies(p, pod):
+                continue
             scores = []
             for n in nodes:
                 s, st = p.score(state, pod, n)

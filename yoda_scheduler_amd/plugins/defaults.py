@@ -117,7 +117,7 @@ def _inert(name: str):
 
 
 INERT_PLUGINS = ["VolumeRestrictions", "EBSLimits", "GCEPDLimits", "NodeVolumeLimits", "AzureDiskLimits",
-                 "VolumeBinding", "VolumeZone", "PodTopologySpread", "InterPodAffinity", "ImageLocality",
+                 "VolumeBinding", "VolumeZone", "ImageLocality",
                  "NodePreferAvoidPods", "NodeLabel", "ServiceAffinity", "SelectorSpread", "CSILimits"]
 
 
@@ -194,5 +194,8 @@ def register_defaults(registry) -> None:
                 NodeResourcesLeastAllocated, NodeResourcesMostAllocated, NodeResourcesBalancedAllocation,
                 NodePorts, DefaultBinder, DefaultPreemption):
         registry.register(cls.name, cls)
+    from .spread_affinity import InterPodAffinity, PodTopologySpread
+    registry.register(PodTopologySpread.name, PodTopologySpread)
+    registry.register(InterPodAffinity.name, InterPodAffinity)
     for n in INERT_PLUGINS:
         registry.register(n, _inert(n))

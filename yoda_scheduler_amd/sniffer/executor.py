@@ -1,0 +1,91 @@
+"""Node-side pod executor ("kubelet-lite") that turns a binding into a real GPU workload —
+the last hop of SURVEY §7.2's minimum end-to-end slice: scheduler decision →
+``scv.amd.com/gpus`` annotation → a ROCm process pinned with ``HIP_VISIBLE_DEVICES`` that
+allocates the pod's ``scv/memory`` MB of HBM on those GPUs → the next amd-smi sample shows
+the HBM drop, closing the telemetry loop the reference never closes (its burst pods are
+invisible to the sniffer).
+
+Used for validation and demos against the fake apiserver; in a real cluster the kubelet +
+a device plugin reading the annotation play this role.
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import subprocess
+import sys
+from dataclasses import dataclass, field
+from typing import Optional
+
+from ..models.labels import ANNOTATION_GPUS, LABEL_MEMORY
+
+HOLD_SCRIPT = r"""
+import os, sys, time, torch
+mb = int(sys.argv[1]); secs = float(sys.argv[2])
+bufs = [torch.empty(mb * (1 << 20), dtype=torch.uint8, device=f"cuda:{i}") for i in range(torch.cuda.device_count())]
+for b in bufs:
+    b.fill_(1)
+torch.cuda.synchronize()
+print("allocated", mb, "MB on", len(bufs), "GPU(s) HIP_VISIBLE_DEVICES=", os.environ.get("HIP_VISIBLE_DEVICES"), flush=True)
+time.sleep(secs)
+"""
+
+
+@dataclass
+class Running:
+    key: str
+    gpus: list[int]
+    mb: int
+    proc: subprocess.Popen
+    log: list[str] = field(default_factory=list)
+
+
+class PodExecutor:
+    def __init__(self, client, node: str, hold_seconds: float = 30.0) -> None:
+        self.client = client
+        self.node = node
+        self.hold_seconds = hold_seconds
+        self.running: dict[str, Running] = {}
+
+    def launch(self, pod: dict) -> Optional[Running]:
+        meta = pod.get("metadata") or {}
+        key = f"{meta.get('namespace', 'default')}/{meta.get('name')}"
+        if key in self.running or (pod.get("spec") or {}).get("nodeName") != self.node:
+            return None
+        ann = meta.get("annotations") or {}
+        gpus = [int(x) for x in (ann.get(ANNOTATION_GPUS) or "").split(",") if x.strip()]
+        mb = int((meta.get("labels") or {}).get(LABEL_MEMORY, "0") or 0)
+        env = dict(os.environ, HIP_VISIBLE_DEVICES=",".join(map(str, gpus)),
+                   ROCR_VISIBLE_DEVICES=",".join(map(str, gpus)))
+        env.pop("CUDA_VISIBLE_DEVICES", None)
+        proc = subprocess.Popen([sys.executable, "-c", HOLD_SCRIPT, str(mb), str(self.hold_seconds)], env=env,
+                                stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        r = Running(key, gpus, mb, proc)
+        self.running[key] = r
+        return r
+
+    async def wait_allocated(self, r: Running, timeout: float = 180.0) -> bool:
+        """Wait for the workload's 'allocated' line (first torch import can be slow)."""
+        loop = asyncio.get_event_loop()
+
+        def read():
+            for line in r.proc.stdout:   # type: ignore[union-attr]
+                r.log.append(line.rstrip())
+                if line.startswith("allocated"):
+                    return True
+            return False
+
+        try:
+            return await asyncio.wait_for(loop.run_in_executor(None, read), timeout)
+        except asyncio.TimeoutError:
+            return False
+
+    def stop_all(self) -> None:
+        for r in self.running.values():
+            if r.proc.poll() is None:
+                r.proc.terminate()
+                try:
+                    r.proc.wait(10)
+                except subprocess.TimeoutExpired:
+                    r.proc.kill()
+        self.running.clear()
