@@ -53,7 +53,9 @@ def main(argv=None) -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
+    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5, 6])
+    ap.add_argument("--device", choices=["auto", "on", "off"], default="auto",
+                    help="gfx950 device scorer (used automatically for clusters >= 256 nodes)")
     ap.add_argument("--qps", type=float, default=5000.0, help="client QPS (deploy default 5000; reference 50)")
     ap.add_argument("--burst", type=int, default=10000, help="client burst (deploy default 10000; reference 100)")
     ap.add_argument("--reference-qps", action="store_true", help="use the reference's client limits 50/100")
@@ -91,7 +93,7 @@ def main(argv=None) -> int:
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
     shards = [Shard(w, qps=a.qps, burst=a.burst, batch=a.batch, template=tmpl, events=not a.no_events,
-                    compat=a.compat, seed=rank * 1000 + i) for i in range(a.warmup + a.steps)]
+                    compat=a.compat, seed=rank * 1000 + i, device=a.device) for i in range(a.warmup + a.steps)]
     for s in shards:
         loop.run_until_complete(s.start())
     for i in range(a.warmup):
@@ -103,6 +105,7 @@ def main(argv=None) -> int:
     sync()
     elapsed = time.perf_counter() - t0
 
+    device_cycles = sum(s.sched.engine.device_cycles for s in shards)
     bound = sum(r.bound for r in results)
     unsched = sum(r.unschedulable for r in results)
     lats = [x for r in results for x in r.latencies_s]
@@ -147,6 +150,7 @@ def main(argv=None) -> int:
             "pods_bound": bound,
             "pods_unschedulable": unsched,
             "client_qps": a.qps, "client_burst": a.burst, "native_batch": a.batch, "compat": a.compat,
+            "device_scorer": a.device, "device_cycles": device_cycles,
             "baseline_note": "vs_baseline against BASELINE.md's derived (unmeasured) ~55 pods/s reference ceiling "
                              "(kube-scheduler v1.20 client QPS 50 / burst 100)",
             "telemetry": tels[0],

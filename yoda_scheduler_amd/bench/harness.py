@@ -21,7 +21,8 @@ from ..utils.metrics import NullMetrics, SchedulerMetrics
 from .workloads import Workload, pod_object, populate
 
 
-def bench_config(scheduler_name: str, qps: float, burst: int, batch: int, compat: bool = False) -> dict:
+def bench_config(scheduler_name: str, qps: float, burst: int, batch: int, compat: bool = False,
+                 device: str = "auto") -> dict:
     """The shipped deploy profile (yoda at filter + score weight 300 on top of the
     upstream defaults) with the yoda QueueSort enabled (Q7) and the given client QPS."""
     prof = {"schedulerName": scheduler_name,
@@ -34,7 +35,7 @@ def bench_config(scheduler_name: str, qps: float, burst: int, batch: int, compat
             "leaderElection": {"leaderElect": False},
             "clientConnection": {"qps": qps, "burst": burst},
             "percentageOfNodesToScore": 0, "podInitialBackoffSeconds": 1, "podMaxBackoffSeconds": 10,
-            "yodaRuntime": {"batchSize": batch, "bindConcurrency": 256},
+            "yodaRuntime": {"batchSize": batch, "bindConcurrency": 256, "deviceScorer": {"enabled": device}},
             "profiles": [prof]}
 
 
@@ -62,12 +63,12 @@ def percentile(xs: list[float], q: float) -> float:
 class Shard:
     def __init__(self, w: Workload, qps: float = 5000.0, burst: int = 10000, batch: int = 256,
                  template: Optional[dict] = None, metrics: bool = False, events: bool = True,
-                 compat: bool = False, seed: int = 0, engine_threads: int = 1) -> None:
+                 compat: bool = False, seed: int = 0, engine_threads: int = 1, device: str = "auto") -> None:
         self.w = w
         self.server = FakeApiServer()
         self.client = InProcessClient(self.server)
         populate(self.server, w, template, link_load=0.2 if w.id == 5 else 0.0, seed=seed)
-        cfg = parse_config(bench_config(w.scheduler_name, qps, burst, batch, compat))
+        cfg = parse_config(bench_config(w.scheduler_name, qps, burst, batch, compat, device))
         self.sched = Scheduler(self.client, cfg, metrics=SchedulerMetrics() if metrics else NullMetrics(),
                                record_events=events, seed=seed, engine_threads=engine_threads)
         self._loop_task: Optional[asyncio.Task] = None

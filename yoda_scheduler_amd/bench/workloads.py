@@ -75,6 +75,11 @@ def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None) -> W
         w = Workload(5, "5000-pod burst mixed + multi-GPU, 4 nodes x 8 MI355X (xGMI gang scoring)",
                      [(f"node-{i}", MI355X, 8) for i in range(4)])
         w.pods = [_mixed_labels(rng) for _ in range(5000)]
+    elif cfg == 6:
+        # beyond BASELINE: a large cluster where the gfx950 device scorer takes the cycle
+        w = Workload(6, "1000-pod burst mixed + multi-GPU, 4096 nodes x 8 MI355X (device scorer)",
+                     [(f"node-{i}", MI355X, 8) for i in range(4096)])
+        w.pods = [_mixed_labels(rng) for _ in range(1000)]
     else:
         raise ValueError(f"unknown config {cfg}")
     return w

@@ -99,7 +99,8 @@ class Scheduler:
         if seed is not None:
             self.engine.seed(seed)
         self.device_error = ""
-        self._maybe_enable_device(bool(compat))
+        self._compat = bool(compat)
+        self._device_checked = False
         self.engine.set_percentage_of_nodes_to_score(config.percentage_of_nodes_to_score)
         self.cache = SchedulerCache(self.engine, compat=bool(compat), stale_factor=stale_factor, clock=clock)
         self.frameworks: dict[str, Framework] = {p.scheduler_name: Framework(p, self.registry, self.handle)
@@ -121,20 +122,25 @@ class Scheduler:
         self.batching = config.batch_size > 1
         self.tracer = Tracer() if config.trace else None
 
-    def _maybe_enable_device(self, compat: bool) -> None:
-        """Attach the gfx950 device scorer (large clusters): ``auto`` uses it only when a
-        GPU is visible and the library loads; ``on`` makes any failure fatal."""
+    def _maybe_enable_device(self) -> None:
+        """Attach the gfx950 device scorer once the cluster is big enough for it to pay
+        (``deviceScorer.minNodes``). ``auto`` uses it only when a GPU is visible and the
+        library loads; ``on`` attaches at start-up and makes any failure fatal. Called after
+        the informers synced and from housekeeping (clusters grow)."""
         mode = self.config.device_scorer
-        if mode == "off" or compat:
+        if mode == "off" or self._compat or self._device_checked or self.engine.device_enabled:
             return
+        nodes = self.engine.live_nodes
+        if mode == "auto" and nodes < self.config.device_min_nodes:
+            return
+        self._device_checked = True
         try:
             from ..ops import device_scorer, hip
             if mode == "auto" and hip.device_count() <= 0:
                 return
-            device_scorer.enable(self.engine, self.config.device_index, self.config.device_capacity,
-                                 self.config.device_min_nodes)
-            log.info("device scorer enabled on GPU %d (>= %d nodes)", self.config.device_index,
-                     self.config.device_min_nodes)
+            cap = max(self.config.device_capacity, 4 * nodes)
+            device_scorer.enable(self.engine, self.config.device_index, cap, self.config.device_min_nodes)
+            log.info("device scorer enabled on GPU %d (%d nodes, capacity %d)", self.config.device_index, nodes, cap)
         except Exception as e:  # noqa: BLE001
             self.device_error = str(e)
             if mode == "on":
@@ -463,13 +469,29 @@ class Scheduler:
                 self.pending_binds -= 1
 
     # ================================================================== loops
+    def _export_gpu_metrics(self, max_nodes: int = 2048) -> None:
+        """yoda_gpu_* gauges (per-GPU reserved / sniffed free HBM, Scv staleness)."""
+        m = self.metrics
+        for k, name in enumerate(self.cache.nodes):
+            if k >= max_nodes:
+                break
+            for i, g in enumerate(self.cache.node_gpu_state(name)):
+                m.child(m.gpu_reserved, name, str(i)).set(g["reserved"])
+                m.child(m.gpu_free, name, str(i)).set(g["free"])
+            m.child(m.scv_stale, name).set(1 if self.cache._stale.get(name) else 0)
+
     async def _housekeeping(self, period: float = 0.5) -> None:
         m = self.metrics
+        tick = 0
         while True:
             await asyncio.sleep(period)
             self.queue.flush_backoff_completed()
             self.queue.flush_unschedulable_leftover()
             self.cache.cleanup_expired()
+            self._maybe_enable_device()
+            tick += 1
+            if tick % 4 == 0 and isinstance(m, SchedulerMetrics):
+                self._export_gpu_metrics()
             flipped = self.cache.refresh_staleness()
             if flipped:
                 self.queue.move_all_to_active_or_backoff("ScvStale")
@@ -507,6 +529,7 @@ class Scheduler:
         self._tasks.append(loop.create_task(self._housekeeping()))
         if wait_sync:
             await self.wait_synced()
+        self._maybe_enable_device()
         gctune.tune(self.config.gc_threshold)
 
     async def wait_synced(self) -> None:
