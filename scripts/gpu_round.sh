@@ -22,6 +22,9 @@ for s in $STEPS; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     bench5) step bench5 600 python bench.py --config 5 ;;
+    bench6on) step bench6_on 600 python bench.py --config 6 --steps 3 --warmup 1 --device on ;;
+    bench6off) step bench6_off 600 python bench.py --config 6 --steps 3 --warmup 1 --device off ;;
+    benchref) step bench_refqps 600 python bench.py --steps 2 --warmup 0 --reference-qps ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
 done

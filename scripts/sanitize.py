@@ -5,6 +5,7 @@ Host code only — GPU sanitizers are not part of this pool."""
 from __future__ import annotations
 
 import os
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -32,8 +33,12 @@ def run(variant: str, nodes: int = 700, steps: int = 2000, threads: int = 4) -> 
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1",
                TSAN_OPTIONS="halt_on_error=1")
     env.pop("LD_PRELOAD", None)
-    r = subprocess.run([out, str(nodes), str(steps), str(threads)], capture_output=True, text=True, env=env,
-                       timeout=600)
+    argv = [out, str(nodes), str(steps), str(threads)]
+    if variant == "tsan" and shutil.which("setarch"):
+        # TSan's shadow layout can collide with a randomised mmap base on recent kernels
+        # ("unexpected memory mapping"); run the driver with ASLR off
+        argv = ["setarch", os.uname().machine, "-R", *argv]
+    r = subprocess.run(argv, capture_output=True, text=True, env=env, timeout=600)
     sys.stdout.write(f"[{variant}] {r.stdout}")
     if r.returncode != 0:
         sys.stderr.write(r.stderr[-4000:])

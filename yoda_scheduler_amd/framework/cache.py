@@ -50,11 +50,29 @@ class SchedulerCache:
         self.pods: dict[str, PodState] = {}
         self.node_pods: dict[str, set[str]] = {}
         self._anti: set[str] = set()
+        self.image_nodes: dict[str, int] = {}    # image → number of nodes holding it (ImageLocality)
+        self.avoid_nodes: set[str] = set()       # nodes with a preferAvoidPods annotation
         self.generation = 0
 
     # ------------------------------------------------------------------ nodes
+    def _index_node(self, info: NodeInfo, sign: int) -> None:
+        for im in info.images:
+            c = self.image_nodes.get(im, 0) + sign
+            if c > 0:
+                self.image_nodes[im] = c
+            else:
+                self.image_nodes.pop(im, None)
+        if sign > 0 and info.avoid:
+            self.avoid_nodes.add(info.name)
+        elif sign < 0:
+            self.avoid_nodes.discard(info.name)
+
     def add_node(self, obj: dict) -> None:
         info = NodeInfo.from_obj(obj)
+        old = self.nodes.get(info.name)
+        if old is not None:
+            self._index_node(old, -1)
+        self._index_node(info, +1)
         self.nodes[info.name] = info
         idx = push_node(self.engine, info)
         self.node_pods.setdefault(info.name, set())
@@ -66,7 +84,9 @@ class SchedulerCache:
     update_node = add_node
 
     def remove_node(self, name: str) -> None:
-        self.nodes.pop(name, None)
+        old = self.nodes.pop(name, None)
+        if old is not None:
+            self._index_node(old, -1)
         idx = self.engine.node_index(name)
         if idx >= 0:
             self.engine.remove_node(idx)

@@ -84,10 +84,11 @@ class Framework:
         # Python plugins that are no-ops for most pods (NodePorts without hostPorts,
         # PodTopologySpread without constraints, InterPodAffinity without terms) keep a
         # pod on the native path unless they actually apply to it.
-        py_plugins = self.filter_py + [p for p, _ in self.score_py] + self.pre_filter + self.pre_score
+        py_plugins = self.filter_py + [p for p, _ in self.score_py] + self.pre_filter + self.pre_score + self.reserve
         self.conditional = list({id(p): p for p in py_plugins if hasattr(p, "is_noop_for")}.values())
         static = [p for p in py_plugins if not hasattr(p, "is_noop_for")]
-        self.fully_native_static = not (static or self.reserve or self.permit)
+        self.reserve_static = [p for p in self.reserve if not hasattr(p, "is_noop_for")]
+        self.fully_native_static = not (static or self.permit)
         self.fully_native = self.fully_native_static and not self.conditional
 
     def native_for(self, pod) -> bool:
@@ -169,17 +170,19 @@ class Framework:
         return total
 
     def run_reserve(self, state: CycleState, pod, node: str) -> Status:
-        for i, p in enumerate(self.reserve):
+        active = [p for p in self.reserve if self._applies(p, pod)]
+        for i, p in enumerate(active):
             st = p.reserve(state, pod, node)
             if not st.is_success():
-                for q in reversed(self.reserve[:i]):
+                for q in reversed(active[:i]):
                     q.unreserve(state, pod, node)
                 return st
         return Status.ok()
 
     def run_unreserve(self, state: CycleState, pod, node: str) -> None:
         for p in reversed(self.reserve):
-            p.unreserve(state, pod, node)
+            if self._applies(p, pod):
+                p.unreserve(state, pod, node)
 
     def run_permit(self, state: CycleState, pod, node: str) -> tuple[Status, float]:
         wait = 0.0
@@ -192,6 +195,8 @@ class Framework:
 
     async def run_bind(self, state: CycleState, pod, node: str) -> Status:
         for p in self.pre_bind:
+            if not self._applies(p, pod):
+                continue
             st = await p.pre_bind(state, pod, node)
             if not st.is_success():
                 return st

@@ -74,6 +74,11 @@ class Handle:
     def recorder(self) -> EventRecorder:
         return self._s.recorder
 
+    def lister(self, res: str) -> dict:
+        """Informer store (key → object) of a resource a plugin declared in ``watches``."""
+        inf = self._s.informers.get(res)
+        return inf.store if inf is not None else {}
+
     def preempt(self, pod: PodInfo, node: str, victims: list[PodInfo]) -> None:
         self._s._preempt(pod, node, victims)
 
@@ -228,6 +233,15 @@ class Scheduler:
             "scvs": Informer(self.client, "scvs", self.on_scv, self.on_scv_update, self.on_scv_delete),
             "pods": Informer(self.client, "pods", self.on_pod_add, self.on_pod_update, self.on_pod_delete),
         }
+        # objects only some plugins need (PVCs, PVs, StorageClasses, CSINodes): watched when
+        # an enabled plugin declares them; any change may make a parked pod schedulable
+        extra = sorted({r for fw in self.frameworks.values() for p in fw.plugins.values()
+                        if not getattr(p, "inert", False) for r in getattr(p, "watches", ())})
+        for res in extra:
+            ev = f"{res}Change"
+            self.informers[res] = Informer(self.client, res,
+                                           lambda o, ev=ev: self.queue.move_all_to_active_or_backoff(ev),
+                                           lambda a, b, ev=ev: self.queue.move_all_to_active_or_backoff(ev), None)
         return self.informers
 
     # ================================================================== cycle
@@ -294,7 +308,7 @@ class Scheduler:
         cards = res[3]
         self.cache.assumed(pi, node, cards)
         pi.assigned_cards = cards if (fw.filter_mask & core().F_YODA) else None
-        if fw.reserve:
+        if fw.reserve and state is not None and (fw.reserve_static or not fw.native_for(pi)):
             st = fw.run_reserve(state, pi, node)
             if not st.is_success():
                 self.cache.forget(pi)
@@ -326,7 +340,11 @@ class Scheduler:
                 "GpuFit": "node(s) have too few healthy GPUs matching scv/memory+scv/clock"}
         parts = [f"{c} {text.get(names[i], names[i])}" for i, c in enumerate(reasons) if c and i]
         if len(res) > 8 and res[8]:
-            parts.append(f"{res[8]} node(s) rejected by out-of-tree filters")
+            by_msg: dict[str, int] = {}
+            for st in res[7].values():
+                by_msg[st.message() or "node(s) rejected by out-of-tree filters"] = \
+                    by_msg.get(st.message() or "node(s) rejected by out-of-tree filters", 0) + 1
+            parts.extend(f"{c} {m}" for m, c in by_msg.items())
         return f"0/{res[2]} nodes are available: " + ", ".join(sorted(parts)) + "."
 
     def _fail(self, fw: Framework, state: CycleState, pi: PodInfo, cycle: int, msg: str, t0: float,

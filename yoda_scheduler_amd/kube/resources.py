@@ -38,6 +38,11 @@ RESOURCES = {
     "leases": Resource("leases", "coordination.k8s.io", "v1", "Lease", True),
     "scvs": Resource("scvs", "core.run-linux.com", "v1", "Scv", False),
     "configmaps": Resource("configmaps", "", "v1", "ConfigMap", True),
+    # volume plugins (VolumeBinding / VolumeZone / NodeVolumeLimits)
+    "persistentvolumeclaims": Resource("persistentvolumeclaims", "", "v1", "PersistentVolumeClaim", True),
+    "persistentvolumes": Resource("persistentvolumes", "", "v1", "PersistentVolume", False),
+    "storageclasses": Resource("storageclasses", "storage.k8s.io", "v1", "StorageClass", False),
+    "csinodes": Resource("csinodes", "storage.k8s.io", "v1", "CSINode", False),
 }
 
 

@@ -165,6 +165,8 @@ class NodeInfo:
     cpu_m: int
     mem: int
     pods: int
+    images: dict = field(default_factory=dict)       # normalized image name → size bytes
+    avoid: Optional[str] = None                      # preferAvoidPods annotation (raw JSON)
 
     @classmethod
     def from_obj(cls, obj: dict) -> "NodeInfo":
@@ -176,4 +178,27 @@ class NodeInfo:
         return cls(name=meta.get("name", ""), obj=obj, labels=dict(meta.get("labels") or {}), taints=taints,
                    unschedulable=bool(spec.get("unschedulable", False)),
                    cpu_m=cpu_millis(alloc.get("cpu", "0")), mem=bytes_of(alloc.get("memory", "0")),
-                   pods=int(alloc.get("pods", 110)))
+                   pods=int(alloc.get("pods", 110)), images=_node_images(obj),
+                   avoid=(meta.get("annotations") or _EMPTY).get(ANNOTATION_PREFER_AVOID_PODS))
+
+
+ANNOTATION_PREFER_AVOID_PODS = "scheduler.alpha.kubernetes.io/preferAvoidPods"
+
+
+def normalize_image(name: str) -> str:
+    """Upstream ``normalizedImageName``: an image without a tag or digest means ``:latest``."""
+    if name.rfind(":") <= name.rfind("/") and "@" not in name:
+        return name + ":latest"
+    return name
+
+
+def _node_images(obj: dict) -> dict:
+    imgs = (obj.get("status") or _EMPTY).get("images")
+    if not imgs:
+        return {}
+    out = {}
+    for im in imgs:
+        size = int(im.get("sizeBytes") or 0)
+        for n in im.get("names") or ():
+            out[normalize_image(n)] = size
+    return out

@@ -40,3 +40,50 @@ class LabelSelector:
             else:
                 raise ValueError(f"unknown selector operator {op!r}")
         return True
+
+
+class NodeSelector:
+    """core/v1 NodeSelector (``nodeSelectorTerms`` OR'ed, expressions AND'ed), as used by
+    PV ``spec.nodeAffinity.required``. Operators In/NotIn/Exists/DoesNotExist/Gt/Lt on
+    labels and ``matchFields`` on ``metadata.name``. A term with no requirements matches
+    nothing (upstream)."""
+    __slots__ = ("terms",)
+
+    def __init__(self, sel: Optional[dict]) -> None:
+        self.terms = []
+        for t in (sel or {}).get("nodeSelectorTerms") or []:
+            exprs = [(e.get("key", ""), e.get("operator", "In"), [str(v) for v in e.get("values") or []])
+                     for e in t.get("matchExpressions") or []]
+            fields = [(e.get("key", ""), e.get("operator", "In"), [str(v) for v in e.get("values") or []])
+                      for e in t.get("matchFields") or []]
+            self.terms.append((exprs, fields))
+
+    @staticmethod
+    def _req(op: str, has: bool, val: str, vals: list) -> bool:
+        if op == "In":
+            return has and val in vals
+        if op == "NotIn":
+            return not has or val not in vals
+        if op == "Exists":
+            return has
+        if op == "DoesNotExist":
+            return not has
+        if op in ("Gt", "Lt"):
+            if not has or len(vals) != 1:
+                return False
+            try:
+                a, b = int(val), int(vals[0])
+            except ValueError:
+                return False
+            return a > b if op == "Gt" else a < b
+        raise ValueError(f"unknown node selector operator {op!r}")
+
+    def matches(self, node_name: str, labels: Optional[Mapping[str, str]]) -> bool:
+        labels = labels or {}
+        for exprs, fields in self.terms:
+            if not exprs and not fields:
+                continue
+            if all(self._req(op, k in labels, labels.get(k, ""), vals) for k, op, vals in exprs) and \
+                    all(k == "metadata.name" and self._req(op, True, node_name, vals) for k, op, vals in fields):
+                return True
+        return False

@@ -1,10 +1,12 @@
 """In-tree default plugins (the upstream v1.20 set the reference's profile keeps).
 
 Hot filters/scores are *native*: they declare an engine binding and run inside the
-C++ cycle (``native/core/engine.cpp``). Plugins whose upstream behaviour depends on
-objects this scheduler does not model yet (volumes, inter-pod affinity, topology
-spread, images) are registered as inert so reference configs load unchanged; they
-are listed in ``INERT_PLUGINS`` and documented in README as not yet implemented.
+C++ cycle (``native/core/engine.cpp``). The object-dependent ones — topology spread and
+inter-pod affinity (``spread_affinity.py``), the volume plugins (``volumes.py``),
+ImageLocality and NodePreferAvoidPods (``node_extras.py``) — are Python plugins that are
+no-ops for pods they do not apply to, so those pods stay on the native path. Only
+plugins that v1.20 already dropped from its defaults (``INERT_PLUGINS``: legacy policy
+predicates) are registered as inert so older configs still load.
 """
 from __future__ import annotations
 
@@ -116,9 +118,7 @@ def _inert(name: str):
     return type(name, (_Inert,), {"name": name})
 
 
-INERT_PLUGINS = ["VolumeRestrictions", "EBSLimits", "GCEPDLimits", "NodeVolumeLimits", "AzureDiskLimits",
-                 "VolumeBinding", "VolumeZone", "ImageLocality",
-                 "NodePreferAvoidPods", "NodeLabel", "ServiceAffinity", "SelectorSpread", "CSILimits"]
+INERT_PLUGINS = ["NodeLabel", "ServiceAffinity", "SelectorSpread", "CSILimits"]
 
 
 class DefaultBinder(BindPlugin):
@@ -197,5 +197,9 @@ def register_defaults(registry) -> None:
     from .spread_affinity import InterPodAffinity, PodTopologySpread
     registry.register(PodTopologySpread.name, PodTopologySpread)
     registry.register(InterPodAffinity.name, InterPodAffinity)
+    from .node_extras import ImageLocality, NodePreferAvoidPods
+    from .volumes import VOLUME_PLUGINS
+    for cls in (ImageLocality, NodePreferAvoidPods, *VOLUME_PLUGINS):
+        registry.register(cls.name, cls)
     for n in INERT_PLUGINS:
         registry.register(n, _inert(n))

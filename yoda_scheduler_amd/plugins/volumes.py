@@ -1,0 +1,485 @@
+"""Volume plugins of the upstream default profile (the reference's profile only
+lists ``yoda``, so kube-scheduler v1.20's volume Filter/Reserve/PreBind plugins stay on):
+
+* ``VolumeRestrictions`` — in-tree disks that cannot be mounted twice on one node
+  (GCE PD / AWS EBS / RBD / iSCSI conflict rules).
+* ``VolumeZone`` — a bound PV's zone/region labels must match the node's.
+* ``VolumeBinding`` — PVCs must exist; bound PVs' node affinity must admit the node;
+  ``WaitForFirstConsumer`` claims get a matching static PV (smallest that fits) or dynamic
+  provisioning on that node; Reserve assumes the choice, PreBind writes it to the
+  apiserver and waits until the PV controller reports the claims bound.
+* ``NodeVolumeLimits`` (CSI attach limits from ``CSINode``) and the in-tree
+  ``EBSLimits`` / ``GCEPDLimits`` / ``AzureDiskLimits`` counters.
+
+All of them are no-ops for pods without the relevant volumes (``is_noop_for``), so GPU
+pods without PVCs keep the fully native scheduling cycle. The objects come from
+informers the scheduler starts only because these plugins declare ``watches``.
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+from typing import Optional
+
+from ..framework.interfaces import (Code, CycleState, FilterPlugin, PreBindPlugin, PreFilterPlugin, ReservePlugin,
+                                    StateData, Status)
+from ..models.selectors import LabelSelector, NodeSelector
+from ..utils.quantity import bytes_of
+
+ZONE_LABELS = ("topology.kubernetes.io/zone", "topology.kubernetes.io/region",
+               "failure-domain.beta.kubernetes.io/zone", "failure-domain.beta.kubernetes.io/region")
+ANN_SELECTED_NODE = "volume.kubernetes.io/selected-node"
+NO_PROVISIONER = "kubernetes.io/no-provisioner"
+WFFC = "WaitForFirstConsumer"
+
+ERR_DISK_CONFLICT = "node(s) had no available disk"
+ERR_ZONE_CONFLICT = "node(s) had no available volume zone"
+ERR_NODE_CONFLICT = "node(s) had volume node affinity conflict"
+ERR_NO_PV = "node(s) didn't find available persistent volumes to bind"
+ERR_UNBOUND_IMMEDIATE = "pod has unbound immediate PersistentVolumeClaims"
+ERR_MAX_VOLUMES = "node(s) exceed max volume count"
+
+
+def _volumes(pod) -> list:
+    return (pod.obj.get("spec") or {}).get("volumes") or []
+
+
+def _claim_names(pod) -> list[str]:
+    out = []
+    for v in _volumes(pod):
+        if "persistentVolumeClaim" in v:
+            out.append((v["persistentVolumeClaim"] or {}).get("claimName", ""))
+        elif "ephemeral" in v:                      # generic ephemeral volume → <pod>-<volume>
+            out.append(f"{pod.name}-{v.get('name', '')}")
+    return out
+
+
+def _unresolvable(msg: str, plugin: str) -> Status:
+    return Status(Code.UNSCHEDULABLE_AND_UNRESOLVABLE, [msg], plugin)
+
+
+class _VolumeBase:
+    watches = ("persistentvolumeclaims", "persistentvolumes", "storageclasses")
+
+    def _lister(self, res: str) -> dict:
+        return self.handle.lister(res)
+
+    def _pvc(self, ns: str, name: str) -> Optional[dict]:
+        return self._lister("persistentvolumeclaims").get(f"{ns}/{name}")
+
+    def _pv(self, name: str) -> Optional[dict]:
+        return self._lister("persistentvolumes").get(name) if name else None
+
+    def _sc(self, name: str) -> Optional[dict]:
+        return self._lister("storageclasses").get(name) if name else None
+
+    def _node_labels(self, node: str) -> dict:
+        n = self.handle.cache.nodes.get(node)
+        return n.labels if n is not None else {}
+
+    def _node_pod_objs(self, node: str):
+        cache = self.handle.cache
+        for uid in cache.node_pods.get(node, ()):
+            ps = cache.pods.get(uid)
+            if ps is not None:
+                yield ps.info.obj
+
+
+# ================================================================= VolumeRestrictions
+def _disk_conflict(a: dict, b: dict) -> bool:
+    if "gcePersistentDisk" in a and "gcePersistentDisk" in b:
+        x, y = a["gcePersistentDisk"] or {}, b["gcePersistentDisk"] or {}
+        return x.get("pdName") == y.get("pdName") and not (x.get("readOnly") and y.get("readOnly"))
+    if "awsElasticBlockStore" in a and "awsElasticBlockStore" in b:
+        return (a["awsElasticBlockStore"] or {}).get("volumeID") == (b["awsElasticBlockStore"] or {}).get("volumeID")
+    if "iscsi" in a and "iscsi" in b:
+        x, y = a["iscsi"] or {}, b["iscsi"] or {}
+        return x.get("iqn") == y.get("iqn") and not (x.get("readOnly") and y.get("readOnly"))
+    if "rbd" in a and "rbd" in b:
+        x, y = a["rbd"] or {}, b["rbd"] or {}
+        share_mon = bool(set(x.get("monitors") or []) & set(y.get("monitors") or []))
+        return (share_mon and x.get("pool", "rbd") == y.get("pool", "rbd") and x.get("image") == y.get("image")
+                and not (x.get("readOnly") and y.get("readOnly")))
+    return False
+
+
+_EXCLUSIVE_KINDS = ("gcePersistentDisk", "awsElasticBlockStore", "iscsi", "rbd")
+
+
+class VolumeRestrictions(_VolumeBase, FilterPlugin):
+    name = "VolumeRestrictions"
+    watches = ()
+
+    def is_noop_for(self, pod) -> bool:
+        return not any(k in v for v in _volumes(pod) for k in _EXCLUSIVE_KINDS)
+
+    def filter(self, state: CycleState, pod, node_name: str) -> Status:
+        mine = [v for v in _volumes(pod) if any(k in v for k in _EXCLUSIVE_KINDS)]
+        for obj in self._node_pod_objs(node_name):
+            for ev in (obj.get("spec") or {}).get("volumes") or ():
+                for v in mine:
+                    if _disk_conflict(v, ev):
+                        return Status.unschedulable(ERR_DISK_CONFLICT, plugin=self.name)
+        return Status.ok()
+
+
+# ================================================================= VolumeZone
+class VolumeZone(_VolumeBase, FilterPlugin):
+    name = "VolumeZone"
+
+    def is_noop_for(self, pod) -> bool:
+        return not _claim_names(pod)
+
+    def filter(self, state: CycleState, pod, node_name: str) -> Status:
+        labels = self._node_labels(node_name)
+        node_zone = {k: labels[k] for k in ZONE_LABELS if k in labels}
+        if not node_zone:
+            return Status.ok()          # a node without zone labels takes any volume
+        for claim in _claim_names(pod):
+            pvc = self._pvc(pod.namespace, claim)
+            if pvc is None:
+                return _unresolvable(f'persistentvolumeclaim "{claim}" not found', self.name)
+            pv_name = (pvc.get("spec") or {}).get("volumeName", "")
+            if not pv_name:
+                scn = (pvc.get("spec") or {}).get("storageClassName", "")
+                if not scn:
+                    return _unresolvable("PersistentVolumeClaim had no pv name and storageClass name", self.name)
+                sc = self._sc(scn)
+                if sc is None:
+                    return _unresolvable(f'StorageClass "{scn}" claimed by PersistentVolumeClaim "{claim}" not found',
+                                         self.name)
+                if sc.get("volumeBindingMode") == WFFC:
+                    continue            # VolumeBinding decides where it is provisioned
+                return _unresolvable("PersistentVolume had no name", self.name)
+            pv = self._pv(pv_name)
+            if pv is None:
+                return _unresolvable(f'persistentvolume "{pv_name}" not found', self.name)
+            pv_labels = (pv.get("metadata") or {}).get("labels") or {}
+            for k in ZONE_LABELS:
+                if k not in pv_labels:
+                    continue
+                allowed = set(pv_labels[k].split("__"))
+                if k not in node_zone or node_zone[k] not in allowed:
+                    return _unresolvable(ERR_ZONE_CONFLICT, self.name)
+        return Status.ok()
+
+
+# ================================================================= VolumeBinding
+def _pvc_key(pvc: dict) -> str:
+    m = pvc.get("metadata") or {}
+    return f"{m.get('namespace') or 'default'}/{m.get('name', '')}"
+
+
+def _storage(obj: dict, *path) -> int:
+    cur = obj
+    for p in path:
+        cur = (cur or {}).get(p)
+    return bytes_of(cur or "0")
+
+
+def _pv_class(pv: dict) -> str:
+    return (pv.get("spec") or {}).get("storageClassName", "") or ""
+
+
+def _pv_node_ok(pv: dict, node: str, labels: dict) -> bool:
+    req = ((pv.get("spec") or {}).get("nodeAffinity") or {}).get("required")
+    return req is None or NodeSelector(req).matches(node, labels)
+
+
+class _BindingState(StateData):
+    def __init__(self, bound, delayed, candidates) -> None:
+        self.bound = bound                  # [(pvc, pv)] already bound claims
+        self.delayed = delayed              # [pvc] unbound WaitForFirstConsumer claims
+        self.candidates = candidates        # pvc key → [pv] static candidates, smallest first
+        self.decisions: dict[str, tuple[list, list]] = {}   # node → ([(pvc, pv name)], [pvc to provision])
+
+    def clone(self) -> "_BindingState":
+        return self
+
+
+class VolumeBinding(_VolumeBase, PreFilterPlugin, FilterPlugin, ReservePlugin, PreBindPlugin):
+    name = "VolumeBinding"
+    KEY = "PreFilterVolumeBinding"
+
+    def __init__(self, args=None, handle=None) -> None:
+        super().__init__(args, handle)
+        self.bind_timeout = float((args or {}).get("bindTimeoutSeconds", 600))
+        self._assumed: dict[str, str] = {}      # pv name → pvc key (chosen, not yet bound)
+        self._pod_choice: dict[str, tuple[list, list]] = {}   # pod uid → decision
+
+    def is_noop_for(self, pod) -> bool:
+        return not _claim_names(pod)
+
+    def pre_filter(self, state: CycleState, pod) -> Status:
+        bound, delayed, immediate = [], [], 0
+        for claim in _claim_names(pod):
+            pvc = self._pvc(pod.namespace, claim)
+            if pvc is None:
+                return _unresolvable(f'persistentvolumeclaim "{claim}" not found', self.name)
+            if (pvc.get("metadata") or {}).get("deletionTimestamp"):
+                return _unresolvable(f'persistentvolumeclaim "{claim}" is being deleted', self.name)
+            spec = pvc.get("spec") or {}
+            if spec.get("volumeName"):
+                bound.append((pvc, self._pv(spec["volumeName"])))
+                continue
+            sc = self._sc(spec.get("storageClassName", ""))
+            if sc is not None and sc.get("volumeBindingMode") == WFFC:
+                delayed.append(pvc)
+            else:
+                immediate += 1
+        if immediate:
+            return _unresolvable(ERR_UNBOUND_IMMEDIATE, self.name)
+        candidates = {_pvc_key(p): self._static_candidates(p) for p in delayed}
+        state.write(self.KEY, _BindingState(bound, delayed, candidates))
+        return Status.ok()
+
+    def _static_candidates(self, pvc: dict) -> list[dict]:
+        spec = pvc.get("spec") or {}
+        key = _pvc_key(pvc)
+        want = _storage(pvc, "spec", "resources", "requests", "storage")
+        modes = set(spec.get("accessModes") or [])
+        vmode = spec.get("volumeMode") or "Filesystem"
+        scn = spec.get("storageClassName", "") or ""
+        sel = LabelSelector(spec["selector"]) if spec.get("selector") else None
+        uid = (pvc.get("metadata") or {}).get("uid")
+        out = []
+        for pv in self._lister("persistentvolumes").values():
+            ps = pv.get("spec") or {}
+            name = (pv.get("metadata") or {}).get("name", "")
+            ref = ps.get("claimRef")
+            if ref and not (ref.get("uid") == uid or (not ref.get("uid") and
+                                                      f"{ref.get('namespace')}/{ref.get('name')}" == key)):
+                continue
+            if self._assumed.get(name, key) != key:
+                continue
+            if _pv_class(pv) != scn or (ps.get("volumeMode") or "Filesystem") != vmode:
+                continue
+            if (pv.get("status") or {}).get("phase", "Available") not in ("Available", "Pending", ""):
+                continue
+            if _storage(pv, "spec", "capacity", "storage") < want or not modes <= set(ps.get("accessModes") or []):
+                continue
+            if sel is not None and not sel.matches((pv.get("metadata") or {}).get("labels")):
+                continue
+            out.append(pv)
+        out.sort(key=lambda p: (_storage(p, "spec", "capacity", "storage"), p["metadata"]["name"]))
+        return out
+
+    def _can_provision(self, pvc: dict, node: str, labels: dict) -> bool:
+        sc = self._sc((pvc.get("spec") or {}).get("storageClassName", ""))
+        if sc is None or sc.get("provisioner", NO_PROVISIONER) == NO_PROVISIONER:
+            return False
+        topo = sc.get("allowedTopologies")
+        if not topo:
+            return True
+        for term in topo:
+            exprs = term.get("matchLabelExpressions") or []
+            if all(labels.get(e.get("key")) in (e.get("values") or []) for e in exprs):
+                return True
+        return False
+
+    def filter(self, state: CycleState, pod, node_name: str) -> Status:
+        try:
+            s: _BindingState = state.read(self.KEY)
+        except KeyError:
+            return Status.ok()
+        labels = self._node_labels(node_name)
+        for pvc, pv in s.bound:
+            if pv is None:
+                return _unresolvable(f'persistentvolume "{pvc["spec"]["volumeName"]}" not found', self.name)
+            if not _pv_node_ok(pv, node_name, labels):
+                return _unresolvable(ERR_NODE_CONFLICT, self.name)
+        static, provision, taken = [], [], set()
+        for pvc in s.delayed:
+            pick = None
+            for pv in s.candidates[_pvc_key(pvc)]:
+                name = pv["metadata"]["name"]
+                if name not in taken and _pv_node_ok(pv, node_name, labels):
+                    pick = name
+                    break
+            if pick is not None:
+                taken.add(pick)
+                static.append((pvc, pick))
+            elif self._can_provision(pvc, node_name, labels):
+                provision.append(pvc)
+            else:
+                return Status.unschedulable(ERR_NO_PV, plugin=self.name)
+        with state.lock():
+            s.decisions[node_name] = (static, provision)
+        return Status.ok()
+
+    def reserve(self, state: CycleState, pod, node_name: str) -> Status:
+        try:
+            s: _BindingState = state.read(self.KEY)
+        except KeyError:
+            return Status.ok()
+        static, provision = s.decisions.get(node_name, ([], []))
+        for pvc, pv_name in static:
+            owner = self._assumed.get(pv_name)
+            if owner is not None and owner != _pvc_key(pvc):
+                self.unreserve(state, pod, node_name)
+                return Status.error(f"persistentvolume {pv_name} was assumed by {owner}", plugin=self.name)
+            self._assumed[pv_name] = _pvc_key(pvc)
+        self._pod_choice[pod.uid] = (static, provision)
+        return Status.ok()
+
+    def unreserve(self, state: CycleState, pod, node_name: str) -> None:
+        static, _ = self._pod_choice.pop(pod.uid, ([], []))
+        for pvc, pv_name in static:
+            if self._assumed.get(pv_name) == _pvc_key(pvc):
+                self._assumed.pop(pv_name, None)
+
+    async def pre_bind(self, state: CycleState, pod, node_name: str) -> Status:
+        choice = self._pod_choice.get(pod.uid)
+        if choice is None:
+            return Status.ok()
+        static, provision = choice
+        client = self.handle.client
+        try:
+            for pvc, pv_name in static:
+                m = pvc["metadata"]
+                ref = {"kind": "PersistentVolumeClaim", "apiVersion": "v1", "namespace": m.get("namespace", "default"),
+                       "name": m["name"], "uid": m.get("uid", "")}
+                await client.patch("persistentvolumes", pv_name, {"spec": {"claimRef": ref}})
+            for pvc in provision:
+                m = pvc["metadata"]
+                await client.patch("persistentvolumeclaims", m["name"],
+                                   {"metadata": {"annotations": {ANN_SELECTED_NODE: node_name}}},
+                                   namespace=m.get("namespace", "default"))
+            keys = [_pvc_key(p) for p, _ in static] + [_pvc_key(p) for p in provision]
+            deadline = time.monotonic() + self.bind_timeout
+            pvcs = self._lister("persistentvolumeclaims")
+            while True:
+                if all(((pvcs.get(k) or {}).get("status") or {}).get("phase") == "Bound" for k in keys):
+                    break
+                if time.monotonic() > deadline:
+                    return Status.error(f"binding volumes: timed out waiting for {len(keys)} claim(s)",
+                                        plugin=self.name)
+                await asyncio.sleep(0.01)
+        except Exception as e:  # noqa: BLE001 - apiserver errors fail the bind (pod is retried)
+            return Status.error(f"binding volumes: {e}", plugin=self.name)
+        finally:
+            self.unreserve(state, pod, node_name)
+        return Status.ok()
+
+
+# ================================================================= attach limits
+class _LimitsBase(_VolumeBase, FilterPlugin):
+    """Counts unique attachable volumes per (driver) on the node plus the pod's new ones."""
+
+    def _pod_ids(self, ns: str, spec: dict) -> dict[str, set[str]]:
+        raise NotImplementedError
+
+    def _limits(self, node: str) -> dict[str, int]:
+        raise NotImplementedError
+
+    def filter(self, state: CycleState, pod, node_name: str) -> Status:
+        mine = self._pod_ids(pod.namespace, pod.obj.get("spec") or {})
+        if not any(mine.values()):
+            return Status.ok()
+        limits = self._limits(node_name)
+        if not limits:
+            return Status.ok()
+        attached: dict[str, set[str]] = {}
+        for obj in self._node_pod_objs(node_name):
+            ns = (obj.get("metadata") or {}).get("namespace", "default")
+            for d, ids in self._pod_ids(ns, obj.get("spec") or {}).items():
+                attached.setdefault(d, set()).update(ids)
+        for d, ids in mine.items():
+            lim = limits.get(d)
+            if lim is not None and len(attached.get(d, set()) | ids) > lim:
+                return Status.unschedulable(ERR_MAX_VOLUMES, plugin=self.name)
+        return Status.ok()
+
+
+class NodeVolumeLimits(_LimitsBase):
+    """CSI attach limits: ``CSINode.spec.drivers[].allocatable.count`` (or node allocatable
+    ``attachable-volumes-csi-<driver>``)."""
+    name = "NodeVolumeLimits"
+    watches = ("persistentvolumeclaims", "persistentvolumes", "storageclasses", "csinodes")
+
+    def is_noop_for(self, pod) -> bool:
+        return not _claim_names(pod)
+
+    def _pod_ids(self, ns: str, spec: dict) -> dict[str, set[str]]:
+        out: dict[str, set[str]] = {}
+        for v in spec.get("volumes") or ():
+            if "persistentVolumeClaim" not in v:
+                continue
+            claim = (v["persistentVolumeClaim"] or {}).get("claimName", "")
+            pvc = self._pvc(ns, claim)
+            if pvc is None:
+                continue
+            pv = self._pv((pvc.get("spec") or {}).get("volumeName", ""))
+            if pv is not None:
+                csi = (pv.get("spec") or {}).get("csi")
+                if csi:
+                    d = csi.get("driver", "")
+                    out.setdefault(d, set()).add(f"{d}/{csi.get('volumeHandle', '')}")
+                continue
+            sc = self._sc((pvc.get("spec") or {}).get("storageClassName", ""))
+            if sc is not None and sc.get("provisioner", NO_PROVISIONER) != NO_PROVISIONER:
+                d = sc["provisioner"]
+                out.setdefault(d, set()).add(f"{d}/{ns}/{claim}")
+        return out
+
+    def _limits(self, node: str) -> dict[str, int]:
+        out: dict[str, int] = {}
+        n = self.handle.cache.nodes.get(node)
+        if n is not None:
+            alloc = (n.obj.get("status") or {}).get("allocatable") or {}
+            for k, v in alloc.items():
+                if k.startswith("attachable-volumes-csi-"):
+                    out[k[len("attachable-volumes-csi-"):]] = int(v)
+        csinode = self._lister("csinodes").get(node)
+        for d in ((csinode or {}).get("spec") or {}).get("drivers") or ():
+            cnt = (d.get("allocatable") or {}).get("count")
+            if cnt is not None:
+                out[d.get("name", "")] = int(cnt)
+        return out
+
+
+class _InTreeLimits(_LimitsBase):
+    kind = ""
+    id_field = ""
+    alloc_key = ""
+    default_max = 0
+
+    def is_noop_for(self, pod) -> bool:
+        return not any(self.kind in v or "persistentVolumeClaim" in v for v in _volumes(pod))
+
+    def _pod_ids(self, ns: str, spec: dict) -> dict[str, set[str]]:
+        ids: set[str] = set()
+        for v in spec.get("volumes") or ():
+            if self.kind in v:
+                ids.add(str((v[self.kind] or {}).get(self.id_field, "")))
+            elif "persistentVolumeClaim" in v:
+                pvc = self._pvc(ns, (v["persistentVolumeClaim"] or {}).get("claimName", ""))
+                pv = self._pv(((pvc or {}).get("spec") or {}).get("volumeName", ""))
+                src = ((pv or {}).get("spec") or {}).get(self.kind)
+                if src:
+                    ids.add(str(src.get(self.id_field, "")))
+        return {self.kind: ids} if ids else {}
+
+    def _limits(self, node: str) -> dict[str, int]:
+        n = self.handle.cache.nodes.get(node)
+        alloc = ((n.obj.get("status") or {}).get("allocatable") or {}) if n is not None else {}
+        return {self.kind: int(alloc.get(self.alloc_key, self.default_max))}
+
+
+class EBSLimits(_InTreeLimits):
+    name = "EBSLimits"
+    kind, id_field, alloc_key, default_max = "awsElasticBlockStore", "volumeID", "attachable-volumes-aws-ebs", 39
+
+
+class GCEPDLimits(_InTreeLimits):
+    name = "GCEPDLimits"
+    kind, id_field, alloc_key, default_max = "gcePersistentDisk", "pdName", "attachable-volumes-gce-pd", 16
+
+
+class AzureDiskLimits(_InTreeLimits):
+    name = "AzureDiskLimits"
+    kind, id_field, alloc_key, default_max = "azureDisk", "diskName", "attachable-volumes-azure-disk", 16
+
+
+VOLUME_PLUGINS = (VolumeRestrictions, VolumeZone, VolumeBinding, NodeVolumeLimits, EBSLimits, GCEPDLimits,
+                  AzureDiskLimits)
