@@ -1,6 +1,8 @@
 // amd-smi collector implementation (see collector.hpp).
 #include "collector.hpp"
 
+#include <cmath>
+
 #include <amd_smi/amdsmi.h>
 
 #include <algorithm>
@@ -26,12 +28,38 @@ std::string bdf_str(const amdsmi_bdf_t& b) {
   return buf;
 }
 
+// JSON string body: escape quotes/backslashes, drop control characters, and replace bytes
+// that are not part of a well-formed UTF-8 sequence (driver strings are not guaranteed
+// UTF-8; the Python side decodes the JSON strictly).
 std::string esc(const std::string& s) {
   std::string o;
-  for (char c : s) {
-    if (c == '"' || c == '\\') o += '\\';
-    if ((unsigned char)c < 0x20) continue;
-    o += c;
+  o.reserve(s.size());
+  const size_t n = s.size();
+  for (size_t i = 0; i < n;) {
+    const unsigned char c = (unsigned char)s[i];
+    if (c < 0x80) {
+      if (c == '"' || c == '\\') o += '\\';
+      if (c >= 0x20) o += (char)c;
+      ++i;
+      continue;
+    }
+    int len = (c >= 0xC2 && c <= 0xDF) ? 2 : (c >= 0xE0 && c <= 0xEF) ? 3 : (c >= 0xF0 && c <= 0xF4) ? 4 : 0;
+    bool ok = len > 0 && i + len <= n;
+    for (int k = 1; ok && k < len; ++k) ok = ((unsigned char)s[i + k] & 0xC0) == 0x80;
+    if (ok && len == 3) {
+      const unsigned char c1 = (unsigned char)s[i + 1];
+      ok = !(c == 0xE0 && c1 < 0xA0) && !(c == 0xED && c1 >= 0xA0);   // overlong / surrogates
+    } else if (ok && len == 4) {
+      const unsigned char c1 = (unsigned char)s[i + 1];
+      ok = !(c == 0xF0 && c1 < 0x90) && !(c == 0xF4 && c1 >= 0x90);
+    }
+    if (ok) {
+      o.append(s, i, len);
+      i += len;
+    } else {
+      o += '?';
+      ++i;
+    }
   }
   return o;
 }
@@ -194,6 +222,9 @@ std::vector<GpuSample> Collector::sample() {
   return out;
 }
 
+// JSON has no NaN/Inf literals
+static double finite(double v) { return std::isfinite(v) ? v : 0.0; }
+
 std::string to_json(const std::vector<GpuSample>& s) {
   std::ostringstream o;
   o.precision(17);
@@ -210,16 +241,17 @@ std::string to_json(const std::vector<GpuSample>& s) {
       << ",\"eccUncorrectable\":" << g.ecc_uncorrectable << ",\"eccCorrectable\":" << g.ecc_correctable
       << ",\"numaNode\":" << g.numa << ",\"computePartition\":\"" << esc(g.compute_partition)
       << "\",\"memoryPartition\":\"" << esc(g.memory_partition) << "\",\"xgmiLinksUp\":" << g.links_up
-      << ",\"xgmiLinksDown\":" << g.links_down << ",\"time\":" << g.t << ",\"links\":[";
+      << ",\"xgmiLinksDown\":" << g.links_down << ",\"time\":" << finite(g.t) << ",\"links\":[";
     for (size_t l = 0; l < g.links.size(); ++l) {
       const LinkSample& x = g.links[l];
       if (l) o << ",";
       o << "{\"peerBdf\":\"" << esc(x.peer_bdf) << "\",\"type\":" << x.type << ",\"bitRateGbps\":" << x.bit_rate
         << ",\"maxBandwidthGbps\":" << x.max_bw << ",\"readKB\":" << x.read_kb << ",\"writeKB\":" << x.write_kb
-        << ",\"readKBps\":" << x.read_kbps << ",\"writeKBps\":" << x.write_kbps << ",\"load\":" << x.load << "}";
+        << ",\"readKBps\":" << finite(x.read_kbps) << ",\"writeKBps\":" << finite(x.write_kbps)
+        << ",\"load\":" << finite(x.load) << "}";
     }
     o << "],\"errors\":[";
-    for (size_t e = 0; e < g.errors.size(); ++e) o << (e ? "," : "") << "\"" << g.errors[e] << "\"";
+    for (size_t e = 0; e < g.errors.size(); ++e) o << (e ? "," : "") << "\"" << esc(g.errors[e]) << "\"";
     o << "]}";
   }
   o << "]";

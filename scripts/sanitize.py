@@ -20,6 +20,34 @@ VARIANTS = {
 }
 
 
+SNIFFER = os.path.join(ROOT, "native", "sniffer")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
+def run_sniffer(variant: str = "asan-ubsan", iters: int = 3000) -> int:
+    """The amd-smi collector's host code (JSON encoding fuzz + real sampling when a
+    driver is present) under ASan+UBSan; the emitted JSON must parse."""
+    import json
+    out = os.path.join(tempfile.gettempdir(), f"yoda_sniffer_stress_{variant}")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", *VARIANTS[variant], f"-I{ROCM}/include",
+           os.path.join(SNIFFER, "collector.cpp"), os.path.join(SNIFFER, "stress_main.cpp"), "-o", out,
+           f"-L{ROCM}/lib", "-lamd_smi", f"-Wl,-rpath,{ROCM}/lib", "-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stderr)
+        return r.returncode
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
+    env.pop("LD_PRELOAD", None)
+    r = subprocess.run([out, str(iters)], capture_output=True, text=True, env=env, timeout=600)
+    sys.stdout.write(f"[sniffer-{variant}] {r.stderr.strip()[-300:]}\n")
+    if r.returncode != 0:
+        sys.stderr.write(r.stderr[-4000:])
+        return r.returncode
+    doc = json.loads(r.stdout.strip().splitlines()[-1])
+    assert isinstance(doc, list) and len(doc) == 8, doc
+    return 0
+
+
 def run(variant: str, nodes: int = 700, steps: int = 2000, threads: int = 4) -> int:
     # > 512 nodes so the ThreadPool parallel filter/score paths run under TSan
     flags = VARIANTS[variant]
@@ -49,6 +77,7 @@ def main() -> int:
     rc = 0
     for v in VARIANTS:
         rc |= run(v)
+    rc |= run_sniffer()
     return rc
 
 

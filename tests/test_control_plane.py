@@ -260,12 +260,20 @@ def test_cli_fake_cluster_serves_health_and_schedules():
                     health = await r.text()
                 async with s.get(f"http://127.0.0.1:{status_port}/metrics") as r:
                     metrics = await r.text()
-            return pod, health, metrics
+                async with s.get(f"http://127.0.0.1:{status_port}/debug/pprof/profile?seconds=0.3&limit=5") as r:
+                    prof = await r.text()
+                async with s.get(f"http://127.0.0.1:{status_port}/debug/pprof/goroutine") as r:
+                    stacks = await r.text()
+                async with s.get(f"http://127.0.0.1:{status_port}/debug/pprof/heap") as r:
+                    heap = await r.json()
+                async with s.get(f"http://127.0.0.1:{status_port}/configz") as r:
+                    configz = await r.json()
+            return pod, health, metrics, (prof, stacks, heap, configz)
         finally:
             await cl.close()
 
     try:
-        pod, health, metrics = run(go())
+        pod, health, metrics, (prof, stacks, heap, configz) = run(go())
     finally:
         proc.terminate()
         try:
@@ -275,6 +283,8 @@ def test_cli_fake_cluster_serves_health_and_schedules():
     assert pod["spec"]["nodeName"].startswith("mi355x-")
     assert health == "ok"
     assert "scheduler_schedule_attempts_total" in metrics
+    assert "function calls" in prof and "asyncio task(s)" in stacks and heap["objects"] > 0
+    assert "componentconfig" in configz
 
 
 def test_tracer_chrome_trace():

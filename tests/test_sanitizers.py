@@ -15,3 +15,10 @@ def test_engine_stress_under_sanitizers(variant):
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import sanitize
     assert sanitize.run(variant) == 0
+
+
+@pytest.mark.slow
+def test_sniffer_json_under_sanitizers():
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import sanitize
+    assert sanitize.run_sniffer("asan-ubsan") == 0

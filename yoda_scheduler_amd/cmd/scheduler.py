@@ -145,7 +145,8 @@ async def _run(args, cfg, registry: Registry) -> int:
                                          "scheduled": sched.scheduled, "failed": sched.failed,
                                          "device_cycles": sched.engine.device_cycles,
                                          "device_error": sched.device_error},
-                          trace=lambda: sched.tracer.chrome_trace() if sched.tracer else {})
+                          trace=lambda: sched.tracer.chrome_trace() if sched.tracer else {},
+                          profiling=cfg.enable_profiling)
     try:
         log.info("serving /healthz and /metrics on port %d", await status.start())
     except OSError as e:

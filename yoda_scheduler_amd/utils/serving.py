@@ -11,7 +11,8 @@ from aiohttp import web
 class StatusServer:
     def __init__(self, host: str, port: int, metrics_render: Callable[[], bytes],
                  healthy: Callable[[], bool] = lambda: True, configz: Optional[Callable[[], dict]] = None,
-                 debug: Optional[Callable[[], dict]] = None, trace: Optional[Callable[[], dict]] = None) -> None:
+                 debug: Optional[Callable[[], dict]] = None, trace: Optional[Callable[[], dict]] = None,
+                 profiling: bool = False) -> None:
         self.host, self.port = host, port
         self.app = web.Application()
         self.app.router.add_get("/healthz", self._health(healthy))
@@ -24,6 +25,24 @@ class StatusServer:
         for path, fn in (("/configz", configz), ("/debug/yoda", debug), ("/debug/trace", trace)):
             if fn is not None:
                 self.app.router.add_get(path, self._json(fn))
+        if profiling:
+            from . import pprof
+
+            async def profile(r):
+                q = r.query
+                txt = await pprof.profile_text(float(q.get("seconds", 5)), q.get("sort", "cumulative"),
+                                               int(q.get("limit", 60)))
+                return web.Response(text=txt)
+
+            async def goroutine(_r):
+                return web.Response(text=pprof.goroutine_text())
+
+            async def heap(_r):
+                return web.json_response(pprof.heap_summary(), dumps=_dumps)
+
+            self.app.router.add_get("/debug/pprof/profile", profile)
+            self.app.router.add_get("/debug/pprof/goroutine", goroutine)
+            self.app.router.add_get("/debug/pprof/heap", heap)
         self._runner: Optional[web.AppRunner] = None
 
     @staticmethod
