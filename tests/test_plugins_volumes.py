@@ -276,3 +276,39 @@ def test_volume_plugins_keep_plain_pods_native():
     assert {"VolumeBinding", "VolumeZone", "VolumeRestrictions", "NodeVolumeLimits", "ImageLocality"} <= names
     assert plain and not with_pvc
     assert {"persistentvolumeclaims", "persistentvolumes", "storageclasses", "csinodes"} <= informers
+
+
+def test_flag_fast_path_agrees_with_plugins():
+    """The one-mask native_for fast path must give the same answer as asking every
+    conditional plugin, for plain pods and for each optional feature."""
+    specs = [
+        {},
+        {"volumes": [{"name": "t", "projected": {"sources": []}}, {"name": "c", "configMap": {"name": "x"}}]},
+        {"volumes": [claim_vol("x")]},
+        {"volumes": [{"name": "e", "ephemeral": {"volumeClaimTemplate": {}}}]},
+        {"volumes": [{"name": "d", "gcePersistentDisk": {"pdName": "a"}}]},
+        {"volumes": [{"name": "d", "azureDisk": {"diskName": "a"}}]},
+        {"containers": [{"name": "c", "image": "x", "ports": [{"containerPort": 80, "hostPort": 8080}]}]},
+        {"topologySpreadConstraints": [{"maxSkew": 1, "topologyKey": "z", "labelSelector": {}}]},
+        {"affinity": {"podAntiAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": []}}},
+        {"affinity": {"nodeAffinity": {}}},
+    ]
+
+    async def go():
+        c = FakeCluster(yoda_config())
+        c.add_node("n0")
+        await c.start()
+        fw = c.sched.frameworks["yoda-scheduler"]
+        out = []
+        for i, sp in enumerate(specs):
+            for owner in (None, {"kind": "ReplicaSet", "uid": "r", "controller": True}):
+                meta = {"name": f"p{i}", "namespace": "default", "uid": f"u{i}"}
+                if owner:
+                    meta["ownerReferences"] = [owner]
+                pi = PodInfo.from_obj({"metadata": meta, "spec": {"schedulerName": "yoda-scheduler", **sp}})
+                out.append((i, bool(owner), fw.native_for(pi), all(p.is_noop_for(pi) for p in fw.conditional)))
+        await c.stop()
+        return out
+    rows = run(go())
+    assert all(fast == slow for _, _, fast, slow in rows), rows
+    assert rows[0][2] and rows[2][2] and not rows[4][2] and not rows[6][2]

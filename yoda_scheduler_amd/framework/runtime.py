@@ -90,10 +90,23 @@ class Framework:
         self.reserve_static = [p for p in self.reserve if not hasattr(p, "is_noop_for")]
         self.fully_native_static = not (static or self.permit)
         self.fully_native = self.fully_native_static and not self.conditional
+        # one-mask fast path: valid when every conditional plugin declares its pod flags
+        # (it is a no-op for pods without them unless its cluster gate is active)
+        self._flag_mask: Optional[int] = 0
+        for p in self.conditional:
+            f = getattr(p, "pod_flags", None)
+            if f is None:
+                self._flag_mask = None
+                break
+            self._flag_mask |= f
+        self._gates = [p.cluster_active for p in self.conditional if hasattr(p, "cluster_active")]
 
     def native_for(self, pod) -> bool:
         if not self.fully_native_static:
             return False
+        m = self._flag_mask
+        if m is not None and not (pod.flags & m) and not any(g() for g in self._gates):
+            return True
         return all(p.is_noop_for(pod) for p in self.conditional)
 
     @staticmethod

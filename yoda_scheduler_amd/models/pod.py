@@ -66,6 +66,37 @@ def _terms(terms: list | None) -> list[list[tuple[str, str, list[str]]]]:
     return out
 
 
+# Pod feature flags: which optional scheduling features a pod uses. Conditional Python
+# plugins declare the flags that make them relevant, so the framework can decide "fully
+# native cycle" for a plain pod with one mask test instead of asking every plugin.
+PF_HOST_PORTS = 1
+PF_SPREAD = 2          # topologySpreadConstraints
+PF_POD_AFFINITY = 4    # podAffinity / podAntiAffinity
+PF_CLAIMS = 8          # persistentVolumeClaim / ephemeral volumes
+PF_DISKS = 16          # in-tree attachable disks (GCE PD, EBS, Azure disk, iSCSI, RBD)
+PF_CONTROLLER = 32     # controlled by a ReplicationController / ReplicaSet
+
+_DISK_KINDS = ("gcePersistentDisk", "awsElasticBlockStore", "azureDisk", "iscsi", "rbd")
+
+
+def pod_flags(meta: dict, spec: dict, host_ports) -> int:
+    f = PF_HOST_PORTS if host_ports else 0
+    if spec.get("topologySpreadConstraints"):
+        f |= PF_SPREAD
+    aff = spec.get("affinity")
+    if aff and (aff.get("podAffinity") or aff.get("podAntiAffinity")):
+        f |= PF_POD_AFFINITY
+    for v in spec.get("volumes") or ():
+        if "persistentVolumeClaim" in v or "ephemeral" in v:
+            f |= PF_CLAIMS
+        elif any(k in v for k in _DISK_KINDS):
+            f |= PF_DISKS
+    for r in meta.get("ownerReferences") or ():
+        if r.get("controller") and r.get("kind") in ("ReplicationController", "ReplicaSet"):
+            f |= PF_CONTROLLER
+    return f
+
+
 class PodInfo:
     """Parsed pod. ``__slots__`` + a hand-written constructor: one of these is built per
     pod per informer event on the scheduling hot path."""
@@ -73,14 +104,15 @@ class PodInfo:
     __slots__ = ("obj", "uid", "namespace", "name", "num_id", "labels", "gpu", "scheduler_name", "node_name",
                  "cpu_m", "mem", "priority", "node_selector", "required_terms", "preferred_terms", "tolerations",
                  "annotations", "host_ports", "attempts", "initial_attempt", "enqueued", "native_req",
-                 "native_owner", "assigned_cards", "_creation")
+                 "native_owner", "assigned_cards", "_creation", "flags")
 
     def __init__(self, obj: dict, uid: str, namespace: str, name: str, num_id: int, labels: dict, gpu: GpuRequest,
                  scheduler_name: str = "default-scheduler", node_name: str = "", cpu_m: int = 0, mem: int = 0,
                  priority: int = 0, node_selector: Optional[dict] = None, required_terms: Optional[list] = None,
                  preferred_terms: Optional[list] = None, tolerations: Optional[list] = None,
-                 annotations: Optional[dict] = None, host_ports: Optional[list] = None) -> None:
+                 annotations: Optional[dict] = None, host_ports: Optional[list] = None, flags: int = 0) -> None:
         self.obj = obj
+        self.flags = flags
         self.uid = uid
         self.namespace = namespace
         self.name = name
@@ -148,7 +180,8 @@ class PodInfo:
         return cls(obj, uid, meta.get("namespace", "default"), meta.get("name", ""), pod_num_id(uid), labels,
                    parse_gpu_request(labels), spec.get("schedulerName") or "default-scheduler",
                    spec.get("nodeName") or "", cpu, mem, int(spec.get("priority") or 0),
-                   dict(ns) if ns else None, req, pref, tols or None, dict(ann) if ann else None, ports)
+                   dict(ns) if ns else None, req, pref, tols or None, dict(ann) if ann else None, ports,
+                   pod_flags(meta, spec, ports))
 
 
 _EMPTY: dict = {}

@@ -15,6 +15,7 @@ from typing import Optional
 from ..framework.interfaces import (BindPlugin, CycleState, FilterPlugin, NativeBinding, Plugin,
                                     PostFilterPlugin, PostFilterResult, QueueSortPlugin, ScorePlugin, Status)
 from ..models.labels import ANNOTATION_GPUS, ANNOTATION_RESERVED
+from ..models.pod import PF_HOST_PORTS
 from ..ops.native import core
 
 
@@ -105,6 +106,8 @@ class NodePorts(FilterPlugin):
                 return Status.unschedulable("node(s) didn't have free ports for the requested pod ports",
                                             plugin=self.name)
         return Status.ok()
+
+    pod_flags = PF_HOST_PORTS
 
     def is_noop_for(self, pod) -> bool:
         return not pod.host_ports

@@ -12,7 +12,7 @@ from __future__ import annotations
 import json
 
 from ..framework.interfaces import CycleState, ScorePlugin, Status, MAX_NODE_SCORE
-from ..models.pod import normalize_image
+from ..models.pod import PF_CONTROLLER, normalize_image
 
 MB = 1024 * 1024
 MIN_THRESHOLD = 23 * MB           # upstream: below this an image is "not there"
@@ -28,6 +28,10 @@ class ImageLocality(ScorePlugin):
     """score = 100·(clamp(Σ size·spread) − 23MB)/(1000MB·#containers − 23MB), where
     spread = (#nodes holding the image)/(#nodes) damps images present everywhere."""
     name = "ImageLocality"
+    pod_flags = 0
+
+    def cluster_active(self) -> bool:
+        return bool(self.handle.cache.image_nodes)
 
     def is_noop_for(self, pod) -> bool:
         have = self.handle.cache.image_nodes
@@ -61,6 +65,7 @@ class NodePreferAvoidPods(ScorePlugin):
     """0 on nodes whose ``scheduler.alpha.kubernetes.io/preferAvoidPods`` annotation names
     the pod's controller, 100 elsewhere."""
     name = "NodePreferAvoidPods"
+    pod_flags = PF_CONTROLLER
 
     def is_noop_for(self, pod) -> bool:
         return not self.handle.cache.avoid_nodes or _controller(pod) is None

@@ -13,6 +13,7 @@ from typing import Optional
 
 from ..framework.interfaces import (CycleState, FilterPlugin, NodeScore, PreFilterPlugin, PreScorePlugin, ScorePlugin,
                                     StateData, Status, MAX_NODE_SCORE)
+from ..models.pod import PF_POD_AFFINITY, PF_SPREAD
 from ..models.selectors import LabelSelector
 
 
@@ -36,6 +37,8 @@ class PodTopologySpread(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlug
     Score (fewer matching pods in the domain scores higher)."""
     name = "PodTopologySpread"
     KEY = "PreFilterPodTopologySpread"
+
+    pod_flags = PF_SPREAD
 
     def is_noop_for(self, pod) -> bool:
         return not _spec(pod).get("topologySpreadConstraints")
@@ -135,6 +138,12 @@ class _AffinityState(StateData):
 class InterPodAffinity(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin):
     name = "InterPodAffinity"
     KEY = "PreFilterInterPodAffinity"
+
+    pod_flags = PF_POD_AFFINITY
+
+    def cluster_active(self) -> bool:
+        """Bound pods with required anti-affinity can reject any new pod (symmetry)."""
+        return bool(self.handle.cache.pods_with_required_anti_affinity())
 
     def is_noop_for(self, pod) -> bool:
         aff = _spec(pod).get("affinity") or {}

@@ -23,6 +23,7 @@ from typing import Optional
 
 from ..framework.interfaces import (Code, CycleState, FilterPlugin, PreBindPlugin, PreFilterPlugin, ReservePlugin,
                                     StateData, Status)
+from ..models.pod import PF_CLAIMS, PF_DISKS
 from ..models.selectors import LabelSelector, NodeSelector
 from ..utils.quantity import bytes_of
 
@@ -109,6 +110,7 @@ _EXCLUSIVE_KINDS = ("gcePersistentDisk", "awsElasticBlockStore", "iscsi", "rbd")
 class VolumeRestrictions(_VolumeBase, FilterPlugin):
     name = "VolumeRestrictions"
     watches = ()
+    pod_flags = PF_DISKS
 
     def is_noop_for(self, pod) -> bool:
         return not any(k in v for v in _volumes(pod) for k in _EXCLUSIVE_KINDS)
@@ -126,6 +128,7 @@ class VolumeRestrictions(_VolumeBase, FilterPlugin):
 # ================================================================= VolumeZone
 class VolumeZone(_VolumeBase, FilterPlugin):
     name = "VolumeZone"
+    pod_flags = PF_CLAIMS
 
     def is_noop_for(self, pod) -> bool:
         return not _claim_names(pod)
@@ -200,6 +203,7 @@ class _BindingState(StateData):
 class VolumeBinding(_VolumeBase, PreFilterPlugin, FilterPlugin, ReservePlugin, PreBindPlugin):
     name = "VolumeBinding"
     KEY = "PreFilterVolumeBinding"
+    pod_flags = PF_CLAIMS
 
     def __init__(self, args=None, handle=None) -> None:
         super().__init__(args, handle)
@@ -395,6 +399,7 @@ class NodeVolumeLimits(_LimitsBase):
     """CSI attach limits: ``CSINode.spec.drivers[].allocatable.count`` (or node allocatable
     ``attachable-volumes-csi-<driver>``)."""
     name = "NodeVolumeLimits"
+    pod_flags = PF_CLAIMS
     watches = ("persistentvolumeclaims", "persistentvolumes", "storageclasses", "csinodes")
 
     def is_noop_for(self, pod) -> bool:
@@ -443,6 +448,7 @@ class _InTreeLimits(_LimitsBase):
     id_field = ""
     alloc_key = ""
     default_max = 0
+    pod_flags = PF_CLAIMS | PF_DISKS
 
     def is_noop_for(self, pod) -> bool:
         return not any(self.kind in v or "persistentVolumeClaim" in v for v in _volumes(pod))
