@@ -129,6 +129,7 @@ PYBIND11_MODULE(_yoda_core, m) {
       .def_property_readonly("device_cycles", &Engine::device_cycles)
       .def_property_readonly("device_fallbacks", &Engine::device_fallbacks)
       .def("device_last_us", &Engine::device_last_us)
+      .def("device_set_timing", &Engine::device_set_timing, py::arg("on"))
       .def("device_eligible", &Engine::device_eligible)
       .def("device_cycle",
            [](Engine& e, const PodReq& r) -> py::object {

@@ -873,6 +873,7 @@ bool Engine::enable_device(const std::string& lib_path, int device, int capacity
   fn_upload_ = dlsym(lib, "yoda_dev_upload");
   fn_schedule_ = dlsym(lib, "yoda_dev_schedule");
   fn_last_us_ = dlsym(lib, "yoda_dev_last_us");
+  fn_set_timing_ = dlsym(lib, "yoda_dev_set_timing");
   if (!create || !fn_destroy_ || !fn_upload_ || !fn_schedule_ || !fn_last_us_) {
     if (err) *err = "libyoda_hip.so lacks the yoda_dev_* entry points";
     dlclose(lib);
@@ -905,6 +906,10 @@ void Engine::disable_device() {
 }
 
 float Engine::device_last_us() const { return dev_ctx_ ? ((dev_last_us_t)fn_last_us_)(dev_ctx_) : 0.f; }
+
+void Engine::device_set_timing(bool on) {
+  if (dev_ctx_ && fn_set_timing_) ((void (*)(void*, int))fn_set_timing_)(dev_ctx_, on ? 1 : 0);
+}
 
 bool Engine::pack_node(int32_t idx, void* out) const {
   yoda_dev_node_t* row = (yoda_dev_node_t*)out;

@@ -249,6 +249,7 @@ class Engine {
   uint64_t device_cycles() const { return dev_cycles_; }
   uint64_t device_fallbacks() const { return dev_fallbacks_; }
   float device_last_us() const;
+  void device_set_timing(bool on);   // per-cycle event timing (benchmarks)
   bool device_eligible(const PodReq& req) const;
   // parity hook: run one device cycle without reserving; false if not eligible/failed
   bool device_cycle(const PodReq& req, CycleResult* out);
@@ -298,6 +299,7 @@ class Engine {
   void* fn_upload_ = nullptr;
   void* fn_schedule_ = nullptr;
   void* fn_last_us_ = nullptr;
+  void* fn_set_timing_ = nullptr;   // optional entry point
   double now() const;
   bool is_pending(const Node& n, const Assignment& a) const { return a.t_res > n.sample_ts - settle_s_; }
   int32_t next_start_ = 0;

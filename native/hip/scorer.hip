@@ -15,14 +15,18 @@
 //    + integer-correction path instead of the ~100-instruction software divide;
 //  * blocks of 4 waves grid-stride over nodes; per-block LDS reductions, XCD-sharded
 //    counters and check-before-atomic max/min keep cross-workgroup atomics to a handful;
-//  * the select kernel's last block (agent-scope ticket, release/acquire per the CDNA
-//    visibility rules) decodes the winner, writes the result straight into mapped pinned
-//    host memory and re-arms the accumulators — 3 launches and no memcpy per pod in the
-//    steady state (dirty node rows ride in a patch kernel's arguments).
+//  * the dirty node rows of the last reservation ride in the filter kernel's arguments
+//    (it reads them from there and block 0 writes them back to the table), and up to
+//    kFuseSelectMax nodes the score kernel's last block (agent-scope ticket, release/
+//    acquire per the CDNA visibility rules) runs the normalise+argmax itself: 2 launches
+//    and no memcpy per pod in the steady state (3 above kFuseSelectMax);
+//  * the winner is written straight into mapped pinned host memory, the `feasible` field
+//    last with a system-scope release, and the host spins on it instead of a stream sync.
 // No MFMA: the work is integer compare/reduce, not matmul-shaped.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
 #include <climits>
 #include <cstdint>
 #include <cstdio>
@@ -43,7 +47,8 @@ constexpr int kWaves = 4;
 constexpr int kBlock = 64 * kWaves;
 constexpr int kGroup = 8;                 // lanes per node
 constexpr int kNodesPerWave = 64 / kGroup;
-constexpr int kPatchRows = 6;             // dirty rows passed by value (6 × 512 B + idx < 4 KiB of kernarg)
+constexpr int kPatchRows = 4;             // dirty rows passed by value (4 × 512 B + the filter's args < 4 KiB)
+constexpr int kFuseSelectMax = 2048;      // one block normalises + argmaxes up to this many nodes
 constexpr int kShards = 8;
 
 struct Globals {
@@ -177,7 +182,65 @@ __global__ void k_scatter(const yoda_dev_node_t* __restrict__ stage, const int32
 }
 
 // ------------------------------------------------------------------ K1: filter + maxima
-__global__ __launch_bounds__(kBlock) void k_filter(const yoda_dev_node_t* __restrict__ nodes, int n,
+// One lane group = one node (lane `sub` = GPU slot). Writes feas/elig, counts the reason,
+// folds the card metrics of feasible nodes into the wave maxima `wmx`.
+__device__ __forceinline__ void filter_group(const yoda_dev_node_t* nd, int i, bool valid, const yoda_dev_req_t& r,
+                                             const uint8_t* __restrict__ cand, uint8_t* __restrict__ feas,
+                                             uint8_t* __restrict__ elig, int* s_reason, unsigned long long* wmx,
+                                             int& nfeas, int grp, int sub) {
+  const bool yoda = (r.filters & F_YODA) != 0;
+  // every load of the node issued up front: one memory round trip per node
+  const uint8_t flags = valid ? nd->flags : 0, ncards = nd->ncards;
+  const uint32_t card_number = nd->card_number;
+  const int64_t pod_count = nd->pod_count, alloc_pods = nd->alloc_pods, alloc_cpu = nd->alloc_cpu,
+                req_cpu = nd->req_cpu, alloc_mem = nd->alloc_mem, req_mem = nd->req_mem;
+  const yoda_dev_card_t cd = nd->cards[sub];
+  const uint8_t healthy = nd->healthy[sub];
+  const uint8_t cnd = (r.use_candidates && valid) ? cand[i] : 0;
+  int reason = 0;
+  if (!(flags & YODA_DEV_ALIVE)) {
+    reason = RS_DEAD;
+  } else if ((r.filters & F_NODE_UNSCHEDULABLE) && (flags & YODA_DEV_UNSCHEDULABLE) && !r.tolerates_unschedulable) {
+    reason = RS_UNSCHEDULABLE;
+  } else if (r.filters & F_NODE_RESOURCES_FIT) {
+    if (pod_count + 1 > alloc_pods) reason = RS_RESOURCES;
+    else if (r.cpu_m > 0 && alloc_cpu < r.cpu_m + req_cpu) reason = RS_RESOURCES;
+    else if (r.mem > 0 && alloc_mem < r.mem + req_mem) reason = RS_RESOURCES;
+  }
+  if (!reason && cnd) reason = cnd;
+  bool yoda_stage = false;
+  if (!reason && yoda) {
+    if (!(flags & YODA_DEV_HAS_SCV)) reason = RS_NO_SCV;
+    else if (r.has_number ? !(r.number <= (uint64_t)card_number) : !(card_number > 0)) reason = RS_GPU_NUMBER;
+    else if (flags & YODA_DEV_STALE) reason = RS_STALE;
+    else yoda_stage = true;
+  }
+  const uint64_t ef = eff_free(cd.free, cd.pending, cd.total, cd.reserved);
+  const bool e = yoda_stage && sub < ncards && healthy && ef >= r.memory &&
+                 (!r.has_clock || (uint64_t)cd.clock == r.clock) && (!r.clock_min || (uint64_t)cd.clock >= r.clock_min);
+  const uint32_t emask = (uint32_t)((__ballot(e) >> (grp * kGroup)) & 0xFFu);
+  if (yoda_stage && (uint64_t)__popc(emask) < r.number) reason = RS_GPU_FIT;
+  const bool ok = valid && reason == 0;
+  if (valid && sub == 0) {
+    feas[i] = ok;
+    elig[i] = (uint8_t)emask;
+    if (reason) atomicAdd(&s_reason[reason], 1);
+  }
+  if (sub == 0 && ok) ++nfeas;
+  if (yoda) {
+    const bool take = ok && ((emask >> sub) & 1u);
+    unsigned long long v[6];
+    v[0] = take ? cd.bandwidth : 0; v[1] = take ? cd.clock : 0; v[2] = take ? cd.core : 0;
+    v[3] = take ? ef : 0; v[4] = take ? cd.power : 0; v[5] = take ? cd.total : 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const unsigned long long m = wmax_across_groups(gmax(v[k]));
+      wmx[k] = m > wmx[k] ? m : wmx[k];
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_filter(const PatchArgs pa, yoda_dev_node_t* __restrict__ nodes, int n,
                                                    const yoda_dev_req_t r, const uint8_t* __restrict__ cand,
                                                    uint8_t* __restrict__ feas, uint8_t* __restrict__ elig,
                                                    Globals* __restrict__ g) {
@@ -189,63 +252,31 @@ __global__ __launch_bounds__(kBlock) void k_filter(const yoda_dev_node_t* __rest
   if (threadIdx.x < YODA_DEV_REASONS) s_reason[threadIdx.x] = 0;
   if (threadIdx.x == 0) s_feas = 0;
   __syncthreads();
-  const bool yoda = (r.filters & F_YODA) != 0;
   unsigned long long wmx[6] = {1, 1, 1, 1, 1, 1};
   int nfeas = 0;
-  const int stride = gridDim.x * kWaves * kNodesPerWave;
-  for (int base = uniform((blockIdx.x * kWaves + wave) * kNodesPerWave); base < n; base += stride) {
-    const int i = base + grp;
-    const bool valid = i < n;
-    const yoda_dev_node_t* nd = nodes + (valid ? i : n - 1);
-    // every load of the node issued up front: one memory round trip per node
-    const uint8_t flags = valid ? nd->flags : 0, ncards = nd->ncards;
-    const uint32_t card_number = nd->card_number;
-    const int64_t pod_count = nd->pod_count, alloc_pods = nd->alloc_pods, alloc_cpu = nd->alloc_cpu,
-                  req_cpu = nd->req_cpu, alloc_mem = nd->alloc_mem, req_mem = nd->req_mem;
-    const yoda_dev_card_t cd = nd->cards[sub];
-    const uint8_t healthy = nd->healthy[sub];
-    const uint8_t cnd = (r.use_candidates && valid) ? cand[i] : 0;
-    int reason = 0;
-    if (!(flags & YODA_DEV_ALIVE)) {
-      reason = RS_DEAD;
-    } else if ((r.filters & F_NODE_UNSCHEDULABLE) && (flags & YODA_DEV_UNSCHEDULABLE) && !r.tolerates_unschedulable) {
-      reason = RS_UNSCHEDULABLE;
-    } else if (r.filters & F_NODE_RESOURCES_FIT) {
-      if (pod_count + 1 > alloc_pods) reason = RS_RESOURCES;
-      else if (r.cpu_m > 0 && alloc_cpu < r.cpu_m + req_cpu) reason = RS_RESOURCES;
-      else if (r.mem > 0 && alloc_mem < r.mem + req_mem) reason = RS_RESOURCES;
+  // with dirty rows the host launches one extra block: it writes them back to the table
+  // for the score kernel and evaluates them from the arguments, in parallel with the rest
+  const int workers = pa.n > 0 ? (int)gridDim.x - 1 : (int)gridDim.x;
+  if ((int)blockIdx.x == workers) {
+    if ((int)(threadIdx.x >> 5) < pa.n) {
+      const int rec = threadIdx.x >> 5;
+      reinterpret_cast<uint4*>(nodes + pa.idx[rec])[threadIdx.x & 31] =
+          reinterpret_cast<const uint4*>(&pa.rows[rec])[threadIdx.x & 31];
     }
-    if (!reason && cnd) reason = cnd;
-    bool yoda_stage = false;
-    if (!reason && yoda) {
-      if (!(flags & YODA_DEV_HAS_SCV)) reason = RS_NO_SCV;
-      else if (r.has_number ? !(r.number <= (uint64_t)card_number) : !(card_number > 0)) reason = RS_GPU_NUMBER;
-      else if (flags & YODA_DEV_STALE) reason = RS_STALE;
-      else yoda_stage = true;
+    if (wave == 0) {
+      const int j = grp < pa.n ? grp : 0;
+      filter_group(&pa.rows[j], pa.idx[j], grp < pa.n && pa.idx[j] < n, r, cand, feas, elig, s_reason, wmx, nfeas,
+                   grp, sub);
     }
-    const uint64_t ef = eff_free(cd.free, cd.pending, cd.total, cd.reserved);
-    const bool e = yoda_stage && sub < ncards && healthy && ef >= r.memory &&
-                   (!r.has_clock || (uint64_t)cd.clock == r.clock) && (!r.clock_min || (uint64_t)cd.clock >= r.clock_min);
-    const uint32_t emask = (uint32_t)((__ballot(e) >> (grp * kGroup)) & 0xFFu);
-    if (yoda_stage && (uint64_t)__popc(emask) < r.number) reason = RS_GPU_FIT;
-    const bool ok = valid && reason == 0;
-    if (valid && sub == 0) {
-      feas[i] = ok;
-      elig[i] = (uint8_t)emask;
-      if (reason && reason != RS_DEAD) atomicAdd(&s_reason[reason], 1);
-      else if (reason == RS_DEAD) atomicAdd(&s_reason[RS_DEAD], 1);
-    }
-    if (sub == 0 && ok) ++nfeas;
-    if (yoda) {
-      const bool take = ok && ((emask >> sub) & 1u);
-      unsigned long long v[6];
-      v[0] = take ? cd.bandwidth : 0; v[1] = take ? cd.clock : 0; v[2] = take ? cd.core : 0;
-      v[3] = take ? ef : 0; v[4] = take ? cd.power : 0; v[5] = take ? cd.total : 0;
+  } else {
+    const int stride = workers * kWaves * kNodesPerWave;
+    for (int base = uniform((blockIdx.x * kWaves + wave) * kNodesPerWave); base < n; base += stride) {
+      const int i = base + grp;
+      bool valid = i < n;
+      // patched nodes are evaluated by the patch block, not from the (stale) table
 #pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const unsigned long long m = wmax_across_groups(gmax(v[k]));
-        wmx[k] = m > wmx[k] ? m : wmx[k];
-      }
+      for (int j = 0; j < kPatchRows; ++j) valid = valid && !(j < pa.n && pa.idx[j] == i);
+      filter_group(nodes + (i < n ? i : n - 1), i, valid, r, cand, feas, elig, s_reason, wmx, nfeas, grp, sub);
     }
   }
   nfeas = gsum(nfeas);
@@ -268,6 +299,81 @@ __global__ __launch_bounds__(kBlock) void k_filter(const yoda_dev_node_t* __rest
   if (threadIdx.x == 0 && s_feas) atomicAdd(&g->feasible[sh], s_feas);
 }
 
+// ------------------------------------------------------------------ normalise + argmax helpers
+// Block-wide best key over nodes blk*kBlock+tid, stride nblk*kBlock (returned by thread 0).
+// scheduler.go:132-157: highest seeded 0, lowest = min; equal → lowest − 1.
+__device__ unsigned long long select_block(int n, const yoda_dev_req_t& r, const uint8_t* __restrict__ feas,
+                                           const int64_t* __restrict__ raw, const int64_t* __restrict__ total,
+                                           Globals* __restrict__ g, int blk, int nblk) {
+  __shared__ unsigned long long s_key[kWaves];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool yoda_s = (r.filters & F_YODA) && r.w_yoda != 0;
+  const int64_t hi = (int64_t)g->raw_hi;
+  int64_t lo = (int64_t)g->raw_lo;
+  if (hi == lo) --lo;
+  const uint64_t den = (uint64_t)hi - (uint64_t)lo;
+  unsigned long long best = 0;
+#pragma unroll 4
+  for (int i = blk * kBlock + threadIdx.x; i < n; i += nblk * kBlock) {
+    const uint8_t fe = feas[i];          // loads issued together; the branch comes after
+    int64_t f = total[i];
+    const int64_t rw = raw[i];
+    if (!fe) continue;
+    if (yoda_s) f += (int64_t)udiv(((uint64_t)rw - (uint64_t)lo) * 100ull, den) * r.w_yoda;
+    const uint32_t p = ((uint32_t)i * r.perm_mul + r.perm_add) & 0xFFFFFFu;
+    const unsigned long long key = ((unsigned long long)f << 24) | p;
+    best = key > best ? key : best;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_xor(best, off, 64);
+    best = o > best ? o : best;
+  }
+  if (lane == 0) s_key[wave] = best;
+  __syncthreads();
+  unsigned long long b = 0;
+  for (int w = 0; w < kWaves; ++w) b = s_key[w] > b ? s_key[w] : b;
+  return b;
+}
+
+// Decode the winning key into the mapped result (single thread, after an acquire fence or
+// a kernel boundary, so plain loads see every block's accumulators). The record goes out
+// with `feasible` = -1 first, then `feasible` alone with a system-scope release, so the
+// spinning host never sees a half-written result. Then re-arm the accumulators for the
+// next pod (the kernel boundary publishes them on the device).
+__device__ void publish(int n, const yoda_dev_req_t& r, unsigned long long key, const uint32_t* __restrict__ mask,
+                        const int32_t* __restrict__ quality, Globals* __restrict__ g,
+                        yoda_dev_result_t* __restrict__ out) {
+  int nf = 0;
+  for (int s = 0; s < kShards; ++s) nf += g->feasible[s];
+  yoda_dev_result_t res;
+  res.feasible = -1;
+  if (nf == 0) {
+    res.node = -1;
+    res.score = 0;
+    res.mask = 0;
+    res.quality = 0;
+  } else {
+    const uint32_t p = (uint32_t)(key & 0xFFFFFFull);
+    const int32_t node = (int32_t)(((p - r.perm_add) * r.perm_inv) & 0xFFFFFFu);
+    res.node = node;
+    res.score = nf == 1 ? 0 : (int64_t)(key >> 24);
+    res.mask = mask[node];
+    res.quality = quality[node];
+  }
+  for (int k = 0; k < YODA_DEV_REASONS; ++k) {
+    int s = 0;
+    for (int h = 0; h < kShards; ++h) s += g->reasons[h][k];
+    res.reasons[k] = s;
+  }
+  for (int k = 0; k < 6; ++k) res.maxima[k] = g->maxima[k];
+  res.raw_lo = (int64_t)g->raw_lo;
+  res.raw_hi = (int64_t)g->raw_hi;
+  *out = res;
+  __hip_atomic_store(&out->feasible, nf, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  globals_reset(g);
+}
+
 // (obj, mask) a better than b: smaller objective, then lexicographically smaller subset
 __device__ __forceinline__ bool better(int64_t oa, uint32_t ma, int64_t ob, uint32_t mb) {
   if (oa != ob) return oa < ob;
@@ -280,8 +386,10 @@ __global__ __launch_bounds__(kBlock) void k_score(const yoda_dev_node_t* __restr
                                                   const yoda_dev_req_t r, const uint8_t* __restrict__ feas,
                                                   const uint8_t* __restrict__ elig, int64_t* __restrict__ raw,
                                                   int64_t* __restrict__ total_out, uint32_t* __restrict__ mask_out,
-                                                  int32_t* __restrict__ quality_out, Globals* __restrict__ g) {
+                                                  int32_t* __restrict__ quality_out, Globals* __restrict__ g,
+                                                  yoda_dev_result_t* __restrict__ out, int fuse_select) {
   __shared__ unsigned long long s_lo[kWaves], s_hi[kWaves];
+  __shared__ bool s_last;
   const int lane = threadIdx.x & 63, wave = uniform(threadIdx.x >> 6);
   const int grp = lane >> 3, sub = lane & 7;
   const bool yoda_f = (r.filters & F_YODA) != 0;
@@ -456,6 +564,18 @@ __global__ __launch_bounds__(kBlock) void k_score(const yoda_dev_node_t* __restr
     if (blo != ULLONG_MAX) min_if(&g->raw_lo, blo);
     if (bhi) max_if(&g->raw_hi, bhi);
   }
+  if (!fuse_select) return;
+  // last block in: every block's raw/total/mask/quality stores and lo/hi atomics are visible
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned t = __hip_atomic_fetch_add(&g->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const unsigned long long best = select_block(n, r, feas, raw, total_out, g, 0, 1);
+  if (threadIdx.x == 0) publish(n, r, best, mask_out, quality_out, g, out);
 }
 
 // ------------------------------------------------------------------ K3: normalize + argmax + result
@@ -463,34 +583,9 @@ __global__ __launch_bounds__(kBlock) void k_select(int n, const yoda_dev_req_t r
                                                    const int64_t* __restrict__ raw, const int64_t* __restrict__ total,
                                                    const uint32_t* __restrict__ mask, const int32_t* __restrict__ quality,
                                                    Globals* __restrict__ g, yoda_dev_result_t* __restrict__ out) {
-  __shared__ unsigned long long s_key[kWaves];
   __shared__ bool s_last;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool yoda_s = (r.filters & F_YODA) && r.w_yoda != 0;
-  // scheduler.go:132-157: highest seeded 0, lowest = min; equal → lowest − 1
-  const int64_t hi = (int64_t)g->raw_hi;
-  int64_t lo = (int64_t)g->raw_lo;
-  if (hi == lo) --lo;
-  const uint64_t den = (uint64_t)hi - (uint64_t)lo;
-  unsigned long long best = 0;
-  for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-    if (!feas[i]) continue;
-    int64_t f = total[i];
-    if (yoda_s) f += (int64_t)udiv(((uint64_t)raw[i] - (uint64_t)lo) * 100ull, den) * r.w_yoda;
-    const uint32_t p = ((uint32_t)i * r.perm_mul + r.perm_add) & 0xFFFFFFu;
-    const unsigned long long key = ((unsigned long long)f << 24) | p;
-    best = key > best ? key : best;
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const unsigned long long o = __shfl_xor(best, off, 64);
-    best = o > best ? o : best;
-  }
-  if (lane == 0) s_key[wave] = best;
-  __syncthreads();
+  const unsigned long long b = select_block(n, r, feas, raw, total, g, blockIdx.x, gridDim.x);
   if (threadIdx.x == 0) {
-    unsigned long long b = 0;
-    for (int w = 0; w < kWaves; ++w) b = s_key[w] > b ? s_key[w] : b;
     if (b) max_if(&g->best_key, b);
     // release this block's contribution, then take a ticket (agent scope: other XCDs)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -502,33 +597,7 @@ __global__ __launch_bounds__(kBlock) void k_select(int n, const yoda_dev_req_t r
   // last block: every other block's atomicMax has landed
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const unsigned long long key = __hip_atomic_load(&g->best_key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  int nf = 0;
-  for (int s = 0; s < kShards; ++s) nf += g->feasible[s];
-  yoda_dev_result_t res;
-  res.feasible = nf;
-  if (nf == 0) {
-    res.node = -1;
-    res.score = 0;
-    res.mask = 0;
-    res.quality = 0;
-  } else {
-    const uint32_t p = (uint32_t)(key & 0xFFFFFFull);
-    const int32_t node = (int32_t)(((p - r.perm_add) * r.perm_inv) & 0xFFFFFFu);
-    res.node = node;
-    res.score = nf == 1 ? 0 : (int64_t)(key >> 24);
-    res.mask = mask[node];
-    res.quality = quality[node];
-  }
-  for (int k = 0; k < YODA_DEV_REASONS; ++k) {
-    int s = 0;
-    for (int h = 0; h < kShards; ++h) s += g->reasons[h][k];
-    res.reasons[k] = s;
-  }
-  for (int k = 0; k < 6; ++k) res.maxima[k] = g->maxima[k];
-  res.raw_lo = (int64_t)g->raw_lo;
-  res.raw_hi = (int64_t)g->raw_hi;
-  *out = res;                 // mapped pinned host memory
-  globals_reset(g);           // re-arm for the next pod; the kernel boundary publishes it
+  publish(n, r, key, mask, quality, g, out);
 }
 
 struct Ctx {
@@ -545,7 +614,8 @@ struct Ctx {
   Globals* d_g = nullptr;
   float last_us = 0;
   int grid = 1024;
-  bool timing = true;
+  bool timing = false;        // event timing of each cycle (benchmarks); off in the scheduler
+  PatchArgs pend{};           // dirty rows waiting to ride in the next filter launch
 };
 
 #define CK(x)                               \
@@ -553,6 +623,33 @@ struct Ctx {
     hipError_t e__ = (x);                   \
     if (e__ != hipSuccess) return (int)e__; \
   } while (0)
+
+// launch the pending rows on their own (before a bulk scatter or a debug read)
+int flush_pending(Ctx* c) {
+  if (c->pend.n == 0) return 0;
+  hipLaunchKernelGGL(k_patch, dim3(1), dim3(32 * kPatchRows), 0, c->stream, c->pend, c->d_nodes);
+  c->pend.n = 0;
+  CK(hipGetLastError());
+  return 0;
+}
+
+// Wait for the device to publish the result: spin on the mapped `feasible` field (written
+// last, system-scope release), polling the stream now and then so a failed launch or a
+// result that never comes cannot hang the scheduler.
+int wait_result(Ctx* c) {
+  volatile int32_t* flag = &c->h_res->feasible;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 1;; ++spin) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) >= 0) return 0;
+    if ((spin & 4095) == 0) {
+      const hipError_t q = hipStreamQuery(c->stream);
+      if (q == hipSuccess) return __atomic_load_n(flag, __ATOMIC_ACQUIRE) >= 0 ? 0 : -4;
+      if (q != hipErrorNotReady) return (int)q;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) return -5;
+    }
+    __builtin_ia32_pause();
+  }
+}
 
 }  // namespace
 
@@ -627,17 +724,26 @@ int yoda_dev_upload(void* p, int n, const int32_t* idx, const yoda_dev_node_t* r
     if (idx[i] < 0 || idx[i] >= c->cap) return -2;   // never scatter outside the node table
   CK(hipSetDevice(c->device));
   if (n <= kPatchRows) {
-    // steady state (a reservation dirtied one node): rows travel in the kernel arguments
-    PatchArgs a;
-    a.n = n;
+    // steady state (a reservation dirtied one node): the rows wait host-side and travel in
+    // the next filter launch's arguments; a newer row for the same node replaces the old
+    PatchArgs& a = c->pend;
+    int fresh = 0;
     for (int i = 0; i < n; ++i) {
-      a.idx[i] = idx[i];
-      a.rows[i] = rows[i];
+      bool seen = false;
+      for (int j = 0; j < a.n; ++j) seen |= a.idx[j] == idx[i];
+      fresh += !seen;
     }
-    hipLaunchKernelGGL(k_patch, dim3(1), dim3(32 * kPatchRows), 0, c->stream, a, c->d_nodes);
-    CK(hipGetLastError());
-    return 0;      // stream-ordered before the next schedule; nothing host-side to protect
+    if (a.n + fresh > kPatchRows && flush_pending(c) != 0) return -6;
+    for (int i = 0; i < n; ++i) {
+      int j = 0;
+      while (j < a.n && a.idx[j] != idx[i]) ++j;
+      if (j == a.n) ++a.n;
+      a.idx[j] = idx[i];
+      a.rows[j] = rows[i];
+    }
+    return 0;
   }
+  if (flush_pending(c) != 0) return -6;   // older rows first: the bulk upload may overwrite them
   memcpy(c->h_stage, rows, (size_t)n * sizeof(yoda_dev_node_t));
   memcpy(c->h_idx, idx, (size_t)n * sizeof(int32_t));
   CK(hipMemcpyAsync(c->d_stage, c->h_stage, (size_t)n * sizeof(yoda_dev_node_t), hipMemcpyHostToDevice, c->stream));
@@ -665,31 +771,39 @@ int yoda_dev_schedule(void* p, int n, const yoda_dev_req_t* req, const uint8_t* 
   grid = grid < c->grid ? grid : c->grid;
   int grid_sel = (n + kBlock - 1) / kBlock;
   grid_sel = grid_sel < c->grid ? grid_sel : c->grid;
-  c->h_res->feasible = -1;   // sentinel: overwritten by the device
+  const int fuse = n <= kFuseSelectMax;
+  __atomic_store_n(&c->h_res->feasible, -1, __ATOMIC_RELEASE);   // sentinel: overwritten by the device
   if (c->timing) CK(hipEventRecord(c->e0, c->stream));
-  hipLaunchKernelGGL(k_filter, dim3(grid), dim3(kBlock), 0, c->stream, c->d_nodes, n, r, c->d_cand, c->d_feas,
-                     c->d_elig, c->d_g);
+  hipLaunchKernelGGL(k_filter, dim3(grid + (c->pend.n > 0 ? 1 : 0)), dim3(kBlock), 0, c->stream, c->pend, c->d_nodes,
+                     n, r, c->d_cand, c->d_feas, c->d_elig, c->d_g);
+  c->pend.n = 0;
   hipLaunchKernelGGL(k_score, dim3(grid), dim3(kBlock), 0, c->stream, c->d_nodes, n, r, c->d_feas, c->d_elig,
-                     c->d_raw, c->d_total, c->d_mask, c->d_quality, c->d_g);
-  hipLaunchKernelGGL(k_select, dim3(grid_sel), dim3(kBlock), 0, c->stream, n, r, c->d_feas, c->d_raw, c->d_total,
-                     c->d_mask, c->d_quality, c->d_g, c->d_res_map);
+                     c->d_raw, c->d_total, c->d_mask, c->d_quality, c->d_g, c->d_res_map, fuse);
+  if (!fuse)
+    hipLaunchKernelGGL(k_select, dim3(grid_sel), dim3(kBlock), 0, c->stream, n, r, c->d_feas, c->d_raw, c->d_total,
+                       c->d_mask, c->d_quality, c->d_g, c->d_res_map);
   CK(hipGetLastError());
-  if (c->timing) CK(hipEventRecord(c->e1, c->stream));
-  CK(hipStreamSynchronize(c->stream));
   if (c->timing) {
+    CK(hipEventRecord(c->e1, c->stream));
+    CK(hipEventSynchronize(c->e1));
     float ms = 0;
     if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) c->last_us = ms * 1000.0f;
   }
-  std::atomic_thread_fence(std::memory_order_acquire);
+  const int w = wait_result(c);
+  if (w != 0) return w;
   memcpy(out, c->h_res, sizeof(*out));
-  if (out->feasible < 0) return -4;    // the result never arrived
   return 0;
+}
+
+void yoda_dev_set_timing(void* p, int on) {
+  if (p) ((Ctx*)p)->timing = on != 0;
 }
 
 int yoda_dev_debug(void* p, int n, uint8_t* feas, int64_t* raw, int64_t* total, uint32_t* mask, int32_t* quality) {
   Ctx* c = (Ctx*)p;
   if (n <= 0 || n > c->cap) return -1;
   CK(hipSetDevice(c->device));
+  if (flush_pending(c) != 0) return -6;
   CK(hipStreamSynchronize(c->stream));
   if (feas) CK(hipMemcpy(feas, c->d_feas, (size_t)n, hipMemcpyDeviceToHost));
   if (raw) CK(hipMemcpy(raw, c->d_raw, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost));

@@ -81,6 +81,8 @@ int yoda_dev_debug(void* ctx, int n_nodes, uint8_t* feas, int64_t* raw, int64_t*
                    int32_t* quality);
 // last kernel time of yoda_dev_schedule in microseconds (device events)
 float yoda_dev_last_us(void* ctx);
+// per-cycle event timing (yoda_dev_last_us); off by default — it adds a stream sync
+void yoda_dev_set_timing(void* ctx, int on);
 
 #ifdef __cplusplus
 }

@@ -39,9 +39,16 @@ def bench(nodes: int, kind: str, path: str, pods: int, threads: int) -> dict:
         dt = time.perf_counter() - t0
         if k >= 5:
             ts.append(dt * 1e6)
-            if path == "gpu":
-                dev_us.append(eng.device_last_us())
         assert res[0] >= 0, res
+    if path == "gpu":
+        # kernel time (events around the launches) in a separate pass: timing adds a sync
+        eng.device_set_timing(True)
+        for k in range(max(10, pods // 4)):
+            pi = PodInfo.from_obj({"metadata": {"name": f"t{k}", "uid": f"t-{nodes}-{kind}-{k}", "labels": labels},
+                                   "spec": {}})
+            eng.schedule(pi.num_id, pod_req(eng, pi), True)
+            dev_us.append(eng.device_last_us())
+        eng.device_set_timing(False)
     out = {"nodes": nodes, "gpus": nodes * 8, "pod": kind, "path": path, "threads": threads,
            "cycle_us_p50": round(statistics.median(ts), 1), "cycle_us_p90": round(sorted(ts)[int(len(ts) * .9)], 1),
            "pods_per_s": round(1e6 / statistics.mean(ts), 1)}
