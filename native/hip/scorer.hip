@@ -30,6 +30,7 @@
 #include <climits>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "yoda_dev_abi.h"
@@ -110,11 +111,15 @@ __device__ __forceinline__ unsigned long long peek(unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // atomics only when this block can still change the accumulator
-__device__ __forceinline__ void max_if(unsigned long long* p, unsigned long long v) {
-  if (v > peek(p)) atomicMax(p, v);
+// (`direct`: skip the check — one dependent memory round trip less per block, at the cost
+// of every block's atomic reaching the accumulator. Measured on MI355X: direct wins by
+// ≈1.5 µs up to ~256 blocks and loses by ≈2 µs from ~500 blocks on, so the host picks it
+// per launch from the grid size; YODA_DEV_DIRECT_ATOMICS=0/1 forces either.)
+__device__ __forceinline__ void max_if(unsigned long long* p, unsigned long long v, bool direct = false) {
+  if (direct || v > peek(p)) atomicMax(p, v);
 }
-__device__ __forceinline__ void min_if(unsigned long long* p, unsigned long long v) {
-  if (v < peek(p)) atomicMin(p, v);
+__device__ __forceinline__ void min_if(unsigned long long* p, unsigned long long v, bool direct = false) {
+  if (direct || v < peek(p)) atomicMin(p, v);
 }
 
 // Exact floor(n / d) for d > 0: a correctly rounded double quotient is within 1 of the
@@ -292,7 +297,7 @@ __global__ __launch_bounds__(kBlock) void k_filter(const PatchArgs pa, yoda_dev_
   if (threadIdx.x < 6) {
     unsigned long long m = 1;
     for (int w = 0; w < kWaves; ++w) m = s_max[w][threadIdx.x] > m ? s_max[w][threadIdx.x] : m;
-    if (m > 1) max_if(&g->maxima[threadIdx.x], m);
+    if (m > 1) max_if(&g->maxima[threadIdx.x], m, r.dev_flags & 1u);
   }
   const int sh = blockIdx.x % kShards;
   if (threadIdx.x < YODA_DEV_REASONS && s_reason[threadIdx.x]) atomicAdd(&g->reasons[sh][threadIdx.x], s_reason[threadIdx.x]);
@@ -390,6 +395,10 @@ __global__ __launch_bounds__(kBlock) void k_score(const yoda_dev_node_t* __restr
                                                   yoda_dev_result_t* __restrict__ out, int fuse_select) {
   __shared__ unsigned long long s_lo[kWaves], s_hi[kWaves];
   __shared__ bool s_last;
+  __shared__ uint8_t s_masks[256];   // subset table in LDS: the search loop reads it every step
+  static_assert(kBlock == 256, "one table byte per thread");
+  s_masks[threadIdx.x] = c_subsets.masks[threadIdx.x];
+  __syncthreads();
   const int lane = threadIdx.x & 63, wave = uniform(threadIdx.x >> 6);
   const int grp = lane >> 3, sub = lane & 7;
   const bool yoda_f = (r.filters & F_YODA) != 0;
@@ -406,8 +415,9 @@ __global__ __launch_bounds__(kBlock) void k_score(const yoda_dev_node_t* __restr
   const int stride = gridDim.x * kWaves * kNodesPerWave;
   for (int base = uniform((blockIdx.x * kWaves + wave) * kNodesPerWave); base < n; base += stride) {
     const int i = base + grp;
+    // no early exit on an all-infeasible wave: the node loads below then issue together
+    // with feas/elig instead of one round trip later
     const bool act = i < n && feas[i];
-    if (!__any(act)) continue;
     const yoda_dev_node_t* nd = nodes + (i < n ? i : n - 1);
     const uint32_t emask = act ? elig[i] : 0u;
     const uint8_t ncards = nd->ncards;
@@ -438,7 +448,7 @@ __global__ __launch_bounds__(kBlock) void k_score(const yoda_dev_node_t* __restr
     bool found = false;
     if (search && act) {
       for (int t = s_begin + sub; t < s_end; t += kGroup) {
-        const uint32_t m = c_subsets.masks[t];
+        const uint32_t m = s_masks[t];
         if (m & ~emask) continue;
         int32_t qsum = 0;
         uint64_t nmask = 0;
@@ -561,8 +571,8 @@ __global__ __launch_bounds__(kBlock) void k_score(const yoda_dev_node_t* __restr
       blo = s_lo[w] < blo ? s_lo[w] : blo;
       bhi = s_hi[w] > bhi ? s_hi[w] : bhi;
     }
-    if (blo != ULLONG_MAX) min_if(&g->raw_lo, blo);
-    if (bhi) max_if(&g->raw_hi, bhi);
+    if (blo != ULLONG_MAX) min_if(&g->raw_lo, blo, r.dev_flags & 1u);
+    if (bhi) max_if(&g->raw_hi, bhi, r.dev_flags & 1u);
   }
   if (!fuse_select) return;
   // last block in: every block's raw/total/mask/quality stores and lo/hi atomics are visible
@@ -586,7 +596,7 @@ __global__ __launch_bounds__(kBlock) void k_select(int n, const yoda_dev_req_t r
   __shared__ bool s_last;
   const unsigned long long b = select_block(n, r, feas, raw, total, g, blockIdx.x, gridDim.x);
   if (threadIdx.x == 0) {
-    if (b) max_if(&g->best_key, b);
+    if (b) max_if(&g->best_key, b, r.dev_flags & 1u);
     // release this block's contribution, then take a ticket (agent scope: other XCDs)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const unsigned t = __hip_atomic_fetch_add(&g->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -615,6 +625,7 @@ struct Ctx {
   float last_us = 0;
   int grid = 1024;
   bool timing = false;        // event timing of each cycle (benchmarks); off in the scheduler
+  int direct_atomics = -1;    // -1: by grid size; 0/1 forced (YODA_DEV_DIRECT_ATOMICS)
   PatchArgs pend{};           // dirty rows waiting to ride in the next filter launch
 };
 
@@ -668,6 +679,7 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
   if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
   int cus = 256;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess) c->grid = cus * 4;
+  if (const char* v = getenv("YODA_DEV_DIRECT_ATOMICS")) c->direct_atomics = v[0] == '1' ? 1 : 0;
   const SubsetTable st = make_subsets();
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_subsets), &st, sizeof st)) != hipSuccess) return fail("subsets", e);
   if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
@@ -761,7 +773,7 @@ int yoda_dev_schedule(void* p, int n, const yoda_dev_req_t* req, const uint8_t* 
   if (n <= 0 || n > c->cap) return -1;
   if (req->use_candidates && !cand) return -3;
   CK(hipSetDevice(c->device));
-  const yoda_dev_req_t r = *req;
+  yoda_dev_req_t r = *req;
   if (r.use_candidates) {
     memcpy(c->h_cand, cand, (size_t)n);
     CK(hipMemcpyAsync(c->d_cand, c->h_cand, (size_t)n, hipMemcpyHostToDevice, c->stream));
@@ -771,6 +783,7 @@ int yoda_dev_schedule(void* p, int n, const yoda_dev_req_t* req, const uint8_t* 
   grid = grid < c->grid ? grid : c->grid;
   int grid_sel = (n + kBlock - 1) / kBlock;
   grid_sel = grid_sel < c->grid ? grid_sel : c->grid;
+  r.dev_flags = (c->direct_atomics < 0 ? grid <= 256 : c->direct_atomics == 1) ? 1u : 0u;
   const int fuse = n <= kFuseSelectMax;
   __atomic_store_n(&c->h_res->feasible, -1, __ATOMIC_RELEASE);   // sentinel: overwritten by the device
   if (c->timing) CK(hipEventRecord(c->e0, c->stream));

@@ -53,7 +53,7 @@ typedef struct {
   uint32_t tolerates_unschedulable;
   uint32_t use_candidates;   // 1: per-node first-failing NodeName/Affinity/Taint reason uploaded
   uint32_t perm_mul, perm_add, perm_inv;   // random tie-break: p(i) = (i*mul + add) mod 2^24
-  uint32_t pad;
+  uint32_t dev_flags;     // set by the device context, not the engine
 } yoda_dev_req_t;
 
 typedef struct {
