@@ -109,6 +109,7 @@ def main(argv=None) -> int:
     bound = sum(r.bound for r in results)
     unsched = sum(r.unschedulable for r in results)
     lats = [x for r in results for x in r.latencies_s]
+    e2e = [x for r in results for x in r.e2e_s]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -119,6 +120,9 @@ def main(argv=None) -> int:
         gathered: list = [None] * world
         dist.all_gather_object(gathered, lats)
         lats = [x for g in gathered for x in g]
+        gathered_e2e: list = [None] * world
+        dist.all_gather_object(gathered_e2e, e2e)
+        e2e = [x for g in gathered_e2e for x in g]
         tels: list = [None] * world
         dist.all_gather_object(tels, tel)
     else:
@@ -147,6 +151,8 @@ def main(argv=None) -> int:
             "p50_latency_ms": round(percentile(lats, 50) * 1000.0, 3),
             "p99_latency_ms": round(percentile(lats, 99) * 1000.0, 3),
             "max_latency_ms": round(max(lats) * 1000.0, 3) if lats else None,
+            "e2e_scheduling_p50_ms": round(percentile(e2e, 50) * 1000.0, 3) if e2e else None,
+            "e2e_scheduling_p99_ms": round(percentile(e2e, 99) * 1000.0, 3) if e2e else None,
             "pods_bound": bound,
             "pods_unschedulable": unsched,
             "client_qps": a.qps, "client_burst": a.burst, "native_batch": a.batch, "compat": a.compat,

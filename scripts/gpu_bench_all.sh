@@ -6,7 +6,8 @@ mkdir -p gpurun_out
 out=gpurun_out/bench_all.jsonl
 : > $out
 for args in "--config 1 --steps 20" "--config 2" "--config 3" "--config 4" "--config 5 --steps 5 --warmup 1" \
-            "--config 3 --batch 1" "--config 3 --compat" "--config 3 --reference-qps --steps 1 --warmup 0"; do
+            "--config 6 --steps 3 --warmup 1" "--config 3 --batch 1" "--config 3 --compat" \
+            "--config 3 --reference-qps --steps 1 --warmup 0"; do
   echo "=== bench $args ($(date +%T))"
   timeout -k 10 300 python bench.py $args > gpurun_out/bench_one.log 2>&1
   rc=$?

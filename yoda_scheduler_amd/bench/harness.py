@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import asyncio
 import time
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Optional
 
 from ..fakeapi.client import InProcessClient
@@ -46,6 +46,7 @@ class BurstResult:
     unschedulable: int
     elapsed_s: float
     latencies_s: list[float]
+    e2e_s: list[float] = field(default_factory=list)   # scheduler-internal: cycle start → bind ack
 
     @property
     def pods_per_s(self) -> float:
@@ -71,6 +72,7 @@ class Shard:
         cfg = parse_config(bench_config(w.scheduler_name, qps, burst, batch, compat, device))
         self.sched = Scheduler(self.client, cfg, metrics=SchedulerMetrics() if metrics else NullMetrics(),
                                record_events=events, seed=seed, engine_threads=engine_threads)
+        self.sched.e2e_samples = []
         self._loop_task: Optional[asyncio.Task] = None
 
     async def start(self) -> None:
@@ -80,6 +82,7 @@ class Shard:
     async def burst(self, tag: str = "b", timeout: float = 600.0) -> BurstResult:
         srv, w = self.server, self.w
         srv.reset_logs()
+        self.sched.e2e_samples.clear()
         objs = [pod_object(i, lab, w.scheduler_name, prefix=tag) for i, lab in enumerate(w.pods)]
         t0 = time.perf_counter()
         for i, o in enumerate(objs):
@@ -100,7 +103,8 @@ class Shard:
             await asyncio.sleep(0.0005)
         t_end = max(srv.bind_log.values()) if srv.bind_log else time.perf_counter()
         lat = srv.latencies()
-        return BurstResult(n, len(srv.bind_log), n - len(srv.bind_log), t_end - t0, lat)
+        return BurstResult(n, len(srv.bind_log), n - len(srv.bind_log), t_end - t0, lat,
+                           list(self.sched.e2e_samples))
 
     async def stop(self) -> None:
         await self.sched.shutdown()

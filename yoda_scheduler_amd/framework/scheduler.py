@@ -126,6 +126,9 @@ class Scheduler:
         self.pending_binds = 0
         self.batching = config.batch_size > 1
         self.tracer = Tracer() if config.trace else None
+        # optional raw samples of scheduler-internal e2e (cycle start → bind acknowledged,
+        # queue wait excluded; BASELINE.md protocol item 4) without the Prometheus cost
+        self.e2e_samples: Optional[list] = None
 
     def _maybe_enable_device(self) -> None:
         """Attach the gfx950 device scorer once the cluster is big enough for it to pay
@@ -472,6 +475,8 @@ class Scheduler:
                     self.cache.finish_binding(pi)
                     fw.run_post_bind(state, pi, node)
                     self.scheduled += 1
+                    if self.e2e_samples is not None:
+                        self.e2e_samples.append(time.perf_counter() - t0)
                     m.child(m.e2e, "scheduled", fw.name).observe(time.perf_counter() - t0)
                     self.recorder.pod_event(pi, "Normal", "Scheduled",
                                             f"Successfully assigned {pi.key} to {node}")
