@@ -97,7 +97,8 @@ def pod_object(i: int, labels: dict, scheduler_name: str, namespace: str = "defa
 def populate(server, w: Workload, template: Optional[dict] = None, link_load: float = 0.0,
              seed: int = 0) -> None:
     """Create the workload's nodes and their Scv telemetry in a fake apiserver.
-    ``template`` (from a real amd-smi sample) overrides the per-card static fields."""
+    ``template`` (from a real amd-smi sample of the local MI355X) overrides the per-card
+    static fields of the MI355X nodes."""
     rng = random.Random(seed)
     for name, spec, gpus in w.nodes:
         # kubelet --max-pods 2048: config 5 packs 5000 HBM-sharing pods onto 4 nodes
@@ -105,7 +106,7 @@ def populate(server, w: Workload, template: Optional[dict] = None, link_load: fl
         scv = make_scv(name, spec, gpus, update_time=time.time(), link_load=link_load, rng=rng,
                        jitter=link_load > 0)
         scv.update_interval_ms = 60_000     # one sample stays fresh for the whole burst
-        if template:
+        if template and spec is MI355X:     # the template is a real MI355X; MI350X nodes keep their spec
             for c in scv.status.card_list:
                 for k, v in template.items():
                     setattr(c, k, v)
