@@ -3,10 +3,12 @@
 //   * HBM pattern write/verify          → Card.Health (uncorrectable data errors)
 //   * xGMI peer-write bandwidth          → per-link quality for gang placement
 //
-// Wave64 / CDNA4 notes: 16 B per lane per access (float4), 4 independent loads in flight
-// per lane, grid = 8 blocks per CU × 256 CUs with grid-stride loops (cdna guide G11/G13);
-// the pattern check reduces mismatches per wave with a 64-bit ballot and issues ONE
-// atomic per wave (G12).
+// Wave64 / CDNA4 notes: 16 B per lane per access, grid-stride loops, nontemporal (streaming)
+// loads/stores; shape picked by the sweep in scripts/hipbench/hbm_variants.hip
+// (profiles/hbm_probe_sweep.jsonl, MI355X): 8 loads in flight per lane and 64 blocks per CU
+// read at 6.1 TB/s (1 GiB) – 6.7 TB/s (4 GiB) of the 8 TB/s peak, vs 5.1–5.5 TB/s for the
+// first version (4 plain loads, 8 blocks/CU); copies 4 in flight at 5.2–5.5 TB/s. The
+// pattern check reduces mismatches per wave and issues ONE atomic per wave (G12).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -31,32 +33,34 @@ __device__ __forceinline__ uint32_t mix32(uint64_t i, uint32_t seed) {
   return (uint32_t)(z ^ (z >> 31));
 }
 
-__global__ __launch_bounds__(kBlock) void k_read(const float4* __restrict__ src, size_t n4, float* __restrict__ sink) {
+typedef float f4 __attribute__((ext_vector_type(4)));
+constexpr int kReadInFlight = 8, kCopyInFlight = 4, kBlocksPerCu = 64;
+
+__global__ __launch_bounds__(kBlock) void k_read(const f4* __restrict__ src, size_t n4, float* __restrict__ sink) {
   const size_t stride = (size_t)gridDim.x * kBlock;
   size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  // 4 independent 16-B loads in flight per lane
-  for (; i + 3 * stride < n4; i += 4 * stride) {
-    float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-    acc.x += a.x + b.x + c.x + d.x;
-    acc.y += a.y + b.y + c.y + d.y;
-    acc.z += a.z + b.z + c.z + d.z;
-    acc.w += a.w + b.w + c.w + d.w;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (; i + (kReadInFlight - 1) * stride < n4; i += kReadInFlight * stride) {
+    f4 v[kReadInFlight];
+#pragma unroll
+    for (int u = 0; u < kReadInFlight; ++u) v[u] = __builtin_nontemporal_load(&src[i + u * stride]);
+#pragma unroll
+    for (int u = 0; u < kReadInFlight; ++u) acc += v[u];
   }
-  for (; i < n4; i += stride) {
-    float4 a = src[i];
-    acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
-  }
-  float s = acc.x + acc.y + acc.z + acc.w;
+  for (; i < n4; i += stride) acc += src[i];
+  const float s = acc.x + acc.y + acc.z + acc.w;
   if (s == 1234.5f) sink[blockIdx.x] = s;   // practically never: keeps the loads alive
 }
 
-__global__ __launch_bounds__(kBlock) void k_copy(const float4* __restrict__ src, float4* __restrict__ dst, size_t n4) {
+__global__ __launch_bounds__(kBlock) void k_copy(const f4* __restrict__ src, f4* __restrict__ dst, size_t n4) {
   const size_t stride = (size_t)gridDim.x * kBlock;
   size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
-  for (; i + 3 * stride < n4; i += 4 * stride) {
-    float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-    dst[i] = a; dst[i + stride] = b; dst[i + 2 * stride] = c; dst[i + 3 * stride] = d;
+  for (; i + (kCopyInFlight - 1) * stride < n4; i += kCopyInFlight * stride) {
+    f4 v[kCopyInFlight];
+#pragma unroll
+    for (int u = 0; u < kCopyInFlight; ++u) v[u] = __builtin_nontemporal_load(&src[i + u * stride]);
+#pragma unroll
+    for (int u = 0; u < kCopyInFlight; ++u) __builtin_nontemporal_store(v[u], &dst[i + u * stride]);
   }
   for (; i < n4; i += stride) dst[i] = src[i];
 }
@@ -84,10 +88,10 @@ __global__ __launch_bounds__(kBlock) void k_verify(const uint4* __restrict__ buf
   if ((threadIdx.x & 63) == 0 && bad) atomicAdd(errors, (unsigned long long)bad);
 }
 
-int grid_for(int device) {
+int grid_for(int device, int per_cu = 8) {
   int cus = 256;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-  return cus * 8;
+  return cus * per_cu;
 }
 
 }  // namespace
@@ -116,12 +120,12 @@ int yoda_hip_device_info(int device, char* arch, int arch_len, int* cus, unsigne
 int yoda_hbm_bandwidth(int device, unsigned long long bytes, int iters, double* read_gbps, double* copy_gbps) {
   YODA_CHECK(hipSetDevice(device));
   const size_t n4 = (size_t)(bytes / 16);
-  float4 *a = nullptr, *b = nullptr;
+  f4 *a = nullptr, *b = nullptr;
   float* sink = nullptr;
   hipEvent_t e0, e1;
   YODA_CHECK(hipMalloc(&a, n4 * 16));
   YODA_CHECK(hipMalloc(&b, n4 * 16));
-  const int grid = grid_for(device);
+  const int grid = grid_for(device, kBlocksPerCu);
   YODA_CHECK(hipMalloc(&sink, grid * sizeof(float)));
   YODA_CHECK(hipMemset(a, 0, n4 * 16));
   YODA_CHECK(hipMemset(b, 0, n4 * 16));
@@ -197,13 +201,13 @@ int yoda_peer_write_bandwidth(int src, int dst, unsigned long long bytes, int it
   if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) return (int)pe;
   (void)hipGetLastError();
   const size_t n4 = (size_t)(bytes / 16);
-  float4 *local = nullptr, *remote = nullptr;
+  f4 *local = nullptr, *remote = nullptr;
   YODA_CHECK(hipMalloc(&local, n4 * 16));
   YODA_CHECK(hipMemset(local, 0, n4 * 16));
   YODA_CHECK(hipSetDevice(dst));
   YODA_CHECK(hipMalloc(&remote, n4 * 16));
   YODA_CHECK(hipSetDevice(src));
-  const int grid = grid_for(src);
+  const int grid = grid_for(src, kBlocksPerCu);
   hipEvent_t e0, e1;
   YODA_CHECK(hipEventCreate(&e0));
   YODA_CHECK(hipEventCreate(&e1));

@@ -33,9 +33,10 @@ def test_hbm_pattern_probe_detects_mismatch_semantics(require_gpu):
 def test_hbm_bandwidth_probe(require_gpu):
     from yoda_scheduler_amd.ops import hip
     r = hip.hbm_bandwidth(0, 1 << 30, 10)
-    # MI355X: 8 TB/s peak, ~6.3 TB/s achievable; anything below 2 TB/s means a broken probe
-    assert r["read_gbps"] > 2000, r
-    assert r["copy_gbps"] > 2000, r
+    # MI355X: 8 TB/s peak, ≈6.3 TB/s achievable; the probe's shape reads ≈6.1 TB/s at 1 GiB
+    # (profiles/hbm_probe_sweep.jsonl) — well below 4.5 TB/s means a regressed probe
+    assert r["read_gbps"] > 4500, r
+    assert r["copy_gbps"] > 3500, r
 
 
 def test_amdsmi_collector_real(require_gpu):
