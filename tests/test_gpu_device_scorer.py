@@ -61,3 +61,47 @@ def test_device_cycle_latency(require_gpu):
     ts.sort()
     # two launches over 8192 nodes x 8 GPUs: must stay far below a millisecond
     assert ts[len(ts) // 2] < 1000, ts
+
+
+def test_scheduler_auto_enables_device_scorer_and_matches_cpu(require_gpu):
+    """The full scheduler (informers → queue → batch cycles → bind) on a 512-node fake
+    cluster: `deviceScorer: auto` attaches the gfx950 scorer after sync and the cycles run
+    on the device; every pod is bound with the GPU count it asked for, no GPU is
+    over-reserved, and the CPU-only run of the same burst binds the same pods (node choice
+    may differ only between tied nodes — cycle-level parity is pinned above)."""
+    import asyncio
+
+    from yoda_scheduler_amd.testing import FakeCluster, yoda_config
+
+    def run(device):
+        async def go():
+            cfg = yoda_config(batch=64)
+            cfg["yodaRuntime"]["deviceScorer"] = {"enabled": device, "minNodes": 256}
+            c = FakeCluster(cfg, seed=7)
+            rng = random.Random(11)
+            for i in range(512):
+                c.add_node(f"n{i:03d}", used_mb=[rng.choice([0, 20000, 90000]) for _ in range(8)])
+            sched = await c.start()
+            for i in range(300):
+                lab = {"scv/memory": str(rng.choice([1024, 4096, 30000]))}
+                if i % 5 == 0:
+                    lab["scv/number"] = str(rng.choice([2, 4]))
+                c.add_pod(f"p{i}", lab)
+            ok = await c.wait_bound(300, 30.0)
+            placed = {f"p{i}": (c.node_of(f"p{i}"), tuple(c.gpus_of(f"p{i}"))) for i in range(300)}
+            want = {f"p{i}": int(c.pod(f"p{i}")["metadata"]["labels"].get("scv/number", "1")) for i in range(300)}
+            assert all(len(g) == want[p] and node for p, (node, g) in placed.items())
+            for n in {node for node, _ in placed.values()}:
+                assert all(st["reserved"] <= st["total"] for st in sched.cache.node_gpu_state(n))
+            stats = (sched.engine.device_enabled, sched.engine.device_cycles, sched.engine.device_fallbacks,
+                     sched.device_error)
+            await c.stop()
+            return ok, placed, stats
+        return asyncio.run(go())
+
+    ok_d, placed_d, (enabled, cycles, fallbacks, err) = run("auto")
+    ok_c, placed_c, (enabled_c, cycles_c, _, _) = run("off")
+    assert ok_d and ok_c
+    assert enabled and cycles >= 300 and fallbacks == 0, (enabled, cycles, fallbacks, err)
+    assert not enabled_c and cycles_c == 0
+    assert placed_d.keys() == placed_c.keys()
