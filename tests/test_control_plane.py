@@ -306,3 +306,81 @@ def test_tracer_chrome_trace():
     tr = run(go())
     names = {e["name"] for e in tr["traceEvents"]}
     assert "bind" in names and ({"cycle", "native_batch"} & names)
+
+
+def test_https_kubeconfig_with_ca_data_and_token(tmp_path):
+    """The production client path: HTTPS with the cluster CA from a kubeconfig's
+    ``certificate-authority-data`` and a bearer token; a wrong token is rejected (401) and
+    an unknown CA fails the TLS handshake. A scheduler over that client binds a pod."""
+    import base64
+    import shutil
+    import ssl
+
+    if not shutil.which("openssl"):
+        pytest.skip("openssl not available")
+    d = tmp_path
+    sh = lambda *a: subprocess.run(a, check=True, capture_output=True)  # noqa: E731
+    sh("openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-days", "1", "-subj", "/CN=yoda-test-ca",
+       "-keyout", str(d / "ca.key"), "-out", str(d / "ca.crt"))
+    sh("openssl", "req", "-newkey", "rsa:2048", "-nodes", "-subj", "/CN=127.0.0.1",
+       "-keyout", str(d / "srv.key"), "-out", str(d / "srv.csr"))
+    (d / "ext.cnf").write_text("subjectAltName=IP:127.0.0.1\n")
+    sh("openssl", "x509", "-req", "-in", str(d / "srv.csr"), "-CA", str(d / "ca.crt"), "-CAkey", str(d / "ca.key"),
+       "-CAcreateserial", "-days", "1", "-extfile", str(d / "ext.cnf"), "-out", str(d / "srv.crt"))
+    ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+    ctx.load_cert_chain(str(d / "srv.crt"), str(d / "srv.key"))
+
+    async def go():
+        from yoda_scheduler_amd.framework.config import parse_config
+        from yoda_scheduler_amd.framework.scheduler import Scheduler
+        from yoda_scheduler_amd.testing import yoda_config
+        srv = FakeApiServer()
+        srv.create("nodes", make_node("n0"))
+        scv = make_scv("n0", update_time=time.time())
+        scv.update_interval_ms = 60_000
+        srv.create("scvs", scv.to_json())
+        api = FakeApiHttp(srv, ssl_context=ctx, token="s3cret")
+        url = await api.start()
+        ca_b64 = base64.b64encode((d / "ca.crt").read_bytes()).decode()
+        kc = {"apiVersion": "v1", "kind": "Config", "current-context": "t",
+              "clusters": [{"name": "c", "cluster": {"server": url, "certificate-authority-data": ca_b64}}],
+              "users": [{"name": "u", "user": {"token": "s3cret"}}],
+              "contexts": [{"name": "t", "context": {"cluster": "c", "user": "u"}}]}
+        import yaml
+        (d / "kubeconfig").write_text(yaml.safe_dump(kc))
+        good = KubeClient(KubeConfig.load(str(d / "kubeconfig")))
+        bad_token = KubeClient(KubeConfig(url, token="nope", ca_file=str(d / "ca.crt")))
+        no_ca = KubeClient(KubeConfig(url, token="s3cret"))
+        errors = []
+        try:
+            nodes, _ = await good.list("nodes")
+            for cl in (bad_token, no_ca):
+                try:
+                    await cl.list("nodes")
+                    errors.append("accepted")
+                except ApiError as e:
+                    errors.append(e.code)
+                except Exception as e:  # noqa: BLE001 - TLS verification failure
+                    errors.append(type(e).__name__)
+            sched = Scheduler(good, parse_config(yoda_config()))
+            await sched.start()
+            loop_t = asyncio.get_event_loop().create_task(sched.scheduling_loop())
+            await good.create("pods", {"metadata": {"name": "tls", "namespace": "default",
+                                                    "labels": {"scv/memory": "1000"}},
+                                       "spec": {"schedulerName": "yoda-scheduler"}})
+            for _ in range(400):
+                if srv.bind_log:
+                    break
+                await asyncio.sleep(0.01)
+            await sched.shutdown()
+            loop_t.cancel()
+            return len(nodes), errors, dict(srv.bind_node)
+        finally:
+            for cl in (good, bad_token, no_ca):
+                await cl.close()
+            await api.stop()
+
+    n, errors, bound = run(go())
+    assert n == 1
+    assert errors[0] == 401 and errors[1] != "accepted"
+    assert bound == {"default/tls": "n0"}

@@ -36,10 +36,15 @@ def _status(e: ApiError) -> web.Response:
 
 
 class FakeApiHttp:
-    def __init__(self, server: Optional[FakeApiServer] = None, host: str = "127.0.0.1", port: int = 0) -> None:
+    def __init__(self, server: Optional[FakeApiServer] = None, host: str = "127.0.0.1", port: int = 0,
+                 ssl_context=None, token: Optional[str] = None) -> None:
+        """``ssl_context`` serves HTTPS (as a real apiserver does); ``token`` makes every
+        API route require ``Authorization: Bearer <token>`` (401 otherwise)."""
         self.server = server or FakeApiServer()
         self.host = host
         self.port = port
+        self.ssl_context = ssl_context
+        self.token = token
         self._runner: Optional[web.AppRunner] = None
         self.app = web.Application()
         async def healthz(_r):
@@ -54,12 +59,12 @@ class FakeApiHttp:
 
     @property
     def url(self) -> str:
-        return f"http://{self.host}:{self.port}"
+        return f"{'https' if self.ssl_context else 'http'}://{self.host}:{self.port}"
 
     async def start(self) -> str:
         self._runner = web.AppRunner(self.app)
         await self._runner.setup()
-        site = web.TCPSite(self._runner, self.host, self.port)
+        site = web.TCPSite(self._runner, self.host, self.port, ssl_context=self.ssl_context)
         await site.start()
         self.port = site._server.sockets[0].getsockname()[1]   # type: ignore[union-attr]
         return self.url
@@ -70,6 +75,8 @@ class FakeApiHttp:
             await self._runner.cleanup()
 
     async def dispatch(self, req: web.Request) -> web.StreamResponse:
+        if self.token is not None and req.headers.get("Authorization") != f"Bearer {self.token}":
+            return _status(ApiError(401, "Unauthorized", "Unauthorized"))
         r = _resolve(req.path)
         if r is None:
             return _status(ApiError(404, "NotFound", f"no route for {req.path}"))
