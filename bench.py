@@ -62,6 +62,9 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=256, help="native batch size (1 = strictly one pod per cycle)")
     ap.add_argument("--compat", action="store_true", help="reference-compatible yoda scoring (no HBM ledger)")
     ap.add_argument("--no-events", action="store_true")
+    ap.add_argument("--transport", choices=["inproc", "http"], default="inproc",
+                    help="inproc: fake apiserver in the scheduler process (headline); http: apiserver in its own "
+                         "process, scheduler over the production HTTP/JSON client")
     a = ap.parse_args(argv)
     if a.reference_qps:
         a.qps, a.burst = 50.0, 100
@@ -87,15 +90,22 @@ def main(argv=None) -> int:
 
     tmpl, tel = _telemetry_template(local_rank)
 
-    from yoda_scheduler_amd.bench.harness import Shard, percentile
+    from yoda_scheduler_amd.bench.harness import HttpShard, Shard, percentile
     from yoda_scheduler_amd.bench.workloads import make_workload
     w = make_workload(a.config, seed=rank)
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
-    shards = [Shard(w, qps=a.qps, burst=a.burst, batch=a.batch, template=tmpl, events=not a.no_events,
-                    compat=a.compat, seed=rank * 1000 + i, device=a.device) for i in range(a.warmup + a.steps)]
-    for s in shards:
-        loop.run_until_complete(s.start())
+    if a.transport == "http":
+        # one apiserver process per rank; bursts reuse it (the previous burst is deleted first)
+        one = HttpShard(w, qps=a.qps, burst=a.burst, batch=a.batch, template=tmpl, events=not a.no_events,
+                        compat=a.compat, seed=rank * 1000, device=a.device)
+        shards = [one] * (a.warmup + a.steps)
+        loop.run_until_complete(one.start())
+    else:
+        shards = [Shard(w, qps=a.qps, burst=a.burst, batch=a.batch, template=tmpl, events=not a.no_events,
+                        compat=a.compat, seed=rank * 1000 + i, device=a.device) for i in range(a.warmup + a.steps)]
+        for s in shards:
+            loop.run_until_complete(s.start())
     for i in range(a.warmup):
         loop.run_until_complete(shards[i].burst(f"w{i}"))
 
@@ -105,7 +115,7 @@ def main(argv=None) -> int:
     sync()
     elapsed = time.perf_counter() - t0
 
-    device_cycles = sum(s.sched.engine.device_cycles for s in shards)
+    device_cycles = sum(s.sched.engine.device_cycles for s in {id(x): x for x in shards}.values())
     bound = sum(r.bound for r in results)
     unsched = sum(r.unschedulable for r in results)
     lats = [x for r in results for x in r.latencies_s]
@@ -127,7 +137,7 @@ def main(argv=None) -> int:
         dist.all_gather_object(tels, tel)
     else:
         tels = [tel]
-    for s in shards:
+    for s in {id(x): x for x in shards}.values():
         loop.run_until_complete(s.stop())
 
     if rank == 0:
@@ -156,7 +166,7 @@ def main(argv=None) -> int:
             "pods_bound": bound,
             "pods_unschedulable": unsched,
             "client_qps": a.qps, "client_burst": a.burst, "native_batch": a.batch, "compat": a.compat,
-            "device_scorer": a.device, "device_cycles": device_cycles,
+            "device_scorer": a.device, "device_cycles": device_cycles, "transport": a.transport,
             "baseline_note": "vs_baseline against BASELINE.md's derived (unmeasured) ~55 pods/s reference ceiling "
                              "(kube-scheduler v1.20 client QPS 50 / burst 100)",
             "telemetry": tels[0],

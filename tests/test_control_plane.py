@@ -384,3 +384,16 @@ def test_https_kubeconfig_with_ca_data_and_token(tmp_path):
     assert n == 1
     assert errors[0] == 401 and errors[1] != "accepted"
     assert bound == {"default/tls": "n0"}
+
+
+def test_bench_http_transport_contract():
+    """bench.py --transport http: apiserver in its own process, scheduler over the HTTP
+    client; every pod of a config-2 burst is bound and the JSON line follows the contract."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--transport", "http", "--config", "2",
+                        "--steps", "2", "--warmup", "1"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["transport"] == "http" and d["pods_bound"] == 200 and d["pods_unschedulable"] == 0
+    assert d["value"] > 0 and d["p99_latency_ms"] > 0 and d["e2e_scheduling_p99_ms"] is not None

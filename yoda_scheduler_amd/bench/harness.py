@@ -126,3 +126,105 @@ async def run_bursts(w: Workload, steps: int, warmup: int, **kw) -> tuple[list[B
     for s in shards:
         await s.stop()
     return res, total
+
+
+class HttpShard:
+    """The same burst over real HTTP/JSON: the fake apiserver runs in its own process
+    (``yoda-fake-apiserver --bench-config N``), the scheduler talks to it through the
+    production client (:class:`~yoda_scheduler_amd.kube.client.KubeClient`: list/watch
+    streams, binding POSTs), and the apiserver creates the pods and measures latency on
+    its own clock. Between bursts the apiserver deletes the previous burst's pods, which
+    releases their reservations through the scheduler's informer."""
+
+    def __init__(self, w: Workload, qps: float = 5000.0, burst: int = 10000, batch: int = 256,
+                 template: Optional[dict] = None, events: bool = True, compat: bool = False, seed: int = 0,
+                 device: str = "auto") -> None:
+        import json
+        import subprocess
+        import sys
+        import tempfile
+        self.w = w
+        self._dir = tempfile.mkdtemp(prefix="yoda-bench-")
+        self.port_file = f"{self._dir}/port"
+        cmd = [sys.executable, "-m", "yoda_scheduler_amd.cmd.fakeapi", "--port", "0", "--bench-config", str(w.id),
+               "--seed", str(seed), "--port-file", self.port_file]
+        if template:
+            cmd += ["--template", json.dumps(template)]
+        self.proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+        self.cfg = parse_config(bench_config(w.scheduler_name, qps, burst, batch, compat, device))
+        self.events, self.seed = events, seed
+        self.sched: Optional[Scheduler] = None
+        self.client = None
+        self._loop_task: Optional[asyncio.Task] = None
+        self._bursts = 0
+
+    async def _port(self, timeout: float = 120.0) -> int:
+        import os
+        t = time.monotonic() + timeout
+        while time.monotonic() < t:
+            if os.path.exists(self.port_file):
+                with open(self.port_file) as f:
+                    return int(f.read())
+            if self.proc.poll() is not None:
+                raise RuntimeError(f"fake apiserver exited: {self.proc.stderr.read().decode()[-2000:]}")
+            await asyncio.sleep(0.05)
+        raise TimeoutError("fake apiserver did not start")
+
+    async def start(self) -> None:
+        import aiohttp
+
+        from ..kube.client import KubeClient, KubeConfig
+        port = await self._port()
+        self.base = f"http://127.0.0.1:{port}"
+        self.client = KubeClient(KubeConfig(self.base))
+        self._http = aiohttp.ClientSession()
+        self.sched = Scheduler(self.client, self.cfg, metrics=NullMetrics(), record_events=self.events,
+                               seed=self.seed)
+        self.sched.e2e_samples = []
+        await self.sched.start()
+        self._loop_task = asyncio.get_event_loop().create_task(self.sched.scheduling_loop())
+
+    async def _call(self, method: str, path: str, body: Optional[dict] = None) -> dict:
+        async with self._http.request(method, self.base + path, json=body) as r:
+            r.raise_for_status()
+            return await r.json()
+
+    async def burst(self, tag: str = "b", timeout: float = 600.0) -> BurstResult:
+        if self._bursts:
+            await self._call("POST", "/debug/bench/reset")
+            q = self.sched.queue
+            while self.sched.cache.pods or q._active_entries or self.sched.pending_binds:
+                await asyncio.sleep(0.001)      # the deletes reached the scheduler
+        self._bursts += 1
+        self.sched.e2e_samples.clear()
+        n = (await self._call("POST", "/debug/bench/burst", {"tag": tag}))["n"]
+        q = self.sched.queue
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            st = await self._call("GET", "/debug/bench/status")
+            if st["bound"] >= n:
+                break
+            if not q._active_entries and self.sched.pending_binds == 0 and \
+                    st["bound"] + len(q._unsched) + len(q._backoff_pods) >= n:
+                break
+            await asyncio.sleep(0.002)
+        st = await self._call("GET", "/debug/bench/status?full=1")
+        return BurstResult(n, st["bound"], n - st["bound"], st["elapsed"], st["latencies"],
+                           list(self.sched.e2e_samples))
+
+    async def stop(self) -> None:
+        import shutil
+        if self.sched is not None:
+            await self.sched.shutdown()
+        if self._loop_task:
+            self._loop_task.cancel()
+            await asyncio.gather(self._loop_task, return_exceptions=True)
+        if self.client is not None:
+            await self.client.close()
+            await self._http.close()
+        self.proc.terminate()
+        try:
+            self.proc.wait(10)
+        except Exception:  # noqa: BLE001
+            self.proc.kill()
+        shutil.rmtree(self._dir, ignore_errors=True)

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import asyncio
 import json
+import os
 import re
 from typing import Optional
 
@@ -37,7 +38,7 @@ def _status(e: ApiError) -> web.Response:
 
 class FakeApiHttp:
     def __init__(self, server: Optional[FakeApiServer] = None, host: str = "127.0.0.1", port: int = 0,
-                 ssl_context=None, token: Optional[str] = None) -> None:
+                 ssl_context=None, token: Optional[str] = None, bench: bool = False) -> None:
         """``ssl_context`` serves HTTPS (as a real apiserver does); ``token`` makes every
         API route require ``Authorization: Bearer <token>`` (401 otherwise)."""
         self.server = server or FakeApiServer()
@@ -55,6 +56,13 @@ class FakeApiHttp:
 
         self.app.router.add_get("/healthz", healthz)
         self.app.router.add_get("/version", version)
+        if bench:
+            # burst driver for the HTTP transport of bench.py: pods are created and the
+            # latencies measured here, on the apiserver's clock, like the in-process harness
+            self.app.router.add_post("/debug/bench/burst", self._bench_burst)
+            self.app.router.add_get("/debug/bench/status", self._bench_status)
+            self.app.router.add_post("/debug/bench/reset", self._bench_reset)
+            self.bench_workload = None
         self.app.router.add_route("*", "/{tail:.*}", self.dispatch)
 
     @property
@@ -68,6 +76,35 @@ class FakeApiHttp:
         await site.start()
         self.port = site._server.sockets[0].getsockname()[1]   # type: ignore[union-attr]
         return self.url
+
+    async def _bench_burst(self, req: web.Request) -> web.Response:
+        from ..bench.workloads import pod_object
+        body = await req.json()
+        w = self.bench_workload
+        tag = body.get("tag", "b")
+        self.server.reset_logs()
+        for i, lab in enumerate(w.pods):
+            self.server.create("pods", pod_object(i, lab, w.scheduler_name, prefix=tag))
+            if i % 64 == 63:
+                await asyncio.sleep(0)
+        return web.json_response({"n": len(w.pods)})
+
+    async def _bench_status(self, req: web.Request) -> web.Response:
+        s = self.server
+        out = {"created": len(s.create_log), "bound": len(s.bind_log)}
+        if req.query.get("full"):
+            out["latencies"] = s.latencies()
+            t0 = min(s.create_log.values()) if s.create_log else 0.0
+            out["elapsed"] = (max(s.bind_log.values()) - t0) if s.bind_log else 0.0
+        return web.json_response(out)
+
+    async def _bench_reset(self, _req: web.Request) -> web.Response:
+        items, _ = self.server.list("pods")
+        for o in items:
+            m = o["metadata"]
+            self.server.delete("pods", m["name"], m.get("namespace", "default"))
+        self.server.reset_logs()
+        return web.json_response({"deleted": len(items)})
 
     async def stop(self) -> None:
         self.server.close_watches()
@@ -138,9 +175,15 @@ class FakeApiHttp:
         return resp
 
 
-async def serve_forever(host: str = "127.0.0.1", port: int = 8001, server: Optional[FakeApiServer] = None) -> None:
-    api = FakeApiHttp(server, host, port)
+async def serve_forever(host: str = "127.0.0.1", port: int = 8001, server: Optional[FakeApiServer] = None,
+                        workload=None, port_file: str = "") -> None:
+    api = FakeApiHttp(server, host, port, bench=workload is not None)
+    api.bench_workload = workload
     url = await api.start()
+    if port_file:
+        with open(port_file + ".tmp", "w") as f:
+            f.write(str(api.port))
+        os.replace(port_file + ".tmp", port_file)
     print(f"fake apiserver listening on {url}", flush=True)
     while True:
         await asyncio.sleep(3600)

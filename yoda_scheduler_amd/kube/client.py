@@ -153,8 +153,10 @@ class KubeClient:
             buf = b""
             async for chunk in r.content.iter_any():
                 buf += chunk
-                while b"\n" in buf:
-                    line, buf = buf.split(b"\n", 1)
+                if b"\n" not in chunk:
+                    continue
+                *lines, buf = buf.split(b"\n")     # one split per chunk, not per event
+                for line in lines:
                     if not line.strip():
                         continue
                     ev = json.loads(line)
