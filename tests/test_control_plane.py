@@ -397,3 +397,67 @@ def test_bench_http_transport_contract():
     d = json.loads(line)
     assert d["transport"] == "http" and d["pods_bound"] == 200 and d["pods_unschedulable"] == 0
     assert d["value"] > 0 and d["p99_latency_ms"] > 0 and d["e2e_scheduling_p99_ms"] is not None
+
+
+def test_fastbind_pipelining_errors_chunked_and_reconnect():
+    """The pipelined binding client: many binds in flight over a few connections against
+    the fake apiserver (404 / 409 surface as ApiError), and against a raw server that
+    answers with a chunked body and then closes the connection (the client reconnects)."""
+    from yoda_scheduler_amd.kube.fastbind import FastBinder
+
+    async def go():
+        srv = FakeApiServer()
+        srv.create("nodes", make_node("n0"))
+        for i in range(300):
+            srv.create("pods", {"metadata": {"name": f"p{i}", "namespace": "default"}, "spec": {}})
+        api = FakeApiHttp(srv)
+        url = await api.start()
+        fb = FastBinder(url, conns=3, max_inflight=8)
+        await asyncio.gather(*(fb.bind("default", f"p{i}", "", "n0") for i in range(300)))
+        codes = []
+        for name in ("p0", "missing"):
+            try:
+                await fb.bind("default", name, "", "n0")
+            except ApiError as e:
+                codes.append(e.code)
+        await fb.close()
+        await api.stop()
+
+        # raw server: chunked 201, then "Connection: close"
+        served = []
+
+        async def handle(r, w):
+            while True:
+                line = await r.readline()
+                if not line:
+                    break
+                length = 0
+                while True:
+                    h = await r.readline()
+                    if h in (b"\r\n", b""):
+                        break
+                    if h.lower().startswith(b"content-length:"):
+                        length = int(h.split(b":")[1])
+                await r.readexactly(length)
+                served.append(1)
+                close = len(served) % 2 == 0
+                w.write(b"HTTP/1.1 201 Created\r\nTransfer-Encoding: chunked\r\n" +
+                        (b"Connection: close\r\n" if close else b"") + b"\r\n4\r\n{\"a\"\r\n3\r\n:1}\r\n0\r\n\r\n")
+                await w.drain()
+                if close:
+                    w.close()
+                    return
+        raw = await asyncio.start_server(handle, "127.0.0.1", 0)
+        port = raw.sockets[0].getsockname()[1]
+        fb2 = FastBinder(f"http://127.0.0.1:{port}", conns=1)
+        for i in range(6):
+            await fb2.bind("default", f"x{i}", "", "n0")
+        await fb2.close()
+        raw.close()
+        await raw.wait_closed()
+        return len(srv.bind_log), codes, len(served)
+
+    bound, codes, served = run(go())
+    assert bound == 300
+    assert codes == [409, 404]
+    assert served == 6
