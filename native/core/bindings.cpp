@@ -247,11 +247,13 @@ PYBIND11_MODULE(_yoda_core, m) {
              return py::make_tuple(ok, out, q);
            })
       .def("feasible_nodes",
-           [](Engine& e, const PodReq& r, const std::vector<int32_t>& cand) {
+           [](Engine& e, const PodReq& r, const std::vector<int32_t>& cand, bool exhaustive) {
              std::vector<int32_t> reasons;
-             auto f = e.feasible_nodes(r, cand, &reasons);
+             auto f = e.feasible_nodes(r, cand, &reasons, exhaustive);
              return py::make_tuple(f, reasons);
-           })
+           },
+           py::arg("req"), py::arg("candidates"), py::arg("exhaustive") = false)
+      .def("num_feasible_to_find", &Engine::num_feasible_to_find)
       .def("score_nodes", &Engine::score_nodes)
       .def("schedule",
            [](Engine& e, uint64_t pod, const PodReq& r, bool assume, const std::vector<int32_t>& cand,

@@ -645,7 +645,7 @@ int32_t Engine::num_feasible_to_find(int32_t all) const {
 }
 
 std::vector<int32_t> Engine::feasible_nodes(const PodReq& req, const std::vector<int32_t>& candidates,
-                                            std::vector<int32_t>* reasons) {
+                                            std::vector<int32_t>* reasons, bool exhaustive) {
   std::vector<int32_t> all;
   if (candidates.empty()) {
     all.reserve(live_);
@@ -658,7 +658,7 @@ std::vector<int32_t> Engine::feasible_nodes(const PodReq& req, const std::vector
   std::vector<int32_t> feasible;
   if (reasons) reasons->assign(RS_NUM, 0);
   if (N == 0) return feasible;
-  const int32_t want = num_feasible_to_find(N);
+  const int32_t want = exhaustive ? N : num_feasible_to_find(N);
   const int32_t start = next_start_ % N;
   std::vector<int8_t> res;
   int32_t processed = 0;

@@ -173,6 +173,7 @@ class Engine {
   int64_t score_weight(int idx) const { return score_w_[idx]; }
   Weights& weights() { return wt_; }
   void set_percentage_of_nodes_to_score(int p) { pct_nodes_ = p; }
+  int32_t num_feasible_to_find(int32_t all) const;   // upstream numFeasibleNodesToFind
   void seed(uint64_t s) { rng_.seed(s); }
   int32_t intern(const std::string& s);
   const std::string& str(int32_t id) const { return strings_[id]; }
@@ -227,8 +228,10 @@ class Engine {
                                           const std::vector<const PodReq*>& reqs);
 
   // Filter only → feasible node indices (for the hybrid runner)
+  // exhaustive: ignore percentageOfNodesToScore (the caller applies further filters and
+  // does its own early exit, so the sample must be taken over nodes passing ALL filters)
   std::vector<int32_t> feasible_nodes(const PodReq& req, const std::vector<int32_t>& candidates,
-                                      std::vector<int32_t>* reasons);
+                                      std::vector<int32_t>* reasons, bool exhaustive = false);
   // Native weighted score of the given feasible nodes (normalized per plugin, summed).
   std::vector<int64_t> score_nodes(const PodReq& req, const std::vector<int32_t>& feasible);
 
@@ -267,7 +270,6 @@ class Engine {
   uint64_t eff_free(const Card& c) const;
   int64_t gang_objective(const Node& n, const std::vector<int32_t>& set, uint64_t m,
                          int64_t* link_bad) const;
-  int32_t num_feasible_to_find(int32_t all) const;
 
   bool compat_;
   uint32_t filters_ = F_NODE_UNSCHEDULABLE | F_NODE_NAME | F_TAINT_TOLERATION | F_NODE_AFFINITY |

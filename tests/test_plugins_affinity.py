@@ -89,3 +89,78 @@ def test_required_affinity_and_symmetry():
     cache_node, client_node, noisy_nodes = run(go())
     assert client_node == cache_node
     assert cache_node not in noisy_nodes
+
+
+def test_preferred_affinity_and_hard_pod_affinity_weight_scoring():
+    """Preferred pod affinity pulls a pod into the zone of matching pods; an existing pod's
+    required affinity term that matches the incoming pod scores its domain with
+    hardPodAffinityWeight (upstream symmetric scoring)."""
+    async def go():
+        cfg = default_cfg()
+        cfg["profiles"][0]["pluginConfig"].append({"name": "InterPodAffinity", "args": {"hardPodAffinityWeight": 5}})
+        # weight the affinity score above yoda's so the test isolates it
+        cfg["profiles"][0]["plugins"]["score"]["enabled"].append({"name": "InterPodAffinity", "weight": 1000})
+        c = FakeCluster(cfg)
+        for i, zone in enumerate(("z1", "z1", "z2", "z2")):
+            c.add_node(f"n{i}", labels={"topology.kubernetes.io/zone": zone})
+        await c.start()
+        c.add_pod("web", {"app": "web", "scv/memory": "1000"}, nodeSelector={"kubernetes.io/hostname": "n3"})
+        await c.wait_bound(1)
+        pref = {"podAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+            {"weight": 100, "podAffinityTerm": {"topologyKey": "topology.kubernetes.io/zone",
+                                                "labelSelector": {"matchLabels": {"app": "web"}}}}]}}
+        c.add_pod("near-web", {"app": "x", "scv/memory": "1000"}, affinity=pref)
+        # an existing pod that *requires* affinity to app=db (satisfied by db0 in zone z1):
+        # a new db pod is pulled to z1 by hardPodAffinityWeight
+        c.add_pod("db0", {"app": "db", "scv/memory": "1000"}, nodeSelector={"kubernetes.io/hostname": "n1"})
+        await c.wait_bound(3)
+        req = {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+            {"topologyKey": "topology.kubernetes.io/zone", "labelSelector": {"matchLabels": {"app": "db"}}}]}}
+        c.add_pod("db-client", {"app": "dbc", "scv/memory": "1000"}, affinity=req)
+        await c.wait_bound(4)
+        # the plugin's own view for a db pod: z1 nodes carry hardPodAffinityWeight (5)
+        from yoda_scheduler_amd.framework.interfaces import CycleState
+        from yoda_scheduler_amd.models.pod import PodInfo
+        ipa = c.sched.frameworks["yoda-scheduler"].plugins["InterPodAffinity"]
+        probe = PodInfo.from_obj({"metadata": {"name": "probe", "namespace": "default", "uid": "probe",
+                                               "labels": {"app": "db"}}, "spec": {}})
+        st = CycleState()
+        ipa.pre_score(st, probe, [])
+        raw = {n: ipa.score(st, probe, n)[0] for n in ("n0", "n1", "n2", "n3")}
+        c.add_pod("db", {"app": "db", "scv/memory": "1000"})
+        await c.wait_bound(5)
+        out = c.node_of("near-web"), c.node_of("db-client"), c.node_of("db"), raw
+        await c.stop()
+        return out
+    near, dbc, db, raw = run(go())
+    assert raw == {"n0": 5, "n1": 5, "n2": 0, "n3": 0}
+    assert near in ("n2", "n3")
+    assert dbc in ("n0", "n1") and db in ("n0", "n1")
+
+
+def test_anti_affinity_symmetry_scales():
+    """300 bound pods with hostname anti-affinity on a 400-node cluster: the per-cycle
+    precomputation keeps scheduling 100 more pods fast (no node × pod rescans)."""
+    import time
+
+    async def go():
+        c = FakeCluster(default_cfg())
+        for i in range(400):
+            c.add_node(f"n{i:03d}")
+        await c.start()
+        anti = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+            {"topologyKey": "kubernetes.io/hostname", "labelSelector": {"matchLabels": {"app": "solo"}}}]}}
+        for i in range(300):
+            c.add_pod(f"solo{i}", {"app": "solo", "scv/memory": "1000"}, affinity=anti)
+        ok1 = await c.wait_bound(300, 60)
+        t = time.perf_counter()
+        for i in range(100):
+            c.add_pod(f"plain{i}", {"app": "plain", "scv/memory": "1000"})
+        ok2 = await c.wait_bound(400, 60)
+        dt = time.perf_counter() - t
+        solo_nodes = {c.node_of(f"solo{i}") for i in range(300)}
+        await c.stop()
+        return ok1, ok2, dt, len(solo_nodes)
+    ok1, ok2, dt, distinct = run(go())
+    assert ok1 and ok2 and distinct == 300
+    assert dt < 20, dt

@@ -140,12 +140,22 @@ class Framework:
                 return st
         return Status.ok()
 
-    def run_filter_py(self, state: CycleState, pod, nodes: list[str]) -> tuple[list[str], dict]:
+    def has_active_filter_py(self, pod) -> bool:
+        return any(self._applies(p, pod) for p in self.filter_py)
+
+    def run_filter_py(self, state: CycleState, pod, nodes: list[str],
+                      limit: Optional[int] = None) -> tuple[list[str], dict]:
+        """Python filters over the native-feasible ``nodes``; stops once ``limit`` nodes
+        passed (numFeasibleNodesToFind)."""
         if not self.filter_py:
             return nodes, {}
         out, failed = [], {}
         active = [p for p in self.filter_py if self._applies(p, pod)]
+        if not active:
+            return nodes, {}
         for n in nodes:
+            if limit is not None and len(out) >= limit:
+                break
             for p in active:
                 st = p.filter(state, pod, n)
                 if not st.is_success():

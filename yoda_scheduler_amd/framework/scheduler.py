@@ -287,9 +287,18 @@ class Scheduler:
                        f"{st.message()}", time.perf_counter())
             return None
         req = pod_req(self.engine, pi)
-        feas_idx, reasons = self.engine.feasible_nodes(req, [])
-        names = [self.engine.node_name(i) for i in feas_idx]
-        names2, failed = fw.run_filter_py(state, pi, names)
+        eng = self.engine
+        if fw.has_active_filter_py(pi):
+            # percentageOfNodesToScore must sample nodes that pass ALL filters (upstream runs
+            # every filter plugin inside the same search): take every native-feasible node,
+            # let the Python filters stop at numFeasibleNodesToFind
+            feas_idx, reasons = eng.feasible_nodes(req, [], True)
+            limit = eng.num_feasible_to_find(eng.live_nodes)
+        else:
+            feas_idx, reasons = eng.feasible_nodes(req, [])
+            limit = None
+        names = [eng.node_name(i) for i in feas_idx]
+        names2, failed = fw.run_filter_py(state, pi, names, limit)
         if len(names2) != len(names):
             keep = set(names2)
             feas_idx = [i for i, n in zip(feas_idx, names) if n in keep]

@@ -30,6 +30,8 @@ def _node_labels(handle, node: str) -> dict:
 class _SpreadState(StateData):
     def __init__(self, hard, soft, counts, domains):
         self.hard, self.soft, self.counts, self.domains = hard, soft, counts, domains
+        # global minimum matching count per hard constraint (computed once, not per node)
+        self.min_count = [min((counts.get((ci, d), 0) for d in domains[ci]), default=0) for ci in range(len(hard))]
 
 
 class PodTopologySpread(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin):
@@ -85,8 +87,7 @@ class PodTopologySpread(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlug
                 return Status.unschedulable("node(s) didn't match pod topology spread constraints (missing label)",
                                             plugin=self.name)
             self_match = 1 if sel.matches(pod.labels) else 0
-            min_count = min((s.counts.get((ci, d), 0) for d in s.domains[ci]), default=0)
-            if s.counts.get((ci, labels[key]), 0) + self_match - min_count > max_skew:
+            if s.counts.get((ci, labels[key]), 0) + self_match - s.min_count[ci] > max_skew:
                 return Status.unschedulable("node(s) didn't match pod topology spread constraints", plugin=self.name)
         return Status.ok()
 
@@ -131,15 +132,38 @@ def _term_matches(term: dict, owner_ns: str, other) -> bool:
 
 
 class _AffinityState(StateData):
-    def __init__(self, by_node):
-        self.by_node = by_node      # node → list[PodInfo]
+    """Topology-pair counts computed once per cycle (upstream ``preFilterState``):
+    ``existing_anti``: (key, value) domains where an existing pod's required anti-affinity
+    matches the incoming pod; ``affinity`` / ``anti``: per required term of the incoming pod,
+    the (key, value) domains holding pods that match it; ``scores``: (key, value) → weight
+    for the preferred terms (both directions) and existing pods' required affinity
+    (``hardPodAffinityWeight``)."""
+
+    def __init__(self) -> None:
+        self.existing_anti: dict = defaultdict(set)     # topology key → values with a blocking pod
+        self.affinity: dict = defaultdict(int)
+        self.any_affinity_match = False
+        self.anti: dict = defaultdict(int)
+        self.aff_terms: list = []
+        self.anti_terms: list = []
+        self.scores: Optional[dict] = None      # topology key → value → weight
+
+    def clone(self) -> "_AffinityState":
+        return self
 
 
 class InterPodAffinity(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin):
+    """Required pod (anti-)affinity as a filter (incl. the symmetric rule for existing
+    pods' required anti-affinity), preferred terms + ``hardPodAffinityWeight`` as a score.
+    Each cycle walks the bound/assumed pods once; per-node work is a few dict lookups."""
     name = "InterPodAffinity"
     KEY = "PreFilterInterPodAffinity"
 
     pod_flags = PF_POD_AFFINITY
+
+    def __init__(self, args=None, handle=None) -> None:
+        super().__init__(args, handle)
+        self.hard_weight = int(self.args.get("hardPodAffinityWeight", 1))
 
     def cluster_active(self) -> bool:
         """Bound pods with required anti-affinity can reject any new pod (symmetry)."""
@@ -151,67 +175,98 @@ class InterPodAffinity(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugi
             return False
         return not self.handle.cache.pods_with_required_anti_affinity()
 
-    def pre_filter(self, state: CycleState, pod) -> Status:
+    def _existing(self):
+        """(pod info, node labels) for every bound/assumed pod."""
         cache = self.handle.cache
-        by_node = {n: [cache.pods[u].info for u in uids if u in cache.pods] for n, uids in cache.node_pods.items()}
-        state.write(self.KEY, _AffinityState(by_node))
+        for node, uids in cache.node_pods.items():
+            labels = _node_labels(self.handle, node)
+            for u in uids:
+                ps = cache.pods.get(u)
+                if ps is not None:
+                    yield ps.info, labels
+
+    def pre_filter(self, state: CycleState, pod) -> Status:
+        st = _AffinityState()
+        aff_terms = [t for t, _ in _terms(pod, "podAffinity", True)]
+        anti_terms = [t for t, _ in _terms(pod, "podAntiAffinity", True)]
+        for o, labels in self._existing():
+            for term, _w in _terms(o, "podAntiAffinity", True):
+                key = term.get("topologyKey", "")
+                if key in labels and _term_matches(term, o.namespace, pod):
+                    st.existing_anti[key].add(labels[key])
+            if aff_terms and all(_term_matches(t, pod.namespace, o) for t in aff_terms):
+                st.any_affinity_match = True
+                for t in aff_terms:
+                    key = t.get("topologyKey", "")
+                    if key in labels:
+                        st.affinity[(key, labels[key])] += 1
+            for t in anti_terms:
+                key = t.get("topologyKey", "")
+                if key in labels and _term_matches(t, pod.namespace, o):
+                    st.anti[(key, labels[key])] += 1
+        st.aff_terms, st.anti_terms = aff_terms, anti_terms
+        state.write(self.KEY, st)
         return Status.ok()
 
-    def _pods_in_domain(self, s: _AffinityState, key: str, value: str):
-        for node, pods in s.by_node.items():
-            if _node_labels(self.handle, node).get(key) == value:
-                yield from pods
-
-    def filter(self, state: CycleState, pod, node_name: str) -> Status:
+    def _state(self, state: CycleState, pod) -> _AffinityState:
         try:
-            s: _AffinityState = state.read(self.KEY)
+            return state.read(self.KEY)
         except KeyError:
             self.pre_filter(state, pod)
-            s = state.read(self.KEY)
+            return state.read(self.KEY)
+
+    def filter(self, state: CycleState, pod, node_name: str) -> Status:
+        st = self._state(state, pod)
         labels = _node_labels(self.handle, node_name)
-        for term, _w in _terms(pod, "podAffinity", True):
-            key = term.get("topologyKey", "")
-            if key not in labels:
-                return Status.unschedulable("node(s) didn't match pod affinity rules", plugin=self.name)
-            if not any(_term_matches(term, pod.namespace, o) for o in self._pods_in_domain(s, key, labels[key])):
-                # upstream: the first pod of a self-affine group may land anywhere in a domain
-                if not (_term_matches(term, pod.namespace, pod) and
-                        not any(_term_matches(term, pod.namespace, o) for ps in s.by_node.values() for o in ps)):
+        for key, values in st.existing_anti.items():
+            if key in labels and labels[key] in values:
+                return Status.unschedulable("node(s) didn't satisfy existing pods anti-affinity rules",
+                                            plugin=self.name)
+        if st.aff_terms:
+            ok = all(k in labels and st.affinity.get((k, labels[k]), 0) > 0
+                     for k in (t.get("topologyKey", "") for t in st.aff_terms))
+            if not ok:
+                # upstream: the first pod of a self-affine group may go to any node that has
+                # the topology keys, when no existing pod matches the terms yet
+                first = (not st.any_affinity_match and all(_term_matches(t, pod.namespace, pod) for t in st.aff_terms)
+                         and all(t.get("topologyKey", "") in labels for t in st.aff_terms))
+                if not first:
                     return Status.unschedulable("node(s) didn't match pod affinity rules", plugin=self.name)
-        for term, _w in _terms(pod, "podAntiAffinity", True):
-            key = term.get("topologyKey", "")
-            if key in labels and any(_term_matches(term, pod.namespace, o)
-                                     for o in self._pods_in_domain(s, key, labels[key])):
+        for t in st.anti_terms:
+            k = t.get("topologyKey", "")
+            if k in labels and st.anti.get((k, labels[k]), 0) > 0:
                 return Status.unschedulable("node(s) didn't match pod anti-affinity rules", plugin=self.name)
-        # symmetry: existing pods' required anti-affinity against the incoming pod
-        for node, pods in s.by_node.items():
-            nl = _node_labels(self.handle, node)
-            for o in pods:
-                for term, _w in _terms(o, "podAntiAffinity", True):
-                    key = term.get("topologyKey", "")
-                    if key in nl and nl.get(key) == labels.get(key) and _term_matches(term, o.namespace, pod):
-                        return Status.unschedulable("node(s) didn't satisfy existing pods anti-affinity rules",
-                                                    plugin=self.name)
         return Status.ok()
 
     def pre_score(self, state: CycleState, pod, nodes: list[str]) -> Status:
-        try:
-            state.read(self.KEY)
-        except KeyError:
-            self.pre_filter(state, pod)
+        st = self._state(state, pod)
+        scores: dict = defaultdict(lambda: defaultdict(int))
+        pref = [(t, w, 1) for t, w in _terms(pod, "podAffinity", False)] + \
+               [(t, w, -1) for t, w in _terms(pod, "podAntiAffinity", False)]
+        for o, labels in self._existing():
+            for t, w, sign in pref:                     # incoming pod's preferred terms
+                key = t.get("topologyKey", "")
+                if key in labels and _term_matches(t, pod.namespace, o):
+                    scores[key][labels[key]] += sign * w
+            if self.hard_weight:                        # existing pods' required affinity
+                for t, _w in _terms(o, "podAffinity", True):
+                    key = t.get("topologyKey", "")
+                    if key in labels and _term_matches(t, o.namespace, pod):
+                        scores[key][labels[key]] += self.hard_weight
+            for kind, sign in (("podAffinity", 1), ("podAntiAffinity", -1)):   # existing preferred
+                for t, w in _terms(o, kind, False):
+                    key = t.get("topologyKey", "")
+                    if key in labels and _term_matches(t, o.namespace, pod):
+                        scores[key][labels[key]] += sign * w
+        st.scores = scores
         return Status.ok()
 
     def score(self, state: CycleState, pod, node_name: str) -> tuple[int, Status]:
-        s: _AffinityState = state.read(self.KEY)
+        st = self._state(state, pod)
+        if st.scores is None:
+            self.pre_score(state, pod, [])
         labels = _node_labels(self.handle, node_name)
-        total = 0
-        for kind, sign in (("podAffinity", 1), ("podAntiAffinity", -1)):
-            for term, w in _terms(pod, kind, False):
-                key = term.get("topologyKey", "")
-                if key in labels:
-                    n = sum(1 for o in self._pods_in_domain(s, key, labels[key]) if _term_matches(term, pod.namespace, o))
-                    total += sign * w * n
-        return total, Status.ok()
+        return sum(by_val.get(labels.get(k), 0) for k, by_val in st.scores.items()), Status.ok()
 
     def normalize_score(self, state: CycleState, pod, scores: list[NodeScore]) -> Status:
         if not scores:
