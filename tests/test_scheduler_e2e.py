@@ -327,3 +327,55 @@ def test_hybrid_python_plugins():
         await c.stop()
         return n
     assert run(go()) == "n4"
+
+
+def test_extended_resources_amd_gpu_device_plugin():
+    """Pods requesting ``amd.com/gpu`` (AMD device plugin) are fitted against node
+    allocatable and what bound/assumed pods already requested; ``ignoredResourceGroups``
+    turns the check off for a resource group."""
+    import asyncio
+
+    from yoda_scheduler_amd.testing import FakeCluster, yoda_config
+
+    def gpu_pod(c, name, n):
+        c.server.create("pods", {"metadata": {"name": name, "namespace": "default", "labels": {}},
+                                 "spec": {"schedulerName": "yoda-scheduler", "containers": [
+                                     {"name": "c", "image": "x", "resources": {"requests": {"amd.com/gpu": str(n)}}}]}})
+
+    def msg(c, name):
+        for cond in (c.pod(name).get("status") or {}).get("conditions") or []:
+            if cond.get("type") == "PodScheduled" and cond.get("status") == "False":
+                return cond.get("message", "")
+        return ""
+
+    async def go(ignore):
+        cfg = yoda_config()
+        if ignore:
+            cfg["profiles"][0]["pluginConfig"].append({"name": "NodeResourcesFit",
+                                                       "args": {"ignoredResourceGroups": ["amd.com"]}})
+        c = FakeCluster(cfg)
+        c.add_node("gpu-node")
+        c.add_node("cpu-node")
+        node = c.server.get("nodes", "gpu-node")
+        c.server.patch("nodes", "gpu-node", {"status": {"allocatable": dict(node["status"]["allocatable"],
+                                                                          **{"amd.com/gpu": "8"})}})
+        await c.start()
+        for i in range(4):
+            gpu_pod(c, f"g{i}", 2)
+        await c.wait_bound(4)
+        gpu_pod(c, "extra", 1)
+        await c.wait(lambda: msg(c, "extra") or c.node_of("extra"), 3.0)
+        first = (sorted({c.node_of(f"g{i}") for i in range(4)}), c.node_of("extra"), msg(c, "extra"))
+        if not ignore:
+            c.server.delete("pods", "g0", "default")
+            await c.wait(lambda: c.node_of("extra"), 5.0)
+        out = first + (c.node_of("extra"),)
+        await c.stop()
+        return out
+
+    nodes, extra_node, extra_msg, later = asyncio.run(go(False))
+    assert nodes == ["gpu-node"] and extra_node == ""
+    assert "Insufficient amd.com/gpu" in extra_msg
+    assert later == "gpu-node"
+    nodes, extra_node, _, _ = asyncio.run(go(True))
+    assert extra_node in ("gpu-node", "cpu-node")

@@ -52,6 +52,7 @@ class SchedulerCache:
         self._anti: set[str] = set()
         self.image_nodes: dict[str, int] = {}    # image → number of nodes holding it (ImageLocality)
         self.avoid_nodes: set[str] = set()       # nodes with a preferAvoidPods annotation
+        self.node_ext_used: dict[str, dict[str, int]] = {}   # node → extended resource → requested
         self.generation = 0
 
     # ------------------------------------------------------------------ nodes
@@ -84,6 +85,7 @@ class SchedulerCache:
     update_node = add_node
 
     def remove_node(self, name: str) -> None:
+        self.node_ext_used.pop(name, None)
         old = self.nodes.pop(name, None)
         if old is not None:
             self._index_node(old, -1)
@@ -133,7 +135,14 @@ class SchedulerCache:
         return flipped
 
     # ------------------------------------------------------------------ pods
+    def _ext(self, ps: PodState, sign: int) -> None:
+        used = self.node_ext_used.setdefault(ps.node, {})
+        for k, v in ps.info.ext.items():
+            used[k] = used.get(k, 0) + sign * v
+
     def _track(self, ps: PodState) -> None:
+        if ps.info.ext:
+            self._ext(ps, +1)
         self.pods[ps.info.uid] = ps
         self.node_pods.setdefault(ps.node, set()).add(ps.info.uid)
         aff = ((ps.info.obj.get("spec") or {}).get("affinity") or {}).get("podAntiAffinity") or {}
@@ -168,6 +177,8 @@ class SchedulerCache:
         ps = self.pods.pop(pi.uid, None)
         if ps is not None:
             self.node_pods.get(ps.node, set()).discard(pi.uid)
+            if ps.info.ext:
+                self._ext(ps, -1)
         self.engine.release(pi.num_id)
 
     def add_pod(self, obj: dict) -> None:
@@ -210,6 +221,8 @@ class SchedulerCache:
         ps = self.pods.pop(uid, None)
         if ps is not None:
             self.node_pods.get(ps.node, set()).discard(uid)
+            if ps.info.ext:
+                self._ext(ps, -1)
             self.engine.release(ps.info.num_id)
 
     def cleanup_expired(self) -> list[PodInfo]:

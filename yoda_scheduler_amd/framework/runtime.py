@@ -65,6 +65,8 @@ class Framework:
             nb = p.native()
             if nb is not None and nb.filter_bit:
                 self.filter_mask |= nb.filter_bit
+                if getattr(p, "python_filter_too", False):
+                    self.filter_py.append(p)      # native half + a conditional Python half
             else:
                 self.filter_py.append(p)
         for p, w in self.points["score"]:

@@ -52,6 +52,44 @@ def _requests(spec: dict) -> tuple[int, int]:
     return cpu, mem
 
 
+_BASIC = ("cpu", "memory")
+
+
+def _has_ext(spec: dict) -> bool:
+    """Cheap pre-check: does any container request something besides cpu/memory?"""
+    for key in ("containers", "initContainers"):
+        for c in spec.get(key) or ():
+            r = (c.get("resources") or _EMPTY).get("requests")
+            if r and any(k not in _BASIC for k in r):
+                return True
+    ov = spec.get("overhead")
+    return bool(ov) and any(k not in _BASIC for k in ov)
+
+
+def ext_requests(spec: dict) -> dict:
+    """Requests other than cpu/memory (``amd.com/gpu``, ``ephemeral-storage``, hugepages,
+    any extended resource) as integer units: max(Σ containers, max init container) +
+    overhead, upstream ``computePodResourceRequest`` semantics. Empty for most pods."""
+    out: dict = {}
+    for c in spec.get("containers") or ():
+        for k, v in (((c.get("resources") or _EMPTY).get("requests")) or _EMPTY).items():
+            if k not in _BASIC:
+                out[k] = out.get(k, 0) + quantity_int(v)
+    for c in spec.get("initContainers") or ():
+        for k, v in (((c.get("resources") or _EMPTY).get("requests")) or _EMPTY).items():
+            if k not in _BASIC:
+                out[k] = max(out.get(k, 0), quantity_int(v))
+    for k, v in (spec.get("overhead") or _EMPTY).items():
+        if k not in _BASIC:
+            out[k] = out.get(k, 0) + quantity_int(v)
+    return {k: v for k, v in out.items() if v}
+
+
+def quantity_int(q) -> int:
+    """Integer value of a quantity (bytes for storage, count for devices), rounded up."""
+    return bytes_of(q)
+
+
 def _terms(terms: list | None) -> list[list[tuple[str, str, list[str]]]]:
     out = []
     for t in terms or []:
@@ -75,12 +113,15 @@ PF_POD_AFFINITY = 4    # podAffinity / podAntiAffinity
 PF_CLAIMS = 8          # persistentVolumeClaim / ephemeral volumes
 PF_DISKS = 16          # in-tree attachable disks (GCE PD, EBS, Azure disk, iSCSI, RBD)
 PF_CONTROLLER = 32     # controlled by a ReplicationController / ReplicaSet
+PF_EXTENDED = 64       # requests resources beyond cpu/memory (amd.com/gpu, ephemeral-storage, ...)
 
 _DISK_KINDS = ("gcePersistentDisk", "awsElasticBlockStore", "azureDisk", "iscsi", "rbd")
 
 
-def pod_flags(meta: dict, spec: dict, host_ports) -> int:
+def pod_flags(meta: dict, spec: dict, host_ports, ext: Optional[dict] = None) -> int:
     f = PF_HOST_PORTS if host_ports else 0
+    if ext:
+        f |= PF_EXTENDED
     if spec.get("topologySpreadConstraints"):
         f |= PF_SPREAD
     aff = spec.get("affinity")
@@ -104,15 +145,17 @@ class PodInfo:
     __slots__ = ("obj", "uid", "namespace", "name", "num_id", "labels", "gpu", "scheduler_name", "node_name",
                  "cpu_m", "mem", "priority", "node_selector", "required_terms", "preferred_terms", "tolerations",
                  "annotations", "host_ports", "attempts", "initial_attempt", "enqueued", "native_req",
-                 "native_owner", "assigned_cards", "_creation", "flags")
+                 "native_owner", "assigned_cards", "_creation", "flags", "ext")
 
     def __init__(self, obj: dict, uid: str, namespace: str, name: str, num_id: int, labels: dict, gpu: GpuRequest,
                  scheduler_name: str = "default-scheduler", node_name: str = "", cpu_m: int = 0, mem: int = 0,
                  priority: int = 0, node_selector: Optional[dict] = None, required_terms: Optional[list] = None,
                  preferred_terms: Optional[list] = None, tolerations: Optional[list] = None,
-                 annotations: Optional[dict] = None, host_ports: Optional[list] = None, flags: int = 0) -> None:
+                 annotations: Optional[dict] = None, host_ports: Optional[list] = None, flags: int = 0,
+                 ext: Optional[dict] = None) -> None:
         self.obj = obj
         self.flags = flags
+        self.ext = ext if ext is not None else _EMPTY
         self.uid = uid
         self.namespace = namespace
         self.name = name
@@ -177,11 +220,12 @@ class PodInfo:
                     (ports := ports or []).append((p.get("hostPort"), p.get("protocol", "TCP"), p.get("hostIP", "")))
         ns = spec.get("nodeSelector")
         ann = meta.get("annotations")
+        ext = ext_requests(spec) if _has_ext(spec) else None
         return cls(obj, uid, meta.get("namespace", "default"), meta.get("name", ""), pod_num_id(uid), labels,
                    parse_gpu_request(labels), spec.get("schedulerName") or "default-scheduler",
                    spec.get("nodeName") or "", cpu, mem, int(spec.get("priority") or 0),
                    dict(ns) if ns else None, req, pref, tols or None, dict(ann) if ann else None, ports,
-                   pod_flags(meta, spec, ports))
+                   pod_flags(meta, spec, ports, ext), ext)
 
 
 _EMPTY: dict = {}
@@ -199,6 +243,7 @@ class NodeInfo:
     mem: int
     pods: int
     images: dict = field(default_factory=dict)       # normalized image name → size bytes
+    ext_alloc: dict = field(default_factory=dict)    # allocatable beyond cpu/memory/pods
     avoid: Optional[str] = None                      # preferAvoidPods annotation (raw JSON)
 
     @classmethod
@@ -212,6 +257,7 @@ class NodeInfo:
                    unschedulable=bool(spec.get("unschedulable", False)),
                    cpu_m=cpu_millis(alloc.get("cpu", "0")), mem=bytes_of(alloc.get("memory", "0")),
                    pods=int(alloc.get("pods", 110)), images=_node_images(obj),
+                   ext_alloc={k: quantity_int(v) for k, v in alloc.items() if k not in ("cpu", "memory", "pods")},
                    avoid=(meta.get("annotations") or _EMPTY).get(ANNOTATION_PREFER_AVOID_PODS))
 
 

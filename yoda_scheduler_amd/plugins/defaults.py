@@ -15,7 +15,7 @@ from typing import Optional
 from ..framework.interfaces import (BindPlugin, CycleState, FilterPlugin, NativeBinding, Plugin,
                                     PostFilterPlugin, PostFilterResult, QueueSortPlugin, ScorePlugin, Status)
 from ..models.labels import ANNOTATION_GPUS, ANNOTATION_RESERVED
-from ..models.pod import PF_HOST_PORTS
+from ..models.pod import PF_EXTENDED, PF_HOST_PORTS
 from ..ops.native import core
 
 
@@ -46,10 +46,38 @@ class NodeName(FilterPlugin):
 
 
 class NodeResourcesFit(FilterPlugin):
+    """cpu / memory / pod count natively; everything else a pod requests (``amd.com/gpu``
+    from the AMD device plugin, ``ephemeral-storage``, hugepages, other extended resources)
+    in Python against the node's allocatable and the cache's per-node usage — only for
+    pods that request such resources (``PF_EXTENDED``). ``ignoredResources`` /
+    ``ignoredResourceGroups`` args as upstream."""
     name = "NodeResourcesFit"
+    python_filter_too = True
+    pod_flags = PF_EXTENDED
+
+    def __init__(self, args: Optional[dict] = None, handle=None) -> None:
+        super().__init__(args, handle)
+        self.ignored = set(self.args.get("ignoredResources") or [])
+        self.ignored_groups = set(self.args.get("ignoredResourceGroups") or [])
 
     def native(self):
         return NativeBinding(filter_bit=_c().F_NODE_RESOURCES_FIT)
+
+    def _checked(self, res: str) -> bool:
+        return res not in self.ignored and res.split("/", 1)[0] not in self.ignored_groups
+
+    def is_noop_for(self, pod) -> bool:
+        return not pod.ext
+
+    def filter(self, state: CycleState, pod, node_name: str) -> Status:
+        cache = self.handle.cache
+        node = cache.nodes.get(node_name)
+        alloc = node.ext_alloc if node is not None else {}
+        used = cache.node_ext_used.get(node_name, {})
+        short = [r for r, v in pod.ext.items() if self._checked(r) and used.get(r, 0) + v > alloc.get(r, 0)]
+        if short:
+            return Status.unschedulable(*(f"Insufficient {r}" for r in sorted(short)), plugin=self.name)
+        return Status.ok()
 
 
 class NodeAffinity(FilterPlugin, ScorePlugin):
