@@ -85,6 +85,8 @@ PYBIND11_MODULE(_yoda_core, m) {
       .def_property("compat", &Engine::compat, &Engine::set_compat)
       .def_property("filters", &Engine::filters, &Engine::set_filters)
       .def("set_score_weight", &Engine::set_score_weight)
+      .def("set_alloc_weights", &Engine::set_alloc_weights, py::arg("most"), py::arg("cpu"), py::arg("mem"),
+           py::arg("other"))
       .def("score_weight", &Engine::score_weight)
       .def("set_gang_weights",
            [](Engine& e, int64_t link, int64_t numa, int64_t fit, int64_t occ, bool binpack, int64_t gang_score,

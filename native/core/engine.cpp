@@ -733,12 +733,18 @@ std::vector<int64_t> Engine::score_nodes(const PodReq& req, const std::vector<in
     for (size_t i = 0; i < F; ++i) {
       const Node& n = nodes_[feas[i]];
       int64_t rc = n.req_cpu_m + nz_cpu, rm = n.req_mem + nz_mem;
-      int64_t least = 0, most = 0;
-      if (n.alloc_cpu_m > 0 && rc <= n.alloc_cpu_m) least += (n.alloc_cpu_m - rc) * 100 / n.alloc_cpu_m;
-      if (n.alloc_mem > 0 && rm <= n.alloc_mem) least += (int64_t)((__int128)(n.alloc_mem - rm) * 100 / n.alloc_mem);
-      if (n.alloc_cpu_m > 0) most += std::min<int64_t>(rc, n.alloc_cpu_m) * 100 / n.alloc_cpu_m;
-      if (n.alloc_mem > 0) most += (int64_t)((__int128)std::min<int64_t>(rm, n.alloc_mem) * 100 / n.alloc_mem);
-      total[i] += score_w_[S_LEAST_ALLOCATED] * (least / 2) + score_w_[S_MOST_ALLOCATED] * (most / 2);
+      int64_t lc = 0, lm = 0, mc = 0, mm = 0;
+      if (n.alloc_cpu_m > 0 && rc <= n.alloc_cpu_m) lc = (n.alloc_cpu_m - rc) * 100 / n.alloc_cpu_m;
+      if (n.alloc_mem > 0 && rm <= n.alloc_mem) lm = (int64_t)((__int128)(n.alloc_mem - rm) * 100 / n.alloc_mem);
+      if (n.alloc_cpu_m > 0) mc = std::min<int64_t>(rc, n.alloc_cpu_m) * 100 / n.alloc_cpu_m;
+      if (n.alloc_mem > 0) mm = (int64_t)((__int128)std::min<int64_t>(rm, n.alloc_mem) * 100 / n.alloc_mem);
+      // upstream resourceAllocationScorer: Σ score_r·w_r / Σ w_r (default cpu=memory=1 → (c+m)/2)
+      const int64_t* wl = alloc_w_[0];
+      const int64_t* wm = alloc_w_[1];
+      const int64_t dl = wl[0] + wl[1] + wl[2], dm = wm[0] + wm[1] + wm[2];
+      const int64_t least = dl > 0 ? (lc * wl[0] + lm * wl[1]) / dl : 0;
+      const int64_t most = dm > 0 ? (mc * wm[0] + mm * wm[1]) / dm : 0;
+      total[i] += score_w_[S_LEAST_ALLOCATED] * least + score_w_[S_MOST_ALLOCATED] * most;
       if (score_w_[S_BALANCED_ALLOCATION]) {
         double cf = n.alloc_cpu_m > 0 ? (double)rc / (double)n.alloc_cpu_m : 1.0;
         double mf = n.alloc_mem > 0 ? (double)rm / (double)n.alloc_mem : 1.0;
@@ -979,6 +985,7 @@ bool Engine::device_eligible(const PodReq& req) const {
   if (wsum * 200 >= ((int64_t)1 << 38)) return false;          // key = (final << 24) | perm
   if (wt_.w_link < 0 || wt_.w_link > 1000000 || wt_.w_numa > 1000000 || wt_.w_fit > 1000000 || wt_.w_occ > 1000000)
     return false;
+  if (!default_alloc_weights()) return false;                    // device computes (c + m) / 2
   return true;
 }
 

@@ -170,6 +170,18 @@ class Engine {
   void set_filters(uint32_t mask) { filters_ = mask; }
   uint32_t filters() const { return filters_; }
   void set_score_weight(int idx, int64_t w) { score_w_[idx] = w; }
+  // Least/MostAllocated `resources` weights (args): cpu, memory, and the summed weight of
+  // resources this engine does not track (they score 0 upstream but count in the divisor)
+  void set_alloc_weights(bool most, int64_t cpu, int64_t mem, int64_t other) {
+    alloc_w_[most ? 1 : 0][0] = cpu;
+    alloc_w_[most ? 1 : 0][1] = mem;
+    alloc_w_[most ? 1 : 0][2] = other;
+  }
+  bool default_alloc_weights() const {
+    for (int k = 0; k < 2; ++k)
+      if (alloc_w_[k][0] != 1 || alloc_w_[k][1] != 1 || alloc_w_[k][2] != 0) return false;
+    return true;
+  }
   int64_t score_weight(int idx) const { return score_w_[idx]; }
   Weights& weights() { return wt_; }
   void set_percentage_of_nodes_to_score(int p) { pct_nodes_ = p; }
@@ -275,6 +287,7 @@ class Engine {
   uint32_t filters_ = F_NODE_UNSCHEDULABLE | F_NODE_NAME | F_TAINT_TOLERATION | F_NODE_AFFINITY |
                       F_NODE_RESOURCES_FIT | F_YODA;
   int64_t score_w_[S_NUM] = {300, 1, 1, 1, 1, 0};
+  int64_t alloc_w_[2][3] = {{1, 1, 0}, {1, 1, 0}};   // [least, most][cpu, memory, other]
   Weights wt_;
   int pct_nodes_ = 0;
   int32_t unsched_key_ = 0;

@@ -165,3 +165,39 @@ def test_registry_with_plugin_out_of_tree():
     assert "OnlyNode1" in r.names()
     with pytest.raises(ValueError):
         r.register("OnlyNode1", lambda a, h: None)
+
+
+def test_least_allocated_resource_weights():
+    """NodeResourcesLeastAllocated ``resources`` weights (upstream resourceAllocationScorer):
+    Σ score_r·w_r / Σ w_r, untracked resources only in the divisor."""
+    from yoda_scheduler_amd.ops.native import core, pod_req
+    from yoda_scheduler_amd.models.pod import PodInfo
+    eng = core().Engine(False, 1)
+    eng.filters = core().F_NODE_RESOURCES_FIT
+    for i in range(6):
+        eng.set_score_weight(i, 0)
+    eng.set_score_weight(core().S_LEAST_ALLOCATED, 1)
+    a = eng.upsert_node("a")
+    b = eng.upsert_node("b")
+    # a: cpu mostly free, memory mostly used; b: the opposite
+    eng.set_node_meta(a, False, [], [], 100_000, 100 << 30, 110)
+    eng.set_node_meta(b, False, [], [], 100_000, 100 << 30, 110)
+
+    def load(idx, uid, cpu, mem):
+        p = PodInfo.from_obj({"metadata": {"name": uid, "uid": uid}, "spec": {"containers": [
+            {"name": "c", "resources": {"requests": {"cpu": cpu, "memory": mem}}}]}})
+        assert eng.reserve(p.num_id, pod_req(eng, p), idx, [])
+    load(a, "load-a", "10", "90Gi")
+    load(b, "load-b", "90", "10Gi")
+    pi = PodInfo.from_obj({"metadata": {"name": "p", "uid": "u-lw"},
+                           "spec": {"containers": [{"name": "c", "resources": {"requests": {"cpu": "1", "memory": "1Gi"}}}]}})
+    req = pod_req(eng, pi)
+    default = eng.score_nodes(req, [a, b])
+    eng.set_alloc_weights(False, 3, 1, 0)          # cpu counts 3×
+    cpu_heavy = eng.score_nodes(req, [a, b])
+    eng.set_alloc_weights(False, 1, 1, 2)          # two untracked resources in the divisor
+    diluted = eng.score_nodes(req, [a, b])
+    # a: cpu (100-11)% free = 89, memory (100-91)% = 9; b mirrored
+    assert default == [49, 49]                      # (89 + 9) / 2
+    assert cpu_heavy == [69, 29]                    # (89·3 + 9) / 4, (9·3 + 89) / 4
+    assert diluted == [24, 24]                      # (89 + 9) / 4

@@ -128,6 +128,9 @@ class Framework:
         engine.filters = self.filter_mask
         for i, w in enumerate(self.score_w):
             engine.set_score_weight(i, w)
+        for most, name in ((False, "NodeResourcesLeastAllocated"), (True, "NodeResourcesMostAllocated")):
+            p = self.plugins.get(name)
+            engine.set_alloc_weights(most, *(p.alloc_weights() if p is not None else (1, 1, 0)))
         if self.yoda is not None:
             self.yoda.configure_engine(engine)
 

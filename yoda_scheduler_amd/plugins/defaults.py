@@ -94,8 +94,20 @@ class TaintToleration(FilterPlugin, ScorePlugin):
         return NativeBinding(filter_bit=_c().F_TAINT_TOLERATION, score_index=_c().S_TAINT_TOLERATION)
 
 
+def _alloc_weights(args: dict) -> tuple[int, int, int]:
+    """``resources: [{name, weight}]`` → (cpu, memory, Σ others); default cpu=memory=1."""
+    res = args.get("resources")
+    if not res:
+        return 1, 1, 0
+    w = {r.get("name", ""): int(r.get("weight", 1)) for r in res}
+    return w.pop("cpu", 0), w.pop("memory", 0), sum(w.values())
+
+
 class NodeResourcesLeastAllocated(ScorePlugin):
     name = "NodeResourcesLeastAllocated"
+
+    def alloc_weights(self) -> tuple[int, int, int]:
+        return _alloc_weights(self.args)
 
     def native(self):
         return NativeBinding(score_index=_c().S_LEAST_ALLOCATED)
@@ -103,6 +115,9 @@ class NodeResourcesLeastAllocated(ScorePlugin):
 
 class NodeResourcesMostAllocated(ScorePlugin):
     name = "NodeResourcesMostAllocated"
+
+    def alloc_weights(self) -> tuple[int, int, int]:
+        return _alloc_weights(self.args)
 
     def native(self):
         return NativeBinding(score_index=_c().S_MOST_ALLOCATED)
