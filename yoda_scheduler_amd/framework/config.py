@@ -83,6 +83,20 @@ class Profile:
 
 
 @dataclass
+class ExtenderConfig:
+    """``extenders[]`` of KubeSchedulerConfiguration (upstream HTTP scheduler extenders)."""
+    url_prefix: str
+    filter_verb: str = ""
+    prioritize_verb: str = ""
+    bind_verb: str = ""
+    weight: int = 1
+    http_timeout: float = 30.0
+    node_cache_capable: bool = False
+    managed_resources: list = field(default_factory=list)   # [(name, ignoredByScheduler)]
+    ignorable: bool = False
+
+
+@dataclass
 class SchedulerConfig:
     api_version: str = SUPPORTED_API_VERSIONS[0]
     leader_election: LeaderElectionConfig = field(default_factory=LeaderElectionConfig)
@@ -107,6 +121,7 @@ class SchedulerConfig:
     device_capacity: int = 65536
     engine_threads: int = 1
     trace: bool = False
+    extenders: list = field(default_factory=list)     # [ExtenderConfig]
 
     def profile(self, name: str) -> Optional[Profile]:
         for p in self.profiles:
@@ -232,6 +247,21 @@ def parse_config(doc: dict) -> SchedulerConfig:
     cfg.device_capacity = int(_f(ds, "capacity", 65536))
     cfg.engine_threads = int(_f(rt, "engineThreads", 1))
     cfg.trace = bool(_f(rt, "trace", False))
+    for e in doc.get("extenders") or []:
+        if not e.get("urlPrefix"):
+            raise ValueError("extender urlPrefix is required")
+        cfg.extenders.append(ExtenderConfig(
+            url_prefix=str(e["urlPrefix"]).rstrip("/"), filter_verb=e.get("filterVerb", ""),
+            prioritize_verb=e.get("prioritizeVerb", ""), bind_verb=e.get("bindVerb", ""),
+            weight=int(e.get("weight", 1)), http_timeout=parse_duration(e.get("httpTimeout", "30s")) or 30.0,
+            node_cache_capable=bool(e.get("nodeCacheCapable", False)),
+            managed_resources=[(r.get("name", ""), bool(r.get("ignoredByScheduler", False)))
+                               for r in e.get("managedResources") or []],
+            ignorable=bool(e.get("ignorable", False))))
+        if cfg.extenders[-1].prioritize_verb and cfg.extenders[-1].weight <= 0:
+            raise ValueError("extender weight must be positive")
+    if sum(1 for e in cfg.extenders if e.bind_verb) > 1:
+        raise ValueError("only one extender can implement bind")
     if not 0 <= cfg.percentage_of_nodes_to_score <= 100:
         raise ValueError("percentageOfNodesToScore must be in [0, 100]")
     if cfg.pod_initial_backoff_seconds <= 0 or cfg.pod_max_backoff_seconds < cfg.pod_initial_backoff_seconds:

@@ -221,13 +221,19 @@ class Framework:
             wait = max(wait, t)
         return Status.ok(), wait
 
-    async def run_bind(self, state: CycleState, pod, node: str) -> Status:
+    async def run_bind(self, state: CycleState, pod, node: str, extender=None) -> Status:
         for p in self.pre_bind:
             if not self._applies(p, pod):
                 continue
             st = await p.pre_bind(state, pod, node)
             if not st.is_success():
                 return st
+        if extender is not None:           # upstream extendersBinding: the extender binds
+            try:
+                await extender.bind(pod, node)
+            except Exception as e:  # noqa: BLE001 - surfaced as a bind failure
+                return Status.error(f"extender bind: {e}")
+            return Status.ok()
         for p in self.bind_plugins:
             st = await p.bind(state, pod, node)
             if st.code.name == "SKIP":

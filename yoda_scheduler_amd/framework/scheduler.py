@@ -126,6 +126,14 @@ class Scheduler:
         self.pending_binds = 0
         self.batching = config.batch_size > 1
         self.tracer = Tracer() if config.trace else None
+        from .extender import HTTPExtender
+        self.extenders = [HTTPExtender(e) for e in config.extenders]
+        # resources an extender manages with ignoredByScheduler are not fitted here (upstream)
+        ignored = {n for e in config.extenders for n, ign in e.managed_resources if ign}
+        for fw in self.frameworks.values():
+            fit = fw.plugins.get("NodeResourcesFit")
+            if ignored and fit is not None and hasattr(fit, "ignored"):
+                fit.ignored |= ignored
         # optional raw samples of scheduler-internal e2e (cycle start → bind acknowledged,
         # queue wait excluded; BASELINE.md protocol item 4) without the Prometheus cost
         self.e2e_samples: Optional[list] = None
@@ -281,6 +289,44 @@ class Scheduler:
                     feasible=res[1], native=fw.native_for(pi))
 
     def _hybrid_cycle(self, fw: Framework, state: CycleState, pi: PodInfo):
+        pre = self._hybrid_filter(fw, state, pi)
+        if pre is None:
+            return None
+        return self._hybrid_finish(fw, state, pi, *pre)
+
+    async def schedule_one_async(self, pi: PodInfo) -> None:
+        """The cycle with HTTP extenders: framework filters, then every interested
+        extender's filter (in config order), then Python + extender priorities on top of
+        the native scores."""
+        from .extender import ExtenderError, run_extenders
+        fw = self.frameworks.get(pi.scheduler_name)
+        if fw is None or self._pod_gone(pi):
+            return
+        self._activate(fw)
+        cycle = self.queue.scheduling_cycle
+        t0 = time.perf_counter()
+        state = CycleState()
+        pre = self._hybrid_filter(fw, state, pi)
+        if pre is None:
+            return
+        req, feas_idx, reasons, failed = pre
+        names = [self.engine.node_name(i) for i in feas_idx]
+        node_objs = {n: self.cache.nodes[n].obj for n in names if n in self.cache.nodes}
+        try:
+            keep, ext_failed, ext_scores = await run_extenders(self.extenders, pi, names, node_objs)
+        except ExtenderError as e:
+            self._fail(fw, state, pi, cycle, f"extender: {e}", t0, unschedulable=False)
+            return
+        self._activate(fw)               # other cycles may have run while awaiting
+        for n, why in ext_failed.items():
+            failed[n] = Status.unschedulable(why or "node(s) rejected by an extender")
+        keep_set = set(keep)
+        feas_idx = [i for i, n in zip(feas_idx, names) if n in keep_set]
+        res = self._hybrid_finish(fw, state, pi, req, feas_idx, reasons, failed, ext_scores)
+        if res is not None:
+            self._finish_cycle(fw, state, pi, res, cycle, t0)
+
+    def _hybrid_filter(self, fw: Framework, state: CycleState, pi: PodInfo):
         st = fw.run_pre_filter(state, pi)
         if not st.is_success():
             self._fail(fw, state, pi, self.queue.scheduling_cycle, f"0/{self.engine.live_nodes} nodes are available: "
@@ -302,11 +348,16 @@ class Scheduler:
         if len(names2) != len(names):
             keep = set(names2)
             feas_idx = [i for i, n in zip(feas_idx, names) if n in keep]
-        extra = fw.run_score_py(state, pi, names2) if (len(names2) > 1 and fw.score_py) else []
+        return req, feas_idx, reasons, failed
+
+    def _hybrid_finish(self, fw: Framework, state: CycleState, pi: PodInfo, req, feas_idx, reasons, failed,
+                       ext_scores: Optional[dict] = None):
         if not feas_idx:
-            py_fail = len(failed)
-            reasons = list(reasons)
-            return (-1, 0, self.engine.live_nodes, [], 0, reasons, 0, failed, py_fail)
+            return (-1, 0, self.engine.live_nodes, [], 0, list(reasons), 0, failed, len(failed))
+        names = [self.engine.node_name(i) for i in feas_idx]
+        extra = fw.run_score_py(state, pi, names) if (len(names) > 1 and fw.score_py) else []
+        if ext_scores:
+            extra = [(extra[k] if extra else 0) + ext_scores.get(n, 0) for k, n in enumerate(names)]
         return self.engine.schedule(pi.num_id, req, True, feas_idx, extra)
 
     def _finish_cycle(self, fw: Framework, state: CycleState, pi: PodInfo, res, cycle: int, t0: float) -> None:
@@ -473,7 +524,7 @@ class Scheduler:
                 await self.limiter.acquire()
                 tb = time.perf_counter()
                 try:
-                    st = await fw.run_bind(state, pi, node)
+                    st = await fw.run_bind(state, pi, node, self._extender_binder(pi))
                 except Exception as e:  # noqa: BLE001
                     st = Status.error(repr(e))
                 m.binding.observe(time.perf_counter() - tb)
@@ -499,6 +550,12 @@ class Scheduler:
                     self.queue.add_unschedulable(pi, cycle, unschedulable=False)
             finally:
                 self.pending_binds -= 1
+
+    def _extender_binder(self, pi: PodInfo):
+        for e in self.extenders:
+            if e.cfg.bind_verb and e.is_interested(pi):
+                return e
+        return None
 
     # ================================================================== loops
     def _export_gpu_metrics(self, max_nodes: int = 2048) -> None:
@@ -539,7 +596,9 @@ class Scheduler:
                 if q.closed:
                     return
                 continue
-            if self.batching and q._active_entries:
+            if self.extenders:
+                await self.schedule_one_async(pi)
+            elif self.batching and q._active_entries:
                 batch = [pi] + q.pop_batch(bs - 1)
                 self.schedule_batch(batch)
             else:
@@ -595,6 +654,8 @@ class Scheduler:
             t.cancel()
         await asyncio.gather(*self._tasks, return_exceptions=True)
         self._tasks.clear()
+        for e in self.extenders:
+            await e.close()
 
     async def drain_binds(self) -> None:
         while self.pending_binds:
