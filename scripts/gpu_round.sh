@@ -25,6 +25,7 @@ for s in $STEPS; do
     bench6on) step bench6_on 600 python bench.py --config 6 --steps 3 --warmup 1 --device on ;;
     bench6off) step bench6_off 600 python bench.py --config 6 --steps 3 --warmup 1 --device off ;;
     benchref) step bench_refqps 600 python bench.py --steps 2 --warmup 0 --reference-qps ;;
+    benchhttp) step bench_http 600 python bench.py --transport http ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
 done

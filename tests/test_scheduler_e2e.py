@@ -379,3 +379,38 @@ def test_extended_resources_amd_gpu_device_plugin():
     assert later == "gpu-node"
     nodes, extra_node, _, _ = asyncio.run(go(True))
     assert extra_node in ("gpu-node", "cpu-node")
+
+
+def test_preemption_reprieves_and_respects_pdbs():
+    """Upstream victim selection: on each node the fewest / lowest-priority victims are
+    kept (reprieve by descending priority); nodes are ranked by PDB violations first, so
+    the pod protected by a PodDisruptionBudget survives; the ledger is untouched for
+    nodes that are not chosen."""
+    async def go():
+        c = FakeCluster()
+        # two single-GPU nodes with 20 GB usable each
+        c.add_node("a", gpus=1, used_mb=[294912 - 20000])
+        c.add_node("b", gpus=1, used_mb=[294912 - 20000])
+        await c.start()
+        # node a: two small low-priority pods (prio 1 and 5); node b: one pod protected by a PDB
+        c.add_pod("a-low1", {"scv/memory": "8000", "app": "batch"}, priority=1, nodeSelector={"kubernetes.io/hostname": "a"})
+        c.add_pod("a-low5", {"scv/memory": "8000", "app": "batch"}, priority=5, nodeSelector={"kubernetes.io/hostname": "a"})
+        c.add_pod("b-prot", {"scv/memory": "16000", "app": "db"}, priority=1, nodeSelector={"kubernetes.io/hostname": "b"})
+        assert await c.wait_bound(3)
+        c.server.create("poddisruptionbudgets", {"metadata": {"name": "db", "namespace": "default"},
+                                                 "spec": {"selector": {"matchLabels": {"app": "db"}}},
+                                                 "status": {"disruptionsAllowed": 0}})
+        await asyncio.sleep(0.05)
+        before_b = [g["reserved"] for g in c.sched.cache.node_gpu_state("b")]
+        # needs 12 GB: on a, evicting a-low1 (8 GB) frees 4+8=12 → enough; a-low5 reprieved
+        c.add_pod("high", {"scv/memory": "12000"}, priority=100)
+        ok = await c.wait(lambda: "default/high" in c.server.bind_log, 5)
+        names = {o["metadata"]["name"] for o in c.server.list("pods")[0]}
+        after_b = [g["reserved"] for g in c.sched.cache.node_gpu_state("b")]
+        node = c.node_of("high")
+        await c.stop()
+        return ok, names, node, before_b, after_b
+    ok, names, node, before_b, after_b = run(go())
+    assert ok and node == "a"
+    assert "a-low1" not in names and "a-low5" in names and "b-prot" in names
+    assert before_b == after_b

@@ -43,6 +43,8 @@ RESOURCES = {
     "persistentvolumes": Resource("persistentvolumes", "", "v1", "PersistentVolume", False),
     "storageclasses": Resource("storageclasses", "storage.k8s.io", "v1", "StorageClass", False),
     "csinodes": Resource("csinodes", "storage.k8s.io", "v1", "CSINode", False),
+    # DefaultPreemption honours PodDisruptionBudgets
+    "poddisruptionbudgets": Resource("poddisruptionbudgets", "policy", "v1", "PodDisruptionBudget", True),
 }
 
 

@@ -187,47 +187,99 @@ class DefaultBinder(BindPlugin):
 
 
 class DefaultPreemption(PostFilterPlugin):
-    """Evict lower-priority pods so a high-priority pod fits (GPU-aware).
+    """Evict lower-priority pods so a high-priority pod fits (GPU-aware), upstream v1.20
+    ``selectVictimsOnNode`` + ``pickOneNodeForPreemption`` semantics on the native ledger:
 
-    For every node that failed for a resolvable reason, remove that node's
-    lower-priority pods lowest-priority first from the native ledger (a what-if), and
-    stop as soon as the engine's filter passes. The node with the fewest victims — then
-    the lowest highest-victim priority — wins; victims are deleted through the API and
-    the preemptor is nominated to the node. The ledger is restored before returning.
+    * per node: take every lower-priority pod off the ledger (a what-if); if the pod still
+      does not fit, the node is no candidate. Otherwise *reprieve* victims, PDB-violating
+      ones first and then by descending priority, re-adding each one that leaves the pod
+      still fitting — what remains are the victims;
+    * candidates are ranked by fewest PodDisruptionBudget violations, lowest highest-victim
+      priority, lowest sum of victim priorities, fewest victims;
+    * a pod whose nominated node still has terminating lower-priority pods waits instead
+      of preempting again (``PodEligibleToPreemptOthers``).
+
+    Victims are deleted through the API and the preemptor is nominated to the node; the
+    ledger is restored exactly before returning.
     """
     name = "DefaultPreemption"
+    watches = ("poddisruptionbudgets",)
+
+    def _pdbs(self) -> list:
+        from ..models.selectors import LabelSelector
+        out = []
+        for o in self.handle.lister("poddisruptionbudgets").values():
+            m = o.get("metadata") or {}
+            allowed = int(((o.get("status") or {}).get("disruptionsAllowed")) or 0)
+            out.append((m.get("namespace", "default"), LabelSelector((o.get("spec") or {}).get("selector") or {}),
+                        allowed))
+        return out
+
+    @staticmethod
+    def _violates(pdbs: list, info, budget: dict) -> bool:
+        """Evicting ``info`` would exceed some PDB's remaining budget (consumes it)."""
+        bad = False
+        for k, (ns, sel, _allowed) in enumerate(pdbs):
+            if ns == info.namespace and sel.matches(info.labels):
+                budget[k] -= 1
+                bad = bad or budget[k] < 0
+        return bad
+
+    def _eligible(self, pod) -> bool:
+        nominated = ((pod.obj.get("status") or {}).get("nominatedNodeName")) or ""
+        if not nominated:
+            return True
+        cache = self.handle.cache
+        for u in cache.node_pods.get(nominated, ()):
+            ps = cache.pods.get(u)
+            if ps is not None and ps.info.priority < pod.priority and \
+                    (ps.info.obj.get("metadata") or {}).get("deletionTimestamp"):
+                return False
+        return True
 
     def post_filter(self, state: CycleState, pod, statuses: dict) -> tuple[Optional[PostFilterResult], Status]:
         h = self.handle
         if pod.priority <= 0 and not self.args.get("preemptZeroPriority", False):
             return None, Status.unschedulable("preemption: pod has no priority", plugin=self.name)
+        if not self._eligible(pod):
+            return None, Status.unschedulable("preemption: victims on the nominated node are still terminating",
+                                              plugin=self.name)
         eng, cache = h.engine, h.cache
         from ..ops.native import pod_req
         req = pod_req(eng, pod)
+        pdbs = self._pdbs()
         best = None
         for node, ps_uids in cache.node_pods.items():
             idx = eng.node_index(node)
             if idx < 0:
                 continue
-            cands = sorted((cache.pods[u] for u in ps_uids if u in cache.pods and cache.pods[u].info.priority < pod.priority),
-                           key=lambda ps: ps.info.priority)
-            if not cands:
+            lower = [cache.pods[u] for u in ps_uids if u in cache.pods and cache.pods[u].info.priority < pod.priority]
+            if not lower:
                 continue
-            removed = []
-            fit = False
-            for ps in cands:
+            for ps in lower:
                 eng.release(ps.info.num_id)
-                removed.append(ps)
-                if eng.filter_node(req, idx) == 0:
-                    fit = True
-                    break
-            # restore the ledger exactly
-            for ps in removed:
+            if eng.filter_node(req, idx) != 0:          # no candidate: put everything back
+                for ps in lower:
+                    eng.reserve(ps.info.num_id, pod_req(eng, ps.info), idx, list(ps.cards))
+                continue
+            victims, violations = [], 0
+            budget = {k: allowed for k, (_ns, _sel, allowed) in enumerate(pdbs)}
+            flagged = [(self._violates(pdbs, ps.info, budget), ps) for ps in lower]
+            # reprieve PDB-violating pods first, then higher priorities first
+            for violating, ps in sorted(flagged, key=lambda t: (not t[0], -t[1].info.priority)):
                 eng.reserve(ps.info.num_id, pod_req(eng, ps.info), idx, list(ps.cards))
-            if fit:
-                key = (len(removed), max(p.info.priority for p in removed))
+                if eng.filter_node(req, idx) != 0:
+                    eng.release(ps.info.num_id)
+                    victims.append(ps)
+                    violations += violating
+            # restore the ledger exactly (victims are still released at this point)
+            for ps in victims:
+                eng.reserve(ps.info.num_id, pod_req(eng, ps.info), idx, list(ps.cards))
+            if victims:
+                prios = [v.info.priority for v in victims]
+                key = (violations, max(prios), sum(prios), len(victims))
                 if best is None or key < best[0]:
-                    best = (key, node, removed)
+                    best = (key, node, victims)
         if best is None:
             return None, Status.unschedulable("preemption: no node can be freed", plugin=self.name)
         _, node, victims = best
