@@ -78,9 +78,17 @@ def main(argv=None) -> int:
     cuda = torch.cuda.is_available()
     if cuda:
         torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
+    backend = None
     if world > 1:
-        dist.init_process_group("nccl" if cuda else "gloo")
-    dev = torch.device("cuda", torch.cuda.current_device()) if cuda else torch.device("cpu")
+        # RCCL ("nccl") with one rank per GPU; YODA_BENCH_BACKEND=gloo rehearses several ranks
+        # sharing one GPU (RCCL refuses two ranks on the same device)
+        backend = os.environ.get("YODA_BENCH_BACKEND") or ("nccl" if cuda else "gloo")
+        if backend == "nccl":
+            dist.init_process_group(backend, device_id=torch.device("cuda", torch.cuda.current_device()))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", torch.cuda.current_device()) if cuda and (world == 1 or backend == "nccl") \
+        else torch.device("cpu")
 
     def sync() -> None:
         if world > 1:
