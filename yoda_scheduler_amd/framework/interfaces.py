@@ -177,7 +177,38 @@ class ReservePlugin(Plugin):
 
 class PermitPlugin(Plugin):
     def permit(self, state: CycleState, pod, node_name: str) -> tuple[Status, float]:
+        """Success, an error/unschedulable status, or ``Status(Code.WAIT)`` with a timeout in
+        seconds: the pod is then held (assumed, not bound) until every waiting plugin calls
+        ``allow`` on its :class:`WaitingPod` or one calls ``reject``, or the timeout hits."""
         return Status.ok(), 0.0
+
+
+class WaitingPod:
+    """A pod whose Permit returned Wait (upstream ``framework.WaitingPod``)."""
+
+    def __init__(self, pod, node: str, plugins: set, timeout: float) -> None:
+        import asyncio
+        self.pod = pod
+        self.node = node
+        self.pending = set(plugins)
+        self.timeout = timeout
+        self._fut = asyncio.get_event_loop().create_future()
+
+    def allow(self, plugin: str) -> None:
+        self.pending.discard(plugin)
+        if not self.pending and not self._fut.done():
+            self._fut.set_result(_OK)
+
+    def reject(self, plugin: str, msg: str = "") -> None:
+        if not self._fut.done():
+            self._fut.set_result(Status(Code.UNSCHEDULABLE, [msg or f"rejected by {plugin}"], plugin))
+
+    async def wait(self) -> "Status":
+        import asyncio
+        try:
+            return await asyncio.wait_for(asyncio.shield(self._fut), self.timeout)
+        except asyncio.TimeoutError:
+            return Status(Code.UNSCHEDULABLE, ["rejected due to timeout after waiting at permit"], "")
 
 
 class PreBindPlugin(Plugin):

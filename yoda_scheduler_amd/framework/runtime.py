@@ -86,11 +86,13 @@ class Framework:
         # Python plugins that are no-ops for most pods (NodePorts without hostPorts,
         # PodTopologySpread without constraints, InterPodAffinity without terms) keep a
         # pod on the native path unless they actually apply to it.
-        py_plugins = self.filter_py + [p for p, _ in self.score_py] + self.pre_filter + self.pre_score + self.reserve
+        py_plugins = (self.filter_py + [p for p, _ in self.score_py] + self.pre_filter + self.pre_score + self.reserve
+                      + self.permit)
         self.conditional = list({id(p): p for p in py_plugins if hasattr(p, "is_noop_for")}.values())
         static = [p for p in py_plugins if not hasattr(p, "is_noop_for")]
         self.reserve_static = [p for p in self.reserve if not hasattr(p, "is_noop_for")]
-        self.fully_native_static = not (static or self.permit)
+        self.fully_native_static = not static
+        self.waiting: dict = {}            # pod uid → WaitingPod
         self.fully_native = self.fully_native_static and not self.conditional
         # one-mask fast path: valid when every conditional plugin declares its pod flags
         # (it is a no-op for pods without them unless its cluster gate is active)
@@ -213,13 +215,39 @@ class Framework:
                 p.unreserve(state, pod, node)
 
     def run_permit(self, state: CycleState, pod, node: str) -> tuple[Status, float]:
-        wait = 0.0
+        """Returns success, a rejection, or WAIT (the pod is registered in ``waiting``;
+        the binding cycle awaits it)."""
+        from .interfaces import Code, WaitingPod
+        wait, waiters = 0.0, set()
         for p in self.permit:
+            if not self._applies(p, pod):
+                continue
             st, t = p.permit(state, pod, node)
-            if not st.is_success() and st.code.name != "WAIT":
+            if st.code == Code.WAIT:
+                waiters.add(p.name)
+                wait = max(wait, t)
+            elif not st.is_success():
+                st.plugin = st.plugin or p.name
                 return st, 0.0
-            wait = max(wait, t)
-        return Status.ok(), wait
+        if waiters:
+            self.waiting[pod.uid] = WaitingPod(pod, node, waiters, wait)
+            return Status(Code.WAIT, [], ""), wait
+        return Status.ok(), 0.0
+
+    def get_waiting_pod(self, uid: str):
+        return self.waiting.get(uid)
+
+    def iterate_waiting_pods(self):
+        return list(self.waiting.values())
+
+    async def wait_on_permit(self, pod) -> Status:
+        wp = self.waiting.get(pod.uid)
+        if wp is None:
+            return Status.ok()
+        try:
+            return await wp.wait()
+        finally:
+            self.waiting.pop(pod.uid, None)
 
     async def run_bind(self, state: CycleState, pod, node: str, extender=None) -> Status:
         for p in self.pre_bind:

@@ -79,6 +79,16 @@ class Handle:
         inf = self._s.informers.get(res)
         return inf.store if inf is not None else {}
 
+    def get_waiting_pod(self, uid: str):
+        for fw in self._s.frameworks.values():
+            wp = fw.get_waiting_pod(uid)
+            if wp is not None:
+                return wp
+        return None
+
+    def iterate_waiting_pods(self):
+        return [wp for fw in self._s.frameworks.values() for wp in fw.iterate_waiting_pods()]
+
     def preempt(self, pod: PodInfo, node: str, victims: list[PodInfo]) -> None:
         self._s._preempt(pod, node, victims)
 
@@ -377,9 +387,11 @@ class Scheduler:
                 self.cache.forget(pi)
                 self._fail(fw, state, pi, cycle, st.message(), t0, unschedulable=False)
                 return
-        if fw.permit:
+        waiting = False
+        if fw.permit and state is not None:
             st, _wait = fw.run_permit(state, pi, node)
-            if not st.is_success():
+            waiting = st.code.name == "WAIT"
+            if not st.is_success() and not waiting:
                 fw.run_unreserve(state, pi, node)
                 self.cache.forget(pi)
                 self._fail(fw, state, pi, cycle, st.message(), t0, unschedulable=st.is_unschedulable())
@@ -389,7 +401,23 @@ class Scheduler:
         if klog.V(3):
             log.info("pod %s → node %s gpus=%s score=%d feasible=%d", pi.key, node, cards, res[4], res[1])
         self.pending_binds += 1
-        self._enqueue_bind((fw, state, pi, node, cycle, t0))
+        if waiting:       # held at Permit: its own task waits, then hands it to the binders
+            asyncio.get_event_loop().create_task(self._permit_then_bind((fw, state, pi, node, cycle, t0)))
+        else:
+            self._enqueue_bind((fw, state, pi, node, cycle, t0))
+
+    async def _permit_then_bind(self, item: tuple) -> None:
+        fw, state, pi, node, cycle, t0 = item
+        st = await fw.wait_on_permit(pi)
+        if st.is_success():
+            self._enqueue_bind(item)
+            return
+        self.pending_binds -= 1
+        fw.run_unreserve(state, pi, node)
+        self.cache.forget(pi)
+        self.failed += 1
+        self.recorder.pod_event(pi, "Warning", "FailedScheduling", st.message())
+        self.queue.add_unschedulable(pi, cycle, unschedulable=True)
 
     def _fit_error(self, res) -> str:
         reasons = res[5]

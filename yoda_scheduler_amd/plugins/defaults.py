@@ -295,6 +295,8 @@ def register_defaults(registry) -> None:
     from .spread_affinity import InterPodAffinity, PodTopologySpread
     registry.register(PodTopologySpread.name, PodTopologySpread)
     registry.register(InterPodAffinity.name, InterPodAffinity)
+    from .coscheduling import Coscheduling
+    registry.register(Coscheduling.name, Coscheduling)
     from .node_extras import ImageLocality, NodePreferAvoidPods
     from .volumes import VOLUME_PLUGINS
     for cls in (ImageLocality, NodePreferAvoidPods, *VOLUME_PLUGINS):
