@@ -414,3 +414,37 @@ def test_preemption_reprieves_and_respects_pdbs():
     assert ok and node == "a"
     assert "a-low1" not in names and "a-low5" in names and "b-prot" in names
     assert before_b == after_b
+
+
+def test_nominated_preemptor_keeps_freed_capacity():
+    """After preemption the preemptor's request is held on the nominated node, so a burst
+    of lower-priority pods arriving while the victim terminates cannot take the space."""
+    async def go():
+        c = FakeCluster()
+        c.add_node("n", gpus=1, used_mb=[294912 - 10000])
+        await c.start()
+        c.add_pod("low", {"scv/memory": "8000"}, priority=1)
+        assert await c.wait_bound(1)
+        # slow victim deletion: intercept the scheduler's delete so the burst lands first
+        real_delete = c.client.delete
+        gate = asyncio.Event()
+
+        async def slow_delete(res, name, namespace=None):
+            await gate.wait()
+            return await real_delete(res, name, namespace)
+        c.client.delete = slow_delete
+        c.add_pod("high", {"scv/memory": "8000"}, priority=100)
+        await c.wait(lambda: c.sched.nominations, 3)
+        nominated = dict(c.sched.nominations)
+        for i in range(5):
+            c.add_pod(f"small{i}", {"scv/memory": "1000"}, priority=0)
+        await asyncio.sleep(0.3)
+        smalls_before = sum(1 for i in range(5) if c.node_of(f"small{i}"))
+        gate.set()
+        ok = await c.wait(lambda: "default/high" in c.server.bind_log, 5)
+        await c.stop()
+        return nominated, smalls_before, ok
+    nominated, smalls_before, ok = run(go())
+    assert list(v[0] for v in nominated.values()) == ["n"]
+    assert smalls_before == 0          # without the hold, 2 of the 1 GB pods would have fit (2 GB free)
+    assert ok

@@ -142,8 +142,9 @@ class FilterPlugin(Plugin):
 
 
 class PostFilterResult:
-    def __init__(self, nominated_node: str = "") -> None:
+    def __init__(self, nominated_node: str = "", cards: Optional[list] = None) -> None:
         self.nominated_node = nominated_node
+        self.cards = cards          # GPUs the preemptor will use there (nominated reservation)
 
 
 class PostFilterPlugin(Plugin):

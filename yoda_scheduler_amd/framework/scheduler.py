@@ -147,6 +147,9 @@ class Scheduler:
         # optional raw samples of scheduler-internal e2e (cycle start → bind acknowledged,
         # queue wait excluded; BASELINE.md protocol item 4) without the Prometheus cost
         self.e2e_samples: Optional[list] = None
+        # preemptors nominated to a node: their request is held there (over the victims
+        # until those are gone) so lower-priority pods cannot take the freed capacity
+        self.nominations: dict[str, tuple[str, int, float]] = {}   # uid → (node, num_id, since)
 
     def _maybe_enable_device(self) -> None:
         """Attach the gfx950 device scorer once the cluster is big enough for it to pay
@@ -187,6 +190,8 @@ class Scheduler:
 
     def on_pod_add(self, obj: dict) -> None:
         if self._assigned(obj):
+            if self.nominations:
+                self._clear_nomination((obj.get("metadata") or {}).get("uid"))
             if not self._terminal(obj):
                 self.cache.add_pod(obj)
         elif self._responsible(obj) and not self._terminal(obj):
@@ -201,6 +206,8 @@ class Scheduler:
                 return
             if not self._assigned(old):
                 self.queue.delete(uid)
+                if uid in self.nominations:
+                    self._clear_nomination(uid)
                 if self.cache.is_assumed(uid):
                     ps = self.cache.pods[uid]
                     self.metrics.pod_scheduling.observe(max(0.0, time.monotonic() - ps.info.initial_attempt))
@@ -217,6 +224,8 @@ class Scheduler:
 
     def on_pod_delete(self, obj: dict) -> None:
         uid = (obj.get("metadata") or {}).get("uid")
+        if uid in self.nominations:
+            self._clear_nomination(uid)
         if self._assigned(obj) or self.cache.is_assumed(uid):
             self.cache.remove_pod(uid)
             self.queue.move_all_to_active_or_backoff("AssignedPodDelete")
@@ -282,6 +291,7 @@ class Scheduler:
         fw = self.frameworks.get(pi.scheduler_name)
         if fw is None or self._pod_gone(pi):
             return
+        self._clear_nominations_for((pi,))       # the preemptor competes with its own hold gone
         self._activate(fw)
         cycle = self.queue.scheduling_cycle
         t0 = time.perf_counter()
@@ -312,6 +322,7 @@ class Scheduler:
         fw = self.frameworks.get(pi.scheduler_name)
         if fw is None or self._pod_gone(pi):
             return
+        self._clear_nominations_for((pi,))
         self._activate(fw)
         cycle = self.queue.scheduling_cycle
         t0 = time.perf_counter()
@@ -454,6 +465,7 @@ class Scheduler:
                     continue
                 if st.is_success() and r is not None and r.nominated_node:
                     nominated = r.nominated_node
+                    self._nominate(pi, nominated, r.cards or [])
                     break
         m.child(m.attempts, "unschedulable" if unschedulable else "error", fw.name).inc()
         m.algorithm.observe(time.perf_counter() - t0)
@@ -473,6 +485,23 @@ class Scheduler:
             await self.client.patch("pods", pi.name, patch, pi.namespace)
         except Exception as e:  # noqa: BLE001 - best effort like upstream
             log.debug("condition update for %s failed: %r", pi.key, e)
+
+    def _nominate(self, pi: PodInfo, node: str, cards: list) -> None:
+        self._clear_nomination(pi.uid)
+        idx = self.engine.node_index(node)
+        if idx >= 0 and self.engine.reserve(pi.num_id, pod_req(self.engine, pi), idx, list(cards)):
+            self.nominations[pi.uid] = (node, pi.num_id, time.monotonic())
+
+    def _clear_nomination(self, uid: str) -> None:
+        nom = self.nominations.pop(uid, None)
+        if nom is not None:
+            self.engine.release(nom[1])
+
+    def _clear_nominations_for(self, pods) -> None:
+        if self.nominations:
+            for p in pods:
+                if p.uid in self.nominations:
+                    self._clear_nomination(p.uid)
 
     def _preempt(self, pod: PodInfo, node: str, victims: list[PodInfo]) -> None:
         self.metrics.preemption_attempts.inc()
@@ -509,6 +538,7 @@ class Scheduler:
             if not run:
                 continue
             self._activate(fw)
+            self._clear_nominations_for(run)
             cycle = self.queue.scheduling_cycle
             t0 = time.perf_counter()
             eng = self.engine
@@ -605,6 +635,10 @@ class Scheduler:
             self.queue.flush_backoff_completed()
             self.queue.flush_unschedulable_leftover()
             self.cache.cleanup_expired()
+            if self.nominations:                 # a nomination never outlives a minute
+                now = time.monotonic()
+                for uid in [u for u, (_n, _i, t) in self.nominations.items() if now - t > 60.0]:
+                    self._clear_nomination(uid)
             self._maybe_enable_device()
             tick += 1
             if tick % 4 == 0 and isinstance(m, SchedulerMetrics):

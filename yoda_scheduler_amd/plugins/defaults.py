@@ -272,6 +272,8 @@ class DefaultPreemption(PostFilterPlugin):
                     eng.release(ps.info.num_id)
                     victims.append(ps)
                     violations += violating
+            # the GPUs the preemptor would take once the victims are gone
+            ok_cards, cards, _q = eng.select_gpus(req, idx)
             # restore the ledger exactly (victims are still released at this point)
             for ps in victims:
                 eng.reserve(ps.info.num_id, pod_req(eng, ps.info), idx, list(ps.cards))
@@ -279,12 +281,12 @@ class DefaultPreemption(PostFilterPlugin):
                 prios = [v.info.priority for v in victims]
                 key = (violations, max(prios), sum(prios), len(victims))
                 if best is None or key < best[0]:
-                    best = (key, node, victims)
+                    best = (key, node, victims, list(cards) if ok_cards else [])
         if best is None:
             return None, Status.unschedulable("preemption: no node can be freed", plugin=self.name)
-        _, node, victims = best
+        _, node, victims, cards = best
         h.preempt(pod, node, [v.info for v in victims])
-        return PostFilterResult(node), Status.ok()
+        return PostFilterResult(node, cards), Status.ok()
 
 
 def register_defaults(registry) -> None:
