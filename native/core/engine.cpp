@@ -844,6 +844,8 @@ CycleResult Engine::schedule(uint64_t pod, const PodReq& req, bool assume, const
 std::vector<CycleResult> Engine::schedule_batch(const std::vector<uint64_t>& pods,
                                                 const std::vector<const PodReq*>& reqs) {
   std::vector<CycleResult> out;
+  if (schedule_batch_device(pods, reqs, &out)) return out;
+  out.clear();
   out.reserve(pods.size());
   static const std::vector<int32_t> none;
   static const std::vector<int64_t> nox;
@@ -880,6 +882,7 @@ bool Engine::enable_device(const std::string& lib_path, int device, int capacity
   fn_schedule_ = dlsym(lib, "yoda_dev_schedule");
   fn_last_us_ = dlsym(lib, "yoda_dev_last_us");
   fn_set_timing_ = dlsym(lib, "yoda_dev_set_timing");
+  fn_schedule_batch_ = dlsym(lib, "yoda_dev_schedule_batch");   // optional
   if (!create || !fn_destroy_ || !fn_upload_ || !fn_schedule_ || !fn_last_us_) {
     if (err) *err = "libyoda_hip.so lacks the yoda_dev_* entry points";
     dlclose(lib);
@@ -996,12 +999,9 @@ Reason Engine::candidate_reason(const PodReq& req, const Node& n) const {
   return RS_OK;
 }
 
-bool Engine::schedule_device(const PodReq& req, CycleResult* r) {
-  if (!flush_dirty()) {
-    ++dev_fallbacks_;
-    return false;
-  }
-  yoda_dev_req_t d{};
+void Engine::make_dev_req(const PodReq& req, yoda_dev_req_t* out) {
+  yoda_dev_req_t& d = *out;
+  d = yoda_dev_req_t{};
   d.number = req.has_number ? req.number : 1;
   d.memory = req.has_memory ? req.memory : 0;
   d.clock = req.has_clock ? req.clock : 0;
@@ -1034,23 +1034,15 @@ bool Engine::schedule_device(const PodReq& req, CycleResult* r) {
   d.perm_mul = mul;
   d.perm_add = add;
   d.perm_inv = inv & 0xFFFFFFu;
-  std::vector<uint8_t> cand;
-  const bool need_cand = ((filters_ & F_NODE_NAME) && req.node_name > 0) ||
-                         ((filters_ & F_NODE_AFFINITY) && (!req.node_selector.empty() || !req.required_terms.empty())) ||
-                         ((filters_ & F_TAINT_TOLERATION) && hard_taint_nodes_ > 0);
-  if (need_cand) {
-    cand.assign(nodes_.size(), 0);
-    for (int32_t i = 0; i < (int32_t)nodes_.size(); ++i)
-      if (nodes_[i].alive) cand[i] = (uint8_t)candidate_reason(req, nodes_[i]);
-    d.use_candidates = 1;
-  }
-  yoda_dev_result_t res{};
-  int rc = ((dev_schedule_t)fn_schedule_)(dev_ctx_, (int)nodes_.size(), &d, need_cand ? cand.data() : nullptr, &res);
-  if (rc != 0) {
-    ++dev_fallbacks_;
-    return false;
-  }
-  ++dev_cycles_;
+}
+
+bool Engine::needs_candidates(const PodReq& req) const {
+  return ((filters_ & F_NODE_NAME) && req.node_name > 0) ||
+         ((filters_ & F_NODE_AFFINITY) && (!req.node_selector.empty() || !req.required_terms.empty())) ||
+         ((filters_ & F_TAINT_TOLERATION) && hard_taint_nodes_ > 0);
+}
+
+void Engine::fill_result(const yoda_dev_result_t& res, CycleResult* r) const {
   r->node = res.node;
   r->feasible = res.feasible;
   r->evaluated = live_;
@@ -1064,6 +1056,70 @@ bool Engine::schedule_device(const PodReq& req, CycleResult* r) {
     for (int c = 0; c < YODA_DEV_CARDS; ++c)
       if ((res.mask >> c) & 1u) r->cards.push_back(c);
     r->gang_quality = res.quality;
+  }
+}
+
+bool Engine::schedule_device(const PodReq& req, CycleResult* r) {
+  if (!flush_dirty()) {
+    ++dev_fallbacks_;
+    return false;
+  }
+  yoda_dev_req_t d;
+  make_dev_req(req, &d);
+  std::vector<uint8_t> cand;
+  const bool need_cand = needs_candidates(req);
+  if (need_cand) {
+    cand.assign(nodes_.size(), 0);
+    for (int32_t i = 0; i < (int32_t)nodes_.size(); ++i)
+      if (nodes_[i].alive) cand[i] = (uint8_t)candidate_reason(req, nodes_[i]);
+    d.use_candidates = 1;
+  }
+  yoda_dev_result_t res{};
+  int rc = ((dev_schedule_t)fn_schedule_)(dev_ctx_, (int)nodes_.size(), &d, need_cand ? cand.data() : nullptr, &res);
+  if (rc != 0) {
+    ++dev_fallbacks_;
+    return false;
+  }
+  ++dev_cycles_;
+  fill_result(res, r);
+  return true;
+}
+
+bool Engine::schedule_batch_device(const std::vector<uint64_t>& pods, const std::vector<const PodReq*>& reqs,
+                                   std::vector<CycleResult>* out) {
+  if (!dev_ctx_ || !fn_schedule_batch_ || live_ < dev_min_nodes_ || pods.size() < 2) return false;
+  for (const PodReq* q : reqs)
+    if (!device_eligible(*q) || needs_candidates(*q) || (q->has_memory && q->memory > UINT32_MAX)) return false;
+  // the device assumes each winner with its reservation counted as pending (Engine::reserve
+  // with is_pending true); that holds for every node whose sample is not from the future
+  const double t = now();
+  for (const Node& n : nodes_)
+    if (n.alive && !(t > n.sample_ts - settle_s_)) return false;
+  if (!flush_dirty()) {
+    ++dev_fallbacks_;
+    return false;
+  }
+  // rng draws happen in make_dev_req, in pod order — the same sequence as per-pod cycles
+  std::vector<yoda_dev_req_t> d(reqs.size());
+  for (size_t i = 0; i < reqs.size(); ++i) make_dev_req(*reqs[i], &d[i]);
+  std::vector<yoda_dev_result_t> res(reqs.size());
+  using batch_t = int (*)(void*, int, int, const yoda_dev_req_t*, yoda_dev_result_t*);
+  const int rc = ((batch_t)fn_schedule_batch_)(dev_ctx_, (int)nodes_.size(), (int)d.size(), d.data(), res.data());
+  if (rc != 0) {
+    // the device table may hold partial in-batch assumptions: re-upload every row
+    ++dev_fallbacks_;
+    for (int32_t i = 0; i < (int32_t)nodes_.size(); ++i) mark_dirty(i);
+    return false;
+  }
+  out->clear();
+  out->reserve(pods.size());
+  for (size_t i = 0; i < pods.size(); ++i) {
+    ++cycles_;
+    ++dev_cycles_;
+    CycleResult r;
+    fill_result(res[i], &r);
+    if (r.node >= 0) reserve(pods[i], *reqs[i], r.node, r.cards);   // marks the row dirty: re-synced next
+    out->push_back(std::move(r));
   }
   return true;
 }

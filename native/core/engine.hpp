@@ -12,6 +12,7 @@
 // yoda_scheduler_amd/plugins/yoda_policy.py for the executable Python spec).
 #pragma once
 
+#include "yoda_dev_abi.h"
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -274,6 +275,11 @@ class Engine {
   bool pack_node(int32_t idx, void* row) const;   // row: yoda_dev_node_t*
   bool flush_dirty();
   bool schedule_device(const PodReq& req, CycleResult* r);
+  bool schedule_batch_device(const std::vector<uint64_t>& pods, const std::vector<const PodReq*>& reqs,
+                             std::vector<CycleResult>* out);
+  void make_dev_req(const PodReq& req, yoda_dev_req_t* out);
+  bool needs_candidates(const PodReq& req) const;
+  void fill_result(const yoda_dev_result_t& res, CycleResult* r) const;
   Reason candidate_reason(const PodReq& req, const Node& n) const;
   bool taints_ok(const PodReq& req, const Node& n) const;
   bool affinity_ok(const PodReq& req, const Node& n) const;
@@ -314,7 +320,8 @@ class Engine {
   void* fn_upload_ = nullptr;
   void* fn_schedule_ = nullptr;
   void* fn_last_us_ = nullptr;
-  void* fn_set_timing_ = nullptr;   // optional entry point
+  void* fn_set_timing_ = nullptr;   // optional entry points
+  void* fn_schedule_batch_ = nullptr;
   double now() const;
   bool is_pending(const Node& n, const Assignment& a) const { return a.t_res > n.sample_ts - settle_s_; }
   int32_t next_start_ = 0;

@@ -50,6 +50,7 @@ constexpr int kGroup = 8;                 // lanes per node
 constexpr int kNodesPerWave = 64 / kGroup;
 constexpr int kPatchRows = 4;             // dirty rows passed by value (4 × 512 B + the filter's args < 4 KiB)
 constexpr int kFuseSelectMax = 2048;      // one block normalises + argmaxes up to this many nodes
+constexpr int kBatchCap = 256;            // pods per batched launch sequence
 constexpr int kShards = 8;
 
 struct Globals {
@@ -348,7 +349,7 @@ __device__ unsigned long long select_block(int n, const yoda_dev_req_t& r, const
 // next pod (the kernel boundary publishes them on the device).
 __device__ void publish(int n, const yoda_dev_req_t& r, unsigned long long key, const uint32_t* __restrict__ mask,
                         const int32_t* __restrict__ quality, Globals* __restrict__ g,
-                        yoda_dev_result_t* __restrict__ out) {
+                        yoda_dev_result_t* __restrict__ out, yoda_dev_node_t* __restrict__ nodes) {
   int nf = 0;
   for (int s = 0; s < kShards; ++s) nf += g->feasible[s];
   yoda_dev_result_t res;
@@ -374,6 +375,21 @@ __device__ void publish(int n, const yoda_dev_req_t& r, unsigned long long key, 
   for (int k = 0; k < 6; ++k) res.maxima[k] = g->maxima[k];
   res.raw_lo = (int64_t)g->raw_lo;
   res.raw_hi = (int64_t)g->raw_hi;
+  // batched cycles (dev_flags bit 1): assume the pod on the device too — the next pod's
+  // filter launch reads the updated row (engine.cpp Engine::reserve, non-compat, with the
+  // host having checked that every reservation counts as pending)
+  if ((r.dev_flags & 2u) && nf > 0) {
+    yoda_dev_node_t* nd = nodes + res.node;
+    const uint32_t mb = (uint32_t)r.memory;
+    for (int c = 0; c < YODA_DEV_CARDS; ++c)
+      if ((res.mask >> c) & 1u) {
+        nd->cards[c].reserved += mb;
+        nd->cards[c].pending += mb;
+      }
+    nd->pod_count += 1;
+    nd->req_cpu += r.cpu_m;
+    nd->req_mem += r.mem;
+  }
   *out = res;
   __hip_atomic_store(&out->feasible, nf, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   globals_reset(g);
@@ -387,7 +403,7 @@ __device__ __forceinline__ bool better(int64_t oa, uint32_t ma, int64_t ob, uint
 }
 
 // ------------------------------------------------------------------ K2: scores + gang search
-__global__ __launch_bounds__(kBlock) void k_score(const yoda_dev_node_t* __restrict__ nodes, int n,
+__global__ __launch_bounds__(kBlock) void k_score(yoda_dev_node_t* __restrict__ nodes, int n,
                                                   const yoda_dev_req_t r, const uint8_t* __restrict__ feas,
                                                   const uint8_t* __restrict__ elig, int64_t* __restrict__ raw,
                                                   int64_t* __restrict__ total_out, uint32_t* __restrict__ mask_out,
@@ -585,14 +601,15 @@ __global__ __launch_bounds__(kBlock) void k_score(const yoda_dev_node_t* __restr
   if (!s_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const unsigned long long best = select_block(n, r, feas, raw, total_out, g, 0, 1);
-  if (threadIdx.x == 0) publish(n, r, best, mask_out, quality_out, g, out);
+  if (threadIdx.x == 0) publish(n, r, best, mask_out, quality_out, g, out, nodes);
 }
 
 // ------------------------------------------------------------------ K3: normalize + argmax + result
 __global__ __launch_bounds__(kBlock) void k_select(int n, const yoda_dev_req_t r, const uint8_t* __restrict__ feas,
                                                    const int64_t* __restrict__ raw, const int64_t* __restrict__ total,
                                                    const uint32_t* __restrict__ mask, const int32_t* __restrict__ quality,
-                                                   Globals* __restrict__ g, yoda_dev_result_t* __restrict__ out) {
+                                                   Globals* __restrict__ g, yoda_dev_result_t* __restrict__ out,
+                                                   yoda_dev_node_t* __restrict__ nodes) {
   __shared__ bool s_last;
   const unsigned long long b = select_block(n, r, feas, raw, total, g, blockIdx.x, gridDim.x);
   if (threadIdx.x == 0) {
@@ -607,7 +624,7 @@ __global__ __launch_bounds__(kBlock) void k_select(int n, const yoda_dev_req_t r
   // last block: every other block's atomicMax has landed
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const unsigned long long key = __hip_atomic_load(&g->best_key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  publish(n, r, key, mask, quality, g, out);
+  publish(n, r, key, mask, quality, g, out, nodes);
 }
 
 struct Ctx {
@@ -621,6 +638,7 @@ struct Ctx {
   uint32_t* d_mask = nullptr;
   int32_t* d_quality = nullptr;
   yoda_dev_result_t *h_res = nullptr, *d_res_map = nullptr;
+  yoda_dev_result_t *h_resb = nullptr, *d_resb = nullptr;   // batched cycles: one slot per pod
   Globals* d_g = nullptr;
   float last_us = 0;
   int grid = 1024;
@@ -706,6 +724,10 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
       hipSuccess)
     return fail("result", e);
   if ((e = hipHostGetDevicePointer((void**)&c->d_res_map, c->h_res, 0)) != hipSuccess) return fail("result map", e);
+  if ((e = hipHostMalloc(&c->h_resb, kBatchCap * sizeof(yoda_dev_result_t),
+                         hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+    return fail("batch results", e);
+  if ((e = hipHostGetDevicePointer((void**)&c->d_resb, c->h_resb, 0)) != hipSuccess) return fail("batch map", e);
   if ((e = hipMalloc(&c->d_g, sizeof(Globals))) != hipSuccess) return fail("globals", e);
   Globals init;
   globals_reset(&init);
@@ -720,7 +742,7 @@ void yoda_dev_destroy(void* p) {
   hipStreamSynchronize(c->stream);
   hipFree(c->d_nodes); hipFree(c->d_stage); hipHostFree(c->h_stage); hipFree(c->d_idx); hipHostFree(c->h_idx);
   hipFree(c->d_feas); hipFree(c->d_elig); hipFree(c->d_cand); hipHostFree(c->h_cand); hipFree(c->d_raw);
-  hipFree(c->d_total); hipFree(c->d_mask); hipFree(c->d_quality); hipHostFree(c->h_res); hipFree(c->d_g);
+  hipFree(c->d_total); hipFree(c->d_mask); hipFree(c->d_quality); hipHostFree(c->h_res); hipHostFree(c->h_resb); hipFree(c->d_g);
   hipEventDestroy(c->e0); hipEventDestroy(c->e1);
   hipStreamDestroy(c->stream);
   delete c;
@@ -768,34 +790,65 @@ int yoda_dev_upload(void* p, int n, const int32_t* idx, const yoda_dev_node_t* r
   return 0;
 }
 
-int yoda_dev_schedule(void* p, int n, const yoda_dev_req_t* req, const uint8_t* cand, yoda_dev_result_t* out) {
-  Ctx* c = (Ctx*)p;
-  if (n <= 0 || n > c->cap) return -1;
-  if (req->use_candidates && !cand) return -3;
-  CK(hipSetDevice(c->device));
-  yoda_dev_req_t r = *req;
-  if (r.use_candidates) {
-    memcpy(c->h_cand, cand, (size_t)n);
-    CK(hipMemcpyAsync(c->d_cand, c->h_cand, (size_t)n, hipMemcpyHostToDevice, c->stream));
-  }
+}  // extern "C"
+
+namespace {
+
+// Enqueue one scheduling cycle (filter → score [→ select]) writing its result to `out`
+// (device view of mapped host memory). `extra_flags` is OR'ed into dev_flags.
+int launch_cycle(Ctx* c, int n, yoda_dev_req_t r, yoda_dev_result_t* out, uint32_t extra_flags) {
   const int per_block = kWaves * kNodesPerWave;
   int grid = (n + per_block - 1) / per_block;
   grid = grid < c->grid ? grid : c->grid;
   int grid_sel = (n + kBlock - 1) / kBlock;
   grid_sel = grid_sel < c->grid ? grid_sel : c->grid;
-  r.dev_flags = (c->direct_atomics < 0 ? grid <= 256 : c->direct_atomics == 1) ? 1u : 0u;
+  r.dev_flags = ((c->direct_atomics < 0 ? grid <= 256 : c->direct_atomics == 1) ? 1u : 0u) | extra_flags;
   const int fuse = n <= kFuseSelectMax;
-  __atomic_store_n(&c->h_res->feasible, -1, __ATOMIC_RELEASE);   // sentinel: overwritten by the device
-  if (c->timing) CK(hipEventRecord(c->e0, c->stream));
   hipLaunchKernelGGL(k_filter, dim3(grid + (c->pend.n > 0 ? 1 : 0)), dim3(kBlock), 0, c->stream, c->pend, c->d_nodes,
                      n, r, c->d_cand, c->d_feas, c->d_elig, c->d_g);
   c->pend.n = 0;
   hipLaunchKernelGGL(k_score, dim3(grid), dim3(kBlock), 0, c->stream, c->d_nodes, n, r, c->d_feas, c->d_elig,
-                     c->d_raw, c->d_total, c->d_mask, c->d_quality, c->d_g, c->d_res_map, fuse);
+                     c->d_raw, c->d_total, c->d_mask, c->d_quality, c->d_g, out, fuse);
   if (!fuse)
     hipLaunchKernelGGL(k_select, dim3(grid_sel), dim3(kBlock), 0, c->stream, n, r, c->d_feas, c->d_raw, c->d_total,
-                       c->d_mask, c->d_quality, c->d_g, c->d_res_map);
+                       c->d_mask, c->d_quality, c->d_g, out, c->d_nodes);
   CK(hipGetLastError());
+  return 0;
+}
+
+// Spin until `slot->feasible` is published (see wait_result).
+int wait_slot(Ctx* c, yoda_dev_result_t* slot) {
+  volatile int32_t* flag = &slot->feasible;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 1;; ++spin) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) >= 0) return 0;
+    if ((spin & 4095) == 0) {
+      const hipError_t q = hipStreamQuery(c->stream);
+      if (q == hipSuccess) return __atomic_load_n(flag, __ATOMIC_ACQUIRE) >= 0 ? 0 : -4;
+      if (q != hipErrorNotReady) return (int)q;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) return -5;
+    }
+    __builtin_ia32_pause();
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int yoda_dev_schedule(void* p, int n, const yoda_dev_req_t* req, const uint8_t* cand, yoda_dev_result_t* out) {
+  Ctx* c = (Ctx*)p;
+  if (n <= 0 || n > c->cap) return -1;
+  if (req->use_candidates && !cand) return -3;
+  CK(hipSetDevice(c->device));
+  if (req->use_candidates) {
+    memcpy(c->h_cand, cand, (size_t)n);
+    CK(hipMemcpyAsync(c->d_cand, c->h_cand, (size_t)n, hipMemcpyHostToDevice, c->stream));
+  }
+  __atomic_store_n(&c->h_res->feasible, -1, __ATOMIC_RELEASE);   // sentinel: overwritten by the device
+  if (c->timing) CK(hipEventRecord(c->e0, c->stream));
+  const int rc = launch_cycle(c, n, *req, c->d_res_map, 0u);
+  if (rc != 0) return rc;
   if (c->timing) {
     CK(hipEventRecord(c->e1, c->stream));
     CK(hipEventSynchronize(c->e1));
@@ -805,6 +858,33 @@ int yoda_dev_schedule(void* p, int n, const yoda_dev_req_t* req, const uint8_t* 
   const int w = wait_result(c);
   if (w != 0) return w;
   memcpy(out, c->h_res, sizeof(*out));
+  return 0;
+}
+
+// B consecutive cycles enqueued back to back: each cycle's winner is assumed on the
+// device (its node row updated in place by the publishing block), so cycle b+1 sees cycle
+// b's reservation exactly as sequential host cycles would — no host round trip between
+// pods. Candidates are not supported here (callers use yoda_dev_schedule for those).
+int yoda_dev_schedule_batch(void* p, int n, int B, const yoda_dev_req_t* reqs, yoda_dev_result_t* out) {
+  Ctx* c = (Ctx*)p;
+  if (n <= 0 || n > c->cap || B < 0) return -1;
+  CK(hipSetDevice(c->device));
+  for (int base = 0; base < B; base += kBatchCap) {
+    const int m = B - base < kBatchCap ? B - base : kBatchCap;
+    for (int j = 0; j < m; ++j) {
+      if (reqs[base + j].use_candidates) return -3;
+      __atomic_store_n(&c->h_resb[j].feasible, -1, __ATOMIC_RELEASE);
+    }
+    for (int j = 0; j < m; ++j) {
+      const int rc = launch_cycle(c, n, reqs[base + j], c->d_resb + j, 2u);
+      if (rc != 0) return rc;
+    }
+    const int w = wait_slot(c, &c->h_resb[m - 1]);
+    if (w != 0) return w;
+    for (int j = 0; j < m; ++j)
+      if (__atomic_load_n(&c->h_resb[j].feasible, __ATOMIC_ACQUIRE) < 0) return -4;
+    memcpy(out + base, c->h_resb, (size_t)m * sizeof(yoda_dev_result_t));
+  }
   return 0;
 }
 

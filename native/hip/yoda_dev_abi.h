@@ -77,6 +77,8 @@ int yoda_dev_upload(void* ctx, int n, const int32_t* idx, const yoda_dev_node_t*
 int yoda_dev_schedule(void* ctx, int n_nodes, const yoda_dev_req_t* req, const uint8_t* candidates,
                       yoda_dev_result_t* out);
 // debug/parity: per-node arrays from the last schedule call
+// B cycles back to back, each winner assumed on the device before the next (no candidates)
+int yoda_dev_schedule_batch(void* ctx, int n_nodes, int B, const yoda_dev_req_t* reqs, yoda_dev_result_t* out);
 int yoda_dev_debug(void* ctx, int n_nodes, uint8_t* feas, int64_t* raw, int64_t* total, uint32_t* mask,
                    int32_t* quality);
 // last kernel time of yoda_dev_schedule in microseconds (device events)

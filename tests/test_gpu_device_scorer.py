@@ -105,3 +105,33 @@ def test_scheduler_auto_enables_device_scorer_and_matches_cpu(require_gpu):
     assert enabled and cycles >= 300 and fallbacks == 0, (enabled, cycles, fallbacks, err)
     assert not enabled_c and cycles_c == 0
     assert placed_d.keys() == placed_c.keys()
+
+
+@pytest.mark.parametrize("n", [600, 4096])
+def test_device_batch_equals_sequential_device_cycles(require_gpu, n):
+    """yoda_dev_schedule_batch (cycles enqueued back to back, winners assumed on the device)
+    gives exactly the results of the same pods scheduled one device cycle at a time, and
+    leaves the same ledger; afterwards the device table still matches the host."""
+    from yoda_scheduler_amd.ops import device_scorer as ds
+    from yoda_scheduler_amd.ops.native import pod_req
+
+    def build():
+        eng = _engine(n, 21)
+        eng.seed(99)
+        return eng
+    a, b = build(), build()
+    rng = random.Random(5)
+    pods = [ds.random_request(a, rng, f"batch-{n}-{k}")[0] for k in range(200)]
+    res_a = a.schedule_batch([p.num_id for p in pods], [pod_req(a, p) for p in pods])
+    res_b = [b.schedule(p.num_id, pod_req(b, p), True) for p in pods]
+    key = lambda r: (r[0], r[1], list(r[3]), r[4], list(r[5]), r[6])   # node, feasible, cards, score, reasons, quality
+    assert [key(r) for r in res_a] == [key(r) for r in res_b]
+    assert sum(1 for r in res_a if r[0] >= 0) > 100
+    assert a.device_cycles >= 200 and a.device_fallbacks == 0
+    for i in range(n):
+        assert a.node_cards(i) == b.node_cards(i)
+    rng2 = random.Random(6)
+    for k in range(10):
+        pi, req = ds.random_request(a, rng2, f"after-{n}-{k}")
+        assert not ds.compare_cycle(a, req)
+        a.schedule(pi.num_id, req, True)
