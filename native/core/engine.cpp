@@ -38,6 +38,10 @@ void ThreadPool::worker() {
       cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
       if (stop_) return;
       seen = gen_;
+      // A worker that wakes after the caller already drained and retired the job must not
+      // join it: the caller may reset next_ for the following job while this worker would
+      // still be looping on the retired (dangling) one.
+      if (job_ == nullptr) continue;
       job = job_;
       n = job_n_;
       grain = job_grain_;
