@@ -22,7 +22,8 @@ import sys
 import time
 from typing import Callable, Optional, Sequence
 
-from ..framework.config import default_config, load_config, parse_duration
+from ..framework.config import apply_policy, default_config, load_config, parse_duration, resolve_policy_configmap
+from ..framework.policy import load_policy_file
 from ..framework.leader import LeaderElector
 from ..framework.registry import Registry, default_registry
 from ..framework.scheduler import Scheduler
@@ -62,6 +63,12 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--fake-apiserver-port", type=int, default=-1, help="dev: expose the fake apiserver over HTTP")
     p.add_argument("--trace", action="store_true", help="record scheduling spans (served at /debug/trace)")
     p.add_argument("--write-config-to", default="", help="print the effective configuration and exit")
+    # deprecated upstream flags for the legacy Policy API (used only without --config)
+    p.add_argument("--policy-config-file", default="", help="legacy Policy file (JSON/YAML)")
+    p.add_argument("--policy-configmap", default="", help="ConfigMap holding a legacy Policy under 'policy.cfg'")
+    p.add_argument("--policy-configmap-namespace", default="kube-system")
+    p.add_argument("--use-legacy-policy-config", type=_bool, default=False,
+                   help="read the Policy from --policy-config-file instead of --policy-configmap")
     return p
 
 
@@ -77,6 +84,11 @@ def new_scheduler_command(*plugins: PluginOption) -> Callable[[Optional[Sequence
         for name, factory in plugins:
             registry.register(name, factory)
         cfg = load_config(args.config) if args.config else default_config(args.scheduler_name or "yoda-scheduler")
+        if not args.config and (args.policy_config_file or args.policy_configmap):
+            if args.policy_config_file and (args.use_legacy_policy_config or not args.policy_configmap):
+                cfg = apply_policy(cfg, load_policy_file(args.policy_config_file))
+            else:
+                cfg.policy_configmap = (args.policy_configmap_namespace, args.policy_configmap)
         le = cfg.leader_election
         if args.leader_elect is not None:
             le.leader_elect = args.leader_elect
@@ -135,6 +147,7 @@ async def _run(args, cfg, registry: Registry) -> int:
     else:
         from ..kube.client import KubeClient, KubeConfig
         client = KubeClient(KubeConfig.load(args.kubeconfig, args.master))
+    cfg = await resolve_policy_configmap(cfg, client)
     sched = Scheduler(client, cfg, registry)
     host, _, port = cfg.metrics_bind_address.rpartition(":")
     port = args.port if args.port is not None else int(port or 10251)

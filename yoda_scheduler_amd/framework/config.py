@@ -122,6 +122,10 @@ class SchedulerConfig:
     engine_threads: int = 1
     trace: bool = False
     extenders: list = field(default_factory=list)     # [ExtenderConfig]
+    # legacy Policy held in a ConfigMap (algorithmSource.policy.configMap / --policy-configmap):
+    # resolved against the apiserver by ``resolve_policy_configmap`` before the scheduler starts
+    policy_configmap: Optional[tuple] = None
+    source_doc: Optional[dict] = None
 
     def profile(self, name: str) -> Optional[Profile]:
         for p in self.profiles:
@@ -208,6 +212,22 @@ def parse_config(doc: dict) -> SchedulerConfig:
         raise ValueError(f"unsupported apiVersion {av!r}")
     if doc.get("kind", "KubeSchedulerConfiguration") != "KubeSchedulerConfiguration":
         raise ValueError("kind must be KubeSchedulerConfiguration")
+    policy_cm = None
+    pol = (doc.get("algorithmSource") or {}).get("policy")
+    if pol:
+        if av != SUPPORTED_API_VERSIONS[0]:
+            raise ValueError("algorithmSource (legacy Policy) is only supported in v1beta1")
+        from . import policy as _policy
+        if (pol.get("file") or {}).get("path"):
+            doc = _policy.apply_to_document(doc, _policy.load_policy_file(pol["file"]["path"]),
+                                            _policy.builtin_plugin_names())
+        elif pol.get("configMap"):
+            cm = pol["configMap"]
+            if not cm.get("name"):
+                raise ValueError("algorithmSource.policy.configMap.name is required")
+            policy_cm = (cm.get("namespace") or "kube-system", cm["name"])
+        else:
+            raise ValueError("algorithmSource.policy needs file.path or configMap")
     le = doc.get("leaderElection") or {}
     cc = doc.get("clientConnection") or {}
     cfg = SchedulerConfig(
@@ -280,7 +300,27 @@ def parse_config(doc: dict) -> SchedulerConfig:
     qs = {tuple(p.name for p in pr.plugins["queueSort"]) for pr in cfg.profiles}
     if len(qs) > 1:
         raise ValueError("all profiles must use the same queueSort plugin")
+    cfg.policy_configmap = policy_cm
+    cfg.source_doc = doc
     return cfg
+
+
+def apply_policy(cfg: SchedulerConfig, policy: dict) -> SchedulerConfig:
+    """Re-parse ``cfg``'s document with a legacy Policy applied to its profile."""
+    from . import policy as _policy
+    doc = dict(cfg.source_doc or {"apiVersion": SUPPORTED_API_VERSIONS[0], "kind": "KubeSchedulerConfiguration"})
+    doc.pop("algorithmSource", None)
+    return parse_config(_policy.apply_to_document(doc, policy, _policy.builtin_plugin_names()))
+
+
+async def resolve_policy_configmap(cfg: SchedulerConfig, client) -> SchedulerConfig:
+    """Fetch a ConfigMap-held Policy (``policy.cfg`` key) and apply it."""
+    if cfg.policy_configmap is None:
+        return cfg
+    from . import policy as _policy
+    ns, name = cfg.policy_configmap
+    cm = await client.get("configmaps", name, ns)
+    return apply_policy(cfg, _policy.policy_from_configmap(cm))
 
 
 def load_config(path: str) -> SchedulerConfig:

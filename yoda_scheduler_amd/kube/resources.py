@@ -45,6 +45,11 @@ RESOURCES = {
     "csinodes": Resource("csinodes", "storage.k8s.io", "v1", "CSINode", False),
     # DefaultPreemption honours PodDisruptionBudgets
     "poddisruptionbudgets": Resource("poddisruptionbudgets", "policy", "v1", "PodDisruptionBudget", True),
+    # SelectorSpread / ServiceAffinity (DefaultSelector: services + the pod's controller)
+    "services": Resource("services", "", "v1", "Service", True),
+    "replicationcontrollers": Resource("replicationcontrollers", "", "v1", "ReplicationController", True),
+    "replicasets": Resource("replicasets", "apps", "v1", "ReplicaSet", True),
+    "statefulsets": Resource("statefulsets", "apps", "v1", "StatefulSet", True),
 }
 
 

@@ -111,14 +111,14 @@ PF_HOST_PORTS = 1
 PF_SPREAD = 2          # topologySpreadConstraints
 PF_POD_AFFINITY = 4    # podAffinity / podAntiAffinity
 PF_CLAIMS = 8          # persistentVolumeClaim / ephemeral volumes
-PF_DISKS = 16          # in-tree attachable disks (GCE PD, EBS, Azure disk, iSCSI, RBD)
-PF_CONTROLLER = 32     # controlled by a ReplicationController / ReplicaSet
+PF_DISKS = 16          # in-tree attachable disks (GCE PD, EBS, Azure disk, Cinder, iSCSI, RBD)
+PF_CONTROLLER = 32     # controlled by a ReplicationController / ReplicaSet / StatefulSet
 PF_EXTENDED = 64       # requests resources beyond cpu/memory (amd.com/gpu, ephemeral-storage, ...)
 PF_POD_GROUP = 128     # member of a co-scheduled pod group (Coscheduling)
 LABEL_POD_GROUP = "pod-group.scheduling.sigs.k8s.io"
 LABEL_POD_GROUP_MIN = "pod-group.scheduling.sigs.k8s.io/min-available"
 
-_DISK_KINDS = ("gcePersistentDisk", "awsElasticBlockStore", "azureDisk", "iscsi", "rbd")
+_DISK_KINDS = ("gcePersistentDisk", "awsElasticBlockStore", "azureDisk", "cinder", "iscsi", "rbd")
 
 
 def pod_flags(meta: dict, spec: dict, host_ports, ext: Optional[dict] = None) -> int:
@@ -138,7 +138,7 @@ def pod_flags(meta: dict, spec: dict, host_ports, ext: Optional[dict] = None) ->
     if LABEL_POD_GROUP in (meta.get("labels") or _EMPTY):
         f |= PF_POD_GROUP
     for r in meta.get("ownerReferences") or ():
-        if r.get("controller") and r.get("kind") in ("ReplicationController", "ReplicaSet"):
+        if r.get("controller") and r.get("kind") in ("ReplicationController", "ReplicaSet", "StatefulSet"):
             f |= PF_CONTROLLER
     return f
 

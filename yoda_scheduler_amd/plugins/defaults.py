@@ -4,9 +4,11 @@ Hot filters/scores are *native*: they declare an engine binding and run inside t
 C++ cycle (``native/core/engine.cpp``). The object-dependent ones — topology spread and
 inter-pod affinity (``spread_affinity.py``), the volume plugins (``volumes.py``),
 ImageLocality and NodePreferAvoidPods (``node_extras.py``) — are Python plugins that are
-no-ops for pods they do not apply to, so those pods stay on the native path. Only
-plugins that v1.20 already dropped from its defaults (``INERT_PLUGINS``: legacy policy
-predicates) are registered as inert so older configs still load.
+no-ops for pods they do not apply to, so those pods stay on the native path. The
+registered-but-not-default v1.20 plugins (NodeLabel, ServiceAffinity, SelectorSpread,
+RequestedToCapacityRatio) live in ``optional.py``, CinderLimits in ``volumes.py``. Only
+``CSILimits`` (a pre-1.17 name of NodeVolumeLimits) is registered as inert so older
+configs still load.
 """
 from __future__ import annotations
 
@@ -164,7 +166,7 @@ def _inert(name: str):
     return type(name, (_Inert,), {"name": name})
 
 
-INERT_PLUGINS = ["NodeLabel", "ServiceAffinity", "SelectorSpread", "CSILimits"]
+INERT_PLUGINS = ["CSILimits"]
 
 
 class DefaultBinder(BindPlugin):
@@ -301,7 +303,8 @@ def register_defaults(registry) -> None:
     registry.register(Coscheduling.name, Coscheduling)
     from .node_extras import ImageLocality, NodePreferAvoidPods
     from .volumes import VOLUME_PLUGINS
-    for cls in (ImageLocality, NodePreferAvoidPods, *VOLUME_PLUGINS):
+    from .optional import OPTIONAL_PLUGINS
+    for cls in (ImageLocality, NodePreferAvoidPods, *VOLUME_PLUGINS, *OPTIONAL_PLUGINS):
         registry.register(cls.name, cls)
     for n in INERT_PLUGINS:
         registry.register(n, _inert(n))

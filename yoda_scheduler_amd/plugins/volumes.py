@@ -487,5 +487,11 @@ class AzureDiskLimits(_InTreeLimits):
     kind, id_field, alloc_key, default_max = "azureDisk", "diskName", "attachable-volumes-azure-disk", 16
 
 
+class CinderLimits(_InTreeLimits):
+    """Not in the v1.20 default profile; enabled by configs that name it."""
+    name = "CinderLimits"
+    kind, id_field, alloc_key, default_max = "cinder", "volumeID", "attachable-volumes-cinder", 256
+
+
 VOLUME_PLUGINS = (VolumeRestrictions, VolumeZone, VolumeBinding, NodeVolumeLimits, EBSLimits, GCEPDLimits,
-                  AzureDiskLimits)
+                  AzureDiskLimits, CinderLimits)
