@@ -173,13 +173,14 @@ PYBIND11_MODULE(_yoda_core, m) {
       .def("node_usage",
            [](Engine& e, int32_t idx) {
              const Node& n = e.node(idx);
-             return py::make_tuple(n.req_cpu_m, n.req_mem, n.pod_count, n.label_mem_sum);
+             return py::make_tuple(n.req_cpu_m, n.req_mem, n.pod_count, n.label_mem_sum, n.nz_cpu_m, n.nz_mem);
            })
       .def("make_req",
            [](Engine& e, bool has_number, uint64_t number, bool has_memory, uint64_t memory, bool has_clock,
               uint64_t clock, uint64_t clock_min, int64_t priority, const std::string& node_name, int64_t cpu_m,
               int64_t mem, const std::vector<std::pair<std::string, std::string>>& node_selector,
-              const py::list& required, const py::list& preferred, const py::list& tolerations) {
+              const py::list& required, const py::list& preferred, const py::list& tolerations,
+              int64_t nz_cpu_m, int64_t nz_mem) {
              PodReq r;
              r.has_number = has_number;
              r.number = has_number ? number : 1;
@@ -192,6 +193,9 @@ PYBIND11_MODULE(_yoda_core, m) {
              r.node_name = node_name.empty() ? -1 : e.intern(node_name);
              r.cpu_m = cpu_m;
              r.mem = mem;
+             // -1: derive at pod level (one container); PodInfo passes per-container values
+             r.nz_cpu_m = nz_cpu_m >= 0 ? nz_cpu_m : (cpu_m > 0 ? cpu_m : 100);
+             r.nz_mem = nz_mem >= 0 ? nz_mem : (mem > 0 ? mem : 200LL * 1024 * 1024);
              for (auto& kv : node_selector) r.node_selector.emplace_back(e.intern(kv.first), e.intern(kv.second));
              for (auto t : required) r.required_terms.push_back(make_term(e, t.cast<py::list>()));
              for (auto p : preferred) {
@@ -214,7 +218,8 @@ PYBIND11_MODULE(_yoda_core, m) {
            py::arg("clock"), py::arg("clock_min") = 0, py::arg("priority") = 0, py::arg("node_name") = "",
            py::arg("cpu_m") = 0, py::arg("mem") = 0,
            py::arg("node_selector") = std::vector<std::pair<std::string, std::string>>{},
-           py::arg("required") = py::list(), py::arg("preferred") = py::list(), py::arg("tolerations") = py::list())
+           py::arg("required") = py::list(), py::arg("preferred") = py::list(), py::arg("tolerations") = py::list(),
+           py::arg("nz_cpu_m") = -1, py::arg("nz_mem") = -1)
       .def("reserve", &Engine::reserve)
       .def("release", &Engine::release)
       .def("has_pod", &Engine::has_pod)

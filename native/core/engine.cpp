@@ -260,10 +260,14 @@ bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::ve
   n.pods.push_back(pod);
   a.cpu_m = req.cpu_m;
   a.mem = req.mem;
+  a.nz_cpu_m = req.nz_cpu_m;
+  a.nz_mem = req.nz_mem;
   a.has_label_mem = req.has_memory;
   a.label_mem = req.memory;
   n.req_cpu_m += a.cpu_m;
   n.req_mem += a.mem;
+  n.nz_cpu_m += a.nz_cpu_m;
+  n.nz_mem += a.nz_mem;
   n.pod_count += 1;
   if (a.has_label_mem) n.label_mem_sum += a.label_mem;
   ledger_.emplace(pod, std::move(a));
@@ -295,6 +299,8 @@ bool Engine::release(uint64_t pod) {
     }
     n.req_cpu_m -= a.cpu_m;
     n.req_mem -= a.mem;
+    n.nz_cpu_m -= a.nz_cpu_m;
+    n.nz_mem -= a.nz_mem;
     n.pod_count -= 1;
     if (a.has_label_mem) n.label_mem_sum -= a.label_mem;
     mark_dirty(a.node);
@@ -731,12 +737,12 @@ std::vector<int64_t> Engine::score_nodes(const PodReq& req, const std::vector<in
     normalize_yoda(s);
     for (size_t i = 0; i < F; ++i) total[i] += s[i] * score_w_[S_YODA];
   }
-  const int64_t nz_cpu = req.cpu_m > 0 ? req.cpu_m : 100;               // upstream non-zero defaults
-  const int64_t nz_mem = req.mem > 0 ? req.mem : 200LL * 1024 * 1024;
+  // upstream resourceAllocationScorer: node NonZeroRequested + the pod's non-zero request
+  const int64_t nz_cpu = req.nz_cpu_m, nz_mem = req.nz_mem;
   if (score_w_[S_LEAST_ALLOCATED] || score_w_[S_MOST_ALLOCATED] || score_w_[S_BALANCED_ALLOCATION]) {
     for (size_t i = 0; i < F; ++i) {
       const Node& n = nodes_[feas[i]];
-      int64_t rc = n.req_cpu_m + nz_cpu, rm = n.req_mem + nz_mem;
+      int64_t rc = n.nz_cpu_m + nz_cpu, rm = n.nz_mem + nz_mem;
       int64_t lc = 0, lm = 0, mc = 0, mm = 0;
       if (n.alloc_cpu_m > 0 && rc <= n.alloc_cpu_m) lc = (n.alloc_cpu_m - rc) * 100 / n.alloc_cpu_m;
       if (n.alloc_mem > 0 && rm <= n.alloc_mem) lm = (int64_t)((__int128)(n.alloc_mem - rm) * 100 / n.alloc_mem);
@@ -940,6 +946,8 @@ bool Engine::pack_node(int32_t idx, void* out) const {
   row->alloc_pods = n.alloc_pods;
   row->req_cpu = n.req_cpu_m;
   row->req_mem = n.req_mem;
+  row->nz_cpu = n.nz_cpu_m;
+  row->nz_mem = n.nz_mem;
   row->pod_count = n.pod_count;
   if (n.alloc_mem > (int64_t)1 << 56 || n.alloc_cpu_m > (int64_t)1 << 56) return false;
   for (size_t c = 0; c < n.cards.size(); ++c) {
@@ -1012,6 +1020,8 @@ void Engine::make_dev_req(const PodReq& req, yoda_dev_req_t* out) {
   d.clock_min = req.clock_min;
   d.cpu_m = req.cpu_m;
   d.mem = req.mem;
+  d.nz_cpu_m = req.nz_cpu_m;
+  d.nz_mem = req.nz_mem;
   d.has_number = req.has_number;
   d.has_memory = req.has_memory;
   d.has_clock = req.has_clock;

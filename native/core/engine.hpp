@@ -90,6 +90,7 @@ struct Node {
   std::vector<Taint> taints;
   int64_t alloc_cpu_m = 0, alloc_mem = 0, alloc_pods = 0;
   int64_t req_cpu_m = 0, req_mem = 0, pod_count = 0;
+  int64_t nz_cpu_m = 0, nz_mem = 0;     // Σ non-zero requests (upstream NodeInfo.NonZeroRequested)
   uint64_t label_mem_sum = 0;         // Σ scv/memory labels of pods on node (compat Allocate)
   bool hard_taint = false, prefer_taint = false;   // has NoSchedule/NoExecute, PreferNoSchedule taints
   double sample_ts = 0;               // unix time of the Scv sample the cards came from
@@ -104,6 +105,7 @@ struct PodReq {
   // k8s spec
   int32_t node_name = -1;                // interned spec.nodeName, -1 = none
   int64_t cpu_m = 0, mem = 0;
+  int64_t nz_cpu_m = 100, nz_mem = 200LL * 1024 * 1024;   // per-container non-zero defaults applied
   std::vector<std::pair<int32_t, int32_t>> node_selector;
   std::vector<SelTerm> required_terms;   // ORed
   std::vector<PrefTerm> preferred_terms;
@@ -123,6 +125,7 @@ struct Assignment {
   std::vector<int32_t> cards;
   uint64_t mb = 0;              // per card
   int64_t cpu_m = 0, mem = 0;
+  int64_t nz_cpu_m = 0, nz_mem = 0;
   uint64_t label_mem = 0;
   bool has_label_mem = false;
   double t_res = 0;             // unix time of the reservation

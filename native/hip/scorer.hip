@@ -389,6 +389,8 @@ __device__ void publish(int n, const yoda_dev_req_t& r, unsigned long long key, 
     nd->pod_count += 1;
     nd->req_cpu += r.cpu_m;
     nd->req_mem += r.mem;
+    nd->nz_cpu += r.nz_cpu_m;
+    nd->nz_mem += r.nz_mem;
   }
   *out = res;
   __hip_atomic_store(&out->feasible, nf, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -425,8 +427,7 @@ __global__ __launch_bounds__(kBlock) void k_score(yoda_dev_node_t* __restrict__ 
   const bool search = yoda_f && k >= 1 && k <= YODA_DEV_CARDS;
   const int32_t P = k * (k - 1) / 2;
   const int s_begin = search ? c_subsets.start[k] : 0, s_end = search ? c_subsets.start[k + 1] : 0;
-  const int64_t nz_cpu = r.cpu_m > 0 ? r.cpu_m : 100;
-  const int64_t nz_mem = r.mem > 0 ? r.mem : 200LL * 1024 * 1024;
+  const int64_t nz_cpu = r.nz_cpu_m, nz_mem = r.nz_mem;
   unsigned long long lo = ULLONG_MAX, hi = 0;
   const int stride = gridDim.x * kWaves * kNodesPerWave;
   for (int base = uniform((blockIdx.x * kWaves + wave) * kNodesPerWave); base < n; base += stride) {
@@ -549,7 +550,7 @@ __global__ __launch_bounds__(kBlock) void k_score(yoda_dev_node_t* __restrict__ 
         hi = us > hi ? us : hi;
       }
       // upstream default scores (engine.cpp Engine::score_nodes)
-      const int64_t rc = nd->req_cpu + nz_cpu, rm = nd->req_mem + nz_mem;
+      const int64_t rc = nd->nz_cpu + nz_cpu, rm = nd->nz_mem + nz_mem;
       const int64_t ac = nd->alloc_cpu, am = nd->alloc_mem;
       int64_t least = 0, most = 0, extra = r.w_const;
       if (ac > 0 && rc <= ac) least += (int64_t)udiv((uint64_t)(ac - rc) * 100, (uint64_t)ac);

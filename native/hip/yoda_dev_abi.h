@@ -37,15 +37,20 @@ typedef struct {
   int64_t req_cpu, req_mem, pod_count;       // 24
   uint32_t card_number;                      // 4  (Scv.Status.CardNumber)
   uint8_t ncards, nphys, flags, pad0;        // 4
-  uint8_t pad[32];
+  int64_t nz_cpu, nz_mem;                    // 16 Σ non-zero requests (scores)
+  uint8_t pad[16];
 } yoda_dev_node_t;   // 512 B
+#ifdef __cplusplus
+static_assert(sizeof(yoda_dev_node_t) == 512, "node record must stay 512 B");
+#endif
 
 typedef struct {
   uint64_t number;        // effective GPU count (1 when the label is absent)
   uint64_t memory;        // MB per GPU (0 when absent)
   uint64_t clock;         // exact-match clock (0 when absent)
   uint64_t clock_min;
-  int64_t cpu_m, mem;     // pod requests
+  int64_t cpu_m, mem;     // pod requests (fit)
+  int64_t nz_cpu_m, nz_mem;   // pod non-zero requests (Least/Most/Balanced scores)
   int64_t w_yoda, w_least, w_balanced, w_most, w_const;   // score weights; w_const added to every node
   int64_t w_link, w_numa, w_fit, w_occ, w_gang_score;
   uint32_t has_number, has_memory, has_clock, binpack;

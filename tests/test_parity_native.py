@@ -187,3 +187,36 @@ def test_ledger_reserve_release_roundtrip():
     for pi in pis:
         assert e.release(pi.num_id)
     assert e.node_cards(0) == before and e.ledger_size == 0
+
+
+def test_nonzero_requests_feed_allocation_scores():
+    """upstream NonZeroRequested: an absent cpu/memory request counts as 100m / 200 MiB
+    per container for Least/Most/Balanced scoring (an explicit 0 stays 0), while the
+    resource fit uses the plain requests."""
+    from yoda_scheduler_amd.models.pod import PodInfo, _requests
+    mi = 1024 * 1024
+    assert _requests({"containers": [{}, {}]}) == (0, 0, 200, 400 * mi)
+    assert _requests({"containers": [{"resources": {"requests": {"cpu": "0", "memory": "1Gi"}}}]}) == \
+        (0, 1024 * mi, 0, 1024 * mi)
+    assert _requests({"containers": [{}], "initContainers": [{"resources": {"requests": {"cpu": "2"}}}]}) == \
+        (2000, 0, 2000, 200 * mi)
+    assert _requests({"containers": [{}], "overhead": {"cpu": "50m"}}) == (50, 0, 150, 200 * mi)
+    c = core()
+    eng = c.Engine(False, 1)
+    for name in ("busy", "idle"):
+        idx = eng.upsert_node(name)
+        eng.set_node_meta(idx, False, [], [], 4000, 8 << 30, 110)
+    eng.filters = 0
+    for i in range(6):
+        eng.set_score_weight(i, 0)
+    eng.set_score_weight(c.S_LEAST_ALLOCATED, 1)
+    plain = PodInfo.from_obj({"metadata": {"name": "p", "uid": "u-p"}, "spec": {"containers": [{}]}})
+    assert (plain.cpu_m, plain.mem, plain.nz_cpu_m, plain.nz_mem) == (0, 0, 100, 200 * mi)
+    busy = eng.node_index("busy")
+    for i in range(10):      # ten request-less pods: 1000m / 2000 MiB non-zero on "busy"
+        pi = PodInfo.from_obj({"metadata": {"name": f"b{i}", "uid": f"u-b{i}"}, "spec": {"containers": [{}]}})
+        assert eng.reserve(pi.num_id, pod_req(eng, pi), busy, [])
+    assert eng.node_usage(busy)[:2] == (0, 0) and eng.node_usage(busy)[4:6] == (1000, 2000 * mi)
+    s = eng.score_nodes(pod_req(eng, plain), [busy, eng.node_index("idle")])
+    # busy: cpu (4000−1100)/4000 → 72, mem (8192−2200)/8192 → 73 → 72; idle: 97, 97 → 97
+    assert s == [72, 97]

@@ -164,7 +164,7 @@ def test_broken_linear_function():
 
 
 def test_requested_to_capacity_ratio_score():
-    engine = SimpleNamespace(node_index=lambda n: 0, node_usage=lambda i: (2000, 4 << 30, 0, 0))
+    engine = SimpleNamespace(node_index=lambda n: 0, node_usage=lambda i: (0, 0, 3, 0, 2000, 4 << 30))
     node = SimpleNamespace(labels={}, cpu_m=8000, mem=16 << 30, ext_alloc={"amd.com/gpu": 8})
     cache = SimpleNamespace(nodes={"n": node}, engine=engine, node_ext_used={"n": {"amd.com/gpu": 2}})
     h = SimpleNamespace(cache=cache)
@@ -173,7 +173,7 @@ def test_requested_to_capacity_ratio_score():
                                    "resources": [{"name": "cpu", "weight": 2}, {"name": "memory", "weight": 1},
                                                  {"name": "amd.com/gpu", "weight": 3}]}, h)
     p = pod("p")
-    p.cpu_m, p.mem, p.ext = 2000, 0, {"amd.com/gpu": 2}
+    p.nz_cpu_m, p.nz_mem, p.ext = 2000, 200 * 1024 * 1024, {"amd.com/gpu": 2}
     # cpu (2000+2000)/8000 = 50 → 50; memory (4Gi+200Mi)/16Gi → util 100 − (16Gi−4.2Gi)·100//16Gi = 27 → 27;
     # gpu 4/8 = 50 → 50;  (50·2 + 27·1 + 50·3)/6 = 277/6 = 46.17 → 46
     assert pl.score(CycleState(), p, "n")[0] == 46

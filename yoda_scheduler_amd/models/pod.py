@@ -36,20 +36,45 @@ def pod_key(obj: dict) -> str:
     return f"{m.get('namespace', 'default')}/{m.get('name', '')}"
 
 
-def _requests(spec: dict) -> tuple[int, int]:
-    cpu = mem = 0
-    for c in spec.get("containers") or []:
-        r = ((c.get("resources") or {}).get("requests")) or {}
-        cpu += cpu_millis(r.get("cpu")) if "cpu" in r else 0
-        mem += bytes_of(r.get("memory")) if "memory" in r else 0
-    for c in spec.get("initContainers") or []:
-        r = ((c.get("resources") or {}).get("requests")) or {}
-        cpu = max(cpu, cpu_millis(r.get("cpu")) if "cpu" in r else 0)
-        mem = max(mem, bytes_of(r.get("memory")) if "memory" in r else 0)
-    ov = spec.get("overhead") or {}
-    cpu += cpu_millis(ov["cpu"]) if "cpu" in ov else 0
-    mem += bytes_of(ov["memory"]) if "memory" in ov else 0
-    return cpu, mem
+DEFAULT_MILLI_CPU_REQUEST = 100                 # upstream schedutil non-zero defaults
+DEFAULT_MEMORY_REQUEST = 200 * 1024 * 1024
+
+
+def _requests(spec: dict) -> tuple[int, int, int, int]:
+    """(cpu_m, mem, non-zero cpu_m, non-zero mem): Σ containers, max with each init
+    container, + overhead. The non-zero pair substitutes upstream's defaults (100m,
+    200 MiB) per container whose request is *absent* (``GetNonzeroRequests``); it feeds
+    the Least/Most/Balanced allocation scores, the plain pair the resource fit."""
+    cpu = mem = nzc = nzm = 0
+    for c in spec.get("containers") or ():
+        r = ((c.get("resources") or _EMPTY).get("requests")) or _EMPTY
+        if "cpu" in r:
+            v = cpu_millis(r["cpu"])
+            cpu += v
+            nzc += v
+        else:
+            nzc += DEFAULT_MILLI_CPU_REQUEST
+        if "memory" in r:
+            v = bytes_of(r["memory"])
+            mem += v
+            nzm += v
+        else:
+            nzm += DEFAULT_MEMORY_REQUEST
+    for c in spec.get("initContainers") or ():
+        r = ((c.get("resources") or _EMPTY).get("requests")) or _EMPTY
+        v = cpu_millis(r["cpu"]) if "cpu" in r else 0
+        cpu, nzc = max(cpu, v), max(nzc, v if "cpu" in r else DEFAULT_MILLI_CPU_REQUEST)
+        v = bytes_of(r["memory"]) if "memory" in r else 0
+        mem, nzm = max(mem, v), max(nzm, v if "memory" in r else DEFAULT_MEMORY_REQUEST)
+    ov = spec.get("overhead")
+    if ov:
+        v = cpu_millis(ov["cpu"]) if "cpu" in ov else 0
+        cpu += v
+        nzc += v
+        v = bytes_of(ov["memory"]) if "memory" in ov else 0
+        mem += v
+        nzm += v
+    return cpu, mem, nzc, nzm
 
 
 _BASIC = ("cpu", "memory")
@@ -150,15 +175,18 @@ class PodInfo:
     __slots__ = ("obj", "uid", "namespace", "name", "num_id", "labels", "gpu", "scheduler_name", "node_name",
                  "cpu_m", "mem", "priority", "node_selector", "required_terms", "preferred_terms", "tolerations",
                  "annotations", "host_ports", "attempts", "initial_attempt", "enqueued", "native_req",
-                 "native_owner", "assigned_cards", "_creation", "flags", "ext")
+                 "native_owner", "assigned_cards", "_creation", "flags", "ext", "nz_cpu_m", "nz_mem")
 
     def __init__(self, obj: dict, uid: str, namespace: str, name: str, num_id: int, labels: dict, gpu: GpuRequest,
                  scheduler_name: str = "default-scheduler", node_name: str = "", cpu_m: int = 0, mem: int = 0,
                  priority: int = 0, node_selector: Optional[dict] = None, required_terms: Optional[list] = None,
                  preferred_terms: Optional[list] = None, tolerations: Optional[list] = None,
                  annotations: Optional[dict] = None, host_ports: Optional[list] = None, flags: int = 0,
-                 ext: Optional[dict] = None) -> None:
+                 ext: Optional[dict] = None, nz_cpu_m: int = -1, nz_mem: int = -1) -> None:
         self.obj = obj
+        # -1: a single container's non-zero request derived from cpu_m / mem
+        self.nz_cpu_m = nz_cpu_m if nz_cpu_m >= 0 else (cpu_m or DEFAULT_MILLI_CPU_REQUEST)
+        self.nz_mem = nz_mem if nz_mem >= 0 else (mem or DEFAULT_MEMORY_REQUEST)
         self.flags = flags
         self.ext = ext if ext is not None else _EMPTY
         self.uid = uid
@@ -206,7 +234,7 @@ class PodInfo:
         spec = obj.get("spec") or _EMPTY
         labels = meta.get("labels") or {}
         uid = meta.get("uid") or pod_key(obj)
-        cpu, mem = _requests(spec)
+        cpu, mem, nzc, nzm = _requests(spec)
         aff = spec.get("affinity")
         req = pref = None
         if aff:
@@ -230,7 +258,7 @@ class PodInfo:
                    parse_gpu_request(labels), spec.get("schedulerName") or "default-scheduler",
                    spec.get("nodeName") or "", cpu, mem, int(spec.get("priority") or 0),
                    dict(ns) if ns else None, req, pref, tols or None, dict(ann) if ann else None, ports,
-                   pod_flags(meta, spec, ports, ext), ext)
+                   pod_flags(meta, spec, ports, ext), ext, nzc, nzm)
 
 
 _EMPTY: dict = {}

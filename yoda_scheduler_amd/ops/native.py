@@ -95,6 +95,6 @@ def pod_req(engine, pi: PodInfo):
     r = engine.make_req(g.has_number, g.number, g.has_memory, g.memory, g.has_clock, g.clock,
                         g.clock_min, g.priority, pi.node_name, pi.cpu_m, pi.mem,
                         list(pi.node_selector.items()), pi.required_terms, pi.preferred_terms,
-                        pi.tolerations)
+                        pi.tolerations, pi.nz_cpu_m, pi.nz_mem)
     pi.native_req, pi.native_owner = r, engine
     return r

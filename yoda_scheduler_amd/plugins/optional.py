@@ -26,8 +26,6 @@ from ..models.selectors import LabelSelector
 LABEL_ZONE = ("failure-domain.beta.kubernetes.io/zone", "topology.kubernetes.io/zone")
 LABEL_REGION = ("failure-domain.beta.kubernetes.io/region", "topology.kubernetes.io/region")
 ZONE_WEIGHTING = 2.0 / 3.0
-DEFAULT_CPU_M = 100                    # upstream non-zero request defaults
-DEFAULT_MEM = 200 * 1024 * 1024
 
 
 def _node_labels(handle, node: str) -> dict:
@@ -358,7 +356,7 @@ def broken_linear(shape: list[tuple[int, int]]):
 
 class RequestedToCapacityRatio(ScorePlugin):
     """score = Σ_r w_r·shape(utilization_r) / Σ_r w_r over resources with a non-zero shape
-    value, utilization = requested (incl. this pod, non-zero defaults for cpu/memory) ÷
+    value, utilization = requested (incl. this pod; cpu/memory as NonZeroRequested) ÷
     allocatable in percent; ``shape`` scores 0–10 are scaled to 0–100."""
     name = "RequestedToCapacityRatio"
 
@@ -400,9 +398,8 @@ class RequestedToCapacityRatio(ScorePlugin):
         if node is None:
             return {}
         idx = cache.engine.node_index(node_name)
-        req_cpu, req_mem = cache.engine.node_usage(idx)[:2] if idx >= 0 else (0, 0)
-        out = {"cpu": (req_cpu + (pod.cpu_m or DEFAULT_CPU_M), node.cpu_m),
-               "memory": (req_mem + (pod.mem or DEFAULT_MEM), node.mem)}
+        nz_cpu, nz_mem = cache.engine.node_usage(idx)[4:6] if idx >= 0 else (0, 0)
+        out = {"cpu": (nz_cpu + pod.nz_cpu_m, node.cpu_m), "memory": (nz_mem + pod.nz_mem, node.mem)}
         used = cache.node_ext_used.get(node_name, {})
         for r, _w in self.weights:
             if r not in out:
