@@ -150,6 +150,42 @@ def test_leader_election_single_leader_and_failover():
     assert run(go())
 
 
+@pytest.mark.parametrize("lock", ["endpoints", "configmaps", "endpointsleases"])
+def test_leader_election_legacy_and_multi_locks(lock):
+    """client-go EndpointsLock / ConfigMapLock (record in the leader annotation) and the
+    endpointsleases multilock (legacy primary + Lease kept in step)."""
+    from yoda_scheduler_amd.fakeapi.client import InProcessClient
+    from yoda_scheduler_amd.framework.leader import LEADER_ANNOTATION, LeaderElector
+
+    async def go():
+        srv = FakeApiServer()
+        cl = InProcessClient(srv)
+        kw = dict(lease_duration=0.6, renew_deadline=0.4, retry_period=0.1, resource_lock=lock)
+        a = LeaderElector(cl, identity="a", **kw)
+        b = LeaderElector(cl, identity="b", **kw)
+        await a.acquire()
+        tb = asyncio.get_event_loop().create_task(b.acquire())
+        await asyncio.sleep(0.5)
+        assert a.is_leader and not tb.done()
+        a._task.cancel()
+        await asyncio.wait_for(tb, 3)
+        res = "configmaps" if lock == "configmaps" else "endpoints"
+        rec = json.loads(srv.get(res, "yoda-scheduler", "kube-system")["metadata"]["annotations"][LEADER_ANNOTATION])
+        lease = srv.get("leases", "yoda-scheduler", "kube-system") if lock.endswith("leases") else None
+        await b.release()
+        return rec, lease
+    rec, lease = run(go())
+    assert rec["holderIdentity"] == "b" and rec["leaderTransitions"] == 1
+    if lock.endswith("leases"):
+        assert lease["spec"]["holderIdentity"] == "b"
+
+
+def test_unknown_lock_type_rejected():
+    from yoda_scheduler_amd.framework.leader import LeaderElector
+    with pytest.raises(ValueError):
+        LeaderElector(object(), resource_lock="etcd")
+
+
 def test_leader_loses_lease_when_apiserver_unreachable():
     from yoda_scheduler_amd.framework.leader import LeaderElector
 
@@ -248,7 +284,8 @@ def test_cli_fake_cluster_serves_health_and_schedules():
                     await asyncio.sleep(0.05)
             await cl.create("pods", {"metadata": {"name": "cli", "namespace": "default",
                                                   "labels": {"scv/memory": "1000"}},
-                                     "spec": {"schedulerName": "yoda-scheduler"}})
+                                     "spec": {"schedulerName": "yoda-scheduler", "priority": 7, "containers": [
+                                         {"name": "c", "resources": {"requests": {"cpu": "250m"}}}]}})
             for _ in range(200):
                 pod = await cl.get("pods", "cli", "default")
                 if pod["spec"].get("nodeName"):
@@ -268,23 +305,36 @@ def test_cli_fake_cluster_serves_health_and_schedules():
                     heap = await r.json()
                 async with s.get(f"http://127.0.0.1:{status_port}/configz") as r:
                     configz = await r.json()
-            return pod, health, metrics, (prof, stacks, heap, configz)
+                async with s.get(f"http://127.0.0.1:{status_port}/metrics/resources") as r:
+                    resources = await r.text()
+                async with s.get(f"http://127.0.0.1:{status_port}/debug/cache") as r:
+                    cache = await r.json()
+                proc.send_signal(__import__("signal").SIGUSR2)      # cache comparer + dump to the log
+                await asyncio.sleep(0.3)
+            return pod, health, metrics, (prof, stacks, heap, configz, resources, cache)
         finally:
             await cl.close()
 
     try:
-        pod, health, metrics, (prof, stacks, heap, configz) = run(go())
+        pod, health, metrics, (prof, stacks, heap, configz, resources, cache) = run(go())
     finally:
         proc.terminate()
         try:
-            proc.wait(10)
+            out, _ = proc.communicate(timeout=10)
         except subprocess.TimeoutExpired:
             proc.kill()
+            out = ""
     assert pod["spec"]["nodeName"].startswith("mi355x-")
     assert health == "ok"
     assert "scheduler_schedule_attempts_total" in metrics
     assert "function calls" in prof and "asyncio task(s)" in stacks and heap["objects"] > 0
     assert "componentconfig" in configz
+    node = pod["spec"]["nodeName"]
+    assert (f'kube_pod_resource_request{{namespace="default",node="{node}",pod="cli",priority="7",resource="cpu",'
+            f'scheduler="yoda-scheduler",unit="cores"}} 0.25') in resources
+    assert all(not v for section in cache["comparison"].values() for v in section.values()), cache["comparison"]
+    assert cache["dump"]["nodes"][node]["pods"] == ["default/cli"]
+    assert "cache comparer: cache matches the informers" in out
 
 
 def test_tracer_chrome_trace():

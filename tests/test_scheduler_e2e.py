@@ -244,6 +244,22 @@ def test_preemption_evicts_lower_priority():
     assert ok and not low_exists
 
 
+def test_preemption_policy_never_does_not_evict():
+    async def go():
+        c = FakeCluster()
+        c.add_node("n", gpus=1, used_mb=[294912 - 10000])
+        await c.start()
+        c.add_pod("low", {"scv/memory": "8000"}, priority=1)
+        assert await c.wait_bound(1)
+        c.add_pod("high", {"scv/memory": "8000"}, priority=100, preemptionPolicy="Never")
+        await asyncio.sleep(0.3)
+        bound = "default/high" in c.server.bind_log
+        c.pod("low")                     # still there: no victim was deleted
+        await c.stop()
+        return bound
+    assert run(go()) is False
+
+
 def test_restart_rebuilds_ledger_from_annotations():
     async def go():
         c = FakeCluster()
@@ -448,3 +464,29 @@ def test_nominated_preemptor_keeps_freed_capacity():
     assert list(v[0] for v in nominated.values()) == ["n"]
     assert smalls_before == 0          # without the hold, 2 of the 1 GB pods would have fit (2 GB free)
     assert ok
+
+
+def test_cache_debugger_detects_drift():
+    """Upstream cache debugger: no drift after a normal burst; a pod dropped from the cache
+    and a node missing from it are reported."""
+    async def go():
+        c = FakeCluster()
+        c.add_node("n0")
+        c.add_node("n1")
+        await c.start()
+        for i in range(6):
+            c.add_pod(f"p{i}", {"scv/memory": "1000"})
+        assert await c.wait_bound(6)
+        await asyncio.sleep(0.05)
+        clean = c.sched.debugger.drift()
+        uid = c.pod("p0")["metadata"]["uid"]
+        c.sched.cache.remove_pod(uid)                  # simulate a lost informer event
+        c.sched.cache.nodes.pop("n1")
+        drift = c.sched.debugger.drift()
+        dump = c.sched.debugger.dump()
+        await c.stop()
+        return clean, drift, uid, dump
+    clean, drift, uid, dump = run(go())
+    assert clean == {}
+    assert drift["pods"]["missed"] == [uid] and drift["nodes"]["missed"] == ["n1"]
+    assert set(dump["queue"]) == {"active", "backoff", "unschedulable"}

@@ -28,6 +28,7 @@ from ..framework.leader import LeaderElector
 from ..framework.registry import Registry, default_registry
 from ..framework.scheduler import Scheduler
 from ..utils import klog
+from ..utils.metrics import pod_resource_metrics
 from ..utils.serving import StatusServer
 
 log = logging.getLogger("yoda.cmd")
@@ -56,6 +57,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--bind-address", default="0.0.0.0")
     p.add_argument("--port", "--secure-port", dest="port", type=int, default=None,
                    help="health/metrics port (default from config, 10251)")
+    p.add_argument("--tls-cert-file", default="", help="serve health/metrics over HTTPS with this certificate")
+    p.add_argument("--tls-private-key-file", default="")
     p.add_argument("--kube-api-qps", type=float, default=None)
     p.add_argument("--kube-api-burst", type=int, default=None)
     p.add_argument("--device-scorer", choices=["auto", "on", "off"], default=None)
@@ -126,6 +129,16 @@ def new_scheduler_command(*plugins: PluginOption) -> Callable[[Optional[Sequence
     return main
 
 
+def _ssl_context(args):
+    """Secure serving (upstream serves :10259 over TLS): enabled by --tls-cert-file."""
+    if not args.tls_cert_file:
+        return None
+    import ssl
+    ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+    ctx.load_cert_chain(args.tls_cert_file, args.tls_private_key_file or None)
+    return ctx
+
+
 async def _run(args, cfg, registry: Registry) -> int:
     fake_http = None
     if args.fake_cluster:
@@ -159,7 +172,10 @@ async def _run(args, cfg, registry: Registry) -> int:
                                          "device_cycles": sched.engine.device_cycles,
                                          "device_error": sched.device_error},
                           trace=lambda: sched.tracer.chrome_trace() if sched.tracer else {},
-                          profiling=cfg.enable_profiling)
+                          profiling=cfg.enable_profiling,
+                          resources=lambda: pod_resource_metrics(
+                              sched.informers["pods"].store.values() if "pods" in sched.informers else ()),
+                          cache=sched.debugger.report, ssl_context=_ssl_context(args))
     try:
         log.info("serving /healthz and /metrics on port %d", await status.start())
     except OSError as e:
@@ -168,8 +184,10 @@ async def _run(args, cfg, registry: Registry) -> int:
     le = cfg.leader_election
     if le.leader_elect:
         elector = LeaderElector(client, le.resource_name, le.resource_namespace, lease_duration=le.lease_duration,
-                                renew_deadline=le.renew_deadline, retry_period=le.retry_period)
+                                renew_deadline=le.renew_deadline, retry_period=le.retry_period,
+                                resource_lock=le.resource_lock)
     loop = asyncio.get_event_loop()
+    sched.debugger.install(loop)          # SIGUSR2: cache comparer + dump (upstream debugger)
     stop = asyncio.Event()
     for sig in (signal.SIGINT, signal.SIGTERM):
         try:

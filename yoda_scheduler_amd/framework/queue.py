@@ -39,6 +39,8 @@ class SchedulingQueue:
         self.scheduling_cycle = 0
         self._move_request_cycle = -1
         self.closed = False
+        # (event, queue, n) → scheduler_queue_incoming_pods_total; None = not counted
+        self.incoming_hook: Optional[Callable[[str, str, int], None]] = None
 
     # ------------------------------------------------------------------ helpers
     def _event(self) -> asyncio.Event:
@@ -159,8 +161,12 @@ class SchedulingQueue:
         pi.enqueued = self.clock()          # backoff counts from the failed attempt
         if not unschedulable or self._move_request_cycle >= cycle:
             self._to_backoff(pi)
+            where = "backoff"
         else:
             self._unsched[pi.uid] = (pi, self.clock())
+            where = "unschedulable"
+        if self.incoming_hook is not None:
+            self.incoming_hook("ScheduleAttemptFailure", where, 1)
 
     def _to_backoff(self, pi: PodInfo) -> None:
         t = self.clock() + self.backoff_duration(pi)
@@ -189,21 +195,29 @@ class SchedulingQueue:
             self._route(pi)
         return len(old)
 
-    def _route(self, pi: PodInfo) -> None:
+    def _route(self, pi: PodInfo) -> bool:
+        """Backoff if the pod's backoff has not expired yet, else active; True = active."""
         if self.clock() - pi.enqueued < self.backoff_duration(pi):
             self._to_backoff(pi)
-        else:
-            self._push_active(pi)
+            return False
+        self._push_active(pi)
+        return True
 
     def move_all_to_active_or_backoff(self, event: str = "") -> int:
         """A cluster event (node add, Scv update, pod delete...) may make parked pods
         schedulable."""
         pods = [pi for pi, _ in self._unsched.values()]
         self._unsched.clear()
+        active = 0
         for pi in pods:
             self._pods.pop(pi.uid, None)
-            self._route(pi)
+            active += self._route(pi)
         self._move_request_cycle = self.scheduling_cycle
+        if pods and self.incoming_hook is not None:
+            if active:
+                self.incoming_hook(event, "active", active)
+            if len(pods) > active:
+                self.incoming_hook(event, "backoff", len(pods) - active)
         return len(pods)
 
     def close(self) -> None:

@@ -150,6 +150,11 @@ class Scheduler:
         # preemptors nominated to a node: their request is held there (over the victims
         # until those are gone) so lower-priority pods cannot take the freed capacity
         self.nominations: dict[str, tuple[str, int, float]] = {}   # uid → (node, num_id, since)
+        from .debugger import CacheDebugger
+        self.debugger = CacheDebugger(self)
+        if isinstance(self.metrics, SchedulerMetrics):
+            m = self.metrics
+            self.queue.incoming_hook = lambda ev, q, n: m.child(m.incoming, ev, q).inc(n)
 
     def _maybe_enable_device(self) -> None:
         """Attach the gfx950 device scorer once the cluster is big enough for it to pay
@@ -196,6 +201,7 @@ class Scheduler:
                 self.cache.add_pod(obj)
         elif self._responsible(obj) and not self._terminal(obj):
             self.queue.add(PodInfo.from_obj(obj))
+            self.metrics.child(self.metrics.incoming, "PodAdd", "active").inc()
 
     def on_pod_update(self, old: dict, new: dict) -> None:
         if self._assigned(new):
@@ -419,7 +425,10 @@ class Scheduler:
 
     async def _permit_then_bind(self, item: tuple) -> None:
         fw, state, pi, node, cycle, t0 = item
+        tw = time.perf_counter()
         st = await fw.wait_on_permit(pi)
+        self.metrics.child(self.metrics.permit_wait, "Success" if st.is_success() else "Unschedulable").observe(
+            time.perf_counter() - tw)
         if st.is_success():
             self._enqueue_bind(item)
             return
@@ -648,6 +657,10 @@ class Scheduler:
                 self.queue.move_all_to_active_or_backoff("ScvStale")
             for q, n in self.queue.pending().items():
                 m.child(m.pending, q).set(n)
+            counts = self.cache.snapshot_counts()
+            m.child(m.cache_size, "nodes").set(counts["nodes"])
+            m.child(m.cache_size, "pods").set(counts["pods"])
+            m.child(m.cache_size, "assumed_pods").set(counts["assumed"])
 
     async def scheduling_loop(self) -> None:
         q = self.queue

@@ -38,6 +38,7 @@ RESOURCES = {
     "leases": Resource("leases", "coordination.k8s.io", "v1", "Lease", True),
     "scvs": Resource("scvs", "core.run-linux.com", "v1", "Scv", False),
     "configmaps": Resource("configmaps", "", "v1", "ConfigMap", True),
+    "endpoints": Resource("endpoints", "", "v1", "Endpoints", True),      # legacy leader-election lock
     # volume plugins (VolumeBinding / VolumeZone / NodeVolumeLimits)
     "persistentvolumeclaims": Resource("persistentvolumeclaims", "", "v1", "PersistentVolumeClaim", True),
     "persistentvolumes": Resource("persistentvolumes", "", "v1", "PersistentVolume", False),

@@ -228,6 +228,8 @@ class DefaultPreemption(PostFilterPlugin):
         return bad
 
     def _eligible(self, pod) -> bool:
+        if (pod.obj.get("spec") or {}).get("preemptionPolicy") == "Never":
+            return False
         nominated = ((pod.obj.get("status") or {}).get("nominatedNodeName")) or ""
         if not nominated:
             return True
@@ -244,8 +246,8 @@ class DefaultPreemption(PostFilterPlugin):
         if pod.priority <= 0 and not self.args.get("preemptZeroPriority", False):
             return None, Status.unschedulable("preemption: pod has no priority", plugin=self.name)
         if not self._eligible(pod):
-            return None, Status.unschedulable("preemption: victims on the nominated node are still terminating",
-                                              plugin=self.name)
+            return None, Status.unschedulable("preemption: pod is not eligible (preemptionPolicy Never, or victims"
+                                              " on its nominated node are still terminating)", plugin=self.name)
         eng, cache = h.engine, h.cache
         from ..ops.native import pod_req
         req = pod_req(eng, pod)

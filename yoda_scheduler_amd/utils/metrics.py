@@ -42,6 +42,13 @@ class SchedulerMetrics:
                                   registry=r)
         self.gpu_free = Gauge("yoda_gpu_free_mb", "Sniffed free HBM per GPU", ["node", "gpu"], registry=r)
         self.scv_stale = Gauge("yoda_scv_stale", "1 if the node's Scv sample is stale", ["node"], registry=r)
+        self.incoming = Counter("scheduler_queue_incoming_pods_total",
+                                "Number of pods added to scheduling queues by event and queue type",
+                                ["event", "queue"], registry=r)
+        self.cache_size = Gauge("scheduler_scheduler_cache_size", "Number of nodes, pods, and assumed (bound) pods "
+                                "in the scheduler cache", ["type"], registry=r)
+        self.permit_wait = Histogram("scheduler_permit_wait_duration_seconds", "Duration of waiting on permit",
+                                     ["result"], buckets=_BUCKETS, registry=r)
         self.batch_size = Histogram("yoda_native_batch_size", "Pods per native scheduling batch",
                                     buckets=(1, 2, 4, 8, 16, 32, 64, 128, 256, 512), registry=r)
         self._children: dict = {}
@@ -55,6 +62,59 @@ class SchedulerMetrics:
 
     def render(self) -> bytes:
         return generate_latest(self.registry)
+
+
+def _fmt_labels(d: dict) -> str:
+    esc = lambda v: str(v).replace("\\", "\\\\").replace('"', '\\"').replace("\n", "\\n")   # noqa: E731
+    return ",".join(f'{k}="{esc(v)}"' for k, v in sorted(d.items()))
+
+
+def _res_value(res: str, qty) -> tuple[float, str]:
+    from .quantity import bytes_of, cpu_millis, parse_quantity
+    if res == "cpu":
+        return cpu_millis(qty) / 1000.0, "cores"
+    if res in ("memory", "ephemeral-storage") or res.startswith("hugepages-"):
+        return float(bytes_of(qty)), "bytes"
+    return float(parse_quantity(qty)), ""
+
+
+def pod_resource_metrics(pods) -> bytes:
+    """``/metrics/resources`` (upstream v1.20 ``kube_pod_resource_request`` /
+    ``kube_pod_resource_limit``): the effective request/limit of every non-terminal pod —
+    Σ containers, max with each init container, + overhead — labelled with namespace, pod,
+    node (empty while pending), scheduler, priority, resource and unit."""
+    out = ["# HELP kube_pod_resource_request Resources requested by workloads on the cluster, broken down by pod.",
+           "# TYPE kube_pod_resource_request gauge",
+           "# HELP kube_pod_resource_limit Resources limit for workloads on the cluster, broken down by pod.",
+           "# TYPE kube_pod_resource_limit gauge"]
+    for o in pods:
+        spec, meta = o.get("spec") or {}, o.get("metadata") or {}
+        if (o.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
+            continue
+        base = {"namespace": meta.get("namespace", "default"), "pod": meta.get("name", ""),
+                "node": spec.get("nodeName") or "", "scheduler": spec.get("schedulerName") or "default-scheduler",
+                "priority": str(spec["priority"]) if spec.get("priority") is not None else ""}
+        for kind, metric in (("requests", "kube_pod_resource_request"), ("limits", "kube_pod_resource_limit")):
+            tot: dict = {}
+            for c in spec.get("containers") or ():
+                for r, q in (((c.get("resources") or {}).get(kind)) or {}).items():
+                    v, unit = _res_value(r, q)
+                    tot[r] = (tot.get(r, (0.0, unit))[0] + v, unit)
+            for c in spec.get("initContainers") or ():
+                for r, q in (((c.get("resources") or {}).get(kind)) or {}).items():
+                    v, unit = _res_value(r, q)
+                    if v > tot.get(r, (0.0, unit))[0]:
+                        tot[r] = (v, unit)
+            if tot:
+                for r, q in (spec.get("overhead") or {}).items():
+                    if r in tot:
+                        v, unit = _res_value(r, q)
+                        tot[r] = (tot[r][0] + v, unit)
+            for r in sorted(tot):
+                v, unit = tot[r]
+                txt = str(int(v)) if v == int(v) else repr(v)
+                out.append(f"{metric}{{{_fmt_labels(dict(base, resource=r, unit=unit))}}} {txt}")
+    return ("\n".join(out) + "\n").encode()
 
 
 class NullMetrics:

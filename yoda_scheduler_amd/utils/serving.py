@@ -12,7 +12,9 @@ class StatusServer:
     def __init__(self, host: str, port: int, metrics_render: Callable[[], bytes],
                  healthy: Callable[[], bool] = lambda: True, configz: Optional[Callable[[], dict]] = None,
                  debug: Optional[Callable[[], dict]] = None, trace: Optional[Callable[[], dict]] = None,
-                 profiling: bool = False) -> None:
+                 profiling: bool = False, resources: Optional[Callable[[], bytes]] = None,
+                 cache: Optional[Callable[[], dict]] = None, ssl_context=None) -> None:
+        self.ssl_context = ssl_context
         self.host, self.port = host, port
         self.app = web.Application()
         self.app.router.add_get("/healthz", self._health(healthy))
@@ -22,7 +24,13 @@ class StatusServer:
             return web.Response(body=metrics_render(), content_type="text/plain", charset="utf-8")
 
         self.app.router.add_get("/metrics", metrics)
-        for path, fn in (("/configz", configz), ("/debug/yoda", debug), ("/debug/trace", trace)):
+        if resources is not None:
+            async def metrics_resources(_r):
+                return web.Response(body=resources(), content_type="text/plain", charset="utf-8")
+
+            self.app.router.add_get("/metrics/resources", metrics_resources)
+        for path, fn in (("/configz", configz), ("/debug/yoda", debug), ("/debug/trace", trace),
+                         ("/debug/cache", cache)):
             if fn is not None:
                 self.app.router.add_get(path, self._json(fn))
         if profiling:
@@ -60,7 +68,7 @@ class StatusServer:
     async def start(self) -> int:
         self._runner = web.AppRunner(self.app)
         await self._runner.setup()
-        site = web.TCPSite(self._runner, self.host, self.port)
+        site = web.TCPSite(self._runner, self.host, self.port, ssl_context=self.ssl_context)
         await site.start()
         self.port = site._server.sockets[0].getsockname()[1]   # type: ignore[union-attr]
         return self.port
