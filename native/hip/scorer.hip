@@ -645,6 +645,7 @@ struct Ctx {
   int grid = 1024;
   bool timing = false;        // event timing of each cycle (benchmarks); off in the scheduler
   int direct_atomics = -1;    // -1: by grid size; 0/1 forced (YODA_DEV_DIRECT_ATOMICS)
+  int fuse_max = kFuseSelectMax;   // YODA_DEV_FUSE_MAX overrides (A/B of the fused select)
   PatchArgs pend{};           // dirty rows waiting to ride in the next filter launch
 };
 
@@ -699,6 +700,7 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
   int cus = 256;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess) c->grid = cus * 4;
   if (const char* v = getenv("YODA_DEV_DIRECT_ATOMICS")) c->direct_atomics = v[0] == '1' ? 1 : 0;
+  if (const char* v = getenv("YODA_DEV_FUSE_MAX")) c->fuse_max = atoi(v);
   const SubsetTable st = make_subsets();
   if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_subsets), &st, sizeof st)) != hipSuccess) return fail("subsets", e);
   if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
@@ -804,7 +806,7 @@ int launch_cycle(Ctx* c, int n, yoda_dev_req_t r, yoda_dev_result_t* out, uint32
   int grid_sel = (n + kBlock - 1) / kBlock;
   grid_sel = grid_sel < c->grid ? grid_sel : c->grid;
   r.dev_flags = ((c->direct_atomics < 0 ? grid <= 256 : c->direct_atomics == 1) ? 1u : 0u) | extra_flags;
-  const int fuse = n <= kFuseSelectMax;
+  const int fuse = n <= c->fuse_max;
   hipLaunchKernelGGL(k_filter, dim3(grid + (c->pend.n > 0 ? 1 : 0)), dim3(kBlock), 0, c->stream, c->pend, c->d_nodes,
                      n, r, c->d_cand, c->d_feas, c->d_elig, c->d_g);
   c->pend.n = 0;
