@@ -3,7 +3,10 @@
 
 Events are buffered and written by a background task with their own rate limiter and
 a per-(object, reason, message) de-duplication counter, so recording never blocks the
-scheduling loop.
+scheduling loop. Like client-go's broadcaster (``maxQueuedEvents = 1000``,
+``DropIfChannelFull``) the buffer is bounded and a full buffer drops the *incoming*
+event: a burst of thousands of pods produces more ``Scheduled`` events than the event
+QPS can write, and those must not pile up in memory.
 """
 from __future__ import annotations
 
@@ -21,12 +24,13 @@ log = logging.getLogger("yoda.events")
 
 class EventRecorder:
     def __init__(self, client, component: str = "yoda-scheduler", qps: float = 50.0, burst: int = 300,
-                 max_buffer: int = 100_000, enabled: bool = True) -> None:
+                 max_buffer: int = 1000, enabled: bool = True) -> None:
         self.client = client
         self.component = component
         self.enabled = enabled
         self.limiter = TokenBucket(qps, burst)
-        self._buf: collections.deque = collections.deque(maxlen=max_buffer)
+        self.max_buffer = max_buffer
+        self._buf: collections.deque = collections.deque()
         self._wake = asyncio.Event()
         self._dedup: dict[tuple, dict] = {}
         self.recorded = collections.Counter()
@@ -36,8 +40,9 @@ class EventRecorder:
         if not self.enabled:
             return
         self.recorded[reason] += 1
-        if len(self._buf) == self._buf.maxlen:
+        if len(self._buf) >= self.max_buffer:
             self.dropped += 1
+            return
         self._buf.append((pod_obj_meta, kind, typ, reason, message, time.time()))
         self._wake.set()
 
