@@ -43,6 +43,11 @@ class Status:
         return cls(Code.UNSCHEDULABLE, list(reasons), plugin)
 
     @classmethod
+    def unresolvable(cls, *reasons: str, plugin: str = "") -> "Status":
+        """``UnschedulableAndUnresolvable``: preemption cannot help on this node."""
+        return cls(Code.UNSCHEDULABLE_AND_UNRESOLVABLE, list(reasons), plugin)
+
+    @classmethod
     def error(cls, *reasons: str, plugin: str = "") -> "Status":
         return cls(Code.ERROR, list(reasons), plugin)
 

@@ -8,13 +8,15 @@ done once per cycle in PreFilter over the cache's bound + assumed pods.
 """
 from __future__ import annotations
 
+import math
 from collections import defaultdict
 from typing import Optional
 
 from ..framework.interfaces import (CycleState, FilterPlugin, NodeScore, PreFilterPlugin, PreScorePlugin, ScorePlugin,
                                     StateData, Status, MAX_NODE_SCORE)
-from ..models.pod import PF_POD_AFFINITY, PF_SPREAD
-from ..models.selectors import LabelSelector
+from ..models.pod import PF_CONTROLLER, PF_POD_AFFINITY, PF_SPREAD
+from ..models.selectors import LabelSelector, NodeSelector
+from .optional import default_selector
 
 
 def _spec(pod) -> dict:
@@ -27,93 +29,262 @@ def _node_labels(handle, node: str) -> dict:
 
 
 # ============================================================== PodTopologySpread
-class _SpreadState(StateData):
-    def __init__(self, hard, soft, counts, domains):
-        self.hard, self.soft, self.counts, self.domains = hard, soft, counts, domains
-        # global minimum matching count per hard constraint (computed once, not per node)
-        self.min_count = [min((counts.get((ci, d), 0) for d in domains[ci]), default=0) for ci in range(len(hard))]
+LABEL_HOSTNAME = "kubernetes.io/hostname"
+# upstream v1.20 ``systemDefaultConstraints`` (DefaultPodTopologySpread, beta and on in v1.20)
+SYSTEM_DEFAULT_CONSTRAINTS = (
+    {"topologyKey": LABEL_HOSTNAME, "whenUnsatisfiable": "ScheduleAnyway", "maxSkew": 3},
+    {"topologyKey": "topology.kubernetes.io/zone", "whenUnsatisfiable": "ScheduleAnyway", "maxSkew": 5},
+)
+
+
+def pod_matches_node_affinity(pod, node_name: str, labels: dict) -> bool:
+    """upstream ``helper.PodMatchesNodeSelectorAndAffinityTerms``: ``spec.nodeSelector``
+    plus the required node-affinity terms (preferred terms are ignored)."""
+    spec = _spec(pod)
+    for k, v in (spec.get("nodeSelector") or {}).items():
+        if labels.get(k) != v:
+            return False
+    req = ((spec.get("affinity") or {}).get("nodeAffinity") or {}).get("requiredDuringSchedulingIgnoredDuringExecution")
+    if req is not None and not NodeSelector(req).matches(node_name, labels):
+        return False
+    return True
+
+
+def _has_keys(labels: dict, constraints) -> bool:
+    """upstream ``nodeLabelsMatchSpreadConstraints``: the node carries every topology key."""
+    return all(c[0] in labels for c in constraints)
+
+
+def _count_matching(cache, uids, sel, namespace: str) -> int:
+    """upstream ``countPodsMatchSelector``: same namespace, not terminating, selector match."""
+    n = 0
+    for uid in uids:
+        ps = cache.pods.get(uid)
+        if ps is None:
+            continue
+        info = ps.info
+        if info.namespace != namespace or (info.obj.get("metadata") or {}).get("deletionTimestamp"):
+            continue
+        if sel.matches(info.labels):
+            n += 1
+    return n
+
+
+class _SpreadFilterState(StateData):
+    """upstream ``preFilterState``: the hard constraints, matching-pod count per
+    (key, value) pair over the nodes that pass the pod's node affinity and carry every key,
+    and the global minimum per key (``TpKeyToCriticalPaths[key][0]``)."""
+
+    def __init__(self, constraints, pair_counts, min_count):
+        self.constraints, self.pair_counts, self.min_count = constraints, pair_counts, min_count
+
+    def clone(self) -> "_SpreadFilterState":
+        return self
+
+
+class _SpreadScoreState(StateData):
+    """upstream ``preScoreState``: soft constraints, nodes missing a key (score 0), counts
+    per non-hostname pair and ``log(size + 2)`` normalising weights."""
+
+    def __init__(self, constraints, ignored, pair_counts, weights):
+        self.constraints, self.ignored, self.pair_counts, self.weights = constraints, ignored, pair_counts, weights
+
+    def clone(self) -> "_SpreadScoreState":
+        return self
+
+
+def _parse_constraints(items, action: str, selector=None) -> list:
+    """upstream ``filterTopologySpreadConstraints``: (topologyKey, maxSkew, selector) of the
+    constraints whose ``whenUnsatisfiable`` is ``action``."""
+    out = []
+    for c in items or ():
+        if c.get("whenUnsatisfiable", "DoNotSchedule") != action:
+            continue
+        sel = selector if selector is not None else LabelSelector(c.get("labelSelector"))
+        out.append((c.get("topologyKey", ""), int(c.get("maxSkew", 1)), sel))
+    return out
 
 
 class PodTopologySpread(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin):
-    """topologySpreadConstraints: DoNotSchedule → Filter (skew ≤ maxSkew), ScheduleAnyway →
-    Score (fewer matching pods in the domain scores higher)."""
+    """upstream v1.20 ``podtopologyspread``: ``DoNotSchedule`` constraints filter
+    (matching pods in the node's domain + self − global minimum ≤ maxSkew; domains and
+    counts only over nodes that pass the pod's nodeSelector/required node affinity and
+    carry every key), ``ScheduleAnyway`` constraints score (Σ count·log(#domains + 2) +
+    maxSkew − 1, normalised ``100·(max + min − s)/max``; nodes missing a key score 0).
+
+    Pods without constraints get the profile's default constraints with the
+    ``DefaultSelector`` of their Services / controller: ``defaultingType: System`` (the
+    v1.20 default when ``defaultConstraints`` is empty) uses hostname maxSkew 3 and zone
+    maxSkew 5, both ``ScheduleAnyway``; ``List`` uses ``args.defaultConstraints``."""
     name = "PodTopologySpread"
     KEY = "PreFilterPodTopologySpread"
+    SCORE_KEY = "PreScorePodTopologySpread"
+    watches = ("services", "replicationcontrollers", "replicasets", "statefulsets")
 
-    pod_flags = PF_SPREAD
+    pod_flags = PF_SPREAD | PF_CONTROLLER
+
+    def __init__(self, args: Optional[dict] = None, handle=None) -> None:
+        super().__init__(args, handle)
+        listed = list(self.args.get("defaultConstraints") or [])
+        dtype = self.args.get("defaultingType") or ("List" if listed else "System")
+        if dtype not in ("System", "List"):
+            raise ValueError(f"PodTopologySpread: defaultingType must be System or List, got {dtype!r}")
+        if dtype == "System" and listed:
+            raise ValueError("PodTopologySpread: when defaultingType is System, defaultConstraints must be empty")
+        for c in listed:
+            if c.get("labelSelector") is not None:
+                raise ValueError("PodTopologySpread: defaultConstraints must not set labelSelector")
+            if int(c.get("maxSkew", 0)) <= 0 or not c.get("topologyKey") or \
+                    c.get("whenUnsatisfiable") not in ("DoNotSchedule", "ScheduleAnyway"):
+                raise ValueError(f"PodTopologySpread: invalid default constraint {c!r}")
+        self.defaulting_type = dtype
+        self.default_constraints = list(SYSTEM_DEFAULT_CONSTRAINTS) if dtype == "System" else listed
+
+    def cluster_active(self) -> bool:
+        """Default constraints apply to pods selected by a Service (controller-owned pods
+        carry ``PF_CONTROLLER``)."""
+        return bool(self.default_constraints) and bool(self.handle.lister("services"))
 
     def is_noop_for(self, pod) -> bool:
-        return not _spec(pod).get("topologySpreadConstraints")
+        if _spec(pod).get("topologySpreadConstraints"):
+            return False
+        if not self.default_constraints:
+            return True
+        return default_selector(self.handle, pod).empty
 
-    def _constraints(self, pod):
-        hard, soft = [], []
-        for c in _spec(pod).get("topologySpreadConstraints") or []:
-            item = (c.get("topologyKey", ""), int(c.get("maxSkew", 1)), LabelSelector(c.get("labelSelector")))
-            (hard if c.get("whenUnsatisfiable", "DoNotSchedule") == "DoNotSchedule" else soft).append(item)
-        return hard, soft
+    def _constraints(self, pod, action: str) -> list:
+        explicit = _spec(pod).get("topologySpreadConstraints")
+        if explicit:
+            return _parse_constraints(explicit, action)
+        if not self.default_constraints:
+            return []
+        sel = default_selector(self.handle, pod)
+        if sel.empty:
+            return []
+        return _parse_constraints(self.default_constraints, action, sel)
 
+    def _qualified_nodes(self, pod, constraints):
+        """Nodes that pass the pod's node affinity and carry every topology key."""
+        for name, info in self.handle.cache.nodes.items():
+            labels = info.labels
+            if _has_keys(labels, constraints) and pod_matches_node_affinity(pod, name, labels):
+                yield name, labels
+
+    # ---------------------------------------------------------------- filter
     def pre_filter(self, state: CycleState, pod) -> Status:
-        hard, soft = self._constraints(pod)
-        cache = self.handle.cache
-        counts: dict = defaultdict(int)        # (constraint idx, domain value) → matching pods
-        domains: dict = defaultdict(set)       # constraint idx → domain values that exist
-        allc = hard + soft
-        for node, uids in cache.node_pods.items():
-            labels = _node_labels(self.handle, node)
-            for ci, (key, _skew, sel) in enumerate(allc):
-                if key not in labels:
-                    continue
-                dom = labels[key]
-                domains[ci].add(dom)
-                for uid in uids:
-                    ps = cache.pods.get(uid)
-                    if ps is not None and ps.info.namespace == pod.namespace and sel.matches(ps.info.labels):
-                        counts[(ci, dom)] += 1
-        for node, info in cache.nodes.items():        # nodes without pods are domains too
-            for ci, (key, _s, _sel) in enumerate(allc):
-                if key in info.labels:
-                    domains[ci].add(info.labels[key])
-        state.write(self.KEY, _SpreadState(hard, soft, counts, domains))
+        hard = self._constraints(pod, "DoNotSchedule")
+        pair_counts: dict = {}
+        min_count: dict = {}
+        if hard:
+            cache = self.handle.cache
+            for name, labels in self._qualified_nodes(pod, hard):
+                uids = cache.node_pods.get(name, ())
+                for key, _skew, sel in hard:
+                    pair = (key, labels[key])
+                    pair_counts[pair] = pair_counts.get(pair, 0) + (
+                        _count_matching(cache, uids, sel, pod.namespace) if uids else 0)
+            for (key, _v), n in pair_counts.items():
+                if key not in min_count or n < min_count[key]:
+                    min_count[key] = n
+        state.write(self.KEY, _SpreadFilterState(hard, pair_counts, min_count))
         return Status.ok()
 
     def filter(self, state: CycleState, pod, node_name: str) -> Status:
         try:
-            s: _SpreadState = state.read(self.KEY)
+            s: _SpreadFilterState = state.read(self.KEY)
         except KeyError:
+            self.pre_filter(state, pod)
+            s = state.read(self.KEY)
+        if not s.constraints:
             return Status.ok()
         labels = _node_labels(self.handle, node_name)
-        for ci, (key, max_skew, sel) in enumerate(s.hard):
+        for key, max_skew, sel in s.constraints:
             if key not in labels:
-                return Status.unschedulable("node(s) didn't match pod topology spread constraints (missing label)",
-                                            plugin=self.name)
+                return Status.unresolvable("node(s) didn't match pod topology spread constraints "
+                                           "(missing required label)", plugin=self.name)
             self_match = 1 if sel.matches(pod.labels) else 0
-            if s.counts.get((ci, labels[key]), 0) + self_match - s.min_count[ci] > max_skew:
+            skew = s.pair_counts.get((key, labels[key]), 0) + self_match - s.min_count.get(key, 0)
+            if skew > max_skew:
                 return Status.unschedulable("node(s) didn't match pod topology spread constraints", plugin=self.name)
         return Status.ok()
 
+    # ---------------------------------------------------------------- score
     def pre_score(self, state: CycleState, pod, nodes: list[str]) -> Status:
-        try:
-            state.read(self.KEY)
-        except KeyError:
-            self.pre_filter(state, pod)
+        soft = self._constraints(pod, "ScheduleAnyway")
+        ignored: set = set()
+        pair_counts: dict = {}
+        weights: list = []
+        if soft and nodes:
+            sizes = [0] * len(soft)
+            for name in nodes:
+                labels = _node_labels(self.handle, name)
+                if not _has_keys(labels, soft):
+                    ignored.add(name)
+                    continue
+                for i, (key, _skew, _sel) in enumerate(soft):
+                    if key == LABEL_HOSTNAME:
+                        continue          # per-node counts are taken in Score
+                    pair = (key, labels[key])
+                    if pair not in pair_counts:
+                        pair_counts[pair] = 0
+                        sizes[i] += 1
+            for i, (key, _skew, _sel) in enumerate(soft):
+                size = len(nodes) - len(ignored) if key == LABEL_HOSTNAME else sizes[i]
+                weights.append(math.log(size + 2))
+            if pair_counts:
+                cache = self.handle.cache
+                for name, labels in self._qualified_nodes(pod, soft):
+                    uids = cache.node_pods.get(name, ())
+                    if not uids:
+                        continue
+                    for key, _skew, sel in soft:
+                        pair = (key, labels[key])
+                        if pair in pair_counts:
+                            pair_counts[pair] += _count_matching(cache, uids, sel, pod.namespace)
+        state.write(self.SCORE_KEY, _SpreadScoreState(soft, ignored, pair_counts, weights))
         return Status.ok()
 
+    def _score_state(self, state: CycleState, pod) -> _SpreadScoreState:
+        try:
+            return state.read(self.SCORE_KEY)
+        except KeyError:
+            self.pre_score(state, pod, list(self.handle.cache.nodes))
+            return state.read(self.SCORE_KEY)
+
     def score(self, state: CycleState, pod, node_name: str) -> tuple[int, Status]:
-        s: _SpreadState = state.read(self.KEY)
+        s = self._score_state(state, pod)
+        if not s.constraints or node_name in s.ignored:
+            return 0, Status.ok()
         labels = _node_labels(self.handle, node_name)
-        off = len(s.hard)
-        total = 0
-        for j, (key, _skew, _sel) in enumerate(s.soft):
-            if key in labels:
-                total += s.counts.get((off + j, labels[key]), 0)
-        return total, Status.ok()
+        total = 0.0
+        for i, (key, max_skew, sel) in enumerate(s.constraints):
+            if key not in labels:
+                continue
+            if key == LABEL_HOSTNAME:
+                cnt = _count_matching(self.handle.cache, self.handle.cache.node_pods.get(node_name, ()), sel,
+                                      pod.namespace)
+            else:
+                cnt = s.pair_counts.get((key, labels[key]), 0)
+            total += cnt * s.weights[i] + (max_skew - 1)
+        return int(total), Status.ok()
 
     def normalize_score(self, state: CycleState, pod, scores: list[NodeScore]) -> Status:
-        if not scores:
+        s = self._score_state(state, pod)
+        if not s.constraints or not scores:
             return Status.ok()
-        hi, lo = max(x.score for x in scores), min(x.score for x in scores)
+        lo, hi = None, 0
         for x in scores:
-            x.score = MAX_NODE_SCORE if hi == lo else MAX_NODE_SCORE * (hi - x.score) // (hi - lo)
+            if x.name in s.ignored:
+                continue
+            lo = x.score if lo is None or x.score < lo else lo
+            hi = max(hi, x.score)
+        for x in scores:
+            if x.name in s.ignored:
+                x.score = 0
+            elif hi == 0:
+                x.score = MAX_NODE_SCORE
+            else:
+                x.score = MAX_NODE_SCORE * (hi + lo - x.score) // hi
         return Status.ok()
 
 
