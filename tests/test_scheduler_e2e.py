@@ -244,6 +244,55 @@ def test_preemption_evicts_lower_priority():
     assert ok and not low_exists
 
 
+def test_preemption_frees_required_anti_affinity():
+    """The victim is needed for a Python filter (required pod anti-affinity), not for GPU
+    capacity: the what-if hides it from InterPodAffinity too (upstream RemovePod)."""
+    anti = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+        {"topologyKey": "kubernetes.io/hostname", "labelSelector": {"matchLabels": {"app": "noisy"}}}]}}
+
+    async def go():
+        c = FakeCluster()
+        c.add_node("n")
+        await c.start()
+        c.add_pod("noisy", {"app": "noisy", "scv/memory": "1000"}, priority=1)
+        c.add_pod("boss", {"app": "noisy", "scv/memory": "1000"}, priority=1000)
+        c.add_pod("other", {"app": "web", "scv/memory": "1000"}, priority=1)
+        assert await c.wait_bound(3)
+        c.add_pod("quiet", {"app": "quiet", "scv/memory": "1000"}, priority=100, affinity=anti)
+        await asyncio.sleep(0.5)
+        deleted = []
+        for name in ("noisy", "boss", "other"):
+            try:
+                c.pod(name)
+            except Exception:
+                deleted.append(name)
+        await c.stop()
+        return deleted
+    # only the lower-priority matching pod could go, and it would not be enough: "boss"
+    # (higher priority) still repels the pod, so nothing is evicted
+    assert run(go()) == []
+
+    async def go2():
+        c = FakeCluster()
+        c.add_node("n")
+        await c.start()
+        c.add_pod("noisy", {"app": "noisy", "scv/memory": "1000"}, priority=1)
+        c.add_pod("other", {"app": "web", "scv/memory": "1000"}, priority=1)
+        assert await c.wait_bound(2)
+        c.add_pod("quiet", {"app": "quiet", "scv/memory": "1000"}, priority=100, affinity=anti)
+        ok = await c.wait(lambda: "default/quiet" in c.server.bind_log, 5)
+        deleted = []
+        for name in ("noisy", "other"):
+            try:
+                c.pod(name)
+            except Exception:
+                deleted.append(name)
+        await c.stop()
+        return ok, deleted
+    ok, deleted = run(go2())
+    assert ok and deleted == ["noisy"]       # "other" is reprieved: it does not block the pod
+
+
 def test_preemption_policy_never_does_not_evict():
     async def go():
         c = FakeCluster()

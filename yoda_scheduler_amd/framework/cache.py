@@ -151,6 +151,25 @@ class SchedulerCache:
         else:
             self._anti.discard(ps.info.uid)
 
+    def hide(self, uids) -> list:
+        """Drop pods from the Python-side views (``pods`` / ``node_pods`` / extended-resource
+        usage) without touching the engine ledger: the preemption what-if of upstream's
+        ``RemovePod`` on a NodeInfo copy. ``unhide`` puts them back."""
+        out = []
+        for uid in uids:
+            ps = self.pods.pop(uid, None)
+            if ps is None:
+                continue
+            self.node_pods.get(ps.node, set()).discard(uid)
+            if ps.info.ext:
+                self._ext(ps, -1)
+            out.append(ps)
+        return out
+
+    def unhide(self, states) -> None:
+        for ps in states:
+            self._track(ps)
+
     def pods_with_required_anti_affinity(self) -> int:
         """Bound/assumed pods whose required anti-affinity can reject new pods (symmetry)."""
         if self._anti:

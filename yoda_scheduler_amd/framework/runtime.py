@@ -122,6 +122,8 @@ class Framework:
         inst = self.plugins.get(name)
         if inst is None:
             inst = registry.create(name, self.profile.plugin_config.get(name, {}), self.handle)
+            if hasattr(inst, "bind_framework"):
+                inst.bind_framework(self)
             self.plugins[name] = inst
         return inst
 
@@ -146,6 +148,17 @@ class Framework:
                 st.plugin = st.plugin or p.name
                 return st
         return Status.ok()
+
+    def passes_py_filters(self, pod, node: str) -> bool:
+        """Upstream ``PodPassesFiltersOnNode`` for the Python side of a profile: PreFilter
+        over the cache as it stands (state rebuilt, which equals upstream's AddPod /
+        RemovePod extensions applied to the cycle state), then the Python filters on
+        ``node``. The native filters are checked by the caller."""
+        state = CycleState()
+        if not self.run_pre_filter(state, pod).is_success():
+            return False
+        ok, _ = self.run_filter_py(state, pod, [node])
+        return bool(ok)
 
     def has_active_filter_py(self, pod) -> bool:
         return any(self._applies(p, pod) for p in self.filter_py)

@@ -202,10 +202,18 @@ class DefaultPreemption(PostFilterPlugin):
       of preempting again (``PodEligibleToPreemptOthers``).
 
     Victims are deleted through the API and the preemptor is nominated to the node; the
-    ledger is restored exactly before returning.
+    ledger is restored exactly before returning. When the pod uses a Python filter plugin
+    of the profile (pod (anti-)affinity, topology spread, host ports, volumes) each what-if
+    also hides the removed pods from the cache and re-runs PreFilter + those filters, so a
+    victim whose removal satisfies e.g. required anti-affinity is found (upstream's
+    ``RunPreFilterExtensionRemovePod`` / ``AddPod``).
     """
     name = "DefaultPreemption"
     watches = ("poddisruptionbudgets",)
+    framework = None
+
+    def bind_framework(self, fw) -> None:
+        self.framework = fw
 
     def _pdbs(self) -> list:
         from ..models.selectors import LabelSelector
@@ -252,8 +260,15 @@ class DefaultPreemption(PostFilterPlugin):
         from ..ops.native import pod_req
         req = pod_req(eng, pod)
         pdbs = self._pdbs()
+        fw = self.framework
+        py = fw is not None and (fw.has_active_filter_py(pod) or
+                                 any(fw._applies(p, pod) for p in fw.pre_filter))
+
+        def fits(node: str, idx: int) -> bool:
+            return eng.filter_node(req, idx) == 0 and (not py or fw.passes_py_filters(pod, node))
+
         best = None
-        for node, ps_uids in cache.node_pods.items():
+        for node, ps_uids in list(cache.node_pods.items()):
             idx = eng.node_index(node)
             if idx < 0:
                 continue
@@ -262,25 +277,35 @@ class DefaultPreemption(PostFilterPlugin):
                 continue
             for ps in lower:
                 eng.release(ps.info.num_id)
-            if eng.filter_node(req, idx) != 0:          # no candidate: put everything back
-                for ps in lower:
+            if py:
+                cache.hide([ps.info.uid for ps in lower])
+            try:
+                if not fits(node, idx):                     # no candidate: put everything back
+                    for ps in lower:
+                        eng.reserve(ps.info.num_id, pod_req(eng, ps.info), idx, list(ps.cards))
+                    continue
+                victims, violations = [], 0
+                budget = {k: allowed for k, (_ns, _sel, allowed) in enumerate(pdbs)}
+                flagged = [(self._violates(pdbs, ps.info, budget), ps) for ps in lower]
+                # reprieve PDB-violating pods first, then higher priorities first
+                for violating, ps in sorted(flagged, key=lambda t: (not t[0], -t[1].info.priority)):
                     eng.reserve(ps.info.num_id, pod_req(eng, ps.info), idx, list(ps.cards))
-                continue
-            victims, violations = [], 0
-            budget = {k: allowed for k, (_ns, _sel, allowed) in enumerate(pdbs)}
-            flagged = [(self._violates(pdbs, ps.info, budget), ps) for ps in lower]
-            # reprieve PDB-violating pods first, then higher priorities first
-            for violating, ps in sorted(flagged, key=lambda t: (not t[0], -t[1].info.priority)):
-                eng.reserve(ps.info.num_id, pod_req(eng, ps.info), idx, list(ps.cards))
-                if eng.filter_node(req, idx) != 0:
-                    eng.release(ps.info.num_id)
-                    victims.append(ps)
-                    violations += violating
-            # the GPUs the preemptor would take once the victims are gone
-            ok_cards, cards, _q = eng.select_gpus(req, idx)
-            # restore the ledger exactly (victims are still released at this point)
-            for ps in victims:
-                eng.reserve(ps.info.num_id, pod_req(eng, ps.info), idx, list(ps.cards))
+                    if py:
+                        cache.unhide([ps])
+                    if not fits(node, idx):
+                        eng.release(ps.info.num_id)
+                        if py:
+                            cache.hide([ps.info.uid])
+                        victims.append(ps)
+                        violations += violating
+                # the GPUs the preemptor would take once the victims are gone
+                ok_cards, cards, _q = eng.select_gpus(req, idx)
+                # restore the ledger exactly (victims are still released at this point)
+                for ps in victims:
+                    eng.reserve(ps.info.num_id, pod_req(eng, ps.info), idx, list(ps.cards))
+            finally:
+                if py:
+                    cache.unhide([ps for ps in lower if ps.info.uid not in cache.pods])
             if victims:
                 prios = [v.info.priority for v in victims]
                 key = (violations, max(prios), sum(prios), len(victims))
