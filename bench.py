@@ -54,6 +54,8 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5, 6])
+    ap.add_argument("--node-gpus", type=int, default=None, choices=[1, 2, 4, 8],
+                    help="GPUs per synthetic node (BASELINE protocol item 5); default: the config's own")
     ap.add_argument("--device", choices=["auto", "on", "off"], default="auto",
                     help="gfx950 device scorer (used automatically for clusters >= 256 nodes)")
     ap.add_argument("--qps", type=float, default=5000.0, help="client QPS (deploy default 5000; reference 50)")
@@ -100,7 +102,7 @@ def main(argv=None) -> int:
 
     from yoda_scheduler_amd.bench.harness import HttpShard, Shard, percentile
     from yoda_scheduler_amd.bench.workloads import make_workload
-    w = make_workload(a.config, seed=rank)
+    w = make_workload(a.config, seed=rank, node_gpus=a.node_gpus)
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
     if a.transport == "http":
@@ -173,6 +175,7 @@ def main(argv=None) -> int:
             "e2e_scheduling_p99_ms": round(percentile(e2e, 99) * 1000.0, 3) if e2e else None,
             "pods_bound": bound,
             "pods_unschedulable": unsched,
+            "node_gpus": a.node_gpus or w.nodes[0][2],
             "client_qps": a.qps, "client_burst": a.burst, "native_batch": a.batch, "compat": a.compat,
             "device_scorer": a.device, "device_cycles": device_cycles, "transport": a.transport,
             "baseline_note": "vs_baseline against BASELINE.md's derived (unmeasured) ~55 pods/s reference ceiling "

@@ -511,3 +511,18 @@ def test_fastbind_pipelining_errors_chunked_and_reconnect():
     assert bound == 300
     assert codes == [409, 404]
     assert served == 6
+
+
+def test_bench_node_gpus_sweep_option():
+    """BASELINE protocol item 5 (every config at 1/2/4/8 GPUs per node): ``--node-gpus``
+    resizes the synthetic nodes; pods asking for more GPUs than a node has are reported as
+    unschedulable, everything else binds."""
+    from yoda_scheduler_amd.bench.workloads import make_workload
+    w = make_workload(5, node_gpus=2)
+    assert [g for _n, _s, g in w.nodes] == [2, 2, 2, 2] and "4 nodes x 2 MI355X" in w.name
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "2", "--node-gpus", "4",
+                        "--steps", "1", "--warmup", "0"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["node_gpus"] == 4 and d["pods_bound"] == 100 and "1 node x 4 MI355X" in d["config"]["model"]

@@ -16,6 +16,7 @@ measures scheduling, not capacity exhaustion.
 from __future__ import annotations
 
 import random
+import re
 import time
 from dataclasses import dataclass, field
 from typing import Optional
@@ -50,7 +51,21 @@ def _mixed_labels(rng: random.Random) -> dict:
     return {"scv/number": "8", "scv/memory": "1024"}
 
 
-def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None) -> Workload:
+def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None,
+                  node_gpus: Optional[int] = None) -> Workload:
+    """``node_gpus`` overrides the GPUs per node (BASELINE.md protocol item 5: every
+    config at 1, 2, 4 and 8 GPUs per node); pods keep their labels, so e.g. ``scv/number: 8``
+    pods are unschedulable on smaller nodes and are reported as such."""
+    w = _make_workload(cfg, seed, template)
+    if node_gpus is not None:
+        if node_gpus < 1:
+            raise ValueError("node_gpus must be >= 1")
+        w.nodes = [(name, spec, node_gpus) for name, spec, _g in w.nodes]
+        w.name = re.sub(r"x \d+ (MI3\d\dX|GPUs)", rf"x {node_gpus} \1", w.name)
+    return w
+
+
+def _make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None) -> Workload:
     rng = random.Random(seed * 7919 + cfg)
     if cfg == 1:
         w = Workload(1, "1 pod scv/memory=1000, 1 node x 8 MI355X (fake CRD)", [("node-0", MI355X, 8)])
