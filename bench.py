@@ -121,9 +121,11 @@ def main(argv=None) -> int:
 
     sync()
     t0 = time.perf_counter()
+    c0 = time.process_time()
     results = [loop.run_until_complete(shards[a.warmup + i].burst(f"s{i}")) for i in range(a.steps)]
     sync()
     elapsed = time.perf_counter() - t0
+    cpu_s = time.process_time() - c0     # this rank's process: scheduler (+ in-process apiserver)
 
     device_cycles = sum(s.sched.engine.device_cycles for s in {id(x): x for x in shards}.values())
     bound = sum(r.bound for r in results)
@@ -134,9 +136,9 @@ def main(argv=None) -> int:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        c = torch.tensor([bound, unsched], dtype=torch.float64, device=dev)
+        c = torch.tensor([bound, unsched, cpu_s], dtype=torch.float64, device=dev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        bound, unsched = int(c[0].item()), int(c[1].item())
+        bound, unsched, cpu_s = int(c[0].item()), int(c[1].item()), float(c[2].item())
         gathered: list = [None] * world
         dist.all_gather_object(gathered, lats)
         lats = [x for g in gathered for x in g]
@@ -173,6 +175,9 @@ def main(argv=None) -> int:
             "max_latency_ms": round(max(lats) * 1000.0, 3) if lats else None,
             "e2e_scheduling_p50_ms": round(percentile(e2e, 50) * 1000.0, 3) if e2e else None,
             "e2e_scheduling_p99_ms": round(percentile(e2e, 99) * 1000.0, 3) if e2e else None,
+            # process CPU time per bound pod, summed over ranks: with --transport http this is
+            # the scheduler alone (the apiserver is another process); inproc includes the fake apiserver
+            "cpu_us_per_pod": round(cpu_s / bound * 1e6, 2) if bound else None,
             "pods_bound": bound,
             "pods_unschedulable": unsched,
             "node_gpus": a.node_gpus or w.nodes[0][2],

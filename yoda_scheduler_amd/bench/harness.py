@@ -150,7 +150,10 @@ class HttpShard:
                "--seed", str(seed), "--port-file", self.port_file]
         if template:
             cmd += ["--template", json.dumps(template)]
-        self.proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+        import os
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env = dict(os.environ, PYTHONPATH=os.pathsep.join(p for p in (root, os.environ.get("PYTHONPATH")) if p))
+        self.proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env)
         self.cfg = parse_config(bench_config(w.scheduler_name, qps, burst, batch, compat, device))
         self.events, self.seed = events, seed
         self.sched: Optional[Scheduler] = None
