@@ -88,6 +88,75 @@ def test_watch_too_old_resource_version_is_gone():
     assert run(go()) == 410
 
 
+def test_chunked_list_and_expired_continue_over_http():
+    """client-go pager semantics: ``limit`` chunks joined through ``continue`` tokens; a
+    token older than the apiserver's history window is 410 Expired."""
+    async def go():
+        srv = FakeApiServer(history=50)
+        api = FakeApiHttp(srv)
+        url = await api.start()
+        cl = KubeClient(KubeConfig(url))
+        try:
+            for i in range(1234):
+                srv.create("nodes", make_node(f"n{i:04d}"))
+            before = srv.calls["list"]
+            items, rv = await cl.list("nodes", resource_version="", limit=500)
+            pages = srv.calls["list"] - before
+            first, _rv, cont = srv.list_page("nodes", None, 10, "")
+            for i in range(60):                          # push the token's RV out of the window
+                srv.create("nodes", make_node(f"late{i}"))
+            with pytest.raises(ApiError) as ei:
+                srv.list_page("nodes", None, 10, cont)
+            return [o["metadata"]["name"] for o in items], rv, pages, ei.value.code, len(first)
+        finally:
+            await cl.close()
+            await api.stop()
+    names, rv, pages, code, first = run(go())
+    assert names == sorted(f"n{i:04d}" for i in range(1234)) and rv == "1234"
+    assert pages == 3 and code == 410 and first == 10
+
+
+def test_informer_bookmarks_and_consistent_relist_after_gone():
+    """BOOKMARK events advance the informer's resourceVersion without touching the store;
+    after a 410 the relist is a consistent, paged read."""
+    from yoda_scheduler_amd.fakeapi.client import InProcessClient
+    from yoda_scheduler_amd.kube.informer import Informer
+
+    async def go():
+        srv = FakeApiServer(history=5)
+        adds = []
+        inf = Informer(InProcessClient(srv), "nodes", on_add=lambda o: adds.append(o["metadata"]["name"]))
+        inf.page_size = 2
+        srv.create("nodes", make_node("a"))
+        task = asyncio.get_event_loop().create_task(inf.run())
+        await asyncio.wait_for(inf.synced.wait(), 5)
+        srv.create("scvs", make_scv("a", update_time=time.time()).to_json())   # RV moves, no node change
+        srv.bookmark("nodes")
+        for _ in range(200):
+            if inf.bookmarks:
+                break
+            await asyncio.sleep(0.005)
+        rv_after_bookmark = inf.resource_version
+        # force a 410: the watch drops, history moves past the informer's RV
+        srv.close_watches()
+        for i in range(8):
+            srv.create("nodes", make_node(f"b{i}"))
+        lists0 = srv.calls["list"]
+        for _ in range(400):
+            if len(inf.store) == 9:
+                break
+            await asyncio.sleep(0.005)
+        inf.stop()
+        srv.close_watches()
+        task.cancel()
+        await asyncio.gather(task, return_exceptions=True)
+        return rv_after_bookmark, inf.bookmarks, sorted(inf.store), srv.calls["list"] - lists0, adds
+    rv, bookmarks, store, lists, adds = run(go())
+    assert bookmarks == 1 and rv == "2"
+    assert store == ["a"] + [f"b{i}" for i in range(8)] and sorted(adds) == store
+    assert lists >= 5            # 9 nodes in pages of 2
+
+
 def test_schedule_over_http_with_informer_relist():
     from yoda_scheduler_amd.framework.config import parse_config
     from yoda_scheduler_amd.framework.scheduler import Scheduler

@@ -20,9 +20,17 @@ class InProcessClient:
         if self.server.faults.latency_s:
             await asyncio.sleep(self.server.faults.latency_s)
 
-    async def list(self, res: str, namespace: Optional[str] = None) -> tuple[list[dict], str]:
+    async def list(self, res: str, namespace: Optional[str] = None, resource_version: Optional[str] = None,
+                   limit: int = 0) -> tuple[list[dict], str]:
         await self._lat()
-        return self.server.list(res, namespace)
+        if not limit:
+            return self.server.list(res, namespace)
+        items, cont = [], ""
+        while True:
+            page, rv, cont = self.server.list_page(res, namespace, limit, cont)
+            items.extend(page)
+            if not cont:
+                return items, rv
 
     async def watch(self, res: str, resource_version: str) -> AsyncIterator[tuple[str, dict]]:
         w = self.server.watch(res, resource_version)

@@ -124,9 +124,16 @@ class FakeApiHttp:
                 if name is None:
                     if req.query.get("watch") in ("1", "true"):
                         return await self._watch(req, res, req.query.get("resourceVersion", "0"))
-                    items, rv = s.list(res, ns)
+                    limit, cont = int(req.query.get("limit", "0") or 0), req.query.get("continue", "")
+                    if limit or cont:
+                        items, rv, nxt = s.list_page(res, ns, limit, cont)
+                    else:
+                        (items, rv), nxt = s.list(res, ns), ""
+                    meta = {"resourceVersion": rv}
+                    if nxt:
+                        meta["continue"] = nxt
                     return web.json_response({"kind": RESOURCES[res].kind + "List", "apiVersion": RESOURCES[res].api_version,
-                                              "metadata": {"resourceVersion": rv}, "items": items})
+                                              "metadata": meta, "items": items})
                 return web.json_response(s.get(res, name, ns))
             body = await req.json() if req.can_read_body else {}
             if req.method == "POST":

@@ -20,8 +20,10 @@ produces a new dict, so consumers never need deep copies.
 from __future__ import annotations
 
 import asyncio
+import base64
 import collections
 import itertools
+import json
 import random
 import time
 import uuid
@@ -213,6 +215,38 @@ class FakeApiServer:
         if namespace and resource(res).namespaced:
             items = [o for o in items if o["metadata"].get("namespace") == namespace]
         return items, str(self._last_rv)
+
+    def list_page(self, res: str, namespace: Optional[str] = None, limit: int = 0,
+                  cont: str = "") -> tuple[list[dict], str, str]:
+        """Chunked list (``limit`` / ``continue``): items in key order; the continue token
+        pins the list's resourceVersion and the last key served, like the apiserver's. A
+        token older than the watch history window is expired (410)."""
+        self.calls["list"] += 1
+        if cont:
+            try:
+                tok = json.loads(base64.urlsafe_b64decode(cont.encode()).decode())
+                rv, start = int(tok["rv"]), str(tok["start"])
+            except (ValueError, KeyError, TypeError):
+                raise ApiError(400, "BadRequest", "invalid continue token") from None
+            if rv < self._oldest_rv[res]:
+                raise ApiError(410, "Expired", "the provided continue parameter is too old")
+        else:
+            rv, start = self._last_rv, ""
+        keys = sorted(k for k in self._objs[res] if k > start)
+        if namespace and resource(res).namespaced:
+            keys = [k for k in keys if self._objs[res][k]["metadata"].get("namespace") == namespace]
+        nxt = ""
+        if limit and len(keys) > limit:
+            keys = keys[:limit]
+            nxt = base64.urlsafe_b64encode(json.dumps({"rv": rv, "start": keys[-1]}).encode()).decode()
+        return [self._objs[res][k] for k in keys], str(rv), nxt
+
+    def bookmark(self, res: str) -> None:
+        """Send a BOOKMARK (current resourceVersion, no object change) to every watcher."""
+        obj = {"kind": resource(res).kind, "apiVersion": resource(res).api_version,
+               "metadata": {"resourceVersion": str(self._last_rv)}}
+        for w in tuple(self._watchers[res]):
+            w.push(("BOOKMARK", obj))
 
     def watch(self, res: str, resource_version: str = "0") -> Watch:
         self.calls["watch"] += 1

@@ -154,9 +154,25 @@ class KubeClient:
             return json.loads(text) if text else {}
 
     # ------------------------------------------------------------------ verbs
-    async def list(self, res: str, namespace: Optional[str] = None) -> tuple[list[dict], str]:
-        out = await self._req("GET", self._url(res, namespace))
-        return out.get("items") or [], (out.get("metadata") or {}).get("resourceVersion", "0")
+    async def list(self, res: str, namespace: Optional[str] = None, resource_version: Optional[str] = None,
+                   limit: int = 0) -> tuple[list[dict], str]:
+        """List (client-go pager semantics): ``resource_version="0"`` may be served from the
+        apiserver's watch cache (which ignores ``limit``); otherwise a consistent read in
+        ``limit``-sized chunks, following ``continue`` tokens. Returns (items, list RV)."""
+        params: dict = {}
+        if resource_version is not None:
+            params["resourceVersion"] = resource_version
+        if limit:
+            params["limit"] = str(limit)
+        items: list = []
+        while True:
+            out = await self._req("GET", self._url(res, namespace), params=params or None)
+            items.extend(out.get("items") or [])
+            meta = out.get("metadata") or {}
+            cont = meta.get("continue")
+            if not cont:
+                return items, meta.get("resourceVersion", "0")
+            params = {"limit": str(limit), "continue": cont} if limit else {"continue": cont}
 
     async def watch(self, res: str, resource_version: str, timeout_s: int = 300) -> AsyncIterator[tuple[str, dict]]:
         s = await self.session()
@@ -180,9 +196,7 @@ class KubeClient:
                     typ, obj = ev.get("type"), ev.get("object") or {}
                     if typ == "ERROR":
                         raise ApiError(int(obj.get("code", 500)), obj.get("reason", "Error"), obj.get("message", ""))
-                    if typ == "BOOKMARK":
-                        continue
-                    yield typ, obj
+                    yield typ, obj          # BOOKMARK too: the informer advances its RV
 
     async def get(self, res: str, name: str, namespace: Optional[str] = None) -> dict:
         return await self._req("GET", self._url(res, namespace, name))

@@ -31,6 +31,9 @@ class Informer:
         self.resource_version = "0"
         self.relist_backoff = relist_backoff
         self.relists = 0
+        self.bookmarks = 0
+        self.page_size = 500            # client-go pager default
+        self._consistent_relist = False
         self._stop = False
 
     def _dispatch(self, typ: str, obj: dict) -> None:
@@ -52,7 +55,13 @@ class Informer:
             self.resource_version = rv
 
     async def _list(self) -> None:
-        items, rv = await self.client.list(self.res)
+        # client-go reflector: the first list may come from the watch cache (RV "0");
+        # after a 410 the relist is a consistent read, paged like client-go's pager
+        if self._consistent_relist:
+            items, rv = await self.client.list(self.res, resource_version="", limit=self.page_size)
+            self._consistent_relist = False
+        else:
+            items, rv = await self.client.list(self.res, resource_version="0")
         fresh = {obj_key(self.r, o): o for o in items}
         # deletions that happened while we were not watching
         for key in [k for k in self.store if k not in fresh]:
@@ -83,6 +92,12 @@ class Informer:
                     if typ == "ERROR":
                         need_list = True
                         break
+                    if typ == "BOOKMARK":
+                        rv = (obj.get("metadata") or {}).get("resourceVersion")
+                        if rv:
+                            self.resource_version = rv
+                            self.bookmarks += 1
+                        continue
                     self._dispatch(typ, obj)
                     if self._stop:
                         return
@@ -90,6 +105,7 @@ class Informer:
             except ApiError as e:
                 if e.code == 410:
                     need_list = True
+                    self._consistent_relist = True
                 else:
                     log.warning("informer %s: %s", self.res, e)
                     await asyncio.sleep(self.relist_backoff)
