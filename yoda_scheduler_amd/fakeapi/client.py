@@ -21,19 +21,20 @@ class InProcessClient:
             await asyncio.sleep(self.server.faults.latency_s)
 
     async def list(self, res: str, namespace: Optional[str] = None, resource_version: Optional[str] = None,
-                   limit: int = 0) -> tuple[list[dict], str]:
+                   limit: int = 0, field_selector: Optional[str] = None) -> tuple[list[dict], str]:
         await self._lat()
         if not limit:
-            return self.server.list(res, namespace)
+            return self.server.list(res, namespace, field_selector)
         items, cont = [], ""
         while True:
-            page, rv, cont = self.server.list_page(res, namespace, limit, cont)
+            page, rv, cont = self.server.list_page(res, namespace, limit, cont, field_selector)
             items.extend(page)
             if not cont:
                 return items, rv
 
-    async def watch(self, res: str, resource_version: str) -> AsyncIterator[tuple[str, dict]]:
-        w = self.server.watch(res, resource_version)
+    async def watch(self, res: str, resource_version: str,
+                    field_selector: Optional[str] = None) -> AsyncIterator[tuple[str, dict]]:
+        w = self.server.watch(res, resource_version, field_selector)
         try:
             async for ev in w:
                 yield ev

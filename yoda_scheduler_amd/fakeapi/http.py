@@ -122,13 +122,14 @@ class FakeApiHttp:
         try:
             if req.method == "GET":
                 if name is None:
+                    fsel = req.query.get("fieldSelector") or None
                     if req.query.get("watch") in ("1", "true"):
-                        return await self._watch(req, res, req.query.get("resourceVersion", "0"))
+                        return await self._watch(req, res, req.query.get("resourceVersion", "0"), fsel)
                     limit, cont = int(req.query.get("limit", "0") or 0), req.query.get("continue", "")
                     if limit or cont:
-                        items, rv, nxt = s.list_page(res, ns, limit, cont)
+                        items, rv, nxt = s.list_page(res, ns, limit, cont, fsel)
                     else:
-                        (items, rv), nxt = s.list(res, ns), ""
+                        (items, rv), nxt = s.list(res, ns, fsel), ""
                     meta = {"resourceVersion": rv}
                     if nxt:
                         meta["continue"] = nxt
@@ -153,9 +154,9 @@ class FakeApiHttp:
             return _status(e)
         return _status(ApiError(405, "MethodNotAllowed", req.method))
 
-    async def _watch(self, req: web.Request, res: str, rv: str) -> web.StreamResponse:
+    async def _watch(self, req: web.Request, res: str, rv: str, fsel: Optional[str] = None) -> web.StreamResponse:
         try:
-            w = self.server.watch(res, rv)
+            w = self.server.watch(res, rv, fsel)
         except ApiError as e:
             resp = web.StreamResponse(status=200, headers={"Content-Type": "application/json"})
             await resp.prepare(req)

@@ -31,6 +31,8 @@ from dataclasses import dataclass
 from typing import Optional
 
 from ..kube.errors import ApiError, already_exists, conflict, gone, not_found
+from ..kube.fields import FieldSelector, filter_event
+from ..kube.fields import parse as parse_fields
 from ..kube.resources import RESOURCES, obj_key, resource
 from ..models.scv import rfc3339
 
@@ -48,11 +50,12 @@ class Faults:
 
 
 class Watch:
-    __slots__ = ("resource", "queue", "closed", "sent", "server")
+    __slots__ = ("resource", "queue", "closed", "sent", "server", "selector")
 
-    def __init__(self, server: "FakeApiServer", resource: str) -> None:
+    def __init__(self, server: "FakeApiServer", resource: str, selector: Optional[FieldSelector] = None) -> None:
         self.server = server
         self.resource = resource
+        self.selector = selector
         self.queue: asyncio.Queue = asyncio.Queue()
         self.closed = False
         self.sent = 0
@@ -107,14 +110,19 @@ class FakeApiServer:
         self._last_rv = next(self._rv)
         return str(self._last_rv)
 
-    def _emit(self, res: str, typ: str, obj: dict) -> None:
+    def _emit(self, res: str, typ: str, obj: dict, old: Optional[dict] = None) -> None:
         rv = int(obj["metadata"]["resourceVersion"])
         h = self._history[res]
         if len(h) == h.maxlen:
             self._oldest_rv[res] = h[0][0]
-        h.append((rv, typ, obj))
+        h.append((rv, typ, obj, old))
         for w in tuple(self._watchers[res]):
-            w.push((typ, obj))
+            if w.selector is None:
+                w.push((typ, obj))
+            else:
+                ev = filter_event(w.selector, typ, obj, old)
+                if ev is not None:
+                    w.push(ev)
 
     @staticmethod
     def _with_meta(obj: dict, **meta) -> dict:
@@ -181,7 +189,7 @@ class FakeApiServer:
                                                    if k not in ("uid", "creationTimestamp", "resourceVersion")})
         new["metadata"]["resourceVersion"] = self._next_rv()
         self._objs[res][obj_key(r, new)] = new
-        self._emit(res, "MODIFIED", new)
+        self._emit(res, "MODIFIED", new, cur)
         return new
 
     def patch(self, res: str, name: str, patch: dict, namespace: Optional[str] = None) -> dict:
@@ -195,7 +203,7 @@ class FakeApiServer:
             if k in cur["metadata"]:
                 new["metadata"][k] = cur["metadata"][k]
         self._objs[res][obj_key(resource(res), new)] = new
-        self._emit(res, "MODIFIED", new)
+        self._emit(res, "MODIFIED", new, cur)
         return new
 
     def delete(self, res: str, name: str, namespace: Optional[str] = None) -> dict:
@@ -209,15 +217,19 @@ class FakeApiServer:
         self._emit(res, "DELETED", gone_obj)
         return gone_obj
 
-    def list(self, res: str, namespace: Optional[str] = None) -> tuple[list[dict], str]:
+    def list(self, res: str, namespace: Optional[str] = None,
+             field_selector: Optional[str] = None) -> tuple[list[dict], str]:
         self.calls["list"] += 1
         items = list(self._objs[res].values())
         if namespace and resource(res).namespaced:
             items = [o for o in items if o["metadata"].get("namespace") == namespace]
+        sel = parse_fields(field_selector)
+        if sel is not None:
+            items = [o for o in items if sel.matches(o)]
         return items, str(self._last_rv)
 
     def list_page(self, res: str, namespace: Optional[str] = None, limit: int = 0,
-                  cont: str = "") -> tuple[list[dict], str, str]:
+                  cont: str = "", field_selector: Optional[str] = None) -> tuple[list[dict], str, str]:
         """Chunked list (``limit`` / ``continue``): items in key order; the continue token
         pins the list's resourceVersion and the last key served, like the apiserver's. A
         token older than the watch history window is expired (410)."""
@@ -235,6 +247,9 @@ class FakeApiServer:
         keys = sorted(k for k in self._objs[res] if k > start)
         if namespace and resource(res).namespaced:
             keys = [k for k in keys if self._objs[res][k]["metadata"].get("namespace") == namespace]
+        sel = parse_fields(field_selector)
+        if sel is not None:
+            keys = [k for k in keys if sel.matches(self._objs[res][k])]
         nxt = ""
         if limit and len(keys) > limit:
             keys = keys[:limit]
@@ -248,16 +263,19 @@ class FakeApiServer:
         for w in tuple(self._watchers[res]):
             w.push(("BOOKMARK", obj))
 
-    def watch(self, res: str, resource_version: str = "0") -> Watch:
+    def watch(self, res: str, resource_version: str = "0", field_selector: Optional[str] = None) -> Watch:
         self.calls["watch"] += 1
         rv = int(resource_version or 0)
         if rv and rv < self._oldest_rv[res]:
             raise gone()
-        w = Watch(self, res)
+        sel = parse_fields(field_selector)
+        w = Watch(self, res, sel)
         if rv:
-            for erv, typ, obj in self._history[res]:
+            for erv, typ, obj, old in self._history[res]:
                 if erv > rv:
-                    w.queue.put_nowait((typ, obj))
+                    ev = (typ, obj) if sel is None else filter_event(sel, typ, obj, old)
+                    if ev is not None:
+                        w.queue.put_nowait(ev)
         self._watchers[res].add(w)
         return w
 
@@ -297,7 +315,7 @@ class FakeApiServer:
         self._objs["pods"][key] = new
         self.bind_log[key] = self.clock()
         self.bind_node[key] = node
-        self._emit("pods", "MODIFIED", new)
+        self._emit("pods", "MODIFIED", new, cur)
         return new
 
     # ------------------------------------------------------------------ bench helpers

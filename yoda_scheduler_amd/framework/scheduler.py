@@ -38,6 +38,7 @@ from .runtime import Framework
 log = logging.getLogger("yoda.scheduler")
 
 _EMPTY_STATE = CycleState()      # shared read-only state for all-native cycles
+POD_FIELD_SELECTOR = "status.phase!=Succeeded,status.phase!=Failed"   # upstream NewPodInformer
 _VOLATILE_META = ("resourceVersion", "generation", "managedFields")
 
 
@@ -267,7 +268,9 @@ class Scheduler:
         self.informers = {
             "nodes": Informer(self.client, "nodes", self.on_node_add, self.on_node_update, self.on_node_delete),
             "scvs": Informer(self.client, "scvs", self.on_scv, self.on_scv_update, self.on_scv_delete),
-            "pods": Informer(self.client, "pods", self.on_pod_add, self.on_pod_update, self.on_pod_delete),
+            # upstream v1.20 scheduler pod informer: terminal pods are filtered by the apiserver
+            "pods": Informer(self.client, "pods", self.on_pod_add, self.on_pod_update, self.on_pod_delete,
+                             field_selector=POD_FIELD_SELECTOR),
         }
         # objects only some plugins need (PVCs, PVs, StorageClasses, CSINodes): watched when
         # an enabled plugin declares them; any change may make a parked pod schedulable

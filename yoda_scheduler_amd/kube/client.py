@@ -155,7 +155,7 @@ class KubeClient:
 
     # ------------------------------------------------------------------ verbs
     async def list(self, res: str, namespace: Optional[str] = None, resource_version: Optional[str] = None,
-                   limit: int = 0) -> tuple[list[dict], str]:
+                   limit: int = 0, field_selector: Optional[str] = None) -> tuple[list[dict], str]:
         """List (client-go pager semantics): ``resource_version="0"`` may be served from the
         apiserver's watch cache (which ignores ``limit``); otherwise a consistent read in
         ``limit``-sized chunks, following ``continue`` tokens. Returns (items, list RV)."""
@@ -164,6 +164,8 @@ class KubeClient:
             params["resourceVersion"] = resource_version
         if limit:
             params["limit"] = str(limit)
+        if field_selector:
+            params["fieldSelector"] = field_selector
         items: list = []
         while True:
             out = await self._req("GET", self._url(res, namespace), params=params or None)
@@ -173,11 +175,16 @@ class KubeClient:
             if not cont:
                 return items, meta.get("resourceVersion", "0")
             params = {"limit": str(limit), "continue": cont} if limit else {"continue": cont}
+            if field_selector:
+                params["fieldSelector"] = field_selector
 
-    async def watch(self, res: str, resource_version: str, timeout_s: int = 300) -> AsyncIterator[tuple[str, dict]]:
+    async def watch(self, res: str, resource_version: str, field_selector: Optional[str] = None,
+                    timeout_s: int = 300) -> AsyncIterator[tuple[str, dict]]:
         s = await self.session()
         params = {"watch": "1", "resourceVersion": resource_version or "0", "allowWatchBookmarks": "true",
                   "timeoutSeconds": str(timeout_s)}
+        if field_selector:
+            params["fieldSelector"] = field_selector
         async with s.get(self._url(res), params=params,
                          timeout=aiohttp.ClientTimeout(total=None, sock_read=timeout_s + 30)) as r:
             if r.status >= 400:

@@ -21,8 +21,10 @@ Handler = Callable[[dict], None]
 class Informer:
     def __init__(self, client, res: str, on_add: Optional[Handler] = None,
                  on_update: Optional[Callable[[dict, dict], None]] = None,
-                 on_delete: Optional[Handler] = None, relist_backoff: float = 0.2) -> None:
+                 on_delete: Optional[Handler] = None, relist_backoff: float = 0.2,
+                 field_selector: Optional[str] = None) -> None:
         self.client = client
+        self.field_selector = field_selector
         self.res = res
         self.r = resource(res)
         self.on_add, self.on_update, self.on_delete = on_add, on_update, on_delete
@@ -54,14 +56,18 @@ class Informer:
         if rv:
             self.resource_version = rv
 
+    def _fs(self) -> dict:
+        return {"field_selector": self.field_selector} if self.field_selector else {}
+
     async def _list(self) -> None:
         # client-go reflector: the first list may come from the watch cache (RV "0");
         # after a 410 the relist is a consistent read, paged like client-go's pager
         if self._consistent_relist:
-            items, rv = await self.client.list(self.res, resource_version="", limit=self.page_size)
+            items, rv = await self.client.list(self.res, resource_version="", limit=self.page_size,
+                                               **self._fs())
             self._consistent_relist = False
         else:
-            items, rv = await self.client.list(self.res, resource_version="0")
+            items, rv = await self.client.list(self.res, resource_version="0", **self._fs())
         fresh = {obj_key(self.r, o): o for o in items}
         # deletions that happened while we were not watching
         for key in [k for k in self.store if k not in fresh]:
@@ -88,7 +94,7 @@ class Informer:
                     await self._list()
                     self.synced.set()
                     need_list = False
-                async for typ, obj in self.client.watch(self.res, self.resource_version):
+                async for typ, obj in self.client.watch(self.res, self.resource_version, **self._fs()):
                     if typ == "ERROR":
                         need_list = True
                         break
