@@ -125,6 +125,18 @@ def test_queue_delete_and_update():
     assert q.pop_nowait().gpu.priority == 3
 
 
+def test_queue_update_resorts_active_pod():
+    """A priority edit on a pod waiting in activeQ re-sorts it (upstream activeQ.Update);
+    among equal priorities the original FIFO order is kept."""
+    q = SchedulingQueue(lambda p: (-p.gpu.priority,))
+    for n in ("a", "b", "c"):
+        q.add(_pi(n, 1))
+    q.update(_pi("c", 9))
+    q.update(_pi("a", 1))                     # unchanged key: stays first among the 1s
+    assert [q.pop_nowait().name for _ in range(3)] == ["c", "a", "b"]
+    assert q.pop_nowait() is None and len(q) == 0
+
+
 def test_queue_async_pop_wakes():
     async def run():
         q = SchedulingQueue(lambda p: (0,))

@@ -87,8 +87,16 @@ class SchedulingQueue:
             self._push_active(pi)
             return
         pi.attempts, pi.initial_attempt = old.attempts, old.initial_attempt
-        if pi.uid in self._active_entries:
-            self._pods[pi.uid] = pi      # heap entry stays; the info is refreshed
+        entry = self._active_entries.get(pi.uid)
+        if entry is not None:
+            self._pods[pi.uid] = pi      # the info is refreshed
+            key = self._sort_key(pi)
+            if tuple(entry[:len(key)]) != tuple(key):
+                # order changed (e.g. scv/priority edited): re-sort like upstream's
+                # activeQ.Update, keeping the original FIFO sequence number
+                new = (*key, entry[-2], pi.uid)
+                self._active_entries[pi.uid] = new
+                heapq.heappush(self._active, new)
             return
         # an update may make an unschedulable pod schedulable: retry now
         self._remove_parked(pi.uid)
