@@ -49,16 +49,64 @@ def test_review_validate_and_mutate():
     # mutate: scv pods left on the default scheduler go to the yoda profile
     m = review(ar({"scv/memory": "1000"}), mutate=True)["response"]
     assert m["allowed"] and m["patchType"] == "JSONPatch"
-    assert json.loads(base64.b64decode(m["patch"])) == [
-        {"op": "add", "path": "/spec/schedulerName", "value": "yoda-scheduler"}]
+    ops = json.loads(base64.b64decode(m["patch"]))
+    assert ops[0] == {"op": "add", "path": "/spec/schedulerName", "value": "yoda-scheduler"}
+    assert [o["path"] for o in ops[1:]] == ["/spec/containers/0/env"]          # GPU pinning, below
     m = review(ar({"scv/memory": "1000"}, scheduler="default-scheduler"), mutate=True)["response"]
     assert json.loads(base64.b64decode(m["patch"]))[0]["op"] == "replace"
-    # explicit profile, non-scv pods and updates are left alone
-    assert "patch" not in review(ar({"scv/memory": "1"}, scheduler="yoda-scheduler2"), mutate=True)["response"]
+    # an explicit yoda profile keeps its name (only the GPU pinning is added); non-scv pods,
+    # other schedulers and updates are left alone
+    ops = json.loads(base64.b64decode(review(ar({"scv/memory": "1"}, scheduler="yoda-scheduler2"),
+                                             mutate=True)["response"]["patch"]))
+    assert [o["path"] for o in ops] == ["/spec/containers/0/env"]
+    assert "patch" not in review(ar({"scv/memory": "1"}, scheduler="other"), mutate=True)["response"]
     assert "patch" not in review(ar({"app": "web"}), mutate=True)["response"]
     assert "patch" not in review(ar({"scv/memory": "1"}, op="UPDATE"), mutate=True)["response"]
     assert "patch" not in review(ar({"scv/memory": "1"}), mutate=True,
-                                 policy=AdmissionPolicy(mutate_scheduler_name=False))["response"]
+                                 policy=AdmissionPolicy(mutate_scheduler_name=False,
+                                                        inject_visible_devices=False))["response"]
+
+
+def _apply(doc, ops):
+    """Minimal RFC 6902 ``add`` (what the webhook emits)."""
+    import copy
+    doc = copy.deepcopy(doc)
+    for o in ops:
+        parts = o["path"].strip("/").split("/")
+        tgt = doc
+        for k in parts[:-1]:
+            tgt = tgt[int(k)] if isinstance(tgt, list) else tgt[k]
+        last = parts[-1]
+        if isinstance(tgt, list):
+            tgt.append(o["value"]) if last == "-" else tgt.insert(int(last), o["value"])
+        else:
+            tgt[last] = o["value"]
+    return doc
+
+
+def test_visible_devices_injection():
+    """Containers of yoda pods read the GPU assignment through the downward API; the
+    Binding copies ``scv.amd.com/gpus`` onto the pod before containers start."""
+    body = ar({"scv/number": "2"}, scheduler="yoda-scheduler")
+    spec = body["request"]["object"]["spec"]
+    spec["containers"].append({"name": "side", "image": "y", "env": [{"name": "A", "value": "1"}]})
+    spec["containers"].append({"name": "own", "image": "z", "env": [{"name": "HIP_VISIBLE_DEVICES", "value": "3"}]})
+    spec["initContainers"] = [{"name": "init", "image": "w"}]
+    ops = json.loads(base64.b64decode(review(body, mutate=True)["response"]["patch"]))
+    pod = _apply(body["request"]["object"], ops)
+    ref = {"fieldRef": {"fieldPath": "metadata.annotations['scv.amd.com/gpus']"}}
+    for c in (pod["spec"]["containers"][0], pod["spec"]["containers"][1], pod["spec"]["initContainers"][0]):
+        env = {e["name"]: e.get("valueFrom") for e in c["env"]}
+        assert env["HIP_VISIBLE_DEVICES"] == ref and env["ROCR_VISIBLE_DEVICES"] == ref
+    assert pod["spec"]["containers"][1]["env"][0] == {"name": "A", "value": "1"}
+    assert pod["spec"]["containers"][2]["env"] == [{"name": "HIP_VISIBLE_DEVICES", "value": "3"}]   # untouched
+    # device-plugin pods and opted-out pods are left alone
+    dp = ar({"scv/number": "1"}, scheduler="yoda-scheduler")
+    dp["request"]["object"]["spec"]["containers"][0]["resources"] = {"limits": {"amd.com/gpu": "1"}}
+    assert "patch" not in review(dp, mutate=True)["response"]
+    out = ar({"scv/number": "1"}, scheduler="yoda-scheduler")
+    out["request"]["object"]["metadata"]["annotations"] = {"scv.amd.com/inject-visible-devices": "false"}
+    assert "patch" not in review(out, mutate=True)["response"]
 
 
 def test_webhook_over_https(tmp_path):

@@ -21,6 +21,8 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     p.add_argument("--tls-private-key-file", default="")
     p.add_argument("--scheduler-name", default="yoda-scheduler", help="profile pods with scv labels are sent to")
     p.add_argument("--no-mutate-scheduler-name", action="store_true")
+    p.add_argument("--no-inject-visible-devices", action="store_true",
+                   help="do not add HIP/ROCR_VISIBLE_DEVICES (downward API of scv.amd.com/gpus) to yoda pods")
     p.add_argument("--max-gpus-per-pod", type=int, default=64)
     p.add_argument("--max-memory-mb", type=int, default=288 * 1024)
     p.add_argument("--v", type=int, default=0)
@@ -30,7 +32,8 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     if a.tls_cert_file:
         ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
         ctx.load_cert_chain(a.tls_cert_file, a.tls_private_key_file or None)
-    pol = AdmissionPolicy(a.max_gpus_per_pod, a.max_memory_mb, a.scheduler_name, not a.no_mutate_scheduler_name)
+    pol = AdmissionPolicy(a.max_gpus_per_pod, a.max_memory_mb, a.scheduler_name, not a.no_mutate_scheduler_name,
+                          not a.no_inject_visible_devices)
 
     async def run() -> int:
         srv = WebhookServer(a.bind_address, a.port, pol, ctx)

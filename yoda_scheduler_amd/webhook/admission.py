@@ -9,6 +9,13 @@ a warning (typos such as ``scv/memroy`` would otherwise be ignored silently).
 Mutation (``/mutate``, optional): pods that carry scv labels but left
 ``spec.schedulerName`` at the default are pointed at ``schedulerName`` (the yoda profile),
 so users cannot forget the profile name (quirk Q6 made that easy in the reference).
+Their containers also get ``HIP_VISIBLE_DEVICES`` / ``ROCR_VISIBLE_DEVICES`` from the
+downward API (``metadata.annotations['scv.amd.com/gpus']``): the Binding copies the
+scheduler's GPU assignment onto the pod before any container starts, so the process sees
+exactly the GPUs whose HBM the scheduler reserved (the reference only picked a node, Q10).
+Containers that set either variable themselves, pods that request ``amd.com/gpu`` through
+the device plugin, and pods annotated ``scv.amd.com/inject-visible-devices: "false"`` are
+left alone.
 """
 from __future__ import annotations
 
@@ -25,12 +32,19 @@ KNOWN = set(_UNSIGNED) | {LABEL_PRIORITY, "scv.amd.com/gang"}
 GANG_VALUES = ("xgmi", "any", "numa")
 
 
+ANNOTATION_GPUS = "scv.amd.com/gpus"
+ANNOTATION_NO_INJECT = "scv.amd.com/inject-visible-devices"
+VISIBLE_ENV = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES")
+
+
 @dataclass
 class AdmissionPolicy:
     max_gpus_per_pod: int = 64            # 8 GPUs × CPX partitions
     max_memory_mb: int = MI355X_HBM_MB
     scheduler_name: str = "yoda-scheduler"
     mutate_scheduler_name: bool = True
+    inject_visible_devices: bool = True
+    yoda_profiles: tuple = ("yoda-scheduler", "yoda-scheduler2")   # deploy/yoda-scheduler.yaml
 
 
 def _is_decimal(v: str, signed: bool) -> bool:
@@ -71,15 +85,50 @@ def _uses_scv(labels: dict) -> bool:
     return any(k in KNOWN for k in labels)
 
 
+def _requests_device_plugin_gpus(c: dict) -> bool:
+    res = c.get("resources") or {}
+    return any(k.startswith("amd.com/") for part in ("limits", "requests") for k in (res.get(part) or {}))
+
+
+def _visible_devices_ops(pod: dict) -> list:
+    spec = pod.get("spec") or {}
+    ann = (pod.get("metadata") or {}).get("annotations") or {}
+    if str(ann.get(ANNOTATION_NO_INJECT, "")).lower() == "false":
+        return []
+    ops = []
+    for key in ("initContainers", "containers"):
+        cs = spec.get(key) or []
+        if any(_requests_device_plugin_gpus(c) for c in cs):
+            return []          # the device plugin owns GPU visibility for this pod
+        for i, c in enumerate(cs):
+            env = c.get("env")
+            names = {e.get("name") for e in env or ()}
+            if names & set(VISIBLE_ENV):
+                continue
+            vals = [{"name": n, "valueFrom": {"fieldRef": {"fieldPath": f"metadata.annotations['{ANNOTATION_GPUS}']"}}}
+                    for n in VISIBLE_ENV]
+            if env is None:
+                ops.append({"op": "add", "path": f"/spec/{key}/{i}/env", "value": vals})
+            else:
+                ops.extend({"op": "add", "path": f"/spec/{key}/{i}/env/-", "value": v} for v in vals)
+    return ops
+
+
 def _patch(pod: dict, policy: AdmissionPolicy) -> list:
     spec = pod.get("spec") or {}
     labels = (pod.get("metadata") or {}).get("labels") or {}
-    if not policy.mutate_scheduler_name or not _uses_scv(labels):
+    if not _uses_scv(labels):
         return []
-    if spec.get("schedulerName") not in (None, "", "default-scheduler"):
-        return []
-    op = "replace" if "schedulerName" in spec else "add"
-    return [{"op": op, "path": "/spec/schedulerName", "value": policy.scheduler_name}]
+    ops = []
+    target = spec.get("schedulerName")
+    if policy.mutate_scheduler_name and target in (None, "", "default-scheduler"):
+        ops.append({"op": "replace" if "schedulerName" in spec else "add", "path": "/spec/schedulerName",
+                    "value": policy.scheduler_name})
+        target = policy.scheduler_name
+    # only pods the yoda profile schedules get an assignment annotation to read
+    if policy.inject_visible_devices and (target == policy.scheduler_name or target in policy.yoda_profiles):
+        ops.extend(_visible_devices_ops(pod))
+    return ops
 
 
 def review(body: dict, mutate: bool, policy: AdmissionPolicy = AdmissionPolicy()) -> dict:
