@@ -5,6 +5,8 @@ pod with a GPU assignment annotation → executor starts a ROCm process pinned w
 HIP_VISIBLE_DEVICES that allocates the pod's HBM → the next amd-smi sample shows the drop,
 and the new Scv makes the scheduler see it (ledger pending → sampled)."""
 import asyncio
+import base64
+import json
 import time
 
 import pytest
@@ -23,6 +25,7 @@ def test_minimum_end_to_end_slice(require_gpu):
     from yoda_scheduler_amd.sniffer.executor import PodExecutor
     from yoda_scheduler_amd.sniffer.publisher import SnifferAgent
     from yoda_scheduler_amd.testing import yoda_config
+    from yoda_scheduler_amd.webhook.admission import apply_add_ops, review
 
     MB = 4096
 
@@ -36,8 +39,15 @@ def test_minimum_end_to_end_slice(require_gpu):
         sched = Scheduler(cl, parse_config(yoda_config(yoda_args={"sampleSettleSeconds": 0.0})))
         await sched.start()
         loop_t = asyncio.get_event_loop().create_task(sched.scheduling_loop())
-        srv.create("pods", {"metadata": {"name": "slice", "namespace": "default", "labels": {"scv/memory": str(MB)}},
-                            "spec": {"schedulerName": "yoda-scheduler"}})
+        # admission first: the webhook points the pod at the yoda profile and pins its
+        # containers to the assignment through the downward API
+        obj = {"metadata": {"name": "slice", "namespace": "default", "labels": {"scv/memory": str(MB)}},
+               "spec": {"containers": [{"name": "main", "image": "rocm/pytorch"}]}}
+        resp = review({"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
+                       "request": {"uid": "u", "kind": {"kind": "Pod"}, "operation": "CREATE", "object": obj}},
+                      mutate=True)["response"]
+        obj = apply_add_ops(obj, json.loads(base64.b64decode(resp["patch"])))
+        srv.create("pods", obj)
         for _ in range(2000):
             if srv.bind_log:
                 break
@@ -56,11 +66,13 @@ def test_minimum_end_to_end_slice(require_gpu):
             ex.stop_all()
             await sched.shutdown()
             loop_t.cancel()
-        return pod, ok, r.log, before, after, gpu_state
+        return pod, ok, r.log, before, after, gpu_state, ex.env_log["default/slice"]
 
-    pod, ok, log, before, after, gpu_state = asyncio.run(go())
+    pod, ok, log, before, after, gpu_state, env = asyncio.run(go())
     gpus = [int(x) for x in pod["metadata"]["annotations"]["scv.amd.com/gpus"].split(",")]
     assert len(gpus) == 1
+    assert pod["spec"]["schedulerName"] == "yoda-scheduler"
+    assert env["HIP_VISIBLE_DEVICES"] == env["ROCR_VISIBLE_DEVICES"] == str(gpus[0])   # via the downward API
     assert ok, log
     g = gpus[0]
     drop = before.status.card_list[g].free_memory - after.status.card_list[g].free_memory

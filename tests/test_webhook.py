@@ -10,7 +10,7 @@ import subprocess
 
 import pytest
 
-from yoda_scheduler_amd.webhook.admission import AdmissionPolicy, review, validate_labels
+from yoda_scheduler_amd.webhook.admission import AdmissionPolicy, apply_add_ops, review, validate_labels
 
 
 def ar(labels, scheduler=None, op="CREATE", uid="u1"):
@@ -67,23 +67,6 @@ def test_review_validate_and_mutate():
                                                         inject_visible_devices=False))["response"]
 
 
-def _apply(doc, ops):
-    """Minimal RFC 6902 ``add`` (what the webhook emits)."""
-    import copy
-    doc = copy.deepcopy(doc)
-    for o in ops:
-        parts = o["path"].strip("/").split("/")
-        tgt = doc
-        for k in parts[:-1]:
-            tgt = tgt[int(k)] if isinstance(tgt, list) else tgt[k]
-        last = parts[-1]
-        if isinstance(tgt, list):
-            tgt.append(o["value"]) if last == "-" else tgt.insert(int(last), o["value"])
-        else:
-            tgt[last] = o["value"]
-    return doc
-
-
 def test_visible_devices_injection():
     """Containers of yoda pods read the GPU assignment through the downward API; the
     Binding copies ``scv.amd.com/gpus`` onto the pod before containers start."""
@@ -93,7 +76,7 @@ def test_visible_devices_injection():
     spec["containers"].append({"name": "own", "image": "z", "env": [{"name": "HIP_VISIBLE_DEVICES", "value": "3"}]})
     spec["initContainers"] = [{"name": "init", "image": "w"}]
     ops = json.loads(base64.b64decode(review(body, mutate=True)["response"]["patch"]))
-    pod = _apply(body["request"]["object"], ops)
+    pod = apply_add_ops(body["request"]["object"], ops)
     ref = {"fieldRef": {"fieldPath": "metadata.annotations['scv.amd.com/gpus']"}}
     for c in (pod["spec"]["containers"][0], pod["spec"]["containers"][1], pod["spec"]["initContainers"][0]):
         env = {e["name"]: e.get("valueFrom") for e in c["env"]}
@@ -154,3 +137,15 @@ def test_deploy_manifest_and_cli_entry():
     from yoda_scheduler_amd.cmd.webhook import main
     with pytest.raises(SystemExit):
         main(["--help"])
+
+
+def test_executor_resolves_downward_api_env():
+    from yoda_scheduler_amd.sniffer.executor import resolve_env
+    body = ar({"scv/number": "2"}, scheduler="yoda-scheduler")
+    ops = json.loads(base64.b64decode(review(body, mutate=True)["response"]["patch"]))
+    pod = apply_add_ops(body["request"]["object"], ops)
+    pod["metadata"]["annotations"] = {"scv.amd.com/gpus": "3,5"}      # written by the Binding
+    pod["spec"]["containers"][0]["env"].append({"name": "NODE", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}})
+    pod["spec"]["nodeName"] = "n7"
+    env = resolve_env(pod, pod["spec"]["containers"][0])
+    assert env == {"HIP_VISIBLE_DEVICES": "3,5", "ROCR_VISIBLE_DEVICES": "3,5", "NODE": "n7"}

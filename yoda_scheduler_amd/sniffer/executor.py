@@ -31,6 +31,38 @@ time.sleep(secs)
 """
 
 
+def _field(pod: dict, path: str) -> str:
+    """Downward-API ``fieldRef.fieldPath``: ``metadata.annotations['k']`` /
+    ``metadata.labels['k']`` and plain dotted paths (``metadata.name``, ``spec.nodeName``)."""
+    for kind in ("annotations", "labels"):
+        pre = f"metadata.{kind}['"
+        if path.startswith(pre) and path.endswith("']"):
+            return str(((pod.get("metadata") or {}).get(kind) or {}).get(path[len(pre):-2], ""))
+    v = pod
+    for k in path.split("."):
+        v = v.get(k) if isinstance(v, dict) else None
+        if v is None:
+            return ""
+    return str(v)
+
+
+def resolve_env(pod: dict, container: dict) -> dict:
+    """A container's environment as the kubelet builds it (``value`` and downward-API
+    ``fieldRef`` entries; later entries win)."""
+    out = {}
+    for e in container.get("env") or ():
+        name = e.get("name")
+        if not name:
+            continue
+        if "value" in e:
+            out[name] = str(e["value"])
+        else:
+            ref = (e.get("valueFrom") or {}).get("fieldRef") or {}
+            if ref.get("fieldPath"):
+                out[name] = _field(pod, ref["fieldPath"])
+    return out
+
+
 @dataclass
 class Running:
     key: str
@@ -46,6 +78,7 @@ class PodExecutor:
         self.node = node
         self.hold_seconds = hold_seconds
         self.running: dict[str, Running] = {}
+        self.env_log: dict[str, dict] = {}
 
     def launch(self, pod: dict) -> Optional[Running]:
         meta = pod.get("metadata") or {}
@@ -55,9 +88,17 @@ class PodExecutor:
         ann = meta.get("annotations") or {}
         gpus = [int(x) for x in (ann.get(ANNOTATION_GPUS) or "").split(",") if x.strip()]
         mb = int((meta.get("labels") or {}).get(LABEL_MEMORY, "0") or 0)
-        env = dict(os.environ, HIP_VISIBLE_DEVICES=",".join(map(str, gpus)),
-                   ROCR_VISIBLE_DEVICES=",".join(map(str, gpus)))
+        containers = (pod.get("spec") or {}).get("containers") or [{}]
+        spec_env = resolve_env(pod, containers[0])
+        env = dict(os.environ)
         env.pop("CUDA_VISIBLE_DEVICES", None)
+        if "HIP_VISIBLE_DEVICES" in spec_env or "ROCR_VISIBLE_DEVICES" in spec_env:
+            # pinned by the pod spec (yoda-webhook's downward-API injection)
+            env.update(spec_env)
+        else:
+            env.update(spec_env, HIP_VISIBLE_DEVICES=",".join(map(str, gpus)),
+                       ROCR_VISIBLE_DEVICES=",".join(map(str, gpus)))
+        self.env_log[key] = {k: env.get(k) for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES")}
         proc = subprocess.Popen([sys.executable, "-c", HOLD_SCRIPT, str(mb), str(self.hold_seconds)], env=env,
                                 stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         r = Running(key, gpus, mb, proc)

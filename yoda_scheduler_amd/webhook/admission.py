@@ -152,3 +152,26 @@ def review(body: dict, mutate: bool, policy: AdmissionPolicy = AdmissionPolicy()
                 resp["patch"] = base64.b64encode(json.dumps(ops).encode()).decode()
     return {"apiVersion": body.get("apiVersion", "admission.k8s.io/v1"), "kind": "AdmissionReview",
             "response": resp}
+
+
+def apply_add_ops(doc: dict, ops: list) -> dict:
+    """Apply the RFC 6902 ``add``/``replace`` operations this webhook emits (what the
+    apiserver does with the response patch) — for tests and the local demo path."""
+    import copy
+    doc = copy.deepcopy(doc)
+    for o in ops:
+        parts = o["path"].strip("/").split("/")
+        tgt = doc
+        for k in parts[:-1]:
+            tgt = tgt[int(k)] if isinstance(tgt, list) else tgt.setdefault(k, {})
+        last = parts[-1]
+        if isinstance(tgt, list):
+            if last == "-":
+                tgt.append(o["value"])
+            elif o["op"] == "replace":
+                tgt[int(last)] = o["value"]
+            else:
+                tgt.insert(int(last), o["value"])
+        else:
+            tgt[last] = o["value"]
+    return doc
