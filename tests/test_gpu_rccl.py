@@ -21,7 +21,8 @@ def test_rccl_allreduce_probe_single_rank(require_gpu):
     import torch.distributed as dist
     from yoda_scheduler_amd.parallel.rccl_probe import allreduce_bandwidth
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", world_size=1, rank=0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", world_size=1, rank=0,
+                            device_id=torch.device("cuda", 0))
     try:
         res = allreduce_bandwidth([1 << 20, 64 << 20], iters=5, warmup=2)
     finally:

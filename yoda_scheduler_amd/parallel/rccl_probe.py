@@ -73,7 +73,10 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     cuda = torch.cuda.is_available()
     if cuda:
         torch.cuda.set_device(local % torch.cuda.device_count())
-    dist.init_process_group("nccl" if cuda else "gloo")
+    if cuda:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+    else:
+        dist.init_process_group("gloo")
     res = allreduce_bandwidth([parse_size(s) for s in a.sizes.split(",")], a.iters,
                               dtype=a.dtype if cuda else "float32")
     if dist.get_rank() == 0:
