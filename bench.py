@@ -58,6 +58,8 @@ def main(argv=None) -> int:
                     help="GPUs per synthetic node (BASELINE protocol item 5); default: the config's own")
     ap.add_argument("--device", choices=["auto", "on", "off"], default="auto",
                     help="gfx950 device scorer (used automatically for clusters >= 256 nodes)")
+    ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
+                    help="native batches on a worker thread, overlapped with binding (auto: with the device scorer)")
     ap.add_argument("--qps", type=float, default=5000.0, help="client QPS (deploy default 5000; reference 50)")
     ap.add_argument("--burst", type=int, default=10000, help="client burst (deploy default 10000; reference 100)")
     ap.add_argument("--reference-qps", action="store_true", help="use the reference's client limits 50/100")
@@ -108,12 +110,12 @@ def main(argv=None) -> int:
     if a.transport == "http":
         # one apiserver process per rank; bursts reuse it (the previous burst is deleted first)
         one = HttpShard(w, qps=a.qps, burst=a.burst, batch=a.batch, template=tmpl, events=not a.no_events,
-                        compat=a.compat, seed=rank * 1000, device=a.device)
+                        compat=a.compat, seed=rank * 1000, device=a.device, overlap=a.overlap)
         shards = [one] * (a.warmup + a.steps)
         loop.run_until_complete(one.start())
     else:
         shards = [Shard(w, qps=a.qps, burst=a.burst, batch=a.batch, template=tmpl, events=not a.no_events,
-                        compat=a.compat, seed=rank * 1000 + i, device=a.device) for i in range(a.warmup + a.steps)]
+                        compat=a.compat, seed=rank * 1000 + i, device=a.device, overlap=a.overlap) for i in range(a.warmup + a.steps)]
         for s in shards:
             loop.run_until_complete(s.start())
     for i in range(a.warmup):
@@ -182,7 +184,7 @@ def main(argv=None) -> int:
             "pods_unschedulable": unsched,
             "node_gpus": a.node_gpus or w.nodes[0][2],
             "client_qps": a.qps, "client_burst": a.burst, "native_batch": a.batch, "compat": a.compat,
-            "device_scorer": a.device, "device_cycles": device_cycles, "transport": a.transport,
+            "device_scorer": a.device, "overlap_engine": a.overlap, "device_cycles": device_cycles, "transport": a.transport,
             "baseline_note": "vs_baseline against BASELINE.md's derived (unmeasured) ~55 pods/s reference ceiling "
                              "(kube-scheduler v1.20 client QPS 50 / burst 100)",
             "telemetry": tels[0],

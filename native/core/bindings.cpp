@@ -1,5 +1,6 @@
 // pybind11 bindings of the native scheduling engine (module yoda_scheduler_amd._native._yoda_core).
 #include <array>
+#include <mutex>
 
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -10,6 +11,14 @@ namespace py = pybind11;
 using namespace yoda;
 
 namespace {
+
+// One process-wide engine lock: a batch scheduled on a worker thread (GIL released, see
+// schedule_batch) may overlap event-loop calls (informer updates, bind failures) on the
+// same engine. Recursive: bound methods never nest today, but a future one may.
+std::recursive_mutex g_engine_mu;
+struct EngineGuard {
+  std::lock_guard<std::recursive_mutex> g{g_engine_mu};
+};
 
 int8_t effect_of(const std::string& e) {
   if (e == "NoSchedule") return kNoSchedule;
@@ -84,10 +93,10 @@ PYBIND11_MODULE(_yoda_core, m) {
       .def(py::init<bool, int>(), py::arg("compat") = false, py::arg("threads") = 1)
       .def_property("compat", &Engine::compat, &Engine::set_compat)
       .def_property("filters", &Engine::filters, &Engine::set_filters)
-      .def("set_score_weight", &Engine::set_score_weight)
+      .def("set_score_weight", &Engine::set_score_weight, py::call_guard<EngineGuard>())
       .def("set_alloc_weights", &Engine::set_alloc_weights, py::arg("most"), py::arg("cpu"), py::arg("mem"),
-           py::arg("other"))
-      .def("score_weight", &Engine::score_weight)
+           py::arg("other"), py::call_guard<EngineGuard>())
+      .def("score_weight", &Engine::score_weight, py::call_guard<EngineGuard>())
       .def("set_gang_weights",
            [](Engine& e, int64_t link, int64_t numa, int64_t fit, int64_t occ, bool binpack, int64_t gang_score,
               int64_t enum_limit) {
@@ -96,18 +105,18 @@ PYBIND11_MODULE(_yoda_core, m) {
              w.gpu_binpack = binpack; w.w_gang_score = gang_score; w.enum_limit = enum_limit;
            },
            py::arg("link") = 4, py::arg("numa") = 2, py::arg("fit") = 1, py::arg("occ") = 1,
-           py::arg("binpack") = false, py::arg("gang_score") = 3, py::arg("enum_limit") = 5000)
-      .def("set_percentage_of_nodes_to_score", &Engine::set_percentage_of_nodes_to_score)
-      .def("seed", &Engine::seed)
-      .def("intern", &Engine::intern)
-      .def("upsert_node", &Engine::upsert_node)
-      .def("node_index", &Engine::node_index)
-      .def("remove_node", &Engine::remove_node)
+           py::arg("binpack") = false, py::arg("gang_score") = 3, py::arg("enum_limit") = 5000, py::call_guard<EngineGuard>())
+      .def("set_percentage_of_nodes_to_score", &Engine::set_percentage_of_nodes_to_score, py::call_guard<EngineGuard>())
+      .def("seed", &Engine::seed, py::call_guard<EngineGuard>())
+      .def("intern", &Engine::intern, py::call_guard<EngineGuard>())
+      .def("upsert_node", &Engine::upsert_node, py::call_guard<EngineGuard>())
+      .def("node_index", &Engine::node_index, py::call_guard<EngineGuard>())
+      .def("remove_node", &Engine::remove_node, py::call_guard<EngineGuard>())
       .def_property_readonly("num_nodes", &Engine::num_nodes)
       .def_property_readonly("live_nodes", &Engine::live_nodes)
       .def_property_readonly("cycles", &Engine::cycles)
       .def_property_readonly("ledger_size", &Engine::ledger_size)
-      .def("node_name", [](Engine& e, int32_t i) { return e.node(i).name; })
+      .def("node_name", [](Engine& e, int32_t i) { return e.node(i).name; }, py::call_guard<EngineGuard>())
       .def("set_node_meta",
            [](Engine& e, int32_t idx, bool unsched, const std::vector<std::pair<std::string, std::string>>& labels,
               const std::vector<std::tuple<std::string, std::string, std::string>>& taints, int64_t cpu_m,
@@ -118,27 +127,27 @@ PYBIND11_MODULE(_yoda_core, m) {
              for (auto& t : taints)
                ts.push_back(Taint{e.intern(std::get<0>(t)), e.intern(std::get<1>(t)), effect_of(std::get<2>(t))});
              e.set_node_meta(idx, unsched, lab, ts, cpu_m, mem, pods);
-           })
+           }, py::call_guard<EngineGuard>())
       .def("enable_device",
            [](Engine& e, const std::string& path, int device, int capacity, int min_nodes) {
              std::string err;
              bool ok = e.enable_device(path, device, capacity, min_nodes, &err);
              return py::make_tuple(ok, err);
            },
-           py::arg("lib_path"), py::arg("device") = 0, py::arg("capacity") = 65536, py::arg("min_nodes") = 256)
-      .def("disable_device", &Engine::disable_device)
+           py::arg("lib_path"), py::arg("device") = 0, py::arg("capacity") = 65536, py::arg("min_nodes") = 256, py::call_guard<EngineGuard>())
+      .def("disable_device", &Engine::disable_device, py::call_guard<EngineGuard>())
       .def_property_readonly("device_enabled", &Engine::device_enabled)
       .def_property_readonly("device_cycles", &Engine::device_cycles)
       .def_property_readonly("device_fallbacks", &Engine::device_fallbacks)
-      .def("device_last_us", &Engine::device_last_us)
-      .def("device_set_timing", &Engine::device_set_timing, py::arg("on"))
-      .def("device_eligible", &Engine::device_eligible)
+      .def("device_last_us", &Engine::device_last_us, py::call_guard<EngineGuard>())
+      .def("device_set_timing", &Engine::device_set_timing, py::arg("on"), py::call_guard<EngineGuard>())
+      .def("device_eligible", &Engine::device_eligible, py::call_guard<EngineGuard>())
       .def("device_cycle",
            [](Engine& e, const PodReq& r) -> py::object {
              CycleResult c;
              if (!e.device_cycle(r, &c)) return py::none();
              return cycle_tuple(c);
-           })
+           }, py::call_guard<EngineGuard>())
       // cards: list of (total, free, clock, bandwidth, core, power, healthy, phys, numa, occ_q)
       .def("set_cards",
            [](Engine& e, int32_t idx,
@@ -157,11 +166,11 @@ PYBIND11_MODULE(_yoda_core, m) {
              e.set_cards(idx, std::move(cards), card_number, free_sum, total_sum, stale, sample_ts);
            },
            py::arg("idx"), py::arg("cards"), py::arg("card_number"), py::arg("free_sum"), py::arg("total_sum"),
-           py::arg("stale"), py::arg("sample_ts") = 0.0)
+           py::arg("stale"), py::arg("sample_ts") = 0.0, py::call_guard<EngineGuard>())
       .def_property("settle_seconds", &Engine::settle_seconds, &Engine::set_settle_seconds)
-      .def("set_fixed_now", &Engine::set_fixed_now)
-      .def("clear_scv", &Engine::clear_scv)
-      .def("set_links", &Engine::set_links)
+      .def("set_fixed_now", &Engine::set_fixed_now, py::call_guard<EngineGuard>())
+      .def("clear_scv", &Engine::clear_scv, py::call_guard<EngineGuard>())
+      .def("set_links", &Engine::set_links, py::call_guard<EngineGuard>())
       .def("node_cards",
            [](Engine& e, int32_t idx) {
              py::list out;
@@ -169,12 +178,12 @@ PYBIND11_MODULE(_yoda_core, m) {
                out.append(py::make_tuple(c.total_mb, c.free_mb, c.reserved_mb, c.pods, c.clock, c.healthy, c.phys,
                                          c.pending_mb));
              return out;
-           })
+           }, py::call_guard<EngineGuard>())
       .def("node_usage",
            [](Engine& e, int32_t idx) {
              const Node& n = e.node(idx);
              return py::make_tuple(n.req_cpu_m, n.req_mem, n.pod_count, n.label_mem_sum, n.nz_cpu_m, n.nz_mem);
-           })
+           }, py::call_guard<EngineGuard>())
       .def("make_req",
            [](Engine& e, bool has_number, uint64_t number, bool has_memory, uint64_t memory, bool has_clock,
               uint64_t clock, uint64_t clock_min, int64_t priority, const std::string& node_name, int64_t cpu_m,
@@ -219,28 +228,28 @@ PYBIND11_MODULE(_yoda_core, m) {
            py::arg("cpu_m") = 0, py::arg("mem") = 0,
            py::arg("node_selector") = std::vector<std::pair<std::string, std::string>>{},
            py::arg("required") = py::list(), py::arg("preferred") = py::list(), py::arg("tolerations") = py::list(),
-           py::arg("nz_cpu_m") = -1, py::arg("nz_mem") = -1)
-      .def("reserve", &Engine::reserve)
-      .def("release", &Engine::release)
-      .def("has_pod", &Engine::has_pod)
+           py::arg("nz_cpu_m") = -1, py::arg("nz_mem") = -1, py::call_guard<EngineGuard>())
+      .def("reserve", &Engine::reserve, py::call_guard<EngineGuard>())
+      .def("release", &Engine::release, py::call_guard<EngineGuard>())
+      .def("has_pod", &Engine::has_pod, py::call_guard<EngineGuard>())
       .def("assignment",
            [](Engine& e, uint64_t pod) -> py::object {
              const Assignment* a = e.assignment(pod);
              if (!a) return py::none();
              return py::make_tuple(a->node, a->cards, a->mb);
-           })
+           }, py::call_guard<EngineGuard>())
       .def("filter_node",
-           [](Engine& e, const PodReq& r, int32_t idx) { return (int)e.filter_node(r, idx, nullptr, nullptr, nullptr); })
+           [](Engine& e, const PodReq& r, int32_t idx) { return (int)e.filter_node(r, idx, nullptr, nullptr, nullptr); }, py::call_guard<EngineGuard>())
       .def("collect_max",
            [](Engine& e, const PodReq& r, const std::vector<int32_t>& idxs) {
              uint64_t mx[6];
              e.collect_max(r, idxs, mx);
              return py::make_tuple(mx[0], mx[1], mx[2], mx[3], mx[4], mx[5]);
-           })
+           }, py::call_guard<EngineGuard>())
       .def("yoda_raw_score",
            [](Engine& e, const PodReq& r, int32_t idx, const std::array<uint64_t, 6>& mx) {
              return e.yoda_raw_score(r, idx, mx.data());
-           })
+           }, py::call_guard<EngineGuard>())
       .def_static("normalize_yoda",
                   [](std::vector<int64_t> s) {
                     Engine::normalize_yoda(s);
@@ -252,28 +261,32 @@ PYBIND11_MODULE(_yoda_core, m) {
              int32_t q = 0;
              bool ok = e.select_gpus(r, idx, &out, &q);
              return py::make_tuple(ok, out, q);
-           })
+           }, py::call_guard<EngineGuard>())
       .def("feasible_nodes",
            [](Engine& e, const PodReq& r, const std::vector<int32_t>& cand, bool exhaustive) {
              std::vector<int32_t> reasons;
              auto f = e.feasible_nodes(r, cand, &reasons, exhaustive);
              return py::make_tuple(f, reasons);
            },
-           py::arg("req"), py::arg("candidates"), py::arg("exhaustive") = false)
-      .def("num_feasible_to_find", &Engine::num_feasible_to_find)
-      .def("score_nodes", &Engine::score_nodes)
+           py::arg("req"), py::arg("candidates"), py::arg("exhaustive") = false, py::call_guard<EngineGuard>())
+      .def("num_feasible_to_find", &Engine::num_feasible_to_find, py::call_guard<EngineGuard>())
+      .def("score_nodes", &Engine::score_nodes, py::call_guard<EngineGuard>())
       .def("schedule",
            [](Engine& e, uint64_t pod, const PodReq& r, bool assume, const std::vector<int32_t>& cand,
               const std::vector<int64_t>& extra) { return cycle_tuple(e.schedule(pod, r, assume, cand, extra)); },
            py::arg("pod"), py::arg("req"), py::arg("assume") = true,
-           py::arg("candidates") = std::vector<int32_t>{}, py::arg("extra") = std::vector<int64_t>{})
+           py::arg("candidates") = std::vector<int32_t>{}, py::arg("extra") = std::vector<int64_t>{}, py::call_guard<EngineGuard>())
       .def("schedule_batch",
            [](Engine& e, const std::vector<uint64_t>& pods, const std::vector<PodReq*>& reqs) {
              if (pods.size() != reqs.size()) throw std::invalid_argument("pods/reqs length mismatch");
              std::vector<const PodReq*> rr(reqs.begin(), reqs.end());
              std::vector<CycleResult> res;
              {
+               // GIL first, then the engine lock: the lock is dropped before the GIL is
+               // re-taken, so an event-loop thread waiting on the lock (holding the GIL)
+               // cannot deadlock against this call
                py::gil_scoped_release nogil;
+               EngineGuard g;
                res = e.schedule_batch(pods, rr);
              }
              py::list out;

@@ -595,3 +595,49 @@ def test_bench_node_gpus_sweep_option():
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["node_gpus"] == 4 and d["pods_bound"] == 100 and "1 node x 4 MI355X" in d["config"]["model"]
+
+
+def test_wait_for_propagates_cancellation_and_fastbind_timeout():
+    """``utils.aio.wait_for`` keeps a caller's cancellation even when the inner awaitable
+    finishes in the same loop iteration (asyncio.wait_for on Python < 3.12 returns the
+    result instead, which left a bind worker running after scheduler shutdown); the
+    pipelined binder times out a request the server never answers."""
+    from yoda_scheduler_amd.kube.fastbind import FastBinder
+    from yoda_scheduler_amd.utils import aio
+
+    async def race():
+        fut = asyncio.get_event_loop().create_future()
+
+        async def inner():
+            return await fut
+        t = asyncio.ensure_future(aio.wait_for(inner(), 10))
+        await asyncio.sleep(0)
+        await asyncio.sleep(0)
+        fut.set_result(1)
+        t.cancel()
+        try:
+            await t
+            return "result"
+        except asyncio.CancelledError:
+            return "cancelled"
+
+    async def timeout():
+        with pytest.raises(asyncio.TimeoutError):
+            await aio.wait_for(asyncio.sleep(5), 0.05)
+
+        async def silent(r, w):
+            await r.read(1 << 16)            # accept the request, never answer
+            await asyncio.sleep(5)
+        srv = await asyncio.start_server(silent, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        fb = FastBinder(f"http://127.0.0.1:{port}", conns=1, timeout=0.1)
+        t0 = time.monotonic()
+        try:
+            with pytest.raises(asyncio.TimeoutError):
+                await fb.bind("default", "p", "u", "n")
+            return time.monotonic() - t0
+        finally:
+            await fb.close()
+            srv.close()
+    assert run(race()) == "cancelled"
+    assert run(timeout()) < 2.0

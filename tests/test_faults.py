@@ -59,6 +59,41 @@ def test_burst_survives_watch_drops_latency_and_bind_faults():
     assert bind_errors > 0 and binds > 240  # injected failures were retried
 
 
+def test_overlapped_engine_batches_keep_ledger_exact():
+    """yodaRuntime.overlapEngine: native batches run on the engine worker thread while the
+    event loop binds, retries failed binds (engine release) and ingests node updates (engine
+    upserts) — the process-wide engine lock keeps every reservation exact."""
+    faults = Faults(bind_conflict_ratio=0.05, bind_fail_ratio=0.05, seed=11)
+
+    async def go():
+        cfg = yoda_config(backoff=0.01, max_backoff=0.05, batch=32)
+        cfg["yodaRuntime"]["overlapEngine"] = "on"
+        c = FakeCluster(cfg, faults=faults)
+        for i in range(4):
+            c.add_node(f"n{i}")
+        await c.start()
+        rng = random.Random(5)
+        pods = {}
+        for i in range(400):
+            mem = rng.choice([1024, 4096, 8192])
+            lab = {"scv/memory": str(mem)}
+            if i % 5 == 0:
+                lab["scv/number"] = "2"
+            c.add_pod(f"p{i}", lab)
+            pods[f"p{i}"] = mem
+            if i % 50 == 25:              # node churn while batches are in flight
+                c.server.patch("nodes", f"n{i % 4}", {"metadata": {"labels": {"tick": str(i)}}})
+                await asyncio.sleep(0)
+        ok = await c.wait(lambda: all(c.node_of(p) for p in pods), 30.0, 0.01)
+        await asyncio.sleep(0.1)
+        overlapped = c.sched._engine_exec is not None
+        _ledger_invariants(c, pods)
+        await c.stop()
+        return ok, overlapped, c.sched.bind_errors
+    ok, overlapped, bind_errors = run(go())
+    assert ok and overlapped and bind_errors > 0
+
+
 def test_amdsmi_faults_steer_placement():
     """GPU 3 reports an uncorrectable ECC error, GPU 5 an xGMI link down, and something
     outside the scheduler filled GPU 0's HBM: none of them may receive pods."""

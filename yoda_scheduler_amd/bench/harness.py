@@ -22,7 +22,7 @@ from .workloads import Workload, pod_object, populate
 
 
 def bench_config(scheduler_name: str, qps: float, burst: int, batch: int, compat: bool = False,
-                 device: str = "auto") -> dict:
+                 device: str = "auto", overlap: str = "auto") -> dict:
     """The shipped deploy profile (yoda at filter + score weight 300 on top of the
     upstream defaults) with the yoda QueueSort enabled (Q7) and the given client QPS."""
     prof = {"schedulerName": scheduler_name,
@@ -35,7 +35,8 @@ def bench_config(scheduler_name: str, qps: float, burst: int, batch: int, compat
             "leaderElection": {"leaderElect": False},
             "clientConnection": {"qps": qps, "burst": burst},
             "percentageOfNodesToScore": 0, "podInitialBackoffSeconds": 1, "podMaxBackoffSeconds": 10,
-            "yodaRuntime": {"batchSize": batch, "bindConcurrency": 256, "deviceScorer": {"enabled": device}},
+            "yodaRuntime": {"batchSize": batch, "bindConcurrency": 256, "deviceScorer": {"enabled": device},
+                            "overlapEngine": overlap},
             "profiles": [prof]}
 
 
@@ -64,12 +65,13 @@ def percentile(xs: list[float], q: float) -> float:
 class Shard:
     def __init__(self, w: Workload, qps: float = 5000.0, burst: int = 10000, batch: int = 256,
                  template: Optional[dict] = None, metrics: bool = False, events: bool = True,
-                 compat: bool = False, seed: int = 0, engine_threads: int = 1, device: str = "auto") -> None:
+                 compat: bool = False, seed: int = 0, engine_threads: int = 1, device: str = "auto",
+                 overlap: str = "auto") -> None:
         self.w = w
         self.server = FakeApiServer()
         self.client = InProcessClient(self.server)
         populate(self.server, w, template, link_load=0.2 if w.id == 5 else 0.0, seed=seed)
-        cfg = parse_config(bench_config(w.scheduler_name, qps, burst, batch, compat, device))
+        cfg = parse_config(bench_config(w.scheduler_name, qps, burst, batch, compat, device, overlap))
         self.sched = Scheduler(self.client, cfg, metrics=SchedulerMetrics() if metrics else NullMetrics(),
                                record_events=events, seed=seed, engine_threads=engine_threads)
         self.sched.e2e_samples = []
@@ -138,7 +140,7 @@ class HttpShard:
 
     def __init__(self, w: Workload, qps: float = 5000.0, burst: int = 10000, batch: int = 256,
                  template: Optional[dict] = None, events: bool = True, compat: bool = False, seed: int = 0,
-                 device: str = "auto") -> None:
+                 device: str = "auto", overlap: str = "auto") -> None:
         import json
         import subprocess
         import sys
@@ -154,7 +156,7 @@ class HttpShard:
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env = dict(os.environ, PYTHONPATH=os.pathsep.join(p for p in (root, os.environ.get("PYTHONPATH")) if p))
         self.proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env)
-        self.cfg = parse_config(bench_config(w.scheduler_name, qps, burst, batch, compat, device))
+        self.cfg = parse_config(bench_config(w.scheduler_name, qps, burst, batch, compat, device, overlap))
         self.events, self.seed = events, seed
         self.sched: Optional[Scheduler] = None
         self.client = None

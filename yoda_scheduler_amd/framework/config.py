@@ -120,6 +120,9 @@ class SchedulerConfig:
     device_min_nodes: int = 256
     device_capacity: int = 65536
     engine_threads: int = 1
+    # run native batches on a worker thread (GIL released) so the event loop binds and
+    # ingests the previous batch meanwhile: auto = when the gfx950 device scorer is active
+    overlap_engine: str = "auto"
     trace: bool = False
     extenders: list = field(default_factory=list)     # [ExtenderConfig]
     # legacy Policy held in a ConfigMap (algorithmSource.policy.configMap / --policy-configmap):
@@ -266,6 +269,10 @@ def parse_config(doc: dict) -> SchedulerConfig:
     cfg.device_min_nodes = int(_f(ds, "minNodes", 256))
     cfg.device_capacity = int(_f(ds, "capacity", 65536))
     cfg.engine_threads = int(_f(rt, "engineThreads", 1))
+    ov = _f(rt, "overlapEngine", "auto")
+    cfg.overlap_engine = {True: "on", False: "off"}.get(ov, str(ov).lower()) if isinstance(ov, bool) else str(ov).lower()
+    if cfg.overlap_engine not in ("auto", "on", "off"):
+        raise ValueError("yodaRuntime.overlapEngine must be auto|on|off")
     cfg.trace = bool(_f(rt, "trace", False))
     for e in doc.get("extenders") or []:
         if not e.get("urlPrefix"):

@@ -28,6 +28,7 @@ from typing import Callable, Optional
 
 from ..kube.errors import ApiError
 from ..models.scv import parse_rfc3339, rfc3339
+from ..utils import aio
 
 log = logging.getLogger("yoda.leader")
 
@@ -223,7 +224,7 @@ class LeaderElector:
             await asyncio.sleep(self.retry_period)
             ok = False
             try:
-                ok = await asyncio.wait_for(self.try_acquire_or_renew(), self.renew_deadline)
+                ok = await aio.wait_for(self.try_acquire_or_renew(), self.renew_deadline)
             except asyncio.TimeoutError:
                 ok = False
             if not ok and self.clock() - self._last_renew > self.renew_deadline:

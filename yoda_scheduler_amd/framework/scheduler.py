@@ -128,6 +128,7 @@ class Scheduler:
         self._bind_dq: collections.deque = collections.deque()
         self._bind_idle: collections.deque = collections.deque()
         self._tasks: list[asyncio.Task] = []
+        self._engine_exec = None          # worker thread of schedule_batch_overlapped
         self.informers: dict[str, Informer] = {}
         self.scheduled = 0
         self.failed = 0
@@ -530,14 +531,14 @@ class Scheduler:
             log.warning("preemption: deleting %s failed: %r", v.key, e)
 
     # ================================================================== batch cycle
-    def schedule_batch(self, pods: list[PodInfo]) -> None:
-        """Schedule a run of popped pods; consecutive pods of an all-native profile go
-        through one GIL-free engine call."""
+    def _batch_runs(self, pods: list[PodInfo]):
+        """Split popped pods into single Python cycles (``(None, pod)``) and runs of
+        consecutive pods of an all-native profile (``(fw, [pods])``)."""
         i = 0
         while i < len(pods):
             fw = self.frameworks.get(pods[i].scheduler_name)
             if fw is None or not fw.native_for(pods[i]):
-                self.schedule_one(pods[i])
+                yield None, pods[i]
                 i += 1
                 continue
             j = i
@@ -547,21 +548,57 @@ class Scheduler:
                     run.append(pods[j])
                 j += 1
             i = j
-            if not run:
+            if run:
+                yield fw, run
+
+    def _prepare_run(self, fw: Framework, run: list[PodInfo]):
+        self._activate(fw)
+        self._clear_nominations_for(run)
+        eng = self.engine
+        return self.queue.scheduling_cycle, time.perf_counter(), [p.num_id for p in run], \
+            [pod_req(eng, p) for p in run]
+
+    def _finish_run(self, fw: Framework, run: list[PodInfo], results, cycle: int, t0: float) -> None:
+        self.metrics.batch_size.observe(len(run))
+        if self.tracer is not None:
+            tr = self.tracer
+            tr.span("native_batch", tr.now_us() - (time.perf_counter() - t0) * 1e6, pods=len(run),
+                    device_cycles=self.engine.device_cycles)
+        for p, res in zip(run, results):
+            self._finish_cycle(fw, None, p, res, cycle, t0)   # all-native: no Python state
+
+    def schedule_batch(self, pods: list[PodInfo]) -> None:
+        """Schedule a run of popped pods; consecutive pods of an all-native profile go
+        through one GIL-free engine call."""
+        for fw, item in self._batch_runs(pods):
+            if fw is None:
+                self.schedule_one(item)
                 continue
-            self._activate(fw)
-            self._clear_nominations_for(run)
-            cycle = self.queue.scheduling_cycle
-            t0 = time.perf_counter()
-            eng = self.engine
-            results = eng.schedule_batch([p.num_id for p in run], [pod_req(eng, p) for p in run])
-            self.metrics.batch_size.observe(len(run))
-            if self.tracer is not None:
-                tr = self.tracer
-                tr.span("native_batch", tr.now_us() - (time.perf_counter() - t0) * 1e6, pods=len(run),
-                        device_cycles=eng.device_cycles)
-            for p, res in zip(run, results):
-                self._finish_cycle(fw, None, p, res, cycle, t0)   # all-native: no Python state
+            cycle, t0, ids, reqs = self._prepare_run(fw, item)
+            self._finish_run(fw, item, self.engine.schedule_batch(ids, reqs), cycle, t0)
+
+    def _overlap(self) -> bool:
+        mode = self.config.overlap_engine
+        return mode == "on" or (mode == "auto" and self.engine.device_enabled and
+                                self.engine.live_nodes >= self.config.device_min_nodes)
+
+    async def schedule_batch_overlapped(self, pods: list[PodInfo]) -> None:
+        """``schedule_batch`` with each native run on the engine worker thread: while the
+        engine (and, with the device scorer, the GPU) places this batch, the event loop
+        keeps binding the previous one and ingesting informer events. The engine's
+        process-wide lock (native/core/bindings.cpp) serialises any engine call the loop
+        makes meanwhile; the batch's own results are applied after the await, in order."""
+        loop = asyncio.get_event_loop()
+        for fw, item in self._batch_runs(pods):
+            if fw is None:
+                self.schedule_one(item)
+                continue
+            cycle, t0, ids, reqs = self._prepare_run(fw, item)
+            if self._engine_exec is None:
+                import concurrent.futures
+                self._engine_exec = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="yoda-engine")
+            results = await loop.run_in_executor(self._engine_exec, self.engine.schedule_batch, ids, reqs)
+            self._finish_run(fw, item, results, cycle, t0)
 
     # ================================================================== binding
     def _enqueue_bind(self, item: tuple) -> None:
@@ -678,7 +715,10 @@ class Scheduler:
                 await self.schedule_one_async(pi)
             elif self.batching and q._active_entries:
                 batch = [pi] + q.pop_batch(bs - 1)
-                self.schedule_batch(batch)
+                if self._overlap():
+                    await self.schedule_batch_overlapped(batch)
+                else:
+                    self.schedule_batch(batch)
             else:
                 self.schedule_one(pi)
             # let informers / binders run between cycles
@@ -734,6 +774,9 @@ class Scheduler:
         self._tasks.clear()
         for e in self.extenders:
             await e.close()
+        if self._engine_exec is not None:
+            self._engine_exec.shutdown(wait=True)
+            self._engine_exec = None
 
     async def drain_binds(self) -> None:
         while self.pending_binds:

@@ -234,8 +234,9 @@ class KubeClient:
         if self.fast_bind:
             if self._binder is None:
                 from .fastbind import FastBinder
-                self._binder = FastBinder(self.config.server, self.config.token, self._binder_ssl())
-            await asyncio.wait_for(self._binder.bind(namespace, name, uid, node, annotations), self.timeout)
+                self._binder = FastBinder(self.config.server, self.config.token, self._binder_ssl(),
+                                          timeout=self.timeout)
+            await self._binder.bind(namespace, name, uid, node, annotations)
             return
         body = {"apiVersion": "v1", "kind": "Binding",
                 "metadata": {"name": name, "namespace": namespace, "uid": uid, "annotations": dict(annotations or {})},

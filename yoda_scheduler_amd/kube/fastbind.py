@@ -83,13 +83,19 @@ class _Conn:
             pass
 
 
+def _expire(fut: asyncio.Future) -> None:
+    if not fut.done():
+        fut.set_exception(asyncio.TimeoutError("binding request timed out"))
+
+
 class FastBinder:
     """Pipelined binding POSTs over ``conns`` keep-alive connections (``max_inflight`` per
     connection). Errors surface as :class:`ApiError` (HTTP status) or ``ConnectionError``
     (the scheduler treats both as a failed bind: forget + requeue)."""
 
     def __init__(self, server: str, token: Optional[str] = None, ssl_context: Optional[_ssl.SSLContext] = None,
-                 conns: int = 16, max_inflight: int = 64) -> None:
+                 conns: int = 16, max_inflight: int = 64, timeout: Optional[float] = None) -> None:
+        self.timeout = timeout
         u = urlsplit(server)
         self.tls = u.scheme == "https"
         self.host = u.hostname or "127.0.0.1"
@@ -130,10 +136,20 @@ class FastBinder:
             c2 = await self._conn(j)
             if len(c2.pending) < len(c.pending):
                 c = c2
-        fut = asyncio.get_event_loop().create_future()
+        loop = asyncio.get_event_loop()
+        fut = loop.create_future()
         c.pending.append(fut)
         c.w.write(req)
-        return await fut
+        if self.timeout is None:
+            return await fut
+        # the timer fails the response future itself (it stays queued, so the pipeline's
+        # request/response pairing holds when the late answer arrives); no wait_for, whose
+        # Python < 3.12 race could swallow the caller's cancellation
+        h = loop.call_later(self.timeout, _expire, fut)
+        try:
+            return await fut
+        finally:
+            h.cancel()
 
     async def bind(self, namespace: str, name: str, uid: str, node: str, annotations: Optional[dict] = None) -> None:
         body = {"apiVersion": "v1", "kind": "Binding",
