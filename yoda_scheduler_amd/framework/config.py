@@ -121,8 +121,10 @@ class SchedulerConfig:
     device_capacity: int = 65536
     engine_threads: int = 1
     # run native batches on a worker thread (GIL released) so the event loop binds and
-    # ingests the previous batch meanwhile: auto = when the gfx950 device scorer is active
-    overlap_engine: str = "auto"
+    # ingests the previous batch meanwhile. Off by default: on MI355X (config 6, device
+    # scorer) it did not raise throughput and tripled p99 (profiles/bench/overlap_ab_r1.jsonl);
+    # auto = only when the gfx950 device scorer is active
+    overlap_engine: str = "off"
     trace: bool = False
     extenders: list = field(default_factory=list)     # [ExtenderConfig]
     # legacy Policy held in a ConfigMap (algorithmSource.policy.configMap / --policy-configmap):
@@ -269,7 +271,7 @@ def parse_config(doc: dict) -> SchedulerConfig:
     cfg.device_min_nodes = int(_f(ds, "minNodes", 256))
     cfg.device_capacity = int(_f(ds, "capacity", 65536))
     cfg.engine_threads = int(_f(rt, "engineThreads", 1))
-    ov = _f(rt, "overlapEngine", "auto")
+    ov = _f(rt, "overlapEngine", cfg.overlap_engine)
     cfg.overlap_engine = {True: "on", False: "off"}.get(ov, str(ov).lower()) if isinstance(ov, bool) else str(ov).lower()
     if cfg.overlap_engine not in ("auto", "on", "off"):
         raise ValueError("yodaRuntime.overlapEngine must be auto|on|off")
