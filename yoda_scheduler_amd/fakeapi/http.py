@@ -14,7 +14,7 @@ from typing import Optional
 from aiohttp import web
 
 from ..kube.errors import ApiError
-from ..kube.resources import RESOURCES
+from ..kube.resources import BY_PATH, RESOURCES
 from .server import FakeApiServer
 
 _PATH = re.compile(
@@ -26,8 +26,8 @@ def _resolve(path: str):
     m = _PATH.match(path)
     if not m:
         return None
-    res = m.group("res")
-    if res not in RESOURCES:
+    res = BY_PATH.get((m.group("group") or "", m.group("res")))
+    if res is None:
         return None
     return res, m.group("ns"), m.group("name"), m.group("sub")
 

@@ -125,6 +125,8 @@ class SchedulerConfig:
     # scorer) it did not raise throughput and tripled p99 (profiles/bench/overlap_ab_r1.jsonl);
     # auto = only when the gfx950 device scorer is active
     overlap_engine: str = "off"
+    # event API (yodaRuntime.eventsAPI): upstream v1.20 records through events.k8s.io/v1
+    events_api: str = "events.k8s.io/v1"
     trace: bool = False
     extenders: list = field(default_factory=list)     # [ExtenderConfig]
     # legacy Policy held in a ConfigMap (algorithmSource.policy.configMap / --policy-configmap):
@@ -271,6 +273,9 @@ def parse_config(doc: dict) -> SchedulerConfig:
     cfg.device_min_nodes = int(_f(ds, "minNodes", 256))
     cfg.device_capacity = int(_f(ds, "capacity", 65536))
     cfg.engine_threads = int(_f(rt, "engineThreads", 1))
+    cfg.events_api = str(_f(rt, "eventsAPI", cfg.events_api))
+    if cfg.events_api not in ("events.k8s.io/v1", "v1"):
+        raise ValueError("yodaRuntime.eventsAPI must be events.k8s.io/v1 or v1")
     ov = _f(rt, "overlapEngine", cfg.overlap_engine)
     cfg.overlap_engine = {True: "on", False: "off"}.get(ov, str(ov).lower()) if isinstance(ov, bool) else str(ov).lower()
     if cfg.overlap_engine not in ("auto", "on", "off"):

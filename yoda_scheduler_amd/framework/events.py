@@ -1,5 +1,12 @@
 """Event recorder: ``Scheduled`` / ``FailedScheduling`` / ``Preempted`` pod events
-(upstream behaviour the reference's RBAC grants, ``deploy/yoda-scheduler.yaml:76-84``).
+(upstream behaviour the reference's RBAC grants, ``deploy/yoda-scheduler.yaml:76-84``
+for core/v1 and ``:197-204`` for events.k8s.io).
+
+Like upstream v1.20 (``EventBroadcasterAdapter``) events go through ``events.k8s.io/v1``
+by default: ``reportingController`` is the profile's scheduler name, ``action`` is
+``Binding`` / ``Scheduling`` / ``Preempting``, the preemptor is the ``related`` object of a
+``Preempted`` event, and repeats of an isomorphic event update its ``series``
+(count, lastObservedTime). ``api="v1"`` keeps the core/v1 shape (count/lastTimestamp).
 
 Events are buffered and written by a background task with their own rate limiter and
 a per-(object, reason, message) de-duplication counter, so recording never blocks the
@@ -13,8 +20,11 @@ from __future__ import annotations
 import asyncio
 import collections
 import logging
+import socket
 import time
 import uuid
+from datetime import datetime, timezone
+from typing import Optional
 
 from ..models.scv import rfc3339
 from ..utils.ratelimit import TokenBucket
@@ -22,11 +32,24 @@ from ..utils.ratelimit import TokenBucket
 log = logging.getLogger("yoda.events")
 
 
+ACTIONS = {"Scheduled": "Binding", "FailedScheduling": "Scheduling", "Preempted": "Preempting"}
+API_EVENTS_V1 = "events.k8s.io/v1"
+
+
+def micro_time(ts: float) -> str:
+    """metav1.MicroTime: RFC 3339 with microseconds."""
+    return datetime.fromtimestamp(ts, timezone.utc).strftime("%Y-%m-%dT%H:%M:%S.%fZ")
+
+
 class EventRecorder:
     def __init__(self, client, component: str = "yoda-scheduler", qps: float = 50.0, burst: int = 300,
-                 max_buffer: int = 1000, enabled: bool = True) -> None:
+                 max_buffer: int = 1000, enabled: bool = True, api: str = API_EVENTS_V1) -> None:
+        if api not in (API_EVENTS_V1, "v1"):
+            raise ValueError(f"events API must be {API_EVENTS_V1} or v1, got {api!r}")
         self.client = client
         self.component = component
+        self.api = api
+        self.host = socket.gethostname()
         self.enabled = enabled
         self.limiter = TokenBucket(qps, burst)
         self.max_buffer = max_buffer
@@ -36,29 +59,66 @@ class EventRecorder:
         self.recorded = collections.Counter()
         self.dropped = 0
 
-    def event(self, pod_obj_meta: dict, kind: str, typ: str, reason: str, message: str) -> None:
+    def event(self, pod_obj_meta: dict, kind: str, typ: str, reason: str, message: str,
+              controller: str = "", related: Optional[dict] = None) -> None:
         if not self.enabled:
             return
         self.recorded[reason] += 1
         if len(self._buf) >= self.max_buffer:
             self.dropped += 1
             return
-        self._buf.append((pod_obj_meta, kind, typ, reason, message, time.time()))
+        self._buf.append((pod_obj_meta, kind, typ, reason, message, time.time(), controller, related))
         self._wake.set()
 
-    def pod_event(self, pi, typ: str, reason: str, message: str) -> None:
+    def pod_event(self, pi, typ: str, reason: str, message: str, related=None) -> None:
         if self.enabled:
-            self.event({"name": pi.name, "namespace": pi.namespace, "uid": pi.uid}, "Pod", typ, reason, message)
+            rel = None if related is None else {"apiVersion": "v1", "kind": "Pod", "name": related.name,
+                                                "namespace": related.namespace, "uid": related.uid}
+            self.event({"name": pi.name, "namespace": pi.namespace, "uid": pi.uid}, "Pod", typ, reason, message,
+                       pi.scheduler_name, rel)
+
+    def _new_v1(self, meta, kind, typ, reason, message, ts, controller, related) -> dict:
+        ctl = controller or self.component
+        ev = {"apiVersion": API_EVENTS_V1, "kind": "Event",
+              "metadata": {"name": f"{meta.get('name')}.{uuid.uuid4().hex[:16]}",
+                           "namespace": meta.get("namespace") or "default"},
+              "eventTime": micro_time(ts), "reportingController": ctl, "reportingInstance": f"{ctl}-{self.host}",
+              "action": ACTIONS.get(reason, reason), "reason": reason,
+              "regarding": {"apiVersion": "v1", "kind": kind, **meta}, "note": message[:1024], "type": typ}
+        if related:
+            ev["related"] = related
+        return ev
+
+    async def _write_v1(self, key, item) -> None:
+        meta, kind, typ, reason, message, ts, controller, related = item
+        prev = self._dedup.get(key)
+        if prev is not None:      # isomorphic event: bump the series
+            series = dict(prev.get("series") or {"count": 1})
+            series["count"] = int(series.get("count", 1)) + 1
+            series["lastObservedTime"] = micro_time(ts)
+            self._dedup[key] = await self.client.patch("events.k8s.io", prev["metadata"]["name"],
+                                                       {"series": series}, meta.get("namespace") or "default")
+        else:
+            self._dedup[key] = await self.client.create(
+                "events.k8s.io", self._new_v1(meta, kind, typ, reason, message, ts, controller, related),
+                meta.get("namespace"))
 
     async def run(self) -> None:
         while True:
             if not self._buf:
                 self._wake.clear()
                 await self._wake.wait()
-            meta, kind, typ, reason, message, ts = self._buf.popleft()
+            item = self._buf.popleft()
+            meta, kind, typ, reason, message, ts, controller, related = item
             await self.limiter.acquire()
-            key = (meta.get("namespace"), meta.get("name"), reason, message)
+            key = (meta.get("namespace"), meta.get("name"), reason, message, controller,
+                   (related or {}).get("uid"))
             try:
+                if self.api == API_EVENTS_V1:
+                    await self._write_v1(key, item)
+                    if len(self._dedup) > 10_000:
+                        self._dedup.clear()
+                    continue
                 prev = self._dedup.get(key)
                 if prev is not None:
                     prev = dict(prev, count=prev.get("count", 1) + 1, lastTimestamp=rfc3339(ts))
@@ -71,7 +131,7 @@ class EventRecorder:
                                      "namespace": meta.get("namespace") or "default"},
                         "involvedObject": {"kind": kind, **meta},
                         "reason": reason, "message": message, "type": typ,
-                        "source": {"component": self.component},
+                        "source": {"component": controller or self.component},
                         "firstTimestamp": rfc3339(ts), "lastTimestamp": rfc3339(ts), "count": 1,
                     }
                     self._dedup[key] = await self.client.create("events", ev, meta.get("namespace"))

@@ -105,7 +105,7 @@ class Scheduler:
         self.metrics = metrics if metrics is not None else SchedulerMetrics()
         cc = config.client_connection
         self.limiter = bind_limiter or TokenBucket(cc.qps, cc.burst)
-        self.recorder = EventRecorder(client, enabled=record_events)
+        self.recorder = EventRecorder(client, enabled=record_events, api=config.events_api)
         self.handle = Handle(self)
         # the engine must exist before plugins are created (they may query it)
         compat = any(((p.plugin_config.get("yoda") or {}).get("compat", False)) for p in config.profiles)
@@ -520,7 +520,7 @@ class Scheduler:
         self.metrics.preemption_attempts.inc()
         self.metrics.preemption_victims.observe(len(victims))
         for v in victims:
-            self.recorder.pod_event(v, "Normal", "Preempted", f"Preempted by {pod.key} on node {node}")
+            self.recorder.pod_event(v, "Normal", "Preempted", f"Preempted by {pod.key} on node {node}", related=pod)
             asyncio.get_event_loop().create_task(self._delete_victim(v))
 
     async def _delete_victim(self, v: PodInfo) -> None:

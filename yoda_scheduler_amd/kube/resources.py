@@ -35,6 +35,8 @@ RESOURCES = {
     "pods": Resource("pods", "", "v1", "Pod", True),
     "nodes": Resource("nodes", "", "v1", "Node", False),
     "events": Resource("events", "", "v1", "Event", True),
+    # upstream v1.20's scheduler records through the events.k8s.io/v1 API (EventBroadcasterAdapter)
+    "events.k8s.io": Resource("events", "events.k8s.io", "v1", "Event", True),
     "leases": Resource("leases", "coordination.k8s.io", "v1", "Lease", True),
     "scvs": Resource("scvs", "core.run-linux.com", "v1", "Scv", False),
     "configmaps": Resource("configmaps", "", "v1", "ConfigMap", True),
@@ -52,6 +54,9 @@ RESOURCES = {
     "replicasets": Resource("replicasets", "apps", "v1", "ReplicaSet", True),
     "statefulsets": Resource("statefulsets", "apps", "v1", "StatefulSet", True),
 }
+
+
+BY_PATH = {(r.group, r.name): key for key, r in RESOURCES.items()}
 
 
 def resource(name: str) -> Resource:
