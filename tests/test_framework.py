@@ -213,3 +213,45 @@ def test_least_allocated_resource_weights():
     assert default == [49, 49]                      # (89 + 9) / 2
     assert cpu_heavy == [69, 29]                    # (89·3 + 9) / 4, (9·3 + 89) / 4
     assert diluted == [24, 24]                      # (89 + 9) / 4
+
+
+def _granted(rules, group, resource, verb, name=None):
+    for r in rules:
+        if group not in r.get("apiGroups", []) or resource not in r.get("resources", []):
+            continue
+        if verb not in r.get("verbs", []) and "*" not in r.get("verbs", []):
+            continue
+        names = r.get("resourceNames")
+        if names and (name is None or name not in names):
+            continue
+        return True
+    return False
+
+
+def test_deploy_rbac_covers_every_api_call():
+    """The ClusterRole in deploy/yoda-scheduler.yaml grants each (group, resource, verb) the
+    scheduler issues: informers, binding, status/condition patches, preemption deletes,
+    events (both APIs), leader-election locks, the Scv CRD (C17, reference
+    ``deploy/yoda-scheduler.yaml:71-216``)."""
+    import os
+    import yaml
+    from yoda_scheduler_amd.kube.resources import RESOURCES
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    docs = [d for d in yaml.safe_load_all(open(os.path.join(root, "deploy", "yoda-scheduler.yaml"))) if d]
+    role = [d for d in docs if d["kind"] == "ClusterRole"][0]
+    assert role["metadata"]["name"] == "yoda-cr"
+    rules = role["rules"]
+    watched = ["pods", "nodes", "scvs", "poddisruptionbudgets", "services", "replicationcontrollers",
+               "replicasets", "statefulsets", "persistentvolumeclaims", "persistentvolumes", "storageclasses",
+               "csinodes"]
+    need = [(RESOURCES[r].group, RESOURCES[r].name, v) for r in watched for v in ("list", "watch")]
+    need += [("", "pods/binding", "create"), ("", "pods", "patch"), ("", "pods", "delete"),
+             ("", "events", "create"), ("", "events", "update"),
+             ("events.k8s.io", "events", "create"), ("events.k8s.io", "events", "patch"),
+             ("coordination.k8s.io", "leases", "get"), ("coordination.k8s.io", "leases", "create"),
+             ("coordination.k8s.io", "leases", "update"), ("core.run-linux.com", "scvs", "patch"),
+             ("core.run-linux.com", "scvs/status", "update"), ("", "configmaps", "get")]
+    missing = [n for n in need if not _granted(rules, *n)]
+    assert missing == []
+    for res in ("endpoints", "configmaps"):          # legacy / multi resourceLocks on the lock object
+        assert _granted(rules, "", res, "create") and _granted(rules, "", res, "update", "yoda-scheduler")
