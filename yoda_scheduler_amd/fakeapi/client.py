@@ -22,7 +22,8 @@ class InProcessClient:
 
     async def list(self, res: str, namespace: Optional[str] = None, resource_version: Optional[str] = None,
                    limit: int = 0, field_selector: Optional[str] = None) -> tuple[list[dict], str]:
-        await self._lat()
+        if self.server.faults.latency_s:
+            await self._lat()
         if not limit:
             return self.server.list(res, namespace, field_selector)
         items, cont = [], ""
@@ -42,31 +43,38 @@ class InProcessClient:
             w.close()
 
     async def get(self, res: str, name: str, namespace: Optional[str] = None) -> dict:
-        await self._lat()
+        if self.server.faults.latency_s:
+            await self._lat()
         return self.server.get(res, name, namespace)
 
     async def create(self, res: str, obj: dict, namespace: Optional[str] = None) -> dict:
-        await self._lat()
+        if self.server.faults.latency_s:
+            await self._lat()
         return self.server.create(res, obj, namespace)
 
     async def update(self, res: str, obj: dict, namespace: Optional[str] = None) -> dict:
-        await self._lat()
+        if self.server.faults.latency_s:
+            await self._lat()
         return self.server.update(res, obj, namespace)
 
     async def update_status(self, res: str, obj: dict, namespace: Optional[str] = None) -> dict:
-        await self._lat()
+        if self.server.faults.latency_s:
+            await self._lat()
         return self.server.update(res, obj, namespace, status_only=True)
 
     async def patch(self, res: str, name: str, patch: dict, namespace: Optional[str] = None) -> dict:
-        await self._lat()
+        if self.server.faults.latency_s:
+            await self._lat()
         return self.server.patch(res, name, patch, namespace)
 
     async def delete(self, res: str, name: str, namespace: Optional[str] = None) -> dict:
-        await self._lat()
+        if self.server.faults.latency_s:
+            await self._lat()
         return self.server.delete(res, name, namespace)
 
     async def bind(self, namespace: str, name: str, uid: str, node: str, annotations: Optional[dict] = None) -> None:
-        await self._lat()
+        if self.server.faults.latency_s:
+            await self._lat()
         self.server.bind(namespace, name, uid, node, annotations)
 
     async def close(self) -> None:

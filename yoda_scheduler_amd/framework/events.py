@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import asyncio
 import collections
+import itertools
 import logging
 import socket
 import time
@@ -50,6 +51,10 @@ class EventRecorder:
         self.component = component
         self.api = api
         self.host = socket.gethostname()
+        # event names: <object>.<16 hex>; a random per-recorder prefix + counter (uuid4 per
+        # event costs more than the rest of recording it)
+        self._name_prefix = uuid.uuid4().hex[:8]
+        self._name_seq = itertools.count(1)
         self.enabled = enabled
         self.limiter = TokenBucket(qps, burst)
         self.max_buffer = max_buffer
@@ -80,7 +85,7 @@ class EventRecorder:
     def _new_v1(self, meta, kind, typ, reason, message, ts, controller, related) -> dict:
         ctl = controller or self.component
         ev = {"apiVersion": API_EVENTS_V1, "kind": "Event",
-              "metadata": {"name": f"{meta.get('name')}.{uuid.uuid4().hex[:16]}",
+              "metadata": {"name": f"{meta.get('name')}.{self._name_prefix}{next(self._name_seq):08x}",
                            "namespace": meta.get("namespace") or "default"},
               "eventTime": micro_time(ts), "reportingController": ctl, "reportingInstance": f"{ctl}-{self.host}",
               "action": ACTIONS.get(reason, reason), "reason": reason,
@@ -127,7 +132,7 @@ class EventRecorder:
                 else:
                     ev = {
                         "apiVersion": "v1", "kind": "Event",
-                        "metadata": {"name": f"{meta.get('name')}.{uuid.uuid4().hex[:16]}",
+                        "metadata": {"name": f"{meta.get('name')}.{self._name_prefix}{next(self._name_seq):08x}",
                                      "namespace": meta.get("namespace") or "default"},
                         "involvedObject": {"kind": kind, **meta},
                         "reason": reason, "message": message, "type": typ,

@@ -262,6 +262,13 @@ class Framework:
         finally:
             self.waiting.pop(pod.uid, None)
 
+    def direct_binder(self):
+        """The single bind plugin when nothing runs around it (no PreBind plugins): the
+        bind workers then await it directly instead of going through ``run_bind``."""
+        if not self.pre_bind and len(self.bind_plugins) == 1:
+            return self.bind_plugins[0]
+        return None
+
     async def run_bind(self, state: CycleState, pod, node: str, extender=None) -> Status:
         for p in self.pre_bind:
             if not self._applies(p, pod):

@@ -628,10 +628,17 @@ class Scheduler:
             if state is None:
                 state = _EMPTY_STATE
             try:
-                await self.limiter.acquire()
+                if not self.limiter.try_acquire():
+                    await self.limiter.acquire()
                 tb = time.perf_counter()
                 try:
-                    st = await fw.run_bind(state, pi, node, self._extender_binder(pi))
+                    direct = fw.direct_binder() if not self.extenders else None
+                    if direct is not None:
+                        st = await direct.bind(state, pi, node)
+                        if st.code.name == "SKIP":
+                            st = Status.error("no bind plugin bound the pod")
+                    else:
+                        st = await fw.run_bind(state, pi, node, self._extender_binder(pi))
                 except Exception as e:  # noqa: BLE001
                     st = Status.error(repr(e))
                 m.binding.observe(time.perf_counter() - tb)
