@@ -539,3 +539,33 @@ def test_cache_debugger_detects_drift():
     assert clean == {}
     assert drift["pods"]["missed"] == [uid] and drift["nodes"]["missed"] == ["n1"]
     assert set(dump["queue"]) == {"active", "backoff", "unschedulable"}
+
+
+def test_partitioned_node_gangs_stay_on_one_physical_gpu():
+    """CPX (8 partitions per MI355X → 64 logical GPUs): a gang prefers partitions of one
+    physical GPU (on-package fabric) over ones spread across xGMI links; each logical GPU
+    has 1/8 of the HBM."""
+    from yoda_scheduler_amd.models.device import make_node, make_scv
+
+    async def go():
+        c = FakeCluster()
+        c.server.create("nodes", make_node("cpx"))
+        s = make_scv("cpx", partition="CPX", update_time=time.time())
+        s.update_interval_ms = 600_000
+        c.server.create("scvs", s.to_json())
+        await c.start()
+        c.add_pod("four", {"scv/number": "4", "scv/memory": "1000"})
+        assert await c.wait_bound(1)
+        c.add_pod("eight", {"scv/number": "8", "scv/memory": "1000"})
+        c.add_pod("two", {"scv/number": "2", "scv/memory": "1000"})
+        assert await c.wait_bound(3)
+        out = {n: c.gpus_of(n) for n in ("four", "eight", "two")}
+        cards = s.status.card_list
+        await c.stop()
+        return out, cards
+    out, cards = run(go())
+    assert len(cards) == 64 and cards[0].total_memory == 294912 // 8
+    phys = {n: {cards[g].phys for g in gs} for n, gs in out.items()}
+    # (scv/memory pods may share a GPU, so gangs may land on the same physical device)
+    assert all(len(p) == 1 for p in phys.values()), (out, phys)
+    assert len(out["eight"]) == 8 and len(set(out["eight"])) == 8

@@ -51,15 +51,26 @@ def compat_card_tuples(scv: Scv) -> list[tuple]:
     return [t[:6] + (c.health == HEALTHY,) + t[7:] for t, c in zip(card_tuples(scv), scv.status.card_list)]
 
 
+# Quality of an idle xGMI link relative to two partitions of the same physical GPU (1e-4
+# units; same physical GPU = 10000 in the engine and the device rows). One xGMI link is
+# ≈153 GB/s while partitions of one MI355X talk over the on-package fabric, so on
+# partitioned (DPX/QPX/CPX) nodes a gang prefers partitions of fewer physical GPUs. On SPX
+# nodes every pair crosses xGMI, so this only shifts all subsets' link term equally.
+XGMI_IDLE_QUALITY = 9000
+
+
 def link_matrix(scv: Scv) -> tuple[int, list[int]]:
-    """Pair quality in 1e-4 units: 10000 × (1 − load) for an up link, 0 for a down one."""
+    """Pair quality in 1e-4 units between physical GPUs: ``XGMI_IDLE_QUALITY × (1 − load)``
+    for an up link (idle when unreported), 0 for a down one."""
     cards = scv.status.card_list
     nphys = max((c.phys for c in cards), default=-1) + 1
-    q = [10000] * (nphys * nphys)
+    q = [XGMI_IDLE_QUALITY] * (nphys * nphys)
+    for a in range(nphys):
+        q[a * nphys + a] = 10000
     for c in cards:
         for l in c.xgmi:
             if 0 <= l.peer < nphys:
-                v = 0 if not l.up else int(round(10000 * (1.0 - min(max(l.load, 0.0), 1.0))))
+                v = 0 if not l.up else int(round(XGMI_IDLE_QUALITY * (1.0 - min(max(l.load, 0.0), 1.0))))
                 q[c.phys * nphys + l.peer] = v
     # symmetrise with the worse direction (a ring uses both)
     for a in range(nphys):

@@ -10,7 +10,7 @@ The reference has no notion of this (``scv/number`` only counts cards,
 Objective (lower is better), integer arithmetic with truncating division:
 
     P        = k(k−1)/2 pairs
-    link_bad = (P·10000 − Σ_pairs q(a,b)) · 100 / P          q = 10000·(1−load), same phys → 10000
+    link_bad = (P·10000 − Σ_pairs q(a,b)) · 100 / P          q = 9000·(1−load) over xGMI, same phys → 10000
     numa_bad = (#NUMA nodes − 1) · 10^6 / (k−1)
     leftover = Σ(eff_free − m) · 10^6 / Σ total                 spread: 10^6 − leftover
     occ_bad  = Σ occupancy(1e-4) · 100 / k
