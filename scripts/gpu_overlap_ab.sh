@@ -1,15 +1,13 @@
 #!/usr/bin/env bash
 # A/B: config 6 (4096 nodes, device scorer) with native batches inline vs overlapped with
-# binding on the engine worker thread; plus the headline config 3 (overlap auto = off).
+# binding on the engine worker thread (the default, auto); plus the headline config 3.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 out=gpurun_out/overlap_ab.jsonl
 : > $out
-for args in "--config 6 --device on --overlap off --steps 3 --warmup 1" \
-            "--config 6 --device on --overlap on --steps 3 --warmup 1" \
-            "--config 6 --device on --overlap off --steps 3 --warmup 1" \
-            "--config 6 --device on --overlap on --steps 3 --warmup 1" \
+for args in "--config 6 --overlap off --steps 3 --warmup 1" "--config 6 --steps 3 --warmup 1" \
+            "--config 6 --overlap off --steps 3 --warmup 1" "--config 6 --steps 3 --warmup 1" \
             "--config 3"; do
   echo "=== bench $args ($(date +%T))"
   timeout -k 10 240 python bench.py $args > gpurun_out/bench_one.log 2>&1

@@ -22,7 +22,7 @@ from .workloads import Workload, pod_object, populate
 
 
 def bench_config(scheduler_name: str, qps: float, burst: int, batch: int, compat: bool = False,
-                 device: str = "auto", overlap: str = "off") -> dict:
+                 device: str = "auto", overlap: str = "auto") -> dict:
     """The shipped deploy profile (yoda at filter + score weight 300 on top of the
     upstream defaults) with the yoda QueueSort enabled (Q7) and the given client QPS."""
     prof = {"schedulerName": scheduler_name,
@@ -66,7 +66,7 @@ class Shard:
     def __init__(self, w: Workload, qps: float = 5000.0, burst: int = 10000, batch: int = 256,
                  template: Optional[dict] = None, metrics: bool = False, events: bool = True,
                  compat: bool = False, seed: int = 0, engine_threads: int = 1, device: str = "auto",
-                 overlap: str = "off") -> None:
+                 overlap: str = "auto") -> None:
         self.w = w
         self.server = FakeApiServer()
         self.client = InProcessClient(self.server)
@@ -140,7 +140,7 @@ class HttpShard:
 
     def __init__(self, w: Workload, qps: float = 5000.0, burst: int = 10000, batch: int = 256,
                  template: Optional[dict] = None, events: bool = True, compat: bool = False, seed: int = 0,
-                 device: str = "auto", overlap: str = "off") -> None:
+                 device: str = "auto", overlap: str = "auto") -> None:
         import json
         import subprocess
         import sys

@@ -121,10 +121,9 @@ class SchedulerConfig:
     device_capacity: int = 65536
     engine_threads: int = 1
     # run native batches on a worker thread (GIL released) so the event loop binds and
-    # ingests the previous batch meanwhile. Off by default: on MI355X (config 6, device
-    # scorer) it did not raise throughput and tripled p99 (profiles/bench/overlap_ab_r1.jsonl);
-    # auto = only when the gfx950 device scorer is active
-    overlap_engine: str = "off"
+    # ingests the previous batch meanwhile; auto = when the gfx950 device scorer is active
+    # (config 6 on MI355X: +45-50 % pods/s, profiles/bench/README.md)
+    overlap_engine: str = "auto"
     # event API (yodaRuntime.eventsAPI): upstream v1.20 records through events.k8s.io/v1
     events_api: str = "events.k8s.io/v1"
     trace: bool = False

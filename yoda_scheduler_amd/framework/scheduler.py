@@ -38,6 +38,7 @@ from .runtime import Framework
 log = logging.getLogger("yoda.scheduler")
 
 _EMPTY_STATE = CycleState()      # shared read-only state for all-native cycles
+ENGINE_SWITCH_INTERVAL_S = 0.0002
 POD_FIELD_SELECTOR = "status.phase!=Succeeded,status.phase!=Failed"   # upstream NewPodInformer
 _VOLATILE_META = ("resourceVersion", "generation", "managedFields")
 
@@ -596,7 +597,12 @@ class Scheduler:
             cycle, t0, ids, reqs = self._prepare_run(fw, item)
             if self._engine_exec is None:
                 import concurrent.futures
+                import sys
                 self._engine_exec = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="yoda-engine")
+                # the worker re-takes the GIL to hand back each batch's results; with the
+                # default 5 ms switch interval it waits that long behind the busy event loop
+                # (measured: +7 µs per pod on MI355X config 6), so ask for 0.2 ms
+                sys.setswitchinterval(min(sys.getswitchinterval(), ENGINE_SWITCH_INTERVAL_S))
             results = await loop.run_in_executor(self._engine_exec, self.engine.schedule_batch, ids, reqs)
             self._finish_run(fw, item, results, cycle, t0)
 
@@ -724,6 +730,9 @@ class Scheduler:
                 batch = [pi] + q.pop_batch(bs - 1)
                 if self._overlap():
                     await self.schedule_batch_overlapped(batch)
+                    # no yield here: the next batch's engine call starts first, and the
+                    # binds / informer events of this one run during its await
+                    continue
                 else:
                     self.schedule_batch(batch)
             else:
