@@ -74,3 +74,13 @@ def test_events_core_v1_fallback_and_preempted_related():
     pre = [e for e in evs if e["reason"] == "Preempted"][0]
     assert pre["action"] == "Preempting" and pre["regarding"]["name"] == "low"
     assert pre["related"]["name"] == "high" and pre["related"]["kind"] == "Pod"
+
+
+def test_micro_time_matches_datetime():
+    import random
+    from datetime import datetime, timezone
+    from yoda_scheduler_amd.framework.events import micro_time
+    rng = random.Random(1)
+    for _ in range(20000):
+        ts = rng.uniform(0, 2e9)
+        assert micro_time(ts) == datetime.fromtimestamp(ts, timezone.utc).strftime("%Y-%m-%dT%H:%M:%S.%fZ")

@@ -37,9 +37,19 @@ ACTIONS = {"Scheduled": "Binding", "FailedScheduling": "Scheduling", "Preempted"
 API_EVENTS_V1 = "events.k8s.io/v1"
 
 
+_SEC_CACHE = [-1, ""]
+
+
 def micro_time(ts: float) -> str:
-    """metav1.MicroTime: RFC 3339 with microseconds."""
-    return datetime.fromtimestamp(ts, timezone.utc).strftime("%Y-%m-%dT%H:%M:%S.%fZ")
+    """metav1.MicroTime: RFC 3339 with microseconds (the per-second prefix is cached: a burst
+    records hundreds of events within the same second)."""
+    sec = int(ts)
+    us = round((ts - sec) * 1e6)
+    if us >= 1_000_000:
+        sec, us = sec + 1, us - 1_000_000
+    if sec != _SEC_CACHE[0]:
+        _SEC_CACHE[0], _SEC_CACHE[1] = sec, datetime.fromtimestamp(sec, timezone.utc).strftime("%Y-%m-%dT%H:%M:%S")
+    return f"{_SEC_CACHE[1]}.{us:06d}Z"
 
 
 class EventRecorder:
