@@ -463,7 +463,40 @@ __global__ __launch_bounds__(kBlock) void k_score(yoda_dev_node_t* __restrict__ 
     int64_t best_o = LLONG_MAX;
     int32_t best_lb = 0;
     bool found = false;
-    if (search && act) {
+    if (search && act && k == 1) {
+      // single-GPU pods (the bulk of a mixed burst): the k = 1 table is {1<<0 … 1<<7} in
+      // order, so lane `sub` owns subset {sub}; no pairs (P = 0) and one NUMA domain leave
+      // only the fit and occupancy terms — the generic loop's 28 predicated pair adds and
+      // 8-card sums are skipped. Same integer arithmetic, so the result is bit-identical.
+      if ((emask >> sub) & 1u) {
+        uint64_t efs = ef[0];
+        uint32_t tos = tot[0], ocs = occ[0];
+#pragma unroll
+        for (int a = 1; a < YODA_DEV_CARDS; ++a) {
+          efs = sub == a ? ef[a] : efs;
+          tos = sub == a ? tot[a] : tos;
+          ocs = sub == a ? occ[a] : ocs;
+        }
+        const uint64_t fa = efs - r.memory;
+        const int64_t leftover = tos ? (int64_t)udiv(fa * 1000000ull, (uint64_t)tos) : 0;
+        const int64_t fit = r.binpack ? leftover : 1000000 - leftover;
+        const int64_t occ_bad = (int64_t)sdiv_small((int32_t)(ocs * 100u), 1);
+        best_o = r.w_fit * fit + r.w_occ * occ_bad;
+        best_m = 1u << sub;
+        best_lb = 0;
+        found = true;
+      }
+#pragma unroll
+      for (int off = 4; off > 0; off >>= 1) {
+        const int64_t oo = __shfl_xor(best_o, off, 64);
+        const uint32_t om = __shfl_xor(best_m, off, 64);
+        const int32_t ol = __shfl_xor(best_lb, off, 64);
+        const int of = __shfl_xor((int)found, off, 64);
+        if (of && (!found || better(oo, om, best_o, best_m))) {
+          best_o = oo; best_m = om; best_lb = ol; found = true;
+        }
+      }
+    } else if (search && act) {
       for (int t = s_begin + sub; t < s_end; t += kGroup) {
         const uint32_t m = s_masks[t];
         if (m & ~emask) continue;

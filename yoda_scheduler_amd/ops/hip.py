@@ -12,13 +12,15 @@ it cannot be loaded the call raises.
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from pathlib import Path
 from typing import Optional
 
 _LIB: Optional[ctypes.CDLL] = None
 _lock = threading.Lock()
-PATH = Path(__file__).resolve().parents[1] / "_native" / "libyoda_hip.so"
+# YODA_HIP_LIB points at another build of the kernels (same-box A/B of kernel variants)
+PATH = Path(os.environ.get("YODA_HIP_LIB") or Path(__file__).resolve().parents[1] / "_native" / "libyoda_hip.so")
 
 c_int, c_uint, c_ull, c_double, c_float, c_char_p, c_void_p = (
     ctypes.c_int, ctypes.c_uint, ctypes.c_ulonglong, ctypes.c_double, ctypes.c_float, ctypes.c_char_p,
