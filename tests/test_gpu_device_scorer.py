@@ -93,16 +93,27 @@ def test_scheduler_auto_enables_device_scorer_and_matches_cpu(require_gpu):
             assert all(len(g) == want[p] and node for p, (node, g) in placed.items())
             for n in {node for node, _ in placed.values()}:
                 assert all(st["reserved"] <= st["total"] for st in sched.cache.node_gpu_state(n))
+            # exact ledger: per GPU reserved == Σ scv/memory of the pods annotated onto it
+            want_mb: dict = {}
+            for i in range(300):
+                node, gs = placed[f"p{i}"]
+                for g in gs:
+                    want_mb[(node, g)] = want_mb.get((node, g), 0) + int(c.pod(f"p{i}")["metadata"]["labels"]["scv/memory"])
+            for n in {node for node, _ in placed.values()}:
+                for g, st in enumerate(sched.cache.node_gpu_state(n)):
+                    assert st["reserved"] == want_mb.get((n, g), 0), (n, g, st)
+            # overlapEngine auto: with the device scorer the batches ran on the engine worker
             stats = (sched.engine.device_enabled, sched.engine.device_cycles, sched.engine.device_fallbacks,
-                     sched.device_error)
+                     sched.device_error, sched._engine_exec is not None)
             await c.stop()
             return ok, placed, stats
         return asyncio.run(go())
 
-    ok_d, placed_d, (enabled, cycles, fallbacks, err) = run("auto")
-    ok_c, placed_c, (enabled_c, cycles_c, _, _) = run("off")
+    ok_d, placed_d, (enabled, cycles, fallbacks, err, overlapped) = run("auto")
+    ok_c, placed_c, (enabled_c, cycles_c, _, _, overlapped_c) = run("off")
     assert ok_d and ok_c
     assert enabled and cycles >= 300 and fallbacks == 0, (enabled, cycles, fallbacks, err)
+    assert overlapped and not overlapped_c
     assert not enabled_c and cycles_c == 0
     assert placed_d.keys() == placed_c.keys()
 
