@@ -50,6 +50,7 @@ constexpr int kGroup = 8;                 // lanes per node
 constexpr int kNodesPerWave = 64 / kGroup;
 constexpr int kPatchRows = 4;             // dirty rows passed by value (4 × 512 B + the filter's args < 4 KiB)
 constexpr int kFuseSelectMax = 2048;      // one block normalises + argmaxes up to this many nodes
+constexpr int kSelBatch = 8;              // nodes per thread whose loads select_block issues together
 constexpr int kBatchCap = 256;            // pods per batched launch sequence
 constexpr int kShards = 8;
 
@@ -319,16 +320,31 @@ __device__ unsigned long long select_block(int n, const yoda_dev_req_t& r, const
   if (hi == lo) --lo;
   const uint64_t den = (uint64_t)hi - (uint64_t)lo;
   unsigned long long best = 0;
-#pragma unroll 4
-  for (int i = blk * kBlock + threadIdx.x; i < n; i += nblk * kBlock) {
-    const uint8_t fe = feas[i];          // loads issued together; the branch comes after
-    int64_t f = total[i];
-    const int64_t rw = raw[i];
-    if (!fe) continue;
-    if (yoda_s) f += (int64_t)udiv(((uint64_t)rw - (uint64_t)lo) * 100ull, den) * r.w_yoda;
-    const uint32_t p = ((uint32_t)i * r.perm_mul + r.perm_add) & 0xFFFFFFu;
-    const unsigned long long key = ((unsigned long long)f << 24) | p;
-    best = key > best ? key : best;
+  // kSelBatch strided nodes per thread per pass: every load of a pass is issued before the
+  // first use, so the single-block (fused) walk pays ~n/(kBlock*kSelBatch) memory round
+  // trips instead of one per node stride
+  const int stride = nblk * kBlock;
+  for (int i0 = blk * kBlock + threadIdx.x; i0 < n; i0 += stride * kSelBatch) {
+    uint8_t fe[kSelBatch];
+    int64_t tv[kSelBatch], rv[kSelBatch];
+#pragma unroll
+    for (int k = 0; k < kSelBatch; ++k) {
+      const int i = i0 + k * stride;
+      const bool in = i < n;
+      fe[k] = in ? feas[i] : (uint8_t)0;
+      tv[k] = in ? total[i] : 0;
+      rv[k] = in ? raw[i] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kSelBatch; ++k) {
+      if (!fe[k]) continue;
+      const int i = i0 + k * stride;
+      int64_t f = tv[k];
+      if (yoda_s) f += (int64_t)udiv(((uint64_t)rv[k] - (uint64_t)lo) * 100ull, den) * r.w_yoda;
+      const uint32_t p = ((uint32_t)i * r.perm_mul + r.perm_add) & 0xFFFFFFu;
+      const unsigned long long key = ((unsigned long long)f << 24) | p;
+      best = key > best ? key : best;
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
