@@ -69,6 +69,10 @@ def main(argv=None) -> int:
     ap.add_argument("--transport", choices=["inproc", "http"], default="inproc",
                     help="inproc: fake apiserver in the scheduler process (headline); http: apiserver in its own "
                          "process, scheduler over the production HTTP/JSON client")
+    ap.add_argument("--apiserver", choices=["native", "python"], default="native",
+                    help="http transport: the C++ epoll fake apiserver (native) or the aiohttp one (python)")
+    ap.add_argument("--client", choices=["native", "aiohttp"], default="native",
+                    help="http transport: scheduler client on the native C++ transport or on aiohttp")
     a = ap.parse_args(argv)
     if a.reference_qps:
         a.qps, a.burst = 50.0, 100
@@ -110,7 +114,8 @@ def main(argv=None) -> int:
     if a.transport == "http":
         # one apiserver process per rank; bursts reuse it (the previous burst is deleted first)
         one = HttpShard(w, qps=a.qps, burst=a.burst, batch=a.batch, template=tmpl, events=not a.no_events,
-                        compat=a.compat, seed=rank * 1000, device=a.device, overlap=a.overlap)
+                        compat=a.compat, seed=rank * 1000, device=a.device, overlap=a.overlap,
+                        apiserver=a.apiserver, client_native=a.client == "native")
         shards = [one] * (a.warmup + a.steps)
         loop.run_until_complete(one.start())
     else:

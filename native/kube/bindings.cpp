@@ -1,0 +1,235 @@
+// pybind11 bindings of the native Kubernetes transport (module yoda_scheduler_amd._native._yoda_kube).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "json.hpp"
+#include "project.hpp"
+#include "transport.hpp"
+
+namespace py = pybind11;
+using namespace yk;
+
+namespace {
+
+py::object kv_dict(const std::vector<KV>& kvs) {
+  py::dict d;
+  for (const auto& kv : kvs) d[py::str(kv.first)] = py::str(kv.second);
+  return std::move(d);
+}
+
+py::list term_list(const TermP& t) {
+  py::list out;
+  for (const auto& r : t) {
+    py::list vals;
+    for (const auto& v : r.values) vals.append(py::str(v));
+    out.append(py::make_tuple(py::str(r.key), py::str(r.op), vals));
+  }
+  return out;
+}
+
+// positional arguments of PodInfo's fast constructor (yoda_scheduler_amd/kube/native.py)
+py::tuple info_args(const PodProj& p) {
+  py::object ann = p.has_annotations ? kv_dict(p.annotations) : py::none();
+  py::object nsel = p.has_node_selector ? kv_dict(p.node_selector) : py::none();
+  py::object req = py::none(), pref = py::none();
+  if (p.has_affinity) {
+    py::list r;
+    for (const auto& t : p.req_terms) r.append(term_list(t));
+    py::list pf;
+    for (const auto& wt : p.pref_terms) pf.append(py::make_tuple(wt.first, term_list(wt.second)));
+    req = std::move(r);
+    pref = std::move(pf);
+  }
+  py::object tols = py::none();
+  if (!p.tolerations.empty()) {
+    py::list t;
+    for (const auto& x : p.tolerations)
+      t.append(py::make_tuple(x.has_key ? py::object(py::str(x.key)) : py::object(py::none()), py::str(x.value),
+                              py::str(x.op), py::str(x.effect)));
+    tols = std::move(t);
+  }
+  py::object ports = py::none();
+  if (!p.ports.empty()) {
+    py::list t;
+    for (const auto& x : p.ports) t.append(py::make_tuple(x.host_port, py::str(x.protocol), py::str(x.host_ip)));
+    ports = std::move(t);
+  }
+  return py::make_tuple(py::str(p.uid), py::str(p.ns), py::str(p.name), kv_dict(p.labels), ann, py::str(p.sched),
+                        py::str(p.node), p.cpu, p.mem, p.nzc, p.nzm, p.priority, nsel, req, pref, tols, ports,
+                        p.flags, py::str(p.creation));
+}
+
+std::shared_ptr<PodEv> project_bytes(const std::string& raw) {
+  auto pe = std::make_shared<PodEv>();
+  try {
+    Value v = parse(raw);
+    project_pod(v, pe->p);
+  } catch (const ParseError& e) {
+    throw py::value_error(std::string("invalid JSON at ") + std::to_string(e.pos) + ": " + e.what);
+  }
+  pe->raw = raw;
+  return pe;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_yoda_kube, m) {
+  m.doc() = "Native Kubernetes API transport: pipelined HTTP/1.1 (+TLS), watch decoding, pod projection";
+
+  py::class_<PodEv, std::shared_ptr<PodEv>>(m, "PodEvent")
+      .def_property_readonly("ok", [](const PodEv& e) { return e.p.ok; })
+      .def_property_readonly("uid", [](const PodEv& e) { return e.p.uid; })
+      .def_property_readonly("namespace", [](const PodEv& e) { return e.p.ns; })
+      .def_property_readonly("name", [](const PodEv& e) { return e.p.name; })
+      .def_property_readonly("key", [](const PodEv& e) { return e.p.ns + "/" + e.p.name; })
+      .def_property_readonly("rv", [](const PodEv& e) { return e.p.rv; })
+      .def_property_readonly("node", [](const PodEv& e) { return e.p.node; })
+      .def_property_readonly("scheduler", [](const PodEv& e) { return e.p.sched; })
+      .def_property_readonly("phase", [](const PodEv& e) { return e.p.phase; })
+      .def_property_readonly("deleting", [](const PodEv& e) { return e.p.deleting; })
+      .def_property_readonly("hash", [](const PodEv& e) { return e.p.spec_meta_hash; })
+      .def_property_readonly("flags", [](const PodEv& e) { return e.p.flags; })
+      // (key, uid, node, scheduler, phase, hash): the per-event fields in one call
+      .def("ident", [](const PodEv& e) {
+        return py::make_tuple(py::str(e.p.ns + "/" + e.p.name), py::str(e.p.uid), py::str(e.p.node),
+                              py::str(e.p.sched), py::str(e.p.phase), e.p.spec_meta_hash);
+      })
+      .def("raw", [](const PodEv& e) { return py::bytes(e.raw); })
+      .def("info_args", [](const PodEv& e) -> py::object {
+        if (!e.p.ok) return py::none();
+        return info_args(e.p);
+      });
+
+  m.def("project", &project_bytes, py::arg("raw"), "Project a pod's JSON (tests / tooling).");
+  // PodList body → (resourceVersion, continue, [PodEvent]) — relists of large clusters
+  // never build Python dicts either
+  m.def("project_list", [](const std::string& body) {
+    std::vector<std::shared_ptr<PodEv>> evs;
+    std::string rv, cont;
+    {
+      py::gil_scoped_release rel;
+      Value v;
+      try {
+        v = parse(body);
+      } catch (const ParseError& e) {
+        py::gil_scoped_acquire acq;
+        throw py::value_error(std::string("invalid JSON list: ") + e.what);
+      }
+      if (const Value* m = v.get("metadata")) {
+        rv = std::string(m->sv("resourceVersion"));
+        cont = std::string(m->sv("continue"));
+      }
+      if (const Value* items = v.get("items"); items && items->t == Value::Arr) {
+        evs.reserve(items->arr.size());
+        for (const auto& it : items->arr) {
+          auto pe = std::make_shared<PodEv>();
+          project_pod(it, pe->p);
+          pe->raw = dump(it);
+          evs.push_back(std::move(pe));
+        }
+      }
+    }
+    py::list out;
+    for (auto& e : evs) out.append(py::cast(e));
+    return py::make_tuple(rv, cont, out);
+  });
+  m.def("quantity", [](const std::string& text, int scale) -> py::object {
+    int64_t out;
+    Value v = Value::str(text);
+    if (!quantity_scaled(v, scale, &out)) return py::none();
+    return py::int_(out);
+  });
+  m.def("canonical", [](const std::string& raw) {
+    try {
+      return py::bytes(dump(parse(raw)));
+    } catch (const ParseError& e) {
+      throw py::value_error(std::string("invalid JSON: ") + e.what);
+    }
+  }, "Parse + compact re-serialise (tests of the JSON codec).");
+  m.def("merge_patch", [](const std::string& target, const std::string& patch) {
+    Value t = parse(target);
+    merge_patch(t, parse(patch));
+    return py::bytes(dump(t));
+  });
+
+  py::class_<Transport>(m, "Transport")
+      .def(py::init([](const std::string& host, int port, bool tls, const std::string& prefix, const std::string& ca,
+                       const std::string& cert, const std::string& key, bool insecure, const std::string& token,
+                       int conns, int max_inflight, double qps, int burst) {
+             ClientConfig c;
+             c.host = host;
+             c.port = port;
+             c.tls = tls;
+             c.prefix = prefix;
+             c.ca_file = ca;
+             c.cert_file = cert;
+             c.key_file = key;
+             c.insecure = insecure;
+             c.token = token;
+             c.conns = conns;
+             c.max_inflight = max_inflight;
+             c.qps = qps;
+             c.burst = burst;
+             return std::make_unique<Transport>(std::move(c));
+           }),
+           py::arg("host"), py::arg("port"), py::arg("tls") = false, py::arg("prefix") = "", py::arg("ca") = "",
+           py::arg("cert") = "", py::arg("key") = "", py::arg("insecure") = false, py::arg("token") = "",
+           py::arg("conns") = 8, py::arg("max_inflight") = 64, py::arg("qps") = 0.0, py::arg("burst") = 0)
+      .def("fileno", &Transport::fd)
+      .def("request", [](Transport& t, const std::string& method, const std::string& path, py::bytes body,
+                         const std::string& ctype, bool limited, double timeout) {
+             return t.request(method, path, std::string(body), ctype, limited, timeout);
+           }, py::arg("method"), py::arg("path"), py::arg("body") = py::bytes(), py::arg("content_type") = "",
+           py::arg("limited") = true, py::arg("timeout") = 0.0)
+      .def("bind", &Transport::bind, py::arg("namespace"), py::arg("name"), py::arg("uid"), py::arg("node"),
+           py::arg("annotations"), py::arg("timeout") = 0.0)
+      .def("watch", &Transport::watch, py::arg("path"), py::arg("pods") = false)
+      .def("cancel", &Transport::cancel)
+      .def("set_token", &Transport::set_token)
+      .def("set_rate", &Transport::set_rate, py::arg("qps"), py::arg("burst"))
+      .def("close", [](Transport& t) {
+        py::gil_scoped_release rel;
+        t.close();
+      })
+      .def("stats", [](Transport& t) {
+        TransportStats s = t.stats();
+        py::dict d;
+        d["requests"] = s.requests;
+        d["responses"] = s.responses;
+        d["errors"] = s.errors;
+        d["timeouts"] = s.timeouts;
+        d["connects"] = s.connects;
+        d["watch_events"] = s.watch_events;
+        d["watch_bytes"] = s.watch_bytes;
+        d["parse_errors"] = s.parse_errors;
+        d["bytes_out"] = s.bytes_out;
+        d["bytes_in"] = s.bytes_in;
+        d["throttled"] = s.throttled;
+        return d;
+      })
+      // [(0, id, status, body) | (1, id, [(type, rv, PodEvent | bytes | None), ...]) | (2, id, status, body)]
+      .def("drain", [](Transport& t) {
+        std::vector<Completion> cs = t.drain();
+        // leaked on purpose: must outlive interpreter finalisation
+        static py::object* types = new py::object[5]{py::str("ADDED"), py::str("MODIFIED"), py::str("DELETED"),
+                                                      py::str("BOOKMARK"), py::str("ERROR")};
+        py::list out;
+        for (auto& c : cs) {
+          if (c.kind == Completion::kEvents) {
+            py::list evs;
+            for (auto& e : c.events) {
+              int ti = e.type == 'A' ? 0 : e.type == 'M' ? 1 : e.type == 'D' ? 2 : e.type == 'B' ? 3 : 4;
+              py::object payload;
+              if (e.pod) payload = py::cast(e.pod);
+              else if (e.type == 'B') payload = py::none();
+              else payload = py::bytes(e.raw);
+              evs.append(py::make_tuple(types[ti], py::str(e.rv), payload));
+            }
+            out.append(py::make_tuple(1, c.id, evs));
+          } else {
+            out.append(py::make_tuple(int(c.kind), c.id, c.status, py::bytes(c.body)));
+          }
+        }
+        return out;
+      });
+}

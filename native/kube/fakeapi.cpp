@@ -1,0 +1,1063 @@
+// Native fake kube-apiserver (see fakeapi.hpp).
+#include "fakeapi.hpp"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <signal.h>
+#include <sys/epoll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <ctime>
+#include <deque>
+#include <map>
+#include <memory>
+#include <random>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "http.hpp"
+#include "json.hpp"
+
+namespace yk {
+
+namespace {
+
+std::atomic<bool> g_stop{false};
+void on_signal(int) { g_stop = true; }
+
+double mono() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+std::string rfc3339_now() {
+  time_t t = time(nullptr);
+  struct tm tm;
+  gmtime_r(&t, &tm);
+  char buf[32];
+  strftime(buf, sizeof(buf), "%Y-%m-%dT%H:%M:%SZ", &tm);
+  return buf;
+}
+
+struct ResDef {
+  const char* key;
+  const char* group;
+  const char* version;
+  const char* name;
+  const char* kind;
+  bool namespaced;
+  std::string api_version() const { return group[0] ? std::string(group) + "/" + version : std::string(version); }
+};
+
+// mirrors yoda_scheduler_amd/kube/resources.py
+const ResDef kRes[] = {
+    {"pods", "", "v1", "pods", "Pod", true},
+    {"nodes", "", "v1", "nodes", "Node", false},
+    {"events", "", "v1", "events", "Event", true},
+    {"events.k8s.io", "events.k8s.io", "v1", "events", "Event", true},
+    {"leases", "coordination.k8s.io", "v1", "leases", "Lease", true},
+    {"scvs", "core.run-linux.com", "v1", "scvs", "Scv", false},
+    {"configmaps", "", "v1", "configmaps", "ConfigMap", true},
+    {"endpoints", "", "v1", "endpoints", "Endpoints", true},
+    {"persistentvolumeclaims", "", "v1", "persistentvolumeclaims", "PersistentVolumeClaim", true},
+    {"persistentvolumes", "", "v1", "persistentvolumes", "PersistentVolume", false},
+    {"storageclasses", "storage.k8s.io", "v1", "storageclasses", "StorageClass", false},
+    {"csinodes", "storage.k8s.io", "v1", "csinodes", "CSINode", false},
+    {"poddisruptionbudgets", "policy", "v1", "poddisruptionbudgets", "PodDisruptionBudget", true},
+    {"services", "", "v1", "services", "Service", true},
+    {"replicationcontrollers", "", "v1", "replicationcontrollers", "ReplicationController", true},
+    {"replicasets", "apps", "v1", "replicasets", "ReplicaSet", true},
+    {"statefulsets", "apps", "v1", "statefulsets", "StatefulSet", true},
+};
+
+struct Stored {
+  Value v;
+  std::string text;
+};
+using SP = std::shared_ptr<const Stored>;
+
+SP make_stored(Value v) {
+  auto s = std::make_shared<Stored>();
+  s->v = std::move(v);
+  s->text = dump(s->v);
+  return s;
+}
+
+struct HistEv {
+  int64_t rv;
+  char type;
+  SP obj, old;
+};
+
+// field selectors (kube/fields.py): requirements AND'ed, '=', '==' and '!=' on dotted paths
+struct FieldSel {
+  struct Req {
+    std::vector<std::string> path;
+    bool eq;
+    std::string val;
+  };
+  std::vector<Req> reqs;
+  bool empty() const { return reqs.empty(); }
+
+  static bool parse(const std::string& text, FieldSel& out) {
+    size_t i = 0;
+    while (i <= text.size()) {
+      size_t c = text.find(',', i);
+      std::string part(trim(std::string_view(text).substr(i, c == std::string::npos ? std::string::npos : c - i)));
+      i = c == std::string::npos ? text.size() + 1 : c + 1;
+      if (part.empty()) continue;
+      Req r;
+      size_t p;
+      std::string k;
+      if ((p = part.find("!=")) != std::string::npos) {
+        k = part.substr(0, p);
+        r.eq = false;
+        r.val = part.substr(p + 2);
+      } else if ((p = part.find("==")) != std::string::npos) {
+        k = part.substr(0, p);
+        r.eq = true;
+        r.val = part.substr(p + 2);
+      } else if ((p = part.find('=')) != std::string::npos) {
+        k = part.substr(0, p);
+        r.eq = true;
+        r.val = part.substr(p + 1);
+      } else {
+        return false;
+      }
+      k = std::string(trim(k));
+      r.val = std::string(trim(r.val));
+      size_t s = 0;
+      while (true) {
+        size_t d = k.find('.', s);
+        r.path.push_back(k.substr(s, d == std::string::npos ? std::string::npos : d - s));
+        if (d == std::string::npos) break;
+        s = d + 1;
+      }
+      out.reqs.push_back(std::move(r));
+    }
+    return true;
+  }
+
+  static std::string field(const Value& obj, const std::vector<std::string>& path) {
+    const Value* v = &obj;
+    for (const auto& k : path) {
+      if (v->t != Value::Obj) return "";
+      v = v->get(k);
+      if (!v || v->t == Value::Null) return "";
+    }
+    if (v->t == Value::Str || v->t == Value::Num) return v->s;
+    if (v->t == Value::Bool) return v->b ? "True" : "False";
+    return dump(*v);
+  }
+
+  bool matches(const Value& obj) const {
+    // group by path like the Python matcher: several '=' on one path never all hold
+    for (size_t i = 0; i < reqs.size(); ++i) {
+      std::string v = field(obj, reqs[i].path);
+      if (reqs[i].eq) {
+        if (v != reqs[i].val) return false;
+      } else if (v == reqs[i].val) {
+        return false;
+      }
+    }
+    return true;
+  }
+};
+
+char filter_event(const FieldSel& sel, char type, const Value& obj, const Value* old) {
+  if (type == 'A' || type == 'D') return sel.matches(obj) ? type : 0;
+  if (type != 'M') return type;
+  bool now = sel.matches(obj);
+  bool before = old && sel.matches(*old);
+  if (now && before) return 'M';
+  if (now) return 'A';
+  if (before) return 'D';
+  return 0;
+}
+
+const char* type_name(char t) {
+  switch (t) {
+    case 'A': return "ADDED";
+    case 'M': return "MODIFIED";
+    case 'D': return "DELETED";
+    case 'B': return "BOOKMARK";
+    default: return "ERROR";
+  }
+}
+
+void chunk(std::string& out, std::string_view data) {
+  char hdr[24];
+  int n = snprintf(hdr, sizeof(hdr), "%zx\r\n", data.size());
+  out.append(hdr, size_t(n));
+  out.append(data);
+  out.append("\r\n");
+}
+
+std::string frame(char type, const std::string& obj_text) {
+  std::string line;
+  line.reserve(obj_text.size() + 32);
+  line.append("{\"type\":\"").append(type_name(type)).append("\",\"object\":").append(obj_text).append("}\n");
+  std::string out;
+  out.reserve(line.size() + 16);
+  chunk(out, line);
+  return out;
+}
+
+const char* reason_phrase(int code) {
+  switch (code) {
+    case 200: return "OK";
+    case 201: return "Created";
+    case 400: return "Bad Request";
+    case 401: return "Unauthorized";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 409: return "Conflict";
+    case 410: return "Gone";
+    case 422: return "Unprocessable Entity";
+    case 500: return "Internal Server Error";
+    default: return "Status";
+  }
+}
+
+struct ApiErr {
+  int code;
+  std::string reason, message;
+};
+
+std::string status_text(const ApiErr& e) {
+  Value s = Value::object();
+  s.at("kind") = Value::str("Status");
+  s.at("apiVersion") = Value::str("v1");
+  s.at("status") = Value::str("Failure");
+  s.at("message") = Value::str(e.message);
+  s.at("reason") = Value::str(e.reason);
+  s.at("code") = Value::num(int64_t(e.code));
+  return dump(s);
+}
+
+struct Conn;
+
+struct Watcher {
+  Conn* conn = nullptr;
+  struct ResState* rs = nullptr;
+  FieldSel sel;
+  std::string ns;          // namespaced watch: only this namespace
+  double deadline = 0;
+  bool bookmarks = false;
+  bool dead = false;
+};
+
+struct ResState {
+  const ResDef* def = nullptr;
+  std::map<std::string, SP> objs;
+  std::deque<HistEv> hist;
+  int64_t oldest_rv = 0;
+  std::vector<Watcher*> watchers;
+};
+
+struct Conn {
+  int fd = -1;
+  RequestParser rp;
+  Request req;
+  std::string wbuf;
+  size_t woff = 0;
+  std::unique_ptr<Watcher> watcher;
+  bool close_after_write = false;
+  bool want_out = false;
+  bool dead = false;
+};
+
+class Server {
+ public:
+  explicit Server(const FakeApiOptions& o) : opt_(o) {
+    for (const auto& d : kRes) {
+      auto rs = std::make_unique<ResState>();
+      rs->def = &d;
+      by_key_[d.key] = rs.get();
+      by_path_[std::string(d.group) + "/" + d.name] = rs.get();
+      res_.push_back(std::move(rs));
+    }
+    std::random_device rd;
+    std::mt19937_64 g(rd());
+    char buf[24];
+    snprintf(buf, sizeof(buf), "%016llx", static_cast<unsigned long long>(g()));
+    uid_prefix_ = std::string("nf") + buf;
+  }
+
+  int run();
+
+ private:
+  // ------------------------------------------------------------------ store
+  std::string key_of(const ResDef& d, const Value& obj) const {
+    const Value* m = obj.get("metadata");
+    std::string name = m ? std::string(m->sv("name")) : "";
+    if (!d.namespaced) return name;
+    std::string ns = m ? std::string(m->sv("namespace")) : "";
+    if (ns.empty()) ns = "default";
+    return ns + "/" + name;
+  }
+
+  void emit(ResState& rs, char type, const SP& obj, const SP& old) {
+    const Value* m = obj->v.get("metadata");
+    int64_t rv = m && m->get("resourceVersion") ? m->get("resourceVersion")->as_int() : last_rv_;
+    rs.hist.push_back(HistEv{rv, type, obj, old});
+    while (rs.hist.size() > opt_.history) {
+      rs.oldest_rv = rs.hist.front().rv;
+      rs.hist.pop_front();
+    }
+    if (rs.watchers.empty()) return;
+    std::string frames[3];
+    std::string ns = m ? std::string(m->sv("namespace")) : "";
+    for (Watcher* w : rs.watchers) {
+      if (w->dead) continue;
+      if (!w->ns.empty() && ns != w->ns) continue;
+      char t = w->sel.empty() ? type : filter_event(w->sel, type, obj->v, old ? &old->v : nullptr);
+      if (!t) continue;
+      int fi = t == 'A' ? 0 : t == 'M' ? 1 : 2;
+      if (frames[fi].empty()) frames[fi] = frame(t, obj->text);
+      w->conn->wbuf.append(frames[fi]);
+      mark_out(w->conn);
+    }
+  }
+
+  std::string next_rv() { return std::to_string(++last_rv_); }
+
+  SP create(ResState& rs, Value obj, const std::string& path_ns, ApiErr* err) {
+    const ResDef& d = *rs.def;
+    if (obj.t != Value::Obj) {
+      *err = {400, "BadRequest", "object expected"};
+      return nullptr;
+    }
+    Value& meta = obj.at("metadata");
+    if (meta.t != Value::Obj) meta = Value::object();
+    if (d.namespaced) {
+      std::string_view ns = meta.sv("namespace");
+      if (ns.empty()) meta.at("namespace") = Value::str(path_ns.empty() ? "default" : path_ns);
+    }
+    if (meta.sv("name").empty()) {
+      std::string_view gen = meta.sv("generateName");
+      if (gen.empty()) {
+        *err = {422, "Invalid", "metadata.name required"};
+        return nullptr;
+      }
+      char buf[8];
+      snprintf(buf, sizeof(buf), "%05x", unsigned(++gen_counter_ & 0xfffff));
+      meta.at("name") = Value::str(std::string(gen) + buf);
+    }
+    if (!obj.get("apiVersion")) obj.at("apiVersion") = Value::str(d.api_version());
+    if (!obj.get("kind")) obj.at("kind") = Value::str(d.kind);
+    Value& m2 = obj.at("metadata");
+    if (m2.sv("uid").empty()) {
+      char buf[24];
+      snprintf(buf, sizeof(buf), "-%012llx", static_cast<unsigned long long>(++uid_counter_));
+      m2.at("uid") = Value::str(uid_prefix_ + buf);
+    }
+    m2.at("resourceVersion") = Value::str(next_rv());
+    if (!m2.get("creationTimestamp")) m2.at("creationTimestamp") = Value::str(rfc3339_now());
+    std::string key = key_of(d, obj);
+    if (rs.objs.count(key)) {
+      --last_rv_;
+      *err = {409, "AlreadyExists", std::string(d.key) + " " + key + " already exists"};
+      return nullptr;
+    }
+    SP s = make_stored(std::move(obj));
+    rs.objs[key] = s;
+    if (&rs == by_key_["pods"]) create_log_[key] = mono();
+    emit(rs, 'A', s, nullptr);
+    return s;
+  }
+
+  SP update(ResState& rs, const Value& body, const std::string& path_ns, const std::string& name, bool status_only,
+            ApiErr* err) {
+    const ResDef& d = *rs.def;
+    const Value* bm = body.get("metadata");
+    std::string nm = bm ? std::string(bm->sv("name")) : "";
+    if (nm.empty()) nm = name;
+    std::string ns = bm ? std::string(bm->sv("namespace")) : "";
+    if (ns.empty()) ns = path_ns.empty() ? "default" : path_ns;
+    std::string key = d.namespaced ? ns + "/" + nm : nm;
+    auto it = rs.objs.find(key);
+    if (it == rs.objs.end()) {
+      *err = {404, "NotFound", std::string(d.key) + " " + key + " not found"};
+      return nullptr;
+    }
+    SP cur = it->second;
+    std::string_view rv = bm ? bm->sv("resourceVersion") : std::string_view();
+    const Value* cm = cur->v.get("metadata");
+    if (!rv.empty() && cm && rv != cm->sv("resourceVersion")) {
+      *err = {409, "Conflict", std::string(d.key) + " " + key + ": the object has been modified"};
+      return nullptr;
+    }
+    Value nv;
+    if (status_only) {
+      nv = cur->v;
+      const Value* st = body.get("status");
+      nv.at("status") = st ? *st : Value();
+    } else {
+      nv = body;
+      if (!body.get("status")) {
+        if (const Value* cst = cur->v.get("status")) nv.at("status") = *cst;
+      }
+    }
+    Value meta = cm ? *cm : Value::object();
+    if (bm && bm->t == Value::Obj) {
+      for (const auto& kv : bm->obj) {
+        if (kv.first == "uid" || kv.first == "creationTimestamp" || kv.first == "resourceVersion") continue;
+        meta.at(kv.first) = kv.second;
+      }
+    }
+    meta.at("resourceVersion") = Value::str(next_rv());
+    nv.at("metadata") = std::move(meta);
+    SP s = make_stored(std::move(nv));
+    it->second = s;
+    emit(rs, 'M', s, cur);
+    return s;
+  }
+
+  SP patch(ResState& rs, const Value& p, const std::string& path_ns, const std::string& name, ApiErr* err) {
+    const ResDef& d = *rs.def;
+    std::string key = d.namespaced ? (path_ns.empty() ? "default" : path_ns) + "/" + name : name;
+    auto it = rs.objs.find(key);
+    if (it == rs.objs.end()) {
+      *err = {404, "NotFound", std::string(d.key) + " " + key + " not found"};
+      return nullptr;
+    }
+    SP cur = it->second;
+    Value nv = cur->v;
+    merge_patch(nv, p);
+    Value& meta = nv.at("metadata");
+    if (meta.t != Value::Obj) meta = Value::object();
+    meta.at("resourceVersion") = Value::str(next_rv());
+    if (const Value* cm = cur->v.get("metadata")) {
+      for (const char* k : {"uid", "name", "namespace", "creationTimestamp"})
+        if (const Value* x = cm->get(k)) meta.at(k) = *x;
+    }
+    SP s = make_stored(std::move(nv));
+    it->second = s;
+    emit(rs, 'M', s, cur);
+    return s;
+  }
+
+  SP remove(ResState& rs, const std::string& key, ApiErr* err) {
+    auto it = rs.objs.find(key);
+    if (it == rs.objs.end()) {
+      *err = {404, "NotFound", std::string(rs.def->key) + " " + key + " not found"};
+      return nullptr;
+    }
+    SP cur = it->second;
+    rs.objs.erase(it);
+    Value gone = cur->v;
+    gone.at("metadata").at("resourceVersion") = Value::str(next_rv());
+    SP s = make_stored(std::move(gone));
+    emit(rs, 'D', s, nullptr);
+    return s;
+  }
+
+  bool bind(const std::string& ns, const std::string& name, const Value& body, ApiErr* err) {
+    ResState& rs = *by_key_["pods"];
+    std::string key = ns + "/" + name;
+    auto it = rs.objs.find(key);
+    if (it == rs.objs.end()) {
+      *err = {404, "NotFound", "pods " + key + " not found"};
+      return false;
+    }
+    SP cur = it->second;
+    const Value* bm = body.get("metadata");
+    std::string_view uid = bm ? bm->sv("uid") : std::string_view();
+    const Value* cm = cur->v.get("metadata");
+    if (!uid.empty() && cm && cm->sv("uid") != uid) {
+      *err = {409, "Conflict", "pod " + key + " uid mismatch"};
+      return false;
+    }
+    const Value* cs = cur->v.get("spec");
+    if (cs && !cs->sv("nodeName").empty()) {
+      *err = {409, "Conflict", "pod " + key + " is already assigned to node " + std::string(cs->sv("nodeName"))};
+      return false;
+    }
+    const Value* tgt = body.get("target");
+    std::string node = tgt ? std::string(tgt->sv("name")) : "";
+    Value nv = cur->v;
+    nv.at("spec").at("nodeName") = Value::str(node);
+    Value& status = nv.at("status");
+    if (status.t != Value::Obj) status = Value::object();
+    Value conds = Value::array();
+    if (const Value* old = status.get("conditions"); old && old->t == Value::Arr) {
+      for (const auto& c : old->arr)
+        if (c.sv("type") != "PodScheduled") conds.arr.push_back(c);
+    }
+    Value c = Value::object();
+    c.at("type") = Value::str("PodScheduled");
+    c.at("status") = Value::str("True");
+    c.at("lastTransitionTime") = Value::str(rfc3339_now());
+    conds.arr.push_back(std::move(c));
+    status.at("conditions") = std::move(conds);
+    Value& meta = nv.at("metadata");
+    if (bm) {
+      if (const Value* ann = bm->get("annotations"); ann && ann->t == Value::Obj && !ann->obj.empty()) {
+        Value& ma = meta.at("annotations");
+        if (ma.t != Value::Obj) ma = Value::object();
+        for (const auto& kv : ann->obj) ma.at(kv.first) = kv.second;
+      }
+    }
+    meta.at("resourceVersion") = Value::str(next_rv());
+    SP s = make_stored(std::move(nv));
+    it->second = s;
+    bind_log_[key] = mono();
+    emit(rs, 'M', s, cur);
+    return true;
+  }
+
+  // ------------------------------------------------------------------ HTTP
+  void respond(Conn* c, int code, std::string_view body, bool keep_alive = true) {
+    std::string& w = c->wbuf;
+    char hdr[160];
+    int n = snprintf(hdr, sizeof(hdr), "HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %zu\r\n%s\r\n",
+                     code, reason_phrase(code), body.size(), keep_alive ? "" : "Connection: close\r\n");
+    w.append(hdr, size_t(n));
+    w.append(body);
+    if (!keep_alive) c->close_after_write = true;
+    mark_out(c);
+  }
+
+  void respond_err(Conn* c, const ApiErr& e) { respond(c, e.code, status_text(e)); }
+
+  void mark_out(Conn* c) {
+    if (!c->want_out) {
+      c->want_out = true;
+      dirty_.push_back(c);
+    }
+  }
+
+  void handle(Conn* c, Request& req);
+  void handle_bench(Conn* c, Request& req);
+  void handle_list(Conn* c, ResState& rs, const std::string& ns, const Request& req);
+  void start_watch(Conn* c, ResState& rs, const std::string& ns, const Request& req);
+  void finish_watch(Conn* c);
+  void flush(Conn* c);
+  void close_conn(Conn* c);
+  void send_bookmarks(ResState& rs);
+
+  FakeApiOptions opt_;
+  std::vector<std::unique_ptr<ResState>> res_;
+  std::unordered_map<std::string, ResState*> by_key_, by_path_;
+  int64_t last_rv_ = 0;
+  uint64_t uid_counter_ = 0, gen_counter_ = 0;
+  std::string uid_prefix_;
+  int ep_ = -1, lfd_ = -1;
+  std::vector<Conn*> dirty_;
+  std::unordered_map<int, std::unique_ptr<Conn>> conns_;
+  // bench
+  std::vector<Value> templates_;
+  std::unordered_map<std::string, double> create_log_, bind_log_;
+};
+
+void Server::flush(Conn* c) {
+  c->want_out = false;
+  if (c->dead) return;
+  while (c->woff < c->wbuf.size()) {
+    ssize_t n = ::send(c->fd, c->wbuf.data() + c->woff, c->wbuf.size() - c->woff, MSG_NOSIGNAL);
+    if (n < 0) {
+      if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+      close_conn(c);
+      return;
+    }
+    c->woff += size_t(n);
+  }
+  epoll_event ev{};
+  ev.data.ptr = c;
+  if (c->woff >= c->wbuf.size()) {
+    c->wbuf.clear();
+    c->woff = 0;
+    if (c->close_after_write) {
+      close_conn(c);
+      return;
+    }
+    ev.events = EPOLLIN | EPOLLRDHUP;
+  } else {
+    if (c->woff > (4u << 20)) {
+      c->wbuf.erase(0, c->woff);
+      c->woff = 0;
+    }
+    ev.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP;
+  }
+  epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &ev);
+}
+
+void Server::close_conn(Conn* c) {
+  if (c->dead) return;
+  c->dead = true;
+  if (c->watcher) {
+    c->watcher->dead = true;
+    auto& ws = c->watcher->rs->watchers;
+    ws.erase(std::remove(ws.begin(), ws.end(), c->watcher.get()), ws.end());
+  }
+  epoll_ctl(ep_, EPOLL_CTL_DEL, c->fd, nullptr);
+  ::close(c->fd);
+}
+
+void Server::finish_watch(Conn* c) {
+  if (!c->watcher) return;
+  auto& ws = c->watcher->rs->watchers;
+  ws.erase(std::remove(ws.begin(), ws.end(), c->watcher.get()), ws.end());
+  c->watcher.reset();
+  c->wbuf.append("0\r\n\r\n");
+  mark_out(c);
+}
+
+void Server::send_bookmarks(ResState& rs) {
+  std::string obj = "{\"kind\":\"" + std::string(rs.def->kind) + "\",\"apiVersion\":\"" + rs.def->api_version() +
+                    "\",\"metadata\":{\"resourceVersion\":\"" + std::to_string(last_rv_) + "\"}}";
+  std::string f = frame('B', obj);
+  for (Watcher* w : rs.watchers) {
+    if (w->dead || !w->bookmarks) continue;
+    w->conn->wbuf.append(f);
+    mark_out(w->conn);
+  }
+}
+
+void Server::handle_list(Conn* c, ResState& rs, const std::string& ns, const Request& req) {
+  const ResDef& d = *rs.def;
+  FieldSel sel;
+  std::string fs = query_param(req.query, "fieldSelector");
+  if (!fs.empty() && !FieldSel::parse(fs, sel)) {
+    respond_err(c, {400, "BadRequest", "invalid field selector"});
+    return;
+  }
+  long limit = std::atol(query_param(req.query, "limit", "0").c_str());
+  std::string cont = query_param(req.query, "continue");
+  int64_t rv = last_rv_;
+  std::string start;
+  bool paged = limit > 0 || !cont.empty();
+  if (!cont.empty()) {
+    size_t dot = cont.find('.');
+    if (dot == std::string::npos) {
+      respond_err(c, {400, "BadRequest", "invalid continue token"});
+      return;
+    }
+    rv = std::atoll(cont.substr(0, dot).c_str());
+    std::string hex = cont.substr(dot + 1);
+    for (size_t i = 0; i + 1 < hex.size(); i += 2) start.push_back(char(unhex(hex[i]) * 16 + unhex(hex[i + 1])));
+    if (rv < rs.oldest_rv) {
+      respond_err(c, {410, "Expired", "the provided continue parameter is too old"});
+      return;
+    }
+  }
+  std::string out;
+  out.reserve(4096);
+  out.append("{\"kind\":\"").append(d.kind).append("List\",\"apiVersion\":\"").append(d.api_version());
+  out.append("\",\"items\":[");
+  long n = 0;
+  std::string last_key;
+  bool more = false;
+  auto it = paged && !start.empty() ? rs.objs.upper_bound(start) : rs.objs.begin();
+  for (; it != rs.objs.end(); ++it) {
+    const Stored& s = *it->second;
+    if (d.namespaced && !ns.empty()) {
+      const Value* m = s.v.get("metadata");
+      if (!m || m->sv("namespace") != ns) continue;
+    }
+    if (!sel.empty() && !sel.matches(s.v)) continue;
+    if (paged && limit > 0 && n >= limit) {
+      more = true;
+      break;
+    }
+    if (n) out.push_back(',');
+    out.append(s.text);
+    last_key = it->first;
+    ++n;
+  }
+  out.append("],\"metadata\":{\"resourceVersion\":\"").append(std::to_string(rv)).append("\"");
+  if (more) {
+    static const char hx[] = "0123456789abcdef";
+    std::string tok = std::to_string(rv) + ".";
+    for (unsigned char ch : last_key) {
+      tok.push_back(hx[ch >> 4]);
+      tok.push_back(hx[ch & 15]);
+    }
+    out.append(",\"continue\":\"").append(tok).append("\"");
+  }
+  out.append("}}");
+  respond(c, 200, out);
+}
+
+void Server::start_watch(Conn* c, ResState& rs, const std::string& ns, const Request& req) {
+  auto w = std::make_unique<Watcher>();
+  std::string fs = query_param(req.query, "fieldSelector");
+  if (!fs.empty() && !FieldSel::parse(fs, w->sel)) {
+    respond_err(c, {400, "BadRequest", "invalid field selector"});
+    return;
+  }
+  c->wbuf.append("HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n\r\n");
+  mark_out(c);
+  int64_t rv = std::atoll(query_param(req.query, "resourceVersion", "0").c_str());
+  if (rv && rv < rs.oldest_rv) {
+    chunk(c->wbuf, "{\"type\":\"ERROR\",\"object\":" + status_text({410, "Expired", "too old resource version"}) + "}\n");
+    c->wbuf.append("0\r\n\r\n");
+    return;
+  }
+  w->conn = c;
+  w->rs = &rs;
+  if (rs.def->namespaced) w->ns = ns;
+  double to = std::atof(query_param(req.query, "timeoutSeconds", "300").c_str());
+  w->deadline = mono() + (to > 0 ? to : 300);
+  std::string bm = query_param(req.query, "allowWatchBookmarks");
+  w->bookmarks = bm == "true" || bm == "1";
+  if (rv) {
+    for (const HistEv& h : rs.hist) {
+      if (h.rv <= rv) continue;
+      if (!w->ns.empty()) {
+        const Value* m = h.obj->v.get("metadata");
+        if (!m || m->sv("namespace") != w->ns) continue;
+      }
+      char t = w->sel.empty() ? h.type : filter_event(w->sel, h.type, h.obj->v, h.old ? &h.old->v : nullptr);
+      if (!t) continue;
+      c->wbuf.append(frame(t, h.obj->text));
+    }
+  }
+  rs.watchers.push_back(w.get());
+  c->watcher = std::move(w);
+}
+
+void Server::handle_bench(Conn* c, Request& req) {
+  const std::string& p = req.path;
+  ResState& pods = *by_key_["pods"];
+  if (p == "/debug/bench/load") {
+    Value b;
+    try {
+      b = parse(req.body);
+    } catch (const ParseError&) {
+      respond_err(c, {400, "BadRequest", "invalid JSON"});
+      return;
+    }
+    templates_.clear();
+    if (const Value* ps = b.get("pods"); ps && ps->t == Value::Arr) templates_ = ps->arr;
+    respond(c, 200, "{\"n\":" + std::to_string(templates_.size()) + "}");
+    return;
+  }
+  if (p == "/debug/bench/burst") {
+    Value b;
+    try {
+      b = parse(req.body.empty() ? std::string("{}") : req.body);
+    } catch (const ParseError&) {
+      respond_err(c, {400, "BadRequest", "invalid JSON"});
+      return;
+    }
+    std::string tag = std::string(b.sv("tag"));
+    if (tag.empty()) tag = "b";
+    create_log_.clear();
+    bind_log_.clear();
+    size_t i = 0;
+    for (const Value& t : templates_) {
+      Value o = t;
+      o.at("metadata").at("name") = Value::str(tag + "-" + std::to_string(i));
+      ApiErr err;
+      create(pods, std::move(o), "", &err);
+      if (++i % 64 == 0) {
+        // let the watchers see the burst while it is being created
+        std::vector<Conn*> d;
+        d.swap(dirty_);
+        for (Conn* x : d) flush(x);
+      }
+    }
+    respond(c, 200, "{\"n\":" + std::to_string(templates_.size()) + "}");
+    return;
+  }
+  if (p == "/debug/bench/status") {
+    std::string out = "{\"created\":" + std::to_string(create_log_.size()) + ",\"bound\":" + std::to_string(bind_log_.size());
+    if (!query_param(req.query, "full").empty()) {
+      out.append(",\"latencies\":[");
+      double t0 = 1e300, tend = 0;
+      for (const auto& kv : create_log_) t0 = std::min(t0, kv.second);
+      bool first = true;
+      char buf[40];
+      for (const auto& kv : bind_log_) {
+        tend = std::max(tend, kv.second);
+        auto ci = create_log_.find(kv.first);
+        if (ci == create_log_.end()) continue;
+        if (!first) out.push_back(',');
+        first = false;
+        int n = snprintf(buf, sizeof(buf), "%.9f", kv.second - ci->second);
+        out.append(buf, size_t(n));
+      }
+      int n = snprintf(buf, sizeof(buf), "%.9f", bind_log_.empty() ? 0.0 : tend - t0);
+      out.append("],\"elapsed\":").append(buf, size_t(n));
+    }
+    out.append("}");
+    respond(c, 200, out);
+    return;
+  }
+  if (p == "/debug/bench/reset") {
+    std::vector<std::string> keys;
+    for (const auto& kv : pods.objs) keys.push_back(kv.first);
+    ApiErr err;
+    for (const auto& k : keys) remove(pods, k, &err);
+    create_log_.clear();
+    bind_log_.clear();
+    respond(c, 200, "{\"deleted\":" + std::to_string(keys.size()) + "}");
+    return;
+  }
+  respond_err(c, {404, "NotFound", "no route for " + p});
+}
+
+void Server::handle(Conn* c, Request& req) {
+  const std::string& path = req.path;
+  if (path == "/healthz" || path == "/readyz" || path == "/livez") {
+    respond(c, 200, "ok");
+    return;
+  }
+  if (path == "/version") {
+    respond(c, 200, "{\"major\":\"1\",\"minor\":\"20\",\"gitVersion\":\"v1.20.0-yoda-fake-native\"}");
+    return;
+  }
+  if (path.rfind("/debug/bench/", 0) == 0) {
+    handle_bench(c, req);
+    return;
+  }
+  if (path == "/debug/bookmark") {
+    auto it = by_key_.find(query_param(req.query, "resource", "pods"));
+    if (it != by_key_.end()) send_bookmarks(*it->second);
+    respond(c, 200, "{}");
+    return;
+  }
+  if (!opt_.token.empty() && req.headers.get("authorization") != "Bearer " + opt_.token) {
+    respond_err(c, {401, "Unauthorized", "Unauthorized"});
+    return;
+  }
+  // /api/v1[/namespaces/NS]/RES[/NAME[/SUB]]  |  /apis/G/V[/namespaces/NS]/RES[/NAME[/SUB]]
+  std::vector<std::string> parts;
+  size_t s = 1;
+  while (s <= path.size()) {
+    size_t e = path.find('/', s);
+    parts.push_back(url_decode(std::string_view(path).substr(s, e == std::string::npos ? std::string::npos : e - s)));
+    if (e == std::string::npos) break;
+    s = e + 1;
+  }
+  size_t i;
+  std::string group;
+  if (parts.size() >= 2 && parts[0] == "api" && parts[1] == "v1") {
+    i = 2;
+  } else if (parts.size() >= 3 && parts[0] == "apis") {
+    group = parts[1];
+    i = 3;
+  } else {
+    respond_err(c, {404, "NotFound", "no route for " + path});
+    return;
+  }
+  std::string ns, name, sub;
+  if (parts.size() > i + 2 && parts[i] == "namespaces") {
+    ns = parts[i + 1];
+    i += 2;
+  }
+  if (i >= parts.size() || parts.size() > i + 3) {
+    respond_err(c, {404, "NotFound", "no route for " + path});
+    return;
+  }
+  auto rit = by_path_.find(group + "/" + parts[i]);
+  if (rit == by_path_.end()) {
+    respond_err(c, {404, "NotFound", "no route for " + path});
+    return;
+  }
+  ResState& rs = *rit->second;
+  if (parts.size() > i + 1) name = parts[i + 1];
+  if (parts.size() > i + 2) sub = parts[i + 2];
+  const std::string& m = req.method;
+  ApiErr err;
+  if (m == "GET") {
+    if (name.empty()) {
+      std::string w = query_param(req.query, "watch");
+      if (w == "1" || w == "true") start_watch(c, rs, ns, req);
+      else handle_list(c, rs, ns, req);
+      return;
+    }
+    std::string key = rs.def->namespaced ? (ns.empty() ? "default" : ns) + "/" + name : name;
+    auto it = rs.objs.find(key);
+    if (it == rs.objs.end()) respond_err(c, {404, "NotFound", std::string(rs.def->key) + " " + key + " not found"});
+    else respond(c, 200, it->second->text);
+    return;
+  }
+  Value body;
+  if (!req.body.empty()) {
+    try {
+      body = parse(req.body);
+    } catch (const ParseError&) {
+      respond_err(c, {400, "BadRequest", "invalid JSON body"});
+      return;
+    }
+  }
+  if (m == "POST") {
+    if (sub == "binding" && rs.def == &kRes[0]) {
+      if (bind(ns.empty() ? "default" : ns, name, body, &err))
+        respond(c, 201, "{\"kind\":\"Status\",\"apiVersion\":\"v1\",\"status\":\"Success\",\"code\":201}");
+      else
+        respond_err(c, err);
+      return;
+    }
+    SP s2 = create(rs, std::move(body), ns, &err);
+    if (s2) respond(c, 201, s2->text);
+    else respond_err(c, err);
+    return;
+  }
+  if (m == "PUT") {
+    SP s2 = update(rs, body, ns, name, sub == "status", &err);
+    if (s2) respond(c, 200, s2->text);
+    else respond_err(c, err);
+    return;
+  }
+  if (m == "PATCH") {
+    SP s2 = patch(rs, body, ns, name, &err);
+    if (s2) respond(c, 200, s2->text);
+    else respond_err(c, err);
+    return;
+  }
+  if (m == "DELETE") {
+    std::string key = rs.def->namespaced ? (ns.empty() ? "default" : ns) + "/" + name : name;
+    SP s2 = remove(rs, key, &err);
+    if (s2) respond(c, 200, s2->text);
+    else respond_err(c, err);
+    return;
+  }
+  respond_err(c, {405, "MethodNotAllowed", m});
+}
+
+int Server::run() {
+  signal(SIGPIPE, SIG_IGN);
+  signal(SIGTERM, on_signal);
+  signal(SIGINT, on_signal);
+  lfd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+  int one = 1;
+  setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(uint16_t(opt_.port));
+  if (inet_pton(AF_INET, opt_.host.c_str(), &a.sin_addr) != 1) {
+    fprintf(stderr, "bad host %s\n", opt_.host.c_str());
+    return 2;
+  }
+  if (::bind(lfd_, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0 || ::listen(lfd_, 1024) != 0) {
+    perror("bind/listen");
+    return 2;
+  }
+  socklen_t al = sizeof(a);
+  getsockname(lfd_, reinterpret_cast<sockaddr*>(&a), &al);
+  int port = ntohs(a.sin_port);
+  if (!opt_.port_file.empty()) {
+    std::string tmp = opt_.port_file + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "w");
+    if (f) {
+      fprintf(f, "%d", port);
+      fclose(f);
+      rename(tmp.c_str(), opt_.port_file.c_str());
+    }
+  }
+  printf("native fake apiserver listening on http://%s:%d\n", opt_.host.c_str(), port);
+  fflush(stdout);
+  ep_ = epoll_create1(EPOLL_CLOEXEC);
+  epoll_event lev{};
+  lev.events = EPOLLIN;
+  lev.data.ptr = nullptr;
+  epoll_ctl(ep_, EPOLL_CTL_ADD, lfd_, &lev);
+  epoll_event evs[256];
+  std::vector<char> buf(1 << 16);
+  double next_tick = mono() + 0.5, next_bm = opt_.bookmark_interval_s > 0 ? mono() + opt_.bookmark_interval_s : 1e300;
+  while (!g_stop) {
+    int n = epoll_wait(ep_, evs, 256, 100);
+    if (n < 0 && errno != EINTR) break;
+    for (int k = 0; k < n; ++k) {
+      if (evs[k].data.ptr == nullptr) {
+        while (true) {
+          int fd = ::accept4(lfd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+          if (fd < 0) break;
+          setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+          auto c = std::make_unique<Conn>();
+          c->fd = fd;
+          epoll_event ev{};
+          ev.events = EPOLLIN | EPOLLRDHUP;
+          ev.data.ptr = c.get();
+          epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &ev);
+          conns_[fd] = std::move(c);
+        }
+        continue;
+      }
+      Conn* c = static_cast<Conn*>(evs[k].data.ptr);
+      if (c->dead) continue;
+      if (evs[k].events & EPOLLOUT) flush(c);
+      if (c->dead) continue;
+      if (evs[k].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) {
+        while (!c->dead) {
+          ssize_t r = ::recv(c->fd, buf.data(), buf.size(), 0);
+          if (r < 0) {
+            if (errno != EAGAIN && errno != EWOULDBLOCK) close_conn(c);
+            break;
+          }
+          if (r == 0) {
+            close_conn(c);
+            break;
+          }
+          size_t off = 0;
+          while (off < size_t(r) && !c->dead) {
+            bool done = false;
+            long used = c->rp.feed(buf.data() + off, size_t(r) - off, &done, c->req);
+            if (used < 0) {
+              respond(c, 400, status_text({400, "BadRequest", "malformed request"}), false);
+              break;
+            }
+            off += size_t(used);
+            if (done) {
+              if (c->watcher) {
+                // a request after a watch on the same connection: end the stream first
+                finish_watch(c);
+              }
+              handle(c, c->req);
+              if (!c->req.keep_alive) c->close_after_write = true;
+            }
+          }
+          if (size_t(r) < buf.size()) break;
+        }
+      }
+    }
+    double now = mono();
+    if (now >= next_tick) {
+      next_tick = now + 0.5;
+      for (auto& rs : res_) {
+        std::vector<Watcher*> expired;
+        for (Watcher* w : rs->watchers)
+          if (!w->dead && now > w->deadline) expired.push_back(w);
+        for (Watcher* w : expired) finish_watch(w->conn);
+      }
+    }
+    if (now >= next_bm) {
+      next_bm = now + opt_.bookmark_interval_s;
+      for (auto& rs : res_) send_bookmarks(*rs);
+    }
+    std::vector<Conn*> d;
+    d.swap(dirty_);
+    for (Conn* c : d) flush(c);
+    for (auto it = conns_.begin(); it != conns_.end();) {
+      if (it->second->dead) it = conns_.erase(it);
+      else ++it;
+    }
+  }
+  for (auto& kv : conns_)
+    if (!kv.second->dead) ::close(kv.second->fd);
+  ::close(lfd_);
+  ::close(ep_);
+  return 0;
+}
+
+}  // namespace
+
+int run_fake_apiserver(const FakeApiOptions& opt) {
+  Server s(opt);
+  return s.run();
+}
+
+}  // namespace yk

@@ -1,0 +1,75 @@
+// Pod projection: everything the scheduling cycle reads from a v1.Pod, computed in C++
+// from the watch event's JSON so the Python control plane never decodes a pod on the hot
+// path. Mirrors yoda_scheduler_amd/models/pod.py::PodInfo.from_obj field for field; a pod
+// using something the projection does not cover (extended resources, quantities outside
+// the exact-decimal range) sets `ok=false` and Python falls back to json + from_obj.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "json.hpp"
+
+namespace yk {
+
+// pod feature flags (models/pod.py PF_*)
+enum : int {
+  PF_HOST_PORTS = 1,
+  PF_SPREAD = 2,
+  PF_POD_AFFINITY = 4,
+  PF_CLAIMS = 8,
+  PF_DISKS = 16,
+  PF_CONTROLLER = 32,
+  PF_EXTENDED = 64,
+  PF_POD_GROUP = 128,
+  PF_REQ_ANTI = 256,    // required pod anti-affinity (symmetry check of other pods)
+};
+
+using KV = std::pair<std::string, std::string>;
+
+struct SelReqP {
+  std::string key, op;
+  std::vector<std::string> values;
+};
+using TermP = std::vector<SelReqP>;
+
+struct TolP {
+  bool has_key = false;
+  std::string key, value, op, effect;
+};
+
+struct PortP {
+  int64_t host_port = 0;
+  std::string protocol, host_ip;
+};
+
+struct PodProj {
+  bool ok = false;                  // full projection available
+  std::string uid, ns, name, rv, sched, node, phase, creation;
+  bool deleting = false;            // metadata.deletionTimestamp set
+  std::vector<KV> labels;
+  bool has_annotations = false;
+  std::vector<KV> annotations;
+  int64_t cpu = 0, mem = 0, nzc = 0, nzm = 0, priority = 0;
+  bool has_node_selector = false;
+  std::vector<KV> node_selector;
+  bool has_affinity = false;        // spec.affinity truthy → terms lists (maybe empty)
+  std::vector<TermP> req_terms;
+  std::vector<std::pair<int64_t, TermP>> pref_terms;
+  std::vector<TolP> tolerations;
+  std::vector<PortP> ports;
+  int flags = 0;
+  uint64_t spec_meta_hash = 0;      // upstream isPodUpdated: spec + metadata minus volatile fields
+};
+
+// Quantity → ceil(q × 10^scale) with exact decimal arithmetic (scale 3: CPU millicores,
+// 0: bytes). False when the text is outside what the projection handles exactly.
+bool quantity_scaled(const Value& q, int scale, int64_t* out);
+
+// Fills `p` from a decoded pod object. Identity fields (uid/ns/name/rv/node/phase/sched,
+// hash) are always set; `p.ok` tells whether the rest is complete.
+void project_pod(const Value& pod, PodProj& p);
+
+}  // namespace yk

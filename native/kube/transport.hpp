@@ -1,0 +1,155 @@
+// Native Kubernetes API transport for the scheduler's hot path.
+//
+// One epoll I/O thread owns every socket: a pool of keep-alive connections carrying
+// pipelined requests (binding POSTs, event writes, any other verb) and one dedicated
+// connection per watch stream. Watch events are framed (chunked encoding → lines), parsed
+// and — for pods — projected (project.hpp) on the I/O thread, so the Python event loop
+// receives ready-to-use records in batches. Completions are handed over through a
+// mutex-protected queue plus an eventfd the asyncio loop watches (`add_reader`).
+//
+// Replaces, for the hot path, the two client-go stacks the reference process runs
+// (kube-scheduler's informers + binder and the controller-runtime cache;
+// reference pkg/yoda/scheduler.go:53-73). HTTPS via OpenSSL (in-cluster CA, client
+// certificates, insecure-skip-tls-verify), bearer token (rotatable), client-side QPS/burst
+// token bucket with the semantics of client-go's flowcontrol limiter.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "project.hpp"
+
+struct ssl_ctx_st;
+
+namespace yk {
+
+struct ClientConfig {
+  std::string host = "127.0.0.1";
+  int port = 80;
+  bool tls = false;
+  std::string prefix;          // path prefix of the server URL ("" normally)
+  std::string ca_file, cert_file, key_file;
+  bool insecure = false;
+  std::string token;
+  int conns = 8;               // pooled request connections
+  int max_inflight = 64;       // pipelined requests per connection
+  double qps = 0.0;            // <= 0: unlimited
+  int burst = 0;
+  std::string user_agent = "yoda-scheduler/0.2 (MI355X)";
+};
+
+struct PodEv {
+  PodProj p;
+  std::string raw;             // the pod object's JSON text
+};
+
+struct WatchEvent {
+  char type = 0;               // 'A' ADDED, 'M' MODIFIED, 'D' DELETED, 'B' BOOKMARK, 'E' ERROR
+  std::string rv;
+  std::string raw;             // object JSON (non-pod watches; ERROR status for pods too)
+  std::shared_ptr<PodEv> pod;  // pod watches
+};
+
+struct Completion {
+  enum Kind : uint8_t { kResponse = 0, kEvents = 1, kWatchEnd = 2 };
+  Kind kind = kResponse;
+  uint64_t id = 0;
+  int status = 0;              // HTTP status; -1 connection error, -2 timeout
+  std::string body;
+  std::vector<WatchEvent> events;
+};
+
+struct TransportStats {
+  uint64_t requests = 0, responses = 0, errors = 0, timeouts = 0, connects = 0;
+  uint64_t watch_events = 0, watch_bytes = 0, parse_errors = 0, bytes_out = 0, bytes_in = 0;
+  uint64_t throttled = 0;
+};
+
+class Transport {
+ public:
+  explicit Transport(ClientConfig cfg);
+  ~Transport();
+  Transport(const Transport&) = delete;
+  Transport& operator=(const Transport&) = delete;
+
+  int fd() const { return out_efd_; }
+  // Generic request. `limited`: goes through the QPS token bucket. timeout_s <= 0: none.
+  uint64_t request(const std::string& method, const std::string& path, const std::string& body,
+                   const std::string& content_type, bool limited, double timeout_s);
+  // POST pods/{name}/binding with the body formatted here (rate-limited).
+  uint64_t bind(const std::string& ns, const std::string& name, const std::string& uid, const std::string& node,
+                const std::vector<KV>& annotations, double timeout_s);
+  // Streaming GET (watch=1 in `path`); `pods` selects the pod projection.
+  uint64_t watch(const std::string& path, bool pods);
+  void cancel(uint64_t id);
+  std::vector<Completion> drain();
+  void set_token(const std::string& token);
+  // client QPS / burst (clientConnection); qps <= 0 disables limiting
+  void set_rate(double qps, int burst);
+  TransportStats stats();
+  void close();
+
+  struct Conn;
+  struct Req;
+
+ private:
+  void run();
+  void submit(std::unique_ptr<Req> r);
+  std::string head(const std::string& method, const std::string& path, size_t body_len,
+                   const std::string& content_type);
+  std::unique_ptr<Conn> open_conn(bool watch);
+  void close_conn(Conn* c, int status, const std::string& why);
+  void on_event(Conn* c, uint32_t ev);
+  void do_handshake(Conn* c);
+  void do_read(Conn* c);
+  void do_write(Conn* c);
+  void update_interest(Conn* c);
+  void on_body(Conn* c, const char* data, size_t n);
+  void on_message_done(Conn* c);
+  void watch_lines(Conn* c);
+  void dispatch();
+  void check_timeouts(double now);
+  void complete(Completion&& c);
+  void flush();
+
+  ClientConfig cfg_;
+  ssl_ctx_st* ssl_ctx_ = nullptr;
+  std::vector<uint8_t> addr_;              // resolved sockaddr
+  int family_ = 0;
+  int ep_ = -1, wake_efd_ = -1, out_efd_ = -1;
+  std::thread th_;
+  std::atomic<bool> stop_{false};
+  std::atomic<uint64_t> next_id_{1};
+
+  std::mutex in_mu_;
+  std::vector<std::unique_ptr<Req>> incoming_;
+  std::vector<uint64_t> cancels_;
+  std::string token_;
+
+  std::mutex out_mu_;
+  std::vector<Completion> out_;
+  std::vector<Completion> local_out_;      // I/O thread: batched before the handover
+
+  // I/O-thread state
+  std::deque<std::unique_ptr<Req>> throttled_, ready_;
+  std::vector<std::unique_ptr<Conn>> pool_;
+  std::unordered_map<uint64_t, std::unique_ptr<Conn>> watches_;
+  std::atomic<double> qps_{0.0};
+  std::atomic<int> burst_{0};
+  std::atomic<bool> refill_{false};
+  double tokens_ = 0.0, last_refill_ = 0.0;
+  double next_timeout_check_ = 0.0;
+
+  std::mutex stats_mu_;
+  TransportStats stats_;
+};
+
+}  // namespace yk

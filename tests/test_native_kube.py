@@ -1,0 +1,515 @@
+"""Native Kubernetes transport (native/kube): JSON codec, quantity + pod projection parity
+with the Python decoders, the C++ transport against both fake apiservers (Python aiohttp
+and the native epoll one), and reflector robustness (backoff, handler isolation, token
+rotation)."""
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import subprocess
+import tempfile
+import time
+
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from yoda_scheduler_amd.fakeapi.http import FakeApiHttp
+from yoda_scheduler_amd.fakeapi.server import FakeApiServer, _merge
+from yoda_scheduler_amd.kube import native as nat
+from yoda_scheduler_amd.kube.client import KubeClient, KubeConfig
+from yoda_scheduler_amd.kube.errors import ApiError
+from yoda_scheduler_amd.models.device import make_node, make_scv
+from yoda_scheduler_amd.models.pod import PodInfo
+from yoda_scheduler_amd.utils.quantity import bytes_of, cpu_millis
+
+K = nat.module()
+
+
+def run(coro):
+    return asyncio.run(coro)
+
+
+# ============================================================== codec
+def test_json_codec_roundtrip_escapes_unicode_numbers():
+    doc = {"s": "a\"b\\c\n\t\u0001é漢🚀", "n": [0, -1, 12345678901234567890, 1.5e-7, 3.25],
+           "o": {"x": None, "t": True, "f": False, "e": {}, "a": []}}
+    raw = json.dumps(doc)
+    assert json.loads(K.canonical(raw)) == doc
+    # surrogate-pair escapes decode to one code point; numbers keep their source text
+    assert json.loads(K.canonical('{"k":"\\ud83d\\ude80","big":12345678901234567890}')) == \
+        {"k": "🚀", "big": 12345678901234567890}
+    assert K.canonical('{"v": 1.50}') == b'{"v":1.50}'
+    for bad in ('{"a":}', '[1,2', '{"a" 1}', '"\x01"', 'nul', '{"a":1}x'):
+        with pytest.raises(ValueError):
+            K.canonical(bad)
+
+
+_json_leaf = st.one_of(st.none(), st.booleans(), st.integers(-10**6, 10**6), st.text(max_size=6))
+_json = st.recursive(_json_leaf, lambda ch: st.one_of(st.lists(ch, max_size=3),
+                                                      st.dictionaries(st.text(max_size=4), ch, max_size=4)),
+                     max_leaves=12)
+
+
+@settings(max_examples=150, deadline=None)
+@given(_json, _json)
+def test_merge_patch_matches_python(target, patch):
+    if not isinstance(target, dict):
+        target = {"v": target}
+    got = json.loads(K.merge_patch(json.dumps(target), json.dumps(patch)))
+    assert got == _merge(target, patch)
+
+
+# ============================================================== quantities
+_qty = st.builds(lambda num, frac, suf: f"{num}{'.' + frac if frac else ''}{suf}",
+                 st.integers(0, 10**7), st.one_of(st.just(""), st.from_regex(r"[0-9]{1,4}", fullmatch=True)),
+                 st.sampled_from(["", "m", "k", "M", "G", "Ki", "Mi", "Gi", "Ti", "n", "u", "e3", "E2"]))
+
+
+@settings(max_examples=300, deadline=None)
+@given(_qty)
+def test_quantity_matches_python_decimal(q):
+    # exact where the value fits int64; beyond that the projection defers to Python (None)
+    for got, want in ((K.quantity(q, 3), cpu_millis(q)), (K.quantity(q, 0), bytes_of(q))):
+        if abs(want) < 2**63:
+            assert got == want
+        else:
+            assert got is None
+
+
+def test_quantity_rejects_what_python_decides():
+    for q in ("1.2.3", "abc", "5x", "--1"):
+        assert K.quantity(q, 0) is None
+
+
+# ============================================================== pod projection
+_labels = st.dictionaries(st.sampled_from(["scv/number", "scv/memory", "scv/clock", "scv/priority", "app",
+                                           "pod-group.scheduling.sigs.k8s.io"]),
+                          st.sampled_from(["1", "2", "512", "x", "-3", "2400"]), max_size=4)
+_expr = st.fixed_dictionaries({"key": st.sampled_from(["zone", "gpu", "kubernetes.io/hostname"]),
+                               "operator": st.sampled_from(["In", "NotIn", "Exists", "Gt"]),
+                               "values": st.lists(st.sampled_from(["a", "b", "3"]), max_size=2)})
+_term = st.fixed_dictionaries({}, optional={
+    "matchExpressions": st.lists(_expr, max_size=2),
+    "matchFields": st.lists(st.fixed_dictionaries({"key": st.sampled_from(["metadata.name", "spec.x"]),
+                                                    "operator": st.just("In"),
+                                                    "values": st.lists(st.just("n1"), max_size=1)}), max_size=1)})
+_container = st.fixed_dictionaries({"name": st.just("c")}, optional={
+    "resources": st.fixed_dictionaries({}, optional={"requests": st.fixed_dictionaries({}, optional={
+        "cpu": st.sampled_from(["100m", "1", "0.5", "2500m", 2]),
+        "memory": st.sampled_from(["128Mi", "1Gi", "1e3", "512", "1.5Gi"])})}),
+    "ports": st.lists(st.fixed_dictionaries({"containerPort": st.just(80)}, optional={
+        "hostPort": st.sampled_from([0, 8080]), "protocol": st.sampled_from(["TCP", "UDP"]),
+        "hostIP": st.just("0.0.0.0")}), max_size=2)})
+_spec = st.fixed_dictionaries({"containers": st.lists(_container, min_size=1, max_size=3)}, optional={
+    "schedulerName": st.sampled_from(["yoda-scheduler", "default-scheduler"]),
+    "nodeName": st.sampled_from(["", "n1"]),
+    "priority": st.sampled_from([0, 5, -2, 1000000000]),
+    "nodeSelector": st.dictionaries(st.sampled_from(["zone", "gpu"]), st.sampled_from(["a", "b"]), max_size=2),
+    "initContainers": st.lists(_container, max_size=2),
+    "overhead": st.fixed_dictionaries({}, optional={"cpu": st.just("50m"), "memory": st.just("64Mi")}),
+    "tolerations": st.lists(st.fixed_dictionaries({}, optional={
+        "key": st.sampled_from(["", "gpu", "node.kubernetes.io/not-ready"]),
+        "operator": st.sampled_from(["Exists", "Equal", ""]), "value": st.sampled_from(["", "x"]),
+        "effect": st.sampled_from(["", "NoSchedule", "NoExecute"]),
+        "tolerationSeconds": st.just(300)}), max_size=3),
+    "affinity": st.fixed_dictionaries({}, optional={
+        "nodeAffinity": st.fixed_dictionaries({}, optional={
+            "requiredDuringSchedulingIgnoredDuringExecution": st.fixed_dictionaries(
+                {"nodeSelectorTerms": st.lists(_term, max_size=2)}),
+            "preferredDuringSchedulingIgnoredDuringExecution": st.lists(st.fixed_dictionaries(
+                {"weight": st.integers(1, 100), "preference": _term}), max_size=2)}),
+        "podAntiAffinity": st.fixed_dictionaries({}, optional={
+            "requiredDuringSchedulingIgnoredDuringExecution": st.lists(st.just({"topologyKey": "zone"}),
+                                                                       max_size=1)}),
+        "podAffinity": st.fixed_dictionaries({}, optional={
+            "preferredDuringSchedulingIgnoredDuringExecution": st.lists(st.just({"weight": 1}), max_size=1)})}),
+    "topologySpreadConstraints": st.lists(st.just({"maxSkew": 1, "topologyKey": "zone"}), max_size=1),
+    "volumes": st.lists(st.sampled_from([{"name": "v", "persistentVolumeClaim": {"claimName": "c"}},
+                                         {"name": "e", "emptyDir": {}}, {"name": "d", "rbd": {}},
+                                         {"name": "g", "ephemeral": {}}]), max_size=2)})
+_pod = st.fixed_dictionaries({
+    "metadata": st.fixed_dictionaries({"name": st.sampled_from(["p1", "p2"])}, optional={
+        "namespace": st.sampled_from(["default", "ml"]), "uid": st.sampled_from(["u1", "u2"]),
+        "labels": _labels, "annotations": st.dictionaries(st.sampled_from(["a", "scv.amd.com/gpus"]),
+                                                          st.sampled_from(["0,1", "x"]), max_size=2),
+        "creationTimestamp": st.just("2026-01-01T00:00:00Z"),
+        "ownerReferences": st.lists(st.fixed_dictionaries({"kind": st.sampled_from(["ReplicaSet", "Job"]),
+                                                           "name": st.just("o")},
+                                                          optional={"controller": st.booleans()}), max_size=2)}),
+    "spec": _spec})
+
+_FIELDS = ("uid", "namespace", "name", "labels", "gpu", "scheduler_name", "node_name", "cpu_m", "mem", "priority",
+           "node_selector", "required_terms", "preferred_terms", "tolerations", "annotations", "host_ports", "flags",
+           "ext", "nz_cpu_m", "nz_mem")
+
+
+def _norm(v):
+    if isinstance(v, list):
+        return [_norm(x) for x in v]
+    if isinstance(v, tuple):
+        return tuple(_norm(x) for x in v)
+    return v
+
+
+@settings(max_examples=250, deadline=None)
+@given(_pod)
+def test_pod_projection_matches_from_obj(pod):
+    raw = json.dumps(pod)
+    ev = K.project(raw)
+    want = PodInfo.from_obj(json.loads(raw))
+    got = PodInfo.from_native(ev)
+    for f in _FIELDS:
+        assert _norm(getattr(got, f)) == _norm(getattr(want, f)), f
+    assert ev.ok, "the generated pods are all within the projection's coverage"
+    # lazy object decodes to the same pod
+    assert got.obj == json.loads(raw)
+    key, uid, node, sched, phase, h = ev.ident()
+    assert (key, uid, node, sched) == (want.key, want.uid, want.node_name, want.scheduler_name)
+
+
+def test_projection_hash_ignores_volatile_metadata_and_status():
+    base = {"metadata": {"name": "p", "resourceVersion": "1", "labels": {"a": "b"}},
+            "spec": {"containers": [{"name": "c"}]}, "status": {"phase": "Pending"}}
+    h0 = K.project(json.dumps(base)).hash
+    moved = json.loads(json.dumps(base))
+    moved["metadata"]["resourceVersion"] = "9"
+    moved["metadata"]["managedFields"] = [{"x": 1}]
+    moved["status"] = {"phase": "Pending", "conditions": [{"type": "PodScheduled", "status": "False"}]}
+    assert K.project(json.dumps(moved)).hash == h0
+    relabel = json.loads(json.dumps(base))
+    relabel["metadata"]["labels"] = {"a": "c"}
+    assert K.project(json.dumps(relabel)).hash != h0
+
+
+def test_projection_falls_back_for_extended_resources():
+    pod = {"metadata": {"name": "p"}, "spec": {"containers": [{"name": "c", "resources": {"requests": {
+        "amd.com/gpu": "2", "cpu": "1"}}}]}}
+    ev = K.project(json.dumps(pod))
+    assert not ev.ok and ev.info_args() is None
+    pi = PodInfo.from_native(ev)
+    assert pi.ext == {"amd.com/gpu": 2} and pi.cpu_m == 1000
+
+
+# ============================================================== native fake apiserver
+class NativeApi:
+    def __init__(self, token: str = "") -> None:
+        from yoda_scheduler_amd.bench.harness import native_apiserver_binary
+        d = tempfile.mkdtemp(prefix="yoda-nfa-")
+        pf = os.path.join(d, "port")
+        cmd = [native_apiserver_binary(), "--port", "0", "--port-file", pf, "--history", "50"]
+        if token:
+            cmd += ["--token", token]
+        self.proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL)
+        t = time.time()
+        while not os.path.exists(pf):
+            assert time.time() - t < 10 and self.proc.poll() is None
+            time.sleep(0.01)
+        with open(pf) as f:
+            self.url = f"http://127.0.0.1:{int(f.read())}"
+
+    def stop(self) -> None:
+        self.proc.terminate()
+        self.proc.wait(10)
+
+
+@pytest.fixture
+def native_api():
+    a = NativeApi()
+    yield a
+    a.stop()
+
+
+def test_native_apiserver_crud_watch_bind_and_selectors(native_api):
+    async def go():
+        cl = KubeClient(KubeConfig(native_api.url), native=True)
+        try:
+            await cl.create("nodes", make_node("n1"))
+            with pytest.raises(ApiError) as ei:
+                await cl.create("nodes", make_node("n1"))
+            assert ei.value.code == 409
+            _, rv = await cl.list("nodes")
+            got = []
+
+            async def watcher():
+                async for typ, obj in cl.watch("pods", rv, field_selector="spec.nodeName="):
+                    got.append((typ, obj["metadata"]["name"]))
+                    if len(got) == 2:
+                        return
+            t = asyncio.get_event_loop().create_task(watcher())
+            await asyncio.sleep(0.05)
+            p = await cl.create("pods", {"metadata": {"name": "p"}, "spec": {"schedulerName": "x"}})
+            assert p["metadata"]["namespace"] == "default" and p["metadata"]["uid"]
+            with pytest.raises(ApiError) as ei:
+                await cl.bind("default", "p", "wrong-uid", "n1")
+            assert ei.value.code == 409
+            await cl.bind("default", "p", p["metadata"]["uid"], "n1", {"scv.amd.com/gpus": "0"})
+            await asyncio.wait_for(t, 5)
+            # leaving the selector (bound) reaches a field-selected watch as DELETED
+            assert got == [("ADDED", "p"), ("DELETED", "p")]
+            pod = await cl.get("pods", "p", "default")
+            assert pod["spec"]["nodeName"] == "n1" and pod["metadata"]["annotations"] == {"scv.amd.com/gpus": "0"}
+            assert [c["type"] for c in pod["status"]["conditions"]] == ["PodScheduled"]
+            with pytest.raises(ApiError) as ei:
+                await cl.bind("default", "p", p["metadata"]["uid"], "n1")
+            assert ei.value.code == 409
+            stale = dict(pod, metadata=dict(pod["metadata"], resourceVersion="1"))
+            with pytest.raises(ApiError) as ei:
+                await cl.update("pods", stale, "default")
+            assert ei.value.code == 409
+            upd = await cl.update_status("pods", dict(pod, status={"phase": "Running"}), "default")
+            assert upd["status"] == {"phase": "Running"} and upd["spec"]["nodeName"] == "n1"
+            pt = await cl.patch("pods", "p", {"metadata": {"labels": {"a": "b"}, "uid": "hijack"}}, "default")
+            assert pt["metadata"]["labels"] == {"a": "b"} and pt["metadata"]["uid"] == p["metadata"]["uid"]
+            sel, _ = await cl.list("pods", field_selector="status.phase!=Running")
+            assert sel == []
+            await cl.delete("pods", "p", "default")
+            with pytest.raises(ApiError) as ei:
+                await cl.get("pods", "p", "default")
+            assert ei.value.code == 404
+            scv = await cl.create("scvs", make_scv("n1").to_json())
+            assert scv["kind"] == "Scv" and scv["apiVersion"] == "core.run-linux.com/v1"
+        finally:
+            await cl.close()
+    run(go())
+
+
+def test_native_apiserver_paging_history_410_and_bookmarks(native_api):
+    async def go():
+        cl = KubeClient(KubeConfig(native_api.url), native=True)
+        try:
+            for i in range(7):
+                await cl.create("nodes", make_node(f"n{i}"))
+            pages = []
+            async for items, rv in cl.list_pages("nodes", resource_version="", limit=3):
+                pages.append([i["metadata"]["name"] for i in items])
+            assert [len(p) for p in pages] == [3, 3, 1] and sum(pages, []) == sorted(f"n{i}" for i in range(7))
+            for i in range(60):                         # history is 50 events: RV 1 is compacted
+                await cl.patch("nodes", "n0", {"metadata": {"labels": {"i": str(i)}}})
+            with pytest.raises(ApiError) as ei:
+                async for _ in cl.watch("nodes", "1"):
+                    pass
+            assert ei.value.code == 410
+            # bookmarks advance the RV without an object
+            _, rv = await cl.list("nodes")
+            seen = []
+
+            async def watcher():
+                async for typ, obj in cl.watch("nodes", rv):
+                    seen.append((typ, obj["metadata"]["resourceVersion"]))
+                    return
+            t = asyncio.get_event_loop().create_task(watcher())
+            await asyncio.sleep(0.05)
+            st, _ = await cl.native.request("GET", "/debug/bookmark?resource=nodes")
+            assert st == 200
+            await asyncio.wait_for(t, 5)
+            assert seen == [("BOOKMARK", rv)]
+        finally:
+            await cl.close()
+    run(go())
+
+
+def test_native_apiserver_token_auth_and_client_rotation(tmp_path):
+    api = NativeApi(token="tok-2")
+    tf = tmp_path / "token"
+    tf.write_text("tok-1")
+
+    async def go():
+        cfg = KubeConfig(api.url, token="tok-1", token_file=str(tf))
+        cl = KubeClient(cfg, native=True)
+        try:
+            # the file still holds the old token: 401 → re-read → still 401 → error
+            with pytest.raises(ApiError) as ei:
+                await cl.list("nodes")
+            assert ei.value.code == 401
+            tf.write_text("tok-2")                         # the kubelet rotated the projected token
+            items, _ = await cl.list("nodes")              # 401 → forced re-read → retry succeeds
+            assert items == [] and cl.retried_401 >= 2
+            await cl.create("nodes", make_node("n1"))
+        finally:
+            await cl.close()
+    try:
+        run(go())
+    finally:
+        api.stop()
+
+
+# ============================================================== transport
+def test_transport_rate_limit_timeouts_and_refused_connection():
+    async def go():
+        srv = FakeApiServer()
+        srv.faults.latency_s = 0.0
+        api = FakeApiHttp(srv)
+        url = await api.start()
+        cl = KubeClient(KubeConfig(url), native=True)
+        try:
+            await cl.create("nodes", make_node("n1"))
+            cl.set_rate(20.0, 1)                           # 20 QPS, burst 1
+            t0 = time.perf_counter()
+            res = await asyncio.gather(*(cl.native.request("GET", "/api/v1/nodes", limited=True) for _ in range(6)))
+            dt = time.perf_counter() - t0
+            assert all(s == 200 for s, _ in res)
+            assert dt >= 0.2, dt                           # 5 waits of 50 ms
+            cl.set_rate(0, 0)
+            st = cl.native.stats()
+            assert st["throttled"] >= 5 and st["errors"] == 0
+        finally:
+            await cl.close()
+            await api.stop()
+        # nothing listens: the request fails with a connection error, not a hang
+        dead = KubeClient(KubeConfig(url), native=True, timeout=2.0)
+        try:
+            with pytest.raises((ConnectionError, asyncio.TimeoutError)):
+                await dead.get("nodes", "n1")
+        finally:
+            await dead.close()
+    run(go())
+
+
+def test_transport_request_timeout_against_silent_server():
+    """A server that accepts and never answers: the request fails with a timeout (-2 →
+    asyncio.TimeoutError) after its deadline instead of hanging the caller."""
+    import socket
+
+    async def go():
+        ls = socket.socket()
+        ls.bind(("127.0.0.1", 0))
+        ls.listen(8)
+        port = ls.getsockname()[1]
+        t = nat.NativeTransport(KubeConfig(f"http://127.0.0.1:{port}"), conns=1)
+        try:
+            t0 = time.perf_counter()
+            st, body = await t.request("GET", "/api/v1/nodes", timeout=0.2)
+            dt = time.perf_counter() - t0
+            assert st == -2 and b"timed out" in body and 0.15 <= dt < 2.0
+            assert isinstance(nat.api_error(st, body), asyncio.TimeoutError)
+            assert t.stats()["timeouts"] == 1
+        finally:
+            t.close()
+            ls.close()
+    run(go())
+
+
+# ============================================================== reflector robustness
+def test_informer_handler_exception_is_isolated_no_relist():
+    from yoda_scheduler_amd.fakeapi.client import InProcessClient
+    from yoda_scheduler_amd.kube.informer import Informer
+
+    async def go():
+        srv = FakeApiServer()
+        seen = []
+
+        def on_add(o):
+            seen.append(o["metadata"]["name"])
+            if o["metadata"]["name"] == "bad":
+                raise RuntimeError("handler bug")
+        inf = Informer(InProcessClient(srv), "nodes", on_add=on_add)
+        task = asyncio.get_event_loop().create_task(inf.run())
+        await asyncio.wait_for(inf.synced.wait(), 5)
+        lists0 = srv.calls["list"]
+        for n in ("a", "bad", "c"):
+            srv.create("nodes", make_node(n))
+        for _ in range(200):
+            if len(seen) == 3:
+                break
+            await asyncio.sleep(0.005)
+        await asyncio.sleep(0.05)
+        inf.stop()
+        srv.close_watches()
+        task.cancel()
+        await asyncio.gather(task, return_exceptions=True)
+        return seen, inf.handler_errors, srv.calls["list"] - lists0, sorted(inf.store)
+    seen, errs, relists, store = run(go())
+    assert seen == ["a", "bad", "c"] and errs == 1
+    assert relists == 0 and store == ["a", "bad", "c"]
+
+
+def test_informer_backoff_bounds_requests_while_apiserver_down():
+    from yoda_scheduler_amd.kube.informer import Backoff, Informer
+
+    class Down:
+        def __init__(self):
+            self.calls = 0
+
+        async def list(self, *a, **k):
+            self.calls += 1
+            raise ConnectionError("connection refused")
+
+    async def go():
+        c = Down()
+        inf = Informer(c, "nodes", relist_backoff=0.01, max_backoff=0.08)
+        task = asyncio.get_event_loop().create_task(inf.run())
+        await asyncio.sleep(0.6)
+        inf.stop()
+        task.cancel()
+        await asyncio.gather(task, return_exceptions=True)
+        return c.calls
+    calls = run(go())
+    # 0.01, 0.02, 0.04, 0.08, 0.08, ... each stretched by up to 2× jitter: ≤ 12 in 0.6 s
+    # (a fixed 0.01 s retry would be ~60)
+    assert 3 <= calls <= 12, calls
+    b = Backoff(1.0, 8.0, jitter=0.0, reset_after=1e9)
+    assert [b.next() for _ in range(5)] == [1.0, 2.0, 4.0, 8.0, 8.0]
+    b.reset()
+    assert b.next() == 1.0
+
+
+# ============================================================== scheduler over the native stack
+@pytest.mark.parametrize("server", ["native", "python"])
+def test_scheduler_binds_over_native_transport(server):
+    from yoda_scheduler_amd.framework.config import parse_config
+    from yoda_scheduler_amd.framework.scheduler import Scheduler
+    from yoda_scheduler_amd.kube.informer import NativePodInformer
+    from yoda_scheduler_amd.testing import yoda_config
+
+    async def go():
+        api = NativeApi() if server == "native" else None
+        papi = None
+        if api is None:
+            papi = FakeApiHttp(FakeApiServer())
+            url = await papi.start()
+        else:
+            url = api.url
+        cl = KubeClient(KubeConfig(url), native=True)
+        try:
+            await cl.create("nodes", make_node("n1"))
+            s = make_scv("n1", update_time=time.time())
+            s.update_interval_ms = 600_000
+            await cl.create("scvs", s.to_json())
+            sched = Scheduler(cl, parse_config(yoda_config()))
+            assert isinstance(sched.make_informers()["pods"], NativePodInformer)
+            await sched.start()
+            loop_t = asyncio.get_event_loop().create_task(sched.scheduling_loop())
+            for i in range(30):
+                await cl.create("pods", {"metadata": {"name": f"p{i}", "labels": {"scv/memory": "1000",
+                                                                                   "scv/number": str(1 + i % 2)}},
+                                         "spec": {"schedulerName": "yoda-scheduler",
+                                                  "tolerations": [{"key": "node.kubernetes.io/not-ready",
+                                                                   "operator": "Exists", "effect": "NoExecute"}]}})
+            t0 = time.time()
+            while sched.scheduled < 30 and time.time() - t0 < 10:
+                await asyncio.sleep(0.01)
+            items, _ = await cl.list("pods")
+            cards = {i["metadata"]["name"]: i["metadata"].get("annotations", {}).get("scv.amd.com/gpus")
+                     for i in items}
+            # the bind echo confirmed every assumed pod; the lazy store decodes on demand
+            await asyncio.sleep(0.1)
+            assumed = [p for p in sched.cache.pods.values() if p.assumed]
+            stored = sched.informers["pods"].store.get("default/p3")
+            await cl.delete("pods", "p3", "default")
+            await asyncio.sleep(0.1)
+            gone = "default/p3" in sched.informers["pods"].store
+            await sched.shutdown()
+            loop_t.cancel()
+            return sched.scheduled, cards, assumed, stored, gone
+        finally:
+            await cl.close()
+            if api:
+                api.stop()
+            if papi:
+                await papi.stop()
+    n, cards, assumed, stored, gone = run(go())
+    assert n == 30 and all(cards.values()) and not assumed and not gone
+    assert len(cards["p1"].split(",")) == 2 and len(cards["p0"].split(",")) == 1
+    assert stored["spec"]["nodeName"] == "n1"

@@ -130,31 +130,64 @@ async def run_bursts(w: Workload, steps: int, warmup: int, **kw) -> tuple[list[B
     return res, total
 
 
+class _Recorder:
+    """Collects ``create`` calls of :func:`populate` so they can be replayed over HTTP."""
+
+    def __init__(self) -> None:
+        self.objs: list[tuple[str, dict]] = []
+
+    def create(self, res: str, obj: dict, namespace=None) -> dict:
+        self.objs.append((res, obj))
+        return obj
+
+
+def native_apiserver_binary() -> str:
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return os.path.join(root, "_native", "yoda-fake-apiserver-native")
+
+
 class HttpShard:
-    """The same burst over real HTTP/JSON: the fake apiserver runs in its own process
-    (``yoda-fake-apiserver --bench-config N``), the scheduler talks to it through the
-    production client (:class:`~yoda_scheduler_amd.kube.client.KubeClient`: list/watch
-    streams, binding POSTs), and the apiserver creates the pods and measures latency on
-    its own clock. Between bursts the apiserver deletes the previous burst's pods, which
-    releases their reservations through the scheduler's informer."""
+    """The same burst over real HTTP/JSON: the fake apiserver runs in its own process and
+    the scheduler talks to it through the production client
+    (:class:`~yoda_scheduler_amd.kube.client.KubeClient`: list/watch streams, binding
+    POSTs — on the native C++ transport when it is built). The apiserver creates the pods
+    and measures latency on its own clock. Between bursts it deletes the previous burst's
+    pods, which releases their reservations through the scheduler's informer.
+
+    ``apiserver="native"`` (default) is the C++ epoll fake apiserver
+    (``native/kube/fakeapi.cpp``): pre-encoded watch frames, ~µs per request, so the
+    measurement is the scheduler's. ``"python"`` is the aiohttp fake apiserver
+    (``yoda-fake-apiserver``), the semantic reference, whose own CPU caps the burst."""
 
     def __init__(self, w: Workload, qps: float = 5000.0, burst: int = 10000, batch: int = 256,
                  template: Optional[dict] = None, events: bool = True, compat: bool = False, seed: int = 0,
-                 device: str = "auto", overlap: str = "auto") -> None:
+                 device: str = "auto", overlap: str = "auto", apiserver: str = "native",
+                 client_native: str | bool = "auto") -> None:
         import json
+        import os
         import subprocess
         import sys
         import tempfile
         self.w = w
+        self.apiserver = apiserver
+        self.client_native = client_native
         self._dir = tempfile.mkdtemp(prefix="yoda-bench-")
         self.port_file = f"{self._dir}/port"
-        cmd = [sys.executable, "-m", "yoda_scheduler_amd.cmd.fakeapi", "--port", "0", "--bench-config", str(w.id),
-               "--seed", str(seed), "--port-file", self.port_file]
-        if template:
-            cmd += ["--template", json.dumps(template)]
-        import os
-        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        env = dict(os.environ, PYTHONPATH=os.pathsep.join(p for p in (root, os.environ.get("PYTHONPATH")) if p))
+        self.template = template
+        if apiserver == "native":
+            exe = native_apiserver_binary()
+            if not os.path.exists(exe):
+                raise RuntimeError(f"{exe} is not built (python -m yoda_scheduler_amd.ops.build)")
+            cmd = [exe, "--port", "0", "--port-file", self.port_file]
+            env = None
+        else:
+            cmd = [sys.executable, "-m", "yoda_scheduler_amd.cmd.fakeapi", "--port", "0", "--bench-config",
+                   str(w.id), "--seed", str(seed), "--port-file", self.port_file]
+            if template:
+                cmd += ["--template", json.dumps(template)]
+            root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+            env = dict(os.environ, PYTHONPATH=os.pathsep.join(p for p in (root, os.environ.get("PYTHONPATH")) if p))
         self.proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env)
         self.cfg = parse_config(bench_config(w.scheduler_name, qps, burst, batch, compat, device, overlap))
         self.events, self.seed = events, seed
@@ -181,8 +214,16 @@ class HttpShard:
         from ..kube.client import KubeClient, KubeConfig
         port = await self._port()
         self.base = f"http://127.0.0.1:{port}"
-        self.client = KubeClient(KubeConfig(self.base))
+        self.client = KubeClient(KubeConfig(self.base), native=self.client_native)
         self._http = aiohttp.ClientSession()
+        if self.apiserver == "native":
+            # the cluster (nodes + Scv telemetry) and the burst's pod templates, over HTTP
+            rec = _Recorder()
+            populate(rec, self.w, self.template, link_load=0.2 if self.w.id == 5 else 0.0, seed=self.seed)
+            for res, obj in rec.objs:
+                await self.client.create(res, obj)
+            pods = [pod_object(i, lab, self.w.scheduler_name, prefix="t") for i, lab in enumerate(self.w.pods)]
+            await self._call("POST", "/debug/bench/load", {"pods": pods})
         self.sched = Scheduler(self.client, self.cfg, metrics=NullMetrics(), record_events=self.events,
                                seed=self.seed)
         self.sched.e2e_samples = []
@@ -195,27 +236,34 @@ class HttpShard:
             return await r.json()
 
     async def burst(self, tag: str = "b", timeout: float = 600.0) -> BurstResult:
+        sched = self.sched
+        q = sched.queue
         if self._bursts:
             await self._call("POST", "/debug/bench/reset")
-            q = self.sched.queue
-            while self.sched.cache.pods or q._active_entries or self.sched.pending_binds:
+            while sched.cache.pods or q._active_entries or sched.pending_binds:
                 await asyncio.sleep(0.001)      # the deletes reached the scheduler
         self._bursts += 1
-        self.sched.e2e_samples.clear()
+        sched.e2e_samples.clear()
+        # every step is an independent burst: the client's token bucket starts full, as
+        # in the in-process harness where each step is a fresh scheduler
+        cc = self.cfg.client_connection
+        self.client.set_rate(cc.qps, cc.burst)
+        done0, fail0 = sched.scheduled, sched.failed
         n = (await self._call("POST", "/debug/bench/burst", {"tag": tag}))["n"]
-        q = self.sched.queue
         deadline = time.monotonic() + timeout
+        # completion is observed locally (every bind acknowledged, or every pod parked):
+        # no polling requests charged to the scheduler process during the burst
         while time.monotonic() < deadline:
-            st = await self._call("GET", "/debug/bench/status")
-            if st["bound"] >= n:
+            bound = sched.scheduled - done0
+            if bound >= n:
                 break
-            if not q._active_entries and self.sched.pending_binds == 0 and \
-                    st["bound"] + len(q._unsched) + len(q._backoff_pods) >= n:
+            if not q._active_entries and sched.pending_binds == 0 and sched.failed > fail0 and \
+                    bound + len(q._unsched) + len(q._backoff_pods) >= n:
                 break
-            await asyncio.sleep(0.002)
+            await asyncio.sleep(0.0005)
         st = await self._call("GET", "/debug/bench/status?full=1")
         return BurstResult(n, st["bound"], n - st["bound"], st["elapsed"], st["latencies"],
-                           list(self.sched.e2e_samples))
+                           list(sched.e2e_samples))
 
     async def stop(self) -> None:
         import shutil

@@ -20,7 +20,7 @@ from dataclasses import dataclass
 from typing import Callable, Optional
 
 from ..models.labels import ANNOTATION_GPUS
-from ..models.pod import NodeInfo, PodInfo
+from ..models.pod import PF_REQ_ANTI, NodeInfo, PodInfo
 from ..models.scv import Scv
 from ..ops.native import pod_req, push_node, push_scv
 
@@ -145,8 +145,7 @@ class SchedulerCache:
             self._ext(ps, +1)
         self.pods[ps.info.uid] = ps
         self.node_pods.setdefault(ps.node, set()).add(ps.info.uid)
-        aff = ((ps.info.obj.get("spec") or {}).get("affinity") or {}).get("podAntiAffinity") or {}
-        if aff.get("requiredDuringSchedulingIgnoredDuringExecution"):
+        if ps.info.flags & PF_REQ_ANTI:
             self._anti.add(ps.info.uid)
         else:
             self._anti.discard(ps.info.uid)
@@ -208,7 +207,27 @@ class SchedulerCache:
             ps.assumed, ps.deadline = False, None      # fast confirm: no re-parse
             ps.info.obj = obj
             return
-        pi = PodInfo.from_obj(obj)
+        self._add_bound(PodInfo.from_obj(obj))
+
+    def add_pod_native(self, ev, uid: str, node: str) -> None:
+        """``add_pod`` for a native transport ``PodEvent`` (decoded only when not a confirm)."""
+        ps = self.pods.get(uid)
+        if ps is not None and ps.assumed and ps.node == node:
+            ps.assumed, ps.deadline = False, None
+            ps.info.set_source(ev)
+            return
+        self._add_bound(PodInfo.from_native(ev))
+
+    def update_pod_native(self, ev, uid: str, node: str, same_spec: bool = False) -> None:
+        ps = self.pods.get(uid)
+        if ps is None or ps.node != node:
+            self.add_pod_native(ev, uid, node)
+        elif same_spec:
+            ps.info.set_source(ev)         # status-only update (kubelet): nothing to re-parse
+        else:
+            ps.info = PodInfo.from_native(ev)
+
+    def _add_bound(self, pi: PodInfo) -> None:
         node = pi.node_name
         ps = self.pods.get(pi.uid)
         if ps is not None:

@@ -115,6 +115,13 @@ class Framework:
 
     @staticmethod
     def _applies(p, pod) -> bool:
+        # one flag test for plugins that declare the pod features they act on (unless a
+        # cluster-wide gate makes them relevant to every pod)
+        pf = getattr(p, "pod_flags", None)
+        if pf is not None and not (pod.flags & pf):
+            gate = getattr(p, "cluster_active", None)
+            if gate is None or not gate():
+                return False
         f = getattr(p, "is_noop_for", None)
         return f is None or not f(pod)
 
@@ -261,6 +268,15 @@ class Framework:
             return await wp.wait()
         finally:
             self.waiting.pop(pod.uid, None)
+
+    def direct_binder_for(self, pod):
+        """``direct_binder`` for one pod: PreBind plugins that are no-ops for it do not count."""
+        if len(self.bind_plugins) != 1:
+            return None
+        for p in self.pre_bind:
+            if self._applies(p, pod):
+                return None
+        return self.bind_plugins[0]
 
     def direct_binder(self):
         """The single bind plugin when nothing runs around it (no PreBind plugins): the

@@ -15,12 +15,13 @@ from __future__ import annotations
 
 import asyncio
 import collections
+import functools
 import gc
 import logging
 import time
 from typing import Callable, Optional
 
-from ..kube.informer import Informer
+from ..kube.informer import Informer, NativePodInformer
 from ..models.pod import PodInfo, forget_num_id
 from ..ops.native import core, pod_req
 from ..utils import gctune, klog
@@ -105,7 +106,15 @@ class Scheduler:
         self.registry = registry or default_registry()
         self.metrics = metrics if metrics is not None else SchedulerMetrics()
         cc = config.client_connection
-        self.limiter = bind_limiter or TokenBucket(cc.qps, cc.burst)
+        # native transport: its C++ token bucket enforces clientConnection QPS/burst for
+        # binds, status patches and deletes (one bucket, as client-go's limiter)
+        self.native = getattr(client, "native", None) if bind_limiter is None else None
+        if self.native is not None:
+            client.set_rate(cc.qps, cc.burst)
+            self.limiter = TokenBucket(0, 1)
+        else:
+            self.limiter = bind_limiter or TokenBucket(cc.qps, cc.burst)
+        self.bind_timeout = float(getattr(client, "timeout", 30.0) or 30.0)
         self.recorder = EventRecorder(client, enabled=record_events, api=config.events_api)
         self.handle = Handle(self)
         # the engine must exist before plugins are created (they may query it)
@@ -242,6 +251,55 @@ class Scheduler:
             self.queue.delete(uid)
         forget_num_id(uid)
 
+    def on_pod_native(self, typ: str, ev, idt: tuple, old: Optional[tuple]) -> None:
+        """Pod events from :class:`NativePodInformer` (C++-decoded ``PodEvent`` + its
+        ident tuple): the same transitions as ``on_pod_add/update/delete`` without a dict."""
+        _key, uid, node, sched, phase, h = idt
+        terminal = phase == "Succeeded" or phase == "Failed"
+        if typ == "DELETED":
+            if uid in self.nominations:
+                self._clear_nomination(uid)
+            if node or self.cache.is_assumed(uid):
+                self.cache.remove_pod(uid)
+                self.queue.move_all_to_active_or_backoff("AssignedPodDelete")
+            else:
+                self.queue.delete(uid)
+            forget_num_id(uid)
+            return
+        if old is None:
+            if node:
+                if self.nominations:
+                    self._clear_nomination(uid)
+                if not terminal:
+                    self.cache.add_pod_native(ev, uid, node)
+            elif sched in self.frameworks and not terminal:
+                self.queue.add(PodInfo.from_native(ev))
+                self.metrics.child(self.metrics.incoming, "PodAdd", "active").inc()
+            return
+        oidt = old[1]
+        if node:
+            if terminal:
+                self.cache.remove_pod(uid)
+                self.queue.move_all_to_active_or_backoff("AssignedPodCompleted")
+                return
+            if not oidt[2]:
+                self.queue.delete(uid)
+                if uid in self.nominations:
+                    self._clear_nomination(uid)
+                if self.cache.is_assumed(uid):
+                    ps = self.cache.pods[uid]
+                    self.metrics.pod_scheduling.observe(max(0.0, time.monotonic() - ps.info.initial_attempt))
+                    self.metrics.pod_attempts.observe(ps.info.attempts)
+                self.cache.add_pod_native(ev, uid, node)
+            else:
+                self.cache.update_pod_native(ev, uid, node, oidt[5] == h)
+        elif sched in self.frameworks and not terminal:
+            if self.cache.is_assumed(uid):
+                return   # upstream skipPodUpdate
+            if oidt[5] == h:
+                return   # status/resourceVersion-only change
+            self.queue.update(PodInfo.from_native(ev))
+
     def on_node_add(self, obj: dict) -> None:
         self.cache.add_node(obj)
         self.queue.move_all_to_active_or_backoff("NodeAdd")
@@ -271,8 +329,10 @@ class Scheduler:
             "nodes": Informer(self.client, "nodes", self.on_node_add, self.on_node_update, self.on_node_delete),
             "scvs": Informer(self.client, "scvs", self.on_scv, self.on_scv_update, self.on_scv_delete),
             # upstream v1.20 scheduler pod informer: terminal pods are filtered by the apiserver
-            "pods": Informer(self.client, "pods", self.on_pod_add, self.on_pod_update, self.on_pod_delete,
-                             field_selector=POD_FIELD_SELECTOR),
+            "pods": (NativePodInformer(self.client, self.on_pod_native, field_selector=POD_FIELD_SELECTOR)
+                     if self.native is not None else
+                     Informer(self.client, "pods", self.on_pod_add, self.on_pod_update, self.on_pod_delete,
+                              field_selector=POD_FIELD_SELECTOR)),
         }
         # objects only some plugins need (PVCs, PVs, StorageClasses, CSINodes): watched when
         # an enabled plugin declares them; any change may make a parked pod schedulable
@@ -295,6 +355,9 @@ class Scheduler:
         inf = self.informers.get("pods")
         if inf is None:
             return False
+        if self.native is not None:
+            e = inf.entries.get(pi.key)
+            return e is None or e[1][1] != pi.uid or bool(e[1][2])
         cur = inf.store.get(pi.key)
         return cur is None or cur["metadata"].get("uid") != pi.uid or self._assigned(cur)
 
@@ -495,8 +558,11 @@ class Scheduler:
         if nominated:
             patch["status"]["nominatedNodeName"] = nominated
         try:
-            await self.limiter.acquire()
-            await self.client.patch("pods", pi.name, patch, pi.namespace)
+            if self.native is not None:
+                await self.client.patch("pods", pi.name, patch, pi.namespace, limited=True)
+            else:
+                await self.limiter.acquire()
+                await self.client.patch("pods", pi.name, patch, pi.namespace)
         except Exception as e:  # noqa: BLE001 - best effort like upstream
             log.debug("condition update for %s failed: %r", pi.key, e)
 
@@ -526,8 +592,11 @@ class Scheduler:
 
     async def _delete_victim(self, v: PodInfo) -> None:
         try:
-            await self.limiter.acquire()
-            await self.client.delete("pods", v.name, v.namespace)
+            if self.native is not None:
+                await self.client.delete("pods", v.name, v.namespace, limited=True)
+            else:
+                await self.limiter.acquire()
+                await self.client.delete("pods", v.name, v.namespace)
         except Exception as e:  # noqa: BLE001
             log.warning("preemption: deleting %s failed: %r", v.key, e)
 
@@ -607,7 +676,23 @@ class Scheduler:
             self._finish_run(fw, item, results, cycle, t0)
 
     # ================================================================== binding
+    def _native_direct(self, fw: Framework, pi: PodInfo) -> bool:
+        """This pod's bind can go straight to the native transport: DefaultBinder is the
+        only bind plugin, no PreBind plugin applies to the pod, no extenders."""
+        if self.extenders:
+            return False
+        b = fw.direct_binder_for(pi)
+        return b is not None and getattr(b, "native_bind", False)
+
     def _enqueue_bind(self, item: tuple) -> None:
+        fw = item[0]
+        if self.native is not None and self._native_direct(fw, item[2]):
+            from ..plugins.defaults import bind_annotations
+            pi, node = item[2], item[3]
+            self.native.bind(pi.namespace, pi.name, pi.uid, node, bind_annotations(pi),
+                             functools.partial(self._native_bind_done, item, time.perf_counter()),
+                             self.bind_timeout)
+            return
         self._bind_dq.append(item)
         idle = self._bind_idle
         while idle:                       # wake exactly one parked worker
@@ -615,6 +700,43 @@ class Scheduler:
             if not fut.done():
                 fut.set_result(None)
                 break
+
+    def _native_bind_done(self, item: tuple, tb: float, status: int, body: bytes) -> None:
+        """Completion of a native binding POST (runs from the transport's eventfd callback)."""
+        fw, state, pi, node, cycle, t0 = item
+        self.pending_binds -= 1
+        if 200 <= status < 300:
+            st = Status.ok()
+        else:
+            from ..kube.native import api_error
+            if status == 401:
+                self.client._refresh_token(force=True)
+            st = Status.error(f"binding rejected: {api_error(status, body)}", plugin="DefaultBinder")
+        self._after_bind(fw, state if state is not None else _EMPTY_STATE, pi, node, cycle, t0, tb, st)
+
+    def _after_bind(self, fw: Framework, state: CycleState, pi: PodInfo, node: str, cycle: int, t0: float,
+                    tb: float, st: Status) -> None:
+        m = self.metrics
+        m.binding.observe(time.perf_counter() - tb)
+        if self.tracer is not None:
+            self.tracer.span("bind", self.tracer.now_us() - (time.perf_counter() - tb) * 1e6, cat="bind",
+                             pod=pi.key, node=node, ok=st.is_success())
+        if st.is_success():
+            self.cache.finish_binding(pi)
+            fw.run_post_bind(state, pi, node)
+            self.scheduled += 1
+            if self.e2e_samples is not None:
+                self.e2e_samples.append(time.perf_counter() - t0)
+            m.child(m.e2e, "scheduled", fw.name).observe(time.perf_counter() - t0)
+            self.recorder.pod_event(pi, "Normal", "Scheduled", f"Successfully assigned {pi.key} to {node}")
+        else:
+            self.bind_errors += 1
+            fw.run_unreserve(state, pi, node)
+            self.cache.forget(pi)
+            m.child(m.e2e, "error", fw.name).observe(time.perf_counter() - t0)
+            self.recorder.pod_event(pi, "Warning", "FailedScheduling", f"Binding rejected: {st.message()}")
+            log.info("bind %s → %s failed: %s", pi.key, node, st.message())
+            self.queue.add_unschedulable(pi, cycle, unschedulable=False)
 
     async def _bind_worker(self) -> None:
         """Bind workers drain a shared deque and park (one future each) only when it is
@@ -647,27 +769,7 @@ class Scheduler:
                         st = await fw.run_bind(state, pi, node, self._extender_binder(pi))
                 except Exception as e:  # noqa: BLE001
                     st = Status.error(repr(e))
-                m.binding.observe(time.perf_counter() - tb)
-                if self.tracer is not None:
-                    self.tracer.span("bind", self.tracer.now_us() - (time.perf_counter() - tb) * 1e6, cat="bind",
-                                     pod=pi.key, node=node, ok=st.is_success())
-                if st.is_success():
-                    self.cache.finish_binding(pi)
-                    fw.run_post_bind(state, pi, node)
-                    self.scheduled += 1
-                    if self.e2e_samples is not None:
-                        self.e2e_samples.append(time.perf_counter() - t0)
-                    m.child(m.e2e, "scheduled", fw.name).observe(time.perf_counter() - t0)
-                    self.recorder.pod_event(pi, "Normal", "Scheduled",
-                                            f"Successfully assigned {pi.key} to {node}")
-                else:
-                    self.bind_errors += 1
-                    fw.run_unreserve(state, pi, node)
-                    self.cache.forget(pi)
-                    m.child(m.e2e, "error", fw.name).observe(time.perf_counter() - t0)
-                    self.recorder.pod_event(pi, "Warning", "FailedScheduling", f"Binding rejected: {st.message()}")
-                    log.info("bind %s → %s failed: %s", pi.key, node, st.message())
-                    self.queue.add_unschedulable(pi, cycle, unschedulable=False)
+                self._after_bind(fw, state, pi, node, cycle, t0, tb, st)
             finally:
                 self.pending_binds -= 1
 
@@ -702,6 +804,9 @@ class Scheduler:
                 for uid in [u for u, (_n, _i, t) in self.nominations.items() if now - t > 60.0]:
                     self._clear_nomination(uid)
             self._maybe_enable_device()
+            refresh = getattr(self.client, "_refresh_token", None)
+            if refresh is not None:
+                refresh()                        # rotated service-account tokens
             tick += 1
             if tick % 4 == 0 and isinstance(m, SchedulerMetrics):
                 self._export_gpu_metrics()

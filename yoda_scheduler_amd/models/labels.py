@@ -55,6 +55,9 @@ class GpuRequest:
         return True
 
 
+_GPU_REQ_CACHE: dict = {}
+
+
 def parse_gpu_request(labels: Mapping[str, str] | None) -> GpuRequest:
     labels = labels or {}
     n_raw = labels.get(LABEL_NUMBER)
@@ -62,6 +65,17 @@ def parse_gpu_request(labels: Mapping[str, str] | None) -> GpuRequest:
     c_raw = labels.get(LABEL_CLOCK)
     p_raw = labels.get(LABEL_PRIORITY)
     cm_raw = labels.get(LABEL_CLOCK_MIN)
+    # GpuRequest is immutable and a burst repeats a handful of label combinations
+    key = (n_raw, m_raw, c_raw, p_raw, cm_raw)
+    r = _GPU_REQ_CACHE.get(key)
+    if r is None:
+        if len(_GPU_REQ_CACHE) > 4096:
+            _GPU_REQ_CACHE.clear()
+        r = _GPU_REQ_CACHE[key] = _parse_gpu_request(n_raw, m_raw, c_raw, p_raw, cm_raw)
+    return r
+
+
+def _parse_gpu_request(n_raw, m_raw, c_raw, p_raw, cm_raw) -> GpuRequest:
     return GpuRequest(
         has_number=n_raw is not None,
         number=str_to_uint(n_raw) if n_raw is not None else 1,

@@ -7,6 +7,7 @@ loops — native or Python — never touch the raw JSON again.
 from __future__ import annotations
 
 import itertools
+import json
 import time
 from dataclasses import dataclass, field
 from typing import Any, Optional
@@ -140,6 +141,7 @@ PF_DISKS = 16          # in-tree attachable disks (GCE PD, EBS, Azure disk, Cind
 PF_CONTROLLER = 32     # controlled by a ReplicationController / ReplicaSet / StatefulSet
 PF_EXTENDED = 64       # requests resources beyond cpu/memory (amd.com/gpu, ephemeral-storage, ...)
 PF_POD_GROUP = 128     # member of a co-scheduled pod group (Coscheduling)
+PF_REQ_ANTI = 256      # required pod anti-affinity (other pods' symmetry check)
 LABEL_POD_GROUP = "pod-group.scheduling.sigs.k8s.io"
 LABEL_POD_GROUP_MIN = "pod-group.scheduling.sigs.k8s.io/min-available"
 
@@ -155,6 +157,9 @@ def pod_flags(meta: dict, spec: dict, host_ports, ext: Optional[dict] = None) ->
     aff = spec.get("affinity")
     if aff and (aff.get("podAffinity") or aff.get("podAntiAffinity")):
         f |= PF_POD_AFFINITY
+        anti = aff.get("podAntiAffinity")
+        if isinstance(anti, dict) and anti.get("requiredDuringSchedulingIgnoredDuringExecution"):
+            f |= PF_REQ_ANTI
     for v in spec.get("volumes") or ():
         if "persistentVolumeClaim" in v or "ephemeral" in v:
             f |= PF_CLAIMS
@@ -170,9 +175,13 @@ def pod_flags(meta: dict, spec: dict, host_ports, ext: Optional[dict] = None) ->
 
 class PodInfo:
     """Parsed pod. ``__slots__`` + a hand-written constructor: one of these is built per
-    pod per informer event on the scheduling hot path."""
+    pod per informer event on the scheduling hot path.
 
-    __slots__ = ("obj", "uid", "namespace", "name", "num_id", "labels", "gpu", "scheduler_name", "node_name",
+    ``obj`` (the full pod dict) is lazy for pods that arrive through the native transport:
+    the C++ projection already holds every field the cycle reads, so the JSON is decoded
+    only if something (an extender, a Python plugin, an event) asks for the object."""
+
+    __slots__ = ("_obj", "_src", "uid", "namespace", "name", "num_id", "labels", "gpu", "scheduler_name", "node_name",
                  "cpu_m", "mem", "priority", "node_selector", "required_terms", "preferred_terms", "tolerations",
                  "annotations", "host_ports", "attempts", "initial_attempt", "enqueued", "native_req",
                  "native_owner", "assigned_cards", "_creation", "flags", "ext", "nz_cpu_m", "nz_mem")
@@ -183,7 +192,8 @@ class PodInfo:
                  preferred_terms: Optional[list] = None, tolerations: Optional[list] = None,
                  annotations: Optional[dict] = None, host_ports: Optional[list] = None, flags: int = 0,
                  ext: Optional[dict] = None, nz_cpu_m: int = -1, nz_mem: int = -1) -> None:
-        self.obj = obj
+        self._obj = obj
+        self._src = None
         # -1: a single container's non-zero request derived from cpu_m / mem
         self.nz_cpu_m = nz_cpu_m if nz_cpu_m >= 0 else (cpu_m or DEFAULT_MILLI_CPU_REQUEST)
         self.nz_mem = nz_mem if nz_mem >= 0 else (mem or DEFAULT_MEMORY_REQUEST)
@@ -215,6 +225,23 @@ class PodInfo:
         self._creation: Optional[float] = None
 
     @property
+    def obj(self) -> dict:
+        o = self._obj
+        if o is None:
+            src = self._src
+            o = self._obj = json.loads(src.raw()) if src is not None else {}
+            self._src = None
+        return o
+
+    @obj.setter
+    def obj(self, value: dict) -> None:
+        self._obj, self._src = value, None
+
+    def set_source(self, ev) -> None:
+        """Point the lazy ``obj`` at a newer native watch event of the same pod."""
+        self._obj, self._src = None, ev
+
+    @property
     def key(self) -> str:
         return f"{self.namespace}/{self.name}"
 
@@ -224,6 +251,21 @@ class PodInfo:
         if self._creation is None:
             self._creation = parse_rfc3339((self.obj.get("metadata") or {}).get("creationTimestamp")) or time.time()
         return self._creation
+
+    @classmethod
+    def from_native(cls, ev) -> "PodInfo":
+        """Build from a native transport ``PodEvent`` (C++ projection of the same fields
+        ``from_obj`` reads); pods the projection does not cover go through ``from_obj``."""
+        a = ev.info_args()
+        if a is None:
+            pi = cls.from_obj(json.loads(ev.raw()))
+            return pi
+        (uid, ns, name, labels, ann, sched, node, cpu, mem, nzc, nzm, prio, nsel, req, pref, tols, ports,
+         flags, _creation) = a
+        pi = cls(None, uid, ns, name, pod_num_id(uid), labels, parse_gpu_request(labels), sched, node, cpu, mem,
+                 prio, nsel, req, pref, tols, ann, ports, flags, None, nzc, nzm)
+        pi._src = ev
+        return pi
 
     def __repr__(self) -> str:
         return f"PodInfo({self.key}, gpu={self.gpu}, node={self.node_name!r})"

@@ -1,6 +1,9 @@
 """In-tree build of every native artefact (``python -m yoda_scheduler_amd.ops.build``).
 
 * ``_yoda_core``    C++17 scheduling engine (pybind11, g++)            native/core/
+* ``_yoda_kube``    C++17 Kubernetes transport: pipelined HTTP/1.1 +
+                    TLS, watch decoding, pod projection (pybind11)      native/kube/
+* ``yoda-fake-apiserver-native`` epoll fake apiserver for HTTP benches  native/kube/
 * ``_yoda_sniffer`` C++ amd-smi collector (pybind11, links libamd_smi)  native/sniffer/
 * ``yoda-sniffer``  standalone collector binary (JSON on stdout)        native/sniffer/
 * ``libyoda_hip``   gfx950 HIP kernels: batched placement scorer, HBM /
@@ -59,6 +62,30 @@ def build_core(force: bool = False) -> Path:
     return out
 
 
+def build_kube(force: bool = False) -> list[Path]:
+    """Native Kubernetes transport (pybind module) + the native fake apiserver binary."""
+    src = NATIVE / "kube"
+    common = [src / "json.cpp", src / "project.cpp"]
+    deps = common + [src / "transport.cpp", src / "bindings.cpp", src / "json.hpp", src / "http.hpp",
+                     src / "project.hpp", src / "transport.hpp"]
+    flags = ["-O3", "-std=c++17", "-Wall", "-Wno-unused-function", f"-I{src}"]
+    outs = []
+    mod = OUT / f"_yoda_kube{EXT}"
+    if force or _stale(mod, deps):
+        _run([os.environ.get("CXX", "g++"), *flags, "-fPIC", "-shared", "-fvisibility=hidden", *_pybind_includes(),
+              *map(str, common), str(src / "transport.cpp"), str(src / "bindings.cpp"), "-o", str(mod),
+              "-lssl", "-lcrypto", "-lpthread"], "kube transport")
+    outs.append(mod)
+    fake_srcs = [src / "fakeapi.cpp", src / "fakeapi_main.cpp"]
+    if all(p.exists() for p in fake_srcs):
+        exe = OUT / "yoda-fake-apiserver-native"
+        if force or _stale(exe, common + fake_srcs + [src / "fakeapi.hpp", src / "json.hpp", src / "http.hpp"]):
+            _run([os.environ.get("CXX", "g++"), *flags, *map(str, common), *map(str, fake_srcs), "-o", str(exe),
+                  "-lpthread"], "native fake apiserver")
+        outs.append(exe)
+    return outs
+
+
 def build_sniffer(force: bool = False) -> list[Path]:
     src = NATIVE / "sniffer"
     lib_srcs = [src / "collector.cpp"]
@@ -99,7 +126,7 @@ def build_hip(force: bool = False) -> Path:
 def build_all(force: bool = False, hip: bool = True, sniffer: bool = True) -> list[Path]:
     OUT.mkdir(parents=True, exist_ok=True)
     (OUT / "__init__.py").touch()
-    jobs = [lambda: [build_core(force)]]
+    jobs = [lambda: [build_core(force)], lambda: build_kube(force)]
     if sniffer:
         jobs.append(lambda: build_sniffer(force))
     if hip:

@@ -169,18 +169,26 @@ def _inert(name: str):
 INERT_PLUGINS = ["CSILimits"]
 
 
+def bind_annotations(pod) -> list:
+    """(key, value) pairs the Binding carries: the GPU assignment and per-GPU HBM reserve."""
+    cards = getattr(pod, "assigned_cards", None)
+    if cards is None:
+        return []
+    ann = [(ANNOTATION_GPUS, ",".join(str(c) for c in cards))]
+    if pod.gpu.has_memory:
+        ann.append((ANNOTATION_RESERVED, str(pod.gpu.memory)))
+    return ann
+
+
 class DefaultBinder(BindPlugin):
     """POST pods/{name}/binding; the GPU assignment rides on the Binding's annotations,
-    which the apiserver copies onto the pod (one round trip, no extra patch)."""
+    which the apiserver copies onto the pod (one round trip, no extra patch). With the
+    native transport the scheduler submits this same POST directly (``native_bind``)."""
     name = "DefaultBinder"
+    native_bind = True
 
     async def bind(self, state: CycleState, pod, node_name: str) -> Status:
-        ann = {}
-        cards = getattr(pod, "assigned_cards", None)
-        if cards is not None:
-            ann[ANNOTATION_GPUS] = ",".join(str(c) for c in cards)
-            if pod.gpu.has_memory:
-                ann[ANNOTATION_RESERVED] = str(pod.gpu.memory)
+        ann = dict(bind_annotations(pod))
         try:
             await self.handle.client.bind(pod.namespace, pod.name, pod.uid, node_name, ann)
         except Exception as e:  # noqa: BLE001 - surfaced as a bind failure
