@@ -156,10 +156,12 @@ int yoda_hbm_bandwidth(int device, unsigned long long bytes, int iters, double* 
   return (int)hipGetLastError();
 }
 
-// Write an address-dependent pattern over `bytes` of HBM and verify it; returns the
-// number of mismatching 32-bit words in *errors.
-int yoda_hbm_pattern_check(int device, unsigned long long bytes, unsigned seed, unsigned long long* errors,
-                           float* ms_out) {
+// Write an address-dependent pattern (fill_seed) over `bytes` of HBM and verify it
+// against verify_seed; returns the number of mismatching 32-bit words in *errors. A
+// health probe uses one seed; a different verify seed is the self-test that the
+// verifier really compares (every word must mismatch).
+int yoda_hbm_pattern_check2(int device, unsigned long long bytes, unsigned fill_seed, unsigned verify_seed,
+                            unsigned long long* errors, float* ms_out) {
   YODA_CHECK(hipSetDevice(device));
   const size_t n16 = (size_t)(bytes / 16);
   uint4* buf = nullptr;
@@ -172,8 +174,8 @@ int yoda_hbm_pattern_check(int device, unsigned long long bytes, unsigned seed, 
   YODA_CHECK(hipEventCreate(&e1));
   const int grid = grid_for(device);
   YODA_CHECK(hipEventRecord(e0, 0));
-  hipLaunchKernelGGL(k_fill, dim3(grid), dim3(kBlock), 0, 0, buf, n16, seed);
-  hipLaunchKernelGGL(k_verify, dim3(grid), dim3(kBlock), 0, 0, buf, n16, seed, d_err);
+  hipLaunchKernelGGL(k_fill, dim3(grid), dim3(kBlock), 0, 0, buf, n16, fill_seed);
+  hipLaunchKernelGGL(k_verify, dim3(grid), dim3(kBlock), 0, 0, buf, n16, verify_seed, d_err);
   YODA_CHECK(hipEventRecord(e1, 0));
   YODA_CHECK(hipEventSynchronize(e1));
   float ms = 0.f;
@@ -185,6 +187,11 @@ int yoda_hbm_pattern_check(int device, unsigned long long bytes, unsigned seed, 
   hipFree(buf);
   hipFree(d_err);
   return (int)hipGetLastError();
+}
+
+int yoda_hbm_pattern_check(int device, unsigned long long bytes, unsigned seed, unsigned long long* errors,
+                           float* ms_out) {
+  return yoda_hbm_pattern_check2(device, bytes, seed, seed, errors, ms_out);
 }
 
 // xGMI peer-write bandwidth: a copy kernel running on `src` streams a local buffer into

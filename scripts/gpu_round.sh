@@ -18,14 +18,18 @@ step() {  # step NAME SECONDS CMD...
 STEPS=${STEPS:-"tests smoke bench"}
 for s in $STEPS; do
   case $s in
-    tests) step gpu_tests 600 python -m pytest tests -m gpu -q -x ;;
+    tests) step gpu_tests 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     bench5) step bench5 600 python bench.py --config 5 ;;
     bench6on) step bench6_on 600 python bench.py --config 6 --steps 3 --warmup 1 --device on ;;
     bench6off) step bench6_off 600 python bench.py --config 6 --steps 3 --warmup 1 --device off ;;
     benchref) step bench_refqps 600 python bench.py --steps 2 --warmup 0 --reference-qps ;;
-    benchhttp) step bench_http 600 python bench.py --transport http ;;
+    benchhttp) step bench_http 600 python bench.py --transport http --steps 20 --warmup 5 ;;
+    benchhttp5) step bench_http5 600 python bench.py --transport http --config 5 --steps 3 --warmup 1 ;;
+    benchhttppy) step bench_http_pyapi 600 python bench.py --transport http --apiserver python --client aiohttp --steps 10 --warmup 2 ;;
+    profhttp) step prof_http 600 python scripts/profile_bench.py --out gpurun_out/prof_http.txt --transport http --steps 20 --warmup 5 ;;
+    profinproc) step prof_inproc 600 python scripts/profile_bench.py --out gpurun_out/prof_inproc.txt --steps 20 --warmup 5 ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
 done

@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""cProfile of the scheduler process during the timed bursts of ``bench.py``.
+
+    python scripts/profile_bench.py [--out FILE] [bench.py args...]
+
+Profiling is enabled only inside the timed steps (not start-up or warmup), and the top
+functions by own time plus a grouped per-stage summary are printed / written to FILE."""
+from __future__ import annotations
+
+import cProfile
+import io
+import os
+import pstats
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+STAGES = [  # (stage, substrings of "file:function" that belong to it), first match wins
+    ("watch decode + informer dispatch", ("informer.py", "kube/native.py:_drain", "json/")),
+    ("pod event handlers", ("scheduler.py:on_pod", "pod.py", "labels.py", "queue.py:add", "queue.py:update",
+                            "queue.py:_push", "queue.py:delete", "cache.py:add_pod", "cache.py:update_pod",
+                            "cache.py:remove_pod", "cache.py:_add_bound", "queue.py:move_all")),
+    ("scheduling cycle (native engine + bookkeeping)", ("scheduler.py:schedule", "scheduler.py:_batch",
+                                                        "scheduler.py:_prepare", "scheduler.py:_finish",
+                                                        "scheduler.py:_pod_gone", "native.py:pod_req",
+                                                        "cache.py:assumed", "cache.py:_track", "runtime.py",
+                                                        "queue.py:pop", "schedule_batch")),
+    ("binding (submit + completion)", ("scheduler.py:_enqueue_bind", "scheduler.py:_native_bind",
+                                       "scheduler.py:_after_bind", "scheduler.py:_bind_worker",
+                                       "kube/native.py:bind", "defaults.py", "fastbind.py", "client.py:bind",
+                                       "cache.py:finish_binding")),
+    ("event recorder", ("events.py",)),
+    ("asyncio / selectors", ("asyncio/", "selectors.py", "select.epoll")),
+]
+
+
+def main() -> int:
+    args = sys.argv[1:]
+    out = None
+    if args[:1] == ["--out"]:
+        out, args = args[1], args[2:]
+    import bench
+    from yoda_scheduler_amd.bench import harness as H
+    pr = cProfile.Profile()
+    for cls in (H.Shard, H.HttpShard):
+        orig = cls.burst
+
+        def wrap(orig):
+            async def burst(self, tag="b", timeout=600.0):
+                if tag.startswith("s"):
+                    pr.enable()
+                try:
+                    return await orig(self, tag, timeout)
+                finally:
+                    pr.disable()
+            return burst
+        cls.burst = wrap(orig)
+    bench.main(args)
+    st = pstats.Stats(pr)
+    total = sum(v[2] for v in st.stats.values())
+    groups = {name: 0.0 for name, _ in STAGES}
+    groups["other"] = 0.0
+    for (fn, _line, func), v in st.stats.items():
+        key = f"{fn.replace(ROOT + '/', '')}:{func}"
+        for name, pats in STAGES:
+            if any(p in key for p in pats):
+                groups[name] += v[2]
+                break
+        else:
+            groups["other"] += v[2]
+    s = io.StringIO()
+    s.write(f"profiled CPU (own time, all functions): {total:.3f} s\n")
+    for name, t in sorted(groups.items(), key=lambda kv: -kv[1]):
+        s.write(f"  {100 * t / total:5.1f} %  {t:.3f} s  {name}\n")
+    s.write("\n")
+    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(45)
+    text = s.getvalue()
+    print(text)
+    if out:
+        with open(out, "w") as f:
+            f.write(text)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

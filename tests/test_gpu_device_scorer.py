@@ -59,8 +59,9 @@ def test_device_cycle_latency(require_gpu):
         eng.schedule(pi.num_id, req, True)
         ts.append(eng.device_last_us())
     ts.sort()
-    # two launches over 8192 nodes x 8 GPUs: must stay far below a millisecond
-    assert ts[len(ts) // 2] < 1000, ts
+    # measured ≈ 30 µs p50 at 4096-16384 nodes (profiles/device_scorer.md, v3 kernels);
+    # 3× that is the regression bound
+    assert ts[len(ts) // 2] < 100, ts
 
 
 def test_scheduler_auto_enables_device_scorer_and_matches_cpu(require_gpu):

@@ -22,12 +22,14 @@ def test_hbm_pattern_probe_clean(require_gpu):
     assert r["errors"] == 0, r
 
 
-def test_hbm_pattern_probe_detects_mismatch_semantics(require_gpu):
-    # different seeds produce different patterns: verify a fresh fill under seed B is clean
+def test_hbm_pattern_probe_detects_mismatch(require_gpu):
+    # fill under seed 1, verify under seed 2: a verifier that really compares must flag
+    # (essentially) every word — one that always returns 0 fails here
     from yoda_scheduler_amd.ops import hip
-    a = hip.hbm_pattern_check(0, 64 << 20, seed=1)
-    b = hip.hbm_pattern_check(0, 64 << 20, seed=2)
-    assert a["errors"] == 0 and b["errors"] == 0
+    bad = hip.hbm_pattern_check(0, 64 << 20, seed=1, verify_seed=2)
+    assert bad["errors"] > 0.999 * bad["words"], bad
+    ok = hip.hbm_pattern_check(0, 64 << 20, seed=2)
+    assert ok["errors"] == 0, ok
 
 
 def test_hbm_bandwidth_probe(require_gpu):

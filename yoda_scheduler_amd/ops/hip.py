@@ -38,6 +38,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "yoda_hip_device_info": [c_int, c_char_p, c_int, P(c_int), P(c_ull), P(c_int)],
         "yoda_hbm_bandwidth": [c_int, c_ull, c_int, P(c_double), P(c_double)],
         "yoda_hbm_pattern_check": [c_int, c_ull, c_uint, P(c_ull), P(c_float)],
+        "yoda_hbm_pattern_check2": [c_int, c_ull, c_uint, c_uint, P(c_ull), P(c_float)],
         "yoda_peer_write_bandwidth": [c_int, c_int, c_ull, c_int, P(c_double), P(c_int)],
     }
     for name, args in sigs.items():
@@ -95,10 +96,15 @@ def hbm_bandwidth(device: int = 0, nbytes: int = 1 << 30, iters: int = 10) -> di
     return {"read_gbps": r.value, "copy_gbps": c.value, "bytes": nbytes, "iters": iters}
 
 
-def hbm_pattern_check(device: int = 0, nbytes: int = 1 << 30, seed: int = 0x5eed) -> dict:
+def hbm_pattern_check(device: int = 0, nbytes: int = 1 << 30, seed: int = 0x5eed,
+                      verify_seed: int | None = None) -> dict:
+    """Fill ``nbytes`` of HBM with a seeded pattern and count mismatching 32-bit words on
+    read-back. ``verify_seed`` ≠ ``seed`` is the verifier's self-test (all words differ)."""
     err, ms = c_ull(0), c_float(0)
-    _check(lib().yoda_hbm_pattern_check(device, nbytes, seed, ctypes.byref(err), ctypes.byref(ms)), "hbm_pattern")
-    return {"errors": err.value, "ms": ms.value, "bytes": nbytes}
+    vs = seed if verify_seed is None else verify_seed
+    _check(lib().yoda_hbm_pattern_check2(device, nbytes, seed, vs, ctypes.byref(err), ctypes.byref(ms)),
+           "hbm_pattern")
+    return {"errors": err.value, "ms": ms.value, "bytes": nbytes, "words": nbytes // 4}
 
 
 def peer_write_bandwidth(src: int, dst: int, nbytes: int = 256 << 20, iters: int = 10) -> dict:
