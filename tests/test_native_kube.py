@@ -193,30 +193,12 @@ def test_projection_falls_back_for_extended_resources():
 
 
 # ============================================================== native fake apiserver
-class NativeApi:
-    def __init__(self, token: str = "") -> None:
-        from yoda_scheduler_amd.bench.harness import native_apiserver_binary
-        d = tempfile.mkdtemp(prefix="yoda-nfa-")
-        pf = os.path.join(d, "port")
-        cmd = [native_apiserver_binary(), "--port", "0", "--port-file", pf, "--history", "50"]
-        if token:
-            cmd += ["--token", token]
-        self.proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL)
-        t = time.time()
-        while not os.path.exists(pf):
-            assert time.time() - t < 10 and self.proc.poll() is None
-            time.sleep(0.01)
-        with open(pf) as f:
-            self.url = f"http://127.0.0.1:{int(f.read())}"
-
-    def stop(self) -> None:
-        self.proc.terminate()
-        self.proc.wait(10)
+from yoda_scheduler_amd.testing import NativeApiServerProcess as NativeApi  # noqa: E402
 
 
 @pytest.fixture
 def native_api():
-    a = NativeApi()
+    a = NativeApi(history=50)
     yield a
     a.stop()
 

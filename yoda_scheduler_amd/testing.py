@@ -108,3 +108,40 @@ class FakeCluster:
         if self._loop_task is not None:
             self._loop_task.cancel()
             await asyncio.gather(self._loop_task, return_exceptions=True)
+
+
+class NativeApiServerProcess:
+    """The native C++ fake apiserver (``yoda-fake-apiserver-native``) as a child process
+    for tests and tools; ``url`` once started, ``stop()`` terminates it."""
+
+    def __init__(self, token: str = "", history: int = 0, extra: Optional[list] = None) -> None:
+        import os
+        import subprocess
+        import tempfile
+
+        from .bench.harness import native_apiserver_binary
+        d = tempfile.mkdtemp(prefix="yoda-nfa-")
+        pf = os.path.join(d, "port")
+        cmd = [native_apiserver_binary(), "--port", "0", "--port-file", pf]
+        if history:
+            cmd += ["--history", str(history)]
+        if token:
+            cmd += ["--token", token]
+        cmd += list(extra or [])
+        self.proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL)
+        t = time.time()
+        while not os.path.exists(pf):
+            if self.proc.poll() is not None or time.time() - t > 15:
+                raise RuntimeError("native fake apiserver did not start")
+            time.sleep(0.01)
+        with open(pf) as f:
+            self.port = int(f.read())
+        self.url = f"http://127.0.0.1:{self.port}"
+
+    def stop(self) -> None:
+        if self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(10)
+            except Exception:  # noqa: BLE001
+                self.proc.kill()
