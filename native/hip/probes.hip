@@ -156,6 +156,13 @@ int yoda_hbm_bandwidth(int device, unsigned long long bytes, int iters, double* 
   return (int)hipGetLastError();
 }
 
+// PCI bus id ("dddd:bb:dd.f", as hipDeviceGetPCIBusId formats it) of HIP ordinal `device`:
+// joins the HIP enumeration to amd-smi's BDF-ordered index for probe attribution.
+int yoda_hip_pci_bus_id(int device, char* buf, int len) {
+  YODA_CHECK(hipDeviceGetPCIBusId(buf, len, device));
+  return 0;
+}
+
 // Write an address-dependent pattern (fill_seed) over `bytes` of HBM and verify it
 // against verify_seed; returns the number of mismatching 32-bit words in *errors. A
 // health probe uses one seed; a different verify seed is the self-test that the

@@ -127,6 +127,57 @@ std::vector<GpuSample> Collector::sample() {
     amdsmi_bdf_t b{};
     if (amdsmi_get_gpu_device_bdf(h, &b) == AMDSMI_STATUS_SUCCESS) g.bdf = bdf_str(b);
     else g.errors.push_back("bdf");
+    char uuid[AMDSMI_GPU_UUID_SIZE + 8] = {0};
+    unsigned int ulen = sizeof(uuid);
+    if (amdsmi_get_gpu_device_uuid(h, &ulen, uuid) == AMDSMI_STATUS_SUCCESS) g.uuid = uuid;
+    else g.errors.push_back("uuid");
+    amdsmi_enumeration_info_t en{};
+    if (amdsmi_get_gpu_enumeration_info(h, &en) == AMDSMI_STATUS_SUCCESS) {
+      g.hip_id = (int)en.hip_id;
+      g.hsa_id = (int)en.hsa_id;
+      g.drm_render = (int)en.drm_render;
+      g.drm_card = (int)en.drm_card;
+      g.hip_uuid = en.hip_uuid;
+    } else {
+      g.errors.push_back("enumeration");
+    }
+    amdsmi_kfd_info_t kf{};
+    if (amdsmi_get_gpu_kfd_info(h, &kf) == AMDSMI_STATUS_SUCCESS) {
+      if (kf.node_id != 0xFFFFFFFFu) g.kfd_node = (int)kf.node_id;
+      if (kf.current_partition_id != 0xFFFFFFFFu) g.partition_id = (int)kf.current_partition_id;
+    }
+    uint32_t np = 0;
+    if (amdsmi_get_gpu_process_list(h, &np, nullptr) == AMDSMI_STATUS_SUCCESS ||
+        np > 0) {
+      std::vector<amdsmi_proc_info_t> procs(np + 4);
+      uint32_t cap = (uint32_t)procs.size();
+      amdsmi_status_t pst = amdsmi_get_gpu_process_list(h, &cap, procs.data());
+      if (pst == AMDSMI_STATUS_SUCCESS || pst == AMDSMI_STATUS_OUT_OF_RESOURCES) {
+        uint32_t n = std::min<uint32_t>(cap, (uint32_t)procs.size());
+        g.processes = (int)cap;
+        for (uint32_t k = 0; k < n; ++k) {
+          g.proc_cus += procs[k].cu_occupancy;
+          g.proc_vram_mb += procs[k].memory_usage.vram_mem >> 20;
+        }
+      }
+    } else {
+      g.errors.push_back("process_list");
+    }
+    for (int j = 0; j < (int)handles_.size(); ++j) {
+      if (j == i) continue;
+      TopoPeer tp;
+      tp.peer = j;
+      amdsmi_link_type_t lt{};
+      uint64_t hops = 0;
+      if (amdsmi_topo_get_link_type(h, (amdsmi_processor_handle)handles_[j], &hops, &lt) != AMDSMI_STATUS_SUCCESS)
+        continue;
+      tp.type = (int)lt;
+      tp.hops = hops;
+      uint64_t w = 0;
+      if (amdsmi_topo_get_link_weight(h, (amdsmi_processor_handle)handles_[j], &w) == AMDSMI_STATUS_SUCCESS)
+        tp.weight = w;
+      g.topo.push_back(tp);
+    }
     amdsmi_vram_usage_t vu{};
     if (amdsmi_get_gpu_vram_usage(h, &vu) == AMDSMI_STATUS_SUCCESS) {
       g.vram_total_mb = vu.vram_total;
@@ -233,7 +284,17 @@ std::string to_json(const std::vector<GpuSample>& s) {
     const GpuSample& g = s[i];
     if (i) o << ",";
     o << "{\"index\":" << g.index << ",\"bdf\":\"" << esc(g.bdf) << "\",\"model\":\"" << esc(g.model)
-      << "\",\"vramTotalMB\":" << g.vram_total_mb << ",\"vramUsedMB\":" << g.vram_used_mb
+      << "\",\"uuid\":\"" << esc(g.uuid) << "\",\"hipUuid\":\"" << esc(g.hip_uuid) << "\",\"hipId\":" << g.hip_id
+      << ",\"hsaId\":" << g.hsa_id << ",\"drmRender\":" << g.drm_render << ",\"drmCard\":" << g.drm_card
+      << ",\"kfdNode\":" << g.kfd_node << ",\"partitionId\":" << g.partition_id
+      << ",\"processes\":" << g.processes << ",\"processCUs\":" << g.proc_cus
+      << ",\"processVramMB\":" << g.proc_vram_mb << ",\"topo\":[";
+    for (size_t k = 0; k < g.topo.size(); ++k) {
+      const TopoPeer& t = g.topo[k];
+      o << (k ? "," : "") << "{\"peer\":" << t.peer << ",\"type\":" << t.type << ",\"hops\":" << t.hops
+        << ",\"weight\":" << t.weight << "}";
+    }
+    o << "],\"vramTotalMB\":" << g.vram_total_mb << ",\"vramUsedMB\":" << g.vram_used_mb
       << ",\"sclkMHz\":" << g.sclk_cur << ",\"sclkMaxMHz\":" << g.sclk_max << ",\"mclkMaxMHz\":" << g.mclk_max
       << ",\"computeUnits\":" << g.cus << ",\"hbmBandwidthGBps\":" << g.hbm_bw_gbps
       << ",\"powerLimitW\":" << g.power_limit_w << ",\"powerW\":" << g.power_w

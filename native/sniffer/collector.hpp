@@ -27,10 +27,29 @@ struct LinkSample {
   double load = 0;           // (read+write rate) / (2 × max bandwidth), clamped to [0, 1]
 };
 
+// amd-smi topology to another GPU of the node (amdsmi_topo_get_link_type / _weight)
+struct TopoPeer {
+  int peer = 0;              // amd-smi index of the peer
+  int type = 0;              // amdsmi_link_type_t (2 = XGMI, 1 = PCIe)
+  uint64_t hops = 0;
+  uint64_t weight = 0;
+};
+
 struct GpuSample {
   int index = 0;
   std::string bdf;
   std::string model;
+  // identity: amd-smi index is BDF order; HIP/ROCr enumerate in KFD order, which can
+  // differ (and partitions add logical GPUs per BDF) — the UUIDs are the stable names
+  std::string uuid;          // amdsmi_get_gpu_device_uuid
+  std::string hip_uuid;      // amdsmi_get_gpu_enumeration_info (what ROCR_VISIBLE_DEVICES accepts)
+  int hip_id = -1, hsa_id = -1, drm_render = -1, drm_card = -1;
+  int kfd_node = -1, partition_id = -1;
+  // tenants: processes with a context on this GPU and the CUs their queues occupy
+  int processes = -1;
+  uint32_t proc_cus = 0;     // Σ amdsmi_proc_info_t.cu_occupancy
+  uint64_t proc_vram_mb = 0;
+  std::vector<TopoPeer> topo;
   uint32_t vram_total_mb = 0, vram_used_mb = 0;
   uint32_t sclk_cur = 0, sclk_max = 0, mclk_max = 0;
   uint32_t cus = 0;

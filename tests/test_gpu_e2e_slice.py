@@ -72,8 +72,13 @@ def test_minimum_end_to_end_slice(require_gpu):
     gpus = [int(x) for x in pod["metadata"]["annotations"]["scv.amd.com/gpus"].split(",")]
     assert len(gpus) == 1
     assert pod["spec"]["schedulerName"] == "yoda-scheduler"
-    assert env["HIP_VISIBLE_DEVICES"] == env["ROCR_VISIBLE_DEVICES"] == str(gpus[0])   # via the downward API
+    # pinned by ROCr UUID through the downward API, and the workload really ran on the
+    # GPU whose amd-smi BDF the scheduler reserved (the identity contract end to end)
+    vis = pod["metadata"]["annotations"]["scv.amd.com/visible-devices"]
+    assert env["ROCR_VISIBLE_DEVICES"] == vis and env.get("HIP_VISIBLE_DEVICES") is None
     assert ok, log
+    bus = next(line for line in log if line.startswith("allocated")).split("pci_bus_ids=")[1].split(",")[0]
+    assert int(bus) == int(before.status.card_list[gpus[0]].bdf.split(":")[1], 16), (bus, log)
     g = gpus[0]
     drop = before.status.card_list[g].free_memory - after.status.card_list[g].free_memory
     assert drop >= MB, (drop, log)                        # the sniffer saw the pod's HBM

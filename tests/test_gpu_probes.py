@@ -96,3 +96,47 @@ def test_real_telemetry_schedules_pod(require_gpu):
     pod = asyncio.run(run())
     assert pod["spec"]["nodeName"] == "gpu-node"
     assert pod["metadata"]["annotations"]["scv.amd.com/gpus"] != ""
+
+
+def test_gpu_identity_mapping_on_box(require_gpu):
+    """amd-smi index ↔ HIP ordinal ↔ PCI address ↔ UUIDs agree on the real driver."""
+    from yoda_scheduler_amd.ops import hip
+    from yoda_scheduler_amd.sniffer.collector import AmdSmiBackend, samples_to_scv
+    from yoda_scheduler_amd.sniffer.publisher import hip_to_index
+    be = AmdSmiBackend()
+    s = be.sample()
+    be.close()
+    n = hip.device_count()
+    m = hip_to_index(s, n, hip.pci_bus_id)
+    assert set(m) == set(range(n)), (m, [(x["index"], x["hipId"], x["bdf"]) for x in s])
+    by_index = {x["index"]: x for x in s}
+    for d, i in m.items():
+        assert hip.pci_bus_id(d) == by_index[i]["bdf"].lower(), (d, i)
+    for x in s:
+        assert x["uuid"] and x["hipUuid"], x
+    cards = samples_to_scv("n", s).status.card_list
+    assert all(c.hip_uuid and c.hip_id >= 0 for c in cards)
+
+
+def test_probe_safety_on_box(require_gpu):
+    """This test process holds a HIP context: the real process list reports it and the
+    agent skips the GPU; marked idle, the same GPU is probed with a free-HBM-sized buffer
+    and the result lands on its amd-smi index."""
+    from yoda_scheduler_amd.ops import hip
+    from yoda_scheduler_amd.sniffer.collector import AmdSmiBackend
+    from yoda_scheduler_amd.sniffer.publisher import SnifferAgent
+    hip.device_info(0)                                 # make sure this process has a context
+    be = AmdSmiBackend()
+    agent = SnifferAgent(None, "n", be, probe=True, probe_bytes=256 << 20, busy_vram_mb=1 << 30)
+    s = be.sample()
+    i0 = next(x["index"] for x in s if x["hipId"] == 0)
+    assert s[i0]["processes"] >= 1, s[i0]              # ourselves
+    res = agent.run_probes(s)
+    assert "busy" in res[i0]["skipped"], res
+    for x in s:
+        x["processes"] = 0
+    res = agent.run_probes(s)
+    be.close()
+    r = res[i0]
+    assert r["hip"] == 0 and r["bytes"] <= 256 << 20 and r["pattern_errors"] == 0, r
+    assert agent.measured_bw[i0] > 3000 and agent.probe_fail_streak[i0] == 0

@@ -69,7 +69,9 @@ def test_review_validate_and_mutate():
 
 def test_visible_devices_injection():
     """Containers of yoda pods read the GPU assignment through the downward API; the
-    Binding copies ``scv.amd.com/gpus`` onto the pod before containers start."""
+    Binding copies ``scv.amd.com/visible-devices`` (ROCr UUIDs) onto the pod before
+    containers start. Only ROCR_VISIBLE_DEVICES is set: HIP_VISIBLE_DEVICES would index
+    the already-filtered devices."""
     body = ar({"scv/number": "2"}, scheduler="yoda-scheduler")
     spec = body["request"]["object"]["spec"]
     spec["containers"].append({"name": "side", "image": "y", "env": [{"name": "A", "value": "1"}]})
@@ -77,10 +79,10 @@ def test_visible_devices_injection():
     spec["initContainers"] = [{"name": "init", "image": "w"}]
     ops = json.loads(base64.b64decode(review(body, mutate=True)["response"]["patch"]))
     pod = apply_add_ops(body["request"]["object"], ops)
-    ref = {"fieldRef": {"fieldPath": "metadata.annotations['scv.amd.com/gpus']"}}
+    ref = {"fieldRef": {"fieldPath": "metadata.annotations['scv.amd.com/visible-devices']"}}
     for c in (pod["spec"]["containers"][0], pod["spec"]["containers"][1], pod["spec"]["initContainers"][0]):
         env = {e["name"]: e.get("valueFrom") for e in c["env"]}
-        assert env["HIP_VISIBLE_DEVICES"] == ref and env["ROCR_VISIBLE_DEVICES"] == ref
+        assert env["ROCR_VISIBLE_DEVICES"] == ref and "HIP_VISIBLE_DEVICES" not in env
     assert pod["spec"]["containers"][1]["env"][0] == {"name": "A", "value": "1"}
     assert pod["spec"]["containers"][2]["env"] == [{"name": "HIP_VISIBLE_DEVICES", "value": "3"}]   # untouched
     # device-plugin pods and opted-out pods are left alone
@@ -144,8 +146,9 @@ def test_executor_resolves_downward_api_env():
     body = ar({"scv/number": "2"}, scheduler="yoda-scheduler")
     ops = json.loads(base64.b64decode(review(body, mutate=True)["response"]["patch"]))
     pod = apply_add_ops(body["request"]["object"], ops)
-    pod["metadata"]["annotations"] = {"scv.amd.com/gpus": "3,5"}      # written by the Binding
+    pod["metadata"]["annotations"] = {"scv.amd.com/gpus": "3,5",                  # written by the Binding
+                                      "scv.amd.com/visible-devices": "GPU-aa,GPU-bb"}
     pod["spec"]["containers"][0]["env"].append({"name": "NODE", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}})
     pod["spec"]["nodeName"] = "n7"
     env = resolve_env(pod, pod["spec"]["containers"][0])
-    assert env == {"HIP_VISIBLE_DEVICES": "3,5", "ROCR_VISIBLE_DEVICES": "3,5", "NODE": "n7"}
+    assert env == {"ROCR_VISIBLE_DEVICES": "GPU-aa,GPU-bb", "NODE": "n7"}

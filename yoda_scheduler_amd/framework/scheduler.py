@@ -689,7 +689,7 @@ class Scheduler:
         if self.native is not None and self._native_direct(fw, item[2]):
             from ..plugins.defaults import bind_annotations
             pi, node = item[2], item[3]
-            self.native.bind(pi.namespace, pi.name, pi.uid, node, bind_annotations(pi),
+            self.native.bind(pi.namespace, pi.name, pi.uid, node, bind_annotations(pi, self.cache.scvs, node),
                              functools.partial(self._native_bind_done, item, time.perf_counter()),
                              self.bind_timeout)
             return

@@ -25,7 +25,12 @@ LABEL_PRIORITY = "scv/priority"
 # additive AMD extensions (not in the reference)
 LABEL_CLOCK_MIN = "scv.amd.com/clock-min"        # card clock >= value (MHz)
 LABEL_GANG_POLICY = "scv.amd.com/gang"           # "xgmi" (default) | "any" | "numa"
-ANNOTATION_GPUS = "scv.amd.com/gpus"             # assigned GPU indices, e.g. "0,3"
+ANNOTATION_GPUS = "scv.amd.com/gpus"             # assigned GPU indices (amd-smi, BDF order), e.g. "0,3"
+# what the pod's ROCr runtime must see, per assigned GPU: the ROCr/HIP UUID ("GPU-…") when
+# the sniffer reported it, else the HIP ordinal, else the amd-smi index — always present on
+# a yoda binding, so a downward-API env var built from it is never empty
+ANNOTATION_VISIBLE = "scv.amd.com/visible-devices"
+ANNOTATION_GPU_UUIDS = "scv.amd.com/gpu-uuids"   # amd-smi device UUIDs of the assigned GPUs
 ANNOTATION_RESERVED = "scv.amd.com/reserved-mb"  # HBM MB reserved per assigned GPU
 ANNOTATION_NODE = "scv.amd.com/node"
 

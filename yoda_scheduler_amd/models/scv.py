@@ -8,8 +8,9 @@ Field names live in ONE place (``_CARD_FIELDS`` / ``_STATUS_FIELDS``) so the CRD
 schema, the sniffer publisher and the scheduler cache agree.
 
 MI355X additions are an additive ``status.amd`` block: per-GPU physical id, PCI BDF,
-NUMA node, compute/memory partition, CU occupancy, sclk and per-peer xGMI link load,
-plus the sample timestamp used for staleness-based health.
+identity (amd-smi UUID, HIP/ROCr UUID and ordinal, render node, partition id), NUMA
+node, compute/memory partition, CU occupancy + GFX activity, tenant process count, sclk
+and per-peer xGMI link load, plus the sample timestamp used for staleness-based health.
 """
 from __future__ import annotations
 
@@ -45,9 +46,18 @@ _AMD_CARD_FIELDS = {
     "compute_partition": "computePartition",
     "memory_partition": "memoryPartition",
     "cu_occupancy": "cuOccupancy",
+    "gfx_activity": "gfxActivity",
+    "occupancy_source": "occupancySource",
     "sclk_mhz": "sclkMhz",
     "ecc_uncorrectable": "eccUncorrectable",
     "xgmi_links_up": "xgmiLinksUp",
+    # identity (amd-smi index = BDF order ≠ HIP/ROCr order in general; UUIDs are stable)
+    "uuid": "uuid",
+    "hip_uuid": "hipUuid",
+    "hip_id": "hipId",
+    "render_node": "renderNode",
+    "partition_id": "partitionId",
+    "processes": "processes",
 }
 
 
@@ -89,11 +99,21 @@ class Card:
     numa_node: int = 0
     compute_partition: str = "SPX"
     memory_partition: str = "NPS1"
-    cu_occupancy: float = 0.0   # 0..100 (gfx activity %)
+    # CU occupancy %: Σ per-process CUs held (amd-smi process list) / CUs when the driver
+    # reports it ("process-cus"), else the GFX-engine busy % as a proxy ("gfx-activity")
+    cu_occupancy: float = 0.0
+    gfx_activity: float = 0.0   # 0..100 GFX engine busy %
+    occupancy_source: str = "gfx-activity"
     sclk_mhz: int = 0           # current sclk
     ecc_uncorrectable: int = 0
     xgmi_links_up: bool = True
     xgmi: list[XgmiLink] = field(default_factory=list)
+    uuid: str = ""              # amd-smi device UUID
+    hip_uuid: str = ""          # HIP/ROCr UUID ("GPU-…", accepted by ROCR_VISIBLE_DEVICES)
+    hip_id: int = -1            # HIP ordinal on the node (-1: unknown)
+    render_node: int = -1       # /dev/dri/renderD<n>
+    partition_id: int = -1      # compute partition of a CPX/DPX/QPX logical GPU
+    processes: int = -1         # processes with a context on the GPU (-1: unknown)
 
     @property
     def phys(self) -> int:
@@ -174,6 +194,8 @@ class Scv:
                 for a, j in _AMD_CARD_FIELDS.items():
                     if j in ext and ext[j] is not None:
                         setattr(c, a, ext[j])
+                if "gfxActivity" not in ext and "cuOccupancy" in ext:      # pre-r2 producers
+                    c.gfx_activity = float(ext["cuOccupancy"])
                 c.physical_id = int(ext.get("physicalId", c.id))
                 c.xgmi = [XgmiLink.from_json(l) for l in ext.get("xgmi") or []]
             cards.append(c)

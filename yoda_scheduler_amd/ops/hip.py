@@ -39,6 +39,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "yoda_hbm_bandwidth": [c_int, c_ull, c_int, P(c_double), P(c_double)],
         "yoda_hbm_pattern_check": [c_int, c_ull, c_uint, P(c_ull), P(c_float)],
         "yoda_hbm_pattern_check2": [c_int, c_ull, c_uint, c_uint, P(c_ull), P(c_float)],
+        "yoda_hip_pci_bus_id": [c_int, c_char_p, c_int],
         "yoda_peer_write_bandwidth": [c_int, c_int, c_ull, c_int, P(c_double), P(c_int)],
     }
     for name, args in sigs.items():
@@ -88,6 +89,13 @@ def device_info(device: int = 0) -> dict:
     _check(lib().yoda_hip_device_info(device, arch, 64, ctypes.byref(cus), ctypes.byref(hbm), ctypes.byref(clk)),
            "hipGetDeviceProperties")
     return {"arch": arch.value.decode(), "cus": cus.value, "hbm_bytes": hbm.value, "clock_khz": clk.value}
+
+
+def pci_bus_id(device: int = 0) -> str:
+    """Lower-case PCI address of a HIP ordinal (amd-smi's ``bdf`` format)."""
+    buf = ctypes.create_string_buffer(64)
+    _check(lib().yoda_hip_pci_bus_id(device, buf, 64), "pci_bus_id")
+    return buf.value.decode().strip().lower()
 
 
 def hbm_bandwidth(device: int = 0, nbytes: int = 1 << 30, iters: int = 10) -> dict:

@@ -16,7 +16,7 @@ from typing import Optional
 
 from ..framework.interfaces import (BindPlugin, CycleState, FilterPlugin, NativeBinding, Plugin,
                                     PostFilterPlugin, PostFilterResult, QueueSortPlugin, ScorePlugin, Status)
-from ..models.labels import ANNOTATION_GPUS, ANNOTATION_RESERVED
+from ..models.labels import ANNOTATION_GPU_UUIDS, ANNOTATION_GPUS, ANNOTATION_RESERVED, ANNOTATION_VISIBLE
 from ..models.pod import PF_EXTENDED, PF_HOST_PORTS
 from ..ops.native import core
 
@@ -169,12 +169,35 @@ def _inert(name: str):
 INERT_PLUGINS = ["CSILimits"]
 
 
-def bind_annotations(pod) -> list:
-    """(key, value) pairs the Binding carries: the GPU assignment and per-GPU HBM reserve."""
+def visible_device_ids(scv, cards: list) -> tuple[str, str]:
+    """(ROCR_VISIBLE_DEVICES value, amd-smi UUID list) for the assigned card positions of a
+    node's Scv. Per card: ROCr UUID, else HIP ordinal, else the amd-smi index."""
+    vis, uuids = [], []
+    cl = scv.status.card_list if scv is not None else []
+    for c in cards:
+        card = cl[c] if 0 <= c < len(cl) else None
+        if card is not None and card.hip_uuid:
+            vis.append(card.hip_uuid)
+        elif card is not None and card.hip_id >= 0:
+            vis.append(str(card.hip_id))
+        else:
+            vis.append(str(card.id if card is not None else c))
+        if card is not None and card.uuid:
+            uuids.append(card.uuid)
+    return ",".join(vis), (",".join(uuids) if len(uuids) == len(cards) else "")
+
+
+def bind_annotations(pod, scvs: Optional[dict] = None, node: str = "") -> list:
+    """(key, value) pairs the Binding carries: the GPU assignment (amd-smi indices, the
+    ROCr-visible ids, the device UUIDs) and the per-GPU HBM reserve."""
     cards = getattr(pod, "assigned_cards", None)
     if cards is None:
         return []
     ann = [(ANNOTATION_GPUS, ",".join(str(c) for c in cards))]
+    vis, uuids = visible_device_ids((scvs or {}).get(node), cards)
+    ann.append((ANNOTATION_VISIBLE, vis))
+    if uuids:
+        ann.append((ANNOTATION_GPU_UUIDS, uuids))
     if pod.gpu.has_memory:
         ann.append((ANNOTATION_RESERVED, str(pod.gpu.memory)))
     return ann
@@ -188,7 +211,7 @@ class DefaultBinder(BindPlugin):
     native_bind = True
 
     async def bind(self, state: CycleState, pod, node_name: str) -> Status:
-        ann = dict(bind_annotations(pod))
+        ann = dict(bind_annotations(pod, self.handle.cache.scvs, node_name))
         try:
             await self.handle.client.bind(pod.namespace, pod.name, pod.uid, node_name, ann)
         except Exception as e:  # noqa: BLE001 - surfaced as a bind failure

@@ -66,10 +66,20 @@ class FakeBackend:
     """Synthetic amd-smi samples for an MI355X node (same JSON shape as the C++ collector)."""
     name = "fake"
 
-    def __init__(self, gpus: int = 8, spec: GpuSpec = MI355X, partition: str = "SPX", seed: int = 0) -> None:
+    def __init__(self, gpus: int = 8, spec: GpuSpec = MI355X, partition: str = "SPX", seed: int = 0,
+                 hip_order: Optional[list[int]] = None, partitions_per_gpu: int = 1, node: str = "node") -> None:
+        """``hip_order[i]``: HIP ordinal of amd-smi index ``i`` (a permutation, as when the
+        KFD enumerates GPUs in another order than PCI address); ``partitions_per_gpu`` > 1
+        models CPX/DPX/QPX: ``gpus`` logical GPUs, consecutive ones sharing a physical BDF."""
         self.spec = spec
         self.gpus = gpus
         self.partition = partition
+        self.ppg = max(1, partitions_per_gpu)
+        self.hip_order = list(hip_order) if hip_order is not None else list(range(gpus))
+        if sorted(self.hip_order) != list(range(gpus)):
+            raise ValueError("hip_order must be a permutation of range(gpus)")
+        self.node = node
+        self.tenants: dict[int, tuple[int, int]] = {}     # index → (processes, CUs held)
         self.state = [FakeGpuState() for _ in range(gpus)]
         self.rng = random.Random(seed)
         self._counters = [[[0, 0] for _ in range(gpus)] for _ in range(gpus)]
@@ -94,12 +104,21 @@ class FakeBackend:
                 rate = load * cap_kbps
                 self._counters[i][j][0] += int(rate * dt)
                 self._counters[i][j][1] += int(rate * dt)
-                links.append({"peerBdf": _bdf(j), "type": 2, "bitRateGbps": 32,
+                if self.ppg > 1 and j // self.ppg == i // self.ppg:
+                    continue              # partitions of one GPU share its links
+                links.append({"peerBdf": self._bdf(j), "type": 2, "bitRateGbps": 32,
                               "maxBandwidthGbps": int(self.spec.xgmi_link_gbps * 8),
                               "readKB": self._counters[i][j][0], "writeKB": self._counters[i][j][1],
                               "readKBps": rate, "writeKBps": rate, "load": load})
+            procs, cus = self.tenants.get(i, (0, 0))
+            hid = self.hip_order[i]
             out.append({
-                "index": i, "bdf": _bdf(i), "model": self.spec.model,
+                "index": i, "bdf": self._bdf(i), "model": self.spec.model,
+                "uuid": self.uuid(i), "hipUuid": f"GPU-{self.uuid(i)[-16:]}", "hipId": hid, "hsaId": hid + 1,
+                "drmRender": 128 + hid, "drmCard": hid + 1, "kfdNode": hid + 1,
+                "partitionId": i % self.ppg if self.ppg > 1 else -1,
+                "processes": procs, "processCUs": cus, "processVramMB": st.used_mb if procs else 0,
+                "topo": [{"peer": j, "type": 2, "hops": 1, "weight": 15} for j in range(self.gpus) if j != i],
                 "vramTotalMB": self.spec.hbm_mb, "vramUsedMB": st.used_mb,
                 "sclkMHz": self.spec.max_sclk_mhz if st.gfx_activity else 150, "sclkMaxMHz": self.spec.max_sclk_mhz,
                 "mclkMaxMHz": 2000, "computeUnits": self.spec.cus, "hbmBandwidthGBps": self.spec.hbm_bw_gbps,
@@ -115,9 +134,18 @@ class FakeBackend:
     def close(self) -> None:
         return None
 
+    def _bdf(self, i: int) -> str:
+        return _bdf(i // self.ppg, i % self.ppg)
 
-def _bdf(i: int) -> str:
-    return f"0000:{0x05 + 0x10 * i:02x}:00.0"
+    def uuid(self, i: int) -> str:
+        """Stable per logical GPU (node name, physical slot, partition)."""
+        import hashlib
+        h = hashlib.sha1(f"{self.node}/{i // self.ppg}/{i % self.ppg}".encode()).hexdigest()
+        return f"{h[:8]}-{h[8:12]}-{h[12:16]}-{h[16:20]}-{h[20:32]}"
+
+
+def _bdf(i: int, fn: int = 0) -> str:
+    return f"0000:{0x05 + 0x10 * i:02x}:00.{fn}"
 
 
 def _phys_key(bdf: str) -> str:
@@ -152,15 +180,24 @@ def samples_to_scv(node: str, samples: list[dict], interval_ms: int = 1000, meas
                                   max_bandwidth_gbps=float(l.get("maxBandwidthGbps", 0)) / 8.0,
                                   up=int(l.get("bitRateGbps", 1)) > 0))
         bw = int((measured_bw or {}).get(i, s.get("hbmBandwidthGBps", 0)) or 0)
+        cus = int(s.get("computeUnits", 0))
+        procs = int(s.get("processes", -1))
+        if procs >= 0 and cus > 0:
+            occ, occ_src = min(100.0, 100.0 * int(s.get("processCUs", 0)) / cus), "process-cus"
+        else:
+            occ, occ_src = float(s.get("gfxActivity", 0)), "gfx-activity"
         cards.append(Card(
             id=i, health=HEALTHY if healthy else UNHEALTHY, model=s.get("model", ""),
             power=int(s.get("powerLimitW", 0)), total_memory=total, clock=int(s.get("sclkMaxMHz", 0)),
             free_memory=total - used, core=int(s.get("computeUnits", 0)), bandwidth=bw,
             physical_id=phys, bdf=s.get("bdf", ""), numa_node=max(int(s.get("numaNode", 0)), 0),
             compute_partition=s.get("computePartition") or "SPX", memory_partition=s.get("memoryPartition") or "NPS1",
-            cu_occupancy=float(s.get("gfxActivity", 0)), sclk_mhz=int(s.get("sclkMHz", 0)),
+            cu_occupancy=occ, gfx_activity=float(s.get("gfxActivity", 0)), occupancy_source=occ_src,
+            sclk_mhz=int(s.get("sclkMHz", 0)),
             ecc_uncorrectable=int(s.get("eccUncorrectable", 0)), xgmi_links_up=int(s.get("xgmiLinksDown", 0)) == 0,
-            xgmi=links))
+            xgmi=links, uuid=str(s.get("uuid", "")), hip_uuid=str(s.get("hipUuid", "")),
+            hip_id=int(s.get("hipId", -1)), render_node=int(s.get("drmRender", -1)),
+            partition_id=int(s.get("partitionId", -1)), processes=procs))
     st = ScvStatus(card_list=cards, update_time=max((float(s.get("time", 0)) for s in samples), default=time.time()),
                    sniffer=sniffer)
     st.recompute_sums()

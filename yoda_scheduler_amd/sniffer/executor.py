@@ -1,6 +1,7 @@
 """Node-side pod executor ("kubelet-lite") that turns a binding into a real GPU workload —
 the last hop of SURVEY §7.2's minimum end-to-end slice: scheduler decision →
-``scv.amd.com/gpus`` annotation → a ROCm process pinned with ``HIP_VISIBLE_DEVICES`` that
+``scv.amd.com/visible-devices`` annotation (ROCr UUIDs) → a ROCm process pinned with
+``ROCR_VISIBLE_DEVICES`` that
 allocates the pod's ``scv/memory`` MB of HBM on those GPUs → the next amd-smi sample shows
 the HBM drop, closing the telemetry loop the reference never closes (its burst pods are
 invisible to the sniffer).
@@ -17,7 +18,7 @@ import sys
 from dataclasses import dataclass, field
 from typing import Optional
 
-from ..models.labels import ANNOTATION_GPUS, LABEL_MEMORY
+from ..models.labels import ANNOTATION_GPUS, ANNOTATION_VISIBLE, LABEL_MEMORY
 
 HOLD_SCRIPT = r"""
 import os, sys, time, torch
@@ -26,7 +27,9 @@ bufs = [torch.empty(mb * (1 << 20), dtype=torch.uint8, device=f"cuda:{i}") for i
 for b in bufs:
     b.fill_(1)
 torch.cuda.synchronize()
-print("allocated", mb, "MB on", len(bufs), "GPU(s) HIP_VISIBLE_DEVICES=", os.environ.get("HIP_VISIBLE_DEVICES"), flush=True)
+buses = [torch.cuda.get_device_properties(i).pci_bus_id for i in range(torch.cuda.device_count())]
+print("allocated", mb, "MB on", len(bufs), "GPU(s) ROCR_VISIBLE_DEVICES=", os.environ.get("ROCR_VISIBLE_DEVICES"),
+      "pci_bus_ids=", ",".join(str(b) for b in buses), flush=True)
 time.sleep(secs)
 """
 
@@ -91,13 +94,14 @@ class PodExecutor:
         containers = (pod.get("spec") or {}).get("containers") or [{}]
         spec_env = resolve_env(pod, containers[0])
         env = dict(os.environ)
-        env.pop("CUDA_VISIBLE_DEVICES", None)
+        for k in ("CUDA_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+            env.pop(k, None)
         if "HIP_VISIBLE_DEVICES" in spec_env or "ROCR_VISIBLE_DEVICES" in spec_env:
             # pinned by the pod spec (yoda-webhook's downward-API injection)
             env.update(spec_env)
         else:
-            env.update(spec_env, HIP_VISIBLE_DEVICES=",".join(map(str, gpus)),
-                       ROCR_VISIBLE_DEVICES=",".join(map(str, gpus)))
+            vis = ann.get(ANNOTATION_VISIBLE) or ",".join(map(str, gpus))
+            env.update(spec_env, ROCR_VISIBLE_DEVICES=vis)
         self.env_log[key] = {k: env.get(k) for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES")}
         proc = subprocess.Popen([sys.executable, "-c", HOLD_SCRIPT, str(mb), str(self.hold_seconds)], env=env,
                                 stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)

@@ -9,10 +9,14 @@ a warning (typos such as ``scv/memroy`` would otherwise be ignored silently).
 Mutation (``/mutate``, optional): pods that carry scv labels but left
 ``spec.schedulerName`` at the default are pointed at ``schedulerName`` (the yoda profile),
 so users cannot forget the profile name (quirk Q6 made that easy in the reference).
-Their containers also get ``HIP_VISIBLE_DEVICES`` / ``ROCR_VISIBLE_DEVICES`` from the
-downward API (``metadata.annotations['scv.amd.com/gpus']``): the Binding copies the
+Their containers also get ``ROCR_VISIBLE_DEVICES`` from the downward API
+(``metadata.annotations['scv.amd.com/visible-devices']``): the Binding copies the
 scheduler's GPU assignment onto the pod before any container starts, so the process sees
 exactly the GPUs whose HBM the scheduler reserved (the reference only picked a node, Q10).
+The value names each GPU by its ROCr UUID (``GPU-…``, from amd-smi's enumeration info),
+so the pinning is right whatever order HIP/KFD enumerate devices in and with CPX/DPX
+partitions; ``HIP_VISIBLE_DEVICES`` is *not* set: it indexes the devices ROCr already
+filtered, so the same list in both variables would hide GPUs.
 Containers that set either variable themselves, pods that request ``amd.com/gpu`` through
 the device plugin, and pods annotated ``scv.amd.com/inject-visible-devices: "false"`` are
 left alone.
@@ -32,9 +36,10 @@ KNOWN = set(_UNSIGNED) | {LABEL_PRIORITY, "scv.amd.com/gang"}
 GANG_VALUES = ("xgmi", "any", "numa")
 
 
-ANNOTATION_GPUS = "scv.amd.com/gpus"
+ANNOTATION_VISIBLE = "scv.amd.com/visible-devices"
 ANNOTATION_NO_INJECT = "scv.amd.com/inject-visible-devices"
-VISIBLE_ENV = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES")
+VISIBLE_ENV = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+INJECT_ENV = "ROCR_VISIBLE_DEVICES"
 
 
 @dataclass
@@ -105,8 +110,8 @@ def _visible_devices_ops(pod: dict) -> list:
             names = {e.get("name") for e in env or ()}
             if names & set(VISIBLE_ENV):
                 continue
-            vals = [{"name": n, "valueFrom": {"fieldRef": {"fieldPath": f"metadata.annotations['{ANNOTATION_GPUS}']"}}}
-                    for n in VISIBLE_ENV]
+            vals = [{"name": INJECT_ENV,
+                     "valueFrom": {"fieldRef": {"fieldPath": f"metadata.annotations['{ANNOTATION_VISIBLE}']"}}}]
             if env is None:
                 ops.append({"op": "add", "path": f"/spec/{key}/{i}/env", "value": vals})
             else:
