@@ -137,6 +137,7 @@ PYBIND11_MODULE(_yoda_core, m) {
            py::arg("lib_path"), py::arg("device") = 0, py::arg("capacity") = 65536, py::arg("min_nodes") = 256, py::call_guard<EngineGuard>())
       .def("disable_device", &Engine::disable_device, py::call_guard<EngineGuard>())
       .def_property_readonly("device_enabled", &Engine::device_enabled)
+      .def_property_readonly("device_ctx", &Engine::device_ctx)
       .def_property_readonly("device_cycles", &Engine::device_cycles)
       .def_property_readonly("device_fallbacks", &Engine::device_fallbacks)
       .def("device_last_us", &Engine::device_last_us, py::call_guard<EngineGuard>())

@@ -1127,14 +1127,22 @@ bool Engine::schedule_batch_device(const std::vector<uint64_t>& pods, const std:
   }
   out->clear();
   out->reserve(pods.size());
+  std::vector<int32_t> diverged;   // device assumed, host refused (duplicate pod): re-upload
   for (size_t i = 0; i < pods.size(); ++i) {
     ++cycles_;
     ++dev_cycles_;
     CycleResult r;
     fill_result(res[i], &r);
-    if (r.node >= 0) reserve(pods[i], *reqs[i], r.node, r.cards);   // marks the row dirty: re-synced next
+    if (r.node >= 0 && !reserve(pods[i], *reqs[i], r.node, r.cards)) diverged.push_back(r.node);
     out->push_back(std::move(r));
   }
+  // the device already applied every winner's assume to its own rows (same fields, same
+  // arithmetic as reserve() with the reservation pending), so the rows reserve() just marked
+  // dirty are identical on both sides: no re-upload. flush_dirty() emptied the list before the
+  // batch, so every entry in it now comes from these reservations.
+  for (int32_t i : dirty_list_) dirty_[i] = 0;
+  dirty_list_.clear();
+  for (int32_t i : diverged) mark_dirty(i);
   return true;
 }
 

@@ -265,6 +265,7 @@ class Engine {
   bool enable_device(const std::string& lib_path, int device, int capacity, int min_nodes, std::string* err);
   void disable_device();
   bool device_enabled() const { return dev_ctx_ != nullptr; }
+  uintptr_t device_ctx() const { return (uintptr_t)dev_ctx_; }   // for yoda_dev_* debug entry points
   uint64_t device_cycles() const { return dev_cycles_; }
   uint64_t device_fallbacks() const { return dev_fallbacks_; }
   float device_last_us() const;

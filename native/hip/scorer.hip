@@ -32,6 +32,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "yoda_dev_abi.h"
 
@@ -189,12 +190,12 @@ __global__ void k_scatter(const yoda_dev_node_t* __restrict__ stage, const int32
 }
 
 // ------------------------------------------------------------------ K1: filter + maxima
-// One lane group = one node (lane `sub` = GPU slot). Writes feas/elig, counts the reason,
-// folds the card metrics of feasible nodes into the wave maxima `wmx`.
-__device__ __forceinline__ void filter_group(const yoda_dev_node_t* nd, int i, bool valid, const yoda_dev_req_t& r,
-                                             const uint8_t* __restrict__ cand, uint8_t* __restrict__ feas,
-                                             uint8_t* __restrict__ elig, int* s_reason, unsigned long long* wmx,
-                                             int& nfeas, int grp, int sub) {
+// One lane group = one node (lane `sub` = GPU slot). Returns the node's filter reason (0 =
+// feasible) and its eligible-GPU mask, and folds the card metrics of feasible nodes into the
+// wave maxima `wmx` (wave-uniform afterwards). Shared by k_filter and k_batch.
+__device__ __forceinline__ int filter_eval(const yoda_dev_node_t* nd, bool valid, const yoda_dev_req_t& r,
+                                           uint8_t cnd, unsigned long long* wmx, uint32_t& emask_out, int grp,
+                                           int sub) {
   const bool yoda = (r.filters & F_YODA) != 0;
   // every load of the node issued up front: one memory round trip per node
   const uint8_t flags = valid ? nd->flags : 0, ncards = nd->ncards;
@@ -203,7 +204,6 @@ __device__ __forceinline__ void filter_group(const yoda_dev_node_t* nd, int i, b
                 req_cpu = nd->req_cpu, alloc_mem = nd->alloc_mem, req_mem = nd->req_mem;
   const yoda_dev_card_t cd = nd->cards[sub];
   const uint8_t healthy = nd->healthy[sub];
-  const uint8_t cnd = (r.use_candidates && valid) ? cand[i] : 0;
   int reason = 0;
   if (!(flags & YODA_DEV_ALIVE)) {
     reason = RS_DEAD;
@@ -228,12 +228,7 @@ __device__ __forceinline__ void filter_group(const yoda_dev_node_t* nd, int i, b
   const uint32_t emask = (uint32_t)((__ballot(e) >> (grp * kGroup)) & 0xFFu);
   if (yoda_stage && (uint64_t)__popc(emask) < r.number) reason = RS_GPU_FIT;
   const bool ok = valid && reason == 0;
-  if (valid && sub == 0) {
-    feas[i] = ok;
-    elig[i] = (uint8_t)emask;
-    if (reason) atomicAdd(&s_reason[reason], 1);
-  }
-  if (sub == 0 && ok) ++nfeas;
+  emask_out = emask;
   if (yoda) {
     const bool take = ok && ((emask >> sub) & 1u);
     unsigned long long v[6];
@@ -245,6 +240,23 @@ __device__ __forceinline__ void filter_group(const yoda_dev_node_t* nd, int i, b
       wmx[k] = m > wmx[k] ? m : wmx[k];
     }
   }
+  return valid ? reason : 0;
+}
+
+__device__ __forceinline__ void filter_group(const yoda_dev_node_t* nd, int i, bool valid, const yoda_dev_req_t& r,
+                                             const uint8_t* __restrict__ cand, uint8_t* __restrict__ feas,
+                                             uint8_t* __restrict__ elig, int* s_reason, unsigned long long* wmx,
+                                             int& nfeas, int grp, int sub) {
+  const uint8_t cnd = (r.use_candidates && valid) ? cand[i] : 0;
+  uint32_t emask = 0;
+  const int reason = filter_eval(nd, valid, r, cnd, wmx, emask, grp, sub);
+  const bool ok = valid && reason == 0;
+  if (valid && sub == 0) {
+    feas[i] = ok;
+    elig[i] = (uint8_t)emask;
+    if (reason) atomicAdd(&s_reason[reason], 1);
+  }
+  if (sub == 0 && ok) ++nfeas;
 }
 
 __global__ __launch_bounds__(kBlock) void k_filter(const PatchArgs pa, yoda_dev_node_t* __restrict__ nodes, int n,
@@ -421,6 +433,219 @@ __device__ __forceinline__ bool better(int64_t oa, uint32_t ma, int64_t ob, uint
 }
 
 // ------------------------------------------------------------------ K2: scores + gang search
+// Per-pod constants of the score phase (maxima from the filter phase, gang-search bounds).
+struct ScoreConsts {
+  uint64_t mx[6];
+  int k, s_begin, s_end;
+  int32_t P;
+  bool search, yoda_s;
+};
+
+__device__ __forceinline__ ScoreConsts score_consts(const yoda_dev_req_t& r, const uint64_t* maxima) {
+  ScoreConsts s;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) s.mx[j] = maxima[j];
+  const bool yoda_f = (r.filters & F_YODA) != 0;
+  s.yoda_s = yoda_f && r.w_yoda != 0;
+  s.k = (int)(r.has_number ? (r.number > 64 ? 64 : r.number) : 1);
+  s.search = yoda_f && s.k >= 1 && s.k <= YODA_DEV_CARDS;
+  s.P = s.k * (s.k - 1) / 2;
+  s.s_begin = s.search ? c_subsets.start[s.k] : 0;
+  s.s_end = s.search ? c_subsets.start[s.k + 1] : 0;
+  return s;
+}
+
+// One lane group scores one node (lane `sub` = card `sub`): the gang / GPU-set choice (the
+// Reserve choice if this node wins), the yoda raw score and the upstream default scores.
+// Outputs are valid on the group's `sub == 0` lane when `act`; `lo`/`hi` fold the raw score.
+// Every shuffle is executed by every lane (callers iterate wave-uniformly). Shared by k_score
+// and k_batch.
+__device__ __forceinline__ void score_node(const yoda_dev_node_t* nd, bool act, uint32_t emask,
+                                           const yoda_dev_req_t& r, const ScoreConsts& sc,
+                                           const uint8_t* s_masks, int sub, int64_t& raw_o, int64_t& total_o,
+                                           uint32_t& mask_o, int32_t& quality_o, unsigned long long& lo,
+                                           unsigned long long& hi, unsigned long long* dbg = nullptr) {
+#define DSTAMP(k)                                                  \
+  do {                                                             \
+    if (dbg) dbg[k] = __builtin_amdgcn_s_memrealtime();            \
+  } while (0)
+  const uint64_t mx0 = sc.mx[0], mx1 = sc.mx[1], mx2 = sc.mx[2], mx3 = sc.mx[3], mx4 = sc.mx[4], mx5 = sc.mx[5];
+  const int k = sc.k;
+  const bool search = sc.search, yoda_s = sc.yoda_s;
+  const int32_t P = sc.P;
+  const int s_begin = sc.s_begin, s_end = sc.s_end;
+  const uint8_t ncards = nd->ncards;
+  // ---- per-node register tables (every lane of the group holds the whole node)
+  uint64_t ef[YODA_DEV_CARDS];
+  uint32_t tot[YODA_DEV_CARDS], occ[YODA_DEV_CARDS], numa[YODA_DEV_CARDS];
+#pragma unroll
+  for (int a = 0; a < YODA_DEV_CARDS; ++a) {
+    const uint4 lo4 = reinterpret_cast<const uint4*>(&nd->cards[a])[0];   // total, free, reserved, pending
+    ef[a] = eff_free(lo4.y, lo4.w, lo4.x, lo4.z);
+    tot[a] = lo4.x;
+    occ[a] = nd->occ[a];
+    numa[a] = nd->numa[a] & 63u;
+  }
+  uint32_t lq[32];   // 64 u16 card-pair qualities, packed 2 per dword
+  {
+    const uint4* q4 = reinterpret_cast<const uint4*>(&nd->linkq[0][0]);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const uint4 v = q4[t];
+      lq[4 * t] = v.x; lq[4 * t + 1] = v.y; lq[4 * t + 2] = v.z; lq[4 * t + 3] = v.w;
+    }
+  }
+  DSTAMP(0);
+  // ---- gang / GPU-set selection (the Reserve choice if this node wins)
+  uint32_t best_m = 0;
+  int64_t best_o = LLONG_MAX;
+  int32_t best_lb = 0;
+  bool found = false;
+  if (search && act && k == 1) {
+    // single-GPU pods (the bulk of a mixed burst): the k = 1 table is {1<<0 … 1<<7} in
+    // order, so lane `sub` owns subset {sub}; no pairs (P = 0) and one NUMA domain leave
+    // only the fit and occupancy terms — the generic loop's 28 predicated pair adds and
+    // 8-card sums are skipped. Same integer arithmetic, so the result is bit-identical.
+    if ((emask >> sub) & 1u) {
+      uint64_t efs = ef[0];
+      uint32_t tos = tot[0], ocs = occ[0];
+#pragma unroll
+      for (int a = 1; a < YODA_DEV_CARDS; ++a) {
+        efs = sub == a ? ef[a] : efs;
+        tos = sub == a ? tot[a] : tos;
+        ocs = sub == a ? occ[a] : ocs;
+      }
+      const uint64_t fa = efs - r.memory;
+      const int64_t leftover = tos ? (int64_t)udiv(fa * 1000000ull, (uint64_t)tos) : 0;
+      const int64_t fit = r.binpack ? leftover : 1000000 - leftover;
+      const int64_t occ_bad = (int64_t)sdiv_small((int32_t)(ocs * 100u), 1);
+      best_o = r.w_fit * fit + r.w_occ * occ_bad;
+      best_m = 1u << sub;
+      best_lb = 0;
+      found = true;
+    }
+#pragma unroll
+    for (int off = 4; off > 0; off >>= 1) {
+      const int64_t oo = __shfl_xor(best_o, off, 64);
+      const uint32_t om = __shfl_xor(best_m, off, 64);
+      const int32_t ol = __shfl_xor(best_lb, off, 64);
+      const int of = __shfl_xor((int)found, off, 64);
+      if (of && (!found || better(oo, om, best_o, best_m))) {
+        best_o = oo; best_m = om; best_lb = ol; found = true;
+      }
+    }
+  } else if (search && act) {
+    for (int t = s_begin + sub; t < s_end; t += kGroup) {
+      const uint32_t m = s_masks[t];
+      if (m & ~emask) continue;
+      int32_t qsum = 0;
+      uint64_t nmask = 0;
+      uint64_t fa = 0, tt = 0;
+      uint32_t oc = 0;
+#pragma unroll
+      for (int a = 0; a < YODA_DEV_CARDS; ++a) {
+        const bool ia = (m >> a) & 1u;
+        nmask |= ia ? (1ull << numa[a]) : 0ull;
+        fa += ia ? ef[a] - r.memory : 0;
+        tt += ia ? tot[a] : 0;
+        oc += ia ? occ[a] : 0u;
+#pragma unroll
+        for (int b = a + 1; b < YODA_DEV_CARDS; ++b) {
+          const int idx = a * YODA_DEV_CARDS + b;
+          const int32_t q = (int32_t)((lq[idx >> 1] >> ((idx & 1) * 16)) & 0xFFFFu);
+          qsum += (ia && ((m >> b) & 1u)) ? q : 0;
+        }
+      }
+      const int32_t lb = P ? sdiv_small((P * 10000 - qsum) * 100, P) : 0;
+      const int32_t d = __popcll(nmask);
+      const int64_t numa_bad = k > 1 ? (int64_t)sdiv_small((d - 1) * 1000000, k - 1) : 0;
+      const int64_t leftover = tt ? (int64_t)udiv(fa * 1000000ull, tt) : 0;
+      const int64_t fit = r.binpack ? leftover : 1000000 - leftover;
+      const int64_t occ_bad = (int64_t)sdiv_small((int32_t)(oc * 100u), k);
+      const int64_t o = r.w_link * (int64_t)lb + r.w_numa * numa_bad + r.w_fit * fit + r.w_occ * occ_bad;
+      if (!found || better(o, m, best_o, best_m)) {
+        best_o = o; best_m = m; best_lb = lb; found = true;
+      }
+    }
+#pragma unroll
+    for (int off = 4; off > 0; off >>= 1) {
+      const int64_t oo = __shfl_xor(best_o, off, 64);
+      const uint32_t om = __shfl_xor(best_m, off, 64);
+      const int32_t ol = __shfl_xor(best_lb, off, 64);
+      const int of = __shfl_xor((int)found, off, 64);
+      if (of && (!found || better(oo, om, best_o, best_m))) {
+        best_o = oo; best_m = om; best_lb = ol; found = true;
+      }
+    }
+  } else {
+    // keep the shuffles wave-uniform for inactive groups
+#pragma unroll
+    for (int off = 4; off > 0; off >>= 1) {
+      (void)__shfl_xor(best_o, off, 64);
+      (void)__shfl_xor(best_m, off, 64);
+      (void)__shfl_xor(best_lb, off, 64);
+      (void)__shfl_xor((int)found, off, 64);
+    }
+  }
+  const int32_t quality = found ? 10000 - sdiv_small(best_lb, 100) : 10000;
+  DSTAMP(1);
+  // ---- yoda raw score (algorithm.go:28-87 with the Q1/Q2/Q3/Q4 fixes); lane sub = card sub
+  uint64_t basic = 0, tsum = 0, fsum = 0, asum = 0;
+  if (act && sub < ncards) {
+    const yoda_dev_card_t cd = nd->cards[sub];
+    tsum = cd.total;
+    fsum = ef[0];
+#pragma unroll
+    for (int a = 1; a < YODA_DEV_CARDS; ++a) fsum = sub == a ? ef[a] : fsum;
+    asum = cd.reserved;
+    if ((emask >> sub) & 1u) {
+      basic = udiv((uint64_t)cd.bandwidth * 100, mx0) + udiv((uint64_t)cd.clock * 100, mx1) +
+              udiv((uint64_t)cd.core * 100, mx2) + udiv((uint64_t)cd.power * 100, mx4) +
+              udiv(fsum * 100, mx3) * 2 + udiv((uint64_t)cd.total * 100, mx5);
+    }
+  }
+  basic = gsum(basic);
+  tsum = gsum(tsum);
+  fsum = gsum(fsum);
+  asum = gsum(asum);
+  DSTAMP(2);
+  if (act && sub == 0) {
+    int64_t s_out = 0;
+    if (yoda_s) {
+      const uint64_t actual = tsum ? udiv(fsum * 100, tsum) * 2 : 0;
+      const uint64_t allocate = (tsum == 0 || tsum < asum) ? 0 : udiv((tsum - asum) * 100, tsum) * 3;
+      uint64_t s = basic + allocate + actual;
+      if (r.has_number && r.number > 1 && r.number <= ncards && found)
+        s += (uint64_t)(quality / 100) * (uint64_t)r.w_gang_score;
+      s_out = s > (uint64_t)LLONG_MAX ? 0 : (int64_t)s;
+      const unsigned long long us = (unsigned long long)s_out;
+      lo = us < lo ? us : lo;
+      hi = us > hi ? us : hi;
+    }
+    // upstream default scores (engine.cpp Engine::score_nodes)
+    const int64_t rc = nd->nz_cpu + r.nz_cpu_m, rm = nd->nz_mem + r.nz_mem;
+    const int64_t ac = nd->alloc_cpu, am = nd->alloc_mem;
+    int64_t least = 0, most = 0, extra = r.w_const;
+    if (ac > 0 && rc <= ac) least += (int64_t)udiv((uint64_t)(ac - rc) * 100, (uint64_t)ac);
+    if (am > 0 && rm <= am) least += (int64_t)udiv((uint64_t)(am - rm) * 100, (uint64_t)am);
+    if (ac > 0) most += (int64_t)udiv((uint64_t)(rc < ac ? rc : ac) * 100, (uint64_t)ac);
+    if (am > 0) most += (int64_t)udiv((uint64_t)(rm < am ? rm : am) * 100, (uint64_t)am);
+    extra += r.w_least * (least / 2) + r.w_most * (most / 2);
+    if (r.w_balanced) {
+      const double cf = ac > 0 ? (double)rc / (double)ac : 1.0;
+      const double mf = am > 0 ? (double)rm / (double)am : 1.0;
+      const int64_t b = (cf >= 1 || mf >= 1) ? 0 : (int64_t)((1.0 - fabs(cf - mf)) * 100);
+      extra += r.w_balanced * b;
+    }
+    raw_o = s_out;
+    total_o = extra;
+    mask_o = best_m;
+    quality_o = quality;
+  }
+  DSTAMP(3);
+#undef DSTAMP
+}
+
 __global__ __launch_bounds__(kBlock) void k_score(yoda_dev_node_t* __restrict__ nodes, int n,
                                                   const yoda_dev_req_t r, const uint8_t* __restrict__ feas,
                                                   const uint8_t* __restrict__ elig, int64_t* __restrict__ raw,
@@ -435,15 +660,8 @@ __global__ __launch_bounds__(kBlock) void k_score(yoda_dev_node_t* __restrict__ 
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = uniform(threadIdx.x >> 6);
   const int grp = lane >> 3, sub = lane & 7;
-  const bool yoda_f = (r.filters & F_YODA) != 0;
-  const bool yoda_s = yoda_f && r.w_yoda != 0;
-  const uint64_t mx0 = g->maxima[0], mx1 = g->maxima[1], mx2 = g->maxima[2], mx3 = g->maxima[3], mx4 = g->maxima[4],
-                 mx5 = g->maxima[5];
-  const int k = (int)(r.has_number ? (r.number > 64 ? 64 : r.number) : 1);
-  const bool search = yoda_f && k >= 1 && k <= YODA_DEV_CARDS;
-  const int32_t P = k * (k - 1) / 2;
-  const int s_begin = search ? c_subsets.start[k] : 0, s_end = search ? c_subsets.start[k + 1] : 0;
-  const int64_t nz_cpu = r.nz_cpu_m, nz_mem = r.nz_mem;
+  const uint64_t gmx[6] = {g->maxima[0], g->maxima[1], g->maxima[2], g->maxima[3], g->maxima[4], g->maxima[5]};
+  const ScoreConsts sc = score_consts(r, gmx);
   unsigned long long lo = ULLONG_MAX, hi = 0;
   const int stride = gridDim.x * kWaves * kNodesPerWave;
   for (int base = uniform((blockIdx.x * kWaves + wave) * kNodesPerWave); base < n; base += stride) {
@@ -453,170 +671,15 @@ __global__ __launch_bounds__(kBlock) void k_score(yoda_dev_node_t* __restrict__ 
     const bool act = i < n && feas[i];
     const yoda_dev_node_t* nd = nodes + (i < n ? i : n - 1);
     const uint32_t emask = act ? elig[i] : 0u;
-    const uint8_t ncards = nd->ncards;
-    // ---- per-node register tables (every lane of the group holds the whole node)
-    uint64_t ef[YODA_DEV_CARDS];
-    uint32_t tot[YODA_DEV_CARDS], occ[YODA_DEV_CARDS], numa[YODA_DEV_CARDS];
-#pragma unroll
-    for (int a = 0; a < YODA_DEV_CARDS; ++a) {
-      const uint4 lo4 = reinterpret_cast<const uint4*>(&nd->cards[a])[0];   // total, free, reserved, pending
-      ef[a] = eff_free(lo4.y, lo4.w, lo4.x, lo4.z);
-      tot[a] = lo4.x;
-      occ[a] = nd->occ[a];
-      numa[a] = nd->numa[a] & 63u;
-    }
-    uint32_t lq[32];   // 64 u16 card-pair qualities, packed 2 per dword
-    {
-      const uint4* q4 = reinterpret_cast<const uint4*>(&nd->linkq[0][0]);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const uint4 v = q4[t];
-        lq[4 * t] = v.x; lq[4 * t + 1] = v.y; lq[4 * t + 2] = v.z; lq[4 * t + 3] = v.w;
-      }
-    }
-    // ---- gang / GPU-set selection (the Reserve choice if this node wins)
-    uint32_t best_m = 0;
-    int64_t best_o = LLONG_MAX;
-    int32_t best_lb = 0;
-    bool found = false;
-    if (search && act && k == 1) {
-      // single-GPU pods (the bulk of a mixed burst): the k = 1 table is {1<<0 … 1<<7} in
-      // order, so lane `sub` owns subset {sub}; no pairs (P = 0) and one NUMA domain leave
-      // only the fit and occupancy terms — the generic loop's 28 predicated pair adds and
-      // 8-card sums are skipped. Same integer arithmetic, so the result is bit-identical.
-      if ((emask >> sub) & 1u) {
-        uint64_t efs = ef[0];
-        uint32_t tos = tot[0], ocs = occ[0];
-#pragma unroll
-        for (int a = 1; a < YODA_DEV_CARDS; ++a) {
-          efs = sub == a ? ef[a] : efs;
-          tos = sub == a ? tot[a] : tos;
-          ocs = sub == a ? occ[a] : ocs;
-        }
-        const uint64_t fa = efs - r.memory;
-        const int64_t leftover = tos ? (int64_t)udiv(fa * 1000000ull, (uint64_t)tos) : 0;
-        const int64_t fit = r.binpack ? leftover : 1000000 - leftover;
-        const int64_t occ_bad = (int64_t)sdiv_small((int32_t)(ocs * 100u), 1);
-        best_o = r.w_fit * fit + r.w_occ * occ_bad;
-        best_m = 1u << sub;
-        best_lb = 0;
-        found = true;
-      }
-#pragma unroll
-      for (int off = 4; off > 0; off >>= 1) {
-        const int64_t oo = __shfl_xor(best_o, off, 64);
-        const uint32_t om = __shfl_xor(best_m, off, 64);
-        const int32_t ol = __shfl_xor(best_lb, off, 64);
-        const int of = __shfl_xor((int)found, off, 64);
-        if (of && (!found || better(oo, om, best_o, best_m))) {
-          best_o = oo; best_m = om; best_lb = ol; found = true;
-        }
-      }
-    } else if (search && act) {
-      for (int t = s_begin + sub; t < s_end; t += kGroup) {
-        const uint32_t m = s_masks[t];
-        if (m & ~emask) continue;
-        int32_t qsum = 0;
-        uint64_t nmask = 0;
-        uint64_t fa = 0, tt = 0;
-        uint32_t oc = 0;
-#pragma unroll
-        for (int a = 0; a < YODA_DEV_CARDS; ++a) {
-          const bool ia = (m >> a) & 1u;
-          nmask |= ia ? (1ull << numa[a]) : 0ull;
-          fa += ia ? ef[a] - r.memory : 0;
-          tt += ia ? tot[a] : 0;
-          oc += ia ? occ[a] : 0u;
-#pragma unroll
-          for (int b = a + 1; b < YODA_DEV_CARDS; ++b) {
-            const int idx = a * YODA_DEV_CARDS + b;
-            const int32_t q = (int32_t)((lq[idx >> 1] >> ((idx & 1) * 16)) & 0xFFFFu);
-            qsum += (ia && ((m >> b) & 1u)) ? q : 0;
-          }
-        }
-        const int32_t lb = P ? sdiv_small((P * 10000 - qsum) * 100, P) : 0;
-        const int32_t d = __popcll(nmask);
-        const int64_t numa_bad = k > 1 ? (int64_t)sdiv_small((d - 1) * 1000000, k - 1) : 0;
-        const int64_t leftover = tt ? (int64_t)udiv(fa * 1000000ull, tt) : 0;
-        const int64_t fit = r.binpack ? leftover : 1000000 - leftover;
-        const int64_t occ_bad = (int64_t)sdiv_small((int32_t)(oc * 100u), k);
-        const int64_t o = r.w_link * (int64_t)lb + r.w_numa * numa_bad + r.w_fit * fit + r.w_occ * occ_bad;
-        if (!found || better(o, m, best_o, best_m)) {
-          best_o = o; best_m = m; best_lb = lb; found = true;
-        }
-      }
-#pragma unroll
-      for (int off = 4; off > 0; off >>= 1) {
-        const int64_t oo = __shfl_xor(best_o, off, 64);
-        const uint32_t om = __shfl_xor(best_m, off, 64);
-        const int32_t ol = __shfl_xor(best_lb, off, 64);
-        const int of = __shfl_xor((int)found, off, 64);
-        if (of && (!found || better(oo, om, best_o, best_m))) {
-          best_o = oo; best_m = om; best_lb = ol; found = true;
-        }
-      }
-    } else {
-      // keep the shuffles wave-uniform for inactive groups
-#pragma unroll
-      for (int off = 4; off > 0; off >>= 1) {
-        (void)__shfl_xor(best_o, off, 64);
-        (void)__shfl_xor(best_m, off, 64);
-        (void)__shfl_xor(best_lb, off, 64);
-        (void)__shfl_xor((int)found, off, 64);
-      }
-    }
-    const int32_t quality = found ? 10000 - sdiv_small(best_lb, 100) : 10000;
-    // ---- yoda raw score (algorithm.go:28-87 with the Q1/Q2/Q3/Q4 fixes); lane sub = card sub
-    uint64_t basic = 0, tsum = 0, fsum = 0, asum = 0;
-    if (act && sub < ncards) {
-      const yoda_dev_card_t cd = nd->cards[sub];
-      tsum = cd.total;
-      fsum = ef[0];
-#pragma unroll
-      for (int a = 1; a < YODA_DEV_CARDS; ++a) fsum = sub == a ? ef[a] : fsum;
-      asum = cd.reserved;
-      if ((emask >> sub) & 1u) {
-        basic = udiv((uint64_t)cd.bandwidth * 100, mx0) + udiv((uint64_t)cd.clock * 100, mx1) +
-                udiv((uint64_t)cd.core * 100, mx2) + udiv((uint64_t)cd.power * 100, mx4) +
-                udiv(fsum * 100, mx3) * 2 + udiv((uint64_t)cd.total * 100, mx5);
-      }
-    }
-    basic = gsum(basic);
-    tsum = gsum(tsum);
-    fsum = gsum(fsum);
-    asum = gsum(asum);
+    int64_t raw_v = 0, total_v = 0;
+    uint32_t mask_v = 0;
+    int32_t quality_v = 0;
+    score_node(nd, act, emask, r, sc, s_masks, sub, raw_v, total_v, mask_v, quality_v, lo, hi);
     if (act && sub == 0) {
-      int64_t s_out = 0;
-      if (yoda_s) {
-        const uint64_t actual = tsum ? udiv(fsum * 100, tsum) * 2 : 0;
-        const uint64_t allocate = (tsum == 0 || tsum < asum) ? 0 : udiv((tsum - asum) * 100, tsum) * 3;
-        uint64_t s = basic + allocate + actual;
-        if (r.has_number && r.number > 1 && r.number <= ncards && found)
-          s += (uint64_t)(quality / 100) * (uint64_t)r.w_gang_score;
-        s_out = s > (uint64_t)LLONG_MAX ? 0 : (int64_t)s;
-        const unsigned long long us = (unsigned long long)s_out;
-        lo = us < lo ? us : lo;
-        hi = us > hi ? us : hi;
-      }
-      // upstream default scores (engine.cpp Engine::score_nodes)
-      const int64_t rc = nd->nz_cpu + nz_cpu, rm = nd->nz_mem + nz_mem;
-      const int64_t ac = nd->alloc_cpu, am = nd->alloc_mem;
-      int64_t least = 0, most = 0, extra = r.w_const;
-      if (ac > 0 && rc <= ac) least += (int64_t)udiv((uint64_t)(ac - rc) * 100, (uint64_t)ac);
-      if (am > 0 && rm <= am) least += (int64_t)udiv((uint64_t)(am - rm) * 100, (uint64_t)am);
-      if (ac > 0) most += (int64_t)udiv((uint64_t)(rc < ac ? rc : ac) * 100, (uint64_t)ac);
-      if (am > 0) most += (int64_t)udiv((uint64_t)(rm < am ? rm : am) * 100, (uint64_t)am);
-      extra += r.w_least * (least / 2) + r.w_most * (most / 2);
-      if (r.w_balanced) {
-        const double cf = ac > 0 ? (double)rc / (double)ac : 1.0;
-        const double mf = am > 0 ? (double)rm / (double)am : 1.0;
-        const int64_t b = (cf >= 1 || mf >= 1) ? 0 : (int64_t)((1.0 - fabs(cf - mf)) * 100);
-        extra += r.w_balanced * b;
-      }
-      raw[i] = s_out;
-      total_out[i] = extra;
-      mask_out[i] = best_m;
-      quality_out[i] = quality;
+      raw[i] = raw_v;
+      total_out[i] = total_v;
+      mask_out[i] = mask_v;
+      quality_out[i] = quality_v;
     }
   }
   // wave-level min/max of the raw score (lanes that scored nothing hold the identities)
@@ -631,7 +694,7 @@ __global__ __launch_bounds__(kBlock) void k_score(yoda_dev_node_t* __restrict__ 
     s_hi[wave] = hi;
   }
   __syncthreads();
-  if (threadIdx.x == 0 && yoda_s) {
+  if (threadIdx.x == 0 && sc.yoda_s) {
     unsigned long long blo = ULLONG_MAX, bhi = 0;
     for (int w = 0; w < kWaves; ++w) {
       blo = s_lo[w] < blo ? s_lo[w] : blo;
@@ -677,6 +740,455 @@ __global__ __launch_bounds__(kBlock) void k_select(int n, const yoda_dev_req_t r
   publish(n, r, key, mask, quality, g, out, nodes);
 }
 
+// ------------------------------------------------------------------ persistent batch kernel
+// k_batch: ONE dispatch schedules a whole batch of pods (filter → maxima → score/gang →
+// normalise/argmax → assume, pod after pod) with the node table resident in LDS.
+//
+//  * block g owns nodes [g*npb, g*npb + npb) for the whole launch; their 512-B rows are read
+//    into LDS once (plus the host's pending dirty rows) and every phase of every pod reads them
+//    from there — no HBM round trip inside the batch. The winner's owner applies the assume to
+//    its LDS row (the same update as `publish`, dev_flags bit 1), so pod b+1 sees pod b's
+//    reservation; dirty rows go back to the table at the end.
+//  * the three cross-workgroup reductions of a pod (maxima + feasible/reason counts, raw
+//    lo/hi, best key) are all-gathers of 8-byte {tag, value} granules: every block stores its
+//    partial record write-through (agent-scope relaxed atomic store = sc1), then one thread
+//    per producer block polls that record until every tag equals the phase's epoch and the
+//    block reduces the G records itself. The data is the flag: no fence, no counter, no
+//    reset (tags grow monotonically across launches). Records are double-buffered by epoch
+//    parity: a block can only overwrite slot e%2 after reading every e+1 record, i.e. after
+//    every block finished reading epoch e.
+//  * the batch's requests are read from mapped host memory, req b+1 prefetched during pod b;
+//    results collect in a device buffer and the last block (agent release/acquire ticket)
+//    copies them to mapped host memory and raises `done` with a system-scope release.
+//  * every spin is bounded (abort word + s_memrealtime deadline): a block that never arrives
+//    makes every waiter give up, the host sees `done` missing and falls back.
+constexpr int kMaxNodesPerBlock = 256;    // 256 × 536 B of LDS per block
+constexpr int kRecStride = 16;            // granules per record slot
+constexpr int kRec1 = 11;                 // maxima[6], feasible, 7 reason counts packed 2 × u16
+constexpr int kRec2 = 4;                  // raw lo, hi (2 granules each)
+constexpr int kRec3 = 2;                  // best key (2 granules)
+constexpr int kMaxGrid = 256;
+// LDS bytes per node: row + raw + total + quality + feas + elig + mask + dirty
+constexpr size_t kBatchRowBytes = sizeof(yoda_dev_node_t) + 8 + 8 + 4 + 4;
+// reason codes the batch path can produce (no candidate reasons: the engine sends no
+// candidates to batches), packed into granules 7..10 of record 1
+__constant__ int c_batch_reasons[7] = {RS_UNSCHEDULABLE, RS_RESOURCES, RS_NO_SCV, RS_STALE, RS_GPU_NUMBER,
+                                       RS_GPU_FIT, RS_DEAD};
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+
+struct BatchArgs {
+  PatchArgs pa;                       // host reservations since the last launch (dirty rows)
+  yoda_dev_node_t* nodes;
+  int n, npb, B, seq;
+  uint32_t tag0;                      // epoch of record 1 of pod 0 (tags: tag0 + 3b + phase)
+  long long deadline_ticks;           // per spin, s_memrealtime ticks (100 MHz)
+  const yoda_dev_req_t* reqs;         // device view of mapped host memory
+  unsigned long long* slots;          // [2][kMaxGrid][kRecStride]
+  yoda_dev_result_t* res;             // device scratch, one per pod
+  yoda_dev_result_t* out;             // device view of mapped host memory
+  int32_t* done;                      // mapped host word: seq when `out` is complete
+  unsigned int* ticket;
+  unsigned int* abort_word;
+  unsigned long long* trace;          // optional: block 0's phase stamps, kTracePts per pod
+};
+constexpr int kTracePts = 16;   // 8 phase stamps + score_node sub-steps (wave 0 of block 0)
+
+__device__ __forceinline__ gu64* slot_ptr(const BatchArgs& a, uint32_t tag, int blk) {
+  return (gu64*)(a.slots + ((size_t)(tag & 1u) * kMaxGrid + blk) * kRecStride);
+}
+
+__device__ __forceinline__ void store_granule(gu64* p, uint32_t tag, uint32_t v) {
+  __hip_atomic_store(p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// true = keep spinning; false = give up (another block aborted, or the deadline passed)
+__device__ __forceinline__ bool spin_ok(const BatchArgs& a, unsigned& spins, long long t0) {
+  __builtin_amdgcn_s_sleep(1);
+  if ((++spins & 63u) != 0) return true;
+  const unsigned ab = __hip_atomic_load((gu32*)a.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (uniform((int)ab)) return false;
+  if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.deadline_ticks) {
+    __hip_atomic_store((gu32*)a.abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+  }
+  return true;
+}
+
+// Thread t < G polls record t of epoch `tag` (K granules) until every tag matches; returns
+// false (block-uniform) when the wait was abandoned.
+template <int K>
+__device__ __forceinline__ bool gather(const BatchArgs& a, uint32_t tag, int G, uint32_t (&v)[K], int* s_fail) {
+  const int t = threadIdx.x;
+  bool failed = false;
+  if (uniform(t & ~63) < G) {   // waves holding at least one producer
+    const gu64* p = slot_ptr(a, tag, t < G ? t : 0);
+    const long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (unsigned spins = 0;;) {
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const unsigned long long x = t < G ? __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                           : ((unsigned long long)tag << 32);
+        v[k] = (uint32_t)x;
+        ok &= (uint32_t)(x >> 32) == tag;
+      }
+      if (__all(ok)) break;
+      if (!spin_ok(a, spins, t0)) {
+        failed = true;
+        break;
+      }
+    }
+  }
+  if (failed && (threadIdx.x & 63) == 0) *s_fail = 1;
+  __syncthreads();
+  return *s_fail == 0;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const T o = __shfl_xor(v, off, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const T o = __shfl_xor(v, off, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+#define TRACE(pt)                                                                      \
+  do {                                                                                 \
+    if (a.trace && g == 0 && tid == 0) a.trace[(size_t)b * kTracePts + (pt)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
+__global__ __launch_bounds__(kBlock) void k_batch(const BatchArgs a) {
+  extern __shared__ __align__(16) unsigned char s_dyn[];
+  __shared__ uint8_t s_masks[256];
+  __shared__ __align__(16) uint32_t s_req[2][sizeof(yoda_dev_req_t) / 4];
+  __shared__ unsigned long long s_part[kWaves][16];
+  __shared__ unsigned long long s_glob[16];
+  __shared__ int s_fail;
+  __shared__ bool s_last;
+  static_assert(sizeof(yoda_dev_req_t) % 4 == 0 && sizeof(yoda_dev_req_t) / 4 <= 64, "req fits one wave");
+  static_assert(sizeof(yoda_dev_result_t) % 8 == 0, "result copied as u64 words");
+  constexpr int kReqWords = sizeof(yoda_dev_req_t) / 4;
+
+  const int npb = a.npb, G = gridDim.x, g = blockIdx.x;
+  const int base = g * npb;
+  const int cnt = a.n - base < npb ? a.n - base : npb;   // ≥ 1: the host sizes G = ceil(n / npb)
+  yoda_dev_node_t* s_rows = reinterpret_cast<yoda_dev_node_t*>(s_dyn);
+  int64_t* s_raw = reinterpret_cast<int64_t*>(s_dyn + (size_t)npb * sizeof(yoda_dev_node_t));
+  int64_t* s_total = s_raw + npb;
+  int32_t* s_quality = reinterpret_cast<int32_t*>(s_total + npb);
+  uint8_t* s_feas = reinterpret_cast<uint8_t*>(s_quality + npb);
+  uint8_t* s_elig = s_feas + npb;
+  uint8_t* s_mask = s_elig + npb;
+  uint8_t* s_dirty = s_mask + npb;
+  const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
+  const int grp = lane >> 3, sub = lane & 7;
+
+  // ---- prologue: rows → LDS (a pending host row replaces the table's), subsets, request 0
+  for (int t = tid; t < cnt * 32; t += kBlock) {
+    const int row = t >> 5, part = t & 31, i = base + row;
+    int pj = -1;
+    for (int j = 0; j < a.pa.n; ++j) pj = a.pa.idx[j] == i ? j : pj;
+    const uint4 v = pj >= 0 ? reinterpret_cast<const uint4*>(&a.pa.rows[pj])[part]
+                            : reinterpret_cast<const uint4*>(a.nodes + i)[part];
+    reinterpret_cast<uint4*>(s_rows + row)[part] = v;
+    if (part == 0) s_dirty[row] = pj >= 0;
+  }
+  // pending rows outside [0, n) belong to no block: block 0 writes them through
+  if (g == 0 && (tid >> 5) < a.pa.n && a.pa.idx[tid >> 5] >= a.n) {
+    const int rec = tid >> 5;
+    reinterpret_cast<uint4*>(a.nodes + a.pa.idx[rec])[tid & 31] = reinterpret_cast<const uint4*>(&a.pa.rows[rec])[tid & 31];
+  }
+  s_masks[tid] = c_subsets.masks[tid];
+  if (tid < kReqWords) s_req[0][tid] = reinterpret_cast<const uint32_t*>(a.reqs)[tid];
+  if (tid == 0) s_fail = 0;
+  __syncthreads();
+
+  bool ok = true;
+  for (int b = 0; b < a.B && ok; ++b) {
+    const yoda_dev_req_t& r = *reinterpret_cast<const yoda_dev_req_t*>(s_req[b & 1]);
+    const uint32_t tag1 = a.tag0 + 3u * (uint32_t)b, tag2 = tag1 + 1u, tag3 = tag1 + 2u;
+    // prefetch request b+1 (lands while this pod's phases run; stored to LDS at the end)
+    uint32_t pre = 0;
+    if (b + 1 < a.B && tid < kReqWords) pre = reinterpret_cast<const uint32_t*>(a.reqs + b + 1)[tid];
+    TRACE(0);
+
+    // ================= phase F: filter + maxima + feasible/reason counts
+    {
+      unsigned long long wmx[6] = {1, 1, 1, 1, 1, 1};
+      int nfeas = 0;
+      int rc[7] = {0, 0, 0, 0, 0, 0, 0};
+      for (int j0 = wave * kNodesPerWave; j0 < cnt; j0 += kWaves * kNodesPerWave) {   // wave-uniform
+        const int j = j0 + grp;
+        const bool valid = j < cnt;
+        uint32_t emask = 0;
+        const int reason = filter_eval(s_rows + (valid ? j : 0), valid, r, 0, wmx, emask, grp, sub);
+        const bool fok = valid && reason == 0;
+        if (valid && sub == 0) {
+          s_feas[j] = fok;
+          s_elig[j] = (uint8_t)emask;
+        }
+        const bool head = sub == 0;
+        nfeas += __popcll(__ballot(head && fok));
+#pragma unroll
+        for (int q = 0; q < 7; ++q) rc[q] += __popcll(__ballot(head && reason == c_batch_reasons[q]));
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) s_part[wave][k] = wmx[k];
+        s_part[wave][6] = (unsigned)nfeas;
+        s_part[wave][7] = (unsigned)rc[0] | ((unsigned)rc[1] << 16);
+        s_part[wave][8] = (unsigned)rc[2] | ((unsigned)rc[3] << 16);
+        s_part[wave][9] = (unsigned)rc[4] | ((unsigned)rc[5] << 16);
+        s_part[wave][10] = (unsigned)rc[6];
+      }
+      __syncthreads();
+      if (tid < kRec1) {
+        unsigned long long v = tid < 6 ? 1 : 0;
+        for (int w = 0; w < kWaves; ++w) v = tid < 6 ? (s_part[w][tid] > v ? s_part[w][tid] : v) : v + s_part[w][tid];
+        store_granule(slot_ptr(a, tag1, g) + tid, tag1, (uint32_t)v);   // ≤ 0xFFFF per u16 half: npb ≤ 256
+      }
+      TRACE(1);
+      uint32_t v[kRec1];
+      if (!gather<kRec1>(a, tag1, G, v, &s_fail)) {
+        ok = false;
+        break;
+      }
+      // block-wide reduction of the G records (threads ≥ G hold identities): 6 maxima, the
+      // feasible count and the 7 reason counts (unpacked: block sums can exceed 16 bits)
+      const bool have = tid < G;
+      unsigned long long red[14];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) red[k] = wave_max<unsigned long long>(have ? v[k] : 1ull);
+      red[6] = wave_sum<unsigned long long>(have ? v[6] : 0ull);
+#pragma unroll
+      for (int q = 0; q < 7; ++q) {
+        const uint32_t w = have ? v[7 + q / 2] : 0u;
+        red[7 + q] = wave_sum<unsigned long long>((q & 1) ? (w >> 16) : (w & 0xFFFFu));
+      }
+      __syncthreads();   // every wave is done reading s_part (phase F partials)
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 14; ++k) s_part[wave][k] = red[k];
+      }
+      __syncthreads();
+      if (tid < 14) {
+        unsigned long long m = tid < 6 ? 1 : 0;
+        for (int w = 0; w < kWaves; ++w) m = tid < 6 ? (s_part[w][tid] > m ? s_part[w][tid] : m) : m + s_part[w][tid];
+        s_glob[tid] = m;
+      }
+      __syncthreads();
+    }
+    int reasons7[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) reasons7[q] = (int)s_glob[7 + q];
+    const int nf = (int)s_glob[6];
+    TRACE(2);
+
+    // ================= phase S: scores + gang search + raw lo/hi
+    const uint64_t gmx[6] = {s_glob[0], s_glob[1], s_glob[2], s_glob[3], s_glob[4], s_glob[5]};
+    const ScoreConsts sc = score_consts(r, gmx);
+    unsigned long long glo = ULLONG_MAX, ghi = 0;
+    {
+      unsigned long long lo = ULLONG_MAX, hi = 0;
+      for (int j0 = wave * kNodesPerWave; j0 < cnt; j0 += kWaves * kNodesPerWave) {
+        const int j = j0 + grp;
+        const bool act = j < cnt && s_feas[j];
+        const uint32_t emask = act ? s_elig[j] : 0u;
+        int64_t raw_v = 0, total_v = 0;
+        uint32_t mask_v = 0;
+        int32_t quality_v = 0;
+        unsigned long long* dbg = (a.trace && g == 0 && tid == 0 && j0 == 0) ? a.trace + (size_t)b * kTracePts + 8 : nullptr;
+        score_node(s_rows + (j < cnt ? j : 0), act, emask, r, sc, s_masks, sub, raw_v, total_v, mask_v, quality_v, lo,
+                   hi, dbg);
+        if (act && sub == 0) {
+          s_raw[j] = raw_v;
+          s_total[j] = total_v;
+          s_mask[j] = (uint8_t)mask_v;
+          s_quality[j] = quality_v;
+        }
+      }
+      lo = wave_min(lo);
+      hi = wave_max(hi);
+      if (lane == 0) {
+        s_part[wave][0] = lo;
+        s_part[wave][1] = hi;
+      }
+      __syncthreads();
+      if (tid < kRec2) {
+        unsigned long long blo = ULLONG_MAX, bhi = 0;
+        for (int w = 0; w < kWaves; ++w) {
+          blo = s_part[w][0] < blo ? s_part[w][0] : blo;
+          bhi = s_part[w][1] > bhi ? s_part[w][1] : bhi;
+        }
+        const unsigned long long x = tid < 2 ? blo : bhi;
+        store_granule(slot_ptr(a, tag2, g) + tid, tag2, (tid & 1) ? (uint32_t)(x >> 32) : (uint32_t)x);
+      }
+      TRACE(3);
+      uint32_t v[kRec2];
+      if (!gather<kRec2>(a, tag2, G, v, &s_fail)) {
+        ok = false;
+        break;
+      }
+      const bool have = tid < G;
+      const unsigned long long mlo = have ? ((unsigned long long)v[1] << 32 | v[0]) : ULLONG_MAX;
+      const unsigned long long mhi = have ? ((unsigned long long)v[3] << 32 | v[2]) : 0ull;
+      const unsigned long long wlo = wave_min(mlo), whi = wave_max(mhi);
+      __syncthreads();
+      if (lane == 0) {
+        s_part[wave][0] = wlo;
+        s_part[wave][1] = whi;
+      }
+      __syncthreads();
+      for (int w = 0; w < kWaves; ++w) {
+        glo = s_part[w][0] < glo ? s_part[w][0] : glo;
+        ghi = s_part[w][1] > ghi ? s_part[w][1] : ghi;
+      }
+      __syncthreads();
+    }
+
+    TRACE(4);
+    // ================= phase Sel: normalise + block argmax → global best key
+    unsigned long long key = 0;
+    {
+      const int64_t hi = (int64_t)ghi;
+      int64_t lo = (int64_t)glo;
+      if (hi == lo) --lo;
+      const uint64_t den = (uint64_t)hi - (uint64_t)lo;
+      unsigned long long best = 0;
+      for (int j = tid; j < cnt; j += kBlock) {
+        if (!s_feas[j]) continue;
+        int64_t f = s_total[j];
+        if (sc.yoda_s) f += (int64_t)udiv(((uint64_t)s_raw[j] - (uint64_t)lo) * 100ull, den) * r.w_yoda;
+        const uint32_t p = ((uint32_t)(base + j) * r.perm_mul + r.perm_add) & 0xFFFFFFu;
+        const unsigned long long k = ((unsigned long long)f << 24) | p;
+        best = k > best ? k : best;
+      }
+      best = wave_max(best);
+      if (lane == 0) s_part[wave][0] = best;
+      __syncthreads();
+      if (tid < kRec3) {
+        unsigned long long bb = 0;
+        for (int w = 0; w < kWaves; ++w) bb = s_part[w][0] > bb ? s_part[w][0] : bb;
+        store_granule(slot_ptr(a, tag3, g) + tid, tag3, tid ? (uint32_t)(bb >> 32) : (uint32_t)bb);
+      }
+      TRACE(5);
+      uint32_t v[kRec3];
+      if (!gather<kRec3>(a, tag3, G, v, &s_fail)) {
+        ok = false;
+        break;
+      }
+      const unsigned long long mk = tid < G ? ((unsigned long long)v[1] << 32 | v[0]) : 0ull;
+      const unsigned long long wk = wave_max(mk);
+      __syncthreads();
+      if (lane == 0) s_part[wave][0] = wk;
+      __syncthreads();
+      for (int w = 0; w < kWaves; ++w) key = s_part[w][0] > key ? s_part[w][0] : key;
+    }
+
+    TRACE(6);
+    // ================= winner: its owner publishes the result and assumes the pod
+    int node = -1;
+    if (nf > 0) {
+      const uint32_t p = (uint32_t)(key & 0xFFFFFFull);
+      node = (int)(((p - r.perm_add) * r.perm_inv) & 0xFFFFFFu);
+    }
+    const bool owner = nf > 0 ? (node >= base && node < base + cnt) : g == 0;
+    if (owner && tid == 0) {
+      yoda_dev_result_t res;
+      res.feasible = nf;
+      res.node = node;
+      if (nf > 0) {
+        const int j = node - base;
+        res.score = nf == 1 ? 0 : (int64_t)(key >> 24);
+        res.mask = s_mask[j];
+        res.quality = s_quality[j];
+        // assume (engine.cpp Engine::reserve, non-compat, reservation pending)
+        yoda_dev_node_t* nd = s_rows + j;
+        const uint32_t mb = (uint32_t)r.memory;
+        for (int c = 0; c < YODA_DEV_CARDS; ++c)
+          if ((res.mask >> c) & 1u) {
+            nd->cards[c].reserved += mb;
+            nd->cards[c].pending += mb;
+          }
+        nd->pod_count += 1;
+        nd->req_cpu += r.cpu_m;
+        nd->req_mem += r.mem;
+        nd->nz_cpu += r.nz_cpu_m;
+        nd->nz_mem += r.nz_mem;
+        s_dirty[j] = 1;
+      } else {
+        res.score = 0;
+        res.mask = 0;
+        res.quality = 0;
+      }
+      for (int k = 0; k < YODA_DEV_REASONS; ++k) res.reasons[k] = 0;
+#pragma unroll
+      for (int q = 0; q < 7; ++q) res.reasons[c_batch_reasons[q]] = reasons7[q];
+      for (int k = 0; k < 6; ++k) res.maxima[k] = gmx[k];
+      res.raw_lo = (int64_t)glo;
+      res.raw_hi = (int64_t)ghi;
+      a.res[b] = res;
+    }
+    if (b + 1 < a.B && tid < kReqWords) s_req[(b + 1) & 1][tid] = pre;
+    __syncthreads();
+    TRACE(7);
+  }
+
+  // ---- epilogue: dirty rows back to the table; the last block hands the results to the host
+  for (int t = tid; t < cnt * 32; t += kBlock) {
+    const int row = t >> 5;
+    if (s_dirty[row]) reinterpret_cast<uint4*>(a.nodes + base + row)[t & 31] = reinterpret_cast<const uint4*>(s_rows + row)[t & 31];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = t == (unsigned)G - 1;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const bool aborted = __hip_atomic_load(a.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  if (!aborted) {
+    const int words = a.B * (int)(sizeof(yoda_dev_result_t) / 8);
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(a.res);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.out);
+    for (int w = tid; w < words; w += kBlock) dst[w] = src[w];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(a.done, aborted ? -a.seq : a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 struct Ctx {
   int device = 0, cap = 0;
   hipStream_t stream = nullptr;
@@ -696,6 +1208,20 @@ struct Ctx {
   int direct_atomics = -1;    // -1: by grid size; 0/1 forced (YODA_DEV_DIRECT_ATOMICS)
   int fuse_max = kFuseSelectMax;   // YODA_DEV_FUSE_MAX overrides (A/B of the fused select)
   PatchArgs pend{};           // dirty rows waiting to ride in the next filter launch
+  // persistent batch kernel (k_batch)
+  bool persist = true;        // YODA_DEV_PERSIST=0: batches run as per-pod launch chains
+  int cus = 256;
+  int npb_min = 32;           // YODA_DEV_NPB: minimum nodes per block (LDS-resident rows)
+  yoda_dev_req_t *h_reqs = nullptr, *d_reqs_map = nullptr;
+  yoda_dev_result_t* d_bres = nullptr;
+  unsigned long long* d_slots = nullptr;
+  unsigned int* d_words = nullptr;     // [0] ticket, [1] abort
+  int32_t *h_done = nullptr, *d_done_map = nullptr;
+  uint32_t epoch = 1;
+  int seq = 0;
+  int last_grid = 0, last_npb = 0;
+  unsigned long long* d_trace = nullptr;   // yoda_dev_batch_trace: block 0's phase stamps
+  int trace_pods = 0;
 };
 
 #define CK(x)                               \
@@ -748,6 +1274,9 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
   if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
   int cus = 256;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess) c->grid = cus * 4;
+  c->cus = cus < kMaxGrid ? cus : kMaxGrid;
+  if (const char* v = getenv("YODA_DEV_PERSIST")) c->persist = v[0] != '0';
+  if (const char* v = getenv("YODA_DEV_NPB")) c->npb_min = atoi(v) > 0 ? atoi(v) : 32;
   if (const char* v = getenv("YODA_DEV_DIRECT_ATOMICS")) c->direct_atomics = v[0] == '1' ? 1 : 0;
   if (const char* v = getenv("YODA_DEV_FUSE_MAX")) c->fuse_max = atoi(v);
   const SubsetTable st = make_subsets();
@@ -781,6 +1310,23 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
     return fail("batch results", e);
   if ((e = hipHostGetDevicePointer((void**)&c->d_resb, c->h_resb, 0)) != hipSuccess) return fail("batch map", e);
   if ((e = hipMalloc(&c->d_g, sizeof(Globals))) != hipSuccess) return fail("globals", e);
+  // persistent batch kernel state
+  if ((e = hipHostMalloc(&c->h_reqs, kBatchCap * sizeof(yoda_dev_req_t), hipHostMallocMapped | hipHostMallocCoherent)) !=
+      hipSuccess)
+    return fail("batch requests", e);
+  if ((e = hipHostGetDevicePointer((void**)&c->d_reqs_map, c->h_reqs, 0)) != hipSuccess) return fail("requests map", e);
+  if ((e = hipHostMalloc(&c->h_done, 64, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+    return fail("batch done", e);
+  if ((e = hipHostGetDevicePointer((void**)&c->d_done_map, c->h_done, 0)) != hipSuccess) return fail("done map", e);
+  if ((e = hipMalloc(&c->d_bres, kBatchCap * sizeof(yoda_dev_result_t))) != hipSuccess) return fail("batch scratch", e);
+  const size_t slot_bytes = 2 * kMaxGrid * kRecStride * sizeof(unsigned long long);
+  if ((e = hipMalloc(&c->d_slots, slot_bytes)) != hipSuccess) return fail("slots", e);
+  if ((e = hipMemset(c->d_slots, 0, slot_bytes)) != hipSuccess) return fail("slots", e);
+  if ((e = hipMalloc(&c->d_words, 64)) != hipSuccess) return fail("words", e);
+  if ((e = hipMemset(c->d_words, 0, 64)) != hipSuccess) return fail("words", e);
+  if ((e = hipFuncSetAttribute((const void*)k_batch, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(kMaxNodesPerBlock * kBatchRowBytes))) != hipSuccess)
+    return fail("k_batch LDS", e);
   Globals init;
   globals_reset(&init);
   if ((e = hipMemcpy(c->d_g, &init, sizeof(Globals), hipMemcpyHostToDevice)) != hipSuccess) return fail("init", e);
@@ -795,6 +1341,7 @@ void yoda_dev_destroy(void* p) {
   hipFree(c->d_nodes); hipFree(c->d_stage); hipHostFree(c->h_stage); hipFree(c->d_idx); hipHostFree(c->h_idx);
   hipFree(c->d_feas); hipFree(c->d_elig); hipFree(c->d_cand); hipHostFree(c->h_cand); hipFree(c->d_raw);
   hipFree(c->d_total); hipFree(c->d_mask); hipFree(c->d_quality); hipHostFree(c->h_res); hipHostFree(c->h_resb); hipFree(c->d_g);
+  hipHostFree(c->h_reqs); hipHostFree(c->h_done); hipFree(c->d_bres); hipFree(c->d_slots); hipFree(c->d_words);
   hipEventDestroy(c->e0); hipEventDestroy(c->e1);
   hipStreamDestroy(c->stream);
   delete c;
@@ -913,6 +1460,81 @@ int yoda_dev_schedule(void* p, int n, const yoda_dev_req_t* req, const uint8_t* 
   return 0;
 }
 
+// Persistent path: one k_batch dispatch per chunk of ≤ kBatchCap pods. Returns 1 when the
+// cluster does not fit the LDS-resident layout (the caller then uses the launch chain).
+static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yoda_dev_result_t* out) {
+  int npb = (n + c->cus - 1) / c->cus;
+  npb = npb < c->npb_min ? c->npb_min : npb;
+  if (npb > kMaxNodesPerBlock) return 1;
+  const int G = (n + npb - 1) / npb;
+  if (G > kMaxGrid) return 1;
+  const size_t lds = (size_t)npb * kBatchRowBytes;
+  c->last_grid = G;
+  c->last_npb = npb;
+  for (int base = 0; base < B; base += kBatchCap) {
+    const int m = B - base < kBatchCap ? B - base : kBatchCap;
+    for (int j = 0; j < m; ++j)
+      if (reqs[base + j].use_candidates) return -3;
+    memcpy(c->h_reqs, reqs + base, (size_t)m * sizeof(yoda_dev_req_t));
+    if (c->epoch > 0xF0000000u) {   // tag space exhausted: forget every old tag
+      CK(hipMemsetAsync(c->d_slots, 0, 2 * kMaxGrid * kRecStride * sizeof(unsigned long long), c->stream));
+      c->epoch = 1;
+    }
+    BatchArgs a;
+    a.pa = c->pend;
+    a.nodes = c->d_nodes;
+    a.n = n;
+    a.npb = npb;
+    a.B = m;
+    c->seq = c->seq >= (1 << 30) ? 1 : c->seq + 1;
+    a.seq = c->seq;
+    a.tag0 = c->epoch;
+    c->epoch += 3u * (uint32_t)m + 3u;
+    a.deadline_ticks = 200000000ll;   // 2 s per wait at 100 MHz
+    a.reqs = c->d_reqs_map;
+    a.slots = c->d_slots;
+    a.res = c->d_bres;
+    a.out = c->d_resb;
+    a.done = c->d_done_map;
+    a.ticket = c->d_words;
+    a.abort_word = c->d_words + 1;
+    a.trace = c->d_trace;
+    __atomic_store_n(c->h_done, 0, __ATOMIC_RELEASE);
+    hipLaunchKernelGGL(k_batch, dim3(G), dim3(kBlock), lds, c->stream, a);
+    c->pend.n = 0;
+    CK(hipGetLastError());
+    // wait for `done` (system-scope release by the last block), polling the stream now and
+    // then so a failed launch cannot hang the scheduler. A batch runs for milliseconds: spin
+    // for the first ~100 µs (short batches), then poll every ~20 µs instead of burning a core.
+    const auto t0 = std::chrono::steady_clock::now();
+    int d = 0;
+    for (unsigned spin = 1;; ++spin) {
+      d = __atomic_load_n(c->h_done, __ATOMIC_ACQUIRE);
+      if (d != 0) break;
+      if (spin > 2048) std::this_thread::sleep_for(std::chrono::microseconds(20));
+      if ((spin & 255) == 0) {
+        const hipError_t q = hipStreamQuery(c->stream);
+        if (q == hipSuccess) {
+          d = __atomic_load_n(c->h_done, __ATOMIC_ACQUIRE);
+          break;
+        }
+        if (q != hipErrorNotReady) return (int)q;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) return -5;
+      }
+      __builtin_ia32_pause();
+    }
+    if (d != c->seq) {   // aborted (a spin gave up) or no result: re-arm and report
+      CK(hipStreamSynchronize(c->stream));
+      CK(hipMemsetAsync(c->d_words, 0, 64, c->stream));
+      CK(hipStreamSynchronize(c->stream));
+      return -7;
+    }
+    memcpy(out + base, c->h_resb, (size_t)m * sizeof(yoda_dev_result_t));
+    c->trace_pods = m;
+  }
+  return 0;
+}
+
 // B consecutive cycles enqueued back to back: each cycle's winner is assumed on the
 // device (its node row updated in place by the publishing block), so cycle b+1 sees cycle
 // b's reservation exactly as sequential host cycles would — no host round trip between
@@ -921,6 +1543,10 @@ int yoda_dev_schedule_batch(void* p, int n, int B, const yoda_dev_req_t* reqs, y
   Ctx* c = (Ctx*)p;
   if (n <= 0 || n > c->cap || B < 0) return -1;
   CK(hipSetDevice(c->device));
+  if (c->persist && B > 0) {
+    const int rc = batch_persistent(c, n, B, reqs, out);
+    if (rc <= 0) return rc;
+  }
   for (int base = 0; base < B; base += kBatchCap) {
     const int m = B - base < kBatchCap ? B - base : kBatchCap;
     for (int j = 0; j < m; ++j) {
@@ -936,8 +1562,31 @@ int yoda_dev_schedule_batch(void* p, int n, int B, const yoda_dev_req_t* reqs, y
     for (int j = 0; j < m; ++j)
       if (__atomic_load_n(&c->h_resb[j].feasible, __ATOMIC_ACQUIRE) < 0) return -4;
     memcpy(out + base, c->h_resb, (size_t)m * sizeof(yoda_dev_result_t));
+    c->trace_pods = m;
   }
   return 0;
+}
+
+// Phase trace of the persistent kernel (benchmarks): on = 1 records, per pod of the last
+// k_batch chunk, block 0's s_memrealtime stamps (100 MHz) at kTracePts phase boundaries:
+// start, F computed, F gathered, S computed, S gathered, Sel computed, Sel gathered, end.
+// Returns the number of pods copied to `out` (kTracePts words each), or the grid/npb of the
+// last launch when out is NULL (grid << 16 | npb).
+int yoda_dev_batch_trace(void* p, int on, unsigned long long* out, int max_pods) {
+  Ctx* c = (Ctx*)p;
+  if (!c) return -1;
+  CK(hipSetDevice(c->device));
+  if (on && !c->d_trace) CK(hipMalloc(&c->d_trace, (size_t)kBatchCap * kTracePts * 8));
+  if (!on && c->d_trace) {
+    CK(hipFree(c->d_trace));
+    c->d_trace = nullptr;
+  }
+  if (!out) return (c->last_grid << 16) | c->last_npb;
+  if (!c->d_trace) return 0;
+  const int m = c->trace_pods < max_pods ? c->trace_pods : max_pods;
+  CK(hipStreamSynchronize(c->stream));
+  if (m > 0) CK(hipMemcpy(out, c->d_trace, (size_t)m * kTracePts * 8, hipMemcpyDeviceToHost));
+  return m;
 }
 
 void yoda_dev_set_timing(void* p, int on) {

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Engine-level throughput of a burst on a large synthetic cluster: per-pod device cycles
-(one host round trip each) vs batched device cycles (yoda_dev_schedule_batch: cycles
-enqueued back to back, winners assumed on the device). One JSON line per (nodes, mode)."""
+(one host round trip each) vs batched device cycles (yoda_dev_schedule_batch) as per-pod launch
+chains enqueued back to back (``batch-chain``) or as ONE persistent k_batch dispatch per batch
+(``batch``, node rows resident in LDS). One JSON line per (nodes, mode)."""
 from __future__ import annotations
 
 import argparse
@@ -14,13 +15,16 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(nodes: int, mode: str, pods: int, batch: int) -> dict:
+def run(nodes: int, mode: str, pods: int, batch: int, trace: bool = False, busy: float = 0.3) -> dict:
     from yoda_scheduler_amd.ops import device_scorer as ds
     from yoda_scheduler_amd.ops.native import core, pod_req
     eng = core().Engine(False, 1)
     eng.set_percentage_of_nodes_to_score(100)
-    ds.synthetic_cluster(eng, nodes, seed=nodes, busy=0.3)
+    ds.synthetic_cluster(eng, nodes, seed=nodes, busy=busy)
+    # batch-chain: per-pod launch chains enqueued back to back; batch: the persistent k_batch
+    os.environ["YODA_DEV_PERSIST"] = "0" if mode == "batch-chain" else "1"
     ds.enable(eng, 0, capacity=nodes + 16, min_nodes=1)
+    os.environ.pop("YODA_DEV_PERSIST", None)
     rng = random.Random(1)
     reqs = []
     for k in range(pods):
@@ -29,7 +33,7 @@ def run(nodes: int, mode: str, pods: int, batch: int) -> dict:
     # warm up (kernels, first full-table upload)
     eng.schedule_batch([p for p, _ in reqs[:8]], [r for _, r in reqs[:8]])
     t0 = time.perf_counter()
-    if mode == "batch":
+    if mode.startswith("batch"):
         for i in range(8, pods, batch):
             chunk = reqs[i:i + batch]
             eng.schedule_batch([p for p, _ in chunk], [r for _, r in chunk])
@@ -38,7 +42,19 @@ def run(nodes: int, mode: str, pods: int, batch: int) -> dict:
             eng.schedule(p, r, True)
     dt = time.perf_counter() - t0
     n = pods - 8
-    return {"nodes": nodes, "mode": mode, "pods": n, "batch": batch if mode == "batch" else 1,
+    extra = {}
+    if mode == "batch":
+        grid, npb = ds.batch_geometry(eng)
+        extra["grid"], extra["nodes_per_block"] = grid, npb
+        if trace:
+            ds.batch_trace(eng, True)
+            chunk = reqs[8:8 + batch]
+            eng.schedule_batch([p for p, _ in chunk], [r for _, r in chunk])
+            tr = ds.read_batch_trace(eng)
+            if tr:
+                extra["phase_us_mean"] = {k: round(sum(x[k] for x in tr) / len(tr), 2) for k in tr[0]}
+            ds.batch_trace(eng, False)
+    return {**extra, "nodes": nodes, "mode": mode, "pods": n, "batch": batch if mode.startswith("batch") else 1,
             "us_per_pod": round(dt / n * 1e6, 1), "pods_per_s": round(n / dt, 1),
             "device_cycles": eng.device_cycles, "fallbacks": eng.device_fallbacks}
 
@@ -48,11 +64,14 @@ def main() -> int:
     ap.add_argument("--nodes", default="1024,4096,16384")
     ap.add_argument("--pods", type=int, default=520)
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--modes", default="per-pod,batch-chain,batch")
+    ap.add_argument("--trace", action="store_true", help="k_batch phase breakdown (block 0 stamps)")
+    ap.add_argument("--busy", type=float, default=0.3, help="synthetic cluster load (0: every node fits)")
     a = ap.parse_args()
     import torch  # noqa: F401 - load torch's HIP runtime first (same SONAME as ours)
     for n in (int(x) for x in a.nodes.split(",")):
-        for mode in ("per-pod", "batch"):
-            print(json.dumps(run(n, mode, a.pods, a.batch)), flush=True)
+        for mode in a.modes.split(","):
+            print(json.dumps(run(n, mode, a.pods, a.batch, a.trace, a.busy)), flush=True)
     return 0
 
 

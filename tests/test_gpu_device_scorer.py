@@ -147,3 +147,46 @@ def test_device_batch_equals_sequential_device_cycles(require_gpu, n):
         pi, req = ds.random_request(a, rng2, f"after-{n}-{k}")
         assert not ds.compare_cycle(a, req)
         a.schedule(pi.num_id, req, True)
+
+
+def _persist_engine(n, seed, persist):
+    import os
+    os.environ["YODA_DEV_PERSIST"] = "1" if persist else "0"
+    try:
+        eng = _engine(n, seed)
+    finally:
+        os.environ.pop("YODA_DEV_PERSIST", None)
+    eng.seed(7)
+    return eng
+
+
+@pytest.mark.parametrize("n,pods", [(257, 40), (4100, 300), (16411, 120)])
+def test_persistent_batch_kernel_matches_launch_chain(require_gpu, n, pods):
+    """k_batch (one dispatch per batch, node rows resident in LDS, all-gather reductions)
+    returns exactly what the per-pod launch chain returns — nodes, GPU sets, scores, reasons,
+    gang quality — including >256-pod batches (two dispatches), node counts that leave the
+    last block partial, and pods no node fits; afterwards both device tables match the host."""
+    from yoda_scheduler_amd.ops import device_scorer as ds
+    from yoda_scheduler_amd.ops.native import pod_req
+    a, b = _persist_engine(n, 31, True), _persist_engine(n, 31, False)
+    rng = random.Random(n)
+    pods_ = [ds.random_request(a, rng, f"pk-{n}-{k}")[0] for k in range(pods)]
+    # a few pods that fit nowhere (nf = 0: block 0 publishes) and one 8-GPU gang
+    from yoda_scheduler_amd.models.pod import PodInfo
+    for k, lab in enumerate([{"scv/memory": "900000"}, {"scv/number": "9"}, {"scv/number": "8", "scv/memory": "1024"}]):
+        pods_.insert(5 + 7 * k, PodInfo.from_obj({"metadata": {"name": f"x{k}", "uid": f"pk-x-{n}-{k}", "labels": lab},
+                                                  "spec": {}}))
+    res_a = a.schedule_batch([p.num_id for p in pods_], [pod_req(a, p) for p in pods_])
+    res_b = b.schedule_batch([p.num_id for p in pods_], [pod_req(b, p) for p in pods_])
+    key = lambda r: (r[0], r[1], list(r[3]), r[4], list(r[5]), r[6])
+    assert [key(r) for r in res_a] == [key(r) for r in res_b]
+    assert any(r[0] < 0 for r in res_a) and sum(1 for r in res_a if r[0] >= 0) > pods // 2
+    assert a.device_fallbacks == 0 and b.device_fallbacks == 0
+    for i in range(0, n, max(1, n // 97)):
+        assert a.node_cards(i) == b.node_cards(i)
+    # the device table left by k_batch is the host's: per-pod device cycles still match the CPU
+    rng2 = random.Random(n + 1)
+    for k in range(8):
+        pi, req = ds.random_request(a, rng2, f"pk-after-{n}-{k}")
+        assert not ds.compare_cycle(a, req)
+        a.schedule(pi.num_id, req, True)

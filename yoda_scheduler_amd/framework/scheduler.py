@@ -139,6 +139,7 @@ class Scheduler:
         self._bind_idle: collections.deque = collections.deque()
         self._tasks: list[asyncio.Task] = []
         self._engine_exec = None          # worker thread of schedule_batch_overlapped
+        self._inflight: Optional[tuple] = None   # (fw, run, cycle, t0, future) on that worker
         self.informers: dict[str, Informer] = {}
         self.scheduled = 0
         self.failed = 0
@@ -653,14 +654,19 @@ class Scheduler:
                                 self.engine.live_nodes >= self.config.device_min_nodes)
 
     async def schedule_batch_overlapped(self, pods: list[PodInfo]) -> None:
-        """``schedule_batch`` with each native run on the engine worker thread: while the
-        engine (and, with the device scorer, the GPU) places this batch, the event loop
-        keeps binding the previous one and ingesting informer events. The engine's
-        process-wide lock (native/core/bindings.cpp) serialises any engine call the loop
-        makes meanwhile; the batch's own results are applied after the await, in order."""
+        """``schedule_batch`` as a two-stage pipeline: each native run goes to the engine
+        worker thread, and the run dispatched before it is finished (assumed into the cache,
+        binds enqueued) while the engine — with the device scorer, the GPU — places this one.
+        The event loop meanwhile keeps binding and ingesting informer events. The engine
+        already reserved every returned placement in its own ledger, so the next run can be
+        placed before Python has applied the previous run's results; those are applied in
+        order. The engine's process-wide lock (native/core/bindings.cpp) serialises any
+        engine call the loop makes meanwhile. The last dispatched run stays in flight until
+        the next batch arrives or the queue runs dry (``finish_inflight``)."""
         loop = asyncio.get_event_loop()
         for fw, item in self._batch_runs(pods):
             if fw is None:
+                await self.finish_inflight()
                 self.schedule_one(item)
                 continue
             cycle, t0, ids, reqs = self._prepare_run(fw, item)
@@ -672,8 +678,21 @@ class Scheduler:
                 # default 5 ms switch interval it waits that long behind the busy event loop
                 # (measured: +7 µs per pod on MI355X config 6), so ask for 0.2 ms
                 sys.setswitchinterval(min(sys.getswitchinterval(), ENGINE_SWITCH_INTERVAL_S))
-            results = await loop.run_in_executor(self._engine_exec, self.engine.schedule_batch, ids, reqs)
-            self._finish_run(fw, item, results, cycle, t0)
+            fut = loop.run_in_executor(self._engine_exec, self.engine.schedule_batch, ids, reqs)
+            prev, self._inflight = self._inflight, (fw, item, cycle, t0, fut)
+            if prev is not None:
+                await self._finish_inflight_run(prev)
+
+    async def _finish_inflight_run(self, run: tuple) -> None:
+        fw, item, cycle, t0, fut = run
+        results = await fut
+        self._finish_run(fw, item, results, cycle, t0)
+
+    async def finish_inflight(self) -> None:
+        """Apply the results of the run still on the engine worker (if any)."""
+        run, self._inflight = self._inflight, None
+        if run is not None:
+            await self._finish_inflight_run(run)
 
     # ================================================================== binding
     def _native_direct(self, fw: Framework, pi: PodInfo) -> bool:
@@ -824,12 +843,17 @@ class Scheduler:
         q = self.queue
         bs = max(1, self.config.batch_size)
         while not self._stop.is_set():
+            if self._inflight is not None and not q._active_entries:
+                await self.finish_inflight()      # nothing to overlap with: apply it now
+                continue
             pi = await q.pop()
             if pi is None:
                 if q.closed:
+                    await self.finish_inflight()
                     return
                 continue
             if self.extenders:
+                await self.finish_inflight()
                 await self.schedule_one_async(pi)
             elif self.batching and q._active_entries:
                 batch = [pi] + q.pop_batch(bs - 1)
@@ -839,8 +863,10 @@ class Scheduler:
                     # binds / informer events of this one run during its await
                     continue
                 else:
+                    await self.finish_inflight()
                     self.schedule_batch(batch)
             else:
+                await self.finish_inflight()
                 self.schedule_one(pi)
             # let informers / binders run between cycles
             await asyncio.sleep(0)

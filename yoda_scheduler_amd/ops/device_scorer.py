@@ -18,6 +18,48 @@ from .hip import PATH, lib as hip_lib
 def declare(lib: ctypes.CDLL) -> None:
     lib.yoda_dev_last_us.argtypes = [ctypes.c_void_p]
     lib.yoda_dev_last_us.restype = ctypes.c_float
+    lib.yoda_dev_batch_trace.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    lib.yoda_dev_batch_trace.restype = ctypes.c_int
+
+
+TRACE_PHASES = ("filter", "gather1", "score", "gather2", "select", "gather3", "publish")
+
+
+def batch_trace(engine, on: bool = True) -> None:
+    """Record block 0's phase stamps in every persistent k_batch launch (benchmarks only)."""
+    lib = hip_lib()
+    declare(lib)
+    if lib.yoda_dev_batch_trace(engine.device_ctx, 1 if on else 0, None, 0) < 0:
+        raise RuntimeError("yoda_dev_batch_trace failed")
+
+
+def batch_geometry(engine) -> tuple[int, int]:
+    """(grid, nodes per block) of the last k_batch launch; (0, 0) if none ran."""
+    lib = hip_lib()
+    declare(lib)
+    v = lib.yoda_dev_batch_trace(engine.device_ctx, 1, None, 0)
+    return v >> 16, v & 0xFFFF
+
+
+def read_batch_trace(engine, max_pods: int = 256) -> list[dict]:
+    """Per pod of the last k_batch chunk: µs spent in each phase (block 0's view)."""
+    lib = hip_lib()
+    declare(lib)
+    W = 16
+    buf = (ctypes.c_ulonglong * (max_pods * W))()
+    m = lib.yoda_dev_batch_trace(engine.device_ctx, 1, buf, max_pods)
+    out = []
+    for b in range(max(m, 0)):
+        t = [buf[b * W + k] for k in range(W)]
+        d = {ph: (t[k + 1] - t[k]) / 100.0 for k, ph in enumerate(TRACE_PHASES)}
+        # score_node sub-steps of wave 0 (tables loaded → gang → raw score → defaults)
+        sub = [t[2], t[8], t[9], t[10], t[11]]
+        if all(sub):
+            for k, ph in enumerate(("s.tables", "s.gang", "s.raw", "s.defaults")):
+                d[ph] = (sub[k + 1] - sub[k]) / 100.0
+            d["s.reduce"] = (t[3] - t[11]) / 100.0
+        out.append(d)
+    return out
 
 
 def enable(engine, device: int = 0, capacity: int = 65536, min_nodes: int = 256) -> None:
