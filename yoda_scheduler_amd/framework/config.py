@@ -124,6 +124,15 @@ class SchedulerConfig:
     # ingests the previous batch meanwhile; auto = when the gfx950 device scorer is active
     # (config 6 on MI355X: +45-50 % pods/s, profiles/bench/README.md)
     overlap_engine: str = "auto"
+    # native runs in flight on the engine worker at once (overlapped mode): 2 = one placing
+    # while the previous is applied; 3 keeps one more queued so the engine (GPU) never idles
+    # while the event loop catches up with binds and watch events
+    overlap_depth: int = 3
+    # Scv updates requeue parked pods only when the new sample can add capacity (a card
+    # healthy again, more effective free HBM, a changed clock, more cards, stale → fresh);
+    # False: every Scv event moves the whole unschedulable queue (upstream's behaviour for
+    # any cluster event)
+    scv_queueing_hint: bool = True
     # event API (yodaRuntime.eventsAPI): upstream v1.20 records through events.k8s.io/v1
     events_api: str = "events.k8s.io/v1"
     trace: bool = False
@@ -279,6 +288,10 @@ def parse_config(doc: dict) -> SchedulerConfig:
     cfg.overlap_engine = {True: "on", False: "off"}.get(ov, str(ov).lower()) if isinstance(ov, bool) else str(ov).lower()
     if cfg.overlap_engine not in ("auto", "on", "off"):
         raise ValueError("yodaRuntime.overlapEngine must be auto|on|off")
+    cfg.overlap_depth = int(_f(rt, "overlapDepth", cfg.overlap_depth))
+    cfg.scv_queueing_hint = bool(_f(rt, "scvQueueingHint", cfg.scv_queueing_hint))
+    if not 2 <= cfg.overlap_depth <= 16:
+        raise ValueError("yodaRuntime.overlapDepth must be in [2, 16]")
     cfg.trace = bool(_f(rt, "trace", False))
     for e in doc.get("extenders") or []:
         if not e.get("urlPrefix"):

@@ -11,6 +11,7 @@
 from __future__ import annotations
 
 import asyncio
+import collections
 import heapq
 import itertools
 import time
@@ -38,6 +39,11 @@ class SchedulingQueue:
         self._cond: Optional[asyncio.Event] = None
         self.scheduling_cycle = 0
         self._move_request_cycle = -1
+        # hinted moves (cycle, predicate), newest last: a pod that fails a cycle started
+        # before one of them retries from backoff only if that predicate accepts it
+        # (upstream's in-flight events + QueueingHint); older entries are dropped
+        self._hint_moves: collections.deque = collections.deque()
+        self._hint_dropped_cycle = -1
         self.closed = False
         # (event, queue, n) → scheduler_queue_incoming_pods_total; None = not counted
         self.incoming_hook: Optional[Callable[[str, str, int], None]] = None
@@ -167,7 +173,7 @@ class SchedulingQueue:
             return
         self._pods[pi.uid] = pi
         pi.enqueued = self.clock()          # backoff counts from the failed attempt
-        if not unschedulable or self._move_request_cycle >= cycle:
+        if not unschedulable or self._move_request_cycle >= cycle or self._hinted_since(pi, cycle):
             self._to_backoff(pi)
             where = "backoff"
         else:
@@ -216,11 +222,45 @@ class SchedulingQueue:
         schedulable."""
         pods = [pi for pi, _ in self._unsched.values()]
         self._unsched.clear()
+        return self._move(pods, event)
+
+    def move_matching_to_active_or_backoff(self, pred, event: str = "") -> int:
+        """Queueing hint: move only the parked pods for which ``pred(pod)`` says the event
+        could make them schedulable. The move request is recorded either way, so a pod in
+        flight when the event arrived retries from backoff instead of parking."""
+        pods = [pi for pi, _ in self._unsched.values() if pred(pi)]
+        for pi in pods:
+            del self._unsched[pi.uid]
+        if self._hint_moves and self._hint_moves[-1][0] == self.scheduling_cycle:
+            c, prev = self._hint_moves.pop()          # same cycle: one entry accepting either
+            self._hint_moves.append((c, lambda pi, a=prev, b=pred: a(pi) or b(pi)))
+        else:
+            self._hint_moves.append((self.scheduling_cycle, pred))
+        while len(self._hint_moves) > self.HINT_HISTORY:
+            self._hint_dropped_cycle = self._hint_moves.popleft()[0]
+        return self._move(pods, event, record=False)
+
+    HINT_HISTORY = 256
+
+    def _hinted_since(self, pi: PodInfo, cycle: int) -> bool:
+        """Did a hinted move accept ``pi`` at or after ``cycle`` (its scheduling attempt)?
+        Conservatively yes when entries that old were already dropped."""
+        if self._hint_dropped_cycle >= cycle:
+            return True
+        for c, pred in reversed(self._hint_moves):
+            if c < cycle:
+                break
+            if pred(pi):
+                return True
+        return False
+
+    def _move(self, pods: list, event: str, record: bool = True) -> int:
         active = 0
         for pi in pods:
             self._pods.pop(pi.uid, None)
             active += self._route(pi)
-        self._move_request_cycle = self.scheduling_cycle
+        if record:
+            self._move_request_cycle = self.scheduling_cycle
         if pods and self.incoming_hook is not None:
             if active:
                 self.incoming_hook(event, "active", active)

@@ -139,10 +139,12 @@ class Scheduler:
         self._bind_idle: collections.deque = collections.deque()
         self._tasks: list[asyncio.Task] = []
         self._engine_exec = None          # worker thread of schedule_batch_overlapped
-        self._inflight: Optional[tuple] = None   # (fw, run, cycle, t0, future) on that worker
+        self._inflight: collections.deque = collections.deque()   # (fw, run, cycle, t0, future) on that worker
         self.informers: dict[str, Informer] = {}
         self.scheduled = 0
         self.failed = 0
+        self.scv_requeues = 0          # Scv updates that moved the parked pods back
+        self.scv_requeue_skips = 0     # Scv updates the queueing hint kept from doing so
         self.bind_errors = 0
         self._stop = asyncio.Event()
         self.leading = asyncio.Event()
@@ -317,10 +319,80 @@ class Scheduler:
 
     def on_scv(self, obj: dict) -> None:
         self.cache.add_scv(obj)
-        self.queue.move_all_to_active_or_backoff("ScvUpdate")
+        self.queue.move_all_to_active_or_backoff("ScvAdd")
+
+    def _capacity(self, name: str) -> Optional[tuple]:
+        """What the yoda filter can see of a node's GPUs, from the engine after pending
+        reservations are settled: (stale, CardNumber, per card (healthy, free, effective
+        free, clock)); None for a node the engine does not know."""
+        rows = self.cache.node_gpu_state(name)
+        if not rows and self.engine.node_index(name) < 0:
+            return None
+        scv = self.cache.scvs.get(name)
+        cards = tuple((g["healthy"], g["free"], max(0, min(g["free"] - g["pending"], g["total"] - g["reserved"])),
+                       g["clock"]) for g in rows)
+        return bool(self.cache._stale.get(name)), (scv.status.card_number if scv else 0), cards
+
+    @staticmethod
+    def _capacity_grew(b: tuple, a: tuple) -> bool:
+        """Can a pod that failed the yoda filter against ``b`` pass against ``a``? The
+        filter is monotone in health, free / effective-free HBM, card count and freshness,
+        and matches the clock exactly, so: anything up, or any clock different."""
+        if (b[0] and not a[0]) or a[1] > b[1] or len(a[2]) > len(b[2]):
+            return True
+        for (hb, fb, eb, cb), (ha, fa, ea, ca) in zip(b[2], a[2]):
+            if (ha and not hb) or fa > fb or ea > eb or ca != cb:
+                return True
+        return False
 
     def on_scv_update(self, old: dict, new: dict) -> None:
-        self.on_scv(new)
+        """Queueing hint for Scv updates (upstream v1.22+ QueueingHint, applied to the
+        telemetry CRD): the update is applied to the cache, and parked pods are moved back
+        only when the node's filter-visible capacity grew. A steady stream of telemetry that
+        only records load then costs one cache update per event, not a retry of every
+        parked pod (``scv_requeues`` / ``scv_requeue_skips`` count both outcomes)."""
+        if not self.config.scv_queueing_hint:
+            self.cache.add_scv(new)
+            self.queue.move_all_to_active_or_backoff("ScvUpdate")
+            self.scv_requeues += 1
+            return
+        name = (new.get("metadata") or {}).get("name", "")
+        before = self._capacity(name)
+        self.cache.add_scv(new)
+        after = self._capacity(name)
+        if before is None or after is None:
+            self.queue.move_all_to_active_or_backoff("ScvUpdate")
+            self.scv_requeues += 1
+        elif self._capacity_grew(before, after):
+            # per pod (upstream QueueingHint): only pods whose GPU request the node's new
+            # capacity satisfies can now pass the yoda filter there; other filters do not
+            # read Scv, so a pod they rejected on this node stays rejected
+            compat = self.cache.compat
+            self.queue.move_matching_to_active_or_backoff(lambda pi: self._gpu_fits(pi, after, compat), "ScvUpdate")
+            self.scv_requeues += 1
+        else:
+            self.scv_requeue_skips += 1
+
+    @staticmethod
+    def _gpu_fits(pi: PodInfo, cap: tuple, compat: bool) -> bool:
+        """Would ``pi`` pass the yoda filter (filter.go PodFitsNumber / PodFitsMemory /
+        PodFitsClock, plus the MI355X freshness and clock-floor rules) on a node with
+        capacity ``cap`` (see ``_capacity``)?"""
+        stale, card_number, cards = cap
+        g = pi.gpu
+        if stale and not compat:
+            return False
+        if g.has_number:
+            if g.number > card_number:
+                return False
+        elif card_number <= 0:
+            return False
+        fit = 0
+        for h, free, eff, clock in cards:
+            if h and (free if compat else eff) >= g.memory and (not g.has_clock or clock == g.clock) \
+                    and clock >= g.clock_min:
+                fit += 1
+        return fit >= g.number
 
     def on_scv_delete(self, obj: dict) -> None:
         self.cache.remove_scv(obj["metadata"]["name"])
@@ -654,16 +726,19 @@ class Scheduler:
                                 self.engine.live_nodes >= self.config.device_min_nodes)
 
     async def schedule_batch_overlapped(self, pods: list[PodInfo]) -> None:
-        """``schedule_batch`` as a two-stage pipeline: each native run goes to the engine
-        worker thread, and the run dispatched before it is finished (assumed into the cache,
-        binds enqueued) while the engine — with the device scorer, the GPU — places this one.
-        The event loop meanwhile keeps binding and ingesting informer events. The engine
-        already reserved every returned placement in its own ledger, so the next run can be
-        placed before Python has applied the previous run's results; those are applied in
-        order. The engine's process-wide lock (native/core/bindings.cpp) serialises any
-        engine call the loop makes meanwhile. The last dispatched run stays in flight until
-        the next batch arrives or the queue runs dry (``finish_inflight``)."""
+        """``schedule_batch`` as a pipeline: each native run goes to the engine worker
+        thread, and older runs are finished (assumed into the cache, binds enqueued) while
+        the engine — with the device scorer, the GPU — places the newer ones. Up to
+        ``yodaRuntime.overlapDepth`` runs are in flight, so the engine keeps a run queued
+        while the event loop catches up with binds and watch events. The event loop
+        meanwhile keeps binding and ingesting informer events. The engine already reserved
+        every returned placement in its own ledger, so a run can be placed before Python has
+        applied the previous runs' results; those are applied in order. The engine's
+        process-wide lock (native/core/bindings.cpp) serialises any engine call the loop
+        makes meanwhile. Runs left in flight are finished when the queue runs dry
+        (``finish_inflight``)."""
         loop = asyncio.get_event_loop()
+        depth = self.config.overlap_depth
         for fw, item in self._batch_runs(pods):
             if fw is None:
                 await self.finish_inflight()
@@ -679,9 +754,9 @@ class Scheduler:
                 # (measured: +7 µs per pod on MI355X config 6), so ask for 0.2 ms
                 sys.setswitchinterval(min(sys.getswitchinterval(), ENGINE_SWITCH_INTERVAL_S))
             fut = loop.run_in_executor(self._engine_exec, self.engine.schedule_batch, ids, reqs)
-            prev, self._inflight = self._inflight, (fw, item, cycle, t0, fut)
-            if prev is not None:
-                await self._finish_inflight_run(prev)
+            self._inflight.append((fw, item, cycle, t0, fut))
+            while len(self._inflight) >= depth:
+                await self._finish_inflight_run(self._inflight.popleft())
 
     async def _finish_inflight_run(self, run: tuple) -> None:
         fw, item, cycle, t0, fut = run
@@ -689,10 +764,9 @@ class Scheduler:
         self._finish_run(fw, item, results, cycle, t0)
 
     async def finish_inflight(self) -> None:
-        """Apply the results of the run still on the engine worker (if any)."""
-        run, self._inflight = self._inflight, None
-        if run is not None:
-            await self._finish_inflight_run(run)
+        """Apply the results of every run still on the engine worker, oldest first."""
+        while self._inflight:
+            await self._finish_inflight_run(self._inflight.popleft())
 
     # ================================================================== binding
     def _native_direct(self, fw: Framework, pi: PodInfo) -> bool:
@@ -843,7 +917,7 @@ class Scheduler:
         q = self.queue
         bs = max(1, self.config.batch_size)
         while not self._stop.is_set():
-            if self._inflight is not None and not q._active_entries:
+            if self._inflight and not q._active_entries:
                 await self.finish_inflight()      # nothing to overlap with: apply it now
                 continue
             pi = await q.pop()
