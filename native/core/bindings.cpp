@@ -1,6 +1,8 @@
 // pybind11 bindings of the native scheduling engine (module yoda_scheduler_amd._native._yoda_core).
 #include <array>
 #include <mutex>
+#include <thread>
+#include <chrono>
 
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -17,8 +19,19 @@ namespace {
 // same engine. Recursive: bound methods never nest today, but a future one may.
 std::recursive_mutex g_engine_mu;
 struct EngineGuard {
-  std::lock_guard<std::recursive_mutex> g{g_engine_mu};
+  std::unique_lock<std::recursive_mutex> g{g_engine_mu};
 };
+
+// The engine lock at a moment no device batch is in flight (schedule_batch drops the lock
+// while it waits for the device; replacing the device context then must wait for it).
+EngineGuard lock_without_batch(Engine& e) {
+  for (;;) {
+    EngineGuard g;
+    if (!e.batch_in_flight()) return g;
+    g.g.unlock();
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
 
 int8_t effect_of(const std::string& e) {
   if (e == "NoSchedule") return kNoSchedule;
@@ -90,7 +103,12 @@ PYBIND11_MODULE(_yoda_core, m) {
       .def_readonly("mem", &PodReq::mem);
 
   py::class_<Engine>(m, "Engine")
-      .def(py::init<bool, int>(), py::arg("compat") = false, py::arg("threads") = 1)
+      .def(py::init([](bool compat, int threads) {
+             auto* e = new Engine(compat, threads);
+             e->set_external_lock(&g_engine_mu);   // schedule_batch drops it during device batches
+             return e;
+           }),
+           py::arg("compat") = false, py::arg("threads") = 1)
       .def_property("compat", &Engine::compat, &Engine::set_compat)
       .def_property("filters", &Engine::filters, &Engine::set_filters)
       .def("set_score_weight", &Engine::set_score_weight, py::call_guard<EngineGuard>())
@@ -131,11 +149,21 @@ PYBIND11_MODULE(_yoda_core, m) {
       .def("enable_device",
            [](Engine& e, const std::string& path, int device, int capacity, int min_nodes) {
              std::string err;
-             bool ok = e.enable_device(path, device, capacity, min_nodes, &err);
+             bool ok = false;
+             {
+               py::gil_scoped_release nogil;
+               EngineGuard g = lock_without_batch(e);
+               ok = e.enable_device(path, device, capacity, min_nodes, &err);
+             }
              return py::make_tuple(ok, err);
            },
-           py::arg("lib_path"), py::arg("device") = 0, py::arg("capacity") = 65536, py::arg("min_nodes") = 256, py::call_guard<EngineGuard>())
-      .def("disable_device", &Engine::disable_device, py::call_guard<EngineGuard>())
+           py::arg("lib_path"), py::arg("device") = 0, py::arg("capacity") = 65536, py::arg("min_nodes") = 256)
+      .def("disable_device",
+           [](Engine& e) {
+             py::gil_scoped_release nogil;
+             EngineGuard g = lock_without_batch(e);
+             e.disable_device();
+           })
       .def_property_readonly("device_enabled", &Engine::device_enabled)
       .def_property_readonly("device_ctx", &Engine::device_ctx)
       .def_property_readonly("device_cycles", &Engine::device_cycles)

@@ -796,7 +796,11 @@ CycleResult Engine::schedule(uint64_t pod, const PodReq& req, bool assume, const
   ++cycles_;
   CycleResult r;
   if (dev_ctx_ && candidates.empty() && extra.empty() && live_ >= dev_min_nodes_ && device_eligible(req)) {
-    if (schedule_device(req, &r)) {
+    // a batch may hold the device (its engine lock dropped): then this cycle runs on the
+    // CPU path, which is bit-exact with the device
+    std::unique_lock<std::mutex> dl(dev_mu_, std::try_to_lock);
+    if (dl.owns_lock() && schedule_device(req, &r)) {
+      dl.unlock();
       if (assume && r.node >= 0) reserve(pod, req, r.node, r.cards);
       return r;
     }
@@ -1102,6 +1106,8 @@ bool Engine::schedule_device(const PodReq& req, CycleResult* r) {
 bool Engine::schedule_batch_device(const std::vector<uint64_t>& pods, const std::vector<const PodReq*>& reqs,
                                    std::vector<CycleResult>* out) {
   if (!dev_ctx_ || !fn_schedule_batch_ || live_ < dev_min_nodes_ || pods.size() < 2) return false;
+  std::unique_lock<std::mutex> dl(dev_mu_, std::try_to_lock);
+  if (!dl.owns_lock()) return false;
   for (const PodReq* q : reqs)
     if (!device_eligible(*q) || needs_candidates(*q) || (q->has_memory && q->memory > UINT32_MAX)) return false;
   // the device assumes each winner with its reservation counted as pending (Engine::reserve
@@ -1118,7 +1124,18 @@ bool Engine::schedule_batch_device(const std::vector<uint64_t>& pods, const std:
   for (size_t i = 0; i < reqs.size(); ++i) make_dev_req(*reqs[i], &d[i]);
   std::vector<yoda_dev_result_t> res(reqs.size());
   using batch_t = int (*)(void*, int, int, const yoda_dev_req_t*, yoda_dev_result_t*);
-  const int rc = ((batch_t)fn_schedule_batch_)(dev_ctx_, (int)nodes_.size(), (int)d.size(), d.data(), res.data());
+  void* ctx = dev_ctx_;
+  const int n_nodes = (int)nodes_.size();
+  // the device works on this snapshot (flushed rows + its own in-batch assumes) with the
+  // engine lock dropped: mutations meanwhile (bind confirmations, releases, Scv samples)
+  // mark their rows dirty and reach the device with the next flush, exactly as if they had
+  // happened after the batch
+  batch_in_flight_.store(true, std::memory_order_release);
+  if (ext_mu_) ext_mu_->unlock();
+  const int rc = ((batch_t)fn_schedule_batch_)(ctx, n_nodes, (int)d.size(), d.data(), res.data());
+  if (ext_mu_) ext_mu_->lock();
+  batch_in_flight_.store(false, std::memory_order_release);
+  dl.unlock();
   if (rc != 0) {
     // the device table may hold partial in-batch assumptions: re-upload every row
     ++dev_fallbacks_;
@@ -1127,7 +1144,9 @@ bool Engine::schedule_batch_device(const std::vector<uint64_t>& pods, const std:
   }
   out->clear();
   out->reserve(pods.size());
-  std::vector<int32_t> diverged;   // device assumed, host refused (duplicate pod): re-upload
+  std::vector<int32_t> diverged;   // device assumed, host refused (duplicate pod, node gone): re-upload
+  // rows dirtied while the lock was dropped are before this mark and stay dirty
+  const size_t mark = dirty_list_.size();
   for (size_t i = 0; i < pods.size(); ++i) {
     ++cycles_;
     ++dev_cycles_;
@@ -1136,18 +1155,19 @@ bool Engine::schedule_batch_device(const std::vector<uint64_t>& pods, const std:
     if (r.node >= 0 && !reserve(pods[i], *reqs[i], r.node, r.cards)) diverged.push_back(r.node);
     out->push_back(std::move(r));
   }
-  // the device already applied every winner's assume to its own rows (same fields, same
-  // arithmetic as reserve() with the reservation pending), so the rows reserve() just marked
-  // dirty are identical on both sides: no re-upload. flush_dirty() emptied the list before the
-  // batch, so every entry in it now comes from these reservations.
-  for (int32_t i : dirty_list_) dirty_[i] = 0;
-  dirty_list_.clear();
+  // a row reserve() just dirtied was clean when the batch started and untouched since, and
+  // the device applied the same assumes to it (same fields, same arithmetic as reserve()
+  // with the reservation pending): both sides hold the same row, no re-upload
+  for (size_t k = mark; k < dirty_list_.size(); ++k) dirty_[dirty_list_[k]] = 0;
+  dirty_list_.resize(mark);
   for (int32_t i : diverged) mark_dirty(i);
   return true;
 }
 
 bool Engine::device_cycle(const PodReq& req, CycleResult* out) {
   if (!device_eligible(req)) return false;
+  std::unique_lock<std::mutex> dl(dev_mu_, std::try_to_lock);
+  if (!dl.owns_lock()) return false;
   return schedule_device(req, out);
 }
 

@@ -266,6 +266,12 @@ class Engine {
   void disable_device();
   bool device_enabled() const { return dev_ctx_ != nullptr; }
   uintptr_t device_ctx() const { return (uintptr_t)dev_ctx_; }   // for yoda_dev_* debug entry points
+  // The caller's engine lock (the Python binding's). schedule_batch drops it while the
+  // device places the batch, so other engine calls (informer updates, bind confirmations)
+  // proceed meanwhile instead of stalling the event loop for the whole batch; the caller
+  // must hold it exactly once. Device use itself is serialised by dev_mu_.
+  void set_external_lock(std::recursive_mutex* m) { ext_mu_ = m; }
+  bool batch_in_flight() const { return batch_in_flight_.load(std::memory_order_acquire); }
   uint64_t device_cycles() const { return dev_cycles_; }
   uint64_t device_fallbacks() const { return dev_fallbacks_; }
   float device_last_us() const;
@@ -326,6 +332,9 @@ class Engine {
   void* fn_last_us_ = nullptr;
   void* fn_set_timing_ = nullptr;   // optional entry points
   void* fn_schedule_batch_ = nullptr;
+  std::recursive_mutex* ext_mu_ = nullptr;
+  std::mutex dev_mu_;                        // device context (stream, staging buffers)
+  std::atomic<bool> batch_in_flight_{false};
   double now() const;
   bool is_pending(const Node& n, const Assignment& a) const { return a.t_res > n.sample_ts - settle_s_; }
   int32_t next_start_ = 0;
