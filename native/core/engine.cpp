@@ -1002,7 +1002,9 @@ bool Engine::device_eligible(const PodReq& req) const {
   int64_t wsum = 0;
   for (int i = 0; i < S_NUM; ++i) wsum += score_w_[i] < 0 ? -score_w_[i] : score_w_[i];
   if (wsum * 200 >= ((int64_t)1 << 38)) return false;          // key = (final << 24) | perm
-  if (wt_.w_link < 0 || wt_.w_link > 1000000 || wt_.w_numa > 1000000 || wt_.w_fit > 1000000 || wt_.w_occ > 1000000)
+  // the device forms the gang objective with 32×32-bit multiply-adds: |w| ≤ 10^6
+  if (wt_.w_link < 0 || wt_.w_link > 1000000 || wt_.w_numa > 1000000 || wt_.w_fit > 1000000 || wt_.w_occ > 1000000 ||
+      wt_.w_numa < -1000000 || wt_.w_fit < -1000000 || wt_.w_occ < -1000000)
     return false;
   if (!default_alloc_weights()) return false;                    // device computes (c + m) / 2
   return true;

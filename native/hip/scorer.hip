@@ -6,7 +6,7 @@
 // CDNA4 mapping
 //  * a 64-lane wave scores 8 nodes at once: lane group g (8 lanes) owns node base+g and
 //    lane s of the group owns GPU slot s, so eligibility is one 64-bit __ballot split in
-//    8-bit fields and every per-node reduction is a 3-step __shfl_xor inside the group;
+//    8-bit fields and every per-node reduction is 3 DPP lane moves inside the group;
 //  * the k-GPU gang search walks a constant table of the C(8,k) subsets with k set bits
 //    (≤ 70), 8 lanes per node, skipping subsets with ineligible GPUs; the objective uses
 //    per-lane register tables (effective free HBM, total, occupancy, NUMA, the 28
@@ -125,12 +125,21 @@ __device__ __forceinline__ void min_if(unsigned long long* p, unsigned long long
   if (direct || v < peek(p)) atomicMin(p, v);
 }
 
-// Exact floor(n / d) for d > 0: a correctly rounded double quotient is within 1 of the
-// truth while n < 2^53; one integer multiply-subtract fixes it. Larger n (not produced
-// by realistic clusters) take the software divide.
-__device__ __forceinline__ uint64_t udiv(uint64_t n, uint64_t d) {
-  if (n < (1ull << 53) && d < (1ull << 53)) {
-    uint64_t q = (uint64_t)((double)n / (double)d);
+// 1/d to full double precision: the hardware reciprocal refined by two Newton steps.
+__device__ __forceinline__ double rcp64(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+// Exact floor(n / d) for d > 0 given r ≈ 1/d (a few ulp): for n < 2^50 the estimate
+// n·r is within 1 of the quotient and one integer multiply-subtract fixes it. Larger n (not
+// produced by realistic clusters) take the software divide. Per-pod or per-node divisors
+// pass a precomputed reciprocal; `udiv` computes it.
+__device__ __forceinline__ uint64_t udiv_r(uint64_t n, uint64_t d, double r) {
+  if (n < (1ull << 50)) {
+    uint64_t q = (uint64_t)((double)n * r);
     const uint64_t qd = q * d;
     if (qd > n) --q;
     else if (n - qd >= d) ++q;
@@ -138,9 +147,18 @@ __device__ __forceinline__ uint64_t udiv(uint64_t n, uint64_t d) {
   }
   return n / d;
 }
-// truncating int division by a tiny divisor (≤ 28): every non-integer quotient is at least
-// 1/28 away from an integer, far beyond the double rounding error → exact
-__device__ __forceinline__ int32_t sdiv_small(int32_t n, int32_t d) { return (int32_t)((double)n / (double)d); }
+__device__ __forceinline__ uint64_t udiv(uint64_t n, uint64_t d) {
+  return d < (1ull << 50) ? udiv_r(n, d, rcp64((double)d)) : n / d;
+}
+// truncating int division by a small positive divisor (|n| < 2^30) from r ≈ 1/d: the
+// estimate on |n| is within 1 of the quotient, one integer check fixes it
+__device__ __forceinline__ int32_t sdiv_small_r(int32_t n, int32_t d, double r) {
+  const int32_t a = n < 0 ? -n : n;
+  int32_t q = (int32_t)((double)a * r);
+  if ((q + 1) * d <= a) ++q;
+  else if (q * d > a) --q;
+  return n < 0 ? -q : q;
+}
 
 __device__ __forceinline__ uint64_t eff_free(uint32_t free, uint32_t pending, uint32_t total, uint32_t reserved) {
   const uint64_t sampled = free > pending ? (uint64_t)(free - pending) : 0;
@@ -148,30 +166,67 @@ __device__ __forceinline__ uint64_t eff_free(uint32_t free, uint32_t pending, ui
   return sampled < cap ? sampled : cap;
 }
 
-template <typename T>
-__device__ __forceinline__ T gmax(T v) {   // max over the 8 lanes of a group
-#pragma unroll
-  for (int off = 4; off > 0; off >>= 1) {
-    const T o = __shfl_xor(v, off, 64);
-    v = o > v ? o : v;
+// ---- cross-lane reductions on DPP lane moves (VALU, no LDS round trip like ds_bpermute).
+// A node's 8 lanes are lanes 8g..8g+7: quad_perm xor 1, xor 2, then row_half_mirror (lane i ↔
+// 7 − i of the same 8) reach every lane of the group; row_mirror (i ↔ 15 − i) pairs the two
+// groups of a 16-lane row; readlane 0/16/32/48 combines the four rows. Every source lane of a
+// move must be active: group reductions run where a whole group takes the same branch, wave
+// reductions in wave-uniform control flow.
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppRowMirror = 0x140, kDppRowHalfMirror = 0x141;
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL, typename T>
+__device__ __forceinline__ T dpp(T v) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit lanes");
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, dpp32<CTRL>(__builtin_bit_cast(uint32_t, v)));
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint64_t r = (uint64_t)dpp32<CTRL>((uint32_t)u) | ((uint64_t)dpp32<CTRL>((uint32_t)(u >> 32)) << 32);
+    return __builtin_bit_cast(T, r);
   }
-  return v;
 }
 template <typename T>
-__device__ __forceinline__ T gsum(T v) {
-#pragma unroll
-  for (int off = 4; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-template <typename T>
-__device__ __forceinline__ T wmax_across_groups(T v) {   // max over the 8 groups of a wave
-#pragma unroll
-  for (int off = 8; off < 64; off <<= 1) {
-    const T o = __shfl_xor(v, off, 64);
-    v = o > v ? o : v;
+__device__ __forceinline__ T readlane(T v, int l) {
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint64_t r = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l) << 32);
+    return __builtin_bit_cast(T, r);
   }
-  return v;
 }
+struct OpMax { template <typename T> __device__ T operator()(T a, T b) const { return a > b ? a : b; } };
+struct OpMin { template <typename T> __device__ T operator()(T a, T b) const { return a < b ? a : b; } };
+struct OpSum { template <typename T> __device__ T operator()(T a, T b) const { return a + b; } };
+
+template <typename T, typename Op>
+__device__ __forceinline__ T group_reduce(T v, Op op) {   // every lane of the 8 gets the result
+  v = op(v, dpp<kDppXor1>(v));
+  v = op(v, dpp<kDppXor2>(v));
+  return op(v, dpp<kDppRowHalfMirror>(v));
+}
+template <typename T, typename Op>
+__device__ __forceinline__ T across_groups(T v, Op op) {  // v group-uniform → wave-uniform
+  v = op(v, dpp<kDppRowMirror>(v));
+  return op(op(readlane(v, 0), readlane(v, 16)), op(readlane(v, 32), readlane(v, 48)));
+}
+template <typename T>
+__device__ __forceinline__ T gmax(T v) { return group_reduce(v, OpMax{}); }
+template <typename T>
+__device__ __forceinline__ T gsum(T v) { return group_reduce(v, OpSum{}); }
+template <typename T>
+__device__ __forceinline__ T wmax_across_groups(T v) { return across_groups(v, OpMax{}); }
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) { return across_groups(group_reduce(v, OpMax{}), OpMax{}); }
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) { return across_groups(group_reduce(v, OpMin{}), OpMin{}); }
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) { return across_groups(group_reduce(v, OpSum{}), OpSum{}); }
 
 // ------------------------------------------------------------------ dirty-row patch
 __global__ void k_patch(PatchArgs a, yoda_dev_node_t* __restrict__ nodes) {
@@ -194,8 +249,7 @@ __global__ void k_scatter(const yoda_dev_node_t* __restrict__ stage, const int32
 // feasible) and its eligible-GPU mask, and folds the card metrics of feasible nodes into the
 // wave maxima `wmx` (wave-uniform afterwards). Shared by k_filter and k_batch.
 __device__ __forceinline__ int filter_eval(const yoda_dev_node_t* nd, bool valid, const yoda_dev_req_t& r,
-                                           uint8_t cnd, unsigned long long* wmx, uint32_t& emask_out, int grp,
-                                           int sub) {
+                                           uint8_t cnd, uint32_t* wmx, uint32_t& emask_out, int grp, int sub) {
   const bool yoda = (r.filters & F_YODA) != 0;
   // every load of the node issued up front: one memory round trip per node
   const uint8_t flags = valid ? nd->flags : 0, ncards = nd->ncards;
@@ -231,12 +285,13 @@ __device__ __forceinline__ int filter_eval(const yoda_dev_node_t* nd, bool valid
   emask_out = emask;
   if (yoda) {
     const bool take = ok && ((emask >> sub) & 1u);
-    unsigned long long v[6];
+    // card metrics are u32 (ef ≤ free): 32-bit shuffles
+    uint32_t v[6];
     v[0] = take ? cd.bandwidth : 0; v[1] = take ? cd.clock : 0; v[2] = take ? cd.core : 0;
-    v[3] = take ? ef : 0; v[4] = take ? cd.power : 0; v[5] = take ? cd.total : 0;
+    v[3] = take ? (uint32_t)ef : 0; v[4] = take ? cd.power : 0; v[5] = take ? cd.total : 0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      const unsigned long long m = wmax_across_groups(gmax(v[k]));
+      const uint32_t m = wmax_across_groups(gmax(v[k]));
       wmx[k] = m > wmx[k] ? m : wmx[k];
     }
   }
@@ -245,7 +300,7 @@ __device__ __forceinline__ int filter_eval(const yoda_dev_node_t* nd, bool valid
 
 __device__ __forceinline__ void filter_group(const yoda_dev_node_t* nd, int i, bool valid, const yoda_dev_req_t& r,
                                              const uint8_t* __restrict__ cand, uint8_t* __restrict__ feas,
-                                             uint8_t* __restrict__ elig, int* s_reason, unsigned long long* wmx,
+                                             uint8_t* __restrict__ elig, int* s_reason, uint32_t* wmx,
                                              int& nfeas, int grp, int sub) {
   const uint8_t cnd = (r.use_candidates && valid) ? cand[i] : 0;
   uint32_t emask = 0;
@@ -271,7 +326,7 @@ __global__ __launch_bounds__(kBlock) void k_filter(const PatchArgs pa, yoda_dev_
   if (threadIdx.x < YODA_DEV_REASONS) s_reason[threadIdx.x] = 0;
   if (threadIdx.x == 0) s_feas = 0;
   __syncthreads();
-  unsigned long long wmx[6] = {1, 1, 1, 1, 1, 1};
+  uint32_t wmx[6] = {1, 1, 1, 1, 1, 1};
   int nfeas = 0;
   // with dirty rows the host launches one extra block: it writes them back to the table
   // for the score kernel and evaluates them from the arguments, in parallel with the rest
@@ -298,10 +353,7 @@ __global__ __launch_bounds__(kBlock) void k_filter(const PatchArgs pa, yoda_dev_
       filter_group(nodes + (i < n ? i : n - 1), i, valid, r, cand, feas, elig, s_reason, wmx, nfeas, grp, sub);
     }
   }
-  nfeas = gsum(nfeas);
-  nfeas += __shfl_xor(nfeas, 8, 64);
-  nfeas += __shfl_xor(nfeas, 16, 64);
-  nfeas += __shfl_xor(nfeas, 32, 64);
+  nfeas = wave_sum(nfeas);
   if (lane == 0) {
 #pragma unroll
     for (int k = 0; k < 6; ++k) s_max[wave][k] = wmx[k];
@@ -358,11 +410,7 @@ __device__ unsigned long long select_block(int n, const yoda_dev_req_t& r, const
       best = key > best ? key : best;
     }
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const unsigned long long o = __shfl_xor(best, off, 64);
-    best = o > best ? o : best;
-  }
+  best = wave_max(best);
   if (lane == 0) s_key[wave] = best;
   __syncthreads();
   unsigned long long b = 0;
@@ -433,18 +481,28 @@ __device__ __forceinline__ bool better(int64_t oa, uint32_t ma, int64_t ob, uint
 }
 
 // ------------------------------------------------------------------ K2: scores + gang search
-// Per-pod constants of the score phase (maxima from the filter phase, gang-search bounds).
+// Per-pod constants of the score phase (maxima from the filter phase, gang-search bounds,
+// reciprocals of the per-pod divisors).
 struct ScoreConsts {
   uint64_t mx[6];
+  double rmx[6];            // 1 / mx[k]
   int k, s_begin, s_end;
   int32_t P;
+  double rP, rk, rk1;       // 1/P, 1/k, 1/(k-1) (0 where unused)
   bool search, yoda_s;
 };
 
+__device__ __forceinline__ void score_consts_maxima(ScoreConsts& s, const uint64_t* maxima) {
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    s.mx[j] = maxima[j];
+    s.rmx[j] = rcp64((double)maxima[j]);
+  }
+}
+
 __device__ __forceinline__ ScoreConsts score_consts(const yoda_dev_req_t& r, const uint64_t* maxima) {
   ScoreConsts s;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) s.mx[j] = maxima[j];
+  if (maxima) score_consts_maxima(s, maxima);
   const bool yoda_f = (r.filters & F_YODA) != 0;
   s.yoda_s = yoda_f && r.w_yoda != 0;
   s.k = (int)(r.has_number ? (r.number > 64 ? 64 : r.number) : 1);
@@ -452,24 +510,21 @@ __device__ __forceinline__ ScoreConsts score_consts(const yoda_dev_req_t& r, con
   s.P = s.k * (s.k - 1) / 2;
   s.s_begin = s.search ? c_subsets.start[s.k] : 0;
   s.s_end = s.search ? c_subsets.start[s.k + 1] : 0;
+  s.rP = s.P ? rcp64((double)s.P) : 0.0;
+  s.rk = rcp64((double)(s.k > 0 ? s.k : 1));
+  s.rk1 = s.k > 1 ? rcp64((double)(s.k - 1)) : 0.0;
   return s;
 }
 
-// One lane group scores one node (lane `sub` = card `sub`): the gang / GPU-set choice (the
-// Reserve choice if this node wins), the yoda raw score and the upstream default scores.
-// Outputs are valid on the group's `sub == 0` lane when `act`; `lo`/`hi` fold the raw score.
-// Every shuffle is executed by every lane (callers iterate wave-uniformly). Shared by k_score
-// and k_batch.
-__device__ __forceinline__ void score_node(const yoda_dev_node_t* nd, bool act, uint32_t emask,
-                                           const yoda_dev_req_t& r, const ScoreConsts& sc,
-                                           const uint8_t* s_masks, int sub, int64_t& raw_o, int64_t& total_o,
-                                           uint32_t& mask_o, int32_t& quality_o, unsigned long long& lo,
-                                           unsigned long long& hi, unsigned long long* dbg = nullptr) {
-#define DSTAMP(k)                                                  \
-  do {                                                             \
-    if (dbg) dbg[k] = __builtin_amdgcn_s_memrealtime();            \
-  } while (0)
-  const uint64_t mx0 = sc.mx[0], mx1 = sc.mx[1], mx2 = sc.mx[2], mx3 = sc.mx[3], mx4 = sc.mx[4], mx5 = sc.mx[5];
+// Part A of scoring one node (lane `sub` = card `sub`), everything that does not depend on
+// the filter phase's maxima: the gang / GPU-set choice (the Reserve choice if this node
+// wins), the yoda score's allocate + actual + gang terms (`rbase_o`) and the upstream default
+// scores (`total_o`). Outputs valid on the group's `sub == 0` lane when `act`. Every shuffle
+// is executed by every lane (callers iterate wave-uniformly).
+__device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act, uint32_t emask,
+                                             const yoda_dev_req_t& r, const ScoreConsts& sc,
+                                             const uint8_t* s_masks, int sub, uint64_t& rbase_o, int64_t& total_o,
+                                             uint32_t& mask_o, int32_t& quality_o) {
   const int k = sc.k;
   const bool search = sc.search, yoda_s = sc.yoda_s;
   const int32_t P = sc.P;
@@ -477,26 +532,43 @@ __device__ __forceinline__ void score_node(const yoda_dev_node_t* nd, bool act, 
   const uint8_t ncards = nd->ncards;
   // ---- per-node register tables (every lane of the group holds the whole node)
   uint64_t ef[YODA_DEV_CARDS];
-  uint32_t tot[YODA_DEV_CARDS], occ[YODA_DEV_CARDS], numa[YODA_DEV_CARDS];
+  uint32_t tot[YODA_DEV_CARDS], occ[YODA_DEV_CARDS];
+  // the allocate/actual terms' card sums, formed from the same registers (every lane holds
+  // the node): no cross-lane reduction
+  uint64_t t64 = 0, a64 = 0, fsum = 0;
 #pragma unroll
   for (int a = 0; a < YODA_DEV_CARDS; ++a) {
     const uint4 lo4 = reinterpret_cast<const uint4*>(&nd->cards[a])[0];   // total, free, reserved, pending
     ef[a] = eff_free(lo4.y, lo4.w, lo4.x, lo4.z);
     tot[a] = lo4.x;
     occ[a] = nd->occ[a];
-    numa[a] = nd->numa[a] & 63u;
-  }
-  uint32_t lq[32];   // 64 u16 card-pair qualities, packed 2 per dword
-  {
-    const uint4* q4 = reinterpret_cast<const uint4*>(&nd->linkq[0][0]);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const uint4 v = q4[t];
-      lq[4 * t] = v.x; lq[4 * t + 1] = v.y; lq[4 * t + 2] = v.z; lq[4 * t + 3] = v.w;
+    if (a < ncards) {
+      t64 += lo4.x;
+      a64 += lo4.z;
+      fsum += ef[a];
     }
   }
-  DSTAMP(0);
-  // ---- gang / GPU-set selection (the Reserve choice if this node wins)
+  // ---- gang / GPU-set selection (the Reserve choice if this node wins); the 8 lanes'
+  // candidates meet through DPP moves inside the group (the whole group is in the branch)
+#define GANG_STEP1(CTRL)                                              \
+  do {                                                                \
+    const int64_t oo = dpp<CTRL>(best_o);                             \
+    const uint32_t om = dpp<CTRL>(best_m);                            \
+    const uint32_t of = dpp<CTRL>((uint32_t)found);                   \
+    if (of && (!found || better(oo, om, best_o, best_m))) {           \
+      best_o = oo; best_m = om; found = true;                         \
+    }                                                                 \
+  } while (0)
+#define GANG_STEP(CTRL)                                               \
+  do {                                                                \
+    const int64_t oo = dpp<CTRL>(best_o);                             \
+    const uint32_t om = dpp<CTRL>(best_m);                            \
+    const int32_t ol = dpp<CTRL>(best_lb);                            \
+    const uint32_t of = dpp<CTRL>((uint32_t)found);                   \
+    if (of && (!found || better(oo, om, best_o, best_m))) {           \
+      best_o = oo; best_m = om; best_lb = ol; found = true;           \
+    }                                                                 \
+  } while (0)
   uint32_t best_m = 0;
   int64_t best_o = LLONG_MAX;
   int32_t best_lb = 0;
@@ -516,25 +588,42 @@ __device__ __forceinline__ void score_node(const yoda_dev_node_t* nd, bool act, 
         ocs = sub == a ? occ[a] : ocs;
       }
       const uint64_t fa = efs - r.memory;
-      const int64_t leftover = tos ? (int64_t)udiv(fa * 1000000ull, (uint64_t)tos) : 0;
-      const int64_t fit = r.binpack ? leftover : 1000000 - leftover;
-      const int64_t occ_bad = (int64_t)sdiv_small((int32_t)(ocs * 100u), 1);
-      best_o = r.w_fit * fit + r.w_occ * occ_bad;
+      const int32_t leftover = tos ? (int32_t)udiv(fa * 1000000ull, (uint64_t)tos) : 0;   // ≤ 10^6
+      const int32_t fit = r.binpack ? leftover : 1000000 - leftover;
+      const int32_t occ_bad = (int32_t)(ocs * 100u);   // sdiv by k = 1
+      best_o = (int64_t)(int32_t)r.w_fit * fit + (int64_t)(int32_t)r.w_occ * occ_bad;
       best_m = 1u << sub;
       best_lb = 0;
       found = true;
     }
+    GANG_STEP1(kDppXor1);
+    GANG_STEP1(kDppXor2);
+    GANG_STEP1(kDppRowHalfMirror);
+  } else if (search && act) {
+    // numa + card-pair qualities: only the multi-GPU search reads them
+    uint32_t numa[YODA_DEV_CARDS];
 #pragma unroll
-    for (int off = 4; off > 0; off >>= 1) {
-      const int64_t oo = __shfl_xor(best_o, off, 64);
-      const uint32_t om = __shfl_xor(best_m, off, 64);
-      const int32_t ol = __shfl_xor(best_lb, off, 64);
-      const int of = __shfl_xor((int)found, off, 64);
-      if (of && (!found || better(oo, om, best_o, best_m))) {
-        best_o = oo; best_m = om; best_lb = ol; found = true;
+    for (int a = 0; a < YODA_DEV_CARDS; ++a) numa[a] = nd->numa[a] & 63u;
+    uint32_t lq[32];   // 64 u16 card-pair qualities, packed 2 per dword
+    {
+      const uint4* q4 = reinterpret_cast<const uint4*>(&nd->linkq[0][0]);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const uint4 v = q4[t];
+        lq[4 * t] = v.x; lq[4 * t + 1] = v.y; lq[4 * t + 2] = v.z; lq[4 * t + 3] = v.w;
       }
     }
-  } else if (search && act) {
+    // every card pair equally good (idle or evenly loaded xGMI, the usual SPX node): a
+    // subset of k cards sums to P·q, no per-pair adds
+    const uint32_t q01 = lq[0] >> 16;   // linkq[0][1]
+    bool uni = true;
+#pragma unroll
+    for (int a = 0; a < YODA_DEV_CARDS; ++a)
+#pragma unroll
+      for (int b = a + 1; b < YODA_DEV_CARDS; ++b) {
+        const int idx = a * YODA_DEV_CARDS + b;
+        uni = uni && ((lq[idx >> 1] >> ((idx & 1) * 16)) & 0xFFFFu) == q01;
+      }
     for (int t = s_begin + sub; t < s_end; t += kGroup) {
       const uint32_t m = s_masks[t];
       if (m & ~emask) continue;
@@ -545,105 +634,121 @@ __device__ __forceinline__ void score_node(const yoda_dev_node_t* nd, bool act, 
 #pragma unroll
       for (int a = 0; a < YODA_DEV_CARDS; ++a) {
         const bool ia = (m >> a) & 1u;
-        nmask |= ia ? (1ull << numa[a]) : 0ull;
+        nmask |= ia ? (1ull << numa[a]) : 0ull;   // numa < 64
         fa += ia ? ef[a] - r.memory : 0;
         tt += ia ? tot[a] : 0;
         oc += ia ? occ[a] : 0u;
+      }
+      if (uni) {
+        qsum = P * (int32_t)q01;
+      } else {
 #pragma unroll
-        for (int b = a + 1; b < YODA_DEV_CARDS; ++b) {
-          const int idx = a * YODA_DEV_CARDS + b;
-          const int32_t q = (int32_t)((lq[idx >> 1] >> ((idx & 1) * 16)) & 0xFFFFu);
-          qsum += (ia && ((m >> b) & 1u)) ? q : 0;
+        for (int a = 0; a < YODA_DEV_CARDS; ++a) {
+          const bool ia = (m >> a) & 1u;
+#pragma unroll
+          for (int b = a + 1; b < YODA_DEV_CARDS; ++b) {
+            const int idx = a * YODA_DEV_CARDS + b;
+            const int32_t q = (int32_t)((lq[idx >> 1] >> ((idx & 1) * 16)) & 0xFFFFu);
+            qsum += (ia && ((m >> b) & 1u)) ? q : 0;
+          }
         }
       }
-      const int32_t lb = P ? sdiv_small((P * 10000 - qsum) * 100, P) : 0;
+      const int32_t lb = P ? sdiv_small_r((P * 10000 - qsum) * 100, P, sc.rP) : 0;
       const int32_t d = __popcll(nmask);
-      const int64_t numa_bad = k > 1 ? (int64_t)sdiv_small((d - 1) * 1000000, k - 1) : 0;
-      const int64_t leftover = tt ? (int64_t)udiv(fa * 1000000ull, tt) : 0;
-      const int64_t fit = r.binpack ? leftover : 1000000 - leftover;
-      const int64_t occ_bad = (int64_t)sdiv_small((int32_t)(oc * 100u), k);
-      const int64_t o = r.w_link * (int64_t)lb + r.w_numa * numa_bad + r.w_fit * fit + r.w_occ * occ_bad;
+      const int32_t numa_bad = k > 1 ? sdiv_small_r((d - 1) * 1000000, k - 1, sc.rk1) : 0;
+      const int32_t leftover = tt ? (int32_t)udiv(fa * 1000000ull, tt) : 0;   // fa ≤ tt: ≤ 10^6
+      const int32_t fit = r.binpack ? leftover : 1000000 - leftover;
+      const int32_t occ_bad = sdiv_small_r((int32_t)(oc * 100u), k, sc.rk);
+      // every term fits 32 bits and the host bounds |w| ≤ 10^6 (Engine::device_eligible):
+      // 32×32→64-bit multiply-adds instead of 64×64
+      const int64_t o = (int64_t)(int32_t)r.w_link * lb + (int64_t)(int32_t)r.w_numa * numa_bad +
+                        (int64_t)(int32_t)r.w_fit * fit + (int64_t)(int32_t)r.w_occ * occ_bad;
       if (!found || better(o, m, best_o, best_m)) {
         best_o = o; best_m = m; best_lb = lb; found = true;
       }
     }
-#pragma unroll
-    for (int off = 4; off > 0; off >>= 1) {
-      const int64_t oo = __shfl_xor(best_o, off, 64);
-      const uint32_t om = __shfl_xor(best_m, off, 64);
-      const int32_t ol = __shfl_xor(best_lb, off, 64);
-      const int of = __shfl_xor((int)found, off, 64);
-      if (of && (!found || better(oo, om, best_o, best_m))) {
-        best_o = oo; best_m = om; best_lb = ol; found = true;
-      }
-    }
-  } else {
-    // keep the shuffles wave-uniform for inactive groups
-#pragma unroll
-    for (int off = 4; off > 0; off >>= 1) {
-      (void)__shfl_xor(best_o, off, 64);
-      (void)__shfl_xor(best_m, off, 64);
-      (void)__shfl_xor(best_lb, off, 64);
-      (void)__shfl_xor((int)found, off, 64);
-    }
+    GANG_STEP(kDppXor1);
+    GANG_STEP(kDppXor2);
+    GANG_STEP(kDppRowHalfMirror);
   }
-  const int32_t quality = found ? 10000 - sdiv_small(best_lb, 100) : 10000;
-  DSTAMP(1);
-  // ---- yoda raw score (algorithm.go:28-87 with the Q1/Q2/Q3/Q4 fixes); lane sub = card sub
-  uint64_t basic = 0, tsum = 0, fsum = 0, asum = 0;
-  if (act && sub < ncards) {
-    const yoda_dev_card_t cd = nd->cards[sub];
-    tsum = cd.total;
-    fsum = ef[0];
-#pragma unroll
-    for (int a = 1; a < YODA_DEV_CARDS; ++a) fsum = sub == a ? ef[a] : fsum;
-    asum = cd.reserved;
-    if ((emask >> sub) & 1u) {
-      basic = udiv((uint64_t)cd.bandwidth * 100, mx0) + udiv((uint64_t)cd.clock * 100, mx1) +
-              udiv((uint64_t)cd.core * 100, mx2) + udiv((uint64_t)cd.power * 100, mx4) +
-              udiv(fsum * 100, mx3) * 2 + udiv((uint64_t)cd.total * 100, mx5);
-    }
-  }
-  basic = gsum(basic);
-  tsum = gsum(tsum);
-  fsum = gsum(fsum);
-  asum = gsum(asum);
-  DSTAMP(2);
+#undef GANG_STEP1
+#undef GANG_STEP
+  const int32_t quality = found ? 10000 - sdiv_small_r(best_lb, 100, 0.01) : 10000;
+  // ---- yoda score terms that need no maxima (algorithm.go:28-87 with the Q1/Q2/Q3/Q4
+  // fixes): allocate + actual over the node's cards (sums above), plus the gang bonus
   if (act && sub == 0) {
-    int64_t s_out = 0;
+    uint64_t rb = 0;
     if (yoda_s) {
-      const uint64_t actual = tsum ? udiv(fsum * 100, tsum) * 2 : 0;
-      const uint64_t allocate = (tsum == 0 || tsum < asum) ? 0 : udiv((tsum - asum) * 100, tsum) * 3;
-      uint64_t s = basic + allocate + actual;
+      const double rt = t64 ? rcp64((double)t64) : 0.0;
+      const uint64_t actual = t64 ? udiv_r(fsum * 100, t64, rt) * 2 : 0;
+      const uint64_t allocate = (t64 == 0 || t64 < a64) ? 0 : udiv_r((t64 - a64) * 100, t64, rt) * 3;
+      rb = allocate + actual;
       if (r.has_number && r.number > 1 && r.number <= ncards && found)
-        s += (uint64_t)(quality / 100) * (uint64_t)r.w_gang_score;
-      s_out = s > (uint64_t)LLONG_MAX ? 0 : (int64_t)s;
-      const unsigned long long us = (unsigned long long)s_out;
-      lo = us < lo ? us : lo;
-      hi = us > hi ? us : hi;
+        rb += (uint64_t)(quality / 100) * (uint64_t)r.w_gang_score;
     }
     // upstream default scores (engine.cpp Engine::score_nodes)
     const int64_t rc = nd->nz_cpu + r.nz_cpu_m, rm = nd->nz_mem + r.nz_mem;
     const int64_t ac = nd->alloc_cpu, am = nd->alloc_mem;
-    int64_t least = 0, most = 0, extra = r.w_const;
-    if (ac > 0 && rc <= ac) least += (int64_t)udiv((uint64_t)(ac - rc) * 100, (uint64_t)ac);
-    if (am > 0 && rm <= am) least += (int64_t)udiv((uint64_t)(am - rm) * 100, (uint64_t)am);
-    if (ac > 0) most += (int64_t)udiv((uint64_t)(rc < ac ? rc : ac) * 100, (uint64_t)ac);
-    if (am > 0) most += (int64_t)udiv((uint64_t)(rm < am ? rm : am) * 100, (uint64_t)am);
-    extra += r.w_least * (least / 2) + r.w_most * (most / 2);
+    int64_t extra = r.w_const;
+    if (r.w_least || r.w_most) {
+      const double rac = ac > 0 ? rcp64((double)ac) : 0.0, ram = am > 0 ? rcp64((double)am) : 0.0;
+      int64_t least = 0, most = 0;
+      if (ac > 0 && rc <= ac) least += (int64_t)udiv_r((uint64_t)(ac - rc) * 100, (uint64_t)ac, rac);
+      if (am > 0 && rm <= am) least += (int64_t)udiv_r((uint64_t)(am - rm) * 100, (uint64_t)am, ram);
+      if (ac > 0) most += (int64_t)udiv_r((uint64_t)(rc < ac ? rc : ac) * 100, (uint64_t)ac, rac);
+      if (am > 0) most += (int64_t)udiv_r((uint64_t)(rm < am ? rm : am) * 100, (uint64_t)am, ram);
+      extra += r.w_least * (least / 2) + r.w_most * (most / 2);
+    }
     if (r.w_balanced) {
       const double cf = ac > 0 ? (double)rc / (double)ac : 1.0;
       const double mf = am > 0 ? (double)rm / (double)am : 1.0;
       const int64_t b = (cf >= 1 || mf >= 1) ? 0 : (int64_t)((1.0 - fabs(cf - mf)) * 100);
       extra += r.w_balanced * b;
     }
-    raw_o = s_out;
+    rbase_o = rb;
     total_o = extra;
     mask_o = best_m;
     quality_o = quality;
   }
-  DSTAMP(3);
-#undef DSTAMP
+}
+
+// Part B: the yoda raw score = Σ over eligible cards of the maxima-normalised card metrics
+// (basic) + part A's `rbase`; folds it into `lo`/`hi`. Valid on `sub == 0` when `act`.
+__device__ __forceinline__ int64_t score_node_b(const yoda_dev_node_t* nd, bool act, uint32_t emask,
+                                                const ScoreConsts& sc, int sub, uint64_t rbase,
+                                                unsigned long long& lo, unsigned long long& hi) {
+  uint64_t basic = 0;
+  if (act && sc.yoda_s && ((emask >> sub) & 1u)) {
+    const yoda_dev_card_t cd = nd->cards[sub];
+    const uint64_t ef = eff_free(cd.free, cd.pending, cd.total, cd.reserved);
+    basic = udiv_r((uint64_t)cd.bandwidth * 100, sc.mx[0], sc.rmx[0]) +
+            udiv_r((uint64_t)cd.clock * 100, sc.mx[1], sc.rmx[1]) +
+            udiv_r((uint64_t)cd.core * 100, sc.mx[2], sc.rmx[2]) +
+            udiv_r((uint64_t)cd.power * 100, sc.mx[4], sc.rmx[4]) +
+            udiv_r(ef * 100, sc.mx[3], sc.rmx[3]) * 2 + udiv_r((uint64_t)cd.total * 100, sc.mx[5], sc.rmx[5]);
+  }
+  basic = gsum((uint32_t)basic);   // ≤ 8 cards × 700: 32-bit lanes
+  int64_t s_out = 0;
+  if (act && sub == 0 && sc.yoda_s) {
+    const uint64_t s = basic + rbase;
+    s_out = s > (uint64_t)LLONG_MAX ? 0 : (int64_t)s;
+    const unsigned long long us = (unsigned long long)s_out;
+    lo = us < lo ? us : lo;
+    hi = us > hi ? us : hi;
+  }
+  return s_out;
+}
+
+// Both parts (the per-pod launch chain's k_score).
+__device__ __forceinline__ void score_node(const yoda_dev_node_t* nd, bool act, uint32_t emask,
+                                           const yoda_dev_req_t& r, const ScoreConsts& sc,
+                                           const uint8_t* s_masks, int sub, int64_t& raw_o, int64_t& total_o,
+                                           uint32_t& mask_o, int32_t& quality_o, unsigned long long& lo,
+                                           unsigned long long& hi) {
+  uint64_t rbase = 0;
+  score_node_a(nd, act, emask, r, sc, s_masks, sub, rbase, total_o, mask_o, quality_o);
+  const int64_t raw = score_node_b(nd, act, emask, sc, sub, rbase, lo, hi);
+  if (act && sub == 0) raw_o = raw;
 }
 
 __global__ __launch_bounds__(kBlock) void k_score(yoda_dev_node_t* __restrict__ nodes, int n,
@@ -683,12 +788,8 @@ __global__ __launch_bounds__(kBlock) void k_score(yoda_dev_node_t* __restrict__ 
     }
   }
   // wave-level min/max of the raw score (lanes that scored nothing hold the identities)
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const unsigned long long ol = __shfl_xor(lo, off, 64), oh = __shfl_xor(hi, off, 64);
-    lo = ol < lo ? ol : lo;
-    hi = oh > hi ? oh : hi;
-  }
+  lo = wave_min(lo);
+  hi = wave_max(hi);
   if (lane == 0) {
     s_lo[wave] = lo;
     s_hi[wave] = hi;
@@ -793,7 +894,9 @@ struct BatchArgs {
   unsigned int* abort_word;
   unsigned long long* trace;          // optional: block 0's phase stamps, kTracePts per pod
 };
-constexpr int kTracePts = 16;   // 8 phase stamps + score_node sub-steps (wave 0 of block 0)
+constexpr int kTracePts = 16;   // 9 phase stamps per pod (block 0), padded
+constexpr int kReqWords = sizeof(yoda_dev_req_t) / 4;
+static_assert(sizeof(yoda_dev_req_t) % 4 == 0 && kReqWords <= 64, "req fits one wave");
 
 __device__ __forceinline__ gu64* slot_ptr(const BatchArgs& a, uint32_t tag, int blk) {
   return (gu64*)(a.slots + ((size_t)(tag & 1u) * kMaxGrid + blk) * kRecStride);
@@ -846,30 +949,6 @@ __device__ __forceinline__ bool gather(const BatchArgs& a, uint32_t tag, int G, 
   return *s_fail == 0;
 }
 
-template <typename T>
-__device__ __forceinline__ T wave_max(T v) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const T o = __shfl_xor(v, off, 64);
-    v = o > v ? o : v;
-  }
-  return v;
-}
-template <typename T>
-__device__ __forceinline__ T wave_min(T v) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const T o = __shfl_xor(v, off, 64);
-    v = o < v ? o : v;
-  }
-  return v;
-}
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
 
 #define TRACE(pt)                                                                      \
   do {                                                                                 \
@@ -882,11 +961,10 @@ __global__ __launch_bounds__(kBlock) void k_batch(const BatchArgs a) {
   __shared__ __align__(16) uint32_t s_req[2][sizeof(yoda_dev_req_t) / 4];
   __shared__ unsigned long long s_part[kWaves][16];
   __shared__ unsigned long long s_glob[16];
+  __shared__ uint32_t s_rec[14][kMaxGrid + 4];   // gather-1 records transposed (+4: bank skew)
   __shared__ int s_fail;
   __shared__ bool s_last;
-  static_assert(sizeof(yoda_dev_req_t) % 4 == 0 && sizeof(yoda_dev_req_t) / 4 <= 64, "req fits one wave");
   static_assert(sizeof(yoda_dev_result_t) % 8 == 0, "result copied as u64 words");
-  constexpr int kReqWords = sizeof(yoda_dev_req_t) / 4;
 
   const int npb = a.npb, G = gridDim.x, g = blockIdx.x;
   const int base = g * npb;
@@ -924,16 +1002,23 @@ __global__ __launch_bounds__(kBlock) void k_batch(const BatchArgs a) {
 
   bool ok = true;
   for (int b = 0; b < a.B && ok; ++b) {
-    const yoda_dev_req_t& r = *reinterpret_cast<const yoda_dev_req_t*>(s_req[b & 1]);
+    // the request in scalar registers (block-uniform): one LDS read per word per pod
+    union {
+      yoda_dev_req_t req;
+      uint32_t w[kReqWords];
+    } ru;
+#pragma unroll
+    for (int k = 0; k < kReqWords; ++k) ru.w[k] = __builtin_amdgcn_readfirstlane(s_req[b & 1][k]);
+    const yoda_dev_req_t& r = ru.req;
     const uint32_t tag1 = a.tag0 + 3u * (uint32_t)b, tag2 = tag1 + 1u, tag3 = tag1 + 2u;
     // prefetch request b+1 (lands while this pod's phases run; stored to LDS at the end)
     uint32_t pre = 0;
     if (b + 1 < a.B && tid < kReqWords) pre = reinterpret_cast<const uint32_t*>(a.reqs + b + 1)[tid];
     TRACE(0);
 
-    // ================= phase F: filter + maxima + feasible/reason counts
+    // ================= phase F: filter + maxima + feasible/reason counts → record 1
     {
-      unsigned long long wmx[6] = {1, 1, 1, 1, 1, 1};
+      uint32_t wmx[6] = {1, 1, 1, 1, 1, 1};
       int nfeas = 0;
       int rc[7] = {0, 0, 0, 0, 0, 0, 0};
       for (int j0 = wave * kNodesPerWave; j0 < cnt; j0 += kWaves * kNodesPerWave) {   // wave-uniform
@@ -966,34 +1051,62 @@ __global__ __launch_bounds__(kBlock) void k_batch(const BatchArgs a) {
         for (int w = 0; w < kWaves; ++w) v = tid < 6 ? (s_part[w][tid] > v ? s_part[w][tid] : v) : v + s_part[w][tid];
         store_granule(slot_ptr(a, tag1, g) + tid, tag1, (uint32_t)v);   // ≤ 0xFFFF per u16 half: npb ≤ 256
       }
-      TRACE(1);
+    }
+    TRACE(1);
+
+    // ================= phase A (while record 1 travels): gang search, the yoda terms that
+    // need no maxima (kept in s_raw until phase B), default scores
+    ScoreConsts sc = score_consts(r, nullptr);
+    for (int j0 = wave * kNodesPerWave; j0 < cnt; j0 += kWaves * kNodesPerWave) {
+      const int j = j0 + grp;
+      const bool act = j < cnt && s_feas[j];
+      const uint32_t emask = act ? s_elig[j] : 0u;
+      uint64_t rbase = 0;
+      int64_t total_v = 0;
+      uint32_t mask_v = 0;
+      int32_t quality_v = 0;
+      score_node_a(s_rows + (j < cnt ? j : 0), act, emask, r, sc, s_masks, sub, rbase, total_v, mask_v, quality_v);
+      if (act && sub == 0) {
+        s_raw[j] = (int64_t)rbase;
+        s_total[j] = total_v;
+        s_mask[j] = (uint8_t)mask_v;
+        s_quality[j] = quality_v;
+      }
+    }
+    TRACE(2);
+
+    // ================= gather 1: global maxima, feasible and reason counts
+    {
       uint32_t v[kRec1];
       if (!gather<kRec1>(a, tag1, G, v, &s_fail)) {
         ok = false;
         break;
       }
-      // block-wide reduction of the G records (threads ≥ G hold identities): 6 maxima, the
-      // feasible count and the 7 reason counts (unpacked: block sums can exceed 16 bits)
-      const bool have = tid < G;
-      unsigned long long red[14];
+      // transpose through LDS (14 fields × G), then 16 threads per field reduce it
+      if (tid < G) {
 #pragma unroll
-      for (int k = 0; k < 6; ++k) red[k] = wave_max<unsigned long long>(have ? v[k] : 1ull);
-      red[6] = wave_sum<unsigned long long>(have ? v[6] : 0ull);
+        for (int k = 0; k < 7; ++k) s_rec[k][tid] = v[k];
 #pragma unroll
-      for (int q = 0; q < 7; ++q) {
-        const uint32_t w = have ? v[7 + q / 2] : 0u;
-        red[7 + q] = wave_sum<unsigned long long>((q & 1) ? (w >> 16) : (w & 0xFFFFu));
-      }
-      __syncthreads();   // every wave is done reading s_part (phase F partials)
-      if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < 14; ++k) s_part[wave][k] = red[k];
+        for (int q = 0; q < 7; ++q) s_rec[7 + q][tid] = (q & 1) ? (v[7 + q / 2] >> 16) : (v[7 + q / 2] & 0xFFFFu);
       }
       __syncthreads();
-      if (tid < 14) {
-        unsigned long long m = tid < 6 ? 1 : 0;
-        for (int w = 0; w < kWaves; ++w) m = tid < 6 ? (s_part[w][tid] > m ? s_part[w][tid] : m) : m + s_part[w][tid];
-        s_glob[tid] = m;
+      const int f = tid >> 4, seg = tid & 15;
+      if (f < 14) {   // waves 0..3 cover fields 0..15; f is uniform per 16 lanes
+        const bool is_max = f < 6;
+        uint32_t acc = is_max ? 1u : 0u;
+        for (int t = seg; t < G; t += 16) {
+          const uint32_t x = s_rec[f][t];
+          acc = is_max ? (x > acc ? x : acc) : acc + x;
+        }
+        // the 16 lanes of a field are one DPP row (f is row-uniform)
+        if (is_max) {
+          acc = group_reduce(acc, OpMax{});
+          acc = OpMax{}(acc, dpp<kDppRowMirror>(acc));
+        } else {
+          acc = group_reduce(acc, OpSum{});
+          acc += dpp<kDppRowMirror>(acc);
+        }
+        if (seg == 0) s_glob[f] = acc;
       }
       __syncthreads();
     }
@@ -1001,11 +1114,11 @@ __global__ __launch_bounds__(kBlock) void k_batch(const BatchArgs a) {
 #pragma unroll
     for (int q = 0; q < 7; ++q) reasons7[q] = (int)s_glob[7 + q];
     const int nf = (int)s_glob[6];
-    TRACE(2);
-
-    // ================= phase S: scores + gang search + raw lo/hi
     const uint64_t gmx[6] = {s_glob[0], s_glob[1], s_glob[2], s_glob[3], s_glob[4], s_glob[5]};
-    const ScoreConsts sc = score_consts(r, gmx);
+    score_consts_maxima(sc, gmx);
+    TRACE(3);
+
+    // ================= phase B: maxima-normalised card metrics → raw scores, lo/hi → record 2
     unsigned long long glo = ULLONG_MAX, ghi = 0;
     {
       unsigned long long lo = ULLONG_MAX, hi = 0;
@@ -1013,18 +1126,9 @@ __global__ __launch_bounds__(kBlock) void k_batch(const BatchArgs a) {
         const int j = j0 + grp;
         const bool act = j < cnt && s_feas[j];
         const uint32_t emask = act ? s_elig[j] : 0u;
-        int64_t raw_v = 0, total_v = 0;
-        uint32_t mask_v = 0;
-        int32_t quality_v = 0;
-        unsigned long long* dbg = (a.trace && g == 0 && tid == 0 && j0 == 0) ? a.trace + (size_t)b * kTracePts + 8 : nullptr;
-        score_node(s_rows + (j < cnt ? j : 0), act, emask, r, sc, s_masks, sub, raw_v, total_v, mask_v, quality_v, lo,
-                   hi, dbg);
-        if (act && sub == 0) {
-          s_raw[j] = raw_v;
-          s_total[j] = total_v;
-          s_mask[j] = (uint8_t)mask_v;
-          s_quality[j] = quality_v;
-        }
+        const uint64_t rbase = (act && sub == 0) ? (uint64_t)s_raw[j] : 0;
+        const int64_t raw_v = score_node_b(s_rows + (j < cnt ? j : 0), act, emask, sc, sub, rbase, lo, hi);
+        if (act && sub == 0) s_raw[j] = raw_v;
       }
       lo = wave_min(lo);
       hi = wave_max(hi);
@@ -1042,7 +1146,7 @@ __global__ __launch_bounds__(kBlock) void k_batch(const BatchArgs a) {
         const unsigned long long x = tid < 2 ? blo : bhi;
         store_granule(slot_ptr(a, tag2, g) + tid, tag2, (tid & 1) ? (uint32_t)(x >> 32) : (uint32_t)x);
       }
-      TRACE(3);
+      TRACE(4);
       uint32_t v[kRec2];
       if (!gather<kRec2>(a, tag2, G, v, &s_fail)) {
         ok = false;
@@ -1064,20 +1168,21 @@ __global__ __launch_bounds__(kBlock) void k_batch(const BatchArgs a) {
       }
       __syncthreads();
     }
+    TRACE(5);
 
-    TRACE(4);
-    // ================= phase Sel: normalise + block argmax → global best key
+    // ================= phase Sel: normalise + block argmax → record 3 → global best key
     unsigned long long key = 0;
     {
       const int64_t hi = (int64_t)ghi;
       int64_t lo = (int64_t)glo;
       if (hi == lo) --lo;
       const uint64_t den = (uint64_t)hi - (uint64_t)lo;
+      const double rden = rcp64((double)den);
       unsigned long long best = 0;
       for (int j = tid; j < cnt; j += kBlock) {
         if (!s_feas[j]) continue;
         int64_t f = s_total[j];
-        if (sc.yoda_s) f += (int64_t)udiv(((uint64_t)s_raw[j] - (uint64_t)lo) * 100ull, den) * r.w_yoda;
+        if (sc.yoda_s) f += (int64_t)udiv_r(((uint64_t)s_raw[j] - (uint64_t)lo) * 100ull, den, rden) * r.w_yoda;
         const uint32_t p = ((uint32_t)(base + j) * r.perm_mul + r.perm_add) & 0xFFFFFFu;
         const unsigned long long k = ((unsigned long long)f << 24) | p;
         best = k > best ? k : best;
@@ -1090,7 +1195,7 @@ __global__ __launch_bounds__(kBlock) void k_batch(const BatchArgs a) {
         for (int w = 0; w < kWaves; ++w) bb = s_part[w][0] > bb ? s_part[w][0] : bb;
         store_granule(slot_ptr(a, tag3, g) + tid, tag3, tid ? (uint32_t)(bb >> 32) : (uint32_t)bb);
       }
-      TRACE(5);
+      TRACE(6);
       uint32_t v[kRec3];
       if (!gather<kRec3>(a, tag3, G, v, &s_fail)) {
         ok = false;
@@ -1103,8 +1208,8 @@ __global__ __launch_bounds__(kBlock) void k_batch(const BatchArgs a) {
       __syncthreads();
       for (int w = 0; w < kWaves; ++w) key = s_part[w][0] > key ? s_part[w][0] : key;
     }
+    TRACE(7);
 
-    TRACE(6);
     // ================= winner: its owner publishes the result and assumes the pod
     int node = -1;
     if (nf > 0) {
@@ -1150,7 +1255,7 @@ __global__ __launch_bounds__(kBlock) void k_batch(const BatchArgs a) {
     }
     if (b + 1 < a.B && tid < kReqWords) s_req[(b + 1) & 1][tid] = pre;
     __syncthreads();
-    TRACE(7);
+    TRACE(8);
   }
 
   // ---- epilogue: dirty rows back to the table; the last block hands the results to the host
@@ -1569,7 +1674,8 @@ int yoda_dev_schedule_batch(void* p, int n, int B, const yoda_dev_req_t* reqs, y
 
 // Phase trace of the persistent kernel (benchmarks): on = 1 records, per pod of the last
 // k_batch chunk, block 0's s_memrealtime stamps (100 MHz) at kTracePts phase boundaries:
-// start, F computed, F gathered, S computed, S gathered, Sel computed, Sel gathered, end.
+// start, F published, A computed, F gathered, B published, B gathered, Sel published, Sel
+// gathered, end.
 // Returns the number of pods copied to `out` (kTracePts words each), or the grid/npb of the
 // last launch when out is NULL (grid << 16 | npb).
 int yoda_dev_batch_trace(void* p, int on, unsigned long long* out, int max_pods) {

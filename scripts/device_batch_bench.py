@@ -26,10 +26,11 @@ def run(nodes: int, mode: str, pods: int, batch: int, trace: bool = False, busy:
     ds.enable(eng, 0, capacity=nodes + 16, min_nodes=1)
     os.environ.pop("YODA_DEV_PERSIST", None)
     rng = random.Random(1)
-    reqs = []
+    reqs, ks = [], []
     for k in range(pods):
         pi, req = ds.random_request(eng, rng, f"{mode}-{nodes}-{k}")
         reqs.append((pi.num_id, req))
+        ks.append(pi.gpu.number if pi.gpu.has_number else 1)
     # warm up (kernels, first full-table upload)
     eng.schedule_batch([p for p, _ in reqs[:8]], [r for _, r in reqs[:8]])
     t0 = time.perf_counter()
@@ -53,6 +54,11 @@ def run(nodes: int, mode: str, pods: int, batch: int, trace: bool = False, busy:
             tr = ds.read_batch_trace(eng)
             if tr:
                 extra["phase_us_mean"] = {k: round(sum(x[k] for x in tr) / len(tr), 2) for k in tr[0]}
+                by_k: dict = {}
+                for x, kk in zip(tr, ks[8:8 + len(tr)]):
+                    by_k.setdefault(kk, []).append(x["score_a"])
+                extra["score_a_us_by_gpus"] = {str(kk): [len(v), round(sum(v) / len(v), 2)]
+                                               for kk, v in sorted(by_k.items())}
             ds.batch_trace(eng, False)
     return {**extra, "nodes": nodes, "mode": mode, "pods": n, "batch": batch if mode.startswith("batch") else 1,
             "us_per_pod": round(dt / n * 1e6, 1), "pods_per_s": round(n / dt, 1),

@@ -22,7 +22,10 @@ def declare(lib: ctypes.CDLL) -> None:
     lib.yoda_dev_batch_trace.restype = ctypes.c_int
 
 
-TRACE_PHASES = ("filter", "gather1", "score", "gather2", "select", "gather3", "publish")
+# k_batch phases (block 0's stamps): filter → record 1 out; part A of scoring (gang search,
+# maxima-free terms) while record 1 travels; gather 1 (maxima); part B (normalised metrics)
+# → record 2 out; gather 2 (raw lo/hi); select → record 3 out; gather 3 (winner); publish
+TRACE_PHASES = ("filter", "score_a", "gather1", "score_b", "gather2", "select", "gather3", "publish")
 
 
 def batch_trace(engine, on: bool = True) -> None:
@@ -51,14 +54,7 @@ def read_batch_trace(engine, max_pods: int = 256) -> list[dict]:
     out = []
     for b in range(max(m, 0)):
         t = [buf[b * W + k] for k in range(W)]
-        d = {ph: (t[k + 1] - t[k]) / 100.0 for k, ph in enumerate(TRACE_PHASES)}
-        # score_node sub-steps of wave 0 (tables loaded → gang → raw score → defaults)
-        sub = [t[2], t[8], t[9], t[10], t[11]]
-        if all(sub):
-            for k, ph in enumerate(("s.tables", "s.gang", "s.raw", "s.defaults")):
-                d[ph] = (sub[k + 1] - sub[k]) / 100.0
-            d["s.reduce"] = (t[3] - t[11]) / 100.0
-        out.append(d)
+        out.append({ph: (t[k + 1] - t[k]) / 100.0 for k, ph in enumerate(TRACE_PHASES)})
     return out
 
 
