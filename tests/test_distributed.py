@@ -43,3 +43,22 @@ def test_allreduce_probe_gloo():
     rows = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert [x["bytes"] for x in rows] == [65536, 1 << 20]
     assert all(x["world"] == 2 and x["busbw_gbps"] > 0 for x in rows)
+
+
+def test_gang_validation_harness_picks_low_load_set_gloo():
+    """parallel/validate_gangs under torch.distributed.run (4 gloo ranks, FakeBackend with
+    an injected hot xGMI link): the engine's placement of a 2-GPU pod avoids the loaded
+    pair, agrees with the Python reference objective, the worst-ranked set is the loaded
+    pair, and rank 0 emits one JSON line with both sets' all-reduce bandwidth."""
+    r = _torchrun(["-m", "yoda_scheduler_amd.parallel.validate_gangs", "--fake", "--k", "2",
+                   "--fake-load", "0-1:0.9", "--sizes", "64K", "--iters", "2"], nproc=4)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["k"] == 2 and d["world"] == 4 and d["engine_matches_spec"] is True
+    assert d["best"] == [2, 3] and d["worst"] == [0, 1]
+    assert d["best_objective"] < d["worst_objective"] and d["best_link_bad"] < d["worst_link_bad"]
+    assert d["sampled_link_load"]["0-1"] == 0.9
+    assert d["busbw_best"][0]["world"] == 2 and d["busbw_worst"][0]["busbw_gbps"] > 0
+    assert d["busbw_ratio_best_over_worst"] > 0 and "no xGMI" in d["backend"]

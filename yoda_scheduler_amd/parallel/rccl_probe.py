@@ -27,12 +27,12 @@ def parse_size(s: str) -> int:
 
 
 def allreduce_bandwidth(sizes: Sequence[int], iters: int = 20, warmup: int = 5, dtype: str = "bfloat16",
-                        device: Optional[str] = None) -> list[dict]:
-    """Run inside an initialised process group; returns one dict per size (rank-local timing,
-    max over ranks)."""
+                        device: Optional[str] = None, group=None) -> list[dict]:
+    """Run inside an initialised process group (every rank of ``group``, default the whole
+    world); returns one dict per size (rank-local timing, max over the group's ranks)."""
     import torch
     import torch.distributed as dist
-    world = dist.get_world_size()
+    world = dist.get_world_size(group)
     dev = torch.device(device) if device else (torch.device("cuda", torch.cuda.current_device())
                                                 if torch.cuda.is_available() else torch.device("cpu"))
     dt = getattr(torch, dtype)
@@ -42,18 +42,18 @@ def allreduce_bandwidth(sizes: Sequence[int], iters: int = 20, warmup: int = 5, 
         n = max(1, nbytes // esz)
         x = torch.ones(n, dtype=dt, device=dev)
         for _ in range(warmup):
-            dist.all_reduce(x)
+            dist.all_reduce(x, group=group)
         if dev.type == "cuda":
             torch.cuda.synchronize()
-        dist.barrier()
+        dist.barrier(group=group)
         t0 = time.perf_counter()
         for _ in range(iters):
-            dist.all_reduce(x)
+            dist.all_reduce(x, group=group)
         if dev.type == "cuda":
             torch.cuda.synchronize()
         el = time.perf_counter() - t0
         t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
         el = float(t.item())
         algbw = n * esz * iters / el / 1e9
         out.append({"bytes": n * esz, "world": world, "us_per_iter": round(el / iters * 1e6, 2),
