@@ -17,7 +17,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-async def run(a) -> dict:
+async def run(a) -> list:
     from yoda_scheduler_amd.bench.harness import HttpShard
     from yoda_scheduler_amd.bench.workloads import make_workload
     w = make_workload(a.config)
@@ -27,76 +27,122 @@ async def run(a) -> dict:
     sched = sh.sched
     for i in range(a.warmup):
         await sh.burst(f"w{i}")
-    arrivals: list[float] = []
-    q = sched.queue
-    orig_add = q.add
+    for i in range(a.repeat - 1):      # extra untimed bursts: steady state like bench.py's later steps
+        await sh.burst(f"x{i}")
+    outs = []
+    for rep in range(a.bursts):
+        arrivals: list[float] = []
+        q = sched.queue
+        orig_add = q.add
 
-    def add(pi, *args, **kw):
-        arrivals.append(time.perf_counter())
-        return orig_add(pi, *args, **kw)
-    q.add = add
-    pops: list = []
-    orig_pb = q.pop_batch
+        def add(pi, *args, **kw):
+            arrivals.append(time.perf_counter())
+            return orig_add(pi, *args, **kw)
+        q.add = add
+        pops: list = []
+        orig_pb = q.pop_batch
 
-    def pop_batch(n, *args, **kw):
-        t = time.perf_counter()
-        out = orig_pb(n, *args, **kw)
-        pops.append((t, len(out), len(q._active_entries)))
-        return out
-    q.pop_batch = pop_batch
-    eng_calls: list = []
-    orig_sb = sched.engine.schedule_batch
-
-    class _EngProxy:      # times every engine batch call (any thread)
-        def __getattr__(self, k):
-            return getattr(eng, k)
-
-        def schedule_batch(self, ids, reqs):
+        def pop_batch(n, *args, **kw):
             t = time.perf_counter()
-            r = orig_sb(ids, reqs)
-            eng_calls.append((t, time.perf_counter(), len(ids)))
-            return r
-    eng = sched.engine
-    sched.engine = _EngProxy()
-    tr = sched.tracer
-    dev_trace = a.device_trace and sched.engine.device_enabled
-    if dev_trace:
-        from yoda_scheduler_amd.ops import device_scorer as ds
-        ds.batch_trace(sched.engine, True)
-    t0 = time.perf_counter()
-    t0_us = tr.now_us()
-    res = await sh.burst("s0")
-    t1 = time.perf_counter()
-    spans = list(tr.chrome_trace()["traceEvents"])
-    batches = [(round((e["ts"] - t0_us) / 1000, 3), round(e.get("dur", 0) / 1000, 3), e["args"].get("pods"))
-               for e in spans if e["name"] == "native_batch"]
-    binds = sorted((e["ts"] + e.get("dur", 0) - t0_us) / 1000 for e in spans if e["name"] == "bind"
-                   and e["ts"] + e.get("dur", 0) >= t0_us)
-    batches = [b for b in batches if b[0] + b[1] >= 0]
-    # everything relative to the first pod reaching the queue (the burst's reset phase and
-    # the create request precede it)
-    ta = min(arrivals) if arrivals else t0
-    t0_us += (ta - t0) * 1e6
-    arr = sorted((x - ta) * 1000 for x in arrivals)
-    calls_rel = [(round((t - ta) * 1000, 3), round((e - t) * 1000, 3), n) for t, e, n in eng_calls if e >= ta]
-    pops_rel = [(round((t - ta) * 1000, 3), n, left) for t, n, left in pops if t >= ta]
-    pct = lambda xs, p: round(xs[min(len(xs) - 1, int(p * (len(xs) - 1)))], 3) if xs else None
-    out = {"config": a.config, "batch": a.batch, "pods": res.pods, "bound": res.bound,
-           "wall_ms": round((t1 - t0) * 1000, 3), "apiserver_elapsed_ms": round(res.elapsed_s * 1000, 3),
-           "arrival_ms": {"first": pct(arr, 0), "p50": pct(arr, .5), "last": pct(arr, 1)},
-           "bind_done_ms": {"first": pct(binds, 0), "p50": pct(binds, .5), "last": pct(binds, 1)},
-           "pop_batch(ms,popped,left)": pops_rel[:20],
-           "engine_schedule_batch(ms,dur_ms,pods)": calls_rel[:20],
-           "device_cycles": sched.engine.device_cycles}
-    if dev_trace:
-        trc = ds.read_batch_trace(sched.engine)
-        if trc:
-            out["k_batch_last_chunk"] = {"pods": len(trc), "grid_npb": ds.batch_geometry(sched.engine),
-                                         "phase_us_mean": {k: round(sum(x[k] for x in trc) / len(trc), 2)
-                                                           for k in trc[0]}}
-    sched.engine = eng
+            out = orig_pb(n, *args, **kw)
+            pops.append((t, len(out), len(q._active_entries)))
+            return out
+        q.pop_batch = pop_batch
+        eng_calls: list = []
+        orig_sb = sched.engine.schedule_batch
+
+        class _EngProxy:      # times every engine batch call (any thread)
+            def __getattr__(self, k):
+                return getattr(eng, k)
+
+            def schedule_batch(self, ids, reqs):
+                t = time.perf_counter()
+                r = orig_sb(ids, reqs)
+                eng_calls.append((t, time.perf_counter(), len(ids)))
+                return r
+        eng = sched.engine
+        sched.engine = _EngProxy()
+        # bind round trips: submit (native transport) → completion callback on the loop
+        submits: dict = {}
+        rtts: list = []
+        nat = sched.native
+        orig_bind = nat.bind if nat is not None else None
+
+        def bind(ns, name, uid, node, ann, cb, timeout=0.0):
+            submits[uid] = time.perf_counter()
+
+            def done(status, body, uid=uid, cb=cb):
+                t = time.perf_counter()
+                rtts.append((submits.get(uid, t), t))
+                return cb(status, body)
+            return orig_bind(ns, name, uid, node, ann, done, timeout)
+        if nat is not None:
+            nat.bind = bind
+        tr = sched.tracer
+        dev_trace = a.device_trace and sched.engine.device_enabled
+        if dev_trace:
+            from yoda_scheduler_amd.ops import device_scorer as ds
+            ds.batch_trace(sched.engine, True)
+        import gc
+        gc_pauses: list = []
+        gc_t = [0.0]
+
+        def gc_cb(phase, info):
+            if phase == "start":
+                gc_t[0] = time.perf_counter()
+            else:
+                gc_pauses.append((info.get("generation"), time.perf_counter() - gc_t[0], info.get("collected", 0)))
+        gc.callbacks.append(gc_cb)
+        t0 = time.perf_counter()
+        t0_us = tr.now_us()
+        res = await sh.burst(f"s{rep}")
+        t1 = time.perf_counter()
+        gc.callbacks.remove(gc_cb)
+        spans = list(tr.chrome_trace()["traceEvents"])
+        batches = [(round((e["ts"] - t0_us) / 1000, 3), round(e.get("dur", 0) / 1000, 3), e["args"].get("pods"))
+                   for e in spans if e["name"] == "native_batch"]
+        binds = sorted((e["ts"] + e.get("dur", 0) - t0_us) / 1000 for e in spans if e["name"] == "bind"
+                       and e["ts"] + e.get("dur", 0) >= t0_us)
+        batches = [b for b in batches if b[0] + b[1] >= 0]
+        # everything relative to the first pod reaching the queue (the burst's reset phase and
+        # the create request precede it)
+        ta = min(arrivals) if arrivals else t0
+        t0_us += (ta - t0) * 1e6
+        arr = sorted((x - ta) * 1000 for x in arrivals)
+        calls_rel = [(round((t - ta) * 1000, 3), round((e - t) * 1000, 3), n) for t, e, n in eng_calls if e >= ta]
+        pops_rel = [(round((t - ta) * 1000, 3), n, left) for t, n, left in pops if t >= ta]
+        pct = lambda xs, p: round(xs[min(len(xs) - 1, int(p * (len(xs) - 1)))], 3) if xs else None
+        out = {"config": a.config, "batch": a.batch, "pods": res.pods, "bound": res.bound,
+               "wall_ms": round((t1 - t0) * 1000, 3), "apiserver_elapsed_ms": round(res.elapsed_s * 1000, 3),
+               "arrival_ms": {"first": pct(arr, 0), "p50": pct(arr, .5), "last": pct(arr, 1)},
+               "bind_done_ms": {"first": pct(binds, 0), "p50": pct(binds, .5), "last": pct(binds, 1)},
+               "pop_batch(ms,popped,left)": pops_rel[:20],
+               "engine_schedule_batch(ms,dur_ms,pods)": calls_rel[:20],
+               "gc": {"collections": len(gc_pauses), "pause_ms_total": round(sum(p[1] for p in gc_pauses) * 1000, 3),
+                      "pause_ms_max": round(max((p[1] for p in gc_pauses), default=0) * 1000, 3),
+                      "by_generation": {str(g): sum(1 for p in gc_pauses if p[0] == g) for g in (0, 1, 2)}},
+               "latency_ms": {"p50": round(sorted(res.latencies_s)[len(res.latencies_s) // 2] * 1000, 3),
+                              "p99": round(sorted(res.latencies_s)[int(len(res.latencies_s) * 0.99)] * 1000, 3)}
+               if res.latencies_s else None,
+               "device_cycles": sched.engine.device_cycles}
+        if dev_trace:
+            trc = ds.read_batch_trace(sched.engine)
+            if trc:
+                out["k_batch_last_chunk"] = {"pods": len(trc), "grid_npb": ds.batch_geometry(sched.engine),
+                                             "phase_us_mean": {k: round(sum(x[k] for x in trc) / len(trc), 2)
+                                                               for k in trc[0]}}
+        out["burst"] = rep
+        if nat is not None:
+            nat.bind = orig_bind
+            rr = sorted((e - s0) * 1000 for s0, e in rtts)
+            subs = sorted((s0 - ta) * 1000 for s0, _ in rtts)
+            out["bind_submit_ms"] = {"first": pct(subs, 0), "p50": pct(subs, .5), "last": pct(subs, 1)}
+            out["bind_rtt_ms"] = {"p50": pct(rr, .5), "p90": pct(rr, .9), "max": pct(rr, 1)}
+        outs.append(out)
+        sched.engine = eng
+        q.add, q.pop_batch = orig_add, orig_pb
     await sh.stop()
-    return out
+    return outs
 
 
 def main() -> int:
@@ -106,13 +152,16 @@ def main() -> int:
     ap.add_argument("--device", default="auto")
     ap.add_argument("--overlap", default="auto")
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--repeat", type=int, default=1, help="untimed bursts before the traced ones")
+    ap.add_argument("--bursts", type=int, default=1, help="consecutive traced bursts (one JSON line each)")
     ap.add_argument("--device-trace", action="store_true", help="k_batch phase stamps of the last chunk")
     a = ap.parse_args()
     try:
         import torch  # noqa: F401 - share torch's HIP runtime, as bench.py does
     except ImportError:
         pass
-    print(json.dumps(asyncio.run(run(a))), flush=True)
+    for o in asyncio.run(run(a)):
+        print(json.dumps(o), flush=True)
     return 0
 
 

@@ -190,3 +190,23 @@ def test_persistent_batch_kernel_matches_launch_chain(require_gpu, n, pods):
         pi, req = ds.random_request(a, rng2, f"pk-after-{n}-{k}")
         assert not ds.compare_cycle(a, req)
         a.schedule(pi.num_id, req, True)
+
+
+def test_fused_select_multi_pass_parity(require_gpu):
+    """the fused select (k_score's last block normalises + argmaxes every node)
+    walks more than kBlock·kSelBatch = 2048 nodes only when YODA_DEV_FUSE_MAX lifts the
+    default cap; force it with 4100 nodes (not a multiple of 256: partial tail batch) and
+    check per-pod device cycles against the CPU engine."""
+    import os
+    from yoda_scheduler_amd.ops import device_scorer as ds
+    os.environ["YODA_DEV_FUSE_MAX"] = "1000000"
+    try:
+        eng = _engine(4100, 41)
+    finally:
+        os.environ.pop("YODA_DEV_FUSE_MAX", None)
+    rng = random.Random(41)
+    for k in range(25):
+        pi, req = ds.random_request(eng, rng, f"fuse-{k}")
+        assert not ds.compare_cycle(eng, req), k
+        eng.schedule(pi.num_id, req, True)
+    assert eng.device_fallbacks == 0

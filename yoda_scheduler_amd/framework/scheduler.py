@@ -140,6 +140,8 @@ class Scheduler:
         self._tasks: list[asyncio.Task] = []
         self._engine_exec = None          # worker thread of schedule_batch_overlapped
         self._inflight: collections.deque = collections.deque()   # (fw, run, cycle, t0, future) on that worker
+        self._ann_memo: dict = {}          # _bind_annotations memo, valid for one cache generation
+        self._ann_gen = -1
         self.informers: dict[str, Informer] = {}
         self.scheduled = 0
         self.failed = 0
@@ -780,9 +782,8 @@ class Scheduler:
     def _enqueue_bind(self, item: tuple) -> None:
         fw = item[0]
         if self.native is not None and self._native_direct(fw, item[2]):
-            from ..plugins.defaults import bind_annotations
             pi, node = item[2], item[3]
-            self.native.bind(pi.namespace, pi.name, pi.uid, node, bind_annotations(pi, self.cache.scvs, node),
+            self.native.bind(pi.namespace, pi.name, pi.uid, node, self._bind_annotations(pi, node),
                              functools.partial(self._native_bind_done, item, time.perf_counter()),
                              self.bind_timeout)
             return
@@ -793,6 +794,26 @@ class Scheduler:
             if not fut.done():
                 fut.set_result(None)
                 break
+
+    def _bind_annotations(self, pi: PodInfo, node: str) -> list:
+        """The Binding's GPU annotations (plugins.defaults.bind_annotations), memoised per
+        (node, GPU set, HBM request) until the cache's node/Scv generation moves: a burst
+        repeats a handful of placements per node."""
+        from ..plugins.defaults import bind_annotations
+        cards = getattr(pi, "assigned_cards", None)
+        if cards is None:
+            return []
+        gen = self.cache.generation
+        if self._ann_gen != gen:
+            self._ann_memo.clear()
+            self._ann_gen = gen
+        key = (node, tuple(cards), pi.gpu.memory if pi.gpu.has_memory else -1)
+        ann = self._ann_memo.get(key)
+        if ann is None:
+            if len(self._ann_memo) > 65536:
+                self._ann_memo.clear()
+            ann = self._ann_memo[key] = bind_annotations(pi, self.cache.scvs, node)
+        return ann
 
     def _native_bind_done(self, item: tuple, tb: float, status: int, body: bytes) -> None:
         """Completion of a native binding POST (runs from the transport's eventfd callback)."""
