@@ -10,7 +10,7 @@ import importlib
 import threading
 
 from ..models.pod import NodeInfo, PodInfo
-from ..models.scv import HEALTHY, Scv
+from ..models.scv import LazyLinks, HEALTHY, Scv
 
 _lock = threading.Lock()
 _core = None
@@ -68,15 +68,26 @@ def link_matrix(scv: Scv) -> tuple[int, list[int]]:
     for a in range(nphys):
         q[a * nphys + a] = 10000
     for c in cards:
-        for l in c.xgmi:
-            if 0 <= l.peer < nphys:
-                v = 0 if not l.up else int(round(XGMI_IDLE_QUALITY * (1.0 - min(max(l.load, 0.0), 1.0))))
-                q[c.phys * nphys + l.peer] = v
+        row = c.phys * nphys
+        links = c.xgmi
+        if isinstance(links, LazyLinks):      # decoded JSON: read the dicts, build no objects
+            for d in links.raw:
+                peer = int(d.get("peer", 0))
+                if 0 <= peer < nphys:
+                    load = float(d.get("load", 0.0))
+                    q[row + peer] = 0 if not d.get("up", True) else \
+                        int(round(XGMI_IDLE_QUALITY * (1.0 - (0.0 if load < 0.0 else 1.0 if load > 1.0 else load))))
+        else:
+            for l in links:
+                if 0 <= l.peer < nphys:
+                    v = 0 if not l.up else int(round(XGMI_IDLE_QUALITY * (1.0 - min(max(l.load, 0.0), 1.0))))
+                    q[row + l.peer] = v
     # symmetrise with the worse direction (a ring uses both)
     for a in range(nphys):
+        ra = a * nphys
         for b in range(a + 1, nphys):
-            v = min(q[a * nphys + b], q[b * nphys + a])
-            q[a * nphys + b] = q[b * nphys + a] = v
+            x, y = q[ra + b], q[b * nphys + a]
+            q[ra + b] = q[b * nphys + a] = x if x < y else y
     return nphys, q
 
 
