@@ -140,13 +140,27 @@ def main(argv=None) -> int:
         for i in range(a.warmup):
             loop.run_until_complete(shards[i].burst(f"w{i}"))
 
+        def api_cpu() -> float:
+            """CPU seconds of the separate apiserver process (http transport), if measurable."""
+            proc = getattr(shards[0], "proc", None)
+            if proc is None:
+                return 0.0
+            try:
+                import psutil
+                t = psutil.Process(proc.pid).cpu_times()
+                return t.user + t.system
+            except Exception:  # noqa: BLE001 - psutil missing / process gone
+                return float("nan")
+
         sync()
+        a0 = api_cpu()
         t0 = time.perf_counter()
         c0 = time.process_time()
         results = [loop.run_until_complete(shards[a.warmup + i].burst(f"s{i}")) for i in range(a.steps)]
         sync()
         elapsed = time.perf_counter() - t0
         cpu_s = time.process_time() - c0     # this rank's process: scheduler (+ in-process apiserver)
+        api_s = api_cpu() - a0
 
         uniq = {id(x): x for x in shards}.values()
         device_cycles = sum(s.sched.engine.device_cycles for s in uniq)
@@ -181,6 +195,9 @@ def main(argv=None) -> int:
             # process CPU time per bound pod, summed over ranks: with --transport http this is
             # the scheduler alone (the apiserver is another process); inproc includes the fake apiserver
             "cpu_us_per_pod": round(cpu_s / bound * 1e6, 2) if bound else None,
+            # the fake apiserver's own CPU (separate process, http transport; rank 0's)
+            **({"apiserver_cpu_us_per_pod": round(api_s / (bound / max(world, 1)) * 1e6, 2)
+                if bound and api_s == api_s else None} if transport == "http" else {}),
             "pods_bound": bound,
             "pods_unschedulable": unsched,
             "device_cycles": device_cycles,

@@ -569,3 +569,34 @@ def test_partitioned_node_gangs_stay_on_one_physical_gpu():
     # (scv/memory pods may share a GPU, so gangs may land on the same physical device)
     assert all(len(p) == 1 for p in phys.values()), (out, phys)
     assert len(out["eight"]) == 8 and len(set(out["eight"])) == 8
+
+
+def test_burst_cost_scales_linearly():
+    """Regression guard for verdict r1 #9: a 5000-pod burst costs at most 2× per pod what a
+    1000-pod burst does (in-process transport, same 4-node cluster, CPU time of the
+    process). Measured on MI355X hosts: ≈1.25× (working-set cost, no O(n) stage)."""
+    from yoda_scheduler_amd.bench.harness import Shard
+    from yoda_scheduler_amd.bench.workloads import make_workload
+
+    def per_pod(n_pods: int) -> float:
+        w = make_workload(5)
+        w.pods = w.pods[:n_pods]
+
+        async def go():
+            s = Shard(w, events=False)
+            await s.start()
+            await s.burst("warm")
+            s2 = Shard(w, events=False, seed=1)
+            await s2.start()
+            c0 = time.process_time()
+            r = await s2.burst("t")
+            dt = time.process_time() - c0
+            await s.stop()
+            await s2.stop()
+            assert r.bound == n_pods
+            return dt / n_pods
+        return asyncio.run(go())
+
+    small = min(per_pod(1000) for _ in range(2))
+    big = per_pod(5000)
+    assert big < 2.0 * small, (big * 1e6, small * 1e6)
