@@ -268,6 +268,8 @@ class NativePodInformer(Informer):
         def on_events(evs) -> None:
             if err:
                 return
+            # _dispatch_native + _call inlined: this loop runs three times per scheduled pod
+            entries, handler = self.entries, self.on_event
             for typ, rv, payload in evs:
                 if typ == "BOOKMARK":
                     if rv:
@@ -284,7 +286,18 @@ class NativePodInformer(Informer):
                     if not done.done():
                         done.set_result((0, b""))
                     return
-                self._dispatch_native(typ, payload)
+                idt = payload.ident()
+                key = idt[0]
+                try:
+                    if typ == "DELETED":
+                        handler("DELETED", payload, idt, entries.pop(key, None))
+                    else:
+                        old = entries.get(key)
+                        entries[key] = (payload, idt)
+                        handler("ADDED" if old is None else "MODIFIED", payload, idt, old)
+                except Exception:  # noqa: BLE001 - isolate handlers: log, count, keep the stream
+                    self.handler_errors += 1
+                    log.exception("informer %s: event handler failed", self.res)
                 if rv:
                     self.resource_version = rv
 

@@ -121,6 +121,7 @@ class NullMetrics:
     """Drop-in no-op for benches that want zero instrumentation overhead."""
 
     def __getattr__(self, name):
+        setattr(self, name, _NULL)       # later lookups hit the instance dict
         return _NULL
 
     def child(self, metric, *labels):
@@ -136,6 +137,16 @@ class _Null:
 
     def __call__(self, *a, **k):
         return self
+
+    # the per-pod calls, as plain methods (no __getattr__ round trip)
+    def observe(self, *a, **k):
+        return None
+
+    def inc(self, *a, **k):
+        return None
+
+    def set(self, *a, **k):
+        return None
 
 
 _NULL = _Null()
