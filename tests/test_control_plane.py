@@ -641,3 +641,50 @@ def test_wait_for_propagates_cancellation_and_fastbind_timeout():
             srv.close()
     assert run(race()) == "cancelled"
     assert run(timeout()) < 2.0
+
+
+def test_scv_engine_view_matches_dataclass_path():
+    """ops.native.scv_engine_view (engine input computed straight from the Scv JSON, the
+    scheduler's per-update path) equals Scv.from_json → card_tuples / compat_card_tuples +
+    link_matrix + the status sums, over randomised objects: missing fields, absent amd
+    blocks, physical ids (partitions), link loads/downs, ECC, health strings, Go-style
+    negative numbers; LazyScv decodes to the same Scv."""
+    import random as _r
+
+    from yoda_scheduler_amd.models.device import make_scv
+    from yoda_scheduler_amd.models.scv import LazyScv, Scv, XgmiLink
+    from yoda_scheduler_amd.ops.native import card_tuples, compat_card_tuples, link_matrix, scv_engine_view
+
+    rng = _r.Random(11)
+    for trial in range(300):
+        s = make_scv(f"n{trial}", update_time=1.7e9 + trial, used_mb=[rng.randint(0, 200_000) for _ in range(8)])
+        for c in s.status.card_list:
+            c.health = rng.choice(["Healthy", "Healthy", "Unhealthy", ""])
+            c.ecc_uncorrectable = rng.choice([0, 0, 0, 2])
+            c.xgmi_links_up = rng.random() > 0.1
+            c.cu_occupancy = rng.choice([0.0, 12.345, 99.99])
+            c.numa_node = rng.choice([0, 1, 3])
+            if trial % 3 == 0:
+                c.physical_id = c.id // 2          # partitions
+            c.xgmi = [XgmiLink(peer=p, load=rng.choice([0.0, 0.2, 0.95, 1.4, -0.1]), up=rng.random() > 0.05)
+                      for p in range(8) if p != c.phys and rng.random() > 0.2]
+        s.status.recompute_sums()
+        obj = s.to_json()
+        if trial % 7 == 0:
+            del obj["status"]["amd"]
+        if trial % 11 == 0:
+            for cj in obj["status"]["cardList"]:
+                cj.pop(rng.choice(list(cj)), None)
+        if trial % 13 == 0:
+            obj["status"]["cardList"][0]["freeMemory"] = -5
+        ref = Scv.from_json(obj)
+        for compat in (False, True):
+            view = scv_engine_view(obj, compat)
+            cards = compat_card_tuples(ref) if compat else card_tuples(ref)
+            st = ref.status
+            want = (cards, st.card_number & (2**64 - 1), st.free_memory_sum & (2**64 - 1),
+                    st.total_memory_sum & (2**64 - 1), float(st.update_time or 0.0), *link_matrix(ref))
+            assert view == want, (trial, compat)
+        lz = LazyScv(obj, scv_engine_view(obj, False))
+        assert lz.is_stale(1.7e9 + trial + 100, 3.0) == ref.is_stale(1.7e9 + trial + 100, 3.0)
+        assert lz.card_number == ref.status.card_number and lz.status.card_list == ref.status.card_list

@@ -21,8 +21,8 @@ from typing import Callable, Optional
 
 from ..models.labels import ANNOTATION_GPUS
 from ..models.pod import PF_REQ_ANTI, NodeInfo, PodInfo
-from ..models.scv import Scv
-from ..ops.native import pod_req, push_node, push_scv
+from ..models.scv import LazyScv, Scv
+from ..ops.native import pod_req, push_node, push_scv, scv_engine_view
 
 
 @dataclass
@@ -107,7 +107,8 @@ class SchedulerCache:
         self.generation += 1
 
     def add_scv(self, obj: dict) -> None:
-        self.set_scv(Scv.from_json(obj))
+        # engine view straight from the JSON; the Scv dataclasses are built only if read
+        self.set_scv(LazyScv(obj, scv_engine_view(obj, self.compat)))
 
     update_scv = add_scv
 

@@ -23,6 +23,7 @@ from typing import Callable, Optional
 
 from ..kube.informer import Informer, NativePodInformer
 from ..models.pod import PodInfo, forget_num_id
+from ..models.scv import LazyScv
 from ..ops.native import core, pod_req
 from ..utils import gctune, klog
 from ..utils.metrics import SchedulerMetrics
@@ -331,9 +332,10 @@ class Scheduler:
         if not rows and self.engine.node_index(name) < 0:
             return None
         scv = self.cache.scvs.get(name)
+        cn = 0 if scv is None else (scv.card_number if isinstance(scv, LazyScv) else scv.status.card_number)
         cards = tuple((g["healthy"], g["free"], max(0, min(g["free"] - g["pending"], g["total"] - g["reserved"])),
                        g["clock"]) for g in rows)
-        return bool(self.cache._stale.get(name)), (scv.status.card_number if scv else 0), cards
+        return bool(self.cache._stale.get(name)), cn, cards
 
     @staticmethod
     def _capacity_grew(b: tuple, a: tuple) -> bool:

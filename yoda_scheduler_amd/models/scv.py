@@ -253,6 +253,42 @@ class Scv:
         return (now - t) * 1000.0 > factor * max(self.update_interval_ms, 1)
 
 
+class LazyScv:
+    """An ``Scv`` as the informer delivered it (decoded JSON), turned into the dataclass
+    tree only when something reads it. The scheduler's per-update path needs neither: the
+    engine view (``engine_view``: card tuples, sums, link matrix — computed straight from the
+    dict by ``ops.native.scv_engine_view``) and the freshness fields are kept here. A 1000-node
+    cluster sends ≈100 Scv updates/s, most of which are never read by anything else."""
+    __slots__ = ("name", "update_time", "update_interval_ms", "card_number", "engine_view", "_obj", "_scv")
+
+    def __init__(self, obj: dict, engine_view) -> None:
+        meta = obj.get("metadata") or {}
+        status = obj.get("status") or {}
+        spec = obj.get("spec") or {}
+        self.name = meta.get("name", "")
+        self.update_time = parse_rfc3339(status.get("updateTime"))
+        self.update_interval_ms = int(spec.get("updateInterval", 1000) or 1000)
+        self.card_number = int(status.get("cardNumber", 0) or 0)
+        self.engine_view = engine_view
+        self._obj = obj
+        self._scv = None
+
+    def decoded(self) -> "Scv":
+        if self._scv is None:
+            self._scv = Scv.from_json(self._obj)
+        return self._scv
+
+    def __getattr__(self, attr):       # status, labels, resource_version, to_json, ...
+        return getattr(self.decoded(), attr)
+
+    def is_stale(self, now: float | None = None, factor: float = 3.0) -> bool:
+        t = self.update_time
+        if t is None:
+            return False
+        now = time.time() if now is None else now
+        return (now - t) * 1000.0 > factor * max(self.update_interval_ms, 1)
+
+
 _rfc_sec = [-1, ""]
 
 

@@ -10,7 +10,7 @@ import importlib
 import threading
 
 from ..models.pod import NodeInfo, PodInfo
-from ..models.scv import LazyLinks, HEALTHY, Scv
+from ..models.scv import HEALTHY, LazyLinks, LazyScv, Scv
 
 _lock = threading.Lock()
 _core = None
@@ -91,12 +91,76 @@ def link_matrix(scv: Scv) -> tuple[int, list[int]]:
     return nphys, q
 
 
-def push_scv(engine, idx: int, scv: Scv, compat: bool, stale: bool = False) -> None:
+_M64 = 0xFFFFFFFFFFFFFFFF
+
+
+def scv_engine_view(obj: dict, compat: bool) -> tuple:
+    """What ``push_scv`` sends the engine for an Scv given as decoded JSON — the card tuples
+    (``card_tuples`` / ``compat_card_tuples``), CardNumber / memory sums, sample time and the
+    link matrix (``link_matrix``) — computed from the dict without building the dataclasses
+    (same field defaults and conversions as ``Scv.from_json``; equivalence pinned by
+    ``tests/test_control_plane.py::test_scv_engine_view_matches_dataclass_path``)."""
+    status = obj.get("status") or {}
+    amd = status.get("amd") or {}
+    amd_cards = {int(c.get("id", i)): c for i, c in enumerate(amd.get("cards") or [])}
+    cards, raw_links = [], []
+    for i, cj in enumerate(status.get("cardList") or []):
+        g = cj.get
+        cid = int(g("id")) if g("id") is not None else 0
+        ext = amd_cards.get(cid) or amd_cards.get(i)
+        v = g("health")
+        health = v if v is not None else HEALTHY
+        num = [int(g(k)) if g(k) is not None else 0
+               for k in ("totalMemory", "freeMemory", "clock", "bandwidth", "core", "power")]
+        if ext:
+            e = ext.get
+            phys = int(ext.get("physicalId", cid))
+            numa = e("numaNode") if e("numaNode") is not None else 0
+            occ = e("cuOccupancy") if e("cuOccupancy") is not None else 0.0
+            ecc = e("eccUncorrectable") if e("eccUncorrectable") is not None else 0
+            up = e("xgmiLinksUp") if e("xgmiLinksUp") is not None else True
+            raw_links.append((phys, ext.get("xgmi") or []))
+        else:
+            phys, numa, occ, ecc, up = cid, 0, 0.0, 0, True
+            raw_links.append((phys, []))
+        healthy = health == HEALTHY if compat else (health == HEALTHY and ecc == 0 and bool(up))
+        cards.append((num[0] & _M64, num[1] & _M64, num[2] & _M64, num[3] & _M64, num[4] & _M64, num[5] & _M64,
+                      healthy, int(phys), int(numa), int(round(float(occ) * 100))))
+    nphys = max((p for p, _ in raw_links), default=-1) + 1
+    q = [XGMI_IDLE_QUALITY] * (nphys * nphys)
+    for a in range(nphys):
+        q[a * nphys + a] = 10000
+    for phys, links in raw_links:
+        row = phys * nphys
+        for d in links:
+            peer = int(d.get("peer", 0))
+            if 0 <= peer < nphys:
+                load = float(d.get("load", 0.0))
+                q[row + peer] = 0 if not bool(d.get("up", True)) else \
+                    int(round(XGMI_IDLE_QUALITY * (1.0 - (0.0 if load < 0.0 else 1.0 if load > 1.0 else load))))
+    for a in range(nphys):
+        ra = a * nphys
+        for b in range(a + 1, nphys):
+            x, y = q[ra + b], q[b * nphys + a]
+            q[ra + b] = q[b * nphys + a] = x if x < y else y
+    ut = status.get("updateTime")
+    from ..models.scv import parse_rfc3339
+    return (cards, int(status.get("cardNumber", 0) or 0) & _M64, int(status.get("freeMemorySum", 0) or 0) & _M64,
+            int(status.get("totalMemorySum", 0) or 0) & _M64, float(parse_rfc3339(ut) or 0.0), nphys, q)
+
+
+def push_scv(engine, idx: int, scv, compat: bool, stale: bool = False) -> None:
+    view = getattr(scv, "engine_view", None) if isinstance(scv, LazyScv) else None
+    if view is not None:
+        cards, cn, fs, ts, ut, nphys, q = view
+        engine.set_cards(idx, cards, cn, fs, ts, stale, ut)
+        if nphys:
+            engine.set_links(idx, nphys, q)
+        return
     st = scv.status
     cards = compat_card_tuples(scv) if compat else card_tuples(scv)
-    engine.set_cards(idx, cards, int(st.card_number) & 0xFFFFFFFFFFFFFFFF,
-                     int(st.free_memory_sum) & 0xFFFFFFFFFFFFFFFF,
-                     int(st.total_memory_sum) & 0xFFFFFFFFFFFFFFFF, stale, float(st.update_time or 0.0))
+    engine.set_cards(idx, cards, int(st.card_number) & _M64, int(st.free_memory_sum) & _M64,
+                     int(st.total_memory_sum) & _M64, stale, float(st.update_time or 0.0))
     nphys, q = link_matrix(scv)
     if nphys:
         engine.set_links(idx, nphys, q)
