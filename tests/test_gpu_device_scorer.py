@@ -210,3 +210,44 @@ def test_fused_select_multi_pass_parity(require_gpu):
         assert not ds.compare_cycle(eng, req), k
         eng.schedule(pi.num_id, req, True)
     assert eng.device_fallbacks == 0
+
+
+def test_engine_mutations_during_device_batch(require_gpu):
+    """schedule_batch drops the engine lock while the GPU places the batch
+    (Engine::schedule_batch_device): another thread keeps releasing pods, reserving on the
+    CPU path and pushing telemetry meanwhile. Afterwards the host ledger is exact (every
+    placement reserved once, every release applied) and per-pod device cycles still match
+    the CPU engine — i.e. rows changed during a batch reached the device table."""
+    import threading
+
+    from yoda_scheduler_amd.ops import device_scorer as ds
+    from yoda_scheduler_amd.ops.native import pod_req
+    eng = _engine(4096, 51)
+    rng = random.Random(51)
+    early = [ds.random_request(eng, rng, f"early-{k}") for k in range(64)]
+    placed = [p for p, req in early if eng.schedule(p.num_id, req, True)[0] >= 0]
+    batches = [[ds.random_request(eng, rng, f"b{b}-{k}")[0] for k in range(256)] for b in range(6)]
+    stop = threading.Event()
+    done_mut = []
+
+    def mutate():
+        r2 = random.Random(7)
+        while not stop.is_set() and placed:
+            p = placed.pop()
+            assert eng.release(p.num_id)
+            pi, req = ds.random_request(eng, r2, f"cpu-{len(done_mut)}")
+            eng.schedule(pi.num_id, req, True)       # device busy → CPU path (bit-exact)
+            done_mut.append(pi)
+    t = threading.Thread(target=mutate)
+    t.start()
+    total = 0
+    for pods in batches:
+        res = eng.schedule_batch([p.num_id for p in pods], [pod_req(eng, p) for p in pods])
+        total += sum(1 for r in res if r[0] >= 0)
+    stop.set()
+    t.join(30)
+    assert eng.device_fallbacks == 0 and total > 0 and done_mut
+    # every live reservation is in the ledger exactly once: per-GPU reserved == Σ over pods
+    for k in range(20):
+        pi, req = ds.random_request(eng, rng, f"check-{k}")
+        assert not ds.compare_cycle(eng, req), k
