@@ -161,5 +161,16 @@ def smoke(device: int = 0, n_nodes: int = 512, pods: int = 32) -> dict:
         res = eng.schedule(pi.num_id, req, True)      # device path + reserve → next pod sees it
     if bad:
         raise AssertionError(f"device scorer mismatch: {bad[:3]}")
+    # one persistent k_batch dispatch over a batch, then the device table must still agree
+    from .native import pod_req
+    batch = [random_request(eng, rng, f"smoke-b{k}")[0] for k in range(pods)]
+    before = eng.device_cycles
+    eng.schedule_batch([p.num_id for p in batch], [pod_req(eng, p) for p in batch])
+    if eng.device_cycles - before != len(batch) or eng.device_fallbacks:
+        raise AssertionError(f"k_batch did not run: {eng.device_cycles - before} cycles, {eng.device_fallbacks} fallbacks")
+    pi, req = random_request(eng, rng, "smoke-after")
+    d = compare_cycle(eng, req)
+    if d:
+        raise AssertionError(f"device table diverged after k_batch: {d}")
     return {"device_cycles": eng.device_cycles, "fallbacks": eng.device_fallbacks,
-            "last_us": round(eng.device_last_us(), 1)}
+            "last_us": round(eng.device_last_us(), 1), "batch_grid_npb": batch_geometry(eng)}
