@@ -386,7 +386,9 @@ __device__ unsigned long long select_block(int n, const yoda_dev_req_t& r, const
   unsigned long long best = 0;
   // kSelBatch strided nodes per thread per pass: every load of a pass is issued before the
   // first use, so the single-block (fused) walk pays ~n/(kBlock*kSelBatch) memory round
-  // trips instead of one per node stride
+  // trips instead of one per node stride. (k_select's grid covers n with one node per
+  // thread, so there slots 1..kSelBatch-1 are always out of range: the batching only pays
+  // in the fused walk.)
   const int stride = nblk * kBlock;
   for (int i0 = blk * kBlock + threadIdx.x; i0 < n; i0 += stride * kSelBatch) {
     uint8_t fe[kSelBatch];
