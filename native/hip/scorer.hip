@@ -912,7 +912,10 @@ __device__ __forceinline__ void store_granule(gu64* p, uint32_t tag, uint32_t v)
 // true = keep spinning; false = give up (another block aborted, or the deadline passed)
 __device__ __forceinline__ bool spin_ok(const BatchArgs& a, unsigned& spins, long long t0) {
   __builtin_amdgcn_s_sleep(1);
-  if ((++spins & 63u) != 0) return true;
+  // the abort word and the clock every 64 spins; every spin under a sub-millisecond deadline
+  // (the failure-path test forces aborts with one)
+  const unsigned every = a.deadline_ticks < 100000 ? 0u : 63u;
+  if ((++spins & every) != 0) return true;
   const unsigned ab = __hip_atomic_load((gu32*)a.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (uniform((int)ab)) return false;
   if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.deadline_ticks) {
@@ -1353,6 +1356,7 @@ struct Ctx {
   int cus = 256;
   int npb_min = 0;            // YODA_DEV_NPB: minimum nodes per block (0: 8 per wave)
   int batch_waves = 0;        // YODA_DEV_BWAVES: k_batch waves per block (4 or 8; 0 = by cluster size)
+  long long deadline_ticks = 200000000ll;   // per spin wait, 100 MHz (YODA_DEV_SPIN_DEADLINE_US)
   yoda_dev_req_t *h_reqs = nullptr, *d_reqs_map = nullptr;
   yoda_dev_result_t* d_bres = nullptr;
   unsigned long long* d_slots = nullptr;
@@ -1418,6 +1422,7 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
   c->cus = cus < kMaxGrid ? cus : kMaxGrid;
   if (const char* v = getenv("YODA_DEV_PERSIST")) c->persist = v[0] != '0';
   if (const char* v = getenv("YODA_DEV_NPB")) c->npb_min = atoi(v) > 0 ? atoi(v) : 0;
+  if (const char* v = getenv("YODA_DEV_SPIN_DEADLINE_US")) c->deadline_ticks = atoll(v) > 0 ? atoll(v) * 100 : 1;
   if (const char* v = getenv("YODA_DEV_BWAVES")) c->batch_waves = atoi(v) == 4 ? 4 : atoi(v) == 8 ? 8 : 0;
   if (const char* v = getenv("YODA_DEV_DIRECT_ATOMICS")) c->direct_atomics = v[0] == '1' ? 1 : 0;
   if (const char* v = getenv("YODA_DEV_FUSE_MAX")) c->fuse_max = atoi(v);
@@ -1640,7 +1645,7 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
     a.seq = c->seq;
     a.tag0 = c->epoch;
     c->epoch += 3u * (uint32_t)m + 3u;
-    a.deadline_ticks = 200000000ll;   // 2 s per wait at 100 MHz
+    a.deadline_ticks = c->deadline_ticks;   // 2 s per wait by default
     a.reqs = c->d_reqs_map;
     a.slots = c->d_slots;
     a.res = c->d_bres;

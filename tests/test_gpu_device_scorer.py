@@ -251,3 +251,27 @@ def test_engine_mutations_during_device_batch(require_gpu):
     for k in range(20):
         pi, req = ds.random_request(eng, rng, f"check-{k}")
         assert not ds.compare_cycle(eng, req), k
+
+
+def test_batch_kernel_abort_falls_back_and_recovers(require_gpu):
+    """Failure path of k_batch: with a 0 µs spin deadline every all-gather wait gives up
+    (abort word), the last block reports `done = -seq`, yoda_dev_schedule_batch returns an
+    error and the engine places the batch on the CPU path instead (exact), marks every row
+    dirty and re-uploads it; device cycles afterwards still match the CPU engine."""
+    import os
+    from yoda_scheduler_amd.ops import device_scorer as ds
+    from yoda_scheduler_amd.ops.native import pod_req
+    os.environ["YODA_DEV_SPIN_DEADLINE_US"] = "0"
+    try:
+        eng = _engine(4096, 61)
+    finally:
+        os.environ.pop("YODA_DEV_SPIN_DEADLINE_US", None)
+    rng = random.Random(61)
+    pods = [ds.random_request(eng, rng, f"abort-{k}")[0] for k in range(64)]
+    res = eng.schedule_batch([p.num_id for p in pods], [pod_req(eng, p) for p in pods])
+    assert eng.device_fallbacks >= 1                     # the device batch gave up
+    assert sum(1 for r in res if r[0] >= 0) > 32          # ... and the CPU path placed the pods
+    for k in range(10):                                   # single cycles (per-pod chain) agree
+        pi, req = ds.random_request(eng, rng, f"abort-after-{k}")
+        assert not ds.compare_cycle(eng, req), k
+        eng.schedule(pi.num_id, req, True)
