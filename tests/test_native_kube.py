@@ -495,3 +495,51 @@ def test_scheduler_binds_over_native_transport(server):
     assert n == 30 and all(cards.values()) and not assumed and not gone
     assert len(cards["p1"].split(",")) == 2 and len(cards["p0"].split(",")) == 1
     assert stored["spec"]["nodeName"] == "n1"
+
+
+def test_bounded_drain_keeps_order_and_yields_between_chunks():
+    """NativeTransport dispatches at most DRAIN_BUDGET watch events per loop turn: a large
+    event batch is split, the rest stays first in line, completions queued behind it run
+    after it, and a continuation is scheduled with call_soon so other tasks (the scheduling
+    loop) run between chunks."""
+    class FakeT:
+        def __init__(self, items):
+            self.items = items
+
+        def drain(self):
+            out, self.items = self.items, []
+            return out
+
+    tr = nat.NativeTransport.__new__(nat.NativeTransport)
+    tr._cbs, tr._watches, tr.callback_errors = {}, {}, 0
+    import collections
+    tr._backlog, tr._continue_pending = collections.deque(), False
+    seen: list = []
+    tr._watches[7] = nat.WatchHandle(7, lambda evs: seen.append(("ev", [e[1] for e in evs])),
+                                     lambda st, b: seen.append(("end", st)))
+    tr._cbs[3] = lambda st, body: seen.append(("bind", st))
+    big = [("ADDED", str(i), None) for i in range(1200)]
+    tr.t = FakeT([(1, 7, big), (0, 3, 201, b""), (1, 7, [("MODIFIED", "x", None)]), (2, 7, 200, b"")])
+
+    async def go():
+        tr._loop = asyncio.get_event_loop()
+        other = []
+
+        async def scheduler_like():
+            for _ in range(5):
+                other.append(len([s for s in seen if s[0] == "ev"]))
+                await asyncio.sleep(0)
+        task = asyncio.ensure_future(scheduler_like())
+        tr._drain()
+        for _ in range(10):
+            await asyncio.sleep(0)
+        await task
+        return other
+    other = asyncio.run(go())
+    evs = [x for kind, v in seen if kind == "ev" for x in v]
+    assert evs == [str(i) for i in range(1200)] + ["x"]          # order kept across splits
+    chunks = [len(v) for kind, v in seen if kind == "ev"]
+    assert chunks[:3] == [512, 512, 176] and max(chunks) <= nat.NativeTransport.DRAIN_BUDGET
+    kinds = [k for k, _ in seen]
+    assert kinds.index("bind") > 2 and kinds[-1] == "end"         # completion after the big batch
+    assert other[0] >= 1 and other[-1] <= len(chunks)             # the other task ran between chunks
