@@ -664,6 +664,9 @@ def test_scv_engine_view_matches_dataclass_path():
             c.xgmi_links_up = rng.random() > 0.1
             c.cu_occupancy = rng.choice([0.0, 12.345, 99.99])
             c.numa_node = rng.choice([0, 1, 3])
+            c.uuid = rng.choice(["", f"uuid-{c.id}"])
+            c.hip_uuid = rng.choice(["", f"GPU-{trial:04d}{c.id}"])
+            c.hip_id = rng.choice([-1, 7 - c.id])
             if trial % 3 == 0:
                 c.physical_id = c.id // 2          # partitions
             c.xgmi = [XgmiLink(peer=p, load=rng.choice([0.0, 0.2, 0.95, 1.4, -0.1]), up=rng.random() > 0.05)
@@ -686,5 +689,7 @@ def test_scv_engine_view_matches_dataclass_path():
                     st.total_memory_sum & (2**64 - 1), float(st.update_time or 0.0), *link_matrix(ref))
             assert view == want, (trial, compat)
         lz = LazyScv(obj, scv_engine_view(obj, False))
+        assert lz.card_idents() == [(c.id, c.uuid, c.hip_uuid, c.hip_id) for c in ref.status.card_list]
+        assert lz._scv is None                     # identities read without decoding
         assert lz.is_stale(1.7e9 + trial + 100, 3.0) == ref.is_stale(1.7e9 + trial + 100, 3.0)
         assert lz.card_number == ref.status.card_number and lz.status.card_list == ref.status.card_list

@@ -259,7 +259,8 @@ class LazyScv:
     engine view (``engine_view``: card tuples, sums, link matrix — computed straight from the
     dict by ``ops.native.scv_engine_view``) and the freshness fields are kept here. A 1000-node
     cluster sends ≈100 Scv updates/s, most of which are never read by anything else."""
-    __slots__ = ("name", "update_time", "update_interval_ms", "card_number", "engine_view", "_obj", "_scv")
+    __slots__ = ("name", "update_time", "update_interval_ms", "card_number", "engine_view", "_obj", "_scv",
+                 "_idents")
 
     def __init__(self, obj: dict, engine_view) -> None:
         meta = obj.get("metadata") or {}
@@ -272,6 +273,27 @@ class LazyScv:
         self.engine_view = engine_view
         self._obj = obj
         self._scv = None
+        self._idents = None
+
+    def card_idents(self) -> list:
+        """Per card position: (id, amd-smi UUID, HIP/ROCr UUID, HIP ordinal) — what a Binding's
+        device annotations need — read from the JSON (same matching and defaults as
+        ``Scv.from_json``) without decoding the rest."""
+        if self._scv is not None:
+            return [(c.id, c.uuid, c.hip_uuid, c.hip_id) for c in self._scv.status.card_list]
+        if self._idents is None:
+            status = self._obj.get("status") or {}
+            amd = status.get("amd") or {}
+            amd_cards = {int(c.get("id", i)): c for i, c in enumerate(amd.get("cards") or [])}
+            out = []
+            for i, cj in enumerate(status.get("cardList") or []):
+                cid = int(cj["id"]) if cj.get("id") is not None else 0
+                ext = amd_cards.get(cid) or amd_cards.get(i) or {}
+                u, hu, hid = ext.get("uuid"), ext.get("hipUuid"), ext.get("hipId")
+                out.append((cid, u if u is not None else "", hu if hu is not None else "",
+                            hid if hid is not None else -1))
+            self._idents = out
+        return self._idents
 
     def decoded(self) -> "Scv":
         if self._scv is None:

@@ -173,17 +173,22 @@ def visible_device_ids(scv, cards: list) -> tuple[str, str]:
     """(ROCR_VISIBLE_DEVICES value, amd-smi UUID list) for the assigned card positions of a
     node's Scv. Per card: ROCr UUID, else HIP ordinal, else the amd-smi index."""
     vis, uuids = [], []
-    cl = scv.status.card_list if scv is not None else []
+    if scv is None:
+        ids = []
+    elif hasattr(scv, "card_idents"):          # LazyScv: identities without a full decode
+        ids = scv.card_idents()
+    else:
+        ids = [(c.id, c.uuid, c.hip_uuid, c.hip_id) for c in scv.status.card_list]
     for c in cards:
-        card = cl[c] if 0 <= c < len(cl) else None
-        if card is not None and card.hip_uuid:
-            vis.append(card.hip_uuid)
-        elif card is not None and card.hip_id >= 0:
-            vis.append(str(card.hip_id))
+        card = ids[c] if 0 <= c < len(ids) else None
+        if card is not None and card[2]:
+            vis.append(card[2])
+        elif card is not None and card[3] >= 0:
+            vis.append(str(card[3]))
         else:
-            vis.append(str(card.id if card is not None else c))
-        if card is not None and card.uuid:
-            uuids.append(card.uuid)
+            vis.append(str(card[0] if card is not None else c))
+        if card is not None and card[1]:
+            uuids.append(card[1])
     return ",".join(vis), (",".join(uuids) if len(uuids) == len(cards) else "")
 
 
