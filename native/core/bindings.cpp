@@ -1,5 +1,6 @@
 // pybind11 bindings of the native scheduling engine (module yoda_scheduler_amd._native._yoda_core).
 #include <array>
+#include <atomic>
 #include <mutex>
 #include <thread>
 #include <chrono>
@@ -18,8 +19,27 @@ namespace {
 // schedule_batch) may overlap event-loop calls (informer updates, bind failures) on the
 // same engine. Recursive: bound methods never nest today, but a future one may.
 std::recursive_mutex g_engine_mu;
+std::atomic<uint64_t> g_lock_contended{0}, g_lock_wait_ns{0};
+// Uncontended: take the lock with the GIL held (the common case, no GIL round trip). Contended
+// — the engine worker is preparing or finishing a batch — wait WITHOUT the GIL, so the event
+// loop's other threads (and the worker itself, which needs the GIL to hand its results back)
+// keep running. No thread therefore ever waits for the lock while holding the GIL, which is
+// what makes re-taking the GIL with the lock held deadlock-free.
 struct EngineGuard {
-  std::unique_lock<std::recursive_mutex> g{g_engine_mu};
+  std::unique_lock<std::recursive_mutex> g{g_engine_mu, std::defer_lock};
+  EngineGuard() {
+    if (g.try_lock()) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (PyGILState_Check()) {
+      py::gil_scoped_release nogil;
+      g.lock();
+    } else {
+      g.lock();
+    }
+    g_lock_contended.fetch_add(1, std::memory_order_relaxed);
+    g_lock_wait_ns.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                 std::chrono::steady_clock::now() - t0).count(), std::memory_order_relaxed);
+  }
 };
 
 // The engine lock at a moment no device batch is in flight (schedule_batch drops the lock
@@ -76,6 +96,9 @@ py::tuple cycle_tuple(const CycleResult& r) {
 
 PYBIND11_MODULE(_yoda_core, m) {
   m.doc() = "Native placement / scheduling-cycle engine (C++17)";
+  m.def("engine_lock_stats", [] {
+    return py::make_tuple(g_lock_contended.load(), g_lock_wait_ns.load() / 1000);
+  }, "(contended acquisitions, total wait in us) of the process-wide engine lock");
   m.attr("F_NODE_UNSCHEDULABLE") = (uint32_t)F_NODE_UNSCHEDULABLE;
   m.attr("F_NODE_NAME") = (uint32_t)F_NODE_NAME;
   m.attr("F_TAINT_TOLERATION") = (uint32_t)F_TAINT_TOLERATION;

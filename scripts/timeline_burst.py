@@ -93,10 +93,29 @@ async def run(a) -> list:
             else:
                 gc_pauses.append((info.get("generation"), time.perf_counter() - gc_t[0], info.get("collected", 0)))
         gc.callbacks.append(gc_cb)
+        from yoda_scheduler_amd.ops.native import core
+        lk0 = core().engine_lock_stats()
+        # event-loop idle time: the time the loop's selector spends blocked in select()
+        sel = asyncio.get_event_loop()._selector
+        orig_select = sel.select
+        idle = [0.0, 0]
+
+        def timed_select(timeout=None):
+            t = time.perf_counter()
+            try:
+                return orig_select(timeout)
+            finally:
+                idle[0] += time.perf_counter() - t
+                idle[1] += 1
+        sel.select = timed_select
         t0 = time.perf_counter()
+        c0 = time.thread_time()
         t0_us = tr.now_us()
         res = await sh.burst(f"s{rep}")
         t1 = time.perf_counter()
+        c1 = time.thread_time()
+        lk1 = core().engine_lock_stats()
+        sel.select = orig_select
         gc.callbacks.remove(gc_cb)
         spans = list(tr.chrome_trace()["traceEvents"])
         batches = [(round((e["ts"] - t0_us) / 1000, 3), round(e.get("dur", 0) / 1000, 3), e["args"].get("pods"))
@@ -124,7 +143,12 @@ async def run(a) -> list:
                "latency_ms": {"p50": round(sorted(res.latencies_s)[len(res.latencies_s) // 2] * 1000, 3),
                               "p99": round(sorted(res.latencies_s)[int(len(res.latencies_s) * 0.99)] * 1000, 3)}
                if res.latencies_s else None,
-               "device_cycles": sched.engine.device_cycles}
+               "device_cycles": sched.engine.device_cycles,
+               "engine_lock_contended(n,wait_us)": [lk1[0] - lk0[0], lk1[1] - lk0[1]],
+               "loop_idle_ms": round(idle[0] * 1000, 3), "loop_selects": idle[1],
+               # main-thread CPU time: (wall - idle) - cpu ≈ time the loop thread was runnable but
+               # blocked (GIL hand-offs to the engine worker, lock waits, page faults)
+               "main_cpu_ms": round((c1 - c0) * 1000, 3)}
         if dev_trace:
             trc = ds.read_batch_trace(sched.engine)
             if trc:

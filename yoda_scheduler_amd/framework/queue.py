@@ -45,6 +45,10 @@ class SchedulingQueue:
         self._hint_moves: collections.deque = collections.deque()
         self._hint_dropped_cycle = -1
         self.closed = False
+        # one-shot future resolved by the next push to the active queue (the scheduling loop
+        # waits on it together with an engine result: one event-loop hop to wake, where an
+        # asyncio.Event behind asyncio.wait takes three — each behind a chunk of watch events)
+        self.wake: Optional[asyncio.Future] = None
         # (event, queue, n) → scheduler_queue_incoming_pods_total; None = not counted
         self.incoming_hook: Optional[Callable[[str, str, int], None]] = None
 
@@ -64,6 +68,11 @@ class SchedulingQueue:
         heapq.heappush(self._active, entry)
         if self._cond is not None:
             self._cond.set()
+        w = self.wake
+        if w is not None:
+            self.wake = None
+            if not w.done():
+                w.set_result(None)
 
     def backoff_duration(self, pi: PodInfo) -> float:
         d = self.initial_backoff * (2 ** max(pi.attempts - 1, 0))

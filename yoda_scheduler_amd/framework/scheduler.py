@@ -767,6 +767,28 @@ class Scheduler:
         results = await fut
         self._finish_run(fw, item, results, cycle, t0)
 
+    async def _await_pods_or_result(self) -> None:
+        """Wait until the oldest in-flight run's result lands (then apply it) or a pod reaches
+        the active queue, whichever is first."""
+        fut = self._inflight[0][4]
+        if not fut.done():
+            q = self.queue
+            wake = asyncio.get_event_loop().create_future()
+
+            def on_result(_f, wake=wake) -> None:
+                if not wake.done():
+                    wake.set_result(None)
+            q.wake = wake
+            fut.add_done_callback(on_result)
+            try:
+                await wake
+            finally:
+                q.wake = None
+                fut.remove_done_callback(on_result)
+            if not fut.done():
+                return                            # pods first: the loop pops them
+        await self._finish_inflight_run(self._inflight.popleft())
+
     async def finish_inflight(self) -> None:
         """Apply the results of every run still on the engine worker, oldest first."""
         while self._inflight:
@@ -941,7 +963,10 @@ class Scheduler:
         bs = max(1, self.config.batch_size)
         while not self._stop.is_set():
             if self._inflight and not q._active_entries:
-                await self.finish_inflight()      # nothing to overlap with: apply it now
+                # nothing to pop: apply the oldest run when it lands, unless pods arrive first
+                # (then they go to the engine behind it, which keeps the GPU busy while a burst
+                # is still being ingested)
+                await self._await_pods_or_result()
                 continue
             pi = await q.pop()
             if pi is None:

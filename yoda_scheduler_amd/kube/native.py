@@ -14,6 +14,7 @@ import asyncio
 import collections
 import json
 import logging
+import os
 from typing import Callable, Optional
 from urllib.parse import urlsplit
 
@@ -95,7 +96,8 @@ class NativeTransport:
         self._loop = loop
         loop.add_reader(self.t.fileno(), self._drain)
 
-    DRAIN_BUDGET = 512
+    # YODA_DRAIN_BUDGET: A/B knob for the per-turn event budget
+    DRAIN_BUDGET = int(os.environ.get("YODA_DRAIN_BUDGET", "512"))
 
     def _drain(self) -> None:
         self._backlog.extend(self.t.drain())

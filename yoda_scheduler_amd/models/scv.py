@@ -260,7 +260,7 @@ class LazyScv:
     dict by ``ops.native.scv_engine_view``) and the freshness fields are kept here. A 1000-node
     cluster sends ≈100 Scv updates/s, most of which are never read by anything else."""
     __slots__ = ("name", "update_time", "update_interval_ms", "card_number", "engine_view", "_obj", "_scv",
-                 "_idents")
+                 "_idents", "_vis")
 
     def __init__(self, obj: dict, engine_view) -> None:
         meta = obj.get("metadata") or {}
@@ -274,6 +274,15 @@ class LazyScv:
         self._obj = obj
         self._scv = None
         self._idents = None
+        self._vis = None
+
+    def card_vis(self) -> list:
+        """Per card position: (ROCr-visible id, amd-smi UUID) as the Binding annotations spell
+        them (``plugins.defaults.card_vis``), computed once per Scv version."""
+        if self._vis is None:
+            from ..plugins.defaults import card_vis
+            self._vis = card_vis(self.card_idents())
+        return self._vis
 
     def card_idents(self) -> list:
         """Per card position: (id, amd-smi UUID, HIP/ROCr UUID, HIP ordinal) — what a Binding's

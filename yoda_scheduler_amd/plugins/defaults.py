@@ -169,26 +169,24 @@ def _inert(name: str):
 INERT_PLUGINS = ["CSILimits"]
 
 
+def card_vis(ids: list) -> list:
+    """Per card position of ``(id, amd-smi UUID, ROCr UUID, HIP ordinal)`` identities: the
+    ROCr-visible id (ROCr UUID, else HIP ordinal, else the amd-smi index) and the UUID."""
+    return [(c[2] if c[2] else (str(c[3]) if c[3] >= 0 else str(c[0])), c[1]) for c in ids]
+
+
 def visible_device_ids(scv, cards: list) -> tuple[str, str]:
     """(ROCR_VISIBLE_DEVICES value, amd-smi UUID list) for the assigned card positions of a
     node's Scv. Per card: ROCr UUID, else HIP ordinal, else the amd-smi index."""
-    vis, uuids = [], []
     if scv is None:
-        ids = []
-    elif hasattr(scv, "card_idents"):          # LazyScv: identities without a full decode
-        ids = scv.card_idents()
+        per = []
+    elif hasattr(scv, "card_vis"):             # LazyScv: computed once per Scv version
+        per = scv.card_vis()
     else:
-        ids = [(c.id, c.uuid, c.hip_uuid, c.hip_id) for c in scv.status.card_list]
-    for c in cards:
-        card = ids[c] if 0 <= c < len(ids) else None
-        if card is not None and card[2]:
-            vis.append(card[2])
-        elif card is not None and card[3] >= 0:
-            vis.append(str(card[3]))
-        else:
-            vis.append(str(card[0] if card is not None else c))
-        if card is not None and card[1]:
-            uuids.append(card[1])
+        per = card_vis([(c.id, c.uuid, c.hip_uuid, c.hip_id) for c in scv.status.card_list])
+    n = len(per)
+    vis = [per[c][0] if 0 <= c < n else str(c) for c in cards]
+    uuids = [per[c][1] for c in cards if 0 <= c < n and per[c][1]]
     return ",".join(vis), (",".join(uuids) if len(uuids) == len(cards) else "")
 
 
