@@ -1,6 +1,11 @@
 // pybind11 bindings of the native scheduling engine (module yoda_scheduler_amd._native._yoda_core).
 #include <array>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <sys/eventfd.h>
+#include <unistd.h>
 #include <mutex>
 #include <thread>
 #include <chrono>
@@ -91,6 +96,123 @@ SelTerm make_term(Engine& e, const py::list& reqs) {
 py::tuple cycle_tuple(const CycleResult& r) {
   return py::make_tuple(r.node, r.feasible, r.evaluated, r.cards, r.score, r.reason_counts, r.gang_quality);
 }
+
+// Engine batches on a native thread. The event loop submits a batch (ids + request
+// pointers; Python keeps the PodReq objects alive until the result is collected), the
+// thread runs Engine::schedule_batch under the engine lock — which the engine itself drops
+// while a device batch is on the GPU — and signals an eventfd the loop watches; the loop
+// converts the results when it collects them. Unlike an executor thread this one never takes
+// the GIL, so a batch costs the event loop no GIL hand-offs (two or more per batch with a
+// Python worker, each up to the switch interval).
+class BatchWorker {
+ public:
+  struct Job {
+    uint64_t id = 0;
+    std::vector<uint64_t> pods;
+    std::vector<const PodReq*> reqs;
+    std::vector<CycleResult> res;
+    std::string err;
+    double t0 = 0, t1 = 0;   // CLOCK_MONOTONIC seconds (time.perf_counter's clock on Linux)
+  };
+
+  explicit BatchWorker(Engine* e) : e_(e) {
+    efd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    if (efd_ < 0) throw std::runtime_error("eventfd failed");
+    th_ = std::thread([this] { run(); });
+  }
+  ~BatchWorker() { close(); }
+
+  int fileno() const { return efd_; }
+
+  uint64_t submit(std::vector<uint64_t> pods, std::vector<const PodReq*> reqs) {
+    if (pods.size() != reqs.size()) throw std::invalid_argument("pods/reqs length mismatch");
+    auto j = std::make_unique<Job>();
+    j->pods = std::move(pods);
+    j->reqs = std::move(reqs);
+    std::lock_guard<std::mutex> g(mu_);
+    if (stop_) throw std::runtime_error("batch worker closed");
+    j->id = ++next_;
+    const uint64_t id = j->id;
+    q_.push_back(std::move(j));
+    cv_.notify_one();
+    return id;
+  }
+
+  std::vector<std::unique_ptr<Job>> take_done() {
+    uint64_t v;
+    while (::read(efd_, &v, sizeof v) > 0) {
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<std::unique_ptr<Job>> out(std::make_move_iterator(done_.begin()), std::make_move_iterator(done_.end()));
+    done_.clear();
+    return out;
+  }
+
+  size_t pending() {
+    std::lock_guard<std::mutex> g(mu_);
+    return q_.size() + (busy_ ? 1 : 0);
+  }
+
+  void close() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (stop_ && !th_.joinable()) return;
+      stop_ = true;
+      cv_.notify_all();
+    }
+    if (th_.joinable()) th_.join();
+    if (efd_ >= 0) {
+      ::close(efd_);
+      efd_ = -1;
+    }
+  }
+
+ private:
+  static double mono() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+
+  void run() {
+    for (;;) {
+      std::unique_ptr<Job> j;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;   // stop requested and nothing left
+        j = std::move(q_.front());
+        q_.pop_front();
+        busy_ = true;
+      }
+      j->t0 = mono();
+      try {
+        EngineGuard lk;   // this thread never holds the GIL: a plain lock
+        j->res = e_->schedule_batch(j->pods, j->reqs);
+      } catch (const std::exception& ex) {
+        j->err = ex.what();
+      } catch (...) {
+        j->err = "unknown error in schedule_batch";
+      }
+      j->t1 = mono();
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        done_.push_back(std::move(j));
+        busy_ = false;
+      }
+      const uint64_t one = 1;
+      ssize_t w = ::write(efd_, &one, sizeof one);
+      (void)w;
+    }
+  }
+
+  Engine* e_;
+  int efd_ = -1;
+  std::thread th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::unique_ptr<Job>> q_, done_;
+  bool stop_ = false, busy_ = false;
+  uint64_t next_ = 0;
+};
 
 }  // namespace
 
@@ -345,4 +467,34 @@ PYBIND11_MODULE(_yoda_core, m) {
              for (auto& r : res) out.append(cycle_tuple(r));
              return out;
            });
+
+  py::class_<BatchWorker>(m, "BatchWorker")
+      .def(py::init([](Engine& e) { return std::make_unique<BatchWorker>(&e); }), py::keep_alive<1, 2>())
+      .def("fileno", &BatchWorker::fileno)
+      .def("submit",
+           [](BatchWorker& w, std::vector<uint64_t> pods, const std::vector<PodReq*>& reqs) {
+             return w.submit(std::move(pods), std::vector<const PodReq*>(reqs.begin(), reqs.end()));
+           },
+           "queue a batch (the caller keeps the PodReq objects alive until it is collected); returns its id")
+      .def("collect",
+           [](BatchWorker& w) {
+             auto jobs = w.take_done();
+             py::list out;
+             for (auto& j : jobs) {
+               if (!j->err.empty()) {
+                 out.append(py::make_tuple(j->id, py::none(), j->err, j->t0, j->t1));
+                 continue;
+               }
+               py::list res;
+               for (auto& r : j->res) res.append(cycle_tuple(r));
+               out.append(py::make_tuple(j->id, res, py::none(), j->t0, j->t1));
+             }
+             return out;
+           },
+           "finished batches: [(id, results | None, error | None, t_start, t_end)]")
+      .def_property_readonly("pending", &BatchWorker::pending)
+      .def("close", [](BatchWorker& w) {
+        py::gil_scoped_release nogil;
+        w.close();
+      });
 }

@@ -49,19 +49,7 @@ async def run(a) -> list:
             return out
         q.pop_batch = pop_batch
         eng_calls: list = []
-        orig_sb = sched.engine.schedule_batch
-
-        class _EngProxy:      # times every engine batch call (any thread)
-            def __getattr__(self, k):
-                return getattr(eng, k)
-
-            def schedule_batch(self, ids, reqs):
-                t = time.perf_counter()
-                r = orig_sb(ids, reqs)
-                eng_calls.append((t, time.perf_counter(), len(ids)))
-                return r
-        eng = sched.engine
-        sched.engine = _EngProxy()
+        sched.engine_spans = eng_calls        # (start, end, pods) of every native engine batch
         # bind round trips: submit (native transport) → completion callback on the loop
         submits: dict = {}
         rtts: list = []
@@ -163,7 +151,7 @@ async def run(a) -> list:
             out["bind_submit_ms"] = {"first": pct(subs, 0), "p50": pct(subs, .5), "last": pct(subs, 1)}
             out["bind_rtt_ms"] = {"p50": pct(rr, .5), "p90": pct(rr, .9), "max": pct(rr, 1)}
         outs.append(out)
-        sched.engine = eng
+        sched.engine_spans = None
         q.add, q.pop_batch = orig_add, orig_pb
     await sh.stop()
     return outs

@@ -60,7 +60,7 @@ def test_burst_survives_watch_drops_latency_and_bind_faults():
 
 
 def test_overlapped_engine_batches_keep_ledger_exact():
-    """yodaRuntime.overlapEngine: native batches run on the engine worker thread while the
+    """yodaRuntime.overlapEngine: native batches run on the engine's native worker thread while the
     event loop binds, retries failed binds (engine release) and ingests node updates (engine
     upserts) — the process-wide engine lock keeps every reservation exact."""
     faults = Faults(bind_conflict_ratio=0.05, bind_fail_ratio=0.05, seed=11)
@@ -86,7 +86,8 @@ def test_overlapped_engine_batches_keep_ledger_exact():
                 await asyncio.sleep(0)
         ok = await c.wait(lambda: all(c.node_of(p) for p in pods), 30.0, 0.01)
         await asyncio.sleep(0.1)
-        overlapped = c.sched._engine_exec is not None
+        # batches ran on the native engine worker thread (core.BatchWorker), not inline
+        overlapped = c.sched._batch_worker is not None and c.sched._engine_exec is None
         _ledger_invariants(c, pods)
         await c.stop()
         return ok, overlapped, c.sched.bind_errors

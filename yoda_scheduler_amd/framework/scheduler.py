@@ -140,6 +140,9 @@ class Scheduler:
         self._bind_idle: collections.deque = collections.deque()
         self._tasks: list[asyncio.Task] = []
         self._engine_exec = None          # worker thread of schedule_batch_overlapped
+        self._batch_worker = None         # native engine worker (core.BatchWorker)
+        self._batch_futs: dict = {}
+        self.engine_spans: Optional[list] = None   # (t_start, t_end, pods) of native batches
         self._inflight: collections.deque = collections.deque()   # (fw, run, cycle, t0, future) on that worker
         self._ann_memo: dict = {}          # _bind_annotations memo, valid for one cache generation
         self._ann_gen = -1
@@ -749,21 +752,47 @@ class Scheduler:
                 self.schedule_one(item)
                 continue
             cycle, t0, ids, reqs = self._prepare_run(fw, item)
-            if self._engine_exec is None:
-                import concurrent.futures
-                import sys
-                self._engine_exec = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="yoda-engine")
-                # the worker re-takes the GIL to hand back each batch's results; with the
-                # default 5 ms switch interval it waits that long behind the busy event loop
-                # (measured: +7 µs per pod on MI355X config 6), so ask for 0.2 ms
-                sys.setswitchinterval(min(sys.getswitchinterval(), ENGINE_SWITCH_INTERVAL_S))
-            fut = loop.run_in_executor(self._engine_exec, self.engine.schedule_batch, ids, reqs)
-            self._inflight.append((fw, item, cycle, t0, fut))
+            fut = self._submit_engine_batch(loop, ids, reqs)
+            self._inflight.append((fw, item, cycle, t0, fut, reqs))
             while len(self._inflight) >= depth:
                 await self._finish_inflight_run(self._inflight.popleft())
 
+    def _submit_engine_batch(self, loop, ids: list, reqs: list) -> asyncio.Future:
+        """Hand a batch to the engine's native worker thread (``BatchWorker``: no GIL on that
+        thread, results converted here when collected); an engine that is not the native
+        class (test doubles) goes to a Python executor thread instead."""
+        Engine = core().Engine
+        if isinstance(self.engine, Engine):
+            if self._batch_worker is None:
+                self._batch_worker = core().BatchWorker(self.engine)
+                loop.add_reader(self._batch_worker.fileno(), self._collect_engine_batches)
+            fut = loop.create_future()
+            self._batch_futs[self._batch_worker.submit(ids, reqs)] = fut
+            return fut
+        if self._engine_exec is None:
+            import concurrent.futures
+            import sys
+            self._engine_exec = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="yoda-engine")
+            # the worker re-takes the GIL to hand back each batch's results; with the
+            # default 5 ms switch interval it waits that long behind the busy event loop
+            # (measured: +7 µs per pod on MI355X config 6), so ask for 0.2 ms
+            sys.setswitchinterval(min(sys.getswitchinterval(), ENGINE_SWITCH_INTERVAL_S))
+        return loop.run_in_executor(self._engine_exec, self.engine.schedule_batch, ids, reqs)
+
+    def _collect_engine_batches(self) -> None:
+        for jid, res, err, ts, te in self._batch_worker.collect():
+            fut = self._batch_futs.pop(jid, None)
+            if self.engine_spans is not None:
+                self.engine_spans.append((ts, te, len(res) if res is not None else 0))
+            if fut is None or fut.done():
+                continue
+            if err is not None:
+                fut.set_exception(RuntimeError(f"engine batch failed: {err}"))
+            else:
+                fut.set_result(res)
+
     async def _finish_inflight_run(self, run: tuple) -> None:
-        fw, item, cycle, t0, fut = run
+        fw, item, cycle, t0, fut = run[:5]
         results = await fut
         self._finish_run(fw, item, results, cycle, t0)
 
@@ -1046,6 +1075,17 @@ class Scheduler:
         if self._engine_exec is not None:
             self._engine_exec.shutdown(wait=True)
             self._engine_exec = None
+        if self._batch_worker is not None:
+            w, self._batch_worker = self._batch_worker, None
+            try:
+                asyncio.get_event_loop().remove_reader(w.fileno())
+            except (ValueError, OSError):
+                pass
+            w.close()
+            for fut in self._batch_futs.values():
+                if not fut.done():
+                    fut.cancel()
+            self._batch_futs.clear()
 
     async def drain_binds(self) -> None:
         while self.pending_binds:
