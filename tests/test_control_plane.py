@@ -689,7 +689,10 @@ def test_scv_engine_view_matches_dataclass_path():
                     st.total_memory_sum & (2**64 - 1), float(st.update_time or 0.0), *link_matrix(ref))
             assert view == want, (trial, compat)
         lz = LazyScv(obj, scv_engine_view(obj, False))
-        assert lz.card_idents() == [(c.id, c.uuid, c.hip_uuid, c.hip_id) for c in ref.status.card_list]
+        want_ids = [(c.id, c.uuid, c.hip_uuid, c.hip_id) for c in ref.status.card_list]
+        assert lz.card_idents() == want_ids
         assert lz._scv is None                     # identities read without decoding
+        ids: list = []                             # ... or taken in the engine-view pass
+        assert LazyScv(obj, scv_engine_view(obj, False, ids), ids).card_idents() == want_ids
         assert lz.is_stale(1.7e9 + trial + 100, 3.0) == ref.is_stale(1.7e9 + trial + 100, 3.0)
         assert lz.card_number == ref.status.card_number and lz.status.card_list == ref.status.card_list

@@ -107,8 +107,10 @@ class SchedulerCache:
         self.generation += 1
 
     def add_scv(self, obj: dict) -> None:
-        # engine view straight from the JSON; the Scv dataclasses are built only if read
-        self.set_scv(LazyScv(obj, scv_engine_view(obj, self.compat)))
+        # engine view (and the cards' identities) straight from the JSON; the Scv
+        # dataclasses are built only if read
+        idents: list = []
+        self.set_scv(LazyScv(obj, scv_engine_view(obj, self.compat, idents), idents))
 
     update_scv = add_scv
 

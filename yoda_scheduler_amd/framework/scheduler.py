@@ -856,6 +856,18 @@ class Scheduler:
         cards = getattr(pi, "assigned_cards", None)
         if cards is None:
             return []
+        scv = self.cache.scvs.get(node)
+        if isinstance(scv, LazyScv):
+            # per Scv version: survives other nodes' telemetry updates (the generation memo
+            # below is flushed by every one of them)
+            memo = scv.ann_memo
+            key = (tuple(cards), pi.gpu.memory if pi.gpu.has_memory else -1)
+            ann = memo.get(key)
+            if ann is None:
+                if len(memo) >= 1024:
+                    memo.clear()
+                ann = memo[key] = bind_annotations(pi, self.cache.scvs, node)
+            return ann
         gen = self.cache.generation
         if self._ann_gen != gen:
             self._ann_memo.clear()

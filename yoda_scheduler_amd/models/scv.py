@@ -260,9 +260,9 @@ class LazyScv:
     dict by ``ops.native.scv_engine_view``) and the freshness fields are kept here. A 1000-node
     cluster sends ≈100 Scv updates/s, most of which are never read by anything else."""
     __slots__ = ("name", "update_time", "update_interval_ms", "card_number", "engine_view", "_obj", "_scv",
-                 "_idents", "_vis")
+                 "_idents", "_vis", "ann_memo")
 
-    def __init__(self, obj: dict, engine_view) -> None:
+    def __init__(self, obj: dict, engine_view, idents: list | None = None) -> None:
         meta = obj.get("metadata") or {}
         status = obj.get("status") or {}
         spec = obj.get("spec") or {}
@@ -273,8 +273,9 @@ class LazyScv:
         self.engine_view = engine_view
         self._obj = obj
         self._scv = None
-        self._idents = None
+        self._idents = idents
         self._vis = None
+        self.ann_memo: dict = {}       # the scheduler's Binding annotations per (GPU set, HBM)
 
     def card_vis(self) -> list:
         """Per card position: (ROCr-visible id, amd-smi UUID) as the Binding annotations spell

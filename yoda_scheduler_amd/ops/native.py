@@ -94,12 +94,14 @@ def link_matrix(scv: Scv) -> tuple[int, list[int]]:
 _M64 = 0xFFFFFFFFFFFFFFFF
 
 
-def scv_engine_view(obj: dict, compat: bool) -> tuple:
+def scv_engine_view(obj: dict, compat: bool, idents: list | None = None) -> tuple:
     """What ``push_scv`` sends the engine for an Scv given as decoded JSON — the card tuples
     (``card_tuples`` / ``compat_card_tuples``), CardNumber / memory sums, sample time and the
     link matrix (``link_matrix``) — computed from the dict without building the dataclasses
     (same field defaults and conversions as ``Scv.from_json``; equivalence pinned by
-    ``tests/test_control_plane.py::test_scv_engine_view_matches_dataclass_path``)."""
+    ``tests/test_control_plane.py::test_scv_engine_view_matches_dataclass_path``). With
+    ``idents`` the same pass appends each card's (id, amd-smi UUID, ROCr UUID, HIP ordinal)
+    (``LazyScv.card_idents``): the Binding annotations then never walk the JSON again."""
     status = obj.get("status") or {}
     amd = status.get("amd") or {}
     amd_cards = {int(c.get("id", i)): c for i, c in enumerate(amd.get("cards") or [])}
@@ -112,6 +114,10 @@ def scv_engine_view(obj: dict, compat: bool) -> tuple:
         health = v if v is not None else HEALTHY
         num = [int(g(k)) if g(k) is not None else 0
                for k in ("totalMemory", "freeMemory", "clock", "bandwidth", "core", "power")]
+        if idents is not None:
+            x = ext or {}
+            u, hu, hid = x.get("uuid"), x.get("hipUuid"), x.get("hipId")
+            idents.append((cid, u if u is not None else "", hu if hu is not None else "", hid if hid is not None else -1))
         if ext:
             e = ext.get
             phys = int(ext.get("physicalId", cid))
