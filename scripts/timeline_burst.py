@@ -136,7 +136,8 @@ async def run(a) -> list:
                "loop_idle_ms": round(idle[0] * 1000, 3), "loop_selects": idle[1],
                # main-thread CPU time: (wall - idle) - cpu ≈ time the loop thread was runnable but
                # blocked (GIL hand-offs to the engine worker, lock waits, page faults)
-               "main_cpu_ms": round((c1 - c0) * 1000, 3)}
+               "main_cpu_ms": round((c1 - c0) * 1000, 3),
+               "reset_ms": round(getattr(sh, "last_reset_s", 0.0) * 1000, 3)}
         if dev_trace:
             trc = ds.read_batch_trace(sched.engine)
             if trc:

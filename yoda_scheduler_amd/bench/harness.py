@@ -238,10 +238,13 @@ class HttpShard:
     async def burst(self, tag: str = "b", timeout: float = 600.0) -> BurstResult:
         sched = self.sched
         q = sched.queue
+        self.last_reset_s = 0.0
         if self._bursts:
+            tr = time.perf_counter()
             await self._call("POST", "/debug/bench/reset")
             while sched.cache.pods or q._active_entries or sched.pending_binds:
                 await asyncio.sleep(0.001)      # the deletes reached the scheduler
+            self.last_reset_s = time.perf_counter() - tr
         self._bursts += 1
         sched.e2e_samples.clear()
         # every step is an independent burst: the client's token bucket starts full, as
