@@ -523,10 +523,20 @@ __device__ __forceinline__ ScoreConsts score_consts(const yoda_dev_req_t& r, con
 // wins), the yoda score's allocate + actual + gang terms (`rbase_o`) and the upstream default
 // scores (`total_o`). Outputs valid on the group's `sub == 0` lane when `act`. Every shuffle
 // is executed by every lane (callers iterate wave-uniformly).
+struct GangBest {
+  int64_t o;
+  int32_t lb;
+  uint8_t m, found;
+};
+
+// `rep` / `nrep`: this group searches subsets s_begin + 8·rep + sub, step 8·nrep (the batch
+// kernel splits a node's subset table over nrep lane groups; replicas ≥ 1 only search and
+// hand their best back through `gang_o`, valid on sub == 0); replica 0 also scores.
 __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act, uint32_t emask,
                                              const yoda_dev_req_t& r, const ScoreConsts& sc,
                                              const uint8_t* s_masks, int sub, uint64_t& rbase_o, int64_t& total_o,
-                                             uint32_t& mask_o, int32_t& quality_o) {
+                                             uint32_t& mask_o, int32_t& quality_o, int rep = 0, int nrep = 1,
+                                             GangBest* gang_o = nullptr) {
   const int k = sc.k;
   const bool search = sc.search, yoda_s = sc.yoda_s;
   const int32_t P = sc.P;
@@ -575,7 +585,7 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
   int64_t best_o = LLONG_MAX;
   int32_t best_lb = 0;
   bool found = false;
-  if (search && act && k == 1) {
+  if (search && act && k == 1 && rep == 0) {
     // single-GPU pods (the bulk of a mixed burst): the k = 1 table is {1<<0 … 1<<7} in
     // order, so lane `sub` owns subset {sub}; no pairs (P = 0) and one NUMA domain leave
     // only the fit and occupancy terms — the generic loop's 28 predicated pair adds and
@@ -601,7 +611,7 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
     GANG_STEP1(kDppXor1);
     GANG_STEP1(kDppXor2);
     GANG_STEP1(kDppRowHalfMirror);
-  } else if (search && act) {
+  } else if (search && act && k > 1) {
     // numa + card-pair qualities: only the multi-GPU search reads them
     uint32_t numa[YODA_DEV_CARDS];
 #pragma unroll
@@ -626,7 +636,7 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
         const int idx = a * YODA_DEV_CARDS + b;
         uni = uni && ((lq[idx >> 1] >> ((idx & 1) * 16)) & 0xFFFFu) == q01;
       }
-    for (int t = s_begin + sub; t < s_end; t += kGroup) {
+    for (int t = s_begin + kGroup * rep + sub; t < s_end; t += kGroup * nrep) {
       const uint32_t m = s_masks[t];
       if (m & ~emask) continue;
       int32_t qsum = 0;
@@ -675,42 +685,51 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
   }
 #undef GANG_STEP1
 #undef GANG_STEP
+  if (gang_o && act && sub == 0) *gang_o = GangBest{best_o, best_lb, (uint8_t)best_m, (uint8_t)found};
   const int32_t quality = found ? 10000 - sdiv_small_r(best_lb, 100, 0.01) : 10000;
   // ---- yoda score terms that need no maxima (algorithm.go:28-87 with the Q1/Q2/Q3/Q4
-  // fixes): allocate + actual over the node's cards (sums above), plus the gang bonus
-  if (act && sub == 0) {
-    uint64_t rb = 0;
-    if (yoda_s) {
-      const double rt = t64 ? rcp64((double)t64) : 0.0;
-      const uint64_t actual = t64 ? udiv_r(fsum * 100, t64, rt) * 2 : 0;
-      const uint64_t allocate = (t64 == 0 || t64 < a64) ? 0 : udiv_r((t64 - a64) * 100, t64, rt) * 3;
-      rb = allocate + actual;
-      if (r.has_number && r.number > 1 && r.number <= ncards && found)
-        rb += (uint64_t)(quality / 100) * (uint64_t)r.w_gang_score;
-    }
-    // upstream default scores (engine.cpp Engine::score_nodes)
+  // fixes): allocate + actual over the node's cards (sums above), plus the gang bonus, and
+  // the upstream default scores (engine.cpp Engine::score_nodes). The divisions are
+  // independent, so the group's 8 lanes take one each instead of lane 0 chaining them:
+  //   lane 0 actual·2, 1 allocate·3, 2/3 least cpu/mem, 4/5 most cpu/mem, 6 balanced;
+  // every term is ≤ 500 (percentages of a node's own capacity), so one 32-bit DPP group sum
+  // carries them packed: bits 0-8 yoda (≤ 500), 9-16 least (≤ 200), 17-24 most (≤ 200),
+  // 25-31 balanced (≤ 100).
+  if (act && rep == 0) {
     const int64_t rc = nd->nz_cpu + r.nz_cpu_m, rm = nd->nz_mem + r.nz_mem;
     const int64_t ac = nd->alloc_cpu, am = nd->alloc_mem;
-    int64_t extra = r.w_const;
-    if (r.w_least || r.w_most) {
-      const double rac = ac > 0 ? rcp64((double)ac) : 0.0, ram = am > 0 ? rcp64((double)am) : 0.0;
-      int64_t least = 0, most = 0;
-      if (ac > 0 && rc <= ac) least += (int64_t)udiv_r((uint64_t)(ac - rc) * 100, (uint64_t)ac, rac);
-      if (am > 0 && rm <= am) least += (int64_t)udiv_r((uint64_t)(am - rm) * 100, (uint64_t)am, ram);
-      if (ac > 0) most += (int64_t)udiv_r((uint64_t)(rc < ac ? rc : ac) * 100, (uint64_t)ac, rac);
-      if (am > 0) most += (int64_t)udiv_r((uint64_t)(rm < am ? rm : am) * 100, (uint64_t)am, ram);
-      extra += r.w_least * (least / 2) + r.w_most * (most / 2);
+    const bool lm = r.w_least || r.w_most;
+    uint64_t num = 0, den = 0;
+    uint32_t mul = 1, shift = 0;
+    switch (sub) {
+      case 0: if (yoda_s && t64) { num = fsum * 100; den = t64; mul = 2; } break;
+      case 1: if (yoda_s && t64 && t64 >= a64) { num = (t64 - a64) * 100; den = t64; mul = 3; } break;
+      case 2: if (lm && ac > 0 && rc <= ac) { num = (uint64_t)(ac - rc) * 100; den = (uint64_t)ac; } shift = 9; break;
+      case 3: if (lm && am > 0 && rm <= am) { num = (uint64_t)(am - rm) * 100; den = (uint64_t)am; } shift = 9; break;
+      case 4: if (lm && ac > 0) { num = (uint64_t)(rc < ac ? rc : ac) * 100; den = (uint64_t)ac; } shift = 17; break;
+      case 5: if (lm && am > 0) { num = (uint64_t)(rm < am ? rm : am) * 100; den = (uint64_t)am; } shift = 17; break;
+      default: break;
     }
-    if (r.w_balanced) {
+    uint32_t part = den ? (uint32_t)udiv_r(num, den, rcp64((double)den)) * mul << shift : 0u;
+    if (sub == 6 && r.w_balanced) {
       const double cf = ac > 0 ? (double)rc / (double)ac : 1.0;
       const double mf = am > 0 ? (double)rm / (double)am : 1.0;
-      const int64_t b = (cf >= 1 || mf >= 1) ? 0 : (int64_t)((1.0 - fabs(cf - mf)) * 100);
-      extra += r.w_balanced * b;
+      const uint32_t b = (cf >= 1 || mf >= 1) ? 0u : (uint32_t)(int64_t)((1.0 - fabs(cf - mf)) * 100);
+      part = b << 25;
     }
-    rbase_o = rb;
-    total_o = extra;
-    mask_o = best_m;
-    quality_o = quality;
+    const uint32_t packed = gsum(part);
+    if (sub == 0) {
+      uint64_t rb = packed & 0x1FFu;
+      if (yoda_s && r.has_number && r.number > 1 && r.number <= ncards && found)
+        rb += (uint64_t)(quality / 100) * (uint64_t)r.w_gang_score;
+      int64_t extra = r.w_const;
+      if (lm) extra += r.w_least * (int64_t)(((packed >> 9) & 0xFFu) / 2) + r.w_most * (int64_t)(((packed >> 17) & 0xFFu) / 2);
+      if (r.w_balanced) extra += r.w_balanced * (int64_t)(packed >> 25);
+      rbase_o = rb;
+      total_o = extra;
+      mask_o = best_m;
+      quality_o = quality;
+    }
   }
 }
 
@@ -974,6 +993,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   __shared__ uint32_t s_rec[14][kMaxGrid + 4];   // gather-1 records transposed (+4: bank skew)
   // filter aggregates per 8-node group: 6 maxima, feasible count, 7 reason counts
   __shared__ uint32_t s_grp[kMaxGroups][14];
+  __shared__ GangBest s_gang[8 * BW];
   __shared__ int s_fail;
   __shared__ bool s_last;
   static_assert(sizeof(yoda_dev_result_t) % 8 == 0, "result copied as u64 words");
@@ -1093,20 +1113,58 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     // ================= phase A (while record 1 travels): gang search, the yoda terms that
     // need no maxima (kept in s_raw until phase B), default scores
     ScoreConsts sc = score_consts(r, nullptr);
-    for (int j0 = wave * kNodesPerWave; j0 < cnt; j0 += BW * kNodesPerWave) {
-      const int j = j0 + grp;
-      const bool act = j < cnt && s_feas[j];
-      const uint32_t emask = act ? s_elig[j] : 0u;
-      uint64_t rbase = 0;
-      int64_t total_v = 0;
-      uint32_t mask_v = 0;
-      int32_t quality_v = 0;
-      score_node_a(s_rows + (j < cnt ? j : 0), act, emask, r, sc, s_masks, sub, rbase, total_v, mask_v, quality_v);
-      if (act && sub == 0) {
-        s_raw[j] = (int64_t)rbase;
-        s_total[j] = total_v;
-        s_mask[j] = (uint8_t)mask_v;
-        s_quality[j] = quality_v;
+    {
+      // a multi-GPU pod's subset search is split over `nrep` lane groups per node when the
+      // block has more waves than node groups (8 waves over 32 nodes: two groups per node,
+      // two waves per SIMD); the replicas' bests meet through LDS below
+      const int ngroups = (npb + kNodesPerWave - 1) / kNodesPerWave;
+      const int nrep = (sc.search && sc.k > 1 && ngroups <= BW) ? BW / ngroups : 1;
+      for (int it = wave; it < ngroups * nrep; it += BW) {
+        const int rep = it / ngroups;
+        const int j = (it - rep * ngroups) * kNodesPerWave + grp;
+        const bool act = j < cnt && s_feas[j];
+        const uint32_t emask = act ? s_elig[j] : 0u;
+        uint64_t rbase = 0;
+        int64_t total_v = 0;
+        uint32_t mask_v = 0;
+        int32_t quality_v = 0;
+        GangBest gb;
+        score_node_a(s_rows + (j < cnt ? j : 0), act, emask, r, sc, s_masks, sub, rbase, total_v, mask_v, quality_v,
+                     rep, nrep, nrep > 1 ? &gb : nullptr);
+        if (act && sub == 0) {
+          if (rep == 0) {
+            s_raw[j] = (int64_t)rbase;
+            s_total[j] = total_v;
+            s_mask[j] = (uint8_t)mask_v;
+            s_quality[j] = quality_v;
+          }
+          if (nrep > 1) s_gang[rep * npb + j] = gb;   // < nrep·npb ≤ 8·BW
+        }
+      }
+      if (nrep > 1) {
+        __syncthreads();
+        // replica 0 scored with its own best: where another replica found a better set,
+        // take it and move the gang bonus (the only score term that depends on the set)
+        for (int j = tid; j < cnt; j += kBB) {
+          if (!s_feas[j]) continue;
+          const GangBest b0 = s_gang[j];
+          GangBest b = b0;
+          for (int q = 1; q < nrep; ++q) {
+            const GangBest o = s_gang[q * npb + j];
+            if (o.found && (!b.found || better(o.o, o.m, b.o, b.m))) b = o;
+          }
+          if (b.found == b0.found && b.m == b0.m) continue;
+          const int32_t q_old = s_quality[j];
+          const int32_t q_new = b.found ? 10000 - sdiv_small_r(b.lb, 100, 0.01) : 10000;
+          s_mask[j] = b.m;
+          s_quality[j] = q_new;
+          if (sc.yoda_s && r.has_number && r.number > 1 && r.number <= s_rows[j].ncards) {
+            uint64_t rb = (uint64_t)s_raw[j];
+            if (b0.found) rb -= (uint64_t)(q_old / 100) * (uint64_t)r.w_gang_score;
+            if (b.found) rb += (uint64_t)(q_new / 100) * (uint64_t)r.w_gang_score;
+            s_raw[j] = (int64_t)rb;
+          }
+        }
       }
     }
     TRACE(2);

@@ -103,9 +103,9 @@ def test_scheduler_auto_enables_device_scorer_and_matches_cpu(require_gpu):
             for n in {node for node, _ in placed.values()}:
                 for g, st in enumerate(sched.cache.node_gpu_state(n)):
                     assert st["reserved"] == want_mb.get((n, g), 0), (n, g, st)
-            # overlapEngine auto: with the device scorer the batches ran on the engine worker
+            # overlapEngine auto: with the device scorer the batches ran on the native engine worker
             stats = (sched.engine.device_enabled, sched.engine.device_cycles, sched.engine.device_fallbacks,
-                     sched.device_error, sched._engine_exec is not None)
+                     sched.device_error, sched._batch_worker is not None)
             await c.stop()
             return ok, placed, stats
         return asyncio.run(go())
