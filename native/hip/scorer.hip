@@ -954,15 +954,24 @@ __device__ __forceinline__ bool gather(const BatchArgs& a, uint32_t tag, int G, 
     const gu64* p = slot_ptr(a, tag, t < G ? t : 0);
     const long long t0 = __builtin_amdgcn_s_memrealtime();
     for (unsigned spins = 0;;) {
-      bool ok = true;
+      // poll one granule per record until every record's has landed, then read the rest
+      // (written in the same instant by the producer's other threads): a waiting block
+      // loads G words per round instead of G·K — with G blocks all polling each other that
+      // is the fabric traffic of the wait
+      const unsigned long long x0 = t < G ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                          : ((unsigned long long)tag << 32);
+      bool ok = (uint32_t)(x0 >> 32) == tag;
+      if (__all(ok)) {
+        v[0] = (uint32_t)x0;
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const unsigned long long x = t < G ? __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                           : ((unsigned long long)tag << 32);
-        v[k] = (uint32_t)x;
-        ok &= (uint32_t)(x >> 32) == tag;
+        for (int k = 1; k < K; ++k) {
+          const unsigned long long x = t < G ? __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                             : ((unsigned long long)tag << 32);
+          v[k] = (uint32_t)x;
+          ok &= (uint32_t)(x >> 32) == tag;
+        }
+        if (__all(ok)) break;
       }
-      if (__all(ok)) break;
       if (!spin_ok(a, spins, t0)) {
         failed = true;
         break;
