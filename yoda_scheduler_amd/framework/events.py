@@ -85,6 +85,17 @@ class EventRecorder:
         self._buf.append((pod_obj_meta, kind, typ, reason, message, time.time(), controller, related))
         self._wake.set()
 
+    def pod_scheduled(self, pi, node: str) -> None:
+        """``Scheduled`` for a bound pod; the message is formatted only if the event is kept
+        (a burst fills the buffer and then drops most of them)."""
+        if not self.enabled:
+            return
+        if len(self._buf) >= self.max_buffer:
+            self.recorded["Scheduled"] += 1
+            self.dropped += 1
+            return
+        self.pod_event(pi, "Normal", "Scheduled", f"Successfully assigned {pi.namespace}/{pi.name} to {node}")
+
     def pod_event(self, pi, typ: str, reason: str, message: str, related=None) -> None:
         if self.enabled:
             rel = None if related is None else {"apiVersion": "v1", "kind": "Pod", "name": related.name,

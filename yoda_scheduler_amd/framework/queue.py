@@ -229,6 +229,9 @@ class SchedulingQueue:
     def move_all_to_active_or_backoff(self, event: str = "") -> int:
         """A cluster event (node add, Scv update, pod delete...) may make parked pods
         schedulable."""
+        if not self._unsched:                  # the common case (every pod deletion): only
+            self._move_request_cycle = self.scheduling_cycle   # record the move request
+            return 0
         pods = [pi for pi, _ in self._unsched.values()]
         self._unsched.clear()
         return self._move(pods, event)

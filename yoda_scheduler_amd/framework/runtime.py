@@ -305,6 +305,10 @@ class Framework:
             return st
         return Status.error("no bind plugin bound the pod")
 
+    @property
+    def post_bind_noop(self) -> bool:
+        return not self.post_bind
+
     def run_post_bind(self, state: CycleState, pod, node: str) -> None:
         for p in self.post_bind:
             p.post_bind(state, pod, node)

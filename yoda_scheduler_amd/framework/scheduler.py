@@ -885,6 +885,18 @@ class Scheduler:
         fw, state, pi, node, cycle, t0 = item
         self.pending_binds -= 1
         if 200 <= status < 300:
+            if self.tracer is None and fw.post_bind_noop:
+                # the common case inlined (_after_bind's success branch, no tracer / PostBind)
+                now = time.perf_counter()
+                m = self.metrics
+                m.binding.observe(now - tb)
+                self.cache.finish_binding(pi)
+                self.scheduled += 1
+                if self.e2e_samples is not None:
+                    self.e2e_samples.append(now - t0)
+                m.child(m.e2e, "scheduled", fw.name).observe(now - t0)
+                self.recorder.pod_scheduled(pi, node)
+                return
             st = Status.ok()
         else:
             from ..kube.native import api_error
@@ -907,7 +919,7 @@ class Scheduler:
             if self.e2e_samples is not None:
                 self.e2e_samples.append(time.perf_counter() - t0)
             m.child(m.e2e, "scheduled", fw.name).observe(time.perf_counter() - t0)
-            self.recorder.pod_event(pi, "Normal", "Scheduled", f"Successfully assigned {pi.key} to {node}")
+            self.recorder.pod_scheduled(pi, node)
         else:
             self.bind_errors += 1
             fw.run_unreserve(state, pi, node)
