@@ -799,7 +799,16 @@ void Server::handle_bench(Conn* c, Request& req) {
     std::vector<std::string> keys;
     for (const auto& kv : pods.objs) keys.push_back(kv.first);
     ApiErr err;
-    for (const auto& k : keys) remove(pods, k, &err);
+    size_t i = 0;
+    for (const auto& k : keys) {
+      remove(pods, k, &err);
+      if (++i % 64 == 0) {
+        // as for the burst: the watchers see the deletions while they are being made
+        std::vector<Conn*> d;
+        d.swap(dirty_);
+        for (Conn* x : d) flush(x);
+      }
+    }
     create_log_.clear();
     bind_log_.clear();
     respond(c, 200, "{\"deleted\":" + std::to_string(keys.size()) + "}");
