@@ -253,6 +253,12 @@ class Scv:
         return (now - t) * 1000.0 > factor * max(self.update_interval_ms, 1)
 
 
+def card_vis(ids: list) -> list:
+    """Per card position of ``(id, amd-smi UUID, ROCr UUID, HIP ordinal)`` identities: the
+    ROCr-visible id (ROCr UUID, else HIP ordinal, else the amd-smi index) and the UUID."""
+    return [(c[2] if c[2] else (str(c[3]) if c[3] >= 0 else str(c[0])), c[1]) for c in ids]
+
+
 class LazyScv:
     """An ``Scv`` as the informer delivered it (decoded JSON), turned into the dataclass
     tree only when something reads it. The scheduler's per-update path needs neither: the
@@ -274,14 +280,13 @@ class LazyScv:
         self._obj = obj
         self._scv = None
         self._idents = idents
-        self._vis = None
+        self._vis = card_vis(idents) if idents is not None else None   # at ingest, off the bind path
         self.ann_memo: dict = {}       # the scheduler's Binding annotations per (GPU set, HBM)
 
     def card_vis(self) -> list:
         """Per card position: (ROCr-visible id, amd-smi UUID) as the Binding annotations spell
-        them (``plugins.defaults.card_vis``), computed once per Scv version."""
+        them (``card_vis``), computed once per Scv version."""
         if self._vis is None:
-            from ..plugins.defaults import card_vis
             self._vis = card_vis(self.card_idents())
         return self._vis
 

@@ -18,6 +18,7 @@ from ..framework.interfaces import (BindPlugin, CycleState, FilterPlugin, Native
                                     PostFilterPlugin, PostFilterResult, QueueSortPlugin, ScorePlugin, Status)
 from ..models.labels import ANNOTATION_GPU_UUIDS, ANNOTATION_GPUS, ANNOTATION_RESERVED, ANNOTATION_VISIBLE
 from ..models.pod import PF_EXTENDED, PF_HOST_PORTS
+from ..models.scv import LazyScv, card_vis
 from ..ops.native import core
 
 
@@ -169,24 +170,25 @@ def _inert(name: str):
 INERT_PLUGINS = ["CSILimits"]
 
 
-def card_vis(ids: list) -> list:
-    """Per card position of ``(id, amd-smi UUID, ROCr UUID, HIP ordinal)`` identities: the
-    ROCr-visible id (ROCr UUID, else HIP ordinal, else the amd-smi index) and the UUID."""
-    return [(c[2] if c[2] else (str(c[3]) if c[3] >= 0 else str(c[0])), c[1]) for c in ids]
-
-
 def visible_device_ids(scv, cards: list) -> tuple[str, str]:
     """(ROCR_VISIBLE_DEVICES value, amd-smi UUID list) for the assigned card positions of a
     node's Scv. Per card: ROCr UUID, else HIP ordinal, else the amd-smi index."""
     if scv is None:
-        per = []
-    elif hasattr(scv, "card_vis"):             # LazyScv: computed once per Scv version
+        per = ()
+    elif isinstance(scv, LazyScv):             # computed once per Scv version
         per = scv.card_vis()
     else:
         per = card_vis([(c.id, c.uuid, c.hip_uuid, c.hip_id) for c in scv.status.card_list])
     n = len(per)
-    vis = [per[c][0] if 0 <= c < n else str(c) for c in cards]
-    uuids = [per[c][1] for c in cards if 0 <= c < n and per[c][1]]
+    vis, uuids = [], []
+    for c in cards:
+        if 0 <= c < n:
+            v, u = per[c]
+            vis.append(v)
+            if u:
+                uuids.append(u)
+        else:
+            vis.append(str(c))
     return ",".join(vis), (",".join(uuids) if len(uuids) == len(cards) else "")
 
 
@@ -196,7 +198,7 @@ def bind_annotations(pod, scvs: Optional[dict] = None, node: str = "") -> list:
     cards = getattr(pod, "assigned_cards", None)
     if cards is None:
         return []
-    ann = [(ANNOTATION_GPUS, ",".join(str(c) for c in cards))]
+    ann = [(ANNOTATION_GPUS, ",".join(map(str, cards)))]
     vis, uuids = visible_device_ids((scvs or {}).get(node), cards)
     ann.append((ANNOTATION_VISIBLE, vis))
     if uuids:
