@@ -207,7 +207,8 @@ PYBIND11_MODULE(_yoda_kube, m) {
         d["throttled"] = s.throttled;
         return d;
       })
-      // [(0, id, status, body) | (1, id, [(type, rv, PodEvent | bytes | None), ...]) | (2, id, status, body)]
+      // [(0, id, status, body) | (1, id, [(type, rv, PodEvent | bytes | None, ident | None), ...]) |
+      //  (2, id, status, body)]; ident = PodEvent.ident(), built here in the same pass
       .def("drain", [](Transport& t) {
         std::vector<Completion> cs = t.drain();
         // leaked on purpose: must outlive interpreter finalisation
@@ -219,11 +220,18 @@ PYBIND11_MODULE(_yoda_kube, m) {
             py::list evs;
             for (auto& e : c.events) {
               int ti = e.type == 'A' ? 0 : e.type == 'M' ? 1 : e.type == 'D' ? 2 : e.type == 'B' ? 3 : 4;
-              py::object payload;
-              if (e.pod) payload = py::cast(e.pod);
-              else if (e.type == 'B') payload = py::none();
-              else payload = py::bytes(e.raw);
-              evs.append(py::make_tuple(types[ti], py::str(e.rv), payload));
+              py::object payload, ident = py::none();
+              if (e.pod) {
+                payload = py::cast(e.pod);
+                const PodProj& p = e.pod->p;
+                ident = py::make_tuple(py::str(p.ns + "/" + p.name), py::str(p.uid), py::str(p.node), py::str(p.sched),
+                                       py::str(p.phase), p.spec_meta_hash);
+              } else if (e.type == 'B') {
+                payload = py::none();
+              } else {
+                payload = py::bytes(e.raw);
+              }
+              evs.append(py::make_tuple(types[ti], py::str(e.rv), payload, ident));
             }
             out.append(py::make_tuple(1, c.id, evs));
           } else {

@@ -373,7 +373,7 @@ class KubeClient:
         try:
             while True:
                 while q:
-                    typ, _rv, payload = q.popleft()
+                    typ, _rv, payload, _idt = q.popleft()
                     obj = json.loads(payload) if payload else {"metadata": {"resourceVersion": _rv}}
                     if typ == "ERROR":
                         raise ApiError(int(obj.get("code", 500)), obj.get("reason", "Error"), obj.get("message", ""))

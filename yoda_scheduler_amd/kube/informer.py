@@ -270,7 +270,7 @@ class NativePodInformer(Informer):
                 return
             # _dispatch_native + _call inlined: this loop runs three times per scheduled pod
             entries, handler = self.entries, self.on_event
-            for typ, rv, payload in evs:
+            for typ, rv, payload, idt in evs:
                 if typ == "BOOKMARK":
                     if rv:
                         self.resource_version = rv
@@ -286,7 +286,6 @@ class NativePodInformer(Informer):
                     if not done.done():
                         done.set_result((0, b""))
                     return
-                idt = payload.ident()
                 key = idt[0]
                 try:
                     if typ == "DELETED":
