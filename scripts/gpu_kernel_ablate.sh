@@ -1,4 +1,9 @@
-# k_batch phase-time ablations (timing only: the ablated builds compute wrong scores)
+# k_batch phase-time ablations (timing only: the ablated builds compute wrong scores).
+# The variants were built from a copy of native/hip/scorer.hip with (a) the score tail of
+# score_node_a replaced by a trivial assignment (ABL_TAIL) and (b) the k >= 2 gang-search
+# branch disabled (ABL_GANG), each as yoda_scheduler_amd/_native/libyoda_hip_abl_{tail,gang}.so
+# (hipcc --offload-arch=gfx950 -O3 -shared -fPIC scorer.hip probes.hip); results in
+# profiles/device/ablation_r2.jsonl.
 set -u
 mkdir -p gpurun_out
 : > gpurun_out/ablate.jsonl
