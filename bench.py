@@ -71,6 +71,8 @@ def main(argv=None) -> int:
     ap.add_argument("--burst", type=int, default=10000, help="client burst (deploy default 10000; reference 100)")
     ap.add_argument("--reference-qps", action="store_true", help="use the reference's client limits 50/100")
     ap.add_argument("--batch", type=int, default=256, help="native batch size (1 = strictly one pod per cycle)")
+    ap.add_argument("--engine-threads", type=int, default=1,
+                    help="C++ engine worker threads for the CPU filter/score path (yodaRuntime.engineThreads)")
     ap.add_argument("--compat", action="store_true", help="reference-compatible yoda scoring (no HBM ledger)")
     ap.add_argument("--no-events", action="store_true")
     ap.add_argument("--transport", choices=["inproc", "http"], default="http",
@@ -128,12 +130,14 @@ def main(argv=None) -> int:
             # one apiserver process per rank; bursts reuse it (the previous burst is deleted first)
             one = HttpShard(w, qps=a.qps, burst=a.burst, batch=a.batch, template=tmpl, events=not a.no_events,
                             compat=a.compat, seed=rank * 1000, device=a.device, overlap=a.overlap,
-                            apiserver=a.apiserver, client_native=a.client == "native")
+                            apiserver=a.apiserver, client_native=a.client == "native",
+                            engine_threads=a.engine_threads)
             shards = [one] * (a.warmup + a.steps)
             loop.run_until_complete(one.start())
         else:
             shards = [Shard(w, qps=a.qps, burst=a.burst, batch=a.batch, template=tmpl, events=not a.no_events,
-                            compat=a.compat, seed=rank * 1000 + i, device=a.device, overlap=a.overlap)
+                            compat=a.compat, seed=rank * 1000 + i, device=a.device, overlap=a.overlap,
+                            engine_threads=a.engine_threads)
                       for i in range(a.warmup + a.steps)]
             for s in shards:
                 loop.run_until_complete(s.start())
@@ -233,7 +237,7 @@ def main(argv=None) -> int:
                        "parallelism": f"shard{world}" if world > 1 else "shard1"},
             **{k: v for k, v in head.items() if k != "value" and k != "ms_per_step"},
             "node_gpus": a.node_gpus or w.nodes[0][2],
-            "client_qps": a.qps, "client_burst": a.burst, "native_batch": a.batch, "compat": a.compat,
+            "client_qps": a.qps, "client_burst": a.burst, "native_batch": a.batch, "engine_threads": a.engine_threads, "compat": a.compat,
             "device_scorer": a.device, "overlap_engine": a.overlap,
             "baseline_note": "vs_baseline divides by BASELINE.md's derived (unmeasured) ~55 pods/s reference ceiling "
                              "(kube-scheduler v1.20 client QPS 50 / burst 100): a client-QPS bound, not a measured "

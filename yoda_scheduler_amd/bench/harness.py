@@ -22,7 +22,7 @@ from .workloads import Workload, pod_object, populate
 
 
 def bench_config(scheduler_name: str, qps: float, burst: int, batch: int, compat: bool = False,
-                 device: str = "auto", overlap: str = "auto") -> dict:
+                 device: str = "auto", overlap: str = "auto", engine_threads: int = 1) -> dict:
     """The shipped deploy profile (yoda at filter + score weight 300 on top of the
     upstream defaults) with the yoda QueueSort enabled (Q7) and the given client QPS."""
     prof = {"schedulerName": scheduler_name,
@@ -36,7 +36,7 @@ def bench_config(scheduler_name: str, qps: float, burst: int, batch: int, compat
             "clientConnection": {"qps": qps, "burst": burst},
             "percentageOfNodesToScore": 0, "podInitialBackoffSeconds": 1, "podMaxBackoffSeconds": 10,
             "yodaRuntime": {"batchSize": batch, "bindConcurrency": 256, "deviceScorer": {"enabled": device},
-                            "overlapEngine": overlap},
+                            "overlapEngine": overlap, "engineThreads": engine_threads},
             "profiles": [prof]}
 
 
@@ -163,7 +163,7 @@ class HttpShard:
     def __init__(self, w: Workload, qps: float = 5000.0, burst: int = 10000, batch: int = 256,
                  template: Optional[dict] = None, events: bool = True, compat: bool = False, seed: int = 0,
                  device: str = "auto", overlap: str = "auto", apiserver: str = "native",
-                 client_native: str | bool = "auto") -> None:
+                 client_native: str | bool = "auto", engine_threads: int = 1) -> None:
         import json
         import os
         import subprocess
@@ -189,7 +189,8 @@ class HttpShard:
             root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
             env = dict(os.environ, PYTHONPATH=os.pathsep.join(p for p in (root, os.environ.get("PYTHONPATH")) if p))
         self.proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env)
-        self.cfg = parse_config(bench_config(w.scheduler_name, qps, burst, batch, compat, device, overlap))
+        self.cfg = parse_config(bench_config(w.scheduler_name, qps, burst, batch, compat, device, overlap,
+                                             engine_threads))
         self.events, self.seed = events, seed
         self.sched: Optional[Scheduler] = None
         self.client = None
