@@ -78,6 +78,7 @@ async def soak(rounds: int, pods: int, nodes: int, bind_fail: float, drop_watch:
         row = {"round": r, "bound": len(srv.bind_log), "pods_per_s": round(len(srv.bind_log) / dt, 1),
                "drained": drained, "drift": drift, "reserved_mb_left": reserved, "rss_mb": round(rss, 1),
                "objects": len(gc.get_objects()), "bind_errors": sched.bind_errors,
+               "device_cycles": sched.engine.device_cycles, "device_fallbacks": sched.engine.device_fallbacks,
                "relists": sum(inf.relists for inf in sched.informers.values())}
         out["rounds"].append(row)
         log(json.dumps(row))
