@@ -23,6 +23,8 @@ async def run(a) -> list:
     w = make_workload(a.config)
     sh = HttpShard(w, batch=a.batch, device=a.device, overlap=a.overlap)
     sh.cfg.trace = True
+    if a.overlap_depth:
+        sh.cfg.overlap_depth = a.overlap_depth
     await sh.start()
     sched = sh.sched
     for i in range(a.warmup):
@@ -168,6 +170,7 @@ def main() -> int:
     ap.add_argument("--repeat", type=int, default=1, help="untimed bursts before the traced ones")
     ap.add_argument("--bursts", type=int, default=1, help="consecutive traced bursts (one JSON line each)")
     ap.add_argument("--device-trace", action="store_true", help="k_batch phase stamps of the last chunk")
+    ap.add_argument("--overlap-depth", type=int, default=0, help="yodaRuntime.overlapDepth (0: config default)")
     a = ap.parse_args()
     try:
         import torch  # noqa: F401 - share torch's HIP runtime, as bench.py does
