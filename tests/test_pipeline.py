@@ -66,3 +66,58 @@ def test_pods_arriving_during_a_batch_are_submitted_behind_it():
     first_done = calls[0][1]
     # the second batch was handed to the engine while the first one was still running
     assert submits[1][2] >= 1 and submits[1][0] < first_done, (submits, calls)
+
+
+class FlakyEngine(SlowEngine):
+    """``schedule_batch`` raises on its first call (after reserving nothing)."""
+
+    def __init__(self, eng) -> None:
+        super().__init__(eng, 0.0)
+        self.failures = 0
+
+    def schedule_batch(self, ids, reqs):
+        if self.failures == 0:
+            self.failures += 1
+            raise RuntimeError("injected engine failure")
+        return super().schedule_batch(ids, reqs)
+
+
+def test_failed_engine_batch_requeues_its_pods_and_the_loop_keeps_going():
+    async def go():
+        cfg = yoda_config(batch=64, backoff=0.01, max_backoff=0.05)
+        cfg["yodaRuntime"]["overlapEngine"] = "on"
+        c = FakeCluster(cfg)
+        c.add_node("n0")
+        await c.start()
+        sched = c.sched
+        sched.engine = FlakyEngine(sched.engine)
+        names = [f"p{i}" for i in range(12)]
+        for n in names:
+            c.add_pod(n, {"scv/memory": "1024"})
+        ok = await c.wait(lambda: all(c.node_of(p) for p in names), 10.0, 0.005)
+        errors, failures = sched.engine_batch_errors, sched.engine.failures
+        ledger = sched.engine.ledger_size
+        await c.stop()
+        return ok, errors, failures, ledger
+    ok, errors, failures, ledger = asyncio.run(go())
+    assert ok and errors == 1 and failures == 1 and ledger == 12
+
+
+def test_failed_inline_engine_batch_requeues_its_pods():
+    async def go():
+        cfg = yoda_config(batch=64, backoff=0.01, max_backoff=0.05)
+        cfg["yodaRuntime"]["overlapEngine"] = "off"
+        c = FakeCluster(cfg)
+        c.add_node("n0")
+        await c.start()
+        sched = c.sched
+        sched.engine = FlakyEngine(sched.engine)
+        names = [f"q{i}" for i in range(12)]
+        for n in names:
+            c.add_pod(n, {"scv/memory": "1024"})
+        ok = await c.wait(lambda: all(c.node_of(p) for p in names), 10.0, 0.005)
+        errors = sched.engine_batch_errors
+        await c.stop()
+        return ok, errors
+    ok, errors = asyncio.run(go())
+    assert ok and errors == 1

@@ -141,6 +141,7 @@ class Scheduler:
         self._tasks: list[asyncio.Task] = []
         self._engine_exec = None          # worker thread of schedule_batch_overlapped
         self._batch_worker = None         # native engine worker (core.BatchWorker)
+        self.engine_batch_errors = 0
         self._batch_futs: dict = {}
         self.engine_spans: Optional[list] = None   # (t_start, t_end, pods) of native batches
         self._inflight: collections.deque = collections.deque()   # (fw, run, cycle, t0, future) on that worker
@@ -725,7 +726,12 @@ class Scheduler:
                 self.schedule_one(item)
                 continue
             cycle, t0, ids, reqs = self._prepare_run(fw, item)
-            self._finish_run(fw, item, self.engine.schedule_batch(ids, reqs), cycle, t0)
+            try:
+                results = self.engine.schedule_batch(ids, reqs)
+            except Exception as e:  # noqa: BLE001 - as _finish_inflight_run
+                self._engine_batch_failed(item, cycle, e)
+                continue
+            self._finish_run(fw, item, results, cycle, t0)
 
     def _overlap(self) -> bool:
         mode = self.config.overlap_engine
@@ -793,8 +799,23 @@ class Scheduler:
 
     async def _finish_inflight_run(self, run: tuple) -> None:
         fw, item, cycle, t0, fut = run[:5]
-        results = await fut
+        try:
+            results = await fut
+        except asyncio.CancelledError:
+            raise
+        except Exception as e:  # noqa: BLE001 - a failed engine batch must not stop the loop
+            self._engine_batch_failed(item, cycle, e)
+            return
         self._finish_run(fw, item, results, cycle, t0)
+
+    def _engine_batch_failed(self, item: list, cycle: int, e: Exception) -> None:
+        """Drop whatever the engine may have reserved for the run and retry its pods from
+        backoff (an error, not "unschedulable")."""
+        self.engine_batch_errors += 1
+        log.error("engine batch of %d pods failed: %r; pods go back to the queue", len(item), e)
+        for p in item:
+            self.engine.release(p.num_id)
+            self.queue.add_unschedulable(p, cycle, unschedulable=False)
 
     async def _await_pods_or_result(self) -> None:
         """Wait until the oldest in-flight run's result lands (then apply it) or a pod reaches
