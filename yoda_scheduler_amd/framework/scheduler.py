@@ -106,6 +106,8 @@ class Scheduler:
         self.config = config
         self.registry = registry or default_registry()
         self.metrics = metrics if metrics is not None else SchedulerMetrics()
+        from ..utils.metrics import NullMetrics
+        self._metrics_on = not isinstance(self.metrics, NullMetrics)
         cc = config.client_connection
         # native transport: its C++ token bucket enforces clientConnection QPS/burst for
         # binds, status patches and deletes (one bucket, as client-go's limiter)
@@ -293,13 +295,19 @@ class Scheduler:
                 self.queue.move_all_to_active_or_backoff("AssignedPodCompleted")
                 return
             if not oidt[2]:
+                # the Binding's echo (usually of our own assumed pod)
                 self.queue.delete(uid)
                 if uid in self.nominations:
                     self._clear_nomination(uid)
-                if self.cache.is_assumed(uid):
-                    ps = self.cache.pods[uid]
-                    self.metrics.pod_scheduling.observe(max(0.0, time.monotonic() - ps.info.initial_attempt))
-                    self.metrics.pod_attempts.observe(ps.info.attempts)
+                ps = self.cache.pods.get(uid)
+                if ps is not None and ps.assumed:
+                    if self._metrics_on:
+                        self.metrics.pod_scheduling.observe(max(0.0, time.monotonic() - ps.info.initial_attempt))
+                        self.metrics.pod_attempts.observe(ps.info.attempts)
+                    if ps.node == node:          # confirm in place (cache.add_pod_native's fast path)
+                        ps.assumed, ps.deadline = False, None
+                        ps.info.set_source(ev)
+                        return
                 self.cache.add_pod_native(ev, uid, node)
             else:
                 self.cache.update_pod_native(ev, uid, node, oidt[5] == h)
