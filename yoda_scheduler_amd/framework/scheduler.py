@@ -286,7 +286,8 @@ class Scheduler:
                     self.cache.add_pod_native(ev, uid, node)
             elif sched in self.frameworks and not terminal:
                 self.queue.add(PodInfo.from_native(ev))
-                self.metrics.child(self.metrics.incoming, "PodAdd", "active").inc()
+                if self._metrics_on:
+                    self.metrics.child(self.metrics.incoming, "PodAdd", "active").inc()
             return
         oidt = old[1]
         if node:
@@ -570,8 +571,9 @@ class Scheduler:
                 self.cache.forget(pi)
                 self._fail(fw, state, pi, cycle, st.message(), t0, unschedulable=st.is_unschedulable())
                 return
-        m.algorithm.observe(time.perf_counter() - t0)
-        m.child(m.attempts, "scheduled", fw.name).inc()
+        if self._metrics_on:
+            m.algorithm.observe(time.perf_counter() - t0)
+            m.child(m.attempts, "scheduled", fw.name).inc()
         if klog.V(3):
             log.info("pod %s → node %s gpus=%s score=%d feasible=%d", pi.key, node, cards, res[4], res[1])
         self.pending_binds += 1
@@ -917,13 +919,14 @@ class Scheduler:
             if self.tracer is None and fw.post_bind_noop:
                 # the common case inlined (_after_bind's success branch, no tracer / PostBind)
                 now = time.perf_counter()
-                m = self.metrics
-                m.binding.observe(now - tb)
                 self.cache.finish_binding(pi)
                 self.scheduled += 1
                 if self.e2e_samples is not None:
                     self.e2e_samples.append(now - t0)
-                m.child(m.e2e, "scheduled", fw.name).observe(now - t0)
+                if self._metrics_on:
+                    m = self.metrics
+                    m.binding.observe(now - tb)
+                    m.child(m.e2e, "scheduled", fw.name).observe(now - t0)
                 self.recorder.pod_scheduled(pi, node)
                 return
             st = Status.ok()
