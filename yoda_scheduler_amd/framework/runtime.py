@@ -105,6 +105,31 @@ class Framework:
             self._flag_mask |= f
         self._gates = [p.cluster_active for p in self.conditional if hasattr(p, "cluster_active")]
 
+    def native_mask(self) -> Optional[int]:
+        """For a batch of pods: the pod-flag mask such that ``native_for(pod)`` is exactly
+        ``not (pod.flags & mask)``, or None when that shortcut does not hold right now (a
+        plugin without declared flags, or a cluster gate is active). Evaluated once per batch
+        instead of once per pod."""
+        if not self.fully_native_static:
+            return None
+        m = self._flag_mask
+        if m is None or any(g() for g in self._gates):
+            return None
+        return m
+
+    def direct_bind_mask(self) -> Optional[int]:
+        """Likewise for ``direct_binder_for``: pods without these flags get the single bind
+        plugin directly; None when the shortcut does not hold (ask per pod)."""
+        if len(self.bind_plugins) != 1:
+            return None
+        m = 0
+        for p in self.pre_bind:
+            pf = getattr(p, "pod_flags", None)
+            if pf is None or getattr(p, "cluster_active", None) is not None and p.cluster_active():
+                return None
+            m |= pf
+        return m
+
     def native_for(self, pod) -> bool:
         if not self.fully_native_static:
             return False

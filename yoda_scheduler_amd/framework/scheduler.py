@@ -144,6 +144,7 @@ class Scheduler:
         self._engine_exec = None          # worker thread of schedule_batch_overlapped
         self._batch_worker = None         # native engine worker (core.BatchWorker)
         self.engine_batch_errors = 0
+        self._run_direct: Optional[tuple] = None   # (framework, direct_bind_mask) during _finish_run
         self._batch_futs: dict = {}
         self.engine_spans: Optional[list] = None   # (t_start, t_end, pods) of native batches
         self._inflight: collections.deque = collections.deque()   # (fw, run, cycle, t0, future) on that worker
@@ -696,15 +697,21 @@ class Scheduler:
         """Split popped pods into single Python cycles (``(None, pod)``) and runs of
         consecutive pods of an all-native profile (``(fw, [pods])``)."""
         i = 0
+        masks: dict = {}           # framework → native_mask(), once per batch
         while i < len(pods):
             fw = self.frameworks.get(pods[i].scheduler_name)
-            if fw is None or not fw.native_for(pods[i]):
+            if fw is not None and fw not in masks:
+                masks[fw] = fw.native_mask()
+            m = masks.get(fw)
+            # the mask settles the common case; flagged pods still get the per-plugin check
+            if fw is None or not ((m is not None and not (pods[i].flags & m)) or fw.native_for(pods[i])):
                 yield None, pods[i]
                 i += 1
                 continue
             j = i
             run = []
-            while j < len(pods) and pods[j].scheduler_name == fw.name and fw.native_for(pods[j]):
+            while j < len(pods) and pods[j].scheduler_name == fw.name and \
+                    ((m is not None and not (pods[j].flags & m)) or fw.native_for(pods[j])):
                 if not self._pod_gone(pods[j]):
                     run.append(pods[j])
                 j += 1
@@ -725,8 +732,15 @@ class Scheduler:
             tr = self.tracer
             tr.span("native_batch", tr.now_us() - (time.perf_counter() - t0) * 1e6, pods=len(run),
                     device_cycles=self.engine.device_cycles)
-        for p, res in zip(run, results):
-            self._finish_cycle(fw, None, p, res, cycle, t0)   # all-native: no Python state
+        # the direct-bind decision's plugin checks, once for the run (see _native_direct)
+        binder = fw.bind_plugins[0] if len(fw.bind_plugins) == 1 else None
+        if not self.extenders and binder is not None and getattr(binder, "native_bind", False):
+            self._run_direct = (fw, fw.direct_bind_mask())
+        try:
+            for p, res in zip(run, results):
+                self._finish_cycle(fw, None, p, res, cycle, t0)   # all-native: no Python state
+        finally:
+            self._run_direct = None
 
     def schedule_batch(self, pods: list[PodInfo]) -> None:
         """Schedule a run of popped pods; consecutive pods of an all-native profile go
@@ -860,6 +874,9 @@ class Scheduler:
         only bind plugin, no PreBind plugin applies to the pod, no extenders."""
         if self.extenders:
             return False
+        rd = self._run_direct
+        if rd is not None and rd[0] is fw and rd[1] is not None and not (pi.flags & rd[1]):
+            return True                          # the run's mask: no PreBind plugin applies
         b = fw.direct_binder_for(pi)
         return b is not None and getattr(b, "native_bind", False)
 
