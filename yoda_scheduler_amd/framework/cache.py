@@ -54,6 +54,7 @@ class SchedulerCache:
         self.avoid_nodes: set[str] = set()       # nodes with a preferAvoidPods annotation
         self.node_ext_used: dict[str, dict[str, int]] = {}   # node → extended resource → requested
         self.generation = 0
+        self.node_generation = 0                 # node add/remove only (engine index → name stays valid)
 
     # ------------------------------------------------------------------ nodes
     def _index_node(self, info: NodeInfo, sign: int) -> None:
@@ -76,6 +77,8 @@ class SchedulerCache:
         self._index_node(info, +1)
         self.nodes[info.name] = info
         idx = push_node(self.engine, info)
+        if old is None:
+            self.node_generation += 1
         self.node_pods.setdefault(info.name, set())
         scv = self.scvs.get(info.name)
         if scv is not None:
@@ -92,6 +95,7 @@ class SchedulerCache:
         idx = self.engine.node_index(name)
         if idx >= 0:
             self.engine.remove_node(idx)
+        self.node_generation += 1
         for uid in list(self.node_pods.pop(name, ())):
             self.pods.pop(uid, None)
         self.generation += 1

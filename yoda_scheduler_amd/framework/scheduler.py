@@ -145,6 +145,9 @@ class Scheduler:
         self._batch_worker = None         # native engine worker (core.BatchWorker)
         self.engine_batch_errors = 0
         self._run_direct: Optional[tuple] = None   # (framework, direct_bind_mask) during _finish_run
+        self._names: dict = {}                     # engine node index → name (_node_name)
+        self._names_gen = -1
+        self._f_yoda = core().F_YODA
         self._batch_futs: dict = {}
         self.engine_spans: Optional[list] = None   # (t_start, t_end, pods) of native batches
         self._inflight: collections.deque = collections.deque()   # (fw, run, cycle, t0, future) on that worker
@@ -553,10 +556,10 @@ class Scheduler:
             msg = self._fit_error(res)
             self._fail(fw, state, pi, cycle, msg, t0)
             return
-        node = self.engine.node_name(node_idx)
+        node = self._node_name(node_idx)
         cards = res[3]
         self.cache.assumed(pi, node, cards)
-        pi.assigned_cards = cards if (fw.filter_mask & core().F_YODA) else None
+        pi.assigned_cards = cards if (fw.filter_mask & self._f_yoda) else None
         if fw.reserve and state is not None and (fw.reserve_static or not fw.native_for(pi)):
             st = fw.run_reserve(state, pi, node)
             if not st.is_success():
@@ -582,6 +585,16 @@ class Scheduler:
             asyncio.get_event_loop().create_task(self._permit_then_bind((fw, state, pi, node, cycle, t0)))
         else:
             self._enqueue_bind((fw, state, pi, node, cycle, t0))
+
+    def _node_name(self, idx: int) -> str:
+        """Engine node index → name, memoised until a node is added or removed."""
+        if self._names_gen != self.cache.node_generation:
+            self._names.clear()
+            self._names_gen = self.cache.node_generation
+        name = self._names.get(idx)
+        if name is None:
+            name = self._names[idx] = self.engine.node_name(idx)
+        return name
 
     async def _permit_then_bind(self, item: tuple) -> None:
         fw, state, pi, node, cycle, t0 = item
