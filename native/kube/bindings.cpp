@@ -183,6 +183,21 @@ PYBIND11_MODULE(_yoda_kube, m) {
            py::arg("limited") = true, py::arg("timeout") = 0.0)
       .def("bind", &Transport::bind, py::arg("namespace"), py::arg("name"), py::arg("uid"), py::arg("node"),
            py::arg("annotations"), py::arg("timeout") = 0.0)
+      // [(namespace, name, uid, node, annotations), ...] -> id of the first (ids consecutive)
+      .def("bind_many", [](Transport& t, const py::list& items, double timeout) {
+             std::vector<Transport::BindSpec> binds(items.size());
+             for (size_t k = 0; k < binds.size(); ++k) {
+               py::tuple it = items[k].cast<py::tuple>();
+               if (it.size() != 5) throw py::value_error("bind_many: (namespace, name, uid, node, annotations)");
+               Transport::BindSpec& b = binds[k];
+               b.ns = it[0].cast<std::string>();
+               b.name = it[1].cast<std::string>();
+               b.uid = it[2].cast<std::string>();
+               b.node = it[3].cast<std::string>();
+               b.annotations = it[4].cast<std::vector<KV>>();
+             }
+             return t.bind_many(binds, timeout);
+           }, py::arg("binds"), py::arg("timeout") = 0.0)
       .def("watch", &Transport::watch, py::arg("path"), py::arg("pods") = false)
       .def("cancel", &Transport::cancel)
       .def("set_token", &Transport::set_token)

@@ -211,8 +211,8 @@ uint64_t Transport::request(const std::string& method, const std::string& path, 
   return id;
 }
 
-uint64_t Transport::bind(const std::string& ns, const std::string& name, const std::string& uid,
-                         const std::string& node, const std::vector<KV>& annotations, double timeout_s) {
+std::string Transport::bind_body(const std::string& ns, const std::string& name, const std::string& uid,
+                                 const std::string& node, const std::vector<KV>& annotations) {
   std::string b;
   b.reserve(256);
   b.append("{\"apiVersion\":\"v1\",\"kind\":\"Binding\",\"metadata\":{\"name\":");
@@ -231,8 +231,42 @@ uint64_t Transport::bind(const std::string& ns, const std::string& name, const s
   b.append("}},\"target\":{\"apiVersion\":\"v1\",\"kind\":\"Node\",\"name\":");
   dump_string(node, b);
   b.append("}}");
+  return b;
+}
+
+uint64_t Transport::bind(const std::string& ns, const std::string& name, const std::string& uid,
+                         const std::string& node, const std::vector<KV>& annotations, double timeout_s) {
+  std::string b = bind_body(ns, name, uid, node, annotations);
   std::string path = "/api/v1/namespaces/" + url_encode(ns) + "/pods/" + url_encode(name) + "/binding";
   return request("POST", path, b, "application/json", true, timeout_s);
+}
+
+uint64_t Transport::bind_many(const std::vector<BindSpec>& binds, double timeout_s) {
+  if (binds.empty()) return 0;
+  const uint64_t first = next_id_.fetch_add(binds.size());
+  const double deadline = timeout_s > 0 ? now_s() + timeout_s : 0.0;
+  std::vector<std::unique_ptr<Req>> rs;
+  rs.reserve(binds.size());
+  for (size_t k = 0; k < binds.size(); ++k) {
+    const BindSpec& s = binds[k];
+    std::string b = bind_body(s.ns, s.name, s.uid, s.node, s.annotations);
+    auto r = std::make_unique<Req>();
+    r->id = first + k;
+    r->wire = head("POST", "/api/v1/namespaces/" + url_encode(s.ns) + "/pods/" + url_encode(s.name) + "/binding",
+                   b.size(), "application/json");
+    r->wire.append(b);
+    r->limited = true;
+    r->deadline = deadline;
+    rs.push_back(std::move(r));
+  }
+  bool was_empty;
+  {
+    std::lock_guard<std::mutex> g(in_mu_);
+    was_empty = incoming_.empty() && cancels_.empty();
+    for (auto& r : rs) incoming_.push_back(std::move(r));
+  }
+  if (was_empty) efd_signal(wake_efd_);
+  return first;
 }
 
 uint64_t Transport::watch(const std::string& path, bool pods) {

@@ -87,6 +87,13 @@ class Transport {
   // POST pods/{name}/binding with the body formatted here (rate-limited).
   uint64_t bind(const std::string& ns, const std::string& name, const std::string& uid, const std::string& node,
                 const std::vector<KV>& annotations, double timeout_s);
+  struct BindSpec {
+    std::string ns, name, uid, node;
+    std::vector<KV> annotations;
+  };
+  // A run of Bindings in one hand-off to the I/O thread (one lock, one wake-up); their
+  // ids are consecutive: the first is returned.
+  uint64_t bind_many(const std::vector<BindSpec>& binds, double timeout_s);
   // Streaming GET (watch=1 in `path`); `pods` selects the pod projection.
   uint64_t watch(const std::string& path, bool pods);
   void cancel(uint64_t id);
@@ -103,6 +110,8 @@ class Transport {
  private:
   void run();
   void submit(std::unique_ptr<Req> r);
+  std::string bind_body(const std::string& ns, const std::string& name, const std::string& uid,
+                        const std::string& node, const std::vector<KV>& annotations);
   std::string head(const std::string& method, const std::string& path, size_t body_len,
                    const std::string& content_type);
   std::unique_ptr<Conn> open_conn(bool watch);

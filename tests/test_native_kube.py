@@ -257,6 +257,35 @@ def test_native_apiserver_crud_watch_bind_and_selectors(native_api):
     run(go())
 
 
+def test_transport_bind_many_routes_each_answer_to_its_callback(native_api):
+    """A run of Bindings handed over in one call: each pod gets its own answer (201 for the
+    good ones, 409 for a wrong uid) through its own callback, with its annotations applied."""
+    async def go():
+        cl = KubeClient(KubeConfig(native_api.url), native=True)
+        try:
+            await cl.create("nodes", make_node("n1"))
+            uids = []
+            for k in range(5):
+                p = await cl.create("pods", {"metadata": {"name": f"p{k}"}, "spec": {"schedulerName": "x"}})
+                uids.append(p["metadata"]["uid"])
+            uids[3] = "wrong-uid"
+            loop = asyncio.get_event_loop()
+            futs = [loop.create_future() for _ in uids]
+            binds = [("default", f"p{k}", u, "n1", [("scv.amd.com/gpus", str(k))]) for k, u in enumerate(uids)]
+            cbs = [(lambda f: (lambda st, body: f.set_result((st, body))))(f) for f in futs]
+            cl.native.bind_many(binds, cbs, 5.0)
+            got = await asyncio.wait_for(asyncio.gather(*futs), 5)
+            assert [st for st, _ in got] == [201, 201, 201, 409, 201]
+            for k in (0, 4):
+                pod = await cl.get("pods", f"p{k}", "default")
+                assert pod["spec"]["nodeName"] == "n1"
+                assert pod["metadata"]["annotations"] == {"scv.amd.com/gpus": str(k)}
+            cl.native.bind_many([], [], 5.0)          # nothing to hand over: no-op
+        finally:
+            await cl.close()
+    run(go())
+
+
 def test_native_apiserver_paging_history_410_and_bookmarks(native_api):
     async def go():
         cl = KubeClient(KubeConfig(native_api.url), native=True)

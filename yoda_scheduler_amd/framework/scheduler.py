@@ -145,6 +145,8 @@ class Scheduler:
         self._batch_worker = None         # native engine worker (core.BatchWorker)
         self.engine_batch_errors = 0
         self._run_direct: Optional[tuple] = None   # (framework, direct_bind_mask) during _finish_run
+        self._bind_buf: Optional[list] = None      # native Bindings of the run being finished
+        self._bind_cbs: list = []
         self._names: dict = {}                     # engine node index → name (_node_name)
         self._names_gen = -1
         self._f_yoda = core().F_YODA
@@ -749,11 +751,18 @@ class Scheduler:
         binder = fw.bind_plugins[0] if len(fw.bind_plugins) == 1 else None
         if not self.extenders and binder is not None and getattr(binder, "native_bind", False):
             self._run_direct = (fw, fw.direct_bind_mask())
+        # the run's native Bindings go to the transport in one hand-off at the end
+        buf = self._bind_buf = [] if self.native is not None else None
         try:
             for p, res in zip(run, results):
                 self._finish_cycle(fw, None, p, res, cycle, t0)   # all-native: no Python state
         finally:
             self._run_direct = None
+            if buf is not None:
+                self._bind_buf = None
+                cbs, self._bind_cbs = self._bind_cbs, []
+                if buf:
+                    self.native.bind_many(buf, cbs, self.bind_timeout)
 
     def schedule_batch(self, pods: list[PodInfo]) -> None:
         """Schedule a run of popped pods; consecutive pods of an all-native profile go
@@ -897,8 +906,13 @@ class Scheduler:
         fw = item[0]
         if self.native is not None and self._native_direct(fw, item[2]):
             pi, node = item[2], item[3]
-            self.native.bind(pi.namespace, pi.name, pi.uid, node, self._bind_annotations(pi, node),
-                             functools.partial(self._native_bind_done, item, time.perf_counter()),
+            cb = functools.partial(self._native_bind_done, item, time.perf_counter())
+            buf = self._bind_buf
+            if buf is not None:                  # inside _finish_run: submitted with the run
+                buf.append((pi.namespace, pi.name, pi.uid, node, self._bind_annotations(pi, node)))
+                self._bind_cbs.append(cb)
+                return
+            self.native.bind(pi.namespace, pi.name, pi.uid, node, self._bind_annotations(pi, node), cb,
                              self.bind_timeout)
             return
         self._bind_dq.append(item)

@@ -168,6 +168,18 @@ class NativeTransport:
         self._cbs[rid] = cb
         return rid
 
+    def bind_many(self, binds: list, cbs: list, timeout: float = 0.0) -> None:
+        """A run of Binding POSTs — ``binds[k] = (namespace, name, uid, node, annotations)``,
+        answered through ``cbs[k](status, body)`` — handed to the I/O thread in one call (one
+        lock and one wake-up for the run instead of one per pod)."""
+        if not binds:
+            return
+        self._attach()
+        first = self.t.bind_many(binds, timeout)
+        cb_map = self._cbs
+        for k, cb in enumerate(cbs):
+            cb_map[first + k] = cb
+
     def watch(self, path: str, pods: bool, on_events: Callable, on_end: Callable) -> int:
         self._attach()
         wid = self.t.watch(path, pods)
