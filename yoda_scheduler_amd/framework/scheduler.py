@@ -24,6 +24,7 @@ from typing import Callable, Optional
 from ..kube.informer import Informer, NativePodInformer
 from ..models.pod import PodInfo, forget_num_id
 from ..models.scv import LazyScv
+from ..plugins.defaults import bind_annotations
 from ..ops.native import core, pod_req
 from ..utils import gctune, klog
 from ..utils.metrics import SchedulerMetrics
@@ -927,8 +928,7 @@ class Scheduler:
         """The Binding's GPU annotations (plugins.defaults.bind_annotations), memoised per
         (node, GPU set, HBM request) until the cache's node/Scv generation moves: a burst
         repeats a handful of placements per node."""
-        from ..plugins.defaults import bind_annotations
-        cards = getattr(pi, "assigned_cards", None)
+        cards = pi.assigned_cards
         if cards is None:
             return []
         scv = self.cache.scvs.get(node)
