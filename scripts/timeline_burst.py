@@ -57,17 +57,26 @@ async def run(a) -> list:
         rtts: list = []
         nat = sched.native
         orig_bind = nat.bind if nat is not None else None
+        orig_many = nat.bind_many if nat is not None else None
 
-        def bind(ns, name, uid, node, ann, cb, timeout=0.0):
-            submits[uid] = time.perf_counter()
+        def traced(uid, cb, now):
+            submits[uid] = now
 
             def done(status, body, uid=uid, cb=cb):
                 t = time.perf_counter()
                 rtts.append((submits.get(uid, t), t))
                 return cb(status, body)
-            return orig_bind(ns, name, uid, node, ann, done, timeout)
+            return done
+
+        def bind(ns, name, uid, node, ann, cb, timeout=0.0):
+            return orig_bind(ns, name, uid, node, ann, traced(uid, cb, time.perf_counter()), timeout)
+
+        def bind_many(binds, cbs, timeout=0.0):
+            now = time.perf_counter()
+            return orig_many(binds, [traced(b[2], cb, now) for b, cb in zip(binds, cbs)], timeout)
         if nat is not None:
             nat.bind = bind
+            nat.bind_many = bind_many
         tr = sched.tracer
         dev_trace = a.device_trace and sched.engine.device_enabled
         if dev_trace:
@@ -149,6 +158,7 @@ async def run(a) -> list:
         out["burst"] = rep
         if nat is not None:
             nat.bind = orig_bind
+            nat.bind_many = orig_many
             rr = sorted((e - s0) * 1000 for s0, e in rtts)
             subs = sorted((s0 - ta) * 1000 for s0, _ in rtts)
             out["bind_submit_ms"] = {"first": pct(subs, 0), "p50": pct(subs, .5), "last": pct(subs, 1)}
