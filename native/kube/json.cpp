@@ -325,10 +325,29 @@ Value parse_prefix(std::string_view text, size_t* pos) {
   return v;
 }
 
+namespace {
+// any byte of w that is '"', '\\' or a control character (< 0x20): SWAR zero-byte tests
+inline bool word_needs_escape(uint64_t w) {
+  constexpr uint64_t ones = 0x0101010101010101ull, highs = 0x8080808080808080ull;
+  const uint64_t q = w ^ (ones * '"'), b = w ^ (ones * '\\');
+  const uint64_t zq = (q - ones) & ~q & highs, zb = (b - ones) & ~b & highs;
+  const uint64_t lt = (w - ones * 0x20) & ~w & highs;   // bytes < 0x20 (ASCII-exact with the & ~w)
+  return (zq | zb | lt) != 0;
+}
+}  // namespace
+
 void dump_string(std::string_view s, std::string& out) {
   out.push_back('"');
+  // clean 8-byte words (the common case: names, labels, timestamps) are copied in one append
+  size_t i0 = 0;
+  while (i0 + 8 <= s.size()) {
+    uint64_t w;
+    std::memcpy(&w, s.data() + i0, 8);
+    if (word_needs_escape(w)) break;
+    i0 += 8;
+  }
   size_t run = 0;
-  for (size_t i = 0; i < s.size(); ++i) {
+  for (size_t i = i0; i < s.size(); ++i) {
     unsigned char c = static_cast<unsigned char>(s[i]);
     const char* rep = nullptr;
     char buf[7];
