@@ -8,7 +8,7 @@ out=gpurun_out/node_gpus_sweep.jsonl
 : > $out
 for cfg in 2 3 4 5; do
   for g in 1 2 4 8; do
-    args="--config $cfg --node-gpus $g --steps 3 --warmup 1"
+    args="--config $cfg --node-gpus $g --steps 3 --warmup 1 --alt none"
     echo "=== bench $args ($(date +%T))"
     timeout -k 10 240 python bench.py $args > gpurun_out/bench_one.log 2>&1
     rc=$?
