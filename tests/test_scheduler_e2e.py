@@ -597,6 +597,7 @@ def test_burst_cost_scales_linearly():
             return dt / n_pods
         return asyncio.run(go())
 
+    # best of two on both sides: a neighbour process (pytest -n) inflates single samples
     small = min(per_pod(1000) for _ in range(2))
-    big = per_pod(5000)
+    big = min(per_pod(5000) for _ in range(2))
     assert big < 2.0 * small, (big * 1e6, small * 1e6)
