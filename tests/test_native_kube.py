@@ -572,3 +572,55 @@ def test_bounded_drain_keeps_order_and_yields_between_chunks():
     kinds = [k for k, _ in seen]
     assert kinds.index("bind") > 2 and kinds[-1] == "end"         # completion after the big batch
     assert other[0] >= 1 and other[-1] <= len(chunks)             # the other task ran between chunks
+
+
+def test_failed_bind_handoff_requeues_the_run():
+    """If handing a run's Bindings to the transport raises, every pod of the run takes the
+    bind-failure path (forgotten, retried from backoff) instead of staying assumed; once the
+    transport accepts again they bind."""
+    from yoda_scheduler_amd.framework.config import parse_config
+    from yoda_scheduler_amd.framework.scheduler import Scheduler
+    from yoda_scheduler_amd.testing import yoda_config
+
+    async def go():
+        api = NativeApi()
+        cl = KubeClient(KubeConfig(api.url), native=True)
+        try:
+            await cl.create("nodes", make_node("n1"))
+            s = make_scv("n1", update_time=time.time())
+            s.update_interval_ms = 600_000
+            await cl.create("scvs", s.to_json())
+            cfg = parse_config(yoda_config())
+            cfg.pod_initial_backoff_seconds = 0.01
+            sched = Scheduler(cl, cfg)
+            await sched.start()
+            orig, calls = cl.native.bind_many, []
+
+            def flaky(binds, cbs, timeout=0.0):
+                calls.append(len(binds))
+                if len(calls) == 1:
+                    raise RuntimeError("transport refused the run")
+                return orig(binds, cbs, timeout)
+            cl.native.bind_many = flaky
+            for i in range(12):
+                await cl.create("pods", {"metadata": {"name": f"f{i}", "labels": {"scv/memory": "1000"}},
+                                         "spec": {"schedulerName": "yoda-scheduler",
+                                                  "tolerations": [{"key": "node.kubernetes.io/not-ready",
+                                                                   "operator": "Exists", "effect": "NoExecute"}]}})
+            t0 = time.time()
+            while len(sched.queue._active_entries) < 12 and time.time() - t0 < 5:
+                await asyncio.sleep(0.01)         # the burst is queued: the loop takes it as one run
+            loop_t = asyncio.get_event_loop().create_task(sched.scheduling_loop())
+            t0 = time.time()
+            while sched.scheduled < 12 and time.time() - t0 < 15:
+                sched.queue.flush_backoff_completed()
+                await asyncio.sleep(0.02)
+            out = sched.scheduled, sched.bind_errors, len(calls), sched.pending_binds
+            await sched.shutdown()
+            loop_t.cancel()
+            return out
+        finally:
+            await cl.close()
+            api.stop()
+    scheduled, errors, calls, pending = run(go())
+    assert scheduled == 12 and errors >= 1 and calls >= 2 and pending == 0, (scheduled, errors, calls, pending)

@@ -763,7 +763,13 @@ class Scheduler:
                 self._bind_buf = None
                 cbs, self._bind_cbs = self._bind_cbs, []
                 if buf:
-                    self.native.bind_many(buf, cbs, self.bind_timeout)
+                    try:
+                        self.native.bind_many(buf, cbs, self.bind_timeout)
+                    except Exception as e:  # noqa: BLE001 - the run's pods must not stay assumed
+                        log.error("handing %d Bindings to the transport failed: %r", len(buf), e)
+                        msg = repr(e).encode()
+                        for cb in cbs:              # each goes through the bind-failure path
+                            cb(-1, msg)
 
     def schedule_batch(self, pods: list[PodInfo]) -> None:
         """Schedule a run of popped pods; consecutive pods of an all-native profile go
