@@ -1166,6 +1166,13 @@ bool Engine::schedule_batch_device(const std::vector<uint64_t>& pods, const std:
   return true;
 }
 
+bool Engine::device_flush() {
+  if (!dev_ctx_) return true;
+  std::unique_lock<std::mutex> dl(dev_mu_, std::try_to_lock);
+  if (!dl.owns_lock()) return false;
+  return flush_dirty();
+}
+
 bool Engine::device_cycle(const PodReq& req, CycleResult* out) {
   if (!device_eligible(req)) return false;
   std::unique_lock<std::mutex> dl(dev_mu_, std::try_to_lock);

@@ -279,6 +279,9 @@ class Engine {
   bool device_eligible(const PodReq& req) const;
   // parity hook: run one device cycle without reserving; false if not eligible/failed
   bool device_cycle(const PodReq& req, CycleResult* out);
+  // push the rows changed since the last device call to the device now (an idle scheduler
+  // does, so the next batch does not carry them); false if the device is busy or refused
+  bool device_flush();
 
  private:
   void mark_dirty(int32_t idx);
