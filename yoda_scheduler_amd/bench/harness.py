@@ -144,7 +144,8 @@ class _Recorder:
 def native_apiserver_binary() -> str:
     import os
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    return os.path.join(root, "_native", "yoda-fake-apiserver-native")
+    # YODA_FAKEAPI_BIN: another build of the native fake apiserver (same-box A/B)
+    return os.environ.get("YODA_FAKEAPI_BIN") or os.path.join(root, "_native", "yoda-fake-apiserver-native")
 
 
 class HttpShard:
