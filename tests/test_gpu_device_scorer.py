@@ -275,3 +275,27 @@ def test_batch_kernel_abort_falls_back_and_recovers(require_gpu):
         pi, req = ds.random_request(eng, rng, f"abort-after-{k}")
         assert not ds.compare_cycle(eng, req), k
         eng.schedule(pi.num_id, req, True)
+
+
+def test_device_flush_uploads_dirty_rows(require_gpu):
+    """Engine.device_flush (the scheduler's idle-time upload) pushes the rows changed since the
+    last device call: afterwards nothing waits for the next cycle, and device cycles still
+    match the CPU engine."""
+    from yoda_scheduler_amd.ops import device_scorer as ds
+    eng = _engine(2048, 17)
+    rng = random.Random(17)
+    placed = []
+    for k in range(40):
+        pi, req = ds.random_request(eng, rng, f"fl-{k}")
+        res = eng.schedule(pi.num_id, req, True)
+        if res[0] >= 0:
+            placed.append(pi.num_id)
+    for nid in placed[::2]:
+        eng.release(nid)                       # dirty rows, as a burst's deletions leave them
+    assert eng.device_flush()
+    assert eng.device_flush()                  # nothing left: a no-op
+    for k in range(10):
+        pi, req = ds.random_request(eng, rng, f"fl-after-{k}")
+        assert not ds.compare_cycle(eng, req), k
+        eng.schedule(pi.num_id, req, True)
+    assert eng.device_fallbacks == 0
