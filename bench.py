@@ -16,6 +16,15 @@ schedules its own burst each step, i.e. N independent scheduling domains. ``valu
 the whole-job aggregate (pods bound on all ranks ÷ the slowest rank's time), latency
 percentiles are over every pod of every rank.
 
+What an N-GPU value means: N scheduler replicas, one per GPU, each serving its own
+scheduling domain (one 8×MI355X node pool, its own apiserver and burst) — the shape of a
+sharded control plane, not N GPUs cooperating on one queue. Rank r owns GPU r
+(``LOCAL_RANK``): its gfx950 device scorer is pinned there
+(``yodaRuntime.deviceScorer.device``), its telemetry template is sampled from that card,
+and its RCCL buffers live there. Shards share nothing but the host, so the aggregate
+measures how the per-shard work scales with the host's cores; the config-3 headline shard
+runs its cycles on the CPU engine (one node is far below ``deviceScorer.minNodes``).
+
 Each rank samples its GPU with the C++ amd-smi collector (when the driver is present)
 and uses the real HBM size / max sclk / CU count / power cap / HBM bandwidth as the
 card template of its synthetic node — pods and node layout are synthetic, the per-GPU
@@ -37,22 +46,39 @@ METRIC = "pods scheduled/sec + p99 scheduling latency, 1000-pod burst on 8×MI35
 def _telemetry_template(local_rank: int) -> tuple[dict | None, dict]:
     info: dict = {"source": "synthetic MI355X spec"}
     try:
-        from yoda_scheduler_amd.sniffer.collector import AmdSmiBackend
-        be = AmdSmiBackend()
+        fake = int(os.environ.get("YODA_BENCH_FAKE_SMI", "0") or 0)
+        if fake > 0:
+            # CPU rehearsal of a multi-GPU node: a fake amd-smi node of `fake` distinct cards
+            # whose HIP order is reversed (so picking by position would be caught)
+            from yoda_scheduler_amd.sniffer.collector import FakeBackend
+            be = FakeBackend(gpus=fake, hip_order=list(range(fake))[::-1], node="bench-host")
+        else:
+            from yoda_scheduler_amd.sniffer.collector import AmdSmiBackend
+            be = AmdSmiBackend()
         samples = be.sample()
         be.close()
         if not samples:
             return None, info
-        s = samples[min(local_rank, len(samples) - 1)]
+        # the card this rank's HIP ordinal names (amd-smi enumerates in BDF order, which
+        # need not be HIP's order); by position when the sample carries no HIP id
+        s = next((x for x in samples if int(x.get("hipId", -1)) == local_rank),
+                 samples[min(local_rank, len(samples) - 1)])
         tmpl = {"total_memory": int(s["vramTotalMB"]), "clock": int(s["sclkMaxMHz"]),
                 "core": int(s["computeUnits"]), "power": int(s["powerLimitW"]),
                 "bandwidth": int(s["hbmBandwidthGBps"]), "model": s.get("model", "")}
         tmpl = {k: v for k, v in tmpl.items() if v}
-        info = {"source": "amd-smi (C++ collector)", "gpu_index": s["index"], "bdf": s["bdf"], **tmpl}
+        info = {"source": "amd-smi (C++ collector)" if be.name == "amd-smi" else f"{be.name} amd-smi backend",
+                "gpu_index": s["index"], "hip_id": int(s.get("hipId", -1)), "bdf": s["bdf"], **tmpl}
         return tmpl, info
     except Exception as e:  # noqa: BLE001 - CPU box / no driver
         info["amd_smi_error"] = str(e)[:200]
         return None, info
+
+
+def rank_gpu_index(local_rank: int, n_visible: int) -> int:
+    """GPU of a rank: LOCAL_RANK modulo the visible devices (one rank per GPU under
+    torch.distributed.run; several ranks share a GPU only in CPU/gloo rehearsals)."""
+    return local_rank % n_visible if n_visible > 0 else local_rank
 
 
 def main(argv=None) -> int:
@@ -95,8 +121,10 @@ def main(argv=None) -> int:
     import torch
     import torch.distributed as dist
     cuda = torch.cuda.is_available()
+    # the HIP ordinal this rank owns: its device scorer, its telemetry and its RCCL buffers
+    gpu_index = rank_gpu_index(local_rank, torch.cuda.device_count() if cuda else 0)
     if cuda:
-        torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
+        torch.cuda.set_device(gpu_index)
     backend = None
     if world > 1:
         # RCCL ("nccl") with one rank per GPU; YODA_BENCH_BACKEND=gloo rehearses several ranks
@@ -115,7 +143,7 @@ def main(argv=None) -> int:
         if cuda:
             torch.cuda.synchronize()
 
-    tmpl, tel = _telemetry_template(local_rank)
+    tmpl, tel = _telemetry_template(gpu_index)
 
     from yoda_scheduler_amd.bench.harness import HttpShard, Shard, percentile
     from yoda_scheduler_amd.bench.workloads import make_workload
@@ -131,13 +159,13 @@ def main(argv=None) -> int:
             one = HttpShard(w, qps=a.qps, burst=a.burst, batch=a.batch, template=tmpl, events=not a.no_events,
                             compat=a.compat, seed=rank * 1000, device=a.device, overlap=a.overlap,
                             apiserver=a.apiserver, client_native=a.client == "native",
-                            engine_threads=a.engine_threads)
+                            engine_threads=a.engine_threads, device_index=gpu_index)
             shards = [one] * (a.warmup + a.steps)
             loop.run_until_complete(one.start())
         else:
             shards = [Shard(w, qps=a.qps, burst=a.burst, batch=a.batch, template=tmpl, events=not a.no_events,
                             compat=a.compat, seed=rank * 1000 + i, device=a.device, overlap=a.overlap,
-                            engine_threads=a.engine_threads)
+                            engine_threads=a.engine_threads, device_index=gpu_index)
                       for i in range(a.warmup + a.steps)]
             for s in shards:
                 loop.run_until_complete(s.start())
@@ -185,6 +213,13 @@ def main(argv=None) -> int:
             gathered_e2e: list = [None] * world
             dist.all_gather_object(gathered_e2e, e2e)
             e2e = [x for g in gathered_e2e for x in g]
+        mine = {"rank": rank, "local_rank": local_rank, "gpu_index": gpu_index,
+                "device_scorer_device": shards[0].sched.config.device_index, "pods_bound": sum(r.bound for r in results),
+                "telemetry_bdf": tel.get("bdf"), "telemetry_hip_id": tel.get("hip_id")}
+        per_rank = [mine]
+        if world > 1:
+            per_rank = [None] * world
+            dist.all_gather_object(per_rank, mine)
         for s in uniq:
             loop.run_until_complete(s.stop())
         value = bound / elapsed if elapsed > 0 else 0.0
@@ -205,6 +240,7 @@ def main(argv=None) -> int:
             "pods_bound": bound,
             "pods_unschedulable": unsched,
             "device_cycles": device_cycles,
+            "ranks": per_rank,
             "transport": transport,
             **({"apiserver": a.apiserver, "client": a.client} if transport == "http" else {}),
         }

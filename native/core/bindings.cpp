@@ -11,6 +11,8 @@
 #include <chrono>
 
 #include <pybind11/pybind11.h>
+
+#include "build_id.h"
 #include <pybind11/stl.h>
 
 #include "engine.hpp"
@@ -217,6 +219,7 @@ class BatchWorker {
 }  // namespace
 
 PYBIND11_MODULE(_yoda_core, m) {
+  m.def("build_id", [] { return std::string(YODA_BUILD_ID); }, "hash of the sources this module was built from");
   m.doc() = "Native placement / scheduling-cycle engine (C++17)";
   m.def("engine_lock_stats", [] {
     return py::make_tuple(g_lock_contended.load(), g_lock_wait_ns.load() / 1000);

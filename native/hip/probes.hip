@@ -11,6 +11,8 @@
 // pattern check reduces mismatches per wave and issues ONE atomic per wave (G12).
 #include <hip/hip_runtime.h>
 
+#include "build_id.h"
+
 #include <cstdint>
 #include <cstdio>
 
@@ -97,6 +99,9 @@ int grid_for(int device, int per_cu = 8) {
 }  // namespace
 
 extern "C" {
+
+// hash of the sources this library was built from (ops/build.py)
+const char* yoda_build_id() { return YODA_BUILD_ID; }
 
 int yoda_hip_device_count(int* n) {
   YODA_CHECK(hipGetDeviceCount(n));

@@ -1,5 +1,7 @@
 // pybind11 bindings of the native Kubernetes transport (module yoda_scheduler_amd._native._yoda_kube).
 #include <pybind11/pybind11.h>
+
+#include "build_id.h"
 #include <pybind11/stl.h>
 
 #include "json.hpp"
@@ -74,6 +76,7 @@ std::shared_ptr<PodEv> project_bytes(const std::string& raw) {
 }  // namespace
 
 PYBIND11_MODULE(_yoda_kube, m) {
+  m.def("build_id", [] { return std::string(YODA_BUILD_ID); }, "hash of the sources this module was built from");
   m.doc() = "Native Kubernetes API transport: pipelined HTTP/1.1 (+TLS), watch decoding, pod projection";
 
   py::class_<PodEv, std::shared_ptr<PodEv>>(m, "PodEvent")
@@ -198,7 +201,7 @@ PYBIND11_MODULE(_yoda_kube, m) {
              }
              return t.bind_many(binds, timeout);
            }, py::arg("binds"), py::arg("timeout") = 0.0)
-      .def("watch", &Transport::watch, py::arg("path"), py::arg("pods") = false)
+      .def("watch", &Transport::watch, py::arg("path"), py::arg("pods") = false, py::arg("idle_timeout") = 0.0)
       .def("cancel", &Transport::cancel)
       .def("set_token", &Transport::set_token)
       .def("set_rate", &Transport::set_rate, py::arg("qps"), py::arg("burst"))

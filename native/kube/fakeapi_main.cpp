@@ -4,6 +4,7 @@
 #include <cstring>
 #include <string>
 
+#include "build_id.h"
 #include "fakeapi.hpp"
 
 int main(int argc, char** argv) {
@@ -23,7 +24,10 @@ int main(int argc, char** argv) {
     else if (a == "--token") o.token = val("--token");
     else if (a == "--history") o.history = size_t(std::atoll(val("--history").c_str()));
     else if (a == "--bookmark-interval") o.bookmark_interval_s = std::atof(val("--bookmark-interval").c_str());
-    else if (a == "-h" || a == "--help") {
+    else if (a == "--build-id") {
+      printf("%s\n", YODA_BUILD_ID);
+      return 0;
+    } else if (a == "-h" || a == "--help") {
       printf("usage: yoda-fake-apiserver-native [--host H] [--port P] [--port-file F] [--token T] "
              "[--history N] [--bookmark-interval S]\n");
       return 0;

@@ -66,6 +66,7 @@ struct Transport::Req {
   bool pods = false;
   bool expired = false;     // completed by timeout; the late response is dropped
   double deadline = 0.0;
+  double idle_timeout = 0.0;  // watch: close when nothing arrived for this long (0 = never)
 };
 
 struct Transport::Conn {
@@ -85,6 +86,8 @@ struct Transport::Conn {
   std::vector<WatchEvent> evs;
   uint32_t interest = 0;
   bool registered = false;
+  double last_rx = 0.0;      // last time bytes arrived (watch idle timeout)
+  double idle_timeout = 0.0;
 };
 
 Transport::Transport(ClientConfig cfg) : cfg_(std::move(cfg)) {
@@ -269,12 +272,13 @@ uint64_t Transport::bind_many(const std::vector<BindSpec>& binds, double timeout
   return first;
 }
 
-uint64_t Transport::watch(const std::string& path, bool pods) {
+uint64_t Transport::watch(const std::string& path, bool pods, double idle_timeout_s) {
   auto r = std::make_unique<Req>();
   r->id = next_id_++;
   r->wire = head("GET", path, 0, "");
   r->watch = true;
   r->pods = pods;
+  r->idle_timeout = idle_timeout_s;
   uint64_t id = r->id;
   submit(std::move(r));
   return id;
@@ -340,6 +344,12 @@ std::unique_ptr<Transport::Conn> Transport::open_conn(bool watch) {
   int one = 1;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
   setsockopt(fd, SOL_SOCKET, SO_KEEPALIVE, &one, sizeof(one));
+  // a black-holed peer (LB / apiserver failover) is detected in ~60 s like Go's dialer
+  // (30 s keep-alive), not after the kernel's 2 h default
+  int idle = 30, intvl = 10, cnt = 3;
+  setsockopt(fd, IPPROTO_TCP, TCP_KEEPIDLE, &idle, sizeof(idle));
+  setsockopt(fd, IPPROTO_TCP, TCP_KEEPINTVL, &intvl, sizeof(intvl));
+  setsockopt(fd, IPPROTO_TCP, TCP_KEEPCNT, &cnt, sizeof(cnt));
   int rc = ::connect(fd, reinterpret_cast<const sockaddr*>(addr_.data()), socklen_t(addr_.size()));
   if (rc != 0 && errno != EINPROGRESS) {
     ::close(fd);
@@ -643,6 +653,7 @@ void Transport::do_read(Conn* c) {
       return;
     }
     got_total += size_t(n);
+    c->last_rx = now_s();
     size_t off = 0;
     while (off < size_t(n) && c->st == Conn::kOpen) {
       bool done = false;
@@ -785,9 +796,24 @@ void Transport::check_timeouts(double now) {
       }
     }
   }
-  for (auto& c : pool_)
+  for (auto& c : pool_) {
+    if (c->st == Conn::kDead || c->inflight.empty()) continue;
+    bool oldest_expired = false;
     for (auto& r : c->inflight)
-      if (!r->expired && r->deadline > 0 && now > r->deadline) expire(*r);
+      if (!r->expired && r->deadline > 0 && now > r->deadline) {
+        if (&r == &c->inflight.front()) oldest_expired = true;
+        expire(*r);
+      }
+    // the connection's oldest request got no answer in time: responses are ordered, so
+    // everything pipelined behind it is stuck too — close it, failing those requests now
+    // (their callers retry), and let dispatch() open a fresh connection for the slot
+    if (oldest_expired) close_conn(c.get(), -1, "connection closed: an earlier request on it timed out");
+  }
+  for (auto& kv : watches_) {
+    Conn* c = kv.second.get();
+    if (c->st != Conn::kDead && c->idle_timeout > 0 && now - c->last_rx > c->idle_timeout)
+      close_conn(c, -1, "watch idle timeout");     // the reflector re-watches / relists
+  }
   if (n) {
     std::lock_guard<std::mutex> g(stats_mu_);
     stats_.timeouts += n;
@@ -842,6 +868,8 @@ void Transport::run() {
           }
           c->watch_id = r->id;
           c->pods = r->pods;
+          c->idle_timeout = r->idle_timeout;
+          c->last_rx = now_s();
           c->wbuf = std::move(r->wire);
           watches_[r->id] = std::move(c);
           continue;

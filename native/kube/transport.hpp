@@ -94,8 +94,9 @@ class Transport {
   // A run of Bindings in one hand-off to the I/O thread (one lock, one wake-up); their
   // ids are consecutive: the first is returned.
   uint64_t bind_many(const std::vector<BindSpec>& binds, double timeout_s);
-  // Streaming GET (watch=1 in `path`); `pods` selects the pod projection.
-  uint64_t watch(const std::string& path, bool pods);
+  // Streaming GET (watch=1 in `path`); `pods` selects the pod projection. The stream is
+  // closed (kWatchEnd, status -1) when no byte arrived for idle_timeout_s (0 = never).
+  uint64_t watch(const std::string& path, bool pods, double idle_timeout_s = 0.0);
   void cancel(uint64_t id);
   std::vector<Completion> drain();
   void set_token(const std::string& token);

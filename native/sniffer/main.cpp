@@ -8,6 +8,7 @@
 #include <cstring>
 #include <thread>
 
+#include "build_id.h"
 #include "collector.hpp"
 
 int main(int argc, char** argv) {
@@ -19,6 +20,9 @@ int main(int argc, char** argv) {
       count = -1;
     } else if (!strcmp(argv[i], "--count") && i + 1 < argc) {
       count = atol(argv[++i]);
+    } else if (!strcmp(argv[i], "--build-id")) {
+      printf("%s\n", YODA_BUILD_ID);
+      return 0;
     } else if (!strcmp(argv[i], "-h") || !strcmp(argv[i], "--help")) {
       printf("usage: yoda-sniffer [--interval SECONDS] [--count N]\n");
       return 0;

@@ -30,6 +30,7 @@ for s in $STEPS; do
     benchhttppy) step bench_http_pyapi 600 python bench.py --transport http --apiserver python --client aiohttp --steps 10 --warmup 2 ;;
     profhttp) step prof_http 600 python scripts/profile_bench.py --out gpurun_out/prof_http.txt --transport http --steps 20 --warmup 5 ;;
     profinproc) step prof_inproc 600 python scripts/profile_bench.py --out gpurun_out/prof_inproc.txt --steps 20 --warmup 5 ;;
+    pmc) step pmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES --kernel-trace --stats --output-format csv -d gpurun_out/pmc -o dev -- python3 scripts/device_bench.py --nodes 4096 --pods 40 --kinds single,gang4 --paths gpu ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -c "import __graft_entry__ as g; g.smoke()" ;;
   esac
 done

@@ -62,3 +62,36 @@ def test_gang_validation_harness_picks_low_load_set_gloo():
     assert d["sampled_link_load"]["0-1"] == 0.9
     assert d["busbw_best"][0]["world"] == 2 and d["busbw_worst"][0]["busbw_gbps"] > 0
     assert d["busbw_ratio_best_over_worst"] > 0 and "no xGMI" in d["backend"]
+
+
+def test_bench_eight_ranks_each_rank_owns_its_gpu_gloo():
+    """8 gloo ranks, each on a fake amd-smi node of 8 distinct cards (HIP order reversed
+    against amd-smi order): rank r's scheduler config pins the device scorer to GPU r, its
+    telemetry template comes from the card whose HIP ordinal is r (a distinct BDF per rank),
+    and the one JSON line aggregates 8 × the per-rank pods."""
+    env_extra = {"YODA_BENCH_FAKE_SMI": "8"}
+    old = {k: os.environ.get(k) for k in env_extra}
+    os.environ.update(env_extra)
+    try:
+        r = _torchrun(["bench.py", "--gpus", "8", "--steps", "1", "--warmup", "0", "--config", "2",
+                       "--alt", "none"], nproc=8, timeout=600)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["pods_bound"] == 8 * 100 and d["config"]["global_batch"] == 800
+    ranks = sorted(d["ranks"], key=lambda x: x["rank"])
+    assert [x["rank"] for x in ranks] == list(range(8))
+    for x in ranks:
+        assert x["gpu_index"] == x["local_rank"] == x["rank"]
+        assert x["device_scorer_device"] == x["rank"]        # yodaRuntime.deviceScorer.device
+        assert x["telemetry_hip_id"] == x["rank"]            # its own card, by HIP ordinal
+        assert x["pods_bound"] == 100
+    assert len({x["telemetry_bdf"] for x in ranks}) == 8     # eight distinct cards
+    assert sum(x["pods_bound"] for x in ranks) == d["pods_bound"]

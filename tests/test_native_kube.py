@@ -402,6 +402,62 @@ def test_transport_request_timeout_against_silent_server():
     run(go())
 
 
+def test_transport_closes_connection_when_oldest_request_times_out():
+    """a black-holed connection must not keep its pool slot. The oldest request
+    times out (-2); everything pipelined behind it fails at once (-1, connection closed)
+    instead of each waiting out its own deadline, and the connection is reopened."""
+    import socket
+
+    async def go():
+        ls = socket.socket()
+        ls.bind(("127.0.0.1", 0))
+        ls.listen(8)
+        port = ls.getsockname()[1]
+        t = nat.NativeTransport(KubeConfig(f"http://127.0.0.1:{port}"), conns=1, max_inflight=8)
+        try:
+            t0 = time.perf_counter()
+            first = asyncio.ensure_future(t.request("GET", "/api/v1/nodes", timeout=0.2))
+            await asyncio.sleep(0.02)
+            later = [asyncio.ensure_future(t.request("GET", "/api/v1/nodes", timeout=30.0)) for _ in range(3)]
+            st0, _ = await first
+            rest = await asyncio.wait_for(asyncio.gather(*later), 5.0)
+            dt = time.perf_counter() - t0
+            assert st0 == -2
+            assert all(st == -1 and b"timed out" in body for st, body in rest), rest
+            assert dt < 2.0                                   # not the 30 s deadlines
+            conns0 = t.stats()["connects"]
+            st2, _ = await t.request("GET", "/api/v1/nodes", timeout=0.1)
+            assert st2 == -2 and t.stats()["connects"] == conns0 + 1    # a fresh connection
+        finally:
+            t.close()
+            ls.close()
+    run(go())
+
+
+def test_native_watch_idle_timeout_ends_a_silent_stream():
+    """A watch on a connection that delivers nothing ends after its idle timeout (status -1)
+    so the reflector re-watches, instead of waiting forever for the server's own end."""
+    import socket
+
+    async def go():
+        ls = socket.socket()
+        ls.bind(("127.0.0.1", 0))
+        ls.listen(8)
+        port = ls.getsockname()[1]
+        t = nat.NativeTransport(KubeConfig(f"http://127.0.0.1:{port}"), conns=1)
+        done = asyncio.get_event_loop().create_future()
+        try:
+            t0 = time.perf_counter()
+            t.watch("/api/v1/pods?watch=1", True, lambda evs: None,
+                    lambda st, body: done.done() or done.set_result((st, body)), idle_timeout=0.3)
+            st, body = await asyncio.wait_for(done, 5.0)
+            assert st == -1 and b"idle" in body and time.perf_counter() - t0 >= 0.25
+        finally:
+            t.close()
+            ls.close()
+    run(go())
+
+
 # ============================================================== reflector robustness
 def test_informer_handler_exception_is_isolated_no_relist():
     from yoda_scheduler_amd.fakeapi.client import InProcessClient

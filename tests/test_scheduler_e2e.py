@@ -601,3 +601,37 @@ def test_burst_cost_scales_linearly():
     small = min(per_pod(1000) for _ in range(2))
     big = min(per_pod(5000) for _ in range(2))
     assert big < 2.0 * small, (big * 1e6, small * 1e6)
+
+
+def test_bind_failure_after_echo_keeps_pod_bound():
+    """a Binding the apiserver applied whose answer was lost (-1 connection
+    closed, -2 timeout) arrives AFTER the watch echo confirmed the pod. Upstream ForgetPod
+    refuses pods that are no longer assumed: the pod stays in the cache, its reservation
+    stays in the ledger, and it is not requeued."""
+    from yoda_scheduler_amd.framework.interfaces import CycleState, Status
+    from yoda_scheduler_amd.models.pod import PodInfo
+    from yoda_scheduler_amd.ops.native import pod_req
+
+    async def go():
+        c = FakeCluster()
+        c.add_node("n0")
+        await c.start()
+        s = c.sched
+        obj = c.server.create("pods", {"metadata": {"name": "p", "namespace": "default",
+                                                    "labels": {"scv/memory": "1000"}},
+                                       "spec": {"schedulerName": "yoda-scheduler-x", "containers": [{"name": "c"}]}})
+        pi = PodInfo.from_obj(obj)
+        res = s.engine.schedule(pi.num_id, pod_req(s.engine, pi), True)
+        node = s.engine.node_name(res[0])
+        s.cache.assumed(pi, node, res[3])
+        s.pending_binds += 1
+        bound = dict(obj, spec=dict(obj["spec"], nodeName=node))
+        s.cache.add_pod(bound)                       # the echo confirms the assumed pod
+        assert not s.cache.is_assumed(pi.uid)
+        fw = next(iter(s.frameworks.values()))
+        s._after_bind(fw, CycleState(), pi, node, 0, 0.0, 0.0, Status.error("request timed out"))
+        kept = pi.uid in s.cache.pods and s.engine.has_pod(pi.num_id) and not s.queue.contains(pi.uid)
+        await c.stop()
+        return kept, s.scheduled
+    kept, scheduled = run(go())
+    assert kept and scheduled == 1

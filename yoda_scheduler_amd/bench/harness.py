@@ -22,9 +22,12 @@ from .workloads import Workload, pod_object, populate
 
 
 def bench_config(scheduler_name: str, qps: float, burst: int, batch: int, compat: bool = False,
-                 device: str = "auto", overlap: str = "auto", engine_threads: int = 1) -> dict:
+                 device: str = "auto", overlap: str = "auto", engine_threads: int = 1,
+                 device_index: int = 0) -> dict:
     """The shipped deploy profile (yoda at filter + score weight 300 on top of the
-    upstream defaults) with the yoda QueueSort enabled (Q7) and the given client QPS."""
+    upstream defaults) with the yoda QueueSort enabled (Q7) and the given client QPS.
+    ``device_index`` is the HIP ordinal the gfx950 device scorer runs on: a rank of a
+    multi-GPU bench passes its LOCAL_RANK, so rank r scores on GPU r."""
     prof = {"schedulerName": scheduler_name,
             "plugins": {"queueSort": {"enabled": [{"name": "yoda"}], "disabled": [{"name": "*"}]},
                         "filter": {"enabled": [{"name": "yoda", "weight": 0}]},
@@ -35,7 +38,7 @@ def bench_config(scheduler_name: str, qps: float, burst: int, batch: int, compat
             "leaderElection": {"leaderElect": False},
             "clientConnection": {"qps": qps, "burst": burst},
             "percentageOfNodesToScore": 0, "podInitialBackoffSeconds": 1, "podMaxBackoffSeconds": 10,
-            "yodaRuntime": {"batchSize": batch, "bindConcurrency": 256, "deviceScorer": {"enabled": device},
+            "yodaRuntime": {"batchSize": batch, "bindConcurrency": 256, "deviceScorer": {"enabled": device, "device": device_index},
                             "overlapEngine": overlap, "engineThreads": engine_threads},
             "profiles": [prof]}
 
@@ -66,12 +69,13 @@ class Shard:
     def __init__(self, w: Workload, qps: float = 5000.0, burst: int = 10000, batch: int = 256,
                  template: Optional[dict] = None, metrics: bool = False, events: bool = True,
                  compat: bool = False, seed: int = 0, engine_threads: int = 1, device: str = "auto",
-                 overlap: str = "auto") -> None:
+                 overlap: str = "auto", device_index: int = 0) -> None:
         self.w = w
         self.server = FakeApiServer()
         self.client = InProcessClient(self.server)
         populate(self.server, w, template, link_load=0.2 if w.id == 5 else 0.0, seed=seed)
-        cfg = parse_config(bench_config(w.scheduler_name, qps, burst, batch, compat, device, overlap))
+        cfg = parse_config(bench_config(w.scheduler_name, qps, burst, batch, compat, device, overlap,
+                                        device_index=device_index))
         self.sched = Scheduler(self.client, cfg, metrics=SchedulerMetrics() if metrics else NullMetrics(),
                                record_events=events, seed=seed, engine_threads=engine_threads)
         self.sched.e2e_samples = []
@@ -164,7 +168,7 @@ class HttpShard:
     def __init__(self, w: Workload, qps: float = 5000.0, burst: int = 10000, batch: int = 256,
                  template: Optional[dict] = None, events: bool = True, compat: bool = False, seed: int = 0,
                  device: str = "auto", overlap: str = "auto", apiserver: str = "native",
-                 client_native: str | bool = "auto", engine_threads: int = 1) -> None:
+                 client_native: str | bool = "auto", engine_threads: int = 1, device_index: int = 0) -> None:
         import json
         import os
         import subprocess
@@ -191,7 +195,7 @@ class HttpShard:
             env = dict(os.environ, PYTHONPATH=os.pathsep.join(p for p in (root, os.environ.get("PYTHONPATH")) if p))
         self.proc = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env)
         self.cfg = parse_config(bench_config(w.scheduler_name, qps, burst, batch, compat, device, overlap,
-                                             engine_threads))
+                                             engine_threads, device_index))
         self.events, self.seed = events, seed
         self.sched: Optional[Scheduler] = None
         self.client = None

@@ -1023,6 +1023,16 @@ class Scheduler:
             self.recorder.pod_scheduled(pi, node)
         else:
             self.bind_errors += 1
+            ps = self.cache.pods.get(pi.uid)
+            if ps is not None and not ps.assumed and ps.node == node:
+                # the Binding was applied — its watch echo already confirmed the pod — and
+                # only the answer was lost (connection closed under pipelined requests,
+                # client timeout): the pod is bound, so neither forget it (its reservation
+                # is real) nor retry it (upstream ForgetPod refuses pods no longer assumed)
+                self.scheduled += 1
+                log.info("bind %s → %s answered %s after its echo confirmed it; kept as bound",
+                         pi.key, node, st.message())
+                return
             fw.run_unreserve(state, pi, node)
             self.cache.forget(pi)
             m.child(m.e2e, "error", fw.name).observe(time.perf_counter() - t0)

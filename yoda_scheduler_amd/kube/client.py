@@ -33,6 +33,9 @@ from .errors import ApiError
 from .resources import resource
 
 SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+# a native watch that delivered nothing (no event, no bookmark, no server-side end) for its
+# timeoutSeconds plus this grace is taken as a black-holed connection and re-watched
+WATCH_IDLE_GRACE_S = 30.0
 TOKEN_REFRESH_S = 60.0          # client-go cachedTokenSource re-reads the file every minute
 log = logging.getLogger("yoda.client")
 
@@ -317,7 +320,8 @@ class KubeClient:
         """Start a native watch stream; events arrive in batches through ``on_events``."""
         self._refresh_token()
         return self.native.watch(self._path(res, params=self._watch_params(resource_version, field_selector,
-                                                                           timeout_s)), pods, on_events, on_end)
+                                                                           timeout_s)), pods, on_events, on_end,
+                                 idle_timeout=timeout_s + WATCH_IDLE_GRACE_S)
 
     async def watch(self, res: str, resource_version: str, field_selector: Optional[str] = None,
                     timeout_s: int = 300) -> AsyncIterator[tuple[str, dict]]:

@@ -29,8 +29,8 @@ def module():
     """The compiled ``_yoda_kube`` extension (raises ImportError when it is not built)."""
     global _mod
     if _mod is None:
-        from .._native import _yoda_kube  # type: ignore[attr-defined]
-        _mod = _yoda_kube
+        from ..ops.native import load_native
+        _mod = load_native("kube", "yoda_scheduler_amd._native._yoda_kube")
     return _mod
 
 
@@ -180,9 +180,11 @@ class NativeTransport:
         for k, cb in enumerate(cbs):
             cb_map[first + k] = cb
 
-    def watch(self, path: str, pods: bool, on_events: Callable, on_end: Callable) -> int:
+    def watch(self, path: str, pods: bool, on_events: Callable, on_end: Callable, idle_timeout: float = 0.0) -> int:
+        """``idle_timeout``: end the stream (status -1) if nothing arrives for that long — a
+        black-holed connection never delivers the server's own ``timeoutSeconds`` end."""
         self._attach()
-        wid = self.t.watch(path, pods)
+        wid = self.t.watch(path, pods, float(idle_timeout))
         self._watches[wid] = WatchHandle(wid, on_events, on_end)
         return wid
 

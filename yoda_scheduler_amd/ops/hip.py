@@ -62,14 +62,25 @@ def lib() -> ctypes.CDLL:
             # No torch import here: a scheduler process should not pay for torch. Processes
             # that use torch (bench, smoke, GPU tests) import it first, so the shared SONAME
             # resolves our NEEDED entry to torch's already-loaded runtime.
-            if not PATH.exists():
-                from .build import build_hip, OUT
-                OUT.mkdir(parents=True, exist_ok=True)
-                build_hip()
+            from . import build
+            if "YODA_HIP_LIB" not in os.environ:
+                build.ensure_fresh("hip")         # missing or built from other sources: rebuild
             l = ctypes.CDLL(str(PATH), mode=ctypes.RTLD_GLOBAL)
             _declare(l)
+            if "YODA_HIP_LIB" not in os.environ and (build.NATIVE / "common" / "build_id.h").exists():
+                build.verify_loaded("hip", build_id(l))
             _LIB = l
     return _LIB
+
+
+def build_id(l: Optional[ctypes.CDLL] = None) -> str:
+    """Source hash compiled into the loaded ``libyoda_hip.so`` (``ops/build.py``)."""
+    l = l if l is not None else lib()
+    f = getattr(l, "yoda_build_id", None)
+    if f is None:
+        return ""
+    f.argtypes, f.restype = [], c_char_p
+    return (f() or b"").decode()
 
 
 def _check(rc: int, what: str) -> None:

@@ -23,16 +23,22 @@ def core():
         return _core
     with _lock:
         if _core is None:
-            try:
-                _core = importlib.import_module("yoda_scheduler_amd._native._yoda_core")
-            except ImportError:
-                from .build import build_core, OUT
-                OUT.mkdir(parents=True, exist_ok=True)
-                (OUT / "__init__.py").touch()
-                build_core()
-                importlib.invalidate_caches()
-                _core = importlib.import_module("yoda_scheduler_amd._native._yoda_core")
+            _core = load_native("core", "yoda_scheduler_amd._native._yoda_core")
     return _core
+
+
+def load_native(name: str, module: str):
+    """Import a pybind artefact after making sure it was built from this tree's sources
+    (rebuilt in-tree if its recorded build id is stale), then check the id compiled into
+    the module actually loaded (``ops/build.py``: build provenance)."""
+    from . import build
+    build.ensure_fresh(name)
+    importlib.invalidate_caches()
+    mod = importlib.import_module(module)
+    bid = getattr(mod, "build_id", None)
+    if (build.NATIVE / "common" / "build_id.h").exists():
+        build.verify_loaded(name, bid() if bid is not None else "")
+    return mod
 
 
 def card_tuples(scv: Scv) -> list[tuple]:

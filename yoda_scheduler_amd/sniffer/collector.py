@@ -30,13 +30,8 @@ class AmdSmiBackend:
     name = "amd-smi"
 
     def __init__(self) -> None:
-        try:
-            mod = importlib.import_module("yoda_scheduler_amd._native._yoda_sniffer")
-        except ImportError:
-            from ..ops.build import build_sniffer
-            build_sniffer()
-            importlib.invalidate_caches()
-            mod = importlib.import_module("yoda_scheduler_amd._native._yoda_sniffer")
+        from ..ops.native import load_native
+        mod = load_native("sniffer", "yoda_scheduler_amd._native._yoda_sniffer")
         self._c = mod.Collector()
         ok, err = self._c.init()
         if not ok:
