@@ -95,8 +95,10 @@ SelTerm make_term(Engine& e, const py::list& reqs) {
   return t;
 }
 
+// (node, feasible, evaluated, cards, score, reason_counts, gang_quality, node_gen, stale)
 py::tuple cycle_tuple(const CycleResult& r) {
-  return py::make_tuple(r.node, r.feasible, r.evaluated, r.cards, r.score, r.reason_counts, r.gang_quality);
+  return py::make_tuple(r.node, r.feasible, r.evaluated, r.cards, r.score, r.reason_counts, r.gang_quality,
+                        r.node_gen, r.stale);
 }
 
 // Engine batches on a native thread. The event loop submits a batch (ids + request
@@ -283,6 +285,8 @@ PYBIND11_MODULE(_yoda_core, m) {
       .def_property_readonly("cycles", &Engine::cycles)
       .def_property_readonly("ledger_size", &Engine::ledger_size)
       .def("node_name", [](Engine& e, int32_t i) { return e.node(i).name; }, py::call_guard<EngineGuard>())
+      .def("node_gen", &Engine::node_gen, py::call_guard<EngineGuard>(),
+           "generation of a node slot (changes when the slot's node is removed or replaced)")
       .def("set_node_meta",
            [](Engine& e, int32_t idx, bool unsched, const std::vector<std::pair<std::string, std::string>>& labels,
               const std::vector<std::tuple<std::string, std::string, std::string>>& taints, int64_t cpu_m,

@@ -95,6 +95,26 @@ Engine::~Engine() {
   delete pool_;
 }
 
+EngineConfig Engine::config() const {
+  EngineConfig c;
+  c.filters = filters_;
+  std::copy(score_w_, score_w_ + S_NUM, c.score_w);
+  for (int k = 0; k < 2; ++k)
+    for (int j = 0; j < 3; ++j) c.alloc_w[k][j] = alloc_w_[k][j];
+  c.wt = wt_;
+  c.settle_s = settle_s_;
+  return c;
+}
+
+void Engine::set_config(const EngineConfig& c) {
+  filters_ = c.filters;
+  std::copy(c.score_w, c.score_w + S_NUM, score_w_);
+  for (int k = 0; k < 2; ++k)
+    for (int j = 0; j < 3; ++j) alloc_w_[k][j] = c.alloc_w[k][j];
+  wt_ = c.wt;
+  settle_s_ = c.settle_s;
+}
+
 int32_t Engine::intern(const std::string& s) {
   auto it = string_idx_.find(s);
   if (it != string_idx_.end()) return it->second;
@@ -118,6 +138,7 @@ int32_t Engine::upsert_node(const std::string& name) {
   }
   nodes_[idx].name = name;
   nodes_[idx].alive = true;
+  nodes_[idx].gen = ++gen_counter_;
   node_idx_[name] = idx;
   ++live_;
   mark_dirty(idx);
@@ -141,6 +162,8 @@ void Engine::remove_node(int32_t idx) {
   prefer_taint_nodes_ -= nodes_[idx].prefer_taint;
   nodes_[idx] = Node();
   nodes_[idx].alive = false;
+  nodes_[idx].gen = ++gen_counter_;
+  if (batch_in_flight_.load(std::memory_order_acquire)) removed_in_flight_.push_back(idx);
   free_slots_.push_back(idx);
   --live_;
   mark_dirty(idx);
@@ -801,6 +824,7 @@ CycleResult Engine::schedule(uint64_t pod, const PodReq& req, bool assume, const
     std::unique_lock<std::mutex> dl(dev_mu_, std::try_to_lock);
     if (dl.owns_lock() && schedule_device(req, &r)) {
       dl.unlock();
+      if (r.node >= 0) r.node_gen = nodes_[r.node].gen;
       if (assume && r.node >= 0) reserve(pod, req, r.node, r.cards);
       return r;
     }
@@ -840,6 +864,7 @@ CycleResult Engine::schedule(uint64_t pod, const PodReq& req, bool assume, const
     r.score = best;
   }
   r.node = chosen;
+  r.node_gen = nodes_[chosen].gen;
   if (filters_ & F_YODA) {
     int32_t q = 10000;
     if (!select_gpus(req, chosen, &r.cards, &q) && !compat_) {
@@ -1132,6 +1157,7 @@ bool Engine::schedule_batch_device(const std::vector<uint64_t>& pods, const std:
   // engine lock dropped: mutations meanwhile (bind confirmations, releases, Scv samples)
   // mark their rows dirty and reach the device with the next flush, exactly as if they had
   // happened after the batch
+  removed_in_flight_.clear();
   batch_in_flight_.store(true, std::memory_order_release);
   if (ext_mu_) ext_mu_->unlock();
   const int rc = ((batch_t)fn_schedule_batch_)(ctx, n_nodes, (int)d.size(), d.data(), res.data());
@@ -1154,7 +1180,18 @@ bool Engine::schedule_batch_device(const std::vector<uint64_t>& pods, const std:
     ++dev_cycles_;
     CycleResult r;
     fill_result(res[i], &r);
-    if (r.node >= 0 && !reserve(pods[i], *reqs[i], r.node, r.cards)) diverged.push_back(r.node);
+    if (r.node >= 0 && std::find(removed_in_flight_.begin(), removed_in_flight_.end(), r.node) !=
+                           removed_in_flight_.end()) {
+      // the node was deleted (and its slot maybe reused by another node) while the device
+      // placed this pod on the old row: never bind it there — the caller retries the pod
+      diverged.push_back(r.node);
+      r.stale = true;
+      r.node = -1;
+      r.cards.clear();
+    } else if (r.node >= 0) {
+      r.node_gen = nodes_[r.node].gen;
+      if (!reserve(pods[i], *reqs[i], r.node, r.cards)) diverged.push_back(r.node);
+    }
     out->push_back(std::move(r));
   }
   // a row reserve() just dirtied was clean when the batch started and untouched since, and
@@ -1163,6 +1200,7 @@ bool Engine::schedule_batch_device(const std::vector<uint64_t>& pods, const std:
   for (size_t k = mark; k < dirty_list_.size(); ++k) dirty_[dirty_list_[k]] = 0;
   dirty_list_.resize(mark);
   for (int32_t i : diverged) mark_dirty(i);
+  removed_in_flight_.clear();
   return true;
 }
 

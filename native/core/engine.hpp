@@ -78,6 +78,7 @@ struct PrefTerm { int32_t weight; SelTerm term; };
 
 struct Node {
   std::string name;
+  uint32_t gen = 0;                   // slot generation: bumped when the slot gets a new node or dies
   bool alive = true;
   bool unschedulable = false;
   bool has_scv = false;
@@ -134,6 +135,8 @@ struct Assignment {
 
 struct CycleResult {
   int32_t node = -1;                 // selected node, -1 = unschedulable
+  uint32_t node_gen = 0;             // generation of that node's slot when it was selected
+  bool stale = false;                // the node was removed / its slot reused while the device placed it
   int32_t feasible = 0;
   int32_t evaluated = 0;
   std::vector<int32_t> cards;        // GPU assignment on the selected node
@@ -163,10 +166,23 @@ class ThreadPool {
   bool stop_ = false;
 };
 
+// Everything a profile configures on the engine (Framework.apply): the native lane keeps one
+// per profile and swaps it in around its batches, restoring the caller's afterwards.
+struct EngineConfig {
+  uint32_t filters = 0;
+  int64_t score_w[S_NUM] = {0, 0, 0, 0, 0, 0};
+  int64_t alloc_w[2][3] = {{1, 1, 0}, {1, 1, 0}};
+  Weights wt;
+  double settle_s = 30.0;
+};
+
 class Engine {
  public:
   Engine(bool compat, int threads);
   ~Engine();
+
+  EngineConfig config() const;
+  void set_config(const EngineConfig& c);
 
   // ---- configuration
   bool compat() const { return compat_; }
@@ -201,6 +217,9 @@ class Engine {
   Node& node(int32_t idx) { return nodes_[idx]; }
   const Node& node(int32_t idx) const { return nodes_[idx]; }
   int32_t num_nodes() const { return (int32_t)nodes_.size(); }
+  uint32_t node_gen(int32_t idx) const {
+    return idx >= 0 && idx < (int32_t)nodes_.size() ? nodes_[idx].gen : 0;
+  }
   int32_t live_nodes() const { return live_; }
   // sample_ts: when the Scv sample was taken (unix s). Reservations younger than
   // sample_ts − settle are "pending": the sample cannot contain their HBM use yet, so
@@ -312,6 +331,8 @@ class Engine {
   int32_t unsched_key_ = 0;
   std::vector<Node> nodes_;
   std::vector<int32_t> free_slots_;
+  uint32_t gen_counter_ = 0;
+  std::vector<int32_t> removed_in_flight_;   // slots removed while a device batch held no lock
   int32_t live_ = 0;
   std::unordered_map<std::string, int32_t> node_idx_;
   std::vector<std::string> strings_;

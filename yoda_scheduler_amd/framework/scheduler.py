@@ -564,7 +564,9 @@ class Scheduler:
     def _hybrid_finish(self, fw: Framework, state: CycleState, pi: PodInfo, req, feas_idx, reasons, failed,
                        ext_scores: Optional[dict] = None):
         if not feas_idx:
-            return (-1, 0, self.engine.live_nodes, [], 0, list(reasons), 0, failed, len(failed))
+            # the engine's cycle tuple (node, feasible, evaluated, cards, score, reasons,
+            # gang quality, node gen, stale) + the Python filters' statuses
+            return (-1, 0, self.engine.live_nodes, [], 0, list(reasons), 0, 0, False, failed, len(failed))
         names = [self.engine.node_name(i) for i in feas_idx]
         extra = fw.run_score_py(state, pi, names) if (len(names) > 1 and fw.score_py) else []
         if ext_scores:
@@ -575,10 +577,22 @@ class Scheduler:
         node_idx = res[0]
         m = self.metrics
         if node_idx < 0:
+            if res[8] is True:
+                # the device placed the pod on a node deleted meanwhile: retry, not unschedulable
+                self._fail(fw, state, pi, cycle, "the selected node was removed during the cycle", t0,
+                           unschedulable=False)
+                return
             msg = self._fit_error(res)
             self._fail(fw, state, pi, cycle, msg, t0)
             return
-        node = self._node_name(node_idx)
+        node, gen = self._node_name(node_idx)
+        if gen != res[7]:
+            # the slot's node was removed (its reservations with it) or replaced by another
+            # node between the engine cycle and now: binding there would skip every filter
+            self.engine.release(pi.num_id)
+            self._fail(fw, state, pi, cycle, "the selected node was removed before the binding", t0,
+                       unschedulable=False)
+            return
         cards = res[3]
         self.cache.assumed(pi, node, cards)
         pi.assigned_cards = cards if (fw.filter_mask & self._f_yoda) else None
@@ -608,15 +622,17 @@ class Scheduler:
         else:
             self._enqueue_bind((fw, state, pi, node, cycle, t0))
 
-    def _node_name(self, idx: int) -> str:
-        """Engine node index → name, memoised until a node is added or removed."""
+    def _node_name(self, idx: int) -> tuple:
+        """Engine node index → (name, slot generation), memoised until a node is added or
+        removed. A cycle result whose generation differs names a slot that was freed (and
+        maybe reused by another node) after the engine placed the pod."""
         if self._names_gen != self.cache.node_generation:
             self._names.clear()
             self._names_gen = self.cache.node_generation
-        name = self._names.get(idx)
-        if name is None:
-            name = self._names[idx] = self.engine.node_name(idx)
-        return name
+        ng = self._names.get(idx)
+        if ng is None:
+            ng = self._names[idx] = (self.engine.node_name(idx), self.engine.node_gen(idx))
+        return ng
 
     async def _permit_then_bind(self, item: tuple) -> None:
         fw, state, pi, node, cycle, t0 = item
@@ -645,9 +661,9 @@ class Scheduler:
                 "GpuClock": "node(s) have too few GPUs with the requested clock",
                 "GpuFit": "node(s) have too few healthy GPUs matching scv/memory+scv/clock"}
         parts = [f"{c} {text.get(names[i], names[i])}" for i, c in enumerate(reasons) if c and i]
-        if len(res) > 8 and res[8]:
+        if len(res) > 10 and res[10]:
             by_msg: dict[str, int] = {}
-            for st in res[7].values():
+            for st in res[9].values():
                 by_msg[st.message() or "node(s) rejected by out-of-tree filters"] = \
                     by_msg.get(st.message() or "node(s) rejected by out-of-tree filters", 0) + 1
             parts.extend(f"{c} {m}" for m, c in by_msg.items())
