@@ -16,6 +16,7 @@
 #include <pybind11/stl.h>
 
 #include "engine.hpp"
+#include "lane.hpp"
 
 namespace py = pybind11;
 using namespace yoda;
@@ -475,6 +476,141 @@ PYBIND11_MODULE(_yoda_core, m) {
              for (auto& r : res) out.append(cycle_tuple(r));
              return out;
            });
+
+  // ---- native pod lane (lane.hpp). PodEvent objects are the _yoda_kube module's type
+  // (pybind11 shares registered types across modules built with the same headers).
+  py::class_<Lane>(m, "Lane")
+      .def(py::init([](Engine& e, int batch, double bind_timeout, int sort_kind, bool events, bool events_v1,
+                       double event_qps, int event_burst, int event_buffer, const std::string& host,
+                       const std::string& name_prefix) {
+             LaneOptions o;
+             o.batch = batch;
+             o.bind_timeout_s = bind_timeout;
+             o.sort_kind = sort_kind;
+             o.events = events;
+             o.events_v1 = events_v1;
+             o.event_qps = event_qps;
+             o.event_burst = event_burst;
+             o.event_buffer = event_buffer;
+             o.host = host;
+             o.name_prefix = name_prefix;
+             return std::make_unique<Lane>(&e, &g_engine_mu, std::move(o));
+           }),
+           py::arg("engine"), py::arg("batch") = 256, py::arg("bind_timeout") = 30.0, py::arg("sort_kind") = 0,
+           py::arg("events") = true, py::arg("events_v1") = true, py::arg("event_qps") = 50.0,
+           py::arg("event_burst") = 300, py::arg("event_buffer") = 1000, py::arg("host") = "localhost",
+           py::arg("name_prefix") = "00000000", py::keep_alive<1, 2>())
+      .def("sink_ptr", [](Lane& l) { return (uintptr_t) static_cast<yk::PodSink*>(&l); })
+      .def("set_port", [](Lane& l, uintptr_t p) { l.set_port(reinterpret_cast<yk::PodPort*>(p)); })
+      // the profile's engine configuration is the engine's current one (the caller applied it)
+      .def("set_profile",
+           [](Lane& l, Engine& e, const std::string& name, bool enabled, int flag_mask, bool annotate) {
+             Lane::Profile p;
+             p.name = name;
+             p.enabled = enabled;
+             p.flag_mask = flag_mask;
+             p.annotate = annotate;
+             {
+               EngineGuard g;
+               p.cfg = e.config();
+             }
+             l.set_profile(p);
+           },
+           py::arg("engine"), py::arg("name"), py::arg("enabled"), py::arg("flag_mask"), py::arg("annotate"))
+      .def("set_active", &Lane::set_active)
+      .def("set_node_cards", &Lane::set_node_cards, py::arg("node"), py::arg("vis"))
+      .def("remove_node_cards", &Lane::remove_node_cards)
+      .def("fileno", &Lane::fileno)
+      // ([(type, PodEvent, old PodEvent | None)], [handoff], moves)
+      // handoff = (kind, PodEvent, profile, cycle tuple, status, message, t_enqueue, t_cycle)
+      .def("drain",
+           [](Lane& l) {
+             std::vector<Lane::Fwd> fwd;
+             std::vector<Lane::Handoff> hand;
+             uint64_t moves = 0;
+             l.drain(&fwd, &hand, &moves);
+             static py::object* types = new py::object[3]{py::str("ADDED"), py::str("MODIFIED"), py::str("DELETED")};
+             py::list f;
+             for (auto& x : fwd)
+               f.append(py::make_tuple(types[x.type == 'A' ? 0 : x.type == 'M' ? 1 : 2], py::cast(x.ev),
+                                       x.old ? py::cast(x.old) : py::none()));
+             py::list h;
+             for (auto& x : hand)
+               h.append(py::make_tuple(x.kind, py::cast(x.ev), x.profile, cycle_tuple(x.res), x.status,
+                                       py::bytes(x.msg), x.t_enqueue, x.t_cycle));
+             return py::make_tuple(f, h, moves);
+           })
+      .def("relist",
+           [](Lane& l, std::vector<std::shared_ptr<yk::PodEv>> items) {
+             std::vector<Lane::Fwd> fwd;
+             {
+               py::gil_scoped_release nogil;
+               fwd = l.relist(std::move(items));
+             }
+             static py::object* types = new py::object[3]{py::str("ADDED"), py::str("MODIFIED"), py::str("DELETED")};
+             py::list f;
+             for (auto& x : fwd)
+               f.append(py::make_tuple(types[x.type == 'A' ? 0 : x.type == 'M' ? 1 : 2], py::cast(x.ev),
+                                       x.old ? py::cast(x.old) : py::none()));
+             return f;
+           })
+      .def("lookup",
+           [](Lane& l, const std::string& key) -> py::object {
+             bool owned = false;
+             std::shared_ptr<yk::PodEv> ev;
+             {
+               py::gil_scoped_release nogil;
+               ev = l.lookup(key, &owned);
+             }
+             if (!ev) return py::none();
+             return py::make_tuple(py::cast(ev), owned);
+           })
+      .def("keys", &Lane::keys, py::call_guard<py::gil_scoped_release>())
+      .def("__len__", &Lane::store_size, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("scheduled", [](Lane& l) { return l.scheduled_.load(std::memory_order_relaxed); })
+      .def("stats",
+           [](Lane& l) {
+             LaneStats s = l.stats();
+             py::dict d;
+             d["admitted"] = s.admitted;
+             d["scheduled"] = s.scheduled;
+             d["unschedulable"] = s.unschedulable;
+             d["bind_errors"] = s.bind_errors;
+             d["stale_retries"] = s.stale_retries;
+             d["forwarded"] = s.forwarded;
+             d["released"] = s.released;
+             d["batches"] = s.batches;
+             d["confirmed"] = s.confirmed;
+             d["events_recorded"] = s.events_recorded;
+             d["events_dropped"] = s.events_dropped;
+             d["events_written"] = s.events_written;
+             d["event_errors"] = s.event_errors;
+             d["lost_answers_kept"] = s.lost_answers_kept;
+             d["queued"] = s.queued;
+             d["inflight"] = s.inflight;
+             d["binding"] = s.binding;
+             d["owned"] = s.owned;
+             return d;
+           })
+      .def("pause", &Lane::pause, py::call_guard<py::gil_scoped_release>())
+      // (full, [(id, add, PodEvent | None, node, cards)])
+      .def("changes",
+           [](Lane& l) {
+             bool full = false;
+             std::vector<Lane::Change> ch;
+             {
+               py::gil_scoped_release nogil;
+               ch = l.changes(&full);
+             }
+             py::list out;
+             for (auto& c : ch)
+               out.append(py::make_tuple(c.id, c.add, c.ev ? py::cast(c.ev) : py::none(), c.node, c.cards));
+             return py::make_tuple(full, out);
+           })
+      .def("take_e2e", &Lane::take_e2e)
+      .def("take_pod_latency", &Lane::take_pod_latency)
+      .def("wait_idle", &Lane::wait_idle, py::arg("timeout") = 5.0, py::call_guard<py::gil_scoped_release>())
+      .def("close", &Lane::close, py::call_guard<py::gil_scoped_release>());
 
   py::class_<BatchWorker>(m, "BatchWorker")
       .def(py::init([](Engine& e) { return std::make_unique<BatchWorker>(&e); }), py::keep_alive<1, 2>())

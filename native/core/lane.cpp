@@ -1,0 +1,1068 @@
+// Native pod lane (see lane.hpp).
+#include "lane.hpp"
+
+#include <sys/eventfd.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <ctime>
+
+namespace yoda {
+
+namespace {
+
+constexpr uint64_t kEventTag = 1ull << 63;
+
+// Go strconv.Atoi: optional sign, decimal digits only, int64 range (utils/gonum.py::atoi).
+bool go_atoi(const std::string& s, int64_t* out) {
+  size_t i = 0;
+  bool neg = false;
+  if (!s.empty() && (s[0] == '+' || s[0] == '-')) {
+    neg = s[0] == '-';
+    i = 1;
+  }
+  if (i >= s.size()) return false;
+  unsigned __int128 v = 0;
+  for (; i < s.size(); ++i) {
+    const char c = s[i];
+    if (c < '0' || c > '9') return false;
+    v = v * 10 + (unsigned)(c - '0');
+    if (v > ((unsigned __int128)1 << 63)) return false;
+  }
+  if (!neg && v > (unsigned __int128)INT64_MAX) return false;
+  *out = neg ? (int64_t)(-(__int128)v) : (int64_t)v;
+  return true;
+}
+
+int64_t atoi_or_zero(const std::string& s) {
+  int64_t v;
+  return go_atoi(s, &v) ? v : 0;
+}
+
+// filter.strToUint / StrToUint64 (filter.go:60-74): Atoi, error → 0, negative wraps
+uint64_t str_to_uint(const std::string& s) { return (uint64_t)atoi_or_zero(s); }
+
+int8_t effect_of(const std::string& e) {
+  if (e == "NoSchedule") return kNoSchedule;
+  if (e == "PreferNoSchedule") return kPreferNoSchedule;
+  if (e == "NoExecute") return kNoExecute;
+  return kEffectAny;
+}
+
+bool selop_of(const std::string& op, int8_t* out) {
+  if (op == "In") *out = kIn;
+  else if (op == "NotIn") *out = kNotIn;
+  else if (op == "Exists") *out = kExists;
+  else if (op == "DoesNotExist") *out = kDoesNotExist;
+  else if (op == "Gt") *out = kGt;
+  else if (op == "Lt") *out = kLt;
+  else return false;
+  return true;
+}
+
+void json_str(const std::string& s, std::string& o) {
+  o.push_back('"');
+  for (unsigned char c : s) {
+    switch (c) {
+      case '"': o += "\\\""; break;
+      case '\\': o += "\\\\"; break;
+      case '\n': o += "\\n"; break;
+      case '\r': o += "\\r"; break;
+      case '\t': o += "\\t"; break;
+      default:
+        if (c < 0x20) {
+          char b[8];
+          snprintf(b, sizeof b, "\\u%04x", c);
+          o += b;
+        } else {
+          o.push_back((char)c);
+        }
+    }
+  }
+  o.push_back('"');
+}
+
+// metav1.MicroTime (framework/events.py::micro_time)
+std::string micro_time(double ts) {
+  time_t sec = (time_t)ts;
+  long us = std::lround((ts - (double)sec) * 1e6);
+  if (us >= 1000000) {
+    sec += 1;
+    us -= 1000000;
+  }
+  struct tm tm;
+  gmtime_r(&sec, &tm);
+  char buf[48];
+  strftime(buf, sizeof buf, "%Y-%m-%dT%H:%M:%S", &tm);
+  char out[64];
+  snprintf(out, sizeof out, "%s.%06ldZ", buf, us);
+  return out;
+}
+
+double wall() {
+  return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+}
+
+std::string key_of(const yk::PodProj& p) { return p.ns + "/" + p.name; }
+
+bool terminal(const yk::PodProj& p) { return p.phase == "Succeeded" || p.phase == "Failed"; }
+
+bool config_eq(const EngineConfig& a, const EngineConfig& b) {
+  if (a.filters != b.filters || a.settle_s != b.settle_s) return false;
+  for (int i = 0; i < S_NUM; ++i)
+    if (a.score_w[i] != b.score_w[i]) return false;
+  for (int k = 0; k < 2; ++k)
+    for (int j = 0; j < 3; ++j)
+      if (a.alloc_w[k][j] != b.alloc_w[k][j]) return false;
+  const Weights &x = a.wt, &y = b.wt;
+  return x.w_link == y.w_link && x.w_numa == y.w_numa && x.w_fit == y.w_fit && x.w_occ == y.w_occ &&
+         x.gpu_binpack == y.gpu_binpack && x.w_gang_score == y.w_gang_score && x.enum_limit == y.enum_limit;
+}
+
+}  // namespace
+
+double Lane::mono() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+Lane::Lane(Engine* e, std::recursive_mutex* engine_mu, LaneOptions o) : eng_(e), emu_(engine_mu), o_(std::move(o)) {
+  if (o_.batch < 1) o_.batch = 1;
+  efd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+  if (efd_ < 0) throw std::runtime_error("eventfd failed");
+  ev_tokens_ = o_.event_burst > 0 ? o_.event_burst : 1;
+  ev_last_ = mono();
+  th_ = std::thread([this] { run(); });
+}
+
+Lane::~Lane() { close(); }
+
+void Lane::close() {
+  {
+    std::lock_guard<std::mutex> g(in_mu_);
+    if (stop_.exchange(true)) {
+      if (!th_.joinable()) return;
+    }
+    in_cv_.notify_all();
+  }
+  if (th_.joinable()) th_.join();
+  relist_cv_.notify_all();
+  if (efd_ >= 0) {
+    ::close(efd_);
+    efd_ = -1;
+  }
+}
+
+// ------------------------------------------------------------------ configuration
+void Lane::set_profile(const Profile& p) {
+  {
+    std::lock_guard<std::mutex> g(prof_mu_);
+    auto it = std::find_if(profiles_.begin(), profiles_.end(), [&](const Profile& x) { return x.name == p.name; });
+    if (it == profiles_.end()) profiles_.push_back(p);
+    else *it = p;
+  }
+  std::lock_guard<std::mutex> g(in_mu_);
+  Item it;
+  it.k = Item::kProfiles;
+  inbox_.push_back(std::move(it));
+  in_cv_.notify_one();
+}
+
+void Lane::set_active(bool on) {
+  std::lock_guard<std::mutex> g(in_mu_);
+  active_.store(on);
+  in_cv_.notify_one();
+}
+
+void Lane::set_node_cards(const std::string& node, std::vector<std::pair<std::string, std::string>> vis) {
+  std::lock_guard<std::mutex> g(vis_mu_);
+  vis_[node] = std::move(vis);
+}
+
+void Lane::remove_node_cards(const std::string& node) {
+  std::lock_guard<std::mutex> g(vis_mu_);
+  vis_.erase(node);
+}
+
+// ------------------------------------------------------------------ transport callbacks
+void Lane::on_pod_events(uint64_t, std::vector<yk::WatchEvent>& evs) {
+  size_t kept = 0;
+  {
+    std::lock_guard<std::mutex> g(in_mu_);
+    for (auto& e : evs) {
+      if (e.pod && (e.type == 'A' || e.type == 'M' || e.type == 'D')) {
+        Item it;
+        it.k = Item::kEvent;
+        it.type = e.type;
+        it.ev = std::move(e.pod);
+        inbox_.push_back(std::move(it));
+      } else {
+        if (&evs[kept] != &e) evs[kept] = std::move(e);
+        ++kept;
+      }
+    }
+    in_cv_.notify_one();
+  }
+  evs.resize(kept);
+}
+
+void Lane::on_answer(uint64_t tag, int status, std::string&& body) {
+  std::lock_guard<std::mutex> g(in_mu_);
+  Item it;
+  it.k = Item::kAnswer;
+  it.tag = tag;
+  it.status = status;
+  it.body = std::move(body);
+  inbox_.push_back(std::move(it));
+  in_cv_.notify_one();
+}
+
+// ------------------------------------------------------------------ Python side
+void Lane::drain(std::vector<Fwd>* fwd, std::vector<Handoff>* hand, uint64_t* moves) {
+  uint64_t v;
+  while (::read(efd_, &v, sizeof v) > 0) {
+  }
+  std::lock_guard<std::mutex> g(out_mu_);
+  fwd->swap(out_fwd_);
+  hand->swap(out_hand_);
+  *moves = out_moves_;
+  out_moves_ = 0;
+  signalled_ = false;
+}
+
+std::vector<Lane::Fwd> Lane::relist(std::vector<std::shared_ptr<yk::PodEv>> items) {
+  uint64_t token;
+  std::unique_lock<std::mutex> lk(in_mu_);
+  token = ++relist_next_;
+  Item it;
+  it.k = Item::kRelist;
+  it.items = std::make_shared<std::vector<std::shared_ptr<yk::PodEv>>>(std::move(items));
+  it.token = token;
+  inbox_.push_back(std::move(it));
+  in_cv_.notify_one();
+  relist_cv_.wait(lk, [&] { return relist_done_ >= token || stop_.load(); });
+  std::vector<Fwd> out;
+  auto f = relist_out_.find(token);
+  if (f != relist_out_.end()) {
+    out = std::move(f->second);
+    relist_out_.erase(f);
+  }
+  return out;
+}
+
+std::shared_ptr<yk::PodEv> Lane::lookup(const std::string& key, bool* owned) {
+  std::lock_guard<std::mutex> g(store_mu_);
+  auto it = by_key_.find(key);
+  if (it == by_key_.end()) return nullptr;
+  if (owned) *owned = it->second->st != PY;
+  return it->second->ev;
+}
+
+std::vector<std::string> Lane::keys() {
+  std::lock_guard<std::mutex> g(store_mu_);
+  std::vector<std::string> out;
+  out.reserve(by_key_.size());
+  for (auto& kv : by_key_) out.push_back(kv.first);
+  return out;
+}
+
+size_t Lane::store_size() {
+  std::lock_guard<std::mutex> g(store_mu_);
+  return by_key_.size();
+}
+
+LaneStats Lane::stats() {
+  LaneStats s;
+  {
+    std::lock_guard<std::mutex> g(stat_mu_);
+    s = st_;
+  }
+  return s;
+}
+
+std::vector<float> Lane::take_e2e() {
+  std::lock_guard<std::mutex> g(stat_mu_);
+  std::vector<float> v;
+  v.swap(e2e_);
+  return v;
+}
+
+std::vector<float> Lane::take_pod_latency() {
+  std::lock_guard<std::mutex> g(stat_mu_);
+  std::vector<float> v;
+  v.swap(pod_lat_);
+  return v;
+}
+
+void Lane::wait_idle(double timeout_s) {
+  const auto until = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+  std::unique_lock<std::mutex> lk(in_mu_);
+  while (std::chrono::steady_clock::now() < until) {
+    bool queued;
+    {
+      std::lock_guard<std::mutex> g(stat_mu_);
+      queued = st_.queued > 0 && active_.load();
+    }
+    if (inbox_.empty() && !busy_ && !queued) return;
+    lk.unlock();
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+    lk.lock();
+  }
+}
+
+// ------------------------------------------------------------------ lane thread
+void Lane::publish(std::vector<Fwd>&& fwd, std::vector<Handoff>&& hand) {
+  if (fwd.empty() && hand.empty()) return;
+  bool sig = false;
+  {
+    std::lock_guard<std::mutex> g(out_mu_);
+    if (out_fwd_.empty()) out_fwd_.swap(fwd);
+    else
+      for (auto& f : fwd) out_fwd_.push_back(std::move(f));
+    if (out_hand_.empty()) out_hand_.swap(hand);
+    else
+      for (auto& h : hand) out_hand_.push_back(std::move(h));
+    if (!signalled_) signalled_ = sig = true;
+  }
+  if (sig) {
+    const uint64_t one = 1;
+    ssize_t w = ::write(efd_, &one, sizeof one);
+    (void)w;
+  }
+}
+
+void Lane::forward(char type, std::shared_ptr<yk::PodEv> ev, std::shared_ptr<yk::PodEv> old, std::vector<Fwd>* out) {
+  out->push_back(Fwd{type, std::move(ev), std::move(old)});
+  std::lock_guard<std::mutex> g(stat_mu_);
+  st_.forwarded++;
+}
+
+int64_t Lane::prio_of(const yk::PodProj& p) const {
+  if (o_.sort_kind == 1) return p.priority;
+  for (const auto& kv : p.labels)
+    if (kv.first == "scv/priority") return atoi_or_zero(kv.second);
+  return 0;
+}
+
+bool Lane::admissible(const yk::PodProj& p, int* prof) const {
+  if (!p.ok || !p.node.empty() || p.deleting || terminal(p)) return false;
+  for (size_t i = 0; i < lp_.size(); ++i) {
+    if (lp_[i].name != p.sched) continue;
+    if (!lp_[i].enabled || (p.flags & lp_[i].flag_mask)) return false;
+    *prof = (int)i;
+    return true;
+  }
+  return false;
+}
+
+namespace {
+// a pod the Python side does not need to see: unassigned, of a scheduler no profile serves
+bool uninteresting(const yk::PodProj& p, const std::vector<Lane::Profile>& lp) {
+  if (!p.node.empty()) return false;
+  for (const auto& x : lp)
+    if (x.name == p.sched) return false;
+  return true;
+}
+}  // namespace
+
+// store mutations: lane thread, store_mu_ held by the caller
+void Lane::handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::vector<Fwd>* out) {
+  const yk::PodProj& p = ev->p;
+  const std::string key = key_of(p);
+  auto it = by_key_.find(key);
+  if (it != by_key_.end() && it->second->ev->p.uid != p.uid && type != 'D') {
+    // the key now names another pod (deleted + recreated while we were not watching)
+    handle_event('D', it->second->ev, out);
+    it = by_key_.end();
+  }
+  if (type == 'D') {
+    if (it == by_key_.end()) return;
+    Entry* e = it->second.get();
+    if (e->st == PY) {
+      if (!uninteresting(e->ev->p, lp_)) forward('D', ev, e->ev, out);
+    } else {
+      const bool held = e->st == BINDING || e->st == BOUND;
+      drop_owned(e, held);
+      if (held) {
+        std::lock_guard<std::mutex> g(stat_mu_);
+        st_.released++;
+        out_moves_pending_++;
+      }
+    }
+    by_key_.erase(it);
+    return;
+  }
+  if (it == by_key_.end()) {
+    auto e = std::make_unique<Entry>();
+    e->ev = ev;
+    int prof = -1;
+    if (active_admission_ && admissible(p, &prof)) {
+      e->st = QUEUED;
+      e->id = next_id_++;
+      e->prof = prof;
+      e->prio = prio_of(p);
+      e->seq = ++seq_;
+      e->t_enq = mono();
+      by_id_[e->id] = e.get();
+      heap_.push(QItem{e->prio, e->seq, e->id});
+      count(QUEUED, +1);
+      std::lock_guard<std::mutex> g(stat_mu_);
+      st_.admitted++;
+    } else if (!uninteresting(p, lp_)) {
+      forward('A', ev, nullptr, out);
+    }
+    by_key_.emplace(key, std::move(e));
+    return;
+  }
+  Entry* e = it->second.get();
+  std::shared_ptr<yk::PodEv> old = e->ev;
+  if (e->st == PY) {
+    e->ev = ev;
+    if (!uninteresting(p, lp_)) forward(uninteresting(old->p, lp_) ? 'A' : 'M', ev, old, out);
+    return;
+  }
+  // lane-owned
+  if (p.node.empty()) {
+    if (e->st == QUEUED && p.spec_meta_hash != old->p.spec_meta_hash) {
+      int prof = -1;
+      if (!admissible(p, &prof)) {
+        // no longer for the lane (a feature a Python plugin handles, another scheduler, ...)
+        drop_owned(e, false);
+        e->ev = ev;
+        if (!uninteresting(p, lp_)) forward('A', ev, nullptr, out);
+        return;
+      }
+      e->prof = prof;
+      const int64_t pr = prio_of(p);
+      if (pr != e->prio) {                 // re-sorted, FIFO position kept (activeQ.Update)
+        e->prio = pr;
+        heap_.push(QItem{e->prio, e->seq, e->id});
+      }
+    }
+    e->ev = ev;                            // assumed pods: status noise only (skipPodUpdate)
+    return;
+  }
+  // the pod is bound
+  if (terminal(p)) {
+    const bool held = e->st == BINDING || e->st == BOUND;
+    drop_owned(e, held);
+    e->ev = ev;
+    if (held) {
+      std::lock_guard<std::mutex> g(stat_mu_);
+      st_.released++;
+      out_moves_pending_++;
+    }
+    return;                                // stays in the store as a Python-visible terminal pod
+  }
+  if ((e->st == BINDING || e->st == BOUND) && p.node == e->node_name) {
+    e->ev = ev;
+    if (!e->confirmed) {
+      e->confirmed = true;
+      set_state(e, BOUND);
+      std::lock_guard<std::mutex> g(stat_mu_);
+      st_.confirmed++;
+      if (pod_lat_.size() < o_.e2e_keep) pod_lat_.push_back((float)(mono() - e->t_enq));
+    }
+    return;
+  }
+  // bound elsewhere (another scheduler, a user): our reservation (if any) goes, Python tracks it
+  drop_owned(e, e->st == BINDING || e->st == BOUND);
+  e->ev = ev;
+  forward('M', ev, old, out);
+}
+
+void Lane::count(St s, int d) {
+  std::lock_guard<std::mutex> g(stat_mu_);
+  if (s == QUEUED) st_.queued += d;
+  else if (s == INFLIGHT) st_.inflight += d;
+  if (s != PY) st_.owned += d;
+}
+
+void Lane::bind_settled(Entry* e) {
+  if (!e->bind_out) return;
+  e->bind_out = false;
+  std::lock_guard<std::mutex> g(stat_mu_);
+  st_.binding--;
+}
+
+void Lane::set_state(Entry* e, St s) {
+  if (e->st == s) return;
+  count(e->st, -1);
+  e->st = s;
+  count(s, +1);
+}
+
+// a lane-owned entry becomes a Python (store-only) entry; `release` drops its reservation
+void Lane::drop_owned(Entry* e, bool release) {
+  bind_settled(e);
+  if (release && e->id) {
+    to_release_.push_back(e->id);
+    log_remove(e->id);
+  }
+  if (e->id) by_id_.erase(e->id);
+  set_state(e, PY);
+  e->id = 0;
+  e->confirmed = e->acked = false;
+  e->node = -1;
+  e->node_name.clear();
+}
+
+void Lane::handle_answer(uint64_t tag, int status, std::string& body) {
+  if (tag & kEventTag) {
+    std::lock_guard<std::mutex> g(stat_mu_);
+    if (status >= 200 && status < 300) st_.events_written++;
+    else st_.event_errors++;
+    return;
+  }
+  auto it = by_id_.find(tag);
+  if (it == by_id_.end()) return;            // deleted meanwhile: its reservation is gone already
+  Entry* e = it->second;
+  if (e->st != BINDING && e->st != BOUND) return;
+  const double now = mono();
+  bind_settled(e);
+  if (status >= 200 && status < 300) {
+    e->acked = true;
+    set_state(e, BOUND);
+    {
+      std::lock_guard<std::mutex> g(stat_mu_);
+      st_.scheduled++;
+      if (e2e_.size() < o_.e2e_keep) e2e_.push_back((float)(now - e->t_cycle));
+    }
+    scheduled_.fetch_add(1, std::memory_order_relaxed);
+    record_scheduled(*e);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> g(stat_mu_);
+    st_.bind_errors++;
+  }
+  if (e->confirmed) {
+    // the Binding was applied (its echo confirmed the pod), only the answer was lost: the
+    // pod is bound — keep it (upstream ForgetPod refuses pods that are no longer assumed)
+    {
+      std::lock_guard<std::mutex> g(stat_mu_);
+      st_.scheduled++;
+      st_.lost_answers_kept++;
+    }
+    scheduled_.fetch_add(1, std::memory_order_relaxed);
+    return;
+  }
+  Handoff h;
+  h.kind = Handoff::kBindError;
+  h.ev = e->ev;
+  h.profile = e->prof >= 0 && e->prof < (int)lp_.size() ? lp_[e->prof].name : std::string();
+  h.status = status;
+  h.msg = std::move(body);
+  h.t_enqueue = e->t_enq;
+  h.t_cycle = e->t_cycle;
+  drop_owned(e, true);
+  hand_pending_.push_back(std::move(h));
+}
+
+void Lane::handle_relist(const std::vector<std::shared_ptr<yk::PodEv>>& items, std::vector<Fwd>* out) {
+  std::unordered_map<std::string, const std::shared_ptr<yk::PodEv>*> fresh;
+  fresh.reserve(items.size());
+  for (const auto& ev : items) fresh[key_of(ev->p)] = &ev;
+  std::vector<std::shared_ptr<yk::PodEv>> gone;
+  for (auto& kv : by_key_)
+    if (!fresh.count(kv.first)) gone.push_back(kv.second->ev);
+  for (auto& ev : gone) handle_event('D', ev, out);
+  for (const auto& ev : items) {
+    auto it = by_key_.find(key_of(ev->p));
+    if (it == by_key_.end()) handle_event('A', ev, out);
+    else if (it->second->ev->p.rv != ev->p.rv) handle_event('M', ev, out);
+  }
+}
+
+void Lane::apply_profiles(std::vector<Fwd>* out) {
+  {
+    std::lock_guard<std::mutex> g(prof_mu_);
+    lp_ = profiles_;
+  }
+  active_admission_ = false;
+  for (const auto& p : lp_) active_admission_ |= p.enabled;
+  // queued pods a profile no longer hands to the lane go to the Python queue
+  std::vector<Entry*> evict;
+  for (auto& kv : by_id_) {
+    Entry* e = kv.second;
+    if (e->st != QUEUED) continue;
+    int prof = -1;
+    if (!admissible(e->ev->p, &prof)) evict.push_back(e);
+    else e->prof = prof;
+  }
+  for (Entry* e : evict) {
+    drop_owned(e, false);
+    if (!uninteresting(e->ev->p, lp_)) forward('A', e->ev, nullptr, out);
+  }
+}
+
+bool Lane::make_req(const yk::PodProj& p, PodReq* r) {
+  const std::string *n = nullptr, *m = nullptr, *c = nullptr, *pr = nullptr, *cm = nullptr;
+  for (const auto& kv : p.labels) {
+    const std::string& k = kv.first;
+    if (k.size() < 5 || k[0] != 's' || k[1] != 'c' || k[2] != 'v') continue;
+    if (k == "scv/number") n = &kv.second;
+    else if (k == "scv/memory") m = &kv.second;
+    else if (k == "scv/clock") c = &kv.second;
+    else if (k == "scv/priority") pr = &kv.second;
+    else if (k == "scv.amd.com/clock-min") cm = &kv.second;
+  }
+  // models/labels.py::parse_gpu_request + ops/native.py::pod_req (Engine.make_req)
+  r->has_number = n != nullptr;
+  r->number = n ? str_to_uint(*n) : 1;
+  r->has_memory = m != nullptr;
+  r->memory = m ? str_to_uint(*m) : 0;
+  r->has_clock = c != nullptr;
+  r->clock = c ? str_to_uint(*c) : 0;
+  r->clock_min = cm ? str_to_uint(*cm) : 0;
+  r->priority = pr ? atoi_or_zero(*pr) : 0;
+  r->node_name = p.node.empty() ? -1 : eng_->intern(p.node);
+  r->cpu_m = p.cpu;
+  r->mem = p.mem;
+  r->nz_cpu_m = p.nzc;
+  r->nz_mem = p.nzm;
+  for (const auto& kv : p.node_selector) r->node_selector.emplace_back(eng_->intern(kv.first), eng_->intern(kv.second));
+  auto term = [&](const yk::TermP& t, SelTerm* out) {
+    for (const auto& q : t) {
+      SelReq x;
+      x.key = eng_->intern(q.key);
+      if (!selop_of(q.op, &x.op)) return false;
+      x.num = 0;
+      for (const auto& v : q.values) {
+        x.values.push_back(eng_->intern(v));
+        if (x.op == kGt || x.op == kLt) {
+          int64_t num;
+          if (!go_atoi(v, &num)) return false;   // Python's stoll would raise: its path decides
+          x.num = num;
+        }
+      }
+      out->reqs.push_back(std::move(x));
+    }
+    return true;
+  };
+  for (const auto& t : p.req_terms) {
+    SelTerm st;
+    if (!term(t, &st)) return false;
+    r->required_terms.push_back(std::move(st));
+  }
+  for (const auto& wt : p.pref_terms) {
+    PrefTerm pt;
+    pt.weight = (int32_t)wt.first;
+    if (!term(wt.second, &pt.term)) return false;
+    r->preferred_terms.push_back(std::move(pt));
+  }
+  for (const auto& t : p.tolerations) {
+    Toleration x;
+    x.key = t.has_key ? eng_->intern(t.key) : -1;
+    if (x.key == 0) x.key = -1;
+    x.value = eng_->intern(t.value);
+    x.op = t.op == "Exists" ? kTolExists : kTolEqual;
+    x.effect = effect_of(t.effect);
+    r->tolerations.push_back(x);
+  }
+  return true;
+}
+
+void Lane::annotations(const Profile& pr, const Entry& e, const PodReq& req, const CycleResult& r,
+                       std::vector<yk::KV>* out) {
+  // plugins/defaults.py::bind_annotations
+  if (!pr.annotate) return;
+  std::string gpus, vis, uu;
+  size_t nu = 0;
+  {
+    std::lock_guard<std::mutex> g(vis_mu_);
+    auto it = vis_.find(e.node_name);
+    const std::vector<std::pair<std::string, std::string>>* per = it == vis_.end() ? nullptr : &it->second;
+    for (size_t i = 0; i < r.cards.size(); ++i) {
+      const int32_t c = r.cards[i];
+      if (i) {
+        gpus.push_back(',');
+        vis.push_back(',');
+      }
+      gpus += std::to_string(c);
+      if (per && c >= 0 && c < (int32_t)per->size()) {
+        vis += (*per)[c].first;
+        if (!(*per)[c].second.empty()) {
+          if (nu) uu.push_back(',');
+          uu += (*per)[c].second;
+          ++nu;
+        }
+      } else {
+        vis += std::to_string(c);
+      }
+    }
+  }
+  out->emplace_back("scv.amd.com/gpus", std::move(gpus));
+  out->emplace_back("scv.amd.com/visible-devices", std::move(vis));
+  if (nu && nu == r.cards.size()) out->emplace_back("scv.amd.com/gpu-uuids", std::move(uu));
+  if (req.has_memory) out->emplace_back("scv.amd.com/reserved-mb", std::to_string(req.memory));
+}
+
+void Lane::schedule_some() {
+  if (!active_.load() || heap_.empty()) return;
+  yk::PodPort* port = port_.load();
+  if (!port) return;
+  std::vector<Entry*> run;
+  {
+    std::lock_guard<std::mutex> g(store_mu_);
+    while (!heap_.empty() && (int)run.size() < o_.batch) {
+      const QItem q = heap_.top();
+      heap_.pop();
+      auto it = by_id_.find(q.id);
+      if (it == by_id_.end()) continue;
+      Entry* e = it->second;
+      if (e->st != QUEUED || e->seq != q.seq || e->prio != q.prio) continue;   // stale heap item
+      set_state(e, INFLIGHT);
+      run.push_back(e);
+    }
+  }
+  if (run.empty()) return;
+  const double t0 = mono();
+  std::vector<yk::BindSpec> binds;
+  std::vector<uint64_t> tags;
+  std::vector<Fwd> fwd;
+  binds.reserve(run.size());
+  tags.reserve(run.size());
+  // consecutive pods of one profile share an engine batch (profiles differ in engine config)
+  size_t i = 0;
+  while (i < run.size()) {
+    size_t j = i;
+    const int prof = run[i]->prof;
+    while (j < run.size() && run[j]->prof == prof) ++j;
+    const Profile& pr = lp_[prof];
+    const size_t n = j - i;
+    std::vector<PodReq> reqs(n);
+    std::vector<char> ok(n, 1);
+    std::vector<uint64_t> ids;
+    std::vector<const PodReq*> rp;
+    std::vector<size_t> slot;
+    std::vector<CycleResult> res;
+    std::vector<std::string> names;
+    {
+      std::unique_lock<std::recursive_mutex> lk(*emu_);
+      for (size_t k = 0; k < n; ++k) {
+        try {
+          ok[k] = make_req(run[i + k]->ev->p, &reqs[k]);
+        } catch (const std::exception&) {
+          ok[k] = 0;
+        }
+        if (!ok[k]) continue;
+        ids.push_back(run[i + k]->id);
+        rp.push_back(&reqs[k]);
+        slot.push_back(k);
+      }
+      const EngineConfig saved = eng_->config();
+      eng_->set_config(pr.cfg);
+      try {
+        res = eng_->schedule_batch(ids, rp);
+      } catch (const std::exception&) {
+        res.clear();
+      }
+      // restore the caller's configuration unless it re-configured the engine while a
+      // device batch had the lock dropped (then its newer configuration stays)
+      if (config_eq(eng_->config(), pr.cfg)) eng_->set_config(saved);
+      names.resize(res.size());
+      for (size_t k = 0; k < res.size(); ++k)
+        if (res[k].node >= 0) names[k] = eng_->node(res[k].node).name;
+    }
+    {
+      std::lock_guard<std::mutex> g(store_mu_);
+      for (size_t k = 0; k < n; ++k)
+        if (!ok[k]) {                     // a pod the projection cannot express natively
+          Entry* e = run[i + k];
+          drop_owned(e, false);
+          forward('A', e->ev, nullptr, &fwd);
+        }
+      if (res.size() != ids.size()) {     // engine failure: the pods retry from the lane queue
+        for (size_t k = 0; k < ids.size(); ++k) {
+          Entry* e = run[i + slot[k]];
+          to_release_.push_back(e->id);
+          set_state(e, QUEUED);
+          e->seq = ++seq_;
+          heap_.push(QItem{e->prio, e->seq, e->id});
+        }
+      } else {
+        for (size_t k = 0; k < res.size(); ++k) {
+          Entry* e = run[i + slot[k]];
+          const CycleResult& r = res[k];
+          e->t_cycle = t0;
+          if (r.stale) {
+            {
+              std::lock_guard<std::mutex> g2(stat_mu_);
+              st_.stale_retries++;
+            }
+            set_state(e, QUEUED);
+            e->seq = ++seq_;
+            heap_.push(QItem{e->prio, e->seq, e->id});
+            continue;
+          }
+          if (r.node < 0) {
+            Handoff h;
+            h.kind = Handoff::kUnschedulable;
+            h.ev = e->ev;
+            h.profile = pr.name;
+            h.res = r;
+            h.t_enqueue = e->t_enq;
+            h.t_cycle = t0;
+            drop_owned(e, false);
+            hand_pending_.push_back(std::move(h));
+            std::lock_guard<std::mutex> g2(stat_mu_);
+            st_.unschedulable++;
+            continue;
+          }
+          e->node = r.node;
+          e->node_name = names[k];
+          e->cards = r.cards;
+          set_state(e, BINDING);
+          log_add(*e);
+          yk::BindSpec b;
+          b.ns = e->ev->p.ns;
+          b.name = e->ev->p.name;
+          b.uid = e->ev->p.uid;
+          b.node = e->node_name;
+          annotations(pr, *e, reqs[slot[k]], r, &b.annotations);
+          binds.push_back(std::move(b));
+          tags.push_back(e->id);
+          e->bind_out = true;
+          std::lock_guard<std::mutex> g2(stat_mu_);
+          st_.binding++;
+        }
+      }
+    }
+    i = j;
+  }
+  if (!binds.empty()) port->bind_native(std::move(binds), tags, o_.bind_timeout_s, this);
+  {
+    std::lock_guard<std::mutex> g(stat_mu_);
+    st_.batches++;
+  }
+  if (!fwd.empty()) publish(std::move(fwd), {});
+}
+
+void Lane::log_add(const Entry& e) {
+  std::lock_guard<std::mutex> g(log_mu_);
+  if (!log_on_ || log_full_) return;
+  log_.push_back(Change{e.id, true, e.ev, e.node_name, e.cards});
+  if (log_.size() > (1u << 20)) {              // Python stopped asking: resync from scratch
+    log_.clear();
+    log_full_ = true;
+  }
+}
+
+void Lane::log_remove(uint64_t id) {
+  std::lock_guard<std::mutex> g(log_mu_);
+  if (!log_on_ || log_full_) return;
+  log_.push_back(Change{id, false, nullptr, std::string(), {}});
+  if (log_.size() > (1u << 20)) {
+    log_.clear();
+    log_full_ = true;
+  }
+}
+
+std::vector<Lane::Change> Lane::changes(bool* full) {
+  std::vector<Change> out;
+  {
+    std::lock_guard<std::mutex> g(log_mu_);
+    if (log_on_ && !log_full_) {
+      out.swap(log_);
+      *full = false;
+      return out;
+    }
+    log_on_ = true;
+    log_full_ = false;
+    log_.clear();
+  }
+  // full snapshot; the log (now on) records everything after it
+  std::lock_guard<std::mutex> g(store_mu_);
+  std::lock_guard<std::mutex> g2(log_mu_);
+  log_.clear();
+  for (auto& kv : by_id_) {
+    const Entry* e = kv.second;
+    if (e->st == BINDING || e->st == BOUND) out.push_back(Change{e->id, true, e->ev, e->node_name, e->cards});
+  }
+  *full = true;
+  return out;
+}
+
+void Lane::pause(bool on) {
+  std::unique_lock<std::mutex> lk(in_mu_);
+  paused_ = on;
+  in_cv_.notify_all();
+  if (on) idle_cv_.wait(lk, [&] { return !busy_ || stop_.load(); });
+}
+
+void Lane::record_scheduled(const Entry& e) {
+  if (!o_.events) return;
+  std::lock_guard<std::mutex> g(stat_mu_);
+  st_.events_recorded++;
+  if ((int)ev_q_.size() >= o_.event_buffer) {     // client-go DropIfChannelFull
+    st_.events_dropped++;
+    return;
+  }
+  const std::string& prof = e.prof >= 0 && e.prof < (int)lp_.size() ? lp_[e.prof].name : std::string();
+  ev_q_.push_back(PendingEvent{e.ev->p.ns, e.ev->p.name, e.ev->p.uid, e.node_name, prof, wall()});
+}
+
+void Lane::flush_events() {
+  if (ev_q_.empty()) return;
+  yk::PodPort* port = port_.load();
+  if (!port) return;
+  const double now = mono();
+  const double cap = o_.event_burst > 0 ? o_.event_burst : 1;
+  if (o_.event_qps > 0) ev_tokens_ = std::min(cap, ev_tokens_ + (now - ev_last_) * o_.event_qps);
+  else ev_tokens_ = cap;
+  ev_last_ = now;
+  while (!ev_q_.empty() && ev_tokens_ >= 1.0) {
+    ev_tokens_ -= 1.0;
+    PendingEvent pe = std::move(ev_q_.front());
+    ev_q_.pop_front();
+    const std::string ctl = pe.profile.empty() ? std::string("yoda-scheduler") : pe.profile;
+    char seq[24];
+    snprintf(seq, sizeof seq, "%08llx", (unsigned long long)++ev_seq_);
+    const std::string name = pe.name + "." + o_.name_prefix + seq;
+    const std::string note = "Successfully assigned " + pe.ns + "/" + pe.name + " to " + pe.node;
+    const std::string t = micro_time(pe.ts);
+    std::string b;
+    b.reserve(512);
+    std::string path;
+    if (o_.events_v1) {
+      // framework/events.py::EventRecorder._new_v1
+      b += "{\"apiVersion\":\"events.k8s.io/v1\",\"kind\":\"Event\",\"metadata\":{\"name\":";
+      json_str(name, b);
+      b += ",\"namespace\":";
+      json_str(pe.ns, b);
+      b += "},\"eventTime\":";
+      json_str(t, b);
+      b += ",\"reportingController\":";
+      json_str(ctl, b);
+      b += ",\"reportingInstance\":";
+      json_str(ctl + "-" + o_.host, b);
+      b += ",\"action\":\"Binding\",\"reason\":\"Scheduled\",\"regarding\":{\"apiVersion\":\"v1\",\"kind\":\"Pod\",\"name\":";
+      json_str(pe.name, b);
+      b += ",\"namespace\":";
+      json_str(pe.ns, b);
+      b += ",\"uid\":";
+      json_str(pe.uid, b);
+      b += "},\"note\":";
+      json_str(note, b);
+      b += ",\"type\":\"Normal\"}";
+      path = "/apis/events.k8s.io/v1/namespaces/" + pe.ns + "/events";
+    } else {
+      b += "{\"apiVersion\":\"v1\",\"kind\":\"Event\",\"metadata\":{\"name\":";
+      json_str(name, b);
+      b += ",\"namespace\":";
+      json_str(pe.ns, b);
+      b += "},\"involvedObject\":{\"kind\":\"Pod\",\"name\":";
+      json_str(pe.name, b);
+      b += ",\"namespace\":";
+      json_str(pe.ns, b);
+      b += ",\"uid\":";
+      json_str(pe.uid, b);
+      b += "},\"reason\":\"Scheduled\",\"message\":";
+      json_str(note, b);
+      b += ",\"type\":\"Normal\",\"source\":{\"component\":";
+      json_str(ctl, b);
+      b += "},\"firstTimestamp\":";
+      json_str(t, b);
+      b += ",\"lastTimestamp\":";
+      json_str(t, b);
+      b += ",\"count\":1}";
+      path = "/api/v1/namespaces/" + pe.ns + "/events";
+    }
+    port->request_native("POST", path, std::move(b), false, 30.0, kEventTag | ev_seq_, this);
+  }
+}
+
+void Lane::run() {
+  std::deque<Item> work;
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> lk(in_mu_);
+      auto ready = [&] {
+        return stop_.load() || (!paused_ && (!inbox_.empty() || (active_.load() && !heap_.empty())));
+      };
+      if (!ready()) {
+        if (!ev_q_.empty() && o_.event_qps > 0) {
+          const double wait = std::max(0.0005, (1.0 - ev_tokens_) / o_.event_qps);
+          in_cv_.wait_for(lk, std::chrono::duration<double>(wait), ready);
+        } else {
+          in_cv_.wait(lk, ready);
+        }
+      }
+      if (stop_.load()) break;
+      work.swap(inbox_);
+      busy_ = true;
+    }
+    std::vector<Fwd> fwd;
+    std::vector<std::pair<uint64_t, std::vector<Fwd>>> relists;
+    {
+      std::lock_guard<std::mutex> g(store_mu_);
+      for (auto& it : work) {
+        switch (it.k) {
+          case Item::kEvent: handle_event(it.type, it.ev, &fwd); break;
+          case Item::kAnswer: handle_answer(it.tag, it.status, it.body); break;
+          case Item::kProfiles: apply_profiles(&fwd); break;
+          case Item::kRelist: {
+            std::vector<Fwd> out;
+            handle_relist(*it.items, &out);
+            relists.emplace_back(it.token, std::move(out));
+            break;
+          }
+        }
+      }
+    }
+    work.clear();
+    if (!to_release_.empty()) {
+      std::lock_guard<std::recursive_mutex> lk(*emu_);
+      for (uint64_t id : to_release_) eng_->release(id);
+      to_release_.clear();
+    }
+    if (!fwd.empty() || !hand_pending_.empty()) publish(std::move(fwd), std::move(hand_pending_));
+    hand_pending_.clear();
+    if (out_moves_pending_) {
+      bool sig = false;
+      {
+        std::lock_guard<std::mutex> g(out_mu_);
+        out_moves_ += out_moves_pending_;
+        if (!signalled_) signalled_ = sig = true;
+      }
+      out_moves_pending_ = 0;
+      if (sig) {
+        const uint64_t one = 1;
+        ssize_t w = ::write(efd_, &one, sizeof one);
+        (void)w;
+      }
+    }
+    if (!relists.empty()) {
+      std::lock_guard<std::mutex> g(in_mu_);
+      for (auto& r : relists) {
+        relist_out_[r.first] = std::move(r.second);
+        relist_done_ = std::max(relist_done_, r.first);
+      }
+      relist_cv_.notify_all();
+    }
+    schedule_some();
+    if (!hand_pending_.empty()) {
+      publish({}, std::move(hand_pending_));
+      hand_pending_.clear();
+    }
+    if (!to_release_.empty()) {
+      std::lock_guard<std::recursive_mutex> lk(*emu_);
+      for (uint64_t id : to_release_) eng_->release(id);
+      to_release_.clear();
+    }
+    flush_events();
+    {
+      std::lock_guard<std::mutex> g(in_mu_);
+      busy_ = false;
+    }
+    idle_cv_.notify_all();
+  }
+  std::lock_guard<std::mutex> g(in_mu_);
+  busy_ = false;
+  idle_cv_.notify_all();
+}
+
+}  // namespace yoda

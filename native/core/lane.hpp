@@ -1,0 +1,263 @@
+// Native pod lane: the per-pod scheduling lifecycle in C++.
+//
+// What upstream kube-scheduler does in compiled Go for the reference plugin — informer →
+// activeQ → scheduleOne → assume → async bind → confirm on the watch echo → forget on
+// delete (the reference only supplies Filter/Score, /root/reference/pkg/yoda/scheduler.go:76-130)
+// — runs here for every pod of an all-native profile without a Python call per pod:
+//
+//   transport I/O thread ── every pod watch event ──► Lane inbox
+//   lane thread: store update → admission → priority queue → Engine::schedule_batch (assume)
+//                → Binding POSTs straight to the transport → answers / echo / delete
+//   Python event loop: only what the lane forwards — pods of other profiles or with features
+//                a Python plugin handles, unschedulable pods (FailedScheduling, backoff,
+//                preemption), bind failures — pulled in batches through an eventfd.
+//
+// The lane owns the pod store (key → latest projected event), so the Python informer keeps no
+// per-pod state for lane pods; a relist is diffed here too. Scheduling semantics match the
+// Python runner's all-native batch path (same engine call, same assume, same annotations);
+// the queue is the profile's QueueSort (scv/priority label or spec.priority) with a FIFO
+// tie-break. The Python queue and the lane queue are independent: a pod is in exactly one.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <queue>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "engine.hpp"
+#include "lane_port.hpp"
+
+namespace yoda {
+
+struct LaneOptions {
+  int batch = 256;                 // pods per engine batch
+  double bind_timeout_s = 30.0;
+  int sort_kind = 0;               // 0: scv/priority label (yoda QueueSort), 1: spec.priority (PrioritySort)
+  // Scheduled events (upstream EventRecorder semantics, native)
+  bool events = true;
+  bool events_v1 = true;           // events.k8s.io/v1 shape (else core/v1)
+  double event_qps = 50.0;
+  int event_burst = 300;
+  int event_buffer = 1000;         // pending events kept; a full buffer drops the incoming one
+  std::string host = "localhost";
+  std::string name_prefix = "00000000";
+  size_t e2e_keep = 1 << 20;       // raw e2e samples kept until Python takes them
+};
+
+struct LaneStats {
+  uint64_t admitted = 0, scheduled = 0, unschedulable = 0, bind_errors = 0, stale_retries = 0;
+  uint64_t forwarded = 0, released = 0, batches = 0, confirmed = 0, events_recorded = 0, events_dropped = 0;
+  uint64_t events_written = 0, event_errors = 0, lost_answers_kept = 0;
+  uint64_t queued = 0, inflight = 0, binding = 0, owned = 0;   // gauges
+};
+
+class Lane : public yk::PodSink {
+ public:
+  enum St : uint8_t { PY = 0, QUEUED, INFLIGHT, BINDING, BOUND };
+
+  struct Profile {
+    std::string name;
+    bool enabled = false;
+    int flag_mask = 0;       // a pod with any of these flags goes to Python
+    bool annotate = true;    // yoda filter in the profile: the Binding carries the GPU assignment
+    EngineConfig cfg;
+  };
+
+  // What the Python informer sees of a forwarded pod event: type 'A'/'M'/'D', the event,
+  // and the previous event of the key (nullptr for a new one).
+  struct Fwd {
+    char type;
+    std::shared_ptr<yk::PodEv> ev, old;
+  };
+  // A pod the lane gives up to the Python path.
+  struct Handoff {
+    enum Kind : int { kUnschedulable = 0, kBindError = 1 };
+    int kind = 0;
+    std::shared_ptr<yk::PodEv> ev;
+    std::string profile;
+    CycleResult res;         // kUnschedulable: the engine's cycle (reasons for FitError)
+    int status = 0;          // kBindError: HTTP status / -1 / -2
+    std::string msg;
+    double t_enqueue = 0;    // monotonic seconds, when the pod entered the lane queue
+    double t_cycle = 0;
+  };
+
+  Lane(Engine* e, std::recursive_mutex* engine_mu, LaneOptions o);
+  ~Lane() override;
+  Lane(const Lane&) = delete;
+  Lane& operator=(const Lane&) = delete;
+
+  // ---- configuration (Python thread)
+  void set_port(yk::PodPort* p) { port_.store(p); }
+  void set_profile(const Profile& p);          // replaces a profile of the same name
+  void set_active(bool on);                    // leader: schedule; otherwise only keep the store
+  void set_node_cards(const std::string& node, std::vector<std::pair<std::string, std::string>> vis);
+  void remove_node_cards(const std::string& node);
+  void close();
+
+  // ---- yk::PodSink (transport I/O thread)
+  void on_pod_events(uint64_t watch_id, std::vector<yk::WatchEvent>& evs) override;
+  void on_answer(uint64_t tag, int status, std::string&& body) override;
+
+  // ---- Python side
+  int fileno() const { return efd_; }
+  void drain(std::vector<Fwd>* fwd, std::vector<Handoff>* hand, uint64_t* moves);
+  // A relist's items (full state of the pod collection): diffed against the store on the
+  // lane thread; returns the events Python must see. Blocks until processed.
+  std::vector<Fwd> relist(std::vector<std::shared_ptr<yk::PodEv>> items);
+  std::shared_ptr<yk::PodEv> lookup(const std::string& key, bool* owned);
+  std::vector<std::string> keys();
+  size_t store_size();
+  LaneStats stats();
+  std::vector<float> take_e2e();
+  std::vector<float> take_pod_latency();
+  void wait_idle(double timeout_s);            // tests: inbox and queue drained
+  // Hold the lane thread between steps (a Python what-if on the ledger — preemption —
+  // must not interleave with lane releases); blocks until the thread is parked.
+  void pause(bool on);
+
+  // The lane pods holding a reservation, for the Python cache's view of the cluster (pod
+  // affinity / spread / preemption plugins). The first call returns the full set and turns
+  // on a change log; later calls return what changed since (add: id, event, node, cards;
+  // remove: id). `full` is set when the log overflowed and the set is complete again.
+  struct Change {
+    uint64_t id;
+    bool add;
+    std::shared_ptr<yk::PodEv> ev;
+    std::string node;
+    std::vector<int32_t> cards;
+  };
+  std::vector<Change> changes(bool* full);
+
+ private:
+  struct Entry {
+    std::shared_ptr<yk::PodEv> ev;
+    St st = PY;
+    uint64_t id = 0;         // engine ledger id while lane-owned
+    int prof = -1;
+    int64_t prio = 0;
+    uint64_t seq = 0;
+    double t_enq = 0, t_cycle = 0;
+    int32_t node = -1;
+    std::string node_name;
+    std::vector<int32_t> cards;
+    bool confirmed = false;  // the watch echo showed the pod bound to node_name
+    bool acked = false;      // the Binding POST was answered 2xx
+    bool bind_out = false;   // a Binding POST is in flight (no answer yet)
+  };
+  struct QItem {             // max-heap: higher priority first, then FIFO
+    int64_t prio;
+    uint64_t seq;
+    uint64_t id;             // entry id; an item whose entry moved on is skipped when popped
+    bool operator<(const QItem& o) const { return prio != o.prio ? prio < o.prio : seq > o.seq; }
+  };
+  struct Item {             // inbox: events, answers, commands — applied in order
+    enum K : uint8_t { kEvent, kAnswer, kRelist, kProfiles } k = kEvent;
+    char type = 0;
+    std::shared_ptr<yk::PodEv> ev;
+    uint64_t tag = 0;
+    int status = 0;
+    std::string body;
+    std::shared_ptr<std::vector<std::shared_ptr<yk::PodEv>>> items;
+    uint64_t token = 0;
+  };
+  struct PendingEvent {
+    std::string ns, name, uid, node, profile;
+    double ts;
+  };
+
+  void run();
+  void handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::vector<Fwd>* out);
+  void handle_answer(uint64_t tag, int status, std::string& body);
+  void handle_relist(const std::vector<std::shared_ptr<yk::PodEv>>& items, std::vector<Fwd>* out);
+  void drop_owned(Entry* e, bool release);
+  void apply_profiles(std::vector<Fwd>* out);
+  void count(St s, int d);
+  void set_state(Entry* e, St s);
+  void bind_settled(Entry* e);
+  void schedule_some();
+  bool admissible(const yk::PodProj& p, int* prof) const;
+  int64_t prio_of(const yk::PodProj& p) const;
+  bool make_req(const yk::PodProj& p, PodReq* r);
+  void annotations(const Profile& pr, const Entry& e, const PodReq& req, const CycleResult& r,
+                   std::vector<yk::KV>* out);
+  void record_scheduled(const Entry& e);
+  void flush_events();
+  void forward(char type, std::shared_ptr<yk::PodEv> ev, std::shared_ptr<yk::PodEv> old, std::vector<Fwd>* out);
+  void publish(std::vector<Fwd>&& fwd, std::vector<Handoff>&& hand);
+  static double mono();
+
+  Engine* eng_;
+  std::recursive_mutex* emu_;
+  LaneOptions o_;
+  std::atomic<yk::PodPort*> port_{nullptr};
+  int efd_ = -1;
+  std::thread th_;
+  std::atomic<bool> stop_{false};
+  std::atomic<bool> active_{false};
+
+  std::mutex in_mu_;
+  std::condition_variable in_cv_;
+  std::deque<Item> inbox_;
+  uint64_t relist_next_ = 0, relist_done_ = 0;
+  std::condition_variable relist_cv_;
+  std::unordered_map<uint64_t, std::vector<Fwd>> relist_out_;
+  bool busy_ = false;                // lane thread is processing (wait_idle)
+  bool paused_ = false;
+  std::condition_variable idle_cv_;
+
+  // change log of reserved lane pods (changes()); off until Python first asks
+  std::mutex log_mu_;
+  bool log_on_ = false, log_full_ = false;
+  std::vector<Change> log_;
+  void log_add(const Entry& e);
+  void log_remove(uint64_t id);
+
+  std::mutex prof_mu_;
+  std::vector<Profile> profiles_;    // copied into lane-thread state on kProfiles
+  std::vector<Profile> lp_;          // lane thread's view
+
+  std::mutex vis_mu_;
+  std::unordered_map<std::string, std::vector<std::pair<std::string, std::string>>> vis_;
+
+  // store: written by the lane thread, read by Python (lookup / keys)
+  std::mutex store_mu_;
+  std::unordered_map<std::string, std::unique_ptr<Entry>> by_key_;
+  std::unordered_map<uint64_t, Entry*> by_id_;       // lane-owned entries
+  std::priority_queue<QItem> heap_;
+  // ledger ids of lane pods: a range disjoint from the Python side's (models/pod.py::pod_num_id)
+  uint64_t seq_ = 0, next_id_ = (1ull << 62);
+  bool active_admission_ = false;                    // some profile hands pods to the lane
+
+  // lane-thread scratch, flushed once per loop turn
+  std::vector<uint64_t> to_release_;                 // engine ledger releases (one lock per turn)
+  std::vector<Handoff> hand_pending_;
+  uint64_t out_moves_pending_ = 0;
+ public:
+  std::atomic<uint64_t> scheduled_{0};               // Bindings acknowledged (incl. lost answers kept)
+ private:
+
+  std::mutex out_mu_;
+  std::vector<Fwd> out_fwd_;
+  std::vector<Handoff> out_hand_;
+  uint64_t out_moves_ = 0;
+  bool signalled_ = false;
+
+  std::mutex stat_mu_;
+  LaneStats st_;
+  std::vector<float> e2e_, pod_lat_;
+
+  // native event recorder (lane thread)
+  std::deque<PendingEvent> ev_q_;
+  double ev_tokens_ = 0, ev_last_ = 0;
+  uint64_t ev_seq_ = 0;
+};
+
+}  // namespace yoda

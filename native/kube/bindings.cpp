@@ -205,6 +205,12 @@ PYBIND11_MODULE(_yoda_kube, m) {
       .def("cancel", &Transport::cancel)
       .def("set_token", &Transport::set_token)
       .def("set_rate", &Transport::set_rate, py::arg("qps"), py::arg("burst"))
+      // native pod lane seam (lane_port.hpp): raw pointers, handed to _yoda_core's Lane
+      .def("port_ptr", [](Transport& t) { return (uintptr_t) static_cast<PodPort*>(&t); })
+      .def("set_pod_sink", [](Transport& t, uintptr_t sink) {
+             py::gil_scoped_release rel;
+             t.set_pod_sink(reinterpret_cast<PodSink*>(sink));
+           }, py::arg("sink"), "attach (pointer from Lane.sink_ptr()) or detach (0) the pod event sink")
       .def("close", [](Transport& t) {
         py::gil_scoped_release rel;
         t.close();

@@ -1,0 +1,63 @@
+// The seam between the native transport (module _yoda_kube) and the native pod lane (module
+// _yoda_core). Header-only abstract interfaces: each side calls the other through a vtable,
+// so neither module links the other's code, and Python only hands raw pointers across
+// (Transport.port_ptr() → Lane, Lane.sink_ptr() → Transport.set_pod_sink()).
+//
+//   transport I/O thread ──on_pod_events──► lane (takes every pod watch event)
+//   lane thread ──bind_native / request_native──► transport (Bindings, Scheduled events)
+//   transport I/O thread ──on_answer──► lane (the apiserver's answers, by tag)
+//
+// Both callbacks run on the transport's I/O thread with the transport's sink lock held;
+// they must only enqueue (never block, never call back into the transport).
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "project.hpp"
+
+namespace yk {
+
+struct PodEv {
+  PodProj p;
+  std::string raw;             // the pod object's JSON text
+};
+
+struct WatchEvent {
+  char type = 0;               // 'A' ADDED, 'M' MODIFIED, 'D' DELETED, 'B' BOOKMARK, 'E' ERROR
+  std::string rv;
+  std::string raw;             // object JSON (non-pod watches; ERROR status for pods too)
+  std::shared_ptr<PodEv> pod;  // pod watches
+};
+
+struct BindSpec {
+  std::string ns, name, uid, node;
+  std::vector<KV> annotations;
+};
+
+class PodSink {
+ public:
+  virtual ~PodSink() = default;
+  // A decoded batch of a pod watch. The sink moves the pod events it wants out of `evs`
+  // (erasing them); what is left (bookmarks, errors, and any pod event it declines) goes
+  // to the Python informer as before, in order.
+  virtual void on_pod_events(uint64_t watch_id, std::vector<WatchEvent>& evs) = 0;
+  // The answer to a request submitted through PodPort with this sink: HTTP status, or -1
+  // (connection failed / closed) / -2 (timed out) with a reason in `body`.
+  virtual void on_answer(uint64_t tag, int status, std::string&& body) = 0;
+};
+
+class PodPort {
+ public:
+  virtual ~PodPort() = default;
+  // Binding POSTs (client rate limit applies), answered through sink->on_answer(tags[k]).
+  virtual void bind_native(std::vector<BindSpec>&& binds, const std::vector<uint64_t>& tags, double timeout_s,
+                           PodSink* sink) = 0;
+  // Any other request (events); answered through sink->on_answer(tag).
+  virtual void request_native(const std::string& method, const std::string& path, std::string&& body,
+                              bool limited, double timeout_s, uint64_t tag, PodSink* sink) = 0;
+};
+
+}  // namespace yk

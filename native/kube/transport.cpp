@@ -64,6 +64,8 @@ struct Transport::Req {
   bool limited = false;
   bool watch = false;
   bool pods = false;
+  PodSink* sink = nullptr;  // native lane request: answered through sink->on_answer(tag)
+  uint64_t tag = 0;
   bool expired = false;     // completed by timeout; the late response is dropped
   double deadline = 0.0;
   double idle_timeout = 0.0;  // watch: close when nothing arrived for this long (0 = never)
@@ -272,6 +274,84 @@ uint64_t Transport::bind_many(const std::vector<BindSpec>& binds, double timeout
   return first;
 }
 
+void Transport::bind_native(std::vector<BindSpec>&& binds, const std::vector<uint64_t>& tags, double timeout_s,
+                            PodSink* sink) {
+  if (binds.empty()) return;
+  const double deadline = timeout_s > 0 ? now_s() + timeout_s : 0.0;
+  std::vector<std::unique_ptr<Req>> rs;
+  rs.reserve(binds.size());
+  for (size_t k = 0; k < binds.size(); ++k) {
+    const BindSpec& s = binds[k];
+    std::string b = bind_body(s.ns, s.name, s.uid, s.node, s.annotations);
+    auto r = std::make_unique<Req>();
+    r->id = next_id_++;
+    r->wire = head("POST", "/api/v1/namespaces/" + url_encode(s.ns) + "/pods/" + url_encode(s.name) + "/binding",
+                   b.size(), "application/json");
+    r->wire.append(b);
+    r->limited = true;
+    r->deadline = deadline;
+    r->sink = sink;
+    r->tag = k < tags.size() ? tags[k] : 0;
+    rs.push_back(std::move(r));
+  }
+  bool was_empty;
+  {
+    std::lock_guard<std::mutex> g(in_mu_);
+    was_empty = incoming_.empty() && cancels_.empty();
+    for (auto& r : rs) incoming_.push_back(std::move(r));
+  }
+  if (was_empty) efd_signal(wake_efd_);
+}
+
+void Transport::request_native(const std::string& method, const std::string& path, std::string&& body,
+                               bool limited, double timeout_s, uint64_t tag, PodSink* sink) {
+  auto r = std::make_unique<Req>();
+  r->id = next_id_++;
+  r->wire = head(method, path, body.size(), "application/json");
+  r->wire.append(body);
+  r->limited = limited;
+  r->deadline = timeout_s > 0 ? now_s() + timeout_s : 0.0;
+  r->sink = sink;
+  r->tag = tag;
+  submit(std::move(r));
+}
+
+void Transport::set_pod_sink(PodSink* sink) {
+  std::lock_guard<std::mutex> g(sink_mu_);
+  pod_sink_ = sink;
+}
+
+void Transport::answer(Req& r, int status, std::string&& body) {
+  if (r.sink) {
+    std::lock_guard<std::mutex> g(sink_mu_);
+    if (r.sink == pod_sink_) r.sink->on_answer(r.tag, status, std::move(body));
+    return;
+  }
+  Completion e;
+  e.kind = Completion::kResponse;
+  e.id = r.id;
+  e.status = status;
+  e.body = std::move(body);
+  complete(std::move(e));
+}
+
+void Transport::offer_pod_events(Conn* c) {
+  if (!c->pods || c->evs.empty()) return;
+  std::lock_guard<std::mutex> g(sink_mu_);
+  if (!pod_sink_) return;
+  // the Python reflector resumes from the last resourceVersion it saw: if the sink takes the
+  // batch's last event, leave a bookmark with that version in its place
+  std::string last_rv = c->evs.back().rv;
+  const size_t n = c->evs.size();
+  pod_sink_->on_pod_events(c->watch_id, c->evs);
+  if (c->evs.size() != n && !last_rv.empty() && (c->evs.empty() || c->evs.back().rv != last_rv)) {
+    WatchEvent b;
+    b.type = 'B';
+    b.rv = std::move(last_rv);
+    c->evs.push_back(std::move(b));
+  }
+}
+
 uint64_t Transport::watch(const std::string& path, bool pods, double idle_timeout_s) {
   auto r = std::make_unique<Req>();
   r->id = next_id_++;
@@ -392,6 +472,7 @@ void Transport::close_conn(Conn* c, int status, const std::string& why) {
   c->fd = -1;
   if (c->watch) {
     if (!c->watch_cancelled) {
+      offer_pod_events(c);
       if (!c->evs.empty()) {
         Completion ce;
         ce.kind = Completion::kEvents;
@@ -411,12 +492,7 @@ void Transport::close_conn(Conn* c, int status, const std::string& why) {
   uint64_t failed = 0;
   for (auto& r : c->inflight) {
     if (r->expired) continue;
-    Completion e;
-    e.kind = Completion::kResponse;
-    e.id = r->id;
-    e.status = status;
-    e.body = why;
-    complete(std::move(e));
+    answer(*r, status, std::string(why));
     failed++;
   }
   c->inflight.clear();
@@ -602,14 +678,7 @@ void Transport::on_message_done(Conn* c) {
   }
   std::unique_ptr<Req> r = std::move(c->inflight.front());
   c->inflight.pop_front();
-  if (!r->expired) {
-    Completion e;
-    e.kind = Completion::kResponse;
-    e.id = r->id;
-    e.status = c->rp.status;
-    e.body.swap(c->body);
-    complete(std::move(e));
-  }
+  if (!r->expired) answer(*r, c->rp.status, std::move(c->body));
   c->body.clear();
   {
     std::lock_guard<std::mutex> g(stats_mu_);
@@ -668,6 +737,7 @@ void Transport::do_read(Conn* c) {
         on_message_done(c);
       }
     }
+    if (c->watch && !c->evs.empty() && c->st == Conn::kOpen) offer_pod_events(c);
     if (c->watch && !c->evs.empty() && c->st == Conn::kOpen) {
       Completion ce;
       ce.kind = Completion::kEvents;
@@ -777,12 +847,7 @@ void Transport::dispatch() {
 void Transport::check_timeouts(double now) {
   uint64_t n = 0;
   auto expire = [&](Req& r) {
-    Completion e;
-    e.kind = Completion::kResponse;
-    e.id = r.id;
-    e.status = -2;
-    e.body = "request timed out";
-    complete(std::move(e));
+    answer(r, -2, std::string("request timed out"));
     r.expired = true;
     n++;
   };
@@ -900,14 +965,7 @@ void Transport::run() {
   }
   // fail everything still pending
   for (auto* q : {&throttled_, &ready_}) {
-    for (auto& r : *q) {
-      Completion e;
-      e.kind = Completion::kResponse;
-      e.id = r->id;
-      e.status = -1;
-      e.body = "transport closed";
-      complete(std::move(e));
-    }
+    for (auto& r : *q) answer(*r, -1, std::string("transport closed"));
     q->clear();
   }
   for (auto& c : pool_) close_conn(c.get(), -1, "transport closed");

@@ -25,6 +25,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "lane_port.hpp"
 #include "project.hpp"
 
 struct ssl_ctx_st;
@@ -46,18 +47,6 @@ struct ClientConfig {
   std::string user_agent = "yoda-scheduler/0.2 (MI355X)";
 };
 
-struct PodEv {
-  PodProj p;
-  std::string raw;             // the pod object's JSON text
-};
-
-struct WatchEvent {
-  char type = 0;               // 'A' ADDED, 'M' MODIFIED, 'D' DELETED, 'B' BOOKMARK, 'E' ERROR
-  std::string rv;
-  std::string raw;             // object JSON (non-pod watches; ERROR status for pods too)
-  std::shared_ptr<PodEv> pod;  // pod watches
-};
-
 struct Completion {
   enum Kind : uint8_t { kResponse = 0, kEvents = 1, kWatchEnd = 2 };
   Kind kind = kResponse;
@@ -73,7 +62,7 @@ struct TransportStats {
   uint64_t throttled = 0;
 };
 
-class Transport {
+class Transport : public PodPort {
  public:
   explicit Transport(ClientConfig cfg);
   ~Transport();
@@ -87,10 +76,7 @@ class Transport {
   // POST pods/{name}/binding with the body formatted here (rate-limited).
   uint64_t bind(const std::string& ns, const std::string& name, const std::string& uid, const std::string& node,
                 const std::vector<KV>& annotations, double timeout_s);
-  struct BindSpec {
-    std::string ns, name, uid, node;
-    std::vector<KV> annotations;
-  };
+  using BindSpec = yk::BindSpec;
   // A run of Bindings in one hand-off to the I/O thread (one lock, one wake-up); their
   // ids are consecutive: the first is returned.
   uint64_t bind_many(const std::vector<BindSpec>& binds, double timeout_s);
@@ -98,6 +84,14 @@ class Transport {
   // closed (kWatchEnd, status -1) when no byte arrived for idle_timeout_s (0 = never).
   uint64_t watch(const std::string& path, bool pods, double idle_timeout_s = 0.0);
   void cancel(uint64_t id);
+  // Native pod lane (lane_port.hpp): every pod watch event goes to `sink` first; nullptr
+  // detaches it (waits for a sink call in progress). Answers of requests submitted for a
+  // sink that is no longer attached are dropped.
+  void set_pod_sink(PodSink* sink);
+  void bind_native(std::vector<BindSpec>&& binds, const std::vector<uint64_t>& tags, double timeout_s,
+                   PodSink* sink) override;
+  void request_native(const std::string& method, const std::string& path, std::string&& body, bool limited,
+                      double timeout_s, uint64_t tag, PodSink* sink) override;
   std::vector<Completion> drain();
   void set_token(const std::string& token);
   // client QPS / burst (clientConnection); qps <= 0 disables limiting
@@ -128,6 +122,8 @@ class Transport {
   void dispatch();
   void check_timeouts(double now);
   void complete(Completion&& c);
+  void answer(Req& r, int status, std::string&& body);   // completion or sink answer
+  void offer_pod_events(Conn* c);
   void flush();
 
   ClientConfig cfg_;
@@ -160,6 +156,9 @@ class Transport {
 
   std::mutex stats_mu_;
   TransportStats stats_;
+
+  std::mutex sink_mu_;                     // held around every sink call (I/O thread)
+  PodSink* pod_sink_ = nullptr;
 };
 
 }  // namespace yk

@@ -523,8 +523,8 @@ def test_informer_backoff_bounds_requests_while_apiserver_down():
 
 
 # ============================================================== scheduler over the native stack
-@pytest.mark.parametrize("server", ["native", "python"])
-def test_scheduler_binds_over_native_transport(server):
+@pytest.mark.parametrize("server,lane", [("native", "on"), ("python", "on"), ("native", "off")])
+def test_scheduler_binds_over_native_transport(server, lane):
     from yoda_scheduler_amd.framework.config import parse_config
     from yoda_scheduler_amd.framework.scheduler import Scheduler
     from yoda_scheduler_amd.kube.informer import NativePodInformer
@@ -544,8 +544,11 @@ def test_scheduler_binds_over_native_transport(server):
             s = make_scv("n1", update_time=time.time())
             s.update_interval_ms = 600_000
             await cl.create("scvs", s.to_json())
-            sched = Scheduler(cl, parse_config(yoda_config()))
+            cfg = yoda_config()
+            cfg["yodaRuntime"]["nativeLane"] = lane
+            sched = Scheduler(cl, parse_config(cfg))
             assert isinstance(sched.make_informers()["pods"], NativePodInformer)
+            assert (sched.lane is not None) == (lane == "on")
             await sched.start()
             loop_t = asyncio.get_event_loop().create_task(sched.scheduling_loop())
             for i in range(30):
@@ -633,7 +636,7 @@ def test_bounded_drain_keeps_order_and_yields_between_chunks():
 def test_failed_bind_handoff_requeues_the_run():
     """If handing a run's Bindings to the transport raises, every pod of the run takes the
     bind-failure path (forgotten, retried from backoff) instead of staying assumed; once the
-    transport accepts again they bind."""
+    transport accepts again they bind. (The Python runner's path: native lane off.)"""
     from yoda_scheduler_amd.framework.config import parse_config
     from yoda_scheduler_amd.framework.scheduler import Scheduler
     from yoda_scheduler_amd.testing import yoda_config
@@ -648,6 +651,7 @@ def test_failed_bind_handoff_requeues_the_run():
             await cl.create("scvs", s.to_json())
             cfg = parse_config(yoda_config())
             cfg.pod_initial_backoff_seconds = 0.01
+            cfg.native_lane = "off"
             sched = Scheduler(cl, cfg)
             await sched.start()
             orig, calls = cl.native.bind_many, []

@@ -1,0 +1,304 @@
+"""Native pod lane (native/core/lane.hpp, framework/lane.py): the per-pod lifecycle in C++.
+
+What upstream kube-scheduler does in compiled Go around the reference plugin
+(/root/reference/pkg/yoda/scheduler.go:76-130) — queue, cycle, assume, Binding, confirm on the
+echo, release on delete — runs here without a Python call per pod. These tests pin that the
+lane (a) schedules exactly like the Python runner (same nodes, same annotations), (b) hands
+pods it cannot finish to the Python path (unschedulable → FailedScheduling + backoff, bind
+failure → retry), (c) keeps the HBM ledger exact through echo, delete and relist, (d) lets
+Python plugins that read other pods see lane pods, and (e) steps aside when a cluster gate
+turns a profile non-native.
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+
+import pytest
+
+from yoda_scheduler_amd.fakeapi.http import FakeApiHttp
+from yoda_scheduler_amd.fakeapi.server import FakeApiServer, Faults
+from yoda_scheduler_amd.framework.config import parse_config
+from yoda_scheduler_amd.framework.scheduler import Scheduler
+from yoda_scheduler_amd.kube.client import KubeClient, KubeConfig
+from yoda_scheduler_amd.models.device import make_node, make_scv
+from yoda_scheduler_amd.testing import NativeApiServerProcess, yoda_config
+
+TOL = [{"key": "node.kubernetes.io/not-ready", "operator": "Exists", "effect": "NoExecute"}]
+
+
+def run(coro):
+    return asyncio.run(coro)
+
+
+def pod(name, labels=None, **spec):
+    return {"metadata": {"name": name, "labels": dict(labels or {})},
+            "spec": {"schedulerName": "yoda-scheduler", "tolerations": TOL, **spec}}
+
+
+class Env:
+    """A scheduler on the native transport against the native (C++) or Python fake apiserver."""
+
+    def __init__(self, server="native", lane="on", faults=None, cfg=None, nodes=(("n1", 8, None),)):
+        self.server_kind, self.lane_mode, self.faults = server, lane, faults
+        self.cfg, self.nodes = cfg, nodes
+
+    async def __aenter__(self):
+        if self.server_kind == "native":
+            self.napi = NativeApiServerProcess()
+            self.papi, url = None, self.napi.url
+        else:
+            self.napi = None
+            self.srv = FakeApiServer(faults=self.faults or Faults())
+            self.papi = FakeApiHttp(self.srv)
+            url = await self.papi.start()
+        self.cl = KubeClient(KubeConfig(url), native=True)
+        for name, gpus, used in self.nodes:
+            await self.cl.create("nodes", make_node(name))
+            s = make_scv(name, gpus=gpus, update_time=time.time(), used_mb=used)
+            s.update_interval_ms = 600_000
+            await self.cl.create("scvs", s.to_json())
+        cfg = self.cfg or yoda_config()
+        cfg.setdefault("yodaRuntime", {})["nativeLane"] = self.lane_mode
+        self.sched = Scheduler(self.cl, parse_config(cfg), seed=1)
+        await self.sched.start()
+        self.loop_t = asyncio.get_event_loop().create_task(self.sched.scheduling_loop())
+        return self
+
+    async def create(self, obj):
+        return await self.cl.create("pods", obj)
+
+    async def wait(self, pred, timeout=10.0):
+        t0 = time.time()
+        while time.time() - t0 < timeout:
+            if pred():
+                return True
+            await asyncio.sleep(0.01)
+        return pred()
+
+    async def pods(self):
+        items, _ = await self.cl.list("pods")
+        return {i["metadata"]["name"]: i for i in items}
+
+    async def __aexit__(self, *exc):
+        await self.sched.shutdown()
+        self.loop_t.cancel()
+        await asyncio.gather(self.loop_t, return_exceptions=True)
+        await self.cl.close()
+        if self.napi:
+            self.napi.stop()
+        if self.papi:
+            await self.papi.stop()
+
+
+WORKLOAD = [({"scv/memory": str(m), **({"scv/number": str(n)} if n > 1 else {})}) for m, n in
+            [(1000, 1), (65536, 2), (4096, 1), (200000, 1), (16384, 4), (2048, 1), (8192, 2), (1024, 8)] * 4]
+
+
+def _placements(lane: str):
+    async def go():
+        async with Env(lane=lane, nodes=(("n1", 8, None), ("n2", 8, None))) as e:
+            for i, lab in enumerate(WORKLOAD):
+                await e.create(pod(f"p{i:02d}", lab))
+                # one pod at a time: both paths see the same queue (and the same ledger) order
+                assert await e.wait(lambda: e.sched.scheduled == i + 1)
+            pods = await e.pods()
+            calls = e.sched.lane.forwarded if e.sched.lane else None
+            return {n: (p["spec"]["nodeName"], {k: v for k, v in (p["metadata"].get("annotations") or {}).items()
+                                                  if k.startswith("scv.amd.com/")}) for n, p in pods.items()}, calls
+    return run(go())
+
+
+def test_lane_places_and_annotates_exactly_like_the_python_runner():
+    """Same seed, same pods in the same order: the lane's node choice, GPU set, ROCr-visible
+    ids, UUIDs and reserved-mb annotations equal the Python runner's — and no pod event
+    reached Python on the lane."""
+    lane, forwarded = _placements("on")
+    py, _ = _placements("off")
+    assert lane == py
+    assert forwarded == 0
+    assert all(a["scv.amd.com/gpus"] and a["scv.amd.com/visible-devices"] for _, a in lane.values())
+
+
+def test_lane_burst_confirms_echoes_and_releases_on_delete():
+    async def go():
+        async with Env() as e:
+            for i in range(60):
+                await e.create(pod(f"b{i}", {"scv/memory": "4096", "scv/number": str(1 + i % 2)}))
+            assert await e.wait(lambda: e.sched.scheduled == 60)
+            lane = e.sched.lane.lane
+            assert await e.wait(lambda: lane.stats()["confirmed"] == 60)
+            st = lane.stats()
+            assert st["owned"] == 60 and st["binding"] == 0 and st["queued"] == 0
+            assert e.sched.engine.ledger_size == 60 and e.sched.pending_binds == 0
+            # the bound pods' reservations: 60 pods × 4096 MB on 90 GPU slots
+            reserved = sum(g["reserved"] for g in e.sched.cache.node_gpu_state("n1"))
+            assert reserved == 4096 * 90
+            for i in range(60):
+                await e.cl.delete("pods", f"b{i}", "default")
+            assert await e.wait(lambda: e.sched.engine.ledger_size == 0 and lane.stats()["owned"] == 0)
+            assert sum(g["reserved"] for g in e.sched.cache.node_gpu_state("n1")) == 0
+            assert e.sched.lane.forwarded == 0 and not e.sched.cache.pods
+    run(go())
+
+
+def test_unschedulable_pod_goes_to_python_path_and_binds_after_capacity_frees():
+    """A pod no node fits is handed to Python: FailedScheduling event, backoff queue; when a
+    lane pod's deletion frees the HBM it is retried on the Python path and binds."""
+    async def go():
+        used = [294912 - 100000] + [294912] * 7           # one GPU with 100 GB free
+        async with Env(nodes=(("n1", 8, used),)) as e:
+            await e.create(pod("big1", {"scv/memory": "80000"}))
+            assert await e.wait(lambda: e.sched.scheduled == 1)
+            await e.create(pod("big2", {"scv/memory": "80000"}))
+            assert await e.wait(lambda: e.sched.failed >= 1)
+            assert e.sched.lane.handoffs >= 1 and e.sched.recorder.recorded["FailedScheduling"] >= 1
+            assert e.sched.queue.contains((await e.pods())["big2"]["metadata"]["uid"])
+            await e.cl.delete("pods", "big1", "default")
+            assert await e.wait(lambda: e.sched.scheduled == 2, 15)
+            return (await e.pods())["big2"]["spec"].get("nodeName")
+    assert run(go()) == "n1"
+
+
+def test_bind_conflicts_are_retried_through_the_python_path():
+    """Bindings answered 409 (Faults.bind_conflict_ratio) release the lane's reservation and
+    retry from the Python backoff queue until they bind; the ledger ends exact."""
+    async def go():
+        cfg = yoda_config(backoff=0.01, max_backoff=0.05)
+        async with Env(server="python", faults=Faults(bind_conflict_ratio=0.4, seed=3), cfg=cfg) as e:
+            for i in range(20):
+                await e.create(pod(f"c{i}", {"scv/memory": "1000"}))
+            ok = await e.wait(lambda: e.sched.scheduled == 20, 20)
+            st = e.sched.lane.lane.stats()
+            await asyncio.sleep(0.1)
+            return ok, st["bind_errors"], e.sched.bind_errors, e.sched.engine.ledger_size
+    ok, lane_err, py_err, ledger = run(go())
+    assert ok and lane_err >= 1 and py_err >= lane_err
+    assert ledger == 20
+
+
+def test_lane_queue_respects_scv_priority_then_fifo():
+    """Pods queued while the lane is inactive bind in scv/priority order, FIFO among equals."""
+    async def go():
+        async with Env(server="python") as e:
+            await asyncio.sleep(0.05)             # the scheduling loop started (it activates the lane)
+            e.sched.lane.set_active(False)
+            names = [("lo1", "1"), ("hi1", "9"), ("mid", "5"), ("hi2", "9"), ("lo2", "1")]
+            for n, pr in names:
+                await e.create(pod(n, {"scv/memory": "1000", "scv/priority": pr}))
+            assert await e.wait(lambda: e.sched.lane.lane.stats()["queued"] == 5)
+            e.sched.lane.set_active(True)
+            assert await e.wait(lambda: e.sched.scheduled == 5)
+            order = sorted(e.srv.bind_log, key=lambda k: e.srv.bind_log[k])
+            return [k.split("/")[1] for k in order]
+    assert run(go()) == ["hi1", "hi2", "mid", "lo1", "lo2"]
+
+
+def test_python_plugins_see_lane_pods_spread():
+    """A pod with topologySpreadConstraints takes the Python path; the spread plugin counts the
+    lane's bound pods (mirrored into the cache) and sends it to the emptier node."""
+    async def go():
+        cfg = yoda_config(extra_filter=["PodTopologySpread"], extra_score=["PodTopologySpread"])
+        async with Env(cfg=cfg, nodes=(("n1", 8, None), ("n2", 8, None))) as e:
+            for n in ("n1", "n2"):
+                e.sched.cache.nodes[n].labels["zone"] = n       # one zone per node
+                e.sched.engine.set_node_meta(e.sched.engine.node_index(n), False, [("zone", n)], [], 192000,
+                                             2 << 40, 110)
+            # three lane pods with app=web, all pinned to n1
+            for i in range(3):
+                await e.create(pod(f"w{i}", {"app": "web", "scv/memory": "1000"}, nodeSelector={"zone": "n1"}))
+            assert await e.wait(lambda: e.sched.scheduled == 3)
+            spread = pod("s0", {"app": "web", "scv/memory": "1000"},
+                         topologySpreadConstraints=[{"maxSkew": 1, "topologyKey": "zone",
+                                                     "whenUnsatisfiable": "DoNotSchedule",
+                                                     "labelSelector": {"matchLabels": {"app": "web"}}}])
+            await e.create(spread)
+            assert await e.wait(lambda: e.sched.scheduled == 4)
+            pods = await e.pods()
+            return [pods[f"w{i}"]["spec"]["nodeName"] for i in range(3)], pods["s0"]["spec"]["nodeName"], \
+                e.sched.lane.lane.stats()["admitted"]
+    lane_nodes, spread_node, admitted = run(go())
+    assert lane_nodes == ["n1"] * 3 and spread_node == "n2" and admitted == 3
+
+
+def test_relist_after_watch_loss_keeps_the_ledger_exact():
+    """The pod watch drops every few events (Faults.drop_watch_every): the informer re-watches
+    / relists through the lane, and every pod still binds exactly once with one reservation."""
+    async def go():
+        async with Env(server="python", faults=Faults(drop_watch_every=7)) as e:
+            for i in range(30):
+                await e.create(pod(f"r{i}", {"scv/memory": "2000"}))
+            ok = await e.wait(lambda: e.sched.scheduled == 30, 20)
+            await asyncio.sleep(0.2)
+            return ok, len(e.srv.bind_log), e.sched.engine.ledger_size, e.sched.lane.lane.stats()["owned"]
+    ok, binds, ledger, owned = run(go())
+    assert ok and binds == 30 and ledger == 30 and owned == 30
+
+
+def test_cluster_gate_hands_the_profile_back_to_python():
+    """A bound pod with required anti-affinity turns InterPodAffinity's symmetry gate on: the
+    lane stops taking the profile's pods (they take the Python path, which checks symmetry)."""
+    async def go():
+        cfg = yoda_config(extra_filter=["InterPodAffinity"])
+        async with Env(cfg=cfg) as e:
+            await e.create(pod("plain0", {"scv/memory": "1000"}))
+            assert await e.wait(lambda: e.sched.scheduled == 1)
+            admitted0 = e.sched.lane.lane.stats()["admitted"]
+            anti = pod("anti", {"app": "db", "scv/memory": "1000"},
+                       affinity={"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                           {"labelSelector": {"matchLabels": {"app": "web"}}, "topologyKey": "kubernetes.io/hostname"}]}})
+            await e.create(anti)
+            assert await e.wait(lambda: e.sched.scheduled == 2)
+            assert await e.wait(lambda: not e.sched.lane._profiles["yoda-scheduler"][0])
+            await e.create(pod("web1", {"app": "web", "scv/memory": "1000"}))
+            await asyncio.sleep(0.5)
+            pods = await e.pods()
+            return admitted0, e.sched.lane.lane.stats()["admitted"], pods["web1"]["spec"].get("nodeName")
+    a0, a1, web_node = run(go())
+    assert a0 == 1 and a1 == 1          # neither anti (PF_POD_AFFINITY) nor web1 (gate on) went to the lane
+    assert not web_node                 # symmetry: the only node holds the anti pod
+
+
+def test_native_lane_off_and_on_agree_on_python_only_pods():
+    """Host-port pods are never admitted by the lane (PF_HOST_PORTS): they bind via Python."""
+    async def go():
+        async with Env() as e:
+            await e.create(pod("hp", {"scv/memory": "1000"},
+                               containers=[{"name": "c", "ports": [{"containerPort": 80, "hostPort": 8080}]}]))
+            assert await e.wait(lambda: e.sched.scheduled == 1)
+            return e.sched.lane.lane.stats()["admitted"], e.sched.lane.forwarded
+    admitted, forwarded = run(go())
+    assert admitted == 0 and forwarded >= 1
+
+
+def test_finish_cycle_refuses_a_result_whose_node_slot_was_reused():
+    """a cycle result names an engine node slot; if that node is deleted and another
+    node re-uses the slot before the result is applied, the pod must not be bound there."""
+    from yoda_scheduler_amd.framework.interfaces import CycleState
+    from yoda_scheduler_amd.models.pod import PodInfo
+    from yoda_scheduler_amd.ops.native import pod_req
+    from yoda_scheduler_amd.testing import FakeCluster
+
+    async def go():
+        c = FakeCluster()
+        c.add_node("old")
+        await c.start()
+        s = c.sched
+        obj = c.server.create("pods", {"metadata": {"name": "p", "namespace": "default",
+                                                    "labels": {"scv/memory": "1000"}},
+                                       "spec": {"schedulerName": "not-served", "containers": [{"name": "c"}]}})
+        pi = PodInfo.from_obj(obj)
+        res = s.engine.schedule(pi.num_id, pod_req(s.engine, pi), True)
+        assert s.engine.node_name(res[0]) == "old"
+        s.on_node_delete(c.server.get("nodes", "old"))
+        c.add_node("new")
+        s.on_node_add(c.server.get("nodes", "new"))
+        assert s.engine.node_index("new") == res[0]           # the slot was reused
+        fw = next(iter(s.frameworks.values()))
+        s._finish_cycle(fw, CycleState(), pi, res, s.queue.scheduling_cycle, time.perf_counter())
+        await asyncio.sleep(0.05)
+        out = (s.pending_binds, pi.uid in s.cache.pods, s.queue.contains(pi.uid), s.engine.has_pod(pi.num_id))
+        await c.stop()
+        return out
+    pending, cached, queued, reserved = run(go())
+    assert pending == 0 and not cached and queued and not reserved

@@ -624,7 +624,7 @@ def test_bind_failure_after_echo_keeps_pod_bound():
         res = s.engine.schedule(pi.num_id, pod_req(s.engine, pi), True)
         node = s.engine.node_name(res[0])
         s.cache.assumed(pi, node, res[3])
-        s.pending_binds += 1
+        s._pending_binds += 1
         bound = dict(obj, spec=dict(obj["spec"], nodeName=node))
         s.cache.add_pod(bound)                       # the echo confirms the assumed pod
         assert not s.cache.is_assumed(pi.uid)

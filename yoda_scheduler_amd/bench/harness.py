@@ -248,10 +248,11 @@ class HttpShard:
         if self._bursts:
             tr = time.perf_counter()
             await self._call("POST", "/debug/bench/reset")
-            while sched.cache.pods or q._active_entries or sched.pending_binds:
+            while sched.cache.pods or q._active_entries or sched.pending_binds or sched.lane_owned():
                 await asyncio.sleep(0.001)      # the deletes reached the scheduler
             self.last_reset_s = time.perf_counter() - tr
         self._bursts += 1
+        sched.take_lane_samples()
         sched.e2e_samples.clear()
         # every step is an independent burst: the client's token bucket starts full, as
         # in the in-process harness where each step is a fresh scheduler
@@ -271,6 +272,7 @@ class HttpShard:
                 break
             await asyncio.sleep(0.0005)
         st = await self._call("GET", "/debug/bench/status?full=1")
+        sched.take_lane_samples()
         return BurstResult(n, st["bound"], n - st["bound"], st["elapsed"], st["latencies"],
                            list(sched.e2e_samples))
 

@@ -32,6 +32,7 @@ class PodState:
     cards: list[int]
     assumed: bool
     deadline: Optional[float] = None      # assumed + binding finished → expiry
+    lane: bool = False                    # mirrored from the native lane (it owns the reservation)
 
 
 class SchedulerCache:
@@ -55,6 +56,9 @@ class SchedulerCache:
         self.node_ext_used: dict[str, dict[str, int]] = {}   # node → extended resource → requested
         self.generation = 0
         self.node_generation = 0                 # node add/remove only (engine index → name stays valid)
+        self.lane = None                         # native lane (core.Lane) whose reserved pods sync_lane mirrors
+        self.on_anti_change = None               # called when the set of required-anti-affinity pods changes
+        self._lane_uids: dict[int, str] = {}     # lane ledger id → uid of the mirrored pod
 
     # ------------------------------------------------------------------ nodes
     def _index_node(self, info: NodeInfo, sign: int) -> None:
@@ -153,9 +157,22 @@ class SchedulerCache:
         self.pods[ps.info.uid] = ps
         self.node_pods.setdefault(ps.node, set()).add(ps.info.uid)
         if ps.info.flags & PF_REQ_ANTI:
-            self._anti.add(ps.info.uid)
+            if ps.info.uid not in self._anti:
+                self._anti.add(ps.info.uid)
+                self._anti_changed()
         else:
-            self._anti.discard(ps.info.uid)
+            self._anti_drop(ps.info.uid)
+
+    def _anti_drop(self, uid: str) -> None:
+        if uid in self._anti:
+            self._anti.discard(uid)
+            self._anti_changed()
+
+    def _anti_changed(self) -> None:
+        """InterPodAffinity's cluster gate (required anti-affinity symmetry) may have flipped:
+        the native lane re-decides which pods it may take."""
+        if self.on_anti_change is not None:
+            self.on_anti_change()
 
     def hide(self, uids) -> list:
         """Drop pods from the Python-side views (``pods`` / ``node_pods`` / extended-resource
@@ -200,6 +217,7 @@ class SchedulerCache:
 
     def forget(self, pi: PodInfo) -> None:
         ps = self.pods.pop(pi.uid, None)
+        self._anti_drop(pi.uid)
         if ps is not None:
             self.node_pods.get(ps.node, set()).discard(pi.uid)
             if ps.info.ext:
@@ -264,6 +282,7 @@ class SchedulerCache:
 
     def remove_pod(self, uid: str) -> None:
         ps = self.pods.pop(uid, None)
+        self._anti_drop(uid)
         if ps is not None:
             self.node_pods.get(ps.node, set()).discard(uid)
             if ps.info.ext:
@@ -277,6 +296,44 @@ class SchedulerCache:
                 self.forget(ps.info)
                 out.append(ps.info)
         return out
+
+    def sync_lane(self) -> int:
+        """Mirror the native lane's reserved pods into ``pods`` / ``node_pods`` (only what
+        changed since the last call) for the Python plugins that read other pods — pod
+        (anti-)affinity, topology spread, preemption. The lane keeps owning them: their
+        ``num_id`` is the lane's ledger id and nothing here releases them. Returns the
+        number of changes applied."""
+        lane = self.lane
+        if lane is None:
+            return 0
+        full, changes = lane.changes()
+        if full:
+            for uid in list(self._lane_uids.values()):
+                self._untrack(uid)
+            self._lane_uids.clear()
+        for lid, add, ev, node, cards in changes:
+            if add:
+                old = self._lane_uids.pop(lid, None)
+                if old is not None:
+                    self._untrack(old)
+                pi = PodInfo.from_native(ev)
+                pi.num_id = lid
+                self._track(PodState(pi, node, list(cards), False, lane=True))
+                self._lane_uids[lid] = pi.uid
+            else:
+                uid = self._lane_uids.pop(lid, None)
+                if uid is not None:
+                    self._untrack(uid)
+        if changes or full:
+            self.generation += 1
+        return len(changes)
+
+    def _untrack(self, uid: str) -> None:
+        ps = self.pods.pop(uid, None)
+        if ps is not None:
+            self.node_pods.get(ps.node, set()).discard(uid)
+            if ps.info.ext:
+                self._ext(ps, -1)
 
     def is_assumed(self, uid: str) -> bool:
         ps = self.pods.get(uid)

@@ -133,6 +133,10 @@ class SchedulerConfig:
     # False: every Scv event moves the whole unschedulable queue (upstream's behaviour for
     # any cluster event)
     scv_queueing_hint: bool = True
+    # native pod lane (yodaRuntime.nativeLane): pods of all-native profiles are queued,
+    # placed, bound, confirmed and released in C++ (native/core/lane.hpp) with no Python call
+    # per pod; auto = on whenever the native Kubernetes transport is in use
+    native_lane: str = "auto"
     # event API (yodaRuntime.eventsAPI): upstream v1.20 records through events.k8s.io/v1
     events_api: str = "events.k8s.io/v1"
     trace: bool = False
@@ -290,6 +294,10 @@ def parse_config(doc: dict) -> SchedulerConfig:
         raise ValueError("yodaRuntime.overlapEngine must be auto|on|off")
     cfg.overlap_depth = int(_f(rt, "overlapDepth", cfg.overlap_depth))
     cfg.scv_queueing_hint = bool(_f(rt, "scvQueueingHint", cfg.scv_queueing_hint))
+    nl = _f(rt, "nativeLane", cfg.native_lane)
+    cfg.native_lane = {True: "on", False: "off"}.get(nl, str(nl).lower()) if isinstance(nl, bool) else str(nl).lower()
+    if cfg.native_lane not in ("auto", "on", "off"):
+        raise ValueError("yodaRuntime.nativeLane must be auto|on|off")
     if not 2 <= cfg.overlap_depth <= 16:
         raise ValueError("yodaRuntime.overlapDepth must be in [2, 16]")
     cfg.trace = bool(_f(rt, "trace", False))

@@ -1,0 +1,214 @@
+"""Python side of the native pod lane (``native/core/lane.hpp``).
+
+The reference plugin only supplies Filter/Score; upstream kube-scheduler runs the per-pod
+lifecycle around it in compiled Go — informer → activeQ → ``scheduleOne`` → assume → bind
+goroutine → confirm / forget (``/root/reference/pkg/yoda/scheduler.go:76-130``). Here that
+lifecycle runs in C++ for every pod an all-native profile can take: the transport hands the
+lane every pod watch event, the lane thread queues, places (``Engine::schedule_batch``),
+assumes and POSTs the Binding, and handles the answer, the watch echo and the deletion.
+
+This module is everything Python still does, none of it per lane pod:
+
+* decides per profile whether the lane may take its pods (the same conditions under which
+  the Python runner would take the fully native path and bind directly) and with which
+  pod-flag mask; re-decided when a cluster-wide plugin gate flips;
+* applies what the lane forwards — events of pods it does not own (dispatched to the
+  scheduler's ``on_pod_native`` exactly as the Python informer would), pods handed over
+  after an unschedulable cycle or a failed Binding (FailedScheduling event, backoff queue,
+  PostFilter/preemption), and a count of releases (the queue's move request);
+* mirrors reserved lane pods into the cache on demand (``SchedulerCache.sync_lane``) for
+  the Python plugins that read other pods, and parks the lane around ledger what-ifs.
+"""
+from __future__ import annotations
+
+import asyncio
+import contextlib
+import logging
+from typing import Optional
+
+from ..models.pod import PodInfo
+from ..ops.native import core
+
+log = logging.getLogger("yoda.lane")
+
+
+class NativeLane:
+    def __init__(self, sched, transport) -> None:
+        from .events import API_EVENTS_V1
+        self.s = sched
+        self.transport = transport            # kube.native.NativeTransport
+        rec = sched.recorder
+        qs = next(iter(sched.frameworks.values())).queue_sort
+        qname = getattr(qs, "name", "")
+        self.sort_kind = {"yoda": 0, "PrioritySort": 1}.get(qname, -1)
+        self.lane = core().Lane(sched.engine, batch=max(1, sched.config.batch_size), bind_timeout=sched.bind_timeout,
+                                sort_kind=max(self.sort_kind, 0), events=rec.enabled,
+                                events_v1=rec.api == API_EVENTS_V1, event_qps=float(rec.limiter.qps),
+                                event_burst=int(rec.limiter.burst), event_buffer=rec.max_buffer, host=rec.host,
+                                name_prefix=rec._name_prefix)
+        self.lane.set_port(transport.t.port_ptr())
+        self._profiles: dict[str, tuple] = {}
+        self._loop: Optional[asyncio.AbstractEventLoop] = None
+        self.handoffs = 0
+        self.forwarded = 0
+
+    # ------------------------------------------------------------------ lifecycle
+    def attach(self) -> None:
+        """Route the transport's pod watch events into the lane and wake the loop on its
+        output. Must precede the pod informer's first watch."""
+        self.transport.t.set_pod_sink(self.lane.sink_ptr())
+        loop = asyncio.get_event_loop()
+        if self._loop is not loop:
+            loop.add_reader(self.lane.fileno(), self._drain)
+            self._loop = loop
+
+    def set_active(self, on: bool) -> None:
+        self.lane.set_active(bool(on))
+
+    def close(self) -> None:
+        if self._loop is not None and not self._loop.is_closed():
+            with contextlib.suppress(Exception):
+                self._loop.remove_reader(self.lane.fileno())
+        self._loop = None
+        self.transport.t.set_pod_sink(0)
+        self.lane.close()
+
+    # ------------------------------------------------------------------ profiles
+    def eligible_mask(self, fw) -> Optional[int]:
+        """Pod-flag mask for which the lane may run ``fw``'s pods end to end, or None: the
+        profile's cycle must be fully native for such pods (Framework.native_mask, which is
+        None while a cluster gate is active) and their binding a direct DefaultBinder POST
+        with no PreBind/Reserve/Permit/PostBind plugin applying (Framework.direct_bind_mask)."""
+        s = self.s
+        if s.extenders or self.sort_kind < 0 or not fw.fully_native_static or not fw.post_bind_noop:
+            return None
+        m = fw.native_mask()
+        if m is None:
+            return None
+        if len(fw.bind_plugins) != 1 or not getattr(fw.bind_plugins[0], "native_bind", False):
+            return None
+        bm = fw.direct_bind_mask()
+        if bm is None:
+            return None
+        return m | bm
+
+    def refresh(self) -> None:
+        """(Re)declare every profile to the lane when its eligibility changed. A profile the
+        lane may no longer run gets its queued pods back through the Python queue."""
+        s = self.s
+        f_yoda = core().F_YODA
+        for name, fw in s.frameworks.items():
+            m = self.eligible_mask(fw)
+            want = (m is not None, m or 0, bool(fw.filter_mask & f_yoda))
+            if self._profiles.get(name) == want:
+                continue
+            s._activate(fw)                    # the lane snapshots the engine config now applied
+            self.lane.set_profile(s.engine, name, want[0], want[1], want[2])
+            self._profiles[name] = want
+            log.info("native lane: profile %s %s (flag mask %#x)", name, "on" if want[0] else "off", want[1])
+
+    # ------------------------------------------------------------------ lane output
+    def _drain(self) -> None:
+        fwd, hand, moves = self.lane.drain()
+        s = self.s
+        if fwd:
+            self.forwarded += len(fwd)
+            handler = s.on_pod_native
+            for typ, ev, old in fwd:
+                try:
+                    handler(typ, ev, ev.ident(), (old, old.ident()) if old is not None else None)
+                except Exception:  # noqa: BLE001 - isolate handlers, like the informer
+                    log.exception("native lane: pod event handler failed")
+        if moves:
+            s.queue.move_all_to_active_or_backoff("AssignedPodDelete")
+            if s._dev_flush:
+                s._request_device_flush()
+        for h in hand:
+            try:
+                self._handoff(h)
+            except Exception:  # noqa: BLE001
+                log.exception("native lane: handoff failed")
+
+    def _handoff(self, h: tuple) -> None:
+        """A pod the lane gave up: from here on it is an ordinary Python-path pod."""
+        kind, ev, prof, res, status, msg, t_enq, t_cycle = h
+        s = self.s
+        self.handoffs += 1
+        fw = s.frameworks.get(prof) or next(iter(s.frameworks.values()))
+        pi = PodInfo.from_native(ev)
+        pi.attempts = 1
+        pi.initial_attempt = pi.enqueued = t_enq
+        if kind == 0:
+            # cycle -1: a move request may have arrived since the lane's cycle, so the pod
+            # retries from backoff rather than parking in unschedulableQ (never lose a wake-up)
+            if fw.post_filter:
+                with self.held():             # preemption reads other pods and what-ifs the ledger
+                    s._fail(fw, None, pi, -1, s._fit_error(res), t_cycle)
+            else:
+                s._fail(fw, None, pi, -1, s._fit_error(res), t_cycle)
+            return
+        from ..kube.native import api_error
+        if status == 401:
+            s.client._refresh_token(force=True)
+        s.bind_errors += 1
+        err = api_error(status, msg)
+        s.recorder.pod_event(pi, "Warning", "FailedScheduling", f"Binding rejected: {err}")
+        log.info("bind %s failed: %s", pi.key, err)
+        s.queue.add_unschedulable(pi, -1, unschedulable=False)
+
+    # ------------------------------------------------------------------ cache view
+    @contextlib.contextmanager
+    def held(self):
+        """The cache mirrors the lane's reserved pods and the lane thread is parked: Python
+        plugins may read other pods and run ledger what-ifs (preemption) safely."""
+        self.s.cache.sync_lane()
+        self.lane.pause(True)
+        try:
+            yield
+        finally:
+            self.lane.pause(False)
+
+    # ------------------------------------------------------------------ counters
+    def pending(self) -> int:
+        st = self.lane.stats()
+        return st["queued"] + st["inflight"] + st["binding"]
+
+    def owned(self) -> int:
+        return self.lane.stats()["owned"]
+
+
+class LaneEntries:
+    """``key → (PodEvent, ident)`` view of the lane's pod store for the pod informer (the
+    informer keeps no per-pod state of its own when the lane owns the stream)."""
+
+    def __init__(self, lane) -> None:
+        self._l = lane
+
+    def get(self, key, default=None):
+        r = self._l.lookup(key)
+        if r is None:
+            return default
+        ev = r[0]
+        return ev, ev.ident()
+
+    def __getitem__(self, key):
+        v = self.get(key)
+        if v is None:
+            raise KeyError(key)
+        return v
+
+    def __contains__(self, key) -> bool:
+        return self._l.lookup(key) is not None
+
+    def __iter__(self):
+        return iter(self._l.keys())
+
+    def __len__(self) -> int:
+        return len(self._l)
+
+    # the lane is the store's only writer: informer-side writes are no-ops
+    def __setitem__(self, key, value) -> None:
+        return None
+
+    def pop(self, key, default=None):
+        return self.get(key, default)

@@ -159,14 +159,16 @@ class Scheduler:
         self._ann_memo: dict = {}          # _bind_annotations memo, valid for one cache generation
         self._ann_gen = -1
         self.informers: dict[str, Informer] = {}
-        self.scheduled = 0
+        self._scheduled = 0                # bound by the Python path (the lane counts its own)
         self.failed = 0
         self.scv_requeues = 0          # Scv updates that moved the parked pods back
         self.scv_requeue_skips = 0     # Scv updates the queueing hint kept from doing so
         self.bind_errors = 0
         self._stop = asyncio.Event()
         self.leading = asyncio.Event()
-        self.pending_binds = 0
+        self._pending_binds = 0
+        self.lane = None                   # framework.lane.NativeLane (native transport only)
+        self._lane_held = False
         self.batching = config.batch_size > 1
         self.tracer = Tracer() if config.trace else None
         from .extender import HTTPExtender
@@ -188,6 +190,48 @@ class Scheduler:
         if isinstance(self.metrics, SchedulerMetrics):
             m = self.metrics
             self.queue.incoming_hook = lambda ev, q, n: m.child(m.incoming, ev, q).inc(n)
+
+    # ------------------------------------------------------------------ counters (Python + lane)
+    @property
+    def scheduled(self) -> int:
+        """Pods whose Binding the apiserver acknowledged, on either path."""
+        return self._scheduled + (self.lane.lane.scheduled if self.lane is not None else 0)
+
+    @property
+    def pending_binds(self) -> int:
+        """Pods placed (or queued on the native lane) whose Binding is not answered yet."""
+        return self._pending_binds + (self.lane.pending() if self.lane is not None else 0)
+
+    def take_lane_samples(self) -> None:
+        """Move the lane's raw e2e samples (cycle start → Binding acknowledged) into
+        ``e2e_samples`` when that list is being collected (benchmarks); drop them otherwise."""
+        if self.lane is None:
+            return
+        xs = self.lane.lane.take_e2e()
+        if self.e2e_samples is not None:
+            self.e2e_samples.extend(xs)
+
+    def lane_owned(self) -> int:
+        """Pods the native lane owns (queued, in flight, binding or bound)."""
+        return self.lane.owned() if self.lane is not None else 0
+
+    def _lane_refresh(self) -> None:
+        if self.lane is not None:
+            self.lane.refresh()
+
+    def _lane_cards(self, name: str) -> None:
+        """The per-card device identities a lane Binding's annotations name (plugins.defaults
+        .visible_device_ids), pushed whenever the node's Scv changes."""
+        if self.lane is None:
+            return
+        scv = self.cache.scvs.get(name)
+        if scv is None:
+            self.lane.lane.remove_node_cards(name)
+            return
+        from ..models.scv import card_vis
+        per = scv.card_vis() if isinstance(scv, LazyScv) else \
+            card_vis([(c.id, c.uuid, c.hip_uuid, c.hip_id) for c in scv.status.card_list])
+        self.lane.lane.set_node_cards(name, [(str(v), str(u or "")) for v, u in per])
 
     def _request_device_flush(self) -> None:
         """Released reservations dirty device rows; when nothing is being placed, upload
@@ -348,9 +392,11 @@ class Scheduler:
     def on_node_add(self, obj: dict) -> None:
         self.cache.add_node(obj)
         self.queue.move_all_to_active_or_backoff("NodeAdd")
+        self._lane_refresh()
 
     def on_node_update(self, old: dict, new: dict) -> None:
         self.cache.update_node(new)
+        self._lane_refresh()
         if old.get("spec") != new.get("spec") or (old.get("metadata") or {}).get("labels") != \
                 (new.get("metadata") or {}).get("labels") or (old.get("status") or {}).get("allocatable") != \
                 (new.get("status") or {}).get("allocatable"):
@@ -358,9 +404,11 @@ class Scheduler:
 
     def on_node_delete(self, obj: dict) -> None:
         self.cache.remove_node(obj["metadata"]["name"])
+        self._lane_refresh()
 
     def on_scv(self, obj: dict) -> None:
         self.cache.add_scv(obj)
+        self._lane_cards((obj.get("metadata") or {}).get("name", ""))
         self.queue.move_all_to_active_or_backoff("ScvAdd")
 
     def _capacity(self, name: str) -> Optional[tuple]:
@@ -396,12 +444,14 @@ class Scheduler:
         parked pod (``scv_requeues`` / ``scv_requeue_skips`` count both outcomes)."""
         if not self.config.scv_queueing_hint:
             self.cache.add_scv(new)
+            self._lane_cards((new.get("metadata") or {}).get("name", ""))
             self.queue.move_all_to_active_or_backoff("ScvUpdate")
             self.scv_requeues += 1
             return
         name = (new.get("metadata") or {}).get("name", "")
         before = self._capacity(name)
         self.cache.add_scv(new)
+        self._lane_cards(name)
         after = self._capacity(name)
         if before is None or after is None:
             self.queue.move_all_to_active_or_backoff("ScvUpdate")
@@ -439,13 +489,15 @@ class Scheduler:
 
     def on_scv_delete(self, obj: dict) -> None:
         self.cache.remove_scv(obj["metadata"]["name"])
+        self._lane_cards(obj["metadata"]["name"])
 
     def make_informers(self) -> dict[str, Informer]:
         self.informers = {
             "nodes": Informer(self.client, "nodes", self.on_node_add, self.on_node_update, self.on_node_delete),
             "scvs": Informer(self.client, "scvs", self.on_scv, self.on_scv_update, self.on_scv_delete),
             # upstream v1.20 scheduler pod informer: terminal pods are filtered by the apiserver
-            "pods": (NativePodInformer(self.client, self.on_pod_native, field_selector=POD_FIELD_SELECTOR)
+            "pods": (NativePodInformer(self.client, self.on_pod_native, field_selector=POD_FIELD_SELECTOR,
+                                       lane=self._make_lane())
                      if self.native is not None else
                      Informer(self.client, "pods", self.on_pod_add, self.on_pod_update, self.on_pod_delete,
                               field_selector=POD_FIELD_SELECTOR)),
@@ -457,9 +509,25 @@ class Scheduler:
         for res in extra:
             ev = f"{res}Change"
             self.informers[res] = Informer(self.client, res,
-                                           lambda o, ev=ev: self.queue.move_all_to_active_or_backoff(ev),
-                                           lambda a, b, ev=ev: self.queue.move_all_to_active_or_backoff(ev), None)
+                                           lambda o, ev=ev: self._extra_event(ev),
+                                           lambda a, b, ev=ev: self._extra_event(ev),
+                                           lambda o, ev=ev: self._lane_refresh())
         return self.informers
+
+    def _extra_event(self, ev: str) -> None:
+        self.queue.move_all_to_active_or_backoff(ev)
+        self._lane_refresh()                      # e.g. the first Service turns a spread gate on
+
+    def _make_lane(self):
+        """The native pod lane when the transport is native and ``yodaRuntime.nativeLane``
+        allows it; returns the ``core.Lane`` for the pod informer (or None)."""
+        if self.native is None or self.config.native_lane == "off" or self.lane is not None:
+            return self.lane.lane if self.lane is not None else None
+        from .lane import NativeLane
+        self.lane = NativeLane(self, self.native)
+        self.cache.lane = self.lane.lane
+        self.cache.on_anti_change = self._lane_refresh
+        return self.lane.lane
 
     # ================================================================== cycle
     def _activate(self, fw: Framework) -> None:
@@ -481,6 +549,8 @@ class Scheduler:
         fw = self.frameworks.get(pi.scheduler_name)
         if fw is None or self._pod_gone(pi):
             return
+        if self.lane is not None and not fw.native_for(pi):
+            self.cache.sync_lane()               # Python plugins read other pods, lane pods included
         self._clear_nominations_for((pi,))       # the preemptor competes with its own hold gone
         self._activate(fw)
         cycle = self.queue.scheduling_cycle
@@ -512,6 +582,8 @@ class Scheduler:
         fw = self.frameworks.get(pi.scheduler_name)
         if fw is None or self._pod_gone(pi):
             return
+        if self.lane is not None:
+            self.cache.sync_lane()
         self._clear_nominations_for((pi,))
         self._activate(fw)
         cycle = self.queue.scheduling_cycle
@@ -616,7 +688,7 @@ class Scheduler:
             m.child(m.attempts, "scheduled", fw.name).inc()
         if klog.V(3):
             log.info("pod %s → node %s gpus=%s score=%d feasible=%d", pi.key, node, cards, res[4], res[1])
-        self.pending_binds += 1
+        self._pending_binds += 1
         if waiting:       # held at Permit: its own task waits, then hands it to the binders
             asyncio.get_event_loop().create_task(self._permit_then_bind((fw, state, pi, node, cycle, t0)))
         else:
@@ -643,7 +715,7 @@ class Scheduler:
         if st.is_success():
             self._enqueue_bind(item)
             return
-        self.pending_binds -= 1
+        self._pending_binds -= 1
         fw.run_unreserve(state, pi, node)
         self.cache.forget(pi)
         self.failed += 1
@@ -677,6 +749,13 @@ class Scheduler:
         if state is None:
             state = CycleState()
         if unschedulable and fw.post_filter:
+            if self.lane is not None and not self._lane_held:
+                self._lane_held = True
+                try:
+                    with self.lane.held():        # mirror lane pods, park the lane: ledger what-ifs
+                        return self._fail(fw, state, pi, cycle, msg, t0, unschedulable)
+                finally:
+                    self._lane_held = False
             for p in fw.post_filter:
                 try:
                     r, st = p.post_filter(state, pi, {})
@@ -999,13 +1078,13 @@ class Scheduler:
     def _native_bind_done(self, item: tuple, tb: float, status: int, body: bytes) -> None:
         """Completion of a native binding POST (runs from the transport's eventfd callback)."""
         fw, state, pi, node, cycle, t0 = item
-        self.pending_binds -= 1
+        self._pending_binds -= 1
         if 200 <= status < 300:
             if self.tracer is None and fw.post_bind_noop:
                 # the common case inlined (_after_bind's success branch, no tracer / PostBind)
                 now = time.perf_counter()
                 self.cache.finish_binding(pi)
-                self.scheduled += 1
+                self._scheduled += 1
                 if self.e2e_samples is not None:
                     self.e2e_samples.append(now - t0)
                 if self._metrics_on:
@@ -1032,7 +1111,7 @@ class Scheduler:
         if st.is_success():
             self.cache.finish_binding(pi)
             fw.run_post_bind(state, pi, node)
-            self.scheduled += 1
+            self._scheduled += 1
             if self.e2e_samples is not None:
                 self.e2e_samples.append(time.perf_counter() - t0)
             m.child(m.e2e, "scheduled", fw.name).observe(time.perf_counter() - t0)
@@ -1045,7 +1124,7 @@ class Scheduler:
                 # only the answer was lost (connection closed under pipelined requests,
                 # client timeout): the pod is bound, so neither forget it (its reservation
                 # is real) nor retry it (upstream ForgetPod refuses pods no longer assumed)
-                self.scheduled += 1
+                self._scheduled += 1
                 log.info("bind %s → %s answered %s after its echo confirmed it; kept as bound",
                          pi.key, node, st.message())
                 return
@@ -1089,7 +1168,7 @@ class Scheduler:
                     st = Status.error(repr(e))
                 self._after_bind(fw, state, pi, node, cycle, t0, tb, st)
             finally:
-                self.pending_binds -= 1
+                self._pending_binds -= 1
 
     def _extender_binder(self, pi: PodInfo):
         for e in self.extenders:
@@ -1122,6 +1201,7 @@ class Scheduler:
                 for uid in [u for u, (_n, _i, t) in self.nominations.items() if now - t > 60.0]:
                     self._clear_nomination(uid)
             self._maybe_enable_device()
+            self._lane_refresh()                 # cluster gates (services, images, anti-affinity)
             refresh = getattr(self.client, "_refresh_token", None)
             if refresh is not None:
                 refresh()                        # rotated service-account tokens
@@ -1141,6 +1221,9 @@ class Scheduler:
     async def scheduling_loop(self) -> None:
         q = self.queue
         bs = max(1, self.config.batch_size)
+        if self.lane is not None:
+            self.lane.refresh()
+            self.lane.set_active(True)           # the lane schedules while this loop does
         while not self._stop.is_set():
             if self._inflight and not q._active_entries:
                 # nothing to pop: apply the oldest run when it lands, unless pods arrive first
@@ -1178,6 +1261,8 @@ class Scheduler:
         loop = asyncio.get_event_loop()
         if not self.informers:
             self.make_informers()
+        if self.lane is not None:
+            self.lane.attach()                   # before the pod watch starts
         for inf in self.informers.values():
             self._tasks.append(loop.create_task(inf.run()))
         n_workers = max(1, self.config.bind_concurrency)
@@ -1188,6 +1273,7 @@ class Scheduler:
         if wait_sync:
             await self.wait_synced()
         self._maybe_enable_device()
+        self._lane_refresh()
         gctune.tune(self.config.gc_threshold)
 
     async def wait_synced(self) -> None:
@@ -1212,6 +1298,8 @@ class Scheduler:
     def stop(self) -> None:
         self._stop.set()
         self.queue.close()
+        if self.lane is not None:
+            self.lane.set_active(False)
         for inf in self.informers.values():
             inf.stop()
 
@@ -1223,6 +1311,8 @@ class Scheduler:
         self._tasks.clear()
         for e in self.extenders:
             await e.close()
+        if self.lane is not None:
+            self.lane.close()
         if self._engine_exec is not None:
             self._engine_exec.shutdown(wait=True)
             self._engine_exec = None

@@ -214,11 +214,20 @@ class NativePodInformer(Informer):
     previous ``(PodEvent, ident)`` of the key (``None`` for a new pod)."""
 
     def __init__(self, client, on_event: PodNativeHandler, field_selector: Optional[str] = None,
-                 relist_backoff: float = 0.8, max_backoff: float = 30.0) -> None:
+                 relist_backoff: float = 0.8, max_backoff: float = 30.0, lane=None) -> None:
+        """``lane``: a native pod lane (``core.Lane``) attached to the transport as its pod
+        sink. It then receives every pod watch event and owns the store; this informer only
+        keeps the stream alive (bookmarks, errors, re-watch / relist) and the lane forwards
+        to ``on_event`` the events Python must see."""
         super().__init__(client, "pods", relist_backoff=relist_backoff, field_selector=field_selector,
                          max_backoff=max_backoff)
         self.on_event = on_event
-        self.entries: dict[str, tuple] = {}
+        self.lane = lane
+        if lane is not None:
+            from ..framework.lane import LaneEntries
+            self.entries = LaneEntries(lane)        # type: ignore[assignment]
+        else:
+            self.entries: dict[str, tuple] = {}
         self.store = LazyPodStore(self.entries)      # type: ignore[assignment]
 
     def ident(self, key: str) -> Optional[tuple]:
@@ -247,9 +256,16 @@ class NativePodInformer(Informer):
             for ev in evs:
                 idt = ev.ident()
                 fresh[idt[0]] = (ev, idt)
-        for key in [k for k in self.entries if k not in fresh]:
+        for key in ([] if self.lane is not None else [k for k in self.entries if k not in fresh]):
             old = self.entries.pop(key)
             self._call(self.on_event, "DELETED", old[0], old[1], old)
+        if self.lane is not None:
+            # the lane diffs the list against its store; Python sees what it forwards
+            for typ, ev, old in self.lane.relist([e[0] for e in fresh.values()]):
+                self._call(self.on_event, typ, ev, ev.ident(), (old, old.ident()) if old is not None else None)
+            self.resource_version = rv
+            self.relists += 1
+            return
         for key, e in fresh.items():
             old = self.entries.get(key)
             self.entries[key] = e
