@@ -104,6 +104,12 @@ PYBIND11_MODULE(_yoda_kube, m) {
       });
 
   m.def("project", &project_bytes, py::arg("raw"), "Project a pod's JSON (tests / tooling).");
+  m.def("project_flat", [](const std::string& raw) {
+    auto pe = std::make_shared<PodEv>();
+    if (!project_pod_text(raw, pe->p)) throw py::value_error("invalid JSON");
+    pe->raw = raw;
+    return pe;
+  }, py::arg("raw"), "Project a pod's JSON through the flat decoder the watch stream uses.");
   // PodList body → (resourceVersion, continue, [PodEvent]) — relists of large clusters
   // never build Python dicts either
   m.def("project_list", [](const std::string& body) {

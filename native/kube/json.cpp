@@ -217,13 +217,32 @@ inline uint64_t mix(uint64_t h, uint64_t x) {
 }
 
 uint64_t hash_bytes(std::string_view s, uint64_t h) {
-  // FNV-1a over the bytes, folded into the running hash
-  uint64_t f = 0xcbf29ce484222325ull;
-  for (unsigned char c : s) f = (f ^ c) * 0x100000001b3ull;
-  return mix(h, f ^ s.size());
+  // 8 bytes per step (multiply-xorshift over little-endian words), folded into the running
+  // hash; the watch stream hashes every pod's spec + metadata three times per scheduled pod
+  uint64_t f = 0xcbf29ce484222325ull ^ (s.size() * 0x9e3779b97f4a7c15ull);
+  const char* p = s.data();
+  size_t n = s.size();
+  while (n >= 8) {
+    uint64_t w;
+    std::memcpy(&w, p, 8);
+    f = (f ^ w) * 0x100000001b3ull;
+    f ^= f >> 29;
+    p += 8;
+    n -= 8;
+  }
+  if (n) {
+    uint64_t w = 0;
+    std::memcpy(&w, p, n);
+    f = (f ^ w) * 0x100000001b3ull;
+    f ^= f >> 29;
+  }
+  return mix(h, f);
 }
 
 }  // namespace
+
+uint64_t hash_mix(uint64_t h, uint64_t x) { return mix(h, x); }
+uint64_t hash_text(std::string_view s, uint64_t h) { return hash_bytes(s, h); }
 
 const Value* Value::get(std::string_view k) const {
   if (t != Obj) return nullptr;

@@ -79,4 +79,8 @@ void merge_patch(Value& target, const Value& patch);
 
 bool equal(const Value& a, const Value& b);
 
+// the hash's building blocks (shared with flatjson.hpp so both hashes agree)
+uint64_t hash_mix(uint64_t h, uint64_t x);
+uint64_t hash_text(std::string_view s, uint64_t h);
+
 }  // namespace yk

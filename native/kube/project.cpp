@@ -82,73 +82,135 @@ bool starts_with(std::string_view s, std::string_view p) { return s.substr(0, p.
 
 bool is_basic(std::string_view k) { return k == "cpu" || k == "memory"; }
 
-bool term_of(const Value* t, TermP& out) {
+// Uniform read-only view of a decoded JSON value, over the DOM (json.hpp) or the flat
+// document (flatjson.hpp): one projection body serves both, so they cannot drift apart.
+struct DomN {
+  const Value* v = nullptr;
+  explicit operator bool() const { return v != nullptr; }
+  bool obj() const { return v && v->t == Value::Obj; }
+  bool arr() const { return v && v->t == Value::Arr; }
+  bool str_t() const { return v && v->t == Value::Str; }
+  bool num_t() const { return v && v->t == Value::Num; }
+  bool null_t() const { return v && v->t == Value::Null; }
+  DomN get(std::string_view k) const { return DomN{v ? v->get(k) : nullptr}; }
+  std::string_view sv(std::string_view k) const { return v ? v->sv(k) : std::string_view(); }
+  std::string_view str() const { return v->s; }
+  bool truthy() const { return v && v->truthy(); }
+  int64_t as_int(bool* ok) const { return v->as_int(ok); }
+  template <class F> bool each(F f) const {     // members (key, value) / elements ("", value)
+    if (v->t == Value::Obj) {
+      for (const auto& m : v->obj)
+        if (!f(std::string_view(m.first), DomN{&m.second})) return false;
+    } else if (v->t == Value::Arr) {
+      for (const auto& x : v->arr)
+        if (!f(std::string_view(), DomN{&x})) return false;
+    }
+    return true;
+  }
+  uint64_t hash(uint64_t h) const { return yk::hash(v ? *v : Value(), h); }
+};
+
+struct FlatN {
+  FlatDoc::View v;
+  explicit operator bool() const { return bool(v); }
+  bool obj() const { return v.is(FlatDoc::Obj); }
+  bool arr() const { return v.is(FlatDoc::Arr); }
+  bool str_t() const { return v.is(FlatDoc::Str); }
+  bool num_t() const { return v.is(FlatDoc::Num); }
+  bool null_t() const { return v.is(FlatDoc::Null); }
+  FlatN get(std::string_view k) const { return FlatN{v.get(k)}; }
+  std::string_view sv(std::string_view k) const { return v ? v.sv(k) : std::string_view(); }
+  std::string_view str() const { return v.str(); }
+  bool truthy() const { return v.truthy(); }
+  int64_t as_int(bool* ok) const { return v.as_int(ok); }
+  template <class F> bool each(F f) const {
+    const bool o = v.is(FlatDoc::Obj);
+    for (FlatDoc::View c = v.first(); c; c = c.next())
+      if (!f(o ? c.key() : std::string_view(), FlatN{c})) return false;
+    return true;
+  }
+  uint64_t hash(uint64_t h) const { return v ? v.hash(h) : hash_mix(h, Value::Null); }
+};
+
+template <class N>
+bool term_of(N t, TermP& out) {
   out.clear();
-  if (!t || t->t != Value::Obj) return t == nullptr || t->t == Value::Null;
-  auto add = [&](const Value& e, bool field) -> bool {
-    if (e.t != Value::Obj) return false;
+  if (!t || !t.obj()) return !t || t.null_t();
+  auto add = [&](N e, bool field) -> bool {
+    if (!e.obj()) return false;
     SelReqP r;
-    const Value* k = e.get("key");
-    if (k && k->t != Value::Str) return false;             // null key: Python keeps None
-    std::string key = k ? k->s : "";
+    N k = e.get("key");
+    if (k && !k.str_t()) return false;                    // null key: Python keeps None
+    std::string key = k ? std::string(k.str()) : "";
     if (field) {
       if (key != "metadata.name") return true;            // other fields: ignored (as in Python)
       key = "kubernetes.io/hostname";
     }
     r.key = key;
-    const Value* op = e.get("operator");
-    if (op && op->t != Value::Str) return false;
-    r.op = op ? op->s : "In";
-    const Value* vs = e.get("values");
-    if (vs && vs->t == Value::Arr) {
-      for (const auto& v : vs->arr) {
-        if (v.t != Value::Str) return false;              // str(non-string) differs: Python decides
-        r.values.push_back(v.s);
-      }
-    } else if (vs && vs->t != Value::Null) {
+    N op = e.get("operator");
+    if (op && !op.str_t()) return false;
+    r.op = op ? std::string(op.str()) : "In";
+    N vs = e.get("values");
+    if (vs && vs.arr()) {
+      bool ok = vs.each([&](std::string_view, N x) {
+        if (!x.str_t()) return false;                     // str(non-string) differs: Python decides
+        r.values.emplace_back(x.str());
+        return true;
+      });
+      if (!ok) return false;
+    } else if (vs && !vs.null_t()) {
       return false;
     }
     out.push_back(std::move(r));
     return true;
   };
-  if (const Value* me = t->get("matchExpressions"); me && me->t == Value::Arr) {
-    for (const auto& e : me->arr)
-      if (!add(e, false)) return false;
+  if (N me = t.get("matchExpressions"); me && me.arr()) {
+    if (!me.each([&](std::string_view, N e) { return add(e, false); })) return false;
   }
-  if (const Value* mf = t->get("matchFields"); mf && mf->t == Value::Arr) {
-    for (const auto& e : mf->arr)
-      if (!add(e, true)) return false;
+  if (N mf = t.get("matchFields"); mf && mf.arr()) {
+    if (!mf.each([&](std::string_view, N e) { return add(e, true); })) return false;
   }
   return true;
 }
 
-bool kvs(const Value* m, std::vector<KV>& out) {
-  if (!m || m->t == Value::Null) return true;
-  if (m->t != Value::Obj) return false;
-  out.reserve(m->obj.size());
-  for (const auto& kv : m->obj) {
-    if (kv.second.t != Value::Str) return false;
-    out.emplace_back(kv.first, kv.second.s);
-  }
-  return true;
+template <class N>
+bool kvs(N m, std::vector<KV>& out) {
+  if (!m || m.null_t()) return true;
+  if (!m.obj()) return false;
+  return m.each([&](std::string_view k, N v) {
+    if (!v.str_t()) return false;
+    out.emplace_back(std::string(k), std::string(v.str()));
+    return true;
+  });
 }
 
-uint64_t meta_hash(const Value* meta) {
+template <class N>
+uint64_t meta_hash(N meta) {
   uint64_t h = 0x51ed270b27cd1f47ull;
-  if (!meta || meta->t != Value::Obj) return hash(meta ? *meta : Value(), h);
-  for (const auto& m : meta->obj) {
-    if (m.first == "resourceVersion" || m.first == "generation" || m.first == "managedFields") continue;
-    h = hash(m.second, hash(Value::str(m.first), h));
-  }
+  if (!meta || !meta.obj()) return meta.hash(h);
+  meta.each([&](std::string_view k, N v) {
+    if (k == "resourceVersion" || k == "generation" || k == "managedFields") return true;
+    h = v.hash(hash_text(k, hash_mix(h, Value::Str)));    // == hash(Value::str(k), h)
+    return true;
+  });
   return h;
+}
+
+bool quantity_text(std::string_view s, int scale, int64_t* out);
+
+template <class N>
+bool quantity_of(N q, int scale, int64_t* out) {
+  if (!q.str_t() && !q.num_t()) return false;
+  return quantity_text(q.str(), scale, out);
 }
 
 }  // namespace
 
-bool quantity_scaled(const Value& q, int scale, int64_t* out) {
-  std::string_view s;
-  if (q.t == Value::Str || q.t == Value::Num) s = q.s;
-  else return false;
+bool quantity_scaled(const Value& q, int scale, int64_t* out) { return quantity_of(DomN{&q}, scale, out); }
+
+namespace {
+
+bool quantity_text(std::string_view s, int scale, int64_t* out) {
   // Python: str(q).strip()
   while (!s.empty() && (s.front() == ' ' || s.front() == '\t' || s.front() == '\n')) s.remove_prefix(1);
   while (!s.empty() && (s.back() == ' ' || s.back() == '\t' || s.back() == '\n')) s.remove_suffix(1);
@@ -188,126 +250,142 @@ bool quantity_scaled(const Value& q, int scale, int64_t* out) {
   return ceil_scaled(n, e + scale, 0, out);
 }
 
-void project_pod(const Value& pod, PodProj& p) {
+template <class N>
+uint64_t spec_hash(N sp, uint64_t h) {
+  // a missing / non-object spec hashes as the empty object the DOM projection substitutes
+  return sp.obj() ? sp.hash(h) : hash_mix(hash_mix(h, Value::Obj), 0);
+}
+
+template <class N>
+void project_generic(N pod, PodProj& p) {
   p = PodProj();
-  static const Value kEmpty = Value::object();
-  const Value* meta = pod.get("metadata");
-  const Value* spec = pod.get("spec");
-  const Value& m = (meta && meta->t == Value::Obj) ? *meta : kEmpty;
-  const Value& sp = (spec && spec->t == Value::Obj) ? *spec : kEmpty;
-  p.ns = m.get("namespace") && m.get("namespace")->t == Value::Str ? m.get("namespace")->s : "default";
+  N meta = pod.get("metadata");
+  N spec = pod.get("spec");
+  const N m = meta.obj() ? meta : N{};
+  const N sp = spec.obj() ? spec : N{};
+  N nsv = m.get("namespace");
+  p.ns = nsv && nsv.str_t() ? std::string(nsv.str()) : "default";
   p.name = std::string(m.sv("name"));
   p.uid = std::string(m.sv("uid"));
   if (p.uid.empty()) p.uid = p.ns + "/" + p.name;
   p.rv = std::string(m.sv("resourceVersion"));
   p.creation = std::string(m.sv("creationTimestamp"));
-  if (const Value* d = m.get("deletionTimestamp")) p.deleting = d->truthy();
+  if (N d = m.get("deletionTimestamp")) p.deleting = d.truthy();
   std::string_view sched = sp.sv("schedulerName");
   p.sched = sched.empty() ? "default-scheduler" : std::string(sched);
   p.node = std::string(sp.sv("nodeName"));
-  if (const Value* st = pod.get("status")) p.phase = std::string(st->sv("phase"));
-  p.spec_meta_hash = hash(sp, meta_hash(meta));
+  if (N st = pod.get("status")) p.phase = std::string(st.sv("phase"));
+  p.spec_meta_hash = spec_hash(sp, meta_hash(meta));
 
   // ---- everything below: fall back to Python on any shape the projection does not mirror
   if (!kvs(m.get("labels"), p.labels)) return;
-  if (const Value* a = m.get("annotations"); a && a->truthy()) {
+  if (N a = m.get("annotations"); a && a.truthy()) {
     p.has_annotations = true;
     if (!kvs(a, p.annotations)) return;
-  } else if (a && a->t != Value::Null && a->t != Value::Obj) {
+  } else if (a && !a.null_t() && !a.obj()) {
     return;
   }
-  if (const Value* pr = sp.get("priority"); pr && pr->truthy()) {
+  if (N pr = sp.get("priority"); pr && pr.truthy()) {
     bool ok;
-    p.priority = pr->as_int(&ok);
-    if (!ok || pr->t != Value::Num) return;
+    p.priority = pr.as_int(&ok);
+    if (!ok || !pr.num_t()) return;
   }
   // requests: Σ containers, max with each init container, + overhead (models/pod.py::_requests)
   int64_t cpu = 0, mem = 0, nzc = 0, nzm = 0;
-  auto reqs_of = [](const Value& c) -> const Value* {
-    const Value* r = c.get("resources");
-    if (!r || !r->truthy()) return nullptr;
-    const Value* q = r->get("requests");
-    return (q && q->truthy()) ? q : nullptr;
+  auto reqs_of = [](N c) -> N {
+    N r = c.get("resources");
+    if (!r || !r.truthy()) return N{};
+    N q = r.get("requests");
+    return (q && q.truthy()) ? q : N{};
   };
-  auto ext_in = [](const Value* r) {
-    if (!r || r->t != Value::Obj) return false;
-    for (const auto& kv : r->obj)
-      if (!is_basic(kv.first)) return true;
-    return false;
+  auto ext_in = [](N r) {
+    if (!r || !r.obj()) return false;
+    bool ext = false;
+    r.each([&](std::string_view k, N) {
+      if (!is_basic(k)) ext = true;
+      return !ext;
+    });
+    return ext;
   };
   int flags = 0;
-  if (const Value* cs = sp.get("containers"); cs && cs->t == Value::Arr) {
-    for (const auto& c : cs->arr) {
-      if (c.t != Value::Obj) return;
-      const Value* r = reqs_of(c);
-      if (r && r->t != Value::Obj) return;
-      if (ext_in(r)) return;                          // extended resources: Python path
+  if (N cs = sp.get("containers"); cs && cs.arr()) {
+    bool ok = cs.each([&](std::string_view, N c) {
+      if (!c.obj()) return false;
+      N r = reqs_of(c);
+      if (r && !r.obj()) return false;
+      if (ext_in(r)) return false;                        // extended resources: Python path
       int64_t v;
-      if (const Value* q = r ? r->get("cpu") : nullptr) {
-        if (!quantity_scaled(*q, 3, &v)) return;
+      if (N q = r ? r.get("cpu") : N{}) {
+        if (!quantity_of(q, 3, &v)) return false;
         cpu += v;
         nzc += v;
       } else {
         nzc += kDefaultMilliCpu;
       }
-      if (const Value* q = r ? r->get("memory") : nullptr) {
-        if (!quantity_scaled(*q, 0, &v)) return;
+      if (N q = r ? r.get("memory") : N{}) {
+        if (!quantity_of(q, 0, &v)) return false;
         mem += v;
         nzm += v;
       } else {
         nzm += kDefaultMemory;
       }
-      if (const Value* ports = c.get("ports"); ports && ports->t == Value::Arr) {
-        for (const auto& pt : ports->arr) {
-          if (pt.t != Value::Obj) return;
-          const Value* hp = pt.get("hostPort");
-          if (!hp || !hp->truthy()) continue;
-          bool ok;
+      if (N ports = c.get("ports"); ports && ports.arr()) {
+        bool pok = ports.each([&](std::string_view, N pt) {
+          if (!pt.obj()) return false;
+          N hp = pt.get("hostPort");
+          if (!hp || !hp.truthy()) return true;
+          bool iok;
           PortP port;
-          port.host_port = hp->as_int(&ok);
-          if (!ok || hp->t != Value::Num) return;
-          const Value* proto = pt.get("protocol");
-          if (proto && proto->t != Value::Str) return;
-          port.protocol = proto ? proto->s : "TCP";
-          const Value* ip = pt.get("hostIP");
-          if (ip && ip->t != Value::Str) return;
-          port.host_ip = ip ? ip->s : "";
+          port.host_port = hp.as_int(&iok);
+          if (!iok || !hp.num_t()) return false;
+          N proto = pt.get("protocol");
+          if (proto && !proto.str_t()) return false;
+          port.protocol = proto ? std::string(proto.str()) : "TCP";
+          N ip = pt.get("hostIP");
+          if (ip && !ip.str_t()) return false;
+          port.host_ip = ip ? std::string(ip.str()) : "";
           p.ports.push_back(std::move(port));
-        }
+          return true;
+        });
+        if (!pok) return false;
       }
-    }
-  } else if (const Value* cs2 = sp.get("containers"); cs2 && cs2->truthy()) {
+      return true;
+    });
+    if (!ok) return;
+  } else if (N cs2 = sp.get("containers"); cs2 && cs2.truthy()) {
     return;
   }
-  if (const Value* ics = sp.get("initContainers"); ics && ics->t == Value::Arr) {
-    for (const auto& c : ics->arr) {
-      if (c.t != Value::Obj) return;
-      const Value* r = reqs_of(c);
-      if (r && r->t != Value::Obj) return;
-      if (ext_in(r)) return;
+  if (N ics = sp.get("initContainers"); ics && ics.arr()) {
+    bool ok = ics.each([&](std::string_view, N c) {
+      if (!c.obj()) return false;
+      N r = reqs_of(c);
+      if (r && !r.obj()) return false;
+      if (ext_in(r)) return false;
       int64_t v = 0;
-      const Value* q = r ? r->get("cpu") : nullptr;
-      if (q && !quantity_scaled(*q, 3, &v)) return;
+      N q = r ? r.get("cpu") : N{};
+      if (q && !quantity_of(q, 3, &v)) return false;
       if (!q) v = 0;
       cpu = std::max(cpu, v);
       nzc = std::max(nzc, q ? v : kDefaultMilliCpu);
-      q = r ? r->get("memory") : nullptr;
+      q = r ? r.get("memory") : N{};
       v = 0;
-      if (q && !quantity_scaled(*q, 0, &v)) return;
+      if (q && !quantity_of(q, 0, &v)) return false;
       mem = std::max(mem, v);
       nzm = std::max(nzm, q ? v : kDefaultMemory);
-    }
+      return true;
+    });
+    if (!ok) return;
   }
-  if (const Value* ov = sp.get("overhead"); ov && ov->truthy()) {
-    if (ov->t != Value::Obj || ext_in(ov)) return;
+  if (N ov = sp.get("overhead"); ov && ov.truthy()) {
+    if (!ov.obj() || ext_in(ov)) return;
     int64_t v;
-    if (const Value* q = ov->get("cpu")) {
-      if (!quantity_scaled(*q, 3, &v)) return;
+    if (N q = ov.get("cpu")) {
+      if (!quantity_of(q, 3, &v)) return;
       cpu += v;
       nzc += v;
     }
-    if (const Value* q = ov->get("memory")) {
-      if (!quantity_scaled(*q, 0, &v)) return;
+    if (N q = ov.get("memory")) {
+      if (!quantity_of(q, 0, &v)) return;
       mem += v;
       nzm += v;
     }
@@ -318,80 +396,85 @@ void project_pod(const Value& pod, PodProj& p) {
   p.nzm = nzm;
   if (!p.ports.empty()) flags |= PF_HOST_PORTS;
 
-  if (const Value* ns = sp.get("nodeSelector"); ns && ns->truthy()) {
+  if (N ns = sp.get("nodeSelector"); ns && ns.truthy()) {
     p.has_node_selector = true;
     if (!kvs(ns, p.node_selector)) return;
   }
-  if (const Value* aff = sp.get("affinity"); aff && aff->truthy()) {
-    if (aff->t != Value::Obj) return;
+  if (N aff = sp.get("affinity"); aff && aff.truthy()) {
+    if (!aff.obj()) return;
     p.has_affinity = true;
-    const Value* na = aff->get("nodeAffinity");
-    if (na && na->truthy()) {
-      if (na->t != Value::Obj) return;
-      const Value* rq = na->get("requiredDuringSchedulingIgnoredDuringExecution");
-      if (rq && rq->truthy()) {
-        if (rq->t != Value::Obj) return;
-        if (const Value* terms = rq->get("nodeSelectorTerms"); terms && terms->truthy()) {
-          if (terms->t != Value::Arr) return;
-          for (const auto& t : terms->arr) {
+    N na = aff.get("nodeAffinity");
+    if (na && na.truthy()) {
+      if (!na.obj()) return;
+      N rq = na.get("requiredDuringSchedulingIgnoredDuringExecution");
+      if (rq && rq.truthy()) {
+        if (!rq.obj()) return;
+        if (N terms = rq.get("nodeSelectorTerms"); terms && terms.truthy()) {
+          if (!terms.arr()) return;
+          bool ok = terms.each([&](std::string_view, N t) {
             TermP tp;
-            if (!term_of(&t, tp)) return;
+            if (!term_of(t, tp)) return false;
             p.req_terms.push_back(std::move(tp));
-          }
+            return true;
+          });
+          if (!ok) return;
         }
       }
-      if (const Value* pf = na->get("preferredDuringSchedulingIgnoredDuringExecution"); pf && pf->truthy()) {
-        if (pf->t != Value::Arr) return;
-        for (const auto& x : pf->arr) {
-          if (x.t != Value::Obj) return;
+      if (N pf = na.get("preferredDuringSchedulingIgnoredDuringExecution"); pf && pf.truthy()) {
+        if (!pf.arr()) return;
+        bool ok = pf.each([&](std::string_view, N x) {
+          if (!x.obj()) return false;
           int64_t w = 0;
-          if (const Value* wv = x.get("weight")) {
-            bool ok;
-            w = wv->as_int(&ok);
-            if (!ok || wv->t != Value::Num) return;
+          if (N wv = x.get("weight")) {
+            bool iok;
+            w = wv.as_int(&iok);
+            if (!iok || !wv.num_t()) return false;
           }
           TermP tp;
-          const Value* pref = x.get("preference");
-          if (pref && pref->t != Value::Obj && pref->t != Value::Null) return;
-          if (!term_of(pref && pref->truthy() ? pref : nullptr, tp)) return;
+          N pref = x.get("preference");
+          if (pref && !pref.obj() && !pref.null_t()) return false;
+          if (!term_of(pref && pref.truthy() ? pref : N{}, tp)) return false;
           p.pref_terms.emplace_back(w, std::move(tp));
-        }
+          return true;
+        });
+        if (!ok) return;
       }
     }
-    const Value* pa = aff->get("podAffinity");
-    const Value* paa = aff->get("podAntiAffinity");
-    if ((pa && pa->truthy()) || (paa && paa->truthy())) flags |= PF_POD_AFFINITY;
-    if (paa && paa->t == Value::Obj) {
-      if (const Value* r = paa->get("requiredDuringSchedulingIgnoredDuringExecution"); r && r->truthy())
-        flags |= PF_REQ_ANTI;
+    N pa = aff.get("podAffinity");
+    N paa = aff.get("podAntiAffinity");
+    if ((pa && pa.truthy()) || (paa && paa.truthy())) flags |= PF_POD_AFFINITY;
+    if (paa && paa.obj()) {
+      if (N r = paa.get("requiredDuringSchedulingIgnoredDuringExecution"); r && r.truthy()) flags |= PF_REQ_ANTI;
     }
   }
-  if (const Value* tols = sp.get("tolerations"); tols && tols->truthy()) {
-    if (tols->t != Value::Arr) return;
-    for (const auto& t : tols->arr) {
-      if (t.t != Value::Obj) return;
+  if (N tols = sp.get("tolerations"); tols && tols.truthy()) {
+    if (!tols.arr()) return;
+    bool ok = tols.each([&](std::string_view, N t) {
+      if (!t.obj()) return false;
       TolP tp;
-      const Value* k = t.get("key");
-      if (k && k->t != Value::Str && k->t != Value::Null) return;
-      tp.has_key = k && k->t == Value::Str && !k->s.empty();
-      if (tp.has_key) tp.key = k->s;
-      const Value* v = t.get("value");
-      if (v && v->t != Value::Str && v->t != Value::Null) return;
-      tp.value = (v && v->t == Value::Str) ? v->s : "";
-      const Value* op = t.get("operator");
-      if (op && op->t != Value::Str && op->t != Value::Null) return;
-      tp.op = (op && op->t == Value::Str && !op->s.empty()) ? op->s : "Equal";
-      const Value* ef = t.get("effect");
-      if (ef && ef->t != Value::Str && ef->t != Value::Null) return;
-      tp.effect = (ef && ef->t == Value::Str) ? ef->s : "";
+      N k = t.get("key");
+      if (k && !k.str_t() && !k.null_t()) return false;
+      tp.has_key = k && k.str_t() && !k.str().empty();
+      if (tp.has_key) tp.key = std::string(k.str());
+      N v = t.get("value");
+      if (v && !v.str_t() && !v.null_t()) return false;
+      tp.value = (v && v.str_t()) ? std::string(v.str()) : "";
+      N op = t.get("operator");
+      if (op && !op.str_t() && !op.null_t()) return false;
+      tp.op = (op && op.str_t() && !op.str().empty()) ? std::string(op.str()) : "Equal";
+      N ef = t.get("effect");
+      if (ef && !ef.str_t() && !ef.null_t()) return false;
+      tp.effect = (ef && ef.str_t()) ? std::string(ef.str()) : "";
       p.tolerations.push_back(std::move(tp));
-    }
+      return true;
+    });
+    if (!ok) return;
   }
-  if (const Value* tsc = sp.get("topologySpreadConstraints"); tsc && tsc->truthy()) flags |= PF_SPREAD;
-  if (const Value* vols = sp.get("volumes"); vols && vols->t == Value::Arr) {
+  if (N tsc = sp.get("topologySpreadConstraints"); tsc && tsc.truthy()) flags |= PF_SPREAD;
+  if (N vols = sp.get("volumes"); vols && vols.arr()) {
     static const char* kDisks[] = {"gcePersistentDisk", "awsElasticBlockStore", "azureDisk", "cinder", "iscsi", "rbd"};
-    for (const auto& v : vols->arr) {
-      if (v.t != Value::Obj) return;
+    bool ok = vols.each([&](std::string_view, N v) {
+      if (!v.obj()) return false;
       if (v.get("persistentVolumeClaim") || v.get("ephemeral")) {
         flags |= PF_CLAIMS;
       } else {
@@ -401,21 +484,38 @@ void project_pod(const Value& pod, PodProj& p) {
             break;
           }
       }
-    }
+      return true;
+    });
+    if (!ok) return;
   }
   for (const auto& kv : p.labels)
     if (kv.first == "pod-group.scheduling.sigs.k8s.io") flags |= PF_POD_GROUP;
-  if (const Value* owners = m.get("ownerReferences"); owners && owners->t == Value::Arr) {
-    for (const auto& r : owners->arr) {
-      if (r.t != Value::Obj) return;
-      const Value* c = r.get("controller");
+  if (N owners = m.get("ownerReferences"); owners && owners.arr()) {
+    bool ok = owners.each([&](std::string_view, N r) {
+      if (!r.obj()) return false;
+      N c = r.get("controller");
       std::string_view kind = r.sv("kind");
-      if (c && c->truthy() && (kind == "ReplicationController" || kind == "ReplicaSet" || kind == "StatefulSet"))
+      if (c && c.truthy() && (kind == "ReplicationController" || kind == "ReplicaSet" || kind == "StatefulSet"))
         flags |= PF_CONTROLLER;
-    }
+      return true;
+    });
+    if (!ok) return;
   }
   p.flags = flags;
   p.ok = true;
+}
+
+}  // namespace
+
+void project_pod(const Value& pod, PodProj& p) { project_generic(DomN{&pod}, p); }
+
+void project_pod(const FlatDoc::View& pod, PodProj& p) { project_generic(FlatN{pod}, p); }
+
+bool project_pod_text(std::string_view text, PodProj& p) {
+  FlatDoc d;
+  if (!d.parse(text)) return false;
+  project_pod(d.root(), p);
+  return true;
 }
 
 }  // namespace yk

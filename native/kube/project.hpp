@@ -10,6 +10,7 @@
 #include <utility>
 #include <vector>
 
+#include "flatjson.hpp"
 #include "json.hpp"
 
 namespace yk {
@@ -71,5 +72,9 @@ bool quantity_scaled(const Value& q, int scale, int64_t* out);
 // Fills `p` from a decoded pod object. Identity fields (uid/ns/name/rv/node/phase/sched,
 // hash) are always set; `p.ok` tells whether the rest is complete.
 void project_pod(const Value& pod, PodProj& p);
+// The same projection over the flat document (the watch stream's decode path).
+void project_pod(const FlatDoc::View& pod, PodProj& p);
+// Parse + project one pod object's JSON text; false when the text is not JSON.
+bool project_pod_text(std::string_view text, PodProj& p);
 
 }  // namespace yk

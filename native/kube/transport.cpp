@@ -20,6 +20,7 @@
 #include <cstring>
 #include <stdexcept>
 
+#include "flatjson.hpp"
 #include "http.hpp"
 #include "json.hpp"
 
@@ -564,53 +565,13 @@ void Transport::on_body(Conn* c, const char* data, size_t n) {
   }
 }
 
-namespace {
-
-// {"type":"ADDED","object":{...}} → type, object value, object JSON slice
-bool parse_event_line(std::string_view line, std::string& type, Value& obj, std::string_view& raw) {
-  size_t pos = 0;
-  auto ws = [&] {
-    while (pos < line.size() && (line[pos] == ' ' || line[pos] == '\t' || line[pos] == '\r')) ++pos;
-  };
-  ws();
-  if (pos >= line.size() || line[pos] != '{') return false;
-  ++pos;
-  bool have_obj = false;
-  while (true) {
-    ws();
-    if (pos < line.size() && line[pos] == '}') break;
-    Value key = parse_prefix(line, &pos);
-    if (key.t != Value::Str) return false;
-    ws();
-    if (pos >= line.size() || line[pos] != ':') return false;
-    ++pos;
-    ws();
-    size_t start = pos;
-    Value v = parse_prefix(line, &pos);
-    if (key.s == "type") {
-      if (v.t != Value::Str) return false;
-      type = v.s;
-    } else if (key.s == "object") {
-      obj = std::move(v);
-      raw = line.substr(start, pos - start);
-      have_obj = true;
-    }
-    ws();
-    if (pos < line.size() && line[pos] == ',') {
-      ++pos;
-      continue;
-    }
-    if (pos < line.size() && line[pos] == '}') break;
-    return false;
-  }
-  return have_obj && !type.empty();
-}
-
-}  // namespace
 
 void Transport::watch_lines(Conn* c) {
+  // one flat parse per event line ({"type":..., "object":{...}}): no per-value allocation;
+  // pods are projected from the same document (project.hpp)
   size_t start = 0;
   uint64_t nev = 0, nerr = 0;
+  FlatDoc doc;
   while (true) {
     size_t nl = c->lines.find('\n', start);
     if (nl == std::string::npos) break;
@@ -623,19 +584,18 @@ void Transport::watch_lines(Conn* c) {
         break;
       }
     if (blank) continue;
-    std::string type;
-    Value obj;
-    std::string_view raw;
-    bool ok = false;
-    try {
-      ok = parse_event_line(line, type, obj, raw);
-    } catch (const ParseError&) {
-      ok = false;
-    }
-    if (!ok) {
+    if (!doc.parse(line) || !doc.root().is(FlatDoc::Obj)) {
       nerr++;
       continue;
     }
+    const FlatDoc::View root = doc.root();
+    const FlatDoc::View tv = root.get("type");
+    const FlatDoc::View obj = root.get("object");
+    if (!tv || !tv.is(FlatDoc::Str) || !obj) {
+      nerr++;
+      continue;
+    }
+    const std::string_view type = tv.str();
     WatchEvent ev;
     ev.type = type == "ADDED" ? 'A' : type == "MODIFIED" ? 'M' : type == "DELETED" ? 'D'
               : type == "BOOKMARK" ? 'B' : type == "ERROR" ? 'E' : '?';
@@ -643,7 +603,8 @@ void Transport::watch_lines(Conn* c) {
       nerr++;
       continue;
     }
-    if (const Value* m = obj.get("metadata")) ev.rv = std::string(m->sv("resourceVersion"));
+    if (const FlatDoc::View m = obj.get("metadata")) ev.rv = std::string(m.sv("resourceVersion"));
+    const std::string_view raw = obj.raw();
     if (c->pods && ev.type != 'B' && ev.type != 'E') {
       auto pe = std::make_shared<PodEv>();
       project_pod(obj, pe->p);

@@ -169,6 +169,31 @@ def test_pod_projection_matches_from_obj(pod):
     assert (key, uid, node, sched) == (want.key, want.uid, want.node_name, want.scheduler_name)
 
 
+@settings(max_examples=250, deadline=None)
+@given(_pod, st.sampled_from([{}, {"phase": "Pending"}, {"phase": "Running", "podIP": "10.0.0.1"}]),
+       st.booleans())
+def test_flat_projection_equals_dom_projection(pod, status, pretty):
+    """The watch stream decodes pods with the flat document (flatjson.hpp); every field of
+    its projection — including the spec/metadata hash and the fallback decision — equals the
+    DOM projection's, on compact and indented JSON and with escaped strings."""
+    pod = dict(pod, status=status)
+    pod["metadata"] = dict(pod["metadata"], annotations={**(pod["metadata"].get("annotations") or {}),
+                                                         "note": "tab\there \"q\" \u00e9\u2603"})
+    raw = json.dumps(pod, indent=2 if pretty else None, ensure_ascii=pretty)
+    a, b = K.project(raw), K.project_flat(raw)
+    assert a.ident() == b.ident() and a.ok == b.ok and a.flags == b.flags and a.rv == b.rv
+    assert a.info_args() == b.info_args()
+    assert a.hash == b.hash
+
+
+def test_flat_projection_rejects_malformed_json_like_the_dom():
+    for bad in ['{"metadata": {"name": "p"}', '{"a": tru}', '{"a": "x\\q"}', '[1, 2,]', '{"a": 01}', '"\x01"']:
+        with pytest.raises(ValueError):
+            K.project_flat(bad)
+        with pytest.raises(ValueError):
+            K.project(bad)
+
+
 def test_projection_hash_ignores_volatile_metadata_and_status():
     base = {"metadata": {"name": "p", "resourceVersion": "1", "labels": {"a": "b"}},
             "spec": {"containers": [{"name": "c"}]}, "status": {"phase": "Pending"}}

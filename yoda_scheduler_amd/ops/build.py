@@ -43,20 +43,21 @@ ARCH = os.environ.get("YODA_HIP_ARCH", "gfx950")
 # Per artefact: output name, the sources compiled, every file whose contents define the
 # artefact (sources + headers), and a recipe tag (bump it when the compile flags change).
 CORE_SRCS = ["core/engine.cpp", "core/lane.cpp", "core/bindings.cpp"]
-KUBE_COMMON = ["kube/json.cpp", "kube/project.cpp"]
+KUBE_COMMON = ["kube/json.cpp", "kube/flatjson.cpp", "kube/project.cpp"]
 ARTEFACTS: dict[str, dict] = {
     "core": {"out": f"_yoda_core{EXT}", "srcs": CORE_SRCS,
              "deps": CORE_SRCS + ["core/engine.hpp", "core/lane.hpp", "hip/yoda_dev_abi.h", "kube/project.hpp",
-                                  "kube/json.hpp", "kube/lane_port.hpp", "common/build_id.h"],
+                                  "kube/json.hpp", "kube/flatjson.hpp", "kube/lane_port.hpp", "common/build_id.h"],
              "recipe": "g++ -O3 -std=c++17 -fPIC -shared -fvisibility=hidden v2"},
     "kube": {"out": f"_yoda_kube{EXT}", "srcs": KUBE_COMMON + ["kube/transport.cpp", "kube/bindings.cpp"],
              "deps": KUBE_COMMON + ["kube/transport.cpp", "kube/bindings.cpp", "kube/json.hpp", "kube/http.hpp",
-                                    "kube/project.hpp", "kube/transport.hpp", "kube/lane_port.hpp",
+                                    "kube/project.hpp", "kube/flatjson.hpp", "kube/transport.hpp", "kube/lane_port.hpp",
                                     "common/build_id.h"],
              "recipe": "g++ -O3 -std=c++17 -fPIC -shared -fvisibility=hidden -lssl -lcrypto v2"},
     "fakeapi": {"out": "yoda-fake-apiserver-native", "srcs": KUBE_COMMON + ["kube/fakeapi.cpp", "kube/fakeapi_main.cpp"],
                 "deps": KUBE_COMMON + ["kube/fakeapi.cpp", "kube/fakeapi_main.cpp", "kube/fakeapi.hpp",
-                                       "kube/json.hpp", "kube/http.hpp", "common/build_id.h"],
+                                       "kube/json.hpp", "kube/flatjson.hpp", "kube/project.hpp", "kube/http.hpp",
+                                       "common/build_id.h"],
                 "recipe": "g++ -O3 -std=c++17 v2"},
     "sniffer": {"out": f"_yoda_sniffer{EXT}", "srcs": ["sniffer/collector.cpp", "sniffer/bindings.cpp"],
                 "deps": ["sniffer/collector.cpp", "sniffer/collector.hpp", "sniffer/bindings.cpp",
