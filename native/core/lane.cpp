@@ -986,7 +986,11 @@ void Lane::run() {
       if (!ready()) {
         if (!ev_q_.empty() && o_.event_qps > 0) {
           const double wait = std::max(0.0005, (1.0 - ev_tokens_) / o_.event_qps);
-          in_cv_.wait_for(lk, std::chrono::duration<double>(wait), ready);
+          // system_clock deadline: pthread_cond_timedwait (steady-clock waits use
+          // pthread_cond_clockwait, which ThreadSanitizer does not model)
+          in_cv_.wait_until(lk, std::chrono::system_clock::now() +
+                                    std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                                        std::chrono::duration<double>(wait)), ready);
         } else {
           in_cv_.wait(lk, ready);
         }

@@ -73,10 +73,42 @@ def run(variant: str, nodes: int = 700, steps: int = 2000, threads: int = 4) -> 
     return r.returncode
 
 
+KUBE = os.path.join(ROOT, "native", "kube")
+COMMON = os.path.join(ROOT, "native", "common")
+
+
+def run_lane(variant: str, bursts: int = 6, pods: int = 400) -> int:
+    """The native pod lane (native/core/lane_stress.cpp): lane thread, a fake transport I/O
+    thread answering Bindings and echoing pods, and the caller feeding bursts and deletions —
+    the ledger must be exact after every burst and every deletion wave."""
+    flags = VARIANTS[variant]
+    out = os.path.join(tempfile.gettempdir(), f"yoda_lane_stress_{variant}")
+    srcs = [os.path.join(CORE, f) for f in ("lane_stress.cpp", "lane.cpp", "engine.cpp")] + \
+        [os.path.join(KUBE, f) for f in ("json.cpp", "flatjson.cpp", "project.cpp")]
+    cmd = ["g++", "-std=c++17", "-O1", "-g", *flags, f"-I{CORE}", f"-I{HIP}", f"-I{KUBE}", f"-I{COMMON}", *srcs,
+           "-o", out, "-lpthread", "-ldl"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stderr)
+        return r.returncode
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1",
+               TSAN_OPTIONS="halt_on_error=1")
+    env.pop("LD_PRELOAD", None)
+    argv = [out, str(bursts), str(pods), "64"]
+    if variant == "tsan" and shutil.which("setarch"):
+        argv = ["setarch", os.uname().machine, "-R", *argv]
+    r = subprocess.run(argv, capture_output=True, text=True, env=env, timeout=600)
+    sys.stdout.write(f"[lane-{variant}] {r.stdout}")
+    if r.returncode != 0:
+        sys.stderr.write(r.stderr[-4000:])
+    return r.returncode
+
+
 def main() -> int:
     rc = 0
     for v in VARIANTS:
         rc |= run(v)
+        rc |= run_lane(v)
     rc |= run_sniffer()
     return rc
 
