@@ -75,6 +75,28 @@ def _telemetry_template(local_rank: int) -> tuple[dict | None, dict]:
         return None, info
 
 
+def thread_cpu() -> dict:
+    """CPU seconds per thread name of this process (/proc/self/task: the native threads are
+    named yoda-io / yoda-lane / yoda-engine; Python's own threads keep the process name)."""
+    out: dict = {}
+    tick = os.sysconf("SC_CLK_TCK")
+    base = "/proc/self/task"
+    try:
+        tids = os.listdir(base)
+    except OSError:
+        return out
+    for tid in tids:
+        try:
+            with open(f"{base}/{tid}/comm") as f:
+                name = f.read().strip()
+            with open(f"{base}/{tid}/stat") as f:
+                fields = f.read().rsplit(")", 1)[1].split()
+            out[name] = out.get(name, 0.0) + (int(fields[11]) + int(fields[12])) / tick
+        except (OSError, IndexError, ValueError):
+            continue
+    return out
+
+
 def rank_gpu_index(local_rank: int, n_visible: int) -> int:
     """GPU of a rank: LOCAL_RANK modulo the visible devices (one rank per GPU under
     torch.distributed.run; several ranks share a GPU only in CPU/gloo rehearsals)."""
@@ -186,6 +208,7 @@ def main(argv=None) -> int:
 
         sync()
         a0 = api_cpu()
+        th0 = thread_cpu()
         t0 = time.perf_counter()
         c0 = time.process_time()
         results = [loop.run_until_complete(shards[a.warmup + i].burst(f"s{i}")) for i in range(a.steps)]
@@ -193,6 +216,10 @@ def main(argv=None) -> int:
         elapsed = time.perf_counter() - t0
         cpu_s = time.process_time() - c0     # this rank's process: scheduler (+ in-process apiserver)
         api_s = api_cpu() - a0
+        th1 = thread_cpu()
+        my_bound = sum(r.bound for r in results)
+        threads = {k: round((v - th0.get(k, 0.0)) / my_bound * 1e6, 2) for k, v in sorted(th1.items())
+                   if my_bound and v - th0.get(k, 0.0) > 0}
 
         uniq = {id(x): x for x in shards}.values()
         device_cycles = sum(s.sched.engine.device_cycles for s in uniq)
@@ -234,6 +261,8 @@ def main(argv=None) -> int:
             # process CPU time per bound pod, summed over ranks: with --transport http this is
             # the scheduler alone (the apiserver is another process); inproc includes the fake apiserver
             "cpu_us_per_pod": round(cpu_s / bound * 1e6, 2) if bound else None,
+            # rank 0's process CPU per pod by thread (≥ 10 ms clock-tick resolution per thread)
+            "thread_cpu_us_per_pod": threads,
             # the fake apiserver's own CPU (separate process, http transport; rank 0's)
             **({"apiserver_cpu_us_per_pod": round(api_s / (bound / max(world, 1)) * 1e6, 2)
                 if bound and api_s == api_s else None} if transport == "http" else {}),

@@ -5,6 +5,7 @@
 #include <deque>
 #include <memory>
 #include <sys/eventfd.h>
+#include <pthread.h>
 #include <unistd.h>
 #include <mutex>
 #include <thread>
@@ -123,7 +124,10 @@ class BatchWorker {
   explicit BatchWorker(Engine* e) : e_(e) {
     efd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     if (efd_ < 0) throw std::runtime_error("eventfd failed");
-    th_ = std::thread([this] { run(); });
+    th_ = std::thread([this] {
+    pthread_setname_np(pthread_self(), "yoda-engine");   // per-thread CPU in bench / top -H
+    run();
+  });
   }
   ~BatchWorker() { close(); }
 
@@ -568,6 +572,7 @@ PYBIND11_MODULE(_yoda_core, m) {
       .def("keys", &Lane::keys, py::call_guard<py::gil_scoped_release>())
       .def("__len__", &Lane::store_size, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("scheduled", [](Lane& l) { return l.scheduled_.load(std::memory_order_relaxed); })
+      .def("set_watermark", &Lane::set_watermark, "signal the eventfd once this many Bindings are acknowledged")
       .def("stats",
            [](Lane& l) {
              LaneStats s = l.stats();

@@ -2,6 +2,7 @@
 #include "lane.hpp"
 
 #include <sys/eventfd.h>
+#include <pthread.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -134,7 +135,10 @@ Lane::Lane(Engine* e, std::recursive_mutex* engine_mu, LaneOptions o) : eng_(e),
   if (efd_ < 0) throw std::runtime_error("eventfd failed");
   ev_tokens_ = o_.event_burst > 0 ? o_.event_burst : 1;
   ev_last_ = mono();
-  th_ = std::thread([this] { run(); });
+  th_ = std::thread([this] {
+    pthread_setname_np(pthread_self(), "yoda-lane");   // per-thread CPU in bench / top -H
+    run();
+  });
 }
 
 Lane::~Lane() { close(); }
@@ -208,14 +212,16 @@ void Lane::on_pod_events(uint64_t, std::vector<yk::WatchEvent>& evs) {
   evs.resize(kept);
 }
 
-void Lane::on_answer(uint64_t tag, int status, std::string&& body) {
+void Lane::on_answers(std::vector<yk::PodSink::Answer>& answers) {
   std::lock_guard<std::mutex> g(in_mu_);
-  Item it;
-  it.k = Item::kAnswer;
-  it.tag = tag;
-  it.status = status;
-  it.body = std::move(body);
-  inbox_.push_back(std::move(it));
+  for (auto& a : answers) {
+    Item it;
+    it.k = Item::kAnswer;
+    it.tag = a.tag;
+    it.status = a.status;
+    it.body = std::move(a.body);
+    inbox_.push_back(std::move(it));
+  }
   in_cv_.notify_one();
 }
 
@@ -398,11 +404,11 @@ void Lane::handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::ve
     auto e = std::make_unique<Entry>();
     e->ev = ev;
     int prof = -1;
-    if (active_admission_ && admissible(p, &prof)) {
+    if (active_admission_ && admissible(ev->full(), &prof)) {
       e->st = QUEUED;
       e->id = next_id_++;
       e->prof = prof;
-      e->prio = prio_of(p);
+      e->prio = prio_of(ev->full());
       e->seq = ++seq_;
       e->t_enq = mono();
       by_id_[e->id] = e.get();
@@ -425,9 +431,9 @@ void Lane::handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::ve
   }
   // lane-owned
   if (p.node.empty()) {
-    if (e->st == QUEUED && p.spec_meta_hash != old->p.spec_meta_hash) {
+    if (e->st == QUEUED && ev->full().spec_meta_hash != old->full().spec_meta_hash) {
       int prof = -1;
-      if (!admissible(p, &prof)) {
+      if (!admissible(ev->full(), &prof)) {
         // no longer for the lane (a feature a Python plugin handles, another scheduler, ...)
         drop_owned(e, false);
         e->ev = ev;
@@ -435,12 +441,13 @@ void Lane::handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::ve
         return;
       }
       e->prof = prof;
-      const int64_t pr = prio_of(p);
+      const int64_t pr = prio_of(ev->full());
       if (pr != e->prio) {                 // re-sorted, FIFO position kept (activeQ.Update)
         e->prio = pr;
         heap_.push(QItem{e->prio, e->seq, e->id});
       }
     }
+    ev->full();                            // a queued / assumed pod's event must stay complete
     e->ev = ev;                            // assumed pods: status noise only (skipPodUpdate)
     return;
   }
@@ -530,7 +537,8 @@ void Lane::handle_answer(uint64_t tag, int status, std::string& body) {
       st_.scheduled++;
       if (e2e_.size() < o_.e2e_keep) e2e_.push_back((float)(now - e->t_cycle));
     }
-    scheduled_.fetch_add(1, std::memory_order_relaxed);
+    if (scheduled_.fetch_add(1, std::memory_order_relaxed) + 1 == watermark_.load(std::memory_order_relaxed))
+      signal_python();
     record_scheduled(*e);
     return;
   }
@@ -589,7 +597,7 @@ void Lane::apply_profiles(std::vector<Fwd>* out) {
     Entry* e = kv.second;
     if (e->st != QUEUED) continue;
     int prof = -1;
-    if (!admissible(e->ev->p, &prof)) evict.push_back(e);
+    if (!admissible(e->ev->full(), &prof)) evict.push_back(e);
     else e->prof = prof;
   }
   for (Entry* e : evict) {
@@ -744,7 +752,7 @@ void Lane::schedule_some() {
       std::unique_lock<std::recursive_mutex> lk(*emu_);
       for (size_t k = 0; k < n; ++k) {
         try {
-          ok[k] = make_req(run[i + k]->ev->p, &reqs[k]);
+          ok[k] = make_req(run[i + k]->ev->full(), &reqs[k]);
         } catch (const std::exception&) {
           ok[k] = 0;
         }
@@ -884,6 +892,24 @@ std::vector<Lane::Change> Lane::changes(bool* full) {
   }
   *full = true;
   return out;
+}
+
+void Lane::signal_python() {
+  bool sig = false;
+  {
+    std::lock_guard<std::mutex> g(out_mu_);
+    if (!signalled_) signalled_ = sig = true;
+  }
+  if (sig) {
+    const uint64_t one = 1;
+    ssize_t w = ::write(efd_, &one, sizeof one);
+    (void)w;
+  }
+}
+
+void Lane::set_watermark(uint64_t n) {
+  watermark_.store(n, std::memory_order_relaxed);
+  if (scheduled_.load(std::memory_order_relaxed) >= n) signal_python();
 }
 
 void Lane::pause(bool on) {

@@ -104,7 +104,7 @@ class Lane : public yk::PodSink {
 
   // ---- yk::PodSink (transport I/O thread)
   void on_pod_events(uint64_t watch_id, std::vector<yk::WatchEvent>& evs) override;
-  void on_answer(uint64_t tag, int status, std::string&& body) override;
+  void on_answers(std::vector<yk::PodSink::Answer>& answers) override;
 
   // ---- Python side
   int fileno() const { return efd_; }
@@ -192,6 +192,7 @@ class Lane : public yk::PodSink {
   void flush_events();
   void forward(char type, std::shared_ptr<yk::PodEv> ev, std::shared_ptr<yk::PodEv> old, std::vector<Fwd>* out);
   void publish(std::vector<Fwd>&& fwd, std::vector<Handoff>&& hand);
+  void signal_python();
   static double mono();
 
   Engine* eng_;
@@ -242,6 +243,9 @@ class Lane : public yk::PodSink {
   uint64_t out_moves_pending_ = 0;
  public:
   std::atomic<uint64_t> scheduled_{0};               // Bindings acknowledged (incl. lost answers kept)
+  // the lane signals its eventfd once scheduled_ reaches this (a waiter on the Python side)
+  std::atomic<uint64_t> watermark_{UINT64_MAX};
+  void set_watermark(uint64_t n);
  private:
 
   std::mutex out_mu_;

@@ -126,10 +126,12 @@ int main(int argc, char** argv) {
         q.swap(port.q);
         evs.swap(port.events);
       }
-      for (auto& x : evs) x.second->on_answer(x.first, 201, std::string());
+      std::vector<yk::PodSink::Answer> ans;
+      for (auto& x : evs) ans.push_back({x.first, 201, std::string()});
+      for (auto& b : q) ans.push_back({b.tag, 201, std::string()});
+      if (!ans.empty()) lane.on_answers(ans);
       std::vector<yk::WatchEvent> echo;
       for (auto& b : q) {
-        b.sink->on_answer(b.tag, 201, std::string());
         yk::WatchEvent w;
         w.type = 'M';
         const int rv = ++port.rv;

@@ -80,7 +80,7 @@ PYBIND11_MODULE(_yoda_kube, m) {
   m.doc() = "Native Kubernetes API transport: pipelined HTTP/1.1 (+TLS), watch decoding, pod projection";
 
   py::class_<PodEv, std::shared_ptr<PodEv>>(m, "PodEvent")
-      .def_property_readonly("ok", [](const PodEv& e) { return e.p.ok; })
+      .def_property_readonly("ok", [](const PodEv& e) { return e.full().ok; })
       .def_property_readonly("uid", [](const PodEv& e) { return e.p.uid; })
       .def_property_readonly("namespace", [](const PodEv& e) { return e.p.ns; })
       .def_property_readonly("name", [](const PodEv& e) { return e.p.name; })
@@ -90,17 +90,19 @@ PYBIND11_MODULE(_yoda_kube, m) {
       .def_property_readonly("scheduler", [](const PodEv& e) { return e.p.sched; })
       .def_property_readonly("phase", [](const PodEv& e) { return e.p.phase; })
       .def_property_readonly("deleting", [](const PodEv& e) { return e.p.deleting; })
-      .def_property_readonly("hash", [](const PodEv& e) { return e.p.spec_meta_hash; })
-      .def_property_readonly("flags", [](const PodEv& e) { return e.p.flags; })
+      .def_property_readonly("hash", [](const PodEv& e) { return e.full().spec_meta_hash; })
+      .def_property_readonly("flags", [](const PodEv& e) { return e.full().flags; })
       // (key, uid, node, scheduler, phase, hash): the per-event fields in one call
       .def("ident", [](const PodEv& e) {
-        return py::make_tuple(py::str(e.p.ns + "/" + e.p.name), py::str(e.p.uid), py::str(e.p.node),
-                              py::str(e.p.sched), py::str(e.p.phase), e.p.spec_meta_hash);
+        const PodProj& p = e.full();
+        return py::make_tuple(py::str(p.ns + "/" + p.name), py::str(p.uid), py::str(p.node),
+                              py::str(p.sched), py::str(p.phase), p.spec_meta_hash);
       })
       .def("raw", [](const PodEv& e) { return py::bytes(e.raw); })
       .def("info_args", [](const PodEv& e) -> py::object {
-        if (!e.p.ok) return py::none();
-        return info_args(e.p);
+        const PodProj& p = e.full();
+        if (!p.ok) return py::none();
+        return info_args(p);
       });
 
   m.def("project", &project_bytes, py::arg("raw"), "Project a pod's JSON (tests / tooling).");
@@ -253,7 +255,7 @@ PYBIND11_MODULE(_yoda_kube, m) {
               py::object payload, ident = py::none();
               if (e.pod) {
                 payload = py::cast(e.pod);
-                const PodProj& p = e.pod->p;
+                const PodProj& p = e.pod->full();
                 ident = py::make_tuple(py::str(p.ns + "/" + p.name), py::str(p.uid), py::str(p.node), py::str(p.sched),
                                        py::str(p.phase), p.spec_meta_hash);
               } else if (e.type == 'B') {
@@ -264,6 +266,8 @@ PYBIND11_MODULE(_yoda_kube, m) {
               evs.append(py::make_tuple(types[ti], py::str(e.rv), payload, ident));
             }
             out.append(py::make_tuple(1, c.id, evs));
+          } else if (c.kind == Completion::kWatchEnd) {
+            out.append(py::make_tuple(int(c.kind), c.id, c.status, py::bytes(c.body), py::str(c.rv)));
           } else {
             out.append(py::make_tuple(int(c.kind), c.id, c.status, py::bytes(c.body)));
           }

@@ -5,7 +5,7 @@
 //
 //   transport I/O thread ──on_pod_events──► lane (takes every pod watch event)
 //   lane thread ──bind_native / request_native──► transport (Bindings, Scheduled events)
-//   transport I/O thread ──on_answer──► lane (the apiserver's answers, by tag)
+//   transport I/O thread ──on_answers──► lane (the apiserver's answers, by tag, per loop turn)
 //
 // Both callbacks run on the transport's I/O thread with the transport's sink lock held;
 // they must only enqueue (never block, never call back into the transport).
@@ -13,6 +13,7 @@
 
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -23,6 +24,17 @@ namespace yk {
 struct PodEv {
   PodProj p;
   std::string raw;             // the pod object's JSON text
+  // A "light" event carries only the identity fields (ns, name, uid, rv, node, scheduler,
+  // phase, deletion, creation) — what the lane reads of a Binding's echo or a deletion. The
+  // rest (labels, requests, selectors, flags, spec/metadata hash, ok) is projected from `raw`
+  // on first use through full(), once, thread-safely; identity fields are never rewritten.
+  bool light = false;
+  void (*complete)(PodEv*) = nullptr;
+  mutable std::once_flag once;
+  const PodProj& full() const {
+    if (light && complete) std::call_once(once, [this] { complete(const_cast<PodEv*>(this)); });
+    return p;
+  }
 };
 
 struct WatchEvent {
@@ -44,18 +56,24 @@ class PodSink {
   // (erasing them); what is left (bookmarks, errors, and any pod event it declines) goes
   // to the Python informer as before, in order.
   virtual void on_pod_events(uint64_t watch_id, std::vector<WatchEvent>& evs) = 0;
-  // The answer to a request submitted through PodPort with this sink: HTTP status, or -1
-  // (connection failed / closed) / -2 (timed out) with a reason in `body`.
-  virtual void on_answer(uint64_t tag, int status, std::string&& body) = 0;
+  // Answers to requests submitted through PodPort with this sink, batched per I/O loop turn
+  // (one hand-off and at most one wake-up of the consumer per turn, not one per response):
+  // HTTP status, or -1 (connection failed / closed) / -2 (timed out) with a reason in `body`.
+  struct Answer {
+    uint64_t tag;
+    int status;
+    std::string body;
+  };
+  virtual void on_answers(std::vector<Answer>& answers) = 0;
 };
 
 class PodPort {
  public:
   virtual ~PodPort() = default;
-  // Binding POSTs (client rate limit applies), answered through sink->on_answer(tags[k]).
+  // Binding POSTs (client rate limit applies), answered through sink->on_answers (tags[k]).
   virtual void bind_native(std::vector<BindSpec>&& binds, const std::vector<uint64_t>& tags, double timeout_s,
                            PodSink* sink) = 0;
-  // Any other request (events); answered through sink->on_answer(tag).
+  // Any other request (events); answered through sink->on_answers (tag).
   virtual void request_native(const std::string& method, const std::string& path, std::string&& body,
                               bool limited, double timeout_s, uint64_t tag, PodSink* sink) = 0;
 };

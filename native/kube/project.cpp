@@ -511,6 +511,47 @@ void project_pod(const Value& pod, PodProj& p) { project_generic(DomN{&pod}, p);
 
 void project_pod(const FlatDoc::View& pod, PodProj& p) { project_generic(FlatN{pod}, p); }
 
+void project_identity(const FlatDoc::View& pod, PodProj& p) {
+  p = PodProj();
+  const FlatDoc::View meta = pod.get("metadata"), spec = pod.get("spec");
+  const FlatDoc::View m = meta.is(FlatDoc::Obj) ? meta : FlatDoc::View();
+  const FlatDoc::View sp = spec.is(FlatDoc::Obj) ? spec : FlatDoc::View();
+  const FlatDoc::View nsv = m ? m.get("namespace") : FlatDoc::View();
+  p.ns = nsv && nsv.is(FlatDoc::Str) ? std::string(nsv.str()) : "default";
+  p.name = std::string(m ? m.sv("name") : std::string_view());
+  p.uid = std::string(m ? m.sv("uid") : std::string_view());
+  if (p.uid.empty()) p.uid = p.ns + "/" + p.name;
+  p.rv = std::string(m ? m.sv("resourceVersion") : std::string_view());
+  p.creation = std::string(m ? m.sv("creationTimestamp") : std::string_view());
+  if (m)
+    if (const FlatDoc::View d = m.get("deletionTimestamp")) p.deleting = d.truthy();
+  const std::string_view sched = sp ? sp.sv("schedulerName") : std::string_view();
+  p.sched = sched.empty() ? "default-scheduler" : std::string(sched);
+  p.node = std::string(sp ? sp.sv("nodeName") : std::string_view());
+  if (const FlatDoc::View st = pod.get("status")) p.phase = std::string(st.sv("phase"));
+}
+
+void merge_non_identity(PodProj& d, PodProj&& s) {
+  d.labels = std::move(s.labels);
+  d.has_annotations = s.has_annotations;
+  d.annotations = std::move(s.annotations);
+  d.cpu = s.cpu;
+  d.mem = s.mem;
+  d.nzc = s.nzc;
+  d.nzm = s.nzm;
+  d.priority = s.priority;
+  d.has_node_selector = s.has_node_selector;
+  d.node_selector = std::move(s.node_selector);
+  d.has_affinity = s.has_affinity;
+  d.req_terms = std::move(s.req_terms);
+  d.pref_terms = std::move(s.pref_terms);
+  d.tolerations = std::move(s.tolerations);
+  d.ports = std::move(s.ports);
+  d.flags = s.flags;
+  d.spec_meta_hash = s.spec_meta_hash;
+  d.ok = s.ok;
+}
+
 bool project_pod_text(std::string_view text, PodProj& p) {
   FlatDoc d;
   if (!d.parse(text)) return false;

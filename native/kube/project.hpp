@@ -76,5 +76,10 @@ void project_pod(const Value& pod, PodProj& p);
 void project_pod(const FlatDoc::View& pod, PodProj& p);
 // Parse + project one pod object's JSON text; false when the text is not JSON.
 bool project_pod_text(std::string_view text, PodProj& p);
+// Identity fields only (ns, name, uid, rv, creation, deleting, scheduler, node, phase); `ok`
+// stays false and the hash 0 — see PodEv::full().
+void project_identity(const FlatDoc::View& pod, PodProj& p);
+// Fill everything but the identity fields from a full projection (`src` is consumed).
+void merge_non_identity(PodProj& dst, PodProj&& src);
 
 }  // namespace yk

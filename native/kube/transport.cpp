@@ -12,6 +12,7 @@
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
+#include <pthread.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -90,6 +91,7 @@ struct Transport::Conn {
   uint32_t interest = 0;
   bool registered = false;
   double last_rx = 0.0;      // last time bytes arrived (watch idle timeout)
+  std::string last_rv;       // watch: resourceVersion of the last event handed to the pod sink
   double idle_timeout = 0.0;
 };
 
@@ -146,7 +148,10 @@ Transport::Transport(ClientConfig cfg) : cfg_(std::move(cfg)) {
   burst_ = cfg_.burst;
   tokens_ = cfg_.burst > 0 ? cfg_.burst : 1;
   last_refill_ = now_s();
-  th_ = std::thread([this] { run(); });
+  th_ = std::thread([this] {
+    pthread_setname_np(pthread_self(), "yoda-io");   // per-thread CPU in bench / top -H
+    run();
+  });
 }
 
 Transport::~Transport() { close(); }
@@ -320,12 +325,22 @@ void Transport::request_native(const std::string& method, const std::string& pat
 void Transport::set_pod_sink(PodSink* sink) {
   std::lock_guard<std::mutex> g(sink_mu_);
   pod_sink_ = sink;
+  light_pods_.store(sink != nullptr, std::memory_order_relaxed);
+}
+
+void complete_pod_ev(PodEv* e) {
+  PodProj full;
+  FlatDoc d;
+  if (d.parse(e->raw)) project_pod(d.root(), full);
+  merge_non_identity(e->p, std::move(full));
 }
 
 void Transport::answer(Req& r, int status, std::string&& body) {
   if (r.sink) {
-    std::lock_guard<std::mutex> g(sink_mu_);
-    if (r.sink == pod_sink_) r.sink->on_answer(r.tag, status, std::move(body));
+    // delivered at flush(), in one batch per loop turn, if the sink is still attached
+    if (answers_for_ != r.sink && !sink_answers_.empty()) flush_answers();
+    answers_for_ = r.sink;
+    sink_answers_.push_back(PodSink::Answer{r.tag, status, std::move(body)});
     return;
   }
   Completion e;
@@ -336,21 +351,28 @@ void Transport::answer(Req& r, int status, std::string&& body) {
   complete(std::move(e));
 }
 
+void Transport::flush_answers() {
+  if (sink_answers_.empty()) return;
+  {
+    std::lock_guard<std::mutex> g(sink_mu_);
+    if (answers_for_ == pod_sink_ && pod_sink_) pod_sink_->on_answers(sink_answers_);
+  }
+  sink_answers_.clear();
+  answers_for_ = nullptr;
+}
+
 void Transport::offer_pod_events(Conn* c) {
   if (!c->pods || c->evs.empty()) return;
   std::lock_guard<std::mutex> g(sink_mu_);
   if (!pod_sink_) return;
-  // the Python reflector resumes from the last resourceVersion it saw: if the sink takes the
-  // batch's last event, leave a bookmark with that version in its place
-  std::string last_rv = c->evs.back().rv;
-  const size_t n = c->evs.size();
+  // the reflector resumes from the stream's last resourceVersion, which the sink's events
+  // no longer show it: the watch-end completion carries it (Completion::rv)
+  for (auto it = c->evs.rbegin(); it != c->evs.rend(); ++it)
+    if (!it->rv.empty()) {
+      c->last_rv = it->rv;
+      break;
+    }
   pod_sink_->on_pod_events(c->watch_id, c->evs);
-  if (c->evs.size() != n && !last_rv.empty() && (c->evs.empty() || c->evs.back().rv != last_rv)) {
-    WatchEvent b;
-    b.type = 'B';
-    b.rv = std::move(last_rv);
-    c->evs.push_back(std::move(b));
-  }
 }
 
 uint64_t Transport::watch(const std::string& path, bool pods, double idle_timeout_s) {
@@ -403,6 +425,7 @@ TransportStats Transport::stats() {
 void Transport::complete(Completion&& c) { local_out_.push_back(std::move(c)); }
 
 void Transport::flush() {
+  flush_answers();
   if (local_out_.empty()) return;
   bool was_empty;
   {
@@ -486,6 +509,7 @@ void Transport::close_conn(Conn* c, int status, const std::string& why) {
       e.id = c->watch_id;
       e.status = status;
       e.body = why;
+      e.rv = c->last_rv;
       complete(std::move(e));
     }
     return;
@@ -607,7 +631,14 @@ void Transport::watch_lines(Conn* c) {
     const std::string_view raw = obj.raw();
     if (c->pods && ev.type != 'B' && ev.type != 'E') {
       auto pe = std::make_shared<PodEv>();
-      project_pod(obj, pe->p);
+      if (ev.type != 'A' && light_pods_.load(std::memory_order_relaxed)) {
+        // echoes and deletions: the lane reads identity fields only; the rest on demand
+        project_identity(obj, pe->p);
+        pe->light = true;
+        pe->complete = &complete_pod_ev;
+      } else {
+        project_pod(obj, pe->p);
+      }
       pe->raw.assign(raw.data(), raw.size());
       ev.pod = std::move(pe);
     } else if (ev.type != 'B') {

@@ -53,6 +53,7 @@ struct Completion {
   uint64_t id = 0;
   int status = 0;              // HTTP status; -1 connection error, -2 timeout
   std::string body;
+  std::string rv;              // kWatchEnd: resourceVersion of the stream's last event
   std::vector<WatchEvent> events;
 };
 
@@ -61,6 +62,9 @@ struct TransportStats {
   uint64_t watch_events = 0, watch_bytes = 0, parse_errors = 0, bytes_out = 0, bytes_in = 0;
   uint64_t throttled = 0;
 };
+
+// PodEv::complete for light events (flat re-parse of `raw`, full projection)
+void complete_pod_ev(PodEv* e);
 
 class Transport : public PodPort {
  public:
@@ -124,6 +128,7 @@ class Transport : public PodPort {
   void complete(Completion&& c);
   void answer(Req& r, int status, std::string&& body);   // completion or sink answer
   void offer_pod_events(Conn* c);
+  void flush_answers();
   void flush();
 
   ClientConfig cfg_;
@@ -159,6 +164,9 @@ class Transport : public PodPort {
 
   std::mutex sink_mu_;                     // held around every sink call (I/O thread)
   PodSink* pod_sink_ = nullptr;
+  std::atomic<bool> light_pods_{false};    // a sink is attached: MODIFIED/DELETED decoded light
+  std::vector<PodSink::Answer> sink_answers_;   // I/O thread: answers for the sink, per loop turn
+  PodSink* answers_for_ = nullptr;
 };
 
 }  // namespace yk

@@ -262,7 +262,12 @@ class HttpShard:
         n = (await self._call("POST", "/debug/bench/burst", {"tag": tag}))["n"]
         deadline = time.monotonic() + timeout
         # completion is observed locally (every bind acknowledged, or every pod parked):
-        # no polling requests charged to the scheduler process during the burst
+        # no polling requests charged to the scheduler process during the burst. With the
+        # native lane the loop sleeps until the lane's acknowledged count reaches the burst
+        # (an eventfd wake-up, not a poll); the poll below then only settles the remainder.
+        if sched.lane is not None:
+            await sched.lane.wait_scheduled(sched.lane.lane.scheduled + n - (sched.scheduled - done0),
+                                            max(0.0, deadline - time.monotonic()))
         while time.monotonic() < deadline:
             bound = sched.scheduled - done0
             if bound >= n:

@@ -51,6 +51,7 @@ class NativeLane:
         self._loop: Optional[asyncio.AbstractEventLoop] = None
         self.handoffs = 0
         self.forwarded = 0
+        self._waiters: list = []           # (target scheduled count, future)
 
     # ------------------------------------------------------------------ lifecycle
     def attach(self) -> None:
@@ -108,8 +109,33 @@ class NativeLane:
             log.info("native lane: profile %s %s (flag mask %#x)", name, "on" if want[0] else "off", want[1])
 
     # ------------------------------------------------------------------ lane output
+    async def wait_scheduled(self, target: int, timeout: float) -> bool:
+        """Until ``target`` lane Bindings are acknowledged (the lane wakes the loop when the
+        count crosses it: no polling), or ``timeout``."""
+        if self.lane.scheduled >= target:
+            return True
+        fut = asyncio.get_event_loop().create_future()
+        self._waiters.append((target, fut))
+        self.lane.set_watermark(min(t for t, _ in self._waiters))
+        try:
+            await asyncio.wait_for(asyncio.shield(fut), timeout)
+            return True
+        except asyncio.TimeoutError:
+            return self.lane.scheduled >= target
+        finally:
+            self._waiters = [(t, f) for t, f in self._waiters if f is not fut]
+            self.lane.set_watermark(min((t for t, _ in self._waiters), default=(1 << 64) - 1))
+
+    def _wake_waiters(self) -> None:
+        n = self.lane.scheduled
+        for t, f in self._waiters:
+            if n >= t and not f.done():
+                f.set_result(None)
+
     def _drain(self) -> None:
         fwd, hand, moves = self.lane.drain()
+        if self._waiters:
+            self._wake_waiters()
         s = self.s
         if fwd:
             self.forwarded += len(fwd)

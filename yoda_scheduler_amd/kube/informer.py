@@ -317,11 +317,16 @@ class NativePodInformer(Informer):
                     self.resource_version = rv
 
         def on_end(status: int, body: bytes) -> None:
+            h = handle[0]
+            if h is not None and h.last_rv and self.lane is not None:
+                self.resource_version = h.last_rv    # events went to the lane: resume after them
             if not done.done():
                 done.set_result((status, body))
 
+        handle: list = [None]
         wid = self.client.watch_native("pods", self.resource_version, on_events, on_end, self.field_selector,
                                        pods=True)
+        handle[0] = self.client.native._watches.get(wid)
         try:
             status, body = await done
         except asyncio.CancelledError:

@@ -60,10 +60,11 @@ class WatchHandle:
     """One native watch stream: ``on_events(list)`` per decoded batch, ``on_end(status, body)``
     once when the stream ends (server timeout, error status, connection loss)."""
 
-    __slots__ = ("id", "on_events", "on_end")
+    __slots__ = ("id", "on_events", "on_end", "last_rv")
 
     def __init__(self, wid: int, on_events: Callable, on_end: Callable) -> None:
         self.id, self.on_events, self.on_end = wid, on_events, on_end
+        self.last_rv = ""        # set at the end: the stream's last event version (pod-sink streams)
 
 
 class NativeTransport:
@@ -133,6 +134,7 @@ class NativeTransport:
                 else:
                     h = self._watches.pop(c[1], None)
                     if h is not None:
+                        h.last_rv = c[4] if len(c) > 4 else ""
                         h.on_end(c[2], c[3])
             except Exception:  # noqa: BLE001 - one failing callback must not stall the rest
                 self.callback_errors += 1
@@ -182,10 +184,13 @@ class NativeTransport:
 
     def watch(self, path: str, pods: bool, on_events: Callable, on_end: Callable, idle_timeout: float = 0.0) -> int:
         """``idle_timeout``: end the stream (status -1) if nothing arrives for that long — a
-        black-holed connection never delivers the server's own ``timeoutSeconds`` end."""
+        black-holed connection never delivers the server's own ``timeoutSeconds`` end.
+        ``on_end`` may take a third argument: the resourceVersion of the stream's last event
+        (the only way to learn it when a native pod lane consumed the events)."""
         self._attach()
         wid = self.t.watch(path, pods, float(idle_timeout))
-        self._watches[wid] = WatchHandle(wid, on_events, on_end)
+        h = WatchHandle(wid, on_events, on_end)
+        self._watches[wid] = h
         return wid
 
     def cancel(self, wid: int) -> None:
