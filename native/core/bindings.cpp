@@ -272,13 +272,15 @@ PYBIND11_MODULE(_yoda_core, m) {
       .def("score_weight", &Engine::score_weight, py::call_guard<EngineGuard>())
       .def("set_gang_weights",
            [](Engine& e, int64_t link, int64_t numa, int64_t fit, int64_t occ, bool binpack, int64_t gang_score,
-              int64_t enum_limit) {
+              int64_t enum_limit, int64_t minlink) {
              auto& w = e.weights();
              w.w_link = link; w.w_numa = numa; w.w_fit = fit; w.w_occ = occ;
              w.gpu_binpack = binpack; w.w_gang_score = gang_score; w.enum_limit = enum_limit;
+             w.w_minlink = minlink;
            },
            py::arg("link") = 4, py::arg("numa") = 2, py::arg("fit") = 1, py::arg("occ") = 1,
-           py::arg("binpack") = false, py::arg("gang_score") = 3, py::arg("enum_limit") = 5000, py::call_guard<EngineGuard>())
+           py::arg("binpack") = false, py::arg("gang_score") = 3, py::arg("enum_limit") = 5000,
+           py::arg("minlink") = 2, py::call_guard<EngineGuard>())
       .def("set_percentage_of_nodes_to_score", &Engine::set_percentage_of_nodes_to_score, py::call_guard<EngineGuard>())
       .def("seed", &Engine::seed, py::call_guard<EngineGuard>())
       .def("intern", &Engine::intern, py::call_guard<EngineGuard>())

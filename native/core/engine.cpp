@@ -556,7 +556,7 @@ int64_t Engine::gang_objective(const Node& n, const std::vector<int32_t>& set, u
                                int64_t* link_bad_out) const {
   const int64_t k = (int64_t)set.size();
   int64_t P = k * (k - 1) / 2;
-  int64_t qsum = 0;
+  int64_t qsum = 0, qmin = 10000;
   uint64_t numa_mask = 0;
   int64_t free_after = 0, total = 0, occ = 0;
   for (int64_t a = 0; a < k; ++a) {
@@ -571,16 +571,19 @@ int64_t Engine::gang_objective(const Node& n, const std::vector<int32_t>& set, u
       if (ca.phys != cb.phys && ca.phys < n.nphys && cb.phys < n.nphys)
         q = n.link_q[(size_t)ca.phys * n.nphys + cb.phys];
       qsum += q;
+      qmin = q < qmin ? q : qmin;
     }
   }
   int64_t link_bad = P ? (P * 10000 - qsum) * 100 / P : 0;
+  int64_t minlink_bad = P ? (10000 - qmin) * 100 : 0;
   int64_t d = __builtin_popcountll(numa_mask);
   int64_t numa_bad = k > 1 ? (d - 1) * 1000000 / (k - 1) : 0;
   int64_t leftover = total ? free_after * 1000000 / total : 0;
   int64_t fit = wt_.gpu_binpack ? leftover : 1000000 - leftover;
   int64_t occ_bad = k ? occ * 100 / k : 0;
   if (link_bad_out) *link_bad_out = link_bad;
-  return wt_.w_link * link_bad + wt_.w_numa * numa_bad + wt_.w_fit * fit + wt_.w_occ * occ_bad;
+  return wt_.w_link * link_bad + wt_.w_minlink * minlink_bad + wt_.w_numa * numa_bad + wt_.w_fit * fit +
+         wt_.w_occ * occ_bad;
 }
 
 static uint64_t n_choose_k(uint64_t n, uint64_t k, uint64_t cap) {
@@ -1028,6 +1031,7 @@ bool Engine::device_eligible(const PodReq& req) const {
   for (int i = 0; i < S_NUM; ++i) wsum += score_w_[i] < 0 ? -score_w_[i] : score_w_[i];
   if (wsum * 200 >= ((int64_t)1 << 38)) return false;          // key = (final << 24) | perm
   // the device forms the gang objective with 32×32-bit multiply-adds: |w| ≤ 10^6
+  if (wt_.w_minlink < 0 || wt_.w_minlink > 1000000) return false;
   if (wt_.w_link < 0 || wt_.w_link > 1000000 || wt_.w_numa > 1000000 || wt_.w_fit > 1000000 || wt_.w_occ > 1000000 ||
       wt_.w_numa < -1000000 || wt_.w_fit < -1000000 || wt_.w_occ < -1000000)
     return false;
@@ -1069,6 +1073,7 @@ void Engine::make_dev_req(const PodReq& req, yoda_dev_req_t* out) {
   d.w_fit = wt_.w_fit;
   d.w_occ = wt_.w_occ;
   d.w_gang_score = wt_.w_gang_score;
+  d.w_minlink = wt_.w_minlink;
   Taint ut{unsched_key_, 0, kNoSchedule};
   for (const Toleration& x : req.tolerations)
     if (tolerates(x, ut)) d.tolerates_unschedulable = 1;

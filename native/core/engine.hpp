@@ -116,6 +116,9 @@ struct PodReq {
 struct Weights {
   // gang / GPU-level selection objective (lower is better), see gang_objective()
   int64_t w_link = 4, w_numa = 2, w_fit = 1, w_occ = 1;
+  // bottleneck term: a ring all-reduce over the set is bound by its slowest xGMI link, so the
+  // worst pair counts on top of the mean (minlink_bad = (10000 − min pair q) · 100)
+  int64_t w_minlink = 2;
   bool gpu_binpack = false;     // false: worst-fit (spread, default); true: best-fit within node
   int64_t w_gang_score = 3;     // node score bonus × xGMI quality for multi-GPU pods (fixed mode)
   int64_t enum_limit = 5000;    // exhaustive k-subset search up to this many subsets

@@ -120,7 +120,8 @@ bool config_eq(const EngineConfig& a, const EngineConfig& b) {
       if (a.alloc_w[k][j] != b.alloc_w[k][j]) return false;
   const Weights &x = a.wt, &y = b.wt;
   return x.w_link == y.w_link && x.w_numa == y.w_numa && x.w_fit == y.w_fit && x.w_occ == y.w_occ &&
-         x.gpu_binpack == y.gpu_binpack && x.w_gang_score == y.w_gang_score && x.enum_limit == y.enum_limit;
+         x.gpu_binpack == y.gpu_binpack && x.w_gang_score == y.w_gang_score && x.enum_limit == y.enum_limit &&
+         x.w_minlink == y.w_minlink;
 }
 
 }  // namespace

@@ -640,6 +640,7 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
       const uint32_t m = s_masks[t];
       if (m & ~emask) continue;
       int32_t qsum = 0;
+      int32_t qmin = 10000;
       uint64_t nmask = 0;
       uint64_t fa = 0, tt = 0;
       uint32_t oc = 0;
@@ -653,6 +654,7 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
       }
       if (uni) {
         qsum = P * (int32_t)q01;
+        qmin = (int32_t)q01 < qmin ? (int32_t)q01 : qmin;
       } else {
 #pragma unroll
         for (int a = 0; a < YODA_DEV_CARDS; ++a) {
@@ -661,7 +663,9 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
           for (int b = a + 1; b < YODA_DEV_CARDS; ++b) {
             const int idx = a * YODA_DEV_CARDS + b;
             const int32_t q = (int32_t)((lq[idx >> 1] >> ((idx & 1) * 16)) & 0xFFFFu);
-            qsum += (ia && ((m >> b) & 1u)) ? q : 0;
+            const bool both = ia && ((m >> b) & 1u);
+            qsum += both ? q : 0;
+            qmin = (both && q < qmin) ? q : qmin;
           }
         }
       }
@@ -673,8 +677,10 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
       const int32_t occ_bad = sdiv_small_r((int32_t)(oc * 100u), k, sc.rk);
       // every term fits 32 bits and the host bounds |w| ≤ 10^6 (Engine::device_eligible):
       // 32×32→64-bit multiply-adds instead of 64×64
-      const int64_t o = (int64_t)(int32_t)r.w_link * lb + (int64_t)(int32_t)r.w_numa * numa_bad +
-                        (int64_t)(int32_t)r.w_fit * fit + (int64_t)(int32_t)r.w_occ * occ_bad;
+      const int32_t mb = P ? (10000 - qmin) * 100 : 0;   // bottleneck pair (≤ 10^6)
+      const int64_t o = (int64_t)(int32_t)r.w_link * lb + (int64_t)(int32_t)r.w_minlink * mb +
+                        (int64_t)(int32_t)r.w_numa * numa_bad + (int64_t)(int32_t)r.w_fit * fit +
+                        (int64_t)(int32_t)r.w_occ * occ_bad;
       if (!found || better(o, m, best_o, best_m)) {
         best_o = o; best_m = m; best_lb = lb; found = true;
       }

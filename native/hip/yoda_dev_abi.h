@@ -53,6 +53,7 @@ typedef struct {
   int64_t nz_cpu_m, nz_mem;   // pod non-zero requests (Least/Most/Balanced scores)
   int64_t w_yoda, w_least, w_balanced, w_most, w_const;   // score weights; w_const added to every node
   int64_t w_link, w_numa, w_fit, w_occ, w_gang_score;
+  int64_t w_minlink;      // bottleneck xGMI pair term (engine.hpp Weights::w_minlink)
   uint32_t has_number, has_memory, has_clock, binpack;
   uint32_t filters;       // engine FilterBit mask (only UNSCHEDULABLE/RESOURCES/YODA are evaluated here)
   uint32_t tolerates_unschedulable;

@@ -11,10 +11,11 @@ Objective (lower is better), integer arithmetic with truncating division:
 
     P        = k(k−1)/2 pairs
     link_bad = (P·10000 − Σ_pairs q(a,b)) · 100 / P          q = 9000·(1−load) over xGMI, same phys → 10000
+    min_bad  = (10000 − min_pairs q(a,b)) · 100               bottleneck: a ring is as fast as its slowest link
     numa_bad = (#NUMA nodes − 1) · 10^6 / (k−1)
     leftover = Σ(eff_free − m) · 10^6 / Σ total                 spread: 10^6 − leftover
     occ_bad  = Σ occupancy(1e-4) · 100 / k
-    obj      = w_link·link_bad + w_numa·numa_bad + w_fit·fit + w_occ·occ_bad
+    obj      = w_link·link_bad + w_minlink·min_bad + w_numa·numa_bad + w_fit·fit + w_occ·occ_bad
 
 All k-subsets of eligible cards are enumerated in lexicographic order when there are at
 most ``enum_limit`` of them (C(8,4)=70 on an SPX node); the first minimum wins.
@@ -37,6 +38,7 @@ class GangWeights:
     binpack: bool = False
     gang_score: int = 3
     enum_limit: int = 5000
+    minlink: int = 2
 
 
 @dataclass
@@ -57,7 +59,7 @@ def objective(cards: Sequence[GpuView], link_q: Sequence[int], nphys: int, subse
               w: GangWeights) -> tuple[int, int]:
     k = len(subset)
     P = k * (k - 1) // 2
-    qsum = 0
+    qsum, qmin = 0, 10000
     numa = set()
     free_after = total = occ = 0
     for ai in range(k):
@@ -72,12 +74,14 @@ def objective(cards: Sequence[GpuView], link_q: Sequence[int], nphys: int, subse
             if a.phys != b.phys and a.phys < nphys and b.phys < nphys:
                 q = link_q[a.phys * nphys + b.phys]
             qsum += q
+            qmin = min(qmin, q)
     link_bad = _trunc_div((P * 10000 - qsum) * 100, P) if P else 0
+    min_bad = (10000 - qmin) * 100 if P else 0
     numa_bad = _trunc_div((len(numa) - 1) * 1_000_000, k - 1) if k > 1 else 0
     leftover = _trunc_div(free_after * 1_000_000, total) if total else 0
     fit = leftover if w.binpack else 1_000_000 - leftover
     occ_bad = _trunc_div(occ * 100, k) if k else 0
-    return w.link * link_bad + w.numa * numa_bad + w.fit * fit + w.occ * occ_bad, link_bad
+    return w.link * link_bad + w.minlink * min_bad + w.numa * numa_bad + w.fit * fit + w.occ * occ_bad, link_bad
 
 
 def select(cards: Sequence[GpuView], eligible: Sequence[int], k: int, m: int, link_q: Sequence[int], nphys: int,

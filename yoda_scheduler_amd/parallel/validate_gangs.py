@@ -135,7 +135,14 @@ def choose_sets(scv, k: int, memory_mb: int = 0) -> dict:
     (worst_obj, worst_link), worst = max(scored, key=lambda x: (x[0][0], [-i for i in x[1]]))
     obj_of = {tuple(s): o for o, s in scored}
     rank = [c.hip_id if c.hip_id >= 0 else c.id for c in cards]
+    # the two objectives the busbw measurement arbitrates: mean pair quality only (rounds 1-2)
+    # vs mean + bottleneck pair (a ring all-reduce runs at its slowest link)
+    mean_only = GangWeights(minlink=0)
+    order = {name: [list(s) for _, s in sorted(((objective(views, lq, nphys, s, memory_mb, ww)[0], list(s))
+                                                  for s in itertools.combinations(elig, k)))[:5]]
+             for name, ww in (("mean_only", mean_only), ("mean_plus_bottleneck", w))}
     return {"best": best, "worst": worst, "best_ranks": sorted(rank[i] for i in best),
+            "predicted_order_top5": order,
             "worst_ranks": sorted(rank[i] for i in worst),
             "best_objective": obj_of[tuple(best)][0], "best_link_bad": obj_of[tuple(best)][1],
             "worst_objective": worst_obj, "worst_link_bad": worst_link,

@@ -48,7 +48,7 @@ class Yoda(QueueSortPlugin, FilterPlugin, PostFilterPlugin, ScorePlugin):
         gw = a.get("gangWeights") or {}
         self.gang = dict(link=int(gw.get("link", 4)), numa=int(gw.get("numa", 2)), fit=int(gw.get("fit", 1)),
                          occ=int(gw.get("occupancy", 1)), gang_score=int(gw.get("score", 3)),
-                         enum_limit=int(gw.get("enumLimit", 5000)))
+                         enum_limit=int(gw.get("enumLimit", 5000)), minlink=int(gw.get("minLink", 2)))
 
     def native(self):
         c = core()
