@@ -1114,6 +1114,7 @@ bool Engine::schedule_device(const PodReq& req, CycleResult* r) {
     ++dev_fallbacks_;
     return false;
   }
+  const std::mt19937_64 rng_before = rng_;
   yoda_dev_req_t d;
   make_dev_req(req, &d);
   std::vector<uint8_t> cand;
@@ -1127,6 +1128,8 @@ bool Engine::schedule_device(const PodReq& req, CycleResult* r) {
   yoda_dev_result_t res{};
   int rc = ((dev_schedule_t)fn_schedule_)(dev_ctx_, (int)nodes_.size(), &d, need_cand ? cand.data() : nullptr, &res);
   if (rc != 0) {
+    // the CPU cycle that follows draws the tie-break exactly as if the device was never tried
+    rng_ = rng_before;
     ++dev_fallbacks_;
     return false;
   }
@@ -1152,6 +1155,7 @@ bool Engine::schedule_batch_device(const std::vector<uint64_t>& pods, const std:
     return false;
   }
   // rng draws happen in make_dev_req, in pod order — the same sequence as per-pod cycles
+  const std::mt19937_64 rng_before = rng_;
   std::vector<yoda_dev_req_t> d(reqs.size());
   for (size_t i = 0; i < reqs.size(); ++i) make_dev_req(*reqs[i], &d[i]);
   std::vector<yoda_dev_result_t> res(reqs.size());
@@ -1170,7 +1174,10 @@ bool Engine::schedule_batch_device(const std::vector<uint64_t>& pods, const std:
   batch_in_flight_.store(false, std::memory_order_release);
   dl.unlock();
   if (rc != 0) {
-    // the device table may hold partial in-batch assumptions: re-upload every row
+    // the device table may hold partial in-batch assumptions: re-upload every row. The CPU
+    // path that places the batch instead draws the same tie-breaks a CPU-only engine would
+    // (-8: abandoned at the host deadline; -9: the device is still draining an abandoned call)
+    rng_ = rng_before;
     ++dev_fallbacks_;
     for (int32_t i = 0; i < (int32_t)nodes_.size(); ++i) mark_dirty(i);
     return false;

@@ -90,6 +90,20 @@ __global__ __launch_bounds__(kBlock) void k_verify(const uint4* __restrict__ buf
   if ((threadIdx.x & 63) == 0 && bad) atomicAdd(errors, (unsigned long long)bad);
 }
 
+// Occupies a CU slot for `ticks` of the 100 MHz clock: LDS claimed, the wave asleep between
+// clock reads. Bounded by construction (every wave exits at its deadline).
+__global__ __launch_bounds__(kBlock) void k_occupy(long long ticks, int* __restrict__ out) {
+  extern __shared__ int hold[];
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  hold[threadIdx.x] = (int)threadIdx.x;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+  __syncthreads();
+  if (hold[(threadIdx.x + 1) % kBlock] < 0) out[blockIdx.x] = 1;   // never: keeps the LDS claim
+}
+
+hipStream_t g_occupy_stream = nullptr;
+int* g_occupy_out = nullptr;
+
 int grid_for(int device, int per_cu = 8) {
   int cus = 256;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -246,6 +260,38 @@ int yoda_peer_write_bandwidth(int src, int dst, unsigned long long bytes, int it
   hipFree(remote);
   YODA_CHECK(hipSetDevice(src));
   return (int)hipGetLastError();
+}
+
+// Test utility: holds every CU of `device` for `ms` milliseconds — each CU's whole LDS and
+// its wave slots — on a stream of its own, and returns at once. tests/test_gpu_device_scorer.py
+// uses it as the "tenant kernel" the device scorer must survive (bounded stall, CPU fallback).
+int yoda_hip_occupy(int device, int ms, int* blocks) {
+  YODA_CHECK(hipSetDevice(device));
+  if (ms <= 0 || ms > 10000) return -1;
+  if (!g_occupy_stream) YODA_CHECK(hipStreamCreateWithFlags(&g_occupy_stream, hipStreamNonBlocking));
+  int cus = 256, lds = 160 * 1024, waves = 32;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device);
+  hipDeviceGetAttribute(&waves, hipDeviceAttributeMaxThreadsPerMultiProcessor, device);
+  waves /= 64;
+  const int per_cu = waves / (kBlock / 64) > 0 ? waves / (kBlock / 64) : 1;
+  size_t lds_block = (size_t)lds / per_cu;
+  if (lds_block > 64 * 1024) lds_block = 64 * 1024;
+  if (lds_block < kBlock * sizeof(int)) lds_block = kBlock * sizeof(int);
+  const int grid = cus * per_cu;
+  if (!g_occupy_out) YODA_CHECK(hipMalloc(&g_occupy_out, sizeof(int) * 65536));
+  if (grid > 65536) return -1;
+  hipLaunchKernelGGL(k_occupy, dim3(grid), dim3(kBlock), lds_block, g_occupy_stream, (long long)ms * 100000ll,
+                     g_occupy_out);
+  YODA_CHECK(hipGetLastError());
+  if (blocks) *blocks = grid;
+  return 0;
+}
+
+int yoda_hip_occupy_wait(int device) {
+  YODA_CHECK(hipSetDevice(device));
+  if (g_occupy_stream) YODA_CHECK(hipStreamSynchronize(g_occupy_stream));
+  return 0;
 }
 
 }  // extern "C"

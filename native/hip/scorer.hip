@@ -1427,9 +1427,23 @@ struct Ctx {
   // persistent batch kernel (k_batch)
   bool persist = true;        // YODA_DEV_PERSIST=0: batches run as per-pod launch chains
   int cus = 256;
+  int cus_total = 256;        // compute units of the device (occupancy check)
   int npb_min = 0;            // YODA_DEV_NPB: minimum nodes per block (0: 8 per wave)
   int batch_waves = 0;        // YODA_DEV_BWAVES: k_batch waves per block (4 or 8; 0 = by cluster size)
-  long long deadline_ticks = 200000000ll;   // per spin wait, 100 MHz (YODA_DEV_SPIN_DEADLINE_US)
+  // per spin wait inside k_batch, 100 MHz ticks (YODA_DEV_SPIN_DEADLINE_US): a gather normally
+  // completes in microseconds; 20 ms only elapses when a block is not resident (a tenant
+  // kernel holds the CUs) — then every block gives up and the batch aborts
+  long long deadline_ticks = 2000000ll;
+  // host-side bound on one device call: base + per pod (YODA_DEV_HOST_DEADLINE_US = base).
+  // Past it the host abandons the call (the engine places the pods on the CPU) and the
+  // context refuses work until its stream drains (busy_check)
+  double host_deadline_us = 20000.0, host_deadline_per_pod_us = 50.0;
+  bool abandoned = false;
+  // counters (yoda_dev_counters): every kernel dispatch, k_batch dispatches and the pods they
+  // placed, abandoned calls, calls refused while draining, k_batch GPU time (timing on)
+  long long n_dispatch = 0, n_kbatch = 0, n_kbatch_pods = 0, n_abandon = 0, n_busy = 0;
+  double kbatch_us = 0;
+  int occ_waves = 0, occ_lds = -1, occ_blocks = 0;   // cached k_batch occupancy query
   yoda_dev_req_t *h_reqs = nullptr, *d_reqs_map = nullptr;
   yoda_dev_result_t* d_bres = nullptr;
   unsigned long long* d_slots = nullptr;
@@ -1448,10 +1462,31 @@ struct Ctx {
     if (e__ != hipSuccess) return (int)e__; \
   } while (0)
 
+// A call the host abandoned at its deadline may still be queued or running on the stream:
+// until it drains, the context takes no new work (-9: the engine stays on the CPU path and
+// keeps its rows dirty). Once drained, the batch words are re-armed.
+int busy_check(Ctx* c) {
+  if (!c->abandoned) return 0;
+  const hipError_t q = hipStreamQuery(c->stream);
+  if (q == hipErrorNotReady) {
+    ++c->n_busy;
+    return -9;
+  }
+  c->abandoned = false;
+  CK(hipMemsetAsync(c->d_words, 0, 64, c->stream));
+  CK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+double host_deadline_s(const Ctx* c, int pods) {
+  return (c->host_deadline_us + c->host_deadline_per_pod_us * (pods > 0 ? pods : 1)) * 1e-6;
+}
+
 // launch the pending rows on their own (before a bulk scatter or a debug read)
 int flush_pending(Ctx* c) {
   if (c->pend.n == 0) return 0;
   hipLaunchKernelGGL(k_patch, dim3(1), dim3(32 * kPatchRows), 0, c->stream, c->pend, c->d_nodes);
+  ++c->n_dispatch;
   c->pend.n = 0;
   CK(hipGetLastError());
   return 0;
@@ -1463,13 +1498,18 @@ int flush_pending(Ctx* c) {
 int wait_result(Ctx* c) {
   volatile int32_t* flag = &c->h_res->feasible;
   const auto t0 = std::chrono::steady_clock::now();
+  const double limit = host_deadline_s(c, 1);
   for (unsigned spin = 1;; ++spin) {
     if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) >= 0) return 0;
-    if ((spin & 4095) == 0) {
+    if ((spin & 1023) == 0) {
       const hipError_t q = hipStreamQuery(c->stream);
       if (q == hipSuccess) return __atomic_load_n(flag, __ATOMIC_ACQUIRE) >= 0 ? 0 : -4;
       if (q != hipErrorNotReady) return (int)q;
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) return -5;
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+        c->abandoned = true;   // the GPU is held by other work: the engine uses the CPU meanwhile
+        ++c->n_abandon;
+        return -8;
+      }
     }
     __builtin_ia32_pause();
   }
@@ -1493,9 +1533,11 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
   int cus = 256;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess) c->grid = cus * 4;
   c->cus = cus < kMaxGrid ? cus : kMaxGrid;
+  c->cus_total = cus;
   if (const char* v = getenv("YODA_DEV_PERSIST")) c->persist = v[0] != '0';
   if (const char* v = getenv("YODA_DEV_NPB")) c->npb_min = atoi(v) > 0 ? atoi(v) : 0;
   if (const char* v = getenv("YODA_DEV_SPIN_DEADLINE_US")) c->deadline_ticks = atoll(v) > 0 ? atoll(v) * 100 : 1;
+  if (const char* v = getenv("YODA_DEV_HOST_DEADLINE_US")) c->host_deadline_us = atof(v) > 0 ? atof(v) : 1.0;
   if (const char* v = getenv("YODA_DEV_BWAVES")) c->batch_waves = atoi(v) == 4 ? 4 : atoi(v) == 8 ? 8 : 0;
   if (const char* v = getenv("YODA_DEV_DIRECT_ATOMICS")) c->direct_atomics = v[0] == '1' ? 1 : 0;
   if (const char* v = getenv("YODA_DEV_FUSE_MAX")) c->fuse_max = atoi(v);
@@ -1579,6 +1621,7 @@ int yoda_dev_upload(void* p, int n, const int32_t* idx, const yoda_dev_node_t* r
   for (int i = 0; i < n; ++i)
     if (idx[i] < 0 || idx[i] >= c->cap) return -2;   // never scatter outside the node table
   CK(hipSetDevice(c->device));
+  if (const int b = busy_check(c)) return b;
   if (n <= kPatchRows) {
     // steady state (a reservation dirtied one node): the rows wait host-side and travel in
     // the next filter launch's arguments; a newer row for the same node replaces the old
@@ -1607,6 +1650,7 @@ int yoda_dev_upload(void* p, int n, const int32_t* idx, const yoda_dev_node_t* r
   const int per_block = 8;   // 8 records × 32 lanes = 256 threads
   hipLaunchKernelGGL(k_scatter, dim3((n + per_block - 1) / per_block), dim3(256), 0, c->stream, c->d_stage, c->d_idx,
                      n, c->d_nodes);
+  ++c->n_dispatch;
   CK(hipGetLastError());
   CK(hipStreamSynchronize(c->stream));   // staging buffers are reused by the next upload
   return 0;
@@ -1628,27 +1672,36 @@ int launch_cycle(Ctx* c, int n, yoda_dev_req_t r, yoda_dev_result_t* out, uint32
   const int fuse = n <= c->fuse_max;
   hipLaunchKernelGGL(k_filter, dim3(grid + (c->pend.n > 0 ? 1 : 0)), dim3(kBlock), 0, c->stream, c->pend, c->d_nodes,
                      n, r, c->d_cand, c->d_feas, c->d_elig, c->d_g);
+  ++c->n_dispatch;
   c->pend.n = 0;
   hipLaunchKernelGGL(k_score, dim3(grid), dim3(kBlock), 0, c->stream, c->d_nodes, n, r, c->d_feas, c->d_elig,
                      c->d_raw, c->d_total, c->d_mask, c->d_quality, c->d_g, out, fuse);
-  if (!fuse)
+  ++c->n_dispatch;
+  if (!fuse) {
     hipLaunchKernelGGL(k_select, dim3(grid_sel), dim3(kBlock), 0, c->stream, n, r, c->d_feas, c->d_raw, c->d_total,
                        c->d_mask, c->d_quality, c->d_g, out, c->d_nodes);
+    ++c->n_dispatch;
+  }
   CK(hipGetLastError());
   return 0;
 }
 
 // Spin until `slot->feasible` is published (see wait_result).
-int wait_slot(Ctx* c, yoda_dev_result_t* slot) {
+int wait_slot(Ctx* c, yoda_dev_result_t* slot, int pods) {
   volatile int32_t* flag = &slot->feasible;
   const auto t0 = std::chrono::steady_clock::now();
+  const double limit = host_deadline_s(c, pods);
   for (unsigned spin = 1;; ++spin) {
     if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) >= 0) return 0;
-    if ((spin & 4095) == 0) {
+    if ((spin & 1023) == 0) {
       const hipError_t q = hipStreamQuery(c->stream);
       if (q == hipSuccess) return __atomic_load_n(flag, __ATOMIC_ACQUIRE) >= 0 ? 0 : -4;
       if (q != hipErrorNotReady) return (int)q;
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) return -5;
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+        c->abandoned = true;
+        ++c->n_abandon;
+        return -8;
+      }
     }
     __builtin_ia32_pause();
   }
@@ -1663,6 +1716,7 @@ int yoda_dev_schedule(void* p, int n, const yoda_dev_req_t* req, const uint8_t* 
   if (n <= 0 || n > c->cap) return -1;
   if (req->use_candidates && !cand) return -3;
   CK(hipSetDevice(c->device));
+  if (const int b = busy_check(c)) return b;
   if (req->use_candidates) {
     memcpy(c->h_cand, cand, (size_t)n);
     CK(hipMemcpyAsync(c->d_cand, c->h_cand, (size_t)n, hipMemcpyHostToDevice, c->stream));
@@ -1697,6 +1751,19 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
   const int G = (n + npb - 1) / npb;
   if (G > kMaxGrid) return 1;
   const size_t lds = (size_t)npb * kBatchRowBytes;
+  // every block spins on the others' records: all G must be resident at once. The device's
+  // capacity for this geometry (blocks per CU × CUs) must cover G, or the batch takes the
+  // launch chain (no cross-block waits). A tenant kernel holding CUs at run time is the
+  // host deadline's job (abandon + CPU path), not this check's.
+  if (c->occ_waves != waves || c->occ_lds != (int)lds) {
+    int nb = 0;
+    const hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &nb, waves == 8 ? (const void*)k_batch<8> : (const void*)k_batch<4>, waves * 64, lds);
+    c->occ_waves = waves;
+    c->occ_lds = (int)lds;
+    c->occ_blocks = oe == hipSuccess ? nb : 0;
+  }
+  if ((long long)c->occ_blocks * c->cus_total < G) return 1;
   c->last_grid = G;
   c->last_npb = npb;
   for (int base = 0; base < B; base += kBatchCap) {
@@ -1718,7 +1785,7 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
     a.seq = c->seq;
     a.tag0 = c->epoch;
     c->epoch += 3u * (uint32_t)m + 3u;
-    a.deadline_ticks = c->deadline_ticks;   // 2 s per wait by default
+    a.deadline_ticks = c->deadline_ticks;   // 20 ms per wait by default
     a.reqs = c->d_reqs_map;
     a.slots = c->d_slots;
     a.res = c->d_bres;
@@ -1728,29 +1795,41 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
     a.abort_word = c->d_words + 1;
     a.trace = c->d_trace;
     __atomic_store_n(c->h_done, 0, __ATOMIC_RELEASE);
+    if (c->timing) CK(hipEventRecord(c->e0, c->stream));
     if (waves == 8)
       hipLaunchKernelGGL(k_batch<8>, dim3(G), dim3(512), lds, c->stream, a);
     else
       hipLaunchKernelGGL(k_batch<4>, dim3(G), dim3(256), lds, c->stream, a);
     c->pend.n = 0;
     CK(hipGetLastError());
+    ++c->n_dispatch;
+    ++c->n_kbatch;
+    if (c->timing) CK(hipEventRecord(c->e1, c->stream));
     // wait for `done` (system-scope release by the last block), polling the stream now and
     // then so a failed launch cannot hang the scheduler. A batch runs for milliseconds: spin
     // for the first ~100 µs (short batches), then poll every ~20 µs instead of burning a core.
+    // Past the host deadline (blocks not resident: a tenant kernel holds the CUs) the batch
+    // is abandoned — the engine places it on the CPU — and the context refuses work until
+    // the stream drains (the kernel's own spin deadline ends it once it gets the CUs).
     const auto t0 = std::chrono::steady_clock::now();
+    const double limit = host_deadline_s(c, m);
     int d = 0;
     for (unsigned spin = 1;; ++spin) {
       d = __atomic_load_n(c->h_done, __ATOMIC_ACQUIRE);
       if (d != 0) break;
       if (spin > 2048) std::this_thread::sleep_for(std::chrono::microseconds(20));
-      if ((spin & 255) == 0) {
+      if ((spin & 255) == 0 || spin > 2048) {
         const hipError_t q = hipStreamQuery(c->stream);
         if (q == hipSuccess) {
           d = __atomic_load_n(c->h_done, __ATOMIC_ACQUIRE);
           break;
         }
         if (q != hipErrorNotReady) return (int)q;
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) return -5;
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+          c->abandoned = true;
+          ++c->n_abandon;
+          return -8;
+        }
       }
       __builtin_ia32_pause();
     }
@@ -1762,6 +1841,15 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
     }
     memcpy(out + base, c->h_resb, (size_t)m * sizeof(yoda_dev_result_t));
     c->trace_pods = m;
+    c->n_kbatch_pods += m;
+    if (c->timing) {
+      CK(hipEventSynchronize(c->e1));
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, c->e0, c->e1) == hipSuccess) {
+        c->last_us = ms * 1000.0f;
+        c->kbatch_us += ms * 1000.0;
+      }
+    }
   }
   return 0;
 }
@@ -1774,6 +1862,7 @@ int yoda_dev_schedule_batch(void* p, int n, int B, const yoda_dev_req_t* reqs, y
   Ctx* c = (Ctx*)p;
   if (n <= 0 || n > c->cap || B < 0) return -1;
   CK(hipSetDevice(c->device));
+  if (const int b = busy_check(c)) return b;
   if (c->persist && B > 0) {
     const int rc = batch_persistent(c, n, B, reqs, out);
     if (rc <= 0) return rc;
@@ -1788,7 +1877,7 @@ int yoda_dev_schedule_batch(void* p, int n, int B, const yoda_dev_req_t* reqs, y
       const int rc = launch_cycle(c, n, reqs[base + j], c->d_resb + j, 2u);
       if (rc != 0) return rc;
     }
-    const int w = wait_slot(c, &c->h_resb[m - 1]);
+    const int w = wait_slot(c, &c->h_resb[m - 1], m);
     if (w != 0) return w;
     for (int j = 0; j < m; ++j)
       if (__atomic_load_n(&c->h_resb[j].feasible, __ATOMIC_ACQUIRE) < 0) return -4;
@@ -1829,6 +1918,7 @@ int yoda_dev_debug(void* p, int n, uint8_t* feas, int64_t* raw, int64_t* total, 
   Ctx* c = (Ctx*)p;
   if (n <= 0 || n > c->cap) return -1;
   CK(hipSetDevice(c->device));
+  if (const int b = busy_check(c)) return b;
   if (flush_pending(c) != 0) return -6;
   CK(hipStreamSynchronize(c->stream));
   if (feas) CK(hipMemcpy(feas, c->d_feas, (size_t)n, hipMemcpyDeviceToHost));
@@ -1840,5 +1930,19 @@ int yoda_dev_debug(void* p, int n, uint8_t* feas, int64_t* raw, int64_t* total, 
 }
 
 float yoda_dev_last_us(void* p) { return p ? ((Ctx*)p)->last_us : 0.f; }
+
+// out[0..5]: kernel dispatches, k_batch dispatches, pods placed by k_batch, calls abandoned at
+// the host deadline, calls refused while an abandoned one drained, k_batch GPU µs (timing on)
+int yoda_dev_counters(void* p, double* out) {
+  const Ctx* c = (const Ctx*)p;
+  if (!c || !out) return -1;
+  out[0] = (double)c->n_dispatch;
+  out[1] = (double)c->n_kbatch;
+  out[2] = (double)c->n_kbatch_pods;
+  out[3] = (double)c->n_abandon;
+  out[4] = (double)c->n_busy;
+  out[5] = c->kbatch_us;
+  return 0;
+}
 
 }  // extern "C"

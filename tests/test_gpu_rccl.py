@@ -31,6 +31,30 @@ def test_rccl_allreduce_probe_single_rank(require_gpu):
     assert all(r["algbw_gbps"] > 0 for r in res)
 
 
+def test_rccl_allreduce_probe_multi_rank(require_gpu):
+    """With ≥ 2 GPUs visible: the probe's own launcher path (one process per GPU through
+    torch.distributed.run, RCCL over xGMI) on 2 ranks — every size moves data at a positive
+    bus bandwidth and reports world 2. A 1-GPU box cannot run two RCCL ranks (one rank per
+    device): skipped there, visibly."""
+    import json
+    import subprocess
+    import sys
+
+    import torch
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip(f"{n} GPU visible: a multi-rank RCCL all-reduce needs 2")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           "-m", "yoda_scheduler_amd.parallel.rccl_probe", "--sizes", "1M,64M", "--iters", "5"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    rows = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert [r["bytes"] for r in rows] == [1 << 20, 64 << 20], p.stdout
+    assert all(r["probe"] == "rccl_allreduce" and r["world"] == 2 and r["busbw_gbps"] > 0 for r in rows), rows
+
+
 def test_xgmi_peer_write_probe(require_gpu):
     from yoda_scheduler_amd.ops import hip
     n = hip.device_count()

@@ -20,6 +20,8 @@ def declare(lib: ctypes.CDLL) -> None:
     lib.yoda_dev_last_us.restype = ctypes.c_float
     lib.yoda_dev_batch_trace.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
     lib.yoda_dev_batch_trace.restype = ctypes.c_int
+    lib.yoda_dev_counters.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.yoda_dev_counters.restype = ctypes.c_int
 
 
 # k_batch phases (block 0's stamps): filter → record 1 out; part A of scoring (gang search,
@@ -56,6 +58,21 @@ def read_batch_trace(engine, max_pods: int = 256) -> list[dict]:
         t = [buf[b * W + k] for k in range(W)]
         out.append({ph: (t[k + 1] - t[k]) / 100.0 for k, ph in enumerate(TRACE_PHASES)})
     return out
+
+
+COUNTERS = ("dispatches", "kbatch_dispatches", "kbatch_pods", "abandoned", "busy_refusals", "kbatch_us")
+
+
+def counters(engine) -> dict:
+    """The device context's counters: every kernel dispatch, k_batch dispatches and the pods
+    they placed, calls abandoned at the host deadline, calls refused while an abandoned one
+    drained, and k_batch GPU time in µs (accumulated while ``engine.device_set_timing(True)``)."""
+    lib = hip_lib()
+    declare(lib)
+    buf = (ctypes.c_double * len(COUNTERS))()
+    if lib.yoda_dev_counters(engine.device_ctx, buf) != 0:
+        raise RuntimeError("yoda_dev_counters failed (device scorer not enabled?)")
+    return {k: (buf[i] if k == "kbatch_us" else int(buf[i])) for i, k in enumerate(COUNTERS)}
 
 
 def enable(engine, device: int = 0, capacity: int = 65536, min_nodes: int = 256) -> None:

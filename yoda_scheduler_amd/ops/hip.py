@@ -41,6 +41,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "yoda_hbm_pattern_check2": [c_int, c_ull, c_uint, c_uint, P(c_ull), P(c_float)],
         "yoda_hip_pci_bus_id": [c_int, c_char_p, c_int],
         "yoda_peer_write_bandwidth": [c_int, c_int, c_ull, c_int, P(c_double), P(c_int)],
+        "yoda_hip_occupy": [c_int, c_int, P(c_int)],
+        "yoda_hip_occupy_wait": [c_int],
     }
     for name, args in sigs.items():
         f = getattr(lib, name)
@@ -131,3 +133,16 @@ def peer_write_bandwidth(src: int, dst: int, nbytes: int = 256 << 20, iters: int
     _check(lib().yoda_peer_write_bandwidth(src, dst, nbytes, iters, ctypes.byref(g), ctypes.byref(sup)),
            "peer_write_bandwidth")
     return {"gbps": g.value, "supported": bool(sup.value)}
+
+
+def occupy(device: int = 0, ms: int = 1000) -> int:
+    """Hold every CU of ``device`` (its LDS and wave slots) for ``ms`` milliseconds with a
+    bounded kernel on a stream of its own; returns the block count at once. Test utility: the
+    "tenant kernel" the device scorer must survive (tests/test_gpu_device_scorer.py)."""
+    blocks = c_int(0)
+    _check(lib().yoda_hip_occupy(device, ms, ctypes.byref(blocks)), "occupy")
+    return blocks.value
+
+
+def occupy_wait(device: int = 0) -> None:
+    _check(lib().yoda_hip_occupy_wait(device), "occupy_wait")
