@@ -97,6 +97,33 @@ def thread_cpu() -> dict:
     return out
 
 
+def host_info() -> dict:
+    """The machine the number was measured on: CPU model, CPUs online and usable by this
+    process (a box's cgroup share can be far below the machine's count), kernel."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = None
+    quota = None
+    try:   # cgroup v2 CPU limit ("max 100000" = none)
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(), "cpus_usable": usable, "cgroup_cpus": quota,
+            "kernel": os.uname().release}
+
+
 def rank_gpu_index(local_rank: int, n_visible: int) -> int:
     """GPU of a rank: LOCAL_RANK modulo the visible devices (one rank per GPU under
     torch.distributed.run; several ranks share a GPU only in CPU/gloo rehearsals)."""
@@ -211,7 +238,11 @@ def main(argv=None) -> int:
         th0 = thread_cpu()
         t0 = time.perf_counter()
         c0 = time.process_time()
-        results = [loop.run_until_complete(shards[a.warmup + i].burst(f"s{i}")) for i in range(a.steps)]
+        results, step_s = [], []
+        for i in range(a.steps):
+            ts = time.perf_counter()
+            results.append(loop.run_until_complete(shards[a.warmup + i].burst(f"s{i}")))
+            step_s.append(time.perf_counter() - ts)
         sync()
         elapsed = time.perf_counter() - t0
         cpu_s = time.process_time() - c0     # this rank's process: scheduler (+ in-process apiserver)
@@ -231,6 +262,9 @@ def main(argv=None) -> int:
             t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
+            st = torch.tensor(step_s, dtype=torch.float64, device=dev)
+            dist.all_reduce(st, op=dist.ReduceOp.MAX)
+            step_s = [float(x) for x in st.tolist()]
             c = torch.tensor([bound, unsched, cpu_s], dtype=torch.float64, device=dev)
             dist.all_reduce(c, op=dist.ReduceOp.SUM)
             bound, unsched, cpu_s = int(c[0].item()), int(c[1].item()), float(c[2].item())
@@ -253,6 +287,8 @@ def main(argv=None) -> int:
         return {
             "value": round(value, 2),
             "ms_per_step": round(elapsed / a.steps * 1000.0, 3),
+            # each timed step (one burst) on its own, max over ranks: drift and outliers show
+            "step_ms": [round(x * 1000.0, 3) for x in step_s],
             "p50_latency_ms": round(percentile(lats, 50) * 1000.0, 3),
             "p99_latency_ms": round(percentile(lats, 99) * 1000.0, 3),
             "max_latency_ms": round(max(lats) * 1000.0, 3) if lats else None,
@@ -308,6 +344,7 @@ def main(argv=None) -> int:
                              "(kube-scheduler v1.20 client QPS 50 / burst 100): a client-QPS bound, not a measured "
                              "reference run; with --reference-qps this scheduler is bound the same way (~55 pods/s)",
             "telemetry": tels[0],
+            "host": host_info(),
         }
         if alt is not None:
             out["alt"] = alt      # the other transport, measured after the headline's timed region

@@ -925,6 +925,7 @@ bool Engine::enable_device(const std::string& lib_path, int device, int capacity
   fn_last_us_ = dlsym(lib, "yoda_dev_last_us");
   fn_set_timing_ = dlsym(lib, "yoda_dev_set_timing");
   fn_schedule_batch_ = dlsym(lib, "yoda_dev_schedule_batch");   // optional
+  fn_busy_ = dlsym(lib, "yoda_dev_busy");                         // optional
   if (!create || !fn_destroy_ || !fn_upload_ || !fn_schedule_ || !fn_last_us_) {
     if (err) *err = "libyoda_hip.so lacks the yoda_dev_* entry points";
     dlclose(lib);
@@ -1010,6 +1011,10 @@ bool Engine::pack_node(int32_t idx, void* out) const {
 }
 
 bool Engine::flush_dirty() {
+  // the device still drains a call it abandoned (a tenant kernel holds the GPU): refuse
+  // before packing rows — after an abandoned batch every row is dirty, and packing them for
+  // each refused per-pod attempt cost more than the CPU cycles themselves
+  if (fn_busy_ && ((int (*)(void*))fn_busy_)(dev_ctx_)) return false;
   if (dirty_list_.empty()) return true;
   std::vector<yoda_dev_node_t> rows(dirty_list_.size());
   for (size_t i = 0; i < dirty_list_.size(); ++i)

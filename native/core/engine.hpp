@@ -359,6 +359,7 @@ class Engine {
   void* fn_last_us_ = nullptr;
   void* fn_set_timing_ = nullptr;   // optional entry points
   void* fn_schedule_batch_ = nullptr;
+  void* fn_busy_ = nullptr;
   std::recursive_mutex* ext_mu_ = nullptr;
   std::mutex dev_mu_;                        // device context (stream, staging buffers)
   std::atomic<bool> batch_in_flight_{false};

@@ -1439,10 +1439,13 @@ struct Ctx {
   // context refuses work until its stream drains (busy_check)
   double host_deadline_us = 20000.0, host_deadline_per_pod_us = 50.0;
   bool abandoned = false;
+  std::chrono::steady_clock::time_point next_probe{};   // busy_check: next stream query
   // counters (yoda_dev_counters): every kernel dispatch, k_batch dispatches and the pods they
   // placed, abandoned calls, calls refused while draining, k_batch GPU time (timing on)
   long long n_dispatch = 0, n_kbatch = 0, n_kbatch_pods = 0, n_abandon = 0, n_busy = 0;
   double kbatch_us = 0;
+  long long n_query = 0;   // stream queries made by busy_check, and their time
+  double query_us = 0;
   int occ_waves = 0, occ_lds = -1, occ_blocks = 0;   // cached k_batch occupancy query
   yoda_dev_req_t *h_reqs = nullptr, *d_reqs_map = nullptr;
   yoda_dev_result_t* d_bres = nullptr;
@@ -1467,7 +1470,18 @@ struct Ctx {
 // keeps its rows dirty). Once drained, the batch words are re-armed.
 int busy_check(Ctx* c) {
   if (!c->abandoned) return 0;
+  // a stream query costs far more than a refusal while the GPU is held (≈ 0.3 ms measured
+  // under a tenant kernel): probe at most every 2 ms, refuse in between
+  const auto now = std::chrono::steady_clock::now();
+  if (now < c->next_probe) {
+    ++c->n_busy;
+    return -9;
+  }
   const hipError_t q = hipStreamQuery(c->stream);
+  const auto after = std::chrono::steady_clock::now();
+  ++c->n_query;
+  c->query_us += std::chrono::duration<double, std::micro>(after - now).count();
+  c->next_probe = after + std::chrono::milliseconds(2);
   if (q == hipErrorNotReady) {
     ++c->n_busy;
     return -9;
@@ -1931,8 +1945,18 @@ int yoda_dev_debug(void* p, int n, uint8_t* feas, int64_t* raw, int64_t* total, 
 
 float yoda_dev_last_us(void* p) { return p ? ((Ctx*)p)->last_us : 0.f; }
 
-// out[0..5]: kernel dispatches, k_batch dispatches, pods placed by k_batch, calls abandoned at
-// the host deadline, calls refused while an abandoned one drained, k_batch GPU µs (timing on)
+// 1 while the context refuses work (an abandoned call still drains; see busy_check), else 0.
+// The engine asks before packing rows for an upload.
+int yoda_dev_busy(void* p) {
+  Ctx* c = (Ctx*)p;
+  if (!c || !c->abandoned) return 0;
+  if (hipSetDevice(c->device) != hipSuccess) return 1;
+  return busy_check(c) != 0;
+}
+
+// out[0..7]: kernel dispatches, k_batch dispatches, pods placed by k_batch, calls abandoned at
+// the host deadline, calls refused while an abandoned one drained, k_batch GPU µs (timing on),
+// stream queries made while draining and their µs
 int yoda_dev_counters(void* p, double* out) {
   const Ctx* c = (const Ctx*)p;
   if (!c || !out) return -1;
@@ -1942,6 +1966,8 @@ int yoda_dev_counters(void* p, double* out) {
   out[3] = (double)c->n_abandon;
   out[4] = (double)c->n_busy;
   out[5] = c->kbatch_us;
+  out[6] = (double)c->n_query;
+  out[7] = c->query_us;
   return 0;
 }
 

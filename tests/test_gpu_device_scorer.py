@@ -343,13 +343,16 @@ def test_batch_survives_a_tenant_kernel(require_gpu):
 
     def both(pods):
         ids = [p.num_id for p in pods]
+        ra_req = [pod_req(a, p) for p in pods]
+        rb_req = [pod_req(b, p) for p in pods]
         t0 = time.perf_counter()
-        ra = a.schedule_batch(ids, [pod_req(a, p) for p in pods])
+        ra = a.schedule_batch(ids, ra_req)
         ta = time.perf_counter() - t0
         t0 = time.perf_counter()
-        rb = b.schedule_batch(ids, [pod_req(b, p) for p in pods])
+        rb = b.schedule_batch(ids, rb_req)
         tb = time.perf_counter() - t0
         assert [key(r) for r in ra] == [key(r) for r in rb]
+        print(f"device-engine {ta * 1e3:.2f} ms, cpu-engine {tb * 1e3:.2f} ms, counters {ds.counters(a)}")
         return ra, ta - tb                                # the stall: time beyond the CPU path's own
 
     first = [ds.random_request(a, rng, f"hog-{k}")[0] for k in range(256)]

@@ -60,7 +60,8 @@ def read_batch_trace(engine, max_pods: int = 256) -> list[dict]:
     return out
 
 
-COUNTERS = ("dispatches", "kbatch_dispatches", "kbatch_pods", "abandoned", "busy_refusals", "kbatch_us")
+COUNTERS = ("dispatches", "kbatch_dispatches", "kbatch_pods", "abandoned", "busy_refusals", "kbatch_us",
+            "drain_queries", "drain_query_us")
 
 
 def counters(engine) -> dict:
@@ -72,7 +73,7 @@ def counters(engine) -> dict:
     buf = (ctypes.c_double * len(COUNTERS))()
     if lib.yoda_dev_counters(engine.device_ctx, buf) != 0:
         raise RuntimeError("yoda_dev_counters failed (device scorer not enabled?)")
-    return {k: (buf[i] if k == "kbatch_us" else int(buf[i])) for i, k in enumerate(COUNTERS)}
+    return {k: (buf[i] if k.endswith("_us") else int(buf[i])) for i, k in enumerate(COUNTERS)}
 
 
 def enable(engine, device: int = 0, capacity: int = 65536, min_nodes: int = 256) -> None:
