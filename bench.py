@@ -120,8 +120,17 @@ def host_info() -> dict:
             quota = None if q == "max" else round(int(q) / int(per), 2)
     except (OSError, ValueError):
         pass
+    # single-thread speed of this box right now (noisy neighbours, clocks): the best of 5 runs
+    # of a fixed pure-Python loop, so per-pod CPU figures can be compared across boxes
+    best = float("inf")
+    for _ in range(5):
+        t0 = time.perf_counter()
+        x = 0
+        for i in range(200_000):
+            x += i & 7
+        best = min(best, time.perf_counter() - t0)
     return {"cpu_model": model, "nproc": os.cpu_count(), "cpus_usable": usable, "cgroup_cpus": quota,
-            "kernel": os.uname().release}
+            "kernel": os.uname().release, "calib_loop_ms": round(best * 1e3, 3)}
 
 
 def rank_gpu_index(local_rank: int, n_visible: int) -> int:

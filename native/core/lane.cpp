@@ -221,6 +221,7 @@ void Lane::on_answers(std::vector<yk::PodSink::Answer>& answers) {
     it.tag = a.tag;
     it.status = a.status;
     it.body = std::move(a.body);
+    it.t = a.t;
     inbox_.push_back(std::move(it));
   }
   in_cv_.notify_one();
@@ -517,7 +518,7 @@ void Lane::drop_owned(Entry* e, bool release) {
   e->node_name.clear();
 }
 
-void Lane::handle_answer(uint64_t tag, int status, std::string& body) {
+void Lane::handle_answer(uint64_t tag, int status, std::string& body, double t_ack) {
   if (tag & kEventTag) {
     std::lock_guard<std::mutex> g(stat_mu_);
     if (status >= 200 && status < 300) st_.events_written++;
@@ -528,7 +529,8 @@ void Lane::handle_answer(uint64_t tag, int status, std::string& body) {
   if (it == by_id_.end()) return;            // deleted meanwhile: its reservation is gone already
   Entry* e = it->second;
   if (e->st != BINDING && e->st != BOUND) return;
-  const double now = mono();
+  // the bind is acknowledged when the I/O thread read the answer, not when this thread got to it
+  const double now = t_ack > 0 ? t_ack : mono();
   bind_settled(e);
   if (status >= 200 && status < 300) {
     e->acked = true;
@@ -1033,7 +1035,7 @@ void Lane::run() {
       for (auto& it : work) {
         switch (it.k) {
           case Item::kEvent: handle_event(it.type, it.ev, &fwd); break;
-          case Item::kAnswer: handle_answer(it.tag, it.status, it.body); break;
+          case Item::kAnswer: handle_answer(it.tag, it.status, it.body, it.t); break;
           case Item::kProfiles: apply_profiles(&fwd); break;
           case Item::kRelist: {
             std::vector<Fwd> out;

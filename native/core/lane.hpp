@@ -165,6 +165,7 @@ class Lane : public yk::PodSink {
     uint64_t tag = 0;
     int status = 0;
     std::string body;
+    double t = 0;             // answers: when the I/O thread read it
     std::shared_ptr<std::vector<std::shared_ptr<yk::PodEv>>> items;
     uint64_t token = 0;
   };
@@ -175,7 +176,7 @@ class Lane : public yk::PodSink {
 
   void run();
   void handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::vector<Fwd>* out);
-  void handle_answer(uint64_t tag, int status, std::string& body);
+  void handle_answer(uint64_t tag, int status, std::string& body, double t_ack);
   void handle_relist(const std::vector<std::shared_ptr<yk::PodEv>>& items, std::vector<Fwd>* out);
   void drop_owned(Entry* e, bool release);
   void apply_profiles(std::vector<Fwd>* out);

@@ -63,6 +63,7 @@ class PodSink {
     uint64_t tag;
     int status;
     std::string body;
+    double t = 0;              // steady-clock seconds when the I/O thread read the answer (0: unknown)
   };
   virtual void on_answers(std::vector<Answer>& answers) = 0;
 };

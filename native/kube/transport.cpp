@@ -340,7 +340,7 @@ void Transport::answer(Req& r, int status, std::string&& body) {
     // delivered at flush(), in one batch per loop turn, if the sink is still attached
     if (answers_for_ != r.sink && !sink_answers_.empty()) flush_answers();
     answers_for_ = r.sink;
-    sink_answers_.push_back(PodSink::Answer{r.tag, status, std::move(body)});
+    sink_answers_.push_back(PodSink::Answer{r.tag, status, std::move(body), now_s()});
     return;
   }
   Completion e;
