@@ -230,6 +230,8 @@ def main(argv=None) -> int:
         for i in range(a.warmup):
             loop.run_until_complete(shards[i].burst(f"w{i}"))
 
+        api_sys = [0.0]
+
         def api_cpu() -> float:
             """CPU seconds of the separate apiserver process (http transport), if measurable."""
             proc = getattr(shards[0], "proc", None)
@@ -238,12 +240,26 @@ def main(argv=None) -> int:
             try:
                 import psutil
                 t = psutil.Process(proc.pid).cpu_times()
+                api_sys[0] = t.system
                 return t.user + t.system
             except Exception:  # noqa: BLE001 - psutil missing / process gone
                 return float("nan")
 
+        def lane_engine() -> tuple[float, int]:
+            """Seconds the native lanes spent inside Engine::schedule_batch (wall, CPU) and waiting
+            for the engine lock, and the pods of those calls."""
+            s, c, lw, n = 0.0, 0.0, 0.0, 0
+            for sh in {id(x): x for x in shards}.values():
+                ln = getattr(sh.sched, "lane", None)
+                if ln is not None:
+                    st = ln.lane.stats()
+                    s, c, lw, n = s + st["engine_s"], c + st["engine_cpu_s"], lw + st["lock_wait_s"], n + st["engine_pods"]
+            return s, c, lw, n
+
         sync()
         a0 = api_cpu()
+        as0 = api_sys[0]
+        le0 = lane_engine()
         th0 = thread_cpu()
         t0 = time.perf_counter()
         c0 = time.process_time()
@@ -256,7 +272,9 @@ def main(argv=None) -> int:
         elapsed = time.perf_counter() - t0
         cpu_s = time.process_time() - c0     # this rank's process: scheduler (+ in-process apiserver)
         api_s = api_cpu() - a0
+        api_sys_s = api_sys[0] - as0
         th1 = thread_cpu()
+        le1 = lane_engine()
         my_bound = sum(r.bound for r in results)
         threads = {k: round((v - th0.get(k, 0.0)) / my_bound * 1e6, 2) for k, v in sorted(th1.items())
                    if my_bound and v - th0.get(k, 0.0) > 0}
@@ -308,8 +326,15 @@ def main(argv=None) -> int:
             "cpu_us_per_pod": round(cpu_s / bound * 1e6, 2) if bound else None,
             # rank 0's process CPU per pod by thread (≥ 10 ms clock-tick resolution per thread)
             "thread_cpu_us_per_pod": threads,
+            # of which the lane thread spent inside the engine's batch cycles (wall, rank 0)
+            "lane_engine_us_per_pod": ({"wall": round((le1[0] - le0[0]) / (le1[3] - le0[3]) * 1e6, 2),
+                                        "cpu": round((le1[1] - le0[1]) / (le1[3] - le0[3]) * 1e6, 2),
+                                        "lock_wait": round((le1[2] - le0[2]) / (le1[3] - le0[3]) * 1e6, 2)}
+                                       if le1[3] > le0[3] else None),
             # the fake apiserver's own CPU (separate process, http transport; rank 0's)
             **({"apiserver_cpu_us_per_pod": round(api_s / (bound / max(world, 1)) * 1e6, 2)
+                if bound and api_s == api_s else None,
+                "apiserver_sys_us_per_pod": round(api_sys_s / (bound / max(world, 1)) * 1e6, 2)
                 if bound and api_s == api_s else None} if transport == "http" else {}),
             "pods_bound": bound,
             "pods_unschedulable": unsched,

@@ -597,6 +597,10 @@ PYBIND11_MODULE(_yoda_core, m) {
              d["inflight"] = s.inflight;
              d["binding"] = s.binding;
              d["owned"] = s.owned;
+             d["engine_s"] = s.engine_s;
+             d["engine_pods"] = s.engine_pods;
+             d["engine_cpu_s"] = s.engine_cpu_s;
+             d["lock_wait_s"] = s.lock_wait_s;
              return d;
            })
       .def("pause", &Lane::pause, py::call_guard<py::gil_scoped_release>())

@@ -618,6 +618,8 @@ bool Engine::select_gpus(const PodReq& req, int32_t idx, std::vector<int32_t>* o
     return out->size() == k;
   }
   if (E.size() < k) return false;
+  if (n.cards.size() <= 16 && n_choose_k(E.size(), k, (uint64_t)wt_.enum_limit) <= (uint64_t)wt_.enum_limit)
+    return select_gpus_small(n, E, k, m, out, quality);
   int64_t best = INT64_MAX, best_link = 0, lb = 0;
   std::vector<int32_t> cur;
   uint64_t total = n_choose_k(E.size(), k, (uint64_t)wt_.enum_limit);
@@ -663,6 +665,85 @@ bool Engine::select_gpus(const PodReq& req, int32_t idx, std::vector<int32_t>* o
     best = gang_objective(n, cur, m, &best_link);
     *out = cur;
   }
+  if (quality) *quality = (int32_t)(10000 - best_link / 100);
+  return true;
+}
+
+// Exhaustive search for nodes of ≤ 16 cards (every MI355X/MI350X node, partitioned ones up to
+// DPX): per-card terms and pair qualities are read once, subsets are bitmasks enumerated in
+// Gosper order, and gang_objective's integer arithmetic is applied to them. Ties go to the
+// lexicographically smallest set — the one holding the lowest card of the symmetric
+// difference — which is the set the lexicographic enumeration above keeps first.
+bool Engine::select_gpus_small(const Node& n, const std::vector<int32_t>& E, uint64_t k, uint64_t m,
+                               std::vector<int32_t>* out, int32_t* quality) const {
+  const int ne = (int)E.size();
+  int64_t fa[16], tt[16], oc[16];
+  uint64_t nb[16];
+  for (int j = 0; j < ne; ++j) {
+    const Card& c = n.cards[E[j]];
+    fa[j] = (int64_t)(eff_free(c) - m);
+    tt[j] = (int64_t)c.total_mb;
+    oc[j] = c.occ_q;
+    nb[j] = 1ull << (c.numa & 63);
+  }
+  const int64_t K = (int64_t)k, P = K * (K - 1) / 2;
+  int32_t q[16][16];
+  bool uniform = true;
+  int32_t q0 = -1;
+  for (int a = 0; a < ne; ++a)
+    for (int b = a + 1; b < ne; ++b) {
+      const Card& ca = n.cards[E[a]];
+      const Card& cb = n.cards[E[b]];
+      int32_t v = 10000;
+      if (ca.phys != cb.phys && ca.phys < n.nphys && cb.phys < n.nphys) v = n.link_q[(size_t)ca.phys * n.nphys + cb.phys];
+      q[a][b] = v;
+      if (q0 < 0) q0 = v;
+      uniform = uniform && v == q0;
+    }
+  int64_t best = INT64_MAX, best_link = 0;
+  uint32_t best_set = 0;
+  // x: a k-bit subset of the ne eligible positions (Gosper's hack walks them all)
+  const uint32_t last = ne >= 32 ? 0u : (1u << ne);
+  for (uint32_t x = (1u << K) - 1u; x < last;) {
+    int64_t qsum = 0, qmin = 10000, free_after = 0, total = 0, occ = 0;
+    uint64_t numa_mask = 0;
+    for (uint32_t r = x; r; r &= r - 1) {
+      const int a = __builtin_ctz(r);
+      numa_mask |= nb[a];
+      free_after += fa[a];
+      total += tt[a];
+      occ += oc[a];
+      if (!uniform)
+        for (uint32_t r2 = r & (r - 1); r2; r2 &= r2 - 1) {
+          const int32_t v = q[a][__builtin_ctz(r2)];
+          qsum += v;
+          qmin = v < qmin ? v : qmin;
+        }
+    }
+    if (uniform && P) {
+      qsum = P * q0;
+      qmin = q0 < qmin ? q0 : qmin;
+    }
+    const int64_t link_bad = P ? (P * 10000 - qsum) * 100 / P : 0;
+    const int64_t minlink_bad = P ? (10000 - qmin) * 100 : 0;
+    const int64_t d = __builtin_popcountll(numa_mask);
+    const int64_t numa_bad = K > 1 ? (d - 1) * 1000000 / (K - 1) : 0;
+    const int64_t leftover = total ? free_after * 1000000 / total : 0;
+    const int64_t fit = wt_.gpu_binpack ? leftover : 1000000 - leftover;
+    const int64_t occ_bad = K ? occ * 100 / K : 0;
+    const int64_t obj = wt_.w_link * link_bad + wt_.w_minlink * minlink_bad + wt_.w_numa * numa_bad +
+                        wt_.w_fit * fit + wt_.w_occ * occ_bad;
+    // positions are in card order, so the lowest differing position is the lowest differing card
+    if (obj < best || (obj == best && ((x ^ best_set) & (0u - (x ^ best_set)) & x))) {
+      best = obj;
+      best_link = link_bad;
+      best_set = x;
+    }
+    const uint32_t lo = x & (0u - x), up = x + lo;   // next subset with the same popcount
+    x = lo ? (((x ^ up) >> 2) / lo) | up : last;
+  }
+  out->clear();
+  for (uint32_t r = best_set; r; r &= r - 1) out->push_back(E[__builtin_ctz(r)]);
   if (quality) *quality = (int32_t)(10000 - best_link / 100);
   return true;
 }

@@ -251,6 +251,8 @@ class Engine {
   static void normalize_yoda(std::vector<int64_t>& s);
   // GPU set on node (empty + false if none)
   bool select_gpus(const PodReq& req, int32_t idx, std::vector<int32_t>* out, int32_t* quality) const;
+  bool select_gpus_small(const Node& n, const std::vector<int32_t>& E, uint64_t k, uint64_t m,
+                         std::vector<int32_t>* out, int32_t* quality) const;
 
   // ---- full native cycle
   // candidates: node indices to consider (empty = all). Python filter/score plugins can

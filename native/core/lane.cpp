@@ -126,6 +126,12 @@ bool config_eq(const EngineConfig& a, const EngineConfig& b) {
 
 }  // namespace
 
+double Lane::thread_cpu() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (double)ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
 double Lane::mono() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -751,8 +757,14 @@ void Lane::schedule_some() {
     std::vector<size_t> slot;
     std::vector<CycleResult> res;
     std::vector<std::string> names;
+    const double tw = mono();
     {
       std::unique_lock<std::recursive_mutex> lk(*emu_);
+      {
+        const double dw = mono() - tw;
+        std::lock_guard<std::mutex> g(stat_mu_);
+        st_.lock_wait_s += dw;
+      }
       for (size_t k = 0; k < n; ++k) {
         try {
           ok[k] = make_req(run[i + k]->ev->full(), &reqs[k]);
@@ -766,10 +778,18 @@ void Lane::schedule_some() {
       }
       const EngineConfig saved = eng_->config();
       eng_->set_config(pr.cfg);
+      const double te = mono(), tc = thread_cpu();
       try {
         res = eng_->schedule_batch(ids, rp);
       } catch (const std::exception&) {
         res.clear();
+      }
+      {
+        const double dc = thread_cpu() - tc;
+        std::lock_guard<std::mutex> g(stat_mu_);
+        st_.engine_s += mono() - te;
+        st_.engine_cpu_s += dc;
+        st_.engine_pods += ids.size();
       }
       // restore the caller's configuration unless it re-configured the engine while a
       // device batch had the lock dropped (then its newer configuration stays)

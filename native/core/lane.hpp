@@ -56,6 +56,10 @@ struct LaneStats {
   uint64_t forwarded = 0, released = 0, batches = 0, confirmed = 0, events_recorded = 0, events_dropped = 0;
   uint64_t events_written = 0, event_errors = 0, lost_answers_kept = 0;
   uint64_t queued = 0, inflight = 0, binding = 0, owned = 0;   // gauges
+  double engine_s = 0;        // wall time inside Engine::schedule_batch (lane thread)
+  double engine_cpu_s = 0;    // ... of which on the CPU (the rest: the engine lock, the device)
+  double lock_wait_s = 0;     // waiting for the engine lock before a run
+  uint64_t engine_pods = 0;   // pods those calls placed or rejected
 };
 
 class Lane : public yk::PodSink {
@@ -195,6 +199,7 @@ class Lane : public yk::PodSink {
   void publish(std::vector<Fwd>&& fwd, std::vector<Handoff>&& hand);
   void signal_python();
   static double mono();
+  static double thread_cpu();   // this thread's CPU seconds
 
   Engine* eng_;
   std::recursive_mutex* emu_;

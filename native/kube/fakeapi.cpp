@@ -1,5 +1,6 @@
 // Native fake kube-apiserver (see fakeapi.hpp).
 #include "fakeapi.hpp"
+#include "flatjson.hpp"
 
 #include <arpa/inet.h>
 #include <fcntl.h>
@@ -79,18 +80,115 @@ const ResDef kRes[] = {
     {"statefulsets", "apps", "v1", "statefulsets", "StatefulSet", true},
 };
 
+// A stored object version: its JSON text is the source of truth (every list and watch frame
+// sends it as is); the DOM and the flat view of it are built on first use and kept (the server
+// is single-threaded, versions are immutable). Hot pod writes (bind, delete) edit the text
+// through the flat view's spans instead of copying and re-serialising a DOM.
 struct Stored {
-  Value v;
   std::string text;
+  int64_t rv = 0;
+  std::string ns;              // metadata.namespace
+  size_t rv_off = std::string::npos, rv_len = 0;   // span of the resourceVersion value, if known
+  mutable std::unique_ptr<Value> dom;
+  mutable std::unique_ptr<FlatDoc> flat;
+  // field-selector values read from this version (dotted path → value); a version made by
+  // editing another inherits the entries its edits cannot have changed
+  mutable std::vector<std::pair<std::string, std::string>> fields;
+  const Value& v() const {
+    if (!dom) dom = std::make_unique<Value>(parse(text));
+    return *dom;
+  }
+  FlatDoc::View fv() const {
+    if (!flat) {
+      flat = std::make_unique<FlatDoc>();
+      if (!flat->parse(text)) return FlatDoc::View();
+    }
+    return flat->root();
+  }
 };
 using SP = std::shared_ptr<const Stored>;
 
+// The span of `"resourceVersion":"<rv>"`'s value in a text we produced, when it occurs once
+// (a JSON string cannot contain the unescaped pattern, so only a nested key could repeat it).
+void locate_rv(Stored& s) {
+  if (!s.rv) return;
+  const std::string pat = "\"resourceVersion\":\"" + std::to_string(s.rv) + "\"";
+  const size_t at = s.text.find(pat);
+  if (at == std::string::npos || s.text.find(pat, at + 1) != std::string::npos) return;
+  s.rv_off = at + 18;   // the opening quote of the value
+  s.rv_len = pat.size() - 18;
+}
+
 SP make_stored(Value v) {
   auto s = std::make_shared<Stored>();
-  s->v = std::move(v);
-  s->text = dump(s->v);
+  s->text = dump(v);
+  if (const Value* m = v.get("metadata")) {
+    if (const Value* r = m->get("resourceVersion")) s->rv = r->as_int();
+    s->ns = std::string(m->sv("namespace"));
+  }
+  s->dom = std::make_unique<Value>(std::move(v));
+  locate_rv(*s);
   return s;
 }
+
+// a version made by editing `from` at `edited` (dotted paths): keeps the field-selector values
+// no edit can have touched (neither path a prefix of the other)
+std::shared_ptr<Stored> make_stored_text(std::string text, int64_t rv, std::string ns, const Stored* from = nullptr,
+                                         std::initializer_list<std::string_view> edited = {}) {
+  auto s = std::make_shared<Stored>();
+  s->text = std::move(text);
+  s->rv = rv;
+  s->ns = std::move(ns);
+  locate_rv(*s);
+  if (from)
+    for (const auto& f : from->fields) {
+      bool hit = false;
+      for (std::string_view e : edited) {
+        const size_t n = std::min(e.size(), f.first.size());
+        if (std::string_view(f.first).substr(0, n) == e.substr(0, n) &&
+            (f.first.size() == n ? (e.size() == n || e[n] == '.') : f.first[n] == '.'))
+          hit = true;
+      }
+      if (!hit) s->fields.push_back(f);
+    }
+  return s;
+}
+
+// Text edits of one JSON document: replace [beg, end) or insert at beg (beg == end). Edits
+// must not overlap; applied in position order.
+struct TextEdits {
+  struct E {
+    size_t beg, end;
+    std::string text;
+  };
+  std::vector<E> es;
+  void replace(std::string_view doc, FlatDoc::View v, std::string t) {
+    const size_t b = size_t(v.raw().data() - doc.data());
+    es.push_back({b, b + v.raw().size(), std::move(t)});
+  }
+  // a member at the front of object `o` (its text starts with '{')
+  void insert_member(std::string_view doc, FlatDoc::View o, const std::string& member) {
+    const size_t b = size_t(o.raw().data() - doc.data()) + 1;
+    es.push_back({b, b, o.size() ? member + "," : member});
+  }
+  std::string apply(std::string_view doc) {
+    std::sort(es.begin(), es.end(), [](const E& a, const E& b) { return a.beg < b.beg; });
+    std::string out;
+    size_t extra = 0;
+    for (const E& e : es) extra += e.text.size();
+    out.reserve(doc.size() + extra);
+    size_t at = 0;
+    for (const E& e : es) {
+      out.append(doc.substr(at, e.beg - at));
+      out.append(e.text);
+      at = e.end;
+    }
+    out.append(doc.substr(at));
+    return out;
+  }
+};
+
+std::string quoted(std::string_view x) { return dump(Value::str(std::string(x))); }
 
 struct HistEv {
   int64_t rv;
@@ -102,6 +200,7 @@ struct HistEv {
 struct FieldSel {
   struct Req {
     std::vector<std::string> path;
+    std::string key;           // the dotted path
     bool eq;
     std::string val;
   };
@@ -134,6 +233,7 @@ struct FieldSel {
         return false;
       }
       k = std::string(trim(k));
+      r.key = k;
       r.val = std::string(trim(r.val));
       size_t s = 0;
       while (true) {
@@ -159,6 +259,45 @@ struct FieldSel {
     return dump(*v);
   }
 
+  static std::string field(FlatDoc::View v, const std::vector<std::string>& path) {
+    for (const auto& k : path) {
+      if (!v.is(FlatDoc::Obj)) return "";
+      v = v.get(k);
+      if (!v || v.t() == FlatDoc::Null) return "";
+    }
+    if (v.t() == FlatDoc::Str || v.t() == FlatDoc::Num) return std::string(v.str());
+    if (v.t() == FlatDoc::Bool) return v.b() ? "True" : "False";
+    return dump(yk::parse(std::string(v.raw())));   // objects / arrays: the DOM's text
+  }
+
+  // through the version's field cache; a miss reads the DOM if it exists, else the flat view
+  static const std::string& field(const Stored& s, const Req& r) {
+    for (const auto& f : s.fields)
+      if (f.first == r.key) return f.second;
+    s.fields.emplace_back(r.key, s.dom ? field(*s.dom, r.path) : field(s.fv(), r.path));
+    return s.fields.back().second;
+  }
+
+  bool matches(const Stored& s) const {
+    for (const Req& r : reqs) {
+      const std::string& v = field(s, r);
+      if (r.eq ? v != r.val : v == r.val) return false;
+    }
+    return true;
+  }
+
+  bool matches(FlatDoc::View obj) const {
+    for (size_t i = 0; i < reqs.size(); ++i) {
+      std::string v = field(obj, reqs[i].path);
+      if (reqs[i].eq) {
+        if (v != reqs[i].val) return false;
+      } else if (v == reqs[i].val) {
+        return false;
+      }
+    }
+    return true;
+  }
+
   bool matches(const Value& obj) const {
     // group by path like the Python matcher: several '=' on one path never all hold
     for (size_t i = 0; i < reqs.size(); ++i) {
@@ -173,7 +312,7 @@ struct FieldSel {
   }
 };
 
-char filter_event(const FieldSel& sel, char type, const Value& obj, const Value* old) {
+char filter_event(const FieldSel& sel, char type, const Stored& obj, const Stored* old) {
   if (type == 'A' || type == 'D') return sel.matches(obj) ? type : 0;
   if (type != 'M') return type;
   bool now = sel.matches(obj);
@@ -307,8 +446,7 @@ class Server {
   }
 
   void emit(ResState& rs, char type, const SP& obj, const SP& old) {
-    const Value* m = obj->v.get("metadata");
-    int64_t rv = m && m->get("resourceVersion") ? m->get("resourceVersion")->as_int() : last_rv_;
+    const int64_t rv = obj->rv ? obj->rv : last_rv_;
     rs.hist.push_back(HistEv{rv, type, obj, old});
     while (rs.hist.size() > opt_.history) {
       rs.oldest_rv = rs.hist.front().rv;
@@ -316,11 +454,11 @@ class Server {
     }
     if (rs.watchers.empty()) return;
     std::string frames[3];
-    std::string ns = m ? std::string(m->sv("namespace")) : "";
+    const std::string& ns = obj->ns;
     for (Watcher* w : rs.watchers) {
       if (w->dead) continue;
       if (!w->ns.empty() && ns != w->ns) continue;
-      char t = w->sel.empty() ? type : filter_event(w->sel, type, obj->v, old ? &old->v : nullptr);
+      char t = w->sel.empty() ? type : filter_event(w->sel, type, *obj, old.get());
       if (!t) continue;
       int fi = t == 'A' ? 0 : t == 'M' ? 1 : 2;
       if (frames[fi].empty()) frames[fi] = frame(t, obj->text);
@@ -392,20 +530,20 @@ class Server {
     }
     SP cur = it->second;
     std::string_view rv = bm ? bm->sv("resourceVersion") : std::string_view();
-    const Value* cm = cur->v.get("metadata");
+    const Value* cm = cur->v().get("metadata");
     if (!rv.empty() && cm && rv != cm->sv("resourceVersion")) {
       *err = {409, "Conflict", std::string(d.key) + " " + key + ": the object has been modified"};
       return nullptr;
     }
     Value nv;
     if (status_only) {
-      nv = cur->v;
+      nv = cur->v();
       const Value* st = body.get("status");
       nv.at("status") = st ? *st : Value();
     } else {
       nv = body;
       if (!body.get("status")) {
-        if (const Value* cst = cur->v.get("status")) nv.at("status") = *cst;
+        if (const Value* cst = cur->v().get("status")) nv.at("status") = *cst;
       }
     }
     Value meta = cm ? *cm : Value::object();
@@ -432,12 +570,12 @@ class Server {
       return nullptr;
     }
     SP cur = it->second;
-    Value nv = cur->v;
+    Value nv = cur->v();
     merge_patch(nv, p);
     Value& meta = nv.at("metadata");
     if (meta.t != Value::Obj) meta = Value::object();
     meta.at("resourceVersion") = Value::str(next_rv());
-    if (const Value* cm = cur->v.get("metadata")) {
+    if (const Value* cm = cur->v().get("metadata")) {
       for (const char* k : {"uid", "name", "namespace", "creationTimestamp"})
         if (const Value* x = cm->get(k)) meta.at(k) = *x;
     }
@@ -455,9 +593,24 @@ class Server {
     }
     SP cur = it->second;
     rs.objs.erase(it);
-    Value gone = cur->v;
-    gone.at("metadata").at("resourceVersion") = Value::str(next_rv());
-    SP s = make_stored(std::move(gone));
+    // the deleted object as stored, with the deletion's resourceVersion
+    const std::string rvs = next_rv();
+    SP s;
+    if (cur->rv_off != std::string::npos) {
+      std::string t;
+      t.reserve(cur->text.size() + 4);
+      t.append(cur->text, 0, cur->rv_off).append(quoted(rvs)).append(cur->text, cur->rv_off + cur->rv_len,
+                                                                       std::string::npos);
+      s = make_stored_text(std::move(t), last_rv_, cur->ns, cur.get(), {"metadata.resourceVersion"});
+    } else if (FlatDoc::View rvv = cur->fv() ? cur->fv().get("metadata").get("resourceVersion") : FlatDoc::View()) {
+      TextEdits ed;
+      ed.replace(cur->text, rvv, quoted(rvs));
+      s = make_stored_text(ed.apply(cur->text), last_rv_, cur->ns, cur.get(), {"metadata.resourceVersion"});
+    } else {
+      Value gone = cur->v();
+      gone.at("metadata").at("resourceVersion") = Value::str(rvs);
+      s = make_stored(std::move(gone));
+    }
     emit(rs, 'D', s, nullptr);
     return s;
   }
@@ -471,45 +624,95 @@ class Server {
       return false;
     }
     SP cur = it->second;
+    const std::string& doc = cur->text;
+    FlatDoc::View root = cur->fv();
+    if (!root.is(FlatDoc::Obj)) {
+      *err = {500, "InternalError", "pods " + key + ": stored object unreadable"};
+      return false;
+    }
+    FlatDoc::View meta = root.get("metadata"), spec = root.get("spec"), status = root.get("status");
     const Value* bm = body.get("metadata");
     std::string_view uid = bm ? bm->sv("uid") : std::string_view();
-    const Value* cm = cur->v.get("metadata");
-    if (!uid.empty() && cm && cm->sv("uid") != uid) {
+    if (!uid.empty() && meta && meta.sv("uid") != uid) {
       *err = {409, "Conflict", "pod " + key + " uid mismatch"};
       return false;
     }
-    const Value* cs = cur->v.get("spec");
-    if (cs && !cs->sv("nodeName").empty()) {
-      *err = {409, "Conflict", "pod " + key + " is already assigned to node " + std::string(cs->sv("nodeName"))};
+    if (spec && !spec.sv("nodeName").empty()) {
+      *err = {409, "Conflict", "pod " + key + " is already assigned to node " + std::string(spec.sv("nodeName"))};
       return false;
     }
     const Value* tgt = body.get("target");
-    std::string node = tgt ? std::string(tgt->sv("name")) : "";
-    Value nv = cur->v;
-    nv.at("spec").at("nodeName") = Value::str(node);
-    Value& status = nv.at("status");
-    if (status.t != Value::Obj) status = Value::object();
-    Value conds = Value::array();
-    if (const Value* old = status.get("conditions"); old && old->t == Value::Arr) {
-      for (const auto& c : old->arr)
-        if (c.sv("type") != "PodScheduled") conds.arr.push_back(c);
+    const std::string node = tgt ? std::string(tgt->sv("name")) : "";
+    const std::string rvs = next_rv();
+    TextEdits ed;
+    // spec.nodeName
+    const std::string nn = "\"nodeName\":" + quoted(node);
+    if (spec.is(FlatDoc::Obj)) {
+      if (FlatDoc::View x = spec.get("nodeName")) ed.replace(doc, x, quoted(node));
+      else ed.insert_member(doc, spec, nn);
+    } else if (spec) {
+      ed.replace(doc, spec, "{" + nn + "}");
+    } else {
+      ed.insert_member(doc, root, "\"spec\":{" + nn + "}");
     }
-    Value c = Value::object();
-    c.at("type") = Value::str("PodScheduled");
-    c.at("status") = Value::str("True");
-    c.at("lastTransitionTime") = Value::str(rfc3339_now());
-    conds.arr.push_back(std::move(c));
-    status.at("conditions") = std::move(conds);
-    Value& meta = nv.at("metadata");
-    if (bm) {
-      if (const Value* ann = bm->get("annotations"); ann && ann->t == Value::Obj && !ann->obj.empty()) {
-        Value& ma = meta.at("annotations");
-        if (ma.t != Value::Obj) ma = Value::object();
-        for (const auto& kv : ann->obj) ma.at(kv.first) = kv.second;
+    // status.conditions: PodScheduled replaced by a fresh True condition
+    std::string conds = "[";
+    FlatDoc::View oc = status.is(FlatDoc::Obj) ? status.get("conditions") : FlatDoc::View();
+    if (oc.is(FlatDoc::Arr))
+      for (FlatDoc::View c = oc.first(); c; c = c.next())
+        if (c.sv("type") != "PodScheduled") conds.append(c.raw()).push_back(',');
+    conds.append("{\"type\":\"PodScheduled\",\"status\":\"True\",\"lastTransitionTime\":\"")
+        .append(rfc3339_now()).append("\"}]");
+    if (status.is(FlatDoc::Obj)) {
+      if (oc) ed.replace(doc, oc, conds);
+      else ed.insert_member(doc, status, "\"conditions\":" + conds);
+    } else if (status) {
+      ed.replace(doc, status, "{\"conditions\":" + conds + "}");
+    } else {
+      ed.insert_member(doc, root, "\"status\":{\"conditions\":" + conds + "}");
+    }
+    // metadata: the Binding's annotations merged, a new resourceVersion
+    if (meta.is(FlatDoc::Obj)) {
+      if (FlatDoc::View x = meta.get("resourceVersion")) ed.replace(doc, x, quoted(rvs));
+      else ed.insert_member(doc, meta, "\"resourceVersion\":" + quoted(rvs));
+      const Value* ann = bm ? bm->get("annotations") : nullptr;
+      if (ann && ann->t == Value::Obj && !ann->obj.empty()) {
+        FlatDoc::View ma = meta.get("annotations");
+        if (ma.is(FlatDoc::Obj)) {
+          std::string add;
+          for (const auto& kv : ann->obj) {
+            if (FlatDoc::View x = ma.get(kv.first)) {
+              ed.replace(doc, x, dump(kv.second));
+            } else {
+              if (!add.empty()) add.push_back(',');
+              add.append(quoted(kv.first)).push_back(':');
+              add.append(dump(kv.second));
+            }
+          }
+          if (!add.empty()) ed.insert_member(doc, ma, add);
+        } else {
+          std::string obj = "{";
+          for (const auto& kv : ann->obj) {
+            if (obj.size() > 1) obj.push_back(',');
+            obj.append(quoted(kv.first)).push_back(':');
+            obj.append(dump(kv.second));
+          }
+          obj.push_back('}');
+          if (ma) ed.replace(doc, ma, obj);
+          else ed.insert_member(doc, meta, "\"annotations\":" + obj);
+        }
       }
+    } else {
+      *err = {500, "InternalError", "pods " + key + ": no metadata"};
+      --last_rv_;
+      return false;
     }
-    meta.at("resourceVersion") = Value::str(next_rv());
-    SP s = make_stored(std::move(nv));
+    SP s = make_stored_text(ed.apply(doc), last_rv_, cur->ns, cur.get(),
+                            {"spec.nodeName", "status.conditions", "metadata.resourceVersion", "metadata.annotations",
+                             // an inserted spec / status holds only the edited member; one that
+                             // was not an object was replaced whole
+                             spec && !spec.is(FlatDoc::Obj) ? "spec" : "spec.nodeName",
+                             status && !status.is(FlatDoc::Obj) ? "status" : "status.conditions"});
     it->second = s;
     bind_log_[key] = mono();
     emit(rs, 'M', s, cur);
@@ -557,6 +760,10 @@ class Server {
   std::unordered_map<int, std::unique_ptr<Conn>> conns_;
   // bench
   std::vector<Value> templates_;
+  struct TmplText {
+    std::string ns, meta_rest, top_rest;   // ",members..." of metadata (less the per-pod ones) / of the root
+  };
+  std::vector<TmplText> tmpl_text_;
   std::unordered_map<std::string, double> create_log_, bind_log_;
 };
 
@@ -661,11 +868,8 @@ void Server::handle_list(Conn* c, ResState& rs, const std::string& ns, const Req
   auto it = paged && !start.empty() ? rs.objs.upper_bound(start) : rs.objs.begin();
   for (; it != rs.objs.end(); ++it) {
     const Stored& s = *it->second;
-    if (d.namespaced && !ns.empty()) {
-      const Value* m = s.v.get("metadata");
-      if (!m || m->sv("namespace") != ns) continue;
-    }
-    if (!sel.empty() && !sel.matches(s.v)) continue;
+    if (d.namespaced && !ns.empty() && s.ns != ns) continue;
+    if (!sel.empty() && !sel.matches(s)) continue;
     if (paged && limit > 0 && n >= limit) {
       more = true;
       break;
@@ -714,11 +918,8 @@ void Server::start_watch(Conn* c, ResState& rs, const std::string& ns, const Req
   if (rv) {
     for (const HistEv& h : rs.hist) {
       if (h.rv <= rv) continue;
-      if (!w->ns.empty()) {
-        const Value* m = h.obj->v.get("metadata");
-        if (!m || m->sv("namespace") != w->ns) continue;
-      }
-      char t = w->sel.empty() ? h.type : filter_event(w->sel, h.type, h.obj->v, h.old ? &h.old->v : nullptr);
+      if (!w->ns.empty() && h.obj->ns != w->ns) continue;
+      char t = w->sel.empty() ? h.type : filter_event(w->sel, h.type, *h.obj, h.old.get());
       if (!t) continue;
       c->wbuf.append(frame(t, h.obj->text));
     }
@@ -739,7 +940,36 @@ void Server::handle_bench(Conn* c, Request& req) {
       return;
     }
     templates_.clear();
+    tmpl_text_.clear();
     if (const Value* ps = b.get("pods"); ps && ps->t == Value::Arr) templates_ = ps->arr;
+    // each template as text around the per-pod metadata (name, uid, resourceVersion,
+    // creationTimestamp): a burst pod is then spliced, not copied and re-serialised — what
+    // create() would store, with those four members first in metadata
+    for (const Value& t : templates_) {
+      TmplText tt;
+      Value o = t;
+      if (o.t != Value::Obj) break;
+      if (!o.get("apiVersion")) o.at("apiVersion") = Value::str(kRes[0].api_version());
+      if (!o.get("kind")) o.at("kind") = Value::str(kRes[0].kind);
+      Value& meta = o.at("metadata");
+      if (meta.t != Value::Obj) meta = Value::object();
+      if (meta.sv("namespace").empty()) meta.at("namespace") = Value::str("default");
+      tt.ns = std::string(meta.sv("namespace"));
+      Value rest = Value::object();
+      for (auto& kv : meta.obj)
+        if (kv.first != "name" && kv.first != "uid" && kv.first != "resourceVersion" &&
+            kv.first != "creationTimestamp" && kv.first != "generateName")
+          rest.obj.push_back(kv);
+      const std::string mr = dump(rest);             // {...}
+      tt.meta_rest = mr.size() > 2 ? "," + mr.substr(1, mr.size() - 2) : "";
+      Value top = Value::object();
+      for (auto& kv : o.obj)
+        if (kv.first != "metadata") top.obj.push_back(kv);
+      const std::string tr = dump(top);
+      tt.top_rest = tr.size() > 2 ? "," + tr.substr(1, tr.size() - 2) : "";
+      tmpl_text_.push_back(std::move(tt));
+    }
+    if (tmpl_text_.size() != templates_.size()) tmpl_text_.clear();   // a template create() must handle
     respond(c, 200, "{\"n\":" + std::to_string(templates_.size()) + "}");
     return;
   }
@@ -756,11 +986,34 @@ void Server::handle_bench(Conn* c, Request& req) {
     create_log_.clear();
     bind_log_.clear();
     size_t i = 0;
+    const std::string ts = rfc3339_now();
     for (const Value& t : templates_) {
-      Value o = t;
-      o.at("metadata").at("name") = Value::str(tag + "-" + std::to_string(i));
-      ApiErr err;
-      create(pods, std::move(o), "", &err);
+      const std::string name = tag + "-" + std::to_string(i);
+      if (!tmpl_text_.empty()) {
+        const TmplText& tt = tmpl_text_[i];
+        std::string key = tt.ns + "/" + name;
+        if (!pods.objs.count(key)) {
+          char ub[24];
+          snprintf(ub, sizeof(ub), "-%012llx", static_cast<unsigned long long>(++uid_counter_));
+          const std::string rvs = next_rv();
+          std::string text;
+          text.reserve(tt.meta_rest.size() + tt.top_rest.size() + 160);
+          text.append("{\"metadata\":{\"name\":").append(quoted(name));
+          text.append(",\"uid\":").append(quoted(uid_prefix_ + ub));
+          text.append(",\"resourceVersion\":\"").append(rvs).append("\"");
+          text.append(",\"creationTimestamp\":\"").append(ts).append("\"");
+          text.append(tt.meta_rest).append("}").append(tt.top_rest).append("}");
+          SP s = make_stored_text(std::move(text), last_rv_, tt.ns);
+          pods.objs[key] = s;
+          create_log_[key] = mono();
+          emit(pods, 'A', s, nullptr);
+        }
+      } else {
+        Value o = t;
+        o.at("metadata").at("name") = Value::str(name);
+        ApiErr err;
+        create(pods, std::move(o), "", &err);
+      }
       if (++i % 64 == 0) {
         // let the watchers see the burst while it is being created
         std::vector<Conn*> d;

@@ -282,6 +282,52 @@ def test_native_apiserver_crud_watch_bind_and_selectors(native_api):
     run(go())
 
 
+def test_native_apiserver_bind_and_delete_edit_the_stored_text(native_api):
+    """The fake apiserver binds and deletes pods by editing the stored JSON text (no DOM copy):
+    the Binding's annotations merge into existing ones (same key replaced), other conditions
+    survive while PodScheduled is replaced, status/spec members the edit does not touch stay,
+    a field selector on an untouched path keeps matching through bind and delete, and every
+    version carries its own resourceVersion."""
+    async def go():
+        cl = KubeClient(KubeConfig(native_api.url), native=True)
+        try:
+            await cl.create("nodes", make_node("n1"))
+            _, rv = await cl.list("pods")
+            got = []
+
+            async def watcher():
+                async for typ, obj in cl.watch("pods", rv, field_selector="status.phase!=Succeeded"):
+                    got.append((typ, obj["metadata"]["resourceVersion"], obj["spec"].get("nodeName")))
+                    if len(got) == 3:
+                        return
+            t = asyncio.get_event_loop().create_task(watcher())
+            await asyncio.sleep(0.05)
+            p = await cl.create("pods", {
+                "metadata": {"name": "q", "annotations": {"keep": "1", "scv.amd.com/gpus": "old"}},
+                "spec": {"schedulerName": "x", "nodeName": ""},
+                "status": {"phase": "Pending", "conditions": [
+                    {"type": "Initialized", "status": "True"},
+                    {"type": "PodScheduled", "status": "False", "reason": "Unschedulable"}]}})
+            await cl.bind("default", "q", p["metadata"]["uid"], "n1",
+                          {"scv.amd.com/gpus": "0,1", "scv.amd.com/reserved-mb": "512"})
+            pod = await cl.get("pods", "q", "default")
+            assert pod["spec"] == {"schedulerName": "x", "nodeName": "n1"}
+            assert pod["metadata"]["annotations"] == {"keep": "1", "scv.amd.com/gpus": "0,1",
+                                                     "scv.amd.com/reserved-mb": "512"}
+            conds = pod["status"]["conditions"]
+            assert [c["type"] for c in conds] == ["Initialized", "PodScheduled"] and conds[1]["status"] == "True"
+            assert pod["status"]["phase"] == "Pending"
+            assert int(pod["metadata"]["resourceVersion"]) > int(p["metadata"]["resourceVersion"])
+            await cl.delete("pods", "q", "default")
+            await asyncio.wait_for(t, 5)
+            assert [g[0] for g in got] == ["ADDED", "MODIFIED", "DELETED"]
+            rvs = [int(g[1]) for g in got]
+            assert rvs == sorted(rvs) and len(set(rvs)) == 3 and got[1][2] == "n1" and got[2][2] == "n1"
+        finally:
+            await cl.close()
+    run(go())
+
+
 def test_transport_bind_many_routes_each_answer_to_its_callback(native_api):
     """A run of Bindings handed over in one call: each pod gets its own answer (201 for the
     good ones, 409 for a wrong uid) through its own callback, with its annotations applied."""
