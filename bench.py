@@ -256,9 +256,22 @@ def main(argv=None) -> int:
                     s, c, lw, n = s + st["engine_s"], c + st["engine_cpu_s"], lw + st["lock_wait_s"], n + st["engine_pods"]
             return s, c, lw, n
 
+        def watch_decode() -> float:
+            """I/O-thread CPU seconds spent decoding watch lines (native transport)."""
+            t = 0.0
+            for sh in {id(x): x for x in shards}.values():
+                nat = getattr(getattr(sh.sched, "client", None), "native", None)
+                if nat is not None:
+                    try:
+                        t += nat.stats().get("watch_cpu_s", 0.0)
+                    except Exception:  # noqa: BLE001 - transport closed
+                        pass
+            return t
+
         sync()
         a0 = api_cpu()
         as0 = api_sys[0]
+        wd0 = watch_decode()
         le0 = lane_engine()
         th0 = thread_cpu()
         t0 = time.perf_counter()
@@ -275,6 +288,7 @@ def main(argv=None) -> int:
         api_sys_s = api_sys[0] - as0
         th1 = thread_cpu()
         le1 = lane_engine()
+        wd1 = watch_decode()
         my_bound = sum(r.bound for r in results)
         threads = {k: round((v - th0.get(k, 0.0)) / my_bound * 1e6, 2) for k, v in sorted(th1.items())
                    if my_bound and v - th0.get(k, 0.0) > 0}
@@ -327,6 +341,7 @@ def main(argv=None) -> int:
             # rank 0's process CPU per pod by thread (≥ 10 ms clock-tick resolution per thread)
             "thread_cpu_us_per_pod": threads,
             # of which the lane thread spent inside the engine's batch cycles (wall, rank 0)
+            "io_watch_decode_us_per_pod": round((wd1 - wd0) / my_bound * 1e6, 2) if my_bound else None,
             "lane_engine_us_per_pod": ({"wall": round((le1[0] - le0[0]) / (le1[3] - le0[3]) * 1e6, 2),
                                         "cpu": round((le1[1] - le0[1]) / (le1[3] - le0[3]) * 1e6, 2),
                                         "lock_wait": round((le1[2] - le0[2]) / (le1[3] - le0[3]) * 1e6, 2)}

@@ -5,6 +5,7 @@
 #include <pybind11/stl.h>
 
 #include "json.hpp"
+#include "flatjson.hpp"
 #include "project.hpp"
 #include "transport.hpp"
 
@@ -112,6 +113,29 @@ PYBIND11_MODULE(_yoda_kube, m) {
     pe->raw = raw;
     return pe;
   }, py::arg("raw"), "Project a pod's JSON through the flat decoder the watch stream uses.");
+  // the watch stream's light path vs its parser path, for parity tests: (type, object text,
+  // identity tuple), or None when the scanner defers to the parser
+  auto ident_tuple = [](const PodProj& p) {
+    return py::make_tuple(p.ns, p.name, p.uid, p.rv, p.creation, p.deleting, p.sched, p.node, p.phase);
+  };
+  m.def("scan_identity", [ident_tuple](const std::string& line) -> py::object {
+    PodProj p;
+    char t = 0;
+    std::string_view obj;
+    if (!scan_watch_identity(line, &t, &obj, p)) return py::none();
+    return py::make_tuple(std::string(1, t), std::string(obj), ident_tuple(p));
+  }, py::arg("line"));
+  m.def("flat_identity", [ident_tuple](const std::string& line) -> py::object {
+    FlatDoc d;
+    if (!d.parse(line) || !d.root().is(FlatDoc::Obj)) return py::none();
+    const FlatDoc::View obj = d.root().get("object");
+    if (!obj) return py::none();
+    PodProj p;
+    project_identity(obj, p);
+    const std::string_view t = d.root().sv("type");
+    return py::make_tuple(std::string(1, t == "ADDED" ? 'A' : t == "MODIFIED" ? 'M' : t == "DELETED" ? 'D' : '?'),
+                          std::string(obj.raw()), ident_tuple(p));
+  }, py::arg("line"));
   // PodList body → (resourceVersion, continue, [PodEvent]) — relists of large clusters
   // never build Python dicts either
   m.def("project_list", [](const std::string& body) {
@@ -234,6 +258,7 @@ PYBIND11_MODULE(_yoda_kube, m) {
         d["watch_events"] = s.watch_events;
         d["watch_bytes"] = s.watch_bytes;
         d["parse_errors"] = s.parse_errors;
+        d["watch_cpu_s"] = s.watch_cpu_s;
         d["bytes_out"] = s.bytes_out;
         d["bytes_in"] = s.bytes_in;
         d["throttled"] = s.throttled;

@@ -4,6 +4,8 @@
 
 #include <cstring>
 
+#include <cstring>
+
 namespace yk {
 
 namespace {
@@ -529,6 +531,228 @@ void project_identity(const FlatDoc::View& pod, PodProj& p) {
   p.sched = sched.empty() ? "default-scheduler" : std::string(sched);
   p.node = std::string(sp ? sp.sv("nodeName") : std::string_view());
   if (const FlatDoc::View st = pod.get("status")) p.phase = std::string(st.sv("phase"));
+}
+
+namespace {
+
+// A skipping scanner over JSON text: walks members without building a document. Strings with
+// escapes in a key or a value the caller reads make it give up (the caller then parses).
+struct Skim {
+  const char* p;
+  const char* e;
+
+  void ws() {
+    while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+  }
+  // p at '"': the raw content, whether it holds a backslash; p past the closing quote
+  bool str(std::string_view* out, bool* esc) {
+    if (p >= e || *p != '"') return false;
+    const char* s = ++p;
+    bool bs = false;
+    for (;;) {
+      const char* q = static_cast<const char*>(std::memchr(p, '"', size_t(e - p)));
+      if (!q) return false;
+      size_t n = 0;
+      for (const char* b = q; b > s && b[-1] == '\\'; --b) ++n;
+      if (n) bs = true;
+      if ((n & 1) == 0) {
+        *out = std::string_view(s, size_t(q - s));
+        *esc = bs || std::memchr(s, '\\', size_t(q - s)) != nullptr;
+        p = q + 1;
+        return true;
+      }
+      p = q + 1;
+    }
+  }
+  bool skip() {
+    ws();
+    if (p >= e) return false;
+    const char c = *p;
+    std::string_view sv;
+    bool esc;
+    if (c == '"') return str(&sv, &esc);
+    if (c == '{' || c == '[') {
+      int depth = 0;
+      while (p < e) {
+        const char ch = *p;
+        if (ch == '"') {
+          if (!str(&sv, &esc)) return false;
+          continue;
+        }
+        if (ch == '{' || ch == '[') {
+          ++depth;
+        } else if (ch == '}' || ch == ']') {
+          if (--depth == 0) {
+            ++p;
+            return true;
+          }
+        }
+        ++p;
+      }
+      return false;
+    }
+    const char* s = p;
+    while (p < e && *p != ',' && *p != '}' && *p != ']' && *p != ' ' && *p != '\n' && *p != '\r' && *p != '\t') ++p;
+    return p > s;
+  }
+  // members of the object at p: on(key) consumes the value and returns true, or returns false
+  // to have it skipped. False on malformed input or an escaped key.
+  template <class F>
+  bool object(F&& on) {
+    ws();
+    if (p >= e || *p != '{') return false;
+    ++p;
+    ws();
+    if (p < e && *p == '}') {
+      ++p;
+      return true;
+    }
+    for (;;) {
+      ws();
+      std::string_view k;
+      bool esc;
+      if (!str(&k, &esc) || esc) return false;
+      ws();
+      if (p >= e || *p != ':') return false;
+      ++p;
+      ws();
+      if (!on(k) && !skip()) return false;
+      ws();
+      if (p < e && *p == ',') {
+        ++p;
+        continue;
+      }
+      if (p < e && *p == '}') {
+        ++p;
+        return true;
+      }
+      return false;
+    }
+  }
+  // a member value read as FlatDoc's sv(): the string, or "" for any other type
+  bool sv(std::string_view* out, bool* ok) {
+    ws();
+    if (p < e && *p == '"') {
+      bool esc;
+      if (!str(out, &esc)) return false;
+      if (esc) *ok = false;
+      return true;
+    }
+    *out = std::string_view();
+    return skip();
+  }
+  // FlatDoc::View::truthy() of the value
+  bool truthy(bool* out) {
+    ws();
+    if (p >= e) return false;
+    const char* s = p;
+    const char c = *p;
+    if (!skip()) return false;
+    const std::string_view t(s, size_t(p - s));
+    if (c == '"') *out = t.size() > 2;
+    else if (c == '{' || c == '[') *out = t.find_first_not_of(" \n\r\t", 1) != t.size() - 1;
+    else if (c == 't') *out = true;
+    else if (c == 'f' || c == 'n') *out = false;
+    else *out = t.find_first_of("123456789") != std::string_view::npos;
+    return true;
+  }
+};
+
+}  // namespace
+
+bool scan_watch_identity(std::string_view line, char* type, std::string_view* obj, PodProj& p) {
+  p = PodProj();
+  Skim k{line.data(), line.data() + line.size()};
+  bool ok = true, have_type = false, have_obj = false;
+  std::string_view tname;
+  bool seen_meta = false, seen_spec = false, seen_status = false;
+  bool ns_set = false;
+  int seen = 0;
+  std::string_view ns, name, uid, rv, creation, sched, node, phase;
+  bool deleting = false;
+  auto meta = [&](std::string_view key) -> bool {
+    if (key == "namespace") {
+      if (ns_set) return false;
+      ns_set = true;
+      k.ws();
+      if (k.p < k.e && *k.p == '"') {
+        bool esc;
+        if (!k.str(&ns, &esc)) return ok = false;
+        if (esc) ok = false;
+        return true;
+      }
+      ns = "default";
+      return k.skip() || (ok = false);
+    }
+    // the first occurrence of a key counts, as FlatDoc::View::get finds it
+    const int bit = key == "name" ? 1 : key == "uid" ? 2 : key == "resourceVersion" ? 4 : key == "creationTimestamp" ? 8
+                    : key == "deletionTimestamp" ? 16 : 0;
+    if (!bit || (seen & bit)) return false;
+    seen |= bit;
+    if (bit == 16) return k.truthy(&deleting) || (ok = false);
+    std::string_view* f = bit == 1 ? &name : bit == 2 ? &uid : bit == 4 ? &rv : &creation;
+    return k.sv(f, &ok) || (ok = false);
+  };
+  auto spec = [&](std::string_view key) -> bool {
+    const int bit = key == "schedulerName" ? 32 : key == "nodeName" ? 64 : 0;
+    if (!bit || (seen & bit)) return false;
+    seen |= bit;
+    return k.sv(bit == 32 ? &sched : &node, &ok) || (ok = false);
+  };
+  auto status = [&](std::string_view key) -> bool {
+    if (key != "phase" || (seen & 128)) return false;
+    seen |= 128;
+    return k.sv(&phase, &ok) || (ok = false);
+  };
+  auto pod = [&](std::string_view key) -> bool {
+    k.ws();
+    const bool is_obj = k.p < k.e && *k.p == '{';
+    if (key == "metadata" && !seen_meta) {
+      seen_meta = true;
+      if (is_obj) return k.object(meta) || (ok = false);
+    } else if (key == "spec" && !seen_spec) {
+      seen_spec = true;
+      if (is_obj) return k.object(spec) || (ok = false);
+    } else if (key == "status" && !seen_status) {
+      seen_status = true;
+      if (is_obj) return k.object(status) || (ok = false);
+    }
+    return false;
+  };
+  auto top = [&](std::string_view key) -> bool {
+    if (key == "type" && !have_type) {
+      have_type = true;
+      bool esc;
+      k.ws();
+      if (k.p >= k.e || *k.p != '"' || !k.str(&tname, &esc) || esc) return ok = false, true;
+      return true;
+    }
+    if (key == "object" && !have_obj) {
+      have_obj = true;
+      k.ws();
+      const char* s = k.p;
+      if (!k.object(pod)) return ok = false, true;
+      *obj = std::string_view(s, size_t(k.p - s));
+      return true;
+    }
+    return false;
+  };
+  if (!k.object(top) || !ok || !have_type || !have_obj) return false;
+  k.ws();
+  if (k.p != k.e) return false;
+  *type = tname == "ADDED" ? 'A' : tname == "MODIFIED" ? 'M' : tname == "DELETED" ? 'D' : tname == "BOOKMARK" ? 'B'
+          : tname == "ERROR" ? 'E' : '?';
+  p.ns = ns_set ? std::string(ns) : "default";
+  p.name = std::string(name);
+  p.uid = std::string(uid);
+  if (p.uid.empty()) p.uid = p.ns + "/" + p.name;
+  p.rv = std::string(rv);
+  p.creation = std::string(creation);
+  p.deleting = deleting;
+  p.sched = sched.empty() ? "default-scheduler" : std::string(sched);
+  p.node = std::string(node);
+  p.phase = std::string(phase);
+  return true;
 }
 
 void merge_non_identity(PodProj& d, PodProj&& s) {

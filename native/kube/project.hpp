@@ -79,6 +79,11 @@ bool project_pod_text(std::string_view text, PodProj& p);
 // Identity fields only (ns, name, uid, rv, creation, deleting, scheduler, node, phase); `ok`
 // stays false and the hash 0 — see PodEv::full().
 void project_identity(const FlatDoc::View& pod, PodProj& p);
+// The watch stream's light path: one skipping scan of an event line {"type":..,"object":{..}}
+// for the event type, the object's text span and the pod's identity fields (as
+// project_identity reads them), building no document. False when the line needs the parser
+// (escapes in a field it reads, malformed text): the caller then takes the FlatDoc path.
+bool scan_watch_identity(std::string_view line, char* type, std::string_view* obj, PodProj& p);
 // Fill everything but the identity fields from a full projection (`src` is consumed).
 void merge_non_identity(PodProj& dst, PodProj&& src);
 

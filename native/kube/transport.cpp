@@ -590,9 +590,18 @@ void Transport::on_body(Conn* c, const char* data, size_t n) {
 }
 
 
+namespace {
+double thread_cpu_s() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (double)ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+}  // namespace
+
 void Transport::watch_lines(Conn* c) {
   // one flat parse per event line ({"type":..., "object":{...}}): no per-value allocation;
   // pods are projected from the same document (project.hpp)
+  const double cpu0 = thread_cpu_s();
   size_t start = 0;
   uint64_t nev = 0, nerr = 0;
   FlatDoc doc;
@@ -608,6 +617,25 @@ void Transport::watch_lines(Conn* c) {
         break;
       }
     if (blank) continue;
+    if (c->pods && light_pods_.load(std::memory_order_relaxed)) {
+      // echoes and deletions with a lane attached: the identity fields by one skipping scan,
+      // the rest of the pod on demand (PodEv::full)
+      char t = 0;
+      std::string_view obj;
+      auto pe = std::make_shared<PodEv>();
+      if (scan_watch_identity(line, &t, &obj, pe->p) && (t == 'M' || t == 'D')) {
+        WatchEvent ev;
+        ev.type = t;
+        ev.rv = pe->p.rv;
+        pe->light = true;
+        pe->complete = &complete_pod_ev;
+        pe->raw.assign(obj.data(), obj.size());
+        ev.pod = std::move(pe);
+        c->evs.push_back(std::move(ev));
+        nev++;
+        continue;
+      }
+    }
     if (!doc.parse(line) || !doc.root().is(FlatDoc::Obj)) {
       nerr++;
       continue;
@@ -649,9 +677,11 @@ void Transport::watch_lines(Conn* c) {
   }
   if (start) c->lines.erase(0, start);
   if (nev || nerr) {
+    const double dc = thread_cpu_s() - cpu0;
     std::lock_guard<std::mutex> g(stats_mu_);
     stats_.watch_events += nev;
     stats_.parse_errors += nerr;
+    stats_.watch_cpu_s += dc;
   }
 }
 

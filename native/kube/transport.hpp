@@ -61,6 +61,7 @@ struct TransportStats {
   uint64_t requests = 0, responses = 0, errors = 0, timeouts = 0, connects = 0;
   uint64_t watch_events = 0, watch_bytes = 0, parse_errors = 0, bytes_out = 0, bytes_in = 0;
   uint64_t throttled = 0;
+  double watch_cpu_s = 0;     // I/O thread CPU decoding watch lines (parse + projection)
 };
 
 // PodEv::complete for light events (flat re-parse of `raw`, full projection)

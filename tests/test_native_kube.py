@@ -186,6 +186,34 @@ def test_flat_projection_equals_dom_projection(pod, status, pretty):
     assert a.hash == b.hash
 
 
+@settings(max_examples=300, deadline=None)
+@given(_pod, st.sampled_from(["MODIFIED", "DELETED", "ADDED"]),
+       st.sampled_from([None, {}, {"phase": "Running"}, {"phase": 3}, [], "x"]),
+       st.sampled_from([None, "", "2026-01-01T00:00:00Z", 0, 1, 0.5, {}, {"a": 1}, [], [0], True, False]),
+       st.booleans(), st.booleans())
+def test_watch_identity_scan_equals_the_parser(pod, typ, status, deletion, pretty, escaped):
+    """The transport reads echo and delete events of a lane-attached pod watch with a skipping
+    scan instead of the flat parser: type, object span and every identity field agree with
+    the parser path; a field with escapes makes the scan defer (None), never disagree."""
+    pod = dict(pod)
+    if status is not None:
+        pod["status"] = status
+    meta = dict(pod["metadata"], resourceVersion="17")
+    if deletion is not None:
+        meta["deletionTimestamp"] = deletion
+    if escaped:
+        meta["name"] = 'p\\"1'
+    pod["metadata"] = meta
+    line = json.dumps({"type": typ, "object": pod}, indent=2 if pretty else None).replace("\n", " ")
+    want = K.flat_identity(line)
+    got = K.scan_identity(line)
+    if escaped:
+        assert got is None
+    else:
+        assert got == want
+        assert json.loads(got[1]) == pod
+
+
 def test_flat_projection_rejects_malformed_json_like_the_dom():
     for bad in ['{"metadata": {"name": "p"}', '{"a": tru}', '{"a": "x\\q"}', '[1, 2,]', '{"a": 01}', '"\x01"']:
         with pytest.raises(ValueError):
