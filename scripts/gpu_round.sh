@@ -32,6 +32,25 @@ for s in $STEPS; do
     profinproc) step prof_inproc 600 python scripts/profile_bench.py --out gpurun_out/prof_inproc.txt --steps 20 --warmup 5 ;;
     pmc) step pmc 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES --kernel-trace --stats --output-format csv -d gpurun_out/pmc -o dev -- python3 scripts/device_bench.py --nodes 4096 --pods 40 --kinds single,gang4 --paths gpu ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    kbprof) step kbprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kbprof -o kb -- python3 scripts/device_batch_bench.py --nodes 4096 --pods 1032 --batch 256 --modes batch ;;
+    kbtrace) step kbtrace 300 python scripts/device_batch_bench.py --nodes 4096,16384 --pods 1032 --batch 256 --modes batch --trace ;;
+    all)   # every BASELINE config (+ 6) on this box, one JSON line each under gpurun_out/all/
+      mkdir -p gpurun_out/all
+      for spec in "c3|--config 3 --steps 20 --warmup 5" "c1|--config 1 --steps 20 --warmup 2" \
+                  "c2|--config 2 --steps 10 --warmup 2" "c4|--config 4 --steps 10 --warmup 2" \
+                  "c5|--config 5 --steps 5 --warmup 2" "c6|--config 6 --steps 5 --warmup 1" \
+                  "c6off|--config 6 --steps 2 --warmup 1 --device off" \
+                  "c3ref|--config 3 --steps 1 --warmup 0 --reference-qps" "c3b|--config 3 --steps 20 --warmup 5"; do
+        step "all/${spec%%|*}" 300 python bench.py --alt none ${spec#*|}
+      done
+      python - <<'PY'
+import glob, json
+for f in sorted(glob.glob("gpurun_out/all/*.log")):
+    d = json.loads(open(f).read().strip().splitlines()[-1])
+    print(f.split("/")[-1], d["value"], d["p50_latency_ms"], d["p99_latency_ms"], d.get("e2e_scheduling_p99_ms"),
+          d["cpu_us_per_pod"], d.get("apiserver_cpu_us_per_pod"), d["device_cycles"])
+PY
+      ;;
   esac
 done
 echo "=== done"
