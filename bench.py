@@ -133,32 +133,6 @@ def host_info() -> dict:
             "kernel": os.uname().release, "calib_loop_ms": round(best * 1e3, 3)}
 
 
-def l3_cpu_sets() -> list:
-    """The CPUs this process may use, grouped by shared last-level cache (one group per CCD on
-    EPYC), in CPU order; [] when the topology is not readable."""
-    groups: dict = {}
-    try:
-        for c in sorted(os.sched_getaffinity(0)):
-            with open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list") as f:
-                groups.setdefault(f.read().strip(), []).append(c)
-    except (OSError, AttributeError):
-        return []
-    return sorted(groups.values(), key=lambda g: g[0])
-
-
-def pin_to_l3(local_rank: int):
-    """Keep this rank's scheduler threads (and its apiserver child) on one last-level cache:
-    watch events, queue entries and Binding answers cross three threads and a process per pod,
-    and cross-CCD cache-line traffic made per-pod CPU vary 3x between runs on one box. Rank r
-    takes the r-th cache domain. Returns the CPU list, or None when there is one domain."""
-    sets = l3_cpu_sets()
-    if len(sets) < 2:
-        return None
-    cpus = sets[local_rank % len(sets)]
-    os.sched_setaffinity(0, cpus)
-    return cpus
-
-
 def rank_gpu_index(local_rank: int, n_visible: int) -> int:
     """GPU of a rank: LOCAL_RANK modulo the visible devices (one rank per GPU under
     torch.distributed.run; several ranks share a GPU only in CPU/gloo rehearsals)."""
@@ -204,7 +178,9 @@ def main(argv=None) -> int:
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     # before any thread exists: threads and the apiserver child inherit the mask
-    pinned = pin_to_l3(local_rank) if a.pin == "l3" else None
+    # (yoda_scheduler_amd/utils/affinity.py: on one box 99-108 k vs 51-68 k pods/s unpinned)
+    from yoda_scheduler_amd.utils.affinity import pin_l3
+    pinned = pin_l3(local_rank) if a.pin == "l3" else None
 
     import torch
     import torch.distributed as dist

@@ -696,3 +696,32 @@ def test_scv_engine_view_matches_dataclass_path():
         assert LazyScv(obj, scv_engine_view(obj, False, ids), ids).card_idents() == want_ids
         assert lz.is_stale(1.7e9 + trial + 100, 3.0) == ref.is_stale(1.7e9 + trial + 100, 3.0)
         assert lz.card_number == ref.status.card_number and lz.status.card_list == ref.status.card_list
+
+
+def test_cpu_affinity_spec_and_l3_grouping(monkeypatch):
+    """--cpu-affinity: `none` leaves the mask alone, `l3:<i>` pins to the i-th last-level-cache
+    domain of the allowed CPUs (modulo their number), a single domain is left alone."""
+    import os
+
+    from yoda_scheduler_amd.utils import affinity
+    assert affinity.apply("none") is None
+    with pytest.raises(ValueError):
+        affinity.apply("numa")
+    shared = {0: "0-1,4-5", 1: "0-1,4-5", 4: "0-1,4-5", 5: "0-1,4-5", 2: "2-3,6-7", 3: "2-3,6-7", 6: "2-3,6-7",
+              7: "2-3,6-7"}
+    real_open = open
+
+    def fake_open(path, *a, **k):
+        if path.startswith("/sys/devices/system/cpu/cpu") and path.endswith("shared_cpu_list"):
+            import io
+            return io.StringIO(shared[int(path.split("/cpu/cpu")[1].split("/")[0])])
+        return real_open(path, *a, **k)
+    got = []
+    monkeypatch.setattr("builtins.open", fake_open)
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(8)))
+    monkeypatch.setattr(os, "sched_setaffinity", lambda pid, cpus: got.append(list(cpus)))
+    assert affinity.l3_cpu_sets() == [[0, 1, 4, 5], [2, 3, 6, 7]]
+    assert affinity.apply("l3") == [0, 1, 4, 5] and affinity.apply("l3:3") == [2, 3, 6, 7]
+    assert got == [[0, 1, 4, 5], [2, 3, 6, 7]]
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: {0, 1})
+    assert affinity.apply("l3") is None

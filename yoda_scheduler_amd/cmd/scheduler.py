@@ -62,6 +62,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--kube-api-qps", type=float, default=None)
     p.add_argument("--kube-api-burst", type=int, default=None)
     p.add_argument("--device-scorer", choices=["auto", "on", "off"], default=None)
+    p.add_argument("--cpu-affinity", default="none",
+                   help="none | l3 | l3:<index>: run the scheduler's threads on one last-level-cache domain")
     p.add_argument("--fake-cluster", type=int, default=0, help="dev: in-process fake apiserver with N 8xMI355X nodes")
     p.add_argument("--fake-apiserver-port", type=int, default=-1, help="dev: expose the fake apiserver over HTTP")
     p.add_argument("--trace", action="store_true", help="record scheduling spans (served at /debug/trace)")
@@ -81,6 +83,11 @@ def new_scheduler_command(*plugins: PluginOption) -> Callable[[Optional[Sequence
     def main(argv: Optional[Sequence[str]] = None) -> int:
         args, unknown = build_parser().parse_known_args(argv)
         klog.setup(args.v)
+        # before the transport, lane and engine threads exist: they inherit the CPU mask
+        from ..utils import affinity
+        pinned = affinity.apply(args.cpu_affinity)
+        if pinned:
+            log.info("cpu affinity: %s", ",".join(map(str, pinned)))
         if unknown:
             log.warning("ignoring unsupported kube-scheduler flags: %s", " ".join(unknown))
         registry = default_registry()
