@@ -488,8 +488,10 @@ PYBIND11_MODULE(_yoda_core, m) {
   py::class_<Lane>(m, "Lane")
       .def(py::init([](Engine& e, int batch, double bind_timeout, int sort_kind, bool events, bool events_v1,
                        double event_qps, int event_burst, int event_buffer, const std::string& host,
-                       const std::string& name_prefix) {
+                       const std::string& name_prefix, int async_mode, int engine_delay_us) {
              LaneOptions o;
+             o.async_mode = async_mode;
+             o.engine_delay_us = engine_delay_us;
              o.batch = batch;
              o.bind_timeout_s = bind_timeout;
              o.sort_kind = sort_kind;
@@ -505,7 +507,8 @@ PYBIND11_MODULE(_yoda_core, m) {
            py::arg("engine"), py::arg("batch") = 256, py::arg("bind_timeout") = 30.0, py::arg("sort_kind") = 0,
            py::arg("events") = true, py::arg("events_v1") = true, py::arg("event_qps") = 50.0,
            py::arg("event_burst") = 300, py::arg("event_buffer") = 1000, py::arg("host") = "localhost",
-           py::arg("name_prefix") = "00000000", py::keep_alive<1, 2>())
+           py::arg("name_prefix") = "00000000", py::arg("async_mode") = 1,
+           py::arg("engine_delay_us") = 0, py::keep_alive<1, 2>())
       .def("sink_ptr", [](Lane& l) { return (uintptr_t) static_cast<yk::PodSink*>(&l); })
       .def("set_port", [](Lane& l, uintptr_t p) { l.set_port(reinterpret_cast<yk::PodPort*>(p)); })
       // the profile's engine configuration is the engine's current one (the caller applied it)
@@ -598,6 +601,7 @@ PYBIND11_MODULE(_yoda_core, m) {
              d["binding"] = s.binding;
              d["owned"] = s.owned;
              d["engine_s"] = s.engine_s;
+             d["left_in_flight"] = s.left_in_flight;
              d["engine_pods"] = s.engine_pods;
              d["engine_cpu_s"] = s.engine_cpu_s;
              d["lock_wait_s"] = s.lock_wait_s;

@@ -146,6 +146,10 @@ Lane::Lane(Engine* e, std::recursive_mutex* engine_mu, LaneOptions o) : eng_(e),
     pthread_setname_np(pthread_self(), "yoda-lane");   // per-thread CPU in bench / top -H
     run();
   });
+  wk_th_ = std::thread([this] {
+    pthread_setname_np(pthread_self(), "yoda-lane-eng");
+    engine_worker();
+  });
 }
 
 Lane::~Lane() { close(); }
@@ -154,11 +158,16 @@ void Lane::close() {
   {
     std::lock_guard<std::mutex> g(in_mu_);
     if (stop_.exchange(true)) {
-      if (!th_.joinable()) return;
+      if (!th_.joinable() && !wk_th_.joinable()) return;
     }
     in_cv_.notify_all();
   }
   if (th_.joinable()) th_.join();
+  {
+    std::lock_guard<std::mutex> g(wk_mu_);
+    wk_cv_.notify_all();
+  }
+  if (wk_th_.joinable()) wk_th_.join();
   relist_cv_.notify_all();
   if (efd_ >= 0) {
     ::close(efd_);
@@ -319,7 +328,7 @@ void Lane::wait_idle(double timeout_s) {
       std::lock_guard<std::mutex> g(stat_mu_);
       queued = st_.queued > 0 && active_.load();
     }
-    if (inbox_.empty() && !busy_ && !queued) return;
+    if (inbox_.empty() && !busy_ && !run_inflight_ && !queued) return;
     lk.unlock();
     std::this_thread::sleep_for(std::chrono::microseconds(200));
     lk.lock();
@@ -717,14 +726,156 @@ void Lane::annotations(const Profile& pr, const Entry& e, const PodReq& req, con
   if (req.has_memory) out->emplace_back("scv.amd.com/reserved-mb", std::to_string(req.memory));
 }
 
+// The engine's part of a run: requests from the pods' projections, the batch cycle under the
+// engine lock (a device batch drops it while the GPU works), node names. Touches no lane
+// store state, so it runs on the lane thread or on the engine worker alike.
+void Lane::engine_step(Run& r) {
+  const size_t n = r.evs.size();
+  r.reqs.resize(n);
+  r.ok.assign(n, 1);
+  std::vector<uint64_t> eids;
+  std::vector<const PodReq*> rp;
+  const double tw = mono();
+  std::unique_lock<std::recursive_mutex> lk(*emu_);
+  {
+    const double dw = mono() - tw;
+    std::lock_guard<std::mutex> g(stat_mu_);
+    st_.lock_wait_s += dw;
+  }
+  for (size_t k = 0; k < n; ++k) {
+    try {
+      r.ok[k] = make_req(r.evs[k]->full(), &r.reqs[k]);
+    } catch (const std::exception&) {
+      r.ok[k] = 0;
+    }
+    if (!r.ok[k]) continue;
+    eids.push_back(r.ids[k]);
+    rp.push_back(&r.reqs[k]);
+    r.slot.push_back(k);
+  }
+  const EngineConfig saved = eng_->config();
+  eng_->set_config(r.cfg);
+  const double te = mono(), tc = thread_cpu();
+  try {
+    r.res = eng_->schedule_batch(eids, rp);
+  } catch (const std::exception&) {
+    r.res.clear();
+  }
+  {
+    const double dc = thread_cpu() - tc;
+    std::lock_guard<std::mutex> g(stat_mu_);
+    st_.engine_s += mono() - te;
+    st_.engine_cpu_s += dc;
+    st_.engine_pods += eids.size();
+  }
+  // restore the caller's configuration unless it re-configured the engine while a device
+  // batch had the lock dropped (then its newer configuration stays)
+  if (config_eq(eng_->config(), r.cfg)) eng_->set_config(saved);
+  r.failed = r.res.size() != eids.size();
+  if (o_.engine_delay_us > 0) {
+    lk.unlock();
+    std::this_thread::sleep_for(std::chrono::microseconds(o_.engine_delay_us));
+    lk.lock();
+  }
+  r.names.resize(r.res.size());
+  for (size_t k = 0; k < r.res.size(); ++k)
+    if (r.res[k].node >= 0) r.names[k] = eng_->node(r.res[k].node).name;
+}
+
+// The lane's part after the engine: assumed pods go to BINDING and their Bindings out;
+// unschedulable ones to Python; failures back to the queue. Entries are looked up by id: a
+// pod deleted, bound elsewhere or taken by Python while its run was on the engine worker is
+// gone from by_id_, and whatever the engine reserved for it is released.
+void Lane::finish_run(Run& r, std::vector<yk::BindSpec>* binds, std::vector<uint64_t>* tags, std::vector<Fwd>* fwd) {
+  const Profile& pr = r.pr;
+  std::lock_guard<std::mutex> g(store_mu_);
+  auto entry = [&](size_t k) -> Entry* {
+    auto it = by_id_.find(r.ids[k]);
+    return it != by_id_.end() && it->second->st == INFLIGHT ? it->second : nullptr;
+  };
+  for (size_t k = 0; k < r.ids.size(); ++k)
+    if (!r.ok[k])
+      if (Entry* e = entry(k)) {          // a pod the projection cannot express natively
+        drop_owned(e, false);
+        forward('A', e->ev, nullptr, fwd);
+      }
+  if (r.failed) {                         // engine failure: the pods retry from the lane queue
+    for (size_t k : r.slot) {
+      to_release_.push_back(r.ids[k]);
+      if (Entry* e = entry(k)) {
+        set_state(e, QUEUED);
+        e->seq = ++seq_;
+        heap_.push(QItem{e->prio, e->seq, e->id});
+      }
+    }
+    return;
+  }
+  for (size_t q = 0; q < r.res.size(); ++q) {
+    const size_t k = r.slot[q];
+    const CycleResult& res = r.res[q];
+    Entry* e = entry(k);
+    if (!e) {
+      if (res.node >= 0 && !res.stale) to_release_.push_back(r.ids[k]);
+      std::lock_guard<std::mutex> g2(stat_mu_);
+      st_.left_in_flight++;
+      continue;
+    }
+    e->t_cycle = r.t0;
+    if (res.stale) {
+      {
+        std::lock_guard<std::mutex> g2(stat_mu_);
+        st_.stale_retries++;
+      }
+      set_state(e, QUEUED);
+      e->seq = ++seq_;
+      heap_.push(QItem{e->prio, e->seq, e->id});
+      continue;
+    }
+    if (res.node < 0) {
+      Handoff h;
+      h.kind = Handoff::kUnschedulable;
+      h.ev = e->ev;
+      h.profile = pr.name;
+      h.res = res;
+      h.t_enqueue = e->t_enq;
+      h.t_cycle = r.t0;
+      drop_owned(e, false);
+      hand_pending_.push_back(std::move(h));
+      std::lock_guard<std::mutex> g2(stat_mu_);
+      st_.unschedulable++;
+      continue;
+    }
+    e->node = res.node;
+    e->node_name = r.names[q];
+    e->cards = res.cards;
+    set_state(e, BINDING);
+    log_add(*e);
+    yk::BindSpec b;
+    b.ns = e->ev->p.ns;
+    b.name = e->ev->p.name;
+    b.uid = e->ev->p.uid;
+    b.node = e->node_name;
+    annotations(pr, *e, r.reqs[k], res, &b.annotations);
+    binds->push_back(std::move(b));
+    tags->push_back(e->id);
+    e->bind_out = true;
+    std::lock_guard<std::mutex> g2(stat_mu_);
+    st_.binding++;
+  }
+}
+
 void Lane::schedule_some() {
   if (!active_.load() || heap_.empty()) return;
+  {
+    std::lock_guard<std::mutex> g(in_mu_);
+    if (paused_ || run_inflight_) return;
+  }
   yk::PodPort* port = port_.load();
   if (!port) return;
-  std::vector<Entry*> run;
+  std::vector<Entry*> picked;
   {
     std::lock_guard<std::mutex> g(store_mu_);
-    while (!heap_.empty() && (int)run.size() < o_.batch) {
+    while (!heap_.empty() && (int)picked.size() < o_.batch) {
       const QItem q = heap_.top();
       heap_.pop();
       auto it = by_id_.find(q.id);
@@ -732,144 +883,82 @@ void Lane::schedule_some() {
       Entry* e = it->second;
       if (e->st != QUEUED || e->seq != q.seq || e->prio != q.prio) continue;   // stale heap item
       set_state(e, INFLIGHT);
-      run.push_back(e);
+      picked.push_back(e);
     }
   }
-  if (run.empty()) return;
+  if (picked.empty()) return;
   const double t0 = mono();
+  // consecutive pods of one profile share an engine batch (profiles differ in engine config)
+  std::vector<std::shared_ptr<Run>> runs;
+  for (size_t i = 0; i < picked.size();) {
+    auto r = std::make_shared<Run>();
+    r->prof = picked[i]->prof;
+    r->pr = lp_[r->prof];
+    r->cfg = r->pr.cfg;
+    r->t0 = t0;
+    for (; i < picked.size() && picked[i]->prof == r->prof; ++i) {
+      r->ids.push_back(picked[i]->id);
+      r->evs.push_back(picked[i]->ev);
+    }
+    runs.push_back(std::move(r));
+  }
+  bool async = false;
+  {
+    std::lock_guard<std::recursive_mutex> lk(*emu_);
+    async = o_.async_mode == 2 || (o_.async_mode == 1 && eng_->device_enabled());
+  }
+  if (async) {
+    // the GPU places the batch while this thread keeps serving answers, echoes and deletions;
+    // the runs come back through the inbox (kRunDone) and the next batch starts after them
+    {
+      std::lock_guard<std::mutex> g(in_mu_);
+      run_inflight_ = true;
+    }
+    {
+      std::lock_guard<std::mutex> g(wk_mu_);
+      wk_jobs_ = std::move(runs);
+    }
+    wk_cv_.notify_one();
+    return;
+  }
+  for (auto& r : runs) engine_step(*r);
+  complete_runs(runs);
+}
+
+void Lane::complete_runs(std::vector<std::shared_ptr<Run>>& runs) {
   std::vector<yk::BindSpec> binds;
   std::vector<uint64_t> tags;
   std::vector<Fwd> fwd;
-  binds.reserve(run.size());
-  tags.reserve(run.size());
-  // consecutive pods of one profile share an engine batch (profiles differ in engine config)
-  size_t i = 0;
-  while (i < run.size()) {
-    size_t j = i;
-    const int prof = run[i]->prof;
-    while (j < run.size() && run[j]->prof == prof) ++j;
-    const Profile& pr = lp_[prof];
-    const size_t n = j - i;
-    std::vector<PodReq> reqs(n);
-    std::vector<char> ok(n, 1);
-    std::vector<uint64_t> ids;
-    std::vector<const PodReq*> rp;
-    std::vector<size_t> slot;
-    std::vector<CycleResult> res;
-    std::vector<std::string> names;
-    const double tw = mono();
-    {
-      std::unique_lock<std::recursive_mutex> lk(*emu_);
-      {
-        const double dw = mono() - tw;
-        std::lock_guard<std::mutex> g(stat_mu_);
-        st_.lock_wait_s += dw;
-      }
-      for (size_t k = 0; k < n; ++k) {
-        try {
-          ok[k] = make_req(run[i + k]->ev->full(), &reqs[k]);
-        } catch (const std::exception&) {
-          ok[k] = 0;
-        }
-        if (!ok[k]) continue;
-        ids.push_back(run[i + k]->id);
-        rp.push_back(&reqs[k]);
-        slot.push_back(k);
-      }
-      const EngineConfig saved = eng_->config();
-      eng_->set_config(pr.cfg);
-      const double te = mono(), tc = thread_cpu();
-      try {
-        res = eng_->schedule_batch(ids, rp);
-      } catch (const std::exception&) {
-        res.clear();
-      }
-      {
-        const double dc = thread_cpu() - tc;
-        std::lock_guard<std::mutex> g(stat_mu_);
-        st_.engine_s += mono() - te;
-        st_.engine_cpu_s += dc;
-        st_.engine_pods += ids.size();
-      }
-      // restore the caller's configuration unless it re-configured the engine while a
-      // device batch had the lock dropped (then its newer configuration stays)
-      if (config_eq(eng_->config(), pr.cfg)) eng_->set_config(saved);
-      names.resize(res.size());
-      for (size_t k = 0; k < res.size(); ++k)
-        if (res[k].node >= 0) names[k] = eng_->node(res[k].node).name;
-    }
-    {
-      std::lock_guard<std::mutex> g(store_mu_);
-      for (size_t k = 0; k < n; ++k)
-        if (!ok[k]) {                     // a pod the projection cannot express natively
-          Entry* e = run[i + k];
-          drop_owned(e, false);
-          forward('A', e->ev, nullptr, &fwd);
-        }
-      if (res.size() != ids.size()) {     // engine failure: the pods retry from the lane queue
-        for (size_t k = 0; k < ids.size(); ++k) {
-          Entry* e = run[i + slot[k]];
-          to_release_.push_back(e->id);
-          set_state(e, QUEUED);
-          e->seq = ++seq_;
-          heap_.push(QItem{e->prio, e->seq, e->id});
-        }
-      } else {
-        for (size_t k = 0; k < res.size(); ++k) {
-          Entry* e = run[i + slot[k]];
-          const CycleResult& r = res[k];
-          e->t_cycle = t0;
-          if (r.stale) {
-            {
-              std::lock_guard<std::mutex> g2(stat_mu_);
-              st_.stale_retries++;
-            }
-            set_state(e, QUEUED);
-            e->seq = ++seq_;
-            heap_.push(QItem{e->prio, e->seq, e->id});
-            continue;
-          }
-          if (r.node < 0) {
-            Handoff h;
-            h.kind = Handoff::kUnschedulable;
-            h.ev = e->ev;
-            h.profile = pr.name;
-            h.res = r;
-            h.t_enqueue = e->t_enq;
-            h.t_cycle = t0;
-            drop_owned(e, false);
-            hand_pending_.push_back(std::move(h));
-            std::lock_guard<std::mutex> g2(stat_mu_);
-            st_.unschedulable++;
-            continue;
-          }
-          e->node = r.node;
-          e->node_name = names[k];
-          e->cards = r.cards;
-          set_state(e, BINDING);
-          log_add(*e);
-          yk::BindSpec b;
-          b.ns = e->ev->p.ns;
-          b.name = e->ev->p.name;
-          b.uid = e->ev->p.uid;
-          b.node = e->node_name;
-          annotations(pr, *e, reqs[slot[k]], r, &b.annotations);
-          binds.push_back(std::move(b));
-          tags.push_back(e->id);
-          e->bind_out = true;
-          std::lock_guard<std::mutex> g2(stat_mu_);
-          st_.binding++;
-        }
-      }
-    }
-    i = j;
-  }
-  if (!binds.empty()) port->bind_native(std::move(binds), tags, o_.bind_timeout_s, this);
+  for (auto& r : runs) finish_run(*r, &binds, &tags, &fwd);
+  yk::PodPort* port = port_.load();
+  if (!binds.empty() && port) port->bind_native(std::move(binds), tags, o_.bind_timeout_s, this);
   {
     std::lock_guard<std::mutex> g(stat_mu_);
     st_.batches++;
   }
   if (!fwd.empty()) publish(std::move(fwd), {});
+}
+
+// The engine worker (async device runs): one set of runs at a time, handed back in order.
+void Lane::engine_worker() {
+  for (;;) {
+    std::vector<std::shared_ptr<Run>> jobs;
+    {
+      std::unique_lock<std::mutex> lk(wk_mu_);
+      wk_cv_.wait(lk, [&] { return stop_.load() || !wk_jobs_.empty(); });
+      if (wk_jobs_.empty()) return;   // stopping and nothing left
+      jobs.swap(wk_jobs_);
+    }
+    for (auto& r : jobs) engine_step(*r);
+    Item it;
+    it.k = Item::kRunDone;
+    it.runs = std::make_shared<std::vector<std::shared_ptr<Run>>>(std::move(jobs));
+    {
+      std::lock_guard<std::mutex> g(in_mu_);
+      inbox_.push_back(std::move(it));
+    }
+    in_cv_.notify_one();
+  }
 }
 
 void Lane::log_add(const Entry& e) {
@@ -939,7 +1028,7 @@ void Lane::pause(bool on) {
   std::unique_lock<std::mutex> lk(in_mu_);
   paused_ = on;
   in_cv_.notify_all();
-  if (on) idle_cv_.wait(lk, [&] { return !busy_ || stop_.load(); });
+  if (on) idle_cv_.wait(lk, [&] { return (!busy_ && !run_inflight_) || stop_.load(); });
 }
 
 void Lane::record_scheduled(const Entry& e) {
@@ -1029,8 +1118,10 @@ void Lane::run() {
   for (;;) {
     {
       std::unique_lock<std::mutex> lk(in_mu_);
+      // paused: only a run already on the engine worker comes back (pause() waits for it)
       auto ready = [&] {
-        return stop_.load() || (!paused_ && (!inbox_.empty() || (active_.load() && !heap_.empty())));
+        return stop_.load() || (!inbox_.empty() && (!paused_ || run_inflight_)) ||
+               (!paused_ && !run_inflight_ && active_.load() && !heap_.empty());
       };
       if (!ready()) {
         if (!ev_q_.empty() && o_.event_qps > 0) {
@@ -1050,10 +1141,14 @@ void Lane::run() {
     }
     std::vector<Fwd> fwd;
     std::vector<std::pair<uint64_t, std::vector<Fwd>>> relists;
+    std::vector<std::shared_ptr<Run>> done;
     {
       std::lock_guard<std::mutex> g(store_mu_);
       for (auto& it : work) {
         switch (it.k) {
+          case Item::kRunDone:
+            for (auto& r : *it.runs) done.push_back(r);
+            break;
           case Item::kEvent: handle_event(it.type, it.ev, &fwd); break;
           case Item::kAnswer: handle_answer(it.tag, it.status, it.body, it.t); break;
           case Item::kProfiles: apply_profiles(&fwd); break;
@@ -1067,6 +1162,12 @@ void Lane::run() {
       }
     }
     work.clear();
+    if (!done.empty()) {
+      // after this turn's events: a pod deleted meanwhile is already out of by_id_
+      complete_runs(done);
+      std::lock_guard<std::mutex> g(in_mu_);
+      run_inflight_ = false;
+    }
     if (!to_release_.empty()) {
       std::lock_guard<std::recursive_mutex> lk(*emu_);
       for (uint64_t id : to_release_) eng_->release(id);

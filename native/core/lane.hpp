@@ -49,6 +49,11 @@ struct LaneOptions {
   std::string host = "localhost";
   std::string name_prefix = "00000000";
   size_t e2e_keep = 1 << 20;       // raw e2e samples kept until Python takes them
+  // runs on an engine worker thread, the lane serving its inbox (answers, echoes, deletions)
+  // meanwhile: 0 never, 1 when the engine has a device scorer (the GPU places the batch),
+  // 2 always (tests of the in-flight paths)
+  int async_mode = 1;
+  int engine_delay_us = 0;         // tests: widen the in-flight window of every run
 };
 
 struct LaneStats {
@@ -56,6 +61,7 @@ struct LaneStats {
   uint64_t forwarded = 0, released = 0, batches = 0, confirmed = 0, events_recorded = 0, events_dropped = 0;
   uint64_t events_written = 0, event_errors = 0, lost_answers_kept = 0;
   uint64_t queued = 0, inflight = 0, binding = 0, owned = 0;   // gauges
+  uint64_t left_in_flight = 0;   // pods gone (deleted, bound elsewhere) while their run was on the engine
   double engine_s = 0;        // wall time inside Engine::schedule_batch (lane thread)
   double engine_cpu_s = 0;    // ... of which on the CPU (the rest: the engine lock, the device)
   double lock_wait_s = 0;     // waiting for the engine lock before a run
@@ -162,8 +168,23 @@ class Lane : public yk::PodSink {
     uint64_t id;             // entry id; an item whose entry moved on is skipped when popped
     bool operator<(const QItem& o) const { return prio != o.prio ? prio < o.prio : seq > o.seq; }
   };
+  // one engine batch of consecutive same-profile pods (engine_step fills the second half)
+  struct Run {
+    int prof = -1;
+    Profile pr;                                      // a copy: profiles may change meanwhile
+    EngineConfig cfg;
+    double t0 = 0;
+    std::vector<uint64_t> ids;                       // entry ids, run order
+    std::vector<std::shared_ptr<yk::PodEv>> evs;
+    std::vector<PodReq> reqs;
+    std::vector<char> ok;                            // projection expressible natively
+    std::vector<size_t> slot;                        // run index of each engine batch member
+    std::vector<CycleResult> res;
+    std::vector<std::string> names;
+    bool failed = false;
+  };
   struct Item {             // inbox: events, answers, commands — applied in order
-    enum K : uint8_t { kEvent, kAnswer, kRelist, kProfiles } k = kEvent;
+    enum K : uint8_t { kEvent, kAnswer, kRelist, kProfiles, kRunDone } k = kEvent;
     char type = 0;
     std::shared_ptr<yk::PodEv> ev;
     uint64_t tag = 0;
@@ -172,6 +193,7 @@ class Lane : public yk::PodSink {
     double t = 0;             // answers: when the I/O thread read it
     std::shared_ptr<std::vector<std::shared_ptr<yk::PodEv>>> items;
     uint64_t token = 0;
+    std::shared_ptr<std::vector<std::shared_ptr<Run>>> runs;   // kRunDone
   };
   struct PendingEvent {
     std::string ns, name, uid, node, profile;
@@ -188,6 +210,10 @@ class Lane : public yk::PodSink {
   void set_state(Entry* e, St s);
   void bind_settled(Entry* e);
   void schedule_some();
+  void engine_step(Run& r);
+  void finish_run(Run& r, std::vector<yk::BindSpec>* binds, std::vector<uint64_t>* tags, std::vector<Fwd>* fwd);
+  void complete_runs(std::vector<std::shared_ptr<Run>>& runs);
+  void engine_worker();
   bool admissible(const yk::PodProj& p, int* prof) const;
   int64_t prio_of(const yk::PodProj& p) const;
   bool make_req(const yk::PodProj& p, PodReq* r);
@@ -218,6 +244,13 @@ class Lane : public yk::PodSink {
   std::unordered_map<uint64_t, std::vector<Fwd>> relist_out_;
   bool busy_ = false;                // lane thread is processing (wait_idle)
   bool paused_ = false;
+  bool run_inflight_ = false;        // runs on the engine worker (in_mu_)
+
+  // engine worker (async device runs)
+  std::thread wk_th_;
+  std::mutex wk_mu_;
+  std::condition_variable wk_cv_;
+  std::vector<std::shared_ptr<Run>> wk_jobs_;
   std::condition_variable idle_cv_;
 
   // change log of reserved lane pods (changes()); off until Python first asks

@@ -467,13 +467,18 @@ def test_transport_rate_limit_timeouts_and_refused_connection():
         finally:
             await cl.close()
             await api.stop()
-        # nothing listens: the request fails with a connection error, not a hang
-        dead = KubeClient(KubeConfig(url), native=True, timeout=2.0)
+        # nothing listens: the request fails with a connection error, not a hang. The port is
+        # held bound (not listening) so a parallel test cannot start a server on it.
+        import socket
+        hold = socket.socket()
+        hold.bind(("127.0.0.1", 0))
+        dead = KubeClient(KubeConfig(f"http://127.0.0.1:{hold.getsockname()[1]}"), native=True, timeout=2.0)
         try:
             with pytest.raises((ConnectionError, asyncio.TimeoutError)):
                 await dead.get("nodes", "n1")
         finally:
             await dead.close()
+            hold.close()
     run(go())
 
 

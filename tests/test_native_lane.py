@@ -302,3 +302,35 @@ def test_finish_cycle_refuses_a_result_whose_node_slot_was_reused():
         return out
     pending, cached, queued, reserved = run(go())
     assert pending == 0 and not cached and queued and not reserved
+
+
+def test_async_runs_survive_deletes_and_rebinds_while_on_the_engine(monkeypatch):
+    """Runs on the engine worker (the device-scorer path, forced here with a widened window):
+    the lane keeps applying events meanwhile. Pods deleted while their run is on the engine
+    never bind and leave no reservation; the others bind and confirm; the ledger is exact."""
+    monkeypatch.setenv("YODA_LANE_ASYNC", "2")
+    monkeypatch.setenv("YODA_LANE_ENGINE_DELAY_US", "30000")
+
+    async def go():
+        cfg = yoda_config(batch=16)
+        async with Env(cfg=cfg, nodes=(("n1", 8, None), ("n2", 8, None))) as e:
+            for i in range(96):
+                await e.create(pod(f"a{i}", {"scv/memory": "2048", "scv/number": str(1 + i % 2)}))
+            await asyncio.sleep(0.02)                # the first runs are on the engine worker
+            for i in range(0, 96, 2):
+                await e.cl.delete("pods", f"a{i}", "default")
+            lane = e.sched.lane.lane
+            assert await e.wait(lambda: lane.stats()["confirmed"] >= 48 and lane.stats()["queued"] == 0
+                                and lane.stats()["inflight"] == 0, 20.0), lane.stats()
+            pods = await e.pods()
+            assert sorted(pods) == sorted(f"a{i}" for i in range(1, 96, 2))
+            assert all(p["spec"].get("nodeName") for p in pods.values())
+            assert await e.wait(lambda: e.sched.engine.ledger_size == 48), e.sched.engine.ledger_size
+            assert lane.stats()["left_in_flight"] > 0      # the in-flight path was taken
+            want = sum(2048 * (1 + i % 2) for i in range(1, 96, 2))
+            got = sum(g["reserved"] for n in ("n1", "n2") for g in e.sched.cache.node_gpu_state(n))
+            assert got == want
+            for i in range(1, 96, 2):
+                await e.cl.delete("pods", f"a{i}", "default")
+            assert await e.wait(lambda: e.sched.engine.ledger_size == 0 and lane.stats()["owned"] == 0)
+    run(go())

@@ -22,6 +22,7 @@ This module is everything Python still does, none of it per lane pod:
 from __future__ import annotations
 
 import asyncio
+import os
 import contextlib
 import logging
 from typing import Optional
@@ -45,7 +46,11 @@ class NativeLane:
                                 sort_kind=max(self.sort_kind, 0), events=rec.enabled,
                                 events_v1=rec.api == API_EVENTS_V1, event_qps=float(rec.limiter.qps),
                                 event_burst=int(rec.limiter.burst), event_buffer=rec.max_buffer, host=rec.host,
-                                name_prefix=rec._name_prefix)
+                                name_prefix=rec._name_prefix,
+                                # runs on an engine worker while the lane serves its inbox: with a
+                                # device scorer (1, default), never (0), always (2: tests)
+                                async_mode=int(os.environ.get("YODA_LANE_ASYNC", "1")),
+                                engine_delay_us=int(os.environ.get("YODA_LANE_ENGINE_DELAY_US", "0")))
         self.lane.set_port(transport.t.port_ptr())
         self._profiles: dict[str, tuple] = {}
         self._loop: Optional[asyncio.AbstractEventLoop] = None
