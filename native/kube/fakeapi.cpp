@@ -742,6 +742,14 @@ class Server {
 
   void handle(Conn* c, Request& req);
   void handle_bench(Conn* c, Request& req);
+  void step_jobs();
+  struct BenchJob {
+    bool del = false;
+    std::string tag, ts;
+    size_t n = 0, next = 0;
+    std::vector<std::string> keys;
+  };
+  std::deque<BenchJob> jobs_;
   void handle_list(Conn* c, ResState& rs, const std::string& ns, const Request& req);
   void start_watch(Conn* c, ResState& rs, const std::string& ns, const Request& req);
   void finish_watch(Conn* c);
@@ -983,44 +991,12 @@ void Server::handle_bench(Conn* c, Request& req) {
     }
     std::string tag = std::string(b.sv("tag"));
     if (tag.empty()) tag = "b";
-    create_log_.clear();
-    bind_log_.clear();
-    size_t i = 0;
-    const std::string ts = rfc3339_now();
-    for (const Value& t : templates_) {
-      const std::string name = tag + "-" + std::to_string(i);
-      if (!tmpl_text_.empty()) {
-        const TmplText& tt = tmpl_text_[i];
-        std::string key = tt.ns + "/" + name;
-        if (!pods.objs.count(key)) {
-          char ub[24];
-          snprintf(ub, sizeof(ub), "-%012llx", static_cast<unsigned long long>(++uid_counter_));
-          const std::string rvs = next_rv();
-          std::string text;
-          text.reserve(tt.meta_rest.size() + tt.top_rest.size() + 160);
-          text.append("{\"metadata\":{\"name\":").append(quoted(name));
-          text.append(",\"uid\":").append(quoted(uid_prefix_ + ub));
-          text.append(",\"resourceVersion\":\"").append(rvs).append("\"");
-          text.append(",\"creationTimestamp\":\"").append(ts).append("\"");
-          text.append(tt.meta_rest).append("}").append(tt.top_rest).append("}");
-          SP s = make_stored_text(std::move(text), last_rv_, tt.ns);
-          pods.objs[key] = s;
-          create_log_[key] = mono();
-          emit(pods, 'A', s, nullptr);
-        }
-      } else {
-        Value o = t;
-        o.at("metadata").at("name") = Value::str(name);
-        ApiErr err;
-        create(pods, std::move(o), "", &err);
-      }
-      if (++i % 64 == 0) {
-        // let the watchers see the burst while it is being created
-        std::vector<Conn*> d;
-        d.swap(dirty_);
-        for (Conn* x : d) flush(x);
-      }
-    }
+    // created in slices between the event loop's turns, like a real apiserver serving the
+    // burst's POSTs concurrently with everything else (the scheduler's Bindings included)
+    BenchJob job;
+    job.tag = tag;
+    job.n = templates_.size();
+    jobs_.push_back(std::move(job));
     respond(c, 200, "{\"n\":" + std::to_string(templates_.size()) + "}");
     return;
   }
@@ -1049,25 +1025,67 @@ void Server::handle_bench(Conn* c, Request& req) {
     return;
   }
   if (p == "/debug/bench/reset") {
-    std::vector<std::string> keys;
-    for (const auto& kv : pods.objs) keys.push_back(kv.first);
-    ApiErr err;
-    size_t i = 0;
-    for (const auto& k : keys) {
-      remove(pods, k, &err);
-      if (++i % 64 == 0) {
-        // as for the burst: the watchers see the deletions while they are being made
-        std::vector<Conn*> d;
-        d.swap(dirty_);
-        for (Conn* x : d) flush(x);
-      }
-    }
-    create_log_.clear();
-    bind_log_.clear();
-    respond(c, 200, "{\"deleted\":" + std::to_string(keys.size()) + "}");
+    BenchJob job;
+    job.del = true;
+    for (const auto& kv : pods.objs) job.keys.push_back(kv.first);
+    const size_t n = job.keys.size();
+    jobs_.push_back(std::move(job));
+    respond(c, 200, "{\"deleted\":" + std::to_string(n) + "}");
     return;
   }
   respond_err(c, {404, "NotFound", "no route for " + p});
+}
+
+// One slice (≤ 64 objects) of the oldest bench job: burst creation or reset deletion.
+void Server::step_jobs() {
+  if (jobs_.empty()) return;
+  BenchJob& job = jobs_.front();
+  ResState& pods = *by_key_["pods"];
+  ApiErr err;
+  if (job.del) {
+    const size_t end = std::min(job.keys.size(), job.next + 64);
+    for (; job.next < end; ++job.next) remove(pods, job.keys[job.next], &err);
+    if (job.next >= job.keys.size()) {
+      create_log_.clear();
+      bind_log_.clear();
+      jobs_.pop_front();
+    }
+    return;
+  }
+  if (job.next == 0) {
+    create_log_.clear();
+    bind_log_.clear();
+    job.ts = rfc3339_now();
+  }
+  const size_t end = std::min(job.n, std::min(templates_.size(), job.next + 64));
+  for (size_t i = job.next; i < end; ++i) {
+    const std::string name = job.tag + "-" + std::to_string(i);
+    if (!tmpl_text_.empty()) {
+      const TmplText& tt = tmpl_text_[i];
+      std::string key = tt.ns + "/" + name;
+      if (pods.objs.count(key)) continue;
+      char ub[24];
+      snprintf(ub, sizeof(ub), "-%012llx", static_cast<unsigned long long>(++uid_counter_));
+      const std::string rvs = next_rv();
+      std::string text;
+      text.reserve(tt.meta_rest.size() + tt.top_rest.size() + 160);
+      text.append("{\"metadata\":{\"name\":").append(quoted(name));
+      text.append(",\"uid\":").append(quoted(uid_prefix_ + ub));
+      text.append(",\"resourceVersion\":\"").append(rvs).append("\"");
+      text.append(",\"creationTimestamp\":\"").append(job.ts).append("\"");
+      text.append(tt.meta_rest).append("}").append(tt.top_rest).append("}");
+      SP s = make_stored_text(std::move(text), last_rv_, tt.ns);
+      pods.objs[key] = s;
+      create_log_[key] = mono();
+      emit(pods, 'A', s, nullptr);
+    } else {
+      Value o = templates_[i];
+      o.at("metadata").at("name") = Value::str(name);
+      create(pods, std::move(o), "", &err);
+    }
+  }
+  job.next = end;
+  if (job.next >= std::min(job.n, templates_.size())) jobs_.pop_front();
 }
 
 void Server::handle(Conn* c, Request& req) {
@@ -1231,7 +1249,7 @@ int Server::run() {
   std::vector<char> buf(1 << 16);
   double next_tick = mono() + 0.5, next_bm = opt_.bookmark_interval_s > 0 ? mono() + opt_.bookmark_interval_s : 1e300;
   while (!g_stop) {
-    int n = epoll_wait(ep_, evs, 256, 100);
+    int n = epoll_wait(ep_, evs, 256, jobs_.empty() ? 100 : 0);
     if (n < 0 && errno != EINTR) break;
     for (int k = 0; k < n; ++k) {
       if (evs[k].data.ptr == nullptr) {
@@ -1286,6 +1304,7 @@ int Server::run() {
         }
       }
     }
+    step_jobs();
     double now = mono();
     if (now >= next_tick) {
       next_tick = now + 0.5;
