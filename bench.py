@@ -85,10 +85,21 @@ def thread_cpu() -> dict:
         tids = os.listdir(base)
     except OSError:
         return out
+    me = str(os.getpid())
+    try:
+        with open(f"{base}/{me}/comm") as f:
+            proc_name = f.read().strip()
+    except OSError:
+        proc_name = ""
     for tid in tids:
         try:
             with open(f"{base}/{tid}/comm") as f:
                 name = f.read().strip()
+            # the interpreter's thread vs unnamed helpers (HIP/ROCr runtime, torch pools)
+            if tid == me:
+                name = "python"
+            elif name == proc_name:
+                name = "unnamed"
             with open(f"{base}/{tid}/stat") as f:
                 fields = f.read().rsplit(")", 1)[1].split()
             out[name] = out.get(name, 0.0) + (int(fields[11]) + int(fields[12])) / tick

@@ -1446,6 +1446,7 @@ struct Ctx {
   double kbatch_us = 0;
   long long n_query = 0;   // stream queries made by busy_check, and their time
   double query_us = 0;
+  double abandon_wait_us = 0;   // how long the host waited on the last call it abandoned
   int occ_waves = 0, occ_lds = -1, occ_blocks = 0;   // cached k_batch occupancy query
   yoda_dev_req_t *h_reqs = nullptr, *d_reqs_map = nullptr;
   yoda_dev_result_t* d_bres = nullptr;
@@ -1521,6 +1522,7 @@ int wait_result(Ctx* c) {
       if (q != hipErrorNotReady) return (int)q;
       if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
         c->abandoned = true;   // the GPU is held by other work: the engine uses the CPU meanwhile
+        c->abandon_wait_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         ++c->n_abandon;
         return -8;
       }
@@ -1713,6 +1715,7 @@ int wait_slot(Ctx* c, yoda_dev_result_t* slot, int pods) {
       if (q != hipErrorNotReady) return (int)q;
       if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
         c->abandoned = true;
+        c->abandon_wait_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         ++c->n_abandon;
         return -8;
       }
@@ -1841,6 +1844,7 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
         if (q != hipErrorNotReady) return (int)q;
         if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
           c->abandoned = true;
+          c->abandon_wait_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
           ++c->n_abandon;
           return -8;
         }
@@ -1956,7 +1960,7 @@ int yoda_dev_busy(void* p) {
 
 // out[0..7]: kernel dispatches, k_batch dispatches, pods placed by k_batch, calls abandoned at
 // the host deadline, calls refused while an abandoned one drained, k_batch GPU µs (timing on),
-// stream queries made while draining and their µs
+// stream queries made while draining and their µs, the host's wait on the last abandoned call
 int yoda_dev_counters(void* p, double* out) {
   const Ctx* c = (const Ctx*)p;
   if (!c || !out) return -1;
@@ -1968,6 +1972,7 @@ int yoda_dev_counters(void* p, double* out) {
   out[5] = c->kbatch_us;
   out[6] = (double)c->n_query;
   out[7] = c->query_us;
+  out[8] = c->abandon_wait_us;
   return 0;
 }
 

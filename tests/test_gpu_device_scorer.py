@@ -370,11 +370,14 @@ def test_batch_survives_a_tenant_kernel(require_gpu):
         assert a.device_fallbacks > f0 and a.device_cycles == c0
         cnt = ds.counters(a)
         assert cnt["abandoned"] == 1 and cnt["busy_refusals"] >= 1, cnt
-        assert stall < 0.050, stall
+        # the stall: the host's wait before it gave up (20 ms + 50 µs × 256 = 32.8 ms), and the
+        # whole call's overhead over a CPU-only engine's (two ~0.3 s CPU runs: a looser bound)
+        assert cnt["abandon_wait_us"] < 50_000, cnt
+        assert stall < 0.100, stall
         assert sum(1 for r in res if r[0] >= 0) > 128
         f1 = a.device_fallbacks
         _, stall2 = both(second)                          # still draining: refused without waiting
-        assert a.device_fallbacks > f1 and stall2 < 0.010, stall2
+        assert a.device_fallbacks > f1 and stall2 < 0.050, stall2
         assert ds.counters(a)["abandoned"] == 1
     finally:
         hip.occupy_wait(0)
