@@ -370,15 +370,16 @@ def test_batch_survives_a_tenant_kernel(require_gpu):
         assert a.device_fallbacks > f0 and a.device_cycles == c0
         cnt = ds.counters(a)
         assert cnt["abandoned"] == 1 and cnt["busy_refusals"] >= 1, cnt
-        # the stall: the host's wait before it gave up (20 ms + 50 µs × 256 = 32.8 ms), and the
-        # whole call's overhead over a CPU-only engine's (two ~0.3 s CPU runs: a looser bound)
+        # the stall: the host's wait before it gave up (20 ms + 50 µs × 256 = 32.8 ms). The
+        # whole call's time over the CPU-only engine's (`stall`, two ~0.3-0.5 s CPU runs) is
+        # printed, not asserted: it swings by ±0.1 s between boxes
         assert cnt["abandon_wait_us"] < 50_000, cnt
-        assert stall < 0.100, stall
         assert sum(1 for r in res if r[0] >= 0) > 128
-        f1 = a.device_fallbacks
-        _, stall2 = both(second)                          # still draining: refused without waiting
-        assert a.device_fallbacks > f1 and stall2 < 0.050, stall2
-        assert ds.counters(a)["abandoned"] == 1
+        f1, q1 = a.device_fallbacks, cnt["drain_query_us"]
+        both(second)                                      # still draining: refused without waiting
+        cnt2 = ds.counters(a)
+        assert a.device_fallbacks > f1 and cnt2["abandoned"] == 1
+        assert cnt2["drain_query_us"] - q1 < 10_000, cnt2  # no wait on the device, only probes
     finally:
         hip.occupy_wait(0)
     time.sleep(0.1)                                       # the abandoned k_batch runs out (bounded spins)
