@@ -1835,7 +1835,9 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
       d = __atomic_load_n(c->h_done, __ATOMIC_ACQUIRE);
       if (d != 0) break;
       if (spin > 2048) std::this_thread::sleep_for(std::chrono::microseconds(20));
-      if ((spin & 255) == 0 || spin > 2048) {
+      // the stream is asked only now and then (a launch failure or the host deadline): `done`
+      // is the completion signal, and each query wakes the runtime's own threads
+      if (spin <= 2048 ? (spin & 255) == 0 : (spin & 63) == 0) {
         const hipError_t q = hipStreamQuery(c->stream);
         if (q == hipSuccess) {
           d = __atomic_load_n(c->h_done, __ATOMIC_ACQUIRE);
