@@ -191,7 +191,8 @@ def main(argv=None) -> int:
     # before any thread exists: threads and the apiserver child inherit the mask
     # (yoda_scheduler_amd/utils/affinity.py: on one box 99-108 k vs 51-68 k pods/s unpinned)
     from yoda_scheduler_amd.utils.affinity import pin_l3
-    pinned = pin_l3(local_rank) if a.pin == "l3" else None
+    # one rank: the least busy domain; several: rank r takes the r-th (they must not collide)
+    pinned = pin_l3(local_rank, least_busy=world == 1) if a.pin == "l3" else None
 
     import torch
     import torch.distributed as dist

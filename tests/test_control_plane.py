@@ -721,7 +721,9 @@ def test_cpu_affinity_spec_and_l3_grouping(monkeypatch):
     monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(8)))
     monkeypatch.setattr(os, "sched_setaffinity", lambda pid, cpus: got.append(list(cpus)))
     assert affinity.l3_cpu_sets() == [[0, 1, 4, 5], [2, 3, 6, 7]]
-    assert affinity.apply("l3") == [0, 1, 4, 5] and affinity.apply("l3:3") == [2, 3, 6, 7]
-    assert got == [[0, 1, 4, 5], [2, 3, 6, 7]]
+    # `l3` takes the least busy domain (other tenants), `l3:<i>` the i-th
+    monkeypatch.setattr(affinity, "_busy_fractions", lambda cpus: {c: (0.9 if c in (0, 1, 4, 5) else 0.1) for c in cpus})
+    assert affinity.apply("l3") == [2, 3, 6, 7] and affinity.apply("l3:2") == [0, 1, 4, 5]
+    assert got == [[2, 3, 6, 7], [0, 1, 4, 5]]
     monkeypatch.setattr(os, "sched_getaffinity", lambda pid: {0, 1})
     assert affinity.apply("l3") is None

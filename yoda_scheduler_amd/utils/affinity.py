@@ -28,23 +28,57 @@ def l3_cpu_sets() -> list[list[int]]:
     return sorted(groups.values(), key=lambda g: g[0])
 
 
-def pin_l3(index: int = 0) -> Optional[list[int]]:
+def _busy_fractions(cpus: list[int], window_s: float = 0.05) -> dict[int, float]:
+    """Per-CPU busy fraction over a short window (/proc/stat); {} when unreadable."""
+    import time
+
+    def snap() -> dict[int, tuple[int, int]]:
+        out = {}
+        with open("/proc/stat") as f:
+            for ln in f:
+                if ln.startswith("cpu") and ln[3:4].isdigit():
+                    parts = ln.split()
+                    vals = [int(x) for x in parts[1:]]
+                    idle = vals[3] + (vals[4] if len(vals) > 4 else 0)
+                    out[int(parts[0][3:])] = (sum(vals), idle)
+        return out
+    try:
+        a = snap()
+        time.sleep(window_s)
+        b = snap()
+    except (OSError, ValueError, IndexError):
+        return {}
+    res = {}
+    for c in cpus:
+        if c in a and c in b:
+            tot = b[c][0] - a[c][0]
+            res[c] = 1.0 - (b[c][1] - a[c][1]) / tot if tot > 0 else 0.0
+    return res
+
+
+def pin_l3(index: int = 0, least_busy: bool = False) -> Optional[list[int]]:
     """Restrict this thread (and what it creates later) to the ``index``-th cache domain
-    (modulo their number). Returns the CPUs, or None when there is a single domain."""
+    (modulo their number), or — ``least_busy`` — to the domain whose CPUs were the most idle
+    over the last 50 ms (a shared host's other tenants). Returns the CPUs, or None when there
+    is a single domain."""
     sets = l3_cpu_sets()
     if len(sets) < 2:
         return None
     cpus = sets[index % len(sets)]
+    if least_busy:
+        busy = _busy_fractions([c for g in sets for c in g])
+        if busy:
+            cpus = min(sets, key=lambda g: sum(busy.get(c, 1.0) for c in g) / len(g))
     os.sched_setaffinity(0, cpus)
     return cpus
 
 
 def apply(spec: str) -> Optional[list[int]]:
-    """``none`` | ``l3`` | ``l3:<index>`` (the CLI's --cpu-affinity)."""
+    """``none`` | ``l3`` (the least busy domain) | ``l3:<index>`` (the CLI's --cpu-affinity)."""
     if not spec or spec == "none":
         return None
     if spec == "l3":
-        return pin_l3(0)
+        return pin_l3(0, least_busy=True)
     if spec.startswith("l3:"):
         return pin_l3(int(spec[3:]))
     raise ValueError(f"--cpu-affinity: expected none, l3 or l3:<index>, got {spec!r}")
