@@ -788,3 +788,59 @@ def test_failed_bind_handoff_requeues_the_run():
             api.stop()
     scheduled, errors, calls, pending = run(go())
     assert scheduled == 12 and errors >= 1 and calls >= 2 and pending == 0, (scheduled, errors, calls, pending)
+
+
+def test_native_apiserver_bench_burst_and_reset_run_in_slices(native_api):
+    """The bench endpoints answer at once and create / delete in 64-pod slices between event
+    loop turns, so other requests (a Binding here) are served while a burst is being created;
+    a watch sees every pod ADDED, the bound one MODIFIED and every pod DELETED after the reset,
+    and the status endpoint's latencies cover the bound pods."""
+    import aiohttp
+
+    from yoda_scheduler_amd.bench.workloads import pod_object
+
+    async def go():
+        cl = KubeClient(KubeConfig(native_api.url), native=True)
+        http = aiohttp.ClientSession()
+        try:
+            await cl.create("nodes", make_node("n1"))
+            _, rv = await cl.list("pods")
+            n = 640
+            async with http.post(native_api.url + "/debug/bench/load",
+                                 json={"pods": [pod_object(i, {"scv/memory": "1"}, "x") for i in range(n)]}) as r:
+                assert (await r.json())["n"] == n
+            seen = {"ADDED": 0, "MODIFIED": 0, "DELETED": 0}
+
+            async def watcher():
+                async for typ, _obj in cl.watch("pods", rv):
+                    seen[typ] += 1
+                    if seen["DELETED"] == n:
+                        return
+            t = asyncio.get_event_loop().create_task(watcher())
+            await asyncio.sleep(0.05)
+            async with http.post(native_api.url + "/debug/bench/burst", json={"tag": "s"}) as r:
+                assert (await r.json())["n"] == n
+            for _ in range(500):                          # the first slice is there soon
+                try:
+                    p = await cl.get("pods", "s-0", "default")
+                    break
+                except ApiError:
+                    await asyncio.sleep(0.002)
+            await cl.bind("default", "s-0", p["metadata"]["uid"], "n1")
+            for _ in range(500):
+                async with http.get(native_api.url + "/debug/bench/status?full=1") as r:
+                    st = await r.json()
+                if st["created"] == n:
+                    break
+                await asyncio.sleep(0.005)
+            assert st["created"] == n and st["bound"] == 1 and len(st["latencies"]) == 1
+            async with http.post(native_api.url + "/debug/bench/reset") as r:
+                assert (await r.json())["deleted"] == n
+            await asyncio.wait_for(t, 10)
+            assert seen == {"ADDED": n, "MODIFIED": 1, "DELETED": n}
+            items, _ = await cl.list("pods")
+            assert items == []
+        finally:
+            await http.close()
+            await cl.close()
+    run(go())
