@@ -305,6 +305,19 @@ def main(argv=None) -> int:
         api_s = api_cpu() - a0
         api_sys_s = api_sys[0] - as0
         th1 = thread_cpu()
+        if os.environ.get("YODA_BENCH_THREADS"):
+            # diagnostics: every thread's CPU over the whole process life, by tid
+            top = []
+            for tid in os.listdir("/proc/self/task"):
+                try:
+                    with open(f"/proc/self/task/{tid}/comm") as f:
+                        nm = f.read().strip()
+                    with open(f"/proc/self/task/{tid}/stat") as f:
+                        fl = f.read().rsplit(")", 1)[1].split()
+                    top.append((int(fl[11]) + int(fl[12]), tid, nm))
+                except (OSError, IndexError, ValueError):
+                    continue
+            sys.stderr.write("threads " + json.dumps(sorted(top, reverse=True)[:12]) + "\n")
         le1 = lane_engine()
         wd1 = watch_decode()
         my_bound = sum(r.bound for r in results)

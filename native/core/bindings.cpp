@@ -368,6 +368,16 @@ PYBIND11_MODULE(_yoda_core, m) {
                                          c.pending_mb));
              return out;
            }, py::call_guard<EngineGuard>())
+      // (has_scv, stale, card_number, [(healthy, free, effective free, clock)]) — the yoda
+      // filter's inputs for the Scv queueing hint; None for an unknown / removed node
+      .def("filter_view",
+           [](Engine& e, int32_t idx) -> py::object {
+             const FilterView v = e.filter_view(idx);
+             if (!v.known) return py::none();
+             py::list cards;
+             for (const auto& c : v.cards) cards.append(py::make_tuple(c.healthy, c.free, c.eff_free, c.clock));
+             return py::make_tuple(v.has_scv, v.stale, v.card_number, cards);
+           }, py::call_guard<EngineGuard>())
       .def("node_usage",
            [](Engine& e, int32_t idx) {
              const Node& n = e.node(idx);

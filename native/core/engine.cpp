@@ -473,6 +473,20 @@ Reason Engine::yoda_filter(const PodReq& req, int32_t idx, uint64_t* pn, uint64_
   return cnt >= num ? RS_OK : RS_GPU_FIT;
 }
 
+FilterView Engine::filter_view(int32_t idx) const {
+  // exactly what yoda_filter / yoda_card_eligible read of a node, so the Scv queueing hint
+  // (framework/scheduler.py::_capacity) cannot drift from the filter: keep the two together
+  FilterView v;
+  if (idx < 0 || idx >= (int32_t)nodes_.size() || !nodes_[idx].alive) return v;
+  const Node& n = nodes_[idx];
+  v.known = true;
+  v.has_scv = n.has_scv;
+  v.stale = n.stale;
+  v.card_number = n.card_number;
+  for (const Card& c : n.cards) v.cards.push_back({c.healthy, c.free_mb, eff_free(c), c.clock});
+  return v;
+}
+
 void Engine::collect_max(const PodReq& req, const std::vector<int32_t>& idxs, uint64_t mx[6]) const {
   // order: bandwidth, clock, core, free, power, total; all seeded 1 (collection.go:31-38)
   for (int i = 0; i < 6; ++i) mx[i] = 1;

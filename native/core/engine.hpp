@@ -124,6 +124,17 @@ struct Weights {
   int64_t enum_limit = 5000;    // exhaustive k-subset search up to this many subsets
 };
 
+// The node as the yoda filter sees it (Engine::filter_view)
+struct FilterView {
+  struct C {
+    bool healthy;
+    uint64_t free, eff_free, clock;
+  };
+  bool known = false, has_scv = false, stale = false;
+  uint64_t card_number = 0;
+  std::vector<C> cards;
+};
+
 struct Assignment {
   int32_t node = -1;
   std::vector<int32_t> cards;
@@ -251,6 +262,7 @@ class Engine {
   static void normalize_yoda(std::vector<int64_t>& s);
   // GPU set on node (empty + false if none)
   bool select_gpus(const PodReq& req, int32_t idx, std::vector<int32_t>* out, int32_t* quality) const;
+  FilterView filter_view(int32_t idx) const;
   bool select_gpus_small(const Node& n, const std::vector<int32_t>& E, uint64_t k, uint64_t m,
                          std::vector<int32_t>* out, int32_t* quality) const;
 

@@ -171,3 +171,28 @@ def test_gpu_fits_rules():
     assert not f(pod({"scv/clock": "2300"}), cap, False)
     assert not f(pod({}), (True,) + cap[1:], False)                # stale
     assert not f(pod({}), (False, 0, ()), False)                   # no cards
+
+
+def test_hint_reads_the_engines_filter_inputs():
+    """the hint's capacity view is the engine's own filter input
+    (`Engine::filter_view`, next to `yoda_filter`), not a Python-side copy: it follows the
+    engine's reservations (effective free HBM), CardNumber and staleness, and a node the
+    engine does not know has none."""
+    async def go():
+        c = FakeCluster(yoda_config())
+        c.add_node("n0", used_mb=[0] * 8)
+        sched = await c.start()
+        cap = sched._capacity("n0")
+        idx = sched.engine.node_index("n0")
+        has_scv, stale, cn, cards = sched.engine.filter_view(idx)
+        assert cap == (bool(stale or not has_scv), cn, tuple(tuple(x) for x in cards))
+        assert cap[0] is False and cap[1] == 8 and len(cap[2]) == 8
+        c.add_pod("p", {"scv/memory": "100000", "scv/number": "2"})
+        assert await c.wait_bound(1, 5.0)
+        after = sched._capacity("n0")
+        # the reservation lowered two cards' effective free HBM; sampled free is unchanged
+        lowered = [i for i in range(8) if after[2][i][2] < cap[2][i][2]]
+        assert len(lowered) == 2 and all(after[2][i][1] == cap[2][i][1] for i in range(8))
+        assert sched._capacity("nope") is None
+        await c.stop()
+    run(go())

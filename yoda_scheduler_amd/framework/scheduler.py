@@ -412,17 +412,16 @@ class Scheduler:
         self.queue.move_all_to_active_or_backoff("ScvAdd")
 
     def _capacity(self, name: str) -> Optional[tuple]:
-        """What the yoda filter can see of a node's GPUs, from the engine after pending
-        reservations are settled: (stale, CardNumber, per card (healthy, free, effective
-        free, clock)); None for a node the engine does not know."""
-        rows = self.cache.node_gpu_state(name)
-        if not rows and self.engine.node_index(name) < 0:
+        """What the yoda filter can see of a node's GPUs — read from the engine's own filter
+        inputs (``Engine::filter_view``, next to ``yoda_filter``), so the hint cannot drift
+        from the filter: (unfit: no Scv or stale, CardNumber, per card (healthy, free,
+        effective free, clock)); None for a node the engine does not know."""
+        idx = self.engine.node_index(name)
+        v = self.engine.filter_view(idx) if idx >= 0 else None
+        if v is None:
             return None
-        scv = self.cache.scvs.get(name)
-        cn = 0 if scv is None else (scv.card_number if isinstance(scv, LazyScv) else scv.status.card_number)
-        cards = tuple((g["healthy"], g["free"], max(0, min(g["free"] - g["pending"], g["total"] - g["reserved"])),
-                       g["clock"]) for g in rows)
-        return bool(self.cache._stale.get(name)), cn, cards
+        has_scv, stale, cn, cards = v
+        return bool(stale or not has_scv), cn, tuple(tuple(c) for c in cards)
 
     @staticmethod
     def _capacity_grew(b: tuple, a: tuple) -> bool:
