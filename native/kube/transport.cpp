@@ -929,6 +929,8 @@ void Transport::run() {
     }
     if (woke) {
       efd_clear(wake_efd_);
+      // the rate read before epoll_wait may predate a set_rate() that came with this wake-up
+      const double qps = qps_.load();
       std::vector<std::unique_ptr<Req>> in;
       std::vector<uint64_t> cancels;
       {

@@ -320,11 +320,15 @@ def test_async_runs_survive_deletes_and_rebinds_while_on_the_engine(monkeypatch)
             for i in range(0, 96, 2):
                 await e.cl.delete("pods", f"a{i}", "default")
             lane = e.sched.lane.lane
-            assert await e.wait(lambda: lane.stats()["confirmed"] >= 48 and lane.stats()["queued"] == 0
-                                and lane.stats()["inflight"] == 0, 20.0), lane.stats()
-            pods = await e.pods()
+            # (`confirmed` also counts deleted pods that were bound first: wait on the apiserver)
+            for _ in range(400):
+                pods = await e.pods()
+                if len(pods) == 48 and all(p["spec"].get("nodeName") for p in pods.values()):
+                    break
+                await asyncio.sleep(0.05)
             assert sorted(pods) == sorted(f"a{i}" for i in range(1, 96, 2))
-            assert all(p["spec"].get("nodeName") for p in pods.values())
+            assert all(p["spec"].get("nodeName") for p in pods.values()), lane.stats()
+            assert await e.wait(lambda: lane.stats()["queued"] == 0 and lane.stats()["inflight"] == 0, 10.0)
             assert await e.wait(lambda: e.sched.engine.ledger_size == 48), e.sched.engine.ledger_size
             assert lane.stats()["left_in_flight"] > 0      # the in-flight path was taken
             want = sum(2048 * (1 + i % 2) for i in range(1, 96, 2))

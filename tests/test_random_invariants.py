@@ -39,6 +39,14 @@ def _scenario(seed: int):
             s.update_interval_ms = 600_000
             c.server.create("scvs", s.to_json())
             nodes[name] = s
+        deleted = []                    # every pod deleted by the test or by preemption
+        real_delete = c.server.delete
+
+        def delete(res, name, namespace=None):
+            if res == "pods":
+                deleted.append(name)
+            return real_delete(res, name, namespace)
+        c.server.delete = delete
         await c.start()
         pods = {}
         for i in range(rng.randint(60, 120)):
@@ -80,21 +88,28 @@ def _scenario(seed: int):
             if stable >= 10:
                 break
         live = {}
+        labels = {name: lab for name, (lab, _) in pods.items()}
         for name in list(pods):
             try:
                 live[name] = c.pod(name)
             except Exception:
                 pods.pop(name)
         state = {n: c.sched.cache.node_gpu_state(n) for n in nodes}
+        q = c.sched.queue
+        diag = {"queue": {pi.name: ("active" if uid in q._active_entries else "backoff" if uid in q._backoff_pods
+                                    else "unschedulable", pi.attempts) for uid, pi in q._pods.items()},
+                "nominations": {uid: v[0] for uid, v in c.sched.nominations.items()},
+                "move_request_cycle": q._move_request_cycle, "cycle": q.scheduling_cycle,
+                "deleted_web": sum(1 for n in deleted if labels.get(n, {}).get("app") == "web")}
         await c.stop()
-        return nodes, pods, live, state
+        return nodes, pods, live, state, diag
 
     return run(go())
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_random_cluster_invariants(seed):
-    nodes, pods, live, state = _scenario(seed)
+    nodes, pods, live, state, diag = _scenario(seed)
     want: dict = {}
     bound = {}
     for name, obj in live.items():
@@ -117,12 +132,14 @@ def test_random_cluster_invariants(seed):
     db_nodes = [bound[n] for n in bound if pods[n][0].get("app") == "db"]
     assert len(db_nodes) == len(set(db_nodes)), db_nodes
     # spread: web pods' zone counts differ by at most maxSkew (2) — checked against the zones
-    # that could host them, i.e. both zones exist on every seed
+    # that could host them, i.e. both zones exist on every seed. Each bind kept the skew of the
+    # scheduler's view ≤ 2; a member deleted afterwards (by the test or as a preemption victim)
+    # may widen it by one, so the bound is 2 + the number of deleted web pods.
     web = [bound[n] for n in bound if pods[n][0].get("app") == "web"]
     zones = {z: 0 for z in ("z0", "z1")}
     for n in web:
         zones["z" + str(int(n[1:]) % 2)] += 1
-    assert max(zones.values()) - min(zones.values()) <= 2 + 1, zones   # +1: a member may be gone
+    assert max(zones.values()) - min(zones.values()) <= 2 + diag["deleted_web"], (zones, diag["deleted_web"])
     # pending plain pods really do not fit anywhere (per-GPU effective free HBM)
     for name, obj in live.items():
         lab, extra = pods[name]
@@ -131,4 +148,4 @@ def test_random_cluster_invariants(seed):
         k, mem = int(lab.get("scv/number", "1")), int(lab["scv/memory"])
         for node, gs in state.items():
             free = [g for g in gs if g["healthy"] and min(g["free"] - g["pending"], g["total"] - g["reserved"]) >= mem]
-            assert len(free) < k, (name, node, k, mem)
+            assert len(free) < k, (name, node, k, mem, free, diag)

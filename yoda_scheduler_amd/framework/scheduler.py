@@ -797,6 +797,9 @@ class Scheduler:
         nom = self.nominations.pop(uid, None)
         if nom is not None:
             self.engine.release(nom[1])
+            # pods parked while the hold stood may fit now: the preemptor need not retake the
+            # same cards (or any, on that node), and no other cluster event reports the release
+            self.queue.move_all_to_active_or_backoff("NominatedPodRelease")
 
     def _clear_nominations_for(self, pods) -> None:
         if self.nominations:
