@@ -263,16 +263,20 @@ def main(argv=None) -> int:
             except Exception:  # noqa: BLE001 - psutil missing / process gone
                 return float("nan")
 
-        def lane_engine() -> tuple[float, int]:
+        lane_keys = ("engine_s", "engine_cpu_s", "lock_wait_s", "engine_pods", "handoff_s", "return_s",
+                     "idle_queued_s", "async_runs")
+
+        def lane_engine() -> tuple:
             """Seconds the native lanes spent inside Engine::schedule_batch (wall, CPU) and waiting
-            for the engine lock, and the pods of those calls."""
-            s, c, lw, n = 0.0, 0.0, 0.0, 0
+            for the engine lock, the pods of those calls, and the async runs' pipeline times
+            (hand-off to the engine worker, hand-back, worker idle while pods waited)."""
+            tot = [0.0] * len(lane_keys)
             for sh in {id(x): x for x in shards}.values():
                 ln = getattr(sh.sched, "lane", None)
                 if ln is not None:
                     st = ln.lane.stats()
-                    s, c, lw, n = s + st["engine_s"], c + st["engine_cpu_s"], lw + st["lock_wait_s"], n + st["engine_pods"]
-            return s, c, lw, n
+                    tot = [t + st.get(k, 0) for t, k in zip(tot, lane_keys)]
+            return tuple(tot)
 
         def watch_decode() -> float:
             """I/O-thread CPU seconds spent decoding watch lines (native transport)."""
@@ -377,6 +381,15 @@ def main(argv=None) -> int:
                                         "cpu": round((le1[1] - le0[1]) / (le1[3] - le0[3]) * 1e6, 2),
                                         "lock_wait": round((le1[2] - le0[2]) / (le1[3] - le0[3]) * 1e6, 2)}
                                        if le1[3] > le0[3] else None),
+            # async device runs (rank 0): count, pods per run, µs per run from pick to the engine
+            # worker and from the worker back to the lane, and the worker's idle µs per pod
+            # while pods that arrived before its last run ended waited
+            "lane_async": ({"runs": int(le1[7] - le0[7]),
+                            "pods_per_run": round((le1[3] - le0[3]) / (le1[7] - le0[7]), 1),
+                            "handoff_us_per_run": round((le1[4] - le0[4]) / (le1[7] - le0[7]) * 1e6, 1),
+                            "return_us_per_run": round((le1[5] - le0[5]) / (le1[7] - le0[7]) * 1e6, 1),
+                            "idle_queued_us_per_pod": round((le1[6] - le0[6]) / my_bound * 1e6, 2) if my_bound else None}
+                           if le1[7] > le0[7] else None),
             # the fake apiserver's own CPU (separate process, http transport; rank 0's)
             **({"apiserver_cpu_us_per_pod": round(api_s / (bound / max(world, 1)) * 1e6, 2)
                 if bound and api_s == api_s else None,

@@ -498,10 +498,11 @@ PYBIND11_MODULE(_yoda_core, m) {
   py::class_<Lane>(m, "Lane")
       .def(py::init([](Engine& e, int batch, double bind_timeout, int sort_kind, bool events, bool events_v1,
                        double event_qps, int event_burst, int event_buffer, const std::string& host,
-                       const std::string& name_prefix, int async_mode, int engine_delay_us) {
+                       const std::string& name_prefix, int async_mode, int engine_delay_us, int spin_us) {
              LaneOptions o;
              o.async_mode = async_mode;
              o.engine_delay_us = engine_delay_us;
+             o.spin_us = spin_us;
              o.batch = batch;
              o.bind_timeout_s = bind_timeout;
              o.sort_kind = sort_kind;
@@ -518,7 +519,7 @@ PYBIND11_MODULE(_yoda_core, m) {
            py::arg("events") = true, py::arg("events_v1") = true, py::arg("event_qps") = 50.0,
            py::arg("event_burst") = 300, py::arg("event_buffer") = 1000, py::arg("host") = "localhost",
            py::arg("name_prefix") = "00000000", py::arg("async_mode") = 1,
-           py::arg("engine_delay_us") = 0, py::keep_alive<1, 2>())
+           py::arg("engine_delay_us") = 0, py::arg("spin_us") = 0, py::keep_alive<1, 2>())
       .def("sink_ptr", [](Lane& l) { return (uintptr_t) static_cast<yk::PodSink*>(&l); })
       .def("set_port", [](Lane& l, uintptr_t p) { l.set_port(reinterpret_cast<yk::PodPort*>(p)); })
       // the profile's engine configuration is the engine's current one (the caller applied it)
@@ -615,6 +616,10 @@ PYBIND11_MODULE(_yoda_core, m) {
              d["engine_pods"] = s.engine_pods;
              d["engine_cpu_s"] = s.engine_cpu_s;
              d["lock_wait_s"] = s.lock_wait_s;
+             d["handoff_s"] = s.handoff_s;
+             d["return_s"] = s.return_s;
+             d["idle_queued_s"] = s.idle_queued_s;
+             d["async_runs"] = s.async_runs;
              return d;
            })
       .def("pause", &Lane::pause, py::call_guard<py::gil_scoped_release>())

@@ -175,6 +175,22 @@ void Lane::close() {
   }
 }
 
+void Lane::push_locked(Item&& it) {
+  inbox_.push_back(std::move(it));
+  inbox_flag_.store(true, std::memory_order_relaxed);
+}
+
+// Busy-wait up to LaneOptions::spin_us for `flag` (or stop); the caller then takes the lock
+// and re-checks its own predicate, so a missed flag only costs the futex wait it replaces.
+void Lane::spin_until(const std::atomic<bool>& flag) const {
+  if (o_.spin_us <= 0) return;
+  const double end = mono() + o_.spin_us * 1e-6;
+  for (int i = 0; !flag.load(std::memory_order_relaxed) && !stop_.load(std::memory_order_relaxed); ++i) {
+    __builtin_ia32_pause();
+    if ((i & 63) == 63 && mono() > end) return;
+  }
+}
+
 // ------------------------------------------------------------------ configuration
 void Lane::set_profile(const Profile& p) {
   {
@@ -186,7 +202,7 @@ void Lane::set_profile(const Profile& p) {
   std::lock_guard<std::mutex> g(in_mu_);
   Item it;
   it.k = Item::kProfiles;
-  inbox_.push_back(std::move(it));
+  push_locked(std::move(it));
   in_cv_.notify_one();
 }
 
@@ -217,7 +233,7 @@ void Lane::on_pod_events(uint64_t, std::vector<yk::WatchEvent>& evs) {
         it.k = Item::kEvent;
         it.type = e.type;
         it.ev = std::move(e.pod);
-        inbox_.push_back(std::move(it));
+        push_locked(std::move(it));
       } else {
         if (&evs[kept] != &e) evs[kept] = std::move(e);
         ++kept;
@@ -237,7 +253,7 @@ void Lane::on_answers(std::vector<yk::PodSink::Answer>& answers) {
     it.status = a.status;
     it.body = std::move(a.body);
     it.t = a.t;
-    inbox_.push_back(std::move(it));
+    push_locked(std::move(it));
   }
   in_cv_.notify_one();
 }
@@ -263,7 +279,7 @@ std::vector<Lane::Fwd> Lane::relist(std::vector<std::shared_ptr<yk::PodEv>> item
   it.k = Item::kRelist;
   it.items = std::make_shared<std::vector<std::shared_ptr<yk::PodEv>>>(std::move(items));
   it.token = token;
-  inbox_.push_back(std::move(it));
+  push_locked(std::move(it));
   in_cv_.notify_one();
   relist_cv_.wait(lk, [&] { return relist_done_ >= token || stop_.load(); });
   std::vector<Fwd> out;
@@ -910,6 +926,12 @@ void Lane::schedule_some() {
   if (async) {
     // the GPU places the batch while this thread keeps serving answers, echoes and deletions;
     // the runs come back through the inbox (kRunDone) and the next batch starts after them
+    double oldest = t0;
+    for (const Entry* e : picked) oldest = std::min(oldest, e->t_enq);
+    if (last_wend_ > 0 && oldest < last_wend_) {
+      std::lock_guard<std::mutex> g(stat_mu_);
+      st_.idle_queued_s += t0 - last_wend_;
+    }
     {
       std::lock_guard<std::mutex> g(in_mu_);
       run_inflight_ = true;
@@ -917,6 +939,7 @@ void Lane::schedule_some() {
     {
       std::lock_guard<std::mutex> g(wk_mu_);
       wk_jobs_ = std::move(runs);
+      wk_flag_.store(true, std::memory_order_relaxed);
     }
     wk_cv_.notify_one();
     return;
@@ -943,19 +966,31 @@ void Lane::complete_runs(std::vector<std::shared_ptr<Run>>& runs) {
 void Lane::engine_worker() {
   for (;;) {
     std::vector<std::shared_ptr<Run>> jobs;
+    spin_until(wk_flag_);
     {
       std::unique_lock<std::mutex> lk(wk_mu_);
       wk_cv_.wait(lk, [&] { return stop_.load() || !wk_jobs_.empty(); });
       if (wk_jobs_.empty()) return;   // stopping and nothing left
       jobs.swap(wk_jobs_);
+      wk_flag_.store(false, std::memory_order_relaxed);
     }
-    for (auto& r : jobs) engine_step(*r);
+    const double ts = mono();
+    {
+      std::lock_guard<std::mutex> g(stat_mu_);
+      st_.handoff_s += ts - jobs.front()->t0;
+      st_.async_runs++;
+    }
+    for (auto& r : jobs) {
+      r->t_wstart = ts;
+      engine_step(*r);
+      r->t_wend = mono();
+    }
     Item it;
     it.k = Item::kRunDone;
     it.runs = std::make_shared<std::vector<std::shared_ptr<Run>>>(std::move(jobs));
     {
       std::lock_guard<std::mutex> g(in_mu_);
-      inbox_.push_back(std::move(it));
+      push_locked(std::move(it));
     }
     in_cv_.notify_one();
   }
@@ -1123,6 +1158,13 @@ void Lane::run() {
         return stop_.load() || (!inbox_.empty() && (!paused_ || run_inflight_)) ||
                (!paused_ && !run_inflight_ && active_.load() && !heap_.empty());
       };
+      if (!ready() && run_inflight_ && o_.spin_us > 0) {
+        // a device run is out: its return (or an answer, an echo) is likely within the spin,
+        // and a futex wake-up would add tens of µs to the engine worker's idle gap
+        lk.unlock();
+        spin_until(inbox_flag_);
+        lk.lock();
+      }
       if (!ready()) {
         if (!ev_q_.empty() && o_.event_qps > 0) {
           const double wait = std::max(0.0005, (1.0 - ev_tokens_) / o_.event_qps);
@@ -1137,6 +1179,7 @@ void Lane::run() {
       }
       if (stop_.load()) break;
       work.swap(inbox_);
+      inbox_flag_.store(false, std::memory_order_relaxed);
       busy_ = true;
     }
     std::vector<Fwd> fwd;
@@ -1164,6 +1207,11 @@ void Lane::run() {
     work.clear();
     if (!done.empty()) {
       // after this turn's events: a pod deleted meanwhile is already out of by_id_
+      last_wend_ = done.back()->t_wend;
+      {
+        std::lock_guard<std::mutex> g(stat_mu_);
+        st_.return_s += mono() - last_wend_;
+      }
       complete_runs(done);
       std::lock_guard<std::mutex> g(in_mu_);
       run_inflight_ = false;

@@ -54,6 +54,9 @@ struct LaneOptions {
   // 2 always (tests of the in-flight paths)
   int async_mode = 1;
   int engine_delay_us = 0;         // tests: widen the in-flight window of every run
+  // async runs: the lane thread (run out) and the engine worker (between runs) busy-wait this
+  // long for their next item before sleeping on the condition variable (0: never spin)
+  int spin_us = 0;
 };
 
 struct LaneStats {
@@ -66,6 +69,10 @@ struct LaneStats {
   double engine_cpu_s = 0;    // ... of which on the CPU (the rest: the engine lock, the device)
   double lock_wait_s = 0;     // waiting for the engine lock before a run
   uint64_t engine_pods = 0;   // pods those calls placed or rejected
+  // async runs: picked → worker start, worker end → lane completes them, and the engine
+  // worker's idle time between runs while pods that arrived before the last run ended waited
+  double handoff_s = 0, return_s = 0, idle_queued_s = 0;
+  uint64_t async_runs = 0;
 };
 
 class Lane : public yk::PodSink {
@@ -174,6 +181,7 @@ class Lane : public yk::PodSink {
     Profile pr;                                      // a copy: profiles may change meanwhile
     EngineConfig cfg;
     double t0 = 0;
+    double t_wstart = 0, t_wend = 0;                 // on the engine worker (async)
     std::vector<uint64_t> ids;                       // entry ids, run order
     std::vector<std::shared_ptr<yk::PodEv>> evs;
     std::vector<PodReq> reqs;
@@ -245,6 +253,11 @@ class Lane : public yk::PodSink {
   bool busy_ = false;                // lane thread is processing (wait_idle)
   bool paused_ = false;
   bool run_inflight_ = false;        // runs on the engine worker (in_mu_)
+  std::atomic<bool> inbox_flag_{false};   // inbox_ non-empty (set under in_mu_, read spinning)
+  std::atomic<bool> wk_flag_{false};      // wk_jobs_ non-empty (set under wk_mu_)
+  void push_locked(Item&& it);            // inbox_.push_back under in_mu_
+  void spin_until(const std::atomic<bool>& flag) const;
+  double last_wend_ = 0;             // when the engine worker finished the last async run (lane thread)
 
   // engine worker (async device runs)
   std::thread wk_th_;

@@ -304,12 +304,15 @@ def test_finish_cycle_refuses_a_result_whose_node_slot_was_reused():
     assert pending == 0 and not cached and queued and not reserved
 
 
-def test_async_runs_survive_deletes_and_rebinds_while_on_the_engine(monkeypatch):
+@pytest.mark.parametrize("spin_us", [0, 200])
+def test_async_runs_survive_deletes_and_rebinds_while_on_the_engine(monkeypatch, spin_us):
     """Runs on the engine worker (the device-scorer path, forced here with a widened window):
     the lane keeps applying events meanwhile. Pods deleted while their run is on the engine
-    never bind and leave no reservation; the others bind and confirm; the ledger is exact."""
+    never bind and leave no reservation; the others bind and confirm; the ledger is exact.
+    With ``spin_us`` the lane thread and the worker busy-wait for each other's hand-offs."""
     monkeypatch.setenv("YODA_LANE_ASYNC", "2")
     monkeypatch.setenv("YODA_LANE_ENGINE_DELAY_US", "30000")
+    monkeypatch.setenv("YODA_LANE_SPIN_US", str(spin_us))
 
     async def go():
         cfg = yoda_config(batch=16)
@@ -330,7 +333,9 @@ def test_async_runs_survive_deletes_and_rebinds_while_on_the_engine(monkeypatch)
             assert all(p["spec"].get("nodeName") for p in pods.values()), lane.stats()
             assert await e.wait(lambda: lane.stats()["queued"] == 0 and lane.stats()["inflight"] == 0, 10.0)
             assert await e.wait(lambda: e.sched.engine.ledger_size == 48), e.sched.engine.ledger_size
-            assert lane.stats()["left_in_flight"] > 0      # the in-flight path was taken
+            st = lane.stats()
+            assert st["left_in_flight"] > 0                # the in-flight path was taken
+            assert st["async_runs"] >= 3 and st["handoff_s"] > 0 and st["return_s"] > 0, st
             want = sum(2048 * (1 + i % 2) for i in range(1, 96, 2))
             got = sum(g["reserved"] for n in ("n1", "n2") for g in e.sched.cache.node_gpu_state(n))
             assert got == want

@@ -50,7 +50,9 @@ class NativeLane:
                                 # runs on an engine worker while the lane serves its inbox: with a
                                 # device scorer (1, default), never (0), always (2: tests)
                                 async_mode=int(os.environ.get("YODA_LANE_ASYNC", "1")),
-                                engine_delay_us=int(os.environ.get("YODA_LANE_ENGINE_DELAY_US", "0")))
+                                engine_delay_us=int(os.environ.get("YODA_LANE_ENGINE_DELAY_US", "0")),
+                                # busy-wait (µs) of the lane thread / engine worker around device runs
+                                spin_us=int(os.environ.get("YODA_LANE_SPIN_US", "0")))
         self.lane.set_port(transport.t.port_ptr())
         self._profiles: dict[str, tuple] = {}
         self._loop: Optional[asyncio.AbstractEventLoop] = None
