@@ -298,11 +298,16 @@ def main(argv=None) -> int:
         th0 = thread_cpu()
         t0 = time.perf_counter()
         c0 = time.process_time()
-        results, step_s = [], []
+        results, step_s, reset_s = [], [], []
         for i in range(a.steps):
             ts = time.perf_counter()
             results.append(loop.run_until_complete(shards[a.warmup + i].burst(f"s{i}")))
             step_s.append(time.perf_counter() - ts)
+            reset_s.append(getattr(shards[a.warmup + i], "last_reset_s", 0.0))
+            if os.environ.get("YODA_BENCH_RUNLOG"):
+                sh = shards[a.warmup + i]
+                sys.stderr.write("runlog " + json.dumps({"step": i, "seen_ms": getattr(sh, "last_seen_ms", None),
+                                                         "runs": getattr(sh, "last_runs", [])}) + "\n")
         sync()
         elapsed = time.perf_counter() - t0
         cpu_s = time.process_time() - c0     # this rank's process: scheduler (+ in-process apiserver)
@@ -365,6 +370,9 @@ def main(argv=None) -> int:
             "ms_per_step": round(elapsed / a.steps * 1000.0, 3),
             # each timed step (one burst) on its own, max over ranks: drift and outliers show
             "step_ms": [round(x * 1000.0, 3) for x in step_s],
+            # of which (http transport, rank 0) deleting the previous burst's pods and waiting until
+            # the scheduler saw the deletions (timed: it is scheduler work, releases included)
+            "reset_ms": [round(x * 1000.0, 3) for x in reset_s],
             "p50_latency_ms": round(percentile(lats, 50) * 1000.0, 3),
             "p99_latency_ms": round(percentile(lats, 99) * 1000.0, 3),
             "max_latency_ms": round(max(lats) * 1000.0, 3) if lats else None,

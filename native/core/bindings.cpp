@@ -622,6 +622,14 @@ PYBIND11_MODULE(_yoda_core, m) {
              d["async_runs"] = s.async_runs;
              return d;
            })
+      // [(t_pick, t_worker_start, t_worker_end, t_done, pods)] of the runs since the last call
+      // (monotonic seconds; worker times 0 for runs the lane thread ran itself)
+      .def("run_log",
+           [](Lane& l) {
+             py::list out;
+             for (const auto& r : l.run_log()) out.append(py::make_tuple(r.t_pick, r.t_wstart, r.t_wend, r.t_done, r.pods));
+             return out;
+           })
       .def("pause", &Lane::pause, py::call_guard<py::gil_scoped_release>())
       // (full, [(id, add, PodEvent | None, node, cards)])
       .def("changes",

@@ -98,7 +98,7 @@ std::string micro_time(double ts) {
   gmtime_r(&sec, &tm);
   char buf[48];
   strftime(buf, sizeof buf, "%Y-%m-%dT%H:%M:%S", &tm);
-  char out[64];
+  char out[80];   // 47 + "." + up to 20 digits + "Z"
   snprintf(out, sizeof out, "%s.%06ldZ", buf, us);
   return out;
 }
@@ -944,14 +944,31 @@ void Lane::schedule_some() {
     wk_cv_.notify_one();
     return;
   }
-  for (auto& r : runs) engine_step(*r);
+  for (auto& r : runs) {
+    r->t_wstart = mono();
+    engine_step(*r);
+    r->t_wend = mono();
+  }
   complete_runs(runs);
+}
+
+std::vector<Lane::RunRec> Lane::run_log() {
+  std::lock_guard<std::mutex> g(rlog_mu_);
+  std::vector<RunRec> out;
+  out.swap(rlog_);
+  return out;
 }
 
 void Lane::complete_runs(std::vector<std::shared_ptr<Run>>& runs) {
   std::vector<yk::BindSpec> binds;
   std::vector<uint64_t> tags;
   std::vector<Fwd> fwd;
+  {
+    const double now = mono();
+    std::lock_guard<std::mutex> g(rlog_mu_);
+    for (auto& r : runs)
+      if (rlog_.size() < 4096) rlog_.push_back(RunRec{r->t0, r->t_wstart, r->t_wend, now, (uint32_t)r->ids.size()});
+  }
   for (auto& r : runs) finish_run(*r, &binds, &tags, &fwd);
   yk::PodPort* port = port_.load();
   if (!binds.empty() && port) port->bind_native(std::move(binds), tags, o_.bind_timeout_s, this);
@@ -1205,22 +1222,30 @@ void Lane::run() {
       }
     }
     work.clear();
+    auto release_pending = [&] {
+      if (to_release_.empty()) return;
+      std::lock_guard<std::recursive_mutex> lk(*emu_);
+      for (uint64_t id : to_release_) eng_->release(id);
+      to_release_.clear();
+    };
     if (!done.empty()) {
+      release_pending();                  // deletions of this turn free capacity for the next run
       // after this turn's events: a pod deleted meanwhile is already out of by_id_
       last_wend_ = done.back()->t_wend;
       {
         std::lock_guard<std::mutex> g(stat_mu_);
         st_.return_s += mono() - last_wend_;
       }
+      {
+        std::lock_guard<std::mutex> g(in_mu_);
+        run_inflight_ = false;
+      }
+      // the next batch goes to the engine worker first: its reservations already hold in the
+      // engine, so building and posting this batch's Bindings overlaps the next device run
+      schedule_some();
       complete_runs(done);
-      std::lock_guard<std::mutex> g(in_mu_);
-      run_inflight_ = false;
     }
-    if (!to_release_.empty()) {
-      std::lock_guard<std::recursive_mutex> lk(*emu_);
-      for (uint64_t id : to_release_) eng_->release(id);
-      to_release_.clear();
-    }
+    release_pending();
     if (!fwd.empty() || !hand_pending_.empty()) publish(std::move(fwd), std::move(hand_pending_));
     hand_pending_.clear();
     if (out_moves_pending_) {
@@ -1250,11 +1275,7 @@ void Lane::run() {
       publish({}, std::move(hand_pending_));
       hand_pending_.clear();
     }
-    if (!to_release_.empty()) {
-      std::lock_guard<std::recursive_mutex> lk(*emu_);
-      for (uint64_t id : to_release_) eng_->release(id);
-      to_release_.clear();
-    }
+    release_pending();
     flush_events();
     {
       std::lock_guard<std::mutex> g(in_mu_);

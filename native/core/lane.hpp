@@ -253,6 +253,16 @@ class Lane : public yk::PodSink {
   bool busy_ = false;                // lane thread is processing (wait_idle)
   bool paused_ = false;
   bool run_inflight_ = false;        // runs on the engine worker (in_mu_)
+  // the last runs' timeline (diagnostics): pick, worker start, worker end, lane completion, pods
+ public:
+  struct RunRec {
+    double t_pick, t_wstart, t_wend, t_done;
+    uint32_t pods;
+  };
+  std::vector<RunRec> run_log();          // and clear it
+ private:
+  std::mutex rlog_mu_;
+  std::vector<RunRec> rlog_;
   std::atomic<bool> inbox_flag_{false};   // inbox_ non-empty (set under in_mu_, read spinning)
   std::atomic<bool> wk_flag_{false};      // wk_jobs_ non-empty (set under wk_mu_)
   void push_locked(Item&& it);            // inbox_.push_back under in_mu_

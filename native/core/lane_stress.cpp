@@ -76,10 +76,9 @@ double cpu_of(pthread_t) { return 0; }
 
 }  // namespace
 
-int main(int argc, char** argv) {
-  const int bursts = argc > 1 ? atoi(argv[1]) : 20;
-  const int per = argc > 2 ? atoi(argv[2]) : 1000;
-  const int batch = argc > 3 ? atoi(argv[3]) : 256;
+// One lane over `bursts` bursts of `per` pods; async_mode / spin_us as in LaneOptions (2 = every
+// run on the engine worker, the device-scorer path's threading without a device).
+int run_mode(int bursts, int per, int batch, int async_mode, int spin_us) {
   std::recursive_mutex emu;
   Engine e(false, 1);
   {
@@ -100,6 +99,8 @@ int main(int argc, char** argv) {
   EngineConfig cfg = e.config();
   LaneOptions o;
   o.batch = batch;
+  o.async_mode = async_mode;
+  o.spin_us = spin_us;
   Lane lane(&e, &emu, o);
   FakePort port;
   lane.set_port(&port);
@@ -210,9 +211,22 @@ int main(int argc, char** argv) {
   port.cv.notify_all();
   io.join();
   lane.close();
-  printf("{\"bursts\": %d, \"pods\": %d, \"scheduled\": %llu, \"confirmed\": %llu, \"released\": %llu, "
-         "\"batches\": %llu, \"us_per_pod_wall\": %.2f, \"fails\": %d}\n",
-         bursts, per, (unsigned long long)st.scheduled, (unsigned long long)st.confirmed,
-         (unsigned long long)st.released, (unsigned long long)st.batches, wall / (bursts * per) * 1e6, fails);
+  printf("{\"async_mode\": %d, \"spin_us\": %d, \"bursts\": %d, \"pods\": %d, \"scheduled\": %llu, "
+         "\"confirmed\": %llu, \"released\": %llu, \"batches\": %llu, \"async_runs\": %llu, "
+         "\"us_per_pod_wall\": %.2f, \"fails\": %d}\n",
+         async_mode, spin_us, bursts, per, (unsigned long long)st.scheduled, (unsigned long long)st.confirmed,
+         (unsigned long long)st.released, (unsigned long long)st.batches, (unsigned long long)st.async_runs,
+         wall / (bursts * per) * 1e6, fails);
+  if (async_mode == 2 && st.async_runs == 0) fails++;
+  return fails;
+}
+
+int main(int argc, char** argv) {
+  const int bursts = argc > 1 ? atoi(argv[1]) : 20;
+  const int per = argc > 2 ? atoi(argv[2]) : 1000;
+  const int batch = argc > 3 ? atoi(argv[3]) : 256;
+  // the lane thread placing inline, then runs on the engine worker with both threads spinning
+  int fails = run_mode(bursts, per, batch, 1, 0);
+  fails += run_mode(bursts, per, batch, 2, 50);
   return fails ? 1 : 0;
 }

@@ -259,6 +259,9 @@ class HttpShard:
         cc = self.cfg.client_connection
         self.client.set_rate(cc.qps, cc.burst)
         done0, fail0 = sched.scheduled, sched.failed
+        if sched.lane is not None:
+            sched.lane.lane.run_log()           # drop the reset's runs
+        t_burst = time.monotonic()
         n = (await self._call("POST", "/debug/bench/burst", {"tag": tag}))["n"]
         deadline = time.monotonic() + timeout
         # completion is observed locally (every bind acknowledged, or every pod parked):
@@ -276,8 +279,14 @@ class HttpShard:
                     bound + len(q._unsched) + len(q._backoff_pods) >= n:
                 break
             await asyncio.sleep(0.0005)
+        t_seen = time.monotonic()
         st = await self._call("GET", "/debug/bench/status?full=1")
         sched.take_lane_samples()
+        # the lane's runs of this burst, ms from the burst request: (pick, worker start, worker
+        # end, lane done, pods), and when the scheduler saw the last acknowledgement
+        self.last_runs = ([tuple(round((x - t_burst) * 1e3, 3) if x else 0.0 for x in r[:4]) + (r[4],)
+                           for r in sched.lane.lane.run_log()] if sched.lane is not None else [])
+        self.last_seen_ms = round((t_seen - t_burst) * 1e3, 3)
         return BurstResult(n, st["bound"], n - st["bound"], st["elapsed"], st["latencies"],
                            list(sched.e2e_samples))
 
