@@ -290,6 +290,13 @@ def main(argv=None) -> int:
                         pass
             return t
 
+        def api_prof() -> dict:
+            try:
+                return loop.run_until_complete(shards[0].api_prof()) if transport == "http" else {}
+            except Exception:  # noqa: BLE001 - python apiserver: no profile
+                return {}
+
+        ap0 = api_prof()
         sync()
         a0 = api_cpu()
         as0 = api_sys[0]
@@ -329,6 +336,7 @@ def main(argv=None) -> int:
             sys.stderr.write("threads " + json.dumps(sorted(top, reverse=True)[:12]) + "\n")
         le1 = lane_engine()
         wd1 = watch_decode()
+        ap1 = api_prof()
         my_bound = sum(r.bound for r in results)
         threads = {k: round((v - th0.get(k, 0.0)) / my_bound * 1e6, 2) for k, v in sorted(th1.items())
                    if my_bound and v - th0.get(k, 0.0) > 0}
@@ -403,6 +411,11 @@ def main(argv=None) -> int:
                 if bound and api_s == api_s else None,
                 "apiserver_sys_us_per_pod": round(api_sys_s / (bound / max(world, 1)) * 1e6, 2)
                 if bound and api_s == api_s else None} if transport == "http" else {}),
+            # the fake apiserver's event loop by request kind (µs per bound pod, rank 0; the
+            # status requests that end each step count under "bench")
+            **({"apiserver_loop_us_per_pod": {k: round((v[0] - ap0.get(k, [0, 0])[0]) / my_bound * 1e6, 2)
+                                              for k, v in ap1.items() if v[0] > ap0.get(k, [0, 0])[0]}}
+               if ap1 and my_bound else {}),
             "pods_bound": bound,
             "pods_unschedulable": unsched,
             "device_cycles": device_cycles,

@@ -40,13 +40,20 @@ double mono() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-std::string rfc3339_now() {
-  time_t t = time(nullptr);
-  struct tm tm;
-  gmtime_r(&t, &tm);
-  char buf[32];
-  strftime(buf, sizeof(buf), "%Y-%m-%dT%H:%M:%SZ", &tm);
-  return buf;
+// second resolution, formatted once per second (the server is single-threaded)
+const std::string& rfc3339_now() {
+  static time_t last = -1;
+  static std::string text;
+  const time_t t = time(nullptr);
+  if (t != last) {
+    struct tm tm;
+    gmtime_r(&t, &tm);
+    char buf[32];
+    strftime(buf, sizeof(buf), "%Y-%m-%dT%H:%M:%SZ", &tm);
+    text = buf;
+    last = t;
+  }
+  return text;
 }
 
 struct ResDef {
@@ -132,14 +139,21 @@ SP make_stored(Value v) {
 }
 
 // a version made by editing `from` at `edited` (dotted paths): keeps the field-selector values
-// no edit can have touched (neither path a prefix of the other)
+// no edit can have touched (neither path a prefix of the other). `rv_at`: where the caller put
+// the resourceVersion value (its opening quote), when it knows — else it is searched for.
 std::shared_ptr<Stored> make_stored_text(std::string text, int64_t rv, std::string ns, const Stored* from = nullptr,
-                                         std::initializer_list<std::string_view> edited = {}) {
+                                         std::initializer_list<std::string_view> edited = {},
+                                         size_t rv_at = std::string::npos) {
   auto s = std::make_shared<Stored>();
   s->text = std::move(text);
   s->rv = rv;
   s->ns = std::move(ns);
-  locate_rv(*s);
+  if (rv_at != std::string::npos && rv > 0) {
+    s->rv_off = rv_at;
+    s->rv_len = std::to_string(rv).size() + 2;
+  } else {
+    locate_rv(*s);
+  }
   if (from)
     for (const auto& f : from->fields) {
       bool hit = false;
@@ -160,11 +174,13 @@ struct TextEdits {
   struct E {
     size_t beg, end;
     std::string text;
+    bool mark = false;
   };
   std::vector<E> es;
-  void replace(std::string_view doc, FlatDoc::View v, std::string t) {
+  size_t marked = std::string::npos;   // after apply(): where the marked edit's text landed
+  void replace(std::string_view doc, FlatDoc::View v, std::string t, bool mark = false) {
     const size_t b = size_t(v.raw().data() - doc.data());
-    es.push_back({b, b + v.raw().size(), std::move(t)});
+    es.push_back({b, b + v.raw().size(), std::move(t), mark});
   }
   // a member at the front of object `o` (its text starts with '{')
   void insert_member(std::string_view doc, FlatDoc::View o, const std::string& member) {
@@ -180,6 +196,7 @@ struct TextEdits {
     size_t at = 0;
     for (const E& e : es) {
       out.append(doc.substr(at, e.beg - at));
+      if (e.mark) marked = out.size();
       out.append(e.text);
       at = e.end;
     }
@@ -601,11 +618,12 @@ class Server {
       t.reserve(cur->text.size() + 4);
       t.append(cur->text, 0, cur->rv_off).append(quoted(rvs)).append(cur->text, cur->rv_off + cur->rv_len,
                                                                        std::string::npos);
-      s = make_stored_text(std::move(t), last_rv_, cur->ns, cur.get(), {"metadata.resourceVersion"});
+      s = make_stored_text(std::move(t), last_rv_, cur->ns, cur.get(), {"metadata.resourceVersion"}, cur->rv_off);
     } else if (FlatDoc::View rvv = cur->fv() ? cur->fv().get("metadata").get("resourceVersion") : FlatDoc::View()) {
       TextEdits ed;
-      ed.replace(cur->text, rvv, quoted(rvs));
-      s = make_stored_text(ed.apply(cur->text), last_rv_, cur->ns, cur.get(), {"metadata.resourceVersion"});
+      ed.replace(cur->text, rvv, quoted(rvs), true);
+      std::string t = ed.apply(cur->text);
+      s = make_stored_text(std::move(t), last_rv_, cur->ns, cur.get(), {"metadata.resourceVersion"}, ed.marked);
     } else {
       Value gone = cur->v();
       gone.at("metadata").at("resourceVersion") = Value::str(rvs);
@@ -615,7 +633,9 @@ class Server {
     return s;
   }
 
-  bool bind(const std::string& ns, const std::string& name, const Value& body, ApiErr* err) {
+  // `body`: the Binding, read through a flat view (no DOM: only uid, target.name and the
+  // annotations are used, the annotation values copied as their JSON text)
+  bool bind(const std::string& ns, const std::string& name, FlatDoc::View body, ApiErr* err) {
     ResState& rs = *by_key_["pods"];
     std::string key = ns + "/" + name;
     auto it = rs.objs.find(key);
@@ -631,8 +651,8 @@ class Server {
       return false;
     }
     FlatDoc::View meta = root.get("metadata"), spec = root.get("spec"), status = root.get("status");
-    const Value* bm = body.get("metadata");
-    std::string_view uid = bm ? bm->sv("uid") : std::string_view();
+    const FlatDoc::View bm = body.is(FlatDoc::Obj) ? body.get("metadata") : FlatDoc::View();
+    std::string_view uid = bm.is(FlatDoc::Obj) ? bm.sv("uid") : std::string_view();
     if (!uid.empty() && meta && meta.sv("uid") != uid) {
       *err = {409, "Conflict", "pod " + key + " uid mismatch"};
       return false;
@@ -641,8 +661,8 @@ class Server {
       *err = {409, "Conflict", "pod " + key + " is already assigned to node " + std::string(spec.sv("nodeName"))};
       return false;
     }
-    const Value* tgt = body.get("target");
-    const std::string node = tgt ? std::string(tgt->sv("name")) : "";
+    const FlatDoc::View tgt = body.is(FlatDoc::Obj) ? body.get("target") : FlatDoc::View();
+    const std::string node = tgt.is(FlatDoc::Obj) ? std::string(tgt.sv("name")) : "";
     const std::string rvs = next_rv();
     TextEdits ed;
     // spec.nodeName
@@ -673,29 +693,29 @@ class Server {
     }
     // metadata: the Binding's annotations merged, a new resourceVersion
     if (meta.is(FlatDoc::Obj)) {
-      if (FlatDoc::View x = meta.get("resourceVersion")) ed.replace(doc, x, quoted(rvs));
+      if (FlatDoc::View x = meta.get("resourceVersion")) ed.replace(doc, x, quoted(rvs), true);
       else ed.insert_member(doc, meta, "\"resourceVersion\":" + quoted(rvs));
-      const Value* ann = bm ? bm->get("annotations") : nullptr;
-      if (ann && ann->t == Value::Obj && !ann->obj.empty()) {
+      const FlatDoc::View ann = bm.is(FlatDoc::Obj) ? bm.get("annotations") : FlatDoc::View();
+      if (ann.is(FlatDoc::Obj) && ann.size()) {
         FlatDoc::View ma = meta.get("annotations");
         if (ma.is(FlatDoc::Obj)) {
           std::string add;
-          for (const auto& kv : ann->obj) {
-            if (FlatDoc::View x = ma.get(kv.first)) {
-              ed.replace(doc, x, dump(kv.second));
+          for (FlatDoc::View kv = ann.first(); kv; kv = kv.next()) {
+            if (FlatDoc::View x = ma.get(kv.key())) {
+              ed.replace(doc, x, std::string(kv.raw()));
             } else {
               if (!add.empty()) add.push_back(',');
-              add.append(quoted(kv.first)).push_back(':');
-              add.append(dump(kv.second));
+              add.append(quoted(kv.key())).push_back(':');
+              add.append(kv.raw());
             }
           }
           if (!add.empty()) ed.insert_member(doc, ma, add);
         } else {
           std::string obj = "{";
-          for (const auto& kv : ann->obj) {
+          for (FlatDoc::View kv = ann.first(); kv; kv = kv.next()) {
             if (obj.size() > 1) obj.push_back(',');
-            obj.append(quoted(kv.first)).push_back(':');
-            obj.append(dump(kv.second));
+            obj.append(quoted(kv.key())).push_back(':');
+            obj.append(kv.raw());
           }
           obj.push_back('}');
           if (ma) ed.replace(doc, ma, obj);
@@ -707,12 +727,14 @@ class Server {
       --last_rv_;
       return false;
     }
-    SP s = make_stored_text(ed.apply(doc), last_rv_, cur->ns, cur.get(),
+    std::string text = ed.apply(doc);
+    SP s = make_stored_text(std::move(text), last_rv_, cur->ns, cur.get(),
                             {"spec.nodeName", "status.conditions", "metadata.resourceVersion", "metadata.annotations",
                              // an inserted spec / status holds only the edited member; one that
                              // was not an object was replaced whole
                              spec && !spec.is(FlatDoc::Obj) ? "spec" : "spec.nodeName",
-                             status && !status.is(FlatDoc::Obj) ? "status" : "status.conditions"});
+                             status && !status.is(FlatDoc::Obj) ? "status" : "status.conditions"},
+                            ed.marked);
     it->second = s;
     bind_log_[key] = mono();
     emit(rs, 'M', s, cur);
@@ -773,6 +795,27 @@ class Server {
   };
   std::vector<TmplText> tmpl_text_;
   std::unordered_map<std::string, double> create_log_, bind_log_;
+  // where the event loop's time goes (seconds, cumulative; /debug/bench/status reports it):
+  // requests by kind, the bench jobs' slices, socket reads + request parsing, response writes
+  enum Prof { kBind, kEvent, kCreate, kDelete, kGetList, kWatch, kUpdate, kBench, kJobCreate, kJobDelete, kRead,
+              kFlush, kNProf };
+  double prof_[kNProf] = {};
+  uint64_t prof_n_[kNProf] = {};
+  static int prof_kind(const Request& r) {
+    const std::string& p = r.path;
+    if (p.rfind("/debug/", 0) == 0) return kBench;
+    if (r.method == "POST") {
+      if (p.size() >= 8 && p.compare(p.size() - 8, 8, "/binding") == 0) return kBind;
+      if (p.size() >= 7 && p.compare(p.size() - 7, 7, "/events") == 0) return kEvent;
+      return kCreate;
+    }
+    if (r.method == "DELETE") return kDelete;
+    if (r.method == "GET") {
+      const std::string& q = r.query;
+      return q.find("watch=1") != std::string::npos || q.find("watch=true") != std::string::npos ? kWatch : kGetList;
+    }
+    return kUpdate;
+  }
 };
 
 void Server::flush(Conn* c) {
@@ -1020,7 +1063,16 @@ void Server::handle_bench(Conn* c, Request& req) {
       int n = snprintf(buf, sizeof(buf), "%.9f", bind_log_.empty() ? 0.0 : tend - t0);
       out.append("],\"elapsed\":").append(buf, size_t(n));
     }
-    out.append("}");
+    static const char* kProfName[kNProf] = {"bind", "event", "create", "delete", "get_list", "watch", "update",
+                                             "bench", "job_create", "job_delete", "read", "flush"};
+    out.append(",\"prof_s\":{");
+    for (int q = 0; q < kNProf; ++q) {
+      char buf[96];
+      int n = snprintf(buf, sizeof(buf), "%s\"%s\":[%.6f,%llu]", q ? "," : "", kProfName[q], prof_[q],
+                       static_cast<unsigned long long>(prof_n_[q]));
+      out.append(buf, size_t(n));
+    }
+    out.append("}}");
     respond(c, 200, out);
     return;
   }
@@ -1071,10 +1123,12 @@ void Server::step_jobs() {
       text.reserve(tt.meta_rest.size() + tt.top_rest.size() + 160);
       text.append("{\"metadata\":{\"name\":").append(quoted(name));
       text.append(",\"uid\":").append(quoted(uid_prefix_ + ub));
-      text.append(",\"resourceVersion\":\"").append(rvs).append("\"");
+      text.append(",\"resourceVersion\":");
+      const size_t rv_at = text.size();
+      text.append("\"").append(rvs).append("\"");
       text.append(",\"creationTimestamp\":\"").append(job.ts).append("\"");
       text.append(tt.meta_rest).append("}").append(tt.top_rest).append("}");
-      SP s = make_stored_text(std::move(text), last_rv_, tt.ns);
+      SP s = make_stored_text(std::move(text), last_rv_, tt.ns, nullptr, {}, rv_at);
       pods.objs[key] = s;
       create_log_[key] = mono();
       emit(pods, 'A', s, nullptr);
@@ -1151,6 +1205,18 @@ void Server::handle(Conn* c, Request& req) {
   if (parts.size() > i + 2) sub = parts[i + 2];
   const std::string& m = req.method;
   ApiErr err;
+  if (m == "POST" && sub == "binding" && rs.def == &kRes[0]) {
+    FlatDoc fd;
+    if (!req.body.empty() && !fd.parse(req.body)) {
+      respond_err(c, {400, "BadRequest", "invalid JSON body"});
+      return;
+    }
+    if (bind(ns.empty() ? "default" : ns, name, req.body.empty() ? FlatDoc::View() : fd.root(), &err))
+      respond(c, 201, "{\"kind\":\"Status\",\"apiVersion\":\"v1\",\"status\":\"Success\",\"code\":201}");
+    else
+      respond_err(c, err);
+    return;
+  }
   if (m == "GET") {
     if (name.empty()) {
       std::string w = query_param(req.query, "watch");
@@ -1174,13 +1240,6 @@ void Server::handle(Conn* c, Request& req) {
     }
   }
   if (m == "POST") {
-    if (sub == "binding" && rs.def == &kRes[0]) {
-      if (bind(ns.empty() ? "default" : ns, name, body, &err))
-        respond(c, 201, "{\"kind\":\"Status\",\"apiVersion\":\"v1\",\"status\":\"Success\",\"code\":201}");
-      else
-        respond_err(c, err);
-      return;
-    }
     SP s2 = create(rs, std::move(body), ns, &err);
     if (s2) respond(c, 201, s2->text);
     else respond_err(c, err);
@@ -1269,9 +1328,17 @@ int Server::run() {
       }
       Conn* c = static_cast<Conn*>(evs[k].data.ptr);
       if (c->dead) continue;
-      if (evs[k].events & EPOLLOUT) flush(c);
+      if (evs[k].events & EPOLLOUT) {
+        const double tf = mono();
+        flush(c);
+        prof_[kFlush] += mono() - tf;
+      }
       if (c->dead) continue;
       if (evs[k].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) {
+        // everything in this block that is not a request's handler counts as reading
+        const double tr = mono();
+        double handled = 0;
+        for (int q = 0; q < kNProf; ++q) handled -= prof_[q];
         while (!c->dead) {
           ssize_t r = ::recv(c->fd, buf.data(), buf.size(), 0);
           if (r < 0) {
@@ -1296,15 +1363,27 @@ int Server::run() {
                 // a request after a watch on the same connection: end the stream first
                 finish_watch(c);
               }
+              const int pk = prof_kind(c->req);
+              const double th = mono();
               handle(c, c->req);
+              prof_[pk] += mono() - th;
+              prof_n_[pk]++;
               if (!c->req.keep_alive) c->close_after_write = true;
             }
           }
           if (size_t(r) < buf.size()) break;
         }
+        for (int q = 0; q < kNProf; ++q) handled += prof_[q];
+        prof_[kRead] += mono() - tr - handled;
       }
     }
-    step_jobs();
+    if (!jobs_.empty()) {
+      const int pk = jobs_.front().del ? kJobDelete : kJobCreate;
+      const double tj = mono();
+      step_jobs();
+      prof_[pk] += mono() - tj;
+      prof_n_[pk]++;
+    }
     double now = mono();
     if (now >= next_tick) {
       next_tick = now + 0.5;
@@ -1321,7 +1400,9 @@ int Server::run() {
     }
     std::vector<Conn*> d;
     d.swap(dirty_);
+    const double tf = mono();
     for (Conn* c : d) flush(c);
+    prof_[kFlush] += mono() - tf;
     for (auto it = conns_.begin(); it != conns_.end();) {
       if (it->second->dead) it = conns_.erase(it);
       else ++it;

@@ -249,7 +249,7 @@ class HttpShard:
             tr = time.perf_counter()
             await self._call("POST", "/debug/bench/reset")
             while sched.cache.pods or q._active_entries or sched.pending_binds or sched.lane_owned():
-                await asyncio.sleep(0.001)      # the deletes reached the scheduler
+                await asyncio.sleep(0.0002)     # the deletes reached the scheduler
             self.last_reset_s = time.perf_counter() - tr
         self._bursts += 1
         sched.take_lane_samples()
@@ -289,6 +289,11 @@ class HttpShard:
         self.last_seen_ms = round((t_seen - t_burst) * 1e3, 3)
         return BurstResult(n, st["bound"], n - st["bound"], st["elapsed"], st["latencies"],
                            list(sched.e2e_samples))
+
+    async def api_prof(self) -> dict:
+        """The fake apiserver's cumulative event-loop seconds and counts by request kind."""
+        st = await self._call("GET", "/debug/bench/status")
+        return st.get("prof_s", {})
 
     async def stop(self) -> None:
         import shutil
