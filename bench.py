@@ -314,6 +314,9 @@ def main(argv=None) -> int:
             if os.environ.get("YODA_BENCH_RUNLOG"):
                 sh = shards[a.warmup + i]
                 sys.stderr.write("runlog " + json.dumps({"step": i, "seen_ms": getattr(sh, "last_seen_ms", None),
+                                                         "reset_post_ms": round(getattr(sh, "last_reset_post_s", 0) * 1e3, 3),
+                                                         "reset_ms": round(getattr(sh, "last_reset_s", 0) * 1e3, 3),
+                                                         "reset_trace": getattr(sh, "last_reset_trace", None),
                                                          "runs": getattr(sh, "last_runs", [])}) + "\n")
         sync()
         elapsed = time.perf_counter() - t0
