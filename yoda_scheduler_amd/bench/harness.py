@@ -262,11 +262,32 @@ class HttpShard:
             await self._call("POST", "/debug/bench/reset")
             self.last_reset_post_s = time.perf_counter() - tr
             trace = [] if os.environ.get("YODA_BENCH_RUNLOG") else None
+            if os.environ.get("YODA_BENCH_LOOPDEBUG"):
+                # name the event-loop callbacks that hold the loop during the reset
+                import logging
+                import sys
+                lg = logging.getLogger("asyncio")
+                lg.setLevel(logging.WARNING)
+                if not lg.handlers:
+                    lg.addHandler(logging.StreamHandler(sys.stderr))
+                    lg.propagate = False
+                lp = asyncio.get_event_loop()
+                lp.slow_callback_duration = 0.0003
+                lp.set_debug(True)
+            if sched.lane is not None:
+                # woken by the lane when its last pod is released (an asyncio sleep shorter than
+                # a millisecond still waits for epoll's 1 ms tick when nothing else wakes the loop)
+                await sched.lane.wait_unowned(60.0)
             while sched.cache.pods or q._active_entries or sched.pending_binds or sched.lane_owned():
                 if trace is not None:
-                    trace.append((round((time.perf_counter() - tr) * 1e3, 3), sched.lane_owned(), len(sched.cache.pods)))
+                    trace.append((round((time.perf_counter() - tr) * 1e3, 3), sched.lane_owned(), len(sched.cache.pods),
+                                  len(q._active_entries), sched.pending_binds))
                 await asyncio.sleep(0.0002)     # the deletes reached the scheduler
+                if trace is not None:
+                    trace.append((round((time.perf_counter() - tr) * 1e3, 3),))
             self.last_reset_trace = trace
+            if os.environ.get("YODA_BENCH_LOOPDEBUG"):
+                asyncio.get_event_loop().set_debug(False)
             self.last_reset_s = time.perf_counter() - tr
         self._bursts += 1
         sched.take_lane_samples()

@@ -59,6 +59,7 @@ class NativeLane:
         self.handoffs = 0
         self.forwarded = 0
         self._waiters: list = []           # (target scheduled count, future)
+        self._unowned_waiters: list = []   # futures resolved once the lane owns no pod
 
     # ------------------------------------------------------------------ lifecycle
     def attach(self) -> None:
@@ -133,6 +134,26 @@ class NativeLane:
             self._waiters = [(t, f) for t, f in self._waiters if f is not fut]
             self.lane.set_watermark(min((t for t, _ in self._waiters), default=(1 << 64) - 1))
 
+    async def wait_unowned(self, timeout: float) -> bool:
+        """Until the lane owns no pod (e.g. every pod of a burst deleted and released), or
+        ``timeout``. Woken by the lane's own signal (a release is a move request), re-checked
+        every 2 ms in case the last change signalled nothing."""
+        loop = asyncio.get_event_loop()
+        end = loop.time() + timeout
+        while self.owned():
+            left = end - loop.time()
+            if left <= 0:
+                return False
+            fut = loop.create_future()
+            self._unowned_waiters.append(fut)
+            try:
+                await asyncio.wait_for(asyncio.shield(fut), min(left, 0.002))
+            except asyncio.TimeoutError:
+                pass
+            finally:
+                self._unowned_waiters = [f for f in self._unowned_waiters if f is not fut]
+        return True
+
     def _wake_waiters(self) -> None:
         n = self.lane.scheduled
         for t, f in self._waiters:
@@ -143,6 +164,10 @@ class NativeLane:
         fwd, hand, moves = self.lane.drain()
         if self._waiters:
             self._wake_waiters()
+        if self._unowned_waiters and not self.owned():
+            for f in self._unowned_waiters:
+                if not f.done():
+                    f.set_result(None)
         s = self.s
         if fwd:
             self.forwarded += len(fwd)
