@@ -1062,6 +1062,21 @@ void Server::handle_bench(Conn* c, Request& req) {
       }
       int n = snprintf(buf, sizeof(buf), "%.9f", bind_log_.empty() ? 0.0 : tend - t0);
       out.append("],\"elapsed\":").append(buf, size_t(n));
+      if (query_param(req.query, "full") == "2") {
+        // [[created, bound], ...] seconds from the first create (bound -1: not yet), by creation
+        std::vector<std::pair<double, double>> pts;
+        for (const auto& kv : create_log_) {
+          auto bi = bind_log_.find(kv.first);
+          pts.emplace_back(kv.second - t0, bi == bind_log_.end() ? -1.0 : bi->second - t0);
+        }
+        std::sort(pts.begin(), pts.end());
+        out.append(",\"timeline\":[");
+        for (size_t k = 0; k < pts.size(); ++k) {
+          n = snprintf(buf, sizeof(buf), "%s[%.6f,%.6f]", k ? "," : "", pts[k].first, pts[k].second);
+          out.append(buf, size_t(n));
+        }
+        out.append("]");
+      }
     }
     static const char* kProfName[kNProf] = {"bind", "event", "create", "delete", "get_list", "watch", "update",
                                              "bench", "job_create", "job_delete", "read", "flush"};

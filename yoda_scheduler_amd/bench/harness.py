@@ -318,7 +318,8 @@ class HttpShard:
                 break
             await asyncio.sleep(0.0005)
         t_seen = time.monotonic()
-        st = await self._call("GET", "/debug/bench/status?full=1")
+        st = await self._call("GET", "/debug/bench/status?full=" + ("2" if os.environ.get("YODA_BENCH_RUNLOG") else "1"))
+        self.last_timeline = st.get("timeline")
         sched.take_lane_samples()
         # the lane's runs of this burst, ms from the burst request: (pick, worker start, worker
         # end, lane done, pods), and when the scheduler saw the last acknowledgement
