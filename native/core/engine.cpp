@@ -916,7 +916,13 @@ CycleResult Engine::schedule(uint64_t pod, const PodReq& req, bool assume, const
                              const std::vector<int64_t>& extra) {
   ++cycles_;
   CycleResult r;
-  if (dev_ctx_ && candidates.empty() && extra.empty() && live_ >= dev_min_nodes_ && device_eligible(req)) {
+  // a cycle the device scorer covers scores every feasible node (the kernel filters and scores
+  // the whole table in one pass, so percentageOfNodesToScore's early exit saves it nothing);
+  // the CPU path of such a cycle (device busy, abandoned or failed) does the same, so both
+  // paths choose from the same node set
+  const bool dev_covers = dev_ctx_ && candidates.empty() && extra.empty() && live_ >= dev_min_nodes_ &&
+                          device_eligible(req);
+  if (dev_covers) {
     // a batch may hold the device (its engine lock dropped): then this cycle runs on the
     // CPU path, which is bit-exact with the device
     std::unique_lock<std::mutex> dl(dev_mu_, std::try_to_lock);
@@ -928,7 +934,7 @@ CycleResult Engine::schedule(uint64_t pod, const PodReq& req, bool assume, const
     }
     r = CycleResult();
   }
-  std::vector<int32_t> feas = feasible_nodes(req, candidates, &r.reason_counts);
+  std::vector<int32_t> feas = feasible_nodes(req, candidates, &r.reason_counts, dev_covers);
   r.feasible = (int32_t)feas.size();
   r.evaluated = candidates.empty() ? live_ : (int32_t)candidates.size();
   if (feas.empty()) return r;

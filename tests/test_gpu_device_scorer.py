@@ -294,6 +294,35 @@ def test_batch_kernel_abort_falls_back_and_recovers(require_gpu):
         eng.schedule(pi.num_id, req, True)
 
 
+def test_adaptive_percentage_cpu_fallback_scores_what_the_device_scores(require_gpu):
+    """percentageOfNodesToScore left adaptive (0: 17 % of 4096 nodes upstream): the device
+    scores every feasible node, and so does the CPU path of a cycle the device covers (a
+    batch that fell back), so both choose from the same set; without the device the CPU
+    path keeps upstream's early exit."""
+    import os
+    from yoda_scheduler_amd.ops import device_scorer as ds
+    from yoda_scheduler_amd.ops.native import core, pod_req
+    os.environ["YODA_DEV_SPIN_DEADLINE_US"] = "0"
+    try:
+        eng = core().Engine(False, 1)
+        ds.synthetic_cluster(eng, 4096, seed=62)
+        ds.enable(eng, 0, capacity=4096, min_nodes=1)
+    finally:
+        os.environ.pop("YODA_DEV_SPIN_DEADLINE_US", None)
+    assert eng.num_feasible_to_find(4096) < 1000
+    rng = random.Random(62)
+    pods = [ds.random_request(eng, rng, f"pct-{k}")[0] for k in range(16)]
+    reqs = [pod_req(eng, p) for p in pods]
+    full = [len(eng.feasible_nodes(q, [], True)[0]) for q in reqs[:1]]
+    res = eng.schedule_batch([p.num_id for p in pods], reqs)
+    assert eng.device_fallbacks >= 1                      # the batch ran on the CPU path
+    assert res[0][1] == full[0] > eng.num_feasible_to_find(4096)
+    cpu = core().Engine(False, 1)                         # no device: upstream early exit
+    ds.synthetic_cluster(cpu, 4096, seed=62)
+    q = pod_req(cpu, ds.random_request(cpu, random.Random(62), "pct-cpu")[0])
+    assert cpu.schedule(1, q, False)[1] == cpu.num_feasible_to_find(4096)
+
+
 def test_device_flush_uploads_dirty_rows(require_gpu):
     """Engine.device_flush (the scheduler's idle-time upload) pushes the rows changed since the
     last device call: afterwards nothing waits for the next cycle, and device cycles still
