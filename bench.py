@@ -290,6 +290,22 @@ def main(argv=None) -> int:
                         pass
             return t
 
+        bind_keys = ("sink_sent", "sink_queue_s", "sink_answered", "sink_rtt_s")
+
+        def bind_pipe() -> tuple:
+            """Lane Bindings in the native transport (rank 0): sent count and seconds from the lane's
+            hand-off to the write, answered count and seconds from the write to the answer read."""
+            tot = [0.0] * len(bind_keys)
+            for sh in {id(x): x for x in shards}.values():
+                nat = getattr(getattr(sh.sched, "client", None), "native", None)
+                if nat is not None:
+                    try:
+                        st = nat.stats()
+                        tot = [t + st.get(k, 0) for t, k in zip(tot, bind_keys)]
+                    except Exception:  # noqa: BLE001 - transport closed
+                        pass
+            return tuple(tot)
+
         def api_prof() -> dict:
             try:
                 return loop.run_until_complete(shards[0].api_prof()) if transport == "http" else {}
@@ -301,6 +317,7 @@ def main(argv=None) -> int:
         a0 = api_cpu()
         as0 = api_sys[0]
         wd0 = watch_decode()
+        bp0 = bind_pipe()
         le0 = lane_engine()
         th0 = thread_cpu()
         t0 = time.perf_counter()
@@ -342,6 +359,7 @@ def main(argv=None) -> int:
             sys.stderr.write("threads " + json.dumps(sorted(top, reverse=True)[:12]) + "\n")
         le1 = lane_engine()
         wd1 = watch_decode()
+        bp1 = bind_pipe()
         ap1 = api_prof()
         my_bound = sum(r.bound for r in results)
         threads = {k: round((v - th0.get(k, 0.0)) / my_bound * 1e6, 2) for k, v in sorted(th1.items())
@@ -403,6 +421,11 @@ def main(argv=None) -> int:
                                         "cpu": round((le1[1] - le0[1]) / (le1[3] - le0[3]) * 1e6, 2),
                                         "lock_wait": round((le1[2] - le0[2]) / (le1[3] - le0[3]) * 1e6, 2)}
                                        if le1[3] > le0[3] else None),
+            # lane Bindings (rank 0): µs from the lane's hand-off to the transport's write, and
+            # from the write to the answer read (the apiserver's queue + handling + the wire)
+            "lane_bind_us": ({"queue": round((bp1[1] - bp0[1]) / (bp1[0] - bp0[0]) * 1e6, 1),
+                              "rtt": round((bp1[3] - bp0[3]) / max(1.0, bp1[2] - bp0[2]) * 1e6, 1)}
+                             if bp1[0] > bp0[0] else None),
             # async device runs (rank 0): count, pods per run, µs per run from pick to the engine
             # worker and from the worker back to the lane, and the worker's idle µs per pod
             # while pods that arrived before its last run ended waited

@@ -259,6 +259,12 @@ PYBIND11_MODULE(_yoda_kube, m) {
         d["watch_bytes"] = s.watch_bytes;
         d["parse_errors"] = s.parse_errors;
         d["watch_cpu_s"] = s.watch_cpu_s;
+        d["sink_sent"] = s.sink_sent;
+        d["sink_answered"] = s.sink_answered;
+        d["sink_queue_s"] = s.sink_queue_s;
+        d["sink_queue_max_s"] = s.sink_queue_max_s;
+        d["sink_rtt_s"] = s.sink_rtt_s;
+        d["sink_rtt_max_s"] = s.sink_rtt_max_s;
         d["bytes_out"] = s.bytes_out;
         d["bytes_in"] = s.bytes_in;
         d["throttled"] = s.throttled;

@@ -429,6 +429,7 @@ struct Conn {
   std::unique_ptr<Watcher> watcher;
   bool close_after_write = false;
   bool want_out = false;
+  bool epoll_out = false;   // EPOLLOUT registered (output left over from a short send)
   bool dead = false;
 };
 
@@ -776,6 +777,7 @@ class Server {
   void start_watch(Conn* c, ResState& rs, const std::string& ns, const Request& req);
   void finish_watch(Conn* c);
   void flush(Conn* c);
+  void flush_dirty();   // every connection with pending output
   void close_conn(Conn* c);
   void send_bookmarks(ResState& rs);
 
@@ -818,6 +820,15 @@ class Server {
   }
 };
 
+void Server::flush_dirty() {
+  if (dirty_.empty()) return;
+  std::vector<Conn*> d;
+  d.swap(dirty_);
+  const double tf = mono();
+  for (Conn* c : d) flush(c);
+  prof_[kFlush] += mono() - tf;
+}
+
 void Server::flush(Conn* c) {
   c->want_out = false;
   if (c->dead) return;
@@ -832,6 +843,7 @@ void Server::flush(Conn* c) {
   }
   epoll_event ev{};
   ev.data.ptr = c;
+  bool out = false;
   if (c->woff >= c->wbuf.size()) {
     c->wbuf.clear();
     c->woff = 0;
@@ -846,8 +858,13 @@ void Server::flush(Conn* c) {
       c->woff = 0;
     }
     ev.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP;
+    out = true;
   }
-  epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &ev);
+  // the registration changes only when a send falls short or the backlog drains
+  if (out != c->epoll_out) {
+    c->epoll_out = out;
+    epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &ev);
+  }
 }
 
 void Server::close_conn(Conn* c) {
@@ -1393,6 +1410,9 @@ int Server::run() {
       }
     }
     if (!jobs_.empty()) {
+      // answers and watch events of this turn leave before the slice (≈ 64 objects of
+      // work): a Binding's answer does not wait behind the burst's next creations
+      flush_dirty();
       const int pk = jobs_.front().del ? kJobDelete : kJobCreate;
       const double tj = mono();
       step_jobs();
@@ -1413,11 +1433,7 @@ int Server::run() {
       next_bm = now + opt_.bookmark_interval_s;
       for (auto& rs : res_) send_bookmarks(*rs);
     }
-    std::vector<Conn*> d;
-    d.swap(dirty_);
-    const double tf = mono();
-    for (Conn* c : d) flush(c);
-    prof_[kFlush] += mono() - tf;
+    flush_dirty();
     for (auto it = conns_.begin(); it != conns_.end();) {
       if (it->second->dead) it = conns_.erase(it);
       else ++it;

@@ -71,6 +71,8 @@ struct Transport::Req {
   bool expired = false;     // completed by timeout; the late response is dropped
   double deadline = 0.0;
   double idle_timeout = 0.0;  // watch: close when nothing arrived for this long (0 = never)
+  double t_submit = 0.0;      // lane Bindings: handed to the transport / written to a connection
+  double t_sent = 0.0;
 };
 
 struct Transport::Conn {
@@ -283,7 +285,8 @@ uint64_t Transport::bind_many(const std::vector<BindSpec>& binds, double timeout
 void Transport::bind_native(std::vector<BindSpec>&& binds, const std::vector<uint64_t>& tags, double timeout_s,
                             PodSink* sink) {
   if (binds.empty()) return;
-  const double deadline = timeout_s > 0 ? now_s() + timeout_s : 0.0;
+  const double t_submit = now_s();
+  const double deadline = timeout_s > 0 ? t_submit + timeout_s : 0.0;
   std::vector<std::unique_ptr<Req>> rs;
   rs.reserve(binds.size());
   for (size_t k = 0; k < binds.size(); ++k) {
@@ -298,6 +301,7 @@ void Transport::bind_native(std::vector<BindSpec>&& binds, const std::vector<uin
     r->deadline = deadline;
     r->sink = sink;
     r->tag = k < tags.size() ? tags[k] : 0;
+    r->t_submit = t_submit;
     rs.push_back(std::move(r));
   }
   bool was_empty;
@@ -337,6 +341,13 @@ void complete_pod_ev(PodEv* e) {
 
 void Transport::answer(Req& r, int status, std::string&& body) {
   if (r.sink) {
+    if (r.t_sent > 0) {
+      const double rtt = now_s() - r.t_sent;
+      std::lock_guard<std::mutex> g(stats_mu_);
+      stats_.sink_rtt_s += rtt;
+      stats_.sink_rtt_max_s = std::max(stats_.sink_rtt_max_s, rtt);
+      stats_.sink_answered++;
+    }
     // delivered at flush(), in one batch per loop turn, if the sink is still attached
     if (answers_for_ != r.sink && !sink_answers_.empty()) flush_answers();
     answers_for_ = r.sink;
@@ -711,6 +722,18 @@ void Transport::on_message_done(Conn* c) {
   if (!ka) close_conn(c, -1, "connection closed by server");
 }
 
+// bytes of a watch stream decoded per I/O loop turn before requests get their turn
+// (YODA_WATCH_READ_SLICE overrides; 0 = read until the socket is drained)
+static size_t watch_read_slice() {
+  static const size_t v = [] {
+    const char* e = getenv("YODA_WATCH_READ_SLICE");
+    if (!e || !*e) return size_t(32) << 10;
+    const long long x = atoll(e);
+    return x > 0 ? size_t(x) : ~size_t(0);
+  }();
+  return v;
+}
+
 void Transport::do_read(Conn* c) {
   char buf[65536];
   size_t got_total = 0;
@@ -767,6 +790,11 @@ void Transport::do_read(Conn* c) {
       ce.events.swap(c->evs);
       complete(std::move(ce));
     }
+    // a watch stream with a backlog (a burst's ADDED events) would keep this thread here until
+    // it drains, while the lane's Bindings wait to be written and their answers to be read:
+    // hand back to the loop after a slice (epoll is level-triggered, the rest is read next
+    // turn). TLS keeps reading: bytes OpenSSL already buffered raise no further epoll event.
+    if (c->watch && !c->ssl && got_total >= watch_read_slice()) break;
   }
   if (got_total) {
     std::lock_guard<std::mutex> g(stats_mu_);
@@ -855,6 +883,14 @@ void Transport::dispatch() {
     std::unique_ptr<Req> r = std::move(ready_.front());
     ready_.pop_front();
     best->wbuf.append(r->wire);
+    if (r->t_submit > 0) {
+      r->t_sent = now;
+      const double q = now - r->t_submit;
+      std::lock_guard<std::mutex> g(stats_mu_);
+      stats_.sink_queue_s += q;
+      stats_.sink_queue_max_s = std::max(stats_.sink_queue_max_s, q);
+      stats_.sink_sent++;
+    }
     r->wire.clear();
     r->wire.shrink_to_fit();
     best->inflight.push_back(std::move(r));

@@ -343,3 +343,17 @@ def test_async_runs_survive_deletes_and_rebinds_while_on_the_engine(monkeypatch,
                 await e.cl.delete("pods", f"a{i}", "default")
             assert await e.wait(lambda: e.sched.engine.ledger_size == 0 and lane.stats()["owned"] == 0)
     run(go())
+
+
+def test_watch_read_sliced_to_one_recv_per_turn_keeps_the_lane_exact():
+    """The transport hands a watch stream back to its event loop after each slice
+    (YODA_WATCH_READ_SLICE; read once per process, so a child process): with a 1-byte slice
+    every recv is followed by a loop turn, and a burst still binds, confirms and releases."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, YODA_WATCH_READ_SLICE="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+                        f"{__file__}::test_lane_burst_confirms_echoes_and_releases_on_delete"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
