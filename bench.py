@@ -190,9 +190,10 @@ def main(argv=None) -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     # before any thread exists: threads and the apiserver child inherit the mask
     # (yoda_scheduler_amd/utils/affinity.py: on one box 99-108 k vs 51-68 k pods/s unpinned)
-    from yoda_scheduler_amd.utils.affinity import pin_l3
-    # one rank: the least busy domain; several: rank r takes the r-th (they must not collide)
-    pinned = pin_l3(local_rank, least_busy=world == 1) if a.pin == "l3" else None
+    from yoda_scheduler_amd.utils import affinity
+    # one rank: the least busy domain now; several: after the process group is up, local rank
+    # 0 ranks the domains by idleness and rank r takes the r-th (they must not collide)
+    pinned = affinity.pin_l3(0, least_busy=True) if a.pin == "l3" and world == 1 else None
 
     import torch
     import torch.distributed as dist
@@ -210,6 +211,14 @@ def main(argv=None) -> int:
             dist.init_process_group(backend, device_id=torch.device("cuda", torch.cuda.current_device()))
         else:
             dist.init_process_group(backend)
+        if a.pin == "l3":
+            # the scheduler's threads and the apiserver child start later and inherit the mask
+            single_node = int(os.environ.get("LOCAL_WORLD_SIZE", world)) == world
+            order = [affinity.ranked_l3_sets() if rank == 0 else None]
+            if single_node:
+                dist.broadcast_object_list(order, src=0)
+            sets = order[0] if single_node else affinity.l3_cpu_sets()
+            pinned = affinity.pin_cpus(sets[local_rank % len(sets)]) if len(sets) > 1 else None
     dev = torch.device("cuda", torch.cuda.current_device()) if cuda and (world == 1 or backend == "nccl") \
         else torch.device("cpu")
 

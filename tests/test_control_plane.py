@@ -725,5 +725,9 @@ def test_cpu_affinity_spec_and_l3_grouping(monkeypatch):
     monkeypatch.setattr(affinity, "_busy_fractions", lambda cpus: {c: (0.9 if c in (0, 1, 4, 5) else 0.1) for c in cpus})
     assert affinity.apply("l3") == [2, 3, 6, 7] and affinity.apply("l3:2") == [0, 1, 4, 5]
     assert got == [[2, 3, 6, 7], [0, 1, 4, 5]]
+    # several bench ranks: rank 0 ranks the domains most idle first, rank r takes the r-th
+    assert affinity.ranked_l3_sets() == [[2, 3, 6, 7], [0, 1, 4, 5]]
+    monkeypatch.setattr(affinity, "_busy_fractions", lambda cpus: {c: 0.0 for c in cpus})
+    assert affinity.ranked_l3_sets() == [[0, 1, 4, 5], [2, 3, 6, 7]]     # ties keep CPU order
     monkeypatch.setattr(os, "sched_getaffinity", lambda pid: {0, 1})
     assert affinity.apply("l3") is None

@@ -73,6 +73,23 @@ def pin_l3(index: int = 0, least_busy: bool = False) -> Optional[list[int]]:
     return cpus
 
 
+def ranked_l3_sets() -> list[list[int]]:
+    """The cache domains this process may use, most idle first over the last 50 ms (ties keep
+    CPU order); [] when the topology is not readable."""
+    sets = l3_cpu_sets()
+    busy = _busy_fractions([c for g in sets for c in g]) if len(sets) > 1 else {}
+    if not busy:
+        return sets
+    return sorted(sets, key=lambda g: (round(sum(busy.get(c, 1.0) for c in g) / len(g), 2), g[0]))
+
+
+def pin_cpus(cpus: Optional[list[int]]) -> Optional[list[int]]:
+    """Restrict this thread (and what it creates later) to ``cpus``; None leaves it alone."""
+    if cpus:
+        os.sched_setaffinity(0, cpus)
+    return cpus
+
+
 def apply(spec: str) -> Optional[list[int]]:
     """``none`` | ``l3`` (the least busy domain) | ``l3:<index>`` (the CLI's --cpu-affinity)."""
     if not spec or spec == "none":
