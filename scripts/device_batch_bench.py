@@ -2,7 +2,9 @@
 """Engine-level throughput of a burst on a large synthetic cluster: per-pod device cycles
 (one host round trip each) vs batched device cycles (yoda_dev_schedule_batch) as per-pod launch
 chains enqueued back to back (``batch-chain``) or as ONE persistent k_batch dispatch per batch
-(``batch``, node rows resident in LDS). One JSON line per (nodes, mode)."""
+(``batch``, node rows resident in LDS), against the CPU engine alone (``cpu``: the same batches
+on one engine thread, no device attached — where the two cross is ``deviceScorer.minNodes``).
+One JSON line per (nodes, mode)."""
 from __future__ import annotations
 
 import argparse
@@ -22,9 +24,10 @@ def run(nodes: int, mode: str, pods: int, batch: int, trace: bool = False, busy:
     eng.set_percentage_of_nodes_to_score(100)
     ds.synthetic_cluster(eng, nodes, seed=nodes, busy=busy)
     # batch-chain: per-pod launch chains enqueued back to back; batch: the persistent k_batch
-    os.environ["YODA_DEV_PERSIST"] = "0" if mode == "batch-chain" else "1"
-    ds.enable(eng, 0, capacity=nodes + 16, min_nodes=1)
-    os.environ.pop("YODA_DEV_PERSIST", None)
+    if mode != "cpu":
+        os.environ["YODA_DEV_PERSIST"] = "0" if mode == "batch-chain" else "1"
+        ds.enable(eng, 0, capacity=nodes + 16, min_nodes=1)
+        os.environ.pop("YODA_DEV_PERSIST", None)
     rng = random.Random(1)
     reqs, ks = [], []
     for k in range(pods):
@@ -34,7 +37,7 @@ def run(nodes: int, mode: str, pods: int, batch: int, trace: bool = False, busy:
     # warm up (kernels, first full-table upload)
     eng.schedule_batch([p for p, _ in reqs[:8]], [r for _, r in reqs[:8]])
     t0 = time.perf_counter()
-    if mode.startswith("batch"):
+    if mode.startswith("batch") or mode == "cpu":
         for i in range(8, pods, batch):
             chunk = reqs[i:i + batch]
             eng.schedule_batch([p for p, _ in chunk], [r for _, r in chunk])
@@ -60,7 +63,7 @@ def run(nodes: int, mode: str, pods: int, batch: int, trace: bool = False, busy:
                 extra["score_a_us_by_gpus"] = {str(kk): [len(v), round(sum(v) / len(v), 2)]
                                                for kk, v in sorted(by_k.items())}
             ds.batch_trace(eng, False)
-    return {**extra, "nodes": nodes, "mode": mode, "pods": n, "batch": batch if mode.startswith("batch") else 1,
+    return {**extra, "nodes": nodes, "mode": mode, "pods": n, "batch": batch if mode.startswith("batch") or mode == "cpu" else 1,
             "us_per_pod": round(dt / n * 1e6, 1), "pods_per_s": round(n / dt, 1),
             "device_cycles": eng.device_cycles, "fallbacks": eng.device_fallbacks}
 
