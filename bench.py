@@ -161,7 +161,7 @@ def main(argv=None) -> int:
     ap.add_argument("--node-gpus", type=int, default=None, choices=[1, 2, 4, 8],
                     help="GPUs per synthetic node (BASELINE protocol item 5); default: the config's own")
     ap.add_argument("--device", choices=["auto", "on", "off"], default="auto",
-                    help="gfx950 device scorer (used automatically for clusters >= 256 nodes)")
+                    help="gfx950 device scorer (used automatically for clusters >= deviceScorer.minNodes = 48 nodes)")
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
                     help="native batches on a worker thread, overlapped with binding (auto: with the device scorer)")
     ap.add_argument("--qps", type=float, default=5000.0, help="client QPS (deploy default 5000; reference 50)")

@@ -17,7 +17,20 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(nodes: int, mode: str, pods: int, batch: int, trace: bool = False, busy: float = 0.3) -> dict:
+def bench_request(engine, rng: random.Random, uid: str):
+    """A pod of the bench's BASELINE label mix (configs 3/5/6: 70 % one GPU, 18 % two, 9 %
+    four, 3 % eight) with the bench's container requests."""
+    from yoda_scheduler_amd.bench.workloads import _mixed_labels
+    from yoda_scheduler_amd.models.pod import PodInfo
+    from yoda_scheduler_amd.ops.native import pod_req
+    pi = PodInfo.from_obj({"metadata": {"name": uid, "uid": uid, "labels": _mixed_labels(rng)},
+                           "spec": {"containers": [{"name": "c", "resources": {"requests": {
+                               "cpu": "100m", "memory": "128Mi"}}}]}})
+    return pi, pod_req(engine, pi)
+
+
+def run(nodes: int, mode: str, pods: int, batch: int, trace: bool = False, busy: float = 0.3,
+        mix: str = "random") -> dict:
     from yoda_scheduler_amd.ops import device_scorer as ds
     from yoda_scheduler_amd.ops.native import core, pod_req
     eng = core().Engine(False, 1)
@@ -31,7 +44,8 @@ def run(nodes: int, mode: str, pods: int, batch: int, trace: bool = False, busy:
     rng = random.Random(1)
     reqs, ks = [], []
     for k in range(pods):
-        pi, req = ds.random_request(eng, rng, f"{mode}-{nodes}-{k}")
+        make = bench_request if mix == "bench" else ds.random_request
+        pi, req = make(eng, rng, f"{mode}-{nodes}-{k}")
         reqs.append((pi.num_id, req))
         ks.append(pi.gpu.number if pi.gpu.has_number else 1)
     # warm up (kernels, first full-table upload)
@@ -63,7 +77,7 @@ def run(nodes: int, mode: str, pods: int, batch: int, trace: bool = False, busy:
                 extra["score_a_us_by_gpus"] = {str(kk): [len(v), round(sum(v) / len(v), 2)]
                                                for kk, v in sorted(by_k.items())}
             ds.batch_trace(eng, False)
-    return {**extra, "nodes": nodes, "mode": mode, "pods": n, "batch": batch if mode.startswith("batch") or mode == "cpu" else 1,
+    return {**extra, "nodes": nodes, "mode": mode, "mix": mix, "pods": n, "batch": batch if mode.startswith("batch") or mode == "cpu" else 1,
             "us_per_pod": round(dt / n * 1e6, 1), "pods_per_s": round(n / dt, 1),
             "device_cycles": eng.device_cycles, "fallbacks": eng.device_fallbacks}
 
@@ -76,11 +90,13 @@ def main() -> int:
     ap.add_argument("--modes", default="per-pod,batch-chain,batch")
     ap.add_argument("--trace", action="store_true", help="k_batch phase breakdown (block 0 stamps)")
     ap.add_argument("--busy", type=float, default=0.3, help="synthetic cluster load (0: every node fits)")
+    ap.add_argument("--mix", choices=["random", "bench"], default="random",
+                    help="random: the parity suite's request mix; bench: the BASELINE label mix")
     a = ap.parse_args()
     import torch  # noqa: F401 - load torch's HIP runtime first (same SONAME as ours)
     for n in (int(x) for x in a.nodes.split(",")):
         for mode in a.modes.split(","):
-            print(json.dumps(run(n, mode, a.pods, a.batch, a.trace, a.busy)), flush=True)
+            print(json.dumps(run(n, mode, a.pods, a.batch, a.trace, a.busy, a.mix)), flush=True)
     return 0
 
 

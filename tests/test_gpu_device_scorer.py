@@ -136,6 +136,34 @@ def test_scheduler_auto_enables_device_scorer_and_matches_cpu(require_gpu):
     assert placed_d.keys() == placed_c.keys()
 
 
+def test_default_min_nodes_puts_a_64_node_cluster_on_the_device(require_gpu):
+    """`deviceScorer.minNodes` defaults to the measured CPU/device crossover (48 nodes,
+    profiles/bench/r3/crossover/): a 64-node cluster schedules on the gfx950 scorer with no
+    explicit device configuration, and binds every pod with the GPU count it asked for."""
+    import asyncio
+
+    from yoda_scheduler_amd.framework.config import SchedulerConfig
+    from yoda_scheduler_amd.testing import FakeCluster, yoda_config
+    assert SchedulerConfig().device_min_nodes == 48
+
+    async def go():
+        c = FakeCluster(yoda_config(batch=64), seed=3)
+        for i in range(64):
+            c.add_node(f"n{i:02d}")
+        sched = await c.start()
+        for i in range(120):
+            c.add_pod(f"p{i}", {"scv/memory": "2048", **({"scv/number": "2"} if i % 4 == 0 else {})})
+        ok = await c.wait_bound(120, 30.0)
+        gpus = [len(c.gpus_of(f"p{i}")) for i in range(120)]
+        stats = (sched.engine.device_enabled, sched.engine.device_cycles, sched.device_error)
+        await c.stop()
+        return ok, gpus, stats
+
+    ok, gpus, (enabled, cycles, err) = asyncio.run(go())
+    assert ok and gpus == [2 if i % 4 == 0 else 1 for i in range(120)]
+    assert enabled and cycles >= 120, (enabled, cycles, err)
+
+
 @pytest.mark.parametrize("n", [600, 4096])
 def test_device_batch_equals_sequential_device_cycles(require_gpu, n):
     """yoda_dev_schedule_batch (cycles enqueued back to back, winners assumed on the device)

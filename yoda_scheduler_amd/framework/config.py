@@ -117,7 +117,8 @@ class SchedulerConfig:
     # gfx950 device scorer (yodaRuntime.deviceScorer): auto = use it when a GPU is visible
     device_scorer: str = "auto"
     device_index: int = 0
-    device_min_nodes: int = 256
+    # CPU engine vs k_batch per pod on MI355X cross at ≈ 44 nodes (profiles/bench/r3/crossover/)
+    device_min_nodes: int = 48
     device_capacity: int = 65536
     engine_threads: int = 1
     # run native batches on a worker thread (GIL released) so the event loop binds and
@@ -282,7 +283,7 @@ def parse_config(doc: dict) -> SchedulerConfig:
     if cfg.device_scorer not in ("auto", "on", "off"):
         raise ValueError("yodaRuntime.deviceScorer.enabled must be auto|on|off")
     cfg.device_index = int(_f(ds, "device", 0))
-    cfg.device_min_nodes = int(_f(ds, "minNodes", 256))
+    cfg.device_min_nodes = int(_f(ds, "minNodes", 48))
     cfg.device_capacity = int(_f(ds, "capacity", 65536))
     cfg.engine_threads = int(_f(rt, "engineThreads", 1))
     cfg.events_api = str(_f(rt, "eventsAPI", cfg.events_api))
