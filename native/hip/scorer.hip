@@ -542,14 +542,17 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
   const int32_t P = sc.P;
   const int s_begin = sc.s_begin, s_end = sc.s_end;
   const uint8_t ncards = nd->ncards;
-  // ---- per-node register tables (every lane of the group holds the whole node)
+  // ---- per-node register tables (every lane of the group holds the whole node). A 1-GPU
+  // search needs only the lane's own card: it skips the tables and forms the tail's card
+  // sums with a group reduction instead (`fast1`, wave-uniform)
+  const bool fast1 = search && k == 1 && rep == 0;
   uint64_t ef[YODA_DEV_CARDS];
   uint32_t tot[YODA_DEV_CARDS], occ[YODA_DEV_CARDS];
   // the allocate/actual terms' card sums, formed from the same registers (every lane holds
   // the node): no cross-lane reduction
   uint64_t t64 = 0, a64 = 0, fsum = 0;
 #pragma unroll
-  for (int a = 0; a < YODA_DEV_CARDS; ++a) {
+  for (int a = 0; a < YODA_DEV_CARDS && !fast1; ++a) {
     const uint4 lo4 = reinterpret_cast<const uint4*>(&nd->cards[a])[0];   // total, free, reserved, pending
     ef[a] = eff_free(lo4.y, lo4.w, lo4.x, lo4.z);
     tot[a] = lo4.x;
@@ -585,20 +588,20 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
   int64_t best_o = LLONG_MAX;
   int32_t best_lb = 0;
   bool found = false;
-  if (search && act && k == 1 && rep == 0) {
+  if (fast1 && act) {
     // single-GPU pods (the bulk of a mixed burst): the k = 1 table is {1<<0 … 1<<7} in
     // order, so lane `sub` owns subset {sub}; no pairs (P = 0) and one NUMA domain leave
     // only the fit and occupancy terms — the generic loop's 28 predicated pair adds and
     // 8-card sums are skipped. Same integer arithmetic, so the result is bit-identical.
+    // Each lane reads only its own card; the tail's card sums meet in one group reduction.
+    const uint4 lo4 = reinterpret_cast<const uint4*>(&nd->cards[sub])[0];   // total, free, reserved, pending
+    const uint64_t efs = eff_free(lo4.y, lo4.w, lo4.x, lo4.z);
+    const bool in = sub < ncards;
+    t64 = gsum(in ? (uint64_t)lo4.x : 0ull);
+    a64 = gsum(in ? (uint64_t)lo4.z : 0ull);
+    fsum = gsum(in ? efs : 0ull);
     if ((emask >> sub) & 1u) {
-      uint64_t efs = ef[0];
-      uint32_t tos = tot[0], ocs = occ[0];
-#pragma unroll
-      for (int a = 1; a < YODA_DEV_CARDS; ++a) {
-        efs = sub == a ? ef[a] : efs;
-        tos = sub == a ? tot[a] : tos;
-        ocs = sub == a ? occ[a] : ocs;
-      }
+      const uint32_t tos = lo4.x, ocs = nd->occ[sub];
       const uint64_t fa = efs - r.memory;
       const int32_t leftover = tos ? (int32_t)udiv(fa * 1000000ull, (uint64_t)tos) : 0;   // ≤ 10^6
       const int32_t fit = r.binpack ? leftover : 1000000 - leftover;
