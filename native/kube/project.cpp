@@ -660,7 +660,7 @@ struct Skim {
 
 }  // namespace
 
-bool scan_watch_identity(std::string_view line, char* type, std::string_view* obj, PodProj& p) {
+bool scan_watch_identity(std::string_view line, char* type, std::string_view* obj, PodProj& p, bool only_md) {
   p = PodProj();
   Skim k{line.data(), line.data() + line.size()};
   bool ok = true, have_type = false, have_obj = false;
@@ -725,6 +725,12 @@ bool scan_watch_identity(std::string_view line, char* type, std::string_view* ob
       bool esc;
       k.ws();
       if (k.p >= k.e || *k.p != '"' || !k.str(&tname, &esc) || esc) return ok = false, true;
+      // the caller only wants echoes and deletions: any other type ends the scan here (the
+      // type leads the apiserver's watch line, so an ADDED pod is not scanned twice)
+      if (only_md && tname != "MODIFIED" && tname != "DELETED") {
+        ok = false;
+        k.p = k.e;
+      }
       return true;
     }
     if (key == "object" && !have_obj) {

@@ -83,7 +83,8 @@ void project_identity(const FlatDoc::View& pod, PodProj& p);
 // for the event type, the object's text span and the pod's identity fields (as
 // project_identity reads them), building no document. False when the line needs the parser
 // (escapes in a field it reads, malformed text): the caller then takes the FlatDoc path.
-bool scan_watch_identity(std::string_view line, char* type, std::string_view* obj, PodProj& p);
+bool scan_watch_identity(std::string_view line, char* type, std::string_view* obj, PodProj& p,
+                         bool only_md = false);
 // Fill everything but the identity fields from a full projection (`src` is consumed).
 void merge_non_identity(PodProj& dst, PodProj&& src);
 

@@ -628,13 +628,15 @@ void Transport::watch_lines(Conn* c) {
         break;
       }
     if (blank) continue;
+    std::shared_ptr<PodEv> pe;
     if (c->pods && light_pods_.load(std::memory_order_relaxed)) {
       // echoes and deletions with a lane attached: the identity fields by one skipping scan,
-      // the rest of the pod on demand (PodEv::full)
+      // the rest of the pod on demand (PodEv::full); other types stop at the type member
       char t = 0;
       std::string_view obj;
-      auto pe = std::make_shared<PodEv>();
-      if (scan_watch_identity(line, &t, &obj, pe->p) && (t == 'M' || t == 'D')) {
+      pe = std::make_shared<PodEv>();
+      static const bool scan_all = getenv("YODA_WATCH_SCAN_ALL") != nullptr;   // A/B: the old full scan
+      if (scan_watch_identity(line, &t, &obj, pe->p, !scan_all) && (t == 'M' || t == 'D')) {
         WatchEvent ev;
         ev.type = t;
         ev.rv = pe->p.rv;
@@ -669,7 +671,8 @@ void Transport::watch_lines(Conn* c) {
     if (const FlatDoc::View m = obj.get("metadata")) ev.rv = std::string(m.sv("resourceVersion"));
     const std::string_view raw = obj.raw();
     if (c->pods && ev.type != 'B' && ev.type != 'E') {
-      auto pe = std::make_shared<PodEv>();
+      if (pe) pe->p = PodProj();
+      else pe = std::make_shared<PodEv>();
       if (ev.type != 'A' && light_pods_.load(std::memory_order_relaxed)) {
         // echoes and deletions: the lane reads identity fields only; the rest on demand
         project_identity(obj, pe->p);
