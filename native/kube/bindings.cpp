@@ -118,13 +118,13 @@ PYBIND11_MODULE(_yoda_kube, m) {
   auto ident_tuple = [](const PodProj& p) {
     return py::make_tuple(p.ns, p.name, p.uid, p.rv, p.creation, p.deleting, p.sched, p.node, p.phase);
   };
-  m.def("scan_identity", [ident_tuple](const std::string& line) -> py::object {
+  m.def("scan_identity", [ident_tuple](const std::string& line, bool only_md) -> py::object {
     PodProj p;
     char t = 0;
     std::string_view obj;
-    if (!scan_watch_identity(line, &t, &obj, p)) return py::none();
+    if (!scan_watch_identity(line, &t, &obj, p, only_md)) return py::none();
     return py::make_tuple(std::string(1, t), std::string(obj), ident_tuple(p));
-  }, py::arg("line"));
+  }, py::arg("line"), py::arg("only_md") = false);
   m.def("flat_identity", [ident_tuple](const std::string& line) -> py::object {
     FlatDoc d;
     if (!d.parse(line) || !d.root().is(FlatDoc::Obj)) return py::none();

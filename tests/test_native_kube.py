@@ -212,6 +212,10 @@ def test_watch_identity_scan_equals_the_parser(pod, typ, status, deletion, prett
     else:
         assert got == want
         assert json.loads(got[1]) == pod
+    # the transport's mode: only echoes and deletions are scanned, any other type stops at
+    # the type member (the line then goes to the full parser)
+    md = K.scan_identity(line, True)
+    assert md == (got if typ in ("MODIFIED", "DELETED") else None)
 
 
 def test_flat_projection_rejects_malformed_json_like_the_dom():
