@@ -160,6 +160,8 @@ def main(argv=None) -> int:
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5, 6])
     ap.add_argument("--node-gpus", type=int, default=None, choices=[1, 2, 4, 8],
                     help="GPUs per synthetic node (BASELINE protocol item 5); default: the config's own")
+    ap.add_argument("--nodes", type=int, default=None,
+                    help="config 6 only: cluster size (default 4096; the CPU/device crossover end to end)")
     ap.add_argument("--device", choices=["auto", "on", "off"], default="auto",
                     help="gfx950 device scorer (used automatically for clusters >= deviceScorer.minNodes = 48 nodes)")
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
@@ -232,7 +234,7 @@ def main(argv=None) -> int:
 
     from yoda_scheduler_amd.bench.harness import HttpShard, Shard, percentile
     from yoda_scheduler_amd.bench.workloads import make_workload
-    w = make_workload(a.config, seed=rank, node_gpus=a.node_gpus)
+    w = make_workload(a.config, seed=rank, node_gpus=a.node_gpus, nodes=a.nodes)
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
 

@@ -52,11 +52,18 @@ def _mixed_labels(rng: random.Random) -> dict:
 
 
 def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None,
-                  node_gpus: Optional[int] = None) -> Workload:
+                  node_gpus: Optional[int] = None, nodes: Optional[int] = None) -> Workload:
     """``node_gpus`` overrides the GPUs per node (BASELINE.md protocol item 5: every
     config at 1, 2, 4 and 8 GPUs per node); pods keep their labels, so e.g. ``scv/number: 8``
-    pods are unschedulable on smaller nodes and are reported as such."""
+    pods are unschedulable on smaller nodes and are reported as such. ``nodes`` resizes
+    config 6's cluster (beyond BASELINE: the CPU/device crossover end to end)."""
     w = _make_workload(cfg, seed, template)
+    if nodes is not None:
+        if cfg != 6 or nodes < 1:
+            raise ValueError("nodes: config 6 only, >= 1")
+        spec = w.nodes[0][1]
+        w.nodes = [(f"node-{i}", spec, 8) for i in range(nodes)]
+        w.name = w.name.replace("4096 nodes", f"{nodes} nodes")
     if node_gpus is not None:
         if node_gpus < 1:
             raise ValueError("node_gpus must be >= 1")
