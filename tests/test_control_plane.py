@@ -597,6 +597,17 @@ def test_bench_node_gpus_sweep_option():
     assert d["node_gpus"] == 4 and d["pods_bound"] == 100 and "1 node x 4 MI355X" in d["config"]["model"]
 
 
+def test_bench_nodes_option_resizes_config_6_only():
+    """``--nodes`` (the CPU/device crossover end to end) resizes config 6's cluster and is
+    refused for the BASELINE configs, whose cluster shapes are fixed by BASELINE.json."""
+    from yoda_scheduler_amd.bench.workloads import make_workload
+    w = make_workload(6, nodes=64)
+    assert len(w.nodes) == 64 and "64 nodes x 8 MI355X" in w.name and w.n_pods == 1000
+    assert len({n for n, _s, _g in w.nodes}) == 64
+    with pytest.raises(ValueError):
+        make_workload(3, nodes=64)
+
+
 def test_wait_for_propagates_cancellation_and_fastbind_timeout():
     """``utils.aio.wait_for`` keeps a caller's cancellation even when the inner awaitable
     finishes in the same loop iteration (asyncio.wait_for on Python < 3.12 returns the
