@@ -1765,7 +1765,11 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
   // fastest then); beyond, 8 waves: two per SIMD hide each other's latency and halve the
   // passes (MI355X, 4096 nodes: 15.7 vs 17.7 µs/pod; 16 384: 25.8 vs 23.0; 65 536: 59 vs 43)
   const int waves = c->batch_waves ? c->batch_waves : (npb > 4 * kNodesPerWave ? 8 : 4);
-  const int npb_min = c->npb_min > 0 ? c->npb_min : waves * kNodesPerWave;
+  // up to 1024 nodes one 8-node group per block (≤ 128 blocks): the block's other waves split
+  // a multi-GPU pod's subset search, and the exchanges stay cheap at that grid (MI355X,
+  // BASELINE mix: 256 nodes 13.4 vs 14.7 µs/pod, 1024 nodes 14.3 vs 14.8; at 2048 nodes 256
+  // blocks lose, profiles/device/r3/geometry/)
+  const int npb_min = c->npb_min > 0 ? c->npb_min : (n <= 1024 ? kNodesPerWave : waves * kNodesPerWave);
   npb = npb < npb_min ? npb_min : npb;
   if (npb > kMaxNodesPerBlock) return 1;
   const int G = (n + npb - 1) / npb;
