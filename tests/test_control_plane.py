@@ -742,3 +742,15 @@ def test_cpu_affinity_spec_and_l3_grouping(monkeypatch):
     assert affinity.ranked_l3_sets() == [[0, 1, 4, 5], [2, 3, 6, 7]]     # ties keep CPU order
     monkeypatch.setattr(os, "sched_getaffinity", lambda pid: {0, 1})
     assert affinity.apply("l3") is None
+
+
+def test_parallelism_sets_engine_threads_unless_engine_threads_is_given():
+    """Upstream `parallelism` (v1beta2+) sizes the C++ engine's node fan-out when the yoda
+    runtime block does not; neither set keeps one thread (the reference's v1beta1 documents)."""
+    from yoda_scheduler_amd.framework.config import parse_config
+    base = {"apiVersion": "kubescheduler.config.k8s.io/v1beta2", "kind": "KubeSchedulerConfiguration"}
+    assert parse_config(dict(base)).engine_threads == 1
+    assert parse_config(dict(base, parallelism=8)).engine_threads == 8
+    assert parse_config(dict(base, parallelism=8, yodaRuntime={"engineThreads": 2})).engine_threads == 2
+    with pytest.raises(ValueError):
+        parse_config(dict(base, parallelism=0))

@@ -285,7 +285,11 @@ def parse_config(doc: dict) -> SchedulerConfig:
     cfg.device_index = int(_f(ds, "device", 0))
     cfg.device_min_nodes = int(_f(ds, "minNodes", 48))
     cfg.device_capacity = int(_f(ds, "capacity", 65536))
-    cfg.engine_threads = int(_f(rt, "engineThreads", 1))
+    # the engine's node fan-out threads: yodaRuntime.engineThreads, else upstream's
+    # `parallelism` (v1beta2+) when the document sets it, else 1 (the benches' setting)
+    cfg.engine_threads = int(_f(rt, "engineThreads", _f(doc, "parallelism", 1)))
+    if cfg.engine_threads < 1 or cfg.parallelism < 1:
+        raise ValueError("engineThreads and parallelism must be >= 1")
     cfg.events_api = str(_f(rt, "eventsAPI", cfg.events_api))
     if cfg.events_api not in ("events.k8s.io/v1", "v1"):
         raise ValueError("yodaRuntime.eventsAPI must be events.k8s.io/v1 or v1")
