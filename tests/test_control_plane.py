@@ -754,3 +754,46 @@ def test_parallelism_sets_engine_threads_unless_engine_threads_is_given():
     assert parse_config(dict(base, parallelism=8, yodaRuntime={"engineThreads": 2})).engine_threads == 2
     with pytest.raises(ValueError):
         parse_config(dict(base, parallelism=0))
+
+
+def test_cli_serves_healthz_on_its_own_bind_address(tmp_path):
+    """v1beta1 `healthzBindAddress` different from `metricsBindAddress`: /healthz answers on
+    its own listener, /metrics on the metrics one (upstream serves two listeners then)."""
+    import socket
+    import time
+    import urllib.request
+
+    def free_port():
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        return p
+
+    mport, hport = free_port(), free_port()
+    cfg = tmp_path / "sched.yaml"
+    cfg.write_text("apiVersion: kubescheduler.config.k8s.io/v1beta1\nkind: KubeSchedulerConfiguration\n"
+                   "leaderElection:\n  leaderElect: false\n"
+                   f"metricsBindAddress: 127.0.0.1:{mport}\nhealthzBindAddress: 127.0.0.1:{hport}\n"
+                   "profiles:\n- schedulerName: yoda-scheduler\n")
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    proc = subprocess.Popen([sys.executable, "-m", "yoda_scheduler_amd.cmd.scheduler", "--config", str(cfg),
+                             "--fake-cluster", "1", "--device-scorer", "off"],
+                            env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        def get(port, path):
+            for _ in range(200):
+                try:
+                    with urllib.request.urlopen(f"http://127.0.0.1:{port}{path}", timeout=2) as r:
+                        return r.status, r.read().decode()
+                except OSError:
+                    if proc.poll() is not None:
+                        raise AssertionError(proc.stdout.read()[-3000:])
+                    time.sleep(0.05)
+            raise AssertionError("no answer")
+        assert get(hport, "/healthz") == (200, "ok")
+        status, body = get(mport, "/metrics")
+        assert status == 200 and "scheduler_" in body
+    finally:
+        proc.terminate()
+        proc.wait(timeout=30)

@@ -187,6 +187,18 @@ async def _run(args, cfg, registry: Registry) -> int:
         log.info("serving /healthz and /metrics on port %d", await status.start())
     except OSError as e:
         log.warning("status server disabled: %s", e)
+    # upstream v1beta1 serves healthz on its own listener when healthzBindAddress differs
+    # from metricsBindAddress (both default to 0.0.0.0:10251: one listener)
+    hhost, _, hport = cfg.health_bind_address.rpartition(":")
+    health = None
+    if args.port is None and hport and (hhost, hport) != (host, str(port)):
+        health = StatusServer(args.bind_address or hhost or "0.0.0.0", int(hport), sched.metrics.render,
+                              healthy=lambda: True, ssl_context=_ssl_context(args))
+        try:
+            log.info("serving /healthz on port %d", await health.start())
+        except OSError as e:
+            log.warning("healthz server disabled: %s", e)
+            health = None
     elector = None
     le = cfg.leader_election
     if le.leader_elect:
@@ -216,6 +228,8 @@ async def _run(args, cfg, registry: Registry) -> int:
     if elector is not None:
         await elector.release()
     await status.stop()
+    if health is not None:
+        await health.stop()
     if fake_http is not None:
         await fake_http.stop()
     close = getattr(client, "close", None)
