@@ -595,6 +595,16 @@ def test_bench_node_gpus_sweep_option():
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["node_gpus"] == 4 and d["pods_bound"] == 100 and "1 node x 4 MI355X" in d["config"]["model"]
+    # a burst that leaves pods unschedulable (config 3's 2/4/8-GPU pods on a 1-GPU node) ends
+    # once every pod is bound or parked, and the next burst's reset waits for the mirror of
+    # lane pods the Python path read to empty (both used to hang)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "3", "--node-gpus", "1",
+                        "--steps", "1", "--warmup", "1", "--alt", "none"], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["pods_bound"] > 0 and d["pods_unschedulable"] > 0
+    assert d["pods_bound"] + d["pods_unschedulable"] == 1000
 
 
 def test_bench_nodes_option_resizes_config_6_only():

@@ -278,7 +278,10 @@ class HttpShard:
                 # woken by the lane when its last pod is released (an asyncio sleep shorter than
                 # a millisecond still waits for epoll's 1 ms tick when nothing else wakes the loop)
                 await sched.lane.wait_unowned(60.0)
-            while sched.cache.pods or q._active_entries or sched.pending_binds or sched.lane_owned():
+            # the cache mirrors lane pods only while Python plugins read them (sync_lane runs
+            # before a Python cycle): bring the mirror up to date before reading it
+            while sched.cache.sync_lane() >= 0 and (sched.cache.pods or q._active_entries or sched.pending_binds
+                                                   or sched.lane_owned()):
                 if trace is not None:
                     trace.append((round((time.perf_counter() - tr) * 1e3, 3), sched.lane_owned(), len(sched.cache.pods),
                                   len(q._active_entries), sched.pending_binds))
@@ -306,15 +309,22 @@ class HttpShard:
         # no polling requests charged to the scheduler process during the burst. With the
         # native lane the loop sleeps until the lane's acknowledged count reaches the burst
         # (an eventfd wake-up, not a poll); the poll below then only settles the remainder.
-        if sched.lane is not None:
-            await sched.lane.wait_scheduled(sched.lane.lane.scheduled + n - (sched.scheduled - done0),
-                                            max(0.0, deadline - time.monotonic()))
-        while time.monotonic() < deadline:
+        def parked() -> bool:
+            # every pod bound or parked (unschedulable pods handed to the Python queue)
             bound = sched.scheduled - done0
-            if bound >= n:
-                break
-            if not q._active_entries and sched.pending_binds == 0 and sched.failed > fail0 and \
-                    bound + len(q._unsched) + len(q._backoff_pods) >= n:
+            return not q._active_entries and sched.pending_binds == 0 and sched.failed > fail0 and \
+                bound + len(q._unsched) + len(q._backoff_pods) >= n
+        if sched.lane is not None:
+            # woken when the lane's count crosses the burst; a burst with unschedulable pods
+            # never gets there, so the parked check runs between short waits
+            target = sched.lane.lane.scheduled + n - (sched.scheduled - done0)
+            while time.monotonic() < deadline:
+                if await sched.lane.wait_scheduled(target, min(0.02, max(0.0, deadline - time.monotonic()))):
+                    break
+                if parked():
+                    break
+        while time.monotonic() < deadline:
+            if sched.scheduled - done0 >= n or parked():
                 break
             await asyncio.sleep(0.0005)
         t_seen = time.monotonic()
