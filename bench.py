@@ -405,6 +405,7 @@ def main(argv=None) -> int:
         if world > 1:
             per_rank = [None] * world
             dist.all_gather_object(per_rank, mine)
+        lane_log_on = any(getattr(s.sched, "lane", None) is not None and s.sched.lane.lane.log_on for s in uniq)
         for s in uniq:
             loop.run_until_complete(s.stop())
         value = bound / elapsed if elapsed > 0 else 0.0
@@ -416,6 +417,14 @@ def main(argv=None) -> int:
             # of which (http transport, rank 0) deleting the previous burst's pods and waiting until
             # the scheduler saw the deletions (timed: it is scheduler work, releases included)
             "reset_ms": [round(x * 1000.0, 3) for x in reset_s],
+            # scheduler vs teardown at a glance: the median reset, and pods/s over the timed
+            # steps with the resets taken out (rank 0's resets; the headline `value` keeps them)
+            "reset_ms_median": round(percentile(reset_s, 50) * 1000.0, 3) if reset_s else None,
+            "burst_only_pods_per_s": (round(bound / (elapsed - sum(reset_s)), 2)
+                                      if elapsed - sum(reset_s) > 0 else None),
+            # the lane's change log (the Python mirror of lane pods) must stay off in an
+            # all-native burst: on, every lane Binding feeds a Python copy (rank 0)
+            "lane_log_on": lane_log_on,
             "p50_latency_ms": round(percentile(lats, 50) * 1000.0, 3),
             "p99_latency_ms": round(percentile(lats, 99) * 1000.0, 3),
             "max_latency_ms": round(max(lats) * 1000.0, 3) if lats else None,

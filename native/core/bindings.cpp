@@ -645,6 +645,12 @@ PYBIND11_MODULE(_yoda_core, m) {
                out.append(py::make_tuple(c.id, c.add, c.ev ? py::cast(c.ev) : py::none(), c.node, c.cards));
              return py::make_tuple(full, out);
            })
+      .def("stop_log", &Lane::stop_log, "turn the change log off (the Python mirror was dropped)",
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("log_on", [](Lane& l) {
+        py::gil_scoped_release nogil;
+        return l.log_on();
+      })
       .def("take_e2e", &Lane::take_e2e)
       .def("take_pod_latency", &Lane::take_pod_latency)
       .def("wait_idle", &Lane::wait_idle, py::arg("timeout") = 5.0, py::call_guard<py::gil_scoped_release>())

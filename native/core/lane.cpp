@@ -969,6 +969,14 @@ void Lane::complete_runs(std::vector<std::shared_ptr<Run>>& runs) {
     for (auto& r : runs)
       if (rlog_.size() < 4096) rlog_.push_back(RunRec{r->t0, r->t_wstart, r->t_wend, now, (uint32_t)r->ids.size()});
   }
+  {
+    // a node removed (its slot maybe reused) between the engine's cycle and now: the pod's
+    // reservation went with it, and binding there would skip every filter — retry instead
+    std::lock_guard<std::recursive_mutex> lk(*emu_);
+    for (auto& r : runs)
+      for (auto& res : r->res)
+        if (res.node >= 0 && !res.stale && eng_->node_gen(res.node) != res.node_gen) res.stale = true;
+  }
   for (auto& r : runs) finish_run(*r, &binds, &tags, &fwd);
   yk::PodPort* port = port_.load();
   if (!binds.empty() && port) port->bind_native(std::move(binds), tags, o_.bind_timeout_s, this);
@@ -1013,12 +1021,19 @@ void Lane::engine_worker() {
   }
 }
 
+namespace {
+constexpr size_t kLogCap = 1u << 18;   // live entries; beyond it Python resyncs from a full snapshot
+}
+
 void Lane::log_add(const Entry& e) {
   std::lock_guard<std::mutex> g(log_mu_);
   if (!log_on_ || log_full_) return;
+  log_adds_[e.id] = log_.size();
   log_.push_back(Change{e.id, true, e.ev, e.node_name, e.cards});
-  if (log_.size() > (1u << 20)) {              // Python stopped asking: resync from scratch
+  if (log_.size() - log_dead_ > kLogCap) {     // Python stopped asking: resync from scratch
     log_.clear();
+    log_adds_.clear();
+    log_dead_ = 0;
     log_full_ = true;
   }
 }
@@ -1026,11 +1041,49 @@ void Lane::log_add(const Entry& e) {
 void Lane::log_remove(uint64_t id) {
   std::lock_guard<std::mutex> g(log_mu_);
   if (!log_on_ || log_full_) return;
+  auto it = log_adds_.find(id);
+  if (it != log_adds_.end()) {
+    // Python never saw this pod: the add and the release cancel (the event goes with them)
+    Change& c = log_[it->second];
+    c.id = 0;
+    c.ev.reset();
+    c.cards.clear();
+    c.node.clear();
+    log_adds_.erase(it);
+    ++log_dead_;
+    if (log_dead_ > 4096 && log_dead_ * 2 > log_.size()) {   // compact
+      size_t w = 0;
+      for (size_t r = 0; r < log_.size(); ++r) {
+        if (log_[r].id == 0) continue;
+        if (w != r) log_[w] = std::move(log_[r]);
+        if (log_[w].add) log_adds_[log_[w].id] = w;
+        ++w;
+      }
+      log_.resize(w);
+      log_dead_ = 0;
+    }
+    return;
+  }
   log_.push_back(Change{id, false, nullptr, std::string(), {}});
-  if (log_.size() > (1u << 20)) {
+  if (log_.size() - log_dead_ > kLogCap) {
     log_.clear();
+    log_adds_.clear();
+    log_dead_ = 0;
     log_full_ = true;
   }
+}
+
+void Lane::stop_log() {
+  std::lock_guard<std::mutex> g(log_mu_);
+  log_on_ = log_full_ = false;
+  std::vector<Change>().swap(log_);
+  log_adds_.clear();
+  log_dead_ = 0;
+}
+
+bool Lane::log_on() {
+  std::lock_guard<std::mutex> g(log_mu_);
+  return log_on_;
 }
 
 std::vector<Lane::Change> Lane::changes(bool* full) {
@@ -1038,18 +1091,27 @@ std::vector<Lane::Change> Lane::changes(bool* full) {
   {
     std::lock_guard<std::mutex> g(log_mu_);
     if (log_on_ && !log_full_) {
-      out.swap(log_);
+      out.reserve(log_.size() - log_dead_);
+      for (auto& c : log_)
+        if (c.id) out.push_back(std::move(c));
+      log_.clear();
+      log_adds_.clear();
+      log_dead_ = 0;
       *full = false;
       return out;
     }
     log_on_ = true;
     log_full_ = false;
     log_.clear();
+    log_adds_.clear();
+    log_dead_ = 0;
   }
   // full snapshot; the log (now on) records everything after it
   std::lock_guard<std::mutex> g(store_mu_);
   std::lock_guard<std::mutex> g2(log_mu_);
   log_.clear();
+  log_adds_.clear();
+  log_dead_ = 0;
   for (auto& kv : by_id_) {
     const Entry* e = kv.second;
     if (e->st == BINDING || e->st == BOUND) out.push_back(Change{e->id, true, e->ev, e->node_name, e->cards});

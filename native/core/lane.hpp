@@ -144,6 +144,9 @@ class Lane : public yk::PodSink {
   // affinity / spread / preemption plugins). The first call returns the full set and turns
   // on a change log; later calls return what changed since (add: id, event, node, cards;
   // remove: id). `full` is set when the log overflowed and the set is complete again.
+  // The log is coalesced by ledger id (a release cancels an add Python has not taken yet),
+  // so it never holds more than the live lane pods plus the releases of pods Python saw;
+  // stop_log() turns it off again (Python dropped its mirror: nothing reads it any more).
   struct Change {
     uint64_t id;
     bool add;
@@ -152,6 +155,8 @@ class Lane : public yk::PodSink {
     std::vector<int32_t> cards;
   };
   std::vector<Change> changes(bool* full);
+  void stop_log();
+  bool log_on();
 
  private:
   struct Entry {
@@ -280,6 +285,8 @@ class Lane : public yk::PodSink {
   std::mutex log_mu_;
   bool log_on_ = false, log_full_ = false;
   std::vector<Change> log_;
+  std::unordered_map<uint64_t, size_t> log_adds_;   // id → index in log_ of an add Python has not taken
+  size_t log_dead_ = 0;                             // cancelled adds (id 0) in log_
   void log_add(const Entry& e);
   void log_remove(uint64_t id);
 

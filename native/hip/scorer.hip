@@ -1967,12 +1967,13 @@ int yoda_dev_busy(void* p) {
   return busy_check(c) != 0;
 }
 
-// out[0..7]: kernel dispatches, k_batch dispatches, pods placed by k_batch, calls abandoned at
-// the host deadline, calls refused while an abandoned one drained, k_batch GPU µs (timing on),
-// stream queries made while draining and their µs, the host's wait on the last abandoned call
-int yoda_dev_counters(void* p, double* out) {
+// out[0..8] (9 values; n = the caller's buffer length, checked): kernel dispatches, k_batch
+// dispatches, pods placed by k_batch, calls abandoned at the host deadline, calls refused while
+// an abandoned one drained, k_batch GPU µs (timing on), stream queries made while draining and
+// their µs, the host's wait on the last abandoned call
+int yoda_dev_counters(void* p, double* out, int n) {
   const Ctx* c = (const Ctx*)p;
-  if (!c || !out) return -1;
+  if (!c || !out || n < 9) return -1;
   out[0] = (double)c->n_dispatch;
   out[1] = (double)c->n_kbatch;
   out[2] = (double)c->n_kbatch_pods;

@@ -607,6 +607,26 @@ def test_bench_node_gpus_sweep_option():
     assert d["pods_bound"] + d["pods_unschedulable"] == 1000
 
 
+def test_bench_headline_reset_stays_small_and_mirror_off():
+    """Guard of the driver's headline: the driver's command on config 3
+    binds every pod, the lane's change log (the Python mirror of lane pods) never switches on
+    in an all-native burst, and the reset between bursts (deleting the previous burst and
+    waiting for the releases, inside the timed step) stays well below the burst itself.
+    Syncing the mirror from the reset loop broke all three in round 3 (≈30 % of the headline)."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--alt", "none"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["pods_bound"] == 3000 and d["pods_unschedulable"] == 0
+    assert d["lane_log_on"] is False
+    bursts = sorted(s - rs for s, rs in zip(d["step_ms"], d["reset_ms"]))
+    assert d["reset_ms_median"] <= 0.5 * bursts[len(bursts) // 2], (d["reset_ms"], d["step_ms"])
+    assert d["burst_only_pods_per_s"] >= d["value"]
+    # the engine's share of a lane pod stays a small part of the scheduler's CPU per pod
+    assert d["lane_engine_us_per_pod"]["cpu"] <= 0.5 * d["cpu_us_per_pod"]
+
+
 def test_bench_nodes_option_resizes_config_6_only():
     """``--nodes`` (the CPU/device crossover end to end) resizes config 6's cluster and is
     refused for the BASELINE configs, whose cluster shapes are fixed by BASELINE.json."""

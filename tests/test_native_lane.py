@@ -357,3 +357,121 @@ def test_watch_read_sliced_to_one_recv_per_turn_keeps_the_lane_exact():
                         f"{__file__}::test_lane_burst_confirms_echoes_and_releases_on_delete"],
                        env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_mirror_settles_off_and_the_change_log_coalesces():
+    """A Python-path pod (topology spread) mirrors the lane's pods into the cache and turns the
+    lane's change log on; lane pods bound and deleted before the next Python cycle cancel out
+    in the log (it never holds deleted pods' events), and once no Python cycle has
+    read the mirror for ``laneMirrorSettleSeconds`` the mirror is dropped and the log is off."""
+    async def go():
+        cfg = yoda_config(extra_filter=["PodTopologySpread"])
+        cfg.setdefault("yodaRuntime", {})["laneMirrorSettleSeconds"] = 0.3
+        async with Env(cfg=cfg) as e:
+            lane, cache = e.sched.lane.lane, e.sched.cache
+            await e.create(pod("w0", {"app": "web", "scv/memory": "1000"}))
+            assert await e.wait(lambda: e.sched.scheduled == 1)
+            assert not lane.log_on
+            spread = pod("s0", {"app": "web", "scv/memory": "1000"},
+                         topologySpreadConstraints=[{"maxSkew": 1, "topologyKey": "kubernetes.io/hostname",
+                                                     "whenUnsatisfiable": "DoNotSchedule",
+                                                     "labelSelector": {"matchLabels": {"app": "web"}}}])
+            await e.create(spread)
+            assert await e.wait(lambda: e.sched.scheduled == 2)
+            on_after_python = lane.log_on
+            mirrored = cache.lane_mirrored()
+            # 20 lane pods bound and deleted with no Python cycle in between: adds and releases cancel
+            for i in range(20):
+                await e.create(pod(f"t{i}", {"scv/memory": "1000"}))
+            assert await e.wait(lambda: e.sched.scheduled == 22)
+            for i in range(20):
+                await e.cl.delete("pods", f"t{i}", "default")
+            assert await e.wait(lambda: lane.stats()["owned"] == 1)
+            full, changes = lane.changes()
+            pending = len(changes)
+            settled = await e.wait(lambda: not lane.log_on, 3.0)
+            return on_after_python, mirrored, full, pending, settled, cache.lane_mirrored(), cache.python_pods()
+    on, mirrored, full, pending, settled, left, py = run(go())
+    assert on and mirrored == 1
+    assert not full and pending == 0
+    assert settled and left == 0 and py == 1
+
+
+class _Ev:
+    """A stand-in for a native PodEvent whose projection is unavailable (from_native decodes raw())."""
+
+    def __init__(self, obj):
+        import json
+        self._raw = json.dumps(obj)
+
+    def info_args(self):
+        return None
+
+    def raw(self):
+        return self._raw
+
+
+class _ScriptedLane:
+    """changes()/stop_log() of core.Lane, driven by the test."""
+
+    def __init__(self):
+        self.live, self.log, self.on = {}, [], False
+
+    def changes(self):
+        if not self.on:
+            self.on, self.log = True, []
+            return True, [(lid, True, ev, node, cards) for lid, (ev, node, cards) in self.live.items()]
+        out, self.log = self.log, []
+        return False, out
+
+    def stop_log(self):
+        self.on, self.log = False, []
+
+    def bind(self, lid, ev, node, cards):
+        self.live[lid] = (ev, node, cards)
+        if self.on:
+            self.log.append((lid, True, ev, node, cards))
+
+    def release(self, lid):
+        self.live.pop(lid)
+        if self.on:
+            self.log.append((lid, False, None, "", []))
+
+
+def test_sync_lane_never_drops_a_pod_python_took_over():
+    """ADVICE r3 (cache.py:300): a lane pod is mirrored, its Binding fails and Python takes it
+    over and assumes it; the lane's stale release must not untrack Python's state, so deleting
+    the pod later still frees its reservation (the ledger ends empty)."""
+    from yoda_scheduler_amd.models.pod import PodInfo
+    from yoda_scheduler_amd.testing import FakeCluster
+
+    async def go():
+        c = FakeCluster()
+        c.add_node("n1")
+        await c.start()
+        s, cache = c.sched, c.sched.cache
+        fake = _ScriptedLane()
+        cache.lane = fake
+        obj = {"metadata": {"name": "p", "namespace": "default", "uid": "uid-p", "labels": {"scv/memory": "1000"}},
+               "spec": {"schedulerName": "nobody", "containers": [{"name": "c"}]}}
+        lid = (1 << 62) + 7
+        fake.bind(lid, _Ev(obj), "n1", [0])
+        cache.sync_lane()
+        assert cache.pods["uid-p"].lane and cache.lane_mirrored() == 1
+        fake.release(lid)                                   # the Binding failed: the lane lets go
+        pi = PodInfo.from_obj(obj)
+        assert cache.assume(pi, "n1", [0])                  # Python's retry assumes it
+        cache.sync_lane()                                   # the lane's release arrives late
+        kept = "uid-p" in cache.pods and not cache.pods["uid-p"].lane
+        ledger_mid = s.engine.ledger_size
+        cache.remove_pod("uid-p")                           # the pod is deleted
+        out = kept, ledger_mid, s.engine.ledger_size, cache.python_pods()
+        # a lane mirror that settles off leaves Python-owned pods alone
+        fake.bind(lid + 1, _Ev(dict(obj, metadata=dict(obj["metadata"], name="q", uid="uid-q"))), "n1", [1])
+        cache.sync_lane()
+        n = cache.drop_lane_mirror()
+        await c.stop()
+        return out + (n, fake.on, len(cache.pods))
+    kept, mid, end, py, dropped, on, left = run(go())
+    assert kept and mid == 1 and end == 0 and py == 0
+    assert dropped == 1 and not on and left == 0

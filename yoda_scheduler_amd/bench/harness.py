@@ -278,10 +278,11 @@ class HttpShard:
                 # woken by the lane when its last pod is released (an asyncio sleep shorter than
                 # a millisecond still waits for epoll's 1 ms tick when nothing else wakes the loop)
                 await sched.lane.wait_unowned(60.0)
-            # the cache mirrors lane pods only while Python plugins read them (sync_lane runs
-            # before a Python cycle): bring the mirror up to date before reading it
-            while sched.cache.sync_lane() >= 0 and (sched.cache.pods or q._active_entries or sched.pending_binds
-                                                   or sched.lane_owned()):
+            # the pods the Python side owns (a mirror of lane pods does not count: the lane's own
+            # count covers them, and syncing the mirror here would switch the lane's change log
+            # on and charge a Python copy of every lane pod to each timed step)
+            while (sched.cache.python_pods() or q._active_entries or sched.pending_binds
+                   or sched.lane_owned()):
                 if trace is not None:
                     trace.append((round((time.perf_counter() - tr) * 1e3, 3), sched.lane_owned(), len(sched.cache.pods),
                                   len(q._active_entries), sched.pending_binds))

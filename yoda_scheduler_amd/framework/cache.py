@@ -59,6 +59,7 @@ class SchedulerCache:
         self.lane = None                         # native lane (core.Lane) whose reserved pods sync_lane mirrors
         self.on_anti_change = None               # called when the set of required-anti-affinity pods changes
         self._lane_uids: dict[int, str] = {}     # lane ledger id → uid of the mirrored pod
+        self.lane_synced_at: Optional[float] = None   # clock() of the last sync_lane
 
     # ------------------------------------------------------------------ nodes
     def _index_node(self, info: NodeInfo, sign: int) -> None:
@@ -306,27 +307,66 @@ class SchedulerCache:
         lane = self.lane
         if lane is None:
             return 0
+        self.lane_synced_at = self.clock()
         full, changes = lane.changes()
         if full:
             for uid in list(self._lane_uids.values()):
-                self._untrack(uid)
+                self._untrack_lane(uid)
             self._lane_uids.clear()
         for lid, add, ev, node, cards in changes:
             if add:
                 old = self._lane_uids.pop(lid, None)
                 if old is not None:
-                    self._untrack(old)
+                    self._untrack_lane(old)
                 pi = PodInfo.from_native(ev)
+                cur = self.pods.get(pi.uid)
+                if cur is not None and not cur.lane:
+                    continue        # Python's own state of the pod (it took the pod over) wins
                 pi.num_id = lid
                 self._track(PodState(pi, node, list(cards), False, lane=True))
                 self._lane_uids[lid] = pi.uid
             else:
                 uid = self._lane_uids.pop(lid, None)
                 if uid is not None:
-                    self._untrack(uid)
+                    self._untrack_lane(uid)
         if changes or full:
             self.generation += 1
         return len(changes)
+
+    def drop_lane_mirror(self) -> int:
+        """Forget every mirrored lane pod and turn the lane's change log off: no Python-path
+        cycle has read the mirror for a while, so lane Bindings stop paying for it (the next
+        Python cycle resyncs from a full snapshot). Returns the number of pods dropped."""
+        n = 0
+        for uid in list(self._lane_uids.values()):
+            n += self._untrack_lane(uid)
+        self._lane_uids.clear()
+        if self.lane is not None:
+            self.lane.stop_log()
+        if n:
+            self.generation += 1
+        return n
+
+    def lane_mirrored(self) -> int:
+        """Pods in ``pods`` that are mirrors of lane pods (not Python-owned)."""
+        n = 0
+        for uid in self._lane_uids.values():
+            ps = self.pods.get(uid)
+            n += ps is not None and ps.lane
+        return n
+
+    def python_pods(self) -> int:
+        """Bound/assumed pods the Python side owns (lane mirrors excluded)."""
+        return len(self.pods) - self.lane_mirrored()
+
+    def _untrack_lane(self, uid: str) -> bool:
+        """Drop a lane mirror; a PodState the Python side owns under that uid (it took the pod
+        over after a failed lane Binding) is left alone."""
+        ps = self.pods.get(uid)
+        if ps is None or not ps.lane:
+            return False
+        self._untrack(uid)
+        return True
 
     def _untrack(self, uid: str) -> None:
         ps = self.pods.pop(uid, None)

@@ -138,6 +138,10 @@ class SchedulerConfig:
     # placed, bound, confirmed and released in C++ (native/core/lane.hpp) with no Python call
     # per pod; auto = on whenever the native Kubernetes transport is in use
     native_lane: str = "auto"
+    # yodaRuntime.laneMirrorSettleSeconds: the Python cache mirrors lane pods for Python
+    # plugins that read other pods (affinity, spread, preemption); once no Python-path cycle
+    # has read the mirror for this long it is dropped and the lane's change log turned off
+    lane_mirror_settle_s: float = 5.0
     # event API (yodaRuntime.eventsAPI): upstream v1.20 records through events.k8s.io/v1
     events_api: str = "events.k8s.io/v1"
     trace: bool = False
@@ -303,6 +307,9 @@ def parse_config(doc: dict) -> SchedulerConfig:
     cfg.native_lane = {True: "on", False: "off"}.get(nl, str(nl).lower()) if isinstance(nl, bool) else str(nl).lower()
     if cfg.native_lane not in ("auto", "on", "off"):
         raise ValueError("yodaRuntime.nativeLane must be auto|on|off")
+    cfg.lane_mirror_settle_s = float(_f(rt, "laneMirrorSettleSeconds", cfg.lane_mirror_settle_s))
+    if cfg.lane_mirror_settle_s < 0:
+        raise ValueError("yodaRuntime.laneMirrorSettleSeconds must be >= 0")
     if not 2 <= cfg.overlap_depth <= 16:
         raise ValueError("yodaRuntime.overlapDepth must be in [2, 16]")
     cfg.trace = bool(_f(rt, "trace", False))

@@ -218,10 +218,12 @@ class NativeLane:
     @contextlib.contextmanager
     def held(self):
         """The cache mirrors the lane's reserved pods and the lane thread is parked: Python
-        plugins may read other pods and run ledger what-ifs (preemption) safely."""
-        self.s.cache.sync_lane()
+        plugins may read other pods and run ledger what-ifs (preemption) safely. The lane is
+        parked first and mirrored second: a pod it placed in between would otherwise be
+        missing from the mirror for the whole hold."""
         self.lane.pause(True)
         try:
+            self.s.cache.sync_lane()
             yield
         finally:
             self.lane.pause(False)

@@ -219,6 +219,19 @@ class Scheduler:
         if self.lane is not None:
             self.lane.refresh()
 
+    def _settle_lane_mirror(self) -> bool:
+        """Drop the cache's mirror of lane pods (and the lane's change log with it) once no
+        Python-path cycle has read it for ``laneMirrorSettleSeconds``: a burst with a few
+        affinity pods must not make every later lane Binding feed a Python mirror."""
+        c = self.cache
+        if self.lane is None or c.lane_synced_at is None or self._lane_held:
+            return False
+        if c.clock() - c.lane_synced_at < self.config.lane_mirror_settle_s:
+            return False
+        c.drop_lane_mirror()
+        c.lane_synced_at = None
+        return True
+
     def _lane_cards(self, name: str) -> None:
         """The per-card device identities a lane Binding's annotations name (plugins.defaults
         .visible_device_ids), pushed whenever the node's Scv changes."""
@@ -548,8 +561,16 @@ class Scheduler:
         fw = self.frameworks.get(pi.scheduler_name)
         if fw is None or self._pod_gone(pi):
             return
-        if self.lane is not None and not fw.native_for(pi):
-            self.cache.sync_lane()               # Python plugins read other pods, lane pods included
+        if self.lane is not None and not fw.native_for(pi) and not self._lane_held:
+            # Python plugins read other pods, lane pods included: the lane is parked and its
+            # pods mirrored for the whole cycle (upstream scheduleOne is serial), so no lane pod
+            # can be placed between the mirror and this pod's assume unseen by its filters
+            self._lane_held = True
+            try:
+                with self.lane.held():
+                    return self.schedule_one(pi)
+            finally:
+                self._lane_held = False
         self._clear_nominations_for((pi,))       # the preemptor competes with its own hold gone
         self._activate(fw)
         cycle = self.queue.scheduling_cycle
@@ -1204,6 +1225,7 @@ class Scheduler:
                     self._clear_nomination(uid)
             self._maybe_enable_device()
             self._lane_refresh()                 # cluster gates (services, images, anti-affinity)
+            self._settle_lane_mirror()
             refresh = getattr(self.client, "_refresh_token", None)
             if refresh is not None:
                 refresh()                        # rotated service-account tokens

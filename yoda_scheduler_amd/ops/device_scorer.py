@@ -20,7 +20,7 @@ def declare(lib: ctypes.CDLL) -> None:
     lib.yoda_dev_last_us.restype = ctypes.c_float
     lib.yoda_dev_batch_trace.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
     lib.yoda_dev_batch_trace.restype = ctypes.c_int
-    lib.yoda_dev_counters.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.yoda_dev_counters.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     lib.yoda_dev_counters.restype = ctypes.c_int
 
 
@@ -71,7 +71,7 @@ def counters(engine) -> dict:
     lib = hip_lib()
     declare(lib)
     buf = (ctypes.c_double * len(COUNTERS))()
-    if lib.yoda_dev_counters(engine.device_ctx, buf) != 0:
+    if lib.yoda_dev_counters(engine.device_ctx, buf, len(COUNTERS)) != 0:
         raise RuntimeError("yoda_dev_counters failed (device scorer not enabled?)")
     return {k: (buf[i] if k.endswith("_us") else int(buf[i])) for i, k in enumerate(COUNTERS)}
 
