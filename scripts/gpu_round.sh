@@ -34,6 +34,31 @@ for s in $STEPS; do
     prof) step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     kbprof) step kbprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kbprof -o kb -- python3 scripts/device_batch_bench.py --nodes 4096 --pods 1032 --batch 256 --modes batch ;;
     kbtrace) step kbtrace 300 python scripts/device_batch_bench.py --nodes 4096,16384 --pods 1032 --batch 256 --modes batch --trace ;;
+    ab3)   # same-box A/B of the driver's command: this tree vs round 3's (ab_r3/, git worktree of 809b08c)
+      mkdir -p gpurun_out/ab3
+      for k in 1 2; do
+        step "ab3/new_$k" 300 python bench.py --gpus 1 --steps 20 --warmup 5 --alt none
+        (cd ab_r3 && timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --alt none) \
+          > "gpurun_out/ab3/r3_$k.log" 2>&1 || { echo "r3 run rc=$?"; exit 1; }
+      done ;;
+    counters) rocprofv3 -L > gpurun_out/rocprof_counters.txt 2>&1 || true ;;
+    pmc4)  # k_batch PMC on the kept kernel at 256 / 1024 / 4096 nodes, one pass per counter group
+      mkdir -p gpurun_out/pmc4
+      for n in 256 1024 4096; do
+        step "pmc4/p1_$n" 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU \
+          SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY --kernel-trace --stats --output-format csv -d gpurun_out/pmc4/p1_$n -o k \
+          -- python3 scripts/device_batch_bench.py --nodes $n --modes batch --busy 0.3 --pods 264 --batch 256
+      done
+      for n in 256 1024 4096; do
+        step "pmc4/p2_$n" 90 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT \
+          SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH --kernel-trace --stats --output-format csv -d gpurun_out/pmc4/p2_$n -o k \
+          -- python3 scripts/device_batch_bench.py --nodes $n --modes batch --busy 0.3 --pods 264 --batch 256
+      done ;;
+    hiptrace6)  # HIP/HSA API census of config 6 (device scorer on): calls per pod, by API
+      step hiptrace6 300 rocprofv3 --hip-trace --hsa-trace --stats --output-format csv -d gpurun_out/hiptrace6 -o c6 \
+        -- python3 bench.py --config 6 --steps 3 --warmup 1 --alt none
+      python scripts/api_census.py gpurun_out/hiptrace6 > gpurun_out/hiptrace6_census.txt 2>&1 || true ;;
+    threads6) step threads6 300 env YODA_BENCH_THREADS=1 python bench.py --config 6 --steps 5 --warmup 1 --alt none ;;
     all)   # every BASELINE config (+ 6) on this box, one JSON line each under gpurun_out/all/
       mkdir -p gpurun_out/all
       for spec in "c3|--config 3 --steps 20 --warmup 5" "c1|--config 1 --steps 20 --warmup 2" \

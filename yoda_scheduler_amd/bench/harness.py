@@ -281,8 +281,10 @@ class HttpShard:
             # the pods the Python side owns (a mirror of lane pods does not count: the lane's own
             # count covers them, and syncing the mirror here would switch the lane's change log
             # on and charge a Python copy of every lane pod to each timed step)
-            while (sched.cache.python_pods() or q._active_entries or sched.pending_binds
-                   or sched.lane_owned()):
+            # (YODA_BENCH_RESET_SYNC=1 restores round 3's sync in this loop: same-box A/B only)
+            old_sync = os.environ.get("YODA_BENCH_RESET_SYNC") == "1"
+            while ((old_sync and sched.cache.sync_lane() >= 0 and sched.cache.pods) or sched.cache.python_pods()
+                   or q._active_entries or sched.pending_binds or sched.lane_owned()):
                 if trace is not None:
                     trace.append((round((time.perf_counter() - tr) * 1e3, 3), sched.lane_owned(), len(sched.cache.pods),
                                   len(q._active_entries), sched.pending_binds))
