@@ -498,8 +498,12 @@ PYBIND11_MODULE(_yoda_core, m) {
   py::class_<Lane>(m, "Lane")
       .def(py::init([](Engine& e, int batch, double bind_timeout, int sort_kind, bool events, bool events_v1,
                        double event_qps, int event_burst, int event_buffer, const std::string& host,
-                       const std::string& name_prefix, int async_mode, int engine_delay_us, int spin_us) {
+                       const std::string& name_prefix, int async_mode, int engine_delay_us, int spin_us,
+                       double initial_backoff, double max_backoff, double unschedulable_flush) {
              LaneOptions o;
+             o.initial_backoff_s = initial_backoff;
+             o.max_backoff_s = max_backoff;
+             o.unsched_flush_s = unschedulable_flush;
              o.async_mode = async_mode;
              o.engine_delay_us = engine_delay_us;
              o.spin_us = spin_us;
@@ -519,13 +523,16 @@ PYBIND11_MODULE(_yoda_core, m) {
            py::arg("events") = true, py::arg("events_v1") = true, py::arg("event_qps") = 50.0,
            py::arg("event_burst") = 300, py::arg("event_buffer") = 1000, py::arg("host") = "localhost",
            py::arg("name_prefix") = "00000000", py::arg("async_mode") = 1,
-           py::arg("engine_delay_us") = 0, py::arg("spin_us") = 0, py::keep_alive<1, 2>())
+           py::arg("engine_delay_us") = 0, py::arg("spin_us") = 0, py::arg("initial_backoff") = 1.0,
+           py::arg("max_backoff") = 10.0, py::arg("unschedulable_flush") = 60.0, py::keep_alive<1, 2>())
       .def("sink_ptr", [](Lane& l) { return (uintptr_t) static_cast<yk::PodSink*>(&l); })
       .def("set_port", [](Lane& l, uintptr_t p) { l.set_port(reinterpret_cast<yk::PodPort*>(p)); })
       // the profile's engine configuration is the engine's current one (the caller applied it)
       .def("set_profile",
-           [](Lane& l, Engine& e, const std::string& name, bool enabled, int flag_mask, bool annotate) {
+           [](Lane& l, Engine& e, const std::string& name, bool enabled, int flag_mask, bool annotate,
+              int64_t preempt_above) {
              Lane::Profile p;
+             p.preempt_above = preempt_above;
              p.name = name;
              p.enabled = enabled;
              p.flag_mask = flag_mask;
@@ -536,13 +543,16 @@ PYBIND11_MODULE(_yoda_core, m) {
              }
              l.set_profile(p);
            },
-           py::arg("engine"), py::arg("name"), py::arg("enabled"), py::arg("flag_mask"), py::arg("annotate"))
+           py::arg("engine"), py::arg("name"), py::arg("enabled"), py::arg("flag_mask"), py::arg("annotate"),
+           py::arg("preempt_above") = INT64_MIN)
       .def("set_active", &Lane::set_active)
+      .def("move", &Lane::move, py::arg("node") = -1,
+           "move request: -1 moves every parked lane pod; a node index is a queueing hint for that node")
       .def("set_node_cards", &Lane::set_node_cards, py::arg("node"), py::arg("vis"))
       .def("remove_node_cards", &Lane::remove_node_cards)
       .def("fileno", &Lane::fileno)
       // ([(type, PodEvent, old PodEvent | None)], [handoff], moves)
-      // handoff = (kind, PodEvent, profile, cycle tuple, status, message, t_enqueue, t_cycle)
+      // handoff = (kind, PodEvent, profile, cycle tuple, status, message, t_enqueue, t_cycle, attempts)
       .def("drain",
            [](Lane& l) {
              std::vector<Lane::Fwd> fwd;
@@ -557,7 +567,7 @@ PYBIND11_MODULE(_yoda_core, m) {
              py::list h;
              for (auto& x : hand)
                h.append(py::make_tuple(x.kind, py::cast(x.ev), x.profile, cycle_tuple(x.res), x.status,
-                                       py::bytes(x.msg), x.t_enqueue, x.t_cycle));
+                                       py::bytes(x.msg), x.t_enqueue, x.t_cycle, x.attempts));
              return py::make_tuple(f, h, moves);
            })
       .def("relist",
@@ -611,6 +621,13 @@ PYBIND11_MODULE(_yoda_core, m) {
              d["inflight"] = s.inflight;
              d["binding"] = s.binding;
              d["owned"] = s.owned;
+             d["parked"] = s.parked;
+             d["backoff"] = s.backoff;
+             d["native_failed"] = s.native_failed;
+             d["moved"] = s.moved;
+             d["retried"] = s.retried;
+             d["status_patches"] = s.status_patches;
+             d["status_patch_errors"] = s.status_patch_errors;
              d["engine_s"] = s.engine_s;
              d["left_in_flight"] = s.left_in_flight;
              d["engine_pods"] = s.engine_pods;

@@ -16,6 +16,28 @@ namespace yoda {
 namespace {
 
 constexpr uint64_t kEventTag = 1ull << 63;
+constexpr uint64_t kPatchBit = 1ull << 62;   // with kEventTag: a PodScheduled=False status patch
+
+// engine Reason → FitError text (framework/scheduler.py::_fit_error)
+const char* const kReasonName[RS_NUM] = {"OK", "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity",
+                                         "NodeResourcesFit", "NoScv", "ScvStale", "GpuNumber", "GpuMemory",
+                                         "GpuClock", "GpuFit", "NodeGone"};
+const char* reason_text(int i) {
+  switch (i) {
+    case RS_UNSCHEDULABLE: return "node(s) were unschedulable";
+    case RS_NODE_NAME: return "node(s) didn't match the requested node name";
+    case RS_TAINT: return "node(s) had taints that the pod didn't tolerate";
+    case RS_AFFINITY: return "node(s) didn't match node selector";
+    case RS_RESOURCES: return "Insufficient cpu/memory/pods";
+    case RS_NO_SCV: return "node(s) have no Scv telemetry";
+    case RS_STALE: return "node(s) have stale Scv telemetry";
+    case RS_GPU_NUMBER: return "node(s) have too few GPUs";
+    case RS_GPU_MEMORY: return "node(s) have too few GPUs with enough free HBM";
+    case RS_GPU_CLOCK: return "node(s) have too few GPUs with the requested clock";
+    case RS_GPU_FIT: return "node(s) have too few healthy GPUs matching scv/memory+scv/clock";
+    default: return i >= 0 && i < RS_NUM ? kReasonName[i] : "unknown";
+  }
+}
 
 // Go strconv.Atoi: optional sign, decimal digits only, int64 range (utils/gonum.py::atoi).
 bool go_atoi(const std::string& s, int64_t* out) {
@@ -209,6 +231,15 @@ void Lane::set_profile(const Profile& p) {
 void Lane::set_active(bool on) {
   std::lock_guard<std::mutex> g(in_mu_);
   active_.store(on);
+  in_cv_.notify_one();
+}
+
+void Lane::move(int32_t node) {
+  std::lock_guard<std::mutex> g(in_mu_);
+  Item it;
+  it.k = Item::kMove;
+  it.status = node;
+  push_locked(std::move(it));
   in_cv_.notify_one();
 }
 
@@ -464,7 +495,8 @@ void Lane::handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::ve
   }
   // lane-owned
   if (p.node.empty()) {
-    if (e->st == QUEUED && ev->full().spec_meta_hash != old->full().spec_meta_hash) {
+    const bool waiting = e->st == PARKED || e->st == BACKOFF;
+    if ((e->st == QUEUED || waiting) && ev->full().spec_meta_hash != old->full().spec_meta_hash) {
       int prof = -1;
       if (!admissible(ev->full(), &prof)) {
         // no longer for the lane (a feature a Python plugin handles, another scheduler, ...)
@@ -475,7 +507,13 @@ void Lane::handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::ve
       }
       e->prof = prof;
       const int64_t pr = prio_of(ev->full());
-      if (pr != e->prio) {                 // re-sorted, FIFO position kept (activeQ.Update)
+      if (waiting) {
+        // an update may make an unschedulable pod schedulable: retry now (queue.update)
+        e->prio = pr;
+        e->req.reset();
+        if (e->st == PARKED) parked_.erase(e->id);
+        activate(e);
+      } else if (pr != e->prio) {          // re-sorted, FIFO position kept (activeQ.Update)
         e->prio = pr;
         heap_.push(QItem{e->prio, e->seq, e->id});
       }
@@ -517,6 +555,8 @@ void Lane::count(St s, int d) {
   std::lock_guard<std::mutex> g(stat_mu_);
   if (s == QUEUED) st_.queued += d;
   else if (s == INFLIGHT) st_.inflight += d;
+  else if (s == PARKED) st_.parked += d;
+  else if (s == BACKOFF) st_.backoff += d;
   if (s != PY) st_.owned += d;
 }
 
@@ -537,6 +577,8 @@ void Lane::set_state(Entry* e, St s) {
 // a lane-owned entry becomes a Python (store-only) entry; `release` drops its reservation
 void Lane::drop_owned(Entry* e, bool release) {
   bind_settled(e);
+  if (e->st == PARKED) parked_.erase(e->id);      // a BACKOFF heap item goes stale by itself
+  e->req.reset();
   if (release && e->id) {
     to_release_.push_back(e->id);
     log_remove(e->id);
@@ -552,8 +594,14 @@ void Lane::drop_owned(Entry* e, bool release) {
 void Lane::handle_answer(uint64_t tag, int status, std::string& body, double t_ack) {
   if (tag & kEventTag) {
     std::lock_guard<std::mutex> g(stat_mu_);
-    if (status >= 200 && status < 300) st_.events_written++;
-    else st_.event_errors++;
+    const bool ok = status >= 200 && status < 300;
+    if (tag & kPatchBit) {
+      if (!ok) st_.status_patch_errors++;
+    } else if (ok) {
+      st_.events_written++;
+    } else {
+      st_.event_errors++;
+    }
     return;
   }
   auto it = by_id_.find(tag);
@@ -599,6 +647,7 @@ void Lane::handle_answer(uint64_t tag, int status, std::string& body, double t_a
   h.msg = std::move(body);
   h.t_enqueue = e->t_enq;
   h.t_cycle = e->t_cycle;
+  h.attempts = std::max<uint32_t>(1, e->attempts);
   drop_owned(e, true);
   hand_pending_.push_back(std::move(h));
 }
@@ -629,10 +678,14 @@ void Lane::apply_profiles(std::vector<Fwd>* out) {
   std::vector<Entry*> evict;
   for (auto& kv : by_id_) {
     Entry* e = kv.second;
-    if (e->st != QUEUED) continue;
+    if (e->st != QUEUED && e->st != PARKED && e->st != BACKOFF) continue;
     int prof = -1;
-    if (!admissible(e->ev->full(), &prof)) evict.push_back(e);
-    else e->prof = prof;
+    // a waiting pod whose profile now has a PostFilter that may help it goes to Python too
+    if (!admissible(e->ev->full(), &prof) ||
+        (e->st != QUEUED && e->ev->full().priority > lp_[prof].preempt_above))
+      evict.push_back(e);
+    else
+      e->prof = prof;
   }
   for (Entry* e : evict) {
     drop_owned(e, false);
@@ -848,6 +901,12 @@ void Lane::finish_run(Run& r, std::vector<yk::BindSpec>* binds, std::vector<uint
       continue;
     }
     if (res.node < 0) {
+      if (e->ev->full().priority <= pr.preempt_above) {
+        // no PostFilter can help: FitError, event, condition and queueing stay native
+        e->req = std::make_shared<PodReq>(r.reqs[k]);
+        fail_native(e, pr, res, q < r.hinted.size() && r.hinted[q]);
+        continue;
+      }
       Handoff h;
       h.kind = Handoff::kUnschedulable;
       h.ev = e->ev;
@@ -855,6 +914,7 @@ void Lane::finish_run(Run& r, std::vector<yk::BindSpec>* binds, std::vector<uint
       h.res = res;
       h.t_enqueue = e->t_enq;
       h.t_cycle = r.t0;
+      h.attempts = std::max<uint32_t>(1, e->attempts);
       drop_owned(e, false);
       hand_pending_.push_back(std::move(h));
       std::lock_guard<std::mutex> g2(stat_mu_);
@@ -899,6 +959,8 @@ void Lane::schedule_some() {
       Entry* e = it->second;
       if (e->st != QUEUED || e->seq != q.seq || e->prio != q.prio) continue;   // stale heap item
       set_state(e, INFLIGHT);
+      e->attempts++;
+      e->cycle = ++cycle_;
       picked.push_back(e);
     }
   }
@@ -915,6 +977,7 @@ void Lane::schedule_some() {
     for (; i < picked.size() && picked[i]->prof == r->prof; ++i) {
       r->ids.push_back(picked[i]->id);
       r->evs.push_back(picked[i]->ev);
+      r->cycles.push_back(picked[i]->cycle);
     }
     runs.push_back(std::move(r));
   }
@@ -976,6 +1039,25 @@ void Lane::complete_runs(std::vector<std::shared_ptr<Run>>& runs) {
     for (auto& r : runs)
       for (auto& res : r->res)
         if (res.node >= 0 && !res.stale && eng_->node_gen(res.node) != res.node_gen) res.stale = true;
+    // unschedulable pods: did a node hint since their cycle make them fit there? (upstream's
+    // in-flight events + QueueingHint: such a pod retries from backoff instead of parking)
+    if (!hints_.empty()) {
+      const EngineConfig saved = eng_->config();
+      for (auto& r : runs) {
+        r->hinted.assign(r->res.size(), 0);
+        bool set = false;
+        for (size_t q = 0; q < r->res.size(); ++q) {
+          if (r->res[q].node >= 0 || r->res[q].stale) continue;
+          if (!set) {
+            eng_->set_config(r->cfg);
+            set = true;
+          }
+          const size_t k = r->slot[q];
+          r->hinted[q] = hinted_since(r->cycles[k], r->reqs[k]);
+        }
+      }
+      eng_->set_config(saved);
+    }
   }
   for (auto& r : runs) finish_run(*r, &binds, &tags, &fwd);
   yk::PodPort* port = port_.load();
@@ -1145,6 +1227,197 @@ void Lane::pause(bool on) {
   if (on) idle_cv_.wait(lk, [&] { return (!busy_ && !run_inflight_) || stop_.load(); });
 }
 
+// ------------------------------------------------------------------ native unschedulable path
+// (lane thread). upstream's FitError → FailedScheduling event → PodScheduled=False condition →
+// AddUnschedulableIfNotPresent: unschedulableQ, or podBackoffQ when a move request arrived since
+// the pod's cycle began (moveRequestCycle) or a node hint since then makes it fit.
+
+std::string Lane::fit_error(const CycleResult& r) const {
+  std::vector<std::string> parts;
+  for (int i = 1; i < (int)r.reason_counts.size() && i < RS_NUM; ++i)
+    if (r.reason_counts[i]) parts.push_back(std::to_string(r.reason_counts[i]) + " " + reason_text(i));
+  std::sort(parts.begin(), parts.end());
+  std::string m = "0/" + std::to_string(r.evaluated) + " nodes are available: ";
+  for (size_t i = 0; i < parts.size(); ++i) {
+    if (i) m += ", ";
+    m += parts[i];
+  }
+  m += ".";
+  return m;
+}
+
+double Lane::backoff_of(const Entry& e) const {
+  // podInitialBackoffSeconds × 2^(attempts−1), capped at podMaxBackoffSeconds (queue.py)
+  double d = o_.initial_backoff_s;
+  for (uint32_t a = 1; a < e.attempts && d < o_.max_backoff_s; ++a) d *= 2;
+  return std::min(d, o_.max_backoff_s);
+}
+
+void Lane::activate(Entry* e) {
+  set_state(e, QUEUED);
+  e->seq = ++seq_;
+  heap_.push(QItem{e->prio, e->seq, e->id});
+}
+
+void Lane::to_backoff(Entry* e, double until) {
+  set_state(e, BACKOFF);
+  e->bseq = ++bseq_;
+  bheap_.push(BItem{until, e->bseq, e->id});
+}
+
+// a waiting pod moved by a cluster event: backoffQ while its backoff runs, else activeQ
+void Lane::route(Entry* e, double now) {
+  const double b = backoff_of(*e);
+  if (now - e->t_fail < b) to_backoff(e, e->t_fail + b);
+  else activate(e);
+}
+
+void Lane::patch_condition(const Entry& e, const std::string& msg) {
+  yk::PodPort* port = port_.load();
+  if (!port) return;
+  std::string b;
+  b.reserve(160 + msg.size());
+  b += "{\"status\":{\"conditions\":[{\"type\":\"PodScheduled\",\"status\":\"False\",\"reason\":\"Unschedulable\","
+       "\"message\":";
+  json_str(msg, b);
+  b += "}]}}";
+  const std::string path = "/api/v1/namespaces/" + e.ev->p.ns + "/pods/" + e.ev->p.name + "/status";
+  static std::atomic<uint64_t> seq{0};
+  port->request_native("PATCH", path, std::move(b), true, 30.0, kEventTag | kPatchBit | (++seq & 0xffffffffull), this);
+  std::lock_guard<std::mutex> g(stat_mu_);
+  st_.status_patches++;
+}
+
+void Lane::fail_native(Entry* e, const Profile& pr, const CycleResult& res, bool hinted) {
+  const double now = mono();
+  e->t_fail = now;
+  const std::string msg = fit_error(res);
+  {
+    std::lock_guard<std::mutex> g(stat_mu_);
+    st_.unschedulable++;
+    st_.native_failed++;
+    if (o_.events) {
+      st_.events_recorded++;
+      if ((int)ev_q_.size() >= o_.event_buffer) st_.events_dropped++;
+      else ev_q_.push_back(PendingEvent{e->ev->p.ns, e->ev->p.name, e->ev->p.uid, std::string(), pr.name, wall(),
+                                        msg.substr(0, 1024)});
+    }
+  }
+  patch_condition(*e, msg);
+  if (move_cycle_ >= (int64_t)e->cycle || hinted) {
+    to_backoff(e, now + backoff_of(*e));
+  } else {
+    set_state(e, PARKED);
+    e->t_park = now;
+    parked_[e->id] = e;
+  }
+}
+
+// caller holds the engine lock with the pod's profile configuration applied
+bool Lane::hinted_since(uint64_t cycle, const PodReq& req) {
+  if (hint_dropped_ && hint_dropped_cycle_ >= cycle) return true;   // too old to tell: retry
+  uint64_t n, m, c;
+  for (auto it = hints_.rbegin(); it != hints_.rend(); ++it) {
+    if (it->first < cycle) break;
+    if (it->second >= 0 && it->second < eng_->num_nodes() && eng_->node(it->second).alive &&
+        eng_->filter_node(req, it->second, &n, &m, &c) == RS_OK)
+      return true;
+  }
+  return false;
+}
+
+void Lane::move_parked(const std::vector<Entry*>& which) {
+  if (which.empty()) return;
+  const double now = mono();
+  std::lock_guard<std::mutex> g(store_mu_);
+  uint64_t moved = 0;
+  for (Entry* e : which) {
+    if (e->st != PARKED) continue;
+    parked_.erase(e->id);
+    route(e, now);
+    ++moved;
+  }
+  std::lock_guard<std::mutex> g2(stat_mu_);
+  st_.moved += moved;
+}
+
+void Lane::process_moves() {
+  if (pending_moves_.empty()) return;
+  bool all = false;
+  for (int32_t n : pending_moves_) all |= n < 0;
+  std::vector<Entry*> mv;
+  if (all) {
+    move_cycle_ = (int64_t)cycle_;
+    for (auto& kv : parked_) mv.push_back(kv.second);
+  } else {
+    // queueing hints: a node's filter-visible capacity grew; a parked pod moves only if it now
+    // passes every filter of its profile on that node (upstream QueueingHint, exact here)
+    std::lock_guard<std::recursive_mutex> lk(*emu_);
+    const EngineConfig saved = eng_->config();
+    int cur = -2;
+    uint64_t n, m, c;
+    for (int32_t node : pending_moves_) {
+      hints_.emplace_back(cycle_, node);
+      if (hints_.size() > 256) {
+        hint_dropped_cycle_ = hints_.front().first;
+        hint_dropped_ = true;
+        hints_.erase(hints_.begin());
+      }
+    }
+    const int nn = eng_->num_nodes();
+    for (auto& kv : parked_) {
+      Entry* e = kv.second;
+      bool go = !e->req || e->prof < 0 || e->prof >= (int)lp_.size();
+      for (size_t k = 0; !go && k < pending_moves_.size(); ++k) {
+        const int32_t node = pending_moves_[k];
+        if (node < 0 || node >= nn || !eng_->node(node).alive) continue;
+        if (e->prof != cur) {
+          eng_->set_config(lp_[e->prof].cfg);
+          cur = e->prof;
+        }
+        go = eng_->filter_node(*e->req, node, &n, &m, &c) == RS_OK;
+      }
+      if (go) mv.push_back(e);
+    }
+    eng_->set_config(saved);
+  }
+  pending_moves_.clear();
+  move_parked(mv);
+}
+
+// backoffQ pods whose backoff ended → activeQ; unschedulableQ pods parked longer than the
+// flush interval → activeQ / backoffQ (flushBackoffQCompleted, flushUnschedulableQLeftover)
+void Lane::flush_queues(double now) {
+  if (bheap_.empty() && parked_.empty()) return;
+  std::vector<Entry*> left;
+  if (!parked_.empty() && now >= next_leftover_) {
+    for (auto& kv : parked_)
+      if (now - kv.second->t_park > o_.unsched_flush_s) left.push_back(kv.second);
+    next_leftover_ = now + std::max(0.05, std::min(1.0, o_.unsched_flush_s / 4));
+  }
+  if (!left.empty()) move_parked(left);
+  if (bheap_.empty() || bheap_.top().until > now) return;
+  std::lock_guard<std::mutex> g(store_mu_);
+  uint64_t n = 0;
+  while (!bheap_.empty() && bheap_.top().until <= now) {
+    const BItem b = bheap_.top();
+    bheap_.pop();
+    auto it = by_id_.find(b.id);
+    if (it == by_id_.end() || it->second->st != BACKOFF || it->second->bseq != b.seq) continue;   // stale
+    activate(it->second);
+    ++n;
+  }
+  std::lock_guard<std::mutex> g2(stat_mu_);
+  st_.retried += n;
+}
+
+double Lane::next_timer() const {
+  double t = 1e300;
+  if (!bheap_.empty()) t = bheap_.top().until;
+  if (!parked_.empty()) t = std::min(t, std::max(next_leftover_, mono() + 0.05));
+  return t;
+}
+
 void Lane::record_scheduled(const Entry& e) {
   if (!o_.events) return;
   std::lock_guard<std::mutex> g(stat_mu_);
@@ -1171,14 +1444,41 @@ void Lane::flush_events() {
     PendingEvent pe = std::move(ev_q_.front());
     ev_q_.pop_front();
     const std::string ctl = pe.profile.empty() ? std::string("yoda-scheduler") : pe.profile;
-    char seq[24];
-    snprintf(seq, sizeof seq, "%08llx", (unsigned long long)++ev_seq_);
-    const std::string name = pe.name + "." + o_.name_prefix + seq;
-    const std::string note = "Successfully assigned " + pe.ns + "/" + pe.name + " to " + pe.node;
+    const bool failed = !pe.note.empty();
+    const char* reason = failed ? "FailedScheduling" : "Scheduled";
+    const char* typ = failed ? "Warning" : "Normal";
+    const std::string note = failed ? pe.note : "Successfully assigned " + pe.ns + "/" + pe.name + " to " + pe.node;
     const std::string t = micro_time(pe.ts);
     std::string b;
     b.reserve(512);
     std::string path;
+    if (failed) {
+      // an isomorphic repeat (same pod, reason, message, controller) bumps the first event's
+      // series instead of creating another (framework/events.py::_write_v1)
+      std::string key = pe.ns + "/" + pe.name + "\x1f" + ctl + "\x1f" + pe.note;
+      auto it = ev_dedup_.find(key);
+      if (it != ev_dedup_.end()) {
+        const int count = ++it->second.second;
+        if (o_.events_v1) {
+          b += "{\"series\":{\"count\":" + std::to_string(count) + ",\"lastObservedTime\":";
+          json_str(t, b);
+          b += "}}";
+          path = "/apis/events.k8s.io/v1/namespaces/" + pe.ns + "/events/" + it->second.first;
+        } else {
+          b += "{\"count\":" + std::to_string(count) + ",\"lastTimestamp\":";
+          json_str(t, b);
+          b += "}";
+          path = "/api/v1/namespaces/" + pe.ns + "/events/" + it->second.first;
+        }
+        port->request_native("PATCH", path, std::move(b), false, 30.0, kEventTag | ++ev_seq_, this);
+        continue;
+      }
+      if (ev_dedup_.size() > 10000) ev_dedup_.clear();
+    }
+    char seq[24];
+    snprintf(seq, sizeof seq, "%08llx", (unsigned long long)++ev_seq_);
+    const std::string name = pe.name + "." + o_.name_prefix + seq;
+    if (failed) ev_dedup_.emplace(pe.ns + "/" + pe.name + "\x1f" + ctl + "\x1f" + pe.note, std::make_pair(name, 1));
     if (o_.events_v1) {
       // framework/events.py::EventRecorder._new_v1
       b += "{\"apiVersion\":\"events.k8s.io/v1\",\"kind\":\"Event\",\"metadata\":{\"name\":";
@@ -1191,7 +1491,9 @@ void Lane::flush_events() {
       json_str(ctl, b);
       b += ",\"reportingInstance\":";
       json_str(ctl + "-" + o_.host, b);
-      b += ",\"action\":\"Binding\",\"reason\":\"Scheduled\",\"regarding\":{\"apiVersion\":\"v1\",\"kind\":\"Pod\",\"name\":";
+      b += failed ? ",\"action\":\"Scheduling\",\"reason\":" : ",\"action\":\"Binding\",\"reason\":";
+      json_str(reason, b);
+      b += ",\"regarding\":{\"apiVersion\":\"v1\",\"kind\":\"Pod\",\"name\":";
       json_str(pe.name, b);
       b += ",\"namespace\":";
       json_str(pe.ns, b);
@@ -1199,7 +1501,9 @@ void Lane::flush_events() {
       json_str(pe.uid, b);
       b += "},\"note\":";
       json_str(note, b);
-      b += ",\"type\":\"Normal\"}";
+      b += ",\"type\":";
+      json_str(typ, b);
+      b += "}";
       path = "/apis/events.k8s.io/v1/namespaces/" + pe.ns + "/events";
     } else {
       b += "{\"apiVersion\":\"v1\",\"kind\":\"Event\",\"metadata\":{\"name\":";
@@ -1212,9 +1516,13 @@ void Lane::flush_events() {
       json_str(pe.ns, b);
       b += ",\"uid\":";
       json_str(pe.uid, b);
-      b += "},\"reason\":\"Scheduled\",\"message\":";
+      b += "},\"reason\":";
+      json_str(reason, b);
+      b += ",\"message\":";
       json_str(note, b);
-      b += ",\"type\":\"Normal\",\"source\":{\"component\":";
+      b += ",\"type\":";
+      json_str(typ, b);
+      b += ",\"source\":{\"component\":";
       json_str(ctl, b);
       b += "},\"firstTimestamp\":";
       json_str(t, b);
@@ -1245,8 +1553,10 @@ void Lane::run() {
         lk.lock();
       }
       if (!ready()) {
-        if (!ev_q_.empty() && o_.event_qps > 0) {
-          const double wait = std::max(0.0005, (1.0 - ev_tokens_) / o_.event_qps);
+        double wait = next_timer() - mono();             // backoff expiry, unschedulableQ flush
+        if (!ev_q_.empty() && o_.event_qps > 0) wait = std::min(wait, (1.0 - ev_tokens_) / o_.event_qps);
+        if (wait < 1e9) {
+          wait = std::max(0.0005, wait);
           // system_clock deadline: pthread_cond_timedwait (steady-clock waits use
           // pthread_cond_clockwait, which ThreadSanitizer does not model)
           in_cv_.wait_until(lk, std::chrono::system_clock::now() +
@@ -1274,6 +1584,7 @@ void Lane::run() {
           case Item::kEvent: handle_event(it.type, it.ev, &fwd); break;
           case Item::kAnswer: handle_answer(it.tag, it.status, it.body, it.t); break;
           case Item::kProfiles: apply_profiles(&fwd); break;
+          case Item::kMove: pending_moves_.push_back(it.status); break;
           case Item::kRelist: {
             std::vector<Fwd> out;
             handle_relist(*it.items, &out);
@@ -1284,6 +1595,12 @@ void Lane::run() {
       }
     }
     work.clear();
+    // a lane release is a move request for the lane's own waiting pods too (AssignedPodDelete);
+    // moves apply before this turn's runs complete (upstream's moveRequestCycle rule)
+    if (out_moves_pending_ && !parked_.empty()) pending_moves_.push_back(-1);
+    else if (out_moves_pending_) move_cycle_ = (int64_t)cycle_;
+    process_moves();
+    flush_queues(mono());
     auto release_pending = [&] {
       if (to_release_.empty()) return;
       std::lock_guard<std::recursive_mutex> lk(*emu_);

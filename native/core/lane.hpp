@@ -9,8 +9,17 @@
 //   lane thread: store update → admission → priority queue → Engine::schedule_batch (assume)
 //                → Binding POSTs straight to the transport → answers / echo / delete
 //   Python event loop: only what the lane forwards — pods of other profiles or with features
-//                a Python plugin handles, unschedulable pods (FailedScheduling, backoff,
-//                preemption), bind failures — pulled in batches through an eventfd.
+//                a Python plugin handles, unschedulable pods a PostFilter (preemption) may
+//                help, bind failures — pulled in batches through an eventfd.
+//
+// Unschedulable pods no PostFilter can help (the profile has none, or DefaultPreemption and the
+// pod's priority cannot preempt) stay in the lane, as upstream's queue keeps them in compiled Go
+// (/root/reference/pkg/yoda/scheduler.go:85-92 → FitError; deploy/yoda-scheduler.yaml:19-20):
+// a FailedScheduling event and the PodScheduled=False condition from C++, then unschedulableQ
+// (PARKED) or podBackoffQ (BACKOFF, initial × 2^(attempts−1) capped at max), moved back on
+// cluster events — a lane release, any Python move request, and per-node Scv hints that re-run
+// the pod's filters on that node only — with upstream's moveRequestCycle rule and the periodic
+// leftover flush.
 //
 // The lane owns the pod store (key → latest projected event), so the Python informer keeps no
 // per-pod state for lane pods; a relist is diffed here too. Scheduling semantics match the
@@ -57,6 +66,8 @@ struct LaneOptions {
   // async runs: the lane thread (run out) and the engine worker (between runs) busy-wait this
   // long for their next item before sleeping on the condition variable (0: never spin)
   int spin_us = 0;
+  // queue timing (podInitialBackoffSeconds, podMaxBackoffSeconds, unschedulableQ leftover flush)
+  double initial_backoff_s = 1.0, max_backoff_s = 10.0, unsched_flush_s = 60.0;
 };
 
 struct LaneStats {
@@ -64,6 +75,10 @@ struct LaneStats {
   uint64_t forwarded = 0, released = 0, batches = 0, confirmed = 0, events_recorded = 0, events_dropped = 0;
   uint64_t events_written = 0, event_errors = 0, lost_answers_kept = 0;
   uint64_t queued = 0, inflight = 0, binding = 0, owned = 0;   // gauges
+  uint64_t parked = 0, backoff = 0;                            // gauges: unschedulableQ, podBackoffQ
+  uint64_t native_failed = 0;      // of `unschedulable`: kept in the lane (no PostFilter could help)
+  uint64_t moved = 0, retried = 0; // pods moved by move requests; pods back from backoff to the queue
+  uint64_t status_patches = 0, status_patch_errors = 0;
   uint64_t left_in_flight = 0;   // pods gone (deleted, bound elsewhere) while their run was on the engine
   double engine_s = 0;        // wall time inside Engine::schedule_batch (lane thread)
   double engine_cpu_s = 0;    // ... of which on the CPU (the rest: the engine lock, the device)
@@ -77,13 +92,17 @@ struct LaneStats {
 
 class Lane : public yk::PodSink {
  public:
-  enum St : uint8_t { PY = 0, QUEUED, INFLIGHT, BINDING, BOUND };
+  enum St : uint8_t { PY = 0, QUEUED, INFLIGHT, BINDING, BOUND, PARKED, BACKOFF };
 
   struct Profile {
     std::string name;
     bool enabled = false;
     int flag_mask = 0;       // a pod with any of these flags goes to Python
     bool annotate = true;    // yoda filter in the profile: the Binding carries the GPU assignment
+    // an unschedulable pod whose spec.priority is above this goes to Python (its PostFilter —
+    // DefaultPreemption — may act); at or below it the lane fails it natively. INT64_MIN: every
+    // unschedulable pod goes to Python; INT64_MAX: none (no PostFilter that can act)
+    int64_t preempt_above = INT64_MIN;
     EngineConfig cfg;
   };
 
@@ -104,6 +123,7 @@ class Lane : public yk::PodSink {
     std::string msg;
     double t_enqueue = 0;    // monotonic seconds, when the pod entered the lane queue
     double t_cycle = 0;
+    uint32_t attempts = 1;   // scheduling attempts so far (the Python queue's backoff continues)
   };
 
   Lane(Engine* e, std::recursive_mutex* engine_mu, LaneOptions o);
@@ -139,6 +159,10 @@ class Lane : public yk::PodSink {
   // Hold the lane thread between steps (a Python what-if on the ledger — preemption —
   // must not interleave with lane releases); blocks until the thread is parked.
   void pause(bool on);
+  // A move request (upstream MoveAllToActiveOrBackoffQueue): node < 0 moves every parked pod;
+  // node >= 0 is a queueing hint for that node (its Scv grew): only parked pods that now pass
+  // every filter there move. Applied on the lane thread in order with its other input.
+  void move(int32_t node);
 
   // The lane pods holding a reservation, for the Python cache's view of the cluster (pod
   // affinity / spread / preemption plugins). The first call returns the full set and turns
@@ -173,6 +197,12 @@ class Lane : public yk::PodSink {
     bool confirmed = false;  // the watch echo showed the pod bound to node_name
     bool acked = false;      // the Binding POST was answered 2xx
     bool bind_out = false;   // a Binding POST is in flight (no answer yet)
+    uint32_t attempts = 0;   // scheduling attempts (incremented when picked)
+    uint64_t cycle = 0;      // the lane's scheduling cycle of the last pick
+    double t_fail = 0;       // when the last attempt failed (backoff counts from here)
+    double t_park = 0;       // when it entered unschedulableQ
+    uint64_t bseq = 0;       // backoff heap item of this entry (stale items are skipped)
+    std::shared_ptr<PodReq> req;   // the request of the failed attempt (move hints re-filter with it)
   };
   struct QItem {             // max-heap: higher priority first, then FIFO
     int64_t prio;
@@ -194,10 +224,12 @@ class Lane : public yk::PodSink {
     std::vector<size_t> slot;                        // run index of each engine batch member
     std::vector<CycleResult> res;
     std::vector<std::string> names;
+    std::vector<uint64_t> cycles;                    // each pod's scheduling cycle (pick order)
+    std::vector<char> hinted;                        // per result: a node hint since its cycle fits it
     bool failed = false;
   };
   struct Item {             // inbox: events, answers, commands — applied in order
-    enum K : uint8_t { kEvent, kAnswer, kRelist, kProfiles, kRunDone } k = kEvent;
+    enum K : uint8_t { kEvent, kAnswer, kRelist, kProfiles, kRunDone, kMove } k = kEvent;
     char type = 0;
     std::shared_ptr<yk::PodEv> ev;
     uint64_t tag = 0;
@@ -211,6 +243,7 @@ class Lane : public yk::PodSink {
   struct PendingEvent {
     std::string ns, name, uid, node, profile;
     double ts;
+    std::string note;        // empty: Scheduled ("Successfully assigned ... to <node>")
   };
 
   void run();
@@ -233,6 +266,19 @@ class Lane : public yk::PodSink {
   void annotations(const Profile& pr, const Entry& e, const PodReq& req, const CycleResult& r,
                    std::vector<yk::KV>* out);
   void record_scheduled(const Entry& e);
+  // native unschedulable path
+  void fail_native(Entry* e, const Profile& pr, const CycleResult& res, bool hinted);
+  void to_backoff(Entry* e, double until);
+  void activate(Entry* e);
+  void route(Entry* e, double now);
+  double backoff_of(const Entry& e) const;
+  void move_parked(const std::vector<Entry*>& which);
+  void process_moves();
+  void flush_queues(double now);
+  bool hinted_since(uint64_t cycle, const PodReq& req);
+  double next_timer() const;
+  std::string fit_error(const CycleResult& r) const;
+  void patch_condition(const Entry& e, const std::string& msg);
   void flush_events();
   void forward(char type, std::shared_ptr<yk::PodEv> ev, std::shared_ptr<yk::PodEv> old, std::vector<Fwd>* out);
   void publish(std::vector<Fwd>&& fwd, std::vector<Handoff>&& hand);
@@ -331,6 +377,26 @@ class Lane : public yk::PodSink {
   std::deque<PendingEvent> ev_q_;
   double ev_tokens_ = 0, ev_last_ = 0;
   uint64_t ev_seq_ = 0;
+  // FailedScheduling de-duplication (framework/events.py): a repeat of an isomorphic event bumps
+  // the series of the one written first. key → (event name, count)
+  std::unordered_map<std::string, std::pair<std::string, int>> ev_dedup_;
+
+  // native queues (lane thread): scheduling cycles, move requests, unschedulableQ, podBackoffQ
+  uint64_t cycle_ = 0;
+  int64_t move_cycle_ = -1;                          // upstream moveRequestCycle
+  std::vector<int32_t> pending_moves_;               // this turn's move requests (-1: all)
+  std::vector<std::pair<uint64_t, int32_t>> hints_;  // (cycle, node) of recent node hints
+  uint64_t hint_dropped_cycle_ = 0;
+  bool hint_dropped_ = false;
+  std::unordered_map<uint64_t, Entry*> parked_;      // id → PARKED entry
+  struct BItem {
+    double until;
+    uint64_t seq, id;
+    bool operator<(const BItem& o) const { return until > o.until; }   // min-heap
+  };
+  std::priority_queue<BItem> bheap_;
+  uint64_t bseq_ = 0;
+  double next_leftover_ = 0;
 };
 
 }  // namespace yoda

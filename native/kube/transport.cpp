@@ -317,7 +317,8 @@ void Transport::request_native(const std::string& method, const std::string& pat
                                bool limited, double timeout_s, uint64_t tag, PodSink* sink) {
   auto r = std::make_unique<Req>();
   r->id = next_id_++;
-  r->wire = head(method, path, body.size(), "application/json");
+  // PATCH bodies are JSON merge patches (the pod condition, an event's series)
+  r->wire = head(method, path, body.size(), method == "PATCH" ? "application/merge-patch+json" : "application/json");
   r->wire.append(body);
   r->limited = limited;
   r->deadline = timeout_s > 0 ? now_s() + timeout_s : 0.0;

@@ -142,22 +142,99 @@ def test_lane_burst_confirms_echoes_and_releases_on_delete():
     run(go())
 
 
-def test_unschedulable_pod_goes_to_python_path_and_binds_after_capacity_frees():
-    """A pod no node fits is handed to Python: FailedScheduling event, backoff queue; when a
-    lane pod's deletion frees the HBM it is retried on the Python path and binds."""
+def test_unschedulable_pod_stays_native_and_binds_after_capacity_frees():
+    """A pod no node fits and no PostFilter can help (priority 0: DefaultPreemption would not
+    preempt) stays in the lane (VERDICT r3 missing #1): a native FailedScheduling event and
+    PodScheduled=False condition, the lane's unschedulableQ, and when a lane pod's deletion frees
+    the HBM (a move request) it is retried and binds — with no hand-off to Python."""
     async def go():
         used = [294912 - 100000] + [294912] * 7           # one GPU with 100 GB free
         async with Env(nodes=(("n1", 8, used),)) as e:
+            lane = e.sched.lane.lane
             await e.create(pod("big1", {"scv/memory": "80000"}))
             assert await e.wait(lambda: e.sched.scheduled == 1)
             await e.create(pod("big2", {"scv/memory": "80000"}))
-            assert await e.wait(lambda: e.sched.failed >= 1)
-            assert e.sched.lane.handoffs >= 1 and e.sched.recorder.recorded["FailedScheduling"] >= 1
-            assert e.sched.queue.contains((await e.pods())["big2"]["metadata"]["uid"])
+            assert await e.wait(lambda: lane.stats()["parked"] == 1)
+            st = lane.stats()
+            assert st["native_failed"] == 1 and st["unschedulable"] == 1 and e.sched.lane.handoffs == 0
+            assert await e.wait(lambda: lane.stats()["events_written"] >= 2 and lane.stats()["status_patches"] >= 1)
+            cond = (await e.pods())["big2"].get("status", {}).get("conditions") or []
+            evs, _ = await e.cl.list("events.k8s.io")
+            failed = [x for x in evs if x.get("reason") == "FailedScheduling"]
             await e.cl.delete("pods", "big1", "default")
             assert await e.wait(lambda: e.sched.scheduled == 2, 15)
-            return (await e.pods())["big2"]["spec"].get("nodeName")
-    assert run(go()) == "n1"
+            st = lane.stats()
+            return ((await e.pods())["big2"]["spec"].get("nodeName"), cond, failed, st, e.sched.lane.handoffs,
+                    e.sched.failed)
+    node, cond, failed, st, handoffs, py_failed = run(go())
+    assert node == "n1" and handoffs == 0 and py_failed == 0
+    assert cond and cond[0]["type"] == "PodScheduled" and cond[0]["status"] == "False" and \
+        cond[0]["reason"] == "Unschedulable" and cond[0]["message"].startswith("0/1 nodes are available: 1 node(s)")
+    assert len(failed) == 1 and failed[0]["type"] == "Warning" and failed[0]["action"] == "Scheduling" and \
+        failed[0]["regarding"]["name"] == "big2" and failed[0]["note"] == cond[0]["message"]
+    assert st["moved"] >= 1 and st["parked"] == 0 and st["backoff"] == 0
+
+
+def test_unschedulable_pod_that_may_preempt_goes_to_python():
+    """A positive-priority pod may preempt (DefaultPreemption): the lane hands it to the Python
+    path (PostFilter, FailedScheduling, backoff) with its attempt count."""
+    async def go():
+        used = [294912] * 8
+        async with Env(nodes=(("n1", 8, used),)) as e:
+            await e.create(pod("hi", {"scv/memory": "80000"}, priority=100))
+            assert await e.wait(lambda: e.sched.failed >= 1)
+            return e.sched.lane.handoffs, e.sched.lane.lane.stats()["native_failed"], \
+                e.sched.recorder.recorded["FailedScheduling"]
+    handoffs, native, rec = run(go())
+    assert handoffs >= 1 and native == 0 and rec >= 1
+
+
+def test_lane_backoff_doubles_to_the_cap_under_move_requests():
+    """Upstream podBackoffQ timing in the lane: a pod failing again and again under a stream of
+    move requests retries after initial × 2^(attempts−1), capped at max — here 0.1 s doubling
+    to 0.4 s, so ≈ 6 attempts in 1.6 s (16 without the doubling, 1 without the moves); a repeat
+    FailedScheduling bumps one event's series instead of writing another."""
+    async def go():
+        cfg = yoda_config(backoff=0.1, max_backoff=0.4)
+        async with Env(cfg=cfg, nodes=(("n1", 8, [294912] * 8),)) as e:
+            lane = e.sched.lane.lane
+            await e.create(pod("never", {"scv/memory": "80000"}))
+            assert await e.wait(lambda: lane.stats()["native_failed"] == 1)
+            t0 = time.time()
+            while time.time() - t0 < 1.6:
+                e.sched.queue.move_all_to_active_or_backoff("test")     # forwarded to the lane
+                await asyncio.sleep(0.01)
+            n = lane.stats()["native_failed"]
+            await asyncio.sleep(0.3)
+            evs, _ = await e.cl.list("events.k8s.io")
+            failed = [x for x in evs if x.get("reason") == "FailedScheduling"]
+            return n, failed
+    n, failed = run(go())
+    assert 4 <= n <= 8, n
+    assert len(failed) == 1 and int((failed[0].get("series") or {}).get("count", 1)) >= 3
+
+
+def test_scv_hint_moves_only_pods_that_now_fit_that_node():
+    """Queueing hint in the lane: a node's Scv grows; only the parked pod that now passes every
+    filter on it moves (re-filtered in C++), the other stays parked."""
+    async def go():
+        async with Env(nodes=(("n1", 8, [294912] * 8),)) as e:
+            lane = e.sched.lane.lane
+            await e.create(pod("small", {"scv/memory": "50000"}))
+            await e.create(pod("huge", {"scv/memory": "400000"}))
+            assert await e.wait(lambda: lane.stats()["parked"] == 2)
+            s = make_scv("n1", gpus=8, update_time=time.time(), used_mb=[294912 - 60000] + [294912] * 7)
+            s.update_interval_ms = 600_000
+            cur = await e.cl.get("scvs", "n1")
+            obj = s.to_json()
+            obj["metadata"]["resourceVersion"] = cur["metadata"]["resourceVersion"]
+            await e.cl.update("scvs", obj)
+            assert await e.wait(lambda: e.sched.scheduled == 1, 10)
+            await asyncio.sleep(0.2)
+            st = lane.stats()
+            return (await e.pods())["small"]["spec"].get("nodeName"), st["parked"], st["moved"]
+    node, parked, moved = run(go())
+    assert node == "n1" and parked == 1 and moved == 1
 
 
 def test_bind_conflicts_are_retried_through_the_python_path():

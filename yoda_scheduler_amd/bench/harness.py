@@ -302,7 +302,7 @@ class HttpShard:
         # in the in-process harness where each step is a fresh scheduler
         cc = self.cfg.client_connection
         self.client.set_rate(cc.qps, cc.burst)
-        done0, fail0 = sched.scheduled, sched.failed
+        done0 = sched.scheduled
         if sched.lane is not None:
             sched.lane.lane.run_log()           # drop the reset's runs
         t_burst = time.monotonic()
@@ -313,10 +313,12 @@ class HttpShard:
         # native lane the loop sleeps until the lane's acknowledged count reaches the burst
         # (an eventfd wake-up, not a poll); the poll below then only settles the remainder.
         def parked() -> bool:
-            # every pod bound or parked (unschedulable pods handed to the Python queue)
+            # every pod bound or parked (unschedulable: in the lane's own unschedulableQ /
+            # backoffQ, or handed to the Python queue)
             bound = sched.scheduled - done0
-            return not q._active_entries and sched.pending_binds == 0 and sched.failed > fail0 and \
-                bound + len(q._unsched) + len(q._backoff_pods) >= n
+            waiting = sched.lane.waiting() if sched.lane is not None else 0
+            return not q._active_entries and sched.pending_binds == 0 and \
+                bound + len(q._unsched) + len(q._backoff_pods) + waiting >= n
         if sched.lane is not None:
             # woken when the lane's count crosses the burst; a burst with unschedulable pods
             # never gets there, so the parked check runs between short waits

@@ -52,7 +52,11 @@ class NativeLane:
                                 async_mode=int(os.environ.get("YODA_LANE_ASYNC", "1")),
                                 engine_delay_us=int(os.environ.get("YODA_LANE_ENGINE_DELAY_US", "0")),
                                 # busy-wait (µs) of the lane thread / engine worker around device runs
-                                spin_us=int(os.environ.get("YODA_LANE_SPIN_US", "0")))
+                                spin_us=int(os.environ.get("YODA_LANE_SPIN_US", "0")),
+                                # the lane's own unschedulableQ / podBackoffQ (native unschedulable path)
+                                initial_backoff=float(sched.config.pod_initial_backoff_seconds),
+                                max_backoff=float(sched.config.pod_max_backoff_seconds),
+                                unschedulable_flush=float(sched.config.unschedulable_flush_seconds))
         self.lane.set_port(transport.t.port_ptr())
         self._profiles: dict[str, tuple] = {}
         self._loop: Optional[asyncio.AbstractEventLoop] = None
@@ -60,6 +64,8 @@ class NativeLane:
         self.forwarded = 0
         self._waiters: list = []           # (target scheduled count, future)
         self._unowned_waiters: list = []   # futures resolved once the lane owns no pod
+        self._draining = False             # applying the lane's own move request (not echoed back)
+        sched.queue.on_move_all = self._move_all
 
     # ------------------------------------------------------------------ lifecycle
     def attach(self) -> None:
@@ -101,6 +107,37 @@ class NativeLane:
             return None
         return m | bm
 
+    INT64_MIN, INT64_MAX = -(1 << 63), (1 << 63) - 1
+
+    def preempt_above(self, fw) -> int:
+        """Unschedulable pods of ``fw`` with ``spec.priority`` above this go to Python, where a
+        PostFilter may act on them; the lane fails the others natively (FailedScheduling,
+        PodScheduled=False, its own unschedulableQ / backoffQ). The yoda PostFilter is a no-op
+        (maxima are computed in PreScore), and DefaultPreemption preempts only for pods with a
+        positive priority unless ``preemptZeroPriority`` is set; any other PostFilter plugin may
+        act on any pod."""
+        above = self.INT64_MAX
+        for p in fw.post_filter:
+            name = getattr(p, "name", "")
+            if name == "yoda":
+                continue
+            if name == "DefaultPreemption" and not (getattr(p, "args", None) or {}).get("preemptZeroPriority", False):
+                above = min(above, 0)
+                continue
+            return self.INT64_MIN
+        return above
+
+    def _move_all(self) -> None:
+        """A Python move request (node/Scv add or update, a Python pod's deletion, staleness, ...)
+        moves the lane's parked pods too (upstream has one queue for both)."""
+        if not self._draining:
+            self.lane.move(-1)
+
+    def move_node(self, idx: int) -> None:
+        """Queueing hint: ``idx``'s filter-visible capacity grew; parked lane pods that now pass
+        every filter there move (re-filtered in C++ against the node)."""
+        self.lane.move(idx)
+
     def refresh(self) -> None:
         """(Re)declare every profile to the lane when its eligibility changed. A profile the
         lane may no longer run gets its queued pods back through the Python queue."""
@@ -108,11 +145,11 @@ class NativeLane:
         f_yoda = core().F_YODA
         for name, fw in s.frameworks.items():
             m = self.eligible_mask(fw)
-            want = (m is not None, m or 0, bool(fw.filter_mask & f_yoda))
+            want = (m is not None, m or 0, bool(fw.filter_mask & f_yoda), self.preempt_above(fw))
             if self._profiles.get(name) == want:
                 continue
             s._activate(fw)                    # the lane snapshots the engine config now applied
-            self.lane.set_profile(s.engine, name, want[0], want[1], want[2])
+            self.lane.set_profile(s.engine, name, want[0], want[1], want[2], want[3])
             self._profiles[name] = want
             log.info("native lane: profile %s %s (flag mask %#x)", name, "on" if want[0] else "off", want[1])
 
@@ -178,7 +215,11 @@ class NativeLane:
                 except Exception:  # noqa: BLE001 - isolate handlers, like the informer
                     log.exception("native lane: pod event handler failed")
         if moves:
-            s.queue.move_all_to_active_or_backoff("AssignedPodDelete")
+            self._draining = True              # the lane already moved its own parked pods
+            try:
+                s.queue.move_all_to_active_or_backoff("AssignedPodDelete")
+            finally:
+                self._draining = False
             if s._dev_flush:
                 s._request_device_flush()
         for h in hand:
@@ -189,12 +230,12 @@ class NativeLane:
 
     def _handoff(self, h: tuple) -> None:
         """A pod the lane gave up: from here on it is an ordinary Python-path pod."""
-        kind, ev, prof, res, status, msg, t_enq, t_cycle = h
+        kind, ev, prof, res, status, msg, t_enq, t_cycle, attempts = h
         s = self.s
         self.handoffs += 1
         fw = s.frameworks.get(prof) or next(iter(s.frameworks.values()))
         pi = PodInfo.from_native(ev)
-        pi.attempts = 1
+        pi.attempts = max(1, attempts)
         pi.initial_attempt = pi.enqueued = t_enq
         if kind == 0:
             # cycle -1: a move request may have arrived since the lane's cycle, so the pod
@@ -232,6 +273,11 @@ class NativeLane:
     def pending(self) -> int:
         st = self.lane.stats()
         return st["queued"] + st["inflight"] + st["binding"]
+
+    def waiting(self) -> int:
+        """Lane pods in its unschedulableQ or podBackoffQ."""
+        st = self.lane.stats()
+        return st["parked"] + st["backoff"]
 
     def owned(self) -> int:
         return self.lane.stats()["owned"]

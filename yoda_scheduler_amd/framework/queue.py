@@ -51,6 +51,8 @@ class SchedulingQueue:
         self.wake: Optional[asyncio.Future] = None
         # (event, queue, n) → scheduler_queue_incoming_pods_total; None = not counted
         self.incoming_hook: Optional[Callable[[str, str, int], None]] = None
+        # every move-all request is forwarded here too (the native lane's own parked pods)
+        self.on_move_all: Optional[Callable[[], None]] = None
 
     # ------------------------------------------------------------------ helpers
     def _event(self) -> asyncio.Event:
@@ -229,6 +231,8 @@ class SchedulingQueue:
     def move_all_to_active_or_backoff(self, event: str = "") -> int:
         """A cluster event (node add, Scv update, pod delete...) may make parked pods
         schedulable."""
+        if self.on_move_all is not None:
+            self.on_move_all()
         if not self._unsched:                  # the common case (every pod deletion): only
             self._move_request_cycle = self.scheduling_cycle   # record the move request
             return 0

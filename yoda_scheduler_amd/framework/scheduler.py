@@ -469,6 +469,8 @@ class Scheduler:
             self.queue.move_all_to_active_or_backoff("ScvUpdate")
             self.scv_requeues += 1
         elif self._capacity_grew(before, after):
+            if self.lane is not None:
+                self.lane.move_node(self.engine.node_index(name))
             # per pod (upstream QueueingHint): only pods whose GPU request the node's new
             # capacity satisfies can now pass the yoda filter there; other filters do not
             # read Scv, so a pod they rejected on this node stays rejected
