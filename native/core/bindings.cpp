@@ -225,6 +225,30 @@ class BatchWorker {
 
 }  // namespace
 
+// (namespaces | None, nothing, [(key, value)], [(key, op, [values])]) → MatchTerm
+MatchTerm match_term(const py::handle& h) {
+  auto t = h.cast<py::tuple>();
+  MatchTerm m;
+  if (!t[0].is_none())
+    for (auto ns : t[0]) m.namespaces.push_back(ns.cast<std::string>());
+  m.nothing = t[1].cast<bool>();
+  for (auto kv : t[2]) {
+    auto p = kv.cast<py::tuple>();
+    m.labels.emplace_back(p[0].cast<std::string>(), p[1].cast<std::string>());
+  }
+  for (auto ex : t[3]) {
+    auto p = ex.cast<py::tuple>();
+    MatchTerm::Expr x;
+    x.key = p[0].cast<std::string>();
+    const std::string op = p[1].cast<std::string>();
+    x.op = op == "In" ? 0 : op == "NotIn" ? 1 : op == "Exists" ? 2 : op == "DoesNotExist" ? 3 : -1;
+    if (x.op < 0) throw std::invalid_argument("unknown selector operator " + op);
+    for (auto v : p[2]) x.values.push_back(v.cast<std::string>());
+    m.exprs.push_back(std::move(x));
+  }
+  return m;
+}
+
 PYBIND11_MODULE(_yoda_core, m) {
   m.def("build_id", [] { return std::string(YODA_BUILD_ID); }, "hash of the sources this module was built from");
   m.doc() = "Native placement / scheduling-cycle engine (C++17)";
@@ -530,9 +554,10 @@ PYBIND11_MODULE(_yoda_core, m) {
       // the profile's engine configuration is the engine's current one (the caller applied it)
       .def("set_profile",
            [](Lane& l, Engine& e, const std::string& name, bool enabled, int flag_mask, bool annotate,
-              int64_t preempt_above) {
+              int64_t preempt_above, const py::list& gate_terms) {
              Lane::Profile p;
              p.preempt_above = preempt_above;
+             for (auto t : gate_terms) p.gate_terms.push_back(match_term(t));
              p.name = name;
              p.enabled = enabled;
              p.flag_mask = flag_mask;
@@ -544,7 +569,7 @@ PYBIND11_MODULE(_yoda_core, m) {
              l.set_profile(p);
            },
            py::arg("engine"), py::arg("name"), py::arg("enabled"), py::arg("flag_mask"), py::arg("annotate"),
-           py::arg("preempt_above") = INT64_MIN)
+           py::arg("preempt_above") = INT64_MIN, py::arg("gate_terms") = py::list())
       .def("set_active", &Lane::set_active)
       .def("move", &Lane::move, py::arg("node") = -1,
            "move request: -1 moves every parked lane pod; a node index is a queueing hint for that node")
@@ -668,6 +693,30 @@ PYBIND11_MODULE(_yoda_core, m) {
         py::gil_scoped_release nogil;
         return l.log_on();
       })
+      // queries: [[term, ...], ...] (a pod counts for a query when it matches all its terms);
+      // term = (namespaces | None, nothing, [(key, value)], [(key, op, [values])]) → [{node: count}]
+      .def("count_matching",
+           [](Lane& l, const py::list& queries, bool skip_deleting) {
+             std::vector<std::vector<MatchTerm>> qs;
+             for (auto q : queries) {
+               std::vector<MatchTerm> terms;
+               for (auto t : q) terms.push_back(match_term(t));
+               qs.push_back(std::move(terms));
+             }
+             std::vector<std::unordered_map<std::string, int32_t>> out;
+             {
+               py::gil_scoped_release nogil;
+               out = l.count_matching(qs, skip_deleting);
+             }
+             py::list res;
+             for (auto& m : out) {
+               py::dict d;
+               for (auto& kv : m) d[py::str(kv.first)] = kv.second;
+               res.append(d);
+             }
+             return res;
+           },
+           py::arg("queries"), py::arg("skip_deleting") = false)
       .def("take_e2e", &Lane::take_e2e)
       .def("take_pod_latency", &Lane::take_pod_latency)
       .def("wait_idle", &Lane::wait_idle, py::arg("timeout") = 5.0, py::call_guard<py::gil_scoped_release>())

@@ -148,6 +148,32 @@ bool config_eq(const EngineConfig& a, const EngineConfig& b) {
 
 }  // namespace
 
+bool MatchTerm::matches(const yk::PodProj& p) const {
+  if (nothing) return false;
+  if (!namespaces.empty() && std::find(namespaces.begin(), namespaces.end(), p.ns) == namespaces.end()) return false;
+  auto get = [&](const std::string& k) -> const std::string* {
+    for (const auto& kv : p.labels)
+      if (kv.first == k) return &kv.second;
+    return nullptr;
+  };
+  for (const auto& kv : labels) {
+    const std::string* v = get(kv.first);
+    if (!v || *v != kv.second) return false;
+  }
+  for (const auto& x : exprs) {
+    const std::string* v = get(x.key);
+    const bool in = v && std::find(x.values.begin(), x.values.end(), *v) != x.values.end();
+    switch (x.op) {
+      case 0: if (!in) return false; break;
+      case 1: if (in) return false; break;
+      case 2: if (!v) return false; break;
+      case 3: if (v) return false; break;
+      default: return false;
+    }
+  }
+  return true;
+}
+
 double Lane::thread_cpu() {
   timespec ts;
   clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
@@ -421,6 +447,8 @@ bool Lane::admissible(const yk::PodProj& p, int* prof) const {
   for (size_t i = 0; i < lp_.size(); ++i) {
     if (lp_[i].name != p.sched) continue;
     if (!lp_[i].enabled || (p.flags & lp_[i].flag_mask)) return false;
+    for (const MatchTerm& t : lp_[i].gate_terms)
+      if (t.matches(p)) return false;     // an existing pod's required anti-affinity may reject it
     *prof = (int)i;
     return true;
   }
@@ -1199,6 +1227,29 @@ std::vector<Lane::Change> Lane::changes(bool* full) {
     if (e->st == BINDING || e->st == BOUND) out.push_back(Change{e->id, true, e->ev, e->node_name, e->cards});
   }
   *full = true;
+  return out;
+}
+
+std::vector<std::unordered_map<std::string, int32_t>> Lane::count_matching(
+    const std::vector<std::vector<MatchTerm>>& queries, bool skip_deleting) {
+  std::vector<std::unordered_map<std::string, int32_t>> out(queries.size());
+  if (queries.empty()) return out;
+  std::lock_guard<std::mutex> g(store_mu_);
+  for (const auto& kv : by_id_) {
+    const Entry* e = kv.second;
+    if (e->st != BINDING && e->st != BOUND) continue;
+    const yk::PodProj& p = e->ev->full();
+    if (skip_deleting && p.deleting) continue;
+    for (size_t q = 0; q < queries.size(); ++q) {
+      bool all = true;
+      for (const MatchTerm& t : queries[q])
+        if (!t.matches(p)) {
+          all = false;
+          break;
+        }
+      if (all) out[q][e->node_name]++;
+    }
+  }
   return out;
 }
 

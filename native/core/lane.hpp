@@ -70,6 +70,21 @@ struct LaneOptions {
   double initial_backoff_s = 1.0, max_backoff_s = 10.0, unsched_flush_s = 60.0;
 };
 
+// metav1.LabelSelector + the namespaces it applies in (a pod (anti-)affinity term, a topology
+// spread selector): models/selectors.py::LabelSelector semantics (nil matches nothing, {} all).
+struct MatchTerm {
+  std::vector<std::string> namespaces;   // empty: every namespace
+  bool nothing = false;                  // nil selector
+  std::vector<std::pair<std::string, std::string>> labels;
+  struct Expr {
+    std::string key;
+    int op = 0;                          // 0 In, 1 NotIn, 2 Exists, 3 DoesNotExist
+    std::vector<std::string> values;
+  };
+  std::vector<Expr> exprs;
+  bool matches(const yk::PodProj& p) const;
+};
+
 struct LaneStats {
   uint64_t admitted = 0, scheduled = 0, unschedulable = 0, bind_errors = 0, stale_retries = 0;
   uint64_t forwarded = 0, released = 0, batches = 0, confirmed = 0, events_recorded = 0, events_dropped = 0;
@@ -103,6 +118,9 @@ class Lane : public yk::PodSink {
     // DefaultPreemption — may act); at or below it the lane fails it natively. INT64_MIN: every
     // unschedulable pod goes to Python; INT64_MAX: none (no PostFilter that can act)
     int64_t preempt_above = INT64_MIN;
+    // bound pods' required anti-affinity terms (InterPodAffinity's symmetric rule): a pod
+    // matching any of them goes to Python, where that rule is checked; the others are unaffected
+    std::vector<MatchTerm> gate_terms;
     EngineConfig cfg;
   };
 
@@ -179,6 +197,11 @@ class Lane : public yk::PodSink {
     std::vector<int32_t> cards;
   };
   std::vector<Change> changes(bool* full);
+  // Lane pods holding a reservation (assumed or bound) that match every term of a query, counted
+  // per node — what InterPodAffinity and PodTopologySpread read of them, without a Python mirror.
+  // skip_deleting: leave out pods with a deletionTimestamp (spread's countPodsMatchSelector).
+  std::vector<std::unordered_map<std::string, int32_t>> count_matching(
+      const std::vector<std::vector<MatchTerm>>& queries, bool skip_deleting);
   void stop_log();
   bool log_on();
 

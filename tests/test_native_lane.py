@@ -312,9 +312,11 @@ def test_relist_after_watch_loss_keeps_the_ledger_exact():
     assert ok and binds == 30 and ledger == 30 and owned == 30
 
 
-def test_cluster_gate_hands_the_profile_back_to_python():
-    """A bound pod with required anti-affinity turns InterPodAffinity's symmetry gate on: the
-    lane stops taking the profile's pods (they take the Python path, which checks symmetry)."""
+def test_anti_affinity_gate_hands_only_matching_pods_to_python():
+    """A bound pod with required anti-affinity (app=web on this host) turns InterPodAffinity's
+    symmetric rule on. The lane keeps the profile but takes only pods the rule cannot touch: a
+    pod labelled app=web goes to the Python path, which rejects it (the only node holds the anti
+    pod); an unrelated pod still binds through the lane."""
     async def go():
         cfg = yoda_config(extra_filter=["InterPodAffinity"])
         async with Env(cfg=cfg) as e:
@@ -326,14 +328,48 @@ def test_cluster_gate_hands_the_profile_back_to_python():
                            {"labelSelector": {"matchLabels": {"app": "web"}}, "topologyKey": "kubernetes.io/hostname"}]}})
             await e.create(anti)
             assert await e.wait(lambda: e.sched.scheduled == 2)
-            assert await e.wait(lambda: not e.sched.lane._profiles["yoda-scheduler"][0])
+            assert await e.wait(lambda: len(e.sched.lane._profiles["yoda-scheduler"][4]) == 1)
+            on = e.sched.lane._profiles["yoda-scheduler"][0]
             await e.create(pod("web1", {"app": "web", "scv/memory": "1000"}))
-            await asyncio.sleep(0.5)
+            await e.create(pod("api1", {"app": "api", "scv/memory": "1000"}))
+            assert await e.wait(lambda: e.sched.scheduled == 3)
+            await asyncio.sleep(0.3)
             pods = await e.pods()
-            return admitted0, e.sched.lane.lane.stats()["admitted"], pods["web1"]["spec"].get("nodeName")
-    a0, a1, web_node = run(go())
-    assert a0 == 1 and a1 == 1          # neither anti (PF_POD_AFFINITY) nor web1 (gate on) went to the lane
-    assert not web_node                 # symmetry: the only node holds the anti pod
+            return (on, admitted0, e.sched.lane.lane.stats()["admitted"], pods["web1"]["spec"].get("nodeName"),
+                    pods["api1"]["spec"].get("nodeName"), e.sched.failed)
+    on, a0, a1, web_node, api_node, failed = run(go())
+    assert on and a0 == 1 and a1 == 2   # anti (PF_POD_AFFINITY) and web1 (matches the term) stayed off the lane
+    assert not web_node and failed >= 1  # symmetry: the only node holds the anti pod
+    assert api_node == "n1"
+
+
+def test_affinity_pods_count_lane_pods_natively_without_a_mirror():
+    """A pod with required pod affinity to lane pods (app=web) and one with required
+    anti-affinity to them: InterPodAffinity counts the lane's pods in C++ (per node, by
+    selector), so the hybrid cycles need no Python mirror of the lane (the change log stays
+    off) and still see them."""
+    async def go():
+        cfg = yoda_config(extra_filter=["InterPodAffinity"])
+        async with Env(cfg=cfg, nodes=(("n1", 8, None), ("n2", 8, None))) as e:
+            for n in ("n1", "n2"):
+                e.sched.cache.nodes[n].labels["zone"] = n
+                e.sched.engine.set_node_meta(e.sched.engine.node_index(n), False, [("zone", n)], [], 192000,
+                                             2 << 40, 110)
+            for i in range(3):
+                await e.create(pod(f"w{i}", {"app": "web", "scv/memory": "1000"}, nodeSelector={"zone": "n2"}))
+            assert await e.wait(lambda: e.sched.scheduled == 3)
+            term = {"labelSelector": {"matchLabels": {"app": "web"}}, "topologyKey": "zone"}
+            await e.create(pod("near", {"app": "cache", "scv/memory": "1000"},
+                               affinity={"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [term]}}))
+            await e.create(pod("far", {"app": "batch", "scv/memory": "1000"},
+                               affinity={"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [term]}}))
+            assert await e.wait(lambda: e.sched.scheduled == 5)
+            pods = await e.pods()
+            return pods["near"]["spec"]["nodeName"], pods["far"]["spec"]["nodeName"], e.sched.lane.lane.log_on, \
+                e.sched.cache.lane_mirrored()
+    near, far, log_on, mirrored = run(go())
+    assert near == "n2" and far == "n1"
+    assert not log_on and mirrored == 0
 
 
 def test_native_lane_off_and_on_agree_on_python_only_pods():
@@ -437,30 +473,29 @@ def test_watch_read_sliced_to_one_recv_per_turn_keeps_the_lane_exact():
 
 
 def test_mirror_settles_off_and_the_change_log_coalesces():
-    """A Python-path pod (topology spread) mirrors the lane's pods into the cache and turns the
-    lane's change log on; lane pods bound and deleted before the next Python cycle cancel out
-    in the log (it never holds deleted pods' events), and once no Python cycle has
-    read the mirror for ``laneMirrorSettleSeconds`` the mirror is dropped and the log is off."""
+    """A Python-path cycle that reads other pods in full (preemption, for an unschedulable pod
+    with a positive priority) mirrors the lane's pods into the cache and turns the lane's change
+    log on; lane pods bound and deleted before the next Python cycle cancel out in the log
+    (it never holds deleted pods' events), and once no Python cycle has read the
+    mirror for ``laneMirrorSettleSeconds`` the mirror is dropped and the log is off."""
     async def go():
-        cfg = yoda_config(extra_filter=["PodTopologySpread"])
+        cfg = yoda_config()
         cfg.setdefault("yodaRuntime", {})["laneMirrorSettleSeconds"] = 0.3
         async with Env(cfg=cfg) as e:
             lane, cache = e.sched.lane.lane, e.sched.cache
             await e.create(pod("w0", {"app": "web", "scv/memory": "1000"}))
             assert await e.wait(lambda: e.sched.scheduled == 1)
             assert not lane.log_on
-            spread = pod("s0", {"app": "web", "scv/memory": "1000"},
-                         topologySpreadConstraints=[{"maxSkew": 1, "topologyKey": "kubernetes.io/hostname",
-                                                     "whenUnsatisfiable": "DoNotSchedule",
-                                                     "labelSelector": {"matchLabels": {"app": "web"}}}])
-            await e.create(spread)
-            assert await e.wait(lambda: e.sched.scheduled == 2)
+            await e.create(pod("hi", {"scv/memory": "900000"}, priority=10))   # fits nowhere: preemption runs
+            assert await e.wait(lambda: e.sched.failed >= 1)
+            await e.cl.delete("pods", "hi", "default")
+            await asyncio.sleep(0.05)
             on_after_python = lane.log_on
             mirrored = cache.lane_mirrored()
             # 20 lane pods bound and deleted with no Python cycle in between: adds and releases cancel
             for i in range(20):
                 await e.create(pod(f"t{i}", {"scv/memory": "1000"}))
-            assert await e.wait(lambda: e.sched.scheduled == 22)
+            assert await e.wait(lambda: e.sched.scheduled == 21)
             for i in range(20):
                 await e.cl.delete("pods", f"t{i}", "default")
             assert await e.wait(lambda: lane.stats()["owned"] == 1)
@@ -471,7 +506,7 @@ def test_mirror_settles_off_and_the_change_log_coalesces():
     on, mirrored, full, pending, settled, left, py = run(go())
     assert on and mirrored == 1
     assert not full and pending == 0
-    assert settled and left == 0 and py == 1
+    assert settled and left == 0 and py == 0
 
 
 class _Ev:

@@ -34,7 +34,7 @@ class FakeHandle:
         node_pods, pods = {n: set() for n in nodes}, {}
         for p, n in placed:
             node_pods[n].add(p.uid)
-            pods[p.uid] = SimpleNamespace(info=p, node=n)
+            pods[p.uid] = SimpleNamespace(info=p, node=n, lane=False)
         self.cache = SimpleNamespace(nodes={n: SimpleNamespace(labels=l) for n, l in nodes.items()},
                                      node_pods=node_pods, pods=pods)
         self.objs = objs or {}

@@ -51,6 +51,7 @@ class SchedulerCache:
         self.pods: dict[str, PodState] = {}
         self.node_pods: dict[str, set[str]] = {}
         self._anti: set[str] = set()
+        self._anti_terms: Optional[list] = None     # required anti-affinity terms of self._anti
         self.image_nodes: dict[str, int] = {}    # image → number of nodes holding it (ImageLocality)
         self.avoid_nodes: set[str] = set()       # nodes with a preferAvoidPods annotation
         self.node_ext_used: dict[str, dict[str, int]] = {}   # node → extended resource → requested
@@ -60,6 +61,7 @@ class SchedulerCache:
         self.on_anti_change = None               # called when the set of required-anti-affinity pods changes
         self._lane_uids: dict[int, str] = {}     # lane ledger id → uid of the mirrored pod
         self.lane_synced_at: Optional[float] = None   # clock() of the last sync_lane
+        self.lane_never_flags = 0                # pod flags no lane pod carries (NativeLane.refresh)
 
     # ------------------------------------------------------------------ nodes
     def _index_node(self, info: NodeInfo, sign: int) -> None:
@@ -172,6 +174,7 @@ class SchedulerCache:
     def _anti_changed(self) -> None:
         """InterPodAffinity's cluster gate (required anti-affinity symmetry) may have flipped:
         the native lane re-decides which pods it may take."""
+        self._anti_terms = None
         if self.on_anti_change is not None:
             self.on_anti_change()
 
@@ -197,8 +200,36 @@ class SchedulerCache:
     def pods_with_required_anti_affinity(self) -> int:
         """Bound/assumed pods whose required anti-affinity can reject new pods (symmetry)."""
         if self._anti:
+            n = len(self._anti)
             self._anti &= self.pods.keys()
+            if len(self._anti) != n:
+                self._anti_terms = None
         return len(self._anti)
+
+    def anti_terms(self) -> list:
+        """(namespaces, LabelSelector) of every required anti-affinity term of a bound/assumed
+        pod: an incoming pod matching none of them is unaffected by the symmetric rule."""
+        if self.pods_with_required_anti_affinity() == 0:
+            return []
+        if self._anti_terms is None:
+            from ..models.selectors import LabelSelector
+            out = []
+            for uid in self._anti:
+                info = self.pods[uid].info
+                aff = ((info.obj.get("spec") or {}).get("affinity") or {}).get("podAntiAffinity") or {}
+                for t in aff.get("requiredDuringSchedulingIgnoredDuringExecution") or ():
+                    out.append((tuple(t.get("namespaces") or (info.namespace,)), LabelSelector(t.get("labelSelector"))))
+            self._anti_terms = out
+        return self._anti_terms
+
+    def lane_counts(self, queries: list, skip_deleting: bool = False) -> list:
+        """Per query (a list of native terms, all of which a pod must match): lane pods holding a
+        reservation counted per node (``core.Lane.count_matching``); empty dicts without a lane.
+        Plugins that count matching pods add these to their walk over the Python-owned pods
+        (lane mirrors skipped), so they need no Python copy of the lane's pods."""
+        if self.lane is None or not queries:
+            return [{} for _ in queries]
+        return self.lane.count_matching(queries, skip_deleting)
 
     def assumed(self, pi: PodInfo, node: str, cards: list[int]) -> None:
         """Record a pod the engine reserved during ``schedule(assume=True)``."""

@@ -97,7 +97,7 @@ class NativeLane:
         s = self.s
         if s.extenders or self.sort_kind < 0 or not fw.fully_native_static or not fw.post_bind_noop:
             return None
-        m = fw.native_mask()
+        m = fw.native_mask(lane=True)
         if m is None:
             return None
         if len(fw.bind_plugins) != 1 or not getattr(fw.bind_plugins[0], "native_bind", False):
@@ -143,15 +143,20 @@ class NativeLane:
         lane may no longer run gets its queued pods back through the Python queue."""
         s = self.s
         f_yoda = core().F_YODA
+        never = (1 << 62) - 1                  # pod flags no lane pod carries (AND of the masks)
         for name, fw in s.frameworks.items():
             m = self.eligible_mask(fw)
-            want = (m is not None, m or 0, bool(fw.filter_mask & f_yoda), self.preempt_above(fw))
+            if m is not None:
+                never &= m
+            want = (m is not None, m or 0, bool(fw.filter_mask & f_yoda), self.preempt_above(fw),
+                    fw.gate_terms() if m is not None else ())
             if self._profiles.get(name) == want:
                 continue
             s._activate(fw)                    # the lane snapshots the engine config now applied
-            self.lane.set_profile(s.engine, name, want[0], want[1], want[2], want[3])
+            self.lane.set_profile(s.engine, name, want[0], want[1], want[2], want[3], list(want[4]))
             self._profiles[name] = want
             log.info("native lane: profile %s %s (flag mask %#x)", name, "on" if want[0] else "off", want[1])
+        s.cache.lane_never_flags = never
 
     # ------------------------------------------------------------------ lane output
     async def wait_scheduled(self, target: int, timeout: float) -> bool:
@@ -257,14 +262,15 @@ class NativeLane:
 
     # ------------------------------------------------------------------ cache view
     @contextlib.contextmanager
-    def held(self):
-        """The cache mirrors the lane's reserved pods and the lane thread is parked: Python
-        plugins may read other pods and run ledger what-ifs (preemption) safely. The lane is
-        parked first and mirrored second: a pod it placed in between would otherwise be
-        missing from the mirror for the whole hold."""
+    def held(self, sync: bool = True):
+        """The lane thread is parked (and, with ``sync``, the cache mirrors its reserved pods):
+        Python plugins may read other pods — natively counted or mirrored — and run ledger
+        what-ifs (preemption) with no lane placement in between. The lane is parked first and
+        mirrored second: a pod it placed in between would otherwise be missing from the mirror."""
         self.lane.pause(True)
         try:
-            self.s.cache.sync_lane()
+            if sync:
+                self.s.cache.sync_lane()
             yield
         finally:
             self.lane.pause(False)

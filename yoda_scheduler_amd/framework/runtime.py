@@ -104,18 +104,42 @@ class Framework:
                 break
             self._flag_mask |= f
         self._gates = [p.cluster_active for p in self.conditional if hasattr(p, "cluster_active")]
+        # gates the native lane applies per pod from selectors (InterPodAffinity's symmetric rule)
+        self._term_gates = [p for p in self.conditional if hasattr(p, "gate_terms")]
+        self._plain_gates = [p.cluster_active for p in self.conditional
+                             if hasattr(p, "cluster_active") and not hasattr(p, "gate_terms")]
 
-    def native_mask(self) -> Optional[int]:
+    def native_mask(self, lane: bool = False) -> Optional[int]:
         """For a batch of pods: the pod-flag mask such that ``native_for(pod)`` is exactly
         ``not (pod.flags & mask)``, or None when that shortcut does not hold right now (a
         plugin without declared flags, or a cluster gate is active). Evaluated once per batch
-        instead of once per pod."""
+        instead of once per pod. ``lane``: for the native lane, which applies selector gates
+        (``gate_terms``) per pod itself, so only the other gates count."""
         if not self.fully_native_static:
             return None
         m = self._flag_mask
-        if m is None or any(g() for g in self._gates):
+        if m is None or any(g() for g in (self._plain_gates if lane else self._gates)):
             return None
         return m
+
+    def gate_terms(self) -> tuple:
+        """Native terms of the active selector gates: a pod matching one is not for the lane."""
+        return tuple(t for p in self._term_gates for t in p.gate_terms())
+
+    def needs_lane_mirror(self, pod, lane_never_flags: int) -> bool:
+        """Does a Python plugin that applies to ``pod`` read other pods in a way only a Python
+        copy of the lane's pods can serve? Plugins declare ``reads_flags``: the features of
+        other pods they read (pods of the lane never carry ``lane_never_flags``); plugins that
+        count pods by selector do the lane's natively (``reads_flags = 0``). A plugin without
+        the declaration (or preemption) needs the mirror."""
+        for p in self.pre_filter + self.filter_py + [q for q, _ in self.score_py] + self.pre_score + self.reserve \
+                + self.permit:
+            if not self._applies(p, pod):
+                continue
+            rf = getattr(p, "reads_flags", None)
+            if rf is None or rf & ~lane_never_flags:
+                return True
+        return False
 
     def direct_bind_mask(self) -> Optional[int]:
         """Likewise for ``direct_binder_for``: pods without these flags get the single bind

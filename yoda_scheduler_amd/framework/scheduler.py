@@ -569,7 +569,7 @@ class Scheduler:
             # can be placed between the mirror and this pod's assume unseen by its filters
             self._lane_held = True
             try:
-                with self.lane.held():
+                with self.lane.held(sync=fw.needs_lane_mirror(pi, self.cache.lane_never_flags)):
                     return self.schedule_one(pi)
             finally:
                 self._lane_held = False

@@ -16,6 +16,15 @@ class LabelSelector:
                       for e in sel.get("matchExpressions") or []]
         self.empty = not self.labels and not self.exprs
 
+    def native(self, namespaces=None) -> tuple:
+        """The selector (+ the namespaces it applies in, None = all) as a native ``MatchTerm``
+        (``core.Lane.count_matching`` / lane gate terms)."""
+        return (None if namespaces is None else tuple(namespaces), self.nothing, tuple(self.labels.items()),
+                tuple((k, op, tuple(sorted(vals))) for k, op, vals in self.exprs))
+
+    def native_query(self, namespaces=None) -> list:
+        return [self.native(namespaces)]
+
     def matches(self, labels: Optional[Mapping[str, str]]) -> bool:
         if self.nothing:
             return False

@@ -34,6 +34,7 @@ def _group(pod):
 class Coscheduling(PreFilterPlugin, PermitPlugin, ReservePlugin):
     name = "Coscheduling"
     pod_flags = PF_POD_GROUP
+    reads_flags = PF_POD_GROUP  # other pods' features this plugin reads (needs_lane_mirror)
 
     def __init__(self, args=None, handle=None) -> None:
         super().__init__(args, handle)

@@ -57,6 +57,7 @@ class NodeResourcesFit(FilterPlugin):
     name = "NodeResourcesFit"
     python_filter_too = True
     pod_flags = PF_EXTENDED
+    reads_flags = PF_EXTENDED  # other pods' features this plugin reads (needs_lane_mirror)
 
     def __init__(self, args: Optional[dict] = None, handle=None) -> None:
         super().__init__(args, handle)
@@ -154,6 +155,7 @@ class NodePorts(FilterPlugin):
         return Status.ok()
 
     pod_flags = PF_HOST_PORTS
+    reads_flags = PF_HOST_PORTS  # other pods' features this plugin reads (needs_lane_mirror)
 
     def is_noop_for(self, pod) -> bool:
         return not pod.host_ports

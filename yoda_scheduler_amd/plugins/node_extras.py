@@ -29,6 +29,7 @@ class ImageLocality(ScorePlugin):
     spread = (#nodes holding the image)/(#nodes) damps images present everywhere."""
     name = "ImageLocality"
     pod_flags = 0
+    reads_flags = 0  # other pods' features this plugin reads (needs_lane_mirror)
 
     def cluster_active(self) -> bool:
         return bool(self.handle.cache.image_nodes)
@@ -66,6 +67,7 @@ class NodePreferAvoidPods(ScorePlugin):
     the pod's controller, 100 elsewhere."""
     name = "NodePreferAvoidPods"
     pod_flags = PF_CONTROLLER
+    reads_flags = 0  # other pods' features this plugin reads (needs_lane_mirror)
 
     def is_noop_for(self, pod) -> bool:
         return not self.handle.cache.avoid_nodes or _controller(pod) is None

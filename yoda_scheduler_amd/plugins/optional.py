@@ -79,6 +79,12 @@ class _Selector:
     def matches(self, labels: dict) -> bool:
         return all(labels.get(k) == v for k, v in self.eq.items()) and all(s.matches(labels) for s in self.sels)
 
+    def native_query(self, namespaces=None) -> list:
+        """The conjunction as native terms (``core.Lane.count_matching``): a pod counts when it
+        matches every one."""
+        ns = None if namespaces is None else tuple(namespaces)
+        return [(ns, False, tuple(self.eq.items()), ())] + [s.native(namespaces) for s in self.sels]
+
 
 _OWNER_KINDS = {("v1", "ReplicationController"): "replicationcontrollers",
                 ("apps/v1", "ReplicaSet"): "replicasets",
@@ -132,6 +138,7 @@ class NodeLabel(FilterPlugin, ScorePlugin):
     key, averaged over the preference keys."""
     name = "NodeLabel"
     pod_flags = None          # applies to every pod once configured
+    reads_flags = 0  # other pods' features this plugin reads (needs_lane_mirror)
 
     def __init__(self, args: Optional[dict] = None, handle=None) -> None:
         super().__init__(args, handle)

@@ -1,10 +1,12 @@
 """PodTopologySpread and InterPodAffinity (upstream default plugins the reference's profile
 keeps), in Python.
 
-Both only matter for pods that declare topology spread constraints / pod (anti-)affinity,
-or when bound pods carry required anti-affinity terms (the symmetric rule); for every
-other pod ``is_noop_for`` is true and the pod stays on the native fast path. Counting is
-done once per cycle in PreFilter over the cache's bound + assumed pods.
+Both only matter for pods that declare topology spread constraints / pod (anti)affinity,
+or match a bound pod's required anti-affinity term (the symmetric rule); for every other pod
+``is_noop_for`` is true and the pod stays on the native fast path. Counting is done once per
+cycle in PreFilter over the cache's bound + assumed pods: the Python-owned ones walked here,
+the native lane's counted in C++ (``SchedulerCache.lane_counts``: per node, the lane pods
+matching a selector), so neither plugin needs a Python copy of the lane's pods.
 """
 from __future__ import annotations
 
@@ -56,11 +58,12 @@ def _has_keys(labels: dict, constraints) -> bool:
 
 
 def _count_matching(cache, uids, sel, namespace: str) -> int:
-    """upstream ``countPodsMatchSelector``: same namespace, not terminating, selector match."""
+    """upstream ``countPodsMatchSelector``: same namespace, not terminating, selector match —
+    over the Python-owned pods (the lane's come from ``_lane_counts``)."""
     n = 0
     for uid in uids:
         ps = cache.pods.get(uid)
-        if ps is None:
+        if ps is None or ps.lane:
             continue
         info = ps.info
         if info.namespace != namespace or (info.obj.get("metadata") or {}).get("deletionTimestamp"):
@@ -68,6 +71,14 @@ def _count_matching(cache, uids, sel, namespace: str) -> int:
         if sel.matches(info.labels):
             n += 1
     return n
+
+
+def _lane_counts(cache, constraints, namespace: str) -> list:
+    """Per constraint: node → lane pods matching its selector in ``namespace``, not terminating."""
+    counts = getattr(cache, "lane_counts", None)
+    if counts is None:                       # a cache without a native lane (tests' stand-ins)
+        return [{} for _ in constraints]
+    return counts([sel.native_query([namespace]) for _k, _s, sel in constraints], True)
 
 
 class _SpreadFilterState(StateData):
@@ -86,8 +97,9 @@ class _SpreadScoreState(StateData):
     """upstream ``preScoreState``: soft constraints, nodes missing a key (score 0), counts
     per non-hostname pair and ``log(size + 2)`` normalising weights."""
 
-    def __init__(self, constraints, ignored, pair_counts, weights):
+    def __init__(self, constraints, ignored, pair_counts, weights, lane=None):
         self.constraints, self.ignored, self.pair_counts, self.weights = constraints, ignored, pair_counts, weights
+        self.lane = lane or []            # per constraint: node → matching lane pods
 
     def clone(self) -> "_SpreadScoreState":
         return self
@@ -122,6 +134,9 @@ class PodTopologySpread(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlug
     watches = ("services", "replicationcontrollers", "replicasets", "statefulsets")
 
     pod_flags = PF_SPREAD | PF_CONTROLLER
+    # other pods read: their labels only, counted per node (the lane's natively) — no Python
+    # copy of the lane's pods is needed (framework.runtime.Framework.needs_lane_mirror)
+    reads_flags = 0
 
     def __init__(self, args: Optional[dict] = None, handle=None) -> None:
         super().__init__(args, handle)
@@ -177,11 +192,12 @@ class PodTopologySpread(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlug
         min_count: dict = {}
         if hard:
             cache = self.handle.cache
+            lane = _lane_counts(cache, hard, pod.namespace)
             for name, labels in self._qualified_nodes(pod, hard):
                 uids = cache.node_pods.get(name, ())
-                for key, _skew, sel in hard:
+                for i, (key, _skew, sel) in enumerate(hard):
                     pair = (key, labels[key])
-                    pair_counts[pair] = pair_counts.get(pair, 0) + (
+                    pair_counts[pair] = pair_counts.get(pair, 0) + lane[i].get(name, 0) + (
                         _count_matching(cache, uids, sel, pod.namespace) if uids else 0)
             for (key, _v), n in pair_counts.items():
                 if key not in min_count or n < min_count[key]:
@@ -231,17 +247,19 @@ class PodTopologySpread(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlug
             for i, (key, _skew, _sel) in enumerate(soft):
                 size = len(nodes) - len(ignored) if key == LABEL_HOSTNAME else sizes[i]
                 weights.append(math.log(size + 2))
+            cache = self.handle.cache
+            lane = _lane_counts(cache, soft, pod.namespace)
             if pair_counts:
-                cache = self.handle.cache
                 for name, labels in self._qualified_nodes(pod, soft):
                     uids = cache.node_pods.get(name, ())
-                    if not uids:
-                        continue
-                    for key, _skew, sel in soft:
+                    for i, (key, _skew, sel) in enumerate(soft):
                         pair = (key, labels[key])
                         if pair in pair_counts:
-                            pair_counts[pair] += _count_matching(cache, uids, sel, pod.namespace)
-        state.write(self.SCORE_KEY, _SpreadScoreState(soft, ignored, pair_counts, weights))
+                            pair_counts[pair] += lane[i].get(name, 0) + (
+                                _count_matching(cache, uids, sel, pod.namespace) if uids else 0)
+        else:
+            lane = []
+        state.write(self.SCORE_KEY, _SpreadScoreState(soft, ignored, pair_counts, weights, lane))
         return Status.ok()
 
     def _score_state(self, state: CycleState, pod) -> _SpreadScoreState:
@@ -262,7 +280,7 @@ class PodTopologySpread(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlug
                 continue
             if key == LABEL_HOSTNAME:
                 cnt = _count_matching(self.handle.cache, self.handle.cache.node_pods.get(node_name, ()), sel,
-                                      pod.namespace)
+                                      pod.namespace) + (s.lane[i].get(node_name, 0) if s.lane else 0)
             else:
                 cnt = s.pair_counts.get((key, labels[key]), 0)
             total += cnt * s.weights[i] + (max_skew - 1)
@@ -302,6 +320,10 @@ def _term_matches(term: dict, owner_ns: str, other) -> bool:
     return other.namespace in namespaces and LabelSelector(term.get("labelSelector")).matches(other.labels)
 
 
+def _native_term(term: dict, owner_ns: str) -> tuple:
+    return LabelSelector(term.get("labelSelector")).native(term.get("namespaces") or [owner_ns])
+
+
 class _AffinityState(StateData):
     """Topology-pair counts computed once per cycle (upstream ``preFilterState``):
     ``existing_anti``: (key, value) domains where an existing pod's required anti-affinity
@@ -331,40 +353,85 @@ class InterPodAffinity(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugi
     KEY = "PreFilterInterPodAffinity"
 
     pod_flags = PF_POD_AFFINITY
+    # other pods read: labels (the lane's counted natively) and the affinity terms of pods
+    # flagged with them, which the lane never takes
+    reads_flags = PF_POD_AFFINITY
 
     def __init__(self, args=None, handle=None) -> None:
         super().__init__(args, handle)
         self.hard_weight = int(self.args.get("hardPodAffinityWeight", 1))
 
     def cluster_active(self) -> bool:
-        """Bound pods with required anti-affinity can reject any new pod (symmetry)."""
+        """Bound pods with required anti-affinity can reject a new pod (symmetry)."""
         return bool(self.handle.cache.pods_with_required_anti_affinity())
+
+    def gate_terms(self) -> list:
+        """The gate as selectors: only pods matching one of these terms (a bound pod's required
+        anti-affinity) are affected by it; the native lane keeps taking all others."""
+        return [sel.native(ns) for ns, sel in self.handle.cache.anti_terms()]
 
     def is_noop_for(self, pod) -> bool:
         aff = _spec(pod).get("affinity") or {}
         if aff.get("podAffinity") or aff.get("podAntiAffinity"):
             return False
-        return not self.handle.cache.pods_with_required_anti_affinity()
+        return not any(pod.namespace in ns and sel.matches(pod.labels) for ns, sel in self.handle.cache.anti_terms())
 
-    def _existing(self):
-        """(pod info, node labels) for every bound/assumed pod."""
+    def _existing(self, flags: int = 0, owned_only: bool = False):
+        """(pod info, node labels) for the bound/assumed pods (with any of ``flags`` if given;
+        Python-owned only if ``owned_only`` — the lane's are counted natively)."""
         cache = self.handle.cache
         for node, uids in cache.node_pods.items():
-            labels = _node_labels(self.handle, node)
+            labels = None
             for u in uids:
                 ps = cache.pods.get(u)
-                if ps is not None:
-                    yield ps.info, labels
+                if ps is None or (owned_only and ps.lane) or (flags and not ps.info.flags & flags):
+                    continue
+                if labels is None:
+                    labels = _node_labels(self.handle, node)
+                yield ps.info, labels
+
+    def _anti_holders(self):
+        """(pod info, node labels) of the bound/assumed pods with required anti-affinity."""
+        cache = self.handle.cache
+        if not cache.pods_with_required_anti_affinity():
+            return
+        for uid in list(cache._anti):
+            ps = cache.pods.get(uid)
+            if ps is not None:
+                yield ps.info, _node_labels(self.handle, ps.node)
+
+    def _by_topology(self, counts: dict, key: str, out, weight: int = 1) -> None:
+        """Add per-node lane counts into ``out[(key, value)]`` by the nodes' topology labels."""
+        for node, n in counts.items():
+            labels = _node_labels(self.handle, node)
+            if key in labels:
+                out[(key, labels[key])] += weight * n
 
     def pre_filter(self, state: CycleState, pod) -> Status:
         st = _AffinityState()
         aff_terms = [t for t, _ in _terms(pod, "podAffinity", True)]
         anti_terms = [t for t, _ in _terms(pod, "podAntiAffinity", True)]
-        for o, labels in self._existing():
+        cache = self.handle.cache
+        # existing pods' required anti-affinity against this pod: only pods flagged with it
+        # carry such terms (the lane never takes them)
+        for o, labels in self._anti_holders():
             for term, _w in _terms(o, "podAntiAffinity", True):
                 key = term.get("topologyKey", "")
                 if key in labels and _term_matches(term, o.namespace, pod):
                     st.existing_anti[key].add(labels[key])
+        # the incoming pod's terms against every existing pod: the lane's in one native pass
+        queries = ([[_native_term(t, pod.namespace) for t in aff_terms]] if aff_terms else []) + \
+            [[_native_term(t, pod.namespace)] for t in anti_terms]
+        lane = cache.lane_counts(queries) if queries and hasattr(cache, "lane_counts") else [{} for _ in queries]
+        if aff_terms:
+            if lane[0]:
+                st.any_affinity_match = True
+                for t in aff_terms:
+                    self._by_topology(lane[0], t.get("topologyKey", ""), st.affinity)
+            lane = lane[1:]
+        for t, counts in zip(anti_terms, lane):
+            self._by_topology(counts, t.get("topologyKey", ""), st.anti)
+        for o, labels in (self._existing(owned_only=True) if aff_terms or anti_terms else ()):
             if aff_terms and all(_term_matches(t, pod.namespace, o) for t in aff_terms):
                 st.any_affinity_match = True
                 for t in aff_terms:
@@ -414,11 +481,23 @@ class InterPodAffinity(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugi
         scores: dict = defaultdict(lambda: defaultdict(int))
         pref = [(t, w, 1) for t, w in _terms(pod, "podAffinity", False)] + \
                [(t, w, -1) for t, w in _terms(pod, "podAntiAffinity", False)]
-        for o, labels in self._existing():
-            for t, w, sign in pref:                     # incoming pod's preferred terms
+        cache = self.handle.cache
+        if pref:
+            # incoming pod's preferred terms: the lane's pods natively, Python-owned pods below
+            queries = [[_native_term(t, pod.namespace)] for t, _w, _s in pref]
+            lane = cache.lane_counts(queries) if hasattr(cache, "lane_counts") else [{} for _ in queries]
+            for (t, w, sign), counts in zip(pref, lane):
                 key = t.get("topologyKey", "")
-                if key in labels and _term_matches(t, pod.namespace, o):
-                    scores[key][labels[key]] += sign * w
+                for node, n in counts.items():
+                    labels = _node_labels(self.handle, node)
+                    if key in labels:
+                        scores[key][labels[key]] += sign * w * n
+            for o, labels in self._existing(owned_only=True):
+                for t, w, sign in pref:
+                    key = t.get("topologyKey", "")
+                    if key in labels and _term_matches(t, pod.namespace, o):
+                        scores[key][labels[key]] += sign * w
+        for o, labels in self._existing(PF_POD_AFFINITY):
             if self.hard_weight:                        # existing pods' required affinity
                 for t, _w in _terms(o, "podAffinity", True):
                     key = t.get("topologyKey", "")

@@ -111,6 +111,7 @@ class VolumeRestrictions(_VolumeBase, FilterPlugin):
     name = "VolumeRestrictions"
     watches = ()
     pod_flags = PF_DISKS
+    reads_flags = PF_DISKS  # other pods' features this plugin reads (needs_lane_mirror)
 
     def is_noop_for(self, pod) -> bool:
         return not any(k in v for v in _volumes(pod) for k in _EXCLUSIVE_KINDS)
@@ -129,6 +130,7 @@ class VolumeRestrictions(_VolumeBase, FilterPlugin):
 class VolumeZone(_VolumeBase, FilterPlugin):
     name = "VolumeZone"
     pod_flags = PF_CLAIMS
+    reads_flags = 0  # other pods' features this plugin reads (needs_lane_mirror)
 
     def is_noop_for(self, pod) -> bool:
         return not _claim_names(pod)
@@ -204,6 +206,7 @@ class VolumeBinding(_VolumeBase, PreFilterPlugin, FilterPlugin, ReservePlugin, P
     name = "VolumeBinding"
     KEY = "PreFilterVolumeBinding"
     pod_flags = PF_CLAIMS
+    reads_flags = PF_CLAIMS  # other pods' features this plugin reads (needs_lane_mirror)
 
     def __init__(self, args=None, handle=None) -> None:
         super().__init__(args, handle)
@@ -400,6 +403,7 @@ class NodeVolumeLimits(_LimitsBase):
     ``attachable-volumes-csi-<driver>``)."""
     name = "NodeVolumeLimits"
     pod_flags = PF_CLAIMS
+    reads_flags = PF_CLAIMS  # other pods' features this plugin reads (needs_lane_mirror)
     watches = ("persistentvolumeclaims", "persistentvolumes", "storageclasses", "csinodes")
 
     def is_noop_for(self, pod) -> bool:
@@ -449,6 +453,7 @@ class _InTreeLimits(_LimitsBase):
     alloc_key = ""
     default_max = 0
     pod_flags = PF_CLAIMS | PF_DISKS
+    reads_flags = PF_CLAIMS | PF_DISKS  # other pods' features this plugin reads (needs_lane_mirror)
 
     def is_noop_for(self, pod) -> bool:
         return not any(self.kind in v or "persistentVolumeClaim" in v for v in _volumes(pod))
