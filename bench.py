@@ -162,6 +162,9 @@ def main(argv=None) -> int:
                     help="GPUs per synthetic node (BASELINE protocol item 5); default: the config's own")
     ap.add_argument("--nodes", type=int, default=None,
                     help="config 6 only: cluster size (default 4096; the CPU/device crossover end to end)")
+    ap.add_argument("--mix-anti", type=int, default=0,
+                    help="beyond BASELINE: replace this many pods of the burst (evenly spread) with pods that carry "
+                         "required pod anti-affinity (Python-path pods reading other pods, lane pods included)")
     ap.add_argument("--device", choices=["auto", "on", "off"], default="auto",
                     help="gfx950 device scorer (used automatically for clusters >= deviceScorer.minNodes = 48 nodes)")
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
@@ -234,7 +237,7 @@ def main(argv=None) -> int:
 
     from yoda_scheduler_amd.bench.harness import HttpShard, Shard, percentile
     from yoda_scheduler_amd.bench.workloads import make_workload
-    w = make_workload(a.config, seed=rank, node_gpus=a.node_gpus, nodes=a.nodes)
+    w = make_workload(a.config, seed=rank, node_gpus=a.node_gpus, nodes=a.nodes, mix_anti=a.mix_anti)
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
 

@@ -148,11 +148,11 @@ bool config_eq(const EngineConfig& a, const EngineConfig& b) {
 
 }  // namespace
 
-bool MatchTerm::matches(const yk::PodProj& p) const {
+bool MatchTerm::matches(const std::string& ns, const std::vector<std::pair<std::string, std::string>>& lab) const {
   if (nothing) return false;
-  if (!namespaces.empty() && std::find(namespaces.begin(), namespaces.end(), p.ns) == namespaces.end()) return false;
+  if (!namespaces.empty() && std::find(namespaces.begin(), namespaces.end(), ns) == namespaces.end()) return false;
   auto get = [&](const std::string& k) -> const std::string* {
-    for (const auto& kv : p.labels)
+    for (const auto& kv : lab)
       if (kv.first == k) return &kv.second;
     return nullptr;
   };
@@ -563,6 +563,7 @@ void Lane::handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::ve
     return;                                // stays in the store as a Python-visible terminal pod
   }
   if ((e->st == BINDING || e->st == BOUND) && p.node == e->node_name) {
+    if (!e->lab_ev || !p.labels_hash || p.labels_hash != e->lab_ev->p.labels_hash) e->lab_ev = ev;
     e->ev = ev;
     if (!e->confirmed) {
       e->confirmed = true;
@@ -607,6 +608,7 @@ void Lane::drop_owned(Entry* e, bool release) {
   bind_settled(e);
   if (e->st == PARKED) parked_.erase(e->id);      // a BACKOFF heap item goes stale by itself
   e->req.reset();
+  e->lab_ev.reset();
   if (release && e->id) {
     to_release_.push_back(e->id);
     log_remove(e->id);
@@ -952,6 +954,7 @@ void Lane::finish_run(Run& r, std::vector<yk::BindSpec>* binds, std::vector<uint
     e->node = res.node;
     e->node_name = r.names[q];
     e->cards = res.cards;
+    e->lab_ev = e->ev;                    // complete (queued pods keep full projections)
     set_state(e, BINDING);
     log_add(*e);
     yk::BindSpec b;
@@ -1238,12 +1241,13 @@ std::vector<std::unordered_map<std::string, int32_t>> Lane::count_matching(
   for (const auto& kv : by_id_) {
     const Entry* e = kv.second;
     if (e->st != BINDING && e->st != BOUND) continue;
-    const yk::PodProj& p = e->ev->full();
+    const yk::PodProj& p = e->ev->p;                  // identity: namespace, deletionTimestamp
     if (skip_deleting && p.deleting) continue;
+    const auto& labels = (e->lab_ev ? e->lab_ev : e->ev)->full().labels;
     for (size_t q = 0; q < queries.size(); ++q) {
       bool all = true;
       for (const MatchTerm& t : queries[q])
-        if (!t.matches(p)) {
+        if (!t.matches(p.ns, labels)) {
           all = false;
           break;
         }

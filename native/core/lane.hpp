@@ -82,7 +82,8 @@ struct MatchTerm {
     std::vector<std::string> values;
   };
   std::vector<Expr> exprs;
-  bool matches(const yk::PodProj& p) const;
+  bool matches(const std::string& ns, const std::vector<std::pair<std::string, std::string>>& labels) const;
+  bool matches(const yk::PodProj& p) const { return matches(p.ns, p.labels); }
 };
 
 struct LaneStats {
@@ -226,6 +227,9 @@ class Lane : public yk::PodSink {
     double t_park = 0;       // when it entered unschedulableQ
     uint64_t bseq = 0;       // backoff heap item of this entry (stale items are skipped)
     std::shared_ptr<PodReq> req;   // the request of the failed attempt (move hints re-filter with it)
+    // a reserved pod's event whose labels are current: later watch echoes keep it while their
+    // labels hash says the labels did not change, so the selector census never projects them
+    std::shared_ptr<yk::PodEv> lab_ev;
   };
   struct QItem {             // max-heap: higher priority first, then FIFO
     int64_t prio;

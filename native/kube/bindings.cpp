@@ -93,6 +93,7 @@ PYBIND11_MODULE(_yoda_kube, m) {
       .def_property_readonly("deleting", [](const PodEv& e) { return e.p.deleting; })
       .def_property_readonly("hash", [](const PodEv& e) { return e.full().spec_meta_hash; })
       .def_property_readonly("flags", [](const PodEv& e) { return e.full().flags; })
+      .def_property_readonly("labels_hash", [](const PodEv& e) { return e.p.labels_hash; })
       // (key, uid, node, scheduler, phase, hash): the per-event fields in one call
       .def("ident", [](const PodEv& e) {
         const PodProj& p = e.full();
@@ -125,6 +126,13 @@ PYBIND11_MODULE(_yoda_kube, m) {
     if (!scan_watch_identity(line, &t, &obj, p, only_md)) return py::none();
     return py::make_tuple(std::string(1, t), std::string(obj), ident_tuple(p));
   }, py::arg("line"), py::arg("only_md") = false);
+  m.def("scan_labels_hash", [](const std::string& line) -> py::object {
+    PodProj p;
+    char t = 0;
+    std::string_view obj;
+    if (!scan_watch_identity(line, &t, &obj, p, false)) return py::none();
+    return py::int_(p.labels_hash);
+  }, py::arg("line"), "the labels hash the watch identity scanner computes for a watch line");
   m.def("flat_identity", [ident_tuple](const std::string& line) -> py::object {
     FlatDoc d;
     if (!d.parse(line) || !d.root().is(FlatDoc::Obj)) return py::none();

@@ -258,6 +258,14 @@ uint64_t spec_hash(N sp, uint64_t h) {
   return sp.obj() ? sp.hash(h) : hash_mix(hash_mix(h, Value::Obj), 0);
 }
 
+constexpr uint64_t kLabelsSeed = 0x6c6162656c73ull;   // "labels"
+
+template <class N>
+uint64_t labels_hash_of(N labels) {
+  const uint64_t h = labels.hash(kLabelsSeed);
+  return h ? h : 1;
+}
+
 template <class N>
 void project_generic(N pod, PodProj& p) {
   p = PodProj();
@@ -278,6 +286,7 @@ void project_generic(N pod, PodProj& p) {
   p.node = std::string(sp.sv("nodeName"));
   if (N st = pod.get("status")) p.phase = std::string(st.sv("phase"));
   p.spec_meta_hash = spec_hash(sp, meta_hash(meta));
+  p.labels_hash = labels_hash_of(m.get("labels"));
 
   // ---- everything below: fall back to Python on any shape the projection does not mirror
   if (!kvs(m.get("labels"), p.labels)) return;
@@ -531,6 +540,7 @@ void project_identity(const FlatDoc::View& pod, PodProj& p) {
   p.sched = sched.empty() ? "default-scheduler" : std::string(sched);
   p.node = std::string(sp ? sp.sv("nodeName") : std::string_view());
   if (const FlatDoc::View st = pod.get("status")) p.phase = std::string(st.sv("phase"));
+  p.labels_hash = labels_hash_of(FlatN{m ? m.get("labels") : FlatDoc::View()});
 }
 
 namespace {
@@ -660,8 +670,18 @@ struct Skim {
 
 }  // namespace
 
+// labels_hash_of over a raw metadata.labels span (empty: no labels member); 0 when it does not parse
+uint64_t labels_span_hash(std::string_view raw) {
+  if (raw.empty()) return labels_hash_of(FlatN{FlatDoc::View()});
+  FlatDoc d;
+  if (!d.parse(raw)) return 0;
+  return labels_hash_of(FlatN{d.root()});
+}
+
 bool scan_watch_identity(std::string_view line, char* type, std::string_view* obj, PodProj& p, bool only_md) {
   p = PodProj();
+  bool labels_seen = false;
+  std::string_view labels_raw;
   Skim k{line.data(), line.data() + line.size()};
   bool ok = true, have_type = false, have_obj = false;
   std::string_view tname;
@@ -671,6 +691,14 @@ bool scan_watch_identity(std::string_view line, char* type, std::string_view* ob
   std::string_view ns, name, uid, rv, creation, sched, node, phase;
   bool deleting = false;
   auto meta = [&](std::string_view key) -> bool {
+    if (key == "labels" && !labels_seen) {
+      labels_seen = true;
+      k.ws();
+      const char* s0 = k.p;
+      if (!k.skip()) return ok = false;
+      labels_raw = std::string_view(s0, size_t(k.p - s0));
+      return true;
+    }
     if (key == "namespace") {
       if (ns_set) return false;
       ns_set = true;
@@ -758,6 +786,7 @@ bool scan_watch_identity(std::string_view line, char* type, std::string_view* ob
   p.sched = sched.empty() ? "default-scheduler" : std::string(sched);
   p.node = std::string(node);
   p.phase = std::string(phase);
+  p.labels_hash = seen_meta ? labels_span_hash(labels_seen ? labels_raw : std::string_view()) : 0;
   return true;
 }
 

@@ -63,6 +63,10 @@ struct PodProj {
   std::vector<PortP> ports;
   int flags = 0;
   uint64_t spec_meta_hash = 0;      // upstream isPodUpdated: spec + metadata minus volatile fields
+  // structural hash of metadata.labels (0: unknown). Set by the full projection and by the
+  // watch identity scanner too, so a light event tells whether a pod's labels changed
+  // without being projected (the lane's per-node selector census keeps the older projection)
+  uint64_t labels_hash = 0;
 };
 
 // Quantity → ceil(q × 10^scale) with exact decimal arithmetic (scale 3: CPU millicores,

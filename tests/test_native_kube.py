@@ -848,3 +848,27 @@ def test_native_apiserver_bench_burst_and_reset_run_in_slices(native_api):
             await http.close()
             await cl.close()
     run(go())
+
+
+def test_labels_hash_agrees_across_scanner_and_projections():
+    """The watch identity scanner's labels hash equals the full projections' (flat and DOM), so
+    the lane's selector census can keep a bound pod's projected labels across light echo events
+    until a label actually changes (then the hashes differ)."""
+    import json
+    from yoda_scheduler_amd._native import _yoda_kube as k
+    base = {"metadata": {"name": "p", "namespace": "ns", "uid": "u1", "resourceVersion": "7",
+                         "labels": {"app": "web", "tier": 'a"b'}},
+            "spec": {"nodeName": "n1", "containers": [{"name": "c"}]}, "status": {"phase": "Running"}}
+    hashes = []
+    for labels in ({"app": "web", "tier": 'a"b'}, {"app": "web", "tier": "x"}, None, {}):
+        obj = json.loads(json.dumps(base))
+        if labels is None:
+            obj["metadata"].pop("labels")
+        else:
+            obj["metadata"]["labels"] = labels
+        raw = json.dumps(obj)
+        line = json.dumps({"type": "MODIFIED", "object": obj})
+        h_scan = k.scan_labels_hash(line)
+        assert h_scan == k.project_flat(raw).labels_hash == k.project(raw).labels_hash != 0
+        hashes.append(h_scan)
+    assert len(set(hashes)) == 4

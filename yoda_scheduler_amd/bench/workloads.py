@@ -32,6 +32,7 @@ class Workload:
     nodes: list[tuple[str, GpuSpec, int]]            # (name, spec, gpus)
     pods: list[dict] = field(default_factory=list)   # label dicts
     scheduler_name: str = "yoda-scheduler"
+    specs: dict = field(default_factory=dict)        # pod index → extra spec fields (e.g. affinity)
 
     @property
     def n_pods(self) -> int:
@@ -52,12 +53,22 @@ def _mixed_labels(rng: random.Random) -> dict:
 
 
 def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None,
-                  node_gpus: Optional[int] = None, nodes: Optional[int] = None) -> Workload:
+                  node_gpus: Optional[int] = None, nodes: Optional[int] = None, mix_anti: int = 0) -> Workload:
     """``node_gpus`` overrides the GPUs per node (BASELINE.md protocol item 5: every
     config at 1, 2, 4 and 8 GPUs per node); pods keep their labels, so e.g. ``scv/number: 8``
     pods are unschedulable on smaller nodes and are reported as such. ``nodes`` resizes
     config 6's cluster (beyond BASELINE: the CPU/device crossover end to end)."""
     w = _make_workload(cfg, seed, template)
+    if mix_anti:
+        # beyond BASELINE: interleave pods with required pod anti-affinity (Python-path plugins
+        # that read other pods, lane pods included) — what such pods cost the native lane
+        n = len(w.pods)
+        for j in range(mix_anti):
+            i = (j + 1) * n // (mix_anti + 1)
+            w.pods[i] = {"app": f"anti-{j}", "scv/memory": "1024"}
+            w.specs[i] = {"affinity": {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                {"labelSelector": {"matchLabels": {"app": f"anti-{j}"}}, "topologyKey": "kubernetes.io/hostname"}]}}}
+        w.name += f" + {mix_anti} required-anti-affinity pods"
     if nodes is not None:
         if cfg != 6 or nodes < 1:
             raise ValueError("nodes: config 6 only, >= 1")
@@ -108,12 +119,13 @@ def _make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None) -> 
 
 
 def pod_object(i: int, labels: dict, scheduler_name: str, namespace: str = "default",
-               prefix: str = "burst") -> dict:
+               prefix: str = "burst", spec: Optional[dict] = None) -> dict:
     return {"apiVersion": "v1", "kind": "Pod",
             "metadata": {"name": f"{prefix}-{i}", "namespace": namespace, "labels": dict(labels)},
             "spec": {"schedulerName": scheduler_name,
                      "containers": [{"name": "main", "image": "rocm/pytorch:latest",
-                                     "resources": {"requests": {"cpu": "100m", "memory": "128Mi"}}}]}}
+                                     "resources": {"requests": {"cpu": "100m", "memory": "128Mi"}}}],
+                     **(spec or {})}}
 
 
 def populate(server, w: Workload, template: Optional[dict] = None, link_load: float = 0.0,
