@@ -653,6 +653,9 @@ PYBIND11_MODULE(_yoda_core, m) {
              d["retried"] = s.retried;
              d["status_patches"] = s.status_patches;
              d["status_patch_errors"] = s.status_patch_errors;
+             d["census_calls"] = s.census_calls;
+             d["census_entries"] = s.census_entries;
+             d["census_s"] = s.census_s;
              d["engine_s"] = s.engine_s;
              d["left_in_flight"] = s.left_in_flight;
              d["engine_pods"] = s.engine_pods;
@@ -717,6 +720,8 @@ PYBIND11_MODULE(_yoda_core, m) {
              return res;
            },
            py::arg("queries"), py::arg("skip_deleting") = false)
+      .def("stop_census", &Lane::stop_census, "drop the selector census (no Python cycle queries it now)",
+           py::call_guard<py::gil_scoped_release>())
       .def("take_e2e", &Lane::take_e2e)
       .def("take_pod_latency", &Lane::take_pod_latency)
       .def("wait_idle", &Lane::wait_idle, py::arg("timeout") = 5.0, py::call_guard<py::gil_scoped_release>())

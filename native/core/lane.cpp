@@ -563,7 +563,11 @@ void Lane::handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::ve
     return;                                // stays in the store as a Python-visible terminal pod
   }
   if ((e->st == BINDING || e->st == BOUND) && p.node == e->node_name) {
-    if (!e->lab_ev || !p.labels_hash || p.labels_hash != e->lab_ev->p.labels_hash) e->lab_ev = ev;
+    if (!e->lab_ev || !p.labels_hash || p.labels_hash != e->lab_ev->p.labels_hash) {
+      e->lab_ev = ev;
+      if (e->crow >= 0) census_[e->crow].dirty = true;
+    }
+    if (e->crow >= 0) census_[e->crow].deleting = p.deleting;
     e->ev = ev;
     if (!e->confirmed) {
       e->confirmed = true;
@@ -608,6 +612,7 @@ void Lane::drop_owned(Entry* e, bool release) {
   bind_settled(e);
   if (e->st == PARKED) parked_.erase(e->id);      // a BACKOFF heap item goes stale by itself
   e->req.reset();
+  if (e->crow >= 0) census_remove(e);
   e->lab_ev.reset();
   if (release && e->id) {
     to_release_.push_back(e->id);
@@ -956,6 +961,7 @@ void Lane::finish_run(Run& r, std::vector<yk::BindSpec>* binds, std::vector<uint
     e->cards = res.cards;
     e->lab_ev = e->ev;                    // complete (queued pods keep full projections)
     set_state(e, BINDING);
+    if (census_on_) census_add(e);
     log_add(*e);
     yk::BindSpec b;
     b.ns = e->ev->p.ns;
@@ -1233,27 +1239,158 @@ std::vector<Lane::Change> Lane::changes(bool* full) {
   return out;
 }
 
+namespace {
+uint64_t chash(std::string_view a, std::string_view b = std::string_view(), bool pair = false) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : a) h = (h ^ c) * 1099511628211ull;
+  if (pair) {
+    h = (h ^ 0x1f) * 1099511628211ull;
+    for (unsigned char c : b) h = (h ^ c) * 1099511628211ull;
+  }
+  return h;
+}
+
+// a MatchTerm over census hashes
+struct CTerm {
+  bool nothing = false;
+  std::vector<uint64_t> ns, kv;                        // allowed namespaces, required key=value
+  struct X {
+    int op;
+    uint64_t k;
+    std::vector<uint64_t> kvs;
+  };
+  std::vector<X> x;
+};
+
+CTerm compile(const MatchTerm& t) {
+  CTerm c;
+  c.nothing = t.nothing;
+  for (const auto& n : t.namespaces) c.ns.push_back(chash(n));
+  for (const auto& kv : t.labels) c.kv.push_back(chash(kv.first, kv.second, true));
+  for (const auto& e : t.exprs) {
+    CTerm::X x{e.op, chash(e.key), {}};
+    for (const auto& v : e.values) x.kvs.push_back(chash(e.key, v, true));
+    c.x.push_back(std::move(x));
+  }
+  return c;
+}
+}  // namespace
+
+void Lane::census_fill(CRow& r) {
+  const Entry* e = r.e;
+  const yk::PodProj& lp = (e->lab_ev ? e->lab_ev : e->ev)->full();
+  r.ns = chash(e->ev->p.ns);
+  r.deleting = e->ev->p.deleting;
+  r.big = lp.labels.size() > (size_t)kCLab;
+  r.n = (uint8_t)std::min<size_t>(lp.labels.size(), kCLab);
+  for (int i = 0; i < r.n; ++i) {
+    r.k[i] = chash(lp.labels[i].first);
+    r.kv[i] = chash(lp.labels[i].first, lp.labels[i].second, true);
+  }
+  r.dirty = false;
+}
+
+void Lane::census_add(Entry* e) {
+  CRow r;
+  r.e = e;
+  auto it = cnode_ids_.find(e->node_name);
+  if (it == cnode_ids_.end()) {
+    it = cnode_ids_.emplace(e->node_name, (uint32_t)cnode_names_.size()).first;
+    cnode_names_.push_back(e->node_name);
+  }
+  r.node = it->second;
+  e->crow = (int32_t)census_.size();
+  census_.push_back(r);                     // derived (dirty) at the next query
+}
+
+void Lane::census_remove(Entry* e) {
+  const int32_t i = e->crow;
+  e->crow = -1;
+  if (i < 0 || i >= (int32_t)census_.size()) return;
+  if (i != (int32_t)census_.size() - 1) {
+    census_[i] = census_.back();
+    census_[i].e->crow = i;
+  }
+  census_.pop_back();
+}
+
+void Lane::stop_census() {
+  std::lock_guard<std::mutex> g(store_mu_);
+  for (auto& r : census_) r.e->crow = -1;
+  std::vector<CRow>().swap(census_);
+  census_on_ = false;
+}
+
 std::vector<std::unordered_map<std::string, int32_t>> Lane::count_matching(
     const std::vector<std::vector<MatchTerm>>& queries, bool skip_deleting) {
   std::vector<std::unordered_map<std::string, int32_t>> out(queries.size());
   if (queries.empty()) return out;
-  std::lock_guard<std::mutex> g(store_mu_);
-  for (const auto& kv : by_id_) {
-    const Entry* e = kv.second;
-    if (e->st != BINDING && e->st != BOUND) continue;
-    const yk::PodProj& p = e->ev->p;                  // identity: namespace, deletionTimestamp
-    if (skip_deleting && p.deleting) continue;
-    const auto& labels = (e->lab_ev ? e->lab_ev : e->ev)->full().labels;
-    for (size_t q = 0; q < queries.size(); ++q) {
+  const double t0 = mono();
+  std::vector<std::vector<CTerm>> cq(queries.size());
+  for (size_t q = 0; q < queries.size(); ++q)
+    for (const auto& t : queries[q]) cq[q].push_back(compile(t));
+  std::unique_lock<std::mutex> g(store_mu_);
+  if (!census_on_) {
+    census_on_ = true;
+    for (auto& kv : by_id_)
+      if ((kv.second->st == BINDING || kv.second->st == BOUND) && kv.second->crow < 0) census_add(kv.second);
+  }
+  std::vector<std::vector<int32_t>> cnt(queries.size(), std::vector<int32_t>(cnode_names_.size(), 0));
+  auto has = [](const uint64_t* a, int n, uint64_t v) {
+    for (int i = 0; i < n; ++i)
+      if (a[i] == v) return true;
+    return false;
+  };
+  for (auto& r : census_) {
+    if (r.dirty) census_fill(r);
+    if (skip_deleting && r.deleting) continue;
+    for (size_t q = 0; q < cq.size(); ++q) {
       bool all = true;
-      for (const MatchTerm& t : queries[q])
-        if (!t.matches(p.ns, labels)) {
-          all = false;
-          break;
+      if (r.big) {                              // more labels than a row holds: exact path
+        const yk::PodProj& lp = (r.e->lab_ev ? r.e->lab_ev : r.e->ev)->full();
+        for (const MatchTerm& t : queries[q])
+          if (!t.matches(r.e->ev->p.ns, lp.labels)) {
+            all = false;
+            break;
+          }
+      } else {
+        for (const CTerm& t : cq[q]) {
+          if (t.nothing || (!t.ns.empty() && std::find(t.ns.begin(), t.ns.end(), r.ns) == t.ns.end())) {
+            all = false;
+            break;
+          }
+          for (uint64_t v : t.kv)
+            if (!has(r.kv, r.n, v)) {
+              all = false;
+              break;
+            }
+          for (size_t j = 0; all && j < t.x.size(); ++j) {
+            const CTerm::X& x = t.x[j];
+            bool in = false;
+            for (uint64_t v : x.kvs) in |= has(r.kv, r.n, v);
+            switch (x.op) {
+              case 0: all = in; break;
+              case 1: all = !in; break;
+              case 2: all = has(r.k, r.n, x.k); break;
+              case 3: all = !has(r.k, r.n, x.k); break;
+              default: all = false;
+            }
+          }
+          if (!all) break;
         }
-      if (all) out[q][e->node_name]++;
+      }
+      if (all) cnt[q][r.node]++;
     }
   }
+  const uint64_t walked = census_.size();
+  for (size_t q = 0; q < cq.size(); ++q)
+    for (size_t n = 0; n < cnt[q].size(); ++n)
+      if (cnt[q][n]) out[q][cnode_names_[n]] = cnt[q][n];
+  g.unlock();
+  std::lock_guard<std::mutex> g2(stat_mu_);
+  st_.census_calls++;
+  st_.census_entries += walked;
+  st_.census_s += mono() - t0;
   return out;
 }
 

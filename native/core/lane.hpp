@@ -95,6 +95,8 @@ struct LaneStats {
   uint64_t native_failed = 0;      // of `unschedulable`: kept in the lane (no PostFilter could help)
   uint64_t moved = 0, retried = 0; // pods moved by move requests; pods back from backoff to the queue
   uint64_t status_patches = 0, status_patch_errors = 0;
+  uint64_t census_calls = 0, census_entries = 0;   // count_matching: calls, reserved pods walked
+  double census_s = 0;
   uint64_t left_in_flight = 0;   // pods gone (deleted, bound elsewhere) while their run was on the engine
   double engine_s = 0;        // wall time inside Engine::schedule_batch (lane thread)
   double engine_cpu_s = 0;    // ... of which on the CPU (the rest: the engine lock, the device)
@@ -203,6 +205,9 @@ class Lane : public yk::PodSink {
   // skip_deleting: leave out pods with a deletionTimestamp (spread's countPodsMatchSelector).
   std::vector<std::unordered_map<std::string, int32_t>> count_matching(
       const std::vector<std::vector<MatchTerm>>& queries, bool skip_deleting);
+  // The census behind count_matching is kept only while queried: the first query builds it,
+  // stop_census() (Python, after a settle window without queries) drops it.
+  void stop_census();
   void stop_log();
   bool log_on();
 
@@ -230,6 +235,7 @@ class Lane : public yk::PodSink {
     // a reserved pod's event whose labels are current: later watch echoes keep it while their
     // labels hash says the labels did not change, so the selector census never projects them
     std::shared_ptr<yk::PodEv> lab_ev;
+    int32_t crow = -1;       // row in census_ (reserved pods, while the census is on)
   };
   struct QItem {             // max-heap: higher priority first, then FIFO
     int64_t prio;
@@ -353,6 +359,26 @@ class Lane : public yk::PodSink {
   std::condition_variable wk_cv_;
   std::vector<std::shared_ptr<Run>> wk_jobs_;
   std::condition_variable idle_cv_;
+
+  // selector census of reserved lane pods (count_matching): one contiguous row per pod with its
+  // namespace and label (key, key=value) hashes, scanned per query without touching the
+  // entries; rows whose labels changed are re-derived lazily at the next query (store_mu_)
+  static constexpr int kCLab = 6;
+  struct CRow {
+    Entry* e = nullptr;
+    uint64_t ns = 0;
+    uint32_t node = 0;       // cnode_names_ index
+    bool deleting = false, dirty = true, big = false;
+    uint8_t n = 0;
+    uint64_t k[kCLab], kv[kCLab];
+  };
+  bool census_on_ = false;
+  std::vector<CRow> census_;
+  std::vector<std::string> cnode_names_;
+  std::unordered_map<std::string, uint32_t> cnode_ids_;
+  void census_add(Entry* e);
+  void census_remove(Entry* e);
+  void census_fill(CRow& r);
 
   // change log of reserved lane pods (changes()); off until Python first asks
   std::mutex log_mu_;

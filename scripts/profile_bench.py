@@ -42,7 +42,8 @@ def main() -> int:
         out, args = args[1], args[2:]
     import bench
     from yoda_scheduler_amd.bench import harness as H
-    pr = cProfile.Profile()
+    # YODA_PROF_CPU=1: the interpreter thread's CPU time (waits on locks and the GIL excluded)
+    pr = cProfile.Profile(__import__("time").thread_time) if os.environ.get("YODA_PROF_CPU") else cProfile.Profile()
     for cls in (H.Shard, H.HttpShard):
         orig = cls.burst
 

@@ -52,6 +52,7 @@ class SchedulerCache:
         self.node_pods: dict[str, set[str]] = {}
         self._anti: set[str] = set()
         self._anti_terms: Optional[list] = None     # required anti-affinity terms of self._anti
+        self._anti_parsed: dict[str, list] = {}     # uid → [(topologyKey, namespaces, LabelSelector)]
         self.image_nodes: dict[str, int] = {}    # image → number of nodes holding it (ImageLocality)
         self.avoid_nodes: set[str] = set()       # nodes with a preferAvoidPods annotation
         self.node_ext_used: dict[str, dict[str, int]] = {}   # node → extended resource → requested
@@ -61,6 +62,7 @@ class SchedulerCache:
         self.on_anti_change = None               # called when the set of required-anti-affinity pods changes
         self._lane_uids: dict[int, str] = {}     # lane ledger id → uid of the mirrored pod
         self.lane_synced_at: Optional[float] = None   # clock() of the last sync_lane
+        self.lane_census_at: Optional[float] = None   # clock() of the last lane_counts
         self.lane_never_flags = 0                # pod flags no lane pod carries (NativeLane.refresh)
 
     # ------------------------------------------------------------------ nodes
@@ -161,6 +163,7 @@ class SchedulerCache:
         self.node_pods.setdefault(ps.node, set()).add(ps.info.uid)
         if ps.info.flags & PF_REQ_ANTI:
             if ps.info.uid not in self._anti:
+                self._anti_parsed.pop(ps.info.uid, None)
                 self._anti.add(ps.info.uid)
                 self._anti_changed()
         else:
@@ -169,6 +172,7 @@ class SchedulerCache:
     def _anti_drop(self, uid: str) -> None:
         if uid in self._anti:
             self._anti.discard(uid)
+            self._anti_parsed.pop(uid, None)
             self._anti_changed()
 
     def _anti_changed(self) -> None:
@@ -206,21 +210,41 @@ class SchedulerCache:
                 self._anti_terms = None
         return len(self._anti)
 
+    def _anti_of(self, uid: str) -> list:
+        """The parsed required anti-affinity terms of a bound/assumed pod (once per pod)."""
+        r = self._anti_parsed.get(uid)
+        if r is None:
+            from ..models.selectors import LabelSelector
+            info = self.pods[uid].info
+            aff = ((info.obj.get("spec") or {}).get("affinity") or {}).get("podAntiAffinity") or {}
+            r = self._anti_parsed[uid] = [
+                (t.get("topologyKey", ""), tuple(t.get("namespaces") or (info.namespace,)),
+                 LabelSelector(t.get("labelSelector")))
+                for t in aff.get("requiredDuringSchedulingIgnoredDuringExecution") or ()]
+        return r
+
     def anti_terms(self) -> list:
         """(namespaces, LabelSelector) of every required anti-affinity term of a bound/assumed
         pod: an incoming pod matching none of them is unaffected by the symmetric rule."""
         if self.pods_with_required_anti_affinity() == 0:
+            if self._anti_parsed:
+                self._anti_parsed.clear()
             return []
         if self._anti_terms is None:
-            from ..models.selectors import LabelSelector
-            out = []
-            for uid in self._anti:
-                info = self.pods[uid].info
-                aff = ((info.obj.get("spec") or {}).get("affinity") or {}).get("podAntiAffinity") or {}
-                for t in aff.get("requiredDuringSchedulingIgnoredDuringExecution") or ():
-                    out.append((tuple(t.get("namespaces") or (info.namespace,)), LabelSelector(t.get("labelSelector"))))
-            self._anti_terms = out
+            if len(self._anti_parsed) > 2 * len(self._anti) + 16:
+                self._anti_parsed = {u: v for u, v in self._anti_parsed.items() if u in self._anti}
+            self._anti_terms = [(ns, sel) for uid in self._anti for _k, ns, sel in self._anti_of(uid)]
         return self._anti_terms
+
+    def anti_holders(self):
+        """(pod info, node, [(topologyKey, namespaces, LabelSelector)]) of every bound/assumed pod
+        with required anti-affinity (InterPodAffinity's symmetric rule), terms parsed once."""
+        if self.pods_with_required_anti_affinity() == 0:
+            return
+        for uid in list(self._anti):
+            ps = self.pods.get(uid)
+            if ps is not None:
+                yield ps.info, ps.node, self._anti_of(uid)
 
     def lane_counts(self, queries: list, skip_deleting: bool = False) -> list:
         """Per query (a list of native terms, all of which a pod must match): lane pods holding a
@@ -229,6 +253,7 @@ class SchedulerCache:
         (lane mirrors skipped), so they need no Python copy of the lane's pods."""
         if self.lane is None or not queries:
             return [{} for _ in queries]
+        self.lane_census_at = self.clock()
         return self.lane.count_matching(queries, skip_deleting)
 
     def assumed(self, pi: PodInfo, node: str, cards: list[int]) -> None:

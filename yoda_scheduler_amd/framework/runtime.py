@@ -160,10 +160,44 @@ class Framework:
         m = self._flag_mask
         if m is not None and not (pod.flags & m) and not any(g() for g in self._gates):
             return True
+        memo = pod.applies_memo
+        if memo is not None:
+            r = memo.get("native")
+            if r is None:
+                r = memo["native"] = all(p.is_noop_for(pod) for p in self.conditional)
+            return r
         return all(p.is_noop_for(pod) for p in self.conditional)
 
     @staticmethod
     def _applies(p, pod) -> bool:
+        memo = pod.applies_memo
+        if memo is not None:
+            r = memo.get(id(p))
+            if r is None:
+                r = memo[id(p)] = Framework._applies_now(p, pod)
+            return r
+        return Framework._applies_now(p, pod)
+
+    @staticmethod
+    def memo_cycle(pod):
+        """Memoise which plugins apply to ``pod`` for one scheduling cycle (a hybrid cycle asks
+        the same plugin about the same pod at every extension point): a context manager."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def scope():
+            if pod.applies_memo is not None:      # nested (preemption inside a cycle)
+                yield
+                return
+            pod.applies_memo = {}
+            try:
+                yield
+            finally:
+                pod.applies_memo = None
+        return scope()
+
+    @staticmethod
+    def _applies_now(p, pod) -> bool:
         # one flag test for plugins that declare the pod features they act on (unless a
         # cluster-wide gate makes them relevant to every pod)
         pf = getattr(p, "pod_flags", None)

@@ -224,9 +224,13 @@ class Scheduler:
         Python-path cycle has read it for ``laneMirrorSettleSeconds``: a burst with a few
         affinity pods must not make every later lane Binding feed a Python mirror."""
         c = self.cache
-        if self.lane is None or c.lane_synced_at is None or self._lane_held:
+        if self.lane is None or self._lane_held:
             return False
-        if c.clock() - c.lane_synced_at < self.config.lane_mirror_settle_s:
+        now, settle = c.clock(), self.config.lane_mirror_settle_s
+        if c.lane_census_at is not None and now - c.lane_census_at >= settle:
+            self.lane.lane.stop_census()        # the selector census, likewise
+            c.lane_census_at = None
+        if c.lane_synced_at is None or now - c.lane_synced_at < settle:
             return False
         c.drop_lane_mirror()
         c.lane_synced_at = None
@@ -563,6 +567,9 @@ class Scheduler:
         fw = self.frameworks.get(pi.scheduler_name)
         if fw is None or self._pod_gone(pi):
             return
+        if pi.applies_memo is None:
+            with fw.memo_cycle(pi):
+                return self.schedule_one(pi)
         if self.lane is not None and not fw.native_for(pi) and not self._lane_held:
             # Python plugins read other pods, lane pods included: the lane is parked and its
             # pods mirrored for the whole cycle (upstream scheduleOne is serial), so no lane pod

@@ -184,7 +184,7 @@ class PodInfo:
     __slots__ = ("_obj", "_src", "uid", "namespace", "name", "num_id", "labels", "gpu", "scheduler_name", "node_name",
                  "cpu_m", "mem", "priority", "node_selector", "required_terms", "preferred_terms", "tolerations",
                  "annotations", "host_ports", "attempts", "initial_attempt", "enqueued", "native_req",
-                 "native_owner", "assigned_cards", "_creation", "flags", "ext", "nz_cpu_m", "nz_mem")
+                 "native_owner", "assigned_cards", "_creation", "flags", "ext", "nz_cpu_m", "nz_mem", "applies_memo")
 
     def __init__(self, obj: dict, uid: str, namespace: str, name: str, num_id: int, labels: dict, gpu: GpuRequest,
                  scheduler_name: str = "default-scheduler", node_name: str = "", cpu_m: int = 0, mem: int = 0,
@@ -221,6 +221,7 @@ class PodInfo:
         self.enqueued = 0.0
         self.native_req: Any = None          # engine-specific PodReq cache
         self.native_owner: Any = None
+        self.applies_memo: Optional[dict] = None   # plugin id → applies (one cycle; Framework.memo_cycle)
         self.assigned_cards: Optional[list] = None
         self._creation: Optional[float] = None
 

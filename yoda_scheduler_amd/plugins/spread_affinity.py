@@ -390,16 +390,6 @@ class InterPodAffinity(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugi
                     labels = _node_labels(self.handle, node)
                 yield ps.info, labels
 
-    def _anti_holders(self):
-        """(pod info, node labels) of the bound/assumed pods with required anti-affinity."""
-        cache = self.handle.cache
-        if not cache.pods_with_required_anti_affinity():
-            return
-        for uid in list(cache._anti):
-            ps = cache.pods.get(uid)
-            if ps is not None:
-                yield ps.info, _node_labels(self.handle, ps.node)
-
     def _by_topology(self, counts: dict, key: str, out, weight: int = 1) -> None:
         """Add per-node lane counts into ``out[(key, value)]`` by the nodes' topology labels."""
         for node, n in counts.items():
@@ -414,10 +404,10 @@ class InterPodAffinity(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugi
         cache = self.handle.cache
         # existing pods' required anti-affinity against this pod: only pods flagged with it
         # carry such terms (the lane never takes them)
-        for o, labels in self._anti_holders():
-            for term, _w in _terms(o, "podAntiAffinity", True):
-                key = term.get("topologyKey", "")
-                if key in labels and _term_matches(term, o.namespace, pod):
+        for _o, node, terms in cache.anti_holders():
+            labels = _node_labels(self.handle, node)
+            for key, ns, sel in terms:
+                if key in labels and pod.namespace in ns and sel.matches(pod.labels):
                     st.existing_anti[key].add(labels[key])
         # the incoming pod's terms against every existing pod: the lane's in one native pass
         queries = ([[_native_term(t, pod.namespace) for t in aff_terms]] if aff_terms else []) + \
