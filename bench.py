@@ -200,13 +200,22 @@ def main(argv=None) -> int:
     # 0 ranks the domains by idleness and rank r takes the r-th (they must not collide)
     pinned = affinity.pin_l3(0, least_busy=True) if a.pin == "l3" and world == 1 else None
 
+    # YODA_BENCH_THREADS=2: attribute the unnamed threads (birth step, syscall/library samples)
+    scope = None
+    if os.environ.get("YODA_BENCH_THREADS") == "2":
+        from yoda_scheduler_amd.utils.threadscope import ThreadScope
+        scope = ThreadScope()
     import torch
     import torch.distributed as dist
+    if scope:
+        scope.mark("import torch")
     cuda = torch.cuda.is_available()
     # the HIP ordinal this rank owns: its device scorer, its telemetry and its RCCL buffers
     gpu_index = rank_gpu_index(local_rank, torch.cuda.device_count() if cuda else 0)
     if cuda:
         torch.cuda.set_device(gpu_index)
+    if scope:
+        scope.mark("hip init (torch.cuda)")
     backend = None
     if world > 1:
         # RCCL ("nccl") with one rank per GPU; YODA_BENCH_BACKEND=gloo rehearses several ranks
@@ -259,8 +268,13 @@ def main(argv=None) -> int:
                       for i in range(a.warmup + a.steps)]
             for s in shards:
                 loop.run_until_complete(s.start())
+        if scope:
+            scope.mark("scheduler start")
         for i in range(a.warmup):
             loop.run_until_complete(shards[i].burst(f"w{i}"))
+        if scope:
+            scope.mark("warmup bursts (device scorer enabled)")
+            scope.start()
 
         api_sys = [0.0]
 
@@ -354,6 +368,9 @@ def main(argv=None) -> int:
                                                          "runs": getattr(sh, "last_runs", [])}) + "\n")
         sync()
         elapsed = time.perf_counter() - t0
+        if scope:
+            scope.stop()
+            sys.stderr.write("threadscope " + json.dumps({"samples": scope.nsamples, "threads": scope.report()}) + "\n")
         cpu_s = time.process_time() - c0     # this rank's process: scheduler (+ in-process apiserver)
         api_s = api_cpu() - a0
         api_sys_s = api_sys[0] - as0

@@ -59,6 +59,15 @@ for s in $STEPS; do
         -- python3 bench.py --config 6 --steps 3 --warmup 1 --alt none
       python scripts/api_census.py gpurun_out/hiptrace6 > gpurun_out/hiptrace6_census.txt 2>&1 || true ;;
     threads6) step threads6 300 env YODA_BENCH_THREADS=1 python bench.py --config 6 --steps 5 --warmup 1 --alt none ;;
+    scope6) step scope6 300 env YODA_BENCH_THREADS=2 python bench.py --config 6 --steps 5 --warmup 1 --alt none ;;
+    nodegpus)   # BASELINE protocol item 5 on config 3: scheduler CPU per attempted pod at 1/2/4/8 GPUs per node
+      mkdir -p gpurun_out/nodegpus
+      for g in 1 2 4 8; do step "nodegpus/g$g" 300 python bench.py --config 3 --node-gpus $g --steps 10 --warmup 3 --alt none; done ;;
+    mixanti)    # 1000-pod burst with 0 / 10 interleaved required-anti-affinity pods, alternated
+      mkdir -p gpurun_out/mixanti
+      for k in 1 2; do for m in 0 10; do
+        step "mixanti/m${m}_$k" 300 python bench.py --config 3 --mix-anti $m --steps 20 --warmup 5 --alt none
+      done; done ;;
     all)   # every BASELINE config (+ 6) on this box, one JSON line each under gpurun_out/all/
       mkdir -p gpurun_out/all
       for spec in "c3|--config 3 --steps 20 --warmup 5" "c1|--config 1 --steps 20 --warmup 2" \
