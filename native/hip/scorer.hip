@@ -244,6 +244,11 @@ __global__ void k_scatter(const yoda_dev_node_t* __restrict__ stage, const int32
   reinterpret_cast<uint4*>(nodes + idx[rec])[threadIdx.x & 31] = src[threadIdx.x & 31];
 }
 
+// stream-ordered after a k_scatter: the staging buffers it read may be reused
+__global__ void k_upload_done(int32_t* flag, int32_t seq) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ------------------------------------------------------------------ K1: filter + maxima
 // One lane group = one node (lane `sub` = GPU slot). Returns the node's filter reason (0 =
 // feasible) and its eligible-GPU mask, and folds the card metrics of feasible nodes into the
@@ -639,9 +644,8 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
         const int idx = a * YODA_DEV_CARDS + b;
         uni = uni && ((lq[idx >> 1] >> ((idx & 1) * 16)) & 0xFFFFu) == q01;
       }
-    for (int t = s_begin + kGroup * rep + sub; t < s_end; t += kGroup * nrep) {
-      const uint32_t m = s_masks[t];
-      if (m & ~emask) continue;
+    // one subset's objective (the per-pod CPU engine's Engine::gang_objective, same integers)
+    auto eval = [&](uint32_t m, int64_t& o_out, int32_t& lb_out) {
       int32_t qsum = 0;
       int32_t qmin = 10000;
       uint64_t nmask = 0;
@@ -681,11 +685,30 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
       // every term fits 32 bits and the host bounds |w| ≤ 10^6 (Engine::device_eligible):
       // 32×32→64-bit multiply-adds instead of 64×64
       const int32_t mb = P ? (10000 - qmin) * 100 : 0;   // bottleneck pair (≤ 10^6)
-      const int64_t o = (int64_t)(int32_t)r.w_link * lb + (int64_t)(int32_t)r.w_minlink * mb +
-                        (int64_t)(int32_t)r.w_numa * numa_bad + (int64_t)(int32_t)r.w_fit * fit +
-                        (int64_t)(int32_t)r.w_occ * occ_bad;
-      if (!found || better(o, m, best_o, best_m)) {
-        best_o = o; best_m = m; best_lb = lb; found = true;
+      o_out = (int64_t)(int32_t)r.w_link * lb + (int64_t)(int32_t)r.w_minlink * mb +
+              (int64_t)(int32_t)r.w_numa * numa_bad + (int64_t)(int32_t)r.w_fit * fit +
+              (int64_t)(int32_t)r.w_occ * occ_bad;
+      lb_out = lb;
+    };
+    // two subsets per step, evaluated as independent chains: one wave per SIMD cannot hide
+    // the latency of a single chain, two interleaved ones fill each other's stalls. `better`
+    // is a strict total order on (objective, mask), so the fold order does not matter.
+    const int step = kGroup * nrep;
+    for (int t = s_begin + kGroup * rep + sub; t < s_end; t += 2 * step) {
+      const int t2 = t + step;
+      const uint32_t m0 = s_masks[t];
+      const uint32_t m1 = t2 < s_end ? (uint32_t)s_masks[t2] : 0u;
+      const bool ok0 = !(m0 & ~emask), ok1 = t2 < s_end && !(m1 & ~emask);
+      if (!ok0 && !ok1) continue;
+      int64_t o0, o1;
+      int32_t lb0, lb1;
+      eval(m0, o0, lb0);
+      eval(m1, o1, lb1);
+      if (ok0 && (!found || better(o0, m0, best_o, best_m))) {
+        best_o = o0; best_m = m0; best_lb = lb0; found = true;
+      }
+      if (ok1 && (!found || better(o1, m1, best_o, best_m))) {
+        best_o = o1; best_m = m1; best_lb = lb1; found = true;
       }
     }
     GANG_STEP(kDppXor1);
@@ -1412,8 +1435,14 @@ struct Ctx {
   int device = 0, cap = 0;
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
+  // bulk row uploads: host rows in mapped pinned memory that k_scatter reads directly (no
+  // DMA copy, no completion signal for the runtime's threads to service); `h_upflag` is
+  // raised by k_upload_done after the scatter, and the host waits on it only before it
+  // rewrites the staging buffers
   yoda_dev_node_t *d_nodes = nullptr, *d_stage = nullptr, *h_stage = nullptr;
   int32_t *d_idx = nullptr, *h_idx = nullptr;
+  int32_t *h_upflag = nullptr, *d_upflag = nullptr;
+  int32_t up_seq = 0;
   uint8_t *d_feas = nullptr, *d_elig = nullptr, *d_cand = nullptr, *h_cand = nullptr;
   int64_t *d_raw = nullptr, *d_total = nullptr;
   uint32_t* d_mask = nullptr;
@@ -1510,6 +1539,22 @@ int flush_pending(Ctx* c) {
   return 0;
 }
 
+// The last bulk upload's scatter has finished reading the staging buffers (its flag is up):
+// usually long ago; otherwise spin, asking the stream now and then (a failed launch).
+int wait_upload(Ctx* c) {
+  if (c->up_seq == 0) return 0;
+  volatile int32_t* flag = c->h_upflag;
+  for (unsigned spin = 1;; ++spin) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == c->up_seq) return 0;
+    if ((spin & 1023) == 0) {
+      const hipError_t q = hipStreamQuery(c->stream);
+      if (q == hipSuccess) return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == c->up_seq ? 0 : -4;
+      if (q != hipErrorNotReady) return (int)q;
+    }
+    __builtin_ia32_pause();
+  }
+}
+
 // Wait for the device to publish the result: spin on the mapped `feasible` field (written
 // last, system-scope release), polling the stream now and then so a failed launch or a
 // result that never comes cannot hang the scheduler.
@@ -1568,11 +1613,15 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
   const size_t N = (size_t)capacity;
   if ((e = hipMalloc(&c->d_nodes, N * sizeof(yoda_dev_node_t))) != hipSuccess) return fail("nodes", e);
   if ((e = hipMemset(c->d_nodes, 0, N * sizeof(yoda_dev_node_t))) != hipSuccess) return fail("memset", e);
-  if ((e = hipMalloc(&c->d_stage, N * sizeof(yoda_dev_node_t))) != hipSuccess) return fail("stage", e);
-  if ((e = hipHostMalloc(&c->h_stage, N * sizeof(yoda_dev_node_t), hipHostMallocDefault)) != hipSuccess)
+  if ((e = hipHostMalloc(&c->h_stage, N * sizeof(yoda_dev_node_t), hipHostMallocMapped)) != hipSuccess)
     return fail("pinned stage", e);
-  if ((e = hipMalloc(&c->d_idx, N * sizeof(int32_t))) != hipSuccess) return fail("idx", e);
-  if ((e = hipHostMalloc(&c->h_idx, N * sizeof(int32_t), hipHostMallocDefault)) != hipSuccess) return fail("idx", e);
+  if ((e = hipHostGetDevicePointer((void**)&c->d_stage, c->h_stage, 0)) != hipSuccess) return fail("stage map", e);
+  if ((e = hipHostMalloc(&c->h_idx, N * sizeof(int32_t), hipHostMallocMapped)) != hipSuccess) return fail("idx", e);
+  if ((e = hipHostGetDevicePointer((void**)&c->d_idx, c->h_idx, 0)) != hipSuccess) return fail("idx map", e);
+  if ((e = hipHostMalloc(&c->h_upflag, 64, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+    return fail("upload flag", e);
+  if ((e = hipHostGetDevicePointer((void**)&c->d_upflag, c->h_upflag, 0)) != hipSuccess) return fail("upload flag map", e);
+  *c->h_upflag = 0;
   if ((e = hipMalloc(&c->d_feas, N)) != hipSuccess) return fail("feas", e);
   if ((e = hipMalloc(&c->d_elig, N)) != hipSuccess) return fail("elig", e);
   if ((e = hipMalloc(&c->d_cand, N)) != hipSuccess) return fail("cand", e);
@@ -1622,7 +1671,7 @@ void yoda_dev_destroy(void* p) {
   if (!c) return;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
-  hipFree(c->d_nodes); hipFree(c->d_stage); hipHostFree(c->h_stage); hipFree(c->d_idx); hipHostFree(c->h_idx);
+  hipFree(c->d_nodes); hipHostFree(c->h_stage); hipHostFree(c->h_idx); hipHostFree(c->h_upflag);
   hipFree(c->d_feas); hipFree(c->d_elig); hipFree(c->d_cand); hipHostFree(c->h_cand); hipFree(c->d_raw);
   hipFree(c->d_total); hipFree(c->d_mask); hipFree(c->d_quality); hipHostFree(c->h_res); hipHostFree(c->h_resb); hipFree(c->d_g);
   hipHostFree(c->h_reqs); hipHostFree(c->h_done); hipFree(c->d_bres); hipFree(c->d_slots); hipFree(c->d_words);
@@ -1662,16 +1711,18 @@ int yoda_dev_upload(void* p, int n, const int32_t* idx, const yoda_dev_node_t* r
     return 0;
   }
   if (flush_pending(c) != 0) return -6;   // older rows first: the bulk upload may overwrite them
+  // the previous upload's scatter must have read the staging buffers before they are rewritten
+  if (const int w = wait_upload(c)) return w;
   memcpy(c->h_stage, rows, (size_t)n * sizeof(yoda_dev_node_t));
   memcpy(c->h_idx, idx, (size_t)n * sizeof(int32_t));
-  CK(hipMemcpyAsync(c->d_stage, c->h_stage, (size_t)n * sizeof(yoda_dev_node_t), hipMemcpyHostToDevice, c->stream));
-  CK(hipMemcpyAsync(c->d_idx, c->h_idx, (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  std::atomic_thread_fence(std::memory_order_release);
   const int per_block = 8;   // 8 records × 32 lanes = 256 threads
   hipLaunchKernelGGL(k_scatter, dim3((n + per_block - 1) / per_block), dim3(256), 0, c->stream, c->d_stage, c->d_idx,
                      n, c->d_nodes);
-  ++c->n_dispatch;
+  c->up_seq = c->up_seq >= (1 << 30) ? 1 : c->up_seq + 1;
+  hipLaunchKernelGGL(k_upload_done, dim3(1), dim3(64), 0, c->stream, c->d_upflag, c->up_seq);
+  c->n_dispatch += 2;
   CK(hipGetLastError());
-  CK(hipStreamSynchronize(c->stream));   // staging buffers are reused by the next upload
   return 0;
 }
 

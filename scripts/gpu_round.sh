@@ -59,6 +59,12 @@ for s in $STEPS; do
         -- python3 bench.py --config 6 --steps 3 --warmup 1 --alt none
       python scripts/api_census.py gpurun_out/hiptrace6 > gpurun_out/hiptrace6_census.txt 2>&1 || true ;;
     threads6) step threads6 300 env YODA_BENCH_THREADS=1 python bench.py --config 6 --steps 5 --warmup 1 --alt none ;;
+    kbab)   # k_batch A/B: this tree's kernel vs abbin/libyoda_hip_base.so (same box, alternated), bench mix
+      mkdir -p gpurun_out/kbab
+      for k in 1 2; do
+        step "kbab/new_$k" 200 python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
+        step "kbab/base_$k" 200 env YODA_HIP_LIB=abbin/libyoda_hip_base.so python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
+      done ;;
     scope6) step scope6 300 env YODA_BENCH_THREADS=2 python bench.py --config 6 --steps 5 --warmup 1 --alt none ;;
     nodegpus)   # BASELINE protocol item 5 on config 3: scheduler CPU per attempted pod at 1/2/4/8 GPUs per node
       mkdir -p gpurun_out/nodegpus

@@ -158,6 +158,23 @@ class NativeLane:
             log.info("native lane: profile %s %s (flag mask %#x)", name, "on" if want[0] else "off", want[1])
         s.cache.lane_never_flags = never
 
+    def refresh_gates(self) -> None:
+        """Only the selector gates changed (a pod with required anti-affinity was assumed or
+        left): re-send the terms of the profiles the lane runs — eligibility itself does not
+        depend on them (``Framework.native_mask(lane=True)``)."""
+        s = self.s
+        for name, fw in s.frameworks.items():
+            want = self._profiles.get(name)
+            if want is None or not want[0]:
+                continue
+            terms = fw.gate_terms()
+            if terms == want[4]:
+                continue
+            new = want[:4] + (terms,)
+            s._activate(fw)
+            self.lane.set_profile(s.engine, name, new[0], new[1], new[2], new[3], list(terms))
+            self._profiles[name] = new
+
     # ------------------------------------------------------------------ lane output
     async def wait_scheduled(self, target: int, timeout: float) -> bool:
         """Until ``target`` lane Bindings are acknowledged (the lane wakes the loop when the

@@ -544,7 +544,7 @@ class Scheduler:
         from .lane import NativeLane
         self.lane = NativeLane(self, self.native)
         self.cache.lane = self.lane.lane
-        self.cache.on_anti_change = self._lane_refresh
+        self.cache.on_anti_change = self.lane.refresh_gates
         return self.lane.lane
 
     # ================================================================== cycle
