@@ -65,6 +65,7 @@ for s in $STEPS; do
         step "kbab/new_$k" 200 python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
         step "kbab/base_$k" 200 env YODA_HIP_LIB=abbin/libyoda_hip_base.so python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
       done ;;
+    mixlog) step mixlog 300 env YODA_BENCH_RUNLOG=1 python bench.py --config 3 --mix-anti 10 --steps 5 --warmup 3 --alt none ;;
     scope6) step scope6 300 env YODA_BENCH_THREADS=2 python bench.py --config 6 --steps 5 --warmup 1 --alt none ;;
     nodegpus)   # BASELINE protocol item 5 on config 3: scheduler CPU per attempted pod at 1/2/4/8 GPUs per node
       mkdir -p gpurun_out/nodegpus

@@ -587,3 +587,27 @@ def test_sync_lane_never_drops_a_pod_python_took_over():
     kept, mid, end, py, dropped, on, left = run(go())
     assert kept and mid == 1 and end == 0 and py == 0
     assert dropped == 1 and not on and left == 0
+
+
+def test_gated_cycle_never_lets_the_lane_violate_a_concurrent_anti_affinity_pod():
+    """The anti-affinity pod's Python cycle runs beside the lane (gated, not parked): lane pods
+    matching its required anti-affinity term are held back from the moment its cycle starts.
+    Whatever the interleaving, the single node never ends up with the anti pod and a pod its
+    term rejects both bound; pods the term does not match keep binding through the lane."""
+    async def go():
+        cfg = yoda_config(extra_filter=["InterPodAffinity"])
+        async with Env(cfg=cfg) as e:
+            term = {"labelSelector": {"matchLabels": {"app": "web"}}, "topologyKey": "kubernetes.io/hostname"}
+            for i in range(40):
+                if i == 20:
+                    await e.create(pod("anti", {"app": "db", "scv/memory": "1000"},
+                                       affinity={"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [term]}}))
+                await e.create(pod(f"web{i}", {"app": "web", "scv/memory": "1000"}))
+                await e.create(pod(f"api{i}", {"app": "api", "scv/memory": "1000"}))
+            await asyncio.sleep(1.5)
+            pods = await e.pods()
+            return {n: p["spec"].get("nodeName") for n, p in pods.items()}
+    nodes = run(go())
+    web_bound = [n for n, v in nodes.items() if n.startswith("web") and v]
+    assert all(nodes[f"api{i}"] == "n1" for i in range(40))
+    assert not (nodes["anti"] and web_bound), (nodes["anti"], len(web_bound))

@@ -65,6 +65,7 @@ class NativeLane:
         self._waiters: list = []           # (target scheduled count, future)
         self._unowned_waiters: list = []   # futures resolved once the lane owns no pod
         self._draining = False             # applying the lane's own move request (not echoed back)
+        self._temp_terms: tuple = ()        # gates of a Python cycle running beside the lane (gated)
         sched.queue.on_move_all = self._move_all
 
     # ------------------------------------------------------------------ lifecycle
@@ -149,7 +150,7 @@ class NativeLane:
             if m is not None:
                 never &= m
             want = (m is not None, m or 0, bool(fw.filter_mask & f_yoda), self.preempt_above(fw),
-                    fw.gate_terms() if m is not None else ())
+                    fw.gate_terms() + self._temp_terms if m is not None else ())
             if self._profiles.get(name) == want:
                 continue
             s._activate(fw)                    # the lane snapshots the engine config now applied
@@ -167,7 +168,7 @@ class NativeLane:
             want = self._profiles.get(name)
             if want is None or not want[0]:
                 continue
-            terms = fw.gate_terms()
+            terms = fw.gate_terms() + self._temp_terms
             if terms == want[4]:
                 continue
             new = want[:4] + (terms,)
@@ -291,6 +292,28 @@ class NativeLane:
             yield
         finally:
             self.lane.pause(False)
+
+    @contextlib.contextmanager
+    def gated(self, queries):
+        """A Python cycle runs while the lane keeps placing pods, except pods matching
+        ``queries`` (the native terms the cycle's plugins are sensitive to; a conjunctive query
+        gates each of its terms: a superset). The gates are sent, then the lane is parked for
+        a moment — it applies them, finishes any run, and evicts queued matching pods to
+        Python — and released: from then on every lane pod the cycle could care about is
+        reserved (the census shows it) or handed to the Python queue."""
+        terms = tuple(t for q in queries for t in q)
+        if not terms:
+            yield
+            return
+        self._temp_terms = terms
+        try:
+            self.refresh_gates()
+            self.lane.pause(True)
+            self.lane.pause(False)
+            yield
+        finally:
+            self._temp_terms = ()
+            self.refresh_gates()
 
     # ------------------------------------------------------------------ counters
     def pending(self) -> int:

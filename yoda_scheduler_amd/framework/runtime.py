@@ -126,6 +126,23 @@ class Framework:
         """Native terms of the active selector gates: a pod matching one is not for the lane."""
         return tuple(t for p in self._term_gates for t in p.gate_terms())
 
+    def own_gate_terms(self, pod) -> Optional[list]:
+        """The lane gates (native queries) under which ``pod``'s Python cycle may run while
+        the lane keeps placing other pods: every applying Python plugin must either ignore
+        other pods or declare the pods it is sensitive to (``own_gate_terms``). None when a
+        plugin cannot say (the lane must be parked for the whole cycle)."""
+        out: list = []
+        for p in self.pre_filter + self.filter_py + [q for q, _ in self.score_py] + self.pre_score + self.reserve \
+                + self.permit:
+            if not self._applies(p, pod):
+                continue
+            f = getattr(p, "own_gate_terms", None)
+            if f is not None:
+                out.extend(f(pod))
+            elif getattr(p, "reads_flags", None) is None:
+                return None
+        return out
+
     def needs_lane_mirror(self, pod, lane_never_flags: int) -> bool:
         """Does a Python plugin that applies to ``pod`` read other pods in a way only a Python
         copy of the lane's pods can serve? Plugins declare ``reads_flags``: the features of

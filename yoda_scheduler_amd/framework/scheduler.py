@@ -168,7 +168,7 @@ class Scheduler:
         self.leading = asyncio.Event()
         self._pending_binds = 0
         self.lane = None                   # framework.lane.NativeLane (native transport only)
-        self._lane_held = False
+        self._lane_held = ""                      # "held": lane parked (+ mirror); "gated": lane gated
         self.batching = config.batch_size > 1
         self.tracer = Tracer() if config.trace else None
         from .extender import HTTPExtender
@@ -571,15 +571,20 @@ class Scheduler:
             with fw.memo_cycle(pi):
                 return self.schedule_one(pi)
         if self.lane is not None and not fw.native_for(pi) and not self._lane_held:
-            # Python plugins read other pods, lane pods included: the lane is parked and its
-            # pods mirrored for the whole cycle (upstream scheduleOne is serial), so no lane pod
-            # can be placed between the mirror and this pod's assume unseen by its filters
-            self._lane_held = True
+            # Python plugins read other pods, lane pods included. Either the lane is gated — it
+            # takes no pod the cycle's plugins are sensitive to (a pod matching this pod's
+            # anti-affinity terms or spread selectors) and keeps placing the others — or, when a
+            # plugin cannot declare that, parked (and mirrored) for the whole cycle, as upstream's
+            # serial scheduleOne: either way no lane pod this pod's filters would have rejected
+            # can be placed between their view of the cluster and this pod's assume
+            mirror = fw.needs_lane_mirror(pi, self.cache.lane_never_flags)
+            terms = None if mirror else fw.own_gate_terms(pi)
+            self._lane_held = "held" if terms is None else "gated"
             try:
-                with self.lane.held(sync=fw.needs_lane_mirror(pi, self.cache.lane_never_flags)):
+                with (self.lane.held(sync=mirror) if terms is None else self.lane.gated(terms)):
                     return self.schedule_one(pi)
             finally:
-                self._lane_held = False
+                self._lane_held = ""
         self._clear_nominations_for((pi,))       # the preemptor competes with its own hold gone
         self._activate(fw)
         cycle = self.queue.scheduling_cycle
@@ -778,13 +783,14 @@ class Scheduler:
         if state is None:
             state = CycleState()
         if unschedulable and fw.post_filter:
-            if self.lane is not None and not self._lane_held:
-                self._lane_held = True
+            if self.lane is not None and self._lane_held != "held" and pi.priority > self.lane.preempt_above(fw):
+                prev = self._lane_held
+                self._lane_held = "held"
                 try:
                     with self.lane.held():        # mirror lane pods, park the lane: ledger what-ifs
                         return self._fail(fw, state, pi, cycle, msg, t0, unschedulable)
                 finally:
-                    self._lane_held = False
+                    self._lane_held = prev
             for p in fw.post_filter:
                 try:
                     r, st = p.post_filter(state, pi, {})

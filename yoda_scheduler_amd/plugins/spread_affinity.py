@@ -178,6 +178,11 @@ class PodTopologySpread(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlug
             return []
         return _parse_constraints(self.default_constraints, action, sel)
 
+    def own_gate_terms(self, pod) -> list:
+        """Native queries the lane must not place pods matching while this pod's cycle runs
+        unparked: its hard constraints' selectors (a matching lane pod would change a skew)."""
+        return [sel.native_query([pod.namespace]) for _k, _s, sel in self._constraints(pod, "DoNotSchedule")]
+
     def _qualified_nodes(self, pod, constraints):
         """Nodes that pass the pod's node affinity and carry every topology key."""
         for name, info in self.handle.cache.nodes.items():
@@ -369,6 +374,12 @@ class InterPodAffinity(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugi
         """The gate as selectors: only pods matching one of these terms (a bound pod's required
         anti-affinity) are affected by it; the native lane keeps taking all others."""
         return [sel.native(ns) for ns, sel in self.handle.cache.anti_terms()]
+
+    def own_gate_terms(self, pod) -> list:
+        """Native queries the lane must not place pods matching while this pod's cycle runs
+        unparked: its required anti-affinity terms (a matching lane pod landing in the chosen
+        domain would violate them). Affinity terms need no gate: more matches only help."""
+        return [[_native_term(t, pod.namespace)] for t, _ in _terms(pod, "podAntiAffinity", True)]
 
     def is_noop_for(self, pod) -> bool:
         aff = _spec(pod).get("affinity") or {}
