@@ -570,6 +570,14 @@ PYBIND11_MODULE(_yoda_core, m) {
            },
            py::arg("engine"), py::arg("name"), py::arg("enabled"), py::arg("flag_mask"), py::arg("annotate"),
            py::arg("preempt_above") = INT64_MIN, py::arg("gate_terms") = py::list())
+      .def("set_gates",
+           [](Lane& l, const std::string& name, const py::list& gate_terms) {
+             std::vector<MatchTerm> v;
+             for (auto t : gate_terms) v.push_back(match_term(t));
+             return l.set_gates(name, std::move(v));
+           },
+           py::arg("name"), py::arg("gate_terms"),
+           "replace a declared profile's selector gates only (no engine-config snapshot)")
       .def("set_active", &Lane::set_active)
       .def("move", &Lane::move, py::arg("node") = -1,
            "move request: -1 moves every parked lane pod; a node index is a queueing hint for that node")

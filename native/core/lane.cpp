@@ -254,6 +254,21 @@ void Lane::set_profile(const Profile& p) {
   in_cv_.notify_one();
 }
 
+bool Lane::set_gates(const std::string& name, std::vector<MatchTerm> terms) {
+  {
+    std::lock_guard<std::mutex> g(prof_mu_);
+    auto it = std::find_if(profiles_.begin(), profiles_.end(), [&](const Profile& x) { return x.name == name; });
+    if (it == profiles_.end()) return false;
+    it->gate_terms = std::move(terms);
+  }
+  std::lock_guard<std::mutex> g(in_mu_);
+  Item it;
+  it.k = Item::kProfiles;
+  push_locked(std::move(it));
+  in_cv_.notify_one();
+  return true;
+}
+
 void Lane::set_active(bool on) {
   std::lock_guard<std::mutex> g(in_mu_);
   active_.store(on);

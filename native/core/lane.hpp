@@ -155,6 +155,9 @@ class Lane : public yk::PodSink {
   // ---- configuration (Python thread)
   void set_port(yk::PodPort* p) { port_.store(p); }
   void set_profile(const Profile& p);          // replaces a profile of the same name
+  // only the selector gates of a declared profile (no engine-config snapshot); false if the
+  // lane has no profile of that name
+  bool set_gates(const std::string& name, std::vector<MatchTerm> terms);
   void set_active(bool on);                    // leader: schedule; otherwise only keep the store
   void set_node_cards(const std::string& node, std::vector<std::pair<std::string, std::string>> vis);
   void remove_node_cards(const std::string& node);

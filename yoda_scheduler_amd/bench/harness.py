@@ -321,9 +321,9 @@ class HttpShard:
             return not q._active_entries and sched.pending_binds == 0 and \
                 bound + len(q._unsched) + len(q._backoff_pods) + waiting >= n
         if sched.lane is not None:
-            # woken when the lane's count crosses the burst; a burst with unschedulable pods
-            # never gets there, so the parked check runs between short waits
-            target = sched.lane.lane.scheduled + n - (sched.scheduled - done0)
+            # woken when the acknowledged count (lane + Python path) crosses the burst; a burst
+            # with unschedulable pods never gets there, so the parked check runs between waits
+            target = done0 + n
             while time.monotonic() < deadline:
                 if await sched.lane.wait_scheduled(target, min(0.02, max(0.0, deadline - time.monotonic()))):
                     break

@@ -204,9 +204,10 @@ class SchedulerCache:
     def pods_with_required_anti_affinity(self) -> int:
         """Bound/assumed pods whose required anti-affinity can reject new pods (symmetry)."""
         if self._anti:
-            n = len(self._anti)
-            self._anti &= self.pods.keys()
-            if len(self._anti) != n:
+            pods = self.pods
+            gone = [u for u in self._anti if u not in pods]   # O(holders), not O(pods)
+            if gone:
+                self._anti.difference_update(gone)
                 self._anti_terms = None
         return len(self._anti)
 

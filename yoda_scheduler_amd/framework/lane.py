@@ -171,28 +171,43 @@ class NativeLane:
             terms = fw.gate_terms() + self._temp_terms
             if terms == want[4]:
                 continue
-            new = want[:4] + (terms,)
-            s._activate(fw)
-            self.lane.set_profile(s.engine, name, new[0], new[1], new[2], new[3], list(terms))
-            self._profiles[name] = new
+            self.lane.set_gates(name, list(terms))
+            self._profiles[name] = want[:4] + (terms,)
 
     # ------------------------------------------------------------------ lane output
     async def wait_scheduled(self, target: int, timeout: float) -> bool:
-        """Until ``target`` lane Bindings are acknowledged (the lane wakes the loop when the
-        count crosses it: no polling), or ``timeout``."""
-        if self.lane.scheduled >= target:
+        """Until ``target`` Bindings are acknowledged on either path (``Scheduler.scheduled``:
+        the lane's count plus the Python path's), or ``timeout``. The lane wakes the loop when
+        its own count crosses ``target`` minus the Python path's (no polling); a Python-path
+        bind re-checks and moves that watermark (``python_bound``)."""
+        if self.s.scheduled >= target:
             return True
         fut = asyncio.get_event_loop().create_future()
         self._waiters.append((target, fut))
-        self.lane.set_watermark(min(t for t, _ in self._waiters))
+        self._set_watermark()
         try:
             await asyncio.wait_for(asyncio.shield(fut), timeout)
             return True
         except asyncio.TimeoutError:
-            return self.lane.scheduled >= target
+            return self.s.scheduled >= target
         finally:
             self._waiters = [(t, f) for t, f in self._waiters if f is not fut]
-            self.lane.set_watermark(min((t for t, _ in self._waiters), default=(1 << 64) - 1))
+            self._set_watermark()
+
+    def _set_watermark(self) -> None:
+        # the lane signals when its own count reaches the nearest total target less the
+        # Python path's binds so far
+        if self._waiters:
+            self.lane.set_watermark(max(0, min(t for t, _ in self._waiters) - self.s._scheduled))
+        else:
+            self.lane.set_watermark((1 << 64) - 1)
+
+    def python_bound(self) -> None:
+        """A Python-path Binding was acknowledged: wake waiters it satisfies, lower the lane's
+        watermark for the rest."""
+        if self._waiters:
+            self._wake_waiters()
+            self._set_watermark()
 
     async def wait_unowned(self, timeout: float) -> bool:
         """Until the lane owns no pod (e.g. every pod of a burst deleted and released), or
@@ -215,7 +230,7 @@ class NativeLane:
         return True
 
     def _wake_waiters(self) -> None:
-        n = self.lane.scheduled
+        n = self.s.scheduled
         for t, f in self._waiters:
             if n >= t and not f.done():
                 f.set_result(None)

@@ -177,13 +177,15 @@ class Framework:
         m = self._flag_mask
         if m is not None and not (pod.flags & m) and not any(g() for g in self._gates):
             return True
+        # every conditional plugin a no-op for the pod: the declared-flags test first (what
+        # ``_applies`` does at every extension point), ``is_noop_for`` only past it
         memo = pod.applies_memo
         if memo is not None:
             r = memo.get("native")
             if r is None:
-                r = memo["native"] = all(p.is_noop_for(pod) for p in self.conditional)
+                r = memo["native"] = not any(self._applies(p, pod) for p in self.conditional)
             return r
-        return all(p.is_noop_for(pod) for p in self.conditional)
+        return not any(self._applies_now(p, pod) for p in self.conditional)
 
     @staticmethod
     def _applies(p, pod) -> bool:

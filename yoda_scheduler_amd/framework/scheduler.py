@@ -1123,6 +1123,8 @@ class Scheduler:
                 now = time.perf_counter()
                 self.cache.finish_binding(pi)
                 self._scheduled += 1
+                if self.lane is not None:
+                    self.lane.python_bound()
                 if self.e2e_samples is not None:
                     self.e2e_samples.append(now - t0)
                 if self._metrics_on:
@@ -1150,6 +1152,8 @@ class Scheduler:
             self.cache.finish_binding(pi)
             fw.run_post_bind(state, pi, node)
             self._scheduled += 1
+            if self.lane is not None:
+                self.lane.python_bound()
             if self.e2e_samples is not None:
                 self.e2e_samples.append(time.perf_counter() - t0)
             m.child(m.e2e, "scheduled", fw.name).observe(time.perf_counter() - t0)
@@ -1163,6 +1167,8 @@ class Scheduler:
                 # client timeout): the pod is bound, so neither forget it (its reservation
                 # is real) nor retry it (upstream ForgetPod refuses pods no longer assumed)
                 self._scheduled += 1
+                if self.lane is not None:
+                    self.lane.python_bound()
                 log.info("bind %s → %s answered %s after its echo confirmed it; kept as bound",
                          pi.key, node, st.message())
                 return

@@ -61,19 +61,20 @@ def read_batch_trace(engine, max_pods: int = 256) -> list[dict]:
 
 
 COUNTERS = ("dispatches", "kbatch_dispatches", "kbatch_pods", "abandoned", "busy_refusals", "kbatch_us",
-            "drain_queries", "drain_query_us", "abandon_wait_us")
+            "drain_queries", "drain_query_us", "abandon_wait_us", "presleeps", "wait_us_per_pod")
 
 
 def counters(engine) -> dict:
     """The device context's counters: every kernel dispatch, k_batch dispatches and the pods
     they placed, calls abandoned at the host deadline, calls refused while an abandoned one
-    drained, and k_batch GPU time in µs (accumulated while ``engine.device_set_timing(True)``)."""
+    drained, k_batch GPU time in µs (accumulated while ``engine.device_set_timing(True)``), and
+    the host's batch wait: pre-sleeps taken and the smoothed wall µs per pod they are sized by."""
     lib = hip_lib()
     declare(lib)
     buf = (ctypes.c_double * len(COUNTERS))()
     if lib.yoda_dev_counters(engine.device_ctx, buf, len(COUNTERS)) != 0:
         raise RuntimeError("yoda_dev_counters failed (device scorer not enabled?)")
-    return {k: (buf[i] if k.endswith("_us") else int(buf[i])) for i, k in enumerate(COUNTERS)}
+    return {k: (buf[i] if k.endswith("_us") or k.endswith("_per_pod") else int(buf[i])) for i, k in enumerate(COUNTERS)}
 
 
 def enable(engine, device: int = 0, capacity: int = 65536, min_nodes: int = 256) -> None:

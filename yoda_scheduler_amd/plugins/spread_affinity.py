@@ -365,6 +365,7 @@ class InterPodAffinity(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugi
     def __init__(self, args=None, handle=None) -> None:
         super().__init__(args, handle)
         self.hard_weight = int(self.args.get("hardPodAffinityWeight", 1))
+        self._gt_src, self._gt = None, []          # gate_terms() of the cache's current term list
 
     def cluster_active(self) -> bool:
         """Bound pods with required anti-affinity can reject a new pod (symmetry)."""
@@ -373,7 +374,10 @@ class InterPodAffinity(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugi
     def gate_terms(self) -> list:
         """The gate as selectors: only pods matching one of these terms (a bound pod's required
         anti-affinity) are affected by it; the native lane keeps taking all others."""
-        return [sel.native(ns) for ns, sel in self.handle.cache.anti_terms()]
+        src = self.handle.cache.anti_terms()
+        if src is not self._gt_src:            # the cache rebuilds the list when a holder changes
+            self._gt_src, self._gt = src, [sel.native(ns) for ns, sel in src]
+        return self._gt
 
     def own_gate_terms(self, pod) -> list:
         """Native queries the lane must not place pods matching while this pod's cycle runs
