@@ -23,6 +23,7 @@ for s in $STEPS; do
     bench) step bench 600 python bench.py ;;
     bench5) step bench5 600 python bench.py --config 5 ;;
     bench6on) step bench6_on 600 python bench.py --config 6 --steps 3 --warmup 1 --device on ;;
+    c6cpu) step c6cpu 600 python bench.py --config 6 --steps 10 --warmup 2 --alt none ;;   # 10k pods: finer thread-CPU ticks
     bench6off) step bench6_off 600 python bench.py --config 6 --steps 3 --warmup 1 --device off ;;
     benchref) step bench_refqps 600 python bench.py --steps 2 --warmup 0 --reference-qps ;;
     benchhttp) step bench_http 600 python bench.py --transport http --steps 20 --warmup 5 ;;

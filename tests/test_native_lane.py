@@ -611,3 +611,50 @@ def test_gated_cycle_never_lets_the_lane_violate_a_concurrent_anti_affinity_pod(
     web_bound = [n for n, v in nodes.items() if n.startswith("web") and v]
     assert all(nodes[f"api{i}"] == "n1" for i in range(40))
     assert not (nodes["anti"] and web_bound), (nodes["anti"], len(web_bound))
+
+
+def test_wait_scheduled_counts_bindings_of_both_paths():
+    """A burst some of whose pods take the Python path (hybrid cycles) completes when the
+    acknowledged Bindings of BOTH paths reach the target: the lane's watermark is the target
+    less the Python path's binds, and a Python-path bind wakes the waiter itself. (A lane-only
+    target made a mixed burst wait out its 20 ms timeout: 42 k instead of ~135 k pods/s.)"""
+    from yoda_scheduler_amd.framework.lane import NativeLane
+
+    class FakeCore:
+        def __init__(self):
+            self.scheduled = 0
+            self.marks = []
+
+        def set_watermark(self, n):
+            self.marks.append(n)
+
+    class FakeSched:
+        def __init__(self, core):
+            self._scheduled = 0
+            self.core = core
+
+        @property
+        def scheduled(self):
+            return self._scheduled + self.core.scheduled
+
+    async def run():
+        core = FakeCore()
+        s = FakeSched(core)
+        nl = object.__new__(NativeLane)
+        nl.s, nl.lane, nl._waiters = s, core, []
+        core.scheduled = 990                  # the lane bound its 990 pods
+        w = asyncio.ensure_future(nl.wait_scheduled(1000, 5.0))
+        await asyncio.sleep(0)
+        assert core.marks[-1] == 1000          # nothing from Python yet: the lane needs them all
+        for _ in range(9):
+            s._scheduled += 1
+            nl.python_bound()
+        assert core.marks[-1] == 1000 - 9 and not w.done()
+        t0 = time.monotonic()
+        s._scheduled += 1
+        nl.python_bound()                      # the 10th Python-path bind completes the burst
+        assert await asyncio.wait_for(w, 1.0) is True
+        assert time.monotonic() - t0 < 0.5
+        assert core.marks[-1] == (1 << 64) - 1  # no waiter left: watermark off
+
+    asyncio.run(run())
