@@ -66,6 +66,7 @@ class NativeLane:
         self._unowned_waiters: list = []   # futures resolved once the lane owns no pod
         self._draining = False             # applying the lane's own move request (not echoed back)
         self._temp_terms: tuple = ()        # gates of a Python cycle running beside the lane (gated)
+        self._in_gated = False             # inside gated(): anti-affinity changes wait for its exit
         sched.queue.on_move_all = self._move_all
 
     # ------------------------------------------------------------------ lifecycle
@@ -163,6 +164,8 @@ class NativeLane:
         """Only the selector gates changed (a pod with required anti-affinity was assumed or
         left): re-send the terms of the profiles the lane runs — eligibility itself does not
         depend on them (``Framework.native_mask(lane=True)``)."""
+        if self._in_gated:
+            return                             # gated() re-sends the gates when the cycle ends
         s = self.s
         for name, fw in s.frameworks.items():
             want = self._profiles.get(name)
@@ -325,8 +328,12 @@ class NativeLane:
             self.refresh_gates()
             self.lane.pause(True)
             self.lane.pause(False)
+            # the cycle's own assume may add gate terms (its required anti-affinity): they are
+            # sent once, with the temporary terms dropped, when the cycle ends
+            self._in_gated = True
             yield
         finally:
+            self._in_gated = False
             self._temp_terms = ()
             self.refresh_gates()
 

@@ -132,10 +132,7 @@ class Framework:
         other pods or declare the pods it is sensitive to (``own_gate_terms``). None when a
         plugin cannot say (the lane must be parked for the whole cycle)."""
         out: list = []
-        for p in self.pre_filter + self.filter_py + [q for q, _ in self.score_py] + self.pre_score + self.reserve \
-                + self.permit:
-            if not self._applies(p, pod):
-                continue
+        for p in self._act(self._py_points(), pod):
             f = getattr(p, "own_gate_terms", None)
             if f is not None:
                 out.extend(f(pod))
@@ -149,10 +146,7 @@ class Framework:
         other pods they read (pods of the lane never carry ``lane_never_flags``); plugins that
         count pods by selector do the lane's natively (``reads_flags = 0``). A plugin without
         the declaration (or preemption) needs the mirror."""
-        for p in self.pre_filter + self.filter_py + [q for q, _ in self.score_py] + self.pre_score + self.reserve \
-                + self.permit:
-            if not self._applies(p, pod):
-                continue
+        for p in self._act(self._py_points(), pod):
             rf = getattr(p, "reads_flags", None)
             if rf is None or rf & ~lane_never_flags:
                 return True
@@ -186,6 +180,26 @@ class Framework:
                 r = memo["native"] = not any(self._applies(p, pod) for p in self.conditional)
             return r
         return not any(self._applies_now(p, pod) for p in self.conditional)
+
+    def _py_points(self) -> list:
+        """Every plugin of the Python extension points a cycle runs (built once)."""
+        pts = self.__dict__.get("_py_points_l")
+        if pts is None:
+            pts = self._py_points_l = (self.pre_filter + self.filter_py + [q for q, _ in self.score_py]
+                                       + self.pre_score + self.reserve + self.permit)
+        return pts
+
+    def _act(self, plugins: list, pod) -> list:
+        """The plugins of ``plugins`` (an extension point's list) that apply to ``pod``; within a
+        cycle (``memo_cycle``) computed once per point."""
+        memo = pod.applies_memo
+        if memo is None:
+            return [p for p in plugins if self._applies_now(p, pod)]
+        k = ("act", id(plugins))
+        r = memo.get(k)
+        if r is None:
+            r = memo[k] = [p for p in plugins if self._applies(p, pod)]
+        return r
 
     @staticmethod
     def _applies(p, pod) -> bool:
@@ -249,9 +263,7 @@ class Framework:
 
     # ------------------------------------------------------------------ Python points
     def run_pre_filter(self, state: CycleState, pod) -> Status:
-        for p in self.pre_filter:
-            if not self._applies(p, pod):
-                continue
+        for p in self._act(self.pre_filter, pod):
             st = p.pre_filter(state, pod)
             if not st.is_success():
                 st.plugin = st.plugin or p.name
@@ -270,7 +282,7 @@ class Framework:
         return bool(ok)
 
     def has_active_filter_py(self, pod) -> bool:
-        return any(self._applies(p, pod) for p in self.filter_py)
+        return bool(self._act(self.filter_py, pod))
 
     def run_filter_py(self, state: CycleState, pod, nodes: list[str],
                       limit: Optional[int] = None) -> tuple[list[str], dict]:
@@ -279,7 +291,7 @@ class Framework:
         if not self.filter_py:
             return nodes, {}
         out, failed = [], {}
-        active = [p for p in self.filter_py if self._applies(p, pod)]
+        active = self._act(self.filter_py, pod)
         if not active:
             return nodes, {}
         for n in nodes:
@@ -296,9 +308,7 @@ class Framework:
 
     def run_score_py(self, state: CycleState, pod, nodes: list[str]) -> list[int]:
         total = [0] * len(nodes)
-        for p in self.pre_score:
-            if not self._applies(p, pod):
-                continue
+        for p in self._act(self.pre_score, pod):
             st = p.pre_score(state, pod, nodes)
             if not st.is_success():
                 raise RuntimeError(f"preScore {p.name}: {st.message()}")
@@ -322,7 +332,7 @@ class Framework:
         return total
 
     def run_reserve(self, state: CycleState, pod, node: str) -> Status:
-        active = [p for p in self.reserve if self._applies(p, pod)]
+        active = self._act(self.reserve, pod)
         for i, p in enumerate(active):
             st = p.reserve(state, pod, node)
             if not st.is_success():
@@ -341,9 +351,7 @@ class Framework:
         the binding cycle awaits it)."""
         from .interfaces import Code, WaitingPod
         wait, waiters = 0.0, set()
-        for p in self.permit:
-            if not self._applies(p, pod):
-                continue
+        for p in self._act(self.permit, pod):
             st, t = p.permit(state, pod, node)
             if st.code == Code.WAIT:
                 waiters.add(p.name)
