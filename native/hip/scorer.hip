@@ -28,6 +28,7 @@
 #include <atomic>
 #include <chrono>
 #include <climits>
+#include <cstddef>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -933,6 +934,16 @@ struct BatchArgs {
   unsigned int* abort_word;
   unsigned long long* trace;          // optional: block 0's phase stamps, kTracePts per pod
 };
+constexpr int kResWords = (int)(sizeof(yoda_dev_result_t) / 8);
+static_assert(kResWords == 19 && YODA_DEV_REASONS == 16 && offsetof(yoda_dev_result_t, feasible) == 4 &&
+                  offsetof(yoda_dev_result_t, score) == 8 && offsetof(yoda_dev_result_t, mask) == 16 &&
+                  offsetof(yoda_dev_result_t, quality) == 20 && offsetof(yoda_dev_result_t, reasons) == 24 &&
+                  offsetof(yoda_dev_result_t, maxima) == 88 && offsetof(yoda_dev_result_t, raw_lo) == 136 &&
+                  offsetof(yoda_dev_result_t, raw_hi) == 144,
+              "the publish step's word layout");
+// the reason codes of c_batch_reasons, for compile-time indexing
+constexpr int kBatchReasonCodes[7] = {RS_UNSCHEDULABLE, RS_RESOURCES, RS_NO_SCV, RS_STALE, RS_GPU_NUMBER,
+                                      RS_GPU_FIT, RS_DEAD};
 constexpr int kTracePts = 16;   // 9 phase stamps per pod (block 0), padded
 constexpr int kReqWords = sizeof(yoda_dev_req_t) / 4;
 static_assert(sizeof(yoda_dev_req_t) % 4 == 0 && kReqWords <= 64, "req fits one wave");
@@ -1094,14 +1105,11 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
 
   bool ok = true;
   for (int b = 0; b < a.B && ok; ++b) {
-    // the request in scalar registers (block-uniform): one LDS read per word per pod
-    union {
-      yoda_dev_req_t req;
-      uint32_t w[kReqWords];
-    } ru;
-#pragma unroll
-    for (int k = 0; k < kReqWords; ++k) ru.w[k] = __builtin_amdgcn_readfirstlane(s_req[b & 1][k]);
-    const yoda_dev_req_t& r = ru.req;
+    // the request is read from LDS where it is used (uniform address: a broadcast read).
+    // Copying all 49 words into scalar registers for the whole pod measured slower — the
+    // copy spilled other scalars (167 vs 131 SGPR spills): 13.7 vs 13.2 µs/pod at 256 nodes,
+    // 16.05 vs 15.9 at 4096 (profiles/device/r4/kernel_ab_r4/)
+    const yoda_dev_req_t& r = *reinterpret_cast<const yoda_dev_req_t*>(s_req[b & 1]);
     const uint32_t tag1 = a.tag0 + 3u * (uint32_t)b, tag2 = tag1 + 1u, tag3 = tag1 + 2u;
     // prefetch request b+1 (lands while this pod's phases run; stored to LDS at the end)
     uint32_t pre = 0;
@@ -1154,9 +1162,10 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         int64_t total_v = 0;
         uint32_t mask_v = 0;
         int32_t quality_v = 0;
-        GangBest gb;
+        // a replica's best goes straight to its LDS slot (a pointer to a local would put
+        // the struct in scratch memory)
         score_node_a(s_rows + (j < cnt ? j : 0), act, emask, r, sc, s_masks, sub, rbase, total_v, mask_v, quality_v,
-                     rep, nrep, nrep > 1 ? &gb : nullptr);
+                     rep, nrep, nrep > 1 ? &s_gang[rep * npb + j] : nullptr);
         if (act && sub == 0) {
           if (rep == 0) {
             s_raw[j] = (int64_t)rbase;
@@ -1164,7 +1173,6 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
             s_mask[j] = (uint8_t)mask_v;
             s_quality[j] = quality_v;
           }
-          if (nrep > 1) s_gang[rep * npb + j] = gb;   // < nrep·npb ≤ 8·BW
         }
       }
       if (nrep > 1) {
@@ -1340,20 +1348,16 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       node = (int)(((p - r.perm_add) * r.perm_inv) & 0xFFFFFFu);
     }
     const bool owner = nf > 0 ? (node >= base && node < base + cnt) : g == 0;
-    if (owner && tid == 0) {
-      yoda_dev_result_t res;
-      res.feasible = nf;
-      res.node = node;
-      if (nf > 0) {
-        const int j = node - base;
-        res.score = nf == 1 ? 0 : (int64_t)(key >> 24);
-        res.mask = s_mask[j];
-        res.quality = s_quality[j];
+    if (owner) {
+      const int j = nf > 0 ? node - base : 0;
+      const uint32_t mask = nf > 0 ? (uint32_t)s_mask[j] : 0u;
+      const int32_t quality = nf > 0 ? s_quality[j] : 0;
+      if (tid == 0 && nf > 0) {
         // assume (engine.cpp Engine::reserve, non-compat, reservation pending)
         yoda_dev_node_t* nd = s_rows + j;
         const uint32_t mb = (uint32_t)r.memory;
         for (int c = 0; c < YODA_DEV_CARDS; ++c)
-          if ((res.mask >> c) & 1u) {
+          if ((mask >> c) & 1u) {
             nd->cards[c].reserved += mb;
             nd->cards[c].pending += mb;
           }
@@ -1363,18 +1367,27 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         nd->nz_cpu += r.nz_cpu_m;
         nd->nz_mem += r.nz_mem;
         s_dirty[j] = 1;
-      } else {
-        res.score = 0;
-        res.mask = 0;
-        res.quality = 0;
       }
-      for (int k = 0; k < YODA_DEV_REASONS; ++k) res.reasons[k] = 0;
+      // the result: lane k of wave 0 writes its 64-bit word k, every value selected with
+      // constant indices (a local struct with the reasons array indexed by reason code lived in
+      // scratch memory: ~30 scratch accesses and vmcnt waits on the owner's path each pod)
+      if (tid < kResWords) {
+        uint64_t w = 0;
+        if (tid == 0) w = (uint64_t)(uint32_t)node | ((uint64_t)(uint32_t)nf << 32);
+        if (tid == 1) w = (uint64_t)(nf > 1 ? (int64_t)(key >> 24) : 0);   // a lone feasible node scores 0
+        if (tid == 2) w = (uint64_t)mask | ((uint64_t)(uint32_t)quality << 32);
 #pragma unroll
-      for (int q = 0; q < 7; ++q) res.reasons[c_batch_reasons[q]] = reasons7[q];
-      for (int k = 0; k < 6; ++k) res.maxima[k] = gmx[k];
-      res.raw_lo = (int64_t)glo;
-      res.raw_hi = (int64_t)ghi;
-      a.res[b] = res;
+        for (int q = 0; q < 7; ++q) {   // reasons[code] as u32 pairs in words 3..10
+          const int code = kBatchReasonCodes[q];
+          if (tid == 3 + code / 2) w |= (uint64_t)(uint32_t)reasons7[q] << (32 * (code & 1));
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+          if (tid == 11 + k) w = gmx[k];
+        if (tid == 17) w = glo;
+        if (tid == 18) w = ghi;
+        reinterpret_cast<unsigned long long*>(a.res + b)[tid] = w;
+      }
     }
     __syncthreads();
     TRACE(8);

@@ -65,6 +65,9 @@ for s in $STEPS; do
       for k in 1 2; do
         step "kbab/new_$k" 200 python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
         step "kbab/base_$k" 200 env YODA_HIP_LIB=abbin/libyoda_hip_base.so python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
+        if [ -f abbin/libyoda_hip_v2.so ]; then
+          step "kbab/v2_$k" 200 env YODA_HIP_LIB=abbin/libyoda_hip_v2.so python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
+        fi
       done ;;
     mixlog) step mixlog 300 env YODA_BENCH_RUNLOG=1 python bench.py --config 3 --mix-anti 10 --steps 5 --warmup 3 --alt none ;;
     scope6) step scope6 300 env YODA_BENCH_THREADS=2 python bench.py --config 6 --steps 5 --warmup 1 --alt none ;;
