@@ -58,6 +58,8 @@ def main() -> int:
             return burst
         cls.burst = wrap(orig)
     bench.main(args)
+    if os.environ.get("YODA_PROF_DUMP"):
+        pr.dump_stats(os.environ["YODA_PROF_DUMP"])
     st = pstats.Stats(pr)
     total = sum(v[2] for v in st.stats.values())
     groups = {name: 0.0 for name, _ in STAGES}

@@ -182,11 +182,15 @@ class Framework:
         return not any(self._applies_now(p, pod) for p in self.conditional)
 
     def _py_points(self) -> list:
-        """Every plugin of the Python extension points a cycle runs (built once)."""
+        """Every plugin of the Python extension points a cycle runs, each once (built once: a
+        plugin at several points would otherwise declare its gate terms several times)."""
         pts = self.__dict__.get("_py_points_l")
         if pts is None:
-            pts = self._py_points_l = (self.pre_filter + self.filter_py + [q for q, _ in self.score_py]
-                                       + self.pre_score + self.reserve + self.permit)
+            seen: set = set()
+            pts = self._py_points_l = [
+                p for p in (self.pre_filter + self.filter_py + [q for q, _ in self.score_py] + self.pre_score
+                            + self.reserve + self.permit)
+                if not (id(p) in seen or seen.add(id(p)))]
         return pts
 
     def _act(self, plugins: list, pod) -> list:
