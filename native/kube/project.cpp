@@ -554,24 +554,37 @@ struct Skim {
   void ws() {
     while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
   }
+  // any byte of an 8-byte word that is '"' or '\\' (SWAR: most strings here are short, so a
+  // word at a time beats a memchr call per string)
+  static bool quote_or_bs(uint64_t w) {
+    constexpr uint64_t ones = 0x0101010101010101ull, highs = 0x8080808080808080ull;
+    const uint64_t q = w ^ (ones * '"'), b = w ^ (ones * '\\');
+    return (((q - ones) & ~q) | ((b - ones) & ~b)) & highs;
+  }
   // p at '"': the raw content, whether it holds a backslash; p past the closing quote
   bool str(std::string_view* out, bool* esc) {
     if (p >= e || *p != '"') return false;
     const char* s = ++p;
     bool bs = false;
     for (;;) {
-      const char* q = static_cast<const char*>(std::memchr(p, '"', size_t(e - p)));
-      if (!q) return false;
-      size_t n = 0;
-      for (const char* b = q; b > s && b[-1] == '\\'; --b) ++n;
-      if (n) bs = true;
-      if ((n & 1) == 0) {
-        *out = std::string_view(s, size_t(q - s));
-        *esc = bs || std::memchr(s, '\\', size_t(q - s)) != nullptr;
-        p = q + 1;
-        return true;
+      while (e - p >= 8) {
+        uint64_t w;
+        std::memcpy(&w, p, 8);
+        if (quote_or_bs(w)) break;
+        p += 8;
       }
-      p = q + 1;
+      while (p < e && *p != '"' && *p != '\\') ++p;
+      if (p >= e) return false;
+      if (*p == '\\') {                 // an escape: skip the escaped character
+        bs = true;
+        p += 2;
+        if (p > e) return false;
+        continue;
+      }
+      *out = std::string_view(s, size_t(p - s));
+      *esc = bs;
+      ++p;
+      return true;
     }
   }
   bool skip() {
@@ -673,6 +686,35 @@ struct Skim {
 // labels_hash_of over a raw metadata.labels span (empty: no labels member); 0 when it does not parse
 uint64_t labels_span_hash(std::string_view raw) {
   if (raw.empty()) return labels_hash_of(FlatN{FlatDoc::View()});
+  {
+    // the usual shape — an object of plain strings — hashed straight from the text, in the
+    // order and with the mixing FlatDoc::View::hash uses (Obj, then per member key, Str, value,
+    // then the member count): no document is built for an echo's labels
+    Skim k{raw.data(), raw.data() + raw.size()};
+    uint64_t h = hash_mix(kLabelsSeed, FlatDoc::Obj);
+    uint64_t cnt = 0;
+    bool plain = true;
+    const bool parsed = k.object([&](std::string_view key) -> bool {
+      std::string_view v;
+      bool esc = false;
+      k.ws();
+      if (k.p >= k.e || *k.p != '"' || !k.str(&v, &esc) || esc) {
+        plain = false;
+        k.p = k.e;                    // stop: the parser below decides
+        return true;
+      }
+      h = hash_text(v, hash_mix(hash_text(key, h), FlatDoc::Str));
+      ++cnt;
+      return true;
+    });
+    if (parsed && plain) {
+      k.ws();
+      if (k.p == k.e) {
+        h = hash_mix(h, cnt);
+        return h ? h : 1;
+      }
+    }
+  }
   FlatDoc d;
   if (!d.parse(raw)) return 0;
   return labels_hash_of(FlatN{d.root()});

@@ -860,15 +860,22 @@ def test_labels_hash_agrees_across_scanner_and_projections():
                          "labels": {"app": "web", "tier": 'a"b'}},
             "spec": {"nodeName": "n1", "containers": [{"name": "c"}]}, "status": {"phase": "Running"}}
     hashes = []
-    for labels in ({"app": "web", "tier": 'a"b'}, {"app": "web", "tier": "x"}, None, {}):
+    # escaped value (parser path), plain strings (hashed from the text), none, empty, raw UTF-8,
+    # several members, an empty value, a non-string value (parser path), compact separators
+    cases = [({"app": "web", "tier": 'a"b'}, True), ({"app": "web", "tier": "x"}, True), (None, True), ({}, True),
+             ({"app": "wéb"}, False), ({"a": "1", "b": "", "c.d/e": "x-y_z"}, True), ({"n": 5}, True),
+             ({"app": "web", "tier": "x"}, "compact")]
+    for labels, ascii_ in cases:
         obj = json.loads(json.dumps(base))
         if labels is None:
             obj["metadata"].pop("labels")
         else:
             obj["metadata"]["labels"] = labels
-        raw = json.dumps(obj)
-        line = json.dumps({"type": "MODIFIED", "object": obj})
+        sep = (",", ":") if ascii_ == "compact" else None
+        raw = json.dumps(obj, ensure_ascii=bool(ascii_), separators=sep)
+        line = json.dumps({"type": "MODIFIED", "object": obj}, ensure_ascii=bool(ascii_), separators=sep)
         h_scan = k.scan_labels_hash(line)
-        assert h_scan == k.project_flat(raw).labels_hash == k.project(raw).labels_hash != 0
+        assert h_scan == k.project_flat(raw).labels_hash == k.project(raw).labels_hash != 0, labels
         hashes.append(h_scan)
-    assert len(set(hashes)) == 4
+    # the same labels hash alike whatever the whitespace; different labels differ
+    assert hashes[1] == hashes[-1] and len(set(hashes)) == len(cases) - 1
