@@ -165,7 +165,7 @@ class SchedulerCache:
             if ps.info.uid not in self._anti:
                 self._anti_parsed.pop(ps.info.uid, None)
                 self._anti.add(ps.info.uid)
-                self._anti_changed()
+                self._anti_changed(True)
         else:
             self._anti_drop(ps.info.uid)
 
@@ -173,14 +173,15 @@ class SchedulerCache:
         if uid in self._anti:
             self._anti.discard(uid)
             self._anti_parsed.pop(uid, None)
-            self._anti_changed()
+            self._anti_changed(False)
 
-    def _anti_changed(self) -> None:
+    def _anti_changed(self, grew: bool) -> None:
         """InterPodAffinity's cluster gate (required anti-affinity symmetry) may have flipped:
-        the native lane re-decides which pods it may take."""
+        the native lane re-decides which pods it may take (``grew``: a holder was added — the
+        lane must learn it before it places another pod; a removal may be applied later)."""
         self._anti_terms = None
         if self.on_anti_change is not None:
-            self.on_anti_change()
+            self.on_anti_change(grew)
 
     def hide(self, uids) -> list:
         """Drop pods from the Python-side views (``pods`` / ``node_pods`` / extended-resource

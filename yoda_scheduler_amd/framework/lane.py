@@ -67,6 +67,7 @@ class NativeLane:
         self._draining = False             # applying the lane's own move request (not echoed back)
         self._temp_terms: tuple = ()        # gates of a Python cycle running beside the lane (gated)
         self._in_gated = False             # inside gated(): anti-affinity changes wait for its exit
+        self._gates_pending = False        # a coalesced gate update (holder removals) is scheduled
         sched.queue.on_move_all = self._move_all
 
     # ------------------------------------------------------------------ lifecycle
@@ -159,6 +160,23 @@ class NativeLane:
             self._profiles[name] = want
             log.info("native lane: profile %s %s (flag mask %#x)", name, "on" if want[0] else "off", want[1])
         s.cache.lane_never_flags = never
+
+    def anti_changed(self, grew: bool = True) -> None:
+        """The bound/assumed pods with required anti-affinity changed. A new holder's terms reach
+        the lane now (it must not place a pod they reject); removals — a burst's deletions come
+        one event at a time — are coalesced into one update at the end of the loop turn (until
+        then the lane only holds back pods it could have taken: safe)."""
+        loop = self._loop
+        if grew or loop is None or loop.is_closed():
+            self.refresh_gates()
+            return
+        if not self._gates_pending:
+            self._gates_pending = True
+            loop.call_soon(self._refresh_pending_gates)
+
+    def _refresh_pending_gates(self) -> None:
+        self._gates_pending = False
+        self.refresh_gates()
 
     def refresh_gates(self) -> None:
         """Only the selector gates changed (a pod with required anti-affinity was assumed or

@@ -223,10 +223,12 @@ class Framework:
 
         @contextlib.contextmanager
         def scope():
-            if pod.applies_memo is not None:      # nested (preemption inside a cycle)
+            memo = pod.applies_memo
+            if memo is not None and not memo.pop("_adopt", False):   # nested (preemption inside a cycle)
                 yield
                 return
-            pod.applies_memo = {}
+            if memo is None:
+                pod.applies_memo = {}
             try:
                 yield
             finally:

@@ -544,7 +544,7 @@ class Scheduler:
         from .lane import NativeLane
         self.lane = NativeLane(self, self.native)
         self.cache.lane = self.lane.lane
-        self.cache.on_anti_change = self.lane.refresh_gates
+        self.cache.on_anti_change = self.lane.anti_changed
         return self.lane.lane
 
     # ================================================================== cycle
@@ -565,9 +565,13 @@ class Scheduler:
 
     def schedule_one(self, pi: PodInfo) -> None:
         fw = self.frameworks.get(pi.scheduler_name)
+        memo = pi.applies_memo
         if fw is None or self._pod_gone(pi):
+            if memo is not None and memo.get("_adopt"):
+                pi.applies_memo = None
             return
-        if pi.applies_memo is None:
+        if memo is None or memo.get("_adopt"):
+            # (a memo _batch_runs started for this pod, with nothing run in between, is adopted)
             with fw.memo_cycle(pi):
                 return self.schedule_one(pi)
         if self.lane is not None and not fw.native_for(pi) and not self._lane_held:
@@ -861,21 +865,29 @@ class Scheduler:
             log.warning("preemption: deleting %s failed: %r", v.key, e)
 
     # ================================================================== batch cycle
-    def _batch_runs(self, pods: list[PodInfo]):
+    def _batch_runs(self, pods: list[PodInfo], adopt: bool = False):
         """Split popped pods into single Python cycles (``(None, pod)``) and runs of
-        consecutive pods of an all-native profile (``(fw, [pods])``)."""
+        consecutive pods of an all-native profile (``(fw, [pods])``). ``adopt``: the consumer
+        runs each single cycle right after it is yielded (no await in between), so the plugin
+        applicability computed here for a flagged pod is handed to its cycle's memo."""
         i = 0
         masks: dict = {}           # framework → native_mask(), once per batch
         while i < len(pods):
-            fw = self.frameworks.get(pods[i].scheduler_name)
+            p = pods[i]
+            fw = self.frameworks.get(p.scheduler_name)
             if fw is not None and fw not in masks:
                 masks[fw] = fw.native_mask()
             m = masks.get(fw)
+            masked = m is not None and not (p.flags & m)
+            if adopt and fw is not None and not masked and p.applies_memo is None:
+                p.applies_memo = {"_adopt": True}
             # the mask settles the common case; flagged pods still get the per-plugin check
-            if fw is None or not ((m is not None and not (pods[i].flags & m)) or fw.native_for(pods[i])):
-                yield None, pods[i]
+            if fw is None or not (masked or fw.native_for(p)):
+                yield None, p
                 i += 1
                 continue
+            if p.applies_memo is not None and p.applies_memo.get("_adopt"):
+                p.applies_memo = None
             j = i
             run = []
             while j < len(pods) and pods[j].scheduler_name == fw.name and \
@@ -926,7 +938,7 @@ class Scheduler:
     def schedule_batch(self, pods: list[PodInfo]) -> None:
         """Schedule a run of popped pods; consecutive pods of an all-native profile go
         through one GIL-free engine call."""
-        for fw, item in self._batch_runs(pods):
+        for fw, item in self._batch_runs(pods, adopt=True):
             if fw is None:
                 self.schedule_one(item)
                 continue
