@@ -35,7 +35,9 @@ for s in $STEPS; do
     prof) step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     kbprof) step kbprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kbprof -o kb -- python3 scripts/device_batch_bench.py --nodes 4096 --pods 1032 --batch 256 --modes batch ;;
     kbtrace) step kbtrace 300 python scripts/device_batch_bench.py --nodes 4096,16384 --pods 1032 --batch 256 --modes batch --trace ;;
-    ab3)   # same-box A/B of the driver's command: this tree vs round 3's (ab_r3/, git worktree of 809b08c)
+    ab3)   # same-box A/B of the driver's command: this tree vs round 3's (ab_r3/, git worktree of 809b08c,
+           # built in place: `git worktree add ab_r3 809b08c && (cd ab_r3 && python -m yoda_scheduler_amd.ops.build)`)
+      [ -d ab_r3 ] || { echo "ab3: no ab_r3/ worktree"; exit 1; }
       mkdir -p gpurun_out/ab3
       for k in 1 2; do
         step "ab3/new_$k" 300 python bench.py --gpus 1 --steps 20 --warmup 5 --alt none
@@ -65,9 +67,11 @@ for s in $STEPS; do
       for k in 1 2; do
         step "kbab/new_$k" 200 python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
         step "kbab/base_$k" 200 env YODA_HIP_LIB=abbin/libyoda_hip_base.so python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
-        if [ -f abbin/libyoda_hip_v2.so ]; then
-          step "kbab/v2_$k" 200 env YODA_HIP_LIB=abbin/libyoda_hip_v2.so python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
-        fi
+        for v in abbin/libyoda_hip_v*.so; do   # candidate variants built from a patched copy
+          [ -f "$v" ] || continue
+          t=$(basename "$v" .so); t=${t#libyoda_hip_}
+          step "kbab/${t}_$k" 200 env YODA_HIP_LIB="$v" python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
+        done
       done ;;
     mixlog) step mixlog 300 env YODA_BENCH_RUNLOG=1 python bench.py --config 3 --mix-anti 10 --steps 5 --warmup 3 --alt none ;;
     scope6) step scope6 300 env YODA_BENCH_THREADS=2 python bench.py --config 6 --steps 5 --warmup 1 --alt none ;;
