@@ -259,11 +259,15 @@ bool Lane::set_gates(const std::string& name, std::vector<MatchTerm> terms) {
     std::lock_guard<std::mutex> g(prof_mu_);
     auto it = std::find_if(profiles_.begin(), profiles_.end(), [&](const Profile& x) { return x.name == name; });
     if (it == profiles_.end()) return false;
+    std::vector<MatchTerm> added;
+    for (const MatchTerm& t : terms)
+      if (std::find(it->gate_terms.begin(), it->gate_terms.end(), t) == it->gate_terms.end()) added.push_back(t);
     it->gate_terms = std::move(terms);
+    if (!added.empty()) gate_adds_.emplace_back(name, std::move(added));
   }
   std::lock_guard<std::mutex> g(in_mu_);
   Item it;
-  it.k = Item::kProfiles;
+  it.k = Item::kGates;
   push_locked(std::move(it));
   in_cv_.notify_one();
   return true;
@@ -714,6 +718,46 @@ void Lane::handle_relist(const std::vector<std::shared_ptr<yk::PodEv>>& items, s
     auto it = by_key_.find(key_of(ev->p));
     if (it == by_key_.end()) handle_event('A', ev, out);
     else if (it->second->ev->p.rv != ev->p.rv) handle_event('M', ev, out);
+  }
+}
+
+// A gates-only update (set_gates): the lane's profiles take the new terms; waiting pods are
+// re-checked against the ADDED terms only — a removed term cannot make a pod inadmissible, and
+// re-running every term for every waiting pod on each update cost O(waiting × terms) per
+// Python cycle while anti-affinity holders accumulate.
+void Lane::apply_gates(std::vector<Fwd>* out) {
+  std::vector<std::pair<std::string, std::vector<MatchTerm>>> adds;
+  {
+    std::lock_guard<std::mutex> g(prof_mu_);
+    adds.swap(gate_adds_);
+    for (auto& lp : lp_)
+      for (const auto& p : profiles_)
+        if (p.name == lp.name) {
+          lp.gate_terms = p.gate_terms;
+          break;
+        }
+  }
+  if (adds.empty()) return;
+  std::vector<Entry*> evict;
+  for (auto& kv : by_id_) {
+    Entry* e = kv.second;
+    if (e->st != QUEUED && e->st != PARKED && e->st != BACKOFF) continue;
+    const yk::PodProj& p = e->ev->full();
+    bool hit = false;
+    for (const auto& a : adds) {
+      if (a.first != p.sched) continue;
+      for (const MatchTerm& t : a.second)
+        if (t.matches(p)) {
+          hit = true;
+          break;
+        }
+      if (hit) break;
+    }
+    if (hit) evict.push_back(e);
+  }
+  for (Entry* e : evict) {
+    drop_owned(e, false);
+    if (!uninteresting(e->ev->p, lp_)) forward('A', e->ev, nullptr, out);
   }
 }
 
@@ -1791,6 +1835,7 @@ void Lane::run() {
           case Item::kEvent: handle_event(it.type, it.ev, &fwd); break;
           case Item::kAnswer: handle_answer(it.tag, it.status, it.body, it.t); break;
           case Item::kProfiles: apply_profiles(&fwd); break;
+          case Item::kGates: apply_gates(&fwd); break;
           case Item::kMove: pending_moves_.push_back(it.status); break;
           case Item::kRelist: {
             std::vector<Fwd> out;

@@ -80,8 +80,12 @@ struct MatchTerm {
     std::string key;
     int op = 0;                          // 0 In, 1 NotIn, 2 Exists, 3 DoesNotExist
     std::vector<std::string> values;
+    bool operator==(const Expr& o) const { return op == o.op && key == o.key && values == o.values; }
   };
   std::vector<Expr> exprs;
+  bool operator==(const MatchTerm& o) const {
+    return nothing == o.nothing && namespaces == o.namespaces && labels == o.labels && exprs == o.exprs;
+  }
   bool matches(const std::string& ns, const std::vector<std::pair<std::string, std::string>>& labels) const;
   bool matches(const yk::PodProj& p) const { return matches(p.ns, p.labels); }
 };
@@ -265,7 +269,7 @@ class Lane : public yk::PodSink {
     bool failed = false;
   };
   struct Item {             // inbox: events, answers, commands — applied in order
-    enum K : uint8_t { kEvent, kAnswer, kRelist, kProfiles, kRunDone, kMove } k = kEvent;
+    enum K : uint8_t { kEvent, kAnswer, kRelist, kProfiles, kRunDone, kMove, kGates } k = kEvent;
     char type = 0;
     std::shared_ptr<yk::PodEv> ev;
     uint64_t tag = 0;
@@ -286,6 +290,7 @@ class Lane : public yk::PodSink {
   void handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::vector<Fwd>* out);
   void handle_answer(uint64_t tag, int status, std::string& body, double t_ack);
   void handle_relist(const std::vector<std::shared_ptr<yk::PodEv>>& items, std::vector<Fwd>* out);
+  void apply_gates(std::vector<Fwd>* out);
   void drop_owned(Entry* e, bool release);
   void apply_profiles(std::vector<Fwd>* out);
   void count(St s, int d);
@@ -394,6 +399,9 @@ class Lane : public yk::PodSink {
 
   std::mutex prof_mu_;
   std::vector<Profile> profiles_;    // copied into lane-thread state on kProfiles
+  // set_gates: per profile, the terms a gate update added (only those can make a waiting pod
+  // inadmissible); taken by the lane thread on kGates (prof_mu_)
+  std::vector<std::pair<std::string, std::vector<MatchTerm>>> gate_adds_;
   std::vector<Profile> lp_;          // lane thread's view
 
   std::mutex vis_mu_;
