@@ -320,13 +320,31 @@ def _terms(pod, kind: str, required: bool):
             for w in aff.get("preferredDuringSchedulingIgnoredDuringExecution") or []]
 
 
+# parsed selectors of affinity terms, by the term dict's identity (a pod's terms are read at
+# several extension points per cycle, and against every existing pod): the entry keeps the
+# dict alive, so an id is never reused while cached
+_TERM_CACHE: dict = {}
+
+
+def _term_entry(term: dict) -> list:
+    e = _TERM_CACHE.get(id(term))
+    if e is None or e[0] is not term:
+        if len(_TERM_CACHE) > 4096:
+            _TERM_CACHE.clear()
+        e = _TERM_CACHE[id(term)] = [term, LabelSelector(term.get("labelSelector")), None, None]
+    return e
+
+
 def _term_matches(term: dict, owner_ns: str, other) -> bool:
     namespaces = term.get("namespaces") or [owner_ns]
-    return other.namespace in namespaces and LabelSelector(term.get("labelSelector")).matches(other.labels)
+    return other.namespace in namespaces and _term_entry(term)[1].matches(other.labels)
 
 
 def _native_term(term: dict, owner_ns: str) -> tuple:
-    return LabelSelector(term.get("labelSelector")).native(term.get("namespaces") or [owner_ns])
+    e = _term_entry(term)
+    if e[2] != owner_ns or e[3] is None:     # the native form depends on the owner's namespace
+        e[2], e[3] = owner_ns, e[1].native(term.get("namespaces") or [owner_ns])
+    return e[3]
 
 
 class _AffinityState(StateData):
