@@ -80,7 +80,7 @@ for s in $STEPS; do
       for g in 1 2 4 8; do step "nodegpus/g$g" 300 python bench.py --config 3 --node-gpus $g --steps 10 --warmup 3 --alt none; done ;;
     mixanti)    # 1000-pod burst with 0 / 10 interleaved required-anti-affinity pods, alternated
       mkdir -p gpurun_out/mixanti
-      for k in 1 2; do for m in 0 10; do
+      for k in $(seq 1 ${MIXANTI_REPS:-2}); do for m in 0 10; do
         step "mixanti/m${m}_$k" 300 python bench.py --config 3 --mix-anti $m --steps 20 --warmup 5 --alt none
       done; done ;;
     all)   # every BASELINE config (+ 6) on this box, one JSON line each under gpurun_out/all/
