@@ -658,3 +658,38 @@ def test_wait_scheduled_counts_bindings_of_both_paths():
         assert core.marks[-1] == (1 << 64) - 1  # no waiter left: watermark off
 
     asyncio.run(run())
+
+
+def test_gate_update_evicts_only_waiting_pods_matching_an_added_term():
+    """A gates-only update (``Lane.set_gates``) re-checks the lane's waiting pods against the
+    terms it ADDS: a queued pod matching one goes to the Python path, the others stay (every
+    waiting pod passed the older terms when it was admitted). Once the term is removed, a
+    matching pod is the lane's again."""
+    from yoda_scheduler_amd.models.selectors import LabelSelector
+
+    async def go():
+        cfg = yoda_config(extra_filter=["InterPodAffinity"])
+        async with Env(cfg=cfg) as e:
+            lane = e.sched.lane.lane
+            await e.create(pod("warm", {"scv/memory": "1000"}))
+            assert await e.wait(lambda: e.sched.scheduled == 1)
+            lane.pause(True)                  # the next pods wait in the lane's inbox
+            await e.create(pod("web1", {"app": "web", "scv/memory": "1000"}))
+            await e.create(pod("api1", {"app": "api", "scv/memory": "1000"}))
+            await asyncio.sleep(0.3)
+            term = LabelSelector({"matchLabels": {"app": "web"}}).native(["default"])
+            assert lane.set_gates("yoda-scheduler", [term])
+            fwd0 = lane.stats()["forwarded"]
+            lane.pause(False)                 # events are admitted, then the added gate applies
+            assert await e.wait(lambda: e.sched.scheduled == 3)
+            fwd1 = lane.stats()["forwarded"]
+            lane_bound, py_bound = lane.scheduled, e.sched._scheduled
+            assert lane.set_gates("yoda-scheduler", [])   # removal only: a later web pod is the lane's
+            await asyncio.sleep(0.1)
+            await e.create(pod("web2", {"app": "web", "scv/memory": "1000"}))
+            assert await e.wait(lambda: e.sched.scheduled == 4)
+            return fwd0, fwd1, lane_bound, py_bound, lane.scheduled, e.sched._scheduled
+    fwd0, fwd1, lane_bound, py_bound, lane_bound2, py_bound2 = run(go())
+    assert lane_bound == 2 and py_bound == 1          # api1 on the lane, web1 handed to Python
+    assert fwd1 >= fwd0 + 1
+    assert lane_bound2 == 3 and py_bound2 == 1        # web2 on the lane
