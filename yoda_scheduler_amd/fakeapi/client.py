@@ -47,7 +47,7 @@ class InProcessClient:
             await self._lat()
         return self.server.get(res, name, namespace)
 
-    async def create(self, res: str, obj: dict, namespace: Optional[str] = None) -> dict:
+    async def create(self, res: str, obj: dict, namespace: Optional[str] = None, parse: bool = True) -> dict:
         if self.server.faults.latency_s:
             await self._lat()
         return self.server.create(res, obj, namespace)

@@ -125,9 +125,11 @@ class EventRecorder:
             self._dedup[key] = await self.client.patch("events.k8s.io", prev["metadata"]["name"],
                                                        {"series": series}, meta.get("namespace") or "default")
         else:
-            self._dedup[key] = await self.client.create(
-                "events.k8s.io", self._new_v1(meta, kind, typ, reason, message, ts, controller, related),
-                meta.get("namespace"))
+            # the dedup record needs only what we sent (the name a series bump patches): the
+            # created object is not decoded
+            ev = self._new_v1(meta, kind, typ, reason, message, ts, controller, related)
+            await self.client.create("events.k8s.io", ev, meta.get("namespace"), parse=False)
+            self._dedup[key] = ev
 
     async def run(self) -> None:
         while True:

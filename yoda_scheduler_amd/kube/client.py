@@ -213,7 +213,7 @@ class KubeClient:
 
     async def _req(self, method: str, res: str, namespace: Optional[str] = None, name: Optional[str] = None,
                    sub: Optional[str] = None, body=None, content_type: str = "application/json",
-                   params: Optional[dict] = None, limited: bool = False) -> dict:
+                   params: Optional[dict] = None, limited: bool = False, parse: bool = True) -> dict:
         for attempt in (0, 1):
             if self.native is not None:
                 self._refresh_token()
@@ -246,7 +246,7 @@ class KubeClient:
                     st = {}
                 raise ApiError(status, st.get("reason", "Error"),
                                st.get("message", text[:300].decode("utf-8", "replace")))
-            return json.loads(text) if text else {}
+            return json.loads(text) if text and parse else {}
         raise AssertionError("unreachable")
 
     # ------------------------------------------------------------------ verbs
@@ -399,9 +399,11 @@ class KubeClient:
     async def get(self, res: str, name: str, namespace: Optional[str] = None) -> dict:
         return await self._req("GET", res, namespace, name)
 
-    async def create(self, res: str, obj: dict, namespace: Optional[str] = None) -> dict:
+    async def create(self, res: str, obj: dict, namespace: Optional[str] = None, parse: bool = True) -> dict:
+        """POST ``obj``; the created object as the apiserver returned it (``parse=False``: an
+        empty dict — the caller needs only the success)."""
         ns = namespace or (obj.get("metadata") or {}).get("namespace") or ("default" if resource(res).namespaced else None)
-        return await self._req("POST", res, ns, body=obj)
+        return await self._req("POST", res, ns, body=obj, parse=parse)
 
     async def update(self, res: str, obj: dict, namespace: Optional[str] = None) -> dict:
         m = obj.get("metadata") or {}
