@@ -972,14 +972,15 @@ __device__ __forceinline__ bool spin_ok(const BatchArgs& a, unsigned& spins, lon
   return true;
 }
 
-// Thread t < G polls record t of epoch `tag` (K granules) until every tag matches; returns
-// false (block-uniform) when the wait was abandoned.
+// Thread t < G polls the record of block p_off + t for epoch `tag` (K granules) until every
+// tag matches; returns false (block-uniform) when the wait was abandoned.
 template <int K>
-__device__ __forceinline__ bool gather(const BatchArgs& a, uint32_t tag, int G, uint32_t (&v)[K], int* s_fail) {
+__device__ __forceinline__ bool gather(const BatchArgs& a, uint32_t tag, int G, int p_off, uint32_t (&v)[K],
+                                       int* s_fail) {
   const int t = threadIdx.x;
   bool failed = false;
   if (uniform(t & ~63) < G) {   // waves holding at least one producer
-    const gu64* p = slot_ptr(a, tag, t < G ? t : 0);
+    const gu64* p = slot_ptr(a, tag, p_off + (t < G ? t : 0));
     const long long t0 = __builtin_amdgcn_s_memrealtime();
     for (unsigned spins = 0;;) {
       // poll one granule per record until every record's has landed, then read the rest
@@ -1014,17 +1015,29 @@ __device__ __forceinline__ bool gather(const BatchArgs& a, uint32_t tag, int G, 
 
 #define TRACE(pt)                                                                      \
   do {                                                                                 \
-    if (a.trace && g == 0 && tid == 0) a.trace[(size_t)b * kTracePts + (pt)] = __builtin_amdgcn_s_memrealtime(); \
+    if (a.trace && gi == 0 && tid == 0) a.trace[(size_t)b * kTracePts + (pt)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 // BW waves per block (4 or 8): 8 puts two waves on every SIMD (latency hiding) and 64 nodes
-// per block, halving the all-gather producers at a given cluster size
-template <int BW>
+// per block, halving the all-gather producers at a given cluster size.
+//
+// PAIRS: two pods in flight. The grid is two sets of blocks holding the same node ranges
+// (replicated rows); set s runs pods s, s+2, s+4, …. While one set runs pod b's exchanges,
+// score B and select, the other set has already filtered and scored pod b+1 against its rows
+// (every assume up to pod b−1 applied). When pod b's winner is known (its record 3 carries the
+// winner's GPU mask), the other set applies that assume to its replica and only the owner of the
+// winner's node redoes the filter of that one 8-node group (before record 1) and its score A
+// (while record 1 travels): an assume changes one row, so every other node's filter and score A
+// for pod b+1 stand. The per-pod critical path loses the filter and score A of every block but
+// one group's; results are bit-identical to the serial order.
+template <int BW, bool PAIRS>
 __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   constexpr int kBB = 64 * BW;
   extern __shared__ __align__(16) unsigned char s_dyn[];
   __shared__ uint8_t s_masks[256];
-  __shared__ __align__(16) uint32_t s_req[2][sizeof(yoda_dev_req_t) / 4];
+  // request ring: pods b (and b−1 in PAIRS mode, for its assume) plus the prefetched next ones
+  __shared__ __align__(16) uint32_t s_req[4][sizeof(yoda_dev_req_t) / 4];
+  __shared__ int s_win[2];   // PAIRS: the previous pod's winner (node or −1) and its GPU mask
   __shared__ unsigned long long s_part[BW][16];
   __shared__ unsigned long long s_glob[16];
   __shared__ uint32_t s_rec[14][kMaxGrid + 4];   // gather-1 records transposed (+4: bank skew)
@@ -1035,8 +1048,14 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   __shared__ bool s_last;
   static_assert(sizeof(yoda_dev_result_t) % 8 == 0, "result copied as u64 words");
 
-  const int npb = a.npb, G = gridDim.x, g = blockIdx.x;
-  const int base = g * npb;
+  const int npb = a.npb, g = blockIdx.x;
+  // G: the blocks that produce one pod's records (one set in PAIRS mode); gi: this block's node
+  // range; p0 / q0: the first block of this set / of the other set
+  const int G = PAIRS ? (int)gridDim.x / 2 : (int)gridDim.x;
+  const int set = PAIRS ? g / G : 0;
+  const int gi = g - set * G;
+  const int p0 = set * G, q0 = (1 - set) * G;
+  const int base = gi * npb;
   const int cnt = a.n - base < npb ? a.n - base : npb;   // ≥ 1: the host sizes G = ceil(n / npb)
   yoda_dev_node_t* s_rows = reinterpret_cast<yoda_dev_node_t*>(s_dyn);
   int64_t* s_raw = reinterpret_cast<int64_t*>(s_dyn + (size_t)npb * sizeof(yoda_dev_node_t));
@@ -1065,7 +1084,10 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     reinterpret_cast<uint4*>(a.nodes + a.pa.idx[rec])[tid & 31] = reinterpret_cast<const uint4*>(&a.pa.rows[rec])[tid & 31];
   }
   if (tid < 256) s_masks[tid] = c_subsets.masks[tid];
-  if (tid < kReqWords) s_req[0][tid] = reinterpret_cast<const uint32_t*>(a.reqs)[tid];
+  if (tid < kReqWords) {
+    s_req[0][tid] = reinterpret_cast<const uint32_t*>(a.reqs)[tid];
+    if (PAIRS && a.B > 1) s_req[1][tid] = reinterpret_cast<const uint32_t*>(a.reqs + 1)[tid];
+  }
   if (tid == 0) s_fail = 0;
   __syncthreads();
 
@@ -1103,28 +1125,144 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     }
   };
 
+  // Score A (gang search, the yoda terms that need no maxima — kept in s_raw until phase B —,
+  // default scores) for the 8-node groups [gfirst, gfirst + gcount) of this block. A
+  // multi-GPU pod's subset search is split over `nrep` lane groups per node when the block has
+  // more waves than those groups (8 waves over 32 nodes: two groups per node; one group alone
+  // — the PAIRS fix-up — gets every wave); the replicas' bests meet through LDS. Wave-uniform.
+  const int ngroups = (npb + kNodesPerWave - 1) / kNodesPerWave;
+  auto score_a_groups = [&](const yoda_dev_req_t& r, const ScoreConsts& sc, const uint8_t* s_feas,
+                            const uint8_t* s_elig, int gfirst, int gcount) {
+    const int nrep = (sc.search && sc.k > 1 && gcount <= BW) ? BW / gcount : 1;
+    const int span = gcount * kNodesPerWave, j_lo = gfirst * kNodesPerWave;
+    for (int it = wave; it < gcount * nrep; it += BW) {
+      const int rep = it / gcount;
+      const int j = j_lo + (it - rep * gcount) * kNodesPerWave + grp;
+      const bool act = j < cnt && s_feas[j];
+      const uint32_t emask = act ? s_elig[j] : 0u;
+      uint64_t rbase = 0;
+      int64_t total_v = 0;
+      uint32_t mask_v = 0;
+      int32_t quality_v = 0;
+      // a replica's best goes straight to its LDS slot (< nrep·span ≤ 8·BW; a pointer to a
+      // local would put the struct in scratch memory)
+      score_node_a(s_rows + (j < cnt ? j : 0), act, emask, r, sc, s_masks, sub, rbase, total_v, mask_v, quality_v,
+                   rep, nrep, nrep > 1 ? &s_gang[rep * span + (j - j_lo)] : nullptr);
+      if (act && sub == 0 && rep == 0) {
+        s_raw[j] = (int64_t)rbase;
+        s_total[j] = total_v;
+        s_mask[j] = (uint8_t)mask_v;
+        s_quality[j] = quality_v;
+      }
+    }
+    if (nrep > 1) {
+      __syncthreads();
+      // replica 0 scored with its own best: where another replica found a better set,
+      // take it and move the gang bonus (the only score term that depends on the set)
+      for (int j = j_lo + tid; j < cnt && j < j_lo + span; j += kBB) {
+        if (!s_feas[j]) continue;
+        const GangBest b0 = s_gang[j - j_lo];
+        GangBest bb = b0;
+        for (int q = 1; q < nrep; ++q) {
+          const GangBest o = s_gang[q * span + (j - j_lo)];
+          if (o.found && (!bb.found || better(o.o, o.m, bb.o, bb.m))) bb = o;
+        }
+        if (bb.found == b0.found && bb.m == b0.m) continue;
+        const int32_t q_old = s_quality[j];
+        const int32_t q_new = bb.found ? 10000 - sdiv_small_r(bb.lb, 100, 0.01) : 10000;
+        s_mask[j] = bb.m;
+        s_quality[j] = q_new;
+        if (sc.yoda_s && r.has_number && r.number > 1 && r.number <= s_rows[j].ncards) {
+          uint64_t rb = (uint64_t)s_raw[j];
+          if (b0.found) rb -= (uint64_t)(q_old / 100) * (uint64_t)r.w_gang_score;
+          if (bb.found) rb += (uint64_t)(q_new / 100) * (uint64_t)r.w_gang_score;
+          s_raw[j] = (int64_t)rb;
+        }
+      }
+    }
+  };
+
+  // assume (engine.cpp Engine::reserve, non-compat, reservation pending) of pod `rq` on row j
+  // with GPU set `mask`: one thread
+  auto assume_row = [&](const yoda_dev_req_t& rq, int j, uint32_t mask) {
+    yoda_dev_node_t* nd = s_rows + j;
+    const uint32_t mb = (uint32_t)rq.memory;
+    for (int c = 0; c < YODA_DEV_CARDS; ++c)
+      if ((mask >> c) & 1u) {
+        nd->cards[c].reserved += mb;
+        nd->cards[c].pending += mb;
+      }
+    nd->pod_count += 1;
+    nd->req_cpu += rq.cpu_m;
+    nd->req_mem += rq.mem;
+    nd->nz_cpu += rq.nz_cpu_m;
+    nd->nz_mem += rq.nz_mem;
+    s_dirty[j] = 1;
+  };
+
   bool ok = true;
-  for (int b = 0; b < a.B && ok; ++b) {
+  for (int b = set; b < a.B && ok; b += PAIRS ? 2 : 1) {
     // the request is read from LDS where it is used (uniform address: a broadcast read).
     // Copying all 49 words into scalar registers for the whole pod measured slower — the
     // copy spilled other scalars (167 vs 131 SGPR spills): 13.7 vs 13.2 µs/pod at 256 nodes,
     // 16.05 vs 15.9 at 4096 (profiles/device/r4/kernel_ab_r4/)
-    const yoda_dev_req_t& r = *reinterpret_cast<const yoda_dev_req_t*>(s_req[b & 1]);
+    const yoda_dev_req_t& r = *reinterpret_cast<const yoda_dev_req_t*>(s_req[b & 3]);
     const uint32_t tag1 = a.tag0 + 3u * (uint32_t)b, tag2 = tag1 + 1u, tag3 = tag1 + 2u;
-    // prefetch request b+1 (lands while this pod's phases run; stored to LDS at the end)
-    uint32_t pre = 0;
-    if (b + 1 < a.B && tid < kReqWords) pre = reinterpret_cast<const uint32_t*>(a.reqs + b + 1)[tid];
+    // prefetch request b+1 (PAIRS: and b+2, this set's next pod; b+1 is the other set's, whose
+    // assume this set applies) — they land while this pod's phases run, stored after gather 1
+    uint32_t pre = 0, pre2 = 0;
+    if (tid < kReqWords) {
+      if (b + 1 < a.B) pre = reinterpret_cast<const uint32_t*>(a.reqs + b + 1)[tid];
+      if (PAIRS && b + 2 < a.B) pre2 = reinterpret_cast<const uint32_t*>(a.reqs + b + 2)[tid];
+    }
     TRACE(0);
 
     // ================= phase F: filter → per-group aggregates → record 1. (Filtering pod
     // b+1 speculatively while pod b's record 3 travels, re-filtering only the winner's group,
     // measured slower on MI355X: 15.9 vs 15.1 µs/pod at 4096 nodes — the filter lands in the
     // gather wait instead of under it.)
-    const int par = b & 1;
+    const int par = PAIRS ? ((b >> 1) & 1) : (b & 1);   // this set's consecutive pods alternate
     uint8_t* s_feas = s_feas2 + par * npb;
     uint8_t* s_elig = s_elig2 + par * npb;
     filter_groups(r, par, -1);
     __syncthreads();
+    ScoreConsts sc = score_consts(r, nullptr);
+    int fix_group = -1;   // PAIRS: the group whose score A is redone while record 1 travels
+    if constexpr (PAIRS) {
+      // score A of every group now, against the rows as of this set's last pod; then the other
+      // set's pod b−1: its winner, from its record 3 (best key, and the GPU mask + feasible bit)
+      score_a_groups(r, sc, s_feas, s_elig, 0, ngroups);
+      if (b >= 1) {
+        uint32_t v[3];
+        if (!gather<3>(a, tag3 - 3u, G, q0, v, &s_fail)) {
+          ok = false;
+          break;
+        }
+        const bool have = tid < G;
+        const unsigned long long mk = have ? ((unsigned long long)v[1] << 32 | v[0]) : 0ull;
+        const unsigned long long wk = wave_max(mk);
+        if (lane == 0) s_part[wave][0] = wk;
+        __syncthreads();
+        unsigned long long key = 0;
+        for (int w = 0; w < BW; ++w) key = s_part[w][0] > key ? s_part[w][0] : key;
+        const bool feas_prev = ((v[2] >> 8) & 1u) != 0;   // every record carries it (thread 0's is read)
+        if (tid == 0) s_win[0] = feas_prev ? 1 : 0;
+        if (have && mk == key) s_win[1] = (int)(v[2] & 0xFFu);   // the winner's record (keys are unique)
+        __syncthreads();
+        if (s_win[0]) {
+          const yoda_dev_req_t& rp = *reinterpret_cast<const yoda_dev_req_t*>(s_req[(b - 1) & 3]);
+          const uint32_t pp = (uint32_t)(key & 0xFFFFFFull);
+          const int w = (int)(((pp - rp.perm_add) * rp.perm_inv) & 0xFFFFFFu);
+          if (w >= base && w < base + cnt) {   // block-uniform: this replica holds the node
+            if (tid == 0) assume_row(rp, w - base, (uint32_t)s_win[1]);
+            __syncthreads();
+            fix_group = (w - base) / kNodesPerWave;
+            filter_groups(r, par, fix_group);
+          }
+        }
+        __syncthreads();
+      }
+    }
     if (tid < kRec1) {   // block totals over the groups → the record's 11 granules
       const int ngr = (cnt + kNodesPerWave - 1) / kNodesPerWave;
       uint32_t v;
@@ -1144,69 +1282,18 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     }
     TRACE(1);
 
-    // ================= phase A (while record 1 travels): gang search, the yoda terms that
-    // need no maxima (kept in s_raw until phase B), default scores
-    ScoreConsts sc = score_consts(r, nullptr);
-    {
-      // a multi-GPU pod's subset search is split over `nrep` lane groups per node when the
-      // block has more waves than node groups (8 waves over 32 nodes: two groups per node,
-      // two waves per SIMD); the replicas' bests meet through LDS below
-      const int ngroups = (npb + kNodesPerWave - 1) / kNodesPerWave;
-      const int nrep = (sc.search && sc.k > 1 && ngroups <= BW) ? BW / ngroups : 1;
-      for (int it = wave; it < ngroups * nrep; it += BW) {
-        const int rep = it / ngroups;
-        const int j = (it - rep * ngroups) * kNodesPerWave + grp;
-        const bool act = j < cnt && s_feas[j];
-        const uint32_t emask = act ? s_elig[j] : 0u;
-        uint64_t rbase = 0;
-        int64_t total_v = 0;
-        uint32_t mask_v = 0;
-        int32_t quality_v = 0;
-        // a replica's best goes straight to its LDS slot (a pointer to a local would put
-        // the struct in scratch memory)
-        score_node_a(s_rows + (j < cnt ? j : 0), act, emask, r, sc, s_masks, sub, rbase, total_v, mask_v, quality_v,
-                     rep, nrep, nrep > 1 ? &s_gang[rep * npb + j] : nullptr);
-        if (act && sub == 0) {
-          if (rep == 0) {
-            s_raw[j] = (int64_t)rbase;
-            s_total[j] = total_v;
-            s_mask[j] = (uint8_t)mask_v;
-            s_quality[j] = quality_v;
-          }
-        }
-      }
-      if (nrep > 1) {
-        __syncthreads();
-        // replica 0 scored with its own best: where another replica found a better set,
-        // take it and move the gang bonus (the only score term that depends on the set)
-        for (int j = tid; j < cnt; j += kBB) {
-          if (!s_feas[j]) continue;
-          const GangBest b0 = s_gang[j];
-          GangBest b = b0;
-          for (int q = 1; q < nrep; ++q) {
-            const GangBest o = s_gang[q * npb + j];
-            if (o.found && (!b.found || better(o.o, o.m, b.o, b.m))) b = o;
-          }
-          if (b.found == b0.found && b.m == b0.m) continue;
-          const int32_t q_old = s_quality[j];
-          const int32_t q_new = b.found ? 10000 - sdiv_small_r(b.lb, 100, 0.01) : 10000;
-          s_mask[j] = b.m;
-          s_quality[j] = q_new;
-          if (sc.yoda_s && r.has_number && r.number > 1 && r.number <= s_rows[j].ncards) {
-            uint64_t rb = (uint64_t)s_raw[j];
-            if (b0.found) rb -= (uint64_t)(q_old / 100) * (uint64_t)r.w_gang_score;
-            if (b.found) rb += (uint64_t)(q_new / 100) * (uint64_t)r.w_gang_score;
-            s_raw[j] = (int64_t)rb;
-          }
-        }
-      }
+    // ================= phase A (while record 1 travels). PAIRS: only the fix-up group
+    if (PAIRS) {
+      if (fix_group >= 0) score_a_groups(r, sc, s_feas, s_elig, fix_group, 1);
+    } else {
+      score_a_groups(r, sc, s_feas, s_elig, 0, ngroups);
     }
     TRACE(2);
 
     // ================= gather 1: global maxima, feasible and reason counts
     {
       uint32_t v[kRec1];
-      if (!gather<kRec1>(a, tag1, G, v, &s_fail)) {
+      if (!gather<kRec1>(a, tag1, G, p0, v, &s_fail)) {
         ok = false;
         break;
       }
@@ -1246,7 +1333,10 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     score_consts_maxima(sc, gmx);
     // request b+1 (prefetched at the start of this pod) to LDS; the barriers of the
     // remaining phases order it before the next pod reads it
-    if (b + 1 < a.B && tid < kReqWords) s_req[(b + 1) & 1][tid] = pre;
+    if (tid < kReqWords) {
+      if (b + 1 < a.B) s_req[(b + 1) & 3][tid] = pre;
+      if (PAIRS && b + 2 < a.B) s_req[(b + 2) & 3][tid] = pre2;
+    }
     TRACE(3);
 
     // ================= phase B: maxima-normalised card metrics → raw scores, lo/hi → record 2
@@ -1279,7 +1369,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       }
       TRACE(4);
       uint32_t v[kRec2];
-      if (!gather<kRec2>(a, tag2, G, v, &s_fail)) {
+      if (!gather<kRec2>(a, tag2, G, p0, v, &s_fail)) {
         ok = false;
         break;
       }
@@ -1321,14 +1411,24 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       best = wave_max(best);
       if (lane == 0) s_part[wave][0] = best;
       __syncthreads();
-      if (tid < kRec3) {
+      if (tid < (PAIRS ? 3 : kRec3)) {
         unsigned long long bb = 0;
         for (int w = 0; w < BW; ++w) bb = s_part[w][0] > bb ? s_part[w][0] : bb;
-        store_granule(slot_ptr(a, tag3, g) + tid, tag3, tid ? (uint32_t)(bb >> 32) : (uint32_t)bb);
+        uint32_t x = tid == 0 ? (uint32_t)bb : (uint32_t)(bb >> 32);
+        if (tid == 2) {   // PAIRS: the block best's GPU mask and whether the pod fits anywhere
+          uint32_t m = 0;
+          if (bb != 0) {
+            const uint32_t pb = (uint32_t)(bb & 0xFFFFFFull);
+            const int nb = (int)(((pb - r.perm_add) * r.perm_inv) & 0xFFFFFFu);
+            if (nb >= base && nb < base + cnt) m = s_mask[nb - base];
+          }
+          x = m | ((nf > 0 ? 1u : 0u) << 8);
+        }
+        store_granule(slot_ptr(a, tag3, g) + tid, tag3, x);
       }
       TRACE(6);
       uint32_t v[kRec3];
-      if (!gather<kRec3>(a, tag3, G, v, &s_fail)) {
+      if (!gather<kRec3>(a, tag3, G, p0, v, &s_fail)) {
         ok = false;
         break;
       }
@@ -1347,27 +1447,12 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       const uint32_t p = (uint32_t)(key & 0xFFFFFFull);
       node = (int)(((p - r.perm_add) * r.perm_inv) & 0xFFFFFFu);
     }
-    const bool owner = nf > 0 ? (node >= base && node < base + cnt) : g == 0;
+    const bool owner = nf > 0 ? (node >= base && node < base + cnt) : gi == 0;
     if (owner) {
       const int j = nf > 0 ? node - base : 0;
       const uint32_t mask = nf > 0 ? (uint32_t)s_mask[j] : 0u;
       const int32_t quality = nf > 0 ? s_quality[j] : 0;
-      if (tid == 0 && nf > 0) {
-        // assume (engine.cpp Engine::reserve, non-compat, reservation pending)
-        yoda_dev_node_t* nd = s_rows + j;
-        const uint32_t mb = (uint32_t)r.memory;
-        for (int c = 0; c < YODA_DEV_CARDS; ++c)
-          if ((mask >> c) & 1u) {
-            nd->cards[c].reserved += mb;
-            nd->cards[c].pending += mb;
-          }
-        nd->pod_count += 1;
-        nd->req_cpu += r.cpu_m;
-        nd->req_mem += r.mem;
-        nd->nz_cpu += r.nz_cpu_m;
-        nd->nz_mem += r.nz_mem;
-        s_dirty[j] = 1;
-      }
+      if (tid == 0 && nf > 0) assume_row(r, j, mask);
       // the result: lane k of wave 0 writes its 64-bit word k, every value selected with
       // constant indices (a local struct with the reasons array indexed by reason code lived in
       // scratch memory: ~30 scratch accesses and vmcnt waits on the owner's path each pod)
@@ -1404,7 +1489,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = t == (unsigned)G - 1;
+    s_last = t == gridDim.x - 1;
     if (s_last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1460,6 +1545,11 @@ struct Ctx {
   int cus_total = 256;        // compute units of the device (occupancy check)
   int npb_min = 0;            // YODA_DEV_NPB: minimum nodes per block (0: 8 per wave)
   int batch_waves = 0;        // YODA_DEV_BWAVES: k_batch waves per block (4 or 8; 0 = by cluster size)
+  // two pods in flight (k_batch PAIRS: two block sets alternate pods, each filtering and
+  // scoring its next pod during the other's exchanges) when twice the grid is resident;
+  // YODA_DEV_PAIRS=0/1
+  bool pairs = false;
+  int occ_blocks_pairs = -1;
   // per spin wait inside k_batch, 100 MHz ticks (YODA_DEV_SPIN_DEADLINE_US): a gather normally
   // completes in microseconds; 20 ms only elapses when a block is not resident (a tenant
   // kernel holds the CUs) — then every block gives up and the batch aborts
@@ -1488,6 +1578,7 @@ struct Ctx {
   uint32_t epoch = 1;
   int seq = 0;
   int last_grid = 0, last_npb = 0;
+  bool last_pairs = false;
   unsigned long long* d_trace = nullptr;   // yoda_dev_batch_trace: block 0's phase stamps
   int trace_pods = 0;
 };
@@ -1603,6 +1694,7 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
   if (const char* v = getenv("YODA_DEV_SPIN_DEADLINE_US")) c->deadline_ticks = atoll(v) > 0 ? atoll(v) * 100 : 1;
   if (const char* v = getenv("YODA_DEV_HOST_DEADLINE_US")) c->host_deadline_us = atof(v) > 0 ? atof(v) : 1.0;
   if (const char* v = getenv("YODA_DEV_BWAVES")) c->batch_waves = atoi(v) == 4 ? 4 : atoi(v) == 8 ? 8 : 0;
+  if (const char* v = getenv("YODA_DEV_PAIRS")) c->pairs = v[0] != '0';
   if (const char* v = getenv("YODA_DEV_DIRECT_ATOMICS")) c->direct_atomics = v[0] == '1' ? 1 : 0;
   if (const char* v = getenv("YODA_DEV_FUSE_MAX")) c->fuse_max = atoi(v);
   const SubsetTable st = make_subsets();
@@ -1654,12 +1746,11 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
   if ((e = hipMemset(c->d_slots, 0, slot_bytes)) != hipSuccess) return fail("slots", e);
   if ((e = hipMalloc(&c->d_words, 64)) != hipSuccess) return fail("words", e);
   if ((e = hipMemset(c->d_words, 0, 64)) != hipSuccess) return fail("words", e);
-  if ((e = hipFuncSetAttribute((const void*)k_batch<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)(kMaxNodesPerBlock * kBatchRowBytes))) != hipSuccess)
-    return fail("k_batch LDS", e);
-  if ((e = hipFuncSetAttribute((const void*)k_batch<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)(kMaxNodesPerBlock * kBatchRowBytes))) != hipSuccess)
-    return fail("k_batch LDS", e);
+  for (const void* kf : {(const void*)k_batch<4, false>, (const void*)k_batch<8, false>, (const void*)k_batch<4, true>,
+                         (const void*)k_batch<8, true>})
+    if ((e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)(kMaxNodesPerBlock * kBatchRowBytes))) != hipSuccess)
+      return fail("k_batch LDS", e);
   Globals init;
   globals_reset(&init);
   if ((e = hipMemcpy(c->d_g, &init, sizeof(Globals), hipMemcpyHostToDevice)) != hipSuccess) return fail("init", e);
@@ -1831,14 +1922,19 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
   // launch chain (no cross-block waits). A tenant kernel holding CUs at run time is the
   // host deadline's job (abandon + CPU path), not this check's.
   if (c->occ_waves != waves || c->occ_lds != (int)lds) {
-    int nb = 0;
+    int nb = 0, np = 0;
     const hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &nb, waves == 8 ? (const void*)k_batch<8> : (const void*)k_batch<4>, waves * 64, lds);
+        &nb, waves == 8 ? (const void*)k_batch<8, false> : (const void*)k_batch<4, false>, waves * 64, lds);
+    const hipError_t op = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &np, waves == 8 ? (const void*)k_batch<8, true> : (const void*)k_batch<4, true>, waves * 64, lds);
     c->occ_waves = waves;
     c->occ_lds = (int)lds;
     c->occ_blocks = oe == hipSuccess ? nb : 0;
+    c->occ_blocks_pairs = op == hipSuccess ? np : 0;
   }
   if ((long long)c->occ_blocks * c->cus_total < G) return 1;
+  // two sets of G blocks: every one resident, and within the slot table
+  const bool pairs = c->pairs && 2 * G <= kMaxGrid && (long long)c->occ_blocks_pairs * c->cus_total >= 2 * G;
   c->last_grid = G;
   c->last_npb = npb;
   for (int base = 0; base < B; base += kBatchCap) {
@@ -1871,10 +1967,14 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
     a.trace = c->d_trace;
     __atomic_store_n(c->h_done, 0, __ATOMIC_RELEASE);
     if (c->timing) CK(hipEventRecord(c->e0, c->stream));
-    if (waves == 8)
-      hipLaunchKernelGGL(k_batch<8>, dim3(G), dim3(512), lds, c->stream, a);
-    else
-      hipLaunchKernelGGL(k_batch<4>, dim3(G), dim3(256), lds, c->stream, a);
+    if (pairs && m >= 2) {
+      if (waves == 8) hipLaunchKernelGGL((k_batch<8, true>), dim3(2 * G), dim3(512), lds, c->stream, a);
+      else hipLaunchKernelGGL((k_batch<4, true>), dim3(2 * G), dim3(256), lds, c->stream, a);
+    } else {
+      if (waves == 8) hipLaunchKernelGGL((k_batch<8, false>), dim3(G), dim3(512), lds, c->stream, a);
+      else hipLaunchKernelGGL((k_batch<4, false>), dim3(G), dim3(256), lds, c->stream, a);
+    }
+    c->last_pairs = pairs && m >= 2;
     c->pend.n = 0;
     CK(hipGetLastError());
     ++c->n_dispatch;
@@ -2033,7 +2133,8 @@ int yoda_dev_busy(void* p) {
   return busy_check(c) != 0;
 }
 
-// out[0..8] (9 values, 11 with the batch wait's pre-sleep count and µs/pod; n = the caller's buffer length, checked): kernel dispatches, k_batch
+// out[0..8] (9 values; 11 with the batch wait's pre-sleep count and µs/pod, 12 with whether the last
+// k_batch ran in PAIRS mode; n = the caller's buffer length, checked): kernel dispatches, k_batch
 // dispatches, pods placed by k_batch, calls abandoned at the host deadline, calls refused while
 // an abandoned one drained, k_batch GPU µs (timing on), stream queries made while draining and
 // their µs, the host's wait on the last abandoned call
@@ -2053,6 +2154,7 @@ int yoda_dev_counters(void* p, double* out, int n) {
     out[9] = (double)c->n_presleep;
     out[10] = c->wait_us_per_pod;
   }
+  if (n >= 12) out[11] = c->last_pairs ? 1.0 : 0.0;   // the last k_batch ran two pods in flight
   return 0;
 }
 

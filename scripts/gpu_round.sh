@@ -80,6 +80,13 @@ for s in $STEPS; do
         step "geo/npb64w8_$k" 200 env YODA_DEV_NPB=64 YODA_DEV_BWAVES=8 python scripts/device_batch_bench.py --nodes 4096,16384 --pods 1032 --batch 256 --modes batch --trace --mix bench
         step "geo/npb16w4_$k" 200 env YODA_DEV_NPB=16 YODA_DEV_BWAVES=4 python scripts/device_batch_bench.py --nodes 4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
       done ;;
+    pairs)  # k_batch two pods in flight (YODA_DEV_PAIRS=1) vs one, alternated; then the parity suite in PAIRS mode
+      mkdir -p gpurun_out/pairs
+      for k in 1 2; do
+        step "pairs/one_$k" 200 env YODA_DEV_PAIRS=0 python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
+        step "pairs/two_$k" 200 env YODA_DEV_PAIRS=1 python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
+      done ;;
+    testspairs) step gpu_tests_pairs 600 env YODA_DEV_PAIRS=1 python -u -m pytest tests/test_gpu_device_scorer.py -x -v --timeout 120 --timeout-method thread ;;
     mixlog) step mixlog 300 env YODA_BENCH_RUNLOG=1 python bench.py --config 3 --mix-anti 10 --steps 5 --warmup 3 --alt none ;;
     scope6) step scope6 300 env YODA_BENCH_THREADS=2 python bench.py --config 6 --steps 5 --warmup 1 --alt none ;;
     nodegpus)   # BASELINE protocol item 5 on config 3: scheduler CPU per attempted pod at 1/2/4/8 GPUs per node

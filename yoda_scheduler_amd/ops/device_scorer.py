@@ -61,7 +61,7 @@ def read_batch_trace(engine, max_pods: int = 256) -> list[dict]:
 
 
 COUNTERS = ("dispatches", "kbatch_dispatches", "kbatch_pods", "abandoned", "busy_refusals", "kbatch_us",
-            "drain_queries", "drain_query_us", "abandon_wait_us", "presleeps", "wait_us_per_pod")
+            "drain_queries", "drain_query_us", "abandon_wait_us", "presleeps", "wait_us_per_pod", "last_pairs")
 
 
 def counters(engine) -> dict:
