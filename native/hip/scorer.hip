@@ -1546,9 +1546,10 @@ struct Ctx {
   int npb_min = 0;            // YODA_DEV_NPB: minimum nodes per block (0: 8 per wave)
   int batch_waves = 0;        // YODA_DEV_BWAVES: k_batch waves per block (4 or 8; 0 = by cluster size)
   // two pods in flight (k_batch PAIRS: two block sets alternate pods, each filtering and
-  // scoring its next pod during the other's exchanges) when twice the grid is resident;
-  // YODA_DEV_PAIRS=0/1
-  bool pairs = false;
+  // scoring its next pod during the other's exchanges) when twice the grid is resident
+  // (≤ 4096 nodes on MI355X). MI355X, bench mix: 13.5 vs 15.6–16.2 µs/pod at 4096 nodes, 11.9
+  // vs 12.8–13.5 at 256 (profiles/device/r4/pairs/). YODA_DEV_PAIRS=0 turns it off
+  bool pairs = true;
   int occ_blocks_pairs = -1;
   // per spin wait inside k_batch, 100 MHz ticks (YODA_DEV_SPIN_DEADLINE_US): a gather normally
   // completes in microseconds; 20 ms only elapses when a block is not resident (a tenant
@@ -2101,6 +2102,11 @@ int yoda_dev_batch_trace(void* p, int on, unsigned long long* out, int max_pods)
   CK(hipStreamSynchronize(c->stream));
   if (m > 0) CK(hipMemcpy(out, c->d_trace, (size_t)m * kTracePts * 8, hipMemcpyDeviceToHost));
   return m;
+}
+
+// PAIRS mode on/off for the next batches (tests compare both; YODA_DEV_PAIRS sets the default)
+void yoda_dev_set_pairs(void* p, int on) {
+  if (p) ((Ctx*)p)->pairs = on != 0;
 }
 
 void yoda_dev_set_timing(void* p, int on) {

@@ -449,3 +449,45 @@ def test_batch_survives_a_tenant_kernel(require_gpu):
         pi, req = ds.random_request(a, rng, f"hog-after-{k}")
         assert not ds.compare_cycle(a, req), k
         a.schedule(pi.num_id, req, True)
+
+
+@pytest.mark.parametrize("n,pods", [(64, 33), (1000, 120), (4096, 300)])
+def test_k_batch_two_pods_in_flight_matches_one_at_a_time(require_gpu, n, pods):
+    """PAIRS mode (two block sets alternate pods; each filters and scores its next pod while
+    the other's exchanges run and redoes only the group of the node the other set's pod took)
+    returns exactly what one-pod-at-a-time k_batch returns — nodes, GPU sets, scores, reasons,
+    gang quality — with pods that fit nowhere and consecutive pods contending for the same
+    node; the device tables agree afterwards."""
+    from yoda_scheduler_amd.models.pod import PodInfo
+    from yoda_scheduler_amd.ops import device_scorer as ds
+    from yoda_scheduler_amd.ops.native import pod_req
+    a, b = _engine(n, 41), _engine(n, 41)
+    a.seed(7)
+    b.seed(7)
+    ds.set_pairs(a, True)
+    ds.set_pairs(b, False)
+    rng = random.Random(n + 5)
+    pods_ = [ds.random_request(a, rng, f"pp-{n}-{k}")[0] for k in range(pods)]
+    # contention: a run of identical 1-GPU pods (each takes the node the previous one made
+    # best or worst), pods that fit nowhere, an 8-GPU gang
+    for k in range(6):
+        pods_.insert(3 + k, PodInfo.from_obj({"metadata": {"name": f"same{k}", "uid": f"pp-s-{n}-{k}",
+                                                           "labels": {"scv/memory": "20000"}}, "spec": {}}))
+    for k, lab in enumerate([{"scv/memory": "900000"}, {"scv/number": "9"}, {"scv/number": "8", "scv/memory": "1024"}]):
+        pods_.insert(12 + 5 * k, PodInfo.from_obj({"metadata": {"name": f"x{k}", "uid": f"pp-x-{n}-{k}", "labels": lab},
+                                                   "spec": {}}))
+    res_a = a.schedule_batch([p.num_id for p in pods_], [pod_req(a, p) for p in pods_])
+    assert ds.counters(a)["last_pairs"] == 1
+    res_b = b.schedule_batch([p.num_id for p in pods_], [pod_req(b, p) for p in pods_])
+    assert ds.counters(b)["last_pairs"] == 0
+    key = lambda r: (r[0], r[1], list(r[3]), r[4], list(r[5]), r[6])
+    assert [key(r) for r in res_a] == [key(r) for r in res_b]
+    assert any(r[0] < 0 for r in res_a) and sum(1 for r in res_a if r[0] >= 0) > pods // 2
+    assert a.device_fallbacks == 0 and b.device_fallbacks == 0
+    for i in range(0, n, max(1, n // 97)):
+        assert a.node_cards(i) == b.node_cards(i)
+    rng2 = random.Random(n + 6)
+    for k in range(6):
+        pi, req = ds.random_request(a, rng2, f"pp-after-{n}-{k}")
+        assert not ds.compare_cycle(a, req)
+        a.schedule(pi.num_id, req, True)

@@ -22,6 +22,16 @@ def declare(lib: ctypes.CDLL) -> None:
     lib.yoda_dev_batch_trace.restype = ctypes.c_int
     lib.yoda_dev_counters.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     lib.yoda_dev_counters.restype = ctypes.c_int
+    lib.yoda_dev_set_pairs.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.yoda_dev_set_pairs.restype = None
+
+
+def set_pairs(engine, on: bool) -> None:
+    """k_batch with two pods in flight (PAIRS, the default where twice the grid fits) or one
+    at a time, for the next batches of ``engine``'s device scorer."""
+    lib = hip_lib()
+    declare(lib)
+    lib.yoda_dev_set_pairs(engine.device_ctx, 1 if on else 0)
 
 
 # k_batch phases (block 0's stamps): filter → record 1 out; part A of scoring (gang search,
