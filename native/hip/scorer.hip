@@ -933,7 +933,6 @@ struct BatchArgs {
   unsigned int* ticket;
   unsigned int* abort_word;
   unsigned long long* trace;          // optional: block 0's phase stamps, kTracePts per pod
-  int twin;                           // PAIRS: start the winner's fix-up on the twin's record 3
 };
 constexpr int kResWords = (int)(sizeof(yoda_dev_result_t) / 8);
 static_assert(kResWords == 19 && YODA_DEV_REASONS == 16 && offsetof(yoda_dev_result_t, feasible) == 4 &&
@@ -1039,13 +1038,6 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   // request ring: pods b (and b−1 in PAIRS mode, for its assume) plus the prefetched next ones
   __shared__ __align__(16) uint32_t s_req[4][sizeof(yoda_dev_req_t) / 4];
   __shared__ int s_win[2];   // PAIRS: the previous pod's winner (node or −1) and its GPU mask
-  // PAIRS + twin speculation: the twin's record 3 and the backed-up group
-  __shared__ uint32_t s_tw[3];
-  __shared__ __align__(16) yoda_dev_node_t s_bak_row;
-  __shared__ int64_t s_bak_raw[kNodesPerWave], s_bak_total[kNodesPerWave];
-  __shared__ int32_t s_bak_quality[kNodesPerWave];
-  __shared__ uint8_t s_bak_feas[kNodesPerWave], s_bak_elig[kNodesPerWave], s_bak_mask[kNodesPerWave], s_bak_dirty;
-  __shared__ uint32_t s_bak_grp[14];
   __shared__ unsigned long long s_part[BW][16];
   __shared__ unsigned long long s_glob[16];
   __shared__ uint32_t s_rec[14][kMaxGrid + 4];   // gather-1 records transposed (+4: bank skew)
@@ -1241,55 +1233,6 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       // set's pod b−1: its winner, from its record 3 (best key, and the GPU mask + feasible bit)
       score_a_groups(r, sc, s_feas, s_elig, 0, ngroups);
       if (b >= 1) {
-        const yoda_dev_req_t& rp = *reinterpret_cast<const yoda_dev_req_t*>(s_req[(b - 1) & 3]);
-        // (a.twin) the twin block — the other set's block over this node range — publishes
-        // its best candidate for pod b−1 before the other set's all-gather completes: if pod
-        // b−1's winner is in this range, it is that candidate. Assume it now and redo the
-        // group's filter and score A while the other records arrive; restore the group if the
-        // winner is elsewhere.
-        int spec_j = -1;   // row of the speculatively assumed node (block-uniform)
-        if (a.twin) {
-          uint32_t tv[3];
-          if (!gather<3>(a, tag3 - 3u, 1, q0 + gi, tv, &s_fail)) {
-            ok = false;
-            break;
-          }
-          if (tid == 0) {
-            s_tw[0] = tv[0];
-            s_tw[1] = tv[1];
-            s_tw[2] = tv[2];
-          }
-          __syncthreads();
-          const unsigned long long tk = (unsigned long long)s_tw[1] << 32 | s_tw[0];
-          if (tk != 0) {
-            const uint32_t pc = (uint32_t)(tk & 0xFFFFFFull);
-            const int c = (int)(((pc - rp.perm_add) * rp.perm_inv) & 0xFFFFFFu);
-            if (c >= base && c < base + cnt) {
-              spec_j = c - base;
-              const int gc = spec_j / kNodesPerWave, j0 = gc * kNodesPerWave;
-              // back up the row, its dirty flag and the group's filter / score A outputs
-              if (tid < 32) reinterpret_cast<uint4*>(&s_bak_row)[tid] = reinterpret_cast<const uint4*>(s_rows + spec_j)[tid];
-              if (tid < kNodesPerWave && j0 + tid < cnt) {
-                const int j = j0 + tid;
-                s_bak_feas[tid] = s_feas[j];
-                s_bak_elig[tid] = s_elig[j];
-                s_bak_mask[tid] = s_mask[j];
-                s_bak_raw[tid] = s_raw[j];
-                s_bak_total[tid] = s_total[j];
-                s_bak_quality[tid] = s_quality[j];
-              }
-              if (tid < 14) s_bak_grp[tid] = s_grp[gc][tid];
-              if (tid == 0) s_bak_dirty = s_dirty[spec_j];
-              __syncthreads();
-              if (tid == 0) assume_row(rp, spec_j, s_tw[2] & 0xFFu);
-              __syncthreads();
-              filter_groups(r, par, gc);
-              __syncthreads();
-              score_a_groups(r, sc, s_feas, s_elig, gc, 1);
-              __syncthreads();
-            }
-          }
-        }
         uint32_t v[3];
         if (!gather<3>(a, tag3 - 3u, G, q0, v, &s_fail)) {
           ok = false;
@@ -1306,35 +1249,16 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         if (tid == 0) s_win[0] = feas_prev ? 1 : 0;
         if (have && mk == key) s_win[1] = (int)(v[2] & 0xFFu);   // the winner's record (keys are unique)
         __syncthreads();
-        int w = -1;   // pod b−1's winner (block-uniform)
         if (s_win[0]) {
+          const yoda_dev_req_t& rp = *reinterpret_cast<const yoda_dev_req_t*>(s_req[(b - 1) & 3]);
           const uint32_t pp = (uint32_t)(key & 0xFFFFFFull);
-          w = (int)(((pp - rp.perm_add) * rp.perm_inv) & 0xFFFFFFu);
-        }
-        const bool mine = w >= base && w < base + cnt;   // this replica holds the node
-        if (spec_j >= 0 && !(mine && w - base == spec_j)) {
-          // the winner is elsewhere (or none): put the group back as it was
-          const int gc = spec_j / kNodesPerWave, j0 = gc * kNodesPerWave;
-          if (tid < 32) reinterpret_cast<uint4*>(s_rows + spec_j)[tid] = reinterpret_cast<const uint4*>(&s_bak_row)[tid];
-          if (tid < kNodesPerWave && j0 + tid < cnt) {
-            const int j = j0 + tid;
-            s_feas[j] = s_bak_feas[tid];
-            s_elig[j] = s_bak_elig[tid];
-            s_mask[j] = s_bak_mask[tid];
-            s_raw[j] = s_bak_raw[tid];
-            s_total[j] = s_bak_total[tid];
-            s_quality[j] = s_bak_quality[tid];
+          const int w = (int)(((pp - rp.perm_add) * rp.perm_inv) & 0xFFFFFFu);
+          if (w >= base && w < base + cnt) {   // block-uniform: this replica holds the node
+            if (tid == 0) assume_row(rp, w - base, (uint32_t)s_win[1]);
+            __syncthreads();
+            fix_group = (w - base) / kNodesPerWave;
+            filter_groups(r, par, fix_group);
           }
-          if (tid < 14) s_grp[gc][tid] = s_bak_grp[tid];
-          if (tid == 0) s_dirty[spec_j] = s_bak_dirty;
-          spec_j = -1;
-          __syncthreads();
-        }
-        if (mine && spec_j < 0) {   // not speculated (twin off): assume and redo the filter now
-          if (tid == 0) assume_row(rp, w - base, (uint32_t)s_win[1]);
-          __syncthreads();
-          fix_group = (w - base) / kNodesPerWave;
-          filter_groups(r, par, fix_group);
         }
         __syncthreads();
       }
@@ -1626,7 +1550,6 @@ struct Ctx {
   // (≤ 4096 nodes on MI355X). MI355X, bench mix: 13.5 vs 15.6–16.2 µs/pod at 4096 nodes, 11.9
   // vs 12.8–13.5 at 256 (profiles/device/r4/pairs/). YODA_DEV_PAIRS=0 turns it off
   bool pairs = true;
-  bool twin = false;          // YODA_DEV_TWIN=1: PAIRS fix-up started on the twin block's record
   int occ_blocks_pairs = -1;
   // per spin wait inside k_batch, 100 MHz ticks (YODA_DEV_SPIN_DEADLINE_US): a gather normally
   // completes in microseconds; 20 ms only elapses when a block is not resident (a tenant
@@ -1773,7 +1696,6 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
   if (const char* v = getenv("YODA_DEV_HOST_DEADLINE_US")) c->host_deadline_us = atof(v) > 0 ? atof(v) : 1.0;
   if (const char* v = getenv("YODA_DEV_BWAVES")) c->batch_waves = atoi(v) == 4 ? 4 : atoi(v) == 8 ? 8 : 0;
   if (const char* v = getenv("YODA_DEV_PAIRS")) c->pairs = v[0] != '0';
-  if (const char* v = getenv("YODA_DEV_TWIN")) c->twin = v[0] != '0';
   if (const char* v = getenv("YODA_DEV_DIRECT_ATOMICS")) c->direct_atomics = v[0] == '1' ? 1 : 0;
   if (const char* v = getenv("YODA_DEV_FUSE_MAX")) c->fuse_max = atoi(v);
   const SubsetTable st = make_subsets();
@@ -2044,7 +1966,6 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
     a.ticket = c->d_words;
     a.abort_word = c->d_words + 1;
     a.trace = c->d_trace;
-    a.twin = c->twin ? 1 : 0;
     __atomic_store_n(c->h_done, 0, __ATOMIC_RELEASE);
     if (c->timing) CK(hipEventRecord(c->e0, c->stream));
     if (pairs && m >= 2) {

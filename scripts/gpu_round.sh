@@ -86,13 +86,6 @@ for s in $STEPS; do
         step "pairs/one_$k" 200 env YODA_DEV_PAIRS=0 python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
         step "pairs/two_$k" 200 env YODA_DEV_PAIRS=1 python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
       done ;;
-    twin)   # PAIRS fix-up started on the twin block's record 3 (YODA_DEV_TWIN=1) vs after the all-gather; parity suite with it
-      mkdir -p gpurun_out/twin
-      step "twin/tests" 600 env YODA_DEV_TWIN=1 python -u -m pytest tests/test_gpu_device_scorer.py -x -q --timeout 120 --timeout-method thread
-      for k in 1 2; do
-        step "twin/off_$k" 200 env YODA_DEV_TWIN=0 python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
-        step "twin/on_$k" 200 env YODA_DEV_TWIN=1 python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
-      done ;;
     testspairs) step gpu_tests_pairs 600 env YODA_DEV_PAIRS=1 python -u -m pytest tests/test_gpu_device_scorer.py -x -v --timeout 120 --timeout-method thread ;;
     mixlog) step mixlog 300 env YODA_BENCH_RUNLOG=1 python bench.py --config 3 --mix-anti 10 --steps 5 --warmup 3 --alt none ;;
     scope6) step scope6 300 env YODA_BENCH_THREADS=2 python bench.py --config 6 --steps 5 --warmup 1 --alt none ;;
