@@ -1478,7 +1478,10 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     TRACE(8);
   }
 
-  // ---- epilogue: dirty rows back to the table; the last block hands the results to the host
+  // ---- epilogue: dirty rows back to the table; the last block hands the results to the host.
+  // PAIRS: only the set that ran the batch's last pod holds every assume (the other set never
+  // learns that pod's winner), so only its replica is written back
+  if (!PAIRS || set == ((a.B - 1) & 1))
   for (int t = tid; t < cnt * 32; t += kBB) {
     const int row = t >> 5;
     if (s_dirty[row]) reinterpret_cast<uint4*>(a.nodes + base + row)[t & 31] = reinterpret_cast<const uint4*>(s_rows + row)[t & 31];

@@ -478,6 +478,11 @@ def test_k_batch_two_pods_in_flight_matches_one_at_a_time(require_gpu, n, pods):
     for k, lab in enumerate([{"scv/memory": "900000"}, {"scv/number": "9"}, {"scv/number": "8", "scv/memory": "1024"}]):
         pods_.insert(12 + 5 * k, PodInfo.from_obj({"metadata": {"name": f"x{k}", "uid": f"pp-x-{n}-{k}", "labels": lab},
                                                    "spec": {}}))
+    # the batch ends with 8-GPU gangs: each takes a whole node, so a device table that missed
+    # the last assumes would offer those nodes to the follow-up gang cycles below
+    for k in range(2):
+        pods_.append(PodInfo.from_obj({"metadata": {"name": f"g8-{k}", "uid": f"pp-g8-{n}-{k}",
+                                                    "labels": {"scv/number": "8", "scv/memory": "1024"}}, "spec": {}}))
     res_a = a.schedule_batch([p.num_id for p in pods_], [pod_req(a, p) for p in pods_])
     assert ds.counters(a)["last_pairs"] == 1
     res_b = b.schedule_batch([p.num_id for p in pods_], [pod_req(b, p) for p in pods_])
@@ -488,6 +493,15 @@ def test_k_batch_two_pods_in_flight_matches_one_at_a_time(require_gpu, n, pods):
     assert a.device_fallbacks == 0 and b.device_fallbacks == 0
     for i in range(0, n, max(1, n // 97)):
         assert a.node_cards(i) == b.node_cards(i)
+    assert res_a[-1][0] >= 0 or res_a[-2][0] >= 0     # a gang placed at the end of the batch
+    # the device tables hold every assume of the batch, the last ones included
+    for k in range(3):
+        gang = PodInfo.from_obj({"metadata": {"name": f"g8-after-{k}", "uid": f"pp-g8a-{n}-{k}",
+                                              "labels": {"scv/number": "8", "scv/memory": "1024"}}, "spec": {}})
+        for e in (a, b):
+            assert not ds.compare_cycle(e, pod_req(e, gang)), (e is a, k)
+        a.schedule(gang.num_id, pod_req(a, gang), True)
+        b.schedule(gang.num_id, pod_req(b, gang), True)
     rng2 = random.Random(n + 6)
     for k in range(6):
         pi, req = ds.random_request(a, rng2, f"pp-after-{n}-{k}")
