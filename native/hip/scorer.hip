@@ -1233,6 +1233,9 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       // set's pod b−1: its winner, from its record 3 (best key, and the GPU mask + feasible bit)
       score_a_groups(r, sc, s_feas, s_elig, 0, ngroups);
       if (b >= 1) {
+        // (slots are double-buffered by tag parity: the other set overwrites this record only
+        // with its pod b+1's record 1, which it publishes after this set's pod b record 3 —
+        // i.e. after this read)
         uint32_t v[3];
         if (!gather<3>(a, tag3 - 3u, G, q0, v, &s_fail)) {
           ok = false;
