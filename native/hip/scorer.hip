@@ -253,7 +253,9 @@ __global__ void k_upload_done(int32_t* flag, int32_t seq) {
 // ------------------------------------------------------------------ K1: filter + maxima
 // One lane group = one node (lane `sub` = GPU slot). Returns the node's filter reason (0 =
 // feasible) and its eligible-GPU mask, and folds the card metrics of feasible nodes into the
-// wave maxima `wmx` (wave-uniform afterwards). Shared by k_filter and k_batch.
+// wave maxima `wmx` (wave-uniform afterwards). Shared by k_filter and k_batch. `MAXIMA`
+// false: the verdict and mask only (wmx untouched; the PAIRS fix-up's scoring waves).
+template <bool MAXIMA = true>
 __device__ __forceinline__ int filter_eval(const yoda_dev_node_t* nd, bool valid, const yoda_dev_req_t& r,
                                            uint8_t cnd, uint32_t* wmx, uint32_t& emask_out, int grp, int sub) {
   const bool yoda = (r.filters & F_YODA) != 0;
@@ -289,7 +291,7 @@ __device__ __forceinline__ int filter_eval(const yoda_dev_node_t* nd, bool valid
   if (yoda_stage && (uint64_t)__popc(emask) < r.number) reason = RS_GPU_FIT;
   const bool ok = valid && reason == 0;
   emask_out = emask;
-  if (yoda) {
+  if (MAXIMA && yoda) {
     const bool take = ok && ((emask >> sub) & 1u);
     // card metrics are u32 (ef ≤ free): 32-bit shuffles
     uint32_t v[6];
@@ -944,7 +946,7 @@ static_assert(kResWords == 19 && YODA_DEV_REASONS == 16 && offsetof(yoda_dev_res
 // the reason codes of c_batch_reasons, for compile-time indexing
 constexpr int kBatchReasonCodes[7] = {RS_UNSCHEDULABLE, RS_RESOURCES, RS_NO_SCV, RS_STALE, RS_GPU_NUMBER,
                                       RS_GPU_FIT, RS_DEAD};
-constexpr int kTracePts = 16;   // 9 phase stamps per pod (block 0), padded
+constexpr int kTracePts = 16;   // 9 phase stamps per pod (block 0), 5 of the PAIRS fix-up's owner, padded
 constexpr int kReqWords = sizeof(yoda_dev_req_t) / 4;
 static_assert(sizeof(yoda_dev_req_t) % 4 == 0 && kReqWords <= 64, "req fits one wave");
 
@@ -1037,7 +1039,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   __shared__ uint8_t s_masks[256];
   // request ring: pods b (and b−1 in PAIRS mode, for its assume) plus the prefetched next ones
   __shared__ __align__(16) uint32_t s_req[4][sizeof(yoda_dev_req_t) / 4];
-  __shared__ int s_win[2];   // PAIRS: the previous pod's winner (node or −1) and its GPU mask
+  __shared__ int s_fix;   // PAIRS: the other set's last winner's row here, or −1
   __shared__ unsigned long long s_part[BW][16];
   __shared__ unsigned long long s_glob[16];
   __shared__ uint32_t s_rec[14][kMaxGrid + 4];   // gather-1 records transposed (+4: bank skew)
@@ -1045,6 +1047,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   __shared__ uint32_t s_grp[kMaxGroups][14];
   __shared__ GangBest s_gang[8 * BW];
   __shared__ int s_fail;
+  __shared__ uint32_t s_bfeas;   // this block's feasible nodes for the current pod (record 1)
   __shared__ bool s_last;
   static_assert(sizeof(yoda_dev_result_t) % 8 == 0, "result copied as u64 words");
 
@@ -1094,13 +1097,10 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   // Filter every 8-node group of this block for request `rq` (or only group `only`) into the
   // parity-`par` feasibility arrays (pod parity: phase A of a pod never reads what the next
   // pod's filter writes) and the per-group aggregates s_grp. Wave-uniform.
-  auto filter_groups = [&](const yoda_dev_req_t& rq, int par, int only) {
-    uint8_t* fe = s_feas2 + par * npb;
-    uint8_t* el = s_elig2 + par * npb;
-    for (int j0 = wave * kNodesPerWave; j0 < cnt; j0 += BW * kNodesPerWave) {
-      const int gq = j0 / kNodesPerWave;
-      if (only >= 0 && gq != only) continue;
-      const int j = j0 + grp;
+  auto filter_one = [&](const yoda_dev_req_t& rq, int par, int gq) {
+      uint8_t* fe = s_feas2 + par * npb;
+      uint8_t* el = s_elig2 + par * npb;
+      const int j = gq * kNodesPerWave + grp;
       const bool valid = j < cnt;
       uint32_t wmx[6] = {1, 1, 1, 1, 1, 1};
       uint32_t emask = 0;
@@ -1122,14 +1122,65 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
 #pragma unroll
         for (int q = 0; q < 7; ++q) s_grp[gq][7 + q] = rc[q];
       }
+  };
+  auto filter_groups = [&](const yoda_dev_req_t& rq, int par) {
+    for (int gq = wave; gq * kNodesPerWave < cnt; gq += BW) filter_one(rq, par, gq);
+  };
+  // record 1 from the group aggregates: threads 0..kRec1-1 (wave 0), after every group's
+  // s_grp row is visible to them
+  auto record1 = [&](uint32_t tag1) {
+    if (tid < kRec1) {   // block totals over the groups → the record's 11 granules
+      const int ngr = (cnt + kNodesPerWave - 1) / kNodesPerWave;
+      uint32_t v;
+      if (tid < 7) {
+        v = tid < 6 ? 1u : 0u;
+        for (int q = 0; q < ngr; ++q) v = tid < 6 ? (s_grp[q][tid] > v ? s_grp[q][tid] : v) : v + s_grp[q][tid];
+        if (tid == 6) s_bfeas = v;
+      } else {   // reason counts packed as u16 pairs (≤ npb ≤ 256 per block)
+        const int r0 = 7 + 2 * (tid - 7);
+        uint32_t lo = 0, hi = 0;
+        for (int q = 0; q < ngr; ++q) {
+          lo += s_grp[q][r0];
+          hi += r0 + 1 < 14 ? s_grp[q][r0 + 1] : 0u;
+        }
+        v = lo | (hi << 16);
+      }
+      store_granule(slot_ptr(a, tag1, g) + tid, tag1, v);
+    }
+  };
+
+  // Replica 0 of each node in [j_lo, j_lo + span) scored with its own subset best: where
+  // another of the `nrep` replicas (s_gang[q·span + node]) found a better set, take it and move
+  // the gang bonus (the only score term that depends on the set). After a barrier.
+  auto merge_gang = [&](const yoda_dev_req_t& r, const ScoreConsts& sc, const uint8_t* s_feas, int j_lo, int span,
+                        int nrep) {
+    for (int j = j_lo + tid; j < cnt && j < j_lo + span; j += kBB) {
+      if (!s_feas[j]) continue;
+      const GangBest b0 = s_gang[j - j_lo];
+      GangBest bb = b0;
+      for (int q = 1; q < nrep; ++q) {
+        const GangBest o = s_gang[q * span + (j - j_lo)];
+        if (o.found && (!bb.found || better(o.o, o.m, bb.o, bb.m))) bb = o;
+      }
+      if (bb.found == b0.found && bb.m == b0.m) continue;
+      const int32_t q_old = s_quality[j];
+      const int32_t q_new = bb.found ? 10000 - sdiv_small_r(bb.lb, 100, 0.01) : 10000;
+      s_mask[j] = bb.m;
+      s_quality[j] = q_new;
+      if (sc.yoda_s && r.has_number && r.number > 1 && r.number <= s_rows[j].ncards) {
+        uint64_t rb = (uint64_t)s_raw[j];
+        if (b0.found) rb -= (uint64_t)(q_old / 100) * (uint64_t)r.w_gang_score;
+        if (bb.found) rb += (uint64_t)(q_new / 100) * (uint64_t)r.w_gang_score;
+        s_raw[j] = (int64_t)rb;
+      }
     }
   };
 
   // Score A (gang search, the yoda terms that need no maxima — kept in s_raw until phase B —,
   // default scores) for the 8-node groups [gfirst, gfirst + gcount) of this block. A
   // multi-GPU pod's subset search is split over `nrep` lane groups per node when the block has
-  // more waves than those groups (8 waves over 32 nodes: two groups per node; one group alone
-  // — the PAIRS fix-up — gets every wave); the replicas' bests meet through LDS. Wave-uniform.
+  // more waves than those groups (8 waves over 32 nodes: two groups per node); the replicas'
+  // bests meet through LDS. Wave-uniform.
   const int ngroups = (npb + kNodesPerWave - 1) / kNodesPerWave;
   auto score_a_groups = [&](const yoda_dev_req_t& r, const ScoreConsts& sc, const uint8_t* s_feas,
                             const uint8_t* s_elig, int gfirst, int gcount) {
@@ -1157,28 +1208,34 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     }
     if (nrep > 1) {
       __syncthreads();
-      // replica 0 scored with its own best: where another replica found a better set,
-      // take it and move the gang bonus (the only score term that depends on the set)
-      for (int j = j_lo + tid; j < cnt && j < j_lo + span; j += kBB) {
-        if (!s_feas[j]) continue;
-        const GangBest b0 = s_gang[j - j_lo];
-        GangBest bb = b0;
-        for (int q = 1; q < nrep; ++q) {
-          const GangBest o = s_gang[q * span + (j - j_lo)];
-          if (o.found && (!bb.found || better(o.o, o.m, bb.o, bb.m))) bb = o;
-        }
-        if (bb.found == b0.found && bb.m == b0.m) continue;
-        const int32_t q_old = s_quality[j];
-        const int32_t q_new = bb.found ? 10000 - sdiv_small_r(bb.lb, 100, 0.01) : 10000;
-        s_mask[j] = bb.m;
-        s_quality[j] = q_new;
-        if (sc.yoda_s && r.has_number && r.number > 1 && r.number <= s_rows[j].ncards) {
-          uint64_t rb = (uint64_t)s_raw[j];
-          if (b0.found) rb -= (uint64_t)(q_old / 100) * (uint64_t)r.w_gang_score;
-          if (bb.found) rb += (uint64_t)(q_new / 100) * (uint64_t)r.w_gang_score;
-          s_raw[j] = (int64_t)rb;
-        }
-      }
+      merge_gang(r, sc, s_feas, j_lo, span, nrep);
+    }
+  };
+
+  // PAIRS fix-up, score A of group `gq` on waves 1..BW−1 while wave 0 re-filters it for record 1:
+  // each scoring wave evaluates the group's filter verdict and eligible mask itself (no maxima,
+  // no LDS hand-off from wave 0), a multi-GPU search split over `nrep` = BW−1 waves (the
+  // caller merges after the barrier that joins wave 0).
+  auto score_a_fix = [&](const yoda_dev_req_t& r, const ScoreConsts& sc, int gq, int nrep) {
+    const int rep = wave - 1;
+    if (rep < 0 || rep >= nrep) return;   // wave-uniform
+    const int j = gq * kNodesPerWave + grp;
+    const bool valid = j < cnt;
+    const yoda_dev_node_t* nd = s_rows + (valid ? j : 0);
+    uint32_t wmx_unused[6], emask = 0;
+    const int reason = filter_eval<false>(nd, valid, r, 0, wmx_unused, emask, grp, sub);
+    const bool act = valid && reason == 0;
+    uint64_t rbase = 0;
+    int64_t total_v = 0;
+    uint32_t mask_v = 0;
+    int32_t quality_v = 0;
+    score_node_a(nd, act, act ? emask : 0u, r, sc, s_masks, sub, rbase, total_v, mask_v, quality_v, rep, nrep,
+                 nrep > 1 ? &s_gang[rep * kNodesPerWave + grp] : nullptr);
+    if (act && sub == 0 && rep == 0) {
+      s_raw[j] = (int64_t)rbase;
+      s_total[j] = total_v;
+      s_mask[j] = (uint8_t)mask_v;
+      s_quality[j] = quality_v;
     }
   };
 
@@ -1187,11 +1244,14 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   auto assume_row = [&](const yoda_dev_req_t& rq, int j, uint32_t mask) {
     yoda_dev_node_t* nd = s_rows + j;
     const uint32_t mb = (uint32_t)rq.memory;
-    for (int c = 0; c < YODA_DEV_CARDS; ++c)
-      if ((mask >> c) & 1u) {
-        nd->cards[c].reserved += mb;
-        nd->cards[c].pending += mb;
-      }
+    // branch-free: every card's two words are loaded together instead of a dependent LDS
+    // round trip per taken card
+#pragma unroll
+    for (int c = 0; c < YODA_DEV_CARDS; ++c) {
+      const uint32_t add = ((mask >> c) & 1u) ? mb : 0u;
+      nd->cards[c].reserved += add;
+      nd->cards[c].pending += add;
+    }
     nd->pod_count += 1;
     nd->req_cpu += rq.cpu_m;
     nd->req_mem += rq.mem;
@@ -1224,15 +1284,17 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     const int par = PAIRS ? ((b >> 1) & 1) : (b & 1);   // this set's consecutive pods alternate
     uint8_t* s_feas = s_feas2 + par * npb;
     uint8_t* s_elig = s_elig2 + par * npb;
-    filter_groups(r, par, -1);
+    filter_groups(r, par);
     __syncthreads();
     ScoreConsts sc = score_consts(r, nullptr);
-    int fix_group = -1;   // PAIRS: the group whose score A is redone while record 1 travels
+    int fix = -1;   // PAIRS: the other set's last winner's row, in its owner block only
     if constexpr (PAIRS) {
       // score A of every group now, against the rows as of this set's last pod; then the other
-      // set's pod b−1: its winner, from its record 3 (best key, and the GPU mask + feasible bit)
+      // set's pod b−1: its winner, from its record 3 (best key; the GPU mask, whether the record's
+      // block had a feasible node, whether the pod fit anywhere)
       score_a_groups(r, sc, s_feas, s_elig, 0, ngroups);
       if (b >= 1) {
+        if (tid == 0) s_fix = -1;   // ordered before the holder's write by the gather's barrier
         // (slots are double-buffered by tag parity: the other set overwrites this record only
         // with its pod b+1's record 1, which it publishes after this set's pod b record 3 —
         // i.e. after this read)
@@ -1241,6 +1303,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           ok = false;
           break;
         }
+        const unsigned long long t_g3 = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
         const bool have = tid < G;
         const unsigned long long mk = have ? ((unsigned long long)v[1] << 32 | v[0]) : 0ull;
         const unsigned long long wk = wave_max(mk);
@@ -1248,50 +1311,52 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         __syncthreads();
         unsigned long long key = 0;
         for (int w = 0; w < BW; ++w) key = s_part[w][0] > key ? s_part[w][0] : key;
-        const bool feas_prev = ((v[2] >> 8) & 1u) != 0;   // every record carries it (thread 0's is read)
-        if (tid == 0) s_win[0] = feas_prev ? 1 : 0;
-        if (have && mk == key) s_win[1] = (int)(v[2] & 0xFFu);   // the winner's record (keys are unique)
-        __syncthreads();
-        if (s_win[0]) {
+        // the one record that holds the winner: its key, from a block with a feasible node
+        // (keys of feasible nodes are unique; a block without one reports key 0), and the pod
+        // fit somewhere. Its thread applies the assume if this block holds the node.
+        if (have && mk == key && ((v[2] >> 9) & 1u) && ((v[2] >> 8) & 1u)) {
           const yoda_dev_req_t& rp = *reinterpret_cast<const yoda_dev_req_t*>(s_req[(b - 1) & 3]);
           const uint32_t pp = (uint32_t)(key & 0xFFFFFFull);
           const int w = (int)(((pp - rp.perm_add) * rp.perm_inv) & 0xFFFFFFu);
-          if (w >= base && w < base + cnt) {   // block-uniform: this replica holds the node
-            if (tid == 0) assume_row(rp, w - base, (uint32_t)s_win[1]);
-            __syncthreads();
-            fix_group = (w - base) / kNodesPerWave;
-            filter_groups(r, par, fix_group);
+          if (w >= base && w < base + cnt) {
+            assume_row(rp, w - base, v[2] & 0xFFu);
+            s_fix = w - base;
+            if (a.trace) a.trace[(size_t)b * kTracePts + 13] = t_g3;
           }
         }
         __syncthreads();
+        fix = s_fix;
       }
-    }
-    if (tid < kRec1) {   // block totals over the groups → the record's 11 granules
-      const int ngr = (cnt + kNodesPerWave - 1) / kNodesPerWave;
-      uint32_t v;
-      if (tid < 7) {
-        v = tid < 6 ? 1u : 0u;
-        for (int q = 0; q < ngr; ++q) v = tid < 6 ? (s_grp[q][tid] > v ? s_grp[q][tid] : v) : v + s_grp[q][tid];
-      } else {   // reason counts packed as u16 pairs (≤ npb ≤ 256 per block)
-        const int r0 = 7 + 2 * (tid - 7);
-        uint32_t lo = 0, hi = 0;
-        for (int q = 0; q < ngr; ++q) {
-          lo += s_grp[q][r0];
-          hi += r0 + 1 < 14 ? s_grp[q][r0 + 1] : 0u;
+      if (fix >= 0) {
+        // owner: wave 0 re-filters the winner's group and sends record 1 (its s_grp row is
+        // written and read by wave 0 alone: LDS operations of one wave complete in order)
+        // while the other waves score it
+        const int fg = fix / kNodesPerWave;
+        const int nrep = (sc.search && sc.k > 1) ? BW - 1 : 1;
+        if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 9] = __builtin_amdgcn_s_memrealtime();
+        if (wave == 0) {
+          filter_one(r, par, fg);
+          __builtin_amdgcn_wave_barrier();
+          record1(tag1);
+          if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 10] = __builtin_amdgcn_s_memrealtime();
+        } else {
+          score_a_fix(r, sc, fg, nrep);
         }
-        v = lo | (hi << 16);
+        __syncthreads();
+        if (nrep > 1) merge_gang(r, sc, s_feas, fg * kNodesPerWave, kNodesPerWave, nrep);
+        if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 11] = __builtin_amdgcn_s_memrealtime();
+      } else {
+        record1(tag1);
       }
-      store_granule(slot_ptr(a, tag1, g) + tid, tag1, v);
-    }
-    TRACE(1);
-
-    // ================= phase A (while record 1 travels). PAIRS: only the fix-up group
-    if (PAIRS) {
-      if (fix_group >= 0) score_a_groups(r, sc, s_feas, s_elig, fix_group, 1);
+      TRACE(1);
+      TRACE(2);
     } else {
+      record1(tag1);
+      TRACE(1);
+      // ================= phase A (while record 1 travels)
       score_a_groups(r, sc, s_feas, s_elig, 0, ngroups);
+      TRACE(2);
     }
-    TRACE(2);
 
     // ================= gather 1: global maxima, feasible and reason counts
     {
@@ -1328,6 +1393,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       }
       __syncthreads();
     }
+    if (PAIRS && fix >= 0 && a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 12] = __builtin_amdgcn_s_memrealtime();
     int reasons7[7];
 #pragma unroll
     for (int q = 0; q < 7; ++q) reasons7[q] = (int)s_glob[7 + q];
@@ -1418,14 +1484,15 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         unsigned long long bb = 0;
         for (int w = 0; w < BW; ++w) bb = s_part[w][0] > bb ? s_part[w][0] : bb;
         uint32_t x = tid == 0 ? (uint32_t)bb : (uint32_t)(bb >> 32);
-        if (tid == 2) {   // PAIRS: the block best's GPU mask and whether the pod fits anywhere
+        if (tid == 2) {   // PAIRS: the block best's GPU mask, whether the pod fits anywhere and here
           uint32_t m = 0;
-          if (bb != 0) {
+          const bool here = s_bfeas > 0;   // (a best key of 0 is a feasible node's when here)
+          if (here) {
             const uint32_t pb = (uint32_t)(bb & 0xFFFFFFull);
             const int nb = (int)(((pb - r.perm_add) * r.perm_inv) & 0xFFFFFFu);
             if (nb >= base && nb < base + cnt) m = s_mask[nb - base];
           }
-          x = m | ((nf > 0 ? 1u : 0u) << 8);
+          x = m | ((nf > 0 ? 1u : 0u) << 8) | ((here ? 1u : 0u) << 9);
         }
         store_granule(slot_ptr(a, tag3, g) + tid, tag3, x);
       }
@@ -2097,7 +2164,11 @@ int yoda_dev_batch_trace(void* p, int on, unsigned long long* out, int max_pods)
   Ctx* c = (Ctx*)p;
   if (!c) return -1;
   CK(hipSetDevice(c->device));
-  if (on && !c->d_trace) CK(hipMalloc(&c->d_trace, (size_t)kBatchCap * kTracePts * 8));
+  if (on && !c->d_trace) {
+    CK(hipMalloc(&c->d_trace, (size_t)kBatchCap * kTracePts * 8));
+    // the PAIRS owner stamps (9..13) are written only for pods with a fix-up: zero = none
+    CK(hipMemset(c->d_trace, 0, (size_t)kBatchCap * kTracePts * 8));
+  }
   if (!on && c->d_trace) {
     CK(hipFree(c->d_trace));
     c->d_trace = nullptr;

@@ -70,7 +70,9 @@ def run(nodes: int, mode: str, pods: int, batch: int, trace: bool = False, busy:
             eng.schedule_batch([p for p, _ in chunk], [r for _, r in chunk])
             tr = ds.read_batch_trace(eng)
             if tr:
-                extra["phase_us_mean"] = {k: round(sum(x[k] for x in tr) / len(tr), 2) for k in tr[0]}
+                keys = list(dict.fromkeys(k for x in tr for k in x))   # owner phases: pods with a fix-up
+                extra["phase_us_mean"] = {k: round(sum(x[k] for x in tr if k in x) / sum(k in x for x in tr), 2)
+                                          for k in keys}
                 by_k: dict = {}
                 for x, kk in zip(tr, ks[8:8 + len(tr)]):
                     by_k.setdefault(kk, []).append(x["score_a"])

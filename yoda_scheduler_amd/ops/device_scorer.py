@@ -38,6 +38,10 @@ def set_pairs(engine, on: bool) -> None:
 # maxima-free terms) while record 1 travels; gather 1 (maxima); part B (normalised metrics)
 # → record 2 out; gather 2 (raw lo/hi); select → record 3 out; gather 3 (winner); publish
 TRACE_PHASES = ("filter", "score_a", "gather1", "score_b", "gather2", "select", "gather3", "publish")
+# PAIRS, the block that owns the other set's last winner (stamps 13, 9..12): record 3 gathered →
+# winner known and assumed, → record 1 sent (re-filtered group), → the group scored, → gather 1 done
+OWNER_PHASES = (("own_winner", 13, 9), ("own_filter_rec1", 9, 10), ("own_score_a", 9, 11),
+                ("own_gather1", 11, 12), ("own_to_gather1", 13, 12))
 
 
 def batch_trace(engine, on: bool = True) -> None:
@@ -66,7 +70,10 @@ def read_batch_trace(engine, max_pods: int = 256) -> list[dict]:
     out = []
     for b in range(max(m, 0)):
         t = [buf[b * W + k] for k in range(W)]
-        out.append({ph: (t[k + 1] - t[k]) / 100.0 for k, ph in enumerate(TRACE_PHASES)})
+        d = {ph: (t[k + 1] - t[k]) / 100.0 for k, ph in enumerate(TRACE_PHASES)}
+        if t[13] and t[9] and t[12]:   # PAIRS: the fix-up owner's stamps (a pod with one)
+            d.update({ph: (t[hi] - t[lo]) / 100.0 for ph, lo, hi in OWNER_PHASES})
+        out.append(d)
     return out
 
 
