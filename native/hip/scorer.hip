@@ -1042,6 +1042,9 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   __shared__ int s_fix;   // PAIRS: the other set's last winner's row here, or −1
   __shared__ unsigned long long s_part[BW][16];
   __shared__ unsigned long long s_glob[16];
+  // G ≤ 64: wave 0 holds every record of a gather and reduces it alone; the result reaches the
+  // block through these words and one barrier (no per-wave partials, no second barrier)
+  __shared__ unsigned long long s_red[2];
   __shared__ uint32_t s_rec[14][kMaxGrid + 4];   // gather-1 records transposed (+4: bank skew)
   // filter aggregates per 8-node group: 6 maxima, feasible count, 7 reason counts
   __shared__ uint32_t s_grp[kMaxGroups][14];
@@ -1306,11 +1309,15 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         const unsigned long long t_g3 = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
         const bool have = tid < G;
         const unsigned long long mk = have ? ((unsigned long long)v[1] << 32 | v[0]) : 0ull;
-        const unsigned long long wk = wave_max(mk);
-        if (lane == 0) s_part[wave][0] = wk;
-        __syncthreads();
         unsigned long long key = 0;
-        for (int w = 0; w < BW; ++w) key = s_part[w][0] > key ? s_part[w][0] : key;
+        if (G <= 64) {
+          if (wave == 0) key = wave_max(mk);   // the holder is in wave 0 too
+        } else {
+          const unsigned long long wk = wave_max(mk);
+          if (lane == 0) s_part[wave][0] = wk;
+          __syncthreads();
+          for (int w = 0; w < BW; ++w) key = s_part[w][0] > key ? s_part[w][0] : key;
+        }
         // the one record that holds the winner: its key, from a block with a feasible node
         // (keys of feasible nodes are unique; a block without one reports key 0), and the pod
         // fit somewhere. Its thread applies the assume if this block holds the node.
@@ -1445,18 +1452,31 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       const bool have = tid < G;
       const unsigned long long mlo = have ? ((unsigned long long)v[1] << 32 | v[0]) : ULLONG_MAX;
       const unsigned long long mhi = have ? ((unsigned long long)v[3] << 32 | v[2]) : 0ull;
-      const unsigned long long wlo = wave_min(mlo), whi = wave_max(mhi);
-      __syncthreads();
-      if (lane == 0) {
-        s_part[wave][0] = wlo;
-        s_part[wave][1] = whi;
+      if (G <= 64) {
+        if (wave == 0) {
+          const unsigned long long wlo = wave_min(mlo), whi = wave_max(mhi);
+          if (lane == 0) {
+            s_red[0] = wlo;
+            s_red[1] = whi;
+          }
+        }
+        __syncthreads();
+        glo = s_red[0];
+        ghi = s_red[1];
+      } else {
+        // (the gather's barrier ordered every read of the record-2 partials before these writes)
+        const unsigned long long wlo = wave_min(mlo), whi = wave_max(mhi);
+        if (lane == 0) {
+          s_part[wave][0] = wlo;
+          s_part[wave][1] = whi;
+        }
+        __syncthreads();
+        for (int w = 0; w < BW; ++w) {
+          glo = s_part[w][0] < glo ? s_part[w][0] : glo;
+          ghi = s_part[w][1] > ghi ? s_part[w][1] : ghi;
+        }
+        __syncthreads();
       }
-      __syncthreads();
-      for (int w = 0; w < BW; ++w) {
-        glo = s_part[w][0] < glo ? s_part[w][0] : glo;
-        ghi = s_part[w][1] > ghi ? s_part[w][1] : ghi;
-      }
-      __syncthreads();
     }
     TRACE(5);
 
@@ -1503,11 +1523,19 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         break;
       }
       const unsigned long long mk = tid < G ? ((unsigned long long)v[1] << 32 | v[0]) : 0ull;
-      const unsigned long long wk = wave_max(mk);
-      __syncthreads();
-      if (lane == 0) s_part[wave][0] = wk;
-      __syncthreads();
-      for (int w = 0; w < BW; ++w) key = s_part[w][0] > key ? s_part[w][0] : key;
+      if (G <= 64) {
+        if (wave == 0) {
+          const unsigned long long wk = wave_max(mk);
+          if (lane == 0) s_red[0] = wk;
+        }
+        __syncthreads();
+        key = s_red[0];
+      } else {
+        const unsigned long long wk = wave_max(mk);
+        if (lane == 0) s_part[wave][0] = wk;
+        __syncthreads();
+        for (int w = 0; w < BW; ++w) key = s_part[w][0] > key ? s_part[w][0] : key;
+      }
     }
     TRACE(7);
 
