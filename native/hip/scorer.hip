@@ -544,7 +544,7 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
                                              const yoda_dev_req_t& r, const ScoreConsts& sc,
                                              const uint8_t* s_masks, int sub, uint64_t& rbase_o, int64_t& total_o,
                                              uint32_t& mask_o, int32_t& quality_o, int rep = 0, int nrep = 1,
-                                             GangBest* gang_o = nullptr) {
+                                             GangBest* gang_o = nullptr, unsigned long long* stamp = nullptr) {
   const int k = sc.k;
   const bool search = sc.search, yoda_s = sc.yoda_s;
   const int32_t P = sc.P;
@@ -571,6 +571,7 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
       fsum += ef[a];
     }
   }
+  if (stamp) stamp[0] = __builtin_amdgcn_s_memrealtime();   // (trace) tables loaded
   // ---- gang / GPU-set selection (the Reserve choice if this node wins); the 8 lanes'
   // candidates meet through DPP moves inside the group (the whole group is in the branch)
 #define GANG_STEP1(CTRL)                                              \
@@ -705,6 +706,7 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
   }
 #undef GANG_STEP1
 #undef GANG_STEP
+  if (stamp) stamp[1] = __builtin_amdgcn_s_memrealtime();   // (trace) GPU set chosen
   if (gang_o && act && sub == 0) *gang_o = GangBest{best_o, best_lb, (uint8_t)best_m, (uint8_t)found};
   const int32_t quality = found ? 10000 - sdiv_small_r(best_lb, 100, 0.01) : 10000;
   // ---- yoda score terms that need no maxima (algorithm.go:28-87 with the Q1/Q2/Q3/Q4
@@ -946,7 +948,7 @@ static_assert(kResWords == 19 && YODA_DEV_REASONS == 16 && offsetof(yoda_dev_res
 // the reason codes of c_batch_reasons, for compile-time indexing
 constexpr int kBatchReasonCodes[7] = {RS_UNSCHEDULABLE, RS_RESOURCES, RS_NO_SCV, RS_STALE, RS_GPU_NUMBER,
                                       RS_GPU_FIT, RS_DEAD};
-constexpr int kTracePts = 16;   // 9 phase stamps per pod (block 0), 5 of the PAIRS fix-up's owner, padded
+constexpr int kTracePts = 24;   // 9 phase stamps per pod (block 0), 9 of the PAIRS fix-up's owner, padded
 constexpr int kReqWords = sizeof(yoda_dev_req_t) / 4;
 static_assert(sizeof(yoda_dev_req_t) % 4 == 0 && kReqWords <= 64, "req fits one wave");
 
@@ -1219,7 +1221,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   // each scoring wave evaluates the group's filter verdict and eligible mask itself (no maxima,
   // no LDS hand-off from wave 0), a multi-GPU search split over `nrep` = BW−1 waves (the
   // caller merges after the barrier that joins wave 0).
-  auto score_a_fix = [&](const yoda_dev_req_t& r, const ScoreConsts& sc, int gq, int nrep) {
+  auto score_a_fix = [&](const yoda_dev_req_t& r, const ScoreConsts& sc, int gq, int nrep, int tb) {
     const int rep = wave - 1;
     if (rep < 0 || rep >= nrep) return;   // wave-uniform
     const int j = gq * kNodesPerWave + grp;
@@ -1228,12 +1230,15 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     uint32_t wmx_unused[6], emask = 0;
     const int reason = filter_eval<false>(nd, valid, r, 0, wmx_unused, emask, grp, sub);
     const bool act = valid && reason == 0;
+    if (a.trace && tid == 64) a.trace[(size_t)tb * kTracePts + 14] = __builtin_amdgcn_s_memrealtime();
     uint64_t rbase = 0;
     int64_t total_v = 0;
     uint32_t mask_v = 0;
     int32_t quality_v = 0;
     score_node_a(nd, act, act ? emask : 0u, r, sc, s_masks, sub, rbase, total_v, mask_v, quality_v, rep, nrep,
-                 nrep > 1 ? &s_gang[rep * kNodesPerWave + grp] : nullptr);
+                 nrep > 1 ? &s_gang[rep * kNodesPerWave + grp] : nullptr,
+                 (a.trace && tid == 64) ? a.trace + (size_t)tb * kTracePts + 16 : nullptr);
+    if (a.trace && tid == 64) a.trace[(size_t)tb * kTracePts + 15] = __builtin_amdgcn_s_memrealtime();
     if (act && sub == 0 && rep == 0) {
       s_raw[j] = (int64_t)rbase;
       s_total[j] = total_v;
@@ -1339,7 +1344,10 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         // written and read by wave 0 alone: LDS operations of one wave complete in order)
         // while the other waves score it
         const int fg = fix / kNodesPerWave;
-        const int nrep = (sc.search && sc.k > 1) ? BW - 1 : 1;
+        // one replica per 8 subsets of the pod's size, at most BW−1: a replica without subsets
+        // would still redo the node's tables and default scores beside the searching waves
+        const int nsub = sc.s_end - sc.s_begin;
+        const int nrep = (sc.search && sc.k > 1) ? min(BW - 1, max(1, (nsub + kGroup - 1) / kGroup)) : 1;
         if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 9] = __builtin_amdgcn_s_memrealtime();
         if (wave == 0) {
           filter_one(r, par, fg);
@@ -1347,7 +1355,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           record1(tag1);
           if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 10] = __builtin_amdgcn_s_memrealtime();
         } else {
-          score_a_fix(r, sc, fg, nrep);
+          score_a_fix(r, sc, fg, nrep, b);
         }
         __syncthreads();
         if (nrep > 1) merge_gang(r, sc, s_feas, fg * kNodesPerWave, kNodesPerWave, nrep);

@@ -78,6 +78,13 @@ def run(nodes: int, mode: str, pods: int, batch: int, trace: bool = False, busy:
                     by_k.setdefault(kk, []).append(x["score_a"])
                 extra["score_a_us_by_gpus"] = {str(kk): [len(v), round(sum(v) / len(v), 2)]
                                                for kk, v in sorted(by_k.items())}
+                by_k = {}
+                for x, kk in zip(tr, ks[8:8 + len(tr)]):
+                    if "own_sa_score" in x:   # PAIRS: the fix-up owner's score A of the pod
+                        by_k.setdefault(kk, []).append(x["own_sa_score"])
+                if by_k:
+                    extra["own_sa_score_us_by_gpus"] = {str(kk): [len(v), round(sum(v) / len(v), 2)]
+                                                        for kk, v in sorted(by_k.items())}
             ds.batch_trace(eng, False)
     return {**extra, "nodes": nodes, "mode": mode, "mix": mix, "pods": n, "batch": batch if mode.startswith("batch") or mode == "cpu" else 1,
             "us_per_pod": round(dt / n * 1e6, 1), "pods_per_s": round(n / dt, 1),

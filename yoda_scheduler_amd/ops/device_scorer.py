@@ -41,7 +41,11 @@ TRACE_PHASES = ("filter", "score_a", "gather1", "score_b", "gather2", "select", 
 # PAIRS, the block that owns the other set's last winner (stamps 13, 9..12): record 3 gathered →
 # winner known and assumed, → record 1 sent (re-filtered group), → the group scored, → gather 1 done
 OWNER_PHASES = (("own_winner", 13, 9), ("own_filter_rec1", 9, 10), ("own_score_a", 9, 11),
-                ("own_gather1", 11, 12), ("own_to_gather1", 13, 12))
+                ("own_gather1", 11, 12), ("own_to_gather1", 13, 12),
+                # wave 1 (scoring replica 0): the group's filter verdict, then score A
+                ("own_sa_filter", 9, 14), ("own_sa_score", 14, 15), ("own_sa_to_merge", 15, 11),
+                # inside wave 1's score A: node tables loaded, GPU set chosen, default scores
+                ("own_sa_tables", 14, 16), ("own_sa_gang", 16, 17), ("own_sa_defaults", 17, 15))
 
 
 def batch_trace(engine, on: bool = True) -> None:
@@ -64,7 +68,7 @@ def read_batch_trace(engine, max_pods: int = 256) -> list[dict]:
     """Per pod of the last k_batch chunk: µs spent in each phase (block 0's view)."""
     lib = hip_lib()
     declare(lib)
-    W = 16
+    W = 24
     buf = (ctypes.c_ulonglong * (max_pods * W))()
     m = lib.yoda_dev_batch_trace(engine.device_ctx, 1, buf, max_pods)
     out = []
