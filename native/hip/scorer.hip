@@ -1016,6 +1016,37 @@ __device__ __forceinline__ bool gather(const BatchArgs& a, uint32_t tag, int G, 
   return *s_fail == 0;
 }
 
+// gather() for wave 0 alone, no barrier (G ≤ 128: lane t polls producers t and t + 64): the
+// PAIRS fix-up owner's wave 0 gathers record 1 while the block's other waves still score the
+// winner's group. Returns false when the wait was abandoned (the caller raises s_fail).
+template <int K>
+__device__ __forceinline__ bool gather_wave0(const BatchArgs& a, uint32_t tag, int G, int p_off, uint32_t (&v)[K],
+                                             uint32_t (&v2)[K]) {
+  const int t = threadIdx.x, t2 = t + 64;
+  const gu64* p = slot_ptr(a, tag, p_off + (t < G ? t : 0));
+  const gu64* p2 = slot_ptr(a, tag, p_off + (t2 < G ? t2 : 0));
+  const unsigned long long none = (unsigned long long)tag << 32;
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (unsigned spins = 0;;) {
+    const unsigned long long x0 = t < G ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
+    const unsigned long long y0 = t2 < G ? __hip_atomic_load(p2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
+    bool ok = (uint32_t)(x0 >> 32) == tag && (uint32_t)(y0 >> 32) == tag;
+    if (__all(ok)) {
+      v[0] = (uint32_t)x0;
+      v2[0] = (uint32_t)y0;
+#pragma unroll
+      for (int k = 1; k < K; ++k) {
+        const unsigned long long x = t < G ? __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
+        const unsigned long long y = t2 < G ? __hip_atomic_load(p2 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
+        v[k] = (uint32_t)x;
+        v2[k] = (uint32_t)y;
+        ok &= (uint32_t)(x >> 32) == tag && (uint32_t)(y >> 32) == tag;
+      }
+      if (__all(ok)) return true;
+    }
+    if (!spin_ok(a, spins, t0)) return false;
+  }
+}
 
 #define TRACE(pt)                                                                      \
   do {                                                                                 \
@@ -1296,6 +1327,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     __syncthreads();
     ScoreConsts sc = score_consts(r, nullptr);
     int fix = -1;   // PAIRS: the other set's last winner's row, in its owner block only
+    bool early1 = false;   // PAIRS owner: wave 0 already gathered record 1 (into s_rec)
     if constexpr (PAIRS) {
       // score A of every group now, against the rows as of this set's last pod; then the other
       // set's pod b−1: its winner, from its record 3 (best key; the GPU mask, whether the record's
@@ -1349,11 +1381,34 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         const int nsub = sc.s_end - sc.s_begin;
         const int nrep = (sc.search && sc.k > 1) ? min(BW - 1, max(1, (nsub + kGroup - 1) / kGroup)) : 1;
         if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 9] = __builtin_amdgcn_s_memrealtime();
+        early1 = G <= 128;
         if (wave == 0) {
           filter_one(r, par, fg);
           __builtin_amdgcn_wave_barrier();
           record1(tag1);
           if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 10] = __builtin_amdgcn_s_memrealtime();
+          if (early1) {
+            // gather 1 now, while the other waves score, into the transposed records the block
+            // reduces after the fix-up barrier
+            uint32_t v[kRec1], v2[kRec1];
+            if (gather_wave0<kRec1>(a, tag1, G, p0, v, v2)) {
+              const int t2 = tid + 64;
+              if (tid < G) {
+#pragma unroll
+                for (int k = 0; k < 7; ++k) s_rec[k][tid] = v[k];
+#pragma unroll
+                for (int q = 0; q < 7; ++q) s_rec[7 + q][tid] = (q & 1) ? (v[7 + q / 2] >> 16) : (v[7 + q / 2] & 0xFFFFu);
+              }
+              if (t2 < G) {
+#pragma unroll
+                for (int k = 0; k < 7; ++k) s_rec[k][t2] = v2[k];
+#pragma unroll
+                for (int q = 0; q < 7; ++q) s_rec[7 + q][t2] = (q & 1) ? (v2[7 + q / 2] >> 16) : (v2[7 + q / 2] & 0xFFFFu);
+              }
+            } else if (lane == 0) {
+              s_fail = 1;
+            }
+          }
         } else {
           score_a_fix(r, sc, fg, nrep, b);
         }
@@ -1375,19 +1430,24 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
 
     // ================= gather 1: global maxima, feasible and reason counts
     {
-      uint32_t v[kRec1];
-      if (!gather<kRec1>(a, tag1, G, p0, v, &s_fail)) {
+      if (!early1) {
+        uint32_t v[kRec1];
+        if (!gather<kRec1>(a, tag1, G, p0, v, &s_fail)) {
+          ok = false;
+          break;
+        }
+        // transpose through LDS (14 fields × G), then 16 threads per field reduce it
+        if (tid < G) {
+#pragma unroll
+          for (int k = 0; k < 7; ++k) s_rec[k][tid] = v[k];
+#pragma unroll
+          for (int q = 0; q < 7; ++q) s_rec[7 + q][tid] = (q & 1) ? (v[7 + q / 2] >> 16) : (v[7 + q / 2] & 0xFFFFu);
+        }
+        __syncthreads();
+      } else if (s_fail) {   // (PAIRS owner: wave 0 gathered before the fix-up barrier)
         ok = false;
         break;
       }
-      // transpose through LDS (14 fields × G), then 16 threads per field reduce it
-      if (tid < G) {
-#pragma unroll
-        for (int k = 0; k < 7; ++k) s_rec[k][tid] = v[k];
-#pragma unroll
-        for (int q = 0; q < 7; ++q) s_rec[7 + q][tid] = (q & 1) ? (v[7 + q / 2] >> 16) : (v[7 + q / 2] & 0xFFFFu);
-      }
-      __syncthreads();
       const int f = tid >> 4, seg = tid & 15;
       if (f < 14) {   // waves 0..3 cover fields 0..15; f is uniform per 16 lanes
         const bool is_max = f < 6;
@@ -1406,6 +1466,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         }
         if (seg == 0) s_glob[f] = acc;
       }
+      // (also orders a PAIRS owner's gang merge before phase B)
       __syncthreads();
     }
     if (PAIRS && fix >= 0 && a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 12] = __builtin_amdgcn_s_memrealtime();
