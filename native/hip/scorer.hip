@@ -1020,8 +1020,8 @@ __device__ __forceinline__ bool gather(const BatchArgs& a, uint32_t tag, int G, 
 // PAIRS fix-up owner's wave 0 gathers record 1 while the block's other waves still score the
 // winner's group. Returns false when the wait was abandoned (the caller raises s_fail).
 template <int K>
-__device__ __forceinline__ bool gather_wave0(const BatchArgs& a, uint32_t tag, int G, int p_off, uint32_t (&v)[K],
-                                             uint32_t (&v2)[K]) {
+__device__ __forceinline__ bool gather_wave0_2(const BatchArgs& a, uint32_t tag, int G, int p_off, uint32_t (&v)[K],
+                                               uint32_t (&v2)[K]) {
   const int t = threadIdx.x, t2 = t + 64;
   const gu64* p = slot_ptr(a, tag, p_off + (t < G ? t : 0));
   const gu64* p2 = slot_ptr(a, tag, p_off + (t2 < G ? t2 : 0));
@@ -1041,6 +1041,34 @@ __device__ __forceinline__ bool gather_wave0(const BatchArgs& a, uint32_t tag, i
         v[k] = (uint32_t)x;
         v2[k] = (uint32_t)y;
         ok &= (uint32_t)(x >> 32) == tag && (uint32_t)(y >> 32) == tag;
+      }
+      if (__all(ok)) return true;
+    }
+    if (!spin_ok(a, spins, t0)) return false;
+  }
+}
+// wave 0's gather; G ≤ 64: one producer per lane (v2 zeroed, unused), else two (gather_wave0_2)
+template <int K>
+__device__ __forceinline__ bool gather_wave0(const BatchArgs& a, uint32_t tag, int G, int p_off, uint32_t (&v)[K],
+                                             uint32_t (&v2)[K]) {
+  if (G > 64) return gather_wave0_2<K>(a, tag, G, p_off, v, v2);
+#pragma unroll
+  for (int k = 0; k < K; ++k) v2[k] = 0;
+  const int t = threadIdx.x;
+  const gu64* p = slot_ptr(a, tag, p_off + (t < G ? t : 0));
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (unsigned spins = 0;;) {
+    const unsigned long long x0 = t < G ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                        : ((unsigned long long)tag << 32);
+    bool ok = (uint32_t)(x0 >> 32) == tag;
+    if (__all(ok)) {
+      v[0] = (uint32_t)x0;
+#pragma unroll
+      for (int k = 1; k < K; ++k) {
+        const unsigned long long x = t < G ? __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                           : ((unsigned long long)tag << 32);
+        v[k] = (uint32_t)x;
+        ok &= (uint32_t)(x >> 32) == tag;
       }
       if (__all(ok)) return true;
     }
@@ -1334,31 +1362,14 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       // block had a feasible node, whether the pod fit anywhere)
       score_a_groups(r, sc, s_feas, s_elig, 0, ngroups);
       if (b >= 1) {
-        if (tid == 0) s_fix = -1;   // ordered before the holder's write by the gather's barrier
+        if (tid == 0) s_fix = -1;   // before the holder's write: same wave, or the gather's barrier
         // (slots are double-buffered by tag parity: the other set overwrites this record only
         // with its pod b+1's record 1, which it publishes after this set's pod b record 3 —
         // i.e. after this read)
-        uint32_t v[3];
-        if (!gather<3>(a, tag3 - 3u, G, q0, v, &s_fail)) {
-          ok = false;
-          break;
-        }
-        const unsigned long long t_g3 = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
-        const bool have = tid < G;
-        const unsigned long long mk = have ? ((unsigned long long)v[1] << 32 | v[0]) : 0ull;
-        unsigned long long key = 0;
-        if (G <= 64) {
-          if (wave == 0) key = wave_max(mk);   // the holder is in wave 0 too
-        } else {
-          const unsigned long long wk = wave_max(mk);
-          if (lane == 0) s_part[wave][0] = wk;
-          __syncthreads();
-          for (int w = 0; w < BW; ++w) key = s_part[w][0] > key ? s_part[w][0] : key;
-        }
         // the one record that holds the winner: its key, from a block with a feasible node
         // (keys of feasible nodes are unique; a block without one reports key 0), and the pod
         // fit somewhere. Its thread applies the assume if this block holds the node.
-        if (have && mk == key && ((v[2] >> 9) & 1u) && ((v[2] >> 8) & 1u)) {
+        auto take_winner = [&](unsigned long long key, const uint32_t (&v)[3], unsigned long long t_g3) {
           const yoda_dev_req_t& rp = *reinterpret_cast<const yoda_dev_req_t*>(s_req[(b - 1) & 3]);
           const uint32_t pp = (uint32_t)(key & 0xFFFFFFull);
           const int w = (int)(((pp - rp.perm_add) * rp.perm_inv) & 0xFFFFFFu);
@@ -1367,8 +1378,48 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
             s_fix = w - base;
             if (a.trace) a.trace[(size_t)b * kTracePts + 13] = t_g3;
           }
+        };
+        auto holds = [&](bool have, unsigned long long mk, unsigned long long key, const uint32_t (&v)[3]) {
+          return have && mk == key && ((v[2] >> 9) & 1u) && ((v[2] >> 8) & 1u);
+        };
+        if (G <= 128) {
+          // wave 0 alone (lane t: producers t and t + 64) gathers, reduces and assumes
+          if (wave == 0) {
+            uint32_t v[3], v2[3];
+            if (gather_wave0<3>(a, tag3 - 3u, G, q0, v, v2)) {
+              const unsigned long long t_g3 = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+              const bool have = tid < G, have2 = tid + 64 < G;
+              const unsigned long long mk = have ? ((unsigned long long)v[1] << 32 | v[0]) : 0ull;
+              const unsigned long long mk2 = have2 ? ((unsigned long long)v2[1] << 32 | v2[0]) : 0ull;
+              const unsigned long long key = wave_max(mk > mk2 ? mk : mk2);
+              if (holds(have, mk, key, v)) take_winner(key, v, t_g3);
+              else if (holds(have2, mk2, key, v2)) take_winner(key, v2, t_g3);
+            } else if (lane == 0) {
+              s_fail = 1;
+            }
+          }
+          __syncthreads();
+          if (s_fail) {
+            ok = false;
+            break;
+          }
+        } else {
+          uint32_t v[3];
+          if (!gather<3>(a, tag3 - 3u, G, q0, v, &s_fail)) {
+            ok = false;
+            break;
+          }
+          const unsigned long long t_g3 = a.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+          const bool have = tid < G;
+          const unsigned long long mk = have ? ((unsigned long long)v[1] << 32 | v[0]) : 0ull;
+          const unsigned long long wk = wave_max(mk);
+          if (lane == 0) s_part[wave][0] = wk;
+          __syncthreads();
+          unsigned long long key = 0;
+          for (int w = 0; w < BW; ++w) key = s_part[w][0] > key ? s_part[w][0] : key;
+          if (holds(have, mk, key, v)) take_winner(key, v, t_g3);
+          __syncthreads();
         }
-        __syncthreads();
         fix = s_fix;
       }
       if (fix >= 0) {
@@ -1513,27 +1564,42 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         store_granule(slot_ptr(a, tag2, g) + tid, tag2, (tid & 1) ? (uint32_t)(x >> 32) : (uint32_t)x);
       }
       TRACE(4);
-      uint32_t v[kRec2];
-      if (!gather<kRec2>(a, tag2, G, p0, v, &s_fail)) {
-        ok = false;
-        break;
-      }
-      const bool have = tid < G;
-      const unsigned long long mlo = have ? ((unsigned long long)v[1] << 32 | v[0]) : ULLONG_MAX;
-      const unsigned long long mhi = have ? ((unsigned long long)v[3] << 32 | v[2]) : 0ull;
-      if (G <= 64) {
+      if (G <= 128) {
+        // wave 0 alone gathers and reduces; one barrier hands lo/hi to the block
         if (wave == 0) {
-          const unsigned long long wlo = wave_min(mlo), whi = wave_max(mhi);
-          if (lane == 0) {
-            s_red[0] = wlo;
-            s_red[1] = whi;
+          uint32_t v[kRec2], v2[kRec2];
+          if (gather_wave0<kRec2>(a, tag2, G, p0, v, v2)) {
+            const bool have = tid < G, have2 = tid + 64 < G;
+            const unsigned long long l1 = have ? ((unsigned long long)v[1] << 32 | v[0]) : ULLONG_MAX;
+            const unsigned long long l2 = have2 ? ((unsigned long long)v2[1] << 32 | v2[0]) : ULLONG_MAX;
+            const unsigned long long h1 = have ? ((unsigned long long)v[3] << 32 | v[2]) : 0ull;
+            const unsigned long long h2 = have2 ? ((unsigned long long)v2[3] << 32 | v2[2]) : 0ull;
+            const unsigned long long wlo = wave_min(l1 < l2 ? l1 : l2), whi = wave_max(h1 > h2 ? h1 : h2);
+            if (lane == 0) {
+              s_red[0] = wlo;
+              s_red[1] = whi;
+            }
+          } else if (lane == 0) {
+            s_fail = 1;
           }
         }
         __syncthreads();
+        if (s_fail) {
+          ok = false;
+          break;
+        }
         glo = s_red[0];
         ghi = s_red[1];
       } else {
+        uint32_t v[kRec2];
+        if (!gather<kRec2>(a, tag2, G, p0, v, &s_fail)) {
+          ok = false;
+          break;
+        }
         // (the gather's barrier ordered every read of the record-2 partials before these writes)
+        const bool have = tid < G;
+        const unsigned long long mlo = have ? ((unsigned long long)v[1] << 32 | v[0]) : ULLONG_MAX;
+        const unsigned long long mhi = have ? ((unsigned long long)v[3] << 32 | v[2]) : 0ull;
         const unsigned long long wlo = wave_min(mlo), whi = wave_max(mhi);
         if (lane == 0) {
           s_part[wave][0] = wlo;
@@ -1586,20 +1652,31 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         store_granule(slot_ptr(a, tag3, g) + tid, tag3, x);
       }
       TRACE(6);
-      uint32_t v[kRec3];
-      if (!gather<kRec3>(a, tag3, G, p0, v, &s_fail)) {
-        ok = false;
-        break;
-      }
-      const unsigned long long mk = tid < G ? ((unsigned long long)v[1] << 32 | v[0]) : 0ull;
-      if (G <= 64) {
+      if (G <= 128) {
         if (wave == 0) {
-          const unsigned long long wk = wave_max(mk);
-          if (lane == 0) s_red[0] = wk;
+          uint32_t v[kRec3], v2[kRec3];
+          if (gather_wave0<kRec3>(a, tag3, G, p0, v, v2)) {
+            const unsigned long long k1 = tid < G ? ((unsigned long long)v[1] << 32 | v[0]) : 0ull;
+            const unsigned long long k2 = tid + 64 < G ? ((unsigned long long)v2[1] << 32 | v2[0]) : 0ull;
+            const unsigned long long wk = wave_max(k1 > k2 ? k1 : k2);
+            if (lane == 0) s_red[0] = wk;
+          } else if (lane == 0) {
+            s_fail = 1;
+          }
         }
         __syncthreads();
+        if (s_fail) {
+          ok = false;
+          break;
+        }
         key = s_red[0];
       } else {
+        uint32_t v[kRec3];
+        if (!gather<kRec3>(a, tag3, G, p0, v, &s_fail)) {
+          ok = false;
+          break;
+        }
+        const unsigned long long mk = tid < G ? ((unsigned long long)v[1] << 32 | v[0]) : 0ull;
         const unsigned long long wk = wave_max(mk);
         if (lane == 0) s_part[wave][0] = wk;
         __syncthreads();
