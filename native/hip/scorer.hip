@@ -1443,6 +1443,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
             // reduces after the fix-up barrier
             uint32_t v[kRec1], v2[kRec1];
             if (gather_wave0<kRec1>(a, tag1, G, p0, v, v2)) {
+              if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 18] = __builtin_amdgcn_s_memrealtime();
               const int t2 = tid + 64;
               if (tid < G) {
 #pragma unroll

@@ -45,7 +45,9 @@ OWNER_PHASES = (("own_winner", 13, 9), ("own_filter_rec1", 9, 10), ("own_score_a
                 # wave 1 (scoring replica 0): the group's filter verdict, then score A
                 ("own_sa_filter", 9, 14), ("own_sa_score", 14, 15), ("own_sa_to_merge", 15, 11),
                 # inside wave 1's score A: node tables loaded, GPU set chosen, default scores
-                ("own_sa_tables", 14, 16), ("own_sa_gang", 16, 17), ("own_sa_defaults", 17, 15))
+                ("own_sa_tables", 14, 16), ("own_sa_gang", 16, 17), ("own_sa_defaults", 17, 15),
+                # wave 0's early gather 1: record 1 sent → every record 1 of the set in hand
+                ("own_early_g1", 10, 18))
 
 
 def batch_trace(engine, on: bool = True) -> None:
