@@ -544,7 +544,8 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
                                              const yoda_dev_req_t& r, const ScoreConsts& sc,
                                              const uint8_t* s_masks, int sub, uint64_t& rbase_o, int64_t& total_o,
                                              uint32_t& mask_o, int32_t& quality_o, int rep = 0, int nrep = 1,
-                                             GangBest* gang_o = nullptr, unsigned long long* stamp = nullptr) {
+                                             GangBest* gang_o = nullptr, unsigned long long* stamp = nullptr,
+                                             int part = 0) {
   const int k = sc.k;
   const bool search = sc.search, yoda_s = sc.yoda_s;
   const int32_t P = sc.P;
@@ -553,7 +554,9 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
   // ---- per-node register tables (every lane of the group holds the whole node). A 1-GPU
   // search needs only the lane's own card: it skips the tables and forms the tail's card
   // sums with a group reduction instead (`fast1`, wave-uniform)
-  const bool fast1 = search && k == 1 && rep == 0;
+  // `part` (the PAIRS fix-up splits the two halves over waves): 0 both, 1 the GPU-set choice
+  // only (into gang_o), 2 the scores only (no set: the caller adds the chosen set's gang bonus)
+  const bool fast1 = search && k == 1 && rep == 0 && part != 2;
   uint64_t ef[YODA_DEV_CARDS];
   uint32_t tot[YODA_DEV_CARDS], occ[YODA_DEV_CARDS];
   // the allocate/actual terms' card sums, formed from the same registers (every lane holds
@@ -597,7 +600,9 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
   int64_t best_o = LLONG_MAX;
   int32_t best_lb = 0;
   bool found = false;
-  if (fast1 && act) {
+  if (part == 2) {
+    // scores only: the tables above hold the node's card sums
+  } else if (fast1 && act) {
     // single-GPU pods (the bulk of a mixed burst): the k = 1 table is {1<<0 … 1<<7} in
     // order, so lane `sub` owns subset {sub}; no pairs (P = 0) and one NUMA domain leave
     // only the fit and occupancy terms — the generic loop's 28 predicated pair adds and
@@ -708,6 +713,7 @@ __device__ __forceinline__ void score_node_a(const yoda_dev_node_t* nd, bool act
 #undef GANG_STEP
   if (stamp) stamp[1] = __builtin_amdgcn_s_memrealtime();   // (trace) GPU set chosen
   if (gang_o && act && sub == 0) *gang_o = GangBest{best_o, best_lb, (uint8_t)best_m, (uint8_t)found};
+  if (part == 1) return;
   const int32_t quality = found ? 10000 - sdiv_small_r(best_lb, 100, 0.01) : 10000;
   // ---- yoda score terms that need no maxima (algorithm.go:28-87 with the Q1/Q2/Q3/Q4
   // fixes): allocate + actual over the node's cards (sums above), plus the gang bonus, and
@@ -1277,12 +1283,14 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   };
 
   // PAIRS fix-up, score A of group `gq` on waves 1..BW−1 while wave 0 re-filters it for record 1:
-  // each scoring wave evaluates the group's filter verdict and eligible mask itself (no maxima,
-  // no LDS hand-off from wave 0), a multi-GPU search split over `nrep` = BW−1 waves (the
-  // caller merges after the barrier that joins wave 0).
+  // each scoring wave evaluates the group's filter verdict and eligible mask itself (no LDS
+  // hand-off from wave 0). The two independent halves of score A run on different waves: waves
+  // 1..nrep choose the GPU set (a multi-GPU subset search split over them, replica wave−1, into
+  // s_gang), wave nrep+1 computes the scores without the set's gang bonus (into s_raw /
+  // s_total); `combine_fix` joins them after the barrier that also joins wave 0.
   auto score_a_fix = [&](const yoda_dev_req_t& r, const ScoreConsts& sc, int gq, int nrep, int tb) {
-    const int rep = wave - 1;
-    if (rep < 0 || rep >= nrep) return;   // wave-uniform
+    const bool gang = wave >= 1 && wave <= nrep, scores = wave == nrep + 1;
+    if (!gang && !scores) return;   // wave-uniform
     const int j = gq * kNodesPerWave + grp;
     const bool valid = j < cnt;
     const yoda_dev_node_t* nd = s_rows + (valid ? j : 0);
@@ -1294,17 +1302,41 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     int64_t total_v = 0;
     uint32_t mask_v = 0;
     int32_t quality_v = 0;
-    score_node_a(nd, act, act ? emask : 0u, r, sc, s_masks, sub, rbase, total_v, mask_v, quality_v, rep, nrep,
-                 nrep > 1 ? &s_gang[rep * kNodesPerWave + grp] : nullptr,
-                 (a.trace && tid == 64) ? a.trace + (size_t)tb * kTracePts + 16 : nullptr);
-    if (a.trace && tid == 64) a.trace[(size_t)tb * kTracePts + 15] = __builtin_amdgcn_s_memrealtime();
-    if (act && sub == 0 && rep == 0) {
-      s_raw[j] = (int64_t)rbase;
-      s_total[j] = total_v;
-      s_mask[j] = (uint8_t)mask_v;
-      s_quality[j] = quality_v;
+    if (gang) {
+      score_node_a(nd, act, act ? emask : 0u, r, sc, s_masks, sub, rbase, total_v, mask_v, quality_v, wave - 1, nrep,
+                   &s_gang[(wave - 1) * kNodesPerWave + grp],
+                   (a.trace && tid == 64) ? a.trace + (size_t)tb * kTracePts + 16 : nullptr, 1);
+      if (a.trace && tid == 64) a.trace[(size_t)tb * kTracePts + 15] = __builtin_amdgcn_s_memrealtime();
+    } else {
+      score_node_a(nd, act, act ? emask : 0u, r, sc, s_masks, sub, rbase, total_v, mask_v, quality_v, 0, 1, nullptr,
+                   nullptr, 2);
+      if (act && sub == 0) {
+        s_raw[j] = (int64_t)rbase;
+        s_total[j] = total_v;
+      }
     }
   };
+  // after the barrier: the best of the nrep GPU-set replicas of each feasible node of the group,
+  // its mask, gang quality and (multi-GPU yoda pods) the gang bonus the scores wave left out —
+  // the same terms score_node_a adds when it does both halves
+  auto combine_fix = [&](const yoda_dev_req_t& r, const ScoreConsts& sc, const uint8_t* s_feas, int j_lo, int nrep) {
+    if (tid < kNodesPerWave) {
+      const int j = j_lo + tid;
+      if (j < cnt && s_feas[j]) {
+        GangBest bb = s_gang[tid];
+        for (int q = 1; q < nrep; ++q) {
+          const GangBest o = s_gang[q * kNodesPerWave + tid];
+          if (o.found && (!bb.found || better(o.o, o.m, bb.o, bb.m))) bb = o;
+        }
+        const int32_t quality = bb.found ? 10000 - sdiv_small_r(bb.lb, 100, 0.01) : 10000;
+        s_mask[j] = bb.found ? bb.m : 0u;
+        s_quality[j] = quality;
+        if (sc.yoda_s && r.has_number && r.number > 1 && r.number <= s_rows[j].ncards && bb.found)
+          s_raw[j] = (int64_t)((uint64_t)s_raw[j] + (uint64_t)(quality / 100) * (uint64_t)r.w_gang_score);
+      }
+    }
+  };
+
 
   // assume (engine.cpp Engine::reserve, non-compat, reservation pending) of pod `rq` on row j
   // with GPU set `mask`: one thread
@@ -1430,7 +1462,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         // one replica per 8 subsets of the pod's size, at most BW−1: a replica without subsets
         // would still redo the node's tables and default scores beside the searching waves
         const int nsub = sc.s_end - sc.s_begin;
-        const int nrep = (sc.search && sc.k > 1) ? min(BW - 1, max(1, (nsub + kGroup - 1) / kGroup)) : 1;
+        const int nrep = (sc.search && sc.k > 1) ? min(BW - 2, max(1, (nsub + kGroup - 1) / kGroup)) : 1;
         if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 9] = __builtin_amdgcn_s_memrealtime();
         early1 = G <= 128;
         if (wave == 0) {
@@ -1465,7 +1497,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           score_a_fix(r, sc, fg, nrep, b);
         }
         __syncthreads();
-        if (nrep > 1) merge_gang(r, sc, s_feas, fg * kNodesPerWave, kNodesPerWave, nrep);
+        combine_fix(r, sc, s_feas, fg * kNodesPerWave, nrep);
         if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 11] = __builtin_amdgcn_s_memrealtime();
       } else {
         record1(tag1);
