@@ -1095,10 +1095,13 @@ __device__ __forceinline__ bool gather_wave0(const BatchArgs& a, uint32_t tag, i
 // score B and select, the other set has already filtered and scored pod b+1 against its rows
 // (every assume up to pod b−1 applied). When pod b's winner is known (its record 3 carries the
 // winner's GPU mask), the other set applies that assume to its replica and only the owner of the
-// winner's node redoes the filter of that one 8-node group (before record 1) and its score A
-// (while record 1 travels): an assume changes one row, so every other node's filter and score A
-// for pod b+1 stand. The per-pod critical path loses the filter and score A of every block but
-// one group's; results are bit-identical to the serial order.
+// winner's node redoes that one 8-node group: its wave 0 re-filters it, sends record 1 and
+// gathers the set's records 1, while waves 1.. choose the group's GPU sets and compute its
+// scores (two halves on different waves, joined after the barrier): an assume changes one row,
+// so every other node's filter and score A for pod b+1 stand. The per-pod critical path loses
+// the filter and score A of every block but one group's; results are bit-identical to the
+// serial order (reference: the per-pod cycle of scheduler.go:132-157 / algorithm.go:28-87,
+// run for consecutive pods against the same node table).
 template <int BW, bool PAIRS>
 __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   constexpr int kBB = 64 * BW;
