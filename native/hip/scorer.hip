@@ -1022,28 +1022,30 @@ __device__ __forceinline__ bool gather(const BatchArgs& a, uint32_t tag, int G, 
   return *s_fail == 0;
 }
 
-// gather() for wave 0 alone, no barrier (G ≤ 128: lane t polls producers t and t + 64): the
-// PAIRS fix-up owner's wave 0 gathers record 1 while the block's other waves still score the
-// winner's group. Returns false when the wait was abandoned (the caller raises s_fail).
+// gather() for one wave alone, no barrier (G ≤ 128: lane t polls producers t and t + 64;
+// producer `skip` is not polled — its values are left 0): wave 0 for records 2 / 3, and the
+// PAIRS fix-up owner's gathering wave for record 1 while the block's other waves still score
+// the winner's group. Returns false when the wait was abandoned (the caller raises s_fail).
 template <int K>
 __device__ __forceinline__ bool gather_wave0_2(const BatchArgs& a, uint32_t tag, int G, int p_off, uint32_t (&v)[K],
-                                               uint32_t (&v2)[K]) {
-  const int t = threadIdx.x, t2 = t + 64;
+                                               uint32_t (&v2)[K], int skip) {
+  const int t = threadIdx.x & 63, t2 = t + 64;
+  const bool in = t < G && t != skip, in2 = t2 < G && t2 != skip;
   const gu64* p = slot_ptr(a, tag, p_off + (t < G ? t : 0));
   const gu64* p2 = slot_ptr(a, tag, p_off + (t2 < G ? t2 : 0));
   const unsigned long long none = (unsigned long long)tag << 32;
   const long long t0 = __builtin_amdgcn_s_memrealtime();
   for (unsigned spins = 0;;) {
-    const unsigned long long x0 = t < G ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
-    const unsigned long long y0 = t2 < G ? __hip_atomic_load(p2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
+    const unsigned long long x0 = in ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
+    const unsigned long long y0 = in2 ? __hip_atomic_load(p2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
     bool ok = (uint32_t)(x0 >> 32) == tag && (uint32_t)(y0 >> 32) == tag;
     if (__all(ok)) {
       v[0] = (uint32_t)x0;
       v2[0] = (uint32_t)y0;
 #pragma unroll
       for (int k = 1; k < K; ++k) {
-        const unsigned long long x = t < G ? __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
-        const unsigned long long y = t2 < G ? __hip_atomic_load(p2 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
+        const unsigned long long x = in ? __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
+        const unsigned long long y = in2 ? __hip_atomic_load(p2 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
         v[k] = (uint32_t)x;
         v2[k] = (uint32_t)y;
         ok &= (uint32_t)(x >> 32) == tag && (uint32_t)(y >> 32) == tag;
@@ -1053,25 +1055,26 @@ __device__ __forceinline__ bool gather_wave0_2(const BatchArgs& a, uint32_t tag,
     if (!spin_ok(a, spins, t0)) return false;
   }
 }
-// wave 0's gather; G ≤ 64: one producer per lane (v2 zeroed, unused), else two (gather_wave0_2)
+// one wave's gather; G ≤ 64: one producer per lane (v2 zeroed, unused), else two (gather_wave0_2)
 template <int K>
 __device__ __forceinline__ bool gather_wave0(const BatchArgs& a, uint32_t tag, int G, int p_off, uint32_t (&v)[K],
-                                             uint32_t (&v2)[K]) {
-  if (G > 64) return gather_wave0_2<K>(a, tag, G, p_off, v, v2);
+                                             uint32_t (&v2)[K], int skip = -1) {
+  if (G > 64) return gather_wave0_2<K>(a, tag, G, p_off, v, v2, skip);
 #pragma unroll
   for (int k = 0; k < K; ++k) v2[k] = 0;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x & 63;
+  const bool in = t < G && t != skip;
   const gu64* p = slot_ptr(a, tag, p_off + (t < G ? t : 0));
   const long long t0 = __builtin_amdgcn_s_memrealtime();
   for (unsigned spins = 0;;) {
-    const unsigned long long x0 = t < G ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+    const unsigned long long x0 = in ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                         : ((unsigned long long)tag << 32);
     bool ok = (uint32_t)(x0 >> 32) == tag;
     if (__all(ok)) {
       v[0] = (uint32_t)x0;
 #pragma unroll
       for (int k = 1; k < K; ++k) {
-        const unsigned long long x = t < G ? __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+        const unsigned long long x = in ? __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                            : ((unsigned long long)tag << 32);
         v[k] = (uint32_t)x;
         ok &= (uint32_t)(x >> 32) == tag;
@@ -1201,10 +1204,10 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   };
   // record 1 from the group aggregates: threads 0..kRec1-1 (wave 0), after every group's
   // s_grp row is visible to them
-  auto record1 = [&](uint32_t tag1) {
+  auto record1 = [&](uint32_t tag1) -> uint32_t {
+    uint32_t v = 0;
     if (tid < kRec1) {   // block totals over the groups → the record's 11 granules
       const int ngr = (cnt + kNodesPerWave - 1) / kNodesPerWave;
-      uint32_t v;
       if (tid < 7) {
         v = tid < 6 ? 1u : 0u;
         for (int q = 0; q < ngr; ++q) v = tid < 6 ? (s_grp[q][tid] > v ? s_grp[q][tid] : v) : v + s_grp[q][tid];
@@ -1220,6 +1223,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       }
       store_granule(slot_ptr(a, tag1, g) + tid, tag1, v);
     }
+    return v;   // (thread tid's granule; 0 beyond the record)
   };
 
   // Replica 0 of each node in [j_lo, j_lo + span) scored with its own subset best: where
@@ -1468,34 +1472,48 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         const int nrep = (sc.search && sc.k > 1) ? min(BW - 2, max(1, (nsub + kGroup - 1) / kGroup)) : 1;
         if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 9] = __builtin_amdgcn_s_memrealtime();
         early1 = G <= 128;
+        // the wave that gathers every other block's record 1 meanwhile: a spare one (beyond the
+        // GPU-set replicas and the scores wave) from the start, else wave 0 after record 1.
+        // Its own record goes into the transposed records from wave 0's registers.
+        const int gw = nrep + 1 < BW - 1 ? BW - 1 : 0;
+        auto gather_early = [&]() {
+          uint32_t v[kRec1], v2[kRec1];
+          if (gather_wave0<kRec1>(a, tag1, G, p0, v, v2, gi)) {
+            if (a.trace && lane == 0) a.trace[(size_t)b * kTracePts + 18] = __builtin_amdgcn_s_memrealtime();
+            const int t2 = lane + 64;
+            if (lane < G && lane != gi) {
+#pragma unroll
+              for (int k = 0; k < 7; ++k) s_rec[k][lane] = v[k];
+#pragma unroll
+              for (int q = 0; q < 7; ++q) s_rec[7 + q][lane] = (q & 1) ? (v[7 + q / 2] >> 16) : (v[7 + q / 2] & 0xFFFFu);
+            }
+            if (t2 < G && t2 != gi) {
+#pragma unroll
+              for (int k = 0; k < 7; ++k) s_rec[k][t2] = v2[k];
+#pragma unroll
+              for (int q = 0; q < 7; ++q) s_rec[7 + q][t2] = (q & 1) ? (v2[7 + q / 2] >> 16) : (v2[7 + q / 2] & 0xFFFFu);
+            }
+          } else if (lane == 0) {
+            s_fail = 1;
+          }
+        };
         if (wave == 0) {
           filter_one(r, par, fg);
           __builtin_amdgcn_wave_barrier();
-          record1(tag1);
-          if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 10] = __builtin_amdgcn_s_memrealtime();
-          if (early1) {
-            // gather 1 now, while the other waves score, into the transposed records the block
-            // reduces after the fix-up barrier
-            uint32_t v[kRec1], v2[kRec1];
-            if (gather_wave0<kRec1>(a, tag1, G, p0, v, v2)) {
-              if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 18] = __builtin_amdgcn_s_memrealtime();
-              const int t2 = tid + 64;
-              if (tid < G) {
-#pragma unroll
-                for (int k = 0; k < 7; ++k) s_rec[k][tid] = v[k];
-#pragma unroll
-                for (int q = 0; q < 7; ++q) s_rec[7 + q][tid] = (q & 1) ? (v[7 + q / 2] >> 16) : (v[7 + q / 2] & 0xFFFFu);
-              }
-              if (t2 < G) {
-#pragma unroll
-                for (int k = 0; k < 7; ++k) s_rec[k][t2] = v2[k];
-#pragma unroll
-                for (int q = 0; q < 7; ++q) s_rec[7 + q][t2] = (q & 1) ? (v2[7 + q / 2] >> 16) : (v2[7 + q / 2] & 0xFFFFu);
-              }
-            } else if (lane == 0) {
-              s_fail = 1;
+          const uint32_t own = record1(tag1);
+          if (early1 && tid < kRec1) {   // this block's column of the transposed records
+            if (tid < 7) {
+              s_rec[tid][gi] = own;
+            } else {
+              const int q0 = 2 * (tid - 7);
+              s_rec[7 + q0][gi] = own & 0xFFFFu;
+              if (q0 + 1 < 7) s_rec[8 + q0][gi] = own >> 16;
             }
           }
+          if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 10] = __builtin_amdgcn_s_memrealtime();
+          if (early1 && gw == 0) gather_early();
+        } else if (early1 && wave == gw) {
+          gather_early();
         } else {
           score_a_fix(r, sc, fg, nrep, b);
         }
