@@ -1,4 +1,5 @@
 // pybind11 bindings of the native scheduling engine (module yoda_scheduler_amd._native._yoda_core).
+#include <algorithm>
 #include <array>
 #include <atomic>
 #include <condition_variable>
@@ -95,6 +96,48 @@ SelTerm make_term(Engine& e, const py::list& reqs) {
     t.reqs.push_back(std::move(r));
   }
   return t;
+}
+
+// LabelSelector.native() tuple (namespaces | None, nothing, [(key, value)], [(key, op, [values])]) or
+// None (a nil selector) → LSel over interned strings; namespaces are not part of an LSel
+LSel lsel_of(Engine& e, const py::handle& h) {
+  LSel s;
+  if (h.is_none()) {
+    s.nothing = true;
+    return s;
+  }
+  auto t = h.cast<py::tuple>();
+  s.nothing = t[1].cast<bool>();
+  for (auto kv : t[2]) {
+    auto p = kv.cast<py::tuple>();
+    s.reqs.push_back(LReq{e.intern(p[0].cast<std::string>()), kIn, {e.intern(p[1].cast<std::string>())}});
+  }
+  for (auto ex : t[3]) {
+    auto p = ex.cast<py::tuple>();
+    LReq r;
+    r.key = e.intern(p[0].cast<std::string>());
+    r.op = selop_of(p[1].cast<std::string>());
+    if (r.op == kGt || r.op == kLt) throw std::invalid_argument("label selectors take In/NotIn/Exists/DoesNotExist");
+    for (auto v : p[2]) r.values.push_back(e.intern(v.cast<std::string>()));
+    s.reqs.push_back(std::move(r));
+  }
+  return s;
+}
+
+Labels labels_of(Engine& e, const std::vector<std::pair<std::string, std::string>>& kv) {
+  Labels l;
+  l.reserve(kv.size());
+  for (const auto& x : kv) l.emplace_back(e.intern(x.first), e.intern(x.second));
+  std::sort(l.begin(), l.end());
+  return l;
+}
+
+int8_t owner_kind_of(const std::string& api, const std::string& kind) {
+  // plugins/optional.py::_OWNER_KINDS
+  if (api == "v1" && kind == "ReplicationController") return 1;
+  if (api == "apps/v1" && kind == "ReplicaSet") return 2;
+  if (api == "apps/v1" && kind == "StatefulSet") return 3;
+  return 0;
 }
 
 // (node, feasible, evaluated, cards, score, reason_counts, gang_quality, node_gen, stale)
@@ -267,9 +310,15 @@ PYBIND11_MODULE(_yoda_core, m) {
   m.attr("S_TAINT_TOLERATION") = (int)S_TAINT_TOLERATION;
   m.attr("S_NODE_AFFINITY") = (int)S_NODE_AFFINITY;
   m.attr("S_MOST_ALLOCATED") = (int)S_MOST_ALLOCATED;
+  m.attr("S_IMAGE_LOCALITY") = (int)S_IMAGE_LOCALITY;
+  m.attr("S_PREFER_AVOID") = (int)S_PREFER_AVOID;
+  m.attr("S_SPREAD") = (int)S_SPREAD;
+  m.attr("S_NUM") = (int)S_NUM;
+  m.attr("F_SPREAD") = (uint32_t)F_SPREAD;
   m.attr("REASONS") = py::make_tuple("OK", "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity",
                                      "NodeResourcesFit", "NoScv", "ScvStale", "GpuNumber", "GpuMemory",
-                                     "GpuClock", "GpuFit", "NodeGone");
+                                     "GpuClock", "GpuFit", "NodeGone", "NodeResourcesFitExtended",
+                                     "PodTopologySpread", "PodTopologySpreadLabel");
 
   py::class_<PodReq>(m, "PodReq")
       .def_readonly("has_number", &PodReq::has_number)
@@ -279,7 +328,11 @@ PYBIND11_MODULE(_yoda_core, m) {
       .def_readonly("has_clock", &PodReq::has_clock)
       .def_readonly("clock", &PodReq::clock)
       .def_readonly("cpu_m", &PodReq::cpu_m)
-      .def_readonly("mem", &PodReq::mem);
+      .def_readonly("mem", &PodReq::mem)
+      .def_readonly("containers", &PodReq::containers)
+      .def_readonly("spread_explicit", &PodReq::spread_explicit)
+      .def_property_readonly("n_ext", [](const PodReq& r) { return r.ext.size(); })
+      .def_property_readonly("n_spread", [](const PodReq& r) { return r.spread.size(); });
 
   py::class_<Engine>(m, "Engine")
       .def(py::init([](bool compat, int threads) {
@@ -452,6 +505,153 @@ PYBIND11_MODULE(_yoda_core, m) {
            py::arg("node_selector") = std::vector<std::pair<std::string, std::string>>{},
            py::arg("required") = py::list(), py::arg("preferred") = py::list(), py::arg("tolerations") = py::list(),
            py::arg("nz_cpu_m") = -1, py::arg("nz_mem") = -1, py::call_guard<EngineGuard>())
+      // the default-plugin inputs of a PodReq (ImageLocality, NodeResourcesFit beyond cpu/memory,
+      // NodePreferAvoidPods, PodTopologySpread and what other pods' spread counts read of it)
+      .def("set_req_extras",
+           [](Engine& e, PodReq& r, const std::string& ns, const std::vector<std::pair<std::string, std::string>>& labels,
+              bool deleting, const std::vector<std::string>& images, int32_t containers,
+              const std::vector<std::pair<std::string, int64_t>>& ext, const py::object& owner,
+              const py::object& avoid, const py::object& spread) {
+             r.ns = e.intern(ns);
+             r.labels = labels_of(e, labels);
+             r.deleting = deleting;
+             r.images.clear();
+             for (const auto& im : images) r.images.push_back(e.intern(im));
+             r.containers = containers;
+             r.ext.clear();
+             for (const auto& x : ext)
+               if (x.second) r.ext.emplace_back(e.intern(x.first), x.second);
+             std::sort(r.ext.begin(), r.ext.end());
+             r.owner_kind = 0;
+             r.owner_name = -1;
+             if (!owner.is_none()) {
+               auto t = owner.cast<py::tuple>();   // (apiVersion, kind, name, uid)
+               r.owner_kind = owner_kind_of(t[0].cast<std::string>(), t[1].cast<std::string>());
+               if (r.owner_kind) r.owner_name = e.intern(t[2].cast<std::string>());
+             }
+             r.avoid_kind = 0;
+             r.avoid_uid = -1;
+             if (!avoid.is_none()) {
+               auto t = avoid.cast<py::tuple>();   // (kind, uid)
+               const std::string k = t[0].cast<std::string>();
+               r.avoid_kind = k == "ReplicationController" ? 1 : k == "ReplicaSet" ? 2 : 0;
+               if (r.avoid_kind) r.avoid_uid = e.intern(t[1].cast<std::string>());
+             }
+             r.spread.clear();
+             r.spread_explicit = false;
+             if (!spread.is_none()) {
+               for (auto c : spread) {
+                 auto t = c.cast<py::tuple>();     // (topologyKey, maxSkew, whenUnsatisfiable, selector | None)
+                 r.spread_explicit = true;
+                 const std::string when = t[2].cast<std::string>();
+                 if (when != "DoNotSchedule" && when != "ScheduleAnyway") continue;   // in neither list
+                 SpreadC x;
+                 x.key = e.intern(t[0].cast<std::string>());
+                 x.max_skew = t[1].cast<int32_t>();
+                 x.hard = when == "DoNotSchedule";
+                 x.sel = lsel_of(e, t[3]);
+                 r.spread.push_back(std::move(x));
+               }
+             }
+           },
+           py::arg("req"), py::arg("ns"), py::arg("labels"), py::arg("deleting") = false,
+           py::arg("images") = std::vector<std::string>{}, py::arg("containers") = 0,
+           py::arg("ext") = std::vector<std::pair<std::string, int64_t>>{}, py::arg("owner") = py::none(),
+           py::arg("avoid") = py::none(), py::arg("spread") = py::none(), py::call_guard<EngineGuard>())
+      .def("set_node_extras",
+           [](Engine& e, int32_t idx, const std::vector<std::pair<std::string, int64_t>>& images,
+              const std::vector<std::pair<std::string, int64_t>>& ext_alloc,
+              const std::vector<std::pair<std::string, std::string>>& avoid) {
+             std::vector<std::pair<int32_t, int64_t>> im, ea;
+             for (const auto& x : images) im.emplace_back(e.intern(x.first), x.second);
+             for (const auto& x : ext_alloc) ea.emplace_back(e.intern(x.first), x.second);
+             std::vector<std::pair<int8_t, int32_t>> av;
+             for (const auto& x : avoid) {
+               const int8_t k = x.first == "ReplicationController" ? 1 : x.first == "ReplicaSet" ? 2 : 0;
+               if (k) av.emplace_back(k, e.intern(x.second));
+             }
+             e.set_node_extras(idx, std::move(im), std::move(ea), std::move(av));
+           },
+           py::arg("idx"), py::arg("images"), py::arg("ext_alloc"), py::arg("avoid"), py::call_guard<EngineGuard>())
+      .def("image_nodes", [](Engine& e, const std::string& im) { return e.image_nodes(e.intern(im)); },
+           py::call_guard<EngineGuard>())
+      .def_property_readonly("avoid_nodes", &Engine::avoid_nodes)
+      .def("set_service",
+           [](Engine& e, const std::string& ns, const std::string& name, const py::object& selector) {
+             if (selector.is_none()) {
+               e.set_service(e.intern(ns), e.intern(name), true, {});
+               return;
+             }
+             e.set_service(e.intern(ns), e.intern(name), false,
+                           labels_of(e, selector.cast<std::vector<std::pair<std::string, std::string>>>()));
+           },
+           py::arg("ns"), py::arg("name"), py::arg("selector"), py::call_guard<EngineGuard>())
+      .def("remove_service",
+           [](Engine& e, const std::string& ns, const std::string& name) {
+             e.remove_service(e.intern(ns), e.intern(name));
+           }, py::call_guard<EngineGuard>())
+      // kind: "replicationcontrollers" (selector: [(key, value)]) | "replicasets" | "statefulsets"
+      // (selector: LabelSelector.native() tuple, or None when nil)
+      .def("set_controller",
+           [](Engine& e, const std::string& kind, const std::string& ns, const std::string& name,
+              const py::object& selector) {
+             const int8_t k = kind == "replicationcontrollers" ? 1 : kind == "replicasets" ? 2 : kind == "statefulsets" ? 3 : 0;
+             if (!k) throw std::invalid_argument("unknown controller kind " + kind);
+             LSel s;
+             if (k == 1) {
+               if (!selector.is_none())
+                 for (const auto& kv : labels_of(e, selector.cast<std::vector<std::pair<std::string, std::string>>>()))
+                   s.reqs.push_back(LReq{kv.first, kIn, {kv.second}});
+             } else {
+               s = lsel_of(e, selector);
+             }
+             e.set_controller(k, e.intern(ns), e.intern(name), std::move(s));
+           },
+           py::arg("kind"), py::arg("ns"), py::arg("name"), py::arg("selector"), py::call_guard<EngineGuard>())
+      .def("remove_controller",
+           [](Engine& e, const std::string& kind, const std::string& ns, const std::string& name) {
+             const int8_t k = kind == "replicationcontrollers" ? 1 : kind == "replicasets" ? 2 : kind == "statefulsets" ? 3 : 0;
+             if (k) e.remove_controller(k, e.intern(ns), e.intern(name));
+           }, py::call_guard<EngineGuard>())
+      // [(key, op, [values])] of the pod's DefaultSelector, or None when it is empty
+      .def("default_selector",
+           [](Engine& e, const PodReq& r) -> py::object {
+             LSel s;
+             if (!e.default_selector(r, &s)) return py::none();
+             py::list out;
+             static const char* kOps[] = {"In", "NotIn", "Exists", "DoesNotExist"};
+             for (const auto& q : s.reqs) {
+               py::list vals;
+               for (int32_t v : q.values) vals.append(e.str(v));
+               out.append(py::make_tuple(e.str(q.key), kOps[q.op], vals));
+             }
+             return out;
+           }, py::call_guard<EngineGuard>())
+      .def("set_pod_meta",
+           [](Engine& e, uint64_t pod, const std::vector<std::pair<std::string, std::string>>& labels, bool deleting) {
+             return e.set_pod_meta(pod, labels_of(e, labels), deleting);
+           }, py::arg("pod"), py::arg("labels"), py::arg("deleting"), py::call_guard<EngineGuard>())
+      .def("count_matching",
+           [](Engine& e, int32_t idx, const std::string& ns, const py::object& selector) {
+             return e.count_matching(idx, e.intern(ns), lsel_of(e, selector));
+           }, py::call_guard<EngineGuard>())
+      // PodTopologySpread args: [(topologyKey, maxSkew, whenUnsatisfiable)]
+      .def("set_spread_defaults",
+           [](Engine& e, const std::vector<std::tuple<std::string, int32_t, std::string>>& d) {
+             std::vector<DefaultSpread> v;
+             for (const auto& x : d) {
+               const std::string& w = std::get<2>(x);
+               if (w != "DoNotSchedule" && w != "ScheduleAnyway") continue;
+               v.push_back(DefaultSpread{e.intern(std::get<0>(x)), std::get<1>(x), w == "DoNotSchedule"});
+             }
+             e.set_spread_defaults(std::move(v));
+           }, py::call_guard<EngineGuard>())
+      .def("set_ext_ignored",
+           [](Engine& e, const std::vector<std::string>& res, const std::vector<std::string>& groups) {
+             std::vector<int32_t> r;
+             for (const auto& x : res) r.push_back(e.intern(x));
+             e.set_ext_ignored(std::move(r), groups);
+           }, py::call_guard<EngineGuard>())
       .def("reserve", &Engine::reserve, py::call_guard<EngineGuard>())
       .def("release", &Engine::release, py::call_guard<EngineGuard>())
       .def("has_pod", &Engine::has_pod, py::call_guard<EngineGuard>())

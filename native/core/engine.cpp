@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <chrono>
 #include <climits>
+#include <cmath>
 #include <cstring>
 
 #include "yoda_dev_abi.h"
@@ -103,6 +104,9 @@ EngineConfig Engine::config() const {
     for (int j = 0; j < 3; ++j) c.alloc_w[k][j] = alloc_w_[k][j];
   c.wt = wt_;
   c.settle_s = settle_s_;
+  c.spread_defaults = spread_defaults_;
+  c.ext_ignored = ext_ignored_;
+  c.ext_ignored_groups = ext_ignored_groups_;
   return c;
 }
 
@@ -113,6 +117,9 @@ void Engine::set_config(const EngineConfig& c) {
     for (int j = 0; j < 3; ++j) alloc_w_[k][j] = c.alloc_w[k][j];
   wt_ = c.wt;
   settle_s_ = c.settle_s;
+  spread_defaults_ = c.spread_defaults;
+  ext_ignored_ = c.ext_ignored;
+  ext_ignored_groups_ = c.ext_ignored_groups;
 }
 
 int32_t Engine::intern(const std::string& s) {
@@ -160,6 +167,9 @@ void Engine::remove_node(int32_t idx) {
   node_idx_.erase(nodes_[idx].name);
   hard_taint_nodes_ -= nodes_[idx].hard_taint;
   prefer_taint_nodes_ -= nodes_[idx].prefer_taint;
+  index_node_extras(nodes_[idx], -1);
+  for (auto& kv : nodes_[idx].labels)
+    if (--label_key_nodes_[kv.first] <= 0) label_key_nodes_.erase(kv.first);
   nodes_[idx] = Node();
   nodes_[idx].alive = false;
   nodes_[idx].gen = ++gen_counter_;
@@ -173,8 +183,11 @@ void Engine::set_node_meta(int32_t idx, bool unschedulable, const std::vector<st
                            const std::vector<Taint>& taints, int64_t cpu_m, int64_t mem, int64_t pods) {
   Node& n = nodes_.at(idx);
   n.unschedulable = unschedulable;
+  for (auto& kv : n.labels)
+    if (--label_key_nodes_[kv.first] <= 0) label_key_nodes_.erase(kv.first);
   n.labels.clear();
   for (auto& kv : labels) n.labels[kv.first] = kv.second;
+  for (auto& kv : n.labels) ++label_key_nodes_[kv.first];
   n.taints = taints;
   hard_taint_nodes_ -= n.hard_taint;
   prefer_taint_nodes_ -= n.prefer_taint;
@@ -293,6 +306,17 @@ bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::ve
   n.nz_mem += a.nz_mem;
   n.pod_count += 1;
   if (a.has_label_mem) n.label_mem_sum += a.label_mem;
+  a.ns = req.ns;
+  a.labels = req.labels;
+  a.deleting = req.deleting;
+  if (!req.ext.empty()) {
+    a.ext = req.ext;
+    for (const auto& r : a.ext) {
+      auto it = std::lower_bound(n.ext_used.begin(), n.ext_used.end(), std::make_pair(r.first, INT64_MIN));
+      if (it != n.ext_used.end() && it->first == r.first) it->second += r.second;
+      else n.ext_used.insert(it, r);
+    }
+  }
   ledger_.emplace(pod, std::move(a));
   mark_dirty(idx);
   return true;
@@ -326,6 +350,10 @@ bool Engine::release(uint64_t pod) {
     n.nz_mem -= a.nz_mem;
     n.pod_count -= 1;
     if (a.has_label_mem) n.label_mem_sum -= a.label_mem;
+    for (const auto& r : a.ext) {
+      auto it = std::lower_bound(n.ext_used.begin(), n.ext_used.end(), std::make_pair(r.first, INT64_MIN));
+      if (it != n.ext_used.end() && it->first == r.first && (it->second -= r.second) == 0) n.ext_used.erase(it);
+    }
     mark_dirty(a.node);
   }
   ledger_.erase(it);
@@ -415,6 +443,14 @@ bool Engine::yoda_card_eligible(const PodReq& req, const Card& c, uint64_t m, ui
 }
 
 Reason Engine::filter_node(const PodReq& req, int32_t idx, uint64_t* pn, uint64_t* pm, uint64_t* pc) const {
+  if (!wants_spread_filter(req)) return filter_node_pf(req, idx, pn, pm, pc, nullptr);
+  SpreadPF pf;
+  spread_prefilter(req, &pf);
+  return filter_node_pf(req, idx, pn, pm, pc, &pf);
+}
+
+Reason Engine::filter_node_pf(const PodReq& req, int32_t idx, uint64_t* pn, uint64_t* pm, uint64_t* pc,
+                              const SpreadPF* pf) const {
   const Node& n = nodes_[idx];
   if (!n.alive) return RS_DEAD;
   if (filters_ & F_NODE_UNSCHEDULABLE) {
@@ -431,12 +467,38 @@ Reason Engine::filter_node(const PodReq& req, int32_t idx, uint64_t* pn, uint64_
     if (n.pod_count + 1 > n.alloc_pods) return RS_RESOURCES;
     if (req.cpu_m > 0 && n.alloc_cpu_m < req.cpu_m + n.req_cpu_m) return RS_RESOURCES;
     if (req.mem > 0 && n.alloc_mem < req.mem + n.req_mem) return RS_RESOURCES;
+    // resources beyond cpu/memory/pods (plugins/defaults.py NodeResourcesFit): requested +
+    // already used must fit the node's allocatable (absent = 0)
+    for (const auto& r : req.ext) {
+      if (!ext_checked(r.first)) continue;
+      int64_t alloc = 0, used = 0;
+      auto a = std::lower_bound(n.ext_alloc.begin(), n.ext_alloc.end(), std::make_pair(r.first, INT64_MIN));
+      if (a != n.ext_alloc.end() && a->first == r.first) alloc = a->second;
+      auto u = std::lower_bound(n.ext_used.begin(), n.ext_used.end(), std::make_pair(r.first, INT64_MIN));
+      if (u != n.ext_used.end() && u->first == r.first) used = u->second;
+      if (used + r.second > alloc) return RS_EXT_RESOURCES;
+    }
   }
   if ((filters_ & F_NODE_NAME) && req.node_name > 0 && strings_[req.node_name] != n.name) return RS_NODE_NAME;
   if ((filters_ & F_NODE_AFFINITY) && !affinity_ok(req, n)) return RS_AFFINITY;
   if ((filters_ & F_TAINT_TOLERATION) && !taints_ok(req, n)) return RS_TAINT;
-  if (!(filters_ & F_YODA)) return RS_OK;
-  return yoda_filter(req, idx, pn, pm, pc);
+  if (filters_ & F_YODA) {
+    const Reason r = yoda_filter(req, idx, pn, pm, pc);
+    if (r != RS_OK) return r;
+  }
+  // PodTopologySpread runs after the built-in filters (a Python filter in the hybrid runner,
+  // where every native filter comes first): same first-failing reason on both paths
+  if (pf && !pf->cons.empty()) return spread_filter(req, n, *pf);
+  return RS_OK;
+}
+
+bool Engine::ext_checked(int32_t res) const {
+  if (ext_ignored_.empty() && ext_ignored_groups_.empty()) return true;
+  if (std::find(ext_ignored_.begin(), ext_ignored_.end(), res) != ext_ignored_.end()) return false;
+  if (ext_ignored_groups_.empty()) return true;
+  const std::string& name = strings_[res];
+  const std::string group = name.substr(0, name.find('/'));
+  return std::find(ext_ignored_groups_.begin(), ext_ignored_groups_.end(), group) == ext_ignored_groups_.end();
 }
 
 Reason Engine::yoda_filter(const PodReq& req, int32_t idx, uint64_t* pn, uint64_t* pm, uint64_t* pc) const {
@@ -791,6 +853,12 @@ std::vector<int32_t> Engine::feasible_nodes(const PodReq& req, const std::vector
   if (N == 0) return feasible;
   const int32_t want = exhaustive ? N : num_feasible_to_find(N);
   const int32_t start = next_start_ % N;
+  SpreadPF pf_store;
+  const SpreadPF* pf = nullptr;
+  if (wants_spread_filter(req)) {
+    spread_prefilter(req, &pf_store);
+    pf = &pf_store;
+  }
   std::vector<int8_t> res;
   int32_t processed = 0;
   // chunks big enough to amortise a parallel_for (>= 512 nodes) yet small enough that the
@@ -802,7 +870,7 @@ std::vector<int32_t> Engine::feasible_nodes(const PodReq& req, const std::vector
     auto body = [&](int b, int e) {
       for (int j = b; j < e; ++j) {
         int32_t idx = all[(start + base + j) % N];
-        res[j] = (int8_t)filter_node(req, idx, nullptr, nullptr, nullptr);
+        res[j] = (int8_t)filter_node_pf(req, idx, nullptr, nullptr, nullptr, pf);
       }
     };
     if (pool_ && len >= 512) pool_->parallel_for(len, 64, body);
@@ -909,7 +977,369 @@ std::vector<int64_t> Engine::score_nodes(const PodReq& req, const std::vector<in
     default_normalize(s, false);
     for (size_t i = 0; i < F; ++i) total[i] += s[i] * score_w_[S_NODE_AFFINITY];
   }
+  if (score_w_[S_IMAGE_LOCALITY] && images_matter(req)) {
+    // plugins/node_extras.py ImageLocality (upstream v1.20 imagelocality): Σ size × spread,
+    // spread = nodes holding the image / all nodes, clamped to [23 MB, 1000 MB × containers]
+    const double all = (double)std::max<int32_t>(1, live_);
+    const int64_t lo = 23LL << 20, hi = (1000LL << 20) * std::max<int32_t>(1, req.containers);
+    for (size_t i = 0; i < F; ++i) {
+      const Node& n = nodes_[feas[i]];
+      int64_t sum = 0;
+      for (int32_t im : req.images) {
+        auto it = std::lower_bound(n.images.begin(), n.images.end(), std::make_pair(im, INT64_MIN));
+        if (it != n.images.end() && it->first == im && it->second)
+          sum += (int64_t)((double)it->second * ((double)image_nodes(im) / all));
+      }
+      sum = std::min(std::max(sum, lo), hi);
+      total[i] += score_w_[S_IMAGE_LOCALITY] * (kMaxNodeScore * (sum - lo) / (hi - lo));
+    }
+  }
+  if (score_w_[S_PREFER_AVOID]) {
+    // plugins/node_extras.py NodePreferAvoidPods: 0 where the node's preferAvoidPods
+    // annotation names the pod's RC / RS controller, 100 elsewhere
+    for (size_t i = 0; i < F; ++i) {
+      int64_t v = kMaxNodeScore;
+      if (req.avoid_kind)
+        for (const auto& a : nodes_[feas[i]].avoid)
+          if (a.first == req.avoid_kind && a.second == req.avoid_uid) {
+            v = 0;
+            break;
+          }
+      total[i] += score_w_[S_PREFER_AVOID] * v;
+    }
+  }
+  if (score_w_[S_SPREAD]) {
+    spread_scores(req, feas, s);
+    for (size_t i = 0; i < F; ++i) total[i] += s[i] * score_w_[S_SPREAD];
+  }
   return total;
+}
+
+// ============================================================== default plugins: node extras
+bool LSel::matches(const Labels& l) const {
+  if (nothing) return false;
+  for (const LReq& r : reqs) {
+    auto it = std::lower_bound(l.begin(), l.end(), std::make_pair(r.key, INT32_MIN));
+    const bool has = it != l.end() && it->first == r.key;
+    switch (r.op) {
+      case kIn:
+        if (!has || std::find(r.values.begin(), r.values.end(), it->second) == r.values.end()) return false;
+        break;
+      case kNotIn:
+        if (has && std::find(r.values.begin(), r.values.end(), it->second) != r.values.end()) return false;
+        break;
+      case kExists:
+        if (!has) return false;
+        break;
+      case kDoesNotExist:
+        if (has) return false;
+        break;
+      default:
+        return false;
+    }
+  }
+  return true;
+}
+
+void Engine::index_node_extras(const Node& n, int sign) {
+  for (const auto& im : n.images) {
+    int32_t& c = image_nodes_[im.first];
+    c += sign;
+    if (c <= 0) image_nodes_.erase(im.first);
+  }
+  if (!n.avoid.empty()) avoid_nodes_ += sign;
+}
+
+void Engine::set_node_extras(int32_t idx, std::vector<std::pair<int32_t, int64_t>> images,
+                             std::vector<std::pair<int32_t, int64_t>> ext_alloc,
+                             std::vector<std::pair<int8_t, int32_t>> avoid) {
+  Node& n = nodes_.at(idx);
+  if (!n.alive) return;
+  index_node_extras(n, -1);
+  std::sort(images.begin(), images.end());
+  images.erase(std::unique(images.begin(), images.end(),
+                           [](const auto& a, const auto& b) { return a.first == b.first; }),
+               images.end());
+  std::sort(ext_alloc.begin(), ext_alloc.end());
+  n.images = std::move(images);
+  n.ext_alloc = std::move(ext_alloc);
+  n.avoid = std::move(avoid);
+  index_node_extras(n, +1);
+  mark_dirty(idx);
+}
+
+int32_t Engine::image_nodes(int32_t image) const {
+  auto it = image_nodes_.find(image);
+  return it == image_nodes_.end() ? 0 : it->second;
+}
+
+bool Engine::images_matter(const PodReq& req) const {
+  // no node reports any of the pod's images: every node scores 0
+  for (int32_t im : req.images)
+    if (image_nodes_.count(im)) return true;
+  return false;
+}
+
+bool Engine::set_pod_meta(uint64_t pod, Labels labels, bool deleting) {
+  auto it = ledger_.find(pod);
+  if (it == ledger_.end()) return false;
+  std::sort(labels.begin(), labels.end());
+  it->second.labels = std::move(labels);
+  it->second.deleting = deleting;
+  return true;
+}
+
+// ============================================================== default plugins: topology spread
+void Engine::set_service(int32_t ns, int32_t name, bool nil_selector, Labels selector) {
+  std::sort(selector.begin(), selector.end());
+  auto& v = svcs_[ns];
+  for (auto& x : v)
+    if (x.name == name) {
+      x.nil = nil_selector;
+      x.sel = std::move(selector);
+      return;
+    }
+  v.push_back(Svc{name, nil_selector, std::move(selector)});
+  // upstream GetPodServices lists them in name order (the merge below is order-independent for
+  // services, which must all agree with the pod's labels, but keep the order anyway)
+  std::sort(v.begin(), v.end(), [&](const Svc& a, const Svc& b) { return strings_[a.name] < strings_[b.name]; });
+}
+
+void Engine::remove_service(int32_t ns, int32_t name) {
+  auto it = svcs_.find(ns);
+  if (it == svcs_.end()) return;
+  auto& v = it->second;
+  v.erase(std::remove_if(v.begin(), v.end(), [&](const Svc& x) { return x.name == name; }), v.end());
+  if (v.empty()) svcs_.erase(it);
+}
+
+void Engine::set_controller(int8_t kind, int32_t ns, int32_t name, LSel sel) {
+  ctrls_[ctrl_key(kind, ns, name)] = std::move(sel);
+}
+
+void Engine::remove_controller(int8_t kind, int32_t ns, int32_t name) { ctrls_.erase(ctrl_key(kind, ns, name)); }
+
+bool Engine::default_selector(const PodReq& req, LSel* out) const {
+  // plugins/optional.py::default_selector (upstream helper.DefaultSelector): the matching
+  // Services' selectors and an RC's map merged as equalities (later keys overwrite), an
+  // RS's / StatefulSet's LabelSelector added as requirements
+  out->nothing = false;
+  out->reqs.clear();
+  Labels eq;
+  auto put = [&](int32_t k, int32_t v) {
+    for (auto& kv : eq)
+      if (kv.first == k) {
+        kv.second = v;
+        return;
+      }
+    eq.emplace_back(k, v);
+  };
+  auto sv = svcs_.find(req.ns);
+  if (sv != svcs_.end())
+    for (const Svc& x : sv->second) {
+      if (x.nil) continue;                      // a nil selector matches nothing
+      bool all = true;
+      for (const auto& kv : x.sel) {
+        auto it = std::lower_bound(req.labels.begin(), req.labels.end(), std::make_pair(kv.first, INT32_MIN));
+        if (it == req.labels.end() || it->first != kv.first || it->second != kv.second) {
+          all = false;
+          break;
+        }
+      }
+      if (all)
+        for (const auto& kv : x.sel) put(kv.first, kv.second);
+    }
+  std::vector<LReq> extra;
+  if (req.owner_kind) {
+    auto c = ctrls_.find(ctrl_key(req.owner_kind, req.ns, req.owner_name));
+    if (c != ctrls_.end()) {
+      if (req.owner_kind == 1) {
+        for (const LReq& r : c->second.reqs)
+          if (r.op == kIn && r.values.size() == 1) put(r.key, r.values[0]);
+      } else if (!c->second.nothing) {
+        extra = c->second.reqs;
+      }
+    }
+  }
+  for (const auto& kv : eq) out->reqs.push_back(LReq{kv.first, kIn, {kv.second}});
+  for (auto& r : extra) out->reqs.push_back(std::move(r));
+  return !out->reqs.empty();
+}
+
+void Engine::spread_constraints(const PodReq& req, bool hard, std::vector<SpreadC>* out) const {
+  out->clear();
+  if (req.spread_explicit) {
+    for (const SpreadC& c : req.spread)
+      if (c.hard == hard) out->push_back(c);
+    return;
+  }
+  bool any = false;
+  for (const DefaultSpread& d : spread_defaults_) any |= d.hard == hard;
+  if (!any) return;
+  LSel sel;
+  if (!default_selector(req, &sel)) return;
+  for (const DefaultSpread& d : spread_defaults_)
+    if (d.hard == hard) out->push_back(SpreadC{d.key, d.max_skew, d.hard, sel});
+}
+
+int64_t Engine::count_matching(int32_t idx, int32_t ns, const LSel& sel) const {
+  // upstream countPodsMatchSelector: same namespace, not terminating, selector match
+  if (idx < 0 || idx >= (int32_t)nodes_.size() || sel.nothing) return 0;
+  int64_t c = 0;
+  for (uint64_t pod : nodes_[idx].pods) {
+    const Assignment& a = ledger_.at(pod);
+    if (a.ns == ns && !a.deleting && sel.matches(a.labels)) ++c;
+  }
+  return c;
+}
+
+bool Engine::wants_spread_filter(const PodReq& req) const {
+  if (!(filters_ & F_SPREAD)) return false;
+  if (req.spread_explicit) {
+    for (const SpreadC& c : req.spread)
+      if (c.hard) return true;
+    return false;
+  }
+  for (const DefaultSpread& d : spread_defaults_)
+    if (d.hard) return true;
+  return false;
+}
+
+static inline uint64_t pair_key(int32_t k, int32_t v) { return ((uint64_t)(uint32_t)k << 32) | (uint32_t)v; }
+
+void Engine::spread_prefilter(const PodReq& req, SpreadPF* pf) const {
+  // PodTopologySpread.pre_filter (plugins/spread_affinity.py): counts per (key, value) pair —
+  // shared by constraints of the same key, as upstream v1.20 — over the nodes that pass the
+  // pod's nodeSelector / required node affinity and carry every key
+  spread_constraints(req, true, &pf->cons);
+  pf->pair_counts.clear();
+  pf->min_count.clear();
+  if (pf->cons.empty()) return;
+  for (int32_t i = 0; i < (int32_t)nodes_.size(); ++i) {
+    const Node& n = nodes_[i];
+    if (!n.alive) continue;
+    bool keys = true;
+    for (const SpreadC& c : pf->cons)
+      if (!n.labels.count(c.key)) {
+        keys = false;
+        break;
+      }
+    if (!keys || !affinity_ok(req, n)) continue;
+    for (const SpreadC& c : pf->cons)
+      pf->pair_counts[pair_key(c.key, n.labels.at(c.key))] += n.pods.empty() ? 0 : count_matching(i, req.ns, c.sel);
+  }
+  for (const auto& kv : pf->pair_counts) {
+    const int32_t k = (int32_t)(kv.first >> 32);
+    auto it = pf->min_count.find(k);
+    if (it == pf->min_count.end() || kv.second < it->second) pf->min_count[k] = kv.second;
+  }
+}
+
+Reason Engine::spread_filter(const PodReq& req, const Node& n, const SpreadPF& pf) const {
+  for (const SpreadC& c : pf.cons) {
+    auto lab = n.labels.find(c.key);
+    if (lab == n.labels.end()) return RS_SPREAD_LABEL;
+    const int64_t self = c.sel.matches(req.labels) ? 1 : 0;
+    auto pc = pf.pair_counts.find(pair_key(c.key, lab->second));
+    auto mc = pf.min_count.find(c.key);
+    const int64_t skew = (pc == pf.pair_counts.end() ? 0 : pc->second) + self - (mc == pf.min_count.end() ? 0 : mc->second);
+    if (skew > c.max_skew) return RS_SPREAD;
+  }
+  return RS_OK;
+}
+
+bool Engine::spread_soft_constant(const std::vector<SpreadC>& soft) const {
+  for (const SpreadC& c : soft)
+    if (!label_key_nodes_.count(c.key)) return true;   // every node is "ignored": all score 0
+  return false;
+}
+
+static inline int64_t floor_div(int64_t a, int64_t b) {
+  int64_t q = a / b;
+  if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+  return q;
+}
+
+void Engine::spread_scores(const PodReq& req, const std::vector<int32_t>& feas, std::vector<int64_t>& s) const {
+  // PodTopologySpread pre_score / score / normalize_score (plugins/spread_affinity.py)
+  const size_t F = feas.size();
+  s.assign(F, 0);
+  std::vector<SpreadC> soft;
+  spread_constraints(req, false, &soft);
+  if (soft.empty() || F == 0 || spread_soft_constant(soft)) return;
+  static const std::string kHostname = "kubernetes.io/hostname";
+  auto hit = string_idx_.find(kHostname);
+  const int32_t host_key = hit == string_idx_.end() ? -1 : hit->second;
+  std::vector<char> ignored(F, 0);
+  size_t n_ignored = 0;
+  std::unordered_map<uint64_t, int64_t> pairs;   // non-hostname pairs among the scored nodes
+  std::vector<int64_t> sizes(soft.size(), 0);
+  for (size_t i = 0; i < F; ++i) {
+    const Node& n = nodes_[feas[i]];
+    bool keys = true;
+    for (const SpreadC& c : soft)
+      if (!n.labels.count(c.key)) {
+        keys = false;
+        break;
+      }
+    if (!keys) {
+      ignored[i] = 1;
+      ++n_ignored;
+      continue;
+    }
+    for (size_t k = 0; k < soft.size(); ++k) {
+      if (soft[k].key == host_key) continue;
+      if (pairs.emplace(pair_key(soft[k].key, n.labels.at(soft[k].key)), 0).second) ++sizes[k];
+    }
+  }
+  std::vector<double> w(soft.size());
+  for (size_t k = 0; k < soft.size(); ++k)
+    w[k] = std::log((double)((soft[k].key == host_key ? (int64_t)(F - n_ignored) : sizes[k]) + 2));
+  if (!pairs.empty()) {
+    for (int32_t i = 0; i < (int32_t)nodes_.size(); ++i) {
+      const Node& n = nodes_[i];
+      if (!n.alive) continue;
+      bool keys = true;
+      for (const SpreadC& c : soft)
+        if (!n.labels.count(c.key)) {
+          keys = false;
+          break;
+        }
+      if (!keys || !affinity_ok(req, n)) continue;
+      for (const SpreadC& c : soft) {
+        auto p = pairs.find(pair_key(c.key, n.labels.at(c.key)));
+        if (p != pairs.end() && !n.pods.empty()) p->second += count_matching(i, req.ns, c.sel);
+      }
+    }
+  }
+  bool any = false;
+  int64_t lo = 0, hi = 0;
+  for (size_t i = 0; i < F; ++i) {
+    if (ignored[i]) continue;
+    const Node& n = nodes_[feas[i]];
+    double total = 0.0;
+    for (size_t k = 0; k < soft.size(); ++k) {
+      auto lab = n.labels.find(soft[k].key);
+      if (lab == n.labels.end()) continue;
+      int64_t cnt;
+      if (soft[k].key == host_key) {
+        cnt = count_matching(feas[i], req.ns, soft[k].sel);
+      } else {
+        auto p = pairs.find(pair_key(soft[k].key, lab->second));
+        cnt = p == pairs.end() ? 0 : p->second;
+      }
+      total += (double)cnt * w[k] + (double)(soft[k].max_skew - 1);
+    }
+    s[i] = (int64_t)total;
+    lo = any ? std::min(lo, s[i]) : s[i];
+    hi = std::max(hi, s[i]);
+    any = true;
+  }
+  for (size_t i = 0; i < F; ++i) {
+    if (ignored[i]) s[i] = 0;
+    else if (hi == 0) s[i] = kMaxNodeScore;
+    else s[i] = floor_div(kMaxNodeScore * (hi + lo - s[i]), hi);
+  }
 }
 
 CycleResult Engine::schedule(uint64_t pod, const PodReq& req, bool assume, const std::vector<int32_t>& candidates,
@@ -1142,6 +1572,21 @@ bool Engine::device_eligible(const PodReq& req) const {
       wt_.w_numa < -1000000 || wt_.w_fit < -1000000 || wt_.w_occ < -1000000)
     return false;
   if (!default_alloc_weights()) return false;                    // device computes (c + m) / 2
+  // default-plugin terms the device row does not carry: only pods for which they are a
+  // constant (or nothing) go to the device
+  if ((filters_ & F_NODE_RESOURCES_FIT) && !req.ext.empty()) return false;
+  if (score_w_[S_IMAGE_LOCALITY] && images_matter(req)) return false;
+  if (score_w_[S_PREFER_AVOID] && req.avoid_kind && avoid_nodes_ > 0) return false;
+  if (wants_spread_filter(req)) {
+    std::vector<SpreadC> hard;
+    spread_constraints(req, true, &hard);
+    if (!hard.empty()) return false;
+  }
+  if (score_w_[S_SPREAD]) {
+    std::vector<SpreadC> soft;
+    spread_constraints(req, false, &soft);
+    if (!soft.empty() && !spread_soft_constant(soft)) return false;
+  }
   return true;
 }
 
@@ -1174,6 +1619,8 @@ void Engine::make_dev_req(const PodReq& req, yoda_dev_req_t* out) {
   d.w_most = score_w_[S_MOST_ALLOCATED];
   // no PreferNoSchedule taints anywhere: TaintToleration normalises every node to 100
   d.w_const = score_w_[S_TAINT_TOLERATION] * kMaxNodeScore;
+  // NodePreferAvoidPods scores every node 100 for a device-eligible pod (device_eligible)
+  d.w_const += score_w_[S_PREFER_AVOID] * kMaxNodeScore;
   d.w_link = wt_.w_link;
   d.w_numa = wt_.w_numa;
   d.w_fit = wt_.w_fit;

@@ -41,6 +41,7 @@ enum FilterBit : uint32_t {
   F_NODE_AFFINITY = 1u << 3,
   F_NODE_RESOURCES_FIT = 1u << 4,
   F_YODA = 1u << 5,
+  F_SPREAD = 1u << 6,          // PodTopologySpread DoNotSchedule constraints (explicit or profile defaults)
 };
 enum ScoreIdx : int {
   S_YODA = 0,
@@ -49,13 +50,20 @@ enum ScoreIdx : int {
   S_TAINT_TOLERATION = 3,
   S_NODE_AFFINITY = 4,
   S_MOST_ALLOCATED = 5,
-  S_NUM = 6,
+  S_IMAGE_LOCALITY = 6,
+  S_PREFER_AVOID = 7,          // NodePreferAvoidPods
+  S_SPREAD = 8,                // PodTopologySpread ScheduleAnyway constraints (explicit or profile defaults)
+  S_NUM = 9,
 };
 
 // Why a node was rejected (first failing plugin), reported for FitError diagnosis.
 enum Reason : int8_t {
   RS_OK = 0, RS_UNSCHEDULABLE, RS_NODE_NAME, RS_TAINT, RS_AFFINITY, RS_RESOURCES, RS_NO_SCV,
-  RS_STALE, RS_GPU_NUMBER, RS_GPU_MEMORY, RS_GPU_CLOCK, RS_GPU_FIT, RS_DEAD, RS_NUM
+  RS_STALE, RS_GPU_NUMBER, RS_GPU_MEMORY, RS_GPU_CLOCK, RS_GPU_FIT, RS_DEAD,
+  RS_EXT_RESOURCES,            // NodeResourcesFit: a resource beyond cpu/memory/pods
+  RS_SPREAD,                   // PodTopologySpread: skew
+  RS_SPREAD_LABEL,             // PodTopologySpread: the node lacks a constraint's topology key
+  RS_NUM
 };
 
 struct Card {
@@ -75,6 +83,39 @@ struct Toleration { int32_t key; int32_t value; int8_t op; int8_t effect; };  //
 struct SelReq { int32_t key; int8_t op; std::vector<int32_t> values; int64_t num; };
 struct SelTerm { std::vector<SelReq> reqs; };
 struct PrefTerm { int32_t weight; SelTerm term; };
+
+// Interned (key, value) pairs sorted by key: a pod's labels as the ledger keeps them.
+using Labels = std::vector<std::pair<int32_t, int32_t>>;
+
+// metav1.LabelSelector over interned strings (models/selectors.py::LabelSelector): every
+// requirement must hold — matchLabels k=v become In {v}, matchExpressions In/NotIn/Exists/
+// DoesNotExist keep their SelOp — and a nil selector (`nothing`) matches no pod.
+struct LReq {
+  int32_t key;
+  int8_t op;
+  std::vector<int32_t> values;
+};
+struct LSel {
+  bool nothing = false;
+  std::vector<LReq> reqs;
+  bool empty() const { return !nothing && reqs.empty(); }
+  bool matches(const Labels& l) const;
+};
+
+// One topology spread constraint (upstream v1.20 podtopologyspread; plugins/spread_affinity.py).
+struct SpreadC {
+  int32_t key = 0;             // interned topologyKey
+  int32_t max_skew = 1;
+  bool hard = true;            // DoNotSchedule (filter) vs ScheduleAnyway (score)
+  LSel sel;
+};
+// A profile's default constraint (PodTopologySpread args: System defaults or a List); its
+// selector is the pod's DefaultSelector (Services + controller)
+struct DefaultSpread {
+  int32_t key = 0;
+  int32_t max_skew = 1;
+  bool hard = false;
+};
 
 struct Node {
   std::string name;
@@ -96,6 +137,10 @@ struct Node {
   bool hard_taint = false, prefer_taint = false;   // has NoSchedule/NoExecute, PreferNoSchedule taints
   double sample_ts = 0;               // unix time of the Scv sample the cards came from
   std::vector<uint64_t> pods;         // ledger entries on this node (for pending recompute)
+  std::vector<std::pair<int32_t, int64_t>> images;     // status.images: (normalized name, bytes), sorted
+  std::vector<std::pair<int32_t, int64_t>> ext_alloc;  // allocatable beyond cpu/memory/pods, sorted
+  std::vector<std::pair<int32_t, int64_t>> ext_used;   // Σ of the ledger's ext requests, sorted
+  std::vector<std::pair<int8_t, int32_t>> avoid;       // preferAvoidPods controllers (kind 1 RC / 2 RS, uid)
 };
 
 struct PodReq {
@@ -111,6 +156,28 @@ struct PodReq {
   std::vector<SelTerm> required_terms;   // ORed
   std::vector<PrefTerm> preferred_terms;
   std::vector<Toleration> tolerations;
+  // what other pods' spread constraints read of this pod once it holds a reservation (the
+  // ledger keeps them): namespace, labels, terminating
+  int32_t ns = 0;
+  Labels labels;
+  bool deleting = false;
+  // ImageLocality: normalized images of spec.containers (interned), and their count
+  std::vector<int32_t> images;
+  int32_t containers = 0;
+  // NodeResourcesFit beyond cpu / memory / pods (ephemeral-storage, hugepages-*, amd.com/gpu,
+  // other extended resources): (interned resource name, amount), sorted by name
+  std::vector<std::pair<int32_t, int64_t>> ext;
+  // controllerRef for DefaultSelector (1 v1 ReplicationController, 2 apps/v1 ReplicaSet,
+  // 3 apps/v1 StatefulSet; 0 none / another kind) and for NodePreferAvoidPods (the first
+  // controller of kind ReplicationController (1) or ReplicaSet (2), any apiVersion, by uid)
+  int8_t owner_kind = 0;
+  int32_t owner_name = -1;
+  int8_t avoid_kind = 0;
+  int32_t avoid_uid = -1;
+  // PodTopologySpread: spec.topologySpreadConstraints (when non-empty the profile's default
+  // constraints do not apply, even for an action none of them has)
+  bool spread_explicit = false;
+  std::vector<SpreadC> spread;
 };
 
 struct Weights {
@@ -145,6 +212,10 @@ struct Assignment {
   bool has_label_mem = false;
   double t_res = 0;             // unix time of the reservation
   int32_t slot = -1;            // index in Node::pods
+  int32_t ns = 0;               // the pod as other pods' spread constraints count it
+  Labels labels;
+  bool deleting = false;
+  std::vector<std::pair<int32_t, int64_t>> ext;   // extended resources it holds on the node
 };
 
 struct CycleResult {
@@ -184,10 +255,13 @@ class ThreadPool {
 // per profile and swaps it in around its batches, restoring the caller's afterwards.
 struct EngineConfig {
   uint32_t filters = 0;
-  int64_t score_w[S_NUM] = {0, 0, 0, 0, 0, 0};
+  int64_t score_w[S_NUM] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   int64_t alloc_w[2][3] = {{1, 1, 0}, {1, 1, 0}};
   Weights wt;
   double settle_s = 30.0;
+  std::vector<DefaultSpread> spread_defaults;   // PodTopologySpread default constraints
+  std::vector<int32_t> ext_ignored;             // NodeResourcesFit ignoredResources
+  std::vector<std::string> ext_ignored_groups;  // NodeResourcesFit ignoredResourceGroups
 };
 
 class Engine {
@@ -292,6 +366,38 @@ class Engine {
   // ---- k8s node facts (keeps the taint census the device path needs)
   void set_node_meta(int32_t idx, bool unschedulable, const std::vector<std::pair<int32_t, int32_t>>& labels,
                      const std::vector<Taint>& taints, int64_t cpu_m, int64_t mem, int64_t pods);
+  // status.images (ImageLocality), allocatable beyond cpu/memory/pods (NodeResourcesFit) and the
+  // preferAvoidPods annotation's controllers (NodePreferAvoidPods); each list sorted by key
+  void set_node_extras(int32_t idx, std::vector<std::pair<int32_t, int64_t>> images,
+                       std::vector<std::pair<int32_t, int64_t>> ext_alloc,
+                       std::vector<std::pair<int8_t, int32_t>> avoid);
+  int32_t image_nodes(int32_t image) const;          // nodes reporting the image
+  int32_t avoid_nodes() const { return avoid_nodes_; }
+
+  // ---- DefaultSelector sources (upstream helper.DefaultSelector: Services selecting the pod,
+  // its ReplicationController's map selector, its ReplicaSet's / StatefulSet's LabelSelector)
+  void set_service(int32_t ns, int32_t name, bool nil_selector, Labels selector);
+  void remove_service(int32_t ns, int32_t name);
+  // kind 1 RC (the map as In requirements), 2 RS, 3 STS
+  void set_controller(int8_t kind, int32_t ns, int32_t name, LSel sel);
+  void remove_controller(int8_t kind, int32_t ns, int32_t name);
+  // the pod's DefaultSelector; false when it is empty (no default constraints apply)
+  bool default_selector(const PodReq& req, LSel* out) const;
+  // the pod's constraints of one action (explicit ones, else the profile defaults with the
+  // DefaultSelector); empty when the pod has none
+  void spread_constraints(const PodReq& req, bool hard, std::vector<SpreadC>* out) const;
+  // a reserved pod's labels or deletionTimestamp changed (spread counts read them)
+  bool set_pod_meta(uint64_t pod, Labels labels, bool deleting);
+  // pods on node idx holding a reservation, in namespace ns, not terminating, matching sel
+  int64_t count_matching(int32_t idx, int32_t ns, const LSel& sel) const;
+
+  // ---- profile configuration of the default plugins beyond the score weights
+  void set_spread_defaults(std::vector<DefaultSpread> d) { spread_defaults_ = std::move(d); }
+  const std::vector<DefaultSpread>& spread_defaults() const { return spread_defaults_; }
+  void set_ext_ignored(std::vector<int32_t> res, std::vector<std::string> groups) {
+    ext_ignored_ = std::move(res);
+    ext_ignored_groups_ = std::move(groups);
+  }
 
   // ---- gfx950 device scorer (libyoda_hip.so, loaded with dlopen; see native/hip/scorer.hip)
   // Offloads whole cycles for clusters of >= min_nodes nodes when the pod/profile is
@@ -328,6 +434,26 @@ class Engine {
                              std::vector<CycleResult>* out);
   void make_dev_req(const PodReq& req, yoda_dev_req_t* out);
   bool needs_candidates(const PodReq& req) const;
+  // PodTopologySpread PreFilter state of one pod's DoNotSchedule constraints (upstream
+  // preFilterState): matching pods per (key, value) over the nodes passing the pod's node
+  // affinity that carry every key, and the minimum per key
+  struct SpreadPF {
+    std::vector<SpreadC> cons;
+    std::unordered_map<uint64_t, int64_t> pair_counts;   // (key << 32) | value
+    std::unordered_map<int32_t, int64_t> min_count;
+  };
+  void spread_prefilter(const PodReq& req, SpreadPF* pf) const;
+  Reason spread_filter(const PodReq& req, const Node& n, const SpreadPF& pf) const;
+  Reason filter_node_pf(const PodReq& req, int32_t idx, uint64_t* n, uint64_t* m, uint64_t* c,
+                        const SpreadPF* pf) const;
+  bool wants_spread_filter(const PodReq& req) const;
+  bool ext_checked(int32_t res) const;
+  // normalized PodTopologySpread scores of the feasible nodes (soft constraints)
+  void spread_scores(const PodReq& req, const std::vector<int32_t>& feas, std::vector<int64_t>& s) const;
+  // the soft constraints score every node 0 (no live node carries one of their keys)
+  bool spread_soft_constant(const std::vector<SpreadC>& soft) const;
+  bool images_matter(const PodReq& req) const;
+  void index_node_extras(const Node& n, int sign);
   void fill_result(const yoda_dev_result_t& res, CycleResult* r) const;
   Reason candidate_reason(const PodReq& req, const Node& n) const;
   bool taints_ok(const PodReq& req, const Node& n) const;
@@ -341,7 +467,7 @@ class Engine {
   bool compat_;
   uint32_t filters_ = F_NODE_UNSCHEDULABLE | F_NODE_NAME | F_TAINT_TOLERATION | F_NODE_AFFINITY |
                       F_NODE_RESOURCES_FIT | F_YODA;
-  int64_t score_w_[S_NUM] = {300, 1, 1, 1, 1, 0};
+  int64_t score_w_[S_NUM] = {300, 1, 1, 1, 1, 0, 0, 0, 0};
   int64_t alloc_w_[2][3] = {{1, 1, 0}, {1, 1, 0}};   // [least, most][cpu, memory, other]
   Weights wt_;
   int pct_nodes_ = 0;
@@ -367,6 +493,23 @@ class Engine {
   std::vector<char> dirty_;
   std::vector<int32_t> dirty_list_;
   int32_t hard_taint_nodes_ = 0, prefer_taint_nodes_ = 0;
+  // default-plugin state beyond the node rows
+  std::unordered_map<int32_t, int32_t> image_nodes_;      // image → nodes reporting it
+  int32_t avoid_nodes_ = 0;                               // nodes with preferAvoidPods controllers
+  std::unordered_map<int32_t, int32_t> label_key_nodes_;  // label key → live nodes carrying it
+  struct Svc {
+    int32_t name;
+    bool nil;
+    Labels sel;
+  };
+  std::unordered_map<int32_t, std::vector<Svc>> svcs_;    // namespace → services
+  std::unordered_map<uint64_t, LSel> ctrls_;              // (kind, ns, name) → selector
+  static uint64_t ctrl_key(int8_t kind, int32_t ns, int32_t name) {
+    return ((uint64_t)(uint8_t)kind << 58) ^ ((uint64_t)(uint32_t)ns << 29) ^ (uint64_t)(uint32_t)name;
+  }
+  std::vector<DefaultSpread> spread_defaults_;
+  std::vector<int32_t> ext_ignored_;
+  std::vector<std::string> ext_ignored_groups_;
   void* fn_destroy_ = nullptr;
   void* fn_upload_ = nullptr;
   void* fn_schedule_ = nullptr;

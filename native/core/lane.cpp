@@ -21,7 +21,8 @@ constexpr uint64_t kPatchBit = 1ull << 62;   // with kEventTag: a PodScheduled=F
 // engine Reason → FitError text (framework/scheduler.py::_fit_error)
 const char* const kReasonName[RS_NUM] = {"OK", "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity",
                                          "NodeResourcesFit", "NoScv", "ScvStale", "GpuNumber", "GpuMemory",
-                                         "GpuClock", "GpuFit", "NodeGone"};
+                                         "GpuClock", "GpuFit", "NodeGone", "NodeResourcesFitExtended",
+                                         "PodTopologySpread", "PodTopologySpreadLabel"};
 const char* reason_text(int i) {
   switch (i) {
     case RS_UNSCHEDULABLE: return "node(s) were unschedulable";
@@ -35,6 +36,9 @@ const char* reason_text(int i) {
     case RS_GPU_MEMORY: return "node(s) have too few GPUs with enough free HBM";
     case RS_GPU_CLOCK: return "node(s) have too few GPUs with the requested clock";
     case RS_GPU_FIT: return "node(s) have too few healthy GPUs matching scv/memory+scv/clock";
+    case RS_EXT_RESOURCES: return "node(s) had insufficient extended resources";
+    case RS_SPREAD: return "node(s) didn't match pod topology spread constraints";
+    case RS_SPREAD_LABEL: return "node(s) didn't match pod topology spread constraints (missing required label)";
     default: return i >= 0 && i < RS_NUM ? kReasonName[i] : "unknown";
   }
 }
@@ -582,9 +586,15 @@ void Lane::handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::ve
     return;                                // stays in the store as a Python-visible terminal pod
   }
   if ((e->st == BINDING || e->st == BOUND) && p.node == e->node_name) {
+    const bool was_deleting = old->p.deleting;
     if (!e->lab_ev || !p.labels_hash || p.labels_hash != e->lab_ev->p.labels_hash) {
+      // the engine ledger's copy of the labels (spread counts) follows a real change only:
+      // the first echo carries the labels the pod was placed with
+      if (e->lab_ev && (!p.labels_hash || p.labels_hash != e->lab_ev->p.labels_hash)) meta_pending_.push_back({e->id, ev});
       e->lab_ev = ev;
       if (e->crow >= 0) census_[e->crow].dirty = true;
+    } else if (p.deleting != was_deleting) {
+      meta_pending_.push_back({e->id, ev});
     }
     if (e->crow >= 0) census_[e->crow].deleting = p.deleting;
     e->ev = ev;
@@ -851,7 +861,51 @@ bool Lane::make_req(const yk::PodProj& p, PodReq* r) {
     x.effect = effect_of(t.effect);
     r->tolerations.push_back(x);
   }
+  // default-plugin inputs (ops/native.py::pod_req → Engine.set_req_extras)
+  r->ns = eng_->intern(p.ns);
+  r->labels = intern_labels(p.labels);
+  r->deleting = p.deleting;
+  for (const auto& im : p.images) r->images.push_back(eng_->intern(im));
+  r->containers = p.containers;
+  for (const auto& x : p.ext) r->ext.emplace_back(eng_->intern(x.first), x.second);
+  std::sort(r->ext.begin(), r->ext.end());
+  if (p.has_owner) {
+    r->owner_kind = p.owner_api == "v1" && p.owner_kind == "ReplicationController" ? 1
+                    : p.owner_api == "apps/v1" && p.owner_kind == "ReplicaSet"  ? 2
+                    : p.owner_api == "apps/v1" && p.owner_kind == "StatefulSet" ? 3 : 0;
+    if (r->owner_kind) r->owner_name = eng_->intern(p.owner_name);
+  }
+  if (p.has_avoid) {
+    r->avoid_kind = p.avoid_kind == "ReplicationController" ? 1 : 2;
+    r->avoid_uid = eng_->intern(p.avoid_uid);
+  }
+  r->spread_explicit = !p.spread.empty();
+  for (const auto& c : p.spread) {
+    if (c.when == 2) continue;               // neither DoNotSchedule nor ScheduleAnyway: in no list
+    SpreadC x;
+    x.key = eng_->intern(c.key);
+    x.max_skew = (int32_t)c.max_skew;
+    x.hard = c.when == 0;
+    x.sel.nothing = !c.has_sel;
+    for (const auto& kv : c.labels) x.sel.reqs.push_back(LReq{eng_->intern(kv.first), kIn, {eng_->intern(kv.second)}});
+    for (const auto& q : c.exprs) {
+      LReq lr;
+      lr.key = eng_->intern(q.key);
+      if (!selop_of(q.op, &lr.op) || lr.op == kGt || lr.op == kLt) return false;
+      for (const auto& v : q.values) lr.values.push_back(eng_->intern(v));
+      x.sel.reqs.push_back(std::move(lr));
+    }
+    r->spread.push_back(std::move(x));
+  }
   return true;
+}
+
+Labels Lane::intern_labels(const std::vector<std::pair<std::string, std::string>>& kv) {
+  Labels l;
+  l.reserve(kv.size());
+  for (const auto& x : kv) l.emplace_back(eng_->intern(x.first), eng_->intern(x.second));
+  std::sort(l.begin(), l.end());
+  return l;
 }
 
 void Lane::annotations(const Profile& pr, const Entry& e, const PodReq& req, const CycleResult& r,
@@ -1483,10 +1537,23 @@ void Lane::pause(bool on) {
 // AddUnschedulableIfNotPresent: unschedulableQ, or podBackoffQ when a move request arrived since
 // the pod's cycle began (moveRequestCycle) or a node hint since then makes it fit.
 
-std::string Lane::fit_error(const CycleResult& r) const {
+std::string Lane::fit_error(const CycleResult& r, const yk::PodProj& p) const {
   std::vector<std::string> parts;
-  for (int i = 1; i < (int)r.reason_counts.size() && i < RS_NUM; ++i)
-    if (r.reason_counts[i]) parts.push_back(std::to_string(r.reason_counts[i]) + " " + reason_text(i));
+  for (int i = 1; i < (int)r.reason_counts.size() && i < RS_NUM; ++i) {
+    if (!r.reason_counts[i]) continue;
+    if (i == RS_EXT_RESOURCES) {
+      // framework/scheduler.py::ext_text: "Insufficient <the pod's resources beyond cpu/memory>"
+      std::vector<std::string> names;
+      for (const auto& x : p.ext) names.push_back(x.first);
+      std::sort(names.begin(), names.end());
+      std::string t = "Insufficient ";
+      for (size_t k = 0; k < names.size(); ++k) t += (k ? "/" : "") + names[k];
+      if (names.empty()) t += "extended resources";
+      parts.push_back(std::to_string(r.reason_counts[i]) + " " + t);
+      continue;
+    }
+    parts.push_back(std::to_string(r.reason_counts[i]) + " " + reason_text(i));
+  }
   std::sort(parts.begin(), parts.end());
   std::string m = "0/" + std::to_string(r.evaluated) + " nodes are available: ";
   for (size_t i = 0; i < parts.size(); ++i) {
@@ -1542,7 +1609,7 @@ void Lane::patch_condition(const Entry& e, const std::string& msg) {
 void Lane::fail_native(Entry* e, const Profile& pr, const CycleResult& res, bool hinted) {
   const double now = mono();
   e->t_fail = now;
-  const std::string msg = fit_error(res);
+  const std::string msg = fit_error(res, e->ev->full());
   {
     std::lock_guard<std::mutex> g(stat_mu_);
     st_.unschedulable++;
@@ -1854,10 +1921,15 @@ void Lane::run() {
     process_moves();
     flush_queues(mono());
     auto release_pending = [&] {
-      if (to_release_.empty()) return;
+      if (to_release_.empty() && meta_pending_.empty()) return;
       std::lock_guard<std::recursive_mutex> lk(*emu_);
       for (uint64_t id : to_release_) eng_->release(id);
       to_release_.clear();
+      for (auto& m : meta_pending_) {
+        const yk::PodProj& q = m.second->full();
+        eng_->set_pod_meta(m.first, intern_labels(q.labels), q.deleting);
+      }
+      meta_pending_.clear();
     };
     if (!done.empty()) {
       release_pending();                  // deletions of this turn free capacity for the next run

@@ -304,6 +304,7 @@ class Lane : public yk::PodSink {
   bool admissible(const yk::PodProj& p, int* prof) const;
   int64_t prio_of(const yk::PodProj& p) const;
   bool make_req(const yk::PodProj& p, PodReq* r);
+  Labels intern_labels(const std::vector<std::pair<std::string, std::string>>& kv);   // engine lock held
   void annotations(const Profile& pr, const Entry& e, const PodReq& req, const CycleResult& r,
                    std::vector<yk::KV>* out);
   void record_scheduled(const Entry& e);
@@ -318,7 +319,7 @@ class Lane : public yk::PodSink {
   void flush_queues(double now);
   bool hinted_since(uint64_t cycle, const PodReq& req);
   double next_timer() const;
-  std::string fit_error(const CycleResult& r) const;
+  std::string fit_error(const CycleResult& r, const yk::PodProj& p) const;
   void patch_condition(const Entry& e, const std::string& msg);
   void flush_events();
   void forward(char type, std::shared_ptr<yk::PodEv> ev, std::shared_ptr<yk::PodEv> old, std::vector<Fwd>* out);
@@ -418,6 +419,8 @@ class Lane : public yk::PodSink {
 
   // lane-thread scratch, flushed once per loop turn
   std::vector<uint64_t> to_release_;                 // engine ledger releases (one lock per turn)
+  // reserved pods whose labels / deletionTimestamp changed: the engine ledger's copy follows
+  std::vector<std::pair<uint64_t, std::shared_ptr<yk::PodEv>>> meta_pending_;
   std::vector<Handoff> hand_pending_;
   uint64_t out_moves_pending_ = 0;
  public:

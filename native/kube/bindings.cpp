@@ -1,4 +1,5 @@
 // pybind11 bindings of the native Kubernetes transport (module yoda_scheduler_amd._native._yoda_kube).
+#include <algorithm>
 #include <pybind11/pybind11.h>
 
 #include "build_id.h"
@@ -57,9 +58,46 @@ py::tuple info_args(const PodProj& p) {
     for (const auto& x : p.ports) t.append(py::make_tuple(x.host_port, py::str(x.protocol), py::str(x.host_ip)));
     ports = std::move(t);
   }
+  py::object ext = py::none();
+  if (!p.ext.empty()) {
+    py::dict d;
+    for (const auto& e : p.ext) d[py::str(e.first)] = e.second;
+    ext = std::move(d);
+  }
+  py::list images;
+  for (const auto& im : p.images) images.append(py::str(im));
+  py::object owner = p.has_owner ? py::object(py::make_tuple(py::str(p.owner_api), py::str(p.owner_kind),
+                                                            py::str(p.owner_name), py::str(p.owner_uid)))
+                                 : py::object(py::none());
+  py::object avoid = p.has_avoid ? py::object(py::make_tuple(py::str(p.avoid_kind), py::str(p.avoid_uid)))
+                                 : py::object(py::none());
+  py::object spread = py::none();
+  if (!p.spread.empty()) {
+    // (topologyKey, maxSkew, whenUnsatisfiable, LabelSelector.native() tuple | None)
+    static const char* kWhen[3] = {"DoNotSchedule", "ScheduleAnyway", "?"};
+    py::list l;
+    for (const auto& c : p.spread) {
+      py::object sel = py::none();
+      if (c.has_sel) {
+        py::list lab, ex;
+        for (const auto& kv : c.labels) lab.append(py::make_tuple(py::str(kv.first), py::str(kv.second)));
+        for (const auto& e : c.exprs) {
+          std::vector<std::string> vals = e.values;
+          std::sort(vals.begin(), vals.end());
+          vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+          py::tuple vt(vals.size());
+          for (size_t i = 0; i < vals.size(); ++i) vt[i] = py::str(vals[i]);
+          ex.append(py::make_tuple(py::str(e.key), py::str(e.op), vt));
+        }
+        sel = py::make_tuple(py::none(), false, py::tuple(lab), py::tuple(ex));
+      }
+      l.append(py::make_tuple(py::str(c.key), c.max_skew, py::str(kWhen[c.when]), sel));
+    }
+    spread = std::move(l);
+  }
   return py::make_tuple(py::str(p.uid), py::str(p.ns), py::str(p.name), kv_dict(p.labels), ann, py::str(p.sched),
                         py::str(p.node), p.cpu, p.mem, p.nzc, p.nzm, p.priority, nsel, req, pref, tols, ports,
-                        p.flags, py::str(p.creation));
+                        p.flags, py::str(p.creation), ext, images, p.containers, owner, avoid, spread, p.deleting);
 }
 
 std::shared_ptr<PodEv> project_bytes(const std::string& raw) {

@@ -84,6 +84,15 @@ bool starts_with(std::string_view s, std::string_view p) { return s.substr(0, p.
 
 bool is_basic(std::string_view k) { return k == "cpu" || k == "memory"; }
 
+// models/pod.py::normalize_image: an image without a tag or digest means ":latest"
+std::string normalize_image(std::string_view name) {
+  const size_t c = name.rfind(':'), sl = name.rfind('/');
+  const long ci = c == std::string_view::npos ? -1 : (long)c, si = sl == std::string_view::npos ? -1 : (long)sl;
+  std::string out(name);
+  if (ci <= si && name.find('@') == std::string_view::npos) out += ":latest";
+  return out;
+}
+
 // Uniform read-only view of a decoded JSON value, over the DOM (json.hpp) or the flat
 // document (flatjson.hpp): one projection body serves both, so they cannot drift apart.
 struct DomN {
@@ -309,22 +318,36 @@ void project_generic(N pod, PodProj& p) {
     N q = r.get("requests");
     return (q && q.truthy()) ? q : N{};
   };
-  auto ext_in = [](N r) {
-    if (!r || !r.obj()) return false;
-    bool ext = false;
-    r.each([&](std::string_view k, N) {
-      if (!is_basic(k)) ext = true;
-      return !ext;
+  // requests beyond cpu/memory (models/pod.py::ext_requests): Σ containers, max with each
+  // init container, + overhead, as integer units
+  std::vector<std::pair<std::string, int64_t>> ext;
+  auto ext_add = [&](N r, bool take_max) {
+    if (!r || !r.obj()) return true;
+    return r.each([&](std::string_view k, N q) {
+      if (is_basic(k)) return true;
+      int64_t v;
+      if (!quantity_of(q, 0, &v)) return false;
+      for (auto& e : ext)
+        if (e.first == k) {
+          e.second = take_max ? std::max(e.second, v) : e.second + v;
+          return true;
+        }
+      ext.emplace_back(std::string(k), take_max ? std::max<int64_t>(0, v) : v);
+      return true;
     });
-    return ext;
   };
   int flags = 0;
   if (N cs = sp.get("containers"); cs && cs.arr()) {
     bool ok = cs.each([&](std::string_view, N c) {
       if (!c.obj()) return false;
+      ++p.containers;
+      if (N im = c.get("image"); im && im.truthy()) {
+        if (!im.str_t()) return false;
+        p.images.push_back(normalize_image(im.str()));
+      }
       N r = reqs_of(c);
       if (r && !r.obj()) return false;
-      if (ext_in(r)) return false;                        // extended resources: Python path
+      if (!ext_add(r, false)) return false;
       int64_t v;
       if (N q = r ? r.get("cpu") : N{}) {
         if (!quantity_of(q, 3, &v)) return false;
@@ -371,7 +394,7 @@ void project_generic(N pod, PodProj& p) {
       if (!c.obj()) return false;
       N r = reqs_of(c);
       if (r && !r.obj()) return false;
-      if (ext_in(r)) return false;
+      if (!ext_add(r, true)) return false;
       int64_t v = 0;
       N q = r ? r.get("cpu") : N{};
       if (q && !quantity_of(q, 3, &v)) return false;
@@ -388,7 +411,7 @@ void project_generic(N pod, PodProj& p) {
     if (!ok) return;
   }
   if (N ov = sp.get("overhead"); ov && ov.truthy()) {
-    if (!ov.obj() || ext_in(ov)) return;
+    if (!ov.obj() || !ext_add(ov, false)) return;
     int64_t v;
     if (N q = ov.get("cpu")) {
       if (!quantity_of(q, 3, &v)) return;
@@ -405,6 +428,9 @@ void project_generic(N pod, PodProj& p) {
   p.mem = mem;
   p.nzc = nzc;
   p.nzm = nzm;
+  for (auto& e : ext)
+    if (e.second) p.ext.push_back(std::move(e));
+  if (!p.ext.empty()) flags |= PF_EXTENDED;
   if (!p.ports.empty()) flags |= PF_HOST_PORTS;
 
   if (N ns = sp.get("nodeSelector"); ns && ns.truthy()) {
@@ -481,7 +507,66 @@ void project_generic(N pod, PodProj& p) {
     });
     if (!ok) return;
   }
-  if (N tsc = sp.get("topologySpreadConstraints"); tsc && tsc.truthy()) flags |= PF_SPREAD;
+  if (N tsc = sp.get("topologySpreadConstraints"); tsc && tsc.truthy()) {
+    flags |= PF_SPREAD;
+    if (!tsc.arr()) return;
+    // plugins/spread_affinity.py::_parse_constraints + models/selectors.py::LabelSelector
+    bool ok = tsc.each([&](std::string_view, N c) {
+      if (!c.obj()) return false;
+      PodProj::SpreadP x;
+      N k = c.get("topologyKey");
+      if (k && !k.str_t()) return false;
+      x.key = k ? std::string(k.str()) : "";
+      if (N ms = c.get("maxSkew")) {
+        bool iok;
+        if (!ms.num_t()) return false;
+        x.max_skew = ms.as_int(&iok);
+        if (!iok) return false;
+      }
+      N wu = c.get("whenUnsatisfiable");
+      if (wu && !wu.str_t()) return false;
+      const std::string_view w = wu ? wu.str() : std::string_view("DoNotSchedule");
+      x.when = w == "DoNotSchedule" ? 0 : w == "ScheduleAnyway" ? 1 : 2;
+      if (x.when == 0) flags |= PF_SPREAD_HARD;
+      N ls = c.get("labelSelector");
+      if (ls && !ls.null_t()) {
+        if (!ls.obj()) return false;
+        x.has_sel = true;
+        N ml = ls.get("matchLabels");
+        if (ml && ml.truthy() && !kvs(ml, x.labels)) return false;
+        if (N me = ls.get("matchExpressions"); me && me.truthy()) {
+          if (!me.arr()) return false;
+          bool eok = me.each([&](std::string_view, N e) {
+            if (!e.obj()) return false;
+            SelReqP r;
+            N ek = e.get("key");
+            if (ek && !ek.str_t()) return false;
+            r.key = ek ? std::string(ek.str()) : "";
+            N op = e.get("operator");
+            if (op && !op.str_t()) return false;
+            r.op = op ? std::string(op.str()) : "In";
+            if (r.op != "In" && r.op != "NotIn" && r.op != "Exists" && r.op != "DoesNotExist") return false;
+            N vs = e.get("values");
+            if (vs && vs.truthy()) {
+              if (!vs.arr()) return false;
+              if (!vs.each([&](std::string_view, N v) {
+                    if (!v.str_t()) return false;
+                    r.values.emplace_back(v.str());
+                    return true;
+                  }))
+                return false;
+            }
+            x.exprs.push_back(std::move(r));
+            return true;
+          });
+          if (!eok) return false;
+        }
+      }
+      p.spread.push_back(std::move(x));
+      return true;
+    });
+    if (!ok) return;
+  }
   if (N vols = sp.get("volumes"); vols && vols.arr()) {
     static const char* kDisks[] = {"gcePersistentDisk", "awsElasticBlockStore", "azureDisk", "cinder", "iscsi", "rbd"};
     bool ok = vols.each([&](std::string_view, N v) {
@@ -506,8 +591,21 @@ void project_generic(N pod, PodProj& p) {
       if (!r.obj()) return false;
       N c = r.get("controller");
       std::string_view kind = r.sv("kind");
-      if (c && c.truthy() && (kind == "ReplicationController" || kind == "ReplicaSet" || kind == "StatefulSet"))
+      const bool ctl = c && c.truthy();
+      if (ctl && (kind == "ReplicationController" || kind == "ReplicaSet" || kind == "StatefulSet"))
         flags |= PF_CONTROLLER;
+      if (ctl && !p.has_owner) {            // DefaultSelector reads the first controller only
+        p.has_owner = true;
+        p.owner_api = std::string(r.sv("apiVersion"));
+        p.owner_kind = std::string(kind);
+        p.owner_name = std::string(r.sv("name"));
+        p.owner_uid = std::string(r.sv("uid"));
+      }
+      if (ctl && !p.has_avoid && (kind == "ReplicationController" || kind == "ReplicaSet")) {
+        p.has_avoid = true;                 // NodePreferAvoidPods: the first RC / RS controller
+        p.avoid_kind = std::string(kind);
+        p.avoid_uid = std::string(r.sv("uid"));
+      }
       return true;
     });
     if (!ok) return;
@@ -848,6 +946,18 @@ void merge_non_identity(PodProj& d, PodProj&& s) {
   d.pref_terms = std::move(s.pref_terms);
   d.tolerations = std::move(s.tolerations);
   d.ports = std::move(s.ports);
+  d.images = std::move(s.images);
+  d.containers = s.containers;
+  d.ext = std::move(s.ext);
+  d.has_owner = s.has_owner;
+  d.owner_api = std::move(s.owner_api);
+  d.owner_kind = std::move(s.owner_kind);
+  d.owner_name = std::move(s.owner_name);
+  d.owner_uid = std::move(s.owner_uid);
+  d.has_avoid = s.has_avoid;
+  d.avoid_kind = std::move(s.avoid_kind);
+  d.avoid_uid = std::move(s.avoid_uid);
+  d.spread = std::move(s.spread);
   d.flags = s.flags;
   d.spec_meta_hash = s.spec_meta_hash;
   d.ok = s.ok;

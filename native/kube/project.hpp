@@ -26,6 +26,7 @@ enum : int {
   PF_EXTENDED = 64,
   PF_POD_GROUP = 128,
   PF_REQ_ANTI = 256,    // required pod anti-affinity (symmetry check of other pods)
+  PF_SPREAD_HARD = 512, // a DoNotSchedule topology spread constraint
 };
 
 using KV = std::pair<std::string, std::string>;
@@ -67,6 +68,26 @@ struct PodProj {
   // watch identity scanner too, so a light event tells whether a pod's labels changed
   // without being projected (the lane's per-node selector census keeps the older projection)
   uint64_t labels_hash = 0;
+  // default-plugin inputs (models/pod.py PodInfo.images / containers / ext / owner / avoid /
+  // spread): normalized images of spec.containers and their count, requests beyond cpu/memory
+  // (non-zero, models/pod.py::ext_requests), the first controller ownerReference, the first
+  // ReplicationController / ReplicaSet controller, spec.topologySpreadConstraints
+  std::vector<std::string> images;
+  int32_t containers = 0;
+  std::vector<std::pair<std::string, int64_t>> ext;
+  bool has_owner = false;
+  std::string owner_api, owner_kind, owner_name, owner_uid;
+  bool has_avoid = false;
+  std::string avoid_kind, avoid_uid;
+  struct SpreadP {
+    std::string key;
+    int64_t max_skew = 1;
+    int when = 0;                   // 0 DoNotSchedule, 1 ScheduleAnyway, 2 another value (in neither list)
+    bool has_sel = false;           // false: nil labelSelector (matches nothing)
+    std::vector<KV> labels;
+    std::vector<SelReqP> exprs;
+  };
+  std::vector<SpreadP> spread;
 };
 
 // Quantity → ceil(q × 10^scale) with exact decimal arithmetic (scale 3: CPU millicores,

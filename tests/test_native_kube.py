@@ -96,9 +96,12 @@ _term = st.fixed_dictionaries({}, optional={
                                                     "operator": st.just("In"),
                                                     "values": st.lists(st.just("n1"), max_size=1)}), max_size=1)})
 _container = st.fixed_dictionaries({"name": st.just("c")}, optional={
+    "image": st.sampled_from(["rocm/pytorch", "rocm/pytorch:7.0", "registry:5000/x", "img@sha256:ab", ""]),
     "resources": st.fixed_dictionaries({}, optional={"requests": st.fixed_dictionaries({}, optional={
         "cpu": st.sampled_from(["100m", "1", "0.5", "2500m", 2]),
-        "memory": st.sampled_from(["128Mi", "1Gi", "1e3", "512", "1.5Gi"])})}),
+        "memory": st.sampled_from(["128Mi", "1Gi", "1e3", "512", "1.5Gi"]),
+        "ephemeral-storage": st.sampled_from(["1Gi", "0", "500M"]),
+        "amd.com/gpu": st.sampled_from(["1", "8", 2])})}),
     "ports": st.lists(st.fixed_dictionaries({"containerPort": st.just(80)}, optional={
         "hostPort": st.sampled_from([0, 8080]), "protocol": st.sampled_from(["TCP", "UDP"]),
         "hostIP": st.just("0.0.0.0")}), max_size=2)})
@@ -125,7 +128,13 @@ _spec = st.fixed_dictionaries({"containers": st.lists(_container, min_size=1, ma
                                                                        max_size=1)}),
         "podAffinity": st.fixed_dictionaries({}, optional={
             "preferredDuringSchedulingIgnoredDuringExecution": st.lists(st.just({"weight": 1}), max_size=1)})}),
-    "topologySpreadConstraints": st.lists(st.just({"maxSkew": 1, "topologyKey": "zone"}), max_size=1),
+    "topologySpreadConstraints": st.lists(st.fixed_dictionaries({"topologyKey": st.sampled_from(["zone", "h"])}, optional={
+        "maxSkew": st.integers(1, 3), "whenUnsatisfiable": st.sampled_from(["DoNotSchedule", "ScheduleAnyway"]),
+        "labelSelector": st.one_of(st.none(), st.fixed_dictionaries({}, optional={
+            "matchLabels": st.dictionaries(st.sampled_from(["app", "tier"]), st.sampled_from(["a", "b"]), max_size=2),
+            "matchExpressions": st.lists(st.fixed_dictionaries({
+                "key": st.sampled_from(["app", "tier"]), "operator": st.sampled_from(["In", "NotIn", "Exists"]),
+                "values": st.lists(st.sampled_from(["a", "b"]), max_size=2)}), max_size=2)}))}), max_size=2),
     "volumes": st.lists(st.sampled_from([{"name": "v", "persistentVolumeClaim": {"claimName": "c"}},
                                          {"name": "e", "emptyDir": {}}, {"name": "d", "rbd": {}},
                                          {"name": "g", "ephemeral": {}}]), max_size=2)})
@@ -135,14 +144,19 @@ _pod = st.fixed_dictionaries({
         "labels": _labels, "annotations": st.dictionaries(st.sampled_from(["a", "scv.amd.com/gpus"]),
                                                           st.sampled_from(["0,1", "x"]), max_size=2),
         "creationTimestamp": st.just("2026-01-01T00:00:00Z"),
-        "ownerReferences": st.lists(st.fixed_dictionaries({"kind": st.sampled_from(["ReplicaSet", "Job"]),
+        "ownerReferences": st.lists(st.fixed_dictionaries({"kind": st.sampled_from(["ReplicaSet", "Job",
+                                                                                     "ReplicationController"]),
                                                            "name": st.just("o")},
-                                                          optional={"controller": st.booleans()}), max_size=2)}),
+                                                          optional={"controller": st.booleans(),
+                                                                    "apiVersion": st.sampled_from(["apps/v1", "v1"]),
+                                                                    "uid": st.sampled_from(["o-1", "o-2"])}),
+                                    max_size=2),
+        "deletionTimestamp": st.sampled_from([None, "2026-01-01T00:00:00Z"])}),
     "spec": _spec})
 
 _FIELDS = ("uid", "namespace", "name", "labels", "gpu", "scheduler_name", "node_name", "cpu_m", "mem", "priority",
            "node_selector", "required_terms", "preferred_terms", "tolerations", "annotations", "host_ports", "flags",
-           "ext", "nz_cpu_m", "nz_mem")
+           "ext", "nz_cpu_m", "nz_mem", "images", "containers", "owner", "avoid", "spread", "deleting")
 
 
 def _norm(v):
@@ -240,13 +254,16 @@ def test_projection_hash_ignores_volatile_metadata_and_status():
     assert K.project(json.dumps(relabel)).hash != h0
 
 
-def test_projection_falls_back_for_extended_resources():
+def test_projection_covers_extended_resources():
+    """Extended resources are projected natively (the native NodeResourcesFit reads them), so
+    such pods no longer fall back to a Python decode of the object."""
     pod = {"metadata": {"name": "p"}, "spec": {"containers": [{"name": "c", "resources": {"requests": {
-        "amd.com/gpu": "2", "cpu": "1"}}}]}}
+        "amd.com/gpu": "2", "cpu": "1", "ephemeral-storage": "1Gi"}}}]}}
     ev = K.project(json.dumps(pod))
-    assert not ev.ok and ev.info_args() is None
+    assert ev.ok and ev.info_args() is not None
     pi = PodInfo.from_native(ev)
-    assert pi.ext == {"amd.com/gpu": 2} and pi.cpu_m == 1000
+    assert pi.ext == {"amd.com/gpu": 2, "ephemeral-storage": 1 << 30} and pi.cpu_m == 1000
+    assert pi.flags & 64                                 # PF_EXTENDED
 
 
 # ============================================================== native fake apiserver

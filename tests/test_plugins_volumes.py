@@ -255,7 +255,9 @@ def test_image_locality_and_prefer_avoid_pods():
     img, rs, native_plain, native_owned = run(go())
     assert img == "n2"                 # the only node holding the image
     assert rs == "n1"                  # the only node not avoiding the ReplicaSet
-    assert native_plain and not native_owned
+    # both score natively now (engine S_IMAGE_LOCALITY / S_PREFER_AVOID): neither the image on
+    # n2 nor the ReplicaSet owner moves a pod off the native cycle
+    assert native_plain and native_owned
 
 
 def test_volume_plugins_keep_plain_pods_native():
@@ -273,7 +275,8 @@ def test_volume_plugins_keep_plain_pods_native():
         await c.stop()
         return names, fw.native_for(plain), fw.native_for(with_pvc), informers
     names, plain, with_pvc, informers = run(go())
-    assert {"VolumeBinding", "VolumeZone", "VolumeRestrictions", "NodeVolumeLimits", "ImageLocality"} <= names
+    assert {"VolumeBinding", "VolumeZone", "VolumeRestrictions", "NodeVolumeLimits"} <= names
+    assert "ImageLocality" not in names and "PodTopologySpread" not in names   # native score terms now
     assert plain and not with_pvc
     assert {"persistentvolumeclaims", "persistentvolumes", "storageclasses", "csinodes"} <= informers
 

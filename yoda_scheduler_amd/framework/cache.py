@@ -309,7 +309,16 @@ class SchedulerCache:
         elif same_spec:
             ps.info.set_source(ev)         # status-only update (kubelet): nothing to re-parse
         else:
-            ps.info = PodInfo.from_native(ev)
+            self._replace_info(ps, PodInfo.from_native(ev))
+
+    def _replace_info(self, ps: PodState, pi: PodInfo) -> None:
+        """A bound pod's spec / metadata changed: keep its ledger id, and let the engine's copy
+        of its labels and deletionTimestamp (what spread constraints count) follow."""
+        old = ps.info
+        pi.num_id = old.num_id
+        ps.info = pi
+        if not ps.lane and (pi.labels != old.labels or pi.deleting != old.deleting):
+            self.engine.set_pod_meta(pi.num_id, list(pi.labels.items()), pi.deleting)
 
     def _add_bound(self, pi: PodInfo) -> None:
         node = pi.node_name
@@ -337,7 +346,7 @@ class SchedulerCache:
         if ps is None or ps.node != pi.node_name:
             self.add_pod(obj)
         else:
-            ps.info = pi
+            self._replace_info(ps, pi)
 
     def remove_pod(self, uid: str) -> None:
         ps = self.pods.pop(uid, None)

@@ -101,8 +101,9 @@ class NativeLane:
         if s.extenders or self.sort_kind < 0 or not fw.fully_native_static or not fw.post_bind_noop:
             return None
         m = fw.native_mask(lane=True)
-        if m is None:
+        if m is None or fw.lane_flags is None:
             return None
+        m |= fw.lane_flags
         if len(fw.bind_plugins) != 1 or not getattr(fw.bind_plugins[0], "native_bind", False):
             return None
         bm = fw.direct_bind_mask()
@@ -301,9 +302,9 @@ class NativeLane:
             # retries from backoff rather than parking in unschedulableQ (never lose a wake-up)
             if fw.post_filter:
                 with self.held():             # preemption reads other pods and what-ifs the ledger
-                    s._fail(fw, None, pi, -1, s._fit_error(res), t_cycle)
+                    s._fail(fw, None, pi, -1, s._fit_error(res, pi), t_cycle)
             else:
-                s._fail(fw, None, pi, -1, s._fit_error(res), t_cycle)
+                s._fail(fw, None, pi, -1, s._fit_error(res, pi), t_cycle)
             return
         from ..kube.native import api_error
         if status == 401:

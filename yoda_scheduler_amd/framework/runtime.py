@@ -20,7 +20,6 @@ from .registry import Registry
 
 log = logging.getLogger("yoda.framework")
 
-S_SLOTS = 6
 
 
 class Framework:
@@ -57,8 +56,9 @@ class Framework:
             raise ValueError(f"profile {self.name}: at least one bind plugin required")
 
         # native split
+        from ..ops.native import core
         self.filter_mask = 0
-        self.score_w = [0] * S_SLOTS
+        self.score_w = [0] * core().S_NUM
         self.filter_py: list[FilterPlugin] = []
         self.score_py: list[tuple[ScorePlugin, int]] = []
         for p, _ in self.points["filter"]:
@@ -108,6 +108,22 @@ class Framework:
         self._term_gates = [p for p in self.conditional if hasattr(p, "gate_terms")]
         self._plain_gates = [p.cluster_active for p in self.conditional
                              if hasattr(p, "cluster_active") and not hasattr(p, "gate_terms")]
+        # native plugins that still keep some pods off the native lane (``lane_flags``: pod
+        # flags, or None: no lane for this profile) and that declare gate terms for a Python
+        # cycle running beside the lane (PodTopologySpread's hard constraints)
+        native_plugins = {id(p): p for p, _ in self.points["filter"] + self.points["score"]
+                          if p.native() is not None}.values()
+        self.lane_flags: Optional[int] = 0
+        for p in native_plugins:
+            lf = getattr(p, "lane_flags", 0)
+            if lf is None:
+                self.lane_flags = None
+                break
+            self.lane_flags |= lf
+        self._native_gaters = [p for p in native_plugins if hasattr(p, "own_gate_terms")]
+        spread = self.plugins.get("PodTopologySpread")
+        self._spread_defaults = spread.engine_defaults() if spread is not None and hasattr(spread, "engine_defaults") \
+            else []
 
     def native_mask(self, lane: bool = False) -> Optional[int]:
         """For a batch of pods: the pod-flag mask such that ``native_for(pod)`` is exactly
@@ -132,6 +148,8 @@ class Framework:
         other pods or declare the pods it is sensitive to (``own_gate_terms``). None when a
         plugin cannot say (the lane must be parked for the whole cycle)."""
         out: list = []
+        for p in self._native_gaters:
+            out.extend(p.own_gate_terms(pod))
         for p in self._act(self._py_points(), pod):
             f = getattr(p, "own_gate_terms", None)
             if f is not None:
@@ -264,6 +282,10 @@ class Framework:
         for most, name in ((False, "NodeResourcesLeastAllocated"), (True, "NodeResourcesMostAllocated")):
             p = self.plugins.get(name)
             engine.set_alloc_weights(most, *(p.alloc_weights() if p is not None else (1, 1, 0)))
+        engine.set_spread_defaults(self._spread_defaults)
+        fit = self.plugins.get("NodeResourcesFit")
+        engine.set_ext_ignored(*(fit.engine_ignored() if fit is not None and hasattr(fit, "engine_ignored")
+                                 else ([], [])))
         if self.yoda is not None:
             self.yoda.configure_engine(engine)
 

@@ -57,6 +57,40 @@ def _pod_updated(old: dict, new: dict) -> bool:
     return om != nm
 
 
+def ext_text(ext) -> str:
+    """FitError text of the native extended-resource fit (engine ``RS_EXT_RESOURCES``): the
+    pod's requested resources beyond cpu/memory, as upstream's "Insufficient <resource>"."""
+    return "Insufficient " + ("/".join(sorted(ext)) if ext else "extended resources")
+
+
+SPREAD_SOURCES = ("services", "replicationcontrollers", "replicasets", "statefulsets")
+
+
+def push_spread_source(engine, res: str, obj: dict, deleted: bool) -> None:
+    """One DefaultSelector source object into the engine (``Engine.set_service`` /
+    ``set_controller``): a Service's map selector (None = nil, matches nothing), an RC's map
+    selector, a ReplicaSet's / StatefulSet's LabelSelector (plugins/optional.py::default_selector)."""
+    from ..models.selectors import LabelSelector
+    meta = obj.get("metadata") or {}
+    ns, name = meta.get("namespace") or "default", meta.get("name", "")
+    spec = obj.get("spec") or {}
+    if res == "services":
+        if deleted:
+            engine.remove_service(ns, name)
+        else:
+            sel = spec.get("selector")
+            engine.set_service(ns, name, None if sel is None else [(str(k), str(v)) for k, v in sel.items()])
+        return
+    if deleted:
+        engine.remove_controller(res, ns, name)
+        return
+    sel = spec.get("selector")
+    if res == "replicationcontrollers":
+        engine.set_controller(res, ns, name, [(str(k), str(v)) for k, v in (sel or {}).items()])
+    else:
+        engine.set_controller(res, ns, name, None if sel is None else LabelSelector(sel).native())
+
+
 class Handle:
     """``framework.Handle`` analogue handed to plugin factories."""
 
@@ -526,6 +560,14 @@ class Scheduler:
                         if not getattr(p, "inert", False) for r in getattr(p, "watches", ())})
         for res in extra:
             ev = f"{res}Change"
+            if res in SPREAD_SOURCES:
+                # DefaultSelector sources: the engine keeps them (native PodTopologySpread)
+                self.informers[res] = Informer(
+                    self.client, res,
+                    lambda o, ev=ev, res=res: self._spread_source(res, o, False, ev),
+                    lambda a, b, ev=ev, res=res: self._spread_source(res, b, False, ev),
+                    lambda o, ev=ev, res=res: self._spread_source(res, o, True, None))
+                continue
             self.informers[res] = Informer(self.client, res,
                                            lambda o, ev=ev: self._extra_event(ev),
                                            lambda a, b, ev=ev: self._extra_event(ev),
@@ -534,7 +576,16 @@ class Scheduler:
 
     def _extra_event(self, ev: str) -> None:
         self.queue.move_all_to_active_or_backoff(ev)
-        self._lane_refresh()                      # e.g. the first Service turns a spread gate on
+        self._lane_refresh()
+
+    def _spread_source(self, res: str, obj: dict, deleted: bool, ev: Optional[str]) -> None:
+        """A Service / RC / ReplicaSet / StatefulSet changed: the engine's DefaultSelector
+        sources follow (upstream helper.DefaultSelector reads them through listers)."""
+        push_spread_source(self.engine, res, obj, deleted)
+        if ev is not None:
+            self._extra_event(ev)
+        else:
+            self._lane_refresh()
 
     def _make_lane(self):
         """The native pod lane when the transport is native and ``yodaRuntime.nativeLane``
@@ -692,7 +743,7 @@ class Scheduler:
                 self._fail(fw, state, pi, cycle, "the selected node was removed during the cycle", t0,
                            unschedulable=False)
                 return
-            msg = self._fit_error(res)
+            msg = self._fit_error(res, pi)
             self._fail(fw, state, pi, cycle, msg, t0)
             return
         node, gen = self._node_name(node_idx)
@@ -760,7 +811,7 @@ class Scheduler:
         self.recorder.pod_event(pi, "Warning", "FailedScheduling", st.message())
         self.queue.add_unschedulable(pi, cycle, unschedulable=True)
 
-    def _fit_error(self, res) -> str:
+    def _fit_error(self, res, pi: Optional[PodInfo] = None) -> str:
         reasons = res[5]
         names = core().REASONS
         text = {"NodeUnschedulable": "node(s) were unschedulable", "NodeName": "node(s) didn't match the requested node name",
@@ -769,7 +820,10 @@ class Scheduler:
                 "NoScv": "node(s) have no Scv telemetry", "ScvStale": "node(s) have stale Scv telemetry",
                 "GpuNumber": "node(s) have too few GPUs", "GpuMemory": "node(s) have too few GPUs with enough free HBM",
                 "GpuClock": "node(s) have too few GPUs with the requested clock",
-                "GpuFit": "node(s) have too few healthy GPUs matching scv/memory+scv/clock"}
+                "GpuFit": "node(s) have too few healthy GPUs matching scv/memory+scv/clock",
+                "NodeResourcesFitExtended": ext_text(pi.ext if pi is not None else None),
+                "PodTopologySpread": "node(s) didn't match pod topology spread constraints",
+                "PodTopologySpreadLabel": "node(s) didn't match pod topology spread constraints (missing required label)"}
         parts = [f"{c} {text.get(names[i], names[i])}" for i, c in enumerate(reasons) if c and i]
         if len(res) > 10 and res[10]:
             by_msg: dict[str, int] = {}

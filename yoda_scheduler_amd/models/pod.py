@@ -142,6 +142,7 @@ PF_CONTROLLER = 32     # controlled by a ReplicationController / ReplicaSet / St
 PF_EXTENDED = 64       # requests resources beyond cpu/memory (amd.com/gpu, ephemeral-storage, ...)
 PF_POD_GROUP = 128     # member of a co-scheduled pod group (Coscheduling)
 PF_REQ_ANTI = 256      # required pod anti-affinity (other pods' symmetry check)
+PF_SPREAD_HARD = 512   # a DoNotSchedule topologySpreadConstraint
 LABEL_POD_GROUP = "pod-group.scheduling.sigs.k8s.io"
 LABEL_POD_GROUP_MIN = "pod-group.scheduling.sigs.k8s.io/min-available"
 
@@ -152,8 +153,11 @@ def pod_flags(meta: dict, spec: dict, host_ports, ext: Optional[dict] = None) ->
     f = PF_HOST_PORTS if host_ports else 0
     if ext:
         f |= PF_EXTENDED
-    if spec.get("topologySpreadConstraints"):
+    tsc = spec.get("topologySpreadConstraints")
+    if tsc:
         f |= PF_SPREAD
+        if any(isinstance(c, dict) and c.get("whenUnsatisfiable", "DoNotSchedule") == "DoNotSchedule" for c in tsc):
+            f |= PF_SPREAD_HARD
     aff = spec.get("affinity")
     if aff and (aff.get("podAffinity") or aff.get("podAntiAffinity")):
         f |= PF_POD_AFFINITY
@@ -184,15 +188,30 @@ class PodInfo:
     __slots__ = ("_obj", "_src", "uid", "namespace", "name", "num_id", "labels", "gpu", "scheduler_name", "node_name",
                  "cpu_m", "mem", "priority", "node_selector", "required_terms", "preferred_terms", "tolerations",
                  "annotations", "host_ports", "attempts", "initial_attempt", "enqueued", "native_req",
-                 "native_owner", "assigned_cards", "_creation", "flags", "ext", "nz_cpu_m", "nz_mem", "applies_memo")
+                 "native_owner", "assigned_cards", "_creation", "flags", "ext", "nz_cpu_m", "nz_mem", "applies_memo",
+                 "images", "containers", "owner", "avoid", "spread", "deleting")
 
     def __init__(self, obj: dict, uid: str, namespace: str, name: str, num_id: int, labels: dict, gpu: GpuRequest,
                  scheduler_name: str = "default-scheduler", node_name: str = "", cpu_m: int = 0, mem: int = 0,
                  priority: int = 0, node_selector: Optional[dict] = None, required_terms: Optional[list] = None,
                  preferred_terms: Optional[list] = None, tolerations: Optional[list] = None,
                  annotations: Optional[dict] = None, host_ports: Optional[list] = None, flags: int = 0,
-                 ext: Optional[dict] = None, nz_cpu_m: int = -1, nz_mem: int = -1) -> None:
+                 ext: Optional[dict] = None, nz_cpu_m: int = -1, nz_mem: int = -1,
+                 images: Optional[list] = None, containers: int = 0, owner: Optional[tuple] = None,
+                 avoid: Optional[tuple] = None, spread: Optional[list] = None, deleting: bool = False) -> None:
         self._obj = obj
+        # default-plugin inputs the native engine reads (ops/native.py::pod_req): normalized
+        # images of spec.containers + their count (ImageLocality), the first controller
+        # ownerReference (apiVersion, kind, name, uid) (DefaultSelector), the first RC / RS
+        # controller (kind, uid) (NodePreferAvoidPods), the topology spread constraints as
+        # (topologyKey, maxSkew, whenUnsatisfiable, LabelSelector.native() | None), and whether
+        # the pod is terminating (other pods' spread counts skip it)
+        self.images = images if images is not None else _NOLIST
+        self.containers = containers
+        self.owner = owner
+        self.avoid = avoid
+        self.spread = spread
+        self.deleting = deleting
         self._src = None
         # -1: a single container's non-zero request derived from cpu_m / mem
         self.nz_cpu_m = nz_cpu_m if nz_cpu_m >= 0 else (cpu_m or DEFAULT_MILLI_CPU_REQUEST)
@@ -262,9 +281,10 @@ class PodInfo:
             pi = cls.from_obj(json.loads(ev.raw()))
             return pi
         (uid, ns, name, labels, ann, sched, node, cpu, mem, nzc, nzm, prio, nsel, req, pref, tols, ports,
-         flags, _creation) = a
+         flags, _creation, ext, images, containers, owner, avoid, spread, deleting) = a
         pi = cls(None, uid, ns, name, pod_num_id(uid), labels, parse_gpu_request(labels), sched, node, cpu, mem,
-                 prio, nsel, req, pref, tols, ann, ports, flags, None, nzc, nzm)
+                 prio, nsel, req, pref, tols, ann, ports, flags, ext, nzc, nzm, images, containers, owner, avoid,
+                 spread, deleting)
         pi._src = ev
         return pi
 
@@ -297,14 +317,34 @@ class PodInfo:
         ns = spec.get("nodeSelector")
         ann = meta.get("annotations")
         ext = ext_requests(spec) if _has_ext(spec) else None
+        containers = spec.get("containers") or ()
+        images = [normalize_image(c.get("image")) for c in containers if c.get("image")]
+        owner = avoid = None
+        for r in meta.get("ownerReferences") or ():
+            if not r.get("controller"):
+                continue
+            if owner is None:
+                owner = (r.get("apiVersion", "") or "", r.get("kind", "") or "", r.get("name", "") or "",
+                         r.get("uid", "") or "")
+            if avoid is None and r.get("kind") in ("ReplicationController", "ReplicaSet"):
+                avoid = (r.get("kind"), r.get("uid", "") or "")
+        spread = None
+        tsc = spec.get("topologySpreadConstraints")
+        if tsc:
+            from .selectors import LabelSelector
+            spread = [(c.get("topologyKey", ""), int(c.get("maxSkew", 1)), c.get("whenUnsatisfiable", "DoNotSchedule"),
+                       None if c.get("labelSelector") is None else LabelSelector(c.get("labelSelector")).native())
+                      for c in tsc]
         return cls(obj, uid, meta.get("namespace", "default"), meta.get("name", ""), pod_num_id(uid), labels,
                    parse_gpu_request(labels), spec.get("schedulerName") or "default-scheduler",
                    spec.get("nodeName") or "", cpu, mem, int(spec.get("priority") or 0),
                    dict(ns) if ns else None, req, pref, tols or None, dict(ann) if ann else None, ports,
-                   pod_flags(meta, spec, ports, ext), ext, nzc, nzm)
+                   pod_flags(meta, spec, ports, ext), ext, nzc, nzm, images, len(containers), owner, avoid, spread,
+                   bool(meta.get("deletionTimestamp")))
 
 
 _EMPTY: dict = {}
+_NOLIST: list = []
 
 
 @dataclass

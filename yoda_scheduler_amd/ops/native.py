@@ -182,7 +182,30 @@ def push_node(engine, info: NodeInfo) -> int:
     idx = engine.upsert_node(info.name)
     engine.set_node_meta(idx, info.unschedulable, list(info.labels.items()), list(info.taints),
                          info.cpu_m, info.mem, info.pods)
+    if info.images or info.ext_alloc or info.avoid:
+        engine.set_node_extras(idx, list(info.images.items()), list(info.ext_alloc.items()), avoid_controllers(info.avoid))
+    else:
+        engine.set_node_extras(idx, [], [], [])
     return idx
+
+
+def avoid_controllers(raw) -> list:
+    """(kind, uid) of every ``podSignature.podController`` in a node's
+    ``scheduler.alpha.kubernetes.io/preferAvoidPods`` annotation (plugins/node_extras.py
+    NodePreferAvoidPods reads the same); an unparsable annotation avoids nothing."""
+    if not raw:
+        return []
+    import json
+    try:
+        items = json.loads(raw).get("preferAvoidPods") or []
+    except (ValueError, AttributeError):
+        return []
+    out = []
+    for a in items:
+        pc = ((a.get("podSignature") or {}).get("podController")) or {} if isinstance(a, dict) else {}
+        if pc.get("kind") in ("ReplicationController", "ReplicaSet"):
+            out.append((pc["kind"], str(pc.get("uid") or "")))
+    return out
 
 
 def pod_req(engine, pi: PodInfo):
@@ -194,5 +217,7 @@ def pod_req(engine, pi: PodInfo):
                         g.clock_min, g.priority, pi.node_name, pi.cpu_m, pi.mem,
                         list(pi.node_selector.items()), pi.required_terms, pi.preferred_terms,
                         pi.tolerations, pi.nz_cpu_m, pi.nz_mem)
+    engine.set_req_extras(r, pi.namespace, list(pi.labels.items()), pi.deleting, pi.images, pi.containers,
+                          list(pi.ext.items()), pi.owner, pi.avoid, pi.spread)
     pi.native_req, pi.native_owner = r, engine
     return r

@@ -17,7 +17,7 @@ from typing import Optional
 from ..framework.interfaces import (BindPlugin, CycleState, FilterPlugin, NativeBinding, Plugin,
                                     PostFilterPlugin, PostFilterResult, QueueSortPlugin, ScorePlugin, Status)
 from ..models.labels import ANNOTATION_GPU_UUIDS, ANNOTATION_GPUS, ANNOTATION_RESERVED, ANNOTATION_VISIBLE
-from ..models.pod import PF_EXTENDED, PF_HOST_PORTS
+from ..models.pod import PF_HOST_PORTS
 from ..models.scv import LazyScv, card_vis
 from ..ops.native import core
 
@@ -49,15 +49,15 @@ class NodeName(FilterPlugin):
 
 
 class NodeResourcesFit(FilterPlugin):
-    """cpu / memory / pod count natively; everything else a pod requests (``amd.com/gpu``
+    """Natively: cpu / memory / pod count and everything else a pod requests (``amd.com/gpu``
     from the AMD device plugin, ``ephemeral-storage``, hugepages, other extended resources)
-    in Python against the node's allocatable and the cache's per-node usage — only for
-    pods that request such resources (``PF_EXTENDED``). ``ignoredResources`` /
-    ``ignoredResourceGroups`` args as upstream."""
+    against the node's allocatable and the engine ledger's per-node usage
+    (``native/core/engine.cpp`` ``RS_EXT_RESOURCES``), so ``PF_EXTENDED`` pods stay on the
+    native cycle and the native lane. ``ignoredResources`` / ``ignoredResourceGroups`` args as
+    upstream (``Engine.set_ext_ignored``). ``filter`` below is the executable spec of the
+    extended-resource check (``tests/test_native_default_plugins.py``)."""
     name = "NodeResourcesFit"
-    python_filter_too = True
-    pod_flags = PF_EXTENDED
-    reads_flags = PF_EXTENDED  # other pods' features this plugin reads (needs_lane_mirror)
+    reads_flags = 0  # other pods' features this plugin reads (needs_lane_mirror)
 
     def __init__(self, args: Optional[dict] = None, handle=None) -> None:
         super().__init__(args, handle)
@@ -70,8 +70,8 @@ class NodeResourcesFit(FilterPlugin):
     def _checked(self, res: str) -> bool:
         return res not in self.ignored and res.split("/", 1)[0] not in self.ignored_groups
 
-    def is_noop_for(self, pod) -> bool:
-        return not pod.ext
+    def engine_ignored(self) -> tuple[list, list]:
+        return sorted(self.ignored), sorted(self.ignored_groups)
 
     def filter(self, state: CycleState, pod, node_name: str) -> Status:
         cache = self.handle.cache

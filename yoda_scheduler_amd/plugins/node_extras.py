@@ -1,18 +1,22 @@
-"""``ImageLocality`` and ``NodePreferAvoidPods`` — the two remaining score plugins of the
-upstream v1.20 default profile that the reference's scheduler runs next to
-``yoda`` (weights 1 and 10000).
+"""``ImageLocality`` and ``NodePreferAvoidPods`` — two score plugins of the upstream v1.20
+default profile that the reference's scheduler runs next to ``yoda`` in the same
+compiled cycle (weights 1 and 10000; ``/root/reference/deploy/yoda-scheduler.yaml:21-31`` keeps
+the defaults, ``/root/reference/pkg/yoda/scheduler.go:76-130`` is the cycle they share).
 
-Both are no-ops for the common case and keep pods on the native cycle: ImageLocality
-when no node reports any of the pod's images (every node would score 0), and
-NodePreferAvoidPods when the pod has no ReplicationController/ReplicaSet owner or no
-node carries the annotation (every node would score 100).
+Both score natively (``native/core/engine.cpp`` ``S_IMAGE_LOCALITY`` / ``S_PREFER_AVOID``): the
+engine keeps every node's ``status.images``, the per-image node count and the preferAvoidPods
+controllers, and each pod's normalized images and RC / RS controller, so a real cluster —
+every kubelet reports its images — keeps its pods on the native cycle and the native lane.
+The Python ``score`` methods below are the executable spec the native terms are pinned
+against (``tests/test_native_default_plugins.py``).
 """
 from __future__ import annotations
 
 import json
 
-from ..framework.interfaces import CycleState, ScorePlugin, Status, MAX_NODE_SCORE
-from ..models.pod import PF_CONTROLLER, normalize_image
+from ..framework.interfaces import CycleState, NativeBinding, ScorePlugin, Status, MAX_NODE_SCORE
+from ..models.pod import normalize_image
+from ..ops.native import core
 
 MB = 1024 * 1024
 MIN_THRESHOLD = 23 * MB           # upstream: below this an image is "not there"
@@ -28,15 +32,10 @@ class ImageLocality(ScorePlugin):
     """score = 100·(clamp(Σ size·spread) − 23MB)/(1000MB·#containers − 23MB), where
     spread = (#nodes holding the image)/(#nodes) damps images present everywhere."""
     name = "ImageLocality"
-    pod_flags = 0
     reads_flags = 0  # other pods' features this plugin reads (needs_lane_mirror)
 
-    def cluster_active(self) -> bool:
-        return bool(self.handle.cache.image_nodes)
-
-    def is_noop_for(self, pod) -> bool:
-        have = self.handle.cache.image_nodes
-        return not have or not any(im in have for im in _images(pod))
+    def native(self):
+        return NativeBinding(score_index=core().S_IMAGE_LOCALITY)
 
     def score(self, state: CycleState, pod, node_name: str) -> tuple[int, Status]:
         cache = self.handle.cache
@@ -66,11 +65,10 @@ class NodePreferAvoidPods(ScorePlugin):
     """0 on nodes whose ``scheduler.alpha.kubernetes.io/preferAvoidPods`` annotation names
     the pod's controller, 100 elsewhere."""
     name = "NodePreferAvoidPods"
-    pod_flags = PF_CONTROLLER
     reads_flags = 0  # other pods' features this plugin reads (needs_lane_mirror)
 
-    def is_noop_for(self, pod) -> bool:
-        return not self.handle.cache.avoid_nodes or _controller(pod) is None
+    def native(self):
+        return NativeBinding(score_index=core().S_PREFER_AVOID)
 
     def score(self, state: CycleState, pod, node_name: str) -> tuple[int, Status]:
         node = self.handle.cache.nodes.get(node_name)

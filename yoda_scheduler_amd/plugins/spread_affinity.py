@@ -1,12 +1,20 @@
 """PodTopologySpread and InterPodAffinity (upstream default plugins the reference's profile
-keeps), in Python.
+keeps).
 
-Both only matter for pods that declare topology spread constraints / pod (anti)affinity,
-or match a bound pod's required anti-affinity term (the symmetric rule); for every other pod
-``is_noop_for`` is true and the pod stays on the native fast path. Counting is done once per
-cycle in PreFilter over the cache's bound + assumed pods: the Python-owned ones walked here,
-the native lane's counted in C++ (``SchedulerCache.lane_counts``: per node, the lane pods
-matching a selector), so neither plugin needs a Python copy of the lane's pods.
+PodTopologySpread runs natively (``native/core/engine.cpp``: ``F_SPREAD`` filter, ``S_SPREAD``
+score): the engine ledger keeps every reserved pod's namespace, labels and terminating flag, the
+engine holds the DefaultSelector sources (Services, RCs, ReplicaSets, StatefulSets), and each
+pod's explicit constraints travel in its request — so the System default constraints a real
+cluster applies to every Service-selected or controller-owned pod no longer move pods off the
+native cycle. The methods below are the executable spec the native code is pinned against
+(``tests/test_native_default_plugins.py``).
+
+InterPodAffinity only matters for pods that declare pod (anti)affinity, or match a bound pod's
+required anti-affinity term (the symmetric rule); for every other pod ``is_noop_for`` is true
+and the pod stays on the native fast path. Counting is done once per cycle in PreFilter over the
+cache's bound + assumed pods: the Python-owned ones walked here, the native lane's counted in C++
+(``SchedulerCache.lane_counts``: per node, the lane pods matching a selector), so it needs no
+Python copy of the lane's pods.
 """
 from __future__ import annotations
 
@@ -14,9 +22,10 @@ import math
 from collections import defaultdict
 from typing import Optional
 
-from ..framework.interfaces import (CycleState, FilterPlugin, NodeScore, PreFilterPlugin, PreScorePlugin, ScorePlugin,
-                                    StateData, Status, MAX_NODE_SCORE)
-from ..models.pod import PF_CONTROLLER, PF_POD_AFFINITY, PF_SPREAD
+from ..framework.interfaces import (CycleState, FilterPlugin, NativeBinding, NodeScore, PreFilterPlugin,
+                                    PreScorePlugin, ScorePlugin, StateData, Status, MAX_NODE_SCORE)
+from ..models.pod import PF_POD_AFFINITY, PF_SPREAD_HARD
+from ..ops.native import core
 from ..models.selectors import LabelSelector, NodeSelector
 from .optional import default_selector
 
@@ -132,11 +141,28 @@ class PodTopologySpread(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlug
     KEY = "PreFilterPodTopologySpread"
     SCORE_KEY = "PreScorePodTopologySpread"
     watches = ("services", "replicationcontrollers", "replicasets", "statefulsets")
-
-    pod_flags = PF_SPREAD | PF_CONTROLLER
     # other pods read: their labels only, counted per node (the lane's natively) — no Python
     # copy of the lane's pods is needed (framework.runtime.Framework.needs_lane_mirror)
     reads_flags = 0
+
+    def native(self):
+        return NativeBinding(filter_bit=core().F_SPREAD, score_index=core().S_SPREAD)
+
+    @property
+    def lane_flags(self):
+        """Pods with these flags stay off the native lane (None: the lane cannot run the
+        profile). A DoNotSchedule constraint's skew must see every pod its selector matches
+        that is placed before it, and a Python-path cycle may assume such a pod between the
+        lane's count and its assume; pods whose constraints are all ScheduleAnyway only score
+        from the counts, so they are lane pods (and so is everything else)."""
+        if any(c.get("whenUnsatisfiable") == "DoNotSchedule" for c in self.default_constraints):
+            return None
+        return PF_SPREAD_HARD
+
+    def engine_defaults(self) -> list:
+        """The default constraints as the engine takes them (``Engine.set_spread_defaults``)."""
+        return [(c.get("topologyKey", ""), int(c.get("maxSkew", 1)), c.get("whenUnsatisfiable", "DoNotSchedule"))
+                for c in self.default_constraints]
 
     def __init__(self, args: Optional[dict] = None, handle=None) -> None:
         super().__init__(args, handle)
@@ -154,11 +180,6 @@ class PodTopologySpread(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlug
                 raise ValueError(f"PodTopologySpread: invalid default constraint {c!r}")
         self.defaulting_type = dtype
         self.default_constraints = list(SYSTEM_DEFAULT_CONSTRAINTS) if dtype == "System" else listed
-
-    def cluster_active(self) -> bool:
-        """Default constraints apply to pods selected by a Service (controller-owned pods
-        carry ``PF_CONTROLLER``)."""
-        return bool(self.default_constraints) and bool(self.handle.lister("services"))
 
     def is_noop_for(self, pod) -> bool:
         if _spec(pod).get("topologySpreadConstraints"):
