@@ -162,6 +162,10 @@ def main(argv=None) -> int:
                     help="GPUs per synthetic node (BASELINE protocol item 5); default: the config's own")
     ap.add_argument("--nodes", type=int, default=None,
                     help="config 6 only: cluster size (default 4096; the CPU/device crossover end to end)")
+    ap.add_argument("--cluster", choices=["synthetic", "kind"], default="synthetic",
+                    help="kind: nodes report 50 images + ephemeral-storage, the cluster has the kubernetes / kube-dns "
+                         "Services, 30%% of pods belong to a Service-selected ReplicaSet, 20%% request "
+                         "ephemeral-storage (bench/workloads.py)")
     ap.add_argument("--mix-anti", type=int, default=0,
                     help="beyond BASELINE: replace this many pods of the burst (evenly spread) with pods that carry "
                          "required pod anti-affinity (Python-path pods reading other pods, lane pods included)")
@@ -246,7 +250,8 @@ def main(argv=None) -> int:
 
     from yoda_scheduler_amd.bench.harness import HttpShard, Shard, percentile
     from yoda_scheduler_amd.bench.workloads import make_workload
-    w = make_workload(a.config, seed=rank, node_gpus=a.node_gpus, nodes=a.nodes, mix_anti=a.mix_anti)
+    w = make_workload(a.config, seed=rank, node_gpus=a.node_gpus, nodes=a.nodes, mix_anti=a.mix_anti,
+                      cluster=a.cluster)
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
 

@@ -832,3 +832,39 @@ def test_cli_serves_healthz_on_its_own_bind_address(tmp_path):
     finally:
         proc.terminate()
         proc.wait(timeout=30)
+
+
+def test_kind_cluster_keeps_the_native_lane_on():
+    """in a realistic cluster — every node reports ``status.images`` and
+    allocatable ``ephemeral-storage``, the ``default/kubernetes`` and ``kube-system/kube-dns``
+    Services exist, 30 % of the burst belongs to a Service-selected ReplicaSet and 20 % requests
+    ``ephemeral-storage`` — every profile stays on the native lane and every pod of the burst is
+    placed there: none is forwarded to or handed over to the Python path."""
+    from yoda_scheduler_amd.bench.harness import HttpShard
+    from yoda_scheduler_amd.bench.workloads import make_workload
+
+    async def go():
+        w = make_workload(3, cluster="kind")
+        assert w.cluster == "kind" and any(w.metas.values())
+        assert sum("ephemeral-storage" in str(s) for s in w.specs.values()) >= 100
+        sh = HttpShard(w, events=False)
+        try:
+            await sh.start()
+            s = sh.sched
+            assert s.lane is not None
+            fw = s.frameworks[w.scheduler_name]
+            assert s.lane.eligible_mask(fw) is not None, "the profile left the lane"
+            assert s.cache.image_nodes and s.engine.image_nodes("docker.io/rocm/vllm:v0.6.4") == 1
+            r1 = await sh.burst("a")
+            r2 = await sh.burst("b")
+            st = s.lane.lane.stats()
+            return r1, r2, st, s.lane.handoffs, s.lane.forwarded, None
+        finally:
+            await sh.stop()
+
+    r1, r2, st, handoffs, forwarded, _ = run(go())
+    assert r1.bound == r2.bound == 1000 and r1.unschedulable == r2.unschedulable == 0
+    assert st["admitted"] >= 2000 and st["scheduled"] >= 2000
+    assert handoffs == 0 and st["unschedulable"] == 0
+    # bound pods' echoes of other schedulers aside, nothing of the burst reached Python
+    assert forwarded == 0, forwarded

@@ -91,7 +91,8 @@ class Shard:
         srv, w = self.server, self.w
         srv.reset_logs()
         self.sched.e2e_samples.clear()
-        objs = [pod_object(i, lab, w.scheduler_name, prefix=tag, spec=w.specs.get(i)) for i, lab in enumerate(w.pods)]
+        objs = [pod_object(i, lab, w.scheduler_name, prefix=tag, spec=w.specs.get(i), meta=w.metas.get(i))
+                for i, lab in enumerate(w.pods)]
         t0 = time.perf_counter()
         for i, o in enumerate(objs):
             srv.create("pods", o)
@@ -230,7 +231,8 @@ class HttpShard:
             populate(rec, self.w, self.template, link_load=0.2 if self.w.id == 5 else 0.0, seed=self.seed)
             for res, obj in rec.objs:
                 await self.client.create(res, obj)
-            pods = [pod_object(i, lab, self.w.scheduler_name, prefix="t", spec=self.w.specs.get(i))
+            pods = [pod_object(i, lab, self.w.scheduler_name, prefix="t", spec=self.w.specs.get(i),
+                               meta=self.w.metas.get(i))
                     for i, lab in enumerate(self.w.pods)]
             await self._call("POST", "/debug/bench/load", {"pods": pods})
         self.sched = Scheduler(self.client, self.cfg, metrics=NullMetrics(), record_events=self.events,

@@ -12,6 +12,15 @@ Config 4 mixes MI355X (2400 MHz max sclk) and MI350X (2200 MHz) nodes so the exa
 ``scv/clock`` selector has something to select. Demand is sized
 so every pod fits with per-GPU HBM reservation (≈60-75 % of HBM), i.e. the burst
 measures scheduling, not capacity exhaustion.
+
+``cluster="kind"`` (``bench.py --cluster kind``) makes any config look like the cluster
+BASELINE config 1 names — a kind cluster — instead of the bare synthetic one: every node
+reports 50 preloaded images in ``status.images`` and allocatable ``ephemeral-storage`` /
+hugepages, the cluster has the ``default/kubernetes`` and ``kube-system/kube-dns`` Services,
+30 % of the burst is owned by a ReplicaSet that a Service selects (so the System default
+topology-spread constraints apply to them), 20 % request ``ephemeral-storage`` and 10 % run an
+image the nodes already hold (ImageLocality has something to score). Each of these alone used
+to move pods — or the whole profile — off the native lane.
 """
 from __future__ import annotations
 
@@ -33,6 +42,8 @@ class Workload:
     pods: list[dict] = field(default_factory=list)   # label dicts
     scheduler_name: str = "yoda-scheduler"
     specs: dict = field(default_factory=dict)        # pod index → extra spec fields (e.g. affinity)
+    metas: dict = field(default_factory=dict)        # pod index → extra metadata fields (ownerReferences)
+    cluster: str = "synthetic"                       # "kind": realistic node/cluster objects (populate)
 
     @property
     def n_pods(self) -> int:
@@ -53,12 +64,18 @@ def _mixed_labels(rng: random.Random) -> dict:
 
 
 def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None,
-                  node_gpus: Optional[int] = None, nodes: Optional[int] = None, mix_anti: int = 0) -> Workload:
+                  node_gpus: Optional[int] = None, nodes: Optional[int] = None, mix_anti: int = 0,
+                  cluster: str = "synthetic") -> Workload:
     """``node_gpus`` overrides the GPUs per node (BASELINE.md protocol item 5: every
     config at 1, 2, 4 and 8 GPUs per node); pods keep their labels, so e.g. ``scv/number: 8``
     pods are unschedulable on smaller nodes and are reported as such. ``nodes`` resizes
-    config 6's cluster (beyond BASELINE: the CPU/device crossover end to end)."""
+    config 6's cluster (beyond BASELINE: the CPU/device crossover end to end). ``cluster``
+    "kind" makes the cluster and the burst realistic (module docstring)."""
     w = _make_workload(cfg, seed, template)
+    if cluster == "kind":
+        _kindify(w, seed)
+    elif cluster != "synthetic":
+        raise ValueError(f"unknown cluster kind {cluster!r}")
     if mix_anti:
         # beyond BASELINE: interleave pods with required pod anti-affinity (Python-path plugins
         # that read other pods, lane pods included) — what such pods cost the native lane
@@ -118,10 +135,79 @@ def _make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None) -> 
     return w
 
 
+# ---------------------------------------------------------------- kind cluster (--cluster kind)
+KIND_IMAGES = (
+    # what a kind v1.2x node image preloads, then the usual ROCm / platform images of a GPU pool
+    "registry.k8s.io/pause:3.9", "registry.k8s.io/kube-proxy:v1.29.2", "registry.k8s.io/kube-apiserver:v1.29.2",
+    "registry.k8s.io/kube-controller-manager:v1.29.2", "registry.k8s.io/kube-scheduler:v1.29.2",
+    "registry.k8s.io/etcd:3.5.10-0", "registry.k8s.io/coredns/coredns:v1.11.1",
+    "docker.io/kindest/kindnetd:v20240202-8f1494ea", "docker.io/kindest/local-path-provisioner:v20240202-8f1494ea",
+    "docker.io/kindest/local-path-helper:v20230510-486859a6",
+)
+KIND_HOT_IMAGE = "docker.io/rocm/vllm:v0.6.4"     # preloaded on every node; 10 % of the burst runs it
+KIND_TRAINER = {"app": "trainer"}                 # Service + ReplicaSet selector of 30 % of the burst
+
+
+def kind_node_images(i_node: int) -> list:
+    extra = [f"docker.io/rocm/tool-{k}:v{(i_node + k) % 7}" for k in range(39)]
+    names = list(KIND_IMAGES) + [KIND_HOT_IMAGE] + extra
+    return [{"names": [n, n.split("/", 1)[1] if n.count("/") > 1 else n], "sizeBytes": (40 + 37 * k % 900) << 20}
+            for k, n in enumerate(names)]
+
+
+def _kindify(w: Workload, seed: int) -> None:
+    rng = random.Random(seed * 104729 + w.id)
+    w.cluster = "kind"
+    w.name += " [kind cluster]"
+    for i in range(len(w.pods)):
+        r = rng.random()
+        if r < 0.30:                                   # a ReplicaSet's pods, selected by a Service
+            w.pods[i] = dict(w.pods[i], **KIND_TRAINER)
+            w.metas[i] = {"ownerReferences": [{"apiVersion": "apps/v1", "kind": "ReplicaSet", "name": "trainer-rs",
+                                               "uid": "rs-trainer-0001", "controller": True,
+                                               "blockOwnerDeletion": True}]}
+        req = {"cpu": "100m", "memory": "128Mi"}
+        if rng.random() < 0.20:
+            req["ephemeral-storage"] = "1Gi"
+        image = KIND_HOT_IMAGE if rng.random() < 0.10 else "rocm/pytorch:latest"
+        w.specs[i] = dict(w.specs.get(i) or {}, containers=[{"name": "main", "image": image,
+                                                             "resources": {"requests": req}}])
+
+
+def kind_objects() -> list:
+    """The cluster objects of a kind cluster that the scheduler's plugins watch."""
+    return [
+        ("services", {"apiVersion": "v1", "kind": "Service",
+                      "metadata": {"name": "kubernetes", "namespace": "default"},
+                      "spec": {"clusterIP": "10.96.0.1", "ports": [{"port": 443, "protocol": "TCP"}]}}),
+        ("services", {"apiVersion": "v1", "kind": "Service",
+                      "metadata": {"name": "kube-dns", "namespace": "kube-system"},
+                      "spec": {"selector": {"k8s-app": "kube-dns"}, "clusterIP": "10.96.0.10",
+                               "ports": [{"port": 53, "protocol": "UDP"}]}}),
+        ("services", {"apiVersion": "v1", "kind": "Service",
+                      "metadata": {"name": "trainer", "namespace": "default"},
+                      "spec": {"selector": dict(KIND_TRAINER), "ports": [{"port": 29500, "protocol": "TCP"}]}}),
+        ("replicasets", {"apiVersion": "apps/v1", "kind": "ReplicaSet",
+                         "metadata": {"name": "trainer-rs", "namespace": "default", "uid": "rs-trainer-0001"},
+                         "spec": {"replicas": 300, "selector": {"matchLabels": dict(KIND_TRAINER)},
+                                  "template": {"metadata": {"labels": dict(KIND_TRAINER)}}}}),
+    ]
+
+
+def kindify_node(obj: dict, i_node: int) -> dict:
+    st = obj["status"]
+    for k in ("allocatable", "capacity"):
+        st[k] = dict(st[k], **{"ephemeral-storage": "1800Gi", "hugepages-1Gi": "0", "hugepages-2Mi": "0"})
+    st["images"] = kind_node_images(i_node)
+    obj["metadata"]["labels"].update({"kubernetes.io/arch": "amd64", "beta.kubernetes.io/arch": "amd64",
+                                      "beta.kubernetes.io/os": "linux"})
+    return obj
+
+
 def pod_object(i: int, labels: dict, scheduler_name: str, namespace: str = "default",
-               prefix: str = "burst", spec: Optional[dict] = None) -> dict:
+               prefix: str = "burst", spec: Optional[dict] = None, meta: Optional[dict] = None) -> dict:
     return {"apiVersion": "v1", "kind": "Pod",
-            "metadata": {"name": f"{prefix}-{i}", "namespace": namespace, "labels": dict(labels)},
+            "metadata": {"name": f"{prefix}-{i}", "namespace": namespace, "labels": dict(labels), **(meta or {})},
             "spec": {"schedulerName": scheduler_name,
                      "containers": [{"name": "main", "image": "rocm/pytorch:latest",
                                      "resources": {"requests": {"cpu": "100m", "memory": "128Mi"}}}],
@@ -134,9 +220,13 @@ def populate(server, w: Workload, template: Optional[dict] = None, link_load: fl
     ``template`` (from a real amd-smi sample of the local MI355X) overrides the per-card
     static fields of the MI355X nodes."""
     rng = random.Random(seed)
-    for name, spec, gpus in w.nodes:
+    if w.cluster == "kind":
+        for res, obj in kind_objects():
+            server.create(res, obj)
+    for k, (name, spec, gpus) in enumerate(w.nodes):
         # kubelet --max-pods 2048: config 5 packs 5000 HBM-sharing pods onto 4 nodes
-        server.create("nodes", make_node(name, pods=2048))
+        node = make_node(name, pods=2048)
+        server.create("nodes", kindify_node(node, k) if w.cluster == "kind" else node)
         scv = make_scv(name, spec, gpus, update_time=time.time(), link_load=link_load, rng=rng,
                        jitter=link_load > 0)
         scv.update_interval_ms = 60_000     # one sample stays fresh for the whole burst

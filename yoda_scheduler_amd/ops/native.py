@@ -201,7 +201,7 @@ def avoid_controllers(raw) -> list:
     except (ValueError, AttributeError):
         return []
     out = []
-    for a in items:
+    for a in items if isinstance(items, list) else ():
         pc = ((a.get("podSignature") or {}).get("podController")) or {} if isinstance(a, dict) else {}
         if pc.get("kind") in ("ReplicationController", "ReplicaSet"):
             out.append((pc["kind"], str(pc.get("uid") or "")))

@@ -79,7 +79,9 @@ class NodePreferAvoidPods(ScorePlugin):
             avoids = json.loads(node.avoid).get("preferAvoidPods") or []
         except (ValueError, AttributeError):
             return MAX_NODE_SCORE, Status.ok()
-        for a in avoids:
+        for a in avoids if isinstance(avoids, list) else ():
+            if not isinstance(a, dict):
+                continue
             pc = ((a.get("podSignature") or {}).get("podController")) or {}
             if (pc.get("kind"), pc.get("uid")) == ctl:
                 return 0, Status.ok()
