@@ -861,6 +861,7 @@ PYBIND11_MODULE(_yoda_core, m) {
              d["retried"] = s.retried;
              d["status_patches"] = s.status_patches;
              d["status_patch_errors"] = s.status_patch_errors;
+             d["status_patches_skipped"] = s.status_patches_skipped;
              d["census_calls"] = s.census_calls;
              d["census_entries"] = s.census_entries;
              d["census_s"] = s.census_s;
@@ -873,6 +874,9 @@ PYBIND11_MODULE(_yoda_core, m) {
              d["return_s"] = s.return_s;
              d["idle_queued_s"] = s.idle_queued_s;
              d["async_runs"] = s.async_runs;
+             py::dict bp;
+             for (const auto& kv : s.by_profile) bp[py::str(kv.first)] = py::make_tuple(kv.second.first, kv.second.second);
+             d["by_profile"] = bp;
              return d;
            })
       // [(t_pick, t_worker_start, t_worker_end, t_done, pods)] of the runs since the last call

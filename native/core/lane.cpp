@@ -133,6 +133,16 @@ double wall() {
   return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
 }
 
+// metav1.Time: RFC 3339 in whole seconds, UTC
+std::string rfc3339(double ts) {
+  time_t sec = (time_t)ts;
+  struct tm tm;
+  gmtime_r(&sec, &tm);
+  char buf[40];
+  strftime(buf, sizeof buf, "%Y-%m-%dT%H:%M:%SZ", &tm);
+  return buf;
+}
+
 std::string key_of(const yk::PodProj& p) { return p.ns + "/" + p.name; }
 
 bool terminal(const yk::PodProj& p) { return p.phase == "Succeeded" || p.phase == "Failed"; }
@@ -681,6 +691,7 @@ void Lane::handle_answer(uint64_t tag, int status, std::string& body, double t_a
     {
       std::lock_guard<std::mutex> g(stat_mu_);
       st_.scheduled++;
+      if (e->prof >= 0 && e->prof < (int)lp_.size()) st_.by_profile[lp_[e->prof].name].first++;
       if (e2e_.size() < o_.e2e_keep) e2e_.push_back((float)(now - e->t_cycle));
     }
     if (scheduled_.fetch_add(1, std::memory_order_relaxed) + 1 == watermark_.load(std::memory_order_relaxed))
@@ -766,9 +777,27 @@ void Lane::apply_gates(std::vector<Fwd>* out) {
     if (hit) evict.push_back(e);
   }
   for (Entry* e : evict) {
+    if (e->st == PARKED || e->st == BACKOFF) {
+      requeue_to_python(e);
+      continue;
+    }
     drop_owned(e, false);
     if (!uninteresting(e->ev->p, lp_)) forward('A', e->ev, nullptr, out);
   }
+}
+
+void Lane::requeue_to_python(Entry* e) {
+  // the pod keeps its attempt count and goes to Python's podBackoffQ instead of
+  // arriving as a fresh add (which retried at once and restarted backoff from the initial value)
+  Handoff h;
+  h.kind = Handoff::kRequeue;
+  h.ev = e->ev;
+  h.profile = e->prof >= 0 && e->prof < (int)lp_.size() ? lp_[e->prof].name : std::string();
+  h.t_enqueue = e->t_enq;
+  h.t_cycle = e->t_fail;
+  h.attempts = std::max<uint32_t>(1, e->attempts);
+  drop_owned(e, false);
+  hand_pending_.push_back(std::move(h));
 }
 
 void Lane::apply_profiles(std::vector<Fwd>* out) {
@@ -792,6 +821,12 @@ void Lane::apply_profiles(std::vector<Fwd>* out) {
       e->prof = prof;
   }
   for (Entry* e : evict) {
+    // a waiting pod of a profile that is still served (now by Python) keeps its backoff state
+    if ((e->st == PARKED || e->st == BACKOFF) && !uninteresting(e->ev->p, lp_) && e->ev->full().ok &&
+        e->ev->full().node.empty()) {
+      requeue_to_python(e);
+      continue;
+    }
     drop_owned(e, false);
     if (!uninteresting(e->ev->p, lp_)) forward('A', e->ev, nullptr, out);
   }
@@ -1590,18 +1625,31 @@ void Lane::route(Entry* e, double now) {
   else activate(e);
 }
 
-void Lane::patch_condition(const Entry& e, const std::string& msg) {
+void Lane::patch_condition(Entry& e, const std::string& msg) {
+  // upstream v1.20 updatePod: the condition goes out as a strategic merge patch of pods/status
+  // (conditions merged by type, so other conditions on the pod stay), and not at all when the
+  // pod already carries the same PodScheduled=False reason and message
   yk::PodPort* port = port_.load();
   if (!port) return;
+  if (!e.cond_msg.empty() && e.cond_msg == msg) {
+    std::lock_guard<std::mutex> g(stat_mu_);
+    st_.status_patches_skipped++;
+    return;
+  }
+  if (e.cond_ltt <= 0) e.cond_ltt = wall();
+  e.cond_msg = msg;
   std::string b;
-  b.reserve(160 + msg.size());
-  b += "{\"status\":{\"conditions\":[{\"type\":\"PodScheduled\",\"status\":\"False\",\"reason\":\"Unschedulable\","
-       "\"message\":";
+  b.reserve(200 + msg.size());
+  b += "{\"status\":{\"conditions\":[{\"type\":\"PodScheduled\",\"status\":\"False\",\"lastProbeTime\":null,"
+       "\"lastTransitionTime\":";
+  json_str(rfc3339(e.cond_ltt), b);
+  b += ",\"reason\":\"Unschedulable\",\"message\":";
   json_str(msg, b);
   b += "}]}}";
   const std::string path = "/api/v1/namespaces/" + e.ev->p.ns + "/pods/" + e.ev->p.name + "/status";
   static std::atomic<uint64_t> seq{0};
-  port->request_native("PATCH", path, std::move(b), true, 30.0, kEventTag | kPatchBit | (++seq & 0xffffffffull), this);
+  port->request_native("PATCH", path, std::move(b), true, 30.0, kEventTag | kPatchBit | (++seq & 0xffffffffull), this,
+                       "application/strategic-merge-patch+json");
   std::lock_guard<std::mutex> g(stat_mu_);
   st_.status_patches++;
 }
@@ -1614,6 +1662,7 @@ void Lane::fail_native(Entry* e, const Profile& pr, const CycleResult& res, bool
     std::lock_guard<std::mutex> g(stat_mu_);
     st_.unschedulable++;
     st_.native_failed++;
+    st_.by_profile[pr.name].second++;
     if (o_.events) {
       st_.events_recorded++;
       if ((int)ev_q_.size() >= o_.event_buffer) st_.events_dropped++;

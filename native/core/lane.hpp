@@ -99,6 +99,7 @@ struct LaneStats {
   uint64_t native_failed = 0;      // of `unschedulable`: kept in the lane (no PostFilter could help)
   uint64_t moved = 0, retried = 0; // pods moved by move requests; pods back from backoff to the queue
   uint64_t status_patches = 0, status_patch_errors = 0;
+  uint64_t status_patches_skipped = 0;   // the pod's condition already said the same (upstream updatePod)
   uint64_t census_calls = 0, census_entries = 0;   // count_matching: calls, reserved pods walked
   double census_s = 0;
   uint64_t left_in_flight = 0;   // pods gone (deleted, bound elsewhere) while their run was on the engine
@@ -110,6 +111,8 @@ struct LaneStats {
   // worker's idle time between runs while pods that arrived before the last run ended waited
   double handoff_s = 0, return_s = 0, idle_queued_s = 0;
   uint64_t async_runs = 0;
+  // per profile: (pods scheduled, unschedulable attempts kept native) — the attempts metric
+  std::unordered_map<std::string, std::pair<uint64_t, uint64_t>> by_profile;
 };
 
 class Lane : public yk::PodSink {
@@ -139,7 +142,9 @@ class Lane : public yk::PodSink {
   };
   // A pod the lane gives up to the Python path.
   struct Handoff {
-    enum Kind : int { kUnschedulable = 0, kBindError = 1 };
+    // kRequeue: a waiting pod (unschedulableQ / podBackoffQ) the lane may no longer run (a gate or
+    // profile change): Python requeues it into backoff with its attempts, no new FailedScheduling
+    enum Kind : int { kUnschedulable = 0, kBindError = 1, kRequeue = 2 };
     int kind = 0;
     std::shared_ptr<yk::PodEv> ev;
     std::string profile;
@@ -239,6 +244,11 @@ class Lane : public yk::PodSink {
     double t_park = 0;       // when it entered unschedulableQ
     uint64_t bseq = 0;       // backoff heap item of this entry (stale items are skipped)
     std::shared_ptr<PodReq> req;   // the request of the failed attempt (move hints re-filter with it)
+    // the PodScheduled=False condition this lane last wrote for the pod: an unchanged message
+    // is not written again, and lastTransitionTime stays that of the first write (upstream
+    // podutil.UpdatePodCondition: the status did not transition)
+    std::string cond_msg;
+    double cond_ltt = 0;
     // a reserved pod's event whose labels are current: later watch echoes keep it while their
     // labels hash says the labels did not change, so the selector census never projects them
     std::shared_ptr<yk::PodEv> lab_ev;
@@ -292,6 +302,8 @@ class Lane : public yk::PodSink {
   void handle_relist(const std::vector<std::shared_ptr<yk::PodEv>>& items, std::vector<Fwd>* out);
   void apply_gates(std::vector<Fwd>* out);
   void drop_owned(Entry* e, bool release);
+  // a waiting (PARKED / BACKOFF) entry leaves for the Python queue keeping attempts and backoff
+  void requeue_to_python(Entry* e);
   void apply_profiles(std::vector<Fwd>* out);
   void count(St s, int d);
   void set_state(Entry* e, St s);
@@ -320,7 +332,7 @@ class Lane : public yk::PodSink {
   bool hinted_since(uint64_t cycle, const PodReq& req);
   double next_timer() const;
   std::string fit_error(const CycleResult& r, const yk::PodProj& p) const;
-  void patch_condition(const Entry& e, const std::string& msg);
+  void patch_condition(Entry& e, const std::string& msg);
   void flush_events();
   void forward(char type, std::shared_ptr<yk::PodEv> ev, std::shared_ptr<yk::PodEv> old, std::vector<Fwd>* out);
   void publish(std::vector<Fwd>&& fwd, std::vector<Handoff>&& hand);

@@ -54,7 +54,7 @@ class FakePort : public yk::PodPort {
     cv.notify_one();
   }
   void request_native(const std::string&, const std::string&, std::string&&, bool, double, uint64_t tag,
-                      yk::PodSink* sink) override {
+                      yk::PodSink* sink, const char*) override {
     std::lock_guard<std::mutex> g(mu);
     events.push_back({tag, sink});
     cv.notify_one();

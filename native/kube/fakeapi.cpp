@@ -579,7 +579,8 @@ class Server {
     return s;
   }
 
-  SP patch(ResState& rs, const Value& p, const std::string& path_ns, const std::string& name, ApiErr* err) {
+  SP patch(ResState& rs, const Value& p, const std::string& path_ns, const std::string& name, ApiErr* err,
+           bool strategic = false) {
     const ResDef& d = *rs.def;
     std::string key = d.namespaced ? (path_ns.empty() ? "default" : path_ns) + "/" + name : name;
     auto it = rs.objs.find(key);
@@ -589,7 +590,8 @@ class Server {
     }
     SP cur = it->second;
     Value nv = cur->v();
-    merge_patch(nv, p);
+    if (strategic) strategic_merge_patch(nv, p);
+    else merge_patch(nv, p);
     Value& meta = nv.at("metadata");
     if (meta.t != Value::Obj) meta = Value::object();
     meta.at("resourceVersion") = Value::str(next_rv());
@@ -1284,7 +1286,9 @@ void Server::handle(Conn* c, Request& req) {
     return;
   }
   if (m == "PATCH") {
-    SP s2 = patch(rs, body, ns, name, &err);
+    // application/merge-patch+json (RFC 7386) or application/strategic-merge-patch+json
+    const bool strategic = req.headers.get("content-type").find("strategic-merge-patch") != std::string::npos;
+    SP s2 = patch(rs, body, ns, name, &err, strategic);
     if (s2) respond(c, 200, s2->text);
     else respond_err(c, err);
     return;

@@ -464,6 +464,80 @@ void merge_patch(Value& target, const Value& patch) {
   }
 }
 
+namespace {
+const char* merge_key_of(std::string_view field) {
+  static const std::pair<const char*, const char*> kKeys[] = {
+      {"conditions", "type"},     {"containers", "name"}, {"initContainers", "name"},
+      {"ephemeralContainers", "name"}, {"volumes", "name"}, {"env", "name"},
+      {"ports", "containerPort"}, {"ownerReferences", "uid"}, {"volumeMounts", "mountPath"},
+      {"imagePullSecrets", "name"}};
+  for (const auto& k : kKeys)
+    if (field == k.first) return k.second;
+  return nullptr;
+}
+}  // namespace
+
+void strategic_merge_patch(Value& target, const Value& patch) {
+  if (patch.t != Value::Obj) {
+    target = patch;
+    return;
+  }
+  if (target.t != Value::Obj) target = Value::object();
+  for (const auto& m : patch.obj) {
+    const std::string& k = m.first;
+    if (!k.empty() && k[0] == '$') continue;                 // $setElementOrder/..., $retainKeys, $patch
+    if (m.second.t == Value::Null) {
+      target.erase(k);
+      continue;
+    }
+    const char* mk = merge_key_of(k);
+    Value* cur = target.get(k);
+    if (mk && m.second.t == Value::Arr && cur && cur->t == Value::Arr) {
+      for (const Value& item : m.second.arr) {
+        const Value* key = item.t == Value::Obj ? item.get(mk) : nullptr;
+        if (!key) {
+          cur->arr.push_back(item);
+          continue;
+        }
+        auto it = cur->arr.begin();
+        for (; it != cur->arr.end(); ++it) {
+          const Value* ck = it->t == Value::Obj ? it->get(mk) : nullptr;
+          if (ck && equal(*ck, *key)) break;
+        }
+        const bool del = item.sv("$patch") == "delete";
+        if (it == cur->arr.end()) {
+          if (!del) {
+            Value fresh = Value::object();
+            strategic_merge_patch(fresh, item);
+            cur->arr.push_back(std::move(fresh));
+          }
+        } else if (del) {
+          cur->arr.erase(it);
+        } else {
+          strategic_merge_patch(*it, item);
+        }
+      }
+      continue;
+    }
+    if (m.second.t == Value::Arr) {
+      // a list without a merge key is replaced, its elements' directives dropped
+      Value repl = Value::array();
+      for (const Value& item : m.second.arr) {
+        if (item.t == Value::Obj) {
+          Value fresh = Value::object();
+          strategic_merge_patch(fresh, item);
+          repl.arr.push_back(std::move(fresh));
+        } else {
+          repl.arr.push_back(item);
+        }
+      }
+      target.at(k) = std::move(repl);
+      continue;
+    }
+    strategic_merge_patch(target.at(k), m.second);
+  }
+}
+
 bool equal(const Value& a, const Value& b) {
   if (a.t != b.t) return false;
   switch (a.t) {

@@ -76,6 +76,12 @@ uint64_t hash(const Value& v, uint64_t seed = 0x9e3779b97f4a7c15ull);
 
 // RFC 7386 JSON merge patch: applies `patch` onto `target` in place
 void merge_patch(Value& target, const Value& patch);
+// Kubernetes strategic merge patch (the subset the core/v1 Pod needs): like a merge patch, but
+// lists with a patch merge key (status.conditions by type, containers / volumes / env by name,
+// ports by containerPort, ownerReferences by uid) merge element-wise by that key, an element
+// with "$patch": "delete" removes its match, and $setElementOrder / $retainKeys directives are
+// accepted and ignored
+void strategic_merge_patch(Value& target, const Value& patch);
 
 bool equal(const Value& a, const Value& b);
 

@@ -74,9 +74,11 @@ class PodPort {
   // Binding POSTs (client rate limit applies), answered through sink->on_answers (tags[k]).
   virtual void bind_native(std::vector<BindSpec>&& binds, const std::vector<uint64_t>& tags, double timeout_s,
                            PodSink* sink) = 0;
-  // Any other request (events); answered through sink->on_answers (tag).
+  // Any other request (events, pod status); answered through sink->on_answers (tag). A PATCH
+  // body is a JSON merge patch unless `content_type` names another patch type.
   virtual void request_native(const std::string& method, const std::string& path, std::string&& body,
-                              bool limited, double timeout_s, uint64_t tag, PodSink* sink) = 0;
+                              bool limited, double timeout_s, uint64_t tag, PodSink* sink,
+                              const char* content_type = nullptr) = 0;
 };
 
 }  // namespace yk

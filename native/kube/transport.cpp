@@ -314,11 +314,13 @@ void Transport::bind_native(std::vector<BindSpec>&& binds, const std::vector<uin
 }
 
 void Transport::request_native(const std::string& method, const std::string& path, std::string&& body,
-                               bool limited, double timeout_s, uint64_t tag, PodSink* sink) {
+                               bool limited, double timeout_s, uint64_t tag, PodSink* sink, const char* content_type) {
   auto r = std::make_unique<Req>();
   r->id = next_id_++;
-  // PATCH bodies are JSON merge patches (the pod condition, an event's series)
-  r->wire = head(method, path, body.size(), method == "PATCH" ? "application/merge-patch+json" : "application/json");
+  // PATCH bodies are JSON merge patches (an event's series) unless the caller names the type
+  // (the PodScheduled condition is a strategic merge patch, conditions merged by type)
+  r->wire = head(method, path, body.size(),
+                 content_type ? content_type : method == "PATCH" ? "application/merge-patch+json" : "application/json");
   r->wire.append(body);
   r->limited = limited;
   r->deadline = timeout_s > 0 ? now_s() + timeout_s : 0.0;

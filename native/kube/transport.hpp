@@ -99,7 +99,7 @@ class Transport : public PodPort {
   void bind_native(std::vector<BindSpec>&& binds, const std::vector<uint64_t>& tags, double timeout_s,
                    PodSink* sink) override;
   void request_native(const std::string& method, const std::string& path, std::string&& body, bool limited,
-                      double timeout_s, uint64_t tag, PodSink* sink) override;
+                      double timeout_s, uint64_t tag, PodSink* sink, const char* content_type = nullptr) override;
   std::vector<Completion> drain();
   void set_token(const std::string& token);
   // client QPS / burst (clientConnection); qps <= 0 disables limiting

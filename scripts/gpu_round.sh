@@ -22,6 +22,8 @@ for s in $STEPS; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     bench5) step bench5 600 python bench.py --config 5 ;;
+    benchkind) step bench_kind 600 python bench.py --cluster kind ;;
+    bench6kind) step bench6_kind 600 python bench.py --config 6 --steps 3 --warmup 1 --device on --cluster kind ;;
     bench6on) step bench6_on 600 python bench.py --config 6 --steps 3 --warmup 1 --device on ;;
     c6cpu) step c6cpu 600 python bench.py --config 6 --steps 10 --warmup 2 --alt none ;;   # 10k pods: finer thread-CPU ticks
     bench6off) step bench6_off 600 python bench.py --config 6 --steps 3 --warmup 1 --device off ;;

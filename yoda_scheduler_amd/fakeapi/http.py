@@ -147,7 +147,8 @@ class FakeApiHttp:
             if req.method == "PUT":
                 return web.json_response(s.update(res, body, ns, status_only=(sub == "status")))
             if req.method == "PATCH":
-                return web.json_response(s.patch(res, name, body, ns))
+                strategic = "strategic-merge-patch" in (req.headers.get("Content-Type") or "")
+                return web.json_response(s.patch(res, name, body, ns, strategic=strategic))
             if req.method == "DELETE":
                 return web.json_response(s.delete(res, name, ns))
         except ApiError as e:

@@ -104,6 +104,7 @@ class FakeApiServer:
         self.bind_log: dict[str, float] = {}
         self.bind_node: dict[str, str] = {}
         self.calls = collections.Counter()
+        self.patch_log: list = []          # (res, namespace, name, strategic, patch) of every PATCH
 
     # ------------------------------------------------------------------ internals
     def _next_rv(self) -> str:
@@ -192,11 +193,14 @@ class FakeApiServer:
         self._emit(res, "MODIFIED", new, cur)
         return new
 
-    def patch(self, res: str, name: str, patch: dict, namespace: Optional[str] = None) -> dict:
-        """JSON merge patch (RFC 7386)."""
+    def patch(self, res: str, name: str, patch: dict, namespace: Optional[str] = None,
+              strategic: bool = False) -> dict:
+        """JSON merge patch (RFC 7386), or a strategic merge patch (lists with a patch merge key —
+        status.conditions by type, ... — merged element-wise, ``_strategic``)."""
         self.calls["patch"] += 1
+        self.patch_log.append((res, namespace, name, strategic, patch))
         cur = self.get(res, name, namespace)
-        new = _merge(cur, patch)
+        new = _strategic(cur, patch) if strategic else _merge(cur, patch)
         new["metadata"] = dict(new.get("metadata") or {})
         new["metadata"]["resourceVersion"] = self._next_rv()
         for k in ("uid", "name", "namespace", "creationTimestamp"):
@@ -337,4 +341,47 @@ def _merge(cur, patch):
             out.pop(k, None)
         else:
             out[k] = _merge(out.get(k), v)
+    return out
+
+
+# patch merge keys of the core/v1 Pod lists (``native/kube/json.cpp::strategic_merge_patch``)
+MERGE_KEYS = {"conditions": "type", "containers": "name", "initContainers": "name", "ephemeralContainers": "name",
+              "volumes": "name", "env": "name", "ports": "containerPort", "ownerReferences": "uid",
+              "volumeMounts": "mountPath", "imagePullSecrets": "name"}
+
+
+def _strategic(cur, patch):
+    """Kubernetes strategic merge patch, the subset a Pod needs: merge-keyed lists merge
+    element-wise (``$patch: delete`` removes an element), other lists are replaced, ``$``
+    directives ($setElementOrder, $retainKeys) are accepted and ignored."""
+    if not isinstance(patch, dict):
+        return patch
+    out = dict(cur) if isinstance(cur, dict) else {}
+    for k, v in patch.items():
+        if k.startswith("$"):
+            continue
+        if v is None:
+            out.pop(k, None)
+            continue
+        mk = MERGE_KEYS.get(k)
+        old = out.get(k)
+        if mk and isinstance(v, list) and isinstance(old, list):
+            items = [dict(x) if isinstance(x, dict) else x for x in old]
+            for item in v:
+                if not isinstance(item, dict) or mk not in item:
+                    items.append(item)
+                    continue
+                at = next((i for i, x in enumerate(items) if isinstance(x, dict) and x.get(mk) == item[mk]), None)
+                if item.get("$patch") == "delete":
+                    if at is not None:
+                        items.pop(at)
+                elif at is None:
+                    items.append(_strategic({}, item))
+                else:
+                    items[at] = _strategic(items[at], item)
+            out[k] = items
+        elif isinstance(v, list):
+            out[k] = [_strategic({}, x) if isinstance(x, dict) else x for x in v]
+        else:
+            out[k] = _strategic(old, v)
     return out

@@ -68,6 +68,7 @@ class NativeLane:
         self._temp_terms: tuple = ()        # gates of a Python cycle running beside the lane (gated)
         self._in_gated = False             # inside gated(): anti-affinity changes wait for its exit
         self._gates_pending = False        # a coalesced gate update (holder removals) is scheduled
+        self._sticky_never = (1 << 62) - 1  # AND of the masks of profiles eligible since the lane last owned nothing
         sched.queue.on_move_all = self._move_all
 
     # ------------------------------------------------------------------ lifecycle
@@ -148,10 +149,15 @@ class NativeLane:
         s = self.s
         f_yoda = core().F_YODA
         never = (1 << 62) - 1                  # pod flags no lane pod carries (AND of the masks)
+        # sticky across eligibility flips: a profile that turned ineligible still has
+        # its reserved pods in the lane, so its mask keeps counting until the lane owns nothing
+        if self._sticky_never != never and self.owned() == 0:
+            self._sticky_never = never
         for name, fw in s.frameworks.items():
             m = self.eligible_mask(fw)
             if m is not None:
                 never &= m
+                self._sticky_never &= m
             want = (m is not None, m or 0, bool(fw.filter_mask & f_yoda), self.preempt_above(fw),
                     fw.gate_terms() + self._temp_terms if m is not None else ())
             if self._profiles.get(name) == want:
@@ -160,7 +166,7 @@ class NativeLane:
             self.lane.set_profile(s.engine, name, want[0], want[1], want[2], want[3], list(want[4]))
             self._profiles[name] = want
             log.info("native lane: profile %s %s (flag mask %#x)", name, "on" if want[0] else "off", want[1])
-        s.cache.lane_never_flags = never
+        s.cache.lane_never_flags = never & self._sticky_never
 
     def anti_changed(self, grew: bool = True) -> None:
         """The bound/assumed pods with required anti-affinity changed. A new holder's terms reach
@@ -297,6 +303,12 @@ class NativeLane:
         pi = PodInfo.from_native(ev)
         pi.attempts = max(1, attempts)
         pi.initial_attempt = pi.enqueued = t_enq
+        if kind == 2:
+            # a waiting lane pod its profile's lane may no longer run: Python's podBackoffQ, its
+            # attempts (and so its backoff) carried over, no second FailedScheduling
+            pi.initial_attempt = t_enq
+            s.queue.add_unschedulable(pi, -1, unschedulable=False)
+            return
         if kind == 0:
             # cycle -1: a move request may have arrived since the lane's cycle, so the pod
             # retries from backoff rather than parking in unschedulableQ (never lose a wake-up)

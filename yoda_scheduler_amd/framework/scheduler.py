@@ -198,6 +198,9 @@ class Scheduler:
         self.scv_requeues = 0          # Scv updates that moved the parked pods back
         self.scv_requeue_skips = 0     # Scv updates the queueing hint kept from doing so
         self.bind_errors = 0
+        self._conditions: dict = {}        # uid → the PodScheduled=False condition last written
+        self._lane_attempts_seen: dict = {}   # profile → lane (scheduled, failed) already exported
+        self.status_patches_skipped = 0
         self._stop = asyncio.Event()
         self.leading = asyncio.Event()
         self._pending_binds = 0
@@ -354,6 +357,7 @@ class Scheduler:
                 self.queue.move_all_to_active_or_backoff("AssignedPodCompleted")
                 return
             if not self._assigned(old):
+                self._conditions.pop(uid, None)
                 self.queue.delete(uid)
                 if uid in self.nominations:
                     self._clear_nomination(uid)
@@ -373,6 +377,7 @@ class Scheduler:
 
     def on_pod_delete(self, obj: dict) -> None:
         uid = (obj.get("metadata") or {}).get("uid")
+        self._conditions.pop(uid, None)
         if uid in self.nominations:
             self._clear_nomination(uid)
         if self._assigned(obj) or self.cache.is_assumed(uid):
@@ -387,6 +392,8 @@ class Scheduler:
         ident tuple): the same transitions as ``on_pod_add/update/delete`` without a dict."""
         _key, uid, node, sched, phase, h = idt
         terminal = phase == "Succeeded" or phase == "Failed"
+        if self._conditions and (typ == "DELETED" or node):
+            self._conditions.pop(uid, None)
         if typ == "DELETED":
             if uid in self.nominations:
                 self._clear_nomination(uid)
@@ -867,17 +874,42 @@ class Scheduler:
         self.queue.add_unschedulable(pi, cycle, unschedulable)
         asyncio.get_event_loop().create_task(self._update_condition(pi, msg, nominated))
 
-    async def _update_condition(self, pi: PodInfo, msg: str, nominated: str) -> None:
-        patch = {"status": {"conditions": [{"type": "PodScheduled", "status": "False", "reason": "Unschedulable",
-                                            "message": msg}]}}
+    def _condition_patch(self, pi: PodInfo, msg: str, nominated: str) -> Optional[dict]:
+        """upstream v1.20 ``updatePod`` + ``podutil.UpdatePodCondition``: the PodScheduled=False
+        condition as a strategic merge patch of pods/status, or None when the pod already says
+        the same (same status, reason and message, no new nominated node) — then nothing is
+        written. lastTransitionTime is set when the condition first appears and kept while its
+        status stays False. What the pod "already says" is what this scheduler last wrote for it
+        (its own writes' echoes are status-only updates the queue does not re-read), or the
+        condition on the pod object when that is already decoded (a condition a previous
+        scheduler instance wrote)."""
+        prev = self._conditions.get(pi.uid)
+        if prev is None and pi._obj is not None:
+            for c in ((pi._obj.get("status") or {}).get("conditions")) or ():
+                if isinstance(c, dict) and c.get("type") == "PodScheduled" and c.get("status") == "False":
+                    prev = (c.get("reason"), c.get("message"), c.get("lastTransitionTime"),
+                            (pi._obj.get("status") or {}).get("nominatedNodeName") or "")
+        if prev is not None and prev[0] == "Unschedulable" and prev[1] == msg and (not nominated or prev[3] == nominated):
+            self.status_patches_skipped += 1
+            return None
+        ltt = prev[2] if prev is not None and prev[2] else time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+        self._conditions[pi.uid] = ("Unschedulable", msg, ltt, nominated or (prev[3] if prev else ""))
+        patch = {"status": {"conditions": [{"type": "PodScheduled", "status": "False", "lastProbeTime": None,
+                                            "lastTransitionTime": ltt, "reason": "Unschedulable", "message": msg}]}}
         if nominated:
             patch["status"]["nominatedNodeName"] = nominated
+        return patch
+
+    async def _update_condition(self, pi: PodInfo, msg: str, nominated: str) -> None:
+        patch = self._condition_patch(pi, msg, nominated)
+        if patch is None:
+            return
         try:
             if self.native is not None:
-                await self.client.patch("pods", pi.name, patch, pi.namespace, limited=True)
+                await self.client.patch("pods", pi.name, patch, pi.namespace, limited=True, strategic=True)
             else:
                 await self.limiter.acquire()
-                await self.client.patch("pods", pi.name, patch, pi.namespace)
+                await self.client.patch("pods", pi.name, patch, pi.namespace, strategic=True)
         except Exception as e:  # noqa: BLE001 - best effort like upstream
             log.debug("condition update for %s failed: %r", pi.key, e)
 
@@ -1322,12 +1354,33 @@ class Scheduler:
             flipped = self.cache.refresh_staleness()
             if flipped:
                 self.queue.move_all_to_active_or_backoff("ScvStale")
-            for q, n in self.queue.pending().items():
+            pend = self.queue.pending()
+            if self.lane is not None:
+                self._lane_metrics(m, pend)
+            for q, n in pend.items():
                 m.child(m.pending, q).set(n)
             counts = self.cache.snapshot_counts()
             m.child(m.cache_size, "nodes").set(counts["nodes"])
             m.child(m.cache_size, "pods").set(counts["pods"])
             m.child(m.cache_size, "assumed_pods").set(counts["assumed"])
+
+    def _lane_metrics(self, m, pend: dict) -> None:
+        """The lane's pods in the scheduler's metrics: its queued / in-flight pods are
+        pending in activeQ, its unschedulableQ and podBackoffQ add to those gauges, and its
+        scheduling attempts — Bindings acknowledged and unschedulable attempts it kept native —
+        feed scheduler_schedule_attempts_total per profile."""
+        st = self.lane.lane.stats()
+        pend["active"] = pend.get("active", 0) + st["queued"] + st["inflight"]
+        pend["backoff"] = pend.get("backoff", 0) + st["backoff"]
+        pend["unschedulable"] = pend.get("unschedulable", 0) + st["parked"]
+        seen = self._lane_attempts_seen
+        for prof, (sched, failed) in st["by_profile"].items():
+            ps, pf = seen.get(prof, (0, 0))
+            if sched > ps:
+                m.child(m.attempts, "scheduled", prof).inc(sched - ps)
+            if failed > pf:
+                m.child(m.attempts, "unschedulable", prof).inc(failed - pf)
+            seen[prof] = (sched, failed)
 
     async def scheduling_loop(self) -> None:
         q = self.queue

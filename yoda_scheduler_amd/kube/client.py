@@ -416,10 +416,13 @@ class KubeClient:
         return await self._req("PUT", res, ns, m["name"], "status", body=obj)
 
     async def patch(self, res: str, name: str, patch: dict, namespace: Optional[str] = None,
-                    limited: bool = False) -> dict:
+                    limited: bool = False, strategic: bool = False) -> dict:
+        """A JSON merge patch, or with ``strategic`` a strategic merge patch (what upstream's
+        scheduler sends for pod status: conditions merge by type instead of replacing the list)."""
         sub = "status" if res == "pods" and set(patch) == {"status"} else None
         return await self._req("PATCH", res, namespace, name, sub, body=patch,
-                               content_type="application/merge-patch+json", limited=limited)
+                               content_type="application/strategic-merge-patch+json" if strategic
+                               else "application/merge-patch+json", limited=limited)
 
     async def delete(self, res: str, name: str, namespace: Optional[str] = None, limited: bool = False) -> dict:
         return await self._req("DELETE", res, namespace, name, limited=limited)
