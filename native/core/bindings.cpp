@@ -315,10 +315,13 @@ PYBIND11_MODULE(_yoda_core, m) {
   m.attr("S_SPREAD") = (int)S_SPREAD;
   m.attr("S_NUM") = (int)S_NUM;
   m.attr("F_SPREAD") = (uint32_t)F_SPREAD;
+  m.attr("F_INTERPOD") = (uint32_t)F_INTERPOD;
+  m.attr("S_INTERPOD") = (int)S_INTERPOD;
   m.attr("REASONS") = py::make_tuple("OK", "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity",
                                      "NodeResourcesFit", "NoScv", "ScvStale", "GpuNumber", "GpuMemory",
                                      "GpuClock", "GpuFit", "NodeGone", "NodeResourcesFitExtended",
-                                     "PodTopologySpread", "PodTopologySpreadLabel");
+                                     "PodTopologySpread", "PodTopologySpreadLabel", "InterPodAffinityExisting",
+                                     "InterPodAffinity", "InterPodAntiAffinity");
 
   py::class_<PodReq>(m, "PodReq")
       .def_readonly("has_number", &PodReq::has_number)
@@ -511,7 +514,7 @@ PYBIND11_MODULE(_yoda_core, m) {
            [](Engine& e, PodReq& r, const std::string& ns, const std::vector<std::pair<std::string, std::string>>& labels,
               bool deleting, const std::vector<std::string>& images, int32_t containers,
               const std::vector<std::pair<std::string, int64_t>>& ext, const py::object& owner,
-              const py::object& avoid, const py::object& spread) {
+              const py::object& avoid, const py::object& spread, const py::object& pod_aff) {
              r.ns = e.intern(ns);
              r.labels = labels_of(e, labels);
              r.deleting = deleting;
@@ -553,11 +556,35 @@ PYBIND11_MODULE(_yoda_core, m) {
                  r.spread.push_back(std::move(x));
                }
              }
+             // (required affinity, required anti-affinity, preferred affinity, preferred anti-affinity),
+             // each [(topologyKey, namespaces | None, LabelSelector.native() | None, weight)]
+             r.aff.reset();
+             if (!pod_aff.is_none()) {
+               auto pa = std::make_shared<PodAffinity>();
+               auto t4 = pod_aff.cast<py::tuple>();
+               std::vector<PodTerm>* dst[4] = {&pa->req_aff, &pa->req_anti, &pa->pref_aff, &pa->pref_anti};
+               for (int k = 0; k < 4; ++k)
+                 for (auto term : t4[k]) {
+                   auto t = term.cast<py::tuple>();
+                   PodTerm x;
+                   x.key = e.intern(t[0].cast<std::string>());
+                   if (t[1].is_none() || py::len(t[1]) == 0) x.ns.push_back(r.ns);
+                   else
+                     for (auto n : t[1]) x.ns.push_back(e.intern(n.cast<std::string>()));
+                   x.sel = lsel_of(e, t[2]);
+                   x.weight = t[3].cast<int32_t>();
+                   dst[k]->push_back(std::move(x));
+                 }
+               if (!pa->empty()) r.aff = std::move(pa);
+             }
            },
            py::arg("req"), py::arg("ns"), py::arg("labels"), py::arg("deleting") = false,
            py::arg("images") = std::vector<std::string>{}, py::arg("containers") = 0,
            py::arg("ext") = std::vector<std::pair<std::string, int64_t>>{}, py::arg("owner") = py::none(),
-           py::arg("avoid") = py::none(), py::arg("spread") = py::none(), py::call_guard<EngineGuard>())
+           py::arg("avoid") = py::none(), py::arg("spread") = py::none(), py::arg("pod_aff") = py::none(),
+           py::call_guard<EngineGuard>())
+      .def("set_hard_pod_affinity_weight", &Engine::set_hard_pod_affinity_weight, py::call_guard<EngineGuard>())
+      .def_property_readonly("affinity_holders", &Engine::affinity_holders)
       .def("set_node_extras",
            [](Engine& e, int32_t idx, const std::vector<std::pair<std::string, int64_t>>& images,
               const std::vector<std::pair<std::string, int64_t>>& ext_alloc,

@@ -15,6 +15,16 @@
 
 namespace yoda {
 
+// (key, value) pair of interned strings as one map key
+static inline uint64_t pair_key(int32_t k, int32_t v) { return ((uint64_t)(uint32_t)k << 32) | (uint32_t)v; }
+
+// Python's // on int64
+static inline int64_t floor_div(int64_t a, int64_t b) {
+  int64_t q = a / b;
+  if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+  return q;
+}
+
 // ============================================================== ThreadPool
 ThreadPool::ThreadPool(int n) {
   for (int i = 0; i < n - 1; ++i) workers_.emplace_back([this] { worker(); });
@@ -89,6 +99,7 @@ Engine::Engine(bool compat, int threads) : compat_(compat) {
   if (threads > 1) pool_ = new ThreadPool(threads);
   intern("");
   unsched_key_ = intern("node.kubernetes.io/unschedulable");
+  dev_ext_res_ = intern("ephemeral-storage");
 }
 
 Engine::~Engine() {
@@ -107,6 +118,7 @@ EngineConfig Engine::config() const {
   c.spread_defaults = spread_defaults_;
   c.ext_ignored = ext_ignored_;
   c.ext_ignored_groups = ext_ignored_groups_;
+  c.hard_pod_affinity_weight = hard_aff_w_;
   return c;
 }
 
@@ -120,6 +132,7 @@ void Engine::set_config(const EngineConfig& c) {
   spread_defaults_ = c.spread_defaults;
   ext_ignored_ = c.ext_ignored;
   ext_ignored_groups_ = c.ext_ignored_groups;
+  hard_aff_w_ = c.hard_pod_affinity_weight;
 }
 
 int32_t Engine::intern(const std::string& s) {
@@ -161,8 +174,13 @@ void Engine::remove_node(int32_t idx) {
   if (idx < 0 || idx >= (int32_t)nodes_.size() || !nodes_[idx].alive) return;
   // drop reservations that point at this node
   for (auto it = ledger_.begin(); it != ledger_.end();) {
-    if (it->second.node == idx) it = ledger_.erase(it);
-    else ++it;
+    if (it->second.node == idx) {
+      aff_holders_.erase(it->first);
+      anti_holders_.erase(it->first);
+      it = ledger_.erase(it);
+    } else {
+      ++it;
+    }
   }
   node_idx_.erase(nodes_[idx].name);
   hard_taint_nodes_ -= nodes_[idx].hard_taint;
@@ -309,6 +327,11 @@ bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::ve
   a.ns = req.ns;
   a.labels = req.labels;
   a.deleting = req.deleting;
+  if (req.aff && !req.aff->empty()) {
+    a.aff = req.aff;
+    aff_holders_.insert(pod);
+    if (!req.aff->req_anti.empty()) anti_holders_.insert(pod);
+  }
   if (!req.ext.empty()) {
     a.ext = req.ext;
     for (const auto& r : a.ext) {
@@ -355,6 +378,10 @@ bool Engine::release(uint64_t pod) {
       if (it != n.ext_used.end() && it->first == r.first && (it->second -= r.second) == 0) n.ext_used.erase(it);
     }
     mark_dirty(a.node);
+  }
+  if (a.aff) {
+    aff_holders_.erase(pod);
+    anti_holders_.erase(pod);
   }
   ledger_.erase(it);
   return true;
@@ -443,14 +470,16 @@ bool Engine::yoda_card_eligible(const PodReq& req, const Card& c, uint64_t m, ui
 }
 
 Reason Engine::filter_node(const PodReq& req, int32_t idx, uint64_t* pn, uint64_t* pm, uint64_t* pc) const {
-  if (!wants_spread_filter(req)) return filter_node_pf(req, idx, pn, pm, pc, nullptr);
   SpreadPF pf;
-  spread_prefilter(req, &pf);
-  return filter_node_pf(req, idx, pn, pm, pc, &pf);
+  InterPodPF ip;
+  const bool sp = wants_spread_filter(req), ia = wants_interpod_filter(req);
+  if (sp) spread_prefilter(req, &pf);
+  if (ia) interpod_prefilter(req, &ip);
+  return filter_node_pf(req, idx, pn, pm, pc, sp ? &pf : nullptr, ia ? &ip : nullptr);
 }
 
 Reason Engine::filter_node_pf(const PodReq& req, int32_t idx, uint64_t* pn, uint64_t* pm, uint64_t* pc,
-                              const SpreadPF* pf) const {
+                              const SpreadPF* pf, const InterPodPF* ip) const {
   const Node& n = nodes_[idx];
   if (!n.alive) return RS_DEAD;
   if (filters_ & F_NODE_UNSCHEDULABLE) {
@@ -488,7 +517,11 @@ Reason Engine::filter_node_pf(const PodReq& req, int32_t idx, uint64_t* pn, uint
   }
   // PodTopologySpread runs after the built-in filters (a Python filter in the hybrid runner,
   // where every native filter comes first): same first-failing reason on both paths
-  if (pf && !pf->cons.empty()) return spread_filter(req, n, *pf);
+  if (pf && !pf->cons.empty()) {
+    const Reason r = spread_filter(req, n, *pf);
+    if (r != RS_OK) return r;
+  }
+  if (ip && ip->active) return interpod_filter(req, n, *ip);
   return RS_OK;
 }
 
@@ -859,6 +892,12 @@ std::vector<int32_t> Engine::feasible_nodes(const PodReq& req, const std::vector
     spread_prefilter(req, &pf_store);
     pf = &pf_store;
   }
+  InterPodPF ip_store;
+  const InterPodPF* ip = nullptr;
+  if (wants_interpod_filter(req)) {
+    interpod_prefilter(req, &ip_store);
+    ip = &ip_store;
+  }
   std::vector<int8_t> res;
   int32_t processed = 0;
   // chunks big enough to amortise a parallel_for (>= 512 nodes) yet small enough that the
@@ -870,7 +909,7 @@ std::vector<int32_t> Engine::feasible_nodes(const PodReq& req, const std::vector
     auto body = [&](int b, int e) {
       for (int j = b; j < e; ++j) {
         int32_t idx = all[(start + base + j) % N];
-        res[j] = (int8_t)filter_node_pf(req, idx, nullptr, nullptr, nullptr, pf);
+        res[j] = (int8_t)filter_node_pf(req, idx, nullptr, nullptr, nullptr, pf, ip);
       }
     };
     if (pool_ && len >= 512) pool_->parallel_for(len, 64, body);
@@ -980,19 +1019,7 @@ std::vector<int64_t> Engine::score_nodes(const PodReq& req, const std::vector<in
   if (score_w_[S_IMAGE_LOCALITY] && images_matter(req)) {
     // plugins/node_extras.py ImageLocality (upstream v1.20 imagelocality): Σ size × spread,
     // spread = nodes holding the image / all nodes, clamped to [23 MB, 1000 MB × containers]
-    const double all = (double)std::max<int32_t>(1, live_);
-    const int64_t lo = 23LL << 20, hi = (1000LL << 20) * std::max<int32_t>(1, req.containers);
-    for (size_t i = 0; i < F; ++i) {
-      const Node& n = nodes_[feas[i]];
-      int64_t sum = 0;
-      for (int32_t im : req.images) {
-        auto it = std::lower_bound(n.images.begin(), n.images.end(), std::make_pair(im, INT64_MIN));
-        if (it != n.images.end() && it->first == im && it->second)
-          sum += (int64_t)((double)it->second * ((double)image_nodes(im) / all));
-      }
-      sum = std::min(std::max(sum, lo), hi);
-      total[i] += score_w_[S_IMAGE_LOCALITY] * (kMaxNodeScore * (sum - lo) / (hi - lo));
-    }
+    for (size_t i = 0; i < F; ++i) total[i] += score_w_[S_IMAGE_LOCALITY] * image_score(req, nodes_[feas[i]]);
   }
   if (score_w_[S_PREFER_AVOID]) {
     // plugins/node_extras.py NodePreferAvoidPods: 0 where the node's preferAvoidPods
@@ -1012,7 +1039,180 @@ std::vector<int64_t> Engine::score_nodes(const PodReq& req, const std::vector<in
     spread_scores(req, feas, s);
     for (size_t i = 0; i < F; ++i) total[i] += s[i] * score_w_[S_SPREAD];
   }
+  if (score_w_[S_INTERPOD]) {
+    interpod_scores(req, feas, s);
+    for (size_t i = 0; i < F; ++i) total[i] += s[i] * score_w_[S_INTERPOD];
+  }
   return total;
+}
+
+// ============================================================== default plugins: inter-pod affinity
+bool Engine::wants_interpod_filter(const PodReq& req) const {
+  if (!(filters_ & F_INTERPOD)) return false;
+  if (req.aff && (!req.aff->req_aff.empty() || !req.aff->req_anti.empty())) return true;
+  return !anti_holders_.empty();
+}
+
+void Engine::interpod_prefilter(const PodReq& req, InterPodPF* pf) const {
+  // InterPodAffinity.pre_filter (plugins/spread_affinity.py): the (key, value) domains where an
+  // existing pod's required anti-affinity matches this pod; per required term of this pod the
+  // domains holding pods that match it (affinity: pods matching every term)
+  pf->active = true;
+  pf->existing_anti.clear();
+  pf->affinity.clear();
+  pf->anti.clear();
+  pf->any_aff_match = false;
+  for (uint64_t id : anti_holders_) {
+    const Assignment& a = ledger_.at(id);
+    if (a.node < 0 || a.node >= (int32_t)nodes_.size() || !nodes_[a.node].alive) continue;
+    const Node& n = nodes_[a.node];
+    for (const PodTerm& t : a.aff->req_anti) {
+      auto lab = n.labels.find(t.key);
+      if (lab != n.labels.end() && t.matches(req.ns, req.labels)) pf->existing_anti[t.key].insert(lab->second);
+    }
+  }
+  if (!req.aff) return;
+  const auto& aff = req.aff->req_aff;
+  const auto& anti = req.aff->req_anti;
+  if (aff.empty() && anti.empty()) return;
+  bool self = true;
+  for (const PodTerm& t : aff) self = self && t.matches(req.ns, req.labels);
+  pf->self_match = self;
+  for (const Node& n : nodes_) {
+    if (!n.alive || n.pods.empty()) continue;
+    for (uint64_t id : n.pods) {
+      const Assignment& a = ledger_.at(id);
+      if (!aff.empty()) {
+        bool all = true;
+        for (const PodTerm& t : aff)
+          if (!t.matches(a.ns, a.labels)) {
+            all = false;
+            break;
+          }
+        if (all) {
+          pf->any_aff_match = true;
+          for (const PodTerm& t : aff) {
+            auto lab = n.labels.find(t.key);
+            if (lab != n.labels.end()) pf->affinity[pair_key(t.key, lab->second)] += 1;
+          }
+        }
+      }
+      for (const PodTerm& t : anti) {
+        auto lab = n.labels.find(t.key);
+        if (lab != n.labels.end() && t.matches(a.ns, a.labels)) pf->anti[pair_key(t.key, lab->second)] += 1;
+      }
+    }
+  }
+}
+
+Reason Engine::interpod_filter(const PodReq& req, const Node& n, const InterPodPF& pf) const {
+  for (const auto& kv : pf.existing_anti) {
+    auto lab = n.labels.find(kv.first);
+    if (lab != n.labels.end() && kv.second.count(lab->second)) return RS_EXISTING_ANTI;
+  }
+  if (!req.aff) return RS_OK;
+  const auto& aff = req.aff->req_aff;
+  if (!aff.empty()) {
+    bool ok = true, keys = true;
+    for (const PodTerm& t : aff) {
+      auto lab = n.labels.find(t.key);
+      if (lab == n.labels.end()) {
+        ok = keys = false;
+        continue;
+      }
+      auto c = pf.affinity.find(pair_key(t.key, lab->second));
+      if (c == pf.affinity.end() || c->second <= 0) ok = false;
+    }
+    // the first pod of a self-affine group may go to any node carrying the keys
+    if (!ok && !(!pf.any_aff_match && pf.self_match && keys)) return RS_POD_AFFINITY;
+  }
+  for (const PodTerm& t : req.aff->req_anti) {
+    auto lab = n.labels.find(t.key);
+    if (lab == n.labels.end()) continue;
+    auto c = pf.anti.find(pair_key(t.key, lab->second));
+    if (c != pf.anti.end() && c->second > 0) return RS_POD_ANTI;
+  }
+  return RS_OK;
+}
+
+void Engine::interpod_scores(const PodReq& req, const std::vector<int32_t>& feas, std::vector<int64_t>& s) const {
+  // InterPodAffinity.pre_score / score / normalize_score: per (key, value) domain, Σ ± weight of
+  // this pod's preferred terms over the pods there, plus existing pods' required affinity
+  // (hardPodAffinityWeight) and preferred terms that match this pod
+  const size_t F = feas.size();
+  s.assign(F, 0);
+  std::unordered_map<uint64_t, int64_t> dom;   // (key, value) → score
+  std::unordered_set<int32_t> keys;
+  const bool pref = req.aff && (!req.aff->pref_aff.empty() || !req.aff->pref_anti.empty());
+  if (pref) {
+    for (const Node& n : nodes_) {
+      if (!n.alive || n.pods.empty()) continue;
+      for (uint64_t id : n.pods) {
+        const Assignment& a = ledger_.at(id);
+        for (int sign = 1; sign >= -1; sign -= 2)
+          for (const PodTerm& t : sign > 0 ? req.aff->pref_aff : req.aff->pref_anti) {
+            auto lab = n.labels.find(t.key);
+            if (lab == n.labels.end() || !t.matches(a.ns, a.labels)) continue;
+            dom[pair_key(t.key, lab->second)] += sign * (int64_t)t.weight;
+            keys.insert(t.key);
+          }
+      }
+    }
+  }
+  for (uint64_t id : aff_holders_) {
+    const Assignment& a = ledger_.at(id);
+    if (a.node < 0 || a.node >= (int32_t)nodes_.size() || !nodes_[a.node].alive) continue;
+    const Node& n = nodes_[a.node];
+    auto add = [&](const PodTerm& t, int64_t w) {
+      auto lab = n.labels.find(t.key);
+      if (lab == n.labels.end() || !t.matches(req.ns, req.labels)) return;
+      dom[pair_key(t.key, lab->second)] += w;
+      keys.insert(t.key);
+    };
+    if (hard_aff_w_)
+      for (const PodTerm& t : a.aff->req_aff) add(t, hard_aff_w_);
+    for (const PodTerm& t : a.aff->pref_aff) add(t, t.weight);
+    for (const PodTerm& t : a.aff->pref_anti) add(t, -(int64_t)t.weight);
+  }
+  if (keys.empty() || F == 0) return;
+  int64_t hi = INT64_MIN, lo = INT64_MAX;
+  for (size_t i = 0; i < F; ++i) {
+    const Node& n = nodes_[feas[i]];
+    int64_t v = 0;
+    for (int32_t k : keys) {
+      auto lab = n.labels.find(k);
+      if (lab == n.labels.end()) continue;
+      auto d = dom.find(pair_key(k, lab->second));
+      if (d != dom.end()) v += d->second;
+    }
+    s[i] = v;
+    hi = std::max(hi, v);
+    lo = std::min(lo, v);
+  }
+  for (size_t i = 0; i < F; ++i) s[i] = hi == lo ? 0 : floor_div(kMaxNodeScore * (s[i] - lo), hi - lo);
+}
+
+bool Engine::interpod_inert(const PodReq& req) const {
+  if (filters_ & F_INTERPOD) {
+    if (req.aff && (!req.aff->req_aff.empty() || !req.aff->req_anti.empty())) return false;
+    for (uint64_t id : anti_holders_)
+      for (const PodTerm& t : ledger_.at(id).aff->req_anti)
+        if (t.matches(req.ns, req.labels)) return false;
+  }
+  if (score_w_[S_INTERPOD]) {
+    if (req.aff && (!req.aff->pref_aff.empty() || !req.aff->pref_anti.empty())) return false;
+    for (uint64_t id : aff_holders_) {
+      const PodAffinity& x = *ledger_.at(id).aff;
+      if (hard_aff_w_)
+        for (const PodTerm& t : x.req_aff)
+          if (t.matches(req.ns, req.labels)) return false;
+      for (const PodTerm& t : x.pref_aff)
+        if (t.matches(req.ns, req.labels)) return false;
+      for (const PodTerm& t : x.pref_anti)
+        if (t.matches(req.ns, req.labels)) return false;
+    }
+  }
+  return true;
 }
 
 // ============================================================== default plugins: node extras
@@ -1046,6 +1246,11 @@ void Engine::index_node_extras(const Node& n, int sign) {
     int32_t& c = image_nodes_[im.first];
     c += sign;
     if (c <= 0) image_nodes_.erase(im.first);
+    auto& sz = image_sizes_[im.first];
+    int32_t& k = sz[im.second];
+    k += sign;
+    if (k <= 0) sz.erase(im.second);
+    if (sz.empty()) image_sizes_.erase(im.first);
   }
   if (!n.avoid.empty()) avoid_nodes_ += sign;
 }
@@ -1071,6 +1276,42 @@ void Engine::set_node_extras(int32_t idx, std::vector<std::pair<int32_t, int64_t
 int32_t Engine::image_nodes(int32_t image) const {
   auto it = image_nodes_.find(image);
   return it == image_nodes_.end() ? 0 : it->second;
+}
+
+int64_t Engine::image_score(const PodReq& req, const Node& n) const {
+  const double all = (double)std::max<int32_t>(1, live_);
+  const int64_t lo = 23LL << 20, hi = (1000LL << 20) * std::max<int32_t>(1, req.containers);
+  int64_t sum = 0;
+  for (int32_t im : req.images) {
+    auto it = std::lower_bound(n.images.begin(), n.images.end(), std::make_pair(im, INT64_MIN));
+    if (it != n.images.end() && it->first == im && it->second)
+      sum += (int64_t)((double)it->second * ((double)image_nodes(im) / all));
+  }
+  sum = std::min(std::max(sum, lo), hi);
+  return kMaxNodeScore * (sum - lo) / (hi - lo);
+}
+
+bool Engine::image_score_const(const PodReq& req, int64_t* v) const {
+  *v = 0;
+  if (!score_w_[S_IMAGE_LOCALITY] || !images_matter(req)) return true;
+  for (int32_t im : req.images) {
+    auto c = image_nodes_.find(im);
+    if (c == image_nodes_.end()) continue;
+    if (c->second != live_) return false;
+    auto sz = image_sizes_.find(im);
+    if (sz == image_sizes_.end() || sz->second.size() != 1) return false;
+  }
+  for (const Node& n : nodes_)
+    if (n.alive) {
+      *v = score_w_[S_IMAGE_LOCALITY] * image_score(req, n);
+      return true;
+    }
+  return true;
+}
+
+int64_t Engine::ext_amount(const std::vector<std::pair<int32_t, int64_t>>& v, int32_t res) const {
+  auto it = std::lower_bound(v.begin(), v.end(), std::make_pair(res, INT64_MIN));
+  return it != v.end() && it->first == res ? it->second : 0;
 }
 
 bool Engine::images_matter(const PodReq& req) const {
@@ -1205,7 +1446,6 @@ bool Engine::wants_spread_filter(const PodReq& req) const {
   return false;
 }
 
-static inline uint64_t pair_key(int32_t k, int32_t v) { return ((uint64_t)(uint32_t)k << 32) | (uint32_t)v; }
 
 void Engine::spread_prefilter(const PodReq& req, SpreadPF* pf) const {
   // PodTopologySpread.pre_filter (plugins/spread_affinity.py): counts per (key, value) pair —
@@ -1254,11 +1494,6 @@ bool Engine::spread_soft_constant(const std::vector<SpreadC>& soft) const {
   return false;
 }
 
-static inline int64_t floor_div(int64_t a, int64_t b) {
-  int64_t q = a / b;
-  if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
-  return q;
-}
 
 void Engine::spread_scores(const PodReq& req, const std::vector<int32_t>& feas, std::vector<int64_t>& s) const {
   // PodTopologySpread pre_score / score / normalize_score (plugins/spread_affinity.py)
@@ -1512,6 +1747,8 @@ bool Engine::pack_node(int32_t idx, void* out) const {
   row->req_mem = n.req_mem;
   row->nz_cpu = n.nz_cpu_m;
   row->nz_mem = n.nz_mem;
+  row->ext_alloc = ext_amount(n.ext_alloc, dev_ext_res_);
+  row->ext_used = ext_amount(n.ext_used, dev_ext_res_);
   row->pod_count = n.pod_count;
   if (n.alloc_mem > (int64_t)1 << 56 || n.alloc_cpu_m > (int64_t)1 << 56) return false;
   for (size_t c = 0; c < n.cards.size(); ++c) {
@@ -1574,8 +1811,12 @@ bool Engine::device_eligible(const PodReq& req) const {
   if (!default_alloc_weights()) return false;                    // device computes (c + m) / 2
   // default-plugin terms the device row does not carry: only pods for which they are a
   // constant (or nothing) go to the device
-  if ((filters_ & F_NODE_RESOURCES_FIT) && !req.ext.empty()) return false;
-  if (score_w_[S_IMAGE_LOCALITY] && images_matter(req)) return false;
+  if ((filters_ & F_NODE_RESOURCES_FIT) && !req.ext.empty())
+    for (const auto& r : req.ext)   // the device carries one extended resource dimension
+      if (r.first != dev_ext_res_ && ext_checked(r.first)) return false;
+  int64_t img;
+  if (!image_score_const(req, &img)) return false;
+  if (!interpod_inert(req)) return false;
   if (score_w_[S_PREFER_AVOID] && req.avoid_kind && avoid_nodes_ > 0) return false;
   if (wants_spread_filter(req)) {
     std::vector<SpreadC> hard;
@@ -1619,8 +1860,12 @@ void Engine::make_dev_req(const PodReq& req, yoda_dev_req_t* out) {
   d.w_most = score_w_[S_MOST_ALLOCATED];
   // no PreferNoSchedule taints anywhere: TaintToleration normalises every node to 100
   d.w_const = score_w_[S_TAINT_TOLERATION] * kMaxNodeScore;
-  // NodePreferAvoidPods scores every node 100 for a device-eligible pod (device_eligible)
+  // NodePreferAvoidPods scores every node 100 for a device-eligible pod (device_eligible), and
+  // ImageLocality scores every node alike (image_score_const)
   d.w_const += score_w_[S_PREFER_AVOID] * kMaxNodeScore;
+  int64_t img = 0;
+  if (image_score_const(req, &img)) d.w_const += img;
+  d.ext = ((filters_ & F_NODE_RESOURCES_FIT) && ext_checked(dev_ext_res_)) ? ext_amount(req.ext, dev_ext_res_) : 0;
   d.w_link = wt_.w_link;
   d.w_numa = wt_.w_numa;
   d.w_fit = wt_.w_fit;

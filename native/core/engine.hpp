@@ -13,6 +13,7 @@
 #pragma once
 
 #include "yoda_dev_abi.h"
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -20,8 +21,10 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <memory>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 namespace yoda {
@@ -42,6 +45,7 @@ enum FilterBit : uint32_t {
   F_NODE_RESOURCES_FIT = 1u << 4,
   F_YODA = 1u << 5,
   F_SPREAD = 1u << 6,          // PodTopologySpread DoNotSchedule constraints (explicit or profile defaults)
+  F_INTERPOD = 1u << 7,        // InterPodAffinity: required (anti-)affinity, existing pods' anti-affinity
 };
 enum ScoreIdx : int {
   S_YODA = 0,
@@ -53,7 +57,8 @@ enum ScoreIdx : int {
   S_IMAGE_LOCALITY = 6,
   S_PREFER_AVOID = 7,          // NodePreferAvoidPods
   S_SPREAD = 8,                // PodTopologySpread ScheduleAnyway constraints (explicit or profile defaults)
-  S_NUM = 9,
+  S_INTERPOD = 9,              // InterPodAffinity: preferred terms both ways + hardPodAffinityWeight
+  S_NUM = 10,
 };
 
 // Why a node was rejected (first failing plugin), reported for FitError diagnosis.
@@ -63,6 +68,9 @@ enum Reason : int8_t {
   RS_EXT_RESOURCES,            // NodeResourcesFit: a resource beyond cpu/memory/pods
   RS_SPREAD,                   // PodTopologySpread: skew
   RS_SPREAD_LABEL,             // PodTopologySpread: the node lacks a constraint's topology key
+  RS_EXISTING_ANTI,            // InterPodAffinity: an existing pod's required anti-affinity
+  RS_POD_AFFINITY,             // InterPodAffinity: the pod's required affinity
+  RS_POD_ANTI,                 // InterPodAffinity: the pod's required anti-affinity
   RS_NUM
 };
 
@@ -109,6 +117,23 @@ struct SpreadC {
   bool hard = true;            // DoNotSchedule (filter) vs ScheduleAnyway (score)
   LSel sel;
 };
+// One pod (anti-)affinity term (plugins/spread_affinity.py InterPodAffinity): topology key, the
+// namespaces it selects pods in (the owner's own when the term lists none) and the selector
+struct PodTerm {
+  int32_t key = 0;
+  std::vector<int32_t> ns;
+  LSel sel;
+  int32_t weight = 1;          // preferred terms
+  bool matches(int32_t pod_ns, const Labels& l) const {
+    return std::find(ns.begin(), ns.end(), pod_ns) != ns.end() && sel.matches(l);
+  }
+};
+// A pod's inter-pod affinity (shared by its request and its ledger entry)
+struct PodAffinity {
+  std::vector<PodTerm> req_aff, req_anti, pref_aff, pref_anti;
+  bool empty() const { return req_aff.empty() && req_anti.empty() && pref_aff.empty() && pref_anti.empty(); }
+};
+
 // A profile's default constraint (PodTopologySpread args: System defaults or a List); its
 // selector is the pod's DefaultSelector (Services + controller)
 struct DefaultSpread {
@@ -178,6 +203,8 @@ struct PodReq {
   // constraints do not apply, even for an action none of them has)
   bool spread_explicit = false;
   std::vector<SpreadC> spread;
+  // InterPodAffinity: the pod's (anti-)affinity terms (null: none)
+  std::shared_ptr<const PodAffinity> aff;
 };
 
 struct Weights {
@@ -216,6 +243,7 @@ struct Assignment {
   Labels labels;
   bool deleting = false;
   std::vector<std::pair<int32_t, int64_t>> ext;   // extended resources it holds on the node
+  std::shared_ptr<const PodAffinity> aff;          // its (anti-)affinity terms (symmetric rule, scoring)
 };
 
 struct CycleResult {
@@ -255,13 +283,14 @@ class ThreadPool {
 // per profile and swaps it in around its batches, restoring the caller's afterwards.
 struct EngineConfig {
   uint32_t filters = 0;
-  int64_t score_w[S_NUM] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int64_t score_w[S_NUM] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   int64_t alloc_w[2][3] = {{1, 1, 0}, {1, 1, 0}};
   Weights wt;
   double settle_s = 30.0;
   std::vector<DefaultSpread> spread_defaults;   // PodTopologySpread default constraints
   std::vector<int32_t> ext_ignored;             // NodeResourcesFit ignoredResources
   std::vector<std::string> ext_ignored_groups;  // NodeResourcesFit ignoredResourceGroups
+  int64_t hard_pod_affinity_weight = 1;         // InterPodAffinity args
 };
 
 class Engine {
@@ -391,9 +420,29 @@ class Engine {
   // pods on node idx holding a reservation, in namespace ns, not terminating, matching sel
   int64_t count_matching(int32_t idx, int32_t ns, const LSel& sel) const;
 
+  // ---- InterPodAffinity pieces (exposed for parity tests)
+  struct InterPodPF {
+    bool active = false;
+    std::unordered_map<int32_t, std::unordered_set<int32_t>> existing_anti;   // key → blocked values
+    std::unordered_map<uint64_t, int64_t> affinity, anti;                      // (key << 32 | value) → pods
+    bool any_aff_match = false, self_match = false;
+  };
+  void interpod_prefilter(const PodReq& req, InterPodPF* pf) const;
+  Reason interpod_filter(const PodReq& req, const Node& n, const InterPodPF& pf) const;
+  void interpod_scores(const PodReq& req, const std::vector<int32_t>& feas, std::vector<int64_t>& s) const;
+  size_t affinity_holders() const { return aff_holders_.size(); }
+  void set_hard_pod_affinity_weight(int64_t w) { hard_aff_w_ = w; }
+
   // ---- profile configuration of the default plugins beyond the score weights
   void set_spread_defaults(std::vector<DefaultSpread> d) { spread_defaults_ = std::move(d); }
   const std::vector<DefaultSpread>& spread_defaults() const { return spread_defaults_; }
+  // the one extended resource the device rows carry (default ephemeral-storage): pods whose only
+  // checked extended request is this one stay device-eligible
+  void set_device_ext_resource(int32_t res) {
+    dev_ext_res_ = res;
+    for (int32_t i = 0; i < (int32_t)nodes_.size(); ++i) mark_dirty(i);
+  }
+  int32_t device_ext_resource() const { return dev_ext_res_; }
   void set_ext_ignored(std::vector<int32_t> res, std::vector<std::string> groups) {
     ext_ignored_ = std::move(res);
     ext_ignored_groups_ = std::move(groups);
@@ -445,14 +494,23 @@ class Engine {
   void spread_prefilter(const PodReq& req, SpreadPF* pf) const;
   Reason spread_filter(const PodReq& req, const Node& n, const SpreadPF& pf) const;
   Reason filter_node_pf(const PodReq& req, int32_t idx, uint64_t* n, uint64_t* m, uint64_t* c,
-                        const SpreadPF* pf) const;
+                        const SpreadPF* pf, const InterPodPF* ip = nullptr) const;
   bool wants_spread_filter(const PodReq& req) const;
+  bool wants_interpod_filter(const PodReq& req) const;
+  // InterPodAffinity is a constant (no filter, equal scores) for this pod: device-eligible
+  bool interpod_inert(const PodReq& req) const;
   bool ext_checked(int32_t res) const;
   // normalized PodTopologySpread scores of the feasible nodes (soft constraints)
   void spread_scores(const PodReq& req, const std::vector<int32_t>& feas, std::vector<int64_t>& s) const;
   // the soft constraints score every node 0 (no live node carries one of their keys)
   bool spread_soft_constant(const std::vector<SpreadC>& soft) const;
   bool images_matter(const PodReq& req) const;
+  // ImageLocality scores every live node alike for this pod (each of its images is on no node,
+  // or on every node with one size): true and the weighted score in *v
+  bool image_score_const(const PodReq& req, int64_t* v) const;
+  int64_t image_score(const PodReq& req, const Node& n) const;
+  int64_t ext_amount(const std::vector<std::pair<int32_t, int64_t>>& v, int32_t res) const;
+  std::unordered_map<int32_t, std::unordered_map<int64_t, int32_t>> image_sizes_;   // image → size → nodes
   void index_node_extras(const Node& n, int sign);
   void fill_result(const yoda_dev_result_t& res, CycleResult* r) const;
   Reason candidate_reason(const PodReq& req, const Node& n) const;
@@ -467,7 +525,7 @@ class Engine {
   bool compat_;
   uint32_t filters_ = F_NODE_UNSCHEDULABLE | F_NODE_NAME | F_TAINT_TOLERATION | F_NODE_AFFINITY |
                       F_NODE_RESOURCES_FIT | F_YODA;
-  int64_t score_w_[S_NUM] = {300, 1, 1, 1, 1, 0, 0, 0, 0};
+  int64_t score_w_[S_NUM] = {300, 1, 1, 1, 1, 0, 0, 0, 0, 0};
   int64_t alloc_w_[2][3] = {{1, 1, 0}, {1, 1, 0}};   // [least, most][cpu, memory, other]
   Weights wt_;
   int pct_nodes_ = 0;
@@ -508,6 +566,10 @@ class Engine {
     return ((uint64_t)(uint8_t)kind << 58) ^ ((uint64_t)(uint32_t)ns << 29) ^ (uint64_t)(uint32_t)name;
   }
   std::vector<DefaultSpread> spread_defaults_;
+  int32_t dev_ext_res_ = -1;                  // set in the constructor: "ephemeral-storage"
+  int64_t hard_aff_w_ = 1;
+  std::unordered_set<uint64_t> aff_holders_;  // ledger pods with any (anti-)affinity term
+  std::unordered_set<uint64_t> anti_holders_; // ... with a required anti-affinity term
   std::vector<int32_t> ext_ignored_;
   std::vector<std::string> ext_ignored_groups_;
   void* fn_destroy_ = nullptr;

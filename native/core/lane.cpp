@@ -22,7 +22,8 @@ constexpr uint64_t kPatchBit = 1ull << 62;   // with kEventTag: a PodScheduled=F
 const char* const kReasonName[RS_NUM] = {"OK", "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity",
                                          "NodeResourcesFit", "NoScv", "ScvStale", "GpuNumber", "GpuMemory",
                                          "GpuClock", "GpuFit", "NodeGone", "NodeResourcesFitExtended",
-                                         "PodTopologySpread", "PodTopologySpreadLabel"};
+                                         "PodTopologySpread", "PodTopologySpreadLabel", "InterPodAffinityExisting",
+                                         "InterPodAffinity", "InterPodAntiAffinity"};
 const char* reason_text(int i) {
   switch (i) {
     case RS_UNSCHEDULABLE: return "node(s) were unschedulable";
@@ -39,6 +40,9 @@ const char* reason_text(int i) {
     case RS_EXT_RESOURCES: return "node(s) had insufficient extended resources";
     case RS_SPREAD: return "node(s) didn't match pod topology spread constraints";
     case RS_SPREAD_LABEL: return "node(s) didn't match pod topology spread constraints (missing required label)";
+    case RS_EXISTING_ANTI: return "node(s) didn't satisfy existing pods anti-affinity rules";
+    case RS_POD_AFFINITY: return "node(s) didn't match pod affinity rules";
+    case RS_POD_ANTI: return "node(s) didn't match pod anti-affinity rules";
     default: return i >= 0 && i < RS_NUM ? kReasonName[i] : "unknown";
   }
 }
@@ -931,6 +935,33 @@ bool Lane::make_req(const yk::PodProj& p, PodReq* r) {
       x.sel.reqs.push_back(std::move(lr));
     }
     r->spread.push_back(std::move(x));
+  }
+  if (p.has_pod_aff) {
+    auto pa = std::make_shared<PodAffinity>();
+    auto conv = [&](const std::vector<yk::PodProj::PodTermP>& src, std::vector<PodTerm>* dst) {
+      for (const auto& t : src) {
+        PodTerm x;
+        x.key = eng_->intern(t.key);
+        if (t.ns.empty()) x.ns.push_back(r->ns);
+        for (const auto& n : t.ns) x.ns.push_back(eng_->intern(n));
+        x.sel.nothing = !t.has_sel;
+        for (const auto& kv : t.labels) x.sel.reqs.push_back(LReq{eng_->intern(kv.first), kIn, {eng_->intern(kv.second)}});
+        for (const auto& q : t.exprs) {
+          LReq lr;
+          lr.key = eng_->intern(q.key);
+          if (!selop_of(q.op, &lr.op) || lr.op == kGt || lr.op == kLt) return false;
+          for (const auto& v : q.values) lr.values.push_back(eng_->intern(v));
+          x.sel.reqs.push_back(std::move(lr));
+        }
+        x.weight = (int32_t)t.weight;
+        dst->push_back(std::move(x));
+      }
+      return true;
+    };
+    if (!conv(p.aff_req, &pa->req_aff) || !conv(p.anti_req, &pa->req_anti) || !conv(p.aff_pref, &pa->pref_aff) ||
+        !conv(p.anti_pref, &pa->pref_anti))
+      return false;
+    if (!pa->empty()) r->aff = std::move(pa);
   }
   return true;
 }

@@ -44,7 +44,7 @@ constexpr uint32_t F_NODE_UNSCHEDULABLE = 1u << 0;
 constexpr uint32_t F_NODE_RESOURCES_FIT = 1u << 4;
 constexpr uint32_t F_YODA = 1u << 5;
 constexpr int RS_UNSCHEDULABLE = 1, RS_RESOURCES = 5, RS_NO_SCV = 6, RS_STALE = 7, RS_GPU_NUMBER = 8,
-              RS_GPU_FIT = 11, RS_DEAD = 12;
+              RS_GPU_FIT = 11, RS_DEAD = 12, RS_EXT_RESOURCES = 13;
 
 constexpr int kWaves = 4;
 constexpr int kBlock = 64 * kWaves;
@@ -264,6 +264,7 @@ __device__ __forceinline__ int filter_eval(const yoda_dev_node_t* nd, bool valid
   const uint32_t card_number = nd->card_number;
   const int64_t pod_count = nd->pod_count, alloc_pods = nd->alloc_pods, alloc_cpu = nd->alloc_cpu,
                 req_cpu = nd->req_cpu, alloc_mem = nd->alloc_mem, req_mem = nd->req_mem;
+  const int64_t ext_alloc = nd->ext_alloc, ext_used = nd->ext_used;
   const yoda_dev_card_t cd = nd->cards[sub];
   const uint8_t healthy = nd->healthy[sub];
   int reason = 0;
@@ -275,6 +276,8 @@ __device__ __forceinline__ int filter_eval(const yoda_dev_node_t* nd, bool valid
     if (pod_count + 1 > alloc_pods) reason = RS_RESOURCES;
     else if (r.cpu_m > 0 && alloc_cpu < r.cpu_m + req_cpu) reason = RS_RESOURCES;
     else if (r.mem > 0 && alloc_mem < r.mem + req_mem) reason = RS_RESOURCES;
+    // the one extended resource the device rows carry (engine.cpp: the device's ext dimension)
+    else if (r.ext > 0 && ext_used + r.ext > ext_alloc) reason = RS_EXT_RESOURCES;
   }
   if (!reason && cnd) reason = cnd;
   bool yoda_stage = false;
@@ -475,6 +478,7 @@ __device__ void publish(int n, const yoda_dev_req_t& r, unsigned long long key, 
     nd->pod_count += 1;
     nd->req_cpu += r.cpu_m;
     nd->req_mem += r.mem;
+    nd->ext_used += r.ext;
     nd->nz_cpu += r.nz_cpu_m;
     nd->nz_mem += r.nz_mem;
   }
@@ -914,7 +918,7 @@ __global__ __launch_bounds__(kBlock) void k_select(int n, const yoda_dev_req_t r
 //    makes every waiter give up, the host sees `done` missing and falls back.
 constexpr int kMaxNodesPerBlock = 256;    // 256 × 536 B of LDS per block
 constexpr int kRecStride = 16;            // granules per record slot
-constexpr int kRec1 = 11;                 // maxima[6], feasible, 7 reason counts packed 2 × u16
+constexpr int kRec1 = 11;                 // maxima[6], feasible, 8 reason counts packed 2 × u16
 constexpr int kRec2 = 4;                  // raw lo, hi (2 granules each)
 constexpr int kRec3 = 2;                  // best key (2 granules)
 constexpr int kMaxGrid = 256;
@@ -923,8 +927,9 @@ constexpr size_t kBatchRowBytes = sizeof(yoda_dev_node_t) + 8 + 8 + 4 + 6;
 constexpr int kMaxGroups = kMaxNodesPerBlock / kNodesPerWave;   // 8-node filter groups per block
 // reason codes the batch path can produce (no candidate reasons: the engine sends no
 // candidates to batches), packed into granules 7..10 of record 1
-__constant__ int c_batch_reasons[7] = {RS_UNSCHEDULABLE, RS_RESOURCES, RS_NO_SCV, RS_STALE, RS_GPU_NUMBER,
-                                       RS_GPU_FIT, RS_DEAD};
+constexpr int kNR = 8;                    // reason codes a batch can produce (record 1 packs 2 per granule)
+__constant__ int c_batch_reasons[kNR] = {RS_UNSCHEDULABLE, RS_RESOURCES, RS_NO_SCV, RS_STALE, RS_GPU_NUMBER,
+                                         RS_GPU_FIT, RS_DEAD, RS_EXT_RESOURCES};
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned int gu32;
@@ -952,8 +957,9 @@ static_assert(kResWords == 19 && YODA_DEV_REASONS == 16 && offsetof(yoda_dev_res
                   offsetof(yoda_dev_result_t, raw_hi) == 144,
               "the publish step's word layout");
 // the reason codes of c_batch_reasons, for compile-time indexing
-constexpr int kBatchReasonCodes[7] = {RS_UNSCHEDULABLE, RS_RESOURCES, RS_NO_SCV, RS_STALE, RS_GPU_NUMBER,
-                                      RS_GPU_FIT, RS_DEAD};
+constexpr int kBatchReasonCodes[kNR] = {RS_UNSCHEDULABLE, RS_RESOURCES, RS_NO_SCV, RS_STALE, RS_GPU_NUMBER,
+                                        RS_GPU_FIT, RS_DEAD, RS_EXT_RESOURCES};
+static_assert(7 + (kNR + 1) / 2 == kRec1, "record 1: 7 fields + the reason counts as u16 pairs");
 constexpr int kTracePts = 24;   // 9 phase stamps per pod (block 0), 9 of the PAIRS fix-up's owner, padded
 constexpr int kReqWords = sizeof(yoda_dev_req_t) / 4;
 static_assert(sizeof(yoda_dev_req_t) % 4 == 0 && kReqWords <= 64, "req fits one wave");
@@ -1118,9 +1124,9 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   // G ≤ 64: wave 0 holds every record of a gather and reduces it alone; the result reaches the
   // block through these words and one barrier (no per-wave partials, no second barrier)
   __shared__ unsigned long long s_red[2];
-  __shared__ uint32_t s_rec[14][kMaxGrid + 4];   // gather-1 records transposed (+4: bank skew)
+  __shared__ uint32_t s_rec[7 + kNR][kMaxGrid + 4];   // gather-1 records transposed (+4: bank skew)
   // filter aggregates per 8-node group: 6 maxima, feasible count, 7 reason counts
-  __shared__ uint32_t s_grp[kMaxGroups][14];
+  __shared__ uint32_t s_grp[kMaxGroups][7 + kNR];
   __shared__ GangBest s_gang[8 * BW];
   __shared__ int s_fail;
   __shared__ uint32_t s_bfeas;   // this block's feasible nodes for the current pod (record 1)
@@ -1188,15 +1194,15 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       }
       const bool head = sub == 0;
       const uint32_t nf = (uint32_t)__popcll(__ballot(head && fok));
-      uint32_t rc[7];
+      uint32_t rc[kNR];
 #pragma unroll
-      for (int q = 0; q < 7; ++q) rc[q] = (uint32_t)__popcll(__ballot(head && reason == c_batch_reasons[q]));
+      for (int q = 0; q < kNR; ++q) rc[q] = (uint32_t)__popcll(__ballot(head && reason == c_batch_reasons[q]));
       if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) s_grp[gq][k] = wmx[k];
         s_grp[gq][6] = nf;
 #pragma unroll
-        for (int q = 0; q < 7; ++q) s_grp[gq][7 + q] = rc[q];
+        for (int q = 0; q < kNR; ++q) s_grp[gq][7 + q] = rc[q];
       }
   };
   auto filter_groups = [&](const yoda_dev_req_t& rq, int par) {
@@ -1217,7 +1223,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         uint32_t lo = 0, hi = 0;
         for (int q = 0; q < ngr; ++q) {
           lo += s_grp[q][r0];
-          hi += r0 + 1 < 14 ? s_grp[q][r0 + 1] : 0u;
+          hi += r0 + 1 < 7 + kNR ? s_grp[q][r0 + 1] : 0u;
         }
         v = lo | (hi << 16);
       }
@@ -1361,6 +1367,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     nd->pod_count += 1;
     nd->req_cpu += rq.cpu_m;
     nd->req_mem += rq.mem;
+    nd->ext_used += rq.ext;
     nd->nz_cpu += rq.nz_cpu_m;
     nd->nz_mem += rq.nz_mem;
     s_dirty[j] = 1;
@@ -1485,13 +1492,13 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
 #pragma unroll
               for (int k = 0; k < 7; ++k) s_rec[k][lane] = v[k];
 #pragma unroll
-              for (int q = 0; q < 7; ++q) s_rec[7 + q][lane] = (q & 1) ? (v[7 + q / 2] >> 16) : (v[7 + q / 2] & 0xFFFFu);
+              for (int q = 0; q < kNR; ++q) s_rec[7 + q][lane] = (q & 1) ? (v[7 + q / 2] >> 16) : (v[7 + q / 2] & 0xFFFFu);
             }
             if (t2 < G && t2 != gi) {
 #pragma unroll
               for (int k = 0; k < 7; ++k) s_rec[k][t2] = v2[k];
 #pragma unroll
-              for (int q = 0; q < 7; ++q) s_rec[7 + q][t2] = (q & 1) ? (v2[7 + q / 2] >> 16) : (v2[7 + q / 2] & 0xFFFFu);
+              for (int q = 0; q < kNR; ++q) s_rec[7 + q][t2] = (q & 1) ? (v2[7 + q / 2] >> 16) : (v2[7 + q / 2] & 0xFFFFu);
             }
           } else if (lane == 0) {
             s_fail = 1;
@@ -1507,7 +1514,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
             } else {
               const int q0 = 2 * (tid - 7);
               s_rec[7 + q0][gi] = own & 0xFFFFu;
-              if (q0 + 1 < 7) s_rec[8 + q0][gi] = own >> 16;
+              if (q0 + 1 < kNR) s_rec[8 + q0][gi] = own >> 16;
             }
           }
           if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 10] = __builtin_amdgcn_s_memrealtime();
@@ -1541,12 +1548,12 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           ok = false;
           break;
         }
-        // transpose through LDS (14 fields × G), then 16 threads per field reduce it
+        // transpose through LDS (7 + kNR fields × G), then 16 threads per field reduce it
         if (tid < G) {
 #pragma unroll
           for (int k = 0; k < 7; ++k) s_rec[k][tid] = v[k];
 #pragma unroll
-          for (int q = 0; q < 7; ++q) s_rec[7 + q][tid] = (q & 1) ? (v[7 + q / 2] >> 16) : (v[7 + q / 2] & 0xFFFFu);
+          for (int q = 0; q < kNR; ++q) s_rec[7 + q][tid] = (q & 1) ? (v[7 + q / 2] >> 16) : (v[7 + q / 2] & 0xFFFFu);
         }
         __syncthreads();
       } else if (s_fail) {   // (PAIRS owner: wave 0 gathered before the fix-up barrier)
@@ -1554,7 +1561,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         break;
       }
       const int f = tid >> 4, seg = tid & 15;
-      if (f < 14) {   // waves 0..3 cover fields 0..15; f is uniform per 16 lanes
+      if (f < 7 + kNR) {   // waves 0..3 cover fields 0..15; f is uniform per 16 lanes
         const bool is_max = f < 6;
         uint32_t acc = is_max ? 1u : 0u;
         for (int t = seg; t < G; t += 16) {
@@ -1575,9 +1582,9 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       __syncthreads();
     }
     if (PAIRS && fix >= 0 && a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 12] = __builtin_amdgcn_s_memrealtime();
-    int reasons7[7];
+    int reasons7[kNR];
 #pragma unroll
-    for (int q = 0; q < 7; ++q) reasons7[q] = (int)s_glob[7 + q];
+    for (int q = 0; q < kNR; ++q) reasons7[q] = (int)s_glob[7 + q];
     const int nf = (int)s_glob[6];
     const uint64_t gmx[6] = {s_glob[0], s_glob[1], s_glob[2], s_glob[3], s_glob[4], s_glob[5]};
     score_consts_maxima(sc, gmx);
@@ -1760,7 +1767,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         if (tid == 1) w = (uint64_t)(nf > 1 ? (int64_t)(key >> 24) : 0);   // a lone feasible node scores 0
         if (tid == 2) w = (uint64_t)mask | ((uint64_t)(uint32_t)quality << 32);
 #pragma unroll
-        for (int q = 0; q < 7; ++q) {   // reasons[code] as u32 pairs in words 3..10
+        for (int q = 0; q < kNR; ++q) {   // reasons[code] as u32 pairs in words 3..10
           const int code = kBatchReasonCodes[q];
           if (tid == 3 + code / 2) w |= (uint64_t)(uint32_t)reasons7[q] << (32 * (code & 1));
         }

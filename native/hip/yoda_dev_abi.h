@@ -38,7 +38,7 @@ typedef struct {
   uint32_t card_number;                      // 4  (Scv.Status.CardNumber)
   uint8_t ncards, nphys, flags, pad0;        // 4
   int64_t nz_cpu, nz_mem;                    // 16 Σ non-zero requests (scores)
-  uint8_t pad[16];
+  int64_t ext_alloc, ext_used;               // 16 the device's one extended resource (engine: dev_ext_res_)
 } yoda_dev_node_t;   // 512 B
 #ifdef __cplusplus
 static_assert(sizeof(yoda_dev_node_t) == 512, "node record must stay 512 B");
@@ -60,6 +60,7 @@ typedef struct {
   uint32_t use_candidates;   // 1: per-node first-failing NodeName/Affinity/Taint reason uploaded
   uint32_t perm_mul, perm_add, perm_inv;   // random tie-break: p(i) = (i*mul + add) mod 2^24
   uint32_t dev_flags;     // set by the device context, not the engine
+  int64_t ext;            // request of the device's extended resource (0: none)
 } yoda_dev_req_t;
 
 typedef struct {

@@ -32,6 +32,42 @@ py::list term_list(const TermP& t) {
 }
 
 // positional arguments of PodInfo's fast constructor (yoda_scheduler_amd/kube/native.py)
+// LabelSelector.native() tuple of a projected selector (sorted, de-duplicated expression values)
+py::object sel_tuple(bool has, const std::vector<KV>& labels, const std::vector<SelReqP>& exprs) {
+  if (!has) return py::none();
+  py::list lab, ex;
+  for (const auto& kv : labels) lab.append(py::make_tuple(py::str(kv.first), py::str(kv.second)));
+  for (const auto& e : exprs) {
+    std::vector<std::string> vals = e.values;
+    std::sort(vals.begin(), vals.end());
+    vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+    py::tuple vt(vals.size());
+    for (size_t i = 0; i < vals.size(); ++i) vt[i] = py::str(vals[i]);
+    ex.append(py::make_tuple(py::str(e.key), py::str(e.op), vt));
+  }
+  return py::make_tuple(py::none(), false, py::tuple(lab), py::tuple(ex));
+}
+
+// (required affinity, required anti, preferred affinity, preferred anti) of
+// (topologyKey, namespaces | None, selector | None, weight), or None without pod (anti-)affinity
+py::object pod_aff_tuple(const PodProj& p) {
+  if (!p.has_pod_aff) return py::none();
+  auto lst = [](const std::vector<PodProj::PodTermP>& v) {
+    py::list out;
+    for (const auto& t : v) {
+      py::object ns = py::none();
+      if (!t.ns.empty()) {
+        py::tuple nt(t.ns.size());
+        for (size_t i = 0; i < t.ns.size(); ++i) nt[i] = py::str(t.ns[i]);
+        ns = std::move(nt);
+      }
+      out.append(py::make_tuple(py::str(t.key), ns, sel_tuple(t.has_sel, t.labels, t.exprs), t.weight));
+    }
+    return out;
+  };
+  return py::make_tuple(lst(p.aff_req), lst(p.anti_req), lst(p.aff_pref), lst(p.anti_pref));
+}
+
 py::tuple info_args(const PodProj& p) {
   py::object ann = p.has_annotations ? kv_dict(p.annotations) : py::none();
   py::object nsel = p.has_node_selector ? kv_dict(p.node_selector) : py::none();
@@ -77,27 +113,15 @@ py::tuple info_args(const PodProj& p) {
     static const char* kWhen[3] = {"DoNotSchedule", "ScheduleAnyway", "?"};
     py::list l;
     for (const auto& c : p.spread) {
-      py::object sel = py::none();
-      if (c.has_sel) {
-        py::list lab, ex;
-        for (const auto& kv : c.labels) lab.append(py::make_tuple(py::str(kv.first), py::str(kv.second)));
-        for (const auto& e : c.exprs) {
-          std::vector<std::string> vals = e.values;
-          std::sort(vals.begin(), vals.end());
-          vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
-          py::tuple vt(vals.size());
-          for (size_t i = 0; i < vals.size(); ++i) vt[i] = py::str(vals[i]);
-          ex.append(py::make_tuple(py::str(e.key), py::str(e.op), vt));
-        }
-        sel = py::make_tuple(py::none(), false, py::tuple(lab), py::tuple(ex));
-      }
+      py::object sel = sel_tuple(c.has_sel, c.labels, c.exprs);
       l.append(py::make_tuple(py::str(c.key), c.max_skew, py::str(kWhen[c.when]), sel));
     }
     spread = std::move(l);
   }
   return py::make_tuple(py::str(p.uid), py::str(p.ns), py::str(p.name), kv_dict(p.labels), ann, py::str(p.sched),
                         py::str(p.node), p.cpu, p.mem, p.nzc, p.nzm, p.priority, nsel, req, pref, tols, ports,
-                        p.flags, py::str(p.creation), ext, images, p.containers, owner, avoid, spread, p.deleting);
+                        p.flags, py::str(p.creation), ext, images, p.containers, owner, avoid, spread, p.deleting,
+                        pod_aff_tuple(p));
 }
 
 std::shared_ptr<PodEv> project_bytes(const std::string& raw) {

@@ -195,6 +195,67 @@ bool kvs(N m, std::vector<KV>& out) {
   });
 }
 
+// metav1.LabelSelector (models/selectors.py::LabelSelector): matchLabels + matchExpressions with
+// In / NotIn / Exists / DoesNotExist; false on a shape the Python path must decide
+template <class N>
+bool label_selector_of(N ls, std::vector<KV>& labels, std::vector<SelReqP>& exprs) {
+  if (!ls.obj()) return false;
+  N ml = ls.get("matchLabels");
+  if (ml && ml.truthy() && !kvs(ml, labels)) return false;
+  if (N me = ls.get("matchExpressions"); me && me.truthy()) {
+    if (!me.arr()) return false;
+    return me.each([&](std::string_view, N e) {
+      if (!e.obj()) return false;
+      SelReqP r;
+      N ek = e.get("key");
+      if (ek && !ek.str_t()) return false;
+      r.key = ek ? std::string(ek.str()) : "";
+      N op = e.get("operator");
+      if (op && !op.str_t()) return false;
+      r.op = op ? std::string(op.str()) : "In";
+      if (r.op != "In" && r.op != "NotIn" && r.op != "Exists" && r.op != "DoesNotExist") return false;
+      N vs = e.get("values");
+      if (vs && vs.truthy()) {
+        if (!vs.arr()) return false;
+        if (!vs.each([&](std::string_view, N v) {
+              if (!v.str_t()) return false;
+              r.values.emplace_back(v.str());
+              return true;
+            }))
+          return false;
+      }
+      exprs.push_back(std::move(r));
+      return true;
+    });
+  }
+  return true;
+}
+
+// one PodAffinityTerm: topologyKey, namespaces, labelSelector
+template <class N>
+bool pod_term_of(N t, PodProj::PodTermP& x) {
+  if (!t || t.null_t()) return true;            // `or {}`: an empty term
+  if (!t.obj()) return false;
+  N k = t.get("topologyKey");
+  if (k && !k.str_t() && !k.null_t()) return false;
+  x.key = k && k.str_t() ? std::string(k.str()) : "";
+  if (N ns = t.get("namespaces"); ns && ns.truthy()) {
+    if (!ns.arr()) return false;
+    if (!ns.each([&](std::string_view, N v) {
+          if (!v.str_t()) return false;
+          x.ns.emplace_back(v.str());
+          return true;
+        }))
+      return false;
+  }
+  N ls = t.get("labelSelector");
+  if (ls && !ls.null_t()) {
+    x.has_sel = true;
+    if (!label_selector_of(ls, x.labels, x.exprs)) return false;
+  }
+  return true;
+}
+
 template <class N>
 uint64_t meta_hash(N meta) {
   uint64_t h = 0x51ed270b27cd1f47ull;
@@ -483,6 +544,44 @@ void project_generic(N pod, PodProj& p) {
     if (paa && paa.obj()) {
       if (N r = paa.get("requiredDuringSchedulingIgnoredDuringExecution"); r && r.truthy()) flags |= PF_REQ_ANTI;
     }
+    // the terms themselves (native InterPodAffinity)
+    auto terms_of = [&](N kind, std::vector<PodProj::PodTermP>& req, std::vector<PodProj::PodTermP>& pref) -> bool {
+      if (!kind || !kind.truthy()) return true;
+      if (!kind.obj()) return false;
+      if (N r = kind.get("requiredDuringSchedulingIgnoredDuringExecution"); r && r.truthy()) {
+        if (!r.arr()) return false;
+        if (!r.each([&](std::string_view, N t) {
+              PodProj::PodTermP x;
+              if (!pod_term_of(t, x)) return false;
+              req.push_back(std::move(x));
+              return true;
+            }))
+          return false;
+      }
+      if (N r = kind.get("preferredDuringSchedulingIgnoredDuringExecution"); r && r.truthy()) {
+        if (!r.arr()) return false;
+        if (!r.each([&](std::string_view, N w) {
+              if (!w.obj()) return false;
+              PodProj::PodTermP x;
+              if (N wv = w.get("weight")) {
+                bool iok;
+                if (!wv.num_t()) return false;
+                x.weight = wv.as_int(&iok);
+                if (!iok) return false;
+              }
+              N t = w.get("podAffinityTerm");
+              if (!pod_term_of(t && t.truthy() ? t : N{}, x)) return false;
+              pref.push_back(std::move(x));
+              return true;
+            }))
+          return false;
+      }
+      return true;
+    };
+    if ((pa && pa.truthy()) || (paa && paa.truthy())) {
+      p.has_pod_aff = true;
+      if (!terms_of(pa, p.aff_req, p.aff_pref) || !terms_of(paa, p.anti_req, p.anti_pref)) return;
+    }
   }
   if (N tols = sp.get("tolerations"); tols && tols.truthy()) {
     if (!tols.arr()) return;
@@ -530,37 +629,8 @@ void project_generic(N pod, PodProj& p) {
       if (x.when == 0) flags |= PF_SPREAD_HARD;
       N ls = c.get("labelSelector");
       if (ls && !ls.null_t()) {
-        if (!ls.obj()) return false;
         x.has_sel = true;
-        N ml = ls.get("matchLabels");
-        if (ml && ml.truthy() && !kvs(ml, x.labels)) return false;
-        if (N me = ls.get("matchExpressions"); me && me.truthy()) {
-          if (!me.arr()) return false;
-          bool eok = me.each([&](std::string_view, N e) {
-            if (!e.obj()) return false;
-            SelReqP r;
-            N ek = e.get("key");
-            if (ek && !ek.str_t()) return false;
-            r.key = ek ? std::string(ek.str()) : "";
-            N op = e.get("operator");
-            if (op && !op.str_t()) return false;
-            r.op = op ? std::string(op.str()) : "In";
-            if (r.op != "In" && r.op != "NotIn" && r.op != "Exists" && r.op != "DoesNotExist") return false;
-            N vs = e.get("values");
-            if (vs && vs.truthy()) {
-              if (!vs.arr()) return false;
-              if (!vs.each([&](std::string_view, N v) {
-                    if (!v.str_t()) return false;
-                    r.values.emplace_back(v.str());
-                    return true;
-                  }))
-                return false;
-            }
-            x.exprs.push_back(std::move(r));
-            return true;
-          });
-          if (!eok) return false;
-        }
+        if (!label_selector_of(ls, x.labels, x.exprs)) return false;
       }
       p.spread.push_back(std::move(x));
       return true;
@@ -958,6 +1028,11 @@ void merge_non_identity(PodProj& d, PodProj&& s) {
   d.avoid_kind = std::move(s.avoid_kind);
   d.avoid_uid = std::move(s.avoid_uid);
   d.spread = std::move(s.spread);
+  d.has_pod_aff = s.has_pod_aff;
+  d.aff_req = std::move(s.aff_req);
+  d.anti_req = std::move(s.anti_req);
+  d.aff_pref = std::move(s.aff_pref);
+  d.anti_pref = std::move(s.anti_pref);
   d.flags = s.flags;
   d.spec_meta_hash = s.spec_meta_hash;
   d.ok = s.ok;

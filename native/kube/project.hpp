@@ -88,6 +88,17 @@ struct PodProj {
     std::vector<SelReqP> exprs;
   };
   std::vector<SpreadP> spread;
+  // spec.affinity.podAffinity / podAntiAffinity terms (plugins/spread_affinity.py::_terms)
+  struct PodTermP {
+    std::string key;
+    std::vector<std::string> ns;    // empty: the pod's own namespace
+    bool has_sel = false;           // false: nil labelSelector (matches nothing)
+    std::vector<KV> labels;
+    std::vector<SelReqP> exprs;
+    int64_t weight = 1;
+  };
+  bool has_pod_aff = false;
+  std::vector<PodTermP> aff_req, anti_req, aff_pref, anti_pref;
 };
 
 // Quantity → ceil(q × 10^scale) with exact decimal arithmetic (scale 3: CPU millicores,

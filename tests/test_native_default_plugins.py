@@ -341,3 +341,83 @@ def test_extended_resource_fit_native_equals_python(allocs, bound, request, args
         got = eng.filter_node(req, eng.node_index(n))
         assert got in (0, ext_reason)
         assert (got == 0) == want, (n, request, args)
+
+
+# ============================================================== InterPodAffinity
+from yoda_scheduler_amd.plugins.spread_affinity import InterPodAffinity  # noqa: E402
+
+_term_sel = st.one_of(st.none(), st.fixed_dictionaries({}, optional={
+    "matchLabels": st.dictionaries(st.sampled_from(["app", "tier"]), st.sampled_from(["a", "b"]), max_size=1),
+    "matchExpressions": st.lists(st.fixed_dictionaries({
+        "key": st.sampled_from(["app", "tier"]), "operator": st.sampled_from(["In", "NotIn", "Exists"]),
+        "values": st.lists(st.sampled_from(["a", "b"]), min_size=1, max_size=2)}), max_size=1)}))
+_pterm = st.fixed_dictionaries({"topologyKey": st.sampled_from([HOST, ZONE, RACK]), "labelSelector": _term_sel},
+                               optional={"namespaces": st.lists(st.sampled_from(["default", "ml"]), max_size=2)})
+_kind_terms = st.fixed_dictionaries({}, optional={
+    "requiredDuringSchedulingIgnoredDuringExecution": st.lists(_pterm, min_size=1, max_size=2),
+    "preferredDuringSchedulingIgnoredDuringExecution": st.lists(
+        st.fixed_dictionaries({"weight": st.integers(1, 100), "podAffinityTerm": _pterm}), min_size=1, max_size=2)})
+_affinity = st.fixed_dictionaries({}, optional={"podAffinity": _kind_terms, "podAntiAffinity": _kind_terms})
+
+
+@st.composite
+def _aff_clusters(draw):
+    n = draw(st.integers(1, 5))
+    nodes = []
+    for i in range(n):
+        labels = {HOST: f"n{i}"}
+        if draw(st.booleans()):
+            labels[ZONE] = draw(st.sampled_from(["z1", "z2"]))
+        if draw(st.booleans()):
+            labels[RACK] = draw(st.sampled_from(["r1", "r2"]))
+        nodes.append(({"metadata": {"name": f"n{i}", "labels": labels},
+                       "status": {"allocatable": {"cpu": "64", "memory": "512Gi", "pods": "110"}}}))
+    placed = []
+    for j in range(draw(st.integers(0, 10))):
+        spec = {"nodeName": f"n{draw(st.integers(0, n - 1))}"}
+        if draw(st.integers(0, 3)) == 0:
+            spec["affinity"] = draw(_affinity)
+        placed.append({"metadata": {"name": f"q{j}", "namespace": draw(st.sampled_from(["default", "ml"])),
+                                    "uid": f"q{j}-{next(_uid)}", "labels": draw(_plabels)}, "spec": spec})
+    spec = {}
+    if draw(st.booleans()):
+        spec["affinity"] = draw(_affinity)
+    newp = {"metadata": {"name": "new", "namespace": "default", "uid": f"new-{next(_uid)}",
+                         "labels": draw(_plabels)}, "spec": spec}
+    return nodes, placed, newp, draw(st.sampled_from([0, 1, 5]))
+
+
+@settings(max_examples=300, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(_aff_clusters())
+def test_interpod_affinity_native_equals_python_on_random_clusters(case):
+    """Filter verdicts (existing pods' required anti-affinity, the pod's required affinity incl. the
+    first-pod-of-a-group rule, its required anti-affinity) and normalized scores (preferred terms
+    both ways, existing pods' required affinity × hardPodAffinityWeight) equal the Python plugin's."""
+    nodes, placed, newp_obj, hard = case
+    eng, cache = cache_with(nodes)
+    eng.filters = C.F_INTERPOD
+    only_weight(eng, C.S_INTERPOD)
+    eng.set_hard_pod_affinity_weight(hard)
+    for o in placed:
+        cache.add_pod(o)
+    pl = InterPodAffinity({"hardPodAffinityWeight": hard}, SimpleNamespace(cache=cache))
+    p = PodInfo.from_obj(newp_obj)
+    names = sorted(cache.nodes)
+    st_ = CycleState()
+    pl.pre_filter(st_, p)
+    msgs = {"existing pods anti-affinity": "InterPodAffinityExisting", "pod affinity rules": "InterPodAffinity",
+            "pod anti-affinity rules": "InterPodAntiAffinity"}
+    want = {}
+    for nm in names:
+        s = pl.filter(st_, p, nm)
+        want[nm] = "OK" if s.is_success() else next(v for k, v in msgs.items() if k in s.message())
+    req = pod_req(eng, p)
+    got = {nm: C.REASONS[eng.filter_node(req, eng.node_index(nm))] for nm in names}
+    assert got == want
+    feas = [nm for nm in names if want[nm] == "OK"]
+    st2 = CycleState()
+    pl.pre_filter(st2, p)
+    pl.pre_score(st2, p, feas)
+    out = [NodeScore(nm, pl.score(st2, p, nm)[0]) for nm in feas]
+    pl.normalize_score(st2, p, out)
+    assert native_scores(eng, p, feas) == {x.name: x.score for x in out}

@@ -271,9 +271,10 @@ def test_lane_queue_respects_scv_priority_then_fifo():
     assert run(go()) == ["hi1", "hi2", "mid", "lo1", "lo2"]
 
 
-def test_python_plugins_see_lane_pods_spread():
-    """A pod with topologySpreadConstraints takes the Python path; the spread plugin counts the
-    lane's bound pods (mirrored into the cache) and sends it to the emptier node."""
+def test_spread_pods_are_lane_pods_and_count_other_lane_pods():
+    """A pod with a DoNotSchedule topologySpreadConstraint is a lane pod too (round 5: native
+    PodTopologySpread); its constraint counts the lane's bound pods from the engine ledger and
+    sends it to the emptier zone."""
     async def go():
         cfg = yoda_config(extra_filter=["PodTopologySpread"], extra_score=["PodTopologySpread"])
         async with Env(cfg=cfg, nodes=(("n1", 8, None), ("n2", 8, None))) as e:
@@ -295,7 +296,7 @@ def test_python_plugins_see_lane_pods_spread():
             return [pods[f"w{i}"]["spec"]["nodeName"] for i in range(3)], pods["s0"]["spec"]["nodeName"], \
                 e.sched.lane.lane.stats()["admitted"]
     lane_nodes, spread_node, admitted = run(go())
-    assert lane_nodes == ["n1"] * 3 and spread_node == "n2" and admitted == 3
+    assert lane_nodes == ["n1"] * 3 and spread_node == "n2" and admitted == 4
 
 
 def test_relist_after_watch_loss_keeps_the_ledger_exact():
@@ -312,11 +313,12 @@ def test_relist_after_watch_loss_keeps_the_ledger_exact():
     assert ok and binds == 30 and ledger == 30 and owned == 30
 
 
-def test_anti_affinity_gate_hands_only_matching_pods_to_python():
+def test_existing_anti_affinity_is_checked_natively_in_the_lane():
     """A bound pod with required anti-affinity (app=web on this host) turns InterPodAffinity's
-    symmetric rule on. The lane keeps the profile but takes only pods the rule cannot touch: a
-    pod labelled app=web goes to the Python path, which rejects it (the only node holds the anti
-    pod); an unrelated pod still binds through the lane."""
+    symmetric rule on. Round 5: the rule is native, so the lane keeps taking every pod — the
+    anti pod itself, a pod labelled app=web (rejected natively: the only node holds the anti pod;
+    FitError, event and backoff in the lane) and an unrelated pod (bound) — and nothing is handed
+    to the Python path."""
     async def go():
         cfg = yoda_config(extra_filter=["InterPodAffinity"])
         async with Env(cfg=cfg) as e:
@@ -328,18 +330,22 @@ def test_anti_affinity_gate_hands_only_matching_pods_to_python():
                            {"labelSelector": {"matchLabels": {"app": "web"}}, "topologyKey": "kubernetes.io/hostname"}]}})
             await e.create(anti)
             assert await e.wait(lambda: e.sched.scheduled == 2)
-            assert await e.wait(lambda: len(e.sched.lane._profiles["yoda-scheduler"][4]) == 1)
+            assert e.sched.engine.affinity_holders == 1
             on = e.sched.lane._profiles["yoda-scheduler"][0]
             await e.create(pod("web1", {"app": "web", "scv/memory": "1000"}))
             await e.create(pod("api1", {"app": "api", "scv/memory": "1000"}))
             assert await e.wait(lambda: e.sched.scheduled == 3)
+            assert await e.wait(lambda: e.sched.lane.lane.stats()["native_failed"] >= 1)
             await asyncio.sleep(0.3)
             pods = await e.pods()
-            return (on, admitted0, e.sched.lane.lane.stats()["admitted"], pods["web1"]["spec"].get("nodeName"),
-                    pods["api1"]["spec"].get("nodeName"), e.sched.failed)
-    on, a0, a1, web_node, api_node, failed = run(go())
-    assert on and a0 == 1 and a1 == 2   # anti (PF_POD_AFFINITY) and web1 (matches the term) stayed off the lane
-    assert not web_node and failed >= 1  # symmetry: the only node holds the anti pod
+            st = e.sched.lane.lane.stats()
+            cond = (pods["web1"].get("status") or {}).get("conditions") or [{}]
+            return (on, admitted0, st["admitted"], pods["web1"]["spec"].get("nodeName"),
+                    pods["api1"]["spec"].get("nodeName"), e.sched.failed, e.sched.lane.handoffs, cond[0].get("message"))
+    on, a0, a1, web_node, api_node, py_failed, handoffs, msg = run(go())
+    assert on and a0 == 1 and a1 == 4           # every pod was the lane's
+    assert not web_node and py_failed == 0 and handoffs == 0
+    assert "existing pods anti-affinity" in (msg or "")
     assert api_node == "n1"
 
 

@@ -283,6 +283,8 @@ class Framework:
             p = self.plugins.get(name)
             engine.set_alloc_weights(most, *(p.alloc_weights() if p is not None else (1, 1, 0)))
         engine.set_spread_defaults(self._spread_defaults)
+        ipa = self.plugins.get("InterPodAffinity")
+        engine.set_hard_pod_affinity_weight(getattr(ipa, "hard_weight", 1) if ipa is not None else 1)
         fit = self.plugins.get("NodeResourcesFit")
         engine.set_ext_ignored(*(fit.engine_ignored() if fit is not None and hasattr(fit, "engine_ignored")
                                  else ([], [])))

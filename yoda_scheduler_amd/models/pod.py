@@ -189,7 +189,7 @@ class PodInfo:
                  "cpu_m", "mem", "priority", "node_selector", "required_terms", "preferred_terms", "tolerations",
                  "annotations", "host_ports", "attempts", "initial_attempt", "enqueued", "native_req",
                  "native_owner", "assigned_cards", "_creation", "flags", "ext", "nz_cpu_m", "nz_mem", "applies_memo",
-                 "images", "containers", "owner", "avoid", "spread", "deleting")
+                 "images", "containers", "owner", "avoid", "spread", "deleting", "pod_aff")
 
     def __init__(self, obj: dict, uid: str, namespace: str, name: str, num_id: int, labels: dict, gpu: GpuRequest,
                  scheduler_name: str = "default-scheduler", node_name: str = "", cpu_m: int = 0, mem: int = 0,
@@ -198,7 +198,8 @@ class PodInfo:
                  annotations: Optional[dict] = None, host_ports: Optional[list] = None, flags: int = 0,
                  ext: Optional[dict] = None, nz_cpu_m: int = -1, nz_mem: int = -1,
                  images: Optional[list] = None, containers: int = 0, owner: Optional[tuple] = None,
-                 avoid: Optional[tuple] = None, spread: Optional[list] = None, deleting: bool = False) -> None:
+                 avoid: Optional[tuple] = None, spread: Optional[list] = None, deleting: bool = False,
+                 pod_aff: Optional[tuple] = None) -> None:
         self._obj = obj
         # default-plugin inputs the native engine reads (ops/native.py::pod_req): normalized
         # images of spec.containers + their count (ImageLocality), the first controller
@@ -212,6 +213,9 @@ class PodInfo:
         self.avoid = avoid
         self.spread = spread
         self.deleting = deleting
+        # (required affinity, required anti-affinity, preferred affinity, preferred anti-affinity),
+        # each [(topologyKey, namespaces | None, LabelSelector.native() | None, weight)]
+        self.pod_aff = pod_aff
         self._src = None
         # -1: a single container's non-zero request derived from cpu_m / mem
         self.nz_cpu_m = nz_cpu_m if nz_cpu_m >= 0 else (cpu_m or DEFAULT_MILLI_CPU_REQUEST)
@@ -281,10 +285,10 @@ class PodInfo:
             pi = cls.from_obj(json.loads(ev.raw()))
             return pi
         (uid, ns, name, labels, ann, sched, node, cpu, mem, nzc, nzm, prio, nsel, req, pref, tols, ports,
-         flags, _creation, ext, images, containers, owner, avoid, spread, deleting) = a
+         flags, _creation, ext, images, containers, owner, avoid, spread, deleting, pod_aff) = a
         pi = cls(None, uid, ns, name, pod_num_id(uid), labels, parse_gpu_request(labels), sched, node, cpu, mem,
                  prio, nsel, req, pref, tols, ann, ports, flags, ext, nzc, nzm, images, containers, owner, avoid,
-                 spread, deleting)
+                 spread, deleting, pod_aff)
         pi._src = ev
         return pi
 
@@ -335,16 +339,40 @@ class PodInfo:
             spread = [(c.get("topologyKey", ""), int(c.get("maxSkew", 1)), c.get("whenUnsatisfiable", "DoNotSchedule"),
                        None if c.get("labelSelector") is None else LabelSelector(c.get("labelSelector")).native())
                       for c in tsc]
+        pod_aff = None
+        if aff and (aff.get("podAffinity") or aff.get("podAntiAffinity")):
+            pod_aff = _pod_aff(aff)
         return cls(obj, uid, meta.get("namespace", "default"), meta.get("name", ""), pod_num_id(uid), labels,
                    parse_gpu_request(labels), spec.get("schedulerName") or "default-scheduler",
                    spec.get("nodeName") or "", cpu, mem, int(spec.get("priority") or 0),
                    dict(ns) if ns else None, req, pref, tols or None, dict(ann) if ann else None, ports,
                    pod_flags(meta, spec, ports, ext), ext, nzc, nzm, images, len(containers), owner, avoid, spread,
-                   bool(meta.get("deletionTimestamp")))
+                   bool(meta.get("deletionTimestamp")), pod_aff)
 
 
 _EMPTY: dict = {}
 _NOLIST: list = []
+
+
+def _pod_aff(aff: dict) -> tuple:
+    """spec.affinity's pod (anti-)affinity terms as the engine takes them (plugins/spread_affinity.py
+    ``_terms``: a required term has weight 1, a preferred one its weight and podAffinityTerm)."""
+    from .selectors import LabelSelector
+
+    def term(t, w):
+        t = t or {}
+        sel = t.get("labelSelector")
+        return (t.get("topologyKey", "") or "", tuple(t.get("namespaces") or ()) or None,
+                None if sel is None else LabelSelector(sel).native(), w)
+    out = []
+    for kind in ("podAffinity", "podAntiAffinity"):
+        k = aff.get(kind) or {}
+        out.append([term(t, 1) for t in k.get("requiredDuringSchedulingIgnoredDuringExecution") or ()])
+    for kind in ("podAffinity", "podAntiAffinity"):
+        k = aff.get(kind) or {}
+        out.append([term(w.get("podAffinityTerm"), int(w.get("weight", 1)))
+                    for w in k.get("preferredDuringSchedulingIgnoredDuringExecution") or ()])
+    return tuple(out)
 
 
 @dataclass

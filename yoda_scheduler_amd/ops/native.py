@@ -218,6 +218,6 @@ def pod_req(engine, pi: PodInfo):
                         list(pi.node_selector.items()), pi.required_terms, pi.preferred_terms,
                         pi.tolerations, pi.nz_cpu_m, pi.nz_mem)
     engine.set_req_extras(r, pi.namespace, list(pi.labels.items()), pi.deleting, pi.images, pi.containers,
-                          list(pi.ext.items()), pi.owner, pi.avoid, pi.spread)
+                          list(pi.ext.items()), pi.owner, pi.avoid, pi.spread, pi.pod_aff)
     pi.native_req, pi.native_owner = r, engine
     return r

@@ -24,7 +24,7 @@ from typing import Optional
 
 from ..framework.interfaces import (CycleState, FilterPlugin, NativeBinding, NodeScore, PreFilterPlugin,
                                     PreScorePlugin, ScorePlugin, StateData, Status, MAX_NODE_SCORE)
-from ..models.pod import PF_POD_AFFINITY, PF_SPREAD_HARD
+from ..models.pod import PF_POD_AFFINITY
 from ..ops.native import core
 from ..models.selectors import LabelSelector, NodeSelector
 from .optional import default_selector
@@ -148,16 +148,13 @@ class PodTopologySpread(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlug
     def native(self):
         return NativeBinding(filter_bit=core().F_SPREAD, score_index=core().S_SPREAD)
 
-    @property
-    def lane_flags(self):
-        """Pods with these flags stay off the native lane (None: the lane cannot run the
-        profile). A DoNotSchedule constraint's skew must see every pod its selector matches
-        that is placed before it, and a Python-path cycle may assume such a pod between the
-        lane's count and its assume; pods whose constraints are all ScheduleAnyway only score
-        from the counts, so they are lane pods (and so is everything else)."""
-        if any(c.get("whenUnsatisfiable") == "DoNotSchedule" for c in self.default_constraints):
-            return None
-        return PF_SPREAD_HARD
+    # Pods with these flags stay off the native lane: none. A lane pod's constraints are counted
+    # and its reservation made under one engine lock (a pod with DoNotSchedule constraints is
+    # never device-eligible, so no device batch drops the lock in between); a Python-path pod
+    # assumed later is a later pod in upstream's serial order, which a spread constraint never
+    # looks back at. The other direction — a Python-path pod's own constraints — is its
+    # declared gate (``own_gate_terms``), and its final engine call re-runs this filter natively.
+    lane_flags = 0
 
     def engine_defaults(self) -> list:
         """The default constraints as the engine takes them (``Engine.set_spread_defaults``)."""
@@ -392,37 +389,25 @@ class _AffinityState(StateData):
 class InterPodAffinity(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugin):
     """Required pod (anti-)affinity as a filter (incl. the symmetric rule for existing
     pods' required anti-affinity), preferred terms + ``hardPodAffinityWeight`` as a score.
-    Each cycle walks the bound/assumed pods once; per-node work is a few dict lookups."""
+
+    Runs natively (``native/core/engine.cpp`` ``F_INTERPOD`` / ``S_INTERPOD``, round 5): the engine
+    ledger keeps every reserved pod's namespace, labels and (anti-)affinity terms, so neither an
+    affinity pod nor a bound pod's required anti-affinity moves pods off the native cycle or the
+    native lane, and a Python-path cycle's final engine call re-checks the rule against every pod
+    placed meanwhile. The methods below are the executable spec the native code is pinned against
+    (``tests/test_native_default_plugins.py``); each cycle walks the bound/assumed pods once."""
     name = "InterPodAffinity"
     KEY = "PreFilterInterPodAffinity"
-
-    pod_flags = PF_POD_AFFINITY
-    # other pods read: labels (the lane's counted natively) and the affinity terms of pods
-    # flagged with them, which the lane never takes
-    reads_flags = PF_POD_AFFINITY
+    # other pods read: labels and affinity terms, which the engine ledger holds for every pod
+    reads_flags = 0
+    lane_flags = 0
 
     def __init__(self, args=None, handle=None) -> None:
         super().__init__(args, handle)
         self.hard_weight = int(self.args.get("hardPodAffinityWeight", 1))
-        self._gt_src, self._gt = None, []          # gate_terms() of the cache's current term list
 
-    def cluster_active(self) -> bool:
-        """Bound pods with required anti-affinity can reject a new pod (symmetry)."""
-        return bool(self.handle.cache.pods_with_required_anti_affinity())
-
-    def gate_terms(self) -> list:
-        """The gate as selectors: only pods matching one of these terms (a bound pod's required
-        anti-affinity) are affected by it; the native lane keeps taking all others."""
-        src = self.handle.cache.anti_terms()
-        if src is not self._gt_src:            # the cache rebuilds the list when a holder changes
-            self._gt_src, self._gt = src, [sel.native(ns) for ns, sel in src]
-        return self._gt
-
-    def own_gate_terms(self, pod) -> list:
-        """Native queries the lane must not place pods matching while this pod's cycle runs
-        unparked: its required anti-affinity terms (a matching lane pod landing in the chosen
-        domain would violate them). Affinity terms need no gate: more matches only help."""
-        return [[_native_term(t, pod.namespace)] for t, _ in _terms(pod, "podAntiAffinity", True)]
+    def native(self):
+        return NativeBinding(filter_bit=core().F_INTERPOD, score_index=core().S_INTERPOD)
 
     def is_noop_for(self, pod) -> bool:
         aff = _spec(pod).get("affinity") or {}
