@@ -168,7 +168,10 @@ def main(argv=None) -> int:
                          "ephemeral-storage (bench/workloads.py)")
     ap.add_argument("--mix-anti", type=int, default=0,
                     help="beyond BASELINE: replace this many pods of the burst (evenly spread) with pods that carry "
-                         "required pod anti-affinity (Python-path pods reading other pods, lane pods included)")
+                         "required pod anti-affinity (native InterPodAffinity since round 5)")
+    ap.add_argument("--mix-spread", type=int, default=0,
+                    help="beyond BASELINE: give this many pods of the burst (evenly spread; 1000 = all) a hostname "
+                         "DoNotSchedule topologySpreadConstraint (native PodTopologySpread since round 5)")
     ap.add_argument("--device", choices=["auto", "on", "off"], default="auto",
                     help="gfx950 device scorer (used automatically for clusters >= deviceScorer.minNodes = 48 nodes)")
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
@@ -251,6 +254,7 @@ def main(argv=None) -> int:
     from yoda_scheduler_amd.bench.harness import HttpShard, Shard, percentile
     from yoda_scheduler_amd.bench.workloads import make_workload
     w = make_workload(a.config, seed=rank, node_gpus=a.node_gpus, nodes=a.nodes, mix_anti=a.mix_anti,
+                      mix_spread=a.mix_spread,
                       cluster=a.cluster)
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)

@@ -868,3 +868,27 @@ def test_kind_cluster_keeps_the_native_lane_on():
     assert handoffs == 0 and st["unschedulable"] == 0
     # bound pods' echoes of other schedulers aside, nothing of the burst reached Python
     assert forwarded == 0, forwarded
+
+
+def test_spread_and_anti_affinity_bursts_stay_on_the_native_lane():
+    """a 1000-pod burst where every pod has a hostname DoNotSchedule
+    topologySpreadConstraint, and a burst with required-anti-affinity pods mixed in, are placed
+    entirely by the native lane (native PodTopologySpread / InterPodAffinity): nothing is handed
+    to or forwarded to the Python path."""
+    from yoda_scheduler_amd.bench.harness import HttpShard
+    from yoda_scheduler_amd.bench.workloads import make_workload
+
+    async def go(w):
+        sh = HttpShard(w, events=False)
+        try:
+            await sh.start()
+            r = await sh.burst("a")
+            st = sh.sched.lane.lane.stats()
+            return r, st, sh.sched.lane.handoffs, sh.sched.lane.forwarded
+        finally:
+            await sh.stop()
+
+    for w in (make_workload(3, mix_spread=1000), make_workload(3, mix_anti=10)):
+        r, st, handoffs, forwarded = run(go(w))
+        assert r.bound == 1000 and r.unschedulable == 0, w.name
+        assert st["admitted"] == 1000 and handoffs == 0 and forwarded == 0, (w.name, st["admitted"], forwarded)

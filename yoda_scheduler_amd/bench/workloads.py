@@ -65,7 +65,7 @@ def _mixed_labels(rng: random.Random) -> dict:
 
 def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None,
                   node_gpus: Optional[int] = None, nodes: Optional[int] = None, mix_anti: int = 0,
-                  cluster: str = "synthetic") -> Workload:
+                  cluster: str = "synthetic", mix_spread: int = 0) -> Workload:
     """``node_gpus`` overrides the GPUs per node (BASELINE.md protocol item 5: every
     config at 1, 2, 4 and 8 GPUs per node); pods keep their labels, so e.g. ``scv/number: 8``
     pods are unschedulable on smaller nodes and are reported as such. ``nodes`` resizes
@@ -86,6 +86,16 @@ def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None,
             w.specs[i] = {"affinity": {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
                 {"labelSelector": {"matchLabels": {"app": f"anti-{j}"}}, "topologyKey": "kubernetes.io/hostname"}]}}}
         w.name += f" + {mix_anti} required-anti-affinity pods"
+    if mix_spread:
+        # beyond BASELINE: pods with a hostname DoNotSchedule spread constraint over their own group
+        n = len(w.pods)
+        for j in range(min(mix_spread, n)):
+            i = j * n // min(mix_spread, n)
+            w.pods[i] = dict(w.pods[i], group=f"g{i % 8}")
+            w.specs[i] = dict(w.specs.get(i) or {}, topologySpreadConstraints=[{
+                "maxSkew": 1, "topologyKey": "kubernetes.io/hostname", "whenUnsatisfiable": "DoNotSchedule",
+                "labelSelector": {"matchLabels": {"group": f"g{i % 8}"}}}])
+        w.name += f" + {min(mix_spread, n)} hostname-spread pods"
     if nodes is not None:
         if cfg != 6 or nodes < 1:
             raise ValueError("nodes: config 6 only, >= 1")
