@@ -1455,6 +1455,11 @@ CTerm compile(const MatchTerm& t) {
 }
 }  // namespace
 
+// A census row keeps 64-bit FNV-1a hashes of a pod's first kCLab labels (key, key=value); a
+// pod with more labels is `big` and matched exactly against its projection. The hash path is a
+// deliberate trade: a false match needs two different label strings with equal 64-bit hashes
+// (≈ n²/2^65 for n distinct labels in a cluster — astronomically small), in exchange for a
+// census scan that never touches strings.
 void Lane::census_fill(CRow& r) {
   const Entry* e = r.e;
   const yk::PodProj& lp = (e->lab_ev ? e->lab_ev : e->ev)->full();

@@ -49,9 +49,11 @@ def test_device_candidates_taints_and_selector(require_gpu):
 
 
 # k_batch kernel time per pod at 4096 nodes, the bench mix, measured on MI355X with two pods in
-# flight (profiles/device/r4/early_gather1/: 12.6; pairs/: 13.5–14.0 before the fix-up overlap;
-# one at a time 15.9–16.0); the test allows 1.5× before it calls a regression
+# flight (profiles/device/r4/early_gather1/: 12.6; round 5 with the extended-resource dimension:
+# 11.7 under rocprofv3, profiles/device/r5/kbprof/; one at a time 15.9–16.0); the test allows
+# 1.25× before it calls a regression (1.5× let a 60 % slowdown pass)
 KBATCH_US_PER_POD_4096 = 12.6
+KBATCH_SLACK = 1.25
 
 
 def test_k_batch_time_per_pod_and_one_dispatch_per_batch(require_gpu):
@@ -80,7 +82,7 @@ def test_k_batch_time_per_pod_and_one_dispatch_per_batch(require_gpu):
         per_pod.append((c1["kbatch_us"] - c0["kbatch_us"]) / size)
     assert eng.device_fallbacks == 0
     per_pod.sort()
-    assert per_pod[len(per_pod) // 2] <= 1.5 * KBATCH_US_PER_POD_4096, per_pod
+    assert per_pod[len(per_pod) // 2] <= KBATCH_SLACK * KBATCH_US_PER_POD_4096, per_pod
 
 
 def test_scheduler_auto_enables_device_scorer_and_matches_cpu(require_gpu):
