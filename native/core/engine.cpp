@@ -332,6 +332,7 @@ bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::ve
     aff_holders_.insert(pod);
     if (!req.aff->req_anti.empty()) anti_holders_.insert(pod);
   }
+  index_pod(n, a, +1);
   if (!req.ext.empty()) {
     a.ext = req.ext;
     for (const auto& r : a.ext) {
@@ -377,6 +378,7 @@ bool Engine::release(uint64_t pod) {
       auto it = std::lower_bound(n.ext_used.begin(), n.ext_used.end(), std::make_pair(r.first, INT64_MIN));
       if (it != n.ext_used.end() && it->first == r.first && (it->second -= r.second) == 0) n.ext_used.erase(it);
     }
+    index_pod(n, a, -1);
     mark_dirty(a.node);
   }
   if (a.aff) {
@@ -1078,29 +1080,57 @@ void Engine::interpod_prefilter(const PodReq& req, InterPodPF* pf) const {
   bool self = true;
   for (const PodTerm& t : aff) self = self && t.matches(req.ns, req.labels);
   pf->self_match = self;
-  for (const Node& n : nodes_) {
-    if (!n.alive || n.pods.empty()) continue;
+  // pods of node n matching one term: from the label index when its selector is a single label
+  // (or empty), else by walking the node's pods
+  auto term_count = [&](const Node& n, const PodTerm& t) -> int64_t {
+    int64_t sum = 0, c = 0;
+    bool ok = true;
+    for (int32_t ns : t.ns) {
+      if (!indexed_count(n, ns, t.sel, false, &c)) {
+        ok = false;
+        break;
+      }
+      sum += c;
+    }
+    if (ok) return sum;
+    sum = 0;
     for (uint64_t id : n.pods) {
       const Assignment& a = ledger_.at(id);
-      if (!aff.empty()) {
-        bool all = true;
-        for (const PodTerm& t : aff)
-          if (!t.matches(a.ns, a.labels)) {
-            all = false;
-            break;
-          }
-        if (all) {
-          pf->any_aff_match = true;
-          for (const PodTerm& t : aff) {
-            auto lab = n.labels.find(t.key);
-            if (lab != n.labels.end()) pf->affinity[pair_key(t.key, lab->second)] += 1;
-          }
+      sum += t.matches(a.ns, a.labels);
+    }
+    return sum;
+  };
+  for (const Node& n : nodes_) {
+    if (!n.alive || n.pods.empty()) continue;
+    if (!aff.empty()) {
+      int64_t all = 0;
+      if (aff.size() == 1) {
+        all = term_count(n, aff[0]);
+      } else {                                  // a pod must match every term: walk
+        for (uint64_t id : n.pods) {
+          const Assignment& a = ledger_.at(id);
+          bool m = true;
+          for (const PodTerm& t : aff)
+            if (!t.matches(a.ns, a.labels)) {
+              m = false;
+              break;
+            }
+          all += m;
         }
       }
-      for (const PodTerm& t : anti) {
-        auto lab = n.labels.find(t.key);
-        if (lab != n.labels.end() && t.matches(a.ns, a.labels)) pf->anti[pair_key(t.key, lab->second)] += 1;
+      if (all > 0) {
+        pf->any_aff_match = true;
+        for (const PodTerm& t : aff) {
+          auto lab = n.labels.find(t.key);
+          if (lab != n.labels.end()) pf->affinity[pair_key(t.key, lab->second)] += all;
+        }
       }
+    }
+    for (const PodTerm& t : anti) {
+      auto lab = n.labels.find(t.key);
+      if (lab == n.labels.end()) continue;
+      const int64_t c = term_count(n, t);
+      if (c) pf->anti[pair_key(t.key, lab->second)] += c;
     }
   }
 }
@@ -1325,8 +1355,41 @@ bool Engine::set_pod_meta(uint64_t pod, Labels labels, bool deleting) {
   auto it = ledger_.find(pod);
   if (it == ledger_.end()) return false;
   std::sort(labels.begin(), labels.end());
-  it->second.labels = std::move(labels);
-  it->second.deleting = deleting;
+  Assignment& a = it->second;
+  const bool live = a.node >= 0 && a.node < (int32_t)nodes_.size() && nodes_[a.node].alive;
+  if (live) index_pod(nodes_[a.node], a, -1);
+  a.labels = std::move(labels);
+  a.deleting = deleting;
+  if (live) index_pod(nodes_[a.node], a, +1);
+  return true;
+}
+
+void Engine::index_pod(Node& n, const Assignment& a, int sign) {
+  const int live = a.deleting ? 0 : sign;
+  auto bump = [&](LKey k) {
+    auto& c = n.lab_idx[k];
+    c.first += sign;
+    c.second += live;
+    if (c.first <= 0) n.lab_idx.erase(k);
+  };
+  bump(LKey{a.ns, -1, -1});
+  for (const auto& kv : a.labels) bump(LKey{a.ns, kv.first, kv.second});
+}
+
+bool Engine::indexed_count(const Node& n, int32_t ns, const LSel& sel, bool skip_deleting, int64_t* out) const {
+  if (sel.nothing) {
+    *out = 0;
+    return true;
+  }
+  LKey k{ns, -1, -1};
+  if (sel.reqs.size() == 1 && sel.reqs[0].op == kIn && sel.reqs[0].values.size() == 1) {
+    k.k = sel.reqs[0].key;
+    k.v = sel.reqs[0].values[0];
+  } else if (!sel.reqs.empty()) {
+    return false;
+  }
+  auto it = n.lab_idx.find(k);
+  *out = it == n.lab_idx.end() ? 0 : (skip_deleting ? it->second.second : it->second.first);
   return true;
 }
 
@@ -1427,6 +1490,7 @@ int64_t Engine::count_matching(int32_t idx, int32_t ns, const LSel& sel) const {
   // upstream countPodsMatchSelector: same namespace, not terminating, selector match
   if (idx < 0 || idx >= (int32_t)nodes_.size() || sel.nothing) return 0;
   int64_t c = 0;
+  if (indexed_count(nodes_[idx], ns, sel, true, &c)) return c;
   for (uint64_t pod : nodes_[idx].pods) {
     const Assignment& a = ledger_.at(pod);
     if (a.ns == ns && !a.deleting && sel.matches(a.labels)) ++c;

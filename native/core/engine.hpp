@@ -142,6 +142,18 @@ struct DefaultSpread {
   bool hard = false;
 };
 
+// (namespace, label key, label value) of the pods on a node; key = value = -1: the namespace alone
+struct LKey {
+  int32_t ns, k, v;
+  bool operator==(const LKey& o) const { return ns == o.ns && k == o.k && v == o.v; }
+};
+struct LKeyHash {
+  size_t operator()(const LKey& x) const {
+    return (size_t)(((uint64_t)(uint32_t)x.ns * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)(uint32_t)x.k * 0xC2B2AE3D27D4EB4Full) ^
+                    ((uint64_t)(uint32_t)x.v * 0x165667B19E3779F9ull));
+  }
+};
+
 struct Node {
   std::string name;
   uint32_t gen = 0;                   // slot generation: bumped when the slot gets a new node or dies
@@ -166,6 +178,9 @@ struct Node {
   std::vector<std::pair<int32_t, int64_t>> ext_alloc;  // allocatable beyond cpu/memory/pods, sorted
   std::vector<std::pair<int32_t, int64_t>> ext_used;   // Σ of the ledger's ext requests, sorted
   std::vector<std::pair<int8_t, int32_t>> avoid;       // preferAvoidPods controllers (kind 1 RC / 2 RS, uid)
+  // label index of the reserved pods: (all, not terminating) per (namespace, key, value) and per
+  // namespace — a single-label selector's count in O(1) (spread / affinity pre-filters)
+  std::unordered_map<LKey, std::pair<int32_t, int32_t>, LKeyHash> lab_idx;
 };
 
 struct PodReq {
@@ -505,6 +520,9 @@ class Engine {
   // the soft constraints score every node 0 (no live node carries one of their keys)
   bool spread_soft_constant(const std::vector<SpreadC>& soft) const;
   bool images_matter(const PodReq& req) const;
+  void index_pod(Node& n, const Assignment& a, int sign);
+  // pods of node n in namespace ns matching sel from the label index; false when sel needs the walk
+  bool indexed_count(const Node& n, int32_t ns, const LSel& sel, bool skip_deleting, int64_t* out) const;
   // ImageLocality scores every live node alike for this pod (each of its images is on no node,
   // or on every node with one size): true and the weighted score in *v
   bool image_score_const(const PodReq& req, int64_t* v) const;
