@@ -89,6 +89,17 @@ for s in $STEPS; do
         step "pairs/two_$k" 200 env YODA_DEV_PAIRS=1 python scripts/device_batch_bench.py --nodes 256,1024,4096 --pods 1032 --batch 256 --modes batch --trace --mix bench
       done ;;
     testspairs) step gpu_tests_pairs 600 env YODA_DEV_PAIRS=1 python -u -m pytest tests/test_gpu_device_scorer.py -x -v --timeout 120 --timeout-method thread ;;
+    altinproc)  # the driver's `alt` (in-process apiserver, Python cycle) three times, + a sampled profile
+      mkdir -p gpurun_out/alt
+      for k in 1 2 3; do step "alt/inproc_$k" 300 python bench.py --transport inproc --alt none --steps 20 --warmup 5; done
+      step alt/sample 300 env YODA_PROF_SAMPLE=1 python scripts/profile_bench.py --out gpurun_out/alt/sample.txt \
+        --transport inproc --alt none --steps 20 --warmup 5 ;;
+    spread)     # config 3 with every pod carrying a hostname spread constraint, next to plain config 3
+      mkdir -p gpurun_out/spread
+      for k in 1 2; do
+        step "spread/c3_$k" 300 python bench.py --config 3 --steps 20 --warmup 5 --alt none
+        step "spread/c3spread_$k" 300 python bench.py --config 3 --steps 20 --warmup 5 --mix-spread 1000 --alt none
+      done ;;
     mixlog) step mixlog 300 env YODA_BENCH_RUNLOG=1 python bench.py --config 3 --mix-anti 10 --steps 5 --warmup 3 --alt none ;;
     scope6) step scope6 300 env YODA_BENCH_THREADS=2 python bench.py --config 6 --steps 5 --warmup 1 --alt none ;;
     nodegpus)   # BASELINE protocol item 5 on config 3: scheduler CPU per attempted pod at 1/2/4/8 GPUs per node
@@ -105,7 +116,11 @@ for s in $STEPS; do
                   "c2|--config 2 --steps 10 --warmup 2" "c4|--config 4 --steps 10 --warmup 2" \
                   "c5|--config 5 --steps 5 --warmup 2" "c6|--config 6 --steps 5 --warmup 1" \
                   "c6off|--config 6 --steps 2 --warmup 1 --device off" \
-                  "c3ref|--config 3 --steps 1 --warmup 0 --reference-qps" "c3b|--config 3 --steps 20 --warmup 5"; do
+                  "c3ref|--config 3 --steps 1 --warmup 0 --reference-qps" "c3b|--config 3 --steps 20 --warmup 5" \
+                  "c3kind|--config 3 --steps 20 --warmup 5 --cluster kind" "c1kind|--config 1 --steps 20 --warmup 2 --cluster kind" \
+                  "c2kind|--config 2 --steps 10 --warmup 2 --cluster kind" "c4kind|--config 4 --steps 10 --warmup 2 --cluster kind" \
+                  "c5kind|--config 5 --steps 5 --warmup 2 --cluster kind" "c6kind|--config 6 --steps 5 --warmup 1 --cluster kind" \
+                  "c3anti|--config 3 --steps 20 --warmup 5 --mix-anti 10" "c3spread|--config 3 --steps 20 --warmup 5 --mix-spread 1000"; do
         step "all/${spec%%|*}" 300 python bench.py --alt none ${spec#*|}
       done
       python - <<'PY'

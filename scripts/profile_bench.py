@@ -42,6 +42,8 @@ def main() -> int:
         out, args = args[1], args[2:]
     import bench
     from yoda_scheduler_amd.bench import harness as H
+    if os.environ.get("YODA_PROF_SAMPLE"):
+        return _sample(args, out, bench, H)
     # YODA_PROF_CPU=1: the interpreter thread's CPU time (waits on locks and the GIL excluded)
     pr = cProfile.Profile(__import__("time").thread_time) if os.environ.get("YODA_PROF_CPU") else cProfile.Profile()
     for cls in (H.Shard, H.HttpShard):
@@ -80,6 +82,74 @@ def main() -> int:
     pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(45)
     if os.environ.get("YODA_PROF_CUM"):
         pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(int(os.environ["YODA_PROF_CUM"]))
+    text = s.getvalue()
+    print(text)
+    if out:
+        with open(out, "w") as f:
+            f.write(text)
+    return 0
+
+
+def _sample(args, out, bench, H) -> int:
+    """YODA_PROF_SAMPLE=1: a statistical profile instead of cProfile (no per-call
+    overhead, so cheap functions are not inflated): a thread samples the interpreter
+    thread's stack every ~0.5 ms during the timed bursts; prints self and inclusive
+    sample shares per function."""
+    import collections
+    import threading
+    import time
+
+    main = threading.main_thread().ident
+    on = [False]
+    self_c, incl_c = collections.Counter(), collections.Counter()
+    n = [0]
+
+    def sampler():
+        while not stop.is_set():
+            time.sleep(0.0005)
+            if not on[0]:
+                continue
+            f = sys._current_frames().get(main)
+            if f is None:
+                continue
+            n[0] += 1
+            seen = set()
+            first = True
+            while f is not None:
+                co = f.f_code
+                key = f"{co.co_filename.replace(ROOT + '/', '')}:{co.co_firstlineno}({co.co_name})"
+                if first:
+                    self_c[key] += 1
+                    first = False
+                if key not in seen:
+                    incl_c[key] += 1
+                    seen.add(key)
+                f = f.f_back
+    stop = threading.Event()
+    sys.setswitchinterval(1e-4)      # let the sampler take the GIL between bytecodes
+    th = threading.Thread(target=sampler, daemon=True)
+    th.start()
+    for cls in (H.Shard, H.HttpShard):
+        orig = cls.burst
+
+        def wrap(orig):
+            async def burst(self, tag="b", timeout=600.0):
+                on[0] = tag.startswith("s")
+                try:
+                    return await orig(self, tag, timeout)
+                finally:
+                    on[0] = False
+            return burst
+        cls.burst = wrap(orig)
+    bench.main(args)
+    stop.set()
+    s = io.StringIO()
+    s.write(f"samples: {n[0]}\n\nself %:\n")
+    for k, v in self_c.most_common(40):
+        s.write(f"  {100 * v / max(1, n[0]):5.1f}  {k}\n")
+    s.write("\ninclusive %:\n")
+    for k, v in incl_c.most_common(60):
+        s.write(f"  {100 * v / max(1, n[0]):5.1f}  {k}\n")
     text = s.getvalue()
     print(text)
     if out:

@@ -170,7 +170,7 @@ class FakeApiHttp:
         try:
             while True:
                 try:
-                    ev = await asyncio.wait_for(w.queue.get(), timeout)
+                    ev = await asyncio.wait_for(w.get(), timeout)
                 except asyncio.TimeoutError:
                     break
                 if ev is None:

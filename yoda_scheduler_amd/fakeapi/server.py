@@ -50,20 +50,36 @@ class Faults:
 
 
 class Watch:
-    __slots__ = ("resource", "queue", "closed", "sent", "server", "selector")
+    """One watch stream: events queue in a deque; a reader parks on one future only when
+    the deque is empty (an ``asyncio.Queue`` costs a put/get pair of coroutine hops per
+    event, which an in-process burst pays twice per pod)."""
+    __slots__ = ("resource", "_dq", "_waiter", "closed", "sent", "server", "selector")
 
     def __init__(self, server: "FakeApiServer", resource: str, selector: Optional[FieldSelector] = None) -> None:
         self.server = server
         self.resource = resource
         self.selector = selector
-        self.queue: asyncio.Queue = asyncio.Queue()
+        self._dq: collections.deque = collections.deque()
+        self._waiter: Optional[asyncio.Future] = None
         self.closed = False
         self.sent = 0
+
+    def _wake(self) -> None:
+        w = self._waiter
+        if w is not None:
+            self._waiter = None
+            if not w.done():
+                w.set_result(None)
+
+    def _put(self, ev) -> None:
+        self._dq.append(ev)
+        if self._waiter is not None:
+            self._wake()
 
     def push(self, ev: tuple) -> None:
         if self.closed:
             return
-        self.queue.put_nowait(ev)
+        self._put(ev)
         self.sent += 1
         dw = self.server.faults.drop_watch_every
         if dw and self.sent % dw == 0:
@@ -72,14 +88,46 @@ class Watch:
     def close(self) -> None:
         if not self.closed:
             self.closed = True
-            self.queue.put_nowait(None)
+            self._put(None)
             self.server._watchers[self.resource].discard(self)
+
+    async def _wait(self) -> None:
+        fut = self._waiter = asyncio.get_running_loop().create_future()
+        try:
+            await fut
+        finally:
+            if self._waiter is fut:
+                self._waiter = None
+
+    async def get(self):
+        """The next event, or None once the watch is closed."""
+        dq = self._dq
+        while not dq:
+            await self._wait()
+        ev = dq[0]
+        if ev is not None:
+            dq.popleft()
+        return ev
+
+    async def next_batch(self) -> Optional[list]:
+        """Every queued event (at least one), or None once the watch is closed."""
+        dq = self._dq
+        while not dq:
+            await self._wait()
+        if dq[-1] is None:
+            out = list(dq)[:-1]
+            dq.clear()
+            dq.append(None)          # the end marker stays for the next call
+            return out or None
+        out = list(dq)
+        dq.clear()
+        return out
 
     def __aiter__(self):
         return self
 
     async def __anext__(self):
-        ev = await self.queue.get()
+        ev = await self.get()
         if ev is None:
             raise StopAsyncIteration
         return ev
@@ -111,13 +159,16 @@ class FakeApiServer:
         self._last_rv = next(self._rv)
         return str(self._last_rv)
 
-    def _emit(self, res: str, typ: str, obj: dict, old: Optional[dict] = None) -> None:
-        rv = int(obj["metadata"]["resourceVersion"])
+    def _emit(self, res: str, typ: str, obj: dict, old: Optional[dict] = None, rv: int = 0) -> None:
+        if not rv:
+            rv = int(obj["metadata"]["resourceVersion"])
         h = self._history[res]
         if len(h) == h.maxlen:
             self._oldest_rv[res] = h[0][0]
         h.append((rv, typ, obj, old))
-        for w in tuple(self._watchers[res]):
+        ws = self._watchers[res]
+        # a push closes its watch (and leaves the set) only under drop_watch_every
+        for w in (tuple(ws) if self.faults.drop_watch_every else ws):
             if w.selector is None:
                 w.push((typ, obj))
             else:
@@ -149,17 +200,19 @@ class FakeApiServer:
         new.setdefault("apiVersion", r.api_version)
         new.setdefault("kind", r.kind)
         meta["uid"] = meta.get("uid") or f"{self._uid_prefix}-{next(self._uids):012x}"
-        meta["resourceVersion"] = self._next_rv()
-        meta.setdefault("creationTimestamp", rfc3339(time.time()))
+        rv = self._last_rv = next(self._rv)
+        meta["resourceVersion"] = str(rv)
+        if "creationTimestamp" not in meta:
+            meta["creationTimestamp"] = rfc3339(time.time())
         new["metadata"] = meta
-        key = obj_key(r, new)
+        key = f"{meta['namespace'] or 'default'}/{meta['name']}" if r.namespaced else meta["name"]
         store = self._objs[res]
         if key in store:
             raise already_exists(f"{res} {key}")
         store[key] = new
         if res == "pods":
             self.create_log[key] = self.clock()
-        self._emit(res, "ADDED", new)
+        self._emit(res, "ADDED", new, None, rv)
         return new
 
     def get(self, res: str, name: str, namespace: Optional[str] = None) -> dict:
@@ -279,7 +332,7 @@ class FakeApiServer:
                 if erv > rv:
                     ev = (typ, obj) if sel is None else filter_event(sel, typ, obj, old)
                     if ev is not None:
-                        w.queue.put_nowait(ev)
+                        w._put(ev)
         self._watchers[res].add(w)
         return w
 
@@ -313,13 +366,14 @@ class FakeApiServer:
         meta = dict(cur["metadata"])
         if annotations:
             meta["annotations"] = dict(meta.get("annotations") or {}, **annotations)
-        meta["resourceVersion"] = self._next_rv()
+        rv = self._last_rv = next(self._rv)
+        meta["resourceVersion"] = str(rv)
         new = dict(cur)
         new["spec"], new["status"], new["metadata"] = spec, status, meta
         self._objs["pods"][key] = new
         self.bind_log[key] = self.clock()
         self.bind_node[key] = node
-        self._emit("pods", "MODIFIED", new, cur)
+        self._emit("pods", "MODIFIED", new, cur, rv)
         return new
 
     # ------------------------------------------------------------------ bench helpers

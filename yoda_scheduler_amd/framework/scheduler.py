@@ -41,6 +41,7 @@ from .runtime import Framework
 log = logging.getLogger("yoda.scheduler")
 
 _EMPTY_STATE = CycleState()      # shared read-only state for all-native cycles
+_EMPTY_DICT: dict = {}
 ENGINE_SWITCH_INTERVAL_S = 0.0002
 POD_FIELD_SELECTOR = "status.phase!=Succeeded,status.phase!=Failed"   # upstream NewPodInformer
 _VOLATILE_META = ("resourceVersion", "generation", "managedFields")
@@ -152,6 +153,11 @@ class Scheduler:
             self.limiter = TokenBucket(0, 1)
         else:
             self.limiter = bind_limiter or TokenBucket(cc.qps, cc.burst)
+        # where all-native runs submit their Bindings directly (no bind worker): the native
+        # transport, or an in-process apiserver's synchronous binder (behind self.limiter)
+        self._binds = self.native
+        if self._binds is None and hasattr(client, "direct_binds"):
+            self._binds = client.direct_binds()
         self.bind_timeout = float(getattr(client, "timeout", 30.0) or 30.0)
         self.recorder = EventRecorder(client, enabled=record_events, api=config.events_api)
         self.handle = Handle(self)
@@ -340,31 +346,41 @@ class Scheduler:
         return (obj.get("status") or {}).get("phase") in ("Succeeded", "Failed")
 
     def on_pod_add(self, obj: dict) -> None:
-        if self._assigned(obj):
+        spec = obj.get("spec") or _EMPTY_DICT
+        if spec.get("nodeName"):
             if self.nominations:
                 self._clear_nomination((obj.get("metadata") or {}).get("uid"))
             if not self._terminal(obj):
                 self.cache.add_pod(obj)
-        elif self._responsible(obj) and not self._terminal(obj):
+        elif (spec.get("schedulerName") or "default-scheduler") in self.frameworks and not self._terminal(obj):
             self.queue.add(PodInfo.from_obj(obj))
-            self.metrics.child(self.metrics.incoming, "PodAdd", "active").inc()
+            if self._metrics_on:
+                self.metrics.child(self.metrics.incoming, "PodAdd", "active").inc()
 
     def on_pod_update(self, old: dict, new: dict) -> None:
-        if self._assigned(new):
+        node = (new.get("spec") or _EMPTY_DICT).get("nodeName")
+        if node:
             uid = new["metadata"].get("uid")
             if self._terminal(new):
                 self.cache.remove_pod(uid)
                 self.queue.move_all_to_active_or_backoff("AssignedPodCompleted")
                 return
-            if not self._assigned(old):
-                self._conditions.pop(uid, None)
+            if not (old.get("spec") or _EMPTY_DICT).get("nodeName"):
+                # the Binding's echo (usually of our own assumed pod)
+                if self._conditions:
+                    self._conditions.pop(uid, None)
                 self.queue.delete(uid)
                 if uid in self.nominations:
                     self._clear_nomination(uid)
-                if self.cache.is_assumed(uid):
-                    ps = self.cache.pods[uid]
-                    self.metrics.pod_scheduling.observe(max(0.0, time.monotonic() - ps.info.initial_attempt))
-                    self.metrics.pod_attempts.observe(ps.info.attempts)
+                ps = self.cache.pods.get(uid)
+                if ps is not None and ps.assumed:
+                    if self._metrics_on:
+                        self.metrics.pod_scheduling.observe(max(0.0, time.monotonic() - ps.info.initial_attempt))
+                        self.metrics.pod_attempts.observe(ps.info.attempts)
+                    if ps.node == node:          # confirm in place (cache.add_pod's fast path)
+                        ps.assumed, ps.deadline = False, None
+                        ps.info.obj = new
+                        return
                 self.cache.add_pod(new)
             else:
                 self.cache.update_pod(new)
@@ -1003,7 +1019,7 @@ class Scheduler:
         if not self.extenders and binder is not None and getattr(binder, "native_bind", False):
             self._run_direct = (fw, fw.direct_bind_mask())
         # the run's native Bindings go to the transport in one hand-off at the end
-        buf = self._bind_buf = [] if self.native is not None else None
+        buf = self._bind_buf = [] if self._binds is not None else None
         try:
             for p, res in zip(run, results):
                 self._finish_cycle(fw, None, p, res, cycle, t0)   # all-native: no Python state
@@ -1014,7 +1030,7 @@ class Scheduler:
                 cbs, self._bind_cbs = self._bind_cbs, []
                 if buf:
                     try:
-                        self.native.bind_many(buf, cbs, self.bind_timeout)
+                        self._binds.bind_many(buf, cbs, self.bind_timeout)
                     except Exception as e:  # noqa: BLE001 - the run's pods must not stay assumed
                         log.error("handing %d Bindings to the transport failed: %r", len(buf), e)
                         msg = repr(e).encode()
@@ -1161,7 +1177,8 @@ class Scheduler:
 
     def _enqueue_bind(self, item: tuple) -> None:
         fw = item[0]
-        if self.native is not None and self._native_direct(fw, item[2]):
+        if (self._binds is not None and self._native_direct(fw, item[2])
+                and (self.native is not None or self.limiter.try_acquire())):
             pi, node = item[2], item[3]
             cb = functools.partial(self._native_bind_done, item, time.perf_counter())
             buf = self._bind_buf
@@ -1169,7 +1186,7 @@ class Scheduler:
                 buf.append((pi.namespace, pi.name, pi.uid, node, self._bind_annotations(pi, node)))
                 self._bind_cbs.append(cb)
                 return
-            self.native.bind(pi.namespace, pi.name, pi.uid, node, self._bind_annotations(pi, node), cb,
+            self._binds.bind(pi.namespace, pi.name, pi.uid, node, self._bind_annotations(pi, node), cb,
                              self.bind_timeout)
             return
         self._bind_dq.append(item)
@@ -1234,7 +1251,7 @@ class Scheduler:
             st = Status.ok()
         else:
             from ..kube.native import api_error
-            if status == 401:
+            if status == 401 and self.native is not None:
                 self.client._refresh_token(force=True)
             st = Status.error(f"binding rejected: {api_error(status, body)}", plugin="DefaultBinder")
         self._after_bind(fw, state if state is not None else _EMPTY_STATE, pi, node, cycle, t0, tb, st)

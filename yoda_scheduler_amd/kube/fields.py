@@ -15,6 +15,18 @@ Matcher = Callable[[dict], bool]
 
 def _getter(path: str):
     keys = tuple(path.split("."))
+    if len(keys) == 2:                 # spec.nodeName, status.phase, metadata.name: unrolled
+        k0, k1 = keys
+
+        def get2(obj: dict) -> str:
+            v = obj.get(k0)
+            if not isinstance(v, dict):
+                return ""
+            v = v.get(k1)
+            if v is None:
+                return ""
+            return v if isinstance(v, str) else str(v)
+        return get2
 
     def get(obj: dict) -> str:
         v = obj

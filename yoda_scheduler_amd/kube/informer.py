@@ -60,6 +60,9 @@ class Backoff:
         self._cur = self.initial
 
 
+_EMPTY: dict = {}
+
+
 class Informer:
     def __init__(self, client, res: str, on_add: Optional[Handler] = None,
                  on_update: Optional[Callable[[dict, dict], None]] = None,
@@ -90,7 +93,8 @@ class Informer:
             log.exception("informer %s: event handler failed", self.res)
 
     def _dispatch(self, typ: str, obj: dict) -> None:
-        key = obj_key(self.r, obj)
+        m = obj.get("metadata") or _EMPTY
+        key = f"{m.get('namespace') or 'default'}/{m.get('name', '')}" if self.r.namespaced else m.get("name", "")
         if typ == "DELETED":
             old = self.store.pop(key, None)
             if self.on_delete:
@@ -103,7 +107,7 @@ class Informer:
                     self._call(self.on_add, obj)
             elif self.on_update:
                 self._call(self.on_update, old, obj)
-        rv = (obj.get("metadata") or {}).get("resourceVersion")
+        rv = m.get("resourceVersion")
         if rv:
             self.resource_version = rv
 
@@ -137,17 +141,28 @@ class Informer:
         self.resource_version = rv
         self.relists += 1
 
+    def _event(self, typ: str, obj: dict) -> None:
+        if typ == "ERROR":
+            raise ApiError(int(obj.get("code", 500)), obj.get("reason", "Error"), obj.get("message", ""))
+        if typ == "BOOKMARK":
+            rv = (obj.get("metadata") or {}).get("resourceVersion")
+            if rv:
+                self.resource_version = rv
+                self.bookmarks += 1
+            return
+        self._dispatch(typ, obj)
+
     async def _watch_once(self) -> None:
+        batches = getattr(self.client, "watch_batches", None)
+        if batches is not None:           # in-process apiserver: a burst's events per read
+            async for batch in batches(self.res, self.resource_version, **self._fs()):
+                for typ, obj in batch:
+                    self._event(typ, obj)
+                    if self._stop:
+                        return
+            return
         async for typ, obj in self.client.watch(self.res, self.resource_version, **self._fs()):
-            if typ == "ERROR":
-                raise ApiError(int(obj.get("code", 500)), obj.get("reason", "Error"), obj.get("message", ""))
-            if typ == "BOOKMARK":
-                rv = (obj.get("metadata") or {}).get("resourceVersion")
-                if rv:
-                    self.resource_version = rv
-                    self.bookmarks += 1
-                continue
-            self._dispatch(typ, obj)
+            self._event(typ, obj)
             if self._stop:
                 return
 

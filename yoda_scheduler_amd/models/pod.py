@@ -301,47 +301,84 @@ class PodInfo:
         spec = obj.get("spec") or _EMPTY
         labels = meta.get("labels") or {}
         uid = meta.get("uid") or pod_key(obj)
-        cpu, mem, nzc, nzm = _requests(spec)
-        aff = spec.get("affinity")
-        req = pref = None
-        if aff:
-            na = aff.get("nodeAffinity") or _EMPTY
-            req = _terms((na.get("requiredDuringSchedulingIgnoredDuringExecution") or _EMPTY).get("nodeSelectorTerms"))
-            pref = [(int(p.get("weight", 0)), _terms([p.get("preference") or {}])[0])
-                    for p in na.get("preferredDuringSchedulingIgnoredDuringExecution") or ()]
-        tols = spec.get("tolerations")
-        if tols:
-            tols = [(t.get("key") or None, str(t.get("value", "") or ""), t.get("operator", "Equal") or "Equal",
-                     t.get("effect", "") or "") for t in tols]
-        ports = None
-        for c in spec.get("containers") or ():
-            for p in c.get("ports") or ():
-                if p.get("hostPort"):
-                    (ports := ports or []).append((p.get("hostPort"), p.get("protocol", "TCP"), p.get("hostIP", "")))
-        ns = spec.get("nodeSelector")
-        ann = meta.get("annotations")
-        ext = ext_requests(spec) if _has_ext(spec) else None
         containers = spec.get("containers") or ()
-        images = [normalize_image(c.get("image")) for c in containers if c.get("image")]
+        # one pass over the containers: requests, extended requests, host ports, images
+        cpu = mem = nzc = nzm = 0
+        ext = ports = None
+        images = []
+        for c in containers:
+            img = c.get("image")
+            if img:
+                images.append(normalize_image(img))
+            res = c.get("resources")
+            r = res.get("requests") if res else None
+            if r:
+                if "cpu" in r:
+                    v = cpu_millis(r["cpu"])
+                    cpu += v
+                    nzc += v
+                else:
+                    nzc += DEFAULT_MILLI_CPU_REQUEST
+                if "memory" in r:
+                    v = bytes_of(r["memory"])
+                    mem += v
+                    nzm += v
+                else:
+                    nzm += DEFAULT_MEMORY_REQUEST
+                if len(r) > ("cpu" in r) + ("memory" in r):
+                    ext = ext if ext is not None else {}
+                    for k, q in r.items():
+                        if k not in _BASIC:
+                            ext[k] = ext.get(k, 0) + quantity_int(q)
+            else:
+                nzc += DEFAULT_MILLI_CPU_REQUEST
+                nzm += DEFAULT_MEMORY_REQUEST
+            cp = c.get("ports")
+            if cp:
+                for p in cp:
+                    if p.get("hostPort"):
+                        (ports := ports or []).append((p.get("hostPort"), p.get("protocol", "TCP"),
+                                                       p.get("hostIP", "")))
+        req = pref = tols = ns = spread = pod_aff = None
+        if not _RARE_SPEC.isdisjoint(spec):
+            if "initContainers" in spec or "overhead" in spec:
+                cpu, mem, nzc, nzm = _requests(spec)
+                ext = ext_requests(spec) if _has_ext(spec) else None
+            aff = spec.get("affinity")
+            if aff:
+                na = aff.get("nodeAffinity") or _EMPTY
+                req = _terms((na.get("requiredDuringSchedulingIgnoredDuringExecution") or _EMPTY)
+                             .get("nodeSelectorTerms"))
+                pref = [(int(p.get("weight", 0)), _terms([p.get("preference") or {}])[0])
+                        for p in na.get("preferredDuringSchedulingIgnoredDuringExecution") or ()]
+                if aff.get("podAffinity") or aff.get("podAntiAffinity"):
+                    pod_aff = _pod_aff(aff)
+            tols = spec.get("tolerations")
+            if tols:
+                tols = [(t.get("key") or None, str(t.get("value", "") or ""), t.get("operator", "Equal") or "Equal",
+                         t.get("effect", "") or "") for t in tols]
+            ns = spec.get("nodeSelector")
+            tsc = spec.get("topologySpreadConstraints")
+            if tsc:
+                from .selectors import LabelSelector
+                spread = [(c.get("topologyKey", ""), int(c.get("maxSkew", 1)),
+                           c.get("whenUnsatisfiable", "DoNotSchedule"),
+                           None if c.get("labelSelector") is None else LabelSelector(c.get("labelSelector")).native())
+                          for c in tsc]
+        if ext:
+            ext = {k: v for k, v in ext.items() if v} or None
         owner = avoid = None
-        for r in meta.get("ownerReferences") or ():
-            if not r.get("controller"):
-                continue
-            if owner is None:
-                owner = (r.get("apiVersion", "") or "", r.get("kind", "") or "", r.get("name", "") or "",
-                         r.get("uid", "") or "")
-            if avoid is None and r.get("kind") in ("ReplicationController", "ReplicaSet"):
-                avoid = (r.get("kind"), r.get("uid", "") or "")
-        spread = None
-        tsc = spec.get("topologySpreadConstraints")
-        if tsc:
-            from .selectors import LabelSelector
-            spread = [(c.get("topologyKey", ""), int(c.get("maxSkew", 1)), c.get("whenUnsatisfiable", "DoNotSchedule"),
-                       None if c.get("labelSelector") is None else LabelSelector(c.get("labelSelector")).native())
-                      for c in tsc]
-        pod_aff = None
-        if aff and (aff.get("podAffinity") or aff.get("podAntiAffinity")):
-            pod_aff = _pod_aff(aff)
+        refs = meta.get("ownerReferences")
+        if refs:
+            for r in refs:
+                if not r.get("controller"):
+                    continue
+                if owner is None:
+                    owner = (r.get("apiVersion", "") or "", r.get("kind", "") or "", r.get("name", "") or "",
+                             r.get("uid", "") or "")
+                if avoid is None and r.get("kind") in ("ReplicationController", "ReplicaSet"):
+                    avoid = (r.get("kind"), r.get("uid", "") or "")
+        ann = meta.get("annotations")
         return cls(obj, uid, meta.get("namespace", "default"), meta.get("name", ""), pod_num_id(uid), labels,
                    parse_gpu_request(labels), spec.get("schedulerName") or "default-scheduler",
                    spec.get("nodeName") or "", cpu, mem, int(spec.get("priority") or 0),
@@ -350,6 +387,9 @@ class PodInfo:
                    bool(meta.get("deletionTimestamp")), pod_aff)
 
 
+# spec fields a plain pod does not carry (from_obj parses them only when one is present)
+_RARE_SPEC = frozenset(("initContainers", "overhead", "affinity", "tolerations", "nodeSelector",
+                        "topologySpreadConstraints"))
 _EMPTY: dict = {}
 _NOLIST: list = []
 

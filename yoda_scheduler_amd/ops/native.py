@@ -208,10 +208,30 @@ def avoid_controllers(raw) -> list:
     return out
 
 
+_shared_reqs: list = [None, {}]      # [engine, {template key: PodReq}]
+
+
 def pod_req(engine, pi: PodInfo):
-    """Build (and cache on the PodInfo) the engine's PodReq."""
+    """Build (and cache on the PodInfo) the engine's PodReq.
+
+    Pods stamped from one template (a ReplicaSet's, a Job's, a burst's) share a PodReq: the
+    engine only ever reads it (``const PodReq&``), so a pod without node-side constraints,
+    extended resources or spread / affinity terms takes the PodReq of the last pod with the
+    same requests, labels, namespace, images and owner instead of two extension calls."""
     if pi.native_owner is engine and pi.native_req is not None:
         return pi.native_req
+    key = None
+    if not (pi.node_name or pi.node_selector or pi.required_terms or pi.preferred_terms or pi.tolerations
+            or pi.ext or pi.spread or pi.pod_aff):
+        key = (pi.gpu, pi.cpu_m, pi.mem, pi.nz_cpu_m, pi.nz_mem, pi.namespace, tuple(pi.labels.items()),
+               tuple(pi.images), pi.containers, pi.owner, pi.avoid, pi.deleting)
+        shared = _shared_reqs
+        if shared[0] is not engine:
+            shared[0], shared[1] = engine, {}
+        r = shared[1].get(key)
+        if r is not None:
+            pi.native_req, pi.native_owner = r, engine
+            return r
     g = pi.gpu
     r = engine.make_req(g.has_number, g.number, g.has_memory, g.memory, g.has_clock, g.clock,
                         g.clock_min, g.priority, pi.node_name, pi.cpu_m, pi.mem,
@@ -220,4 +240,9 @@ def pod_req(engine, pi: PodInfo):
     engine.set_req_extras(r, pi.namespace, list(pi.labels.items()), pi.deleting, pi.images, pi.containers,
                           list(pi.ext.items()), pi.owner, pi.avoid, pi.spread, pi.pod_aff)
     pi.native_req, pi.native_owner = r, engine
+    if key is not None:
+        cache = _shared_reqs[1]
+        if len(cache) >= 4096:
+            cache.clear()
+        cache[key] = r
     return r
