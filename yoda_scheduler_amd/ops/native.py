@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import importlib
 import threading
+import weakref
 
 from ..models.pod import NodeInfo, PodInfo
 from ..models.scv import HEALTHY, LazyLinks, LazyScv, Scv
@@ -208,7 +209,7 @@ def avoid_controllers(raw) -> list:
     return out
 
 
-_shared_reqs: list = [None, {}]      # [engine, {template key: PodReq}]
+_shared_reqs: list = [None, {}]      # [weakref to the engine, {template key: PodReq}]
 
 
 def pod_req(engine, pi: PodInfo):
@@ -226,8 +227,8 @@ def pod_req(engine, pi: PodInfo):
         key = (pi.gpu, pi.cpu_m, pi.mem, pi.nz_cpu_m, pi.nz_mem, pi.namespace, tuple(pi.labels.items()),
                tuple(pi.images), pi.containers, pi.owner, pi.avoid, pi.deleting)
         shared = _shared_reqs
-        if shared[0] is not engine:
-            shared[0], shared[1] = engine, {}
+        if shared[0] is None or shared[0]() is not engine:   # weak: a shut-down engine is freed
+            shared[0], shared[1] = weakref.ref(engine), {}
         r = shared[1].get(key)
         if r is not None:
             pi.native_req, pi.native_owner = r, engine
