@@ -371,6 +371,7 @@ def main(argv=None) -> int:
                                                          "reset_post_ms": round(getattr(sh, "last_reset_post_s", 0) * 1e3, 3),
                                                          "reset_ms": round(getattr(sh, "last_reset_s", 0) * 1e3, 3),
                                                          "reset_trace": getattr(sh, "last_reset_trace", None),
+                                                         "reset_drain": getattr(sh, "last_reset_drain", None),
                                                          # [created, bound] ms of every 50th pod in creation order
                                                          "pods": [[round(c * 1e3, 3), round(b * 1e3, 3)] for c, b in
                                                                   (getattr(sh, "last_timeline", None) or [])[::50]],

@@ -277,7 +277,23 @@ class HttpShard:
                 lp = asyncio.get_event_loop()
                 lp.slow_callback_duration = 0.0003
                 lp.set_debug(True)
-            if sched.lane is not None:
+            if sched.lane is not None and trace is not None:
+                # runlog: the drain curve (ms, lane-owned pods, watch events decoded) every 0.2 ms
+                # (+ the I/O thread's watch-decode CPU ms and the watch bytes read since the POST)
+                nat = getattr(self.client, "native", None)
+                s0 = nat.stats() if nat is not None else {}
+                drain = self.last_reset_drain = []
+                while True:
+                    owned = sched.lane_owned()
+                    s1 = nat.stats() if nat is not None else {}
+                    drain.append((round((time.perf_counter() - tr) * 1e3, 3), owned,
+                                  s1.get("watch_events", 0) - s0.get("watch_events", 0),
+                                  round((s1.get("watch_cpu_s", 0.0) - s0.get("watch_cpu_s", 0.0)) * 1e3, 3),
+                                  s1.get("watch_bytes", 0) - s0.get("watch_bytes", 0)))
+                    if not owned or time.perf_counter() - tr > 60.0:
+                        break
+                    await asyncio.sleep(0.0002)
+            elif sched.lane is not None:
                 # woken by the lane when its last pod is released (an asyncio sleep shorter than
                 # a millisecond still waits for epoll's 1 ms tick when nothing else wakes the loop)
                 await sched.lane.wait_unowned(60.0)
