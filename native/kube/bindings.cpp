@@ -182,12 +182,20 @@ PYBIND11_MODULE(_yoda_kube, m) {
     return py::make_tuple(p.ns, p.name, p.uid, p.rv, p.creation, p.deleting, p.sched, p.node, p.phase);
   };
   m.def("scan_identity", [ident_tuple](const std::string& line, bool only_md) -> py::object {
-    PodProj p;
+    PodEv e;
     char t = 0;
     std::string_view obj;
-    if (!scan_watch_identity(line, &t, &obj, p, only_md)) return py::none();
-    return py::make_tuple(std::string(1, t), std::string(obj), ident_tuple(p));
-  }, py::arg("line"), py::arg("only_md") = false);
+    if (!scan_watch_identity(line, &t, &obj, e.p, only_md)) return py::none();
+    const bool partial = e.p.ident_partial;
+    if (partial) {                         // completed as the transport's PodEv::full() does
+      e.raw.assign(obj.data(), obj.size());
+      e.light = true;
+      e.complete = &complete_pod_ev;
+      e.full();
+    }
+    return py::make_tuple(std::string(1, t), std::string(obj), ident_tuple(e.p), partial);
+  }, py::arg("line"), py::arg("only_md") = false,
+     "(type, object text, identity tuple, scanned to metadata only) or None when the parser must decide");
   m.def("scan_labels_hash", [](const std::string& line) -> py::object {
     PodProj p;
     char t = 0;

@@ -889,7 +889,7 @@ uint64_t labels_span_hash(std::string_view raw) {
 }
 
 bool scan_watch_identity(std::string_view line, char* type, std::string_view* obj, PodProj& p, bool only_md) {
-  p = PodProj();
+  // p: default-constructed by the caller (resetting a PodProj here cost a quarter of the scan)
   bool labels_seen = false;
   std::string_view labels_raw;
   Skim k{line.data(), line.data() + line.size()};
@@ -942,12 +942,23 @@ bool scan_watch_identity(std::string_view line, char* type, std::string_view* ob
     seen |= 128;
     return k.sv(&phase, &ok) || (ok = false);
   };
+  // DELETED (transport mode): the object's closing brace, found from the line's end — a watch
+  // line is {"type":..,"object":{..}} — so the scan can stop after metadata (the lane drops a
+  // deleted pod by key; sched / node / phase are filled on first use, PodProj::ident_partial)
+  const char* obj_close = nullptr;
   auto pod = [&](std::string_view key) -> bool {
     k.ws();
     const bool is_obj = k.p < k.e && *k.p == '{';
     if (key == "metadata" && !seen_meta) {
       seen_meta = true;
-      if (is_obj) return k.object(meta) || (ok = false);
+      if (is_obj) {
+        if (!k.object(meta)) return ok = false;
+        if (obj_close) {
+          k.p = obj_close;           // the object() loop then sees its closing brace
+          p.ident_partial = true;
+        }
+        return true;
+      }
     } else if (key == "spec" && !seen_spec) {
       seen_spec = true;
       if (is_obj) return k.object(spec) || (ok = false);
@@ -975,6 +986,15 @@ bool scan_watch_identity(std::string_view line, char* type, std::string_view* ob
       have_obj = true;
       k.ws();
       const char* s = k.p;
+      if (only_md && have_type && tname == "DELETED" && k.p < k.e && *k.p == '{') {
+        const char* q = k.e;
+        while (q > k.p && (q[-1] == ' ' || q[-1] == '\n' || q[-1] == '\r' || q[-1] == '\t')) --q;
+        if (q > k.p && q[-1] == '}') {       // the line's closing brace
+          --q;
+          while (q > k.p && (q[-1] == ' ' || q[-1] == '\n' || q[-1] == '\r' || q[-1] == '\t')) --q;
+          if (q > k.p + 1 && q[-1] == '}') obj_close = q - 1;
+        }
+      }
       if (!k.object(pod)) return ok = false, true;
       *obj = std::string_view(s, size_t(k.p - s));
       return true;

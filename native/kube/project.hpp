@@ -68,6 +68,10 @@ struct PodProj {
   // watch identity scanner too, so a light event tells whether a pod's labels changed
   // without being projected (the lane's per-node selector census keeps the older projection)
   uint64_t labels_hash = 0;
+  // a DELETED line scanned up to metadata only (scan_watch_identity): sched / node / phase are
+  // not read yet — PodEv::full() fills them. Nothing reads them of a deletion before that: the
+  // lane drops its entry by key, and whatever goes on to Python is completed first.
+  bool ident_partial = false;
   // default-plugin inputs (models/pod.py PodInfo.images / containers / ext / owner / avoid /
   // spread): normalized images of spec.containers and their count, requests beyond cpu/memory
   // (non-zero, models/pod.py::ext_requests), the first controller ownerReference, the first
@@ -119,6 +123,7 @@ void project_identity(const FlatDoc::View& pod, PodProj& p);
 // for the event type, the object's text span and the pod's identity fields (as
 // project_identity reads them), building no document. False when the line needs the parser
 // (escapes in a field it reads, malformed text): the caller then takes the FlatDoc path.
+// `p` must be default-constructed (the scan only sets the fields it reads).
 bool scan_watch_identity(std::string_view line, char* type, std::string_view* obj, PodProj& p,
                          bool only_md = false);
 // Fill everything but the identity fields from a full projection (`src` is consumed).

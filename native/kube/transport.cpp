@@ -339,6 +339,12 @@ void complete_pod_ev(PodEv* e) {
   PodProj full;
   FlatDoc d;
   if (d.parse(e->raw)) project_pod(d.root(), full);
+  if (e->p.ident_partial) {            // a deletion scanned to metadata only
+    e->p.sched = full.sched.empty() ? "default-scheduler" : full.sched;
+    e->p.node = full.node;
+    e->p.phase = full.phase;
+    e->p.ident_partial = false;
+  }
   merge_non_identity(e->p, std::move(full));
 }
 
