@@ -1667,18 +1667,32 @@ void Lane::patch_condition(Entry& e, const std::string& msg) {
   // pod already carries the same PodScheduled=False reason and message
   yk::PodPort* port = port_.load();
   if (!port) return;
-  if (!e.cond_msg.empty() && e.cond_msg == msg) {
+  // upstream podutil.UpdatePodCondition against the pod's current condition (the latest event
+  // of the entry); while none is visible yet, the condition this lane last wrote stands in for
+  // it (its echo is on the way). A condition another writer changed is written again.
+  const yk::PodProj& cur = e.ev->full();
+  bool same;
+  std::string ltt;
+  if (cur.has_sched_cond) {
+    same = cur.sched_cond_status == "False" && cur.sched_cond_reason == "Unschedulable" && cur.sched_cond_msg == msg;
+    if (cur.sched_cond_status == "False" && !cur.sched_cond_ltt.empty()) ltt = cur.sched_cond_ltt;   // no transition
+  } else {
+    same = !e.cond_msg.empty() && e.cond_msg == msg;
+    ltt = e.cond_ltt;
+  }
+  if (same) {
     std::lock_guard<std::mutex> g(stat_mu_);
     st_.status_patches_skipped++;
     return;
   }
-  if (e.cond_ltt <= 0) e.cond_ltt = wall();
+  if (ltt.empty()) ltt = rfc3339(wall());
   e.cond_msg = msg;
+  e.cond_ltt = ltt;
   std::string b;
   b.reserve(200 + msg.size());
   b += "{\"status\":{\"conditions\":[{\"type\":\"PodScheduled\",\"status\":\"False\",\"lastProbeTime\":null,"
        "\"lastTransitionTime\":";
-  json_str(rfc3339(e.cond_ltt), b);
+  json_str(ltt, b);
   b += ",\"reason\":\"Unschedulable\",\"message\":";
   json_str(msg, b);
   b += "}]}}";

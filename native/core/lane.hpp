@@ -244,11 +244,9 @@ class Lane : public yk::PodSink {
     double t_park = 0;       // when it entered unschedulableQ
     uint64_t bseq = 0;       // backoff heap item of this entry (stale items are skipped)
     std::shared_ptr<PodReq> req;   // the request of the failed attempt (move hints re-filter with it)
-    // the PodScheduled=False condition this lane last wrote for the pod: an unchanged message
-    // is not written again, and lastTransitionTime stays that of the first write (upstream
-    // podutil.UpdatePodCondition: the status did not transition)
-    std::string cond_msg;
-    double cond_ltt = 0;
+    // the PodScheduled=False condition this lane last wrote for the pod (message and
+    // lastTransitionTime): what the pod says until the write's echo arrives
+    std::string cond_msg, cond_ltt;
     // a reserved pod's event whose labels are current: later watch echoes keep it while their
     // labels hash says the labels did not change, so the selector census never projects them
     std::shared_ptr<yk::PodEv> lab_ev;

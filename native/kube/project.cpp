@@ -357,6 +357,19 @@ void project_generic(N pod, PodProj& p) {
   if (N st = pod.get("status")) p.phase = std::string(st.sv("phase"));
   p.spec_meta_hash = spec_hash(sp, meta_hash(meta));
   p.labels_hash = labels_hash_of(m.get("labels"));
+  if (N st = pod.get("status"); st && st.obj()) {
+    if (N cs = st.get("conditions"); cs && cs.arr()) {
+      cs.each([&](std::string_view, N c) {
+        if (!c.obj() || c.sv("type") != "PodScheduled") return true;
+        p.has_sched_cond = true;
+        p.sched_cond_status = std::string(c.sv("status"));
+        p.sched_cond_reason = std::string(c.sv("reason"));
+        p.sched_cond_msg = std::string(c.sv("message"));
+        p.sched_cond_ltt = std::string(c.sv("lastTransitionTime"));
+        return false;                       // the first one, as a by-type merge keeps one
+      });
+    }
+  }
 
   // ---- everything below: fall back to Python on any shape the projection does not mirror
   if (!kvs(m.get("labels"), p.labels)) return;
@@ -1056,6 +1069,11 @@ void merge_non_identity(PodProj& d, PodProj&& s) {
   d.flags = s.flags;
   d.spec_meta_hash = s.spec_meta_hash;
   d.ok = s.ok;
+  d.has_sched_cond = s.has_sched_cond;
+  d.sched_cond_status = std::move(s.sched_cond_status);
+  d.sched_cond_reason = std::move(s.sched_cond_reason);
+  d.sched_cond_msg = std::move(s.sched_cond_msg);
+  d.sched_cond_ltt = std::move(s.sched_cond_ltt);
 }
 
 bool project_pod_text(std::string_view text, PodProj& p) {

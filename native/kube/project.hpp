@@ -72,6 +72,10 @@ struct PodProj {
   // not read yet — PodEv::full() fills them. Nothing reads them of a deletion before that: the
   // lane drops its entry by key, and whatever goes on to Python is completed first.
   bool ident_partial = false;
+  // status.conditions' PodScheduled entry (upstream updatePod compares the condition it would
+  // write with the pod's current one): status, reason, message, lastTransitionTime
+  bool has_sched_cond = false;
+  std::string sched_cond_status, sched_cond_reason, sched_cond_msg, sched_cond_ltt;
   // default-plugin inputs (models/pod.py PodInfo.images / containers / ext / owner / avoid /
   // spread): normalized images of spec.containers and their count, requests beyond cpu/memory
   // (non-zero, models/pod.py::ext_requests), the first controller ownerReference, the first

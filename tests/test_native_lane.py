@@ -745,6 +745,39 @@ def test_unschedulable_condition_is_a_strategic_patch_written_once(server, lane)
         assert len(log) == 1 and log[0][3] is True          # one PATCH, strategic
 
 
+@pytest.mark.parametrize("server", ["python", "native"])
+def test_unschedulable_condition_changed_by_another_writer_is_written_again(server):
+    """Upstream updatePod compares the condition with the pod's current one, not with what the
+    scheduler last sent: when another writer replaces the PodScheduled condition between two
+    failed attempts, the lane writes its condition again; lastTransitionTime is kept while the
+    status stays False."""
+    async def go():
+        cfg = yoda_config(backoff=0.05, max_backoff=0.1)
+        async with Env(server=server, lane="on", cfg=cfg, nodes=(("n1", 8, [294912] * 8),)) as e:
+            await e.create(pod("never", {"scv/memory": "80000"}))
+            st = lambda: e.sched.lane.lane.stats()                          # noqa: E731
+            assert await e.wait(lambda: st()["status_patches"] >= 1)
+            await asyncio.sleep(0.1)
+            first = {c["type"]: c for c in (await e.pods())["never"]["status"]["conditions"]}["PodScheduled"]
+            # another writer: same status, another message (strategic: merged by type)
+            await e.cl.patch("pods", "never", {"status": {"conditions": [
+                {"type": "PodScheduled", "status": "False", "reason": "Unschedulable",
+                 "message": "set by someone else", "lastTransitionTime": first["lastTransitionTime"]}]}},
+                "default", strategic=True)
+            n0 = st()["native_failed"]
+            t0 = time.time()
+            while st()["status_patches"] < 2 and time.time() - t0 < 8:
+                e.sched.queue.move_all_to_active_or_backoff("test")
+                await asyncio.sleep(0.05)
+            await asyncio.sleep(0.2)
+            last = {c["type"]: c for c in (await e.pods())["never"]["status"]["conditions"]}["PodScheduled"]
+            return st(), n0, first, last
+    stats, n0, first, last = run(go())
+    assert stats["status_patches"] == 2 and stats["native_failed"] > n0
+    assert last["message"] == first["message"] and last["message"].startswith("0/1 nodes are available")
+    assert last["lastTransitionTime"] == first["lastTransitionTime"]
+
+
 def test_lane_parked_pods_show_in_pending_and_attempt_metrics():
     """a pod the lane keeps in its own unschedulableQ counts in
     scheduler_pending_pods{queue="unschedulable"}, and the lane's attempts — acknowledged
