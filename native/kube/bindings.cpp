@@ -156,6 +156,12 @@ PYBIND11_MODULE(_yoda_kube, m) {
       .def_property_readonly("hash", [](const PodEv& e) { return e.full().spec_meta_hash; })
       .def_property_readonly("flags", [](const PodEv& e) { return e.full().flags; })
       .def_property_readonly("labels_hash", [](const PodEv& e) { return e.p.labels_hash; })
+      // status.conditions' PodScheduled entry: (status, reason, message, lastTransitionTime) or None
+      .def_property_readonly("sched_cond", [](const PodEv& e) -> py::object {
+        const PodProj& p = e.full();
+        if (!p.has_sched_cond) return py::none();
+        return py::make_tuple(p.sched_cond_status, p.sched_cond_reason, p.sched_cond_msg, p.sched_cond_ltt);
+      })
       // (key, uid, node, scheduler, phase, hash): the per-event fields in one call
       .def("ident", [](const PodEv& e) {
         const PodProj& p = e.full();

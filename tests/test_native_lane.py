@@ -745,17 +745,22 @@ def test_unschedulable_condition_is_a_strategic_patch_written_once(server, lane)
         assert len(log) == 1 and log[0][3] is True          # one PATCH, strategic
 
 
-@pytest.mark.parametrize("server", ["python", "native"])
-def test_unschedulable_condition_changed_by_another_writer_is_written_again(server):
+@pytest.mark.parametrize("server,lane", [("python", "on"), ("native", "on"), ("python", "off")])
+def test_unschedulable_condition_changed_by_another_writer_is_written_again(server, lane):
     """Upstream updatePod compares the condition with the pod's current one, not with what the
     scheduler last sent: when another writer replaces the PodScheduled condition between two
     failed attempts, the lane writes its condition again; lastTransitionTime is kept while the
     status stays False."""
     async def go():
         cfg = yoda_config(backoff=0.05, max_backoff=0.1)
-        async with Env(server=server, lane="on", cfg=cfg, nodes=(("n1", 8, [294912] * 8),)) as e:
+        async with Env(server=server, lane=lane, cfg=cfg, nodes=(("n1", 8, [294912] * 8),)) as e:
             await e.create(pod("never", {"scv/memory": "80000"}))
-            st = lambda: e.sched.lane.lane.stats()                          # noqa: E731
+            if lane == "on":
+                st = lambda: e.sched.lane.lane.stats()                      # noqa: E731
+            else:                   # the Python path: the fake apiserver's PATCH log (minus ours below)
+                def st():
+                    log = [x for x in e.srv.patch_log if x[2] == "never" and "someone" not in str(x[4])]
+                    return {"status_patches": len(log), "native_failed": e.sched.failed}
             assert await e.wait(lambda: st()["status_patches"] >= 1)
             await asyncio.sleep(0.1)
             first = {c["type"]: c for c in (await e.pods())["never"]["status"]["conditions"]}["PodScheduled"]

@@ -42,6 +42,15 @@ log = logging.getLogger("yoda.scheduler")
 
 _EMPTY_STATE = CycleState()      # shared read-only state for all-native cycles
 _EMPTY_DICT: dict = {}
+
+
+def _sched_cond(obj: dict) -> Optional[tuple]:
+    """status.conditions' PodScheduled entry of a pod object, as ``PodEvent.sched_cond``."""
+    for c in ((obj.get("status") or _EMPTY_DICT).get("conditions")) or ():
+        if isinstance(c, dict) and c.get("type") == "PodScheduled":
+            return (str(c.get("status") or ""), str(c.get("reason") or ""), str(c.get("message") or ""),
+                    str(c.get("lastTransitionTime") or ""))
+    return None
 ENGINE_SWITCH_INTERVAL_S = 0.0002
 POD_FIELD_SELECTOR = "status.phase!=Succeeded,status.phase!=Failed"   # upstream NewPodInformer
 _VOLATILE_META = ("resourceVersion", "generation", "managedFields")
@@ -385,8 +394,11 @@ class Scheduler:
             else:
                 self.cache.update_pod(new)
         elif self._responsible(new) and not self._terminal(new):
-            if self.cache.is_assumed(new["metadata"].get("uid")):
+            uid = new["metadata"].get("uid")
+            if self.cache.is_assumed(uid):
                 return   # upstream skipPodUpdate: assumed pods only get status noise
+            if self._conditions and uid in self._conditions:
+                self._sync_condition(uid, _sched_cond(new))
             if not _pod_updated(old, new):
                 return   # status/resourceVersion-only change (e.g. our own PodScheduled=False)
             self.queue.update(PodInfo.from_obj(new))
@@ -459,6 +471,8 @@ class Scheduler:
         elif sched in self.frameworks and not terminal:
             if self.cache.is_assumed(uid):
                 return   # upstream skipPodUpdate
+            if self._conditions and uid in self._conditions:
+                self._sync_condition(uid, ev.sched_cond)
             if oidt[5] == h:
                 return   # status/resourceVersion-only change
             self.queue.update(PodInfo.from_native(ev))
@@ -890,15 +904,27 @@ class Scheduler:
         self.queue.add_unschedulable(pi, cycle, unschedulable)
         asyncio.get_event_loop().create_task(self._update_condition(pi, msg, nominated))
 
+    def _sync_condition(self, uid: str, cond: Optional[tuple]) -> None:
+        """A pending pod's PodScheduled condition as its latest update shows it ((status, reason,
+        message, lastTransitionTime) or None): what ``_condition_patch`` compares with next, as
+        upstream compares with the informer's pod. None (not echoed yet) keeps what was written."""
+        if cond is None:
+            return
+        prev = self._conditions.get(uid)
+        if cond[0] == "False":
+            self._conditions[uid] = (cond[1], cond[2], cond[3], prev[3] if prev else "")
+        else:                       # another status: the next write is a transition
+            self._conditions.pop(uid, None)
+
     def _condition_patch(self, pi: PodInfo, msg: str, nominated: str) -> Optional[dict]:
         """upstream v1.20 ``updatePod`` + ``podutil.UpdatePodCondition``: the PodScheduled=False
         condition as a strategic merge patch of pods/status, or None when the pod already says
         the same (same status, reason and message, no new nominated node) — then nothing is
         written. lastTransitionTime is set when the condition first appears and kept while its
-        status stays False. What the pod "already says" is what this scheduler last wrote for it
-        (its own writes' echoes are status-only updates the queue does not re-read), or the
-        condition on the pod object when that is already decoded (a condition a previous
-        scheduler instance wrote)."""
+        status stays False. What the pod "already says" is its condition as its latest update
+        showed it (``_sync_condition``), else what this scheduler last wrote for it (until the
+        write's echo arrives), or the condition on the pod object when that is already decoded
+        (a condition a previous scheduler instance wrote)."""
         prev = self._conditions.get(pi.uid)
         if prev is None and pi._obj is not None:
             for c in ((pi._obj.get("status") or {}).get("conditions")) or ():
