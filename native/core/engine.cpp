@@ -1080,26 +1080,6 @@ void Engine::interpod_prefilter(const PodReq& req, InterPodPF* pf) const {
   bool self = true;
   for (const PodTerm& t : aff) self = self && t.matches(req.ns, req.labels);
   pf->self_match = self;
-  // pods of node n matching one term: from the label index when its selector is a single label
-  // (or empty), else by walking the node's pods
-  auto term_count = [&](const Node& n, const PodTerm& t) -> int64_t {
-    int64_t sum = 0, c = 0;
-    bool ok = true;
-    for (int32_t ns : t.ns) {
-      if (!indexed_count(n, ns, t.sel, false, &c)) {
-        ok = false;
-        break;
-      }
-      sum += c;
-    }
-    if (ok) return sum;
-    sum = 0;
-    for (uint64_t id : n.pods) {
-      const Assignment& a = ledger_.at(id);
-      sum += t.matches(a.ns, a.labels);
-    }
-    return sum;
-  };
   for (const Node& n : nodes_) {
     if (!n.alive || n.pods.empty()) continue;
     if (!aff.empty()) {
@@ -1175,18 +1155,18 @@ void Engine::interpod_scores(const PodReq& req, const std::vector<int32_t>& feas
   std::unordered_set<int32_t> keys;
   const bool pref = req.aff && (!req.aff->pref_aff.empty() || !req.aff->pref_anti.empty());
   if (pref) {
+    // Σ over the pods a term matches of ± its weight = ± weight × the node's matching count
     for (const Node& n : nodes_) {
       if (!n.alive || n.pods.empty()) continue;
-      for (uint64_t id : n.pods) {
-        const Assignment& a = ledger_.at(id);
-        for (int sign = 1; sign >= -1; sign -= 2)
-          for (const PodTerm& t : sign > 0 ? req.aff->pref_aff : req.aff->pref_anti) {
-            auto lab = n.labels.find(t.key);
-            if (lab == n.labels.end() || !t.matches(a.ns, a.labels)) continue;
-            dom[pair_key(t.key, lab->second)] += sign * (int64_t)t.weight;
-            keys.insert(t.key);
-          }
-      }
+      for (int sign = 1; sign >= -1; sign -= 2)
+        for (const PodTerm& t : sign > 0 ? req.aff->pref_aff : req.aff->pref_anti) {
+          auto lab = n.labels.find(t.key);
+          if (lab == n.labels.end()) continue;
+          const int64_t c = term_count(n, t);
+          if (!c) continue;
+          dom[pair_key(t.key, lab->second)] += sign * (int64_t)t.weight * c;
+          keys.insert(t.key);
+        }
     }
   }
   for (uint64_t id : aff_holders_) {
@@ -1374,6 +1354,25 @@ void Engine::index_pod(Node& n, const Assignment& a, int sign) {
   };
   bump(LKey{a.ns, -1, -1});
   for (const auto& kv : a.labels) bump(LKey{a.ns, kv.first, kv.second});
+}
+
+int64_t Engine::term_count(const Node& n, const PodTerm& t) const {
+  int64_t sum = 0, c = 0;
+  bool ok = true;
+  for (int32_t ns : t.ns) {
+    if (!indexed_count(n, ns, t.sel, false, &c)) {
+      ok = false;
+      break;
+    }
+    sum += c;
+  }
+  if (ok) return sum;
+  sum = 0;
+  for (uint64_t id : n.pods) {
+    const Assignment& a = ledger_.at(id);
+    sum += t.matches(a.ns, a.labels);
+  }
+  return sum;
 }
 
 bool Engine::indexed_count(const Node& n, int32_t ns, const LSel& sel, bool skip_deleting, int64_t* out) const {

@@ -523,6 +523,9 @@ class Engine {
   void index_pod(Node& n, const Assignment& a, int sign);
   // pods of node n in namespace ns matching sel from the label index; false when sel needs the walk
   bool indexed_count(const Node& n, int32_t ns, const LSel& sel, bool skip_deleting, int64_t* out) const;
+  // pods of node n one affinity term matches: the label index for a single-label (or empty)
+  // selector, else a walk of the node's pods
+  int64_t term_count(const Node& n, const PodTerm& t) const;
   // ImageLocality scores every live node alike for this pod (each of its images is on no node,
   // or on every node with one size): true and the weighted score in *v
   bool image_score_const(const PodReq& req, int64_t* v) const;
