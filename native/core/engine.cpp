@@ -1086,16 +1086,15 @@ void Engine::interpod_prefilter(const PodReq& req, InterPodPF* pf) const {
       int64_t all = 0;
       if (aff.size() == 1) {
         all = term_count(n, aff[0]);
-      } else {                                  // a pod must match every term: walk
-        for (uint64_t id : n.pods) {
-          const Assignment& a = ledger_.at(id);
+      } else {                                  // a pod must match every term: per label-set group
+        for (const auto& g : n.lab_groups) {
           bool m = true;
           for (const PodTerm& t : aff)
-            if (!t.matches(a.ns, a.labels)) {
+            if (!t.matches(g.first.ns, g.first.labels)) {
               m = false;
               break;
             }
-          all += m;
+          if (m) all += g.second.first;
         }
       }
       if (all > 0) {
@@ -1354,6 +1353,26 @@ void Engine::index_pod(Node& n, const Assignment& a, int sign) {
   };
   bump(LKey{a.ns, -1, -1});
   for (const auto& kv : a.labels) bump(LKey{a.ns, kv.first, kv.second});
+  if (sign > 0) {
+    auto& g = n.lab_groups[LabSet{a.ns, a.labels}];
+    g.first += 1;
+    g.second += live;
+  } else {
+    auto it = n.lab_groups.find(LabSet{a.ns, a.labels});
+    if (it != n.lab_groups.end()) {
+      it->second.first -= 1;
+      it->second.second += live;
+      if (it->second.first <= 0) n.lab_groups.erase(it);
+    }
+  }
+}
+
+int64_t Engine::group_count(const Node& n, int32_t ns, const LSel& sel, bool skip_deleting) const {
+  if (sel.nothing) return 0;
+  int64_t c = 0;
+  for (const auto& g : n.lab_groups)
+    if (g.first.ns == ns && sel.matches(g.first.labels)) c += skip_deleting ? g.second.second : g.second.first;
+  return c;
 }
 
 int64_t Engine::term_count(const Node& n, const PodTerm& t) const {
@@ -1368,10 +1387,7 @@ int64_t Engine::term_count(const Node& n, const PodTerm& t) const {
   }
   if (ok) return sum;
   sum = 0;
-  for (uint64_t id : n.pods) {
-    const Assignment& a = ledger_.at(id);
-    sum += t.matches(a.ns, a.labels);
-  }
+  for (int32_t ns : t.ns) sum += group_count(n, ns, t.sel, false);
   return sum;
 }
 
@@ -1490,11 +1506,7 @@ int64_t Engine::count_matching(int32_t idx, int32_t ns, const LSel& sel) const {
   if (idx < 0 || idx >= (int32_t)nodes_.size() || sel.nothing) return 0;
   int64_t c = 0;
   if (indexed_count(nodes_[idx], ns, sel, true, &c)) return c;
-  for (uint64_t pod : nodes_[idx].pods) {
-    const Assignment& a = ledger_.at(pod);
-    if (a.ns == ns && !a.deleting && sel.matches(a.labels)) ++c;
-  }
-  return c;
+  return group_count(nodes_[idx], ns, sel, true);
 }
 
 bool Engine::wants_spread_filter(const PodReq& req) const {

@@ -154,6 +154,23 @@ struct LKeyHash {
   }
 };
 
+// a reserved pod's (namespace, sorted labels): the key of a node's label-set groups
+struct LabSet {
+  int32_t ns = 0;
+  Labels labels;
+  bool operator==(const LabSet& o) const { return ns == o.ns && labels == o.labels; }
+};
+struct LabSetHash {
+  size_t operator()(const LabSet& x) const {
+    uint64_t h = (uint64_t)(uint32_t)x.ns * 0x9E3779B97F4A7C15ull;
+    for (const auto& kv : x.labels) {
+      h ^= ((uint64_t)(uint32_t)kv.first << 32 | (uint32_t)kv.second) + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+      h *= 0xff51afd7ed558ccdull;
+    }
+    return (size_t)(h ^ (h >> 33));
+  }
+};
+
 struct Node {
   std::string name;
   uint32_t gen = 0;                   // slot generation: bumped when the slot gets a new node or dies
@@ -181,6 +198,10 @@ struct Node {
   // label index of the reserved pods: (all, not terminating) per (namespace, key, value) and per
   // namespace — a single-label selector's count in O(1) (spread / affinity pre-filters)
   std::unordered_map<LKey, std::pair<int32_t, int32_t>, LKeyHash> lab_idx;
+  // the same pods grouped by their exact (namespace, label set) with (all, not terminating)
+  // counts: any other selector is matched once per group instead of once per pod (a node's pods
+  // come from few templates)
+  std::unordered_map<LabSet, std::pair<int32_t, int32_t>, LabSetHash> lab_groups;
 };
 
 struct PodReq {
@@ -526,6 +547,8 @@ class Engine {
   // pods of node n one affinity term matches: the label index for a single-label (or empty)
   // selector, else a walk of the node's pods
   int64_t term_count(const Node& n, const PodTerm& t) const;
+  // pods of node n in namespace ns a selector matches, over the label-set groups
+  int64_t group_count(const Node& n, int32_t ns, const LSel& sel, bool skip_deleting) const;
   // ImageLocality scores every live node alike for this pod (each of its images is on no node,
   // or on every node with one size): true and the weighted score in *v
   bool image_score_const(const PodReq& req, int64_t* v) const;
