@@ -175,8 +175,11 @@ void Engine::remove_node(int32_t idx) {
   // drop reservations that point at this node
   for (auto it = ledger_.begin(); it != ledger_.end();) {
     if (it->second.node == idx) {
-      aff_holders_.erase(it->first);
-      anti_holders_.erase(it->first);
+      if (it->second.aff) {
+        aff_holders_.erase(it->first);
+        anti_holders_.erase(it->first);
+        aff_set_remove(it->second);
+      }
       it = ledger_.erase(it);
     } else {
       ++it;
@@ -331,6 +334,7 @@ bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::ve
     a.aff = req.aff;
     aff_holders_.insert(pod);
     if (!req.aff->req_anti.empty()) anti_holders_.insert(pod);
+    aff_set_add(a);
   }
   index_pod(n, a, +1);
   if (!req.ext.empty()) {
@@ -384,6 +388,7 @@ bool Engine::release(uint64_t pod) {
   if (a.aff) {
     aff_holders_.erase(pod);
     anti_holders_.erase(pod);
+    aff_set_remove(a);
   }
   ledger_.erase(it);
   return true;
@@ -1064,15 +1069,18 @@ void Engine::interpod_prefilter(const PodReq& req, InterPodPF* pf) const {
   pf->affinity.clear();
   pf->anti.clear();
   pf->any_aff_match = false;
-  for (uint64_t id : anti_holders_) {
-    const Assignment& a = ledger_.at(id);
-    if (a.node < 0 || a.node >= (int32_t)nodes_.size() || !nodes_[a.node].alive) continue;
-    const Node& n = nodes_[a.node];
-    for (const PodTerm& t : a.aff->req_anti) {
-      auto lab = n.labels.find(t.key);
-      if (lab != n.labels.end() && t.matches(req.ns, req.labels)) pf->existing_anti[t.key].insert(lab->second);
-    }
-  }
+  if (!anti_holders_.empty())
+    for (const auto& bucket : aff_sets_)
+      for (const AffSet& set : bucket.second)
+        for (const PodTerm& t : set.aff->req_anti) {
+          if (!t.matches(req.ns, req.labels)) continue;
+          for (const auto& nc : set.nodes) {
+            if (nc.first < 0 || nc.first >= (int32_t)nodes_.size() || !nodes_[nc.first].alive) continue;
+            const Node& n = nodes_[nc.first];
+            auto lab = n.labels.find(t.key);
+            if (lab != n.labels.end()) pf->existing_anti[t.key].insert(lab->second);
+          }
+        }
   if (!req.aff) return;
   const auto& aff = req.aff->req_aff;
   const auto& anti = req.aff->req_anti;
@@ -1168,21 +1176,25 @@ void Engine::interpod_scores(const PodReq& req, const std::vector<int32_t>& feas
         }
     }
   }
-  for (uint64_t id : aff_holders_) {
-    const Assignment& a = ledger_.at(id);
-    if (a.node < 0 || a.node >= (int32_t)nodes_.size() || !nodes_[a.node].alive) continue;
-    const Node& n = nodes_[a.node];
-    auto add = [&](const PodTerm& t, int64_t w) {
-      auto lab = n.labels.find(t.key);
-      if (lab == n.labels.end() || !t.matches(req.ns, req.labels)) return;
-      dom[pair_key(t.key, lab->second)] += w;
-      keys.insert(t.key);
-    };
-    if (hard_aff_w_)
-      for (const PodTerm& t : a.aff->req_aff) add(t, hard_aff_w_);
-    for (const PodTerm& t : a.aff->pref_aff) add(t, t.weight);
-    for (const PodTerm& t : a.aff->pref_anti) add(t, -(int64_t)t.weight);
-  }
+  // existing pods' terms, once per term set: a matching term adds its weight per holder pod
+  for (const auto& bucket : aff_sets_)
+    for (const AffSet& set : bucket.second) {
+      auto add = [&](const PodTerm& t, int64_t w) {
+        if (!t.matches(req.ns, req.labels)) return;
+        for (const auto& nc : set.nodes) {
+          if (nc.first < 0 || nc.first >= (int32_t)nodes_.size() || !nodes_[nc.first].alive) continue;
+          const Node& n = nodes_[nc.first];
+          auto lab = n.labels.find(t.key);
+          if (lab == n.labels.end()) continue;
+          dom[pair_key(t.key, lab->second)] += w * nc.second;
+          keys.insert(t.key);
+        }
+      };
+      if (hard_aff_w_)
+        for (const PodTerm& t : set.aff->req_aff) add(t, hard_aff_w_);
+      for (const PodTerm& t : set.aff->pref_aff) add(t, t.weight);
+      for (const PodTerm& t : set.aff->pref_anti) add(t, -(int64_t)t.weight);
+    }
   if (keys.empty() || F == 0) return;
   int64_t hi = INT64_MIN, lo = INT64_MAX;
   for (size_t i = 0; i < F; ++i) {
@@ -1202,26 +1214,85 @@ void Engine::interpod_scores(const PodReq& req, const std::vector<int32_t>& feas
 }
 
 bool Engine::interpod_inert(const PodReq& req) const {
-  if (filters_ & F_INTERPOD) {
-    if (req.aff && (!req.aff->req_aff.empty() || !req.aff->req_anti.empty())) return false;
-    for (uint64_t id : anti_holders_)
-      for (const PodTerm& t : ledger_.at(id).aff->req_anti)
-        if (t.matches(req.ns, req.labels)) return false;
-  }
-  if (score_w_[S_INTERPOD]) {
-    if (req.aff && (!req.aff->pref_aff.empty() || !req.aff->pref_anti.empty())) return false;
-    for (uint64_t id : aff_holders_) {
-      const PodAffinity& x = *ledger_.at(id).aff;
-      if (hard_aff_w_)
-        for (const PodTerm& t : x.req_aff)
+  const bool filt = (filters_ & F_INTERPOD) != 0, score = score_w_[S_INTERPOD] != 0;
+  if (filt && req.aff && (!req.aff->req_aff.empty() || !req.aff->req_anti.empty())) return false;
+  if (score && req.aff && (!req.aff->pref_aff.empty() || !req.aff->pref_anti.empty())) return false;
+  if (!filt && !score) return true;
+  // existing pods' terms that would match this pod, once per term set
+  for (const auto& bucket : aff_sets_)
+    for (const AffSet& set : bucket.second) {
+      const PodAffinity& x = *set.aff;
+      if (filt)
+        for (const PodTerm& t : x.req_anti)
           if (t.matches(req.ns, req.labels)) return false;
-      for (const PodTerm& t : x.pref_aff)
-        if (t.matches(req.ns, req.labels)) return false;
-      for (const PodTerm& t : x.pref_anti)
-        if (t.matches(req.ns, req.labels)) return false;
+      if (score) {
+        if (hard_aff_w_)
+          for (const PodTerm& t : x.req_aff)
+            if (t.matches(req.ns, req.labels)) return false;
+        for (const PodTerm& t : x.pref_aff)
+          if (t.matches(req.ns, req.labels)) return false;
+        for (const PodTerm& t : x.pref_anti)
+          if (t.matches(req.ns, req.labels)) return false;
+      }
+    }
+  return true;
+}
+
+uint64_t PodAffinity::hash() const {
+  uint64_t h = 0x5bd1e9955bd1e995ull;
+  auto mix = [&](uint64_t x) {
+    h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33;
+  };
+  const std::vector<PodTerm>* lists[4] = {&req_aff, &req_anti, &pref_aff, &pref_anti};
+  for (int l = 0; l < 4; ++l) {
+    mix(0x100 + l);
+    for (const PodTerm& t : *lists[l]) {
+      mix((uint64_t)(uint32_t)t.key << 32 | (uint32_t)t.weight);
+      for (int32_t n : t.ns) mix((uint32_t)n);
+      mix(t.sel.nothing ? 1 : 2);
+      for (const LReq& r : t.sel.reqs) {
+        mix((uint64_t)(uint32_t)r.key << 8 | (uint8_t)r.op);
+        for (int32_t v : r.values) mix((uint32_t)v);
+      }
     }
   }
-  return true;
+  return h;
+}
+
+void Engine::aff_set_add(Assignment& a) {
+  const uint64_t h = a.aff->hash();
+  a.aff_hash = h;
+  auto& bucket = aff_sets_[h];
+  for (AffSet& set : bucket)
+    if (set.aff == a.aff || *set.aff == *a.aff) {
+      set.nodes[a.node] += 1;
+      set.pods += 1;
+      return;
+    }
+  AffSet set;
+  set.aff = a.aff;
+  set.nodes[a.node] = 1;
+  set.pods = 1;
+  bucket.push_back(std::move(set));
+}
+
+void Engine::aff_set_remove(const Assignment& a, bool) {
+  auto b = aff_sets_.find(a.aff_hash);
+  if (b == aff_sets_.end()) return;
+  auto& bucket = b->second;
+  for (size_t i = 0; i < bucket.size(); ++i) {
+    AffSet& set = bucket[i];
+    if (set.aff != a.aff && !(*set.aff == *a.aff)) continue;
+    auto nit = set.nodes.find(a.node);
+    if (nit != set.nodes.end() && --nit->second <= 0) set.nodes.erase(nit);
+    if (--set.pods <= 0) {
+      bucket.erase(bucket.begin() + (long)i);
+      if (bucket.empty()) aff_sets_.erase(b);
+    }
+    return;
+  }
 }
 
 // ============================================================== default plugins: node extras

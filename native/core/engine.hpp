@@ -102,12 +102,14 @@ struct LReq {
   int32_t key;
   int8_t op;
   std::vector<int32_t> values;
+  bool operator==(const LReq& o) const { return key == o.key && op == o.op && values == o.values; }
 };
 struct LSel {
   bool nothing = false;
   std::vector<LReq> reqs;
   bool empty() const { return !nothing && reqs.empty(); }
   bool matches(const Labels& l) const;
+  bool operator==(const LSel& o) const { return nothing == o.nothing && reqs == o.reqs; }
 };
 
 // One topology spread constraint (upstream v1.20 podtopologyspread; plugins/spread_affinity.py).
@@ -127,11 +129,25 @@ struct PodTerm {
   bool matches(int32_t pod_ns, const Labels& l) const {
     return std::find(ns.begin(), ns.end(), pod_ns) != ns.end() && sel.matches(l);
   }
+  bool operator==(const PodTerm& o) const { return key == o.key && ns == o.ns && sel == o.sel && weight == o.weight; }
 };
 // A pod's inter-pod affinity (shared by its request and its ledger entry)
 struct PodAffinity {
   std::vector<PodTerm> req_aff, req_anti, pref_aff, pref_anti;
   bool empty() const { return req_aff.empty() && req_anti.empty() && pref_aff.empty() && pref_anti.empty(); }
+  bool operator==(const PodAffinity& o) const {
+    return req_aff == o.req_aff && req_anti == o.req_anti && pref_aff == o.pref_aff && pref_anti == o.pref_anti;
+  }
+  uint64_t hash() const;
+};
+// The reserved pods that carry one (anti-)affinity term set (pods of one template carry equal
+// terms), and how many of them each node holds: the symmetric checks of a new pod (existing
+// pods' required anti-affinity, their required / preferred terms in scoring) run once per set
+// and node, weighted by that count, instead of once per holder pod
+struct AffSet {
+  std::shared_ptr<const PodAffinity> aff;          // a representative (content-equal for every holder)
+  std::unordered_map<int32_t, int32_t> nodes;      // node index → holders there
+  int64_t pods = 0;
 };
 
 // A profile's default constraint (PodTopologySpread args: System defaults or a List); its
@@ -280,6 +296,7 @@ struct Assignment {
   bool deleting = false;
   std::vector<std::pair<int32_t, int64_t>> ext;   // extended resources it holds on the node
   std::shared_ptr<const PodAffinity> aff;          // its (anti-)affinity terms (symmetric rule, scoring)
+  uint64_t aff_hash = 0;                           // its AffSet's bucket (aff_sets_)
 };
 
 struct CycleResult {
@@ -614,6 +631,9 @@ class Engine {
   int64_t hard_aff_w_ = 1;
   std::unordered_set<uint64_t> aff_holders_;  // ledger pods with any (anti-)affinity term
   std::unordered_set<uint64_t> anti_holders_; // ... with a required anti-affinity term
+  std::unordered_map<uint64_t, std::vector<AffSet>> aff_sets_;   // term-set hash → sets (collisions)
+  void aff_set_add(Assignment& a);
+  void aff_set_remove(const Assignment& a, bool whole_node = false);
   std::vector<int32_t> ext_ignored_;
   std::vector<std::string> ext_ignored_groups_;
   void* fn_destroy_ = nullptr;
