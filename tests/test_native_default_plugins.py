@@ -20,6 +20,7 @@ from hypothesis import strategies as st
 from yoda_scheduler_amd.framework.cache import SchedulerCache
 from yoda_scheduler_amd.framework.interfaces import CycleState, NodeScore
 from yoda_scheduler_amd.framework.scheduler import push_spread_source
+from yoda_scheduler_amd.models.device import make_node
 from yoda_scheduler_amd.models.pod import PodInfo
 from yoda_scheduler_amd.ops.native import core, pod_req
 from yoda_scheduler_amd.plugins.defaults import NodeResourcesFit
@@ -421,3 +422,59 @@ def test_interpod_affinity_native_equals_python_on_random_clusters(case):
     out = [NodeScore(nm, pl.score(st2, p, nm)[0]) for nm in feas]
     pl.normalize_score(st2, p, out)
     assert native_scores(eng, p, feas) == {x.name: x.score for x in out}
+
+
+def test_affinity_term_sets_follow_release_and_node_removal():
+    """The engine groups reserved pods' (anti-)affinity terms by term set with per-node holder
+    counts. After releases and a node removal, its filter verdicts and scores equal those of an
+    engine that only ever saw the surviving pods."""
+    import random
+    rng = random.Random(7)
+    nodes = [make_node(f"n{i}", labels={"topology.kubernetes.io/zone": f"z{i % 3}"}) for i in range(6)]
+    term_sets = [
+        {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+            {"labelSelector": {"matchLabels": {"app": "db"}}, "topologyKey": "kubernetes.io/hostname"}]}},
+        {"podAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+            {"weight": 30, "podAffinityTerm": {"labelSelector": {"matchLabels": {"app": "web"}},
+                                               "topologyKey": "topology.kubernetes.io/zone"}}]},
+         "podAntiAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+             {"weight": 70, "podAffinityTerm": {"labelSelector": {"matchExpressions": [
+                 {"key": "app", "operator": "In", "values": ["web", "db"]}]}, "topologyKey": "kubernetes.io/hostname"}}]}},
+        {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+            {"labelSelector": {"matchLabels": {"app": "cache"}}, "topologyKey": "topology.kubernetes.io/zone"}]}},
+    ]
+    pods = []
+    for j in range(60):
+        k = j % 4
+        spec = {"nodeName": f"n{rng.randrange(6)}"}
+        if k < 3:
+            spec["affinity"] = term_sets[k]
+        pods.append({"metadata": {"name": f"p{j}", "namespace": "default", "uid": f"ts-{j}",
+                                  "labels": {"app": rng.choice(["web", "db", "cache"])}}, "spec": spec})
+    eng_a, cache_a = cache_with(nodes)
+    for o in pods:
+        cache_a.add_pod(o)
+    gone = set(rng.sample(range(60), 20))
+    for j in gone:
+        cache_a.remove_pod(f"ts-{j}")
+    cache_a.remove_node("n2")
+    survivors = [o for j, o in enumerate(pods) if j not in gone and o["spec"]["nodeName"] != "n2"]
+    eng_b, cache_b = cache_with([n for n in nodes if n["metadata"]["name"] != "n2"])
+    for o in survivors:
+        cache_b.add_pod(o)
+    names = sorted(n["metadata"]["name"] for n in nodes if n["metadata"]["name"] != "n2")
+    for eng in (eng_a, eng_b):
+        eng.filters = C.F_INTERPOD
+        only_weight(eng, C.S_INTERPOD)
+        eng.set_hard_pod_affinity_weight(5)
+    assert eng_a.affinity_holders == eng_b.affinity_holders > 0
+    for app in ("web", "db", "cache", "other"):
+        for aff in [None] + term_sets:
+            spec = {"affinity": aff} if aff else {}
+            p = PodInfo.from_obj({"metadata": {"name": "new", "namespace": "default", "uid": f"new-{app}-{id(aff)}",
+                                               "labels": {"app": app}}, "spec": spec})
+            ra, rb = pod_req(eng_a, p), pod_req(eng_b, p)
+            fa = {nm: C.REASONS[eng_a.filter_node(ra, eng_a.node_index(nm))] for nm in names}
+            fb = {nm: C.REASONS[eng_b.filter_node(rb, eng_b.node_index(nm))] for nm in names}
+            assert fa == fb
+            assert native_scores(eng_a, p, names) == native_scores(eng_b, p, names)
