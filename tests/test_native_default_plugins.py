@@ -478,3 +478,44 @@ def test_affinity_term_sets_follow_release_and_node_removal():
             fb = {nm: C.REASONS[eng_b.filter_node(rb, eng_b.node_index(nm))] for nm in names}
             assert fa == fb
             assert native_scores(eng_a, p, names) == native_scores(eng_b, p, names)
+
+
+def test_label_index_and_groups_follow_label_changes_deletion_and_release():
+    """count_matching (spread pre-filters / the DefaultSelector census) reads the per-node label
+    index and label-set groups; after label changes, terminating pods and releases it equals a
+    brute-force count over the surviving pods, for single- and multi-label selectors."""
+    import random
+    from yoda_scheduler_amd.models.selectors import LabelSelector
+    rng = random.Random(3)
+    eng, cache = cache_with([make_node(f"n{i}") for i in range(3)])
+    live = {}
+    for j in range(90):
+        labels = {"app": rng.choice(["a", "b"]), "tier": rng.choice(["x", "y"])}
+        ns = rng.choice(["default", "ml"])
+        o = {"metadata": {"name": f"p{j}", "namespace": ns, "uid": f"lg-{j}", "labels": labels},
+             "spec": {"nodeName": f"n{rng.randrange(3)}"}}
+        cache.add_pod(o)
+        live[f"lg-{j}"] = [o["spec"]["nodeName"], ns, dict(labels), False]
+    for uid in rng.sample(sorted(live), 25):            # relabel
+        pi = cache.pods[uid].info
+        new = {"app": rng.choice(["a", "b", "c"]), "tier": rng.choice(["x", "y"])}
+        eng.set_pod_meta(pi.num_id, list(new.items()), False)
+        live[uid][2] = new
+    for uid in rng.sample(sorted(live), 15):            # terminating
+        pi = cache.pods[uid].info
+        eng.set_pod_meta(pi.num_id, list(live[uid][2].items()), True)
+        live[uid][3] = True
+    for uid in rng.sample(sorted(live), 20):            # released
+        cache.remove_pod(uid)
+        del live[uid]
+    sels = [{"matchLabels": {"app": "a"}}, {"matchLabels": {"app": "a", "tier": "x"}},
+            {"matchExpressions": [{"key": "app", "operator": "In", "values": ["b", "c"]}]},
+            {"matchLabels": {"tier": "y"}, "matchExpressions": [{"key": "app", "operator": "NotIn", "values": ["a"]}]},
+            {}]
+    for sel in sels:
+        ls = LabelSelector(sel)
+        for node in ("n0", "n1", "n2"):
+            for ns in ("default", "ml"):
+                want = sum(1 for n, pns, lab, dying in live.values()
+                           if n == node and pns == ns and not dying and ls.matches(lab))
+                assert eng.count_matching(eng.node_index(node), ns, ls.native()) == want, (sel, node, ns)
