@@ -43,6 +43,7 @@ class Workload:
     scheduler_name: str = "yoda-scheduler"
     specs: dict = field(default_factory=dict)        # pod index → extra spec fields (e.g. affinity)
     metas: dict = field(default_factory=dict)        # pod index → extra metadata fields (ownerReferences)
+    objects: list = field(default_factory=list)      # (resource, object) created with the cluster (PVCs, PVs)
     cluster: str = "synthetic"                       # "kind": realistic node/cluster objects (populate)
 
     @property
@@ -65,7 +66,7 @@ def _mixed_labels(rng: random.Random) -> dict:
 
 def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None,
                   node_gpus: Optional[int] = None, nodes: Optional[int] = None, mix_anti: int = 0,
-                  cluster: str = "synthetic", mix_spread: int = 0) -> Workload:
+                  cluster: str = "synthetic", mix_spread: int = 0, mix_volumes: int = 0) -> Workload:
     """``node_gpus`` overrides the GPUs per node (BASELINE.md protocol item 5: every
     config at 1, 2, 4 and 8 GPUs per node); pods keep their labels, so e.g. ``scv/number: 8``
     pods are unschedulable on smaller nodes and are reported as such. ``nodes`` resizes
@@ -96,6 +97,8 @@ def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None,
                 "maxSkew": 1, "topologyKey": "kubernetes.io/hostname", "whenUnsatisfiable": "DoNotSchedule",
                 "labelSelector": {"matchLabels": {"group": f"g{i % 8}"}}}])
         w.name += f" + {min(mix_spread, n)} hostname-spread pods"
+    if mix_volumes:
+        _add_volume_pods(w, mix_volumes)
     if nodes is not None:
         if cfg != 6 or nodes < 1:
             raise ValueError("nodes: config 6 only, >= 1")
@@ -143,6 +146,44 @@ def _make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None) -> 
     else:
         raise ValueError(f"unknown config {cfg}")
     return w
+
+
+# ---------------------------------------------------------------- PVC pods (--mix-volumes)
+VOLUME_CLAIMS = 4           # ReadWriteMany claims the volume pods share (a dataset / checkpoint share)
+
+
+def volume_objects() -> list:
+    """Bound CSI PersistentVolumes and their claims, as a PV controller leaves them."""
+    out = []
+    for j in range(VOLUME_CLAIMS):
+        claim, pv = f"data-{j}", f"pv-data-{j}"
+        out.append(("persistentvolumes", {
+            "apiVersion": "v1", "kind": "PersistentVolume", "metadata": {"name": pv},
+            "spec": {"capacity": {"storage": "10Ti"}, "accessModes": ["ReadWriteMany"], "storageClassName": "shared",
+                     "csi": {"driver": "nfs.csi.k8s.io", "volumeHandle": f"share-{j}"},
+                     "claimRef": {"kind": "PersistentVolumeClaim", "namespace": "default", "name": claim}},
+            "status": {"phase": "Bound"}}))
+        out.append(("persistentvolumeclaims", {
+            "apiVersion": "v1", "kind": "PersistentVolumeClaim", "metadata": {"name": claim, "namespace": "default"},
+            "spec": {"accessModes": ["ReadWriteMany"], "resources": {"requests": {"storage": "10Ti"}},
+                     "storageClassName": "shared", "volumeName": pv},
+            "status": {"phase": "Bound"}}))
+    return out
+
+
+def _add_volume_pods(w: Workload, count: int) -> None:
+    """Beyond BASELINE: ``count`` pods of the burst mount a bound PVC, so the volume plugins
+    (VolumeBinding, VolumeZone, NodeVolumeLimits, the in-tree attach limits) apply to them and
+    they take the Python cycle beside the native lane — what a pod that genuinely needs a
+    Python plugin costs."""
+    n = len(w.pods)
+    count = min(count, n)
+    for j in range(count):
+        i = j * n // count
+        w.specs[i] = dict(w.specs.get(i) or {}, volumes=[
+            {"name": "data", "persistentVolumeClaim": {"claimName": f"data-{j % VOLUME_CLAIMS}"}}])
+    w.objects.extend(volume_objects())
+    w.name += f" + {count} PVC pods"
 
 
 # ---------------------------------------------------------------- kind cluster (--cluster kind)
@@ -233,6 +274,8 @@ def populate(server, w: Workload, template: Optional[dict] = None, link_load: fl
     if w.cluster == "kind":
         for res, obj in kind_objects():
             server.create(res, obj)
+    for res, obj in w.objects:
+        server.create(res, obj)
     for k, (name, spec, gpus) in enumerate(w.nodes):
         # kubelet --max-pods 2048: config 5 packs 5000 HBM-sharing pods onto 4 nodes
         node = make_node(name, pods=2048)

@@ -35,6 +35,11 @@ class PodState:
     lane: bool = False                    # mirrored from the native lane (it owns the reservation)
 
 
+def _csi_attach_limits(obj: dict) -> bool:
+    alloc = (obj.get("status") or {}).get("allocatable") or {}
+    return any(k.startswith("attachable-volumes-csi-") for k in alloc)
+
+
 class SchedulerCache:
     def __init__(self, engine, compat: bool = False, stale_factor: float = 3.0,
                  assume_ttl: float = 30.0, clock: Callable[[], float] = time.monotonic,
@@ -55,6 +60,7 @@ class SchedulerCache:
         self._anti_parsed: dict[str, list] = {}     # uid → [(topologyKey, namespaces, LabelSelector)]
         self.image_nodes: dict[str, int] = {}    # image → number of nodes holding it (ImageLocality)
         self.avoid_nodes: set[str] = set()       # nodes with a preferAvoidPods annotation
+        self.csi_limit_nodes = 0                 # nodes whose allocatable has attachable-volumes-csi-* (NodeVolumeLimits)
         self.node_ext_used: dict[str, dict[str, int]] = {}   # node → extended resource → requested
         self.generation = 0
         self.node_generation = 0                 # node add/remove only (engine index → name stays valid)
@@ -73,6 +79,8 @@ class SchedulerCache:
                 self.image_nodes[im] = c
             else:
                 self.image_nodes.pop(im, None)
+        if _csi_attach_limits(info.obj):
+            self.csi_limit_nodes += sign
         if sign > 0 and info.avoid:
             self.avoid_nodes.add(info.name)
         elif sign < 0:

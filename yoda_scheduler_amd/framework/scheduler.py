@@ -128,6 +128,11 @@ class Handle:
         inf = self._s.informers.get(res)
         return inf.store if inf is not None else {}
 
+    def generation(self, res: str) -> int:
+        """Moves whenever an object of ``res`` (a resource some plugin ``watches``) is added,
+        updated or deleted: plugins key what they derive from a whole lister on it."""
+        return self._s.extra_generation[res]
+
     def get_waiting_pod(self, uid: str):
         for fw in self._s.frameworks.values():
             wp = fw.get_waiting_pod(uid)
@@ -208,6 +213,7 @@ class Scheduler:
         self._ann_memo: dict = {}          # _bind_annotations memo, valid for one cache generation
         self._ann_gen = -1
         self.informers: dict[str, Informer] = {}
+        self.extra_generation: collections.Counter = collections.Counter()   # Handle.generation
         self._scheduled = 0                # bound by the Python path (the lane counts its own)
         self.failed = 0
         self.scv_requeues = 0          # Scv updates that moved the parked pods back
@@ -606,13 +612,16 @@ class Scheduler:
                     lambda o, ev=ev, res=res: self._spread_source(res, o, True, None))
                 continue
             self.informers[res] = Informer(self.client, res,
-                                           lambda o, ev=ev: self._extra_event(ev),
-                                           lambda a, b, ev=ev: self._extra_event(ev),
-                                           lambda o, ev=ev: self._lane_refresh())
+                                           lambda o, ev=ev, res=res: self._extra_event(ev, res),
+                                           lambda a, b, ev=ev, res=res: self._extra_event(ev, res),
+                                           lambda o, res=res: self._extra_event(None, res))
         return self.informers
 
-    def _extra_event(self, ev: str) -> None:
-        self.queue.move_all_to_active_or_backoff(ev)
+    def _extra_event(self, ev: Optional[str], res: str = "") -> None:
+        if res:
+            self.extra_generation[res] += 1
+        if ev is not None:
+            self.queue.move_all_to_active_or_backoff(ev)
         self._lane_refresh()
 
     def _spread_source(self, res: str, obj: dict, deleted: bool, ev: Optional[str]) -> None:

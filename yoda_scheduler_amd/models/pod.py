@@ -189,7 +189,7 @@ class PodInfo:
                  "cpu_m", "mem", "priority", "node_selector", "required_terms", "preferred_terms", "tolerations",
                  "annotations", "host_ports", "attempts", "initial_attempt", "enqueued", "native_req",
                  "native_owner", "assigned_cards", "_creation", "flags", "ext", "nz_cpu_m", "nz_mem", "applies_memo",
-                 "images", "containers", "owner", "avoid", "spread", "deleting", "pod_aff")
+                 "images", "containers", "owner", "avoid", "spread", "deleting", "pod_aff", "vol_memo")
 
     def __init__(self, obj: dict, uid: str, namespace: str, name: str, num_id: int, labels: dict, gpu: GpuRequest,
                  scheduler_name: str = "default-scheduler", node_name: str = "", cpu_m: int = 0, mem: int = 0,
@@ -216,6 +216,7 @@ class PodInfo:
         # (required affinity, required anti-affinity, preferred affinity, preferred anti-affinity),
         # each [(topologyKey, namespaces | None, LabelSelector.native() | None, weight)]
         self.pod_aff = pod_aff
+        self.vol_memo: Optional[tuple] = None   # volume plugins' no-op answers (plugins/volumes.py)
         self._src = None
         # -1: a single container's non-zero request derived from cpu_m / mem
         self.nz_cpu_m = nz_cpu_m if nz_cpu_m >= 0 else (cpu_m or DEFAULT_MILLI_CPU_REQUEST)

@@ -12,8 +12,15 @@ lists ``yoda``, so kube-scheduler v1.20's volume Filter/Reserve/PreBind plugins 
   ``EBSLimits`` / ``GCEPDLimits`` / ``AzureDiskLimits`` counters.
 
 All of them are no-ops for pods without the relevant volumes (``is_noop_for``), so GPU
-pods without PVCs keep the fully native scheduling cycle. The objects come from
-informers the scheduler starts only because these plugins declare ``watches``.
+pods without PVCs keep the fully native scheduling cycle. A pod whose claims are all bound
+is a no-op for each of them too when its bound volumes give that plugin nothing to check —
+no PV node affinity (VolumeBinding), no zone labels on the PVs (VolumeZone), no attach
+limit anywhere or no attachable volume of the plugin's kind (the limits plugins) — so a pod
+that mounts a pre-provisioned dataset / checkpoint share takes the native cycle as well.
+Each test is the plugin's own Filter / PreBind reasoning applied to the current listers,
+so it can only answer "no-op" where every extension point would pass untouched. The
+objects come from informers the scheduler starts only because these plugins declare
+``watches``.
 """
 from __future__ import annotations
 
@@ -32,6 +39,7 @@ ZONE_LABELS = ("topology.kubernetes.io/zone", "topology.kubernetes.io/region",
 ANN_SELECTED_NODE = "volume.kubernetes.io/selected-node"
 NO_PROVISIONER = "kubernetes.io/no-provisioner"
 WFFC = "WaitForFirstConsumer"
+_EMPTY: dict = {}
 
 ERR_DISK_CONFLICT = "node(s) had no available disk"
 ERR_ZONE_CONFLICT = "node(s) had no available volume zone"
@@ -59,6 +67,44 @@ def _unresolvable(msg: str, plugin: str) -> Status:
     return Status(Code.UNSCHEDULABLE_AND_UNRESOLVABLE, [msg], plugin)
 
 
+class _VolFacts:
+    """What the volume plugins' no-op tests read of one pod, resolved in one pass:
+
+    * ``claims`` — the claim names (PVC volumes and generic ephemeral volumes' claims);
+    * ``bound`` — the PV of every claim when each claim exists, is not being deleted and
+      names a PV that exists; None otherwise;
+    * ``inline`` — the attachable-disk kinds among the pod's inline volumes;
+    * ``pv_kinds`` — the attachable-disk kinds of the PVs its PVC volumes are bound to;
+    * ``csi`` — a PVC volume counts against a CSI attach limit (bound to a CSI PV, or
+      unbound with a provisioning StorageClass) — NodeVolumeLimits' own rule."""
+    __slots__ = ("claims", "bound", "inline", "pv_kinds", "csi")
+
+    def __init__(self, plugin: "_VolumeBase", pod) -> None:
+        vols = _volumes(pod)
+        self.claims = _claim_names(pod)
+        self.inline = {k for v in vols for k in _ATTACHABLE_KINDS if k in v}
+        self.pv_kinds: set = set()
+        self.csi = False
+        for v in vols:
+            if "persistentVolumeClaim" not in v:
+                continue
+            pvc = plugin._pvc(pod.namespace, (v["persistentVolumeClaim"] or _EMPTY).get("claimName", ""))
+            if pvc is None:
+                continue
+            spec = pvc.get("spec") or _EMPTY
+            pv = plugin._pv(spec.get("volumeName", ""))
+            if pv is not None:
+                ps = pv.get("spec") or _EMPTY
+                if ps.get("csi"):
+                    self.csi = True
+                self.pv_kinds.update(k for k in _ATTACHABLE_KINDS if ps.get(k))
+                continue
+            sc = plugin._sc(spec.get("storageClassName", ""))
+            if sc is not None and sc.get("provisioner", NO_PROVISIONER) != NO_PROVISIONER:
+                self.csi = True
+        self.bound = plugin._bound_claims(pod, self.claims) if self.claims else []
+
+
 class _VolumeBase:
     watches = ("persistentvolumeclaims", "persistentvolumes", "storageclasses")
 
@@ -77,6 +123,33 @@ class _VolumeBase:
     def _node_labels(self, node: str) -> dict:
         n = self.handle.cache.nodes.get(node)
         return n.labels if n is not None else {}
+
+    def _facts(self, pod) -> "_VolFacts":
+        """The pod's claims resolved against the PVC / PV / StorageClass listers, once for
+        every volume plugin that asks about the pod, until one of those listers changes
+        (their generations move on every event; the pod's volumes are fixed)."""
+        gen = getattr(self.handle, "generation", None)
+        if gen is None or not hasattr(pod, "vol_memo"):
+            return _VolFacts(self, pod)
+        key = (gen("persistentvolumeclaims"), gen("persistentvolumes"), gen("storageclasses"))
+        m = pod.vol_memo
+        if m is None or m[0] != key:
+            m = pod.vol_memo = (key, _VolFacts(self, pod))
+        return m[1]
+
+    def _bound_claims(self, pod, claims: list) -> Optional[list]:
+        """The claims' bound PVs when every claim exists, is not being deleted and names a PV
+        that exists; None otherwise (the plugin's own checks decide)."""
+        out = []
+        for claim in claims:
+            pvc = self._pvc(pod.namespace, claim)
+            if pvc is None or (pvc.get("metadata") or {}).get("deletionTimestamp"):
+                return None
+            pv = self._pv((pvc.get("spec") or {}).get("volumeName", ""))
+            if pv is None:
+                return None
+            out.append(pv)
+        return out
 
     def _node_pod_objs(self, node: str):
         cache = self.handle.cache
@@ -133,7 +206,11 @@ class VolumeZone(_VolumeBase, FilterPlugin):
     reads_flags = 0  # other pods' features this plugin reads (needs_lane_mirror)
 
     def is_noop_for(self, pod) -> bool:
-        return not _claim_names(pod)
+        # no claims, or every claim bound to a PV without zone / region labels (the filter
+        # then passes on every node)
+        f = self._facts(pod)
+        return not f.claims or f.bound is not None and not any(
+            k in ((pv.get("metadata") or _EMPTY).get("labels") or _EMPTY) for pv in f.bound for k in ZONE_LABELS)
 
     def filter(self, state: CycleState, pod, node_name: str) -> Status:
         labels = self._node_labels(node_name)
@@ -215,7 +292,12 @@ class VolumeBinding(_VolumeBase, PreFilterPlugin, FilterPlugin, ReservePlugin, P
         self._pod_choice: dict[str, tuple[list, list]] = {}   # pod uid → decision
 
     def is_noop_for(self, pod) -> bool:
-        return not _claim_names(pod)
+        # no claims, or every claim bound to an existing PV without required node affinity:
+        # PreFilter finds nothing to bind, Filter passes on every node, Reserve assumes
+        # nothing and PreBind has no claim to wait for
+        f = self._facts(pod)
+        return not f.claims or f.bound is not None and all(
+            ((pv.get("spec") or _EMPTY).get("nodeAffinity") or _EMPTY).get("required") is None for pv in f.bound)
 
     def pre_filter(self, state: CycleState, pod) -> Status:
         bound, delayed, immediate = [], [], 0
@@ -406,8 +488,27 @@ class NodeVolumeLimits(_LimitsBase):
     reads_flags = PF_CLAIMS  # other pods' features this plugin reads (needs_lane_mirror)
     watches = ("persistentvolumeclaims", "persistentvolumes", "storageclasses", "csinodes")
 
+    def __init__(self, args=None, handle=None) -> None:
+        super().__init__(args, handle)
+        self._csinode_limits = (-1, False)     # (csinodes generation, any CSINode reports a count)
+
     def is_noop_for(self, pod) -> bool:
-        return not _claim_names(pod)
+        # no claims, no claim counted against a CSI limit, or no attach limit on any node
+        # (the filter returns before counting)
+        f = self._facts(pod)
+        return not f.claims or not f.csi or not self._any_limits()
+
+    def _any_limits(self) -> bool:
+        if getattr(self.handle.cache, "csi_limit_nodes", 1) > 0:
+            return True
+        gen = self.handle.generation("csinodes") if hasattr(self.handle, "generation") else -2
+        g, any_count = self._csinode_limits
+        if g != gen or gen == -2:
+            any_count = any((d.get("allocatable") or _EMPTY).get("count") is not None
+                            for cn in self._lister("csinodes").values()
+                            for d in ((cn.get("spec") or _EMPTY).get("drivers") or ()))
+            self._csinode_limits = (gen, any_count)
+        return any_count
 
     def _pod_ids(self, ns: str, spec: dict) -> dict[str, set[str]]:
         out: dict[str, set[str]] = {}
@@ -456,7 +557,9 @@ class _InTreeLimits(_LimitsBase):
     reads_flags = PF_CLAIMS | PF_DISKS  # other pods' features this plugin reads (needs_lane_mirror)
 
     def is_noop_for(self, pod) -> bool:
-        return not any(self.kind in v or "persistentVolumeClaim" in v for v in _volumes(pod))
+        # no inline volume of this kind and no PVC bound to one: the filter has nothing to count
+        f = self._facts(pod)
+        return self.kind not in f.inline and self.kind not in f.pv_kinds
 
     def _pod_ids(self, ns: str, spec: dict) -> dict[str, set[str]]:
         ids: set[str] = set()
@@ -497,6 +600,9 @@ class CinderLimits(_InTreeLimits):
     name = "CinderLimits"
     kind, id_field, alloc_key, default_max = "cinder", "volumeID", "attachable-volumes-cinder", 256
 
+
+# the in-tree attach-limit plugins' volume kinds (what _VolFacts resolves for them)
+_ATTACHABLE_KINDS = tuple(c.kind for c in (EBSLimits, GCEPDLimits, AzureDiskLimits, CinderLimits))
 
 VOLUME_PLUGINS = (VolumeRestrictions, VolumeZone, VolumeBinding, NodeVolumeLimits, EBSLimits, GCEPDLimits,
                   AzureDiskLimits, CinderLimits)
