@@ -781,9 +781,10 @@ PYBIND11_MODULE(_yoda_core, m) {
       // the profile's engine configuration is the engine's current one (the caller applied it)
       .def("set_profile",
            [](Lane& l, Engine& e, const std::string& name, bool enabled, int flag_mask, bool annotate,
-              int64_t preempt_above, const py::list& gate_terms) {
+              int64_t preempt_above, const py::list& gate_terms, bool claims_ok) {
              Lane::Profile p;
              p.preempt_above = preempt_above;
+             p.claims_ok = claims_ok;
              for (auto t : gate_terms) p.gate_terms.push_back(match_term(t));
              p.name = name;
              p.enabled = enabled;
@@ -796,7 +797,9 @@ PYBIND11_MODULE(_yoda_core, m) {
              l.set_profile(p);
            },
            py::arg("engine"), py::arg("name"), py::arg("enabled"), py::arg("flag_mask"), py::arg("annotate"),
-           py::arg("preempt_above") = INT64_MIN, py::arg("gate_terms") = py::list())
+           py::arg("preempt_above") = INT64_MIN, py::arg("gate_terms") = py::list(), py::arg("claims_ok") = false)
+      .def("set_inert_claims", &Lane::set_inert_claims, py::arg("keys"),
+           "PersistentVolumeClaims (namespace/name) whose pods the profiles with claims_ok may run")
       .def("set_gates",
            [](Lane& l, const std::string& name, const py::list& gate_terms) {
              std::vector<MatchTerm> v;

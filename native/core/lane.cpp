@@ -291,6 +291,20 @@ bool Lane::set_gates(const std::string& name, std::vector<MatchTerm> terms) {
   return true;
 }
 
+void Lane::set_inert_claims(std::vector<std::string> keys) {
+  {
+    std::lock_guard<std::mutex> g(prof_mu_);
+    claims_staged_.clear();
+    for (auto& k : keys) claims_staged_.insert(std::move(k));
+    claims_fresh_ = true;
+  }
+  std::lock_guard<std::mutex> g(in_mu_);
+  Item it;
+  it.k = Item::kClaims;
+  push_locked(std::move(it));
+  in_cv_.notify_one();
+}
+
 void Lane::set_active(bool on) {
   std::lock_guard<std::mutex> g(in_mu_);
   active_.store(on);
@@ -483,7 +497,8 @@ bool Lane::admissible(const yk::PodProj& p, int* prof) const {
   if (!p.ok || !p.node.empty() || p.deleting || terminal(p)) return false;
   for (size_t i = 0; i < lp_.size(); ++i) {
     if (lp_[i].name != p.sched) continue;
-    if (!lp_[i].enabled || (p.flags & lp_[i].flag_mask)) return false;
+    const int f = p.flags & lp_[i].flag_mask;
+    if (!lp_[i].enabled || (f && (f != yk::PF_CLAIMS || !lp_[i].claims_ok || !claims_inert(p)))) return false;
     for (const MatchTerm& t : lp_[i].gate_terms)
       if (t.matches(p)) return false;     // an existing pod's required anti-affinity may reject it
     *prof = (int)i;
@@ -779,6 +794,56 @@ void Lane::apply_gates(std::vector<Fwd>* out) {
       if (hit) break;
     }
     if (hit) evict.push_back(e);
+  }
+  for (Entry* e : evict) {
+    if (e->st == PARKED || e->st == BACKOFF) {
+      requeue_to_python(e);
+      continue;
+    }
+    drop_owned(e, false);
+    if (!uninteresting(e->ev->p, lp_)) forward('A', e->ev, nullptr, out);
+  }
+}
+
+bool Lane::claims_inert(const yk::PodProj& p) const {
+  if (p.claims.empty() || inert_.empty()) return false;
+  std::string key;
+  for (const std::string& c : p.claims) {
+    key.assign(p.ns).append("/").append(c);
+    if (!inert_.count(key)) return false;
+  }
+  return true;
+}
+
+// A new inert-claims set: waiting pods that mount a claim which left it go to Python (a claim
+// that joined the set cannot make a pod inadmissible; pods Python holds stay there).
+void Lane::apply_claims(std::vector<Fwd>* out) {
+  std::unordered_set<std::string> next;
+  {
+    std::lock_guard<std::mutex> g(prof_mu_);
+    if (!claims_fresh_) return;               // an earlier kClaims already took the latest set
+    claims_fresh_ = false;
+    next.swap(claims_staged_);
+  }
+  std::unordered_set<std::string> removed;
+  for (const auto& k : inert_)
+    if (!next.count(k)) removed.insert(k);
+  inert_.swap(next);
+  if (removed.empty()) return;
+  std::vector<Entry*> evict;
+  std::string key;
+  for (auto& kv : by_id_) {
+    Entry* e = kv.second;
+    if (e->st != QUEUED && e->st != PARKED && e->st != BACKOFF) continue;
+    const yk::PodProj& p = e->ev->full();
+    if (!(p.flags & yk::PF_CLAIMS)) continue;
+    for (const std::string& c : p.claims) {
+      key.assign(p.ns).append("/").append(c);
+      if (removed.count(key)) {
+        evict.push_back(e);
+        break;
+      }
+    }
   }
   for (Entry* e : evict) {
     if (e->st == PARKED || e->st == BACKOFF) {
@@ -2002,6 +2067,7 @@ void Lane::run() {
           case Item::kAnswer: handle_answer(it.tag, it.status, it.body, it.t); break;
           case Item::kProfiles: apply_profiles(&fwd); break;
           case Item::kGates: apply_gates(&fwd); break;
+          case Item::kClaims: apply_claims(&fwd); break;
           case Item::kMove: pending_moves_.push_back(it.status); break;
           case Item::kRelist: {
             std::vector<Fwd> out;

@@ -38,6 +38,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "engine.hpp"
@@ -131,6 +132,10 @@ class Lane : public yk::PodSink {
     // bound pods' required anti-affinity terms (InterPodAffinity's symmetric rule): a pod
     // matching any of them goes to Python, where that rule is checked; the others are unaffected
     std::vector<MatchTerm> gate_terms;
+    // a pod whose only flag in flag_mask is PF_CLAIMS is admissible when every claim it mounts
+    // is in the inert set (set_inert_claims): the profile's volume plugins are all no-ops for
+    // it (plugins/volumes.py::inert_claims), so its cycle is the native one
+    bool claims_ok = false;
     EngineConfig cfg;
   };
 
@@ -167,6 +172,9 @@ class Lane : public yk::PodSink {
   // only the selector gates of a declared profile (no engine-config snapshot); false if the
   // lane has no profile of that name
   bool set_gates(const std::string& name, std::vector<MatchTerm> terms);
+  // the PersistentVolumeClaims ("namespace/name") the volume plugins have nothing to check for;
+  // waiting pods mounting a claim that left the set go to Python
+  void set_inert_claims(std::vector<std::string> keys);
   void set_active(bool on);                    // leader: schedule; otherwise only keep the store
   void set_node_cards(const std::string& node, std::vector<std::pair<std::string, std::string>> vis);
   void remove_node_cards(const std::string& node);
@@ -277,7 +285,7 @@ class Lane : public yk::PodSink {
     bool failed = false;
   };
   struct Item {             // inbox: events, answers, commands — applied in order
-    enum K : uint8_t { kEvent, kAnswer, kRelist, kProfiles, kRunDone, kMove, kGates } k = kEvent;
+    enum K : uint8_t { kEvent, kAnswer, kRelist, kProfiles, kRunDone, kMove, kGates, kClaims } k = kEvent;
     char type = 0;
     std::shared_ptr<yk::PodEv> ev;
     uint64_t tag = 0;
@@ -414,6 +422,12 @@ class Lane : public yk::PodSink {
   // inadmissible); taken by the lane thread on kGates (prof_mu_)
   std::vector<std::pair<std::string, std::vector<MatchTerm>>> gate_adds_;
   std::vector<Profile> lp_;          // lane thread's view
+  // set_inert_claims: the latest set, taken by the lane thread on kClaims (prof_mu_)
+  bool claims_fresh_ = false;
+  std::unordered_set<std::string> claims_staged_;
+  std::unordered_set<std::string> inert_;   // lane thread's view
+  bool claims_inert(const yk::PodProj& p) const;
+  void apply_claims(std::vector<Fwd>* out);
 
   std::mutex vis_mu_;
   std::unordered_map<std::string, std::vector<std::pair<std::string, std::string>>> vis_;

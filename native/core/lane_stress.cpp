@@ -32,6 +32,8 @@ std::string pod_json(const std::string& name, const std::string& uid, const std:
                   "\",\"namespace\":\"default\",\"uid\":\"" + uid + "\",\"resourceVersion\":\"" + std::to_string(rv) +
                   "\",\"labels\":{" + labels + "}},\"spec\":{\"schedulerName\":\"yoda-scheduler\",";
   if (!node.empty()) s += "\"nodeName\":\"" + node + "\",";
+  // every pod mounts the claim "data" (inert: the profile admits it, see run_mode)
+  s += "\"volumes\":[{\"name\":\"d\",\"persistentVolumeClaim\":{\"claimName\":\"data\"}}],";
   s += "\"containers\":[{\"name\":\"main\",\"image\":\"x\",\"resources\":{\"requests\":{\"cpu\":\"100m\","
        "\"memory\":\"128Mi\"}}}]},\"status\":{\"phase\":\"Pending\"}}";
   return s;
@@ -108,7 +110,10 @@ int run_mode(int bursts, int per, int batch, int async_mode, int spin_us) {
   pr.name = "yoda-scheduler";
   pr.enabled = true;
   pr.cfg = cfg;
+  pr.flag_mask = yk::PF_CLAIMS;
+  pr.claims_ok = true;
   lane.set_profile(pr);
+  lane.set_inert_claims({"default/data"});
   lane.set_node_cards("node-0", {{"0", "u0"}, {"1", "u1"}, {"2", "u2"}, {"3", "u3"},
                                  {"4", "u4"}, {"5", "u5"}, {"6", "u6"}, {"7", "u7"}});
   lane.set_active(true);
@@ -142,6 +147,15 @@ int run_mode(int bursts, int per, int batch, int async_mode, int spin_us) {
         port.bound++;
       }
       if (!echo.empty()) lane.on_pod_events(1, echo);
+    }
+  });
+
+  // the Python thread re-sending the inert-claims set while the lane admits (TSan: prof_mu_ and
+  // the lane thread's kClaims apply); "default/data" stays in it, so every pod stays admissible
+  std::thread churn([&] {
+    for (int k = 0; !stop.load(); ++k) {
+      lane.set_inert_claims({"default/data", "default/x" + std::to_string(k % 4)});
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
     }
   });
 
@@ -210,6 +224,7 @@ int run_mode(int bursts, int per, int batch, int async_mode, int spin_us) {
   stop = true;
   port.cv.notify_all();
   io.join();
+  churn.join();
   lane.close();
   printf("{\"async_mode\": %d, \"spin_us\": %d, \"bursts\": %d, \"pods\": %d, \"scheduled\": %llu, "
          "\"confirmed\": %llu, \"released\": %llu, \"batches\": %llu, \"async_runs\": %llu, "

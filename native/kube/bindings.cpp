@@ -155,6 +155,7 @@ PYBIND11_MODULE(_yoda_kube, m) {
       .def_property_readonly("deleting", [](const PodEv& e) { return e.p.deleting; })
       .def_property_readonly("hash", [](const PodEv& e) { return e.full().spec_meta_hash; })
       .def_property_readonly("flags", [](const PodEv& e) { return e.full().flags; })
+      .def_property_readonly("claims", [](const PodEv& e) { return e.full().claims; })
       .def_property_readonly("labels_hash", [](const PodEv& e) { return e.p.labels_hash; })
       // status.conditions' PodScheduled entry: (status, reason, message, lastTransitionTime) or None
       .def_property_readonly("sched_cond", [](const PodEv& e) -> py::object {

@@ -654,8 +654,14 @@ void project_generic(N pod, PodProj& p) {
     static const char* kDisks[] = {"gcePersistentDisk", "awsElasticBlockStore", "azureDisk", "cinder", "iscsi", "rbd"};
     bool ok = vols.each([&](std::string_view, N v) {
       if (!v.obj()) return false;
-      if (v.get("persistentVolumeClaim") || v.get("ephemeral")) {
+      if (N pvc = v.get("persistentVolumeClaim")) {
         flags |= PF_CLAIMS;
+        N cn = pvc.obj() ? pvc.get("claimName") : N{};
+        p.claims.emplace_back(!cn ? std::string() : cn.str_t() ? std::string(cn.str()) : std::string("\x01"));
+      } else if (v.get("ephemeral")) {
+        flags |= PF_CLAIMS;
+        N vn = v.get("name");
+        p.claims.emplace_back(vn && !vn.str_t() ? std::string("\x01") : p.name + "-" + std::string(vn ? vn.str() : ""));
       } else {
         for (const char* d : kDisks)
           if (v.get(d)) {
@@ -1067,6 +1073,7 @@ void merge_non_identity(PodProj& d, PodProj&& s) {
   d.aff_pref = std::move(s.aff_pref);
   d.anti_pref = std::move(s.anti_pref);
   d.flags = s.flags;
+  d.claims = std::move(s.claims);
   d.spec_meta_hash = s.spec_meta_hash;
   d.ok = s.ok;
   d.has_sched_cond = s.has_sched_cond;

@@ -63,6 +63,10 @@ struct PodProj {
   std::vector<TolP> tolerations;
   std::vector<PortP> ports;
   int flags = 0;
+  // the claims of spec.volumes (plugins/volumes.py::_claim_names): a persistentVolumeClaim's
+  // claimName, a generic ephemeral volume's "<pod>-<volume>"; "\x01" for a name that is not a
+  // string (it names no PersistentVolumeClaim the lane could call inert)
+  std::vector<std::string> claims;
   uint64_t spec_meta_hash = 0;      // upstream isPodUpdated: spec + metadata minus volatile fields
   // structural hash of metadata.labels (0: unknown). Set by the full projection and by the
   // watch identity scanner too, so a light event tells whether a pod's labels changed

@@ -901,3 +901,28 @@ def test_labels_hash_agrees_across_scanner_and_projections():
         hashes.append(h_scan)
     # the same labels hash alike whatever the whitespace; different labels differ
     assert hashes[1] == hashes[-1] and len(set(hashes)) == len(cases) - 1
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.one_of(
+    st.builds(lambda c: {"name": "v", "persistentVolumeClaim": {"claimName": c}},
+              st.one_of(st.text(min_size=0, max_size=6), st.integers(0, 3), st.none())),
+    st.just({"name": "v", "persistentVolumeClaim": {}}),
+    st.builds(lambda n: {"name": n, "ephemeral": {"volumeClaimTemplate": {}}}, st.text(min_size=0, max_size=6)),
+    st.just({"ephemeral": {}}),
+    st.just({"name": "t", "emptyDir": {}}),
+    st.just({"name": "d", "gcePersistentDisk": {"pdName": "x"}})), max_size=4),
+    st.text(min_size=1, max_size=5))
+def test_projected_claims_equal_the_volume_plugins_claim_names(vols, pod_name):
+    """The lane admits PVC pods by their claim names (``PodEvent.claims``): equal to
+    plugins/volumes.py::_claim_names for string names; a non-string name becomes a sentinel no
+    PersistentVolumeClaim key can equal."""
+    from yoda_scheduler_amd.plugins.volumes import _claim_names
+    obj = {"metadata": {"name": pod_name, "namespace": "default", "uid": "u"},
+           "spec": {"schedulerName": "s", "containers": [{"name": "c", "image": "x"}], "volumes": vols}}
+    ev = K.project_flat(json.dumps(obj))
+    assert ev.ok
+    want = _claim_names(PodInfo.from_obj(obj))
+    assert len(ev.claims) == len(want)
+    for got, w in zip(ev.claims, want):
+        assert got == w if isinstance(w, str) else got == "\x01"

@@ -829,3 +829,64 @@ def test_gated_waiting_pod_moves_to_python_backoff_with_its_attempts():
             return n_failed, pi.attempts, pi.uid in q._backoff_pods or pi.uid in q._unsched, e.sched.lane.handoffs
     n_failed, attempts, waiting, handoffs = run(go())
     assert n_failed >= 3 and attempts >= n_failed and waiting and handoffs == 1
+
+
+def _csi_pv(name, host=None, zone=None):
+    spec = {"capacity": {"storage": "1Ti"}, "accessModes": ["ReadWriteMany"], "storageClassName": "shared",
+            "csi": {"driver": "nfs.csi.k8s.io", "volumeHandle": name}}
+    if host:
+        spec["nodeAffinity"] = {"required": {"nodeSelectorTerms": [{"matchExpressions": [
+            {"key": "kubernetes.io/hostname", "operator": "In", "values": [host]}]}]}}
+    return {"metadata": {"name": name, "labels": {"topology.kubernetes.io/zone": zone} if zone else {}},
+            "spec": spec, "status": {"phase": "Bound"}}
+
+
+def _bound_pvc(name, pv):
+    return {"metadata": {"name": name, "namespace": "default"},
+            "spec": {"accessModes": ["ReadWriteMany"], "resources": {"requests": {"storage": "1Gi"}},
+                     "storageClassName": "shared", "volumeName": pv}, "status": {"phase": "Bound"}}
+
+
+def _claim_pod(name, claim):
+    return pod(name, {"scv/memory": "1000"}, volumes=[{"name": "d", "persistentVolumeClaim": {"claimName": claim}}])
+
+
+@pytest.mark.parametrize("server", ["native", "python"])
+def test_pods_with_inert_claims_are_lane_pods_until_a_claim_needs_a_plugin(server):
+    """A pod mounting only claims every volume plugin has nothing to check for
+    (plugins/volumes.py::inert_claims: bound CSI PV, no node affinity, no zone labels, no attach
+    limit) is admitted by the lane. When its claim's PV gains node affinity the claim leaves the
+    set: a waiting lane pod mounting it goes to Python, and new ones take the Python cycle,
+    where VolumeBinding keeps them on the PV's node."""
+    async def go():
+        async with Env(server=server, nodes=(("n1", 8, None), ("n2", 8, None))) as e:
+            nl = e.sched.lane
+            lane = nl.lane
+            await e.cl.create("persistentvolumes", _csi_pv("pv-a"))
+            await e.cl.create("persistentvolumeclaims", _bound_pvc("data", "pv-a"))
+            await e.cl.create("persistentvolumes", _csi_pv("pv-b"))
+            await e.cl.create("persistentvolumeclaims", _bound_pvc("ckpt", "pv-b"))
+            assert await e.wait(lambda: {"default/data", "default/ckpt"} <= nl._claims)
+            for i in range(4):
+                await e.create(_claim_pod(f"c{i}", "data"))
+            assert await e.wait(lambda: e.sched.scheduled == 4)
+            on_lane = lane.scheduled
+            # a waiting lane pod whose claim stops being inert goes to the Python path
+            lane.pause(True)
+            await e.create(_claim_pod("w0", "ckpt"))
+            await asyncio.sleep(0.3)
+            await e.cl.patch("persistentvolumes", "pv-b", {"spec": _csi_pv("pv-b", host="n2")["spec"]})
+            assert await e.wait(lambda: "default/ckpt" not in nl._claims)
+            lane.pause(False)
+            assert await e.wait(lambda: e.sched.scheduled == 5)
+            await e.create(_claim_pod("w1", "ckpt"))
+            assert await e.wait(lambda: e.sched.scheduled == 6)
+            pods = await e.pods()
+            return on_lane, lane.scheduled, e.sched._scheduled, pods["w0"]["spec"]["nodeName"], \
+                pods["w1"]["spec"]["nodeName"], e.sched.cache.lane_never_flags
+    on_lane, lane_total, py_bound, w0, w1, never = run(go())
+    from yoda_scheduler_amd.models.pod import PF_CLAIMS
+    assert on_lane == 4                       # every inert-claim pod bound by the lane
+    assert lane_total == 4 and py_bound == 2  # w0 (evicted while waiting) and w1 by Python
+    assert w0 == "n2" and w1 == "n2"          # the PV's node affinity, checked by VolumeBinding
+    assert not never & PF_CLAIMS              # lane pods may carry claims: Python's readers see them

@@ -27,7 +27,7 @@ import contextlib
 import logging
 from typing import Optional
 
-from ..models.pod import PodInfo
+from ..models.pod import PF_CLAIMS, PodInfo
 from ..ops.native import core
 
 log = logging.getLogger("yoda.lane")
@@ -69,6 +69,8 @@ class NativeLane:
         self._in_gated = False             # inside gated(): anti-affinity changes wait for its exit
         self._gates_pending = False        # a coalesced gate update (holder removals) is scheduled
         self._sticky_never = (1 << 62) - 1  # AND of the masks of profiles eligible since the lane last owned nothing
+        self._claims_key: Optional[tuple] = None   # listers' generations the inert-claims set was computed at
+        self._claims: frozenset = frozenset()     # the set the lane holds (plugins/volumes.py::inert_claims)
         sched.queue.on_move_all = self._move_all
 
     # ------------------------------------------------------------------ lifecycle
@@ -153,20 +155,45 @@ class NativeLane:
         # its reserved pods in the lane, so its mask keeps counting until the lane owns nothing
         if self._sticky_never != never and self.owned() == 0:
             self._sticky_never = never
+        claims = self._refresh_claims()
         for name, fw in s.frameworks.items():
             m = self.eligible_mask(fw)
+            c_ok = m is not None and fw.claims_ok()
             if m is not None:
-                never &= m
-                self._sticky_never &= m
+                # lane pods may carry PF_CLAIMS (inert claims only) once the set is non-empty
+                lm = m & ~PF_CLAIMS if c_ok and claims else m
+                never &= lm
+                self._sticky_never &= lm
             want = (m is not None, m or 0, bool(fw.filter_mask & f_yoda), self.preempt_above(fw),
-                    fw.gate_terms() + self._temp_terms if m is not None else ())
+                    fw.gate_terms() + self._temp_terms if m is not None else (), c_ok)
             if self._profiles.get(name) == want:
                 continue
             s._activate(fw)                    # the lane snapshots the engine config now applied
-            self.lane.set_profile(s.engine, name, want[0], want[1], want[2], want[3], list(want[4]))
+            self.lane.set_profile(s.engine, name, want[0], want[1], want[2], want[3], list(want[4]), want[5])
             self._profiles[name] = want
             log.info("native lane: profile %s %s (flag mask %#x)", name, "on" if want[0] else "off", want[1])
         s.cache.lane_never_flags = never & self._sticky_never
+
+    def _refresh_claims(self) -> frozenset:
+        """Send the lane the claims a pod may mount and still take the native cycle
+        (plugins/volumes.py::inert_claims) when the objects they derive from changed: the PVC,
+        PV, StorageClass and CSINode listers (their generations) and whether a node has a CSI
+        attach limit. Only profiles whose volume plugins all allow it (``claims_ok``) use it."""
+        s = self.s
+        if not any(fw.claims_ok() for fw in s.frameworks.values()):
+            return self._claims
+        gen = s.handle.generation
+        key = (gen("persistentvolumeclaims"), gen("persistentvolumes"), gen("storageclasses"), gen("csinodes"),
+               s.cache.csi_limit_nodes > 0)
+        if key == self._claims_key:
+            return self._claims
+        from ..plugins.volumes import inert_claims
+        self._claims_key = key
+        new = frozenset(inert_claims(s.handle))
+        if new != self._claims:
+            self._claims = new
+            self.lane.set_inert_claims(sorted(new))
+        return new
 
     def anti_changed(self, grew: bool = True) -> None:
         """The bound/assumed pods with required anti-affinity changed. A new holder's terms reach
@@ -200,7 +227,7 @@ class NativeLane:
             if terms == want[4]:
                 continue
             self.lane.set_gates(name, list(terms))
-            self._profiles[name] = want[:4] + (terms,)
+            self._profiles[name] = want[:4] + (terms,) + want[5:]
 
     # ------------------------------------------------------------------ lane output
     async def wait_scheduled(self, target: int, timeout: float) -> bool:

@@ -170,6 +170,18 @@ class Framework:
                 return True
         return False
 
+    def claims_ok(self) -> bool:
+        """May the native lane run this profile's pods whose only lane-excluding feature is
+        PF_CLAIMS, when every claim is inert (plugins/volumes.py::inert_claims)? Yes when every
+        plugin that acts on claims — conditional or PreBind — declares that inert claims make
+        it a no-op (``claim_inert_ok``)."""
+        from ..models.pod import PF_CLAIMS
+        for p in list(self.conditional) + list(self.pre_bind):
+            pf = getattr(p, "pod_flags", None)
+            if pf is None or (pf & PF_CLAIMS and not getattr(p, "claim_inert_ok", False)):
+                return False
+        return any(getattr(p, "claim_inert_ok", False) for p in self.conditional)
+
     def direct_bind_mask(self) -> Optional[int]:
         """Likewise for ``direct_binder_for``: pods without these flags get the single bind
         plugin directly; None when the shortcut does not hold (ask per pod)."""

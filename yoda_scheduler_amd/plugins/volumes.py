@@ -203,6 +203,7 @@ class VolumeRestrictions(_VolumeBase, FilterPlugin):
 class VolumeZone(_VolumeBase, FilterPlugin):
     name = "VolumeZone"
     pod_flags = PF_CLAIMS
+    claim_inert_ok = True   # a no-op for a pod whose claims are all in inert_claims()
     reads_flags = 0  # other pods' features this plugin reads (needs_lane_mirror)
 
     def is_noop_for(self, pod) -> bool:
@@ -283,7 +284,10 @@ class VolumeBinding(_VolumeBase, PreFilterPlugin, FilterPlugin, ReservePlugin, P
     name = "VolumeBinding"
     KEY = "PreFilterVolumeBinding"
     pod_flags = PF_CLAIMS
-    reads_flags = PF_CLAIMS  # other pods' features this plugin reads (needs_lane_mirror)
+    # other pods' features this plugin reads (needs_lane_mirror): none — it reads the PVC / PV /
+    # StorageClass listers and its own assumed PVs, never another pod
+    reads_flags = 0
+    claim_inert_ok = True   # a no-op for a pod whose claims are all in inert_claims()
 
     def __init__(self, args=None, handle=None) -> None:
         super().__init__(args, handle)
@@ -485,6 +489,7 @@ class NodeVolumeLimits(_LimitsBase):
     ``attachable-volumes-csi-<driver>``)."""
     name = "NodeVolumeLimits"
     pod_flags = PF_CLAIMS
+    claim_inert_ok = True   # a no-op for a pod whose claims are all in inert_claims()
     reads_flags = PF_CLAIMS  # other pods' features this plugin reads (needs_lane_mirror)
     watches = ("persistentvolumeclaims", "persistentvolumes", "storageclasses", "csinodes")
 
@@ -504,9 +509,7 @@ class NodeVolumeLimits(_LimitsBase):
         gen = self.handle.generation("csinodes") if hasattr(self.handle, "generation") else -2
         g, any_count = self._csinode_limits
         if g != gen or gen == -2:
-            any_count = any((d.get("allocatable") or _EMPTY).get("count") is not None
-                            for cn in self._lister("csinodes").values()
-                            for d in ((cn.get("spec") or _EMPTY).get("drivers") or ()))
+            any_count = _csinode_counts(self._lister("csinodes"))
             self._csinode_limits = (gen, any_count)
         return any_count
 
@@ -555,6 +558,7 @@ class _InTreeLimits(_LimitsBase):
     default_max = 0
     pod_flags = PF_CLAIMS | PF_DISKS
     reads_flags = PF_CLAIMS | PF_DISKS  # other pods' features this plugin reads (needs_lane_mirror)
+    claim_inert_ok = True   # a no-op for a pod whose claims are all in inert_claims() (PF_DISKS: not)
 
     def is_noop_for(self, pod) -> bool:
         # no inline volume of this kind and no PVC bound to one: the filter has nothing to count
@@ -599,6 +603,45 @@ class CinderLimits(_InTreeLimits):
     """Not in the v1.20 default profile; enabled by configs that name it."""
     name = "CinderLimits"
     kind, id_field, alloc_key, default_max = "cinder", "volumeID", "attachable-volumes-cinder", 256
+
+
+def _csinode_counts(csinodes: dict) -> bool:
+    """Some CSINode reports an attach limit (``drivers[].allocatable.count``)."""
+    return any((d.get("allocatable") or _EMPTY).get("count") is not None
+               for cn in csinodes.values() for d in ((cn.get("spec") or _EMPTY).get("drivers") or ()))
+
+
+def inert_claims(handle) -> set:
+    """The PersistentVolumeClaims ("namespace/name") every volume plugin has nothing to check
+    for: not being deleted, bound to a PV that exists and has no required node affinity, no
+    zone / region labels and no in-tree attachable disk, and either not a CSI volume or no
+    attach limit anywhere in the cluster. A pod whose claims are all in this set is a no-op for
+    VolumeBinding, VolumeZone, NodeVolumeLimits and the in-tree limits (each claim satisfies
+    the per-claim half of their ``is_noop_for``), so the native lane may run it."""
+    pvcs, pvs = handle.lister("persistentvolumeclaims"), handle.lister("persistentvolumes")
+    limits = None
+    out = set()
+    for key, pvc in pvcs.items():
+        if (pvc.get("metadata") or _EMPTY).get("deletionTimestamp"):
+            continue
+        name = (pvc.get("spec") or _EMPTY).get("volumeName", "")
+        pv = pvs.get(name) if name else None
+        if pv is None:
+            continue
+        ps = pv.get("spec") or _EMPTY
+        if (ps.get("nodeAffinity") or _EMPTY).get("required") is not None:
+            continue
+        labels = (pv.get("metadata") or _EMPTY).get("labels") or _EMPTY
+        if any(k in labels for k in ZONE_LABELS) or any(ps.get(k) for k in _ATTACHABLE_KINDS):
+            continue
+        if ps.get("csi"):
+            if limits is None:
+                limits = getattr(handle.cache, "csi_limit_nodes", 1) > 0 or \
+                    _csinode_counts(handle.lister("csinodes"))
+            if limits:
+                continue
+        out.add(key)
+    return out
 
 
 # the in-tree attach-limit plugins' volume kinds (what _VolFacts resolves for them)
