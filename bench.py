@@ -172,6 +172,9 @@ def main(argv=None) -> int:
     ap.add_argument("--mix-spread", type=int, default=0,
                     help="beyond BASELINE: give this many pods of the burst (evenly spread; 1000 = all) a hostname "
                          "DoNotSchedule topologySpreadConstraint (native PodTopologySpread since round 5)")
+    ap.add_argument("--mix-hostports", type=int, default=0,
+                    help="beyond BASELINE: this many pods of the burst (evenly spread; 1000 = all) request a distinct "
+                         "host port (native NodePorts since round 5)")
     ap.add_argument("--mix-volumes", type=int, default=0,
                     help="beyond BASELINE: this many pods of the burst (evenly spread) mount a bound PVC, so the "
                          "Python volume plugins apply and they take the Python cycle beside the lane")
@@ -257,7 +260,7 @@ def main(argv=None) -> int:
     from yoda_scheduler_amd.bench.harness import HttpShard, Shard, percentile
     from yoda_scheduler_amd.bench.workloads import make_workload
     w = make_workload(a.config, seed=rank, node_gpus=a.node_gpus, nodes=a.nodes, mix_anti=a.mix_anti,
-                      mix_spread=a.mix_spread, mix_volumes=a.mix_volumes,
+                      mix_spread=a.mix_spread, mix_volumes=a.mix_volumes, mix_hostports=a.mix_hostports,
                       cluster=a.cluster)
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)

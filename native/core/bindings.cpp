@@ -316,12 +316,13 @@ PYBIND11_MODULE(_yoda_core, m) {
   m.attr("S_NUM") = (int)S_NUM;
   m.attr("F_SPREAD") = (uint32_t)F_SPREAD;
   m.attr("F_INTERPOD") = (uint32_t)F_INTERPOD;
+  m.attr("F_NODE_PORTS") = (uint32_t)F_NODE_PORTS;
   m.attr("S_INTERPOD") = (int)S_INTERPOD;
   m.attr("REASONS") = py::make_tuple("OK", "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity",
                                      "NodeResourcesFit", "NoScv", "ScvStale", "GpuNumber", "GpuMemory",
                                      "GpuClock", "GpuFit", "NodeGone", "NodeResourcesFitExtended",
                                      "PodTopologySpread", "PodTopologySpreadLabel", "InterPodAffinityExisting",
-                                     "InterPodAffinity", "InterPodAntiAffinity");
+                                     "InterPodAffinity", "InterPodAntiAffinity", "NodePorts");
 
   py::class_<PodReq>(m, "PodReq")
       .def_readonly("has_number", &PodReq::has_number)
@@ -510,6 +511,15 @@ PYBIND11_MODULE(_yoda_core, m) {
            py::arg("nz_cpu_m") = -1, py::arg("nz_mem") = -1, py::call_guard<EngineGuard>())
       // the default-plugin inputs of a PodReq (ImageLocality, NodeResourcesFit beyond cpu/memory,
       // NodePreferAvoidPods, PodTopologySpread and what other pods' spread counts read of it)
+      // NodePorts: the pod's containers' host ports [(hostPort, protocol, hostIP)]
+      .def("set_req_ports",
+           [](Engine& e, PodReq& r, const std::vector<std::tuple<int64_t, std::string, std::string>>& ports) {
+             r.host_ports.clear();
+             HostPort h;
+             for (const auto& t : ports)
+               if (e.host_port(std::get<0>(t), std::get<1>(t), std::get<2>(t), &h)) r.host_ports.push_back(h);
+           },
+           py::arg("req"), py::arg("ports"), py::call_guard<EngineGuard>())
       .def("set_req_extras",
            [](Engine& e, PodReq& r, const std::string& ns, const std::vector<std::pair<std::string, std::string>>& labels,
               bool deleting, const std::vector<std::string>& images, int32_t containers,

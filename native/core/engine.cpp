@@ -99,6 +99,8 @@ Engine::Engine(bool compat, int threads) : compat_(compat) {
   if (threads > 1) pool_ = new ThreadPool(threads);
   intern("");
   unsched_key_ = intern("node.kubernetes.io/unschedulable");
+  any_ip_ = intern("0.0.0.0");
+  tcp_ = intern("TCP");
   dev_ext_res_ = intern("ephemeral-storage");
 }
 
@@ -287,6 +289,29 @@ void Engine::set_links(int32_t idx, int32_t nphys, std::vector<int32_t> q) {
   mark_dirty(idx);
 }
 
+bool Engine::host_port(int64_t port, const std::string& protocol, const std::string& ip, HostPort* out) {
+  // upstream v1.20 framework.HostPortInfo: sanitize (ip "" → 0.0.0.0, protocol "" → TCP); a port
+  // <= 0 is no host port (Add / CheckConflict ignore it)
+  if (port <= 0 || port > INT32_MAX) return false;
+  out->port = (int32_t)port;
+  out->proto = protocol.empty() ? tcp_ : intern(protocol);
+  out->ip = ip.empty() ? any_ip_ : intern(ip);
+  return true;
+}
+
+bool Engine::ports_free(const PodReq& req, const Node& n) const {
+  // HostPortInfo.CheckConflict: a 0.0.0.0 request conflicts with the (protocol, port) on any ip;
+  // a specific ip only with the same ip or 0.0.0.0
+  for (const HostPort& h : req.host_ports) {
+    if (h.ip == any_ip_) {
+      if (n.ports_any.count({h.proto, h.port})) return false;
+    } else if (n.ports.count(HostPort{any_ip_, h.proto, h.port}) || n.ports.count(h)) {
+      return false;
+    }
+  }
+  return true;
+}
+
 const Assignment* Engine::assignment(uint64_t pod) const {
   auto it = ledger_.find(pod);
   return it == ledger_.end() ? nullptr : &it->second;
@@ -337,6 +362,13 @@ bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::ve
     aff_set_add(a);
   }
   index_pod(n, a, +1);
+  if (!req.host_ports.empty()) {
+    a.host_ports = req.host_ports;
+    for (const HostPort& h : a.host_ports) {
+      ++n.ports[h];
+      ++n.ports_any[{h.proto, h.port}];
+    }
+  }
   if (!req.ext.empty()) {
     a.ext = req.ext;
     for (const auto& r : a.ext) {
@@ -383,6 +415,12 @@ bool Engine::release(uint64_t pod) {
       if (it != n.ext_used.end() && it->first == r.first && (it->second -= r.second) == 0) n.ext_used.erase(it);
     }
     index_pod(n, a, -1);
+    for (const HostPort& h : a.host_ports) {
+      auto p = n.ports.find(h);
+      if (p != n.ports.end() && --p->second <= 0) n.ports.erase(p);
+      auto q = n.ports_any.find({h.proto, h.port});
+      if (q != n.ports_any.end() && --q->second <= 0) n.ports_any.erase(q);
+    }
     mark_dirty(a.node);
   }
   if (a.aff) {
@@ -516,6 +554,8 @@ Reason Engine::filter_node_pf(const PodReq& req, int32_t idx, uint64_t* pn, uint
     }
   }
   if ((filters_ & F_NODE_NAME) && req.node_name > 0 && strings_[req.node_name] != n.name) return RS_NODE_NAME;
+  // upstream v1.20 default filter order: NodeName, NodePorts, NodeAffinity, ..., TaintToleration
+  if ((filters_ & F_NODE_PORTS) && !req.host_ports.empty() && !ports_free(req, n)) return RS_NODE_PORTS;
   if ((filters_ & F_NODE_AFFINITY) && !affinity_ok(req, n)) return RS_AFFINITY;
   if ((filters_ & F_TAINT_TOLERATION) && !taints_ok(req, n)) return RS_TAINT;
   if (filters_ & F_YODA) {
@@ -1955,6 +1995,9 @@ bool Engine::device_eligible(const PodReq& req) const {
       wt_.w_numa < -1000000 || wt_.w_fit < -1000000 || wt_.w_occ < -1000000)
     return false;
   if (!default_alloc_weights()) return false;                    // device computes (c + m) / 2
+  // NodePorts: the device row carries no host ports, and pods placed in one device batch would
+  // not see each other's
+  if ((filters_ & F_NODE_PORTS) && !req.host_ports.empty()) return false;
   // default-plugin terms the device row does not carry: only pods for which they are a
   // constant (or nothing) go to the device
   if ((filters_ & F_NODE_RESOURCES_FIT) && !req.ext.empty())

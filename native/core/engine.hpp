@@ -18,6 +18,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <random>
 #include <string>
@@ -46,6 +47,7 @@ enum FilterBit : uint32_t {
   F_YODA = 1u << 5,
   F_SPREAD = 1u << 6,          // PodTopologySpread DoNotSchedule constraints (explicit or profile defaults)
   F_INTERPOD = 1u << 7,        // InterPodAffinity: required (anti-)affinity, existing pods' anti-affinity
+  F_NODE_PORTS = 1u << 8,      // NodePorts: host ports of the pods the ledger holds on the node
 };
 enum ScoreIdx : int {
   S_YODA = 0,
@@ -71,6 +73,7 @@ enum Reason : int8_t {
   RS_EXISTING_ANTI,            // InterPodAffinity: an existing pod's required anti-affinity
   RS_POD_AFFINITY,             // InterPodAffinity: the pod's required affinity
   RS_POD_ANTI,                 // InterPodAffinity: the pod's required anti-affinity
+  RS_NODE_PORTS,               // NodePorts: a requested host port is taken
   RS_NUM
 };
 
@@ -187,6 +190,16 @@ struct LabSetHash {
   }
 };
 
+// NodePorts: a container port with hostPort > 0, sanitized as upstream HostPortInfo (hostIP ""
+// → "0.0.0.0", protocol "" → "TCP"); hostIP and protocol interned
+struct HostPort {
+  int32_t ip = 0, proto = 0, port = 0;
+  bool operator<(const HostPort& o) const {
+    return ip != o.ip ? ip < o.ip : proto != o.proto ? proto < o.proto : port < o.port;
+  }
+  bool operator==(const HostPort& o) const { return ip == o.ip && proto == o.proto && port == o.port; }
+};
+
 struct Node {
   std::string name;
   uint32_t gen = 0;                   // slot generation: bumped when the slot gets a new node or dies
@@ -218,6 +231,10 @@ struct Node {
   // counts: any other selector is matched once per group instead of once per pod (a node's pods
   // come from few templates)
   std::unordered_map<LabSet, std::pair<int32_t, int32_t>, LabSetHash> lab_groups;
+  // NodePorts: host ports of the reserved pods, per (ip, protocol, port) and per (protocol, port)
+  // over every ip (a 0.0.0.0 request conflicts with any ip) — counts, as two pods may hold one
+  std::map<HostPort, int32_t> ports;
+  std::map<std::pair<int32_t, int32_t>, int32_t> ports_any;
 };
 
 struct PodReq {
@@ -257,6 +274,8 @@ struct PodReq {
   std::vector<SpreadC> spread;
   // InterPodAffinity: the pod's (anti-)affinity terms (null: none)
   std::shared_ptr<const PodAffinity> aff;
+  // NodePorts: its containers' host ports (hostPort > 0), sanitized
+  std::vector<HostPort> host_ports;
 };
 
 struct Weights {
@@ -297,6 +316,7 @@ struct Assignment {
   std::vector<std::pair<int32_t, int64_t>> ext;   // extended resources it holds on the node
   std::shared_ptr<const PodAffinity> aff;          // its (anti-)affinity terms (symmetric rule, scoring)
   uint64_t aff_hash = 0;                           // its AffSet's bucket (aff_sets_)
+  std::vector<HostPort> host_ports;                // NodePorts: the host ports it holds on the node
 };
 
 struct CycleResult {
@@ -379,6 +399,10 @@ class Engine {
   void seed(uint64_t s) { rng_.seed(s); }
   int32_t intern(const std::string& s);
   const std::string& str(int32_t id) const { return strings_[id]; }
+  // NodePorts: one requested host port as upstream HostPortInfo keeps it; false for port <= 0
+  // (not a host port: never conflicts)
+  bool host_port(int64_t port, const std::string& protocol, const std::string& ip, HostPort* out);
+  bool ports_free(const PodReq& req, const Node& n) const;
 
   // ---- cluster state
   int32_t upsert_node(const std::string& name);      // returns index (stable)
@@ -591,6 +615,7 @@ class Engine {
   Weights wt_;
   int pct_nodes_ = 0;
   int32_t unsched_key_ = 0;
+  int32_t any_ip_ = 0, tcp_ = 0;      // interned "0.0.0.0" / "TCP" (NodePorts sanitize)
   std::vector<Node> nodes_;
   std::vector<int32_t> free_slots_;
   uint32_t gen_counter_ = 0;

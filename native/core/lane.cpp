@@ -43,6 +43,7 @@ const char* reason_text(int i) {
     case RS_EXISTING_ANTI: return "node(s) didn't satisfy existing pods anti-affinity rules";
     case RS_POD_AFFINITY: return "node(s) didn't match pod affinity rules";
     case RS_POD_ANTI: return "node(s) didn't match pod anti-affinity rules";
+    case RS_NODE_PORTS: return "node(s) didn't have free ports for the requested pod ports";
     default: return i >= 0 && i < RS_NUM ? kReasonName[i] : "unknown";
   }
 }
@@ -973,6 +974,9 @@ bool Lane::make_req(const yk::PodProj& p, PodReq* r) {
   r->containers = p.containers;
   for (const auto& x : p.ext) r->ext.emplace_back(eng_->intern(x.first), x.second);
   std::sort(r->ext.begin(), r->ext.end());
+  HostPort hp;
+  for (const auto& x : p.ports)
+    if (eng_->host_port(x.host_port, x.protocol, x.host_ip, &hp)) r->host_ports.push_back(hp);
   if (p.has_owner) {
     r->owner_kind = p.owner_api == "v1" && p.owner_kind == "ReplicationController" ? 1
                     : p.owner_api == "apps/v1" && p.owner_kind == "ReplicaSet"  ? 2

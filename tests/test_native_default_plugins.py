@@ -344,6 +344,45 @@ def test_extended_resource_fit_native_equals_python(allocs, bound, request, args
         assert (got == 0) == want, (n, request, args)
 
 
+# ============================================================== NodePorts
+from yoda_scheduler_amd.plugins.defaults import NodePorts  # noqa: E402
+
+_host_ports = st.lists(st.tuples(st.sampled_from([0, -1, 80, 8080]), st.sampled_from(["", "TCP", "UDP", "SCTP"]),
+                                 st.sampled_from(["", "0.0.0.0", "10.0.0.1", "10.0.0.2"])), max_size=3)
+
+
+def _ports(lst):
+    return [dict({"containerPort": 1, "hostPort": port}, **({"protocol": proto} if proto else {}),
+                 **({"hostIP": ip} if ip else {})) for port, proto, ip in lst]
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.lists(st.tuples(st.integers(0, 2), _host_ports), max_size=6), _host_ports, st.integers(0, 6))
+def test_node_ports_native_equals_python(bound, want, drop):
+    """Engine F_NODE_PORTS ≡ the Python spec (upstream HostPortInfo.CheckConflict: hostIP "" is
+    0.0.0.0, which conflicts with the port on any IP; protocol "" is TCP; ports <= 0 are no host
+    ports), including after some of the bound pods are released."""
+    eng, cache = cache_with([node_obj(f"n{i}") for i in range(3)])
+    eng.filters = C.F_NODE_PORTS
+    pl = NodePorts({}, SimpleNamespace(cache=cache))
+    uids = []
+    for j, (k, lst) in enumerate(bound):
+        uid = f"b{j}-{next(_uid)}"
+        cache.add_pod({"metadata": {"name": f"b{j}", "namespace": "default", "uid": uid},
+                       "spec": {"nodeName": f"n{k}", "containers": [{"name": "c", "ports": _ports(lst)}]}})
+        uids.append(uid)
+    for uid in uids[:drop]:
+        cache.remove_pod(uid)
+    p = pod("p", containers=[{"name": "c", "ports": _ports(want)}])
+    req = pod_req(eng, p)
+    reason = C.REASONS.index("NodePorts")
+    for n in sorted(cache.nodes):
+        ok = pl.filter(CycleState(), p, n).is_success()
+        got = eng.filter_node(req, eng.node_index(n))
+        assert got in (0, reason)
+        assert (got == 0) == ok, (n, bound, want, drop)
+
+
 # ============================================================== InterPodAffinity
 from yoda_scheduler_amd.plugins.spread_affinity import InterPodAffinity  # noqa: E402
 

@@ -379,15 +379,51 @@ def test_affinity_pods_count_lane_pods_natively_without_a_mirror():
 
 
 def test_native_lane_off_and_on_agree_on_python_only_pods():
-    """Host-port pods are never admitted by the lane (PF_HOST_PORTS): they bind via Python."""
+    """A pod with an inline attachable disk (PF_DISKS: VolumeRestrictions is a Python plugin) is
+    never admitted by the lane: it binds via Python."""
     async def go():
         async with Env() as e:
-            await e.create(pod("hp", {"scv/memory": "1000"},
-                               containers=[{"name": "c", "ports": [{"containerPort": 80, "hostPort": 8080}]}]))
+            await e.create(pod("disk", {"scv/memory": "1000"},
+                               volumes=[{"name": "d", "gcePersistentDisk": {"pdName": "pd-1"}}]))
             assert await e.wait(lambda: e.sched.scheduled == 1)
             return e.sched.lane.lane.stats()["admitted"], e.sched.lane.forwarded
     admitted, forwarded = run(go())
     assert admitted == 0 and forwarded >= 1
+
+
+@pytest.mark.parametrize("lane", ["on", "off"])
+def test_host_port_pods_are_native_and_never_share_a_port(lane):
+    """NodePorts is native (engine ``F_NODE_PORTS``): host-port pods are lane pods, and the lane
+    and the Python path alike keep two pods from holding one host port on a node
+    (0.0.0.0 conflicts with any hostIP; distinct hostIPs share a port; UDP ≠ TCP)."""
+    def hp(port, ip="", proto=""):
+        p = {"containerPort": 80, "hostPort": port}
+        if ip:
+            p["hostIP"] = ip
+        if proto:
+            p["protocol"] = proto
+        return [{"name": "c", "ports": [p]}]
+
+    async def go():
+        async with Env(lane=lane, nodes=(("n1", 8, None), ("n2", 8, None))) as e:
+            specs = [("a", hp(8080)), ("b", hp(8080)), ("c", hp(8080)),            # 3rd has no node left
+                     ("d", hp(9000, "10.0.0.1")), ("e", hp(9000, "10.0.0.2")),   # distinct IPs share
+                     ("f", hp(9000, "10.0.0.1")),                                # same IP twice per node
+                     ("g", hp(8080, proto="UDP")), ("h", hp(8080, proto="UDP"))]
+            for name, containers in specs:
+                await e.create(pod(name, {"scv/memory": "1000"}, containers=containers))
+            assert await e.wait(lambda: e.sched.scheduled == 7)
+            await asyncio.sleep(0.2)
+            pods = await e.pods()
+            nodes = {n: pods[n]["spec"].get("nodeName", "") for n, _ in specs}
+            admitted = e.sched.lane.lane.stats()["admitted"] if e.sched.lane else None
+            return nodes, admitted
+    nodes, admitted = run(go())
+    assert {nodes["a"], nodes["b"]} == {"n1", "n2"} and nodes["c"] == ""
+    assert nodes["d"] != nodes["f"] and "" not in (nodes["d"], nodes["e"], nodes["f"])
+    assert {nodes["g"], nodes["h"]} == {"n1", "n2"}
+    if lane == "on":
+        assert admitted == 8
 
 
 def test_finish_cycle_refuses_a_result_whose_node_slot_was_reused():

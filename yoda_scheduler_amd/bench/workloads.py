@@ -66,7 +66,8 @@ def _mixed_labels(rng: random.Random) -> dict:
 
 def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None,
                   node_gpus: Optional[int] = None, nodes: Optional[int] = None, mix_anti: int = 0,
-                  cluster: str = "synthetic", mix_spread: int = 0, mix_volumes: int = 0) -> Workload:
+                  cluster: str = "synthetic", mix_spread: int = 0, mix_volumes: int = 0,
+                  mix_hostports: int = 0) -> Workload:
     """``node_gpus`` overrides the GPUs per node (BASELINE.md protocol item 5: every
     config at 1, 2, 4 and 8 GPUs per node); pods keep their labels, so e.g. ``scv/number: 8``
     pods are unschedulable on smaller nodes and are reported as such. ``nodes`` resizes
@@ -99,6 +100,20 @@ def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None,
         w.name += f" + {min(mix_spread, n)} hostname-spread pods"
     if mix_volumes:
         _add_volume_pods(w, mix_volumes)
+    if mix_hostports:
+        # beyond BASELINE: pods with a host port each (distinct ports: all fit on one node), as
+        # hostNetwork training pods carry — native NodePorts since round 5
+        n = len(w.pods)
+        count = min(mix_hostports, n)
+        for j in range(count):
+            i = j * n // count
+            spec = dict(w.specs.get(i) or {})
+            c = dict((spec.get("containers") or [{"name": "main", "image": "rocm/pytorch:latest",
+                                                   "resources": {"requests": {"cpu": "100m", "memory": "128Mi"}}}])[0])
+            c["ports"] = [{"containerPort": 29500, "hostPort": 20000 + j, "protocol": "TCP"}]
+            spec["containers"] = [c]
+            w.specs[i] = spec
+        w.name += f" + {count} host-port pods"
     if nodes is not None:
         if cfg != 6 or nodes < 1:
             raise ValueError("nodes: config 6 only, >= 1")

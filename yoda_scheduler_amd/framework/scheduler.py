@@ -869,7 +869,11 @@ class Scheduler:
                 "GpuFit": "node(s) have too few healthy GPUs matching scv/memory+scv/clock",
                 "NodeResourcesFitExtended": ext_text(pi.ext if pi is not None else None),
                 "PodTopologySpread": "node(s) didn't match pod topology spread constraints",
-                "PodTopologySpreadLabel": "node(s) didn't match pod topology spread constraints (missing required label)"}
+                "PodTopologySpreadLabel": "node(s) didn't match pod topology spread constraints (missing required label)",
+                "InterPodAffinityExisting": "node(s) didn't satisfy existing pods anti-affinity rules",
+                "InterPodAffinity": "node(s) didn't match pod affinity rules",
+                "InterPodAntiAffinity": "node(s) didn't match pod anti-affinity rules",
+                "NodePorts": "node(s) didn't have free ports for the requested pod ports"}
         parts = [f"{c} {text.get(names[i], names[i])}" for i, c in enumerate(reasons) if c and i]
         if len(res) > 10 and res[10]:
             by_msg: dict[str, int] = {}

@@ -223,7 +223,7 @@ def pod_req(engine, pi: PodInfo):
         return pi.native_req
     key = None
     if not (pi.node_name or pi.node_selector or pi.required_terms or pi.preferred_terms or pi.tolerations
-            or pi.ext or pi.spread or pi.pod_aff):
+            or pi.ext or pi.spread or pi.pod_aff or pi.host_ports):
         key = (pi.gpu, pi.cpu_m, pi.mem, pi.nz_cpu_m, pi.nz_mem, pi.namespace, tuple(pi.labels.items()),
                tuple(pi.images), pi.containers, pi.owner, pi.avoid, pi.deleting)
         shared = _shared_reqs
@@ -240,6 +240,9 @@ def pod_req(engine, pi: PodInfo):
                         pi.tolerations, pi.nz_cpu_m, pi.nz_mem)
     engine.set_req_extras(r, pi.namespace, list(pi.labels.items()), pi.deleting, pi.images, pi.containers,
                           list(pi.ext.items()), pi.owner, pi.avoid, pi.spread, pi.pod_aff)
+    if pi.host_ports:
+        from ..plugins.defaults import host_port_set
+        engine.set_req_ports(r, [(port, proto, ip) for ip, proto, port in sorted(host_port_set(pi.host_ports))])
     pi.native_req, pi.native_owner = r, engine
     if key is not None:
         cache = _shared_reqs[1]

@@ -17,7 +17,6 @@ from typing import Optional
 from ..framework.interfaces import (BindPlugin, CycleState, FilterPlugin, NativeBinding, Plugin,
                                     PostFilterPlugin, PostFilterResult, QueueSortPlugin, ScorePlugin, Status)
 from ..models.labels import ANNOTATION_GPU_UUIDS, ANNOTATION_GPUS, ANNOTATION_RESERVED, ANNOTATION_VISIBLE
-from ..models.pod import PF_HOST_PORTS
 from ..models.scv import LazyScv, card_vis
 from ..ops.native import core
 
@@ -135,30 +134,48 @@ class NodeResourcesBalancedAllocation(ScorePlugin):
 
 
 class NodePorts(FilterPlugin):
-    """Host-port conflicts against pods already on the node (Python; rare on GPU nodes)."""
+    """Host-port conflicts with the pods on the node, natively (engine ``F_NODE_PORTS``: the
+    ledger keeps every reserved pod's host ports per node), so hostPort / hostNetwork pods —
+    multi-node training pods on RDMA fabrics run with ``hostNetwork: true``, which gives every
+    container port a host port — stay on the native cycle and the native lane. ``filter``
+    below is the executable spec (upstream v1.20 ``HostPortInfo.CheckConflict``), pinned by
+    ``tests/test_native_default_plugins.py``."""
     name = "NodePorts"
+    reads_flags = 0  # other pods' features this plugin reads (needs_lane_mirror): native
+
+    def native(self):
+        return NativeBinding(filter_bit=_c().F_NODE_PORTS)
 
     def filter(self, state: CycleState, pod, node_name: str) -> Status:
-        if not pod.host_ports:
+        want = host_port_set(pod.host_ports)
+        if not want:
             return Status.ok()
         cache = self.handle.cache
-        used = set()
+        used: set = set()
         for uid in cache.node_pods.get(node_name, ()):
             ps = cache.pods.get(uid)
             if ps is not None:
-                for port, proto, ip in ps.info.host_ports:
-                    used.add((port, proto))
-        for port, proto, _ip in pod.host_ports:
-            if (port, proto) in used:
+                used |= host_port_set(ps.info.host_ports)
+        any_ip = {(proto, port) for _ip, proto, port in used}
+        for ip, proto, port in want:
+            if ip == "0.0.0.0":
+                hit = (proto, port) in any_ip
+            else:
+                hit = ("0.0.0.0", proto, port) in used or (ip, proto, port) in used
+            if hit:
                 return Status.unschedulable("node(s) didn't have free ports for the requested pod ports",
                                             plugin=self.name)
         return Status.ok()
 
-    pod_flags = PF_HOST_PORTS
-    reads_flags = PF_HOST_PORTS  # other pods' features this plugin reads (needs_lane_mirror)
 
-    def is_noop_for(self, pod) -> bool:
-        return not pod.host_ports
+def host_port_set(ports) -> set:
+    """(hostIP, protocol, hostPort) of a pod's host ports as upstream HostPortInfo keeps them:
+    hostIP "" → "0.0.0.0", protocol "" → "TCP", ports <= 0 dropped."""
+    out = set()
+    for port, proto, ip in ports or ():
+        if isinstance(port, int) and not isinstance(port, bool) and 0 < port <= 0x7FFFFFFF:
+            out.add((ip or "0.0.0.0", proto or "TCP", port))
+    return out
 
 
 class _Inert(Plugin):
