@@ -926,3 +926,34 @@ def test_pods_with_inert_claims_are_lane_pods_until_a_claim_needs_a_plugin(serve
     assert lane_total == 4 and py_bound == 2  # w0 (evicted while waiting) and w1 by Python
     assert w0 == "n2" and w1 == "n2"          # the PV's node affinity, checked by VolumeBinding
     assert not never & PF_CLAIMS              # lane pods may carry claims: Python's readers see them
+
+
+def test_attach_limit_counts_lane_pods_once_their_claims_stop_being_inert():
+    """Lane pods may hold claims (inert ones). When an attach limit appears, the claims stop
+    being inert and NodeVolumeLimits applies to new CSI pods on the Python path; its count of
+    the volumes already attached on the node must include the lane's pods (PF_CLAIMS left the
+    lane's never-flags, so the cycle reads a mirror of the lane)."""
+    async def go():
+        async with Env(nodes=(("n1", 8, None),)) as e:
+            nl = e.sched.lane
+            for i in range(3):
+                await e.cl.create("persistentvolumes", _csi_pv(f"pv-{i}"))
+                await e.cl.create("persistentvolumeclaims", _bound_pvc(f"d{i}", f"pv-{i}"))
+            assert await e.wait(lambda: {"default/d0", "default/d1", "default/d2"} <= nl._claims)
+            await e.create(_claim_pod("l0", "d0"))
+            await e.create(_claim_pod("l1", "d1"))
+            assert await e.wait(lambda: e.sched.scheduled == 2)
+            on_lane = nl.lane.scheduled
+            await e.cl.create("csinodes", {"metadata": {"name": "n1"}, "spec": {"drivers": [
+                {"name": "nfs.csi.k8s.io", "nodeID": "n1", "allocatable": {"count": 2}}]}})
+            assert await e.wait(lambda: not nl._claims)
+            await e.create(_claim_pod("p2", "d2"))            # a third volume: over the limit of 2
+            await e.create(_claim_pod("p0", "d0"))            # d0 is attached already: fits
+            assert await e.wait(lambda: e.sched.scheduled == 3)
+            await asyncio.sleep(0.5)
+            pods = await e.pods()
+            return on_lane, pods["p2"]["spec"].get("nodeName", ""), pods["p0"]["spec"].get("nodeName", ""), \
+                e.sched.scheduled
+    on_lane, p2, p0, total = run(go())
+    assert on_lane == 2
+    assert p2 == "" and p0 == "n1" and total == 3
