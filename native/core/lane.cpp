@@ -19,11 +19,12 @@ constexpr uint64_t kEventTag = 1ull << 63;
 constexpr uint64_t kPatchBit = 1ull << 62;   // with kEventTag: a PodScheduled=False status patch
 
 // engine Reason → FitError text (framework/scheduler.py::_fit_error)
-const char* const kReasonName[RS_NUM] = {"OK", "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity",
+const char* const kReasonName[] = {"OK", "NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity",
                                          "NodeResourcesFit", "NoScv", "ScvStale", "GpuNumber", "GpuMemory",
                                          "GpuClock", "GpuFit", "NodeGone", "NodeResourcesFitExtended",
                                          "PodTopologySpread", "PodTopologySpreadLabel", "InterPodAffinityExisting",
-                                         "InterPodAffinity", "InterPodAntiAffinity"};
+                                         "InterPodAffinity", "InterPodAntiAffinity", "NodePorts"};
+static_assert(sizeof(kReasonName) / sizeof(kReasonName[0]) == RS_NUM, "kReasonName must name every engine Reason");
 const char* reason_text(int i) {
   switch (i) {
     case RS_UNSCHEDULABLE: return "node(s) were unschedulable";

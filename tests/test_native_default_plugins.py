@@ -558,3 +558,16 @@ def test_label_index_and_groups_follow_label_changes_deletion_and_release():
                 want = sum(1 for n, pns, lab, dying in live.values()
                            if n == node and pns == ns and not dying and ls.matches(lab))
                 assert eng.count_matching(eng.node_index(node), ns, ls.native()) == want, (sel, node, ns)
+
+
+def test_reason_names_cover_every_engine_reason():
+    """Every engine Reason has a name (FitError texts): the histogram a cycle returns is as long
+    as ``REASONS``."""
+    eng, cache = cache_with([node_obj("n0")])
+    eng.filters = C.F_NODE_PORTS
+    cache.add_pod({"metadata": {"name": "b", "namespace": "default", "uid": f"b-{next(_uid)}"},
+                   "spec": {"nodeName": "n0", "containers": [{"name": "c", "ports": _ports([(80, "", "")])}]}})
+    p = pod("p", containers=[{"name": "c", "ports": _ports([(80, "TCP", "10.0.0.1")])}])
+    feasible, reasons = eng.feasible_nodes(pod_req(eng, p), [])
+    assert feasible == [] and len(reasons) == len(C.REASONS)
+    assert reasons[C.REASONS.index("NodePorts")] == 1
