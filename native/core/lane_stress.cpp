@@ -34,7 +34,9 @@ std::string pod_json(const std::string& name, const std::string& uid, const std:
   if (!node.empty()) s += "\"nodeName\":\"" + node + "\",";
   // every pod mounts the claim "data" (inert: the profile admits it, see run_mode)
   s += "\"volumes\":[{\"name\":\"d\",\"persistentVolumeClaim\":{\"claimName\":\"data\"}}],";
-  s += "\"containers\":[{\"name\":\"main\",\"image\":\"x\",\"resources\":{\"requests\":{\"cpu\":\"100m\","
+  // and a host port of its own (NodePorts: the ledger's per-node port maps grow and drain)
+  s += "\"containers\":[{\"name\":\"main\",\"image\":\"x\",\"ports\":[{\"containerPort\":80,\"hostPort\":" +
+       std::to_string(10000 + i) + "}],\"resources\":{\"requests\":{\"cpu\":\"100m\","
        "\"memory\":\"128Mi\"}}}]},\"status\":{\"phase\":\"Pending\"}}";
   return s;
 }
@@ -98,6 +100,7 @@ int run_mode(int bursts, int per, int batch, int async_mode, int spin_us) {
     }
     e.set_cards(idx, cs, 8, 8 * 294912, 8 * 294912, false, 0);
   }
+  e.set_filters(e.filters() | F_NODE_PORTS);
   EngineConfig cfg = e.config();
   LaneOptions o;
   o.batch = batch;
