@@ -957,3 +957,77 @@ def test_attach_limit_counts_lane_pods_once_their_claims_stop_being_inert():
     on_lane, p2, p0, total = run(go())
     assert on_lane == 2
     assert p2 == "" and p0 == "n1" and total == 3
+
+
+def _mixed_pods(seed):
+    """Pods of every class the lane admits since round 5: plain, spread, anti-affinity,
+    host ports (some conflicting), inert PVC claims, ephemeral-storage requests."""
+    import random
+    rng = random.Random(seed)
+    out = []
+    for i in range(24):
+        labels = {"scv/memory": str(rng.choice([1000, 4096, 16384])), "app": rng.choice(["a", "b", "c"])}
+        if rng.random() < 0.25:
+            labels["scv/number"] = str(rng.choice([1, 2, 4]))
+        spec = {}
+        r = rng.random()
+        if r < 0.2:
+            spec["topologySpreadConstraints"] = [{"maxSkew": 1, "topologyKey": "kubernetes.io/hostname",
+                                                  "whenUnsatisfiable": rng.choice(["DoNotSchedule", "ScheduleAnyway"]),
+                                                  "labelSelector": {"matchLabels": {"app": labels["app"]}}}]
+        elif r < 0.35:
+            spec["affinity"] = {"podAntiAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+                {"weight": 50, "podAffinityTerm": {"topologyKey": "kubernetes.io/hostname",
+                                                   "labelSelector": {"matchLabels": {"app": labels["app"]}}}}]}}
+        c = {"name": "c", "image": "x", "resources": {"requests": {"cpu": "100m", "memory": "128Mi"}}}
+        if rng.random() < 0.3:
+            c["ports"] = [{"containerPort": 80, "hostPort": rng.choice([8080, 8081, 9000])}]
+        if rng.random() < 0.2:
+            c["resources"]["requests"]["ephemeral-storage"] = "1Gi"
+        spec["containers"] = [c]
+        if rng.random() < 0.3:
+            spec["volumes"] = [{"name": "d", "persistentVolumeClaim": {"claimName": rng.choice(["d0", "d1"])}}]
+        out.append(pod(f"m{i:02d}", labels, **spec))
+    return out
+
+
+def _mixed_placements(seed, lane):
+    async def go():
+        async with Env(lane=lane, nodes=(("n1", 8, None), ("n2", 8, None), ("n3", 8, None))) as e:
+            for i in range(2):
+                await e.cl.create("persistentvolumes", _csi_pv(f"pv-{i}"))
+                await e.cl.create("persistentvolumeclaims", _bound_pvc(f"d{i}", f"pv-{i}"))
+            if e.sched.lane is not None:
+                assert await e.wait(lambda: {"default/d0", "default/d1"} <= e.sched.lane._claims)
+            else:
+                await asyncio.sleep(0.3)
+            for o in _mixed_pods(seed):
+                await e.create(o)
+                name = o["metadata"]["name"]
+
+                async def settled():
+                    p = (await e.pods())[name]
+                    if p["spec"].get("nodeName"):
+                        return True
+                    return any(c.get("type") == "PodScheduled" and c.get("status") == "False"
+                               for c in (p.get("status") or {}).get("conditions") or [])
+                t0 = time.time()
+                while not await settled():
+                    assert time.time() - t0 < 10, name
+                    await asyncio.sleep(0.01)
+            pods = await e.pods()
+            admitted = e.sched.lane.lane.stats()["admitted"] if e.sched.lane else 0
+            return {n: (p["spec"].get("nodeName", ""), (p["metadata"].get("annotations") or {}).get("scv.amd.com/gpus"))
+                    for n, p in pods.items()}, admitted
+    return run(go())
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_lane_and_python_path_place_mixed_real_cluster_pods_alike(seed):
+    """One pod at a time, so both paths see the same cluster: the lane (which now admits spread,
+    affinity, host-port, extended-resource and inert-PVC pods) places every pod on the node and
+    GPUs the Python path picks, including the pods a host-port conflict leaves unschedulable."""
+    lane, admitted = _mixed_placements(seed, "on")
+    py, _ = _mixed_placements(seed, "off")
+    assert lane == py
+    assert admitted >= 20
