@@ -810,6 +810,8 @@ PYBIND11_MODULE(_yoda_core, m) {
            py::arg("preempt_above") = INT64_MIN, py::arg("gate_terms") = py::list(), py::arg("claims_ok") = false)
       .def("set_inert_claims", &Lane::set_inert_claims, py::arg("keys"),
            "PersistentVolumeClaims (namespace/name) whose pods the profiles with claims_ok may run")
+      .def("update_inert_claims", &Lane::update_inert_claims, py::arg("add"), py::arg("remove"),
+           "add / remove claims of the inert set")
       .def("set_gates",
            [](Lane& l, const std::string& name, const py::list& gate_terms) {
              std::vector<MatchTerm> v;

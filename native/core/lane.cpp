@@ -294,11 +294,27 @@ bool Lane::set_gates(const std::string& name, std::vector<MatchTerm> terms) {
 }
 
 void Lane::set_inert_claims(std::vector<std::string> keys) {
+  ClaimOp op;
+  op.reset = true;
+  op.add = std::move(keys);
   {
     std::lock_guard<std::mutex> g(prof_mu_);
-    claims_staged_.clear();
-    for (auto& k : keys) claims_staged_.insert(std::move(k));
-    claims_fresh_ = true;
+    claim_ops_.push_back(std::move(op));
+  }
+  std::lock_guard<std::mutex> g(in_mu_);
+  Item it;
+  it.k = Item::kClaims;
+  push_locked(std::move(it));
+  in_cv_.notify_one();
+}
+
+void Lane::update_inert_claims(std::vector<std::string> add, std::vector<std::string> remove) {
+  ClaimOp op;
+  op.add = std::move(add);
+  op.remove = std::move(remove);
+  {
+    std::lock_guard<std::mutex> g(prof_mu_);
+    claim_ops_.push_back(std::move(op));
   }
   std::lock_guard<std::mutex> g(in_mu_);
   Item it;
@@ -820,17 +836,27 @@ bool Lane::claims_inert(const yk::PodProj& p) const {
 // A new inert-claims set: waiting pods that mount a claim which left it go to Python (a claim
 // that joined the set cannot make a pod inadmissible; pods Python holds stay there).
 void Lane::apply_claims(std::vector<Fwd>* out) {
-  std::unordered_set<std::string> next;
+  std::vector<ClaimOp> ops;
   {
     std::lock_guard<std::mutex> g(prof_mu_);
-    if (!claims_fresh_) return;               // an earlier kClaims already took the latest set
-    claims_fresh_ = false;
-    next.swap(claims_staged_);
+    ops.swap(claim_ops_);                   // an earlier kClaims may have taken them already
   }
-  std::unordered_set<std::string> removed;
-  for (const auto& k : inert_)
-    if (!next.count(k)) removed.insert(k);
-  inert_.swap(next);
+  if (ops.empty()) return;
+  std::unordered_set<std::string> removed;  // left the set at some op (re-added ones filtered below)
+  for (auto& op : ops) {
+    if (op.reset) {
+      std::unordered_set<std::string> next(std::make_move_iterator(op.add.begin()),
+                                           std::make_move_iterator(op.add.end()));
+      for (const auto& k : inert_)
+        if (!next.count(k)) removed.insert(k);
+      inert_.swap(next);
+      continue;
+    }
+    for (auto& k : op.remove)
+      if (inert_.erase(k)) removed.insert(std::move(k));
+    for (auto& k : op.add) inert_.insert(std::move(k));
+  }
+  for (auto it = removed.begin(); it != removed.end();) it = inert_.count(*it) ? removed.erase(it) : std::next(it);
   if (removed.empty()) return;
   std::vector<Entry*> evict;
   std::string key;

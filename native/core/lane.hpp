@@ -175,6 +175,8 @@ class Lane : public yk::PodSink {
   // the PersistentVolumeClaims ("namespace/name") the volume plugins have nothing to check for;
   // waiting pods mounting a claim that left the set go to Python
   void set_inert_claims(std::vector<std::string> keys);
+  // the same set changed by a few claims (a PVC / PV event): O(change), not O(claims)
+  void update_inert_claims(std::vector<std::string> add, std::vector<std::string> remove);
   void set_active(bool on);                    // leader: schedule; otherwise only keep the store
   void set_node_cards(const std::string& node, std::vector<std::pair<std::string, std::string>> vis);
   void remove_node_cards(const std::string& node);
@@ -422,9 +424,13 @@ class Lane : public yk::PodSink {
   // inadmissible); taken by the lane thread on kGates (prof_mu_)
   std::vector<std::pair<std::string, std::vector<MatchTerm>>> gate_adds_;
   std::vector<Profile> lp_;          // lane thread's view
-  // set_inert_claims: the latest set, taken by the lane thread on kClaims (prof_mu_)
-  bool claims_fresh_ = false;
-  std::unordered_set<std::string> claims_staged_;
+  // set_inert_claims / update_inert_claims, in call order; taken by the lane thread on kClaims
+  // (prof_mu_)
+  struct ClaimOp {
+    bool reset = false;                     // `add` is the whole set
+    std::vector<std::string> add, remove;
+  };
+  std::vector<ClaimOp> claim_ops_;
   std::unordered_set<std::string> inert_;   // lane thread's view
   bool claims_inert(const yk::PodProj& p) const;
   void apply_claims(std::vector<Fwd>* out);

@@ -157,7 +157,8 @@ int run_mode(int bursts, int per, int batch, int async_mode, int spin_us) {
   // the lane thread's kClaims apply); "default/data" stays in it, so every pod stays admissible
   std::thread churn([&] {
     for (int k = 0; !stop.load(); ++k) {
-      lane.set_inert_claims({"default/data", "default/x" + std::to_string(k % 4)});
+      if (k % 2) lane.set_inert_claims({"default/data", "default/x" + std::to_string(k % 4)});
+      else lane.update_inert_claims({"default/y" + std::to_string(k % 3)}, {"default/y" + std::to_string((k + 1) % 3)});
       std::this_thread::sleep_for(std::chrono::microseconds(200));
     }
   });

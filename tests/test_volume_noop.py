@@ -217,3 +217,64 @@ def test_bench_pvc_workload_mounts_bound_claims():
     assert all(("persistentvolumeclaims", m) in made for m in mounts)
     pvs = {o["metadata"]["name"]: o for res, o in w.objects if res == "persistentvolumes"}
     assert all(o["spec"]["volumeName"] in pvs for res, o in w.objects if res == "persistentvolumeclaims")
+
+
+def test_incremental_inert_claims_equal_a_full_recompute():
+    """``InertClaims`` (per-event updates for the lane) ≡ ``inert_claims`` recomputed over every
+    PVC, after each of a random sequence of PVC / PV / CSINode / node-limit changes."""
+    import collections
+    import random
+    from types import SimpleNamespace
+
+    from yoda_scheduler_amd.plugins.volumes import InertClaims, inert_claims
+
+    class H:
+        def __init__(self):
+            self.objs = {"persistentvolumeclaims": {}, "persistentvolumes": {}, "csinodes": {}}
+            self.gen = collections.Counter()
+            self.cache = SimpleNamespace(csi_limit_nodes=0)
+
+        def lister(self, res):
+            return self.objs[res]
+
+        def generation(self, res):
+            return self.gen[res]
+
+    adds = removes = 0
+    for seed in range(40):
+        rng = random.Random(seed)
+        h = H()
+        t = InertClaims(h)
+        for _step in range(60):
+            op = rng.random()
+            if op < 0.4:
+                name = f"c{rng.randrange(6)}"
+                key = f"default/{name}"
+                if rng.random() < 0.2 and key in h.objs["persistentvolumeclaims"]:
+                    obj = h.objs["persistentvolumeclaims"].pop(key)
+                else:
+                    obj = _pvc(name, rng.choice(["", "pv0", "pv1", "pv2", "pv9"]), deleting=rng.random() < 0.1)
+                    h.objs["persistentvolumeclaims"][key] = obj
+                t.pvc_event(obj)
+            elif op < 0.8:
+                name = f"pv{rng.randrange(3)}"
+                if rng.random() < 0.2 and name in h.objs["persistentvolumes"]:
+                    obj = h.objs["persistentvolumes"].pop(name)
+                else:
+                    obj = _pv(name, host=rng.choice([None, None, "n1"]), zone=rng.choice([None, None, "z1"]),
+                              csi=rng.random() < 0.7, ebs=rng.random() < 0.1)
+                    h.objs["persistentvolumes"][name] = obj
+                t.pv_event(obj)
+            elif op < 0.9:
+                h.gen["csinodes"] += 1
+                h.objs["csinodes"] = {} if rng.random() < 0.5 else {"n0": {"metadata": {"name": "n0"}, "spec": {
+                    "drivers": [{"name": "d", "allocatable": {"count": 4}}]}}}
+            else:
+                h.cache.csi_limit_nodes = rng.choice([0, 0, 1])
+            before = set(t.keys)
+            full, added, removed = t.refresh()
+            assert t.keys == inert_claims(h), (seed, _step)
+            if full is None:
+                assert before | added == t.keys | removed and not (added & removed)
+            adds, removes = adds + len(added), removes + len(removed)
+    assert adds > 20 and removes > 20             # the sequences move claims both ways

@@ -69,8 +69,8 @@ class NativeLane:
         self._in_gated = False             # inside gated(): anti-affinity changes wait for its exit
         self._gates_pending = False        # a coalesced gate update (holder removals) is scheduled
         self._sticky_never = (1 << 62) - 1  # AND of the masks of profiles eligible since the lane last owned nothing
-        self._claims_key: Optional[tuple] = None   # listers' generations the inert-claims set was computed at
-        self._claims: frozenset = frozenset()     # the set the lane holds (plugins/volumes.py::inert_claims)
+        self._inert = None                 # plugins/volumes.py::InertClaims, made on first use
+        self._claims: set = set()          # the inert claims the lane holds
         sched.queue.on_move_all = self._move_all
 
     # ------------------------------------------------------------------ lifecycle
@@ -174,26 +174,32 @@ class NativeLane:
             log.info("native lane: profile %s %s (flag mask %#x)", name, "on" if want[0] else "off", want[1])
         s.cache.lane_never_flags = never & self._sticky_never
 
-    def _refresh_claims(self) -> frozenset:
-        """Send the lane the claims a pod may mount and still take the native cycle
-        (plugins/volumes.py::inert_claims) when the objects they derive from changed: the PVC,
-        PV, StorageClass and CSINode listers (their generations) and whether a node has a CSI
-        attach limit. Only profiles whose volume plugins all allow it (``claims_ok``) use it."""
+    def claims_event(self, res: str, obj: dict) -> None:
+        """A PVC / PV changed: its claims are re-tested on the next refresh (O(change))."""
+        if self._inert is None:
+            return
+        if res == "persistentvolumeclaims":
+            self._inert.pvc_event(obj)
+        elif res == "persistentvolumes":
+            self._inert.pv_event(obj)
+
+    def _refresh_claims(self) -> set:
+        """Keep the lane's set of inert claims (plugins/volumes.py::InertClaims) current: the
+        claims a pod may mount and still take the native cycle. Only profiles whose volume
+        plugins all allow it (``claims_ok``) use it; changes go to the lane as deltas."""
         s = self.s
         if not any(fw.claims_ok() for fw in s.frameworks.values()):
             return self._claims
-        gen = s.handle.generation
-        key = (gen("persistentvolumeclaims"), gen("persistentvolumes"), gen("storageclasses"), gen("csinodes"),
-               s.cache.csi_limit_nodes > 0)
-        if key == self._claims_key:
-            return self._claims
-        from ..plugins.volumes import inert_claims
-        self._claims_key = key
-        new = frozenset(inert_claims(s.handle))
-        if new != self._claims:
-            self._claims = new
-            self.lane.set_inert_claims(sorted(new))
-        return new
+        if self._inert is None:
+            from ..plugins.volumes import InertClaims
+            self._inert = InertClaims(s.handle)
+        full, added, removed = self._inert.refresh()
+        if full is not None:
+            self.lane.set_inert_claims(sorted(full))
+        elif added or removed:
+            self.lane.update_inert_claims(sorted(added), sorted(removed))
+        self._claims = self._inert.keys
+        return self._claims
 
     def anti_changed(self, grew: bool = True) -> None:
         """The bound/assumed pods with required anti-affinity changed. A new holder's terms reach

@@ -612,14 +612,16 @@ class Scheduler:
                     lambda o, ev=ev, res=res: self._spread_source(res, o, True, None))
                 continue
             self.informers[res] = Informer(self.client, res,
-                                           lambda o, ev=ev, res=res: self._extra_event(ev, res),
-                                           lambda a, b, ev=ev, res=res: self._extra_event(ev, res),
-                                           lambda o, res=res: self._extra_event(None, res))
+                                           lambda o, ev=ev, res=res: self._extra_event(ev, res, o),
+                                           lambda a, b, ev=ev, res=res: self._extra_event(ev, res, b),
+                                           lambda o, res=res: self._extra_event(None, res, o))
         return self.informers
 
-    def _extra_event(self, ev: Optional[str], res: str = "") -> None:
+    def _extra_event(self, ev: Optional[str], res: str = "", obj: Optional[dict] = None) -> None:
         if res:
             self.extra_generation[res] += 1
+            if obj is not None and self.lane is not None:
+                self.lane.claims_event(res, obj)
         if ev is not None:
             self.queue.move_all_to_active_or_backoff(ev)
         self._lane_refresh()

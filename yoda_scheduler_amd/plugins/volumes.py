@@ -611,37 +611,114 @@ def _csinode_counts(csinodes: dict) -> bool:
                for cn in csinodes.values() for d in ((cn.get("spec") or _EMPTY).get("drivers") or ()))
 
 
-def inert_claims(handle) -> set:
-    """The PersistentVolumeClaims ("namespace/name") every volume plugin has nothing to check
-    for: not being deleted, bound to a PV that exists and has no required node affinity, no
-    zone / region labels and no in-tree attachable disk, and either not a CSI volume or no
-    attach limit anywhere in the cluster. A pod whose claims are all in this set is a no-op for
+def claim_inert(pvc: dict, pvs: dict, limits: bool) -> bool:
+    """One PersistentVolumeClaim every volume plugin has nothing to check for: not being
+    deleted, bound to a PV that exists and has no required node affinity, no zone / region
+    labels and no in-tree attachable disk, and either not a CSI volume or no attach limit
+    anywhere in the cluster (``limits``). A pod whose claims are all inert is a no-op for
     VolumeBinding, VolumeZone, NodeVolumeLimits and the in-tree limits (each claim satisfies
     the per-claim half of their ``is_noop_for``), so the native lane may run it."""
-    pvcs, pvs = handle.lister("persistentvolumeclaims"), handle.lister("persistentvolumes")
-    limits = None
-    out = set()
-    for key, pvc in pvcs.items():
-        if (pvc.get("metadata") or _EMPTY).get("deletionTimestamp"):
-            continue
-        name = (pvc.get("spec") or _EMPTY).get("volumeName", "")
-        pv = pvs.get(name) if name else None
-        if pv is None:
-            continue
-        ps = pv.get("spec") or _EMPTY
-        if (ps.get("nodeAffinity") or _EMPTY).get("required") is not None:
-            continue
-        labels = (pv.get("metadata") or _EMPTY).get("labels") or _EMPTY
-        if any(k in labels for k in ZONE_LABELS) or any(ps.get(k) for k in _ATTACHABLE_KINDS):
-            continue
-        if ps.get("csi"):
-            if limits is None:
-                limits = getattr(handle.cache, "csi_limit_nodes", 1) > 0 or \
-                    _csinode_counts(handle.lister("csinodes"))
-            if limits:
-                continue
-        out.add(key)
-    return out
+    if (pvc.get("metadata") or _EMPTY).get("deletionTimestamp"):
+        return False
+    name = (pvc.get("spec") or _EMPTY).get("volumeName", "")
+    pv = pvs.get(name) if name else None
+    if pv is None:
+        return False
+    ps = pv.get("spec") or _EMPTY
+    if (ps.get("nodeAffinity") or _EMPTY).get("required") is not None:
+        return False
+    labels = (pv.get("metadata") or _EMPTY).get("labels") or _EMPTY
+    if any(k in labels for k in ZONE_LABELS) or any(ps.get(k) for k in _ATTACHABLE_KINDS):
+        return False
+    return not (ps.get("csi") and limits)
+
+
+def attach_limits(handle) -> bool:
+    """Some node has a CSI attach limit (node allocatable ``attachable-volumes-csi-*`` or a
+    CSINode ``allocatable.count``): NodeVolumeLimits counts CSI volumes then."""
+    return getattr(handle.cache, "csi_limit_nodes", 1) > 0 or _csinode_counts(handle.lister("csinodes"))
+
+
+def inert_claims(handle) -> set:
+    """Every inert claim ("namespace/name", ``claim_inert``) of the PVC lister."""
+    pvs, limits = handle.lister("persistentvolumes"), attach_limits(handle)
+    return {key for key, pvc in handle.lister("persistentvolumeclaims").items() if claim_inert(pvc, pvs, limits)}
+
+
+class InertClaims:
+    """``inert_claims`` kept up to date per event instead of recomputed over every PVC: a PVC
+    event re-tests that claim, a PV event the claims bound to it (an index PV name → claim
+    keys), and a change of the cluster's attach limits (CSINode counts, node allocatable)
+    re-tests all. ``refresh`` returns (full set | None, added, removed) since the last call."""
+
+    def __init__(self, handle) -> None:
+        self.handle = handle
+        self.keys: set = set()
+        self._pv_of: dict[str, str] = {}          # claim key → the PV name it is bound to
+        self._claims_of: dict[str, set] = {}      # PV name → claim keys bound to it
+        self._dirty: set = set()
+        self._all = True                          # first refresh: every claim
+        self._limits: Optional[bool] = None
+        self._csinode_gen = -1
+        self._csinode_counts = False
+
+    def pvc_event(self, obj: dict) -> None:
+        m = obj.get("metadata") or _EMPTY
+        self._dirty.add(f"{m.get('namespace') or 'default'}/{m.get('name', '')}")
+
+    def pv_event(self, obj: dict) -> None:
+        self._dirty |= self._claims_of.get((obj.get("metadata") or _EMPTY).get("name", ""), set())
+
+    def _index(self, key: str, pv: str) -> None:
+        old = self._pv_of.get(key)
+        if old == pv:
+            return
+        if old is not None:
+            ks = self._claims_of.get(old)
+            if ks is not None:
+                ks.discard(key)
+                if not ks:
+                    del self._claims_of[old]
+        if pv:
+            self._pv_of[key] = pv
+            self._claims_of.setdefault(pv, set()).add(key)
+        else:
+            self._pv_of.pop(key, None)
+
+    def refresh(self):
+        h = self.handle
+        gen = h.generation("csinodes") if hasattr(h, "generation") else -2
+        if gen != self._csinode_gen or gen == -2:
+            self._csinode_gen = gen
+            self._csinode_counts = _csinode_counts(h.lister("csinodes"))
+        limits = getattr(h.cache, "csi_limit_nodes", 1) > 0 or self._csinode_counts
+        if limits != self._limits:
+            self._limits, self._all = limits, True
+        pvcs, pvs = h.lister("persistentvolumeclaims"), h.lister("persistentvolumes")
+        if self._all:
+            self._all, self._dirty = False, set()
+            self._pv_of, self._claims_of = {}, {}
+            keys = set()
+            for key, pvc in pvcs.items():
+                self._index(key, (pvc.get("spec") or _EMPTY).get("volumeName", "") or "")
+                if claim_inert(pvc, pvs, limits):
+                    keys.add(key)
+            added, removed = keys - self.keys, self.keys - keys
+            self.keys = keys
+            return keys, added, removed
+        added, removed = set(), set()
+        dirty, self._dirty = self._dirty, set()
+        for key in dirty:
+            pvc = pvcs.get(key)
+            self._index(key, ((pvc.get("spec") or _EMPTY).get("volumeName", "") or "") if pvc is not None else "")
+            inert = pvc is not None and claim_inert(pvc, pvs, limits)
+            if inert and key not in self.keys:
+                self.keys.add(key)
+                added.add(key)
+            elif not inert and key in self.keys:
+                self.keys.discard(key)
+                removed.add(key)
+        return None, added, removed
 
 
 # the in-tree attach-limit plugins' volume kinds (what _VolFacts resolves for them)
