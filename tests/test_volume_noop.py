@@ -77,6 +77,9 @@ def _cluster(limits: str = ""):
     if limits == "csinode":
         c.server.create("csinodes", {"metadata": {"name": "n0"}, "spec": {"drivers": [
             {"name": "nfs.csi.k8s.io", "nodeID": "n0", "allocatable": {"count": 8}}]}})
+    elif limits == "other":        # a limit for another CSI driver only
+        c.server.create("csinodes", {"metadata": {"name": "n0"}, "spec": {"drivers": [
+            {"name": "ebs.csi.aws.com", "nodeID": "n0", "allocatable": {"count": 25}}]}})
     elif limits == "node":
         node = c.server.get("nodes", "n1")
         alloc = dict(node["status"]["allocatable"], **{"attachable-volumes-csi-nfs.csi.k8s.io": "8"})
@@ -108,7 +111,7 @@ def test_bound_claim_pods_take_the_native_cycle_and_bind():
 def test_each_volume_feature_moves_the_pod_back_to_its_plugin():
     async def go():
         out = {}
-        for limits in ("", "csinode", "node"):
+        for limits in ("", "csinode", "node", "other"):
             c = _cluster(limits)
             await c.start()
             fw = c.sched.frameworks["yoda-scheduler"]
@@ -133,6 +136,8 @@ def test_each_volume_feature_moves_the_pod_back_to_its_plugin():
     for limits in ("csinode", "node"):
         assert out[(limits, "plain")] == ({"NodeVolumeLimits"}, False), limits
         assert "NodeVolumeLimits" not in out[(limits, "ebs")][0]       # not a CSI volume
+    # a limit for another driver leaves the NFS claim's pod native (limits are per driver)
+    assert out[("other", "plain")] == (set(), True)
 
 
 def test_noop_answer_is_exact_against_the_plugins_own_prefilter_and_filter():
@@ -145,7 +150,7 @@ def test_noop_answer_is_exact_against_the_plugins_own_prefilter_and_filter():
     async def go():
         seen_noop = seen_applies = 0
         bad = []
-        for limits in ("", "csinode", "node"):
+        for limits in ("", "csinode", "node", "other"):
             c = _cluster(limits)
             await c.start()
             fw = c.sched.frameworks["yoda-scheduler"]
@@ -232,7 +237,7 @@ def test_incremental_inert_claims_equal_a_full_recompute():
         def __init__(self):
             self.objs = {"persistentvolumeclaims": {}, "persistentvolumes": {}, "csinodes": {}}
             self.gen = collections.Counter()
-            self.cache = SimpleNamespace(csi_limit_nodes=0)
+            self.cache = SimpleNamespace(csi_limit_drivers={})
 
         def lister(self, res):
             return self.objs[res]
@@ -268,9 +273,10 @@ def test_incremental_inert_claims_equal_a_full_recompute():
             elif op < 0.9:
                 h.gen["csinodes"] += 1
                 h.objs["csinodes"] = {} if rng.random() < 0.5 else {"n0": {"metadata": {"name": "n0"}, "spec": {
-                    "drivers": [{"name": "d", "allocatable": {"count": 4}}]}}}
+                    "drivers": [{"name": rng.choice(["nfs.csi.k8s.io", "ebs.csi.aws.com"]),
+                                 "allocatable": {"count": 4}}]}}}
             else:
-                h.cache.csi_limit_nodes = rng.choice([0, 0, 1])
+                h.cache.csi_limit_drivers = rng.choice([{}, {}, {"nfs.csi.k8s.io": 1}, {"ebs.csi.aws.com": 2}])
             before = set(t.keys)
             full, added, removed = t.refresh()
             assert t.keys == inert_claims(h), (seed, _step)

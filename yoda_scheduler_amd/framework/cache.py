@@ -35,9 +35,13 @@ class PodState:
     lane: bool = False                    # mirrored from the native lane (it owns the reservation)
 
 
-def _csi_attach_limits(obj: dict) -> bool:
+_CSI_ALLOC = "attachable-volumes-csi-"
+
+
+def _csi_attach_limits(obj: dict) -> list:
+    """CSI drivers the node's allocatable limits (``attachable-volumes-csi-<driver>``)."""
     alloc = (obj.get("status") or {}).get("allocatable") or {}
-    return any(k.startswith("attachable-volumes-csi-") for k in alloc)
+    return [k[len(_CSI_ALLOC):] for k in alloc if k.startswith(_CSI_ALLOC)]
 
 
 class SchedulerCache:
@@ -60,7 +64,8 @@ class SchedulerCache:
         self._anti_parsed: dict[str, list] = {}     # uid → [(topologyKey, namespaces, LabelSelector)]
         self.image_nodes: dict[str, int] = {}    # image → number of nodes holding it (ImageLocality)
         self.avoid_nodes: set[str] = set()       # nodes with a preferAvoidPods annotation
-        self.csi_limit_nodes = 0                 # nodes whose allocatable has attachable-volumes-csi-* (NodeVolumeLimits)
+        # CSI driver → nodes whose allocatable limits it (attachable-volumes-csi-<driver>; NodeVolumeLimits)
+        self.csi_limit_drivers: dict[str, int] = {}
         self.node_ext_used: dict[str, dict[str, int]] = {}   # node → extended resource → requested
         self.generation = 0
         self.node_generation = 0                 # node add/remove only (engine index → name stays valid)
@@ -79,8 +84,12 @@ class SchedulerCache:
                 self.image_nodes[im] = c
             else:
                 self.image_nodes.pop(im, None)
-        if _csi_attach_limits(info.obj):
-            self.csi_limit_nodes += sign
+        for d in _csi_attach_limits(info.obj):
+            c = self.csi_limit_drivers.get(d, 0) + sign
+            if c > 0:
+                self.csi_limit_drivers[d] = c
+            else:
+                self.csi_limit_drivers.pop(d, None)
         if sign > 0 and info.avoid:
             self.avoid_nodes.add(info.name)
         elif sign < 0:

@@ -75,8 +75,8 @@ class _VolFacts:
       names a PV that exists; None otherwise;
     * ``inline`` — the attachable-disk kinds among the pod's inline volumes;
     * ``pv_kinds`` — the attachable-disk kinds of the PVs its PVC volumes are bound to;
-    * ``csi`` — a PVC volume counts against a CSI attach limit (bound to a CSI PV, or
-      unbound with a provisioning StorageClass) — NodeVolumeLimits' own rule."""
+    * ``csi`` — the CSI drivers whose attach limit its PVC volumes count against (a bound
+      CSI PV's driver, an unbound claim's provisioner) — NodeVolumeLimits' own rule."""
     __slots__ = ("claims", "bound", "inline", "pv_kinds", "csi")
 
     def __init__(self, plugin: "_VolumeBase", pod) -> None:
@@ -84,7 +84,7 @@ class _VolFacts:
         self.claims = _claim_names(pod)
         self.inline = {k for v in vols for k in _ATTACHABLE_KINDS if k in v}
         self.pv_kinds: set = set()
-        self.csi = False
+        self.csi: set = set()
         for v in vols:
             if "persistentVolumeClaim" not in v:
                 continue
@@ -95,13 +95,14 @@ class _VolFacts:
             pv = plugin._pv(spec.get("volumeName", ""))
             if pv is not None:
                 ps = pv.get("spec") or _EMPTY
-                if ps.get("csi"):
-                    self.csi = True
+                csi = ps.get("csi")
+                if csi:
+                    self.csi.add(csi.get("driver", ""))
                 self.pv_kinds.update(k for k in _ATTACHABLE_KINDS if ps.get(k))
                 continue
             sc = plugin._sc(spec.get("storageClassName", ""))
             if sc is not None and sc.get("provisioner", NO_PROVISIONER) != NO_PROVISIONER:
-                self.csi = True
+                self.csi.add(sc["provisioner"])
         self.bound = plugin._bound_claims(pod, self.claims) if self.claims else []
 
 
@@ -495,23 +496,21 @@ class NodeVolumeLimits(_LimitsBase):
 
     def __init__(self, args=None, handle=None) -> None:
         super().__init__(args, handle)
-        self._csinode_limits = (-1, False)     # (csinodes generation, any CSINode reports a count)
+        self._csinode_limits = (-1, frozenset())   # (csinodes generation, drivers a CSINode limits)
 
     def is_noop_for(self, pod) -> bool:
-        # no claims, no claim counted against a CSI limit, or no attach limit on any node
-        # (the filter returns before counting)
+        # no claims, or none of the CSI drivers its claims count against has an attach limit on
+        # any node (the filter only compares drivers with a limit)
         f = self._facts(pod)
-        return not f.claims or not f.csi or not self._any_limits()
+        return not f.claims or not f.csi or not (f.csi & self._limited_drivers())
 
-    def _any_limits(self) -> bool:
-        if getattr(self.handle.cache, "csi_limit_nodes", 1) > 0:
-            return True
+    def _limited_drivers(self) -> set:
         gen = self.handle.generation("csinodes") if hasattr(self.handle, "generation") else -2
-        g, any_count = self._csinode_limits
+        g, drivers = self._csinode_limits
         if g != gen or gen == -2:
-            any_count = _csinode_counts(self._lister("csinodes"))
-            self._csinode_limits = (gen, any_count)
-        return any_count
+            drivers = frozenset(_csinode_drivers(self._lister("csinodes")))
+            self._csinode_limits = (gen, drivers)
+        return drivers | set(getattr(self.handle.cache, "csi_limit_drivers", ()))
 
     def _pod_ids(self, ns: str, spec: dict) -> dict[str, set[str]]:
         out: dict[str, set[str]] = {}
@@ -605,17 +604,17 @@ class CinderLimits(_InTreeLimits):
     kind, id_field, alloc_key, default_max = "cinder", "volumeID", "attachable-volumes-cinder", 256
 
 
-def _csinode_counts(csinodes: dict) -> bool:
-    """Some CSINode reports an attach limit (``drivers[].allocatable.count``)."""
-    return any((d.get("allocatable") or _EMPTY).get("count") is not None
-               for cn in csinodes.values() for d in ((cn.get("spec") or _EMPTY).get("drivers") or ()))
+def _csinode_drivers(csinodes: dict) -> set:
+    """CSI drivers some CSINode reports an attach limit for (``drivers[].allocatable.count``)."""
+    return {d.get("name", "") for cn in csinodes.values() for d in ((cn.get("spec") or _EMPTY).get("drivers") or ())
+            if (d.get("allocatable") or _EMPTY).get("count") is not None}
 
 
-def claim_inert(pvc: dict, pvs: dict, limits: bool) -> bool:
+def claim_inert(pvc: dict, pvs: dict, limited: set) -> bool:
     """One PersistentVolumeClaim every volume plugin has nothing to check for: not being
     deleted, bound to a PV that exists and has no required node affinity, no zone / region
-    labels and no in-tree attachable disk, and either not a CSI volume or no attach limit
-    anywhere in the cluster (``limits``). A pod whose claims are all inert is a no-op for
+    labels and no in-tree attachable disk, and either not a CSI volume or one whose driver has
+    no attach limit on any node (``limited``: the drivers that have one). A pod whose claims are all inert is a no-op for
     VolumeBinding, VolumeZone, NodeVolumeLimits and the in-tree limits (each claim satisfies
     the per-claim half of their ``is_noop_for``), so the native lane may run it."""
     if (pvc.get("metadata") or _EMPTY).get("deletionTimestamp"):
@@ -630,19 +629,20 @@ def claim_inert(pvc: dict, pvs: dict, limits: bool) -> bool:
     labels = (pv.get("metadata") or _EMPTY).get("labels") or _EMPTY
     if any(k in labels for k in ZONE_LABELS) or any(ps.get(k) for k in _ATTACHABLE_KINDS):
         return False
-    return not (ps.get("csi") and limits)
+    csi = ps.get("csi")
+    return not (csi and csi.get("driver", "") in limited)
 
 
-def attach_limits(handle) -> bool:
-    """Some node has a CSI attach limit (node allocatable ``attachable-volumes-csi-*`` or a
-    CSINode ``allocatable.count``): NodeVolumeLimits counts CSI volumes then."""
-    return getattr(handle.cache, "csi_limit_nodes", 1) > 0 or _csinode_counts(handle.lister("csinodes"))
+def limited_drivers(handle) -> set:
+    """CSI drivers some node limits (node allocatable ``attachable-volumes-csi-<driver>`` or a
+    CSINode ``allocatable.count``): NodeVolumeLimits counts those drivers' volumes."""
+    return _csinode_drivers(handle.lister("csinodes")) | set(getattr(handle.cache, "csi_limit_drivers", ()))
 
 
 def inert_claims(handle) -> set:
     """Every inert claim ("namespace/name", ``claim_inert``) of the PVC lister."""
-    pvs, limits = handle.lister("persistentvolumes"), attach_limits(handle)
-    return {key for key, pvc in handle.lister("persistentvolumeclaims").items() if claim_inert(pvc, pvs, limits)}
+    pvs, limited = handle.lister("persistentvolumes"), limited_drivers(handle)
+    return {key for key, pvc in handle.lister("persistentvolumeclaims").items() if claim_inert(pvc, pvs, limited)}
 
 
 class InertClaims:
@@ -658,9 +658,9 @@ class InertClaims:
         self._claims_of: dict[str, set] = {}      # PV name → claim keys bound to it
         self._dirty: set = set()
         self._all = True                          # first refresh: every claim
-        self._limits: Optional[bool] = None
+        self._limited: Optional[frozenset] = None
         self._csinode_gen = -1
-        self._csinode_counts = False
+        self._csinode_drivers: set = set()
 
     def pvc_event(self, obj: dict) -> None:
         m = obj.get("metadata") or _EMPTY
@@ -690,10 +690,10 @@ class InertClaims:
         gen = h.generation("csinodes") if hasattr(h, "generation") else -2
         if gen != self._csinode_gen or gen == -2:
             self._csinode_gen = gen
-            self._csinode_counts = _csinode_counts(h.lister("csinodes"))
-        limits = getattr(h.cache, "csi_limit_nodes", 1) > 0 or self._csinode_counts
-        if limits != self._limits:
-            self._limits, self._all = limits, True
+            self._csinode_drivers = _csinode_drivers(h.lister("csinodes"))
+        limits = frozenset(self._csinode_drivers | set(getattr(h.cache, "csi_limit_drivers", ())))
+        if limits != self._limited:
+            self._limited, self._all = limits, True
         pvcs, pvs = h.lister("persistentvolumeclaims"), h.lister("persistentvolumes")
         if self._all:
             self._all, self._dirty = False, set()
