@@ -322,7 +322,8 @@ PYBIND11_MODULE(_yoda_core, m) {
                                      "NodeResourcesFit", "NoScv", "ScvStale", "GpuNumber", "GpuMemory",
                                      "GpuClock", "GpuFit", "NodeGone", "NodeResourcesFitExtended",
                                      "PodTopologySpread", "PodTopologySpreadLabel", "InterPodAffinityExisting",
-                                     "InterPodAffinity", "InterPodAntiAffinity", "NodePorts");
+                                     "InterPodAffinity", "InterPodAntiAffinity", "NodePorts", "VolumeBinding",
+                                     "VolumeZone");
 
   py::class_<PodReq>(m, "PodReq")
       .def_readonly("has_number", &PodReq::has_number)
@@ -791,10 +792,12 @@ PYBIND11_MODULE(_yoda_core, m) {
       // the profile's engine configuration is the engine's current one (the caller applied it)
       .def("set_profile",
            [](Lane& l, Engine& e, const std::string& name, bool enabled, int flag_mask, bool annotate,
-              int64_t preempt_above, const py::list& gate_terms, bool claims_ok) {
+              int64_t preempt_above, const py::list& gate_terms, bool claims_ok, bool vol_node, bool vol_zone) {
              Lane::Profile p;
              p.preempt_above = preempt_above;
              p.claims_ok = claims_ok;
+             p.vol_node = vol_node;
+             p.vol_zone = vol_zone;
              for (auto t : gate_terms) p.gate_terms.push_back(match_term(t));
              p.name = name;
              p.enabled = enabled;
@@ -807,7 +810,35 @@ PYBIND11_MODULE(_yoda_core, m) {
              l.set_profile(p);
            },
            py::arg("engine"), py::arg("name"), py::arg("enabled"), py::arg("flag_mask"), py::arg("annotate"),
-           py::arg("preempt_above") = INT64_MIN, py::arg("gate_terms") = py::list(), py::arg("claims_ok") = false)
+           py::arg("preempt_above") = INT64_MIN, py::arg("gate_terms") = py::list(), py::arg("claims_ok") = false,
+           py::arg("vol_node") = false, py::arg("vol_zone") = false)
+      // [(key, node terms | None, zone terms | None)], each terms [[(key, op, [values])]]
+      .def("update_claims",
+           [](Lane& l, Engine& e, bool reset, const py::list& add, const std::vector<std::string>& remove) {
+             std::vector<std::pair<std::string, Lane::ClaimConsP>> a;
+             {
+               EngineGuard g;                  // interning
+               for (auto item : add) {
+                 auto t = item.cast<py::tuple>();
+                 Lane::ClaimConsP cons;
+                 if (!t[1].is_none() || !t[2].is_none()) {
+                   auto c = std::make_shared<Lane::ClaimCons>();
+                   if (!t[1].is_none()) {
+                     c->has_node = true;
+                     for (auto term : t[1]) c->node.push_back(make_term(e, term.cast<py::list>()));
+                   }
+                   if (!t[2].is_none()) {
+                     c->has_zone = true;
+                     for (auto term : t[2]) c->zone.push_back(make_term(e, term.cast<py::list>()));
+                   }
+                   cons = std::move(c);
+                 }
+                 a.emplace_back(t[0].cast<std::string>(), std::move(cons));
+               }
+             }
+             l.update_claims(reset, std::move(a), remove);
+           },
+           py::arg("engine"), py::arg("reset"), py::arg("add"), py::arg("remove"))
       .def("set_inert_claims", &Lane::set_inert_claims, py::arg("keys"),
            "PersistentVolumeClaims (namespace/name) whose pods the profiles with claims_ok may run")
       .def("update_inert_claims", &Lane::update_inert_claims, py::arg("add"), py::arg("remove"),

@@ -568,7 +568,22 @@ Reason Engine::filter_node_pf(const PodReq& req, int32_t idx, uint64_t* pn, uint
     const Reason r = spread_filter(req, n, *pf);
     if (r != RS_OK) return r;
   }
-  if (ip && ip->active) return interpod_filter(req, n, *ip);
+  if (ip && ip->active) {
+    const Reason r = interpod_filter(req, n, *ip);
+    if (r != RS_OK) return r;
+  }
+  // the volume plugins run after every other filter (where the hybrid runner's Python filters
+  // run: same first-failing reason on both paths). A PV's NodeSelector: any term matches; a
+  // term with no requirement matches nothing
+  for (const PodReq::VolTerms& v : req.vol) {
+    bool ok = false;
+    for (const SelTerm& t : *v.terms)
+      if (term_matches(t, n)) {
+        ok = true;
+        break;
+      }
+    if (!ok) return (Reason)v.reason;
+  }
   return RS_OK;
 }
 
@@ -1998,6 +2013,7 @@ bool Engine::device_eligible(const PodReq& req) const {
   // NodePorts: the device row carries no host ports, and pods placed in one device batch would
   // not see each other's
   if ((filters_ & F_NODE_PORTS) && !req.host_ports.empty()) return false;
+  if (!req.vol.empty()) return false;      // PV node affinity / zones: not in the device row
   // default-plugin terms the device row does not carry: only pods for which they are a
   // constant (or nothing) go to the device
   if ((filters_ & F_NODE_RESOURCES_FIT) && !req.ext.empty())

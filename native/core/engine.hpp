@@ -74,6 +74,8 @@ enum Reason : int8_t {
   RS_POD_AFFINITY,             // InterPodAffinity: the pod's required affinity
   RS_POD_ANTI,                 // InterPodAffinity: the pod's required anti-affinity
   RS_NODE_PORTS,               // NodePorts: a requested host port is taken
+  RS_VOLUME_NODE,              // VolumeBinding: a bound PV's node affinity rejects the node
+  RS_VOLUME_ZONE,              // VolumeZone: a bound PV's zone / region labels reject the node
   RS_NUM
 };
 
@@ -276,6 +278,14 @@ struct PodReq {
   std::shared_ptr<const PodAffinity> aff;
   // NodePorts: its containers' host ports (hostPort > 0), sanitized
   std::vector<HostPort> host_ports;
+  // VolumeBinding / VolumeZone for claims bound to PVs with node affinity / zone labels (the
+  // native lane's claim table): each entry's terms are OR'ed, every entry must hold; the
+  // reason says which plugin rejects a node
+  struct VolTerms {
+    std::shared_ptr<const std::vector<SelTerm>> terms;
+    int8_t reason = RS_VOLUME_NODE;
+  };
+  std::vector<VolTerms> vol;
 };
 
 struct Weights {

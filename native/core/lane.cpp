@@ -23,7 +23,8 @@ const char* const kReasonName[] = {"OK", "NodeUnschedulable", "NodeName", "Taint
                                          "NodeResourcesFit", "NoScv", "ScvStale", "GpuNumber", "GpuMemory",
                                          "GpuClock", "GpuFit", "NodeGone", "NodeResourcesFitExtended",
                                          "PodTopologySpread", "PodTopologySpreadLabel", "InterPodAffinityExisting",
-                                         "InterPodAffinity", "InterPodAntiAffinity", "NodePorts"};
+                                         "InterPodAffinity", "InterPodAntiAffinity", "NodePorts", "VolumeBinding",
+                                         "VolumeZone"};
 static_assert(sizeof(kReasonName) / sizeof(kReasonName[0]) == RS_NUM, "kReasonName must name every engine Reason");
 const char* reason_text(int i) {
   switch (i) {
@@ -45,6 +46,8 @@ const char* reason_text(int i) {
     case RS_POD_AFFINITY: return "node(s) didn't match pod affinity rules";
     case RS_POD_ANTI: return "node(s) didn't match pod anti-affinity rules";
     case RS_NODE_PORTS: return "node(s) didn't have free ports for the requested pod ports";
+    case RS_VOLUME_NODE: return "node(s) had volume node affinity conflict";
+    case RS_VOLUME_ZONE: return "node(s) had no available volume zone";
     default: return i >= 0 && i < RS_NUM ? kReasonName[i] : "unknown";
   }
 }
@@ -294,22 +297,23 @@ bool Lane::set_gates(const std::string& name, std::vector<MatchTerm> terms) {
 }
 
 void Lane::set_inert_claims(std::vector<std::string> keys) {
-  ClaimOp op;
-  op.reset = true;
-  op.add = std::move(keys);
-  {
-    std::lock_guard<std::mutex> g(prof_mu_);
-    claim_ops_.push_back(std::move(op));
-  }
-  std::lock_guard<std::mutex> g(in_mu_);
-  Item it;
-  it.k = Item::kClaims;
-  push_locked(std::move(it));
-  in_cv_.notify_one();
+  std::vector<std::pair<std::string, ClaimConsP>> add;
+  add.reserve(keys.size());
+  for (auto& k : keys) add.emplace_back(std::move(k), nullptr);
+  update_claims(true, std::move(add), {});
 }
 
 void Lane::update_inert_claims(std::vector<std::string> add, std::vector<std::string> remove) {
+  std::vector<std::pair<std::string, ClaimConsP>> a;
+  a.reserve(add.size());
+  for (auto& k : add) a.emplace_back(std::move(k), nullptr);
+  update_claims(false, std::move(a), std::move(remove));
+}
+
+void Lane::update_claims(bool reset, std::vector<std::pair<std::string, ClaimConsP>> add,
+                         std::vector<std::string> remove) {
   ClaimOp op;
+  op.reset = reset;
   op.add = std::move(add);
   op.remove = std::move(remove);
   {
@@ -833,8 +837,20 @@ bool Lane::claims_inert(const yk::PodProj& p) const {
   return true;
 }
 
-// A new inert-claims set: waiting pods that mount a claim which left it go to Python (a claim
-// that joined the set cannot make a pod inadmissible; pods Python holds stay there).
+bool Lane::claim_cons(const yk::PodProj& p, std::vector<ClaimConsP>* out) const {
+  std::string key;
+  for (const std::string& c : p.claims) {
+    key.assign(p.ns).append("/").append(c);
+    auto it = inert_.find(key);
+    if (it == inert_.end()) return false;
+    if (it->second) out->push_back(it->second);
+  }
+  return true;
+}
+
+// A claim-table change: waiting pods that mount a claim which left the table, or whose
+// constraints changed (their cached request holds the old ones), go to Python. A claim that
+// joined cannot make a pod inadmissible; pods Python holds stay there.
 void Lane::apply_claims(std::vector<Fwd>* out) {
   std::vector<ClaimOp> ops;
   {
@@ -842,21 +858,30 @@ void Lane::apply_claims(std::vector<Fwd>* out) {
     ops.swap(claim_ops_);                   // an earlier kClaims may have taken them already
   }
   if (ops.empty()) return;
-  std::unordered_set<std::string> removed;  // left the set at some op (re-added ones filtered below)
+  std::unordered_set<std::string> removed;  // left the table or changed at some op
   for (auto& op : ops) {
     if (op.reset) {
-      std::unordered_set<std::string> next(std::make_move_iterator(op.add.begin()),
-                                           std::make_move_iterator(op.add.end()));
-      for (const auto& k : inert_)
-        if (!next.count(k)) removed.insert(k);
+      std::unordered_map<std::string, ClaimConsP> next;
+      for (auto& kv : op.add) next.emplace(std::move(kv.first), std::move(kv.second));
+      for (const auto& kv : inert_) {
+        auto it = next.find(kv.first);
+        if (it == next.end() || it->second != kv.second) removed.insert(kv.first);
+      }
       inert_.swap(next);
       continue;
     }
     for (auto& k : op.remove)
       if (inert_.erase(k)) removed.insert(std::move(k));
-    for (auto& k : op.add) inert_.insert(std::move(k));
+    for (auto& kv : op.add) {
+      auto it = inert_.find(kv.first);
+      if (it != inert_.end()) {
+        if (it->second != kv.second) removed.insert(kv.first);
+        it->second = std::move(kv.second);
+      } else {
+        inert_.emplace(std::move(kv.first), std::move(kv.second));
+      }
+    }
   }
-  for (auto it = removed.begin(); it != removed.end();) it = inert_.count(*it) ? removed.erase(it) : std::next(it);
   if (removed.empty()) return;
   std::vector<Entry*> evict;
   std::string key;
@@ -1127,6 +1152,17 @@ void Lane::engine_step(Run& r) {
     } catch (const std::exception&) {
       r.ok[k] = 0;
     }
+    if (k < r.vol_ok.size() && !r.vol_ok[k]) r.ok[k] = 0;   // a claim left the table meanwhile
+    if (r.ok[k] && k < r.vols.size()) {
+      // VolumeBinding then VolumeZone (upstream's filter order, the hybrid runner's too), as
+      // engine filters; the aliasing pointers keep each claim's constraints alive
+      for (const ClaimConsP& c : r.vols[k])
+        if (c->has_node && r.pr.vol_node)
+          r.reqs[k].vol.push_back({std::shared_ptr<const std::vector<SelTerm>>(c, &c->node), RS_VOLUME_NODE});
+      for (const ClaimConsP& c : r.vols[k])
+        if (c->has_zone && r.pr.vol_zone)
+          r.reqs[k].vol.push_back({std::shared_ptr<const std::vector<SelTerm>>(c, &c->zone), RS_VOLUME_ZONE});
+    }
     if (!r.ok[k]) continue;
     eids.push_back(r.ids[k]);
     rp.push_back(&r.reqs[k]);
@@ -1290,6 +1326,11 @@ void Lane::schedule_some() {
       r->ids.push_back(picked[i]->id);
       r->evs.push_back(picked[i]->ev);
       r->cycles.push_back(picked[i]->cycle);
+      // the claim table is the lane thread's: its constraints are copied into the run here
+      std::vector<ClaimConsP> cons;
+      const yk::PodProj& pp = picked[i]->ev->full();
+      r->vol_ok.push_back(!(pp.flags & yk::PF_CLAIMS) || claim_cons(pp, &cons));
+      r->vols.push_back(std::move(cons));
     }
     runs.push_back(std::move(r));
   }

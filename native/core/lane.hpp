@@ -136,8 +136,18 @@ class Lane : public yk::PodSink {
     // is in the inert set (set_inert_claims): the profile's volume plugins are all no-ops for
     // it (plugins/volumes.py::inert_claims), so its cycle is the native one
     bool claims_ok = false;
+    // VolumeBinding / VolumeZone are enabled: a bound claim's PV node affinity / zone labels
+    // (the claim table's constraints) are engine filters of the pod's cycle
+    bool vol_node = false, vol_zone = false;
     EngineConfig cfg;
   };
+  // What VolumeBinding and VolumeZone check of one bound claim (plugins/volumes.py::claim_lane):
+  // the PV's nodeAffinity terms and its zone / region labels as node-affinity terms, OR'ed
+  struct ClaimCons {
+    bool has_node = false, has_zone = false;
+    std::vector<SelTerm> node, zone;
+  };
+  using ClaimConsP = std::shared_ptr<const ClaimCons>;
 
   // What the Python informer sees of a forwarded pod event: type 'A'/'M'/'D', the event,
   // and the previous event of the key (nullptr for a new one).
@@ -177,6 +187,11 @@ class Lane : public yk::PodSink {
   void set_inert_claims(std::vector<std::string> keys);
   // the same set changed by a few claims (a PVC / PV event): O(change), not O(claims)
   void update_inert_claims(std::vector<std::string> add, std::vector<std::string> remove);
+  // the claim table: every claim the lane may admit, with the constraints its PV puts on nodes
+  // (null: none). `reset`: `add` is the whole table. A claim that leaves it or whose
+  // constraints change sends the waiting lane pods that mount it to Python
+  void update_claims(bool reset, std::vector<std::pair<std::string, ClaimConsP>> add,
+                     std::vector<std::string> remove);
   void set_active(bool on);                    // leader: schedule; otherwise only keep the store
   void set_node_cards(const std::string& node, std::vector<std::pair<std::string, std::string>> vis);
   void remove_node_cards(const std::string& node);
@@ -284,6 +299,8 @@ class Lane : public yk::PodSink {
     std::vector<std::string> names;
     std::vector<uint64_t> cycles;                    // each pod's scheduling cycle (pick order)
     std::vector<char> hinted;                        // per result: a node hint since its cycle fits it
+    std::vector<std::vector<ClaimConsP>> vols;       // per pod: its claims' constraints (claim table)
+    std::vector<char> vol_ok;                        // per pod: every claim was in the table
     bool failed = false;
   };
   struct Item {             // inbox: events, answers, commands — applied in order
@@ -427,12 +444,16 @@ class Lane : public yk::PodSink {
   // set_inert_claims / update_inert_claims, in call order; taken by the lane thread on kClaims
   // (prof_mu_)
   struct ClaimOp {
-    bool reset = false;                     // `add` is the whole set
-    std::vector<std::string> add, remove;
+    bool reset = false;                     // `add` is the whole table
+    std::vector<std::pair<std::string, ClaimConsP>> add;
+    std::vector<std::string> remove;
   };
   std::vector<ClaimOp> claim_ops_;
-  std::unordered_set<std::string> inert_;   // lane thread's view
+  std::unordered_map<std::string, ClaimConsP> inert_;   // lane thread's view of the claim table
   bool claims_inert(const yk::PodProj& p) const;
+  // a picked pod's claims' constraints (run formation, lane thread); false if a claim is not in
+  // the table (the pod goes to Python)
+  bool claim_cons(const yk::PodProj& p, std::vector<ClaimConsP>* out) const;
   void apply_claims(std::vector<Fwd>* out);
 
   std::mutex vis_mu_;

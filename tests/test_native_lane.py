@@ -889,11 +889,12 @@ def _claim_pod(name, claim):
 
 @pytest.mark.parametrize("server", ["native", "python"])
 def test_pods_with_inert_claims_are_lane_pods_until_a_claim_needs_a_plugin(server):
-    """A pod mounting only claims every volume plugin has nothing to check for
-    (plugins/volumes.py::inert_claims: bound CSI PV, no node affinity, no zone labels, no attach
-    limit) is admitted by the lane. When its claim's PV gains node affinity the claim leaves the
-    set: a waiting lane pod mounting it goes to Python, and new ones take the Python cycle,
-    where VolumeBinding keeps them on the PV's node."""
+    """A pod mounting only claims in the lane's claim table (plugins/volumes.py::claim_lane:
+    bound PV, no in-tree disk, no attach limit for its CSI driver) is admitted by the lane. A PV
+    that gains node affinity changes its claim's constraints: a waiting lane pod mounting it goes
+    to Python (VolumeBinding keeps it on the PV's node), and the next one stays on the lane,
+    where the PV's node affinity is an engine filter. A claim whose PV is deleted leaves the
+    table: its pods take the Python path (and fail there: the PV is gone)."""
     async def go():
         async with Env(server=server, nodes=(("n1", 8, None), ("n2", 8, None))) as e:
             nl = e.sched.lane
@@ -907,25 +908,88 @@ def test_pods_with_inert_claims_are_lane_pods_until_a_claim_needs_a_plugin(serve
                 await e.create(_claim_pod(f"c{i}", "data"))
             assert await e.wait(lambda: e.sched.scheduled == 4)
             on_lane = lane.scheduled
-            # a waiting lane pod whose claim stops being inert goes to the Python path
+            # a waiting lane pod whose claim's constraints change goes to the Python path
             lane.pause(True)
             await e.create(_claim_pod("w0", "ckpt"))
             await asyncio.sleep(0.3)
             await e.cl.patch("persistentvolumes", "pv-b", {"spec": _csi_pv("pv-b", host="n2")["spec"]})
-            assert await e.wait(lambda: "default/ckpt" not in nl._claims)
+            assert await e.wait(lambda: nl._inert.table.get("default/ckpt") is not None)
             lane.pause(False)
             assert await e.wait(lambda: e.sched.scheduled == 5)
-            await e.create(_claim_pod("w1", "ckpt"))
+            py_after_w0 = e.sched._scheduled
+            await e.create(_claim_pod("w1", "ckpt"))          # the lane: node affinity as an engine filter
             assert await e.wait(lambda: e.sched.scheduled == 6)
+            await e.cl.delete("persistentvolumes", "pv-a")
+            assert await e.wait(lambda: "default/data" not in nl._claims)
+            await e.create(_claim_pod("w2", "data"))
+            await asyncio.sleep(0.5)
             pods = await e.pods()
-            return on_lane, lane.scheduled, e.sched._scheduled, pods["w0"]["spec"]["nodeName"], \
-                pods["w1"]["spec"]["nodeName"], e.sched.cache.lane_never_flags
-    on_lane, lane_total, py_bound, w0, w1, never = run(go())
+            return on_lane, lane.scheduled, py_after_w0, e.sched._scheduled, pods["w0"]["spec"]["nodeName"], \
+                pods["w1"]["spec"]["nodeName"], pods["w2"]["spec"].get("nodeName", ""), e.sched.cache.lane_never_flags
+    on_lane, lane_total, py_w0, py_bound, w0, w1, w2, never = run(go())
     from yoda_scheduler_amd.models.pod import PF_CLAIMS
     assert on_lane == 4                       # every inert-claim pod bound by the lane
-    assert lane_total == 4 and py_bound == 2  # w0 (evicted while waiting) and w1 by Python
-    assert w0 == "n2" and w1 == "n2"          # the PV's node affinity, checked by VolumeBinding
+    assert py_w0 == 1 and lane_total == 5 and py_bound == 1   # w0 by Python, w1 by the lane
+    assert w0 == "n2" and w1 == "n2"          # the PV's node affinity, on both paths
+    assert w2 == ""                           # its PV is gone: VolumeBinding rejects it
     assert not never & PF_CLAIMS              # lane pods may carry claims: Python's readers see them
+
+
+def _zonal_case(lane):
+    async def go():
+        async with Env(lane=lane, nodes=(("n1", 8, None), ("n2", 8, None), ("n3", 8, None))) as e:
+            for n, z in (("n1", "z1"), ("n2", "z2")):              # n3 has no zone label
+                node = await e.cl.get("nodes", n)
+                labels = dict(node["metadata"].get("labels") or {}, **{"topology.kubernetes.io/zone": z})
+                await e.cl.patch("nodes", n, {"metadata": {"labels": labels}})
+            await e.cl.create("persistentvolumes", _csi_pv("pv-z", zone="z2__z3"))
+            await e.cl.create("persistentvolumeclaims", _bound_pvc("zonal", "pv-z"))
+            await e.cl.create("persistentvolumes", _csi_pv("pv-p", host="n1"))
+            await e.cl.create("persistentvolumeclaims", _bound_pvc("pinned", "pv-p"))
+            await e.cl.create("persistentvolumes", _csi_pv("pv-x", zone="z9"))
+            await e.cl.create("persistentvolumeclaims", _bound_pvc("far", "pv-x"))
+            if e.sched.lane is not None:
+                assert await e.wait(lambda: {"default/zonal", "default/pinned", "default/far"} <= e.sched.lane._claims)
+            else:
+                await asyncio.sleep(0.3)
+            pods = [("z", "zonal"), ("p", "pinned"), ("f", "far")]
+            for name, claim in pods:
+                await e.create(_claim_pod(name, claim))
+            both = pod("zp", {"scv/memory": "1000"}, volumes=[
+                {"name": "a", "persistentVolumeClaim": {"claimName": "zonal"}},
+                {"name": "b", "persistentVolumeClaim": {"claimName": "pinned"}}])
+            await e.create(both)
+            assert await e.wait(lambda: e.sched.scheduled == 3)
+
+            def cond(p):
+                for c in (p.get("status") or {}).get("conditions") or []:
+                    if c.get("type") == "PodScheduled" and c.get("status") == "False":
+                        return c.get("message", "")
+                return None
+            await e.wait(lambda: False, 0.5)         # the unschedulable pod's condition is written
+            got = await e.pods()
+            admitted = e.sched.lane.lane.stats()["admitted"] if e.sched.lane else 0
+            return {n: (got[n]["spec"].get("nodeName", ""), cond(got[n])) for n in ("z", "p", "f", "zp")}, admitted
+    return run(go())
+
+
+@pytest.mark.parametrize("lane", ["on", "off"])
+def test_zonal_and_pinned_claims_place_alike_on_the_lane_and_the_python_path(lane):
+    """PV zone labels (VolumeZone: a node without zone labels takes any volume) and PV node
+    affinity (VolumeBinding) as engine filters on the lane, as Python plugins off it."""
+    out, admitted = _zonal_case(lane)
+    assert out["z"][0] in ("n2", "n3") and out["p"][0] == "n1"
+    assert out["f"][0] == "n3"                # only the node without zone labels takes zone z9
+    assert out["zp"][0] == "" and "volume" in out["zp"][1]   # pinned to n1, whose zone z1 the PV excludes
+    if lane == "on":
+        assert admitted == 4
+
+
+def test_zonal_and_pinned_claims_fit_errors_match_across_paths():
+    """The same nodes and the same FitError text (reason counts) on both paths."""
+    on, _ = _zonal_case("on")
+    off, _ = _zonal_case("off")
+    assert on == off, (on, off)
 
 
 def test_attach_limit_counts_lane_pods_once_their_claims_stop_being_inert():
@@ -986,7 +1050,7 @@ def _mixed_pods(seed):
             c["resources"]["requests"]["ephemeral-storage"] = "1Gi"
         spec["containers"] = [c]
         if rng.random() < 0.3:
-            spec["volumes"] = [{"name": "d", "persistentVolumeClaim": {"claimName": rng.choice(["d0", "d1"])}}]
+            spec["volumes"] = [{"name": "d", "persistentVolumeClaim": {"claimName": rng.choice(["d0", "d1", "dp"])}}]
         out.append(pod(f"m{i:02d}", labels, **spec))
     return out
 
@@ -997,8 +1061,10 @@ def _mixed_placements(seed, lane):
             for i in range(2):
                 await e.cl.create("persistentvolumes", _csi_pv(f"pv-{i}"))
                 await e.cl.create("persistentvolumeclaims", _bound_pvc(f"d{i}", f"pv-{i}"))
+            await e.cl.create("persistentvolumes", _csi_pv("pv-p", host="n2"))      # a local PV on n2
+            await e.cl.create("persistentvolumeclaims", _bound_pvc("dp", "pv-p"))
             if e.sched.lane is not None:
-                assert await e.wait(lambda: {"default/d0", "default/d1"} <= e.sched.lane._claims)
+                assert await e.wait(lambda: {"default/d0", "default/d1", "default/dp"} <= e.sched.lane._claims)
             else:
                 await asyncio.sleep(0.3)
             for o in _mixed_pods(seed):
@@ -1025,8 +1091,9 @@ def _mixed_placements(seed, lane):
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_lane_and_python_path_place_mixed_real_cluster_pods_alike(seed):
     """One pod at a time, so both paths see the same cluster: the lane (which now admits spread,
-    affinity, host-port, extended-resource and inert-PVC pods) places every pod on the node and
-    GPUs the Python path picks, including the pods a host-port conflict leaves unschedulable."""
+    affinity, host-port, extended-resource and PVC pods, a local PV's node affinity included)
+    places every pod on the node and GPUs the Python path picks, including the pods a host-port
+    conflict or the local PV's node leaves unschedulable."""
     lane, admitted = _mixed_placements(seed, "on")
     py, _ = _mixed_placements(seed, "off")
     assert lane == py

@@ -224,14 +224,14 @@ def test_bench_pvc_workload_mounts_bound_claims():
     assert all(o["spec"]["volumeName"] in pvs for res, o in w.objects if res == "persistentvolumeclaims")
 
 
-def test_incremental_inert_claims_equal_a_full_recompute():
-    """``InertClaims`` (per-event updates for the lane) ≡ ``inert_claims`` recomputed over every
-    PVC, after each of a random sequence of PVC / PV / CSINode / node-limit changes."""
+def test_incremental_claim_table_equals_a_full_recompute():
+    """``LaneClaims`` (per-event updates of the lane's claim table) ≡ ``lane_claims`` recomputed
+    over every PVC, after each of a random sequence of PVC / PV / CSINode / node-limit changes."""
     import collections
     import random
     from types import SimpleNamespace
 
-    from yoda_scheduler_amd.plugins.volumes import InertClaims, inert_claims
+    from yoda_scheduler_amd.plugins.volumes import LaneClaims, lane_claims
 
     class H:
         def __init__(self):
@@ -249,7 +249,7 @@ def test_incremental_inert_claims_equal_a_full_recompute():
     for seed in range(40):
         rng = random.Random(seed)
         h = H()
-        t = InertClaims(h)
+        t = LaneClaims(h)
         for _step in range(60):
             op = rng.random()
             if op < 0.4:
@@ -277,10 +277,11 @@ def test_incremental_inert_claims_equal_a_full_recompute():
                                  "allocatable": {"count": 4}}]}}}
             else:
                 h.cache.csi_limit_drivers = rng.choice([{}, {}, {"nfs.csi.k8s.io": 1}, {"ebs.csi.aws.com": 2}])
-            before = set(t.keys)
-            full, added, removed = t.refresh()
-            assert t.keys == inert_claims(h), (seed, _step)
+            before = dict(t.table)
+            full, changed, removed = t.refresh()
+            assert t.table == lane_claims(h), (seed, _step)
             if full is None:
-                assert before | added == t.keys | removed and not (added & removed)
-            adds, removes = adds + len(added), removes + len(removed)
+                assert {**{k: v for k, v in before.items() if k not in removed}, **changed} == t.table
+                assert not (set(changed) & removed)
+            adds, removes = adds + len(changed), removes + len(removed)
     assert adds > 20 and removes > 20             # the sequences move claims both ways

@@ -69,8 +69,8 @@ class NativeLane:
         self._in_gated = False             # inside gated(): anti-affinity changes wait for its exit
         self._gates_pending = False        # a coalesced gate update (holder removals) is scheduled
         self._sticky_never = (1 << 62) - 1  # AND of the masks of profiles eligible since the lane last owned nothing
-        self._inert = None                 # plugins/volumes.py::InertClaims, made on first use
-        self._claims: set = set()          # the inert claims the lane holds
+        self._inert = None                 # plugins/volumes.py::LaneClaims, made on first use
+        self._claims = frozenset()         # the claims the lane may admit (the table's keys)
         sched.queue.on_move_all = self._move_all
 
     # ------------------------------------------------------------------ lifecycle
@@ -164,18 +164,21 @@ class NativeLane:
                 lm = m & ~PF_CLAIMS if c_ok and claims else m
                 never &= lm
                 self._sticky_never &= lm
+            filters = {p.name for p in fw.filter_py}
             want = (m is not None, m or 0, bool(fw.filter_mask & f_yoda), self.preempt_above(fw),
-                    fw.gate_terms() + self._temp_terms if m is not None else (), c_ok)
+                    fw.gate_terms() + self._temp_terms if m is not None else (), c_ok,
+                    "VolumeBinding" in filters, "VolumeZone" in filters)
             if self._profiles.get(name) == want:
                 continue
             s._activate(fw)                    # the lane snapshots the engine config now applied
-            self.lane.set_profile(s.engine, name, want[0], want[1], want[2], want[3], list(want[4]), want[5])
+            self.lane.set_profile(s.engine, name, want[0], want[1], want[2], want[3], list(want[4]), want[5],
+                                  want[6], want[7])
             self._profiles[name] = want
             log.info("native lane: profile %s %s (flag mask %#x)", name, "on" if want[0] else "off", want[1])
         s.cache.lane_never_flags = never & self._sticky_never
 
     def claims_event(self, res: str, obj: dict) -> None:
-        """A PVC / PV changed: its claims are re-tested on the next refresh (O(change))."""
+        """A PVC / PV changed: its claims are re-evaluated on the next refresh (O(change))."""
         if self._inert is None:
             return
         if res == "persistentvolumeclaims":
@@ -191,13 +194,14 @@ class NativeLane:
         if not any(fw.claims_ok() for fw in s.frameworks.values()):
             return self._claims
         if self._inert is None:
-            from ..plugins.volumes import InertClaims
-            self._inert = InertClaims(s.handle)
-        full, added, removed = self._inert.refresh()
+            from ..plugins.volumes import LaneClaims
+            self._inert = LaneClaims(s.handle)
+        full, changed, removed = self._inert.refresh()
         if full is not None:
-            self.lane.set_inert_claims(sorted(full))
-        elif added or removed:
-            self.lane.update_inert_claims(sorted(added), sorted(removed))
+            self.lane.update_claims(s.engine, True, [_claim_item(k, v) for k, v in sorted(full.items())], [])
+        elif changed or removed:
+            self.lane.update_claims(s.engine, False, [_claim_item(k, v) for k, v in sorted(changed.items())],
+                                    sorted(removed))
         self._claims = self._inert.keys
         return self._claims
 
@@ -413,6 +417,16 @@ class NativeLane:
 
     def owned(self) -> int:
         return self.lane.stats()["owned"]
+
+
+def _claim_item(key: str, v) -> tuple:
+    """A claim-table entry for ``Lane.update_claims``: (key, node terms | None, zone terms | None),
+    terms as [[(key, op, [values])]] (plugins/volumes.py::claim_lane)."""
+    if v is None:
+        return key, None, None
+    node, zone = v
+    conv = (lambda terms: None if terms is None else [[(k, op, list(vals)) for k, op, vals in t] for t in terms])
+    return key, conv(node), conv(zone)
 
 
 class LaneEntries:

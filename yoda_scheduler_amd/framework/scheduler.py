@@ -875,7 +875,9 @@ class Scheduler:
                 "InterPodAffinityExisting": "node(s) didn't satisfy existing pods anti-affinity rules",
                 "InterPodAffinity": "node(s) didn't match pod affinity rules",
                 "InterPodAntiAffinity": "node(s) didn't match pod anti-affinity rules",
-                "NodePorts": "node(s) didn't have free ports for the requested pod ports"}
+                "NodePorts": "node(s) didn't have free ports for the requested pod ports",
+                "VolumeBinding": "node(s) had volume node affinity conflict",
+                "VolumeZone": "node(s) had no available volume zone"}
         parts = [f"{c} {text.get(names[i], names[i])}" for i, c in enumerate(reasons) if c and i]
         if len(res) > 10 and res[10]:
             by_msg: dict[str, int] = {}

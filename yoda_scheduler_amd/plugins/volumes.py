@@ -614,23 +614,65 @@ def claim_inert(pvc: dict, pvs: dict, limited: set) -> bool:
     """One PersistentVolumeClaim every volume plugin has nothing to check for: not being
     deleted, bound to a PV that exists and has no required node affinity, no zone / region
     labels and no in-tree attachable disk, and either not a CSI volume or one whose driver has
-    no attach limit on any node (``limited``: the drivers that have one). A pod whose claims are all inert is a no-op for
-    VolumeBinding, VolumeZone, NodeVolumeLimits and the in-tree limits (each claim satisfies
-    the per-claim half of their ``is_noop_for``), so the native lane may run it."""
+    no attach limit on any node (``limited``: the drivers that have one). A pod whose claims
+    are all inert is a no-op for VolumeBinding, VolumeZone, NodeVolumeLimits and the in-tree
+    limits (each claim satisfies the per-claim half of their ``is_noop_for``)."""
+    return claim_lane(pvc, pvs, limited) is None
+
+
+NOT_LANE = "not-lane"                     # claim_lane: the claim needs the Python volume plugins
+_LANE_NODE_OPS = ("In", "NotIn", "Exists", "DoesNotExist")
+
+
+def claim_lane(pvc: dict, pvs: dict, limited: set):
+    """What the native lane needs to run a pod that mounts this claim: ``NOT_LANE`` when the
+    claim needs the Python volume plugins, else the constraints its bound PV puts on nodes —
+    None (an inert claim, ``claim_inert``) or ``(node_terms | None, zone_terms | None)``:
+
+    * ``node_terms`` — the PV's ``nodeAffinity.required`` (VolumeBinding's filter for a bound
+      claim: any term matches; a term without requirements matches nothing), only with the
+      operators In / NotIn / Exists / DoesNotExist and no ``matchFields``;
+    * ``zone_terms`` — VolumeZone's filter as two OR'ed terms: the node has none of the zone /
+      region labels, or it has every label the PV has with a value the PV allows ("__"-separated).
+
+    A lane-able claim is not being deleted, is bound to a PV that exists, has no in-tree
+    attachable disk, and is not a CSI volume whose driver some node limits (``limited``)."""
     if (pvc.get("metadata") or _EMPTY).get("deletionTimestamp"):
-        return False
+        return NOT_LANE
     name = (pvc.get("spec") or _EMPTY).get("volumeName", "")
     pv = pvs.get(name) if name else None
     if pv is None:
-        return False
+        return NOT_LANE
     ps = pv.get("spec") or _EMPTY
-    if (ps.get("nodeAffinity") or _EMPTY).get("required") is not None:
-        return False
-    labels = (pv.get("metadata") or _EMPTY).get("labels") or _EMPTY
-    if any(k in labels for k in ZONE_LABELS) or any(ps.get(k) for k in _ATTACHABLE_KINDS):
-        return False
+    if any(ps.get(k) for k in _ATTACHABLE_KINDS):
+        return NOT_LANE
     csi = ps.get("csi")
-    return not (csi and csi.get("driver", "") in limited)
+    if csi and csi.get("driver", "") in limited:
+        return NOT_LANE
+    node = None
+    req = (ps.get("nodeAffinity") or _EMPTY).get("required")
+    if req is not None:
+        if not isinstance(req, dict):
+            return NOT_LANE
+        terms = []
+        for t in req.get("nodeSelectorTerms") or []:
+            if not isinstance(t, dict) or t.get("matchFields"):
+                return NOT_LANE
+            exprs = []
+            for e in t.get("matchExpressions") or []:
+                op = e.get("operator", "In")
+                if op not in _LANE_NODE_OPS:
+                    return NOT_LANE
+                exprs.append((e.get("key", ""), op, tuple(str(v) for v in e.get("values") or [])))
+            terms.append(tuple(exprs))
+        node = tuple(terms)
+    labels = (pv.get("metadata") or _EMPTY).get("labels") or _EMPTY
+    keys = [k for k in ZONE_LABELS if k in labels]
+    zone = None
+    if keys:
+        zone = (tuple((k, "DoesNotExist", ()) for k in ZONE_LABELS),
+                tuple((k, "In", tuple(str(labels[k]).split("__"))) for k in keys))
+    return None if node is None and zone is None else (node, zone)
 
 
 def limited_drivers(handle) -> set:
@@ -639,21 +681,33 @@ def limited_drivers(handle) -> set:
     return _csinode_drivers(handle.lister("csinodes")) | set(getattr(handle.cache, "csi_limit_drivers", ()))
 
 
+def lane_claims(handle) -> dict:
+    """The claim table over the whole PVC lister: key ("namespace/name") → ``claim_lane``
+    value, for every lane-able claim."""
+    pvs, limited = handle.lister("persistentvolumes"), limited_drivers(handle)
+    out = {}
+    for key, pvc in handle.lister("persistentvolumeclaims").items():
+        v = claim_lane(pvc, pvs, limited)
+        if v is not NOT_LANE:
+            out[key] = v
+    return out
+
+
 def inert_claims(handle) -> set:
     """Every inert claim ("namespace/name", ``claim_inert``) of the PVC lister."""
-    pvs, limited = handle.lister("persistentvolumes"), limited_drivers(handle)
-    return {key for key, pvc in handle.lister("persistentvolumeclaims").items() if claim_inert(pvc, pvs, limited)}
+    return {k for k, v in lane_claims(handle).items() if v is None}
 
 
-class InertClaims:
-    """``inert_claims`` kept up to date per event instead of recomputed over every PVC: a PVC
-    event re-tests that claim, a PV event the claims bound to it (an index PV name → claim
-    keys), and a change of the cluster's attach limits (CSINode counts, node allocatable)
-    re-tests all. ``refresh`` returns (full set | None, added, removed) since the last call."""
+class LaneClaims:
+    """The native lane's claim table (``lane_claims``) kept up to date per event instead of
+    recomputed over every PVC: a PVC event re-evaluates that claim, a PV event the claims
+    bound to it (an index PV name → claim keys), and a change of the cluster's attach limits
+    (CSINode counts, node allocatable) all of them. ``refresh`` returns (whole table | None,
+    {added or changed key: value}, {removed keys}) since the last call."""
 
     def __init__(self, handle) -> None:
         self.handle = handle
-        self.keys: set = set()
+        self.table: dict = {}
         self._pv_of: dict[str, str] = {}          # claim key → the PV name it is bound to
         self._claims_of: dict[str, set] = {}      # PV name → claim keys bound to it
         self._dirty: set = set()
@@ -661,6 +715,10 @@ class InertClaims:
         self._limited: Optional[frozenset] = None
         self._csinode_gen = -1
         self._csinode_drivers: set = set()
+
+    @property
+    def keys(self):
+        return self.table.keys()
 
     def pvc_event(self, obj: dict) -> None:
         m = obj.get("metadata") or _EMPTY
@@ -691,34 +749,37 @@ class InertClaims:
         if gen != self._csinode_gen or gen == -2:
             self._csinode_gen = gen
             self._csinode_drivers = _csinode_drivers(h.lister("csinodes"))
-        limits = frozenset(self._csinode_drivers | set(getattr(h.cache, "csi_limit_drivers", ())))
-        if limits != self._limited:
-            self._limited, self._all = limits, True
+        limited = frozenset(self._csinode_drivers | set(getattr(h.cache, "csi_limit_drivers", ())))
+        if limited != self._limited:
+            self._limited, self._all = limited, True
         pvcs, pvs = h.lister("persistentvolumeclaims"), h.lister("persistentvolumes")
         if self._all:
             self._all, self._dirty = False, set()
             self._pv_of, self._claims_of = {}, {}
-            keys = set()
+            table = {}
             for key, pvc in pvcs.items():
                 self._index(key, (pvc.get("spec") or _EMPTY).get("volumeName", "") or "")
-                if claim_inert(pvc, pvs, limits):
-                    keys.add(key)
-            added, removed = keys - self.keys, self.keys - keys
-            self.keys = keys
-            return keys, added, removed
-        added, removed = set(), set()
+                v = claim_lane(pvc, pvs, limited)
+                if v is not NOT_LANE:
+                    table[key] = v
+            changed = {k: v for k, v in table.items() if k not in self.table or self.table[k] != v}
+            removed = set(self.table) - set(table)
+            self.table = table
+            return table, changed, removed
+        changed, removed = {}, set()
         dirty, self._dirty = self._dirty, set()
         for key in dirty:
             pvc = pvcs.get(key)
             self._index(key, ((pvc.get("spec") or _EMPTY).get("volumeName", "") or "") if pvc is not None else "")
-            inert = pvc is not None and claim_inert(pvc, pvs, limits)
-            if inert and key not in self.keys:
-                self.keys.add(key)
-                added.add(key)
-            elif not inert and key in self.keys:
-                self.keys.discard(key)
-                removed.add(key)
-        return None, added, removed
+            v = NOT_LANE if pvc is None else claim_lane(pvc, pvs, limited)
+            if v is NOT_LANE:
+                if key in self.table:
+                    del self.table[key]
+                    removed.add(key)
+            elif key not in self.table or self.table[key] != v:
+                self.table[key] = v
+                changed[key] = v
+        return None, changed, removed
 
 
 # the in-tree attach-limit plugins' volume kinds (what _VolFacts resolves for them)
