@@ -187,9 +187,10 @@ class NativeLane:
             self._inert.pv_event(obj)
 
     def _refresh_claims(self) -> set:
-        """Keep the lane's set of inert claims (plugins/volumes.py::InertClaims) current: the
-        claims a pod may mount and still take the native cycle. Only profiles whose volume
-        plugins all allow it (``claims_ok``) use it; changes go to the lane as deltas."""
+        """Keep the lane's claim table (plugins/volumes.py::LaneClaims) current: the claims a pod
+        may mount and still take the native cycle, with the node constraints of their PVs. Only
+        profiles whose volume plugins all allow it (``claims_ok``) use it; changes go to the
+        lane as deltas."""
         s = self.s
         if not any(fw.claims_ok() for fw in s.frameworks.values()):
             return self._claims

@@ -172,9 +172,9 @@ class Framework:
 
     def claims_ok(self) -> bool:
         """May the native lane run this profile's pods whose only lane-excluding feature is
-        PF_CLAIMS, when every claim is inert (plugins/volumes.py::inert_claims)? Yes when every
-        plugin that acts on claims — conditional or PreBind — declares that inert claims make
-        it a no-op (``claim_inert_ok``)."""
+        PF_CLAIMS, when every claim is in the lane's claim table (plugins/volumes.py::claim_lane)?
+        Yes when every plugin that acts on claims — conditional or PreBind — declares that such
+        claims make it a no-op or an engine filter (``claim_inert_ok``)."""
         from ..models.pod import PF_CLAIMS
         for p in list(self.conditional) + list(self.pre_bind):
             pf = getattr(p, "pod_flags", None)

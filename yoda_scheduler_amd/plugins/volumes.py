@@ -204,7 +204,7 @@ class VolumeRestrictions(_VolumeBase, FilterPlugin):
 class VolumeZone(_VolumeBase, FilterPlugin):
     name = "VolumeZone"
     pod_flags = PF_CLAIMS
-    claim_inert_ok = True   # a no-op for a pod whose claims are all in inert_claims()
+    claim_inert_ok = True   # the lane's claim table covers it (claim_lane): a no-op or an engine filter
     reads_flags = 0  # other pods' features this plugin reads (needs_lane_mirror)
 
     def is_noop_for(self, pod) -> bool:
@@ -288,7 +288,7 @@ class VolumeBinding(_VolumeBase, PreFilterPlugin, FilterPlugin, ReservePlugin, P
     # other pods' features this plugin reads (needs_lane_mirror): none — it reads the PVC / PV /
     # StorageClass listers and its own assumed PVs, never another pod
     reads_flags = 0
-    claim_inert_ok = True   # a no-op for a pod whose claims are all in inert_claims()
+    claim_inert_ok = True   # the lane's claim table covers it (claim_lane): a no-op or an engine filter
 
     def __init__(self, args=None, handle=None) -> None:
         super().__init__(args, handle)
@@ -490,7 +490,7 @@ class NodeVolumeLimits(_LimitsBase):
     ``attachable-volumes-csi-<driver>``)."""
     name = "NodeVolumeLimits"
     pod_flags = PF_CLAIMS
-    claim_inert_ok = True   # a no-op for a pod whose claims are all in inert_claims()
+    claim_inert_ok = True   # the lane's claim table covers it (claim_lane): a no-op or an engine filter
     reads_flags = PF_CLAIMS  # other pods' features this plugin reads (needs_lane_mirror)
     watches = ("persistentvolumeclaims", "persistentvolumes", "storageclasses", "csinodes")
 
@@ -557,7 +557,7 @@ class _InTreeLimits(_LimitsBase):
     default_max = 0
     pod_flags = PF_CLAIMS | PF_DISKS
     reads_flags = PF_CLAIMS | PF_DISKS  # other pods' features this plugin reads (needs_lane_mirror)
-    claim_inert_ok = True   # a no-op for a pod whose claims are all in inert_claims() (PF_DISKS: not)
+    claim_inert_ok = True   # a no-op for a pod whose claims are all in the lane's claim table (PF_DISKS: not)
 
     def is_noop_for(self, pod) -> bool:
         # no inline volume of this kind and no PVC bound to one: the filter has nothing to count
