@@ -160,7 +160,7 @@ class NativeLane:
             m = self.eligible_mask(fw)
             c_ok = m is not None and fw.claims_ok()
             if m is not None:
-                # lane pods may carry PF_CLAIMS (inert claims only) once the set is non-empty
+                # lane pods may carry PF_CLAIMS (claim-table claims only) once the table is non-empty
                 lm = m & ~PF_CLAIMS if c_ok and claims else m
                 never &= lm
                 self._sticky_never &= lm
