@@ -520,7 +520,7 @@ bool Lane::admissible(const yk::PodProj& p, int* prof) const {
   for (size_t i = 0; i < lp_.size(); ++i) {
     if (lp_[i].name != p.sched) continue;
     const int f = p.flags & lp_[i].flag_mask;
-    if (!lp_[i].enabled || (f && (f != yk::PF_CLAIMS || !lp_[i].claims_ok || !claims_inert(p)))) return false;
+    if (!lp_[i].enabled || (f && (f != yk::PF_CLAIMS || !lp_[i].claims_ok || !claims_in_table(p)))) return false;
     for (const MatchTerm& t : lp_[i].gate_terms)
       if (t.matches(p)) return false;     // an existing pod's required anti-affinity may reject it
     *prof = (int)i;
@@ -827,12 +827,12 @@ void Lane::apply_gates(std::vector<Fwd>* out) {
   }
 }
 
-bool Lane::claims_inert(const yk::PodProj& p) const {
-  if (p.claims.empty() || inert_.empty()) return false;
+bool Lane::claims_in_table(const yk::PodProj& p) const {
+  if (p.claims.empty() || claim_table_.empty()) return false;
   std::string key;
   for (const std::string& c : p.claims) {
     key.assign(p.ns).append("/").append(c);
-    if (!inert_.count(key)) return false;
+    if (!claim_table_.count(key)) return false;
   }
   return true;
 }
@@ -841,8 +841,8 @@ bool Lane::claim_cons(const yk::PodProj& p, std::vector<ClaimConsP>* out) const 
   std::string key;
   for (const std::string& c : p.claims) {
     key.assign(p.ns).append("/").append(c);
-    auto it = inert_.find(key);
-    if (it == inert_.end()) return false;
+    auto it = claim_table_.find(key);
+    if (it == claim_table_.end()) return false;
     if (it->second) out->push_back(it->second);
   }
   return true;
@@ -863,22 +863,22 @@ void Lane::apply_claims(std::vector<Fwd>* out) {
     if (op.reset) {
       std::unordered_map<std::string, ClaimConsP> next;
       for (auto& kv : op.add) next.emplace(std::move(kv.first), std::move(kv.second));
-      for (const auto& kv : inert_) {
+      for (const auto& kv : claim_table_) {
         auto it = next.find(kv.first);
         if (it == next.end() || it->second != kv.second) removed.insert(kv.first);
       }
-      inert_.swap(next);
+      claim_table_.swap(next);
       continue;
     }
     for (auto& k : op.remove)
-      if (inert_.erase(k)) removed.insert(std::move(k));
+      if (claim_table_.erase(k)) removed.insert(std::move(k));
     for (auto& kv : op.add) {
-      auto it = inert_.find(kv.first);
-      if (it != inert_.end()) {
+      auto it = claim_table_.find(kv.first);
+      if (it != claim_table_.end()) {
         if (it->second != kv.second) removed.insert(kv.first);
         it->second = std::move(kv.second);
       } else {
-        inert_.emplace(std::move(kv.first), std::move(kv.second));
+        claim_table_.emplace(std::move(kv.first), std::move(kv.second));
       }
     }
   }

@@ -449,8 +449,8 @@ class Lane : public yk::PodSink {
     std::vector<std::string> remove;
   };
   std::vector<ClaimOp> claim_ops_;
-  std::unordered_map<std::string, ClaimConsP> inert_;   // lane thread's view of the claim table
-  bool claims_inert(const yk::PodProj& p) const;
+  std::unordered_map<std::string, ClaimConsP> claim_table_;   // lane thread's view of the claim table
+  bool claims_in_table(const yk::PodProj& p) const;
   // a picked pod's claims' constraints (run formation, lane thread); false if a claim is not in
   // the table (the pod goes to Python)
   bool claim_cons(const yk::PodProj& p, std::vector<ClaimConsP>* out) const;
