@@ -1098,3 +1098,50 @@ def test_lane_and_python_path_place_mixed_real_cluster_pods_alike(seed):
     py, _ = _mixed_placements(seed, "off")
     assert lane == py
     assert admitted >= 20
+
+
+def _burst_placements(seed, lane):
+    async def go():
+        async with Env(lane=lane, nodes=(("n1", 8, None), ("n2", 8, None), ("n3", 8, None))) as e:
+            for i in range(2):
+                await e.cl.create("persistentvolumes", _csi_pv(f"pv-{i}"))
+                await e.cl.create("persistentvolumeclaims", _bound_pvc(f"d{i}", f"pv-{i}"))
+            await e.cl.create("persistentvolumes", _csi_pv("pv-p", host="n2"))
+            await e.cl.create("persistentvolumeclaims", _bound_pvc("dp", "pv-p"))
+            if e.sched.lane is not None:
+                assert await e.wait(lambda: {"default/d0", "default/d1", "default/dp"} <= e.sched.lane._claims)
+            else:
+                await asyncio.sleep(0.3)
+            ps = _mixed_pods(seed)
+            for i, o in enumerate(ps):                 # distinct host ports: only capacity limits
+                for c in o["spec"]["containers"]:
+                    for p in c.get("ports", []):
+                        p["hostPort"] = 20000 + i
+            for o in ps:                               # one creation order, no wait: a burst
+                await e.create(o)
+
+            def settled(p):
+                return p["spec"].get("nodeName") or any(
+                    c.get("type") == "PodScheduled" and c.get("status") == "False"
+                    for c in (p.get("status") or {}).get("conditions") or [])
+            t0 = time.time()
+            while True:
+                got = await e.pods()
+                if all(settled(got[o["metadata"]["name"]]) for o in ps):
+                    break
+                assert time.time() - t0 < 10
+                await asyncio.sleep(0.05)
+            return {n: (p["spec"].get("nodeName", ""), (p["metadata"].get("annotations") or {}).get("scv.amd.com/gpus"))
+                    for n, p in got.items()}
+    return run(go())
+
+
+@pytest.mark.parametrize("seed", range(1, 7))
+def test_lane_and_python_path_place_a_mixed_burst_alike(seed):
+    """The burst form of the equivalence: the same pods created back to back in one order are
+    placed on the same nodes and GPUs by the lane (its batches, its queue) and by the Python
+    path (its batches, its queue) — batch boundaries do not change a placement."""
+    lane = _burst_placements(seed, "on")
+    py = _burst_placements(seed, "off")
+    assert lane == py
+    assert sum(1 for n, _ in lane.values() if n) >= 15
