@@ -100,6 +100,13 @@ for s in $STEPS; do
         step "spread/c3_$k" 300 python bench.py --config 3 --steps 20 --warmup 5 --alt none
         step "spread/c3spread_$k" 300 python bench.py --config 3 --steps 20 --warmup 5 --mix-spread 1000 --alt none
       done ;;
+    realpods)   # config 3 with PVC pods (claim table) and host-port pods (native NodePorts), next to plain config 3
+      mkdir -p gpurun_out/realpods
+      for k in 1 2; do
+        step "realpods/c3_$k" 300 python bench.py --config 3 --steps 20 --warmup 5 --alt none
+        step "realpods/c3pvc_$k" 300 python bench.py --config 3 --steps 20 --warmup 5 --mix-volumes 1000 --alt none
+        step "realpods/c3hostport_$k" 300 python bench.py --config 3 --steps 20 --warmup 5 --mix-hostports 1000 --alt none
+      done ;;
     mixlog) step mixlog 300 env YODA_BENCH_RUNLOG=1 python bench.py --config 3 --mix-anti 10 --steps 5 --warmup 3 --alt none ;;
     scope6) step scope6 300 env YODA_BENCH_THREADS=2 python bench.py --config 6 --steps 5 --warmup 1 --alt none ;;
     nodegpus)   # BASELINE protocol item 5 on config 3: scheduler CPU per attempted pod at 1/2/4/8 GPUs per node
@@ -120,7 +127,9 @@ for s in $STEPS; do
                   "c3kind|--config 3 --steps 20 --warmup 5 --cluster kind" "c1kind|--config 1 --steps 20 --warmup 2 --cluster kind" \
                   "c2kind|--config 2 --steps 10 --warmup 2 --cluster kind" "c4kind|--config 4 --steps 10 --warmup 2 --cluster kind" \
                   "c5kind|--config 5 --steps 5 --warmup 2 --cluster kind" "c6kind|--config 6 --steps 5 --warmup 1 --cluster kind" \
-                  "c3anti|--config 3 --steps 20 --warmup 5 --mix-anti 10" "c3spread|--config 3 --steps 20 --warmup 5 --mix-spread 1000"; do
+                  "c3anti|--config 3 --steps 20 --warmup 5 --mix-anti 10" "c3spread|--config 3 --steps 20 --warmup 5 --mix-spread 1000" \
+                  "c3pvc|--config 3 --steps 20 --warmup 5 --mix-volumes 1000" \
+                  "c3hostport|--config 3 --steps 20 --warmup 5 --mix-hostports 1000"; do
         step "all/${spec%%|*}" 300 python bench.py --alt none ${spec#*|}
       done
       python - <<'PY'
