@@ -323,7 +323,7 @@ PYBIND11_MODULE(_yoda_core, m) {
                                      "GpuClock", "GpuFit", "NodeGone", "NodeResourcesFitExtended",
                                      "PodTopologySpread", "PodTopologySpreadLabel", "InterPodAffinityExisting",
                                      "InterPodAffinity", "InterPodAntiAffinity", "NodePorts", "VolumeBinding",
-                                     "VolumeZone");
+                                     "VolumeZone", "NodeVolumeLimits");
 
   py::class_<PodReq>(m, "PodReq")
       .def_readonly("has_number", &PodReq::has_number)
@@ -512,6 +512,31 @@ PYBIND11_MODULE(_yoda_core, m) {
            py::arg("nz_cpu_m") = -1, py::arg("nz_mem") = -1, py::call_guard<EngineGuard>())
       // the default-plugin inputs of a PodReq (ImageLocality, NodeResourcesFit beyond cpu/memory,
       // NodePreferAvoidPods, PodTopologySpread and what other pods' spread counts read of it)
+      // NodeVolumeLimits: the "namespace/claim" of the pod's persistentVolumeClaim volumes (the
+      // ledger keeps them per node); count_vols: count them against CSI limits in this cycle
+      .def("set_req_claims",
+           [](Engine& e, PodReq& r, const std::vector<std::string>& claims, bool count_vols) {
+             r.pvc_claims.clear();
+             for (const auto& c : claims) r.pvc_claims.push_back(e.intern(c));
+             r.count_vols = count_vols && !r.pvc_claims.empty();
+           },
+           py::arg("req"), py::arg("claims"), py::arg("count_vols") = false, py::call_guard<EngineGuard>())
+      // claim volumes: [(claim, driver, volume id)] set, [claim] removed (plugins/volumes.py::claim_volume)
+      .def("set_claim_volumes",
+           [](Engine& e, const std::vector<std::tuple<std::string, std::string, std::string>>& add,
+              const std::vector<std::string>& remove) {
+             for (const auto& c : remove) e.clear_claim_volume(e.intern(c));
+             for (const auto& t : add)
+               e.set_claim_volume(e.intern(std::get<0>(t)), e.intern(std::get<1>(t)), e.intern(std::get<2>(t)));
+           },
+           py::arg("add"), py::arg("remove"), py::call_guard<EngineGuard>())
+      .def("set_node_vol_limits",
+           [](Engine& e, int32_t idx, const std::vector<std::pair<std::string, int64_t>>& limits) {
+             std::vector<std::pair<int32_t, int64_t>> v;
+             for (const auto& l : limits) v.emplace_back(e.intern(l.first), l.second);
+             e.set_node_vol_limits(idx, std::move(v));
+           },
+           py::arg("idx"), py::arg("limits"), py::call_guard<EngineGuard>())
       // NodePorts: the pod's containers' host ports [(hostPort, protocol, hostIP)]
       .def("set_req_ports",
            [](Engine& e, PodReq& r, const std::vector<std::tuple<int64_t, std::string, std::string>>& ports) {
@@ -792,8 +817,10 @@ PYBIND11_MODULE(_yoda_core, m) {
       // the profile's engine configuration is the engine's current one (the caller applied it)
       .def("set_profile",
            [](Lane& l, Engine& e, const std::string& name, bool enabled, int flag_mask, bool annotate,
-              int64_t preempt_above, const py::list& gate_terms, bool claims_ok, bool vol_node, bool vol_zone) {
+              int64_t preempt_above, const py::list& gate_terms, bool claims_ok, bool vol_node, bool vol_zone,
+              bool vol_limits) {
              Lane::Profile p;
+             p.vol_limits = vol_limits;
              p.preempt_above = preempt_above;
              p.claims_ok = claims_ok;
              p.vol_node = vol_node;
@@ -811,7 +838,7 @@ PYBIND11_MODULE(_yoda_core, m) {
            },
            py::arg("engine"), py::arg("name"), py::arg("enabled"), py::arg("flag_mask"), py::arg("annotate"),
            py::arg("preempt_above") = INT64_MIN, py::arg("gate_terms") = py::list(), py::arg("claims_ok") = false,
-           py::arg("vol_node") = false, py::arg("vol_zone") = false)
+           py::arg("vol_node") = false, py::arg("vol_zone") = false, py::arg("vol_limits") = false)
       // [(key, node terms | None, zone terms | None)], each terms [[(key, op, [values])]]
       .def("update_claims",
            [](Lane& l, Engine& e, bool reset, const py::list& add, const std::vector<std::string>& remove) {

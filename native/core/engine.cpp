@@ -299,6 +299,41 @@ bool Engine::host_port(int64_t port, const std::string& protocol, const std::str
   return true;
 }
 
+void Engine::set_node_vol_limits(int32_t idx, std::vector<std::pair<int32_t, int64_t>> limits) {
+  std::sort(limits.begin(), limits.end());
+  nodes_.at(idx).vol_limits = std::move(limits);
+}
+
+bool Engine::vols_fit(const PodReq& req, const Node& n) const {
+  // plugins/volumes.py NodeVolumeLimits.filter: per CSI driver the node limits, the unique
+  // volumes of the node's pods plus the pod's own must not exceed the limit
+  std::vector<std::pair<int32_t, int32_t>> mine;   // (driver, volume id) of the pod's claims
+  for (int32_t c : req.pvc_claims) {
+    auto it = claim_vol_.find(c);
+    if (it != claim_vol_.end()) mine.push_back(it->second);
+  }
+  if (mine.empty()) return true;
+  std::sort(mine.begin(), mine.end());
+  mine.erase(std::unique(mine.begin(), mine.end()), mine.end());
+  for (size_t i = 0; i < mine.size();) {
+    const int32_t d = mine[i].first;
+    size_t j = i;
+    while (j < mine.size() && mine[j].first == d) ++j;
+    auto lim = std::lower_bound(n.vol_limits.begin(), n.vol_limits.end(), std::make_pair(d, INT64_MIN));
+    if (lim != n.vol_limits.end() && lim->first == d) {
+      std::unordered_set<int32_t> ids;
+      for (size_t k = i; k < j; ++k) ids.insert(mine[k].second);
+      for (const auto& kv : n.claims) {
+        auto it = claim_vol_.find(kv.first);
+        if (it != claim_vol_.end() && it->second.first == d) ids.insert(it->second.second);
+      }
+      if ((int64_t)ids.size() > lim->second) return false;
+    }
+    i = j;
+  }
+  return true;
+}
+
 bool Engine::ports_free(const PodReq& req, const Node& n) const {
   // HostPortInfo.CheckConflict: a 0.0.0.0 request conflicts with the (protocol, port) on any ip;
   // a specific ip only with the same ip or 0.0.0.0
@@ -362,6 +397,10 @@ bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::ve
     aff_set_add(a);
   }
   index_pod(n, a, +1);
+  if (!req.pvc_claims.empty()) {
+    a.pvc_claims = req.pvc_claims;
+    for (int32_t c : a.pvc_claims) ++n.claims[c];
+  }
   if (!req.host_ports.empty()) {
     a.host_ports = req.host_ports;
     for (const HostPort& h : a.host_ports) {
@@ -415,6 +454,10 @@ bool Engine::release(uint64_t pod) {
       if (it != n.ext_used.end() && it->first == r.first && (it->second -= r.second) == 0) n.ext_used.erase(it);
     }
     index_pod(n, a, -1);
+    for (int32_t c : a.pvc_claims) {
+      auto q = n.claims.find(c);
+      if (q != n.claims.end() && --q->second <= 0) n.claims.erase(q);
+    }
     for (const HostPort& h : a.host_ports) {
       auto p = n.ports.find(h);
       if (p != n.ports.end() && --p->second <= 0) n.ports.erase(p);
@@ -573,8 +616,9 @@ Reason Engine::filter_node_pf(const PodReq& req, int32_t idx, uint64_t* pn, uint
     if (r != RS_OK) return r;
   }
   // the volume plugins run after every other filter (where the hybrid runner's Python filters
-  // run: same first-failing reason on both paths). A PV's NodeSelector: any term matches; a
-  // term with no requirement matches nothing
+  // run: same first-failing reason on both paths): NodeVolumeLimits, then VolumeBinding and
+  // VolumeZone — a PV's NodeSelector: any term matches; a term with no requirement matches nothing
+  if (req.count_vols && !req.pvc_claims.empty() && !n.vol_limits.empty() && !vols_fit(req, n)) return RS_VOLUME_LIMITS;
   for (const PodReq::VolTerms& v : req.vol) {
     bool ok = false;
     for (const SelTerm& t : *v.terms)
@@ -2013,7 +2057,7 @@ bool Engine::device_eligible(const PodReq& req) const {
   // NodePorts: the device row carries no host ports, and pods placed in one device batch would
   // not see each other's
   if ((filters_ & F_NODE_PORTS) && !req.host_ports.empty()) return false;
-  if (!req.vol.empty()) return false;      // PV node affinity / zones: not in the device row
+  if (!req.vol.empty() || req.count_vols) return false;   // PV node affinity / zones / attach limits: not in the device row
   // default-plugin terms the device row does not carry: only pods for which they are a
   // constant (or nothing) go to the device
   if ((filters_ & F_NODE_RESOURCES_FIT) && !req.ext.empty())

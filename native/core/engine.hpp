@@ -76,6 +76,7 @@ enum Reason : int8_t {
   RS_NODE_PORTS,               // NodePorts: a requested host port is taken
   RS_VOLUME_NODE,              // VolumeBinding: a bound PV's node affinity rejects the node
   RS_VOLUME_ZONE,              // VolumeZone: a bound PV's zone / region labels reject the node
+  RS_VOLUME_LIMITS,            // NodeVolumeLimits: a CSI driver's attach limit would be exceeded
   RS_NUM
 };
 
@@ -237,6 +238,10 @@ struct Node {
   // over every ip (a 0.0.0.0 request conflicts with any ip) — counts, as two pods may hold one
   std::map<HostPort, int32_t> ports;
   std::map<std::pair<int32_t, int32_t>, int32_t> ports_any;
+  // NodeVolumeLimits: CSI attach limits (driver → count, sorted) and the PVC claims the node's
+  // reserved pods mount (claim → pods); a claim's volume is looked up when counting
+  std::vector<std::pair<int32_t, int64_t>> vol_limits;
+  std::unordered_map<int32_t, int32_t> claims;
 };
 
 struct PodReq {
@@ -286,6 +291,10 @@ struct PodReq {
     int8_t reason = RS_VOLUME_NODE;
   };
   std::vector<VolTerms> vol;
+  // NodeVolumeLimits: the "namespace/claim" of its persistentVolumeClaim volumes (interned; what
+  // the ledger keeps per node), and whether this cycle counts them against the node's limits
+  std::vector<int32_t> pvc_claims;
+  bool count_vols = false;
 };
 
 struct Weights {
@@ -327,6 +336,7 @@ struct Assignment {
   std::shared_ptr<const PodAffinity> aff;          // its (anti-)affinity terms (symmetric rule, scoring)
   uint64_t aff_hash = 0;                           // its AffSet's bucket (aff_sets_)
   std::vector<HostPort> host_ports;                // NodePorts: the host ports it holds on the node
+  std::vector<int32_t> pvc_claims;                 // NodeVolumeLimits: the PVC claims it mounts
 };
 
 struct CycleResult {
@@ -413,6 +423,13 @@ class Engine {
   // (not a host port: never conflicts)
   bool host_port(int64_t port, const std::string& protocol, const std::string& ip, HostPort* out);
   bool ports_free(const PodReq& req, const Node& n) const;
+  // NodeVolumeLimits: a claim's volume — (CSI driver, unique volume id) of its bound CSI PV, or
+  // (provisioner, "<provisioner>/<namespace>/<claim>") while a provisioning StorageClass binds
+  // it; claims without one are absent (plugins/volumes.py::claim_volume)
+  void set_claim_volume(int32_t claim, int32_t driver, int32_t handle) { claim_vol_[claim] = {driver, handle}; }
+  void clear_claim_volume(int32_t claim) { claim_vol_.erase(claim); }
+  void set_node_vol_limits(int32_t idx, std::vector<std::pair<int32_t, int64_t>> limits);
+  bool vols_fit(const PodReq& req, const Node& n) const;
 
   // ---- cluster state
   int32_t upsert_node(const std::string& name);      // returns index (stable)
@@ -626,6 +643,7 @@ class Engine {
   int pct_nodes_ = 0;
   int32_t unsched_key_ = 0;
   int32_t any_ip_ = 0, tcp_ = 0;      // interned "0.0.0.0" / "TCP" (NodePorts sanitize)
+  std::unordered_map<int32_t, std::pair<int32_t, int32_t>> claim_vol_;   // claim → (driver, volume id)
   std::vector<Node> nodes_;
   std::vector<int32_t> free_slots_;
   uint32_t gen_counter_ = 0;

@@ -24,7 +24,7 @@ const char* const kReasonName[] = {"OK", "NodeUnschedulable", "NodeName", "Taint
                                          "GpuClock", "GpuFit", "NodeGone", "NodeResourcesFitExtended",
                                          "PodTopologySpread", "PodTopologySpreadLabel", "InterPodAffinityExisting",
                                          "InterPodAffinity", "InterPodAntiAffinity", "NodePorts", "VolumeBinding",
-                                         "VolumeZone"};
+                                         "VolumeZone", "NodeVolumeLimits"};
 static_assert(sizeof(kReasonName) / sizeof(kReasonName[0]) == RS_NUM, "kReasonName must name every engine Reason");
 const char* reason_text(int i) {
   switch (i) {
@@ -48,6 +48,7 @@ const char* reason_text(int i) {
     case RS_NODE_PORTS: return "node(s) didn't have free ports for the requested pod ports";
     case RS_VOLUME_NODE: return "node(s) had volume node affinity conflict";
     case RS_VOLUME_ZONE: return "node(s) had no available volume zone";
+    case RS_VOLUME_LIMITS: return "node(s) exceed max volume count";
     default: return i >= 0 && i < RS_NUM ? kReasonName[i] : "unknown";
   }
 }
@@ -1029,6 +1030,8 @@ bool Lane::make_req(const yk::PodProj& p, PodReq* r) {
   HostPort hp;
   for (const auto& x : p.ports)
     if (eng_->host_port(x.host_port, x.protocol, x.host_ip, &hp)) r->host_ports.push_back(hp);
+  for (size_t i = 0; i < p.claims.size(); ++i)   // the ledger keeps every pod's PVC claims (NodeVolumeLimits)
+    if (i < p.claim_pvc.size() && p.claim_pvc[i]) r->pvc_claims.push_back(eng_->intern(p.ns + "/" + p.claims[i]));
   if (p.has_owner) {
     r->owner_kind = p.owner_api == "v1" && p.owner_kind == "ReplicationController" ? 1
                     : p.owner_api == "apps/v1" && p.owner_kind == "ReplicaSet"  ? 2
@@ -1153,6 +1156,7 @@ void Lane::engine_step(Run& r) {
       r.ok[k] = 0;
     }
     if (k < r.vol_ok.size() && !r.vol_ok[k]) r.ok[k] = 0;   // a claim left the table meanwhile
+    if (r.ok[k] && r.pr.vol_limits && !r.reqs[k].pvc_claims.empty()) r.reqs[k].count_vols = true;
     if (r.ok[k] && k < r.vols.size()) {
       // VolumeBinding then VolumeZone (upstream's filter order, the hybrid runner's too), as
       // engine filters; the aliasing pointers keep each claim's constraints alive

@@ -139,6 +139,7 @@ class Lane : public yk::PodSink {
     // VolumeBinding / VolumeZone are enabled: a bound claim's PV node affinity / zone labels
     // (the claim table's constraints) are engine filters of the pod's cycle
     bool vol_node = false, vol_zone = false;
+    bool vol_limits = false;   // NodeVolumeLimits is enabled: the pods' PVC volumes count against CSI limits
     EngineConfig cfg;
   };
   // What VolumeBinding and VolumeZone check of one bound claim (plugins/volumes.py::claim_lane):

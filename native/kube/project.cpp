@@ -658,10 +658,12 @@ void project_generic(N pod, PodProj& p) {
         flags |= PF_CLAIMS;
         N cn = pvc.obj() ? pvc.get("claimName") : N{};
         p.claims.emplace_back(!cn ? std::string() : cn.str_t() ? std::string(cn.str()) : std::string("\x01"));
+        p.claim_pvc.push_back(1);
       } else if (v.get("ephemeral")) {
         flags |= PF_CLAIMS;
         N vn = v.get("name");
         p.claims.emplace_back(vn && !vn.str_t() ? std::string("\x01") : p.name + "-" + std::string(vn ? vn.str() : ""));
+        p.claim_pvc.push_back(0);
       } else {
         for (const char* d : kDisks)
           if (v.get(d)) {
@@ -1074,6 +1076,7 @@ void merge_non_identity(PodProj& d, PodProj&& s) {
   d.anti_pref = std::move(s.anti_pref);
   d.flags = s.flags;
   d.claims = std::move(s.claims);
+  d.claim_pvc = std::move(s.claim_pvc);
   d.spec_meta_hash = s.spec_meta_hash;
   d.ok = s.ok;
   d.has_sched_cond = s.has_sched_cond;

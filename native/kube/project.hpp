@@ -67,6 +67,7 @@ struct PodProj {
   // claimName, a generic ephemeral volume's "<pod>-<volume>"; "\x01" for a name that is not a
   // string (it names no PersistentVolumeClaim the lane could call inert)
   std::vector<std::string> claims;
+  std::vector<char> claim_pvc;      // per claim: 1 a persistentVolumeClaim volume, 0 an ephemeral one
   uint64_t spec_meta_hash = 0;      // upstream isPodUpdated: spec + metadata minus volatile fields
   // structural hash of metadata.labels (0: unknown). Set by the full projection and by the
   // watch identity scanner too, so a light event tells whether a pod's labels changed

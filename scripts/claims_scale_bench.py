@@ -16,7 +16,7 @@ from yoda_scheduler_amd.plugins.volumes import LaneClaims, lane_claims
 
 class H:
     def __init__(self, n):
-        self.objs = {"persistentvolumeclaims": {}, "persistentvolumes": {}, "csinodes": {}}
+        self.objs = {"persistentvolumeclaims": {}, "persistentvolumes": {}, "csinodes": {}, "storageclasses": {}}
         self.gen = collections.Counter()
         self.cache = SimpleNamespace(csi_limit_drivers={})
         for i in range(n):

@@ -571,3 +571,79 @@ def test_reason_names_cover_every_engine_reason():
     feasible, reasons = eng.feasible_nodes(pod_req(eng, p), [])
     assert feasible == [] and len(reasons) == len(C.REASONS)
     assert reasons[C.REASONS.index("NodePorts")] == 1
+
+
+# ============================================================== NodeVolumeLimits (CSI)
+from yoda_scheduler_amd.plugins.volumes import NodeVolumeLimits, claim_volumes, node_csi_limits  # noqa: E402
+
+
+class _VolHandle:
+    def __init__(self, cache, objs):
+        self.cache, self.objs = cache, objs
+
+    def lister(self, res):
+        return self.objs.get(res, {})
+
+
+@settings(max_examples=250, deadline=None)
+@given(st.lists(st.fixed_dictionaries({}, optional={"nfs": st.integers(0, 3), "ebs": st.integers(0, 3)}),
+                min_size=1, max_size=3),
+       st.lists(st.fixed_dictionaries({}, optional={"nfs": st.integers(0, 3)}), min_size=0, max_size=3),
+       st.lists(st.tuples(st.sampled_from(["nfs", "ebs", "local"]), st.integers(0, 4), st.booleans()),
+                min_size=1, max_size=6),
+       st.lists(st.tuples(st.integers(0, 2), st.lists(st.integers(0, 5), max_size=3)), max_size=6),
+       st.lists(st.integers(0, 5), min_size=1, max_size=3), st.integers(0, 6))
+def test_csi_attach_limits_native_equal_python(alloc_limits, csinode_limits, claims, bound, mine, drop):
+    """Engine NodeVolumeLimits (the ledger's PVC claims per node, each claim's CSI volume, the
+    node's per-driver limits) ≡ the Python plugin: unique volumes per limited driver, bound CSI
+    PVs by volumeHandle, unbound claims by their provisioner, non-CSI and missing claims not
+    counted; node allocatable limits overridden by CSINode counts; after releases too."""
+    nodes = []
+    for i, lims in enumerate(alloc_limits):
+        nodes.append(node_obj(f"n{i}", alloc={f"attachable-volumes-csi-{d}.csi": str(v) for d, v in lims.items()}))
+    eng, cache = cache_with(nodes)
+    eng.filters = 0
+    objs = {"persistentvolumeclaims": {}, "persistentvolumes": {}, "storageclasses": {
+        "dyn": {"metadata": {"name": "dyn"}, "provisioner": "ebs.csi"}}, "csinodes": {}}
+    for i, lims in enumerate(csinode_limits[:len(nodes)]):
+        objs["csinodes"][f"n{i}"] = {"metadata": {"name": f"n{i}"}, "spec": {"drivers": [
+            {"name": f"{d}.csi", "allocatable": {"count": v}} for d, v in lims.items()]}}
+    for j, (kind, handle, bound_pv) in enumerate(claims):
+        spec = {"storageClassName": "dyn"}
+        if bound_pv:
+            pv_spec = {"csi": {"driver": f"{kind}.csi", "volumeHandle": f"h{handle}"}} if kind != "local" else \
+                {"local": {"path": "/mnt"}}
+            objs["persistentvolumes"][f"pv{j}"] = {"metadata": {"name": f"pv{j}"}, "spec": pv_spec}
+            spec["volumeName"] = f"pv{j}"
+        objs["persistentvolumeclaims"][f"default/c{j}"] = {"metadata": {"name": f"c{j}", "namespace": "default"},
+                                                          "spec": spec}
+    handle = _VolHandle(cache, objs)
+    vols = claim_volumes(handle)
+    eng.set_claim_volumes([(k, d, h) for k, (d, h) in vols.items()], [])
+    for n in cache.nodes:
+        eng.set_node_vol_limits(eng.node_index(n), sorted(
+            (node_csi_limits(cache.nodes[n].obj, objs["csinodes"].get(n)) or {}).items()))
+
+    def vols_of(idx):
+        return [{"name": f"v{k}", "persistentVolumeClaim": {"claimName": f"c{c % len(claims)}"}}
+                for k, c in enumerate(idx)]
+    uids = []
+    for j, (k, idx) in enumerate(bound):
+        uid = f"b{j}-{next(_uid)}"
+        cache.add_pod({"metadata": {"name": f"b{j}", "namespace": "default", "uid": uid},
+                       "spec": {"nodeName": f"n{k % len(nodes)}", "volumes": vols_of(idx),
+                                "containers": [{"name": "c"}]}})
+        uids.append(uid)
+    for uid in uids[:drop]:
+        cache.remove_pod(uid)
+    pl = NodeVolumeLimits({}, handle)
+    p = pod("p", volumes=vols_of(mine), containers=[{"name": "c"}])
+    req = pod_req(eng, p)
+    from yoda_scheduler_amd.plugins.volumes import pvc_claim_keys
+    eng.set_req_claims(req, pvc_claim_keys(p), True)
+    reason = C.REASONS.index("NodeVolumeLimits")
+    for n in sorted(cache.nodes):
+        want = pl.filter(CycleState(), p, n).is_success()
+        got = eng.filter_node(req, eng.node_index(n))
+        assert got in (0, reason)
+        assert (got == 0) == want, (n, alloc_limits, csinode_limits, claims, bound, mine, drop)

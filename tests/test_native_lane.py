@@ -992,35 +992,52 @@ def test_zonal_and_pinned_claims_fit_errors_match_across_paths():
     assert on == off, (on, off)
 
 
-def test_attach_limit_counts_lane_pods_once_their_claims_stop_being_inert():
-    """Lane pods may hold claims (inert ones). When an attach limit appears, the claims stop
-    being inert and NodeVolumeLimits applies to new CSI pods on the Python path; its count of
-    the volumes already attached on the node must include the lane's pods (PF_CLAIMS left the
-    lane's never-flags, so the cycle reads a mirror of the lane)."""
+@pytest.mark.parametrize("lane", ["on", "off"])
+def test_csi_attach_limits_count_every_pod_on_the_node_on_both_paths(lane):
+    """NodeVolumeLimits on the lane: the engine ledger keeps every pod's PVC claims per node and
+    counts their CSI volumes (unique per driver) against the node's limit — a CSINode count that
+    appears after two pods attached two volumes. A third volume does not fit; a pod on an
+    already attached volume does. The Python path (lane off) decides the same, with the same
+    FitError."""
     async def go():
-        async with Env(nodes=(("n1", 8, None),)) as e:
+        async with Env(lane=lane, nodes=(("n1", 8, None),)) as e:
             nl = e.sched.lane
             for i in range(3):
                 await e.cl.create("persistentvolumes", _csi_pv(f"pv-{i}"))
                 await e.cl.create("persistentvolumeclaims", _bound_pvc(f"d{i}", f"pv-{i}"))
-            assert await e.wait(lambda: {"default/d0", "default/d1", "default/d2"} <= nl._claims)
+            if nl is not None:
+                assert await e.wait(lambda: {"default/d0", "default/d1", "default/d2"} <= nl._claims)
+            else:
+                await asyncio.sleep(0.3)
             await e.create(_claim_pod("l0", "d0"))
             await e.create(_claim_pod("l1", "d1"))
             assert await e.wait(lambda: e.sched.scheduled == 2)
-            on_lane = nl.lane.scheduled
             await e.cl.create("csinodes", {"metadata": {"name": "n1"}, "spec": {"drivers": [
                 {"name": "nfs.csi.k8s.io", "nodeID": "n1", "allocatable": {"count": 2}}]}})
-            assert await e.wait(lambda: not nl._claims)
+            await asyncio.sleep(0.3)
             await e.create(_claim_pod("p2", "d2"))            # a third volume: over the limit of 2
             await e.create(_claim_pod("p0", "d0"))            # d0 is attached already: fits
             assert await e.wait(lambda: e.sched.scheduled == 3)
-            await asyncio.sleep(0.5)
-            pods = await e.pods()
-            return on_lane, pods["p2"]["spec"].get("nodeName", ""), pods["p0"]["spec"].get("nodeName", ""), \
-                e.sched.scheduled
-    on_lane, p2, p0, total = run(go())
-    assert on_lane == 2
-    assert p2 == "" and p0 == "n1" and total == 3
+
+            def msg(p):
+                for c in (p.get("status") or {}).get("conditions") or []:
+                    if c.get("type") == "PodScheduled" and c.get("status") == "False":
+                        return c.get("message", "")
+                return ""
+            pods = {}
+            for _ in range(100):
+                pods = await e.pods()
+                if msg(pods["p2"]):
+                    break
+                await asyncio.sleep(0.02)
+            admitted = nl.lane.stats()["admitted"] if nl is not None else None
+            return pods["p2"]["spec"].get("nodeName", ""), msg(pods["p2"]), pods["p0"]["spec"].get("nodeName", ""), \
+                e.sched.scheduled, admitted
+    p2, p2_msg, p0, total, admitted = run(go())
+    assert p2 == "" and "exceed max volume count" in p2_msg
+    assert p0 == "n1" and total == 3
+    if lane == "on":
+        assert admitted == 4                  # all four on the lane: the engine counted
 
 
 def _mixed_pods(seed):

@@ -231,11 +231,12 @@ def test_incremental_claim_table_equals_a_full_recompute():
     import random
     from types import SimpleNamespace
 
-    from yoda_scheduler_amd.plugins.volumes import LaneClaims, lane_claims
+    from yoda_scheduler_amd.plugins.volumes import LaneClaims, claim_volumes, lane_claims
 
     class H:
         def __init__(self):
-            self.objs = {"persistentvolumeclaims": {}, "persistentvolumes": {}, "csinodes": {}}
+            self.objs = {"persistentvolumeclaims": {}, "persistentvolumes": {}, "csinodes": {}, "storageclasses": {
+                "shared": {"metadata": {"name": "shared"}, "provisioner": "nfs.csi.k8s.io"}}}
             self.gen = collections.Counter()
             self.cache = SimpleNamespace(csi_limit_drivers={})
 
@@ -270,6 +271,11 @@ def test_incremental_claim_table_equals_a_full_recompute():
                               csi=rng.random() < 0.7, ebs=rng.random() < 0.1)
                     h.objs["persistentvolumes"][name] = obj
                 t.pv_event(obj)
+            elif op < 0.85:
+                prov = rng.choice(["nfs.csi.k8s.io", "kubernetes.io/no-provisioner", "ebs.csi.aws.com"])
+                obj = {"metadata": {"name": "shared"}, "provisioner": prov}
+                h.objs["storageclasses"]["shared"] = obj
+                t.sc_event(obj)
             elif op < 0.9:
                 h.gen["csinodes"] += 1
                 h.objs["csinodes"] = {} if rng.random() < 0.5 else {"n0": {"metadata": {"name": "n0"}, "spec": {
@@ -277,11 +283,13 @@ def test_incremental_claim_table_equals_a_full_recompute():
                                  "allocatable": {"count": 4}}]}}}
             else:
                 h.cache.csi_limit_drivers = rng.choice([{}, {}, {"nfs.csi.k8s.io": 1}, {"ebs.csi.aws.com": 2}])
-            before = dict(t.table)
-            full, changed, removed = t.refresh()
+            before, vbefore = dict(t.table), dict(t.vols)
+            full, changed, removed, vfull, vchanged, vremoved = t.refresh()
             assert t.table == lane_claims(h), (seed, _step)
+            assert t.vols == claim_volumes(h), (seed, _step)
             if full is None:
                 assert {**{k: v for k, v in before.items() if k not in removed}, **changed} == t.table
-                assert not (set(changed) & removed)
+                assert {**{k: v for k, v in vbefore.items() if k not in vremoved}, **vchanged} == t.vols
+                assert not (set(changed) & removed) and not (set(vchanged) & vremoved)
             adds, removes = adds + len(changed), removes + len(removed)
     assert adds > 20 and removes > 20             # the sequences move claims both ways

@@ -71,6 +71,8 @@ class NativeLane:
         self._sticky_never = (1 << 62) - 1  # AND of the masks of profiles eligible since the lane last owned nothing
         self._inert = None                 # plugins/volumes.py::LaneClaims, made on first use
         self._claims = frozenset()         # the claims the lane may admit (the table's keys)
+        self._limits_dirty: Optional[set] = None   # nodes whose CSI attach limits to push (None: all)
+        self._limits: dict = {}            # node → the CSI limits pushed to the engine
         sched.queue.on_move_all = self._move_all
 
     # ------------------------------------------------------------------ lifecycle
@@ -167,24 +169,54 @@ class NativeLane:
             filters = {p.name for p in fw.filter_py}
             want = (m is not None, m or 0, bool(fw.filter_mask & f_yoda), self.preempt_above(fw),
                     fw.gate_terms() + self._temp_terms if m is not None else (), c_ok,
-                    "VolumeBinding" in filters, "VolumeZone" in filters)
+                    "VolumeBinding" in filters, "VolumeZone" in filters, "NodeVolumeLimits" in filters)
             if self._profiles.get(name) == want:
                 continue
             s._activate(fw)                    # the lane snapshots the engine config now applied
             self.lane.set_profile(s.engine, name, want[0], want[1], want[2], want[3], list(want[4]), want[5],
-                                  want[6], want[7])
+                                  want[6], want[7], want[8])
             self._profiles[name] = want
             log.info("native lane: profile %s %s (flag mask %#x)", name, "on" if want[0] else "off", want[1])
         s.cache.lane_never_flags = never & self._sticky_never
 
     def claims_event(self, res: str, obj: dict) -> None:
-        """A PVC / PV changed: its claims are re-evaluated on the next refresh (O(change))."""
+        """A PVC / PV / StorageClass / CSINode changed: what it affects is re-evaluated on the next
+        refresh (O(change); a StorageClass re-evaluates every claim)."""
+        if res == "csinodes":
+            self.node_event((obj.get("metadata") or {}).get("name", ""))
+            return
         if self._inert is None:
             return
         if res == "persistentvolumeclaims":
             self._inert.pvc_event(obj)
         elif res == "persistentvolumes":
             self._inert.pv_event(obj)
+        elif res == "storageclasses":
+            self._inert.sc_event(obj)
+
+    def node_event(self, name: str) -> None:
+        """A node (or its CSINode) changed: its CSI attach limits are pushed on the next refresh."""
+        if self._limits_dirty is not None:
+            self._limits_dirty.add(name)
+
+    def _push_limits(self) -> None:
+        """The nodes' CSI attach limits (plugins/volumes.py::node_csi_limits) to the engine, which
+        counts lane pods' PVC volumes against them (NodeVolumeLimits)."""
+        from ..plugins.volumes import node_csi_limits
+        s = self.s
+        dirty, self._limits_dirty = self._limits_dirty, set()
+        names = set(s.cache.nodes) | set(self._limits) if dirty is None else dirty
+        csinodes = s.handle.lister("csinodes")
+        for name in names:
+            info = s.cache.nodes.get(name)
+            idx = s.engine.node_index(name) if info is not None else -1
+            if idx < 0:
+                self._limits.pop(name, None)
+                continue
+            lim = node_csi_limits(info.obj, csinodes.get(name)) or {}
+            if self._limits.get(name, {}) != lim or dirty is None:
+                s.engine.set_node_vol_limits(idx, sorted(lim.items()))
+                self._limits[name] = lim
 
     def _refresh_claims(self) -> set:
         """Keep the lane's claim table (plugins/volumes.py::LaneClaims) current: the claims a pod
@@ -197,7 +229,11 @@ class NativeLane:
         if self._inert is None:
             from ..plugins.volumes import LaneClaims
             self._inert = LaneClaims(s.handle)
-        full, changed, removed = self._inert.refresh()
+        if self._limits_dirty is None or self._limits_dirty:
+            self._push_limits()
+        full, changed, removed, vfull, vchanged, vremoved = self._inert.refresh()
+        if vchanged or vremoved:                 # before the table: a pod admitted next counts them
+            s.engine.set_claim_volumes([(k, d, h) for k, (d, h) in sorted(vchanged.items())], sorted(vremoved))
         if full is not None:
             self.lane.update_claims(s.engine, True, [_claim_item(k, v) for k, v in sorted(full.items())], [])
         elif changed or removed:

@@ -485,11 +485,15 @@ class Scheduler:
 
     def on_node_add(self, obj: dict) -> None:
         self.cache.add_node(obj)
+        if self.lane is not None:
+            self.lane.node_event((obj.get("metadata") or {}).get("name", ""))
         self.queue.move_all_to_active_or_backoff("NodeAdd")
         self._lane_refresh()
 
     def on_node_update(self, old: dict, new: dict) -> None:
         self.cache.update_node(new)
+        if self.lane is not None:
+            self.lane.node_event((new.get("metadata") or {}).get("name", ""))
         self._lane_refresh()
         if old.get("spec") != new.get("spec") or (old.get("metadata") or {}).get("labels") != \
                 (new.get("metadata") or {}).get("labels") or (old.get("status") or {}).get("allocatable") != \
@@ -498,6 +502,8 @@ class Scheduler:
 
     def on_node_delete(self, obj: dict) -> None:
         self.cache.remove_node(obj["metadata"]["name"])
+        if self.lane is not None:
+            self.lane.node_event(obj["metadata"]["name"])
         self._lane_refresh()
 
     def on_scv(self, obj: dict) -> None:

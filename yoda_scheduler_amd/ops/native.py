@@ -10,7 +10,7 @@ import importlib
 import threading
 import weakref
 
-from ..models.pod import NodeInfo, PodInfo
+from ..models.pod import PF_CLAIMS, NodeInfo, PodInfo
 from ..models.scv import HEALTHY, LazyLinks, LazyScv, Scv
 
 _lock = threading.Lock()
@@ -223,7 +223,7 @@ def pod_req(engine, pi: PodInfo):
         return pi.native_req
     key = None
     if not (pi.node_name or pi.node_selector or pi.required_terms or pi.preferred_terms or pi.tolerations
-            or pi.ext or pi.spread or pi.pod_aff or pi.host_ports):
+            or pi.ext or pi.spread or pi.pod_aff or pi.host_ports or pi.flags & PF_CLAIMS):
         key = (pi.gpu, pi.cpu_m, pi.mem, pi.nz_cpu_m, pi.nz_mem, pi.namespace, tuple(pi.labels.items()),
                tuple(pi.images), pi.containers, pi.owner, pi.avoid, pi.deleting)
         shared = _shared_reqs
@@ -243,6 +243,10 @@ def pod_req(engine, pi: PodInfo):
     if pi.host_ports:
         from ..plugins.defaults import host_port_set
         engine.set_req_ports(r, [(port, proto, ip) for ip, proto, port in sorted(host_port_set(pi.host_ports))])
+    if pi.flags & PF_CLAIMS:
+        # the ledger keeps every pod's PVC claims per node: the lane's NodeVolumeLimits counts them
+        from ..plugins.volumes import pvc_claim_keys
+        engine.set_req_claims(r, pvc_claim_keys(pi), False)
     pi.native_req, pi.native_owner = r, engine
     if key is not None:
         cache = _shared_reqs[1]

@@ -617,17 +617,20 @@ def claim_inert(pvc: dict, pvs: dict, limited: set) -> bool:
     no attach limit on any node (``limited``: the drivers that have one). A pod whose claims
     are all inert is a no-op for VolumeBinding, VolumeZone, NodeVolumeLimits and the in-tree
     limits (each claim satisfies the per-claim half of their ``is_noop_for``)."""
-    return claim_lane(pvc, pvs, limited) is None
+    if claim_lane(pvc, pvs) is not None:
+        return False
+    csi = (pvs[pvc["spec"]["volumeName"]].get("spec") or _EMPTY).get("csi")
+    return not (csi and csi.get("driver", "") in limited)
 
 
 NOT_LANE = "not-lane"                     # claim_lane: the claim needs the Python volume plugins
 _LANE_NODE_OPS = ("In", "NotIn", "Exists", "DoesNotExist")
 
 
-def claim_lane(pvc: dict, pvs: dict, limited: set):
+def claim_lane(pvc: dict, pvs: dict):
     """What the native lane needs to run a pod that mounts this claim: ``NOT_LANE`` when the
     claim needs the Python volume plugins, else the constraints its bound PV puts on nodes —
-    None (an inert claim, ``claim_inert``) or ``(node_terms | None, zone_terms | None)``:
+    None or ``(node_terms | None, zone_terms | None)``:
 
     * ``node_terms`` — the PV's ``nodeAffinity.required`` (VolumeBinding's filter for a bound
       claim: any term matches; a term without requirements matches nothing), only with the
@@ -635,8 +638,8 @@ def claim_lane(pvc: dict, pvs: dict, limited: set):
     * ``zone_terms`` — VolumeZone's filter as two OR'ed terms: the node has none of the zone /
       region labels, or it has every label the PV has with a value the PV allows ("__"-separated).
 
-    A lane-able claim is not being deleted, is bound to a PV that exists, has no in-tree
-    attachable disk, and is not a CSI volume whose driver some node limits (``limited``)."""
+    A lane-able claim is not being deleted, is bound to a PV that exists and has no in-tree
+    attachable disk. CSI attach limits are counted by the engine (``claim_volume``)."""
     if (pvc.get("metadata") or _EMPTY).get("deletionTimestamp"):
         return NOT_LANE
     name = (pvc.get("spec") or _EMPTY).get("volumeName", "")
@@ -645,9 +648,6 @@ def claim_lane(pvc: dict, pvs: dict, limited: set):
         return NOT_LANE
     ps = pv.get("spec") or _EMPTY
     if any(ps.get(k) for k in _ATTACHABLE_KINDS):
-        return NOT_LANE
-    csi = ps.get("csi")
-    if csi and csi.get("driver", "") in limited:
         return NOT_LANE
     node = None
     req = (ps.get("nodeAffinity") or _EMPTY).get("required")
@@ -684,10 +684,10 @@ def limited_drivers(handle) -> set:
 def lane_claims(handle) -> dict:
     """The claim table over the whole PVC lister: key ("namespace/name") → ``claim_lane``
     value, for every lane-able claim."""
-    pvs, limited = handle.lister("persistentvolumes"), limited_drivers(handle)
+    pvs = handle.lister("persistentvolumes")
     out = {}
     for key, pvc in handle.lister("persistentvolumeclaims").items():
-        v = claim_lane(pvc, pvs, limited)
+        v = claim_lane(pvc, pvs)
         if v is not NOT_LANE:
             out[key] = v
     return out
@@ -695,26 +695,84 @@ def lane_claims(handle) -> dict:
 
 def inert_claims(handle) -> set:
     """Every inert claim ("namespace/name", ``claim_inert``) of the PVC lister."""
-    return {k for k, v in lane_claims(handle).items() if v is None}
+    pvs, limited = handle.lister("persistentvolumes"), limited_drivers(handle)
+    return {k for k, pvc in handle.lister("persistentvolumeclaims").items() if claim_inert(pvc, pvs, limited)}
+
+
+def claim_volume(key: str, pvc: dict, pvs: dict, scs: dict) -> Optional[tuple]:
+    """(driver, unique volume id) NodeVolumeLimits counts for a pod volume on this claim
+    (``_pod_ids``): a bound CSI PV's (driver, "<driver>/<volumeHandle>"); with no PV yet and a
+    provisioning StorageClass, (provisioner, "<provisioner>/<namespace>/<claim>"); else None."""
+    spec = pvc.get("spec") or _EMPTY
+    name = spec.get("volumeName", "")
+    pv = pvs.get(name) if name else None
+    if pv is not None:
+        csi = (pv.get("spec") or _EMPTY).get("csi")
+        if csi:
+            d = csi.get("driver", "")
+            return d, f"{d}/{csi.get('volumeHandle', '')}"
+        return None
+    scn = spec.get("storageClassName", "")
+    sc = scs.get(scn) if scn else None
+    if sc is not None and sc.get("provisioner", NO_PROVISIONER) != NO_PROVISIONER:
+        d = sc["provisioner"]
+        return d, f"{d}/{key}"
+    return None
+
+
+def claim_volumes(handle) -> dict:
+    """``claim_volume`` of every PVC of the lister that has one."""
+    pvs, scs = handle.lister("persistentvolumes"), handle.lister("storageclasses")
+    out = {}
+    for key, pvc in handle.lister("persistentvolumeclaims").items():
+        v = claim_volume(key, pvc, pvs, scs)
+        if v is not None:
+            out[key] = v
+    return out
+
+
+def node_csi_limits(node_obj: Optional[dict], csinode: Optional[dict]) -> dict:
+    """NodeVolumeLimits._limits: attach limits per CSI driver from the node's allocatable
+    (``attachable-volumes-csi-<driver>``), overridden by its CSINode's ``allocatable.count``.
+    None when a value is not an integer (the Python plugin decides there)."""
+    out = {}
+    try:
+        alloc = ((node_obj or _EMPTY).get("status") or _EMPTY).get("allocatable") or _EMPTY
+        for k, v in alloc.items():
+            if k.startswith("attachable-volumes-csi-"):
+                out[k[len("attachable-volumes-csi-"):]] = int(v)
+        for d in ((csinode or _EMPTY).get("spec") or _EMPTY).get("drivers") or ():
+            cnt = (d.get("allocatable") or _EMPTY).get("count")
+            if cnt is not None:
+                out[d.get("name", "")] = int(cnt)
+    except (TypeError, ValueError, AttributeError):
+        return None
+    return out
+
+
+def pvc_claim_keys(pod) -> list:
+    """"namespace/claim" of a pod's persistentVolumeClaim volumes (what NodeVolumeLimits counts
+    of it: ``_pod_ids`` skips ephemeral volumes)."""
+    return [f"{pod.namespace}/{(v['persistentVolumeClaim'] or _EMPTY).get('claimName', '')}"
+            for v in _volumes(pod) if "persistentVolumeClaim" in v]
 
 
 class LaneClaims:
-    """The native lane's claim table (``lane_claims``) kept up to date per event instead of
-    recomputed over every PVC: a PVC event re-evaluates that claim, a PV event the claims
-    bound to it (an index PV name → claim keys), and a change of the cluster's attach limits
-    (CSINode counts, node allocatable) all of them. ``refresh`` returns (whole table | None,
-    {added or changed key: value}, {removed keys}) since the last call."""
+    """The native lane's claim table (``lane_claims``) and the engine's claim volumes
+    (``claim_volumes``) kept up to date per event instead of recomputed over every PVC: a PVC
+    event re-evaluates that claim, a PV event the claims bound to it (an index PV name → claim
+    keys), a StorageClass event all of them. ``refresh`` returns the changes since the last
+    call: ``(table | None, changed, removed, volumes | None, volumes changed, volumes removed)``
+    — a whole table instead of None on the first call and after a StorageClass event."""
 
     def __init__(self, handle) -> None:
         self.handle = handle
         self.table: dict = {}
+        self.vols: dict = {}
         self._pv_of: dict[str, str] = {}          # claim key → the PV name it is bound to
         self._claims_of: dict[str, set] = {}      # PV name → claim keys bound to it
         self._dirty: set = set()
         self._all = True                          # first refresh: every claim
-        self._limited: Optional[frozenset] = None
-        self._csinode_gen = -1
-        self._csinode_drivers: set = set()
 
     @property
     def keys(self):
@@ -726,6 +784,9 @@ class LaneClaims:
 
     def pv_event(self, obj: dict) -> None:
         self._dirty |= self._claims_of.get((obj.get("metadata") or _EMPTY).get("name", ""), set())
+
+    def sc_event(self, obj: dict) -> None:
+        self._all = True
 
     def _index(self, key: str, pv: str) -> None:
         old = self._pv_of.get(key)
@@ -743,43 +804,51 @@ class LaneClaims:
         else:
             self._pv_of.pop(key, None)
 
+    @staticmethod
+    def _diff(old: dict, new: dict) -> tuple:
+        return {k: v for k, v in new.items() if old.get(k, NOT_LANE) != v}, set(old) - set(new)
+
     def refresh(self):
         h = self.handle
-        gen = h.generation("csinodes") if hasattr(h, "generation") else -2
-        if gen != self._csinode_gen or gen == -2:
-            self._csinode_gen = gen
-            self._csinode_drivers = _csinode_drivers(h.lister("csinodes"))
-        limited = frozenset(self._csinode_drivers | set(getattr(h.cache, "csi_limit_drivers", ())))
-        if limited != self._limited:
-            self._limited, self._all = limited, True
-        pvcs, pvs = h.lister("persistentvolumeclaims"), h.lister("persistentvolumes")
+        pvcs, pvs, scs = h.lister("persistentvolumeclaims"), h.lister("persistentvolumes"), h.lister("storageclasses")
         if self._all:
             self._all, self._dirty = False, set()
             self._pv_of, self._claims_of = {}, {}
-            table = {}
+            table, vols = {}, {}
             for key, pvc in pvcs.items():
                 self._index(key, (pvc.get("spec") or _EMPTY).get("volumeName", "") or "")
-                v = claim_lane(pvc, pvs, limited)
+                v = claim_lane(pvc, pvs)
                 if v is not NOT_LANE:
                     table[key] = v
-            changed = {k: v for k, v in table.items() if k not in self.table or self.table[k] != v}
-            removed = set(self.table) - set(table)
-            self.table = table
-            return table, changed, removed
-        changed, removed = {}, set()
+                cv = claim_volume(key, pvc, pvs, scs)
+                if cv is not None:
+                    vols[key] = cv
+            changed, removed = self._diff(self.table, table)
+            vchanged, vremoved = self._diff(self.vols, vols)
+            self.table, self.vols = table, vols
+            return table, changed, removed, vols, vchanged, vremoved
+        changed, removed, vchanged, vremoved = {}, set(), {}, set()
         dirty, self._dirty = self._dirty, set()
         for key in dirty:
             pvc = pvcs.get(key)
             self._index(key, ((pvc.get("spec") or _EMPTY).get("volumeName", "") or "") if pvc is not None else "")
-            v = NOT_LANE if pvc is None else claim_lane(pvc, pvs, limited)
+            v = NOT_LANE if pvc is None else claim_lane(pvc, pvs)
             if v is NOT_LANE:
                 if key in self.table:
                     del self.table[key]
                     removed.add(key)
-            elif key not in self.table or self.table[key] != v:
+            elif self.table.get(key, NOT_LANE) != v:
                 self.table[key] = v
                 changed[key] = v
-        return None, changed, removed
+            cv = None if pvc is None else claim_volume(key, pvc, pvs, scs)
+            if cv is None:
+                if key in self.vols:
+                    del self.vols[key]
+                    vremoved.add(key)
+            elif self.vols.get(key) != cv:
+                self.vols[key] = cv
+                vchanged[key] = cv
+        return None, changed, removed, None, vchanged, vremoved
 
 
 # the in-tree attach-limit plugins' volume kinds (what _VolFacts resolves for them)
