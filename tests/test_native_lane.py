@@ -1072,9 +1072,12 @@ def _mixed_pods(seed):
     return out
 
 
-def _mixed_placements(seed, lane):
+def _mixed_placements(seed, lane, limits=False):
     async def go():
         async with Env(lane=lane, nodes=(("n1", 8, None), ("n2", 8, None), ("n3", 8, None))) as e:
+            if limits:                                  # n1 attaches one NFS volume at most
+                await e.cl.create("csinodes", {"metadata": {"name": "n1"}, "spec": {"drivers": [
+                    {"name": "nfs.csi.k8s.io", "nodeID": "n1", "allocatable": {"count": 1}}]}})
             for i in range(2):
                 await e.cl.create("persistentvolumes", _csi_pv(f"pv-{i}"))
                 await e.cl.create("persistentvolumeclaims", _bound_pvc(f"d{i}", f"pv-{i}"))
@@ -1105,14 +1108,14 @@ def _mixed_placements(seed, lane):
     return run(go())
 
 
-@pytest.mark.parametrize("seed", range(1, 9))
-def test_lane_and_python_path_place_mixed_real_cluster_pods_alike(seed):
+@pytest.mark.parametrize("seed,limits", [(s, False) for s in range(1, 9)] + [(s, True) for s in range(1, 5)])
+def test_lane_and_python_path_place_mixed_real_cluster_pods_alike(seed, limits):
     """One pod at a time, so both paths see the same cluster: the lane (which now admits spread,
     affinity, host-port, extended-resource and PVC pods, a local PV's node affinity included)
     places every pod on the node and GPUs the Python path picks, including the pods a host-port
     conflict or the local PV's node leaves unschedulable."""
-    lane, admitted = _mixed_placements(seed, "on")
-    py, _ = _mixed_placements(seed, "off")
+    lane, admitted = _mixed_placements(seed, "on", limits)
+    py, _ = _mixed_placements(seed, "off", limits)
     assert lane == py
     assert admitted >= 20
 
