@@ -1985,7 +1985,7 @@ void Lane::record_scheduled(const Entry& e) {
     return;
   }
   const std::string& prof = e.prof >= 0 && e.prof < (int)lp_.size() ? lp_[e.prof].name : std::string();
-  ev_q_.push_back(PendingEvent{e.ev->p.ns, e.ev->p.name, e.ev->p.uid, e.node_name, prof, wall()});
+  ev_q_.push_back(PendingEvent{e.ev->p.ns, e.ev->p.name, e.ev->p.uid, e.node_name, prof, wall(), std::string()});
 }
 
 void Lane::flush_events() {

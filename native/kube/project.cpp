@@ -80,8 +80,6 @@ bool ceil_scaled(__int128 n, int e, int bin_shift, int64_t* out) {
   return true;
 }
 
-bool starts_with(std::string_view s, std::string_view p) { return s.substr(0, p.size()) == p; }
-
 bool is_basic(std::string_view k) { return k == "cpu" || k == "memory"; }
 
 // models/pod.py::normalize_image: an image without a tag or digest means ":latest"
