@@ -599,7 +599,7 @@ void Lane::handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::ve
   // lane-owned
   if (p.node.empty()) {
     const bool waiting = e->st == PARKED || e->st == BACKOFF;
-    if ((e->st == QUEUED || waiting) && ev->full().spec_meta_hash != old->full().spec_meta_hash) {
+    if ((e->st == QUEUED || waiting) && ev->hash() != old->hash()) {
       int prof = -1;
       if (!admissible(ev->full(), &prof)) {
         // no longer for the lane (a feature a Python plugin handles, another scheduler, ...)

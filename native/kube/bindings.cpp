@@ -153,7 +153,7 @@ PYBIND11_MODULE(_yoda_kube, m) {
       .def_property_readonly("scheduler", [](const PodEv& e) { return e.p.sched; })
       .def_property_readonly("phase", [](const PodEv& e) { return e.p.phase; })
       .def_property_readonly("deleting", [](const PodEv& e) { return e.p.deleting; })
-      .def_property_readonly("hash", [](const PodEv& e) { return e.full().spec_meta_hash; })
+      .def_property_readonly("hash", [](const PodEv& e) { return e.hash(); })
       .def_property_readonly("flags", [](const PodEv& e) { return e.full().flags; })
       .def_property_readonly("claims", [](const PodEv& e) { return e.full().claims; })
       .def_property_readonly("labels_hash", [](const PodEv& e) { return e.p.labels_hash; })
@@ -167,7 +167,7 @@ PYBIND11_MODULE(_yoda_kube, m) {
       .def("ident", [](const PodEv& e) {
         const PodProj& p = e.full();
         return py::make_tuple(py::str(p.ns + "/" + p.name), py::str(p.uid), py::str(p.node),
-                              py::str(p.sched), py::str(p.phase), p.spec_meta_hash);
+                              py::str(p.sched), py::str(p.phase), e.hash());
       })
       .def("raw", [](const PodEv& e) { return py::bytes(e.raw); })
       .def("info_args", [](const PodEv& e) -> py::object {
@@ -177,6 +177,15 @@ PYBIND11_MODULE(_yoda_kube, m) {
       });
 
   m.def("project", &project_bytes, py::arg("raw"), "Project a pod's JSON (tests / tooling).");
+  m.def("project_flat_nohash", [](const std::string& raw) {
+    auto pe = std::make_shared<PodEv>();
+    FlatDoc d;
+    if (!d.parse(raw)) throw py::value_error("invalid JSON");
+    project_pod_nohash(d.root(), pe->p);
+    pe->hash_of = &spec_meta_hash_of;
+    pe->raw = raw;
+    return pe;
+  }, py::arg("raw"), "As the watch stream decodes an ADDED pod with a lane attached (hash on first use).");
   m.def("project_flat", [](const std::string& raw) {
     auto pe = std::make_shared<PodEv>();
     if (!project_pod_text(raw, pe->p)) throw py::value_error("invalid JSON");
@@ -373,7 +382,7 @@ PYBIND11_MODULE(_yoda_kube, m) {
                 payload = py::cast(e.pod);
                 const PodProj& p = e.pod->full();
                 ident = py::make_tuple(py::str(p.ns + "/" + p.name), py::str(p.uid), py::str(p.node), py::str(p.sched),
-                                       py::str(p.phase), p.spec_meta_hash);
+                                       py::str(p.phase), e.pod->hash());
               } else if (e.type == 'B') {
                 payload = py::none();
               } else {

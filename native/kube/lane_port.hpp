@@ -35,6 +35,21 @@ struct PodEv {
     if (light && complete) std::call_once(once, [this] { complete(const_cast<PodEv*>(this)); });
     return p;
   }
+  // spec_meta_hash, computed from `raw` on first use when the decode skipped it (hash_pending);
+  // the decoder (the transport, in the kube module) sets the function, as it does `complete`
+  uint64_t (*hash_of)(std::string_view raw) = nullptr;
+  mutable std::once_flag hash_once;
+  uint64_t hash() const {
+    const PodProj& f = full();
+    std::call_once(hash_once, [this, &f] {
+      if (f.hash_pending && hash_of) {
+        PodProj& m = const_cast<PodProj&>(f);
+        m.spec_meta_hash = hash_of(raw);
+        m.hash_pending = false;
+      }
+    });
+    return f.spec_meta_hash;
+  }
 };
 
 struct WatchEvent {

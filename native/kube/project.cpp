@@ -334,6 +334,8 @@ uint64_t labels_hash_of(N labels) {
   return h ? h : 1;
 }
 
+thread_local bool t_skip_hash = false;   // project_pod_nohash
+
 template <class N>
 void project_generic(N pod, PodProj& p) {
   p = PodProj();
@@ -353,7 +355,8 @@ void project_generic(N pod, PodProj& p) {
   p.sched = sched.empty() ? "default-scheduler" : std::string(sched);
   p.node = std::string(sp.sv("nodeName"));
   if (N st = pod.get("status")) p.phase = std::string(st.sv("phase"));
-  p.spec_meta_hash = spec_hash(sp, meta_hash(meta));
+  if (t_skip_hash) p.hash_pending = true;
+  else p.spec_meta_hash = spec_hash(sp, meta_hash(meta));
   p.labels_hash = labels_hash_of(m.get("labels"));
   if (N st = pod.get("status"); st && st.obj()) {
     if (N cs = st.get("conditions"); cs && cs.arr()) {
@@ -708,6 +711,21 @@ void project_generic(N pod, PodProj& p) {
 void project_pod(const Value& pod, PodProj& p) { project_generic(DomN{&pod}, p); }
 
 void project_pod(const FlatDoc::View& pod, PodProj& p) { project_generic(FlatN{pod}, p); }
+
+void project_pod_nohash(const FlatDoc::View& pod, PodProj& p) {
+  t_skip_hash = true;
+  project_generic(FlatN{pod}, p);
+  t_skip_hash = false;
+}
+
+uint64_t spec_meta_hash_of(std::string_view text) {
+  FlatDoc d;
+  if (!d.parse(text)) return 0;
+  const FlatN pod{d.root()};
+  const FlatN meta = pod.get("metadata");
+  const FlatN spec = pod.get("spec");
+  return spec_hash(spec.obj() ? spec : FlatN{}, meta_hash(meta));
+}
 
 void project_identity(const FlatDoc::View& pod, PodProj& p) {
   p = PodProj();

@@ -69,6 +69,9 @@ struct PodProj {
   std::vector<std::string> claims;
   std::vector<char> claim_pvc;      // per claim: 1 a persistentVolumeClaim volume, 0 an ephemeral one
   uint64_t spec_meta_hash = 0;      // upstream isPodUpdated: spec + metadata minus volatile fields
+  // the hash was not computed (a lane-attached ADDED: the lane never compares it); PodEv::hash()
+  // computes it from the raw object on first use
+  bool hash_pending = false;
   // structural hash of metadata.labels (0: unknown). Set by the full projection and by the
   // watch identity scanner too, so a light event tells whether a pod's labels changed
   // without being projected (the lane's per-node selector census keeps the older projection)
@@ -123,6 +126,11 @@ bool quantity_scaled(const Value& q, int scale, int64_t* out);
 void project_pod(const Value& pod, PodProj& p);
 // The same projection over the flat document (the watch stream's decode path).
 void project_pod(const FlatDoc::View& pod, PodProj& p);
+// The same, without the spec / metadata hash (hash_pending): the watch stream's ADDED events
+// when a native lane is attached — the hash only serves Python's update comparisons
+void project_pod_nohash(const FlatDoc::View& pod, PodProj& p);
+// spec_meta_hash of a pod object's text (0 if it does not parse)
+uint64_t spec_meta_hash_of(std::string_view text);
 // Parse + project one pod object's JSON text; false when the text is not JSON.
 bool project_pod_text(std::string_view text, PodProj& p);
 // Identity fields only (ns, name, uid, rv, creation, deleting, scheduler, node, phase); `ok`

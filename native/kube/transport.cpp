@@ -687,6 +687,11 @@ void Transport::watch_lines(Conn* c) {
         project_identity(obj, pe->p);
         pe->light = true;
         pe->complete = &complete_pod_ev;
+      } else if (light_pods_.load(std::memory_order_relaxed)) {
+        // with a lane attached the spec / metadata hash is computed only if something compares
+        // it (PodEv::hash: Python's update check of a forwarded pod, the lane's of a queued one)
+        project_pod_nohash(obj, pe->p);
+        pe->hash_of = &spec_meta_hash_of;
       } else {
         project_pod(obj, pe->p);
       }

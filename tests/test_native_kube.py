@@ -926,3 +926,17 @@ def test_projected_claims_equal_the_volume_plugins_claim_names(vols, pod_name):
     assert len(ev.claims) == len(want)
     for got, w in zip(ev.claims, want):
         assert got == w if isinstance(w, str) else got == "\x01"
+
+
+@settings(max_examples=150, deadline=None)
+@given(_pod, st.sampled_from([{}, {"phase": "Pending"}]))
+def test_lazy_hash_of_a_lane_decoded_pod_equals_the_eager_one(pod, status):
+    """With a native lane attached the watch stream decodes ADDED pods without the spec /
+    metadata hash (only Python's update check of a forwarded pod, or the lane's of a queued one,
+    compares it); ``PodEvent.hash`` computes it from the raw object on first use — equal to the
+    eager projection's, and every other field is the same."""
+    pod = dict(pod, status=status)
+    raw = json.dumps(pod)
+    lazy, eager = K.project_flat_nohash(raw), K.project(raw)
+    assert lazy.info_args() == eager.info_args() and lazy.flags == eager.flags
+    assert lazy.hash == eager.hash and lazy.ident() == eager.ident()
