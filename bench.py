@@ -307,7 +307,7 @@ def main(argv=None) -> int:
                 return float("nan")
 
         lane_keys = ("engine_s", "engine_cpu_s", "lock_wait_s", "engine_pods", "handoff_s", "return_s",
-                     "idle_queued_s", "async_runs")
+                     "idle_queued_s", "async_runs", "scheduled", "forwarded")
 
         def lane_engine() -> tuple:
             """Seconds the native lanes spent inside Engine::schedule_batch (wall, CPU) and waiting
@@ -473,6 +473,11 @@ def main(argv=None) -> int:
             "thread_cpu_us_per_pod": threads,
             # of which the lane thread spent inside the engine's batch cycles (wall, rank 0)
             "io_watch_decode_us_per_pod": round((wd1 - wd0) / my_bound * 1e6, 2) if my_bound else None,
+            # rank 0: the share of its bound pods the native lane placed, and the pod events the
+            # lane handed to Python (pods that needed a Python plugin, or unschedulable ones a
+            # PostFilter may help)
+            "lane_share": round((le1[8] - le0[8]) / my_bound, 3) if my_bound and le1[8] >= le0[8] else None,
+            "lane_forwarded_events": int(le1[9] - le0[9]),
             "lane_engine_us_per_pod": ({"wall": round((le1[0] - le0[0]) / (le1[3] - le0[3]) * 1e6, 2),
                                         "cpu": round((le1[1] - le0[1]) / (le1[3] - le0[3]) * 1e6, 2),
                                         "lock_wait": round((le1[2] - le0[2]) / (le1[3] - le0[3]) * 1e6, 2)}
