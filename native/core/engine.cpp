@@ -7,6 +7,7 @@
 #include <chrono>
 #include <climits>
 #include <cmath>
+#include <cctype>
 #include <cstring>
 
 #include "yoda_dev_abi.h"
@@ -519,7 +520,7 @@ bool Engine::term_matches(const SelTerm& t, const Node& n) const {
         const std::string& s = strings_[it->second];
         char* end = nullptr;
         long long v = std::strtoll(s.c_str(), &end, 10);
-        if (s.empty() || *end != '\0') return false;
+        if (s.empty() || std::isspace((unsigned char)s[0]) || *end != '\0') return false;   // ParseInt syntax
         if (r.op == kGt ? !(v > r.num) : !(v < r.num)) return false;
         break;
       }

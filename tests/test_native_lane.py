@@ -992,6 +992,60 @@ def test_zonal_and_pinned_claims_fit_errors_match_across_paths():
     assert on == off, (on, off)
 
 
+def _rack_pv(name, op, value):
+    pv = _csi_pv(name)
+    pv["spec"]["nodeAffinity"] = {"required": {"nodeSelectorTerms": [{"matchExpressions": [
+        {"key": "example.com/rack", "operator": op, "values": [value]}]}]}}
+    return pv
+
+
+def _rack_case(lane):
+    """Nodes labelled rack 3 / 12 / "7 " (not a Go integer) / none; PVs with Gt / Lt node
+    affinity; one pod per claim."""
+    async def go():
+        async with Env(lane=lane, nodes=(("n1", 8, None), ("n2", 8, None), ("n3", 8, None), ("n4", 8, None))) as e:
+            for n, r in (("n1", "3"), ("n2", "12"), ("n3", "7 ")):
+                node = await e.cl.get("nodes", n)
+                labels = dict(node["metadata"].get("labels") or {}, **{"example.com/rack": r})
+                await e.cl.patch("nodes", n, {"metadata": {"labels": labels}})
+            for claim, op, v in (("gt", "Gt", "5"), ("lt", "Lt", "+4"), ("none", "Gt", "100")):
+                await e.cl.create("persistentvolumes", _rack_pv(f"pv-{claim}", op, v))
+                await e.cl.create("persistentvolumeclaims", _bound_pvc(claim, f"pv-{claim}"))
+            if e.sched.lane is not None:
+                assert await e.wait(lambda: {"default/gt", "default/lt", "default/none"} <= e.sched.lane._claims)
+            else:
+                await asyncio.sleep(0.3)
+            for name in ("gt", "lt", "none"):
+                await e.create(_claim_pod(name, name))
+            assert await e.wait(lambda: e.sched.scheduled == 2)
+            await e.wait(lambda: False, 0.5)
+            got = await e.pods()
+            admitted = e.sched.lane.lane.stats()["admitted"] if e.sched.lane else 0
+            return {n: got[n]["spec"].get("nodeName", "") for n in ("gt", "lt", "none")}, admitted
+    return run(go())
+
+
+@pytest.mark.parametrize("lane", ["on", "off"])
+def test_pv_node_affinity_gt_lt_places_alike_on_both_paths(lane):
+    """PV node affinity with Gt / Lt (one Go int64 threshold) is an engine filter of a lane pod,
+    with upstream's ParseInt on the node label ("7 " matches neither), and VolumeBinding's filter
+    on the Python path: the same nodes."""
+    out, admitted = _rack_case(lane)
+    assert out == {"gt": "n2", "lt": "n1", "none": ""}, out
+    if lane == "on":
+        assert admitted == 3
+
+
+def test_claim_lane_takes_gt_lt_only_with_one_go_integer():
+    from yoda_scheduler_amd.plugins.volumes import NOT_LANE, claim_lane
+    pvs = {"p": _rack_pv("p", "Gt", "5")}
+    node, zone = claim_lane(_bound_pvc("c", "p"), pvs)
+    assert node == ((("example.com/rack", "Gt", ("5",)),),) and zone is None
+    for vals in (["5", "6"], ["5.0"], [" 5"], ["1_0"], [str(1 << 63)], []):
+        pvs["p"]["spec"]["nodeAffinity"]["required"]["nodeSelectorTerms"][0]["matchExpressions"][0]["values"] = vals
+        assert claim_lane(_bound_pvc("c", "p"), pvs) is NOT_LANE, vals
+
+
 @pytest.mark.parametrize("lane", ["on", "off"])
 def test_csi_attach_limits_count_every_pod_on_the_node_on_both_paths(lane):
     """NodeVolumeLimits on the lane: the engine ledger keeps every pod's PVC claims per node and

@@ -1,7 +1,10 @@
 """metav1.LabelSelector matching (matchLabels + matchExpressions)."""
 from __future__ import annotations
 
+import re
 from typing import Mapping, Optional
+
+_GO_INT = re.compile(r"[+-]?[0-9]+\Z")   # strconv.ParseInt(s, 10, 64) syntax
 
 
 class LabelSelector:
@@ -78,12 +81,10 @@ class NodeSelector:
         if op == "DoesNotExist":
             return not has
         if op in ("Gt", "Lt"):
-            if not has or len(vals) != 1:
+            # upstream parses both sides with strconv.ParseInt: no spaces or '_' (Python's int takes them)
+            if not has or len(vals) != 1 or not _GO_INT.match(val) or not _GO_INT.match(vals[0]):
                 return False
-            try:
-                a, b = int(val), int(vals[0])
-            except ValueError:
-                return False
+            a, b = int(val), int(vals[0])
             return a > b if op == "Gt" else a < b
         raise ValueError(f"unknown node selector operator {op!r}")
 

@@ -25,6 +25,7 @@ objects come from informers the scheduler starts only because these plugins decl
 from __future__ import annotations
 
 import asyncio
+import re
 import time
 from typing import Optional
 
@@ -625,6 +626,12 @@ def claim_inert(pvc: dict, pvs: dict, limited: set) -> bool:
 
 NOT_LANE = "not-lane"                     # claim_lane: the claim needs the Python volume plugins
 _LANE_NODE_OPS = ("In", "NotIn", "Exists", "DoesNotExist")
+_GO_INT = re.compile(r"[+-]?[0-9]+\Z")
+
+
+def _go_int64(s: str) -> bool:
+    """``strconv.ParseInt(s, 10, 64)`` succeeds (the engine's Gt / Lt threshold)."""
+    return bool(_GO_INT.match(s)) and -(1 << 63) <= int(s) < (1 << 63)
 
 
 def claim_lane(pvc: dict, pvs: dict):
@@ -634,7 +641,7 @@ def claim_lane(pvc: dict, pvs: dict):
 
     * ``node_terms`` — the PV's ``nodeAffinity.required`` (VolumeBinding's filter for a bound
       claim: any term matches; a term without requirements matches nothing), only with the
-      operators In / NotIn / Exists / DoesNotExist and no ``matchFields``;
+      operators In / NotIn / Exists / DoesNotExist, Gt / Lt on one Go int64, and no ``matchFields``;
     * ``zone_terms`` — VolumeZone's filter as two OR'ed terms: the node has none of the zone /
       region labels, or it has every label the PV has with a value the PV allows ("__"-separated).
 
@@ -661,9 +668,14 @@ def claim_lane(pvc: dict, pvs: dict):
             exprs = []
             for e in t.get("matchExpressions") or []:
                 op = e.get("operator", "In")
-                if op not in _LANE_NODE_OPS:
+                vals = tuple(str(v) for v in e.get("values") or [])
+                if op in ("Gt", "Lt"):
+                    # one Go int64 value (strconv.ParseInt), else the Python plugin decides
+                    if len(vals) != 1 or not _go_int64(vals[0]):
+                        return NOT_LANE
+                elif op not in _LANE_NODE_OPS:
                     return NOT_LANE
-                exprs.append((e.get("key", ""), op, tuple(str(v) for v in e.get("values") or [])))
+                exprs.append((e.get("key", ""), op, vals))
             terms.append(tuple(exprs))
         node = tuple(terms)
     labels = (pv.get("metadata") or _EMPTY).get("labels") or _EMPTY
