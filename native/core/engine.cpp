@@ -103,6 +103,7 @@ Engine::Engine(bool compat, int threads) : compat_(compat) {
   any_ip_ = intern("0.0.0.0");
   tcp_ = intern("TCP");
   dev_ext_res_ = intern("ephemeral-storage");
+  field_name_key_ = intern("@metadata.name");   // '@' is not valid in a label key
 }
 
 Engine::~Engine() {
@@ -499,6 +500,13 @@ bool Engine::taints_ok(const PodReq& req, const Node& n) const {
 bool Engine::term_matches(const SelTerm& t, const Node& n) const {
   if (t.reqs.empty()) return false;   // empty term matches no objects (upstream)
   for (const SelReq& r : t.reqs) {
+    if (r.key == field_name_key_) {   // matchFields metadata.name: the node's name, always present
+      bool in = false;
+      for (int32_t v : r.values) in = in || strings_[v] == n.name;
+      if (r.op == kIn ? !in : r.op == kNotIn ? in : r.op == kDoesNotExist) return false;
+      if (r.op == kGt || r.op == kLt) return false;   // upstream: In / NotIn only
+      continue;
+    }
     auto it = n.labels.find(r.key);
     bool has = it != n.labels.end();
     switch (r.op) {

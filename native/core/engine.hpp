@@ -680,6 +680,7 @@ class Engine {
     return ((uint64_t)(uint8_t)kind << 58) ^ ((uint64_t)(uint32_t)ns << 29) ^ (uint64_t)(uint32_t)name;
   }
   std::vector<DefaultSpread> spread_defaults_;
+  int32_t field_name_key_ = -1;               // "@metadata.name": a matchFields requirement on the node name
   int32_t dev_ext_res_ = -1;                  // set in the constructor: "ephemeral-storage"
   int64_t hard_aff_w_ = 1;
   std::unordered_set<uint64_t> aff_holders_;  // ledger pods with any (anti-)affinity term

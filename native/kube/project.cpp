@@ -153,7 +153,7 @@ bool term_of(N t, TermP& out) {
     std::string key = k ? std::string(k.str()) : "";
     if (field) {
       if (key != "metadata.name") return true;            // other fields: ignored (as in Python)
-      key = "kubernetes.io/hostname";
+      key = "@metadata.name";                             // the engine matches the node name
     }
     r.key = key;
     N op = e.get("operator");

@@ -1036,6 +1036,36 @@ def test_pv_node_affinity_gt_lt_places_alike_on_both_paths(lane):
         assert admitted == 3
 
 
+@pytest.mark.parametrize("lane", ["on", "off"])
+def test_match_fields_metadata_name_is_the_node_name_not_its_hostname_label(lane):
+    """``matchFields`` metadata.name (a pod's node affinity, a PV's node affinity) matches the
+    node's name: node n1 carries the hostname label "n2" and n2 the label "n1"."""
+    async def go():
+        async with Env(lane=lane, nodes=(("n1", 8, None), ("n2", 8, None))) as e:
+            for n, h in (("n1", "n2"), ("n2", "n1")):
+                node = await e.cl.get("nodes", n)
+                labels = dict(node["metadata"].get("labels") or {}, **{"kubernetes.io/hostname": h})
+                await e.cl.patch("nodes", n, {"metadata": {"labels": labels}})
+            pv = _csi_pv("pv-f")
+            pv["spec"]["nodeAffinity"] = {"required": {"nodeSelectorTerms": [{"matchFields": [
+                {"key": "metadata.name", "operator": "In", "values": ["n1"]}]}]}}
+            await e.cl.create("persistentvolumes", pv)
+            await e.cl.create("persistentvolumeclaims", _bound_pvc("f", "pv-f"))
+            if e.sched.lane is not None:
+                assert await e.wait(lambda: "default/f" in e.sched.lane._claims)
+            else:
+                await asyncio.sleep(0.3)
+            await e.create(_claim_pod("v", "f"))
+            p = pod("a", {"scv/memory": "1000"})
+            p["spec"]["affinity"] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+                "nodeSelectorTerms": [{"matchFields": [{"key": "metadata.name", "operator": "In", "values": ["n2"]}]}]}}}
+            await e.create(p)
+            assert await e.wait(lambda: e.sched.scheduled == 2)
+            got = await e.pods()
+            return got["v"]["spec"]["nodeName"], got["a"]["spec"]["nodeName"]
+    assert run(go()) == ("n1", "n2")
+
+
 def test_claim_lane_takes_gt_lt_only_with_one_go_integer():
     from yoda_scheduler_amd.plugins.volumes import NOT_LANE, claim_lane
     pvs = {"p": _rack_pv("p", "Gt", "5")}

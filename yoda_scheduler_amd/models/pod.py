@@ -116,15 +116,18 @@ def quantity_int(q) -> int:
     return bytes_of(q)
 
 
+FIELD_NODE_NAME = "@metadata.name"   # engine key of a matchFields metadata.name requirement
+
+
 def _terms(terms: list | None) -> list[list[tuple[str, str, list[str]]]]:
     out = []
     for t in terms or []:
         reqs = [(e.get("key", ""), e.get("operator", "In"), [str(v) for v in e.get("values") or []])
                 for e in (t.get("matchExpressions") or [])]
-        # matchFields metadata.name → expressed on the hostname label the fake nodes carry
+        # matchFields metadata.name → the engine's node-name requirement (other fields: ignored)
         for f in t.get("matchFields") or []:
             if f.get("key") == "metadata.name":
-                reqs.append(("kubernetes.io/hostname", f.get("operator", "In"),
+                reqs.append((FIELD_NODE_NAME, f.get("operator", "In"),
                              [str(v) for v in f.get("values") or []]))
         out.append(reqs)
     return out

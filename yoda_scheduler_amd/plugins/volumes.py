@@ -31,7 +31,7 @@ from typing import Optional
 
 from ..framework.interfaces import (Code, CycleState, FilterPlugin, PreBindPlugin, PreFilterPlugin, ReservePlugin,
                                     StateData, Status)
-from ..models.pod import PF_CLAIMS, PF_DISKS
+from ..models.pod import FIELD_NODE_NAME, PF_CLAIMS, PF_DISKS
 from ..models.selectors import LabelSelector, NodeSelector
 from ..utils.quantity import bytes_of
 
@@ -641,7 +641,7 @@ def claim_lane(pvc: dict, pvs: dict):
 
     * ``node_terms`` — the PV's ``nodeAffinity.required`` (VolumeBinding's filter for a bound
       claim: any term matches; a term without requirements matches nothing), only with the
-      operators In / NotIn / Exists / DoesNotExist, Gt / Lt on one Go int64, and no ``matchFields``;
+      operators In / NotIn / Exists / DoesNotExist, Gt / Lt on one Go int64, and ``matchFields`` only as In / NotIn on ``metadata.name``;
     * ``zone_terms`` — VolumeZone's filter as two OR'ed terms: the node has none of the zone /
       region labels, or it has every label the PV has with a value the PV allows ("__"-separated).
 
@@ -663,9 +663,13 @@ def claim_lane(pvc: dict, pvs: dict):
             return NOT_LANE
         terms = []
         for t in req.get("nodeSelectorTerms") or []:
-            if not isinstance(t, dict) or t.get("matchFields"):
+            if not isinstance(t, dict):
                 return NOT_LANE
             exprs = []
+            for f in t.get("matchFields") or []:      # the node name; other fields fail the term
+                if f.get("key") != "metadata.name" or f.get("operator", "In") not in ("In", "NotIn"):
+                    return NOT_LANE
+                exprs.append((FIELD_NODE_NAME, f.get("operator", "In"), tuple(str(v) for v in f.get("values") or [])))
             for e in t.get("matchExpressions") or []:
                 op = e.get("operator", "In")
                 vals = tuple(str(v) for v in e.get("values") or [])
