@@ -373,6 +373,7 @@ PYBIND11_MODULE(_yoda_core, m) {
       .def_property_readonly("live_nodes", &Engine::live_nodes)
       .def_property_readonly("cycles", &Engine::cycles)
       .def_property_readonly("ledger_size", &Engine::ledger_size)
+      .def_property_readonly("labsets_used", &Engine::labsets_used)
       .def("node_name", [](Engine& e, int32_t i) { return e.node(i).name; }, py::call_guard<EngineGuard>())
       .def("node_gen", &Engine::node_gen, py::call_guard<EngineGuard>(),
            "generation of a node slot (changes when the slot's node is removed or replaced)")

@@ -177,17 +177,15 @@ int32_t Engine::node_index(const std::string& name) const {
 void Engine::remove_node(int32_t idx) {
   if (idx < 0 || idx >= (int32_t)nodes_.size() || !nodes_[idx].alive) return;
   // drop reservations that point at this node
-  for (auto it = ledger_.begin(); it != ledger_.end();) {
-    if (it->second.node == idx) {
-      if (it->second.aff) {
-        aff_holders_.erase(it->first);
-        anti_holders_.erase(it->first);
-        aff_set_remove(it->second);
-      }
-      it = ledger_.erase(it);
-    } else {
-      ++it;
+  for (int32_t si : nodes_[idx].pods) {
+    Assignment& a = slab_[si];
+    if (!a.live || a.node != idx) continue;
+    if (a.aff) {
+      aff_holders_.erase(a.pod);
+      anti_holders_.erase(a.pod);
+      aff_set_remove(a);
     }
+    free_entry(si);
   }
   node_idx_.erase(nodes_[idx].name);
   hard_taint_nodes_ -= nodes_[idx].hard_taint;
@@ -253,8 +251,8 @@ void Engine::set_cards(int32_t idx, std::vector<Card> cards, uint64_t card_numbe
   }
   // recompute which reservations the new sample cannot reflect yet
   n.sample_ts = sample_ts;
-  for (uint64_t pod : n.pods) {
-    const Assignment& a = ledger_.at(pod);
+  for (int32_t si : n.pods) {
+    const Assignment& a = slab_[si];
     if (!is_pending(n, a)) continue;
     for (int32_t c : a.cards)
       if (c < (int32_t)n.cards.size()) n.cards[c].pending_mb += a.mb;
@@ -350,22 +348,168 @@ bool Engine::ports_free(const PodReq& req, const Node& n) const {
 }
 
 const Assignment* Engine::assignment(uint64_t pod) const {
-  auto it = ledger_.find(pod);
-  return it == ledger_.end() ? nullptr : &it->second;
+  const int32_t si = ledger_.find(pod);
+  return si < 0 ? nullptr : &slab_[si];
 }
 
 // ============================================================== ledger
+bool U64Map::insert(uint64_t k, int32_t v) {
+  if ((size_ + 1) * 10 > cap_ * 7) grow();
+  for (size_t i = slot(k);; i = (i + 1) & (cap_ - 1)) {
+    if (!used_[i]) {
+      used_[i] = 1;
+      keys_[i] = k;
+      vals_[i] = v;
+      ++size_;
+      return true;
+    }
+    if (keys_[i] == k) return false;
+  }
+}
+
+bool U64Map::erase(uint64_t k) {
+  if (cap_ == 0) return false;
+  size_t i = slot(k);
+  for (;; i = (i + 1) & (cap_ - 1)) {
+    if (!used_[i]) return false;
+    if (keys_[i] == k) break;
+  }
+  // backward-shift deletion: move later members of the probe run into the hole when their home
+  // slot does not lie (cyclically) after it, so lookups never need tombstones
+  for (size_t j = (i + 1) & (cap_ - 1);; j = (j + 1) & (cap_ - 1)) {
+    if (!used_[j]) break;
+    const size_t h = slot(keys_[j]);
+    const bool between = i <= j ? (i < h && h <= j) : (i < h || h <= j);
+    if (between) continue;
+    keys_[i] = keys_[j];
+    vals_[i] = vals_[j];
+    i = j;
+  }
+  used_[i] = 0;
+  --size_;
+  return true;
+}
+
+void U64Map::grow() {
+  std::vector<uint64_t> k;
+  std::vector<int32_t> v;
+  std::vector<uint8_t> u;
+  k.swap(keys_);
+  v.swap(vals_);
+  u.swap(used_);
+  const size_t old = cap_;
+  cap_ = cap_ ? cap_ * 2 : 64;
+  keys_.assign(cap_, 0);
+  vals_.assign(cap_, 0);
+  used_.assign(cap_, 0);
+  size_ = 0;
+  for (size_t i = 0; i < old; ++i)
+    if (u[i]) insert(k[i], v[i]);
+}
+
+uint64_t labset_hash(int32_t ns, const Labels& l) {
+  uint64_t h = (uint64_t)(uint32_t)ns * 0x9E3779B97F4A7C15ull;
+  for (const auto& kv : l) {
+    h ^= ((uint64_t)(uint32_t)kv.first << 32 | (uint32_t)kv.second) + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    h *= 0xff51afd7ed558ccdull;
+  }
+  return h ^ (h >> 33);
+}
+
+int32_t Engine::labset_acquire(int32_t ns, const Labels& labels) {
+  const uint64_t h = labset_hash(ns, labels);
+  auto it = labset_by_hash_.find(h);
+  if (it != labset_by_hash_.end())
+    for (int32_t id = it->second; id >= 0; id = labsets_[id].next) {
+      LabSetRec& r = labsets_[id];
+      if (r.ns == ns && r.labels == labels) {
+        if (r.refs++ == 0) --labset_idle_;
+        return id;
+      }
+    }
+  int32_t id;
+  if (!labset_free_.empty()) {
+    id = labset_free_.back();
+    labset_free_.pop_back();
+  } else {
+    id = (int32_t)labsets_.size();
+    labsets_.emplace_back();
+  }
+  LabSetRec& r = labsets_[id];
+  r.ns = ns;
+  r.labels = labels;
+  r.hash = h;
+  r.refs = 1;
+  r.used = true;
+  if (it != labset_by_hash_.end()) {
+    r.next = it->second;
+    it->second = id;
+  } else {
+    r.next = -1;
+    labset_by_hash_.emplace(h, id);
+  }
+  return id;
+}
+
+void Engine::labset_release(int32_t id) {
+  if (id < 0 || id >= (int32_t)labsets_.size()) return;
+  LabSetRec& r = labsets_[id];
+  if (r.refs <= 0 || --r.refs > 0) return;
+  // idle: kept (the next pod of the template finds it without allocating) until idle sets
+  // outnumber held ones
+  if (++labset_idle_ > 1024 && labset_idle_ * 2 > (int64_t)labsets_used()) labset_sweep();
+}
+
+void Engine::labset_sweep() {
+  // node groups of an idle set hold count 0 (a set's refs are its ledger entries), so recycling
+  // its id leaves them correct: a zero-count group matches nothing, and a later set with the id
+  // counts from 0
+  for (int32_t id = 0; id < (int32_t)labsets_.size(); ++id) {
+    LabSetRec& r = labsets_[id];
+    if (!r.used || r.refs > 0) continue;
+    auto it = labset_by_hash_.find(r.hash);
+    if (it != labset_by_hash_.end()) {
+      if (it->second == id) {
+        if (r.next >= 0) it->second = r.next;
+        else labset_by_hash_.erase(it);
+      } else {
+        for (int32_t p = it->second; p >= 0; p = labsets_[p].next)
+          if (labsets_[p].next == id) {
+            labsets_[p].next = r.next;
+            break;
+          }
+      }
+    }
+    r.used = false;
+    r.next = -1;
+    Labels().swap(r.labels);
+    labset_free_.push_back(id);
+  }
+  labset_idle_ = 0;
+}
+
 bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::vector<int32_t>& cards) {
-  if (ledger_.count(pod)) return false;
+  if (ledger_.find(pod) >= 0) return false;
   if (idx < 0 || idx >= (int32_t)nodes_.size() || !nodes_[idx].alive) return false;
   Node& n = nodes_[idx];
-  Assignment a;
-  a.node = idx;
-  a.mb = req.has_memory ? req.memory : 0;
   for (int32_t c : cards) {
     if (c < 0 || c >= (int32_t)n.cards.size()) return false;
   }
-  a.cards = cards;
+  // a free slab entry keeps its vectors' capacity: a pod like one released before allocates nothing
+  int32_t si;
+  if (!slab_free_.empty()) {
+    si = slab_free_.back();
+    slab_free_.pop_back();
+  } else {
+    si = (int32_t)slab_.size();
+    slab_.emplace_back();
+  }
+  Assignment& a = slab_[si];
+  a.pod = pod;
+  a.live = true;
+  a.node = idx;
+  a.mb = req.has_memory ? req.memory : 0;
+  a.cards.assign(cards.begin(), cards.end());
   a.t_res = now();
   if (!compat_) {
     const bool pend = is_pending(n, a);
@@ -376,7 +520,7 @@ bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::ve
     }
   }
   a.slot = (int32_t)n.pods.size();
-  n.pods.push_back(pod);
+  n.pods.push_back(si);
   a.cpu_m = req.cpu_m;
   a.mem = req.mem;
   a.nz_cpu_m = req.nz_cpu_m;
@@ -390,8 +534,10 @@ bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::ve
   n.pod_count += 1;
   if (a.has_label_mem) n.label_mem_sum += a.label_mem;
   a.ns = req.ns;
-  a.labels = req.labels;
+  a.labset = labset_acquire(req.ns, req.labels);
   a.deleting = req.deleting;
+  a.aff.reset();
+  a.aff_hash = 0;
   if (req.aff && !req.aff->empty()) {
     a.aff = req.aff;
     aff_holders_.insert(pod);
@@ -399,34 +545,44 @@ bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::ve
     aff_set_add(a);
   }
   index_pod(n, a, +1);
-  if (!req.pvc_claims.empty()) {
-    a.pvc_claims = req.pvc_claims;
-    for (int32_t c : a.pvc_claims) ++n.claims[c];
+  a.pvc_claims.assign(req.pvc_claims.begin(), req.pvc_claims.end());
+  for (int32_t c : a.pvc_claims) ++n.claims[c];
+  a.host_ports.assign(req.host_ports.begin(), req.host_ports.end());
+  for (const HostPort& h : a.host_ports) {
+    ++n.ports[h];
+    ++n.ports_any[{h.proto, h.port}];
   }
-  if (!req.host_ports.empty()) {
-    a.host_ports = req.host_ports;
-    for (const HostPort& h : a.host_ports) {
-      ++n.ports[h];
-      ++n.ports_any[{h.proto, h.port}];
-    }
+  a.ext.assign(req.ext.begin(), req.ext.end());
+  for (const auto& r : a.ext) {
+    auto it = std::lower_bound(n.ext_used.begin(), n.ext_used.end(), std::make_pair(r.first, INT64_MIN));
+    if (it != n.ext_used.end() && it->first == r.first) it->second += r.second;
+    else n.ext_used.insert(it, r);
   }
-  if (!req.ext.empty()) {
-    a.ext = req.ext;
-    for (const auto& r : a.ext) {
-      auto it = std::lower_bound(n.ext_used.begin(), n.ext_used.end(), std::make_pair(r.first, INT64_MIN));
-      if (it != n.ext_used.end() && it->first == r.first) it->second += r.second;
-      else n.ext_used.insert(it, r);
-    }
-  }
-  ledger_.emplace(pod, std::move(a));
+  ledger_.insert(pod, si);
   mark_dirty(idx);
   return true;
 }
 
+void Engine::free_entry(int32_t si) {
+  Assignment& a = slab_[si];
+  ledger_.erase(a.pod);
+  labset_release(a.labset);
+  a.labset = -1;
+  a.live = false;
+  a.node = -1;
+  a.slot = -1;
+  a.aff.reset();
+  a.cards.clear();
+  a.ext.clear();
+  a.host_ports.clear();
+  a.pvc_claims.clear();
+  slab_free_.push_back(si);
+}
+
 bool Engine::release(uint64_t pod) {
-  auto it = ledger_.find(pod);
-  if (it == ledger_.end()) return false;
-  const Assignment& a = it->second;
+  const int32_t si = ledger_.find(pod);
+  if (si < 0) return false;
+  const Assignment& a = slab_[si];
   if (a.node >= 0 && a.node < (int32_t)nodes_.size() && nodes_[a.node].alive) {
     Node& n = nodes_[a.node];
     if (!compat_) {
@@ -440,10 +596,10 @@ bool Engine::release(uint64_t pod) {
       }
     }
     if (a.slot >= 0 && a.slot < (int32_t)n.pods.size()) {
-      uint64_t last = n.pods.back();
+      const int32_t last = n.pods.back();
       n.pods[a.slot] = last;
       n.pods.pop_back();
-      if (last != pod) ledger_.at(last).slot = a.slot;
+      if (last != si) slab_[last].slot = a.slot;
     }
     n.req_cpu_m -= a.cpu_m;
     n.req_mem -= a.mem;
@@ -473,7 +629,7 @@ bool Engine::release(uint64_t pod) {
     anti_holders_.erase(pod);
     aff_set_remove(a);
   }
-  ledger_.erase(it);
+  free_entry(si);
   return true;
 }
 
@@ -1204,9 +1360,11 @@ void Engine::interpod_prefilter(const PodReq& req, InterPodPF* pf) const {
         all = term_count(n, aff[0]);
       } else {                                  // a pod must match every term: per label-set group
         for (const auto& g : n.lab_groups) {
+          if (g.second.first <= 0) continue;
+          const LabSetRec& ls = labsets_[g.first];
           bool m = true;
           for (const PodTerm& t : aff)
-            if (!t.matches(g.first.ns, g.first.labels)) {
+            if (!t.matches(ls.ns, ls.labels)) {
               m = false;
               break;
             }
@@ -1214,10 +1372,12 @@ void Engine::interpod_prefilter(const PodReq& req, InterPodPF* pf) const {
         }
       }
       if (all > 0) {
-        pf->any_aff_match = true;
+        // upstream topologyToMatchedAffinityTerms only gains pairs of nodes carrying the key
         for (const PodTerm& t : aff) {
           auto lab = n.labels.find(t.key);
-          if (lab != n.labels.end()) pf->affinity[pair_key(t.key, lab->second)] += all;
+          if (lab == n.labels.end()) continue;
+          pf->affinity[pair_key(t.key, lab->second)] += all;
+          pf->any_aff_match = true;
         }
       }
     }
@@ -1304,7 +1464,9 @@ void Engine::interpod_scores(const PodReq& req, const std::vector<int32_t>& feas
       for (const PodTerm& t : set.aff->pref_anti) add(t, -(int64_t)t.weight);
     }
   if (keys.empty() || F == 0) return;
-  int64_t hi = INT64_MIN, lo = INT64_MAX;
+  // upstream v1.20 InterPodAffinity.NormalizeScore: maxCount and minCount start at 0 (so the
+  // range always spans 0) and the scale is float64, truncated
+  int64_t hi = 0, lo = 0;
   for (size_t i = 0; i < F; ++i) {
     const Node& n = nodes_[feas[i]];
     int64_t v = 0;
@@ -1318,7 +1480,8 @@ void Engine::interpod_scores(const PodReq& req, const std::vector<int32_t>& feas
     hi = std::max(hi, v);
     lo = std::min(lo, v);
   }
-  for (size_t i = 0; i < F; ++i) s[i] = hi == lo ? 0 : floor_div(kMaxNodeScore * (s[i] - lo), hi - lo);
+  for (size_t i = 0; i < F; ++i)
+    s[i] = hi - lo > 0 ? (int64_t)((double)kMaxNodeScore * ((double)(s[i] - lo) / (double)(hi - lo))) : 0;
 }
 
 bool Engine::interpod_inert(const PodReq& req) const {
@@ -1510,47 +1673,62 @@ bool Engine::images_matter(const PodReq& req) const {
 }
 
 bool Engine::set_pod_meta(uint64_t pod, Labels labels, bool deleting) {
-  auto it = ledger_.find(pod);
-  if (it == ledger_.end()) return false;
+  const int32_t si = ledger_.find(pod);
+  if (si < 0) return false;
   std::sort(labels.begin(), labels.end());
-  Assignment& a = it->second;
+  Assignment& a = slab_[si];
   const bool live = a.node >= 0 && a.node < (int32_t)nodes_.size() && nodes_[a.node].alive;
   if (live) index_pod(nodes_[a.node], a, -1);
-  a.labels = std::move(labels);
+  const int32_t old = a.labset;
+  a.labset = labset_acquire(a.ns, labels);
+  labset_release(old);
   a.deleting = deleting;
   if (live) index_pod(nodes_[a.node], a, +1);
   return true;
 }
 
 void Engine::index_pod(Node& n, const Assignment& a, int sign) {
+  // counts that reach 0 keep their entry (the next pod of the template bumps it without
+  // allocating); a node sweeps them once they outnumber the live entries
   const int live = a.deleting ? 0 : sign;
-  auto bump = [&](LKey k) {
-    auto& c = n.lab_idx[k];
+  auto count = [&](std::pair<int32_t, int32_t>& c, bool fresh, int32_t& zeros) {
+    if (c.first <= 0 && !fresh) --zeros;
     c.first += sign;
     c.second += live;
-    if (c.first <= 0) n.lab_idx.erase(k);
+    if (c.first <= 0) ++zeros;
+  };
+  auto bump = [&](LKey k) {
+    auto r = n.lab_idx.try_emplace(k, 0, 0);
+    count(r.first->second, r.second, n.lab_idx_zero);
   };
   bump(LKey{a.ns, -1, -1});
-  for (const auto& kv : a.labels) bump(LKey{a.ns, kv.first, kv.second});
-  if (sign > 0) {
-    auto& g = n.lab_groups[LabSet{a.ns, a.labels}];
-    g.first += 1;
-    g.second += live;
-  } else {
-    auto it = n.lab_groups.find(LabSet{a.ns, a.labels});
-    if (it != n.lab_groups.end()) {
-      it->second.first -= 1;
-      it->second.second += live;
-      if (it->second.first <= 0) n.lab_groups.erase(it);
-    }
+  for (const auto& kv : labsets_[a.labset].labels) bump(LKey{a.ns, kv.first, kv.second});
+  auto g = n.lab_groups.try_emplace(a.labset, 0, 0);
+  count(g.first->second, g.second, n.lab_groups_zero);
+  if (sign < 0 && (n.lab_idx_zero > 64 || n.lab_groups_zero > 64)) sweep_lab_index(n);
+}
+
+void Engine::sweep_lab_index(Node& n) {
+  if (n.lab_idx_zero * 2 > (int32_t)n.lab_idx.size()) {
+    for (auto it = n.lab_idx.begin(); it != n.lab_idx.end();)
+      it = it->second.first <= 0 ? n.lab_idx.erase(it) : std::next(it);
+    n.lab_idx_zero = 0;
+  }
+  if (n.lab_groups_zero * 2 > (int32_t)n.lab_groups.size()) {
+    for (auto it = n.lab_groups.begin(); it != n.lab_groups.end();)
+      it = it->second.first <= 0 ? n.lab_groups.erase(it) : std::next(it);
+    n.lab_groups_zero = 0;
   }
 }
 
 int64_t Engine::group_count(const Node& n, int32_t ns, const LSel& sel, bool skip_deleting) const {
   if (sel.nothing) return 0;
   int64_t c = 0;
-  for (const auto& g : n.lab_groups)
-    if (g.first.ns == ns && sel.matches(g.first.labels)) c += skip_deleting ? g.second.second : g.second.first;
+  for (const auto& g : n.lab_groups) {
+    if (g.second.first <= 0) continue;
+    const LabSetRec& ls = labsets_[g.first];
+    if (ls.ns == ns && sel.matches(ls.labels)) c += skip_deleting ? g.second.second : g.second.first;
+  }
   return c;
 }
 

@@ -176,21 +176,47 @@ struct LKeyHash {
   }
 };
 
-// a reserved pod's (namespace, sorted labels): the key of a node's label-set groups
-struct LabSet {
+// A reserved pod's (namespace, sorted labels), interned once by the engine (Engine::labset_acquire):
+// the ledger entry holds its id and a node's label-set groups count pods per id, so reserving or
+// releasing a pod of a known template copies no labels and allocates nothing
+struct LabSetRec {
   int32_t ns = 0;
   Labels labels;
-  bool operator==(const LabSet& o) const { return ns == o.ns && labels == o.labels; }
+  uint64_t hash = 0;
+  int64_t refs = 0;            // ledger entries holding it; 0: idle (kept for reuse until a sweep)
+  int32_t next = -1;           // the next id in its hash chain (labset_by_hash_)
+  bool used = false;           // false: on the free list
 };
-struct LabSetHash {
-  size_t operator()(const LabSet& x) const {
-    uint64_t h = (uint64_t)(uint32_t)x.ns * 0x9E3779B97F4A7C15ull;
-    for (const auto& kv : x.labels) {
-      h ^= ((uint64_t)(uint32_t)kv.first << 32 | (uint32_t)kv.second) + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
-      h *= 0xff51afd7ed558ccdull;
+uint64_t labset_hash(int32_t ns, const Labels& l);
+
+// Open-addressing map uint64 → int32 (linear probing, backward-shift deletion): the ledger's
+// pod → slab index. Inserting a key into a table below its load limit and erasing one never
+// allocate, so a steady reserve / release cycle does not touch the heap.
+class U64Map {
+ public:
+  int32_t find(uint64_t k) const {
+    if (cap_ == 0) return -1;
+    for (size_t i = slot(k);; i = (i + 1) & (cap_ - 1)) {
+      if (!used_[i]) return -1;
+      if (keys_[i] == k) return vals_[i];
     }
-    return (size_t)(h ^ (h >> 33));
   }
+  bool insert(uint64_t k, int32_t v);   // false if present
+  bool erase(uint64_t k);
+  size_t size() const { return size_; }
+
+ private:
+  size_t slot(uint64_t k) const {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    return (size_t)k & (cap_ - 1);
+  }
+  void grow();
+  std::vector<uint64_t> keys_;
+  std::vector<int32_t> vals_;
+  std::vector<uint8_t> used_;
+  size_t cap_ = 0, size_ = 0;
 };
 
 // NodePorts: a container port with hostPort > 0, sanitized as upstream HostPortInfo (hostIP ""
@@ -222,7 +248,7 @@ struct Node {
   uint64_t label_mem_sum = 0;         // Σ scv/memory labels of pods on node (compat Allocate)
   bool hard_taint = false, prefer_taint = false;   // has NoSchedule/NoExecute, PreferNoSchedule taints
   double sample_ts = 0;               // unix time of the Scv sample the cards came from
-  std::vector<uint64_t> pods;         // ledger entries on this node (for pending recompute)
+  std::vector<int32_t> pods;          // ledger slab indices of the pods on this node
   std::vector<std::pair<int32_t, int64_t>> images;     // status.images: (normalized name, bytes), sorted
   std::vector<std::pair<int32_t, int64_t>> ext_alloc;  // allocatable beyond cpu/memory/pods, sorted
   std::vector<std::pair<int32_t, int64_t>> ext_used;   // Σ of the ledger's ext requests, sorted
@@ -230,10 +256,13 @@ struct Node {
   // label index of the reserved pods: (all, not terminating) per (namespace, key, value) and per
   // namespace — a single-label selector's count in O(1) (spread / affinity pre-filters)
   std::unordered_map<LKey, std::pair<int32_t, int32_t>, LKeyHash> lab_idx;
-  // the same pods grouped by their exact (namespace, label set) with (all, not terminating)
-  // counts: any other selector is matched once per group instead of once per pod (a node's pods
-  // come from few templates)
-  std::unordered_map<LabSet, std::pair<int32_t, int32_t>, LabSetHash> lab_groups;
+  // the same pods grouped by their exact (namespace, label set) — an interned label-set id — with
+  // (all, not terminating) counts: any other selector is matched once per group instead of once
+  // per pod (a node's pods come from few templates)
+  std::unordered_map<int32_t, std::pair<int32_t, int32_t>> lab_groups;
+  // entries of lab_idx / lab_groups whose count dropped to 0: kept, so a pod of the same template
+  // arriving again allocates nothing; swept once they outnumber the live entries
+  int32_t lab_idx_zero = 0, lab_groups_zero = 0;
   // NodePorts: host ports of the reserved pods, per (ip, protocol, port) and per (protocol, port)
   // over every ip (a 0.0.0.0 request conflicts with any ip) — counts, as two pods may hold one
   std::map<HostPort, int32_t> ports;
@@ -329,8 +358,10 @@ struct Assignment {
   bool has_label_mem = false;
   double t_res = 0;             // unix time of the reservation
   int32_t slot = -1;            // index in Node::pods
+  uint64_t pod = 0;             // the ledger key (the slab entry is free when !live)
+  bool live = false;
   int32_t ns = 0;               // the pod as other pods' spread constraints count it
-  Labels labels;
+  int32_t labset = -1;          // its interned (namespace, labels) (Engine::labset)
   bool deleting = false;
   std::vector<std::pair<int32_t, int64_t>> ext;   // extended resources it holds on the node
   std::shared_ptr<const PodAffinity> aff;          // its (anti-)affinity terms (symmetric rule, scoring)
@@ -457,9 +488,12 @@ class Engine {
   // ---- ledger
   bool reserve(uint64_t pod, const PodReq& req, int32_t node, const std::vector<int32_t>& cards);
   bool release(uint64_t pod);
-  bool has_pod(uint64_t pod) const { return ledger_.count(pod) != 0; }
+  bool has_pod(uint64_t pod) const { return ledger_.find(pod) >= 0; }
   const Assignment* assignment(uint64_t pod) const;
   size_t ledger_size() const { return ledger_.size(); }
+  // the (namespace, labels) of an interned label set (Assignment::labset)
+  const LabSetRec& labset(int32_t id) const { return labsets_[id]; }
+  size_t labsets_used() const { return labsets_.size() - labset_free_.size(); }
 
   // ---- policy pieces (exposed for parity tests and for the Python runner)
   Reason filter_node(const PodReq& req, int32_t idx, uint64_t* n, uint64_t* m, uint64_t* c) const;
@@ -652,7 +686,21 @@ class Engine {
   std::unordered_map<std::string, int32_t> node_idx_;
   std::vector<std::string> strings_;
   std::unordered_map<std::string, int32_t> string_idx_;
-  std::unordered_map<uint64_t, Assignment> ledger_;
+  // the ledger: a slab of entries (free ones reused with their vectors' capacity) and pod → index
+  std::vector<Assignment> slab_;
+  std::vector<int32_t> slab_free_;
+  U64Map ledger_;
+  // interned label sets (LabSetRec): id → record, hash → first id of its chain; idle ones (no
+  // holder) are reused as they are and recycled by a sweep once they outnumber the held ones
+  std::vector<LabSetRec> labsets_;
+  std::vector<int32_t> labset_free_;
+  std::unordered_map<uint64_t, int32_t> labset_by_hash_;
+  int64_t labset_idle_ = 0;
+  int32_t labset_acquire(int32_t ns, const Labels& labels);
+  void labset_release(int32_t id);
+  void labset_sweep();
+  void sweep_lab_index(Node& n);
+  void free_entry(int32_t si);
   std::mt19937_64 rng_{0x59d4};
   double settle_s_ = 30.0;
   double fixed_now_ = -1.0;

@@ -1032,15 +1032,17 @@ bool Lane::make_req(const yk::PodProj& p, PodReq* r) {
     if (eng_->host_port(x.host_port, x.protocol, x.host_ip, &hp)) r->host_ports.push_back(hp);
   for (size_t i = 0; i < p.claims.size(); ++i)   // the ledger keeps every pod's PVC claims (NodeVolumeLimits)
     if (i < p.claim_pvc.size() && p.claim_pvc[i]) r->pvc_claims.push_back(eng_->intern(p.ns + "/" + p.claims[i]));
-  if (p.has_owner) {
-    r->owner_kind = p.owner_api == "v1" && p.owner_kind == "ReplicationController" ? 1
-                    : p.owner_api == "apps/v1" && p.owner_kind == "ReplicaSet"  ? 2
-                    : p.owner_api == "apps/v1" && p.owner_kind == "StatefulSet" ? 3 : 0;
-    if (r->owner_kind) r->owner_name = eng_->intern(p.owner_name);
-  }
-  if (p.has_avoid) {
-    r->avoid_kind = p.avoid_kind == "ReplicationController" ? 1 : 2;
-    r->avoid_uid = eng_->intern(p.avoid_uid);
+  if (const yk::PodProj::Owners* o = p.owners.get()) {
+    if (o->has_owner) {
+      r->owner_kind = o->owner_api == "v1" && o->owner_kind == "ReplicationController" ? 1
+                      : o->owner_api == "apps/v1" && o->owner_kind == "ReplicaSet"  ? 2
+                      : o->owner_api == "apps/v1" && o->owner_kind == "StatefulSet" ? 3 : 0;
+      if (r->owner_kind) r->owner_name = eng_->intern(o->owner_name);
+    }
+    if (o->has_avoid) {
+      r->avoid_kind = o->avoid_kind == "ReplicationController" ? 1 : 2;
+      r->avoid_uid = eng_->intern(o->avoid_uid);
+    }
   }
   r->spread_explicit = !p.spread.empty();
   for (const auto& c : p.spread) {
@@ -1814,9 +1816,9 @@ void Lane::patch_condition(Entry& e, const std::string& msg) {
   const yk::PodProj& cur = e.ev->full();
   bool same;
   std::string ltt;
-  if (cur.has_sched_cond) {
-    same = cur.sched_cond_status == "False" && cur.sched_cond_reason == "Unschedulable" && cur.sched_cond_msg == msg;
-    if (cur.sched_cond_status == "False" && !cur.sched_cond_ltt.empty()) ltt = cur.sched_cond_ltt;   // no transition
+  if (const auto& c = cur.sched_cond) {
+    same = c->status == "False" && c->reason == "Unschedulable" && c->msg == msg;
+    if (c->status == "False" && !c->ltt.empty()) ltt = c->ltt;   // no transition
   } else {
     same = !e.cond_msg.empty() && e.cond_msg == msg;
     ltt = e.cond_ltt;

@@ -102,11 +102,12 @@ py::tuple info_args(const PodProj& p) {
   }
   py::list images;
   for (const auto& im : p.images) images.append(py::str(im));
-  py::object owner = p.has_owner ? py::object(py::make_tuple(py::str(p.owner_api), py::str(p.owner_kind),
-                                                            py::str(p.owner_name), py::str(p.owner_uid)))
-                                 : py::object(py::none());
-  py::object avoid = p.has_avoid ? py::object(py::make_tuple(py::str(p.avoid_kind), py::str(p.avoid_uid)))
-                                 : py::object(py::none());
+  const PodProj::Owners* o = p.owners.get();
+  py::object owner = o && o->has_owner ? py::object(py::make_tuple(py::str(o->owner_api), py::str(o->owner_kind),
+                                                                  py::str(o->owner_name), py::str(o->owner_uid)))
+                                       : py::object(py::none());
+  py::object avoid = o && o->has_avoid ? py::object(py::make_tuple(py::str(o->avoid_kind), py::str(o->avoid_uid)))
+                                       : py::object(py::none());
   py::object spread = py::none();
   if (!p.spread.empty()) {
     // (topologyKey, maxSkew, whenUnsatisfiable, LabelSelector.native() tuple | None)
@@ -160,8 +161,9 @@ PYBIND11_MODULE(_yoda_kube, m) {
       // status.conditions' PodScheduled entry: (status, reason, message, lastTransitionTime) or None
       .def_property_readonly("sched_cond", [](const PodEv& e) -> py::object {
         const PodProj& p = e.full();
-        if (!p.has_sched_cond) return py::none();
-        return py::make_tuple(p.sched_cond_status, p.sched_cond_reason, p.sched_cond_msg, p.sched_cond_ltt);
+        if (!p.sched_cond) return py::none();
+        const auto& c = *p.sched_cond;
+        return py::make_tuple(c.status, c.reason, c.msg, c.ltt);
       })
       // (key, uid, node, scheduler, phase, hash): the per-event fields in one call
       .def("ident", [](const PodEv& e) {

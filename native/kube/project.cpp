@@ -362,11 +362,15 @@ void project_generic(N pod, PodProj& p) {
     if (N cs = st.get("conditions"); cs && cs.arr()) {
       cs.each([&](std::string_view, N c) {
         if (!c.obj() || c.sv("type") != "PodScheduled") return true;
-        p.has_sched_cond = true;
-        p.sched_cond_status = std::string(c.sv("status"));
-        p.sched_cond_reason = std::string(c.sv("reason"));
-        p.sched_cond_msg = std::string(c.sv("message"));
-        p.sched_cond_ltt = std::string(c.sv("lastTransitionTime"));
+        static const auto kTrue = std::make_shared<const PodProj::SchedCond>(PodProj::SchedCond{"True", "", "", ""});
+        const std::string_view status = c.sv("status");
+        if (status == "True") {
+          p.sched_cond = kTrue;
+        } else {
+          p.sched_cond = std::make_shared<const PodProj::SchedCond>(PodProj::SchedCond{
+              std::string(status), std::string(c.sv("reason")), std::string(c.sv("message")),
+              std::string(c.sv("lastTransitionTime"))});
+        }
         return false;                       // the first one, as a by-type merge keeps one
       });
     }
@@ -679,6 +683,7 @@ void project_generic(N pod, PodProj& p) {
   for (const auto& kv : p.labels)
     if (kv.first == "pod-group.scheduling.sigs.k8s.io") flags |= PF_POD_GROUP;
   if (N owners = m.get("ownerReferences"); owners && owners.arr()) {
+    PodProj::Owners o;
     bool ok = owners.each([&](std::string_view, N r) {
       if (!r.obj()) return false;
       N c = r.get("controller");
@@ -686,20 +691,21 @@ void project_generic(N pod, PodProj& p) {
       const bool ctl = c && c.truthy();
       if (ctl && (kind == "ReplicationController" || kind == "ReplicaSet" || kind == "StatefulSet"))
         flags |= PF_CONTROLLER;
-      if (ctl && !p.has_owner) {            // DefaultSelector reads the first controller only
-        p.has_owner = true;
-        p.owner_api = std::string(r.sv("apiVersion"));
-        p.owner_kind = std::string(kind);
-        p.owner_name = std::string(r.sv("name"));
-        p.owner_uid = std::string(r.sv("uid"));
+      if (ctl && !o.has_owner) {            // DefaultSelector reads the first controller only
+        o.has_owner = true;
+        o.owner_api = std::string(r.sv("apiVersion"));
+        o.owner_kind = std::string(kind);
+        o.owner_name = std::string(r.sv("name"));
+        o.owner_uid = std::string(r.sv("uid"));
       }
-      if (ctl && !p.has_avoid && (kind == "ReplicationController" || kind == "ReplicaSet")) {
-        p.has_avoid = true;                 // NodePreferAvoidPods: the first RC / RS controller
-        p.avoid_kind = std::string(kind);
-        p.avoid_uid = std::string(r.sv("uid"));
+      if (ctl && !o.has_avoid && (kind == "ReplicationController" || kind == "ReplicaSet")) {
+        o.has_avoid = true;                 // NodePreferAvoidPods: the first RC / RS controller
+        o.avoid_kind = std::string(kind);
+        o.avoid_uid = std::string(r.sv("uid"));
       }
       return true;
     });
+    if (o.has_owner || o.has_avoid) p.owners = std::make_shared<const PodProj::Owners>(std::move(o));
     if (!ok) return;
   }
   p.flags = flags;
@@ -1076,14 +1082,7 @@ void merge_non_identity(PodProj& d, PodProj&& s) {
   d.images = std::move(s.images);
   d.containers = s.containers;
   d.ext = std::move(s.ext);
-  d.has_owner = s.has_owner;
-  d.owner_api = std::move(s.owner_api);
-  d.owner_kind = std::move(s.owner_kind);
-  d.owner_name = std::move(s.owner_name);
-  d.owner_uid = std::move(s.owner_uid);
-  d.has_avoid = s.has_avoid;
-  d.avoid_kind = std::move(s.avoid_kind);
-  d.avoid_uid = std::move(s.avoid_uid);
+  d.owners = std::move(s.owners);
   d.spread = std::move(s.spread);
   d.has_pod_aff = s.has_pod_aff;
   d.aff_req = std::move(s.aff_req);
@@ -1095,11 +1094,7 @@ void merge_non_identity(PodProj& d, PodProj&& s) {
   d.claim_pvc = std::move(s.claim_pvc);
   d.spec_meta_hash = s.spec_meta_hash;
   d.ok = s.ok;
-  d.has_sched_cond = s.has_sched_cond;
-  d.sched_cond_status = std::move(s.sched_cond_status);
-  d.sched_cond_reason = std::move(s.sched_cond_reason);
-  d.sched_cond_msg = std::move(s.sched_cond_msg);
-  d.sched_cond_ltt = std::move(s.sched_cond_ltt);
+  d.sched_cond = std::move(s.sched_cond);
 }
 
 bool project_pod_text(std::string_view text, PodProj& p) {

@@ -6,6 +6,7 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <utility>
 #include <vector>
@@ -81,9 +82,12 @@ struct PodProj {
   // lane drops its entry by key, and whatever goes on to Python is completed first.
   bool ident_partial = false;
   // status.conditions' PodScheduled entry (upstream updatePod compares the condition it would
-  // write with the pod's current one): status, reason, message, lastTransitionTime
-  bool has_sched_cond = false;
-  std::string sched_cond_status, sched_cond_reason, sched_cond_msg, sched_cond_ltt;
+  // write with the pod's current one); null: none. Only a False condition's reason, message and
+  // lastTransitionTime are read, so every True one shares one record (no allocation per pod)
+  struct SchedCond {
+    std::string status, reason, msg, ltt;
+  };
+  std::shared_ptr<const SchedCond> sched_cond;
   // default-plugin inputs (models/pod.py PodInfo.images / containers / ext / owner / avoid /
   // spread): normalized images of spec.containers and their count, requests beyond cpu/memory
   // (non-zero, models/pod.py::ext_requests), the first controller ownerReference, the first
@@ -91,10 +95,15 @@ struct PodProj {
   std::vector<std::string> images;
   int32_t containers = 0;
   std::vector<std::pair<std::string, int64_t>> ext;
-  bool has_owner = false;
-  std::string owner_api, owner_kind, owner_name, owner_uid;
-  bool has_avoid = false;
-  std::string avoid_kind, avoid_uid;
+  // the controller references (null: the pod has no controller ownerReference); one record, so
+  // a pod without one carries 16 bytes for them
+  struct Owners {
+    bool has_owner = false;
+    std::string owner_api, owner_kind, owner_name, owner_uid;
+    bool has_avoid = false;
+    std::string avoid_kind, avoid_uid;
+  };
+  std::shared_ptr<const Owners> owners;
   struct SpreadP {
     std::string key;
     int64_t max_skew = 1;

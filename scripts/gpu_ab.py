@@ -31,19 +31,24 @@ import time
 CRASH = {124, 134, 137, 139, -6, -9, -11}
 
 
-def parse_variant(text: str) -> tuple[str, dict]:
-    """``name:VAR=a,VAR2=b`` → (name, env); ``name:`` is the unmodified environment."""
+def parse_variant(text: str) -> tuple[str, dict, str | None]:
+    """``name[@dir]:VAR=a,VAR2=b`` → (name, env, cwd); ``name:`` is the unmodified environment.
+
+    ``@dir`` runs that variant's command in another tree (e.g. a git worktree of an older
+    commit, built in place), so commits can be bisected on one box."""
     name, _, rest = text.partition(":")
+    name, _, cwd = name.partition("@")
     env = {}
     for kv in filter(None, rest.split(",")):
         k, _, v = kv.partition("=")
         env[k.strip()] = v
-    return name or "base", env
+    return name or "base", env, cwd or None
 
 
-def run(cmd: list[str], env: dict, timeout: float, log) -> tuple[int, list[dict]]:
+def run(cmd: list[str], env: dict, timeout: float, log, cwd: str | None = None) -> tuple[int, list[dict]]:
     try:
-        r = subprocess.run(cmd, env={**os.environ, **env}, capture_output=True, text=True, timeout=timeout)
+        r = subprocess.run(cmd, env={**os.environ, **env}, capture_output=True, text=True, timeout=timeout,
+                           cwd=cwd)
     except subprocess.TimeoutExpired as e:
         log.write((e.stdout or b"").decode() if isinstance(e.stdout, bytes) else (e.stdout or ""))
         return 124, []
@@ -61,7 +66,8 @@ def run(cmd: list[str], env: dict, timeout: float, log) -> tuple[int, list[dict]
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--variant", action="append", required=True, help="name:VAR=value[,VAR=value] (repeatable)")
+    ap.add_argument("--variant", action="append", required=True,
+                    help="name[@dir]:VAR=value[,VAR=value] (repeatable)")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--timeout", type=float, default=300.0, help="seconds per run")
     ap.add_argument("--pre", default="", help="command run once per variant before the A/B (e.g. parity tests)")
@@ -76,15 +82,15 @@ def main(argv=None) -> int:
     logp = os.path.splitext(a.out)[0] + ".log"
     with open(a.out, "w") as out, open(logp, "w") as log:
         if a.pre:
-            for name, env in variants:
-                rc, _ = run(shlex.split(a.pre), env, a.timeout, log)
+            for name, env, cwd in variants:
+                rc, _ = run(shlex.split(a.pre), env, a.timeout, log, cwd)
                 print(f"pre[{name}] rc={rc}", flush=True)
                 if rc != 0:
                     return rc if rc > 0 else 1
         for rep in range(a.reps):
-            for name, env in variants:
+            for name, env, cwd in variants:
                 t0 = time.time()
-                rc, rows = run(cmd, env, a.timeout, log)
+                rc, rows = run(cmd, env, a.timeout, log, cwd)
                 for row in rows:
                     out.write(json.dumps({"variant": name, "rep": rep, "env": env, **row}) + "\n")
                 out.flush()

@@ -647,3 +647,104 @@ def test_csi_attach_limits_native_equal_python(alloc_limits, csinode_limits, cla
         got = eng.filter_node(req, eng.node_index(n))
         assert got in (0, reason)
         assert (got == 0) == want, (n, alloc_limits, csinode_limits, claims, bound, mine, drop)
+
+
+def test_label_groups_stay_exact_when_label_set_ids_are_recycled():
+    """Pods with unique label sets (StatefulSet / Job pods) come and go: idle interned label sets
+    are swept and their ids reused, and zero-count node index entries are swept. count_matching
+    still equals a brute-force count over the live pods (single-label, multi-label, expression
+    selectors) after each wave."""
+    import random
+    from yoda_scheduler_amd.models.selectors import LabelSelector
+    rng = random.Random(11)
+    eng, cache = cache_with([make_node(f"n{i}") for i in range(3)])
+    live, nxt = {}, 0
+    sels = [{"matchLabels": {"app": "a"}}, {"matchLabels": {"app": "b", "tier": "x"}},
+            {"matchExpressions": [{"key": "statefulset.kubernetes.io/pod-name", "operator": "In",
+                                   "values": [f"s-{k}" for k in range(0, 6000, 7)]}]},
+            {"matchExpressions": [{"key": "tier", "operator": "Exists"}]}]
+    for wave in range(4):
+        for _ in range(1500):
+            j = nxt
+            nxt += 1
+            labels = {"app": rng.choice(["a", "b"]), "statefulset.kubernetes.io/pod-name": f"s-{j}"}
+            if rng.random() < 0.5:
+                labels["tier"] = rng.choice(["x", "y"])
+            node = f"n{rng.randrange(3)}"
+            o = {"metadata": {"name": f"s-{j}", "namespace": "default", "uid": f"ss-{j}", "labels": labels},
+                 "spec": {"nodeName": node}}
+            cache.add_pod(o)
+            live[f"ss-{j}"] = (node, labels)
+        for uid in rng.sample(sorted(live), len(live) - 200):
+            cache.remove_pod(uid)
+            del live[uid]
+        # idle sets beyond 1024 are swept: the table holds the live pods' sets plus at most that
+        assert eng.labsets_used <= len(live) + 1025, (wave, eng.labsets_used)
+        for sel in sels:
+            ls = LabelSelector(sel)
+            for node in ("n0", "n1", "n2"):
+                want = sum(1 for n, lab in live.values() if n == node and ls.matches(lab))
+                assert eng.count_matching(eng.node_index(node), "default", ls.native()) == want, (wave, sel, node)
+
+
+def _aff_case(node_labels, placed, newp_spec, hard=1):
+    nodes = [{"metadata": {"name": nm, "labels": {HOST: nm, **lab}},
+              "status": {"allocatable": {"cpu": "64", "memory": "512Gi", "pods": "110"}}}
+             for nm, lab in node_labels.items()]
+    eng, cache = cache_with(nodes)
+    eng.filters = C.F_INTERPOD
+    only_weight(eng, C.S_INTERPOD)
+    eng.set_hard_pod_affinity_weight(hard)
+    for j, (node, labels) in enumerate(placed):
+        cache.add_pod({"metadata": {"name": f"e{j}", "namespace": "default", "uid": f"e{j}-{next(_uid)}",
+                                    "labels": labels}, "spec": {"nodeName": node}})
+    pl = InterPodAffinity({"hardPodAffinityWeight": hard}, SimpleNamespace(cache=cache))
+    p = PodInfo.from_obj({"metadata": {"name": "new", "namespace": "default", "uid": f"new-{next(_uid)}",
+                                       "labels": {"app": "web"}}, "spec": newp_spec})
+    return eng, pl, p
+
+
+def test_interpod_normalize_starts_min_and_max_at_zero():
+    """upstream v1.20 NormalizeScore starts maxCount and minCount at 0 and scales in
+    float64. Preferred-affinity scores 5 and 10 (both positive) normalize to 50 and 100, not 0
+    and 100; -3 and -1 (both negative) to 0 and 66 (float: 100 * 2/3 = 66.67, truncated)."""
+    pref = lambda w: {"weight": w, "podAffinityTerm": {"topologyKey": HOST,  # noqa: E731
+                                                        "labelSelector": {"matchLabels": {"app": "db"}}}}
+    eng, pl, p = _aff_case({"n0": {}, "n1": {}}, [("n0", {"app": "db"}), ("n1", {"app": "db"}),
+                                                  ("n1", {"app": "db"})],
+                           {"affinity": {"podAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [pref(5)]}}})
+    st_ = CycleState()
+    pl.pre_filter(st_, p)
+    pl.pre_score(st_, p, ["n0", "n1"])
+    out = [NodeScore(nm, pl.score(st_, p, nm)[0]) for nm in ("n0", "n1")]
+    assert [x.score for x in out] == [5, 10]
+    pl.normalize_score(st_, p, out)
+    assert [x.score for x in out] == [50, 100]
+    assert native_scores(eng, p, ["n0", "n1"]) == {"n0": 50, "n1": 100}
+    eng, pl, p = _aff_case({"n0": {}, "n1": {}}, [("n0", {"app": "db"}), ("n0", {"app": "db"}),
+                                                  ("n0", {"app": "db"}), ("n1", {"app": "db"})],
+                           {"affinity": {"podAntiAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [pref(1)]}}})
+    st_ = CycleState()
+    pl.pre_filter(st_, p)
+    pl.pre_score(st_, p, ["n0", "n1"])
+    out = [NodeScore(nm, pl.score(st_, p, nm)[0]) for nm in ("n0", "n1")]
+    assert [x.score for x in out] == [-3, -1]
+    pl.normalize_score(st_, p, out)
+    assert [x.score for x in out] == [0, 66]
+    assert native_scores(eng, p, ["n0", "n1"]) == {"n0": 0, "n1": 66}
+
+
+def test_first_pod_rule_ignores_matching_pods_on_nodes_without_the_key():
+    """upstream's first-pod-of-a-group exception looks at topologyToMatchedAffinityTerms,
+    which only counts matching pods on nodes carrying the term's topology key. A self-affine pod
+    whose only matches sit on zone-less nodes may go to any zoned node."""
+    req = {"affinity": {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+        {"topologyKey": ZONE, "labelSelector": {"matchLabels": {"app": "web"}}}]}}}
+    eng, pl, p = _aff_case({"n0": {ZONE: "z1"}, "n1": {ZONE: "z2"}, "n2": {}}, [("n2", {"app": "web"})], req)
+    st_ = CycleState()
+    pl.pre_filter(st_, p)
+    want = {nm: pl.filter(st_, p, nm).is_success() for nm in ("n0", "n1", "n2")}
+    assert want == {"n0": True, "n1": True, "n2": False}
+    r = pod_req(eng, p)
+    got = {nm: C.REASONS[eng.filter_node(r, eng.node_index(nm))] == "OK" for nm in ("n0", "n1", "n2")}
+    assert got == want

@@ -454,7 +454,6 @@ class InterPodAffinity(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugi
         lane = cache.lane_counts(queries) if queries and hasattr(cache, "lane_counts") else [{} for _ in queries]
         if aff_terms:
             if lane[0]:
-                st.any_affinity_match = True
                 for t in aff_terms:
                     self._by_topology(lane[0], t.get("topologyKey", ""), st.affinity)
             lane = lane[1:]
@@ -462,7 +461,6 @@ class InterPodAffinity(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugi
             self._by_topology(counts, t.get("topologyKey", ""), st.anti)
         for o, labels in (self._existing(owned_only=True) if aff_terms or anti_terms else ()):
             if aff_terms and all(_term_matches(t, pod.namespace, o) for t in aff_terms):
-                st.any_affinity_match = True
                 for t in aff_terms:
                     key = t.get("topologyKey", "")
                     if key in labels:
@@ -471,6 +469,9 @@ class InterPodAffinity(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugi
                 key = t.get("topologyKey", "")
                 if key in labels and _term_matches(t, pod.namespace, o):
                     st.anti[(key, labels[key])] += 1
+        # upstream topologyToMatchedAffinityTerms is empty: no matching pod sits on a node that
+        # carries the terms' topology keys (matching pods on unlabeled nodes do not count)
+        st.any_affinity_match = any(v > 0 for v in st.affinity.values())
         st.aff_terms, st.anti_terms = aff_terms, anti_terms
         state.write(self.KEY, st)
         return Status.ok()
@@ -550,7 +551,9 @@ class InterPodAffinity(PreFilterPlugin, FilterPlugin, PreScorePlugin, ScorePlugi
     def normalize_score(self, state: CycleState, pod, scores: list[NodeScore]) -> Status:
         if not scores:
             return Status.ok()
-        hi, lo = max(x.score for x in scores), min(x.score for x in scores)
+        # upstream v1.20 NormalizeScore: maxCount / minCount start at 0, float64 scale truncated
+        hi = max(0, max(x.score for x in scores))
+        lo = min(0, min(x.score for x in scores))
         for x in scores:
-            x.score = 0 if hi == lo else MAX_NODE_SCORE * (x.score - lo) // (hi - lo)
+            x.score = int(float(MAX_NODE_SCORE) * ((x.score - lo) / (hi - lo))) if hi - lo > 0 else 0
         return Status.ok()
