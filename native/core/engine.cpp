@@ -322,12 +322,14 @@ bool Engine::vols_fit(const PodReq& req, const Node& n) const {
     auto lim = std::lower_bound(n.vol_limits.begin(), n.vol_limits.end(), std::make_pair(d, INT64_MIN));
     if (lim != n.vol_limits.end() && lim->first == d) {
       std::unordered_set<int32_t> ids;
-      for (size_t k = i; k < j; ++k) ids.insert(mine[k].second);
       for (const auto& kv : n.claims) {
         auto it = claim_vol_.find(kv.first);
         if (it != claim_vol_.end() && it->second.first == d) ids.insert(it->second.second);
       }
-      if ((int64_t)ids.size() > lim->second) return false;
+      // upstream CSILimits: only a driver the pod adds a new volume to is compared
+      bool adds = false;
+      for (size_t k = i; k < j; ++k) adds = ids.insert(mine[k].second).second || adds;
+      if (adds && (int64_t)ids.size() > lim->second) return false;
     }
     i = j;
   }
@@ -656,11 +658,14 @@ bool Engine::taints_ok(const PodReq& req, const Node& n) const {
 bool Engine::term_matches(const SelTerm& t, const Node& n) const {
   if (t.reqs.empty()) return false;   // empty term matches no objects (upstream)
   for (const SelReq& r : t.reqs) {
-    if (r.key == field_name_key_) {   // matchFields metadata.name: the node's name, always present
-      bool in = false;
-      for (int32_t v : r.values) in = in || strings_[v] == n.name;
-      if (r.op == kIn ? !in : r.op == kNotIn ? in : r.op == kDoesNotExist) return false;
-      if (r.op == kGt || r.op == kLt) return false;   // upstream: In / NotIn only
+    const std::string& key = strings_[r.key];
+    if (!key.empty() && key[0] == '@') {
+      // matchFields (upstream v1.20 NodeSelectorRequirementsAsFieldSelector): In / NotIn with
+      // exactly one value, anything else is an error that fails the term; the node's fields
+      // are {metadata.name}, so any other field reads as ""
+      if ((r.op != kIn && r.op != kNotIn) || r.values.size() != 1) return false;
+      const bool eq = strings_[r.values[0]] == (r.key == field_name_key_ ? n.name : std::string());
+      if (r.op == kIn ? !eq : eq) return false;
       continue;
     }
     auto it = n.labels.find(r.key);

@@ -94,8 +94,17 @@ struct Card {
 
 struct Taint { int32_t key, value; int8_t effect; };
 struct Toleration { int32_t key; int32_t value; int8_t op; int8_t effect; };  // key -1 = any
-struct SelReq { int32_t key; int8_t op; std::vector<int32_t> values; int64_t num; };
-struct SelTerm { std::vector<SelReq> reqs; };
+struct SelReq {
+  int32_t key;
+  int8_t op;
+  std::vector<int32_t> values;
+  int64_t num;
+  bool operator==(const SelReq& o) const { return key == o.key && op == o.op && values == o.values && num == o.num; }
+};
+struct SelTerm {
+  std::vector<SelReq> reqs;
+  bool operator==(const SelTerm& o) const { return reqs == o.reqs; }
+};
 struct PrefTerm { int32_t weight; SelTerm term; };
 
 // Interned (key, value) pairs sorted by key: a pod's labels as the ledger keeps them.

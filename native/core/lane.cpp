@@ -860,13 +860,15 @@ void Lane::apply_claims(std::vector<Fwd>* out) {
   }
   if (ops.empty()) return;
   std::unordered_set<std::string> removed;  // left the table or changed at some op
+  // a reset rebuilds every claim's record: compare the constraints, not the pointers
+  auto changed = [](const ClaimConsP& a, const ClaimConsP& b) { return a != b && (!a || !b || !(*a == *b)); };
   for (auto& op : ops) {
     if (op.reset) {
       std::unordered_map<std::string, ClaimConsP> next;
       for (auto& kv : op.add) next.emplace(std::move(kv.first), std::move(kv.second));
       for (const auto& kv : claim_table_) {
         auto it = next.find(kv.first);
-        if (it == next.end() || it->second != kv.second) removed.insert(kv.first);
+        if (it == next.end() || changed(it->second, kv.second)) removed.insert(kv.first);
       }
       claim_table_.swap(next);
       continue;
@@ -876,7 +878,7 @@ void Lane::apply_claims(std::vector<Fwd>* out) {
     for (auto& kv : op.add) {
       auto it = claim_table_.find(kv.first);
       if (it != claim_table_.end()) {
-        if (it->second != kv.second) removed.insert(kv.first);
+        if (changed(it->second, kv.second)) removed.insert(kv.first);
         it->second = std::move(kv.second);
       } else {
         claim_table_.emplace(std::move(kv.first), std::move(kv.second));

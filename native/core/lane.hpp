@@ -147,6 +147,9 @@ class Lane : public yk::PodSink {
   struct ClaimCons {
     bool has_node = false, has_zone = false;
     std::vector<SelTerm> node, zone;
+    bool operator==(const ClaimCons& o) const {
+      return has_node == o.has_node && has_zone == o.has_zone && node == o.node && zone == o.zone;
+    }
   };
   using ClaimConsP = std::shared_ptr<const ClaimCons>;
 

@@ -151,10 +151,7 @@ bool term_of(N t, TermP& out) {
     N k = e.get("key");
     if (k && !k.str_t()) return false;                    // null key: Python keeps None
     std::string key = k ? std::string(k.str()) : "";
-    if (field) {
-      if (key != "metadata.name") return true;            // other fields: ignored (as in Python)
-      key = "@metadata.name";                             // the engine matches the node name
-    }
+    if (field) key = "@" + key;                           // a field requirement (engine: '@' keys)
     r.key = key;
     N op = e.get("operator");
     if (op && !op.str_t()) return false;

@@ -748,3 +748,63 @@ def test_first_pod_rule_ignores_matching_pods_on_nodes_without_the_key():
     r = pod_req(eng, p)
     got = {nm: C.REASONS[eng.filter_node(r, eng.node_index(nm))] == "OK" for nm in ("n0", "n1", "n2")}
     assert got == want
+
+
+def test_match_fields_follow_upstream_field_selector_rules():
+    """matchFields become a field selector over {metadata.name: node} (upstream v1.20
+    NodeSelectorRequirementsAsFieldSelector). In / NotIn need exactly one value, any other
+    operator or value count fails the term, and an unknown field reads as "" (so NotIn on it
+    matches). The engine (a pod's node affinity) and NodeSelector (a PV's) agree."""
+    from yoda_scheduler_amd.models.selectors import NodeSelector
+    eng, cache = cache_with([node_obj("n0"), node_obj("n1")])
+    eng.filters = C.F_NODE_AFFINITY
+    cases = [
+        ({"key": "metadata.name", "operator": "In", "values": ["n0"]}, {"n0": True, "n1": False}),
+        ({"key": "metadata.name", "operator": "NotIn", "values": ["n0"]}, {"n0": False, "n1": True}),
+        ({"key": "metadata.name", "operator": "In", "values": ["n0", "n1"]}, {"n0": False, "n1": False}),
+        ({"key": "metadata.name", "operator": "NotIn", "values": []}, {"n0": False, "n1": False}),
+        ({"key": "metadata.name", "operator": "Exists"}, {"n0": False, "n1": False}),
+        ({"key": "spec.unschedulable", "operator": "In", "values": ["true"]}, {"n0": False, "n1": False}),
+        ({"key": "spec.unschedulable", "operator": "NotIn", "values": ["true"]}, {"n0": True, "n1": True}),
+        ({"key": "spec.unschedulable", "operator": "In", "values": [""]}, {"n0": True, "n1": True}),
+    ]
+    for req, want in cases:
+        term = {"matchFields": [req]}
+        p = pod("p", affinity={"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+            "nodeSelectorTerms": [term]}}})
+        r = pod_req(eng, p)
+        got = {nm: C.REASONS[eng.filter_node(r, eng.node_index(nm))] == "OK" for nm in ("n0", "n1")}
+        assert got == want, req
+        ns = NodeSelector({"nodeSelectorTerms": [term]})
+        assert {nm: ns.matches(nm, {}) for nm in ("n0", "n1")} == want, req
+
+
+def test_csi_limits_skip_a_driver_the_pod_adds_no_volume_to():
+    """upstream v1.20 CSILimits removes already-attached volumes from the pod's new
+    ones and compares only drivers that still have new volumes. A node already over its limit
+    (two volumes attached, limit lowered to 1) takes a pod that only reuses an attached volume,
+    and rejects one that adds a volume. Engine ≡ Python plugin."""
+    nodes = [node_obj("n0", alloc={"attachable-volumes-csi-nfs.csi": "1"})]
+    eng, cache = cache_with(nodes)
+    eng.filters = 0
+    objs = {"persistentvolumeclaims": {}, "persistentvolumes": {}, "storageclasses": {}, "csinodes": {}}
+    for j in range(3):
+        objs["persistentvolumes"][f"pv{j}"] = {"metadata": {"name": f"pv{j}"},
+                                              "spec": {"csi": {"driver": "nfs.csi", "volumeHandle": f"h{j}"}}}
+        objs["persistentvolumeclaims"][f"default/c{j}"] = {"metadata": {"name": f"c{j}", "namespace": "default"},
+                                                          "spec": {"volumeName": f"pv{j}"}}
+    handle = _VolHandle(cache, objs)
+    eng.set_claim_volumes([(k, d, h) for k, (d, h) in claim_volumes(handle).items()], [])
+    eng.set_node_vol_limits(eng.node_index("n0"), sorted(node_csi_limits(cache.nodes["n0"].obj, None).items()))
+    for j in range(2):
+        cache.add_pod({"metadata": {"name": f"b{j}", "namespace": "default", "uid": f"csi{j}-{next(_uid)}"},
+                       "spec": {"nodeName": "n0", "containers": [{"name": "c"}],
+                                "volumes": [{"name": "v", "persistentVolumeClaim": {"claimName": f"c{j}"}}]}})
+    from yoda_scheduler_amd.plugins.volumes import pvc_claim_keys
+    pl = NodeVolumeLimits({}, handle)
+    for claim, want in (("c0", True), ("c2", False)):
+        p = pod("p", containers=[{"name": "c"}], volumes=[{"name": "v", "persistentVolumeClaim": {"claimName": claim}}])
+        req = pod_req(eng, p)
+        eng.set_req_claims(req, pvc_claim_keys(p), True)
+        assert pl.filter(CycleState(), p, "n0").is_success() == want, claim
+        assert (eng.filter_node(req, eng.node_index("n0")) == 0) == want, claim

@@ -1249,3 +1249,24 @@ def test_lane_and_python_path_place_a_mixed_burst_alike(seed):
     py = _burst_placements(seed, "off")
     assert lane == py
     assert sum(1 for n, _ in lane.values() if n) >= 15
+
+
+def test_claim_table_reset_with_unchanged_constraints_keeps_waiting_lane_pods():
+    """a StorageClass event rebuilds the whole claim table (new constraint records for
+    every claim). A waiting lane pod whose claim's constraints did not change stays in the
+    lane's unschedulableQ instead of being sent to Python."""
+    async def go():
+        async with Env(lane="on", nodes=(("n1", 8, None), ("n2", 8, None))) as e:
+            nl = e.sched.lane
+            await e.cl.create("persistentvolumes", _csi_pv("pv-p", host="n1"))
+            await e.cl.create("persistentvolumeclaims", _bound_pvc("pinned", "pv-p"))
+            assert await e.wait(lambda: "default/pinned" in nl._claims)
+            big = pod("big", {"scv/memory": "900000000"},
+                      volumes=[{"name": "d", "persistentVolumeClaim": {"claimName": "pinned"}}])
+            await e.create(big)
+            assert await e.wait(lambda: nl.lane.stats()["parked"] == 1)
+            await e.cl.create("storageclasses", {"metadata": {"name": "fast"}, "provisioner": "nfs.csi.k8s.io"})
+            await e.wait(lambda: False, 0.5)
+            return nl.lane.stats()["parked"], nl.owned()
+    parked, owned = run(go())
+    assert parked == 1 and owned == 1

@@ -124,11 +124,12 @@ def _terms(terms: list | None) -> list[list[tuple[str, str, list[str]]]]:
     for t in terms or []:
         reqs = [(e.get("key", ""), e.get("operator", "In"), [str(v) for v in e.get("values") or []])
                 for e in (t.get("matchExpressions") or [])]
-        # matchFields metadata.name → the engine's node-name requirement (other fields: ignored)
+        # matchFields → '@'-prefixed engine keys: In / NotIn with one value on metadata.name (the
+        # node name); other fields read as "" and other shapes fail the term (upstream
+        # NodeSelectorRequirementsAsFieldSelector)
         for f in t.get("matchFields") or []:
-            if f.get("key") == "metadata.name":
-                reqs.append((FIELD_NODE_NAME, f.get("operator", "In"),
-                             [str(v) for v in f.get("values") or []]))
+            reqs.append(("@" + str(f.get("key", "")), f.get("operator", "In"),
+                         [str(v) for v in f.get("values") or []]))
         out.append(reqs)
     return out
 

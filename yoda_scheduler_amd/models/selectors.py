@@ -94,6 +94,16 @@ class NodeSelector:
             if not exprs and not fields:
                 continue
             if all(self._req(op, k in labels, labels.get(k, ""), vals) for k, op, vals in exprs) and \
-                    all(k == "metadata.name" and self._req(op, True, node_name, vals) for k, op, vals in fields):
+                    all(self._field(k, op, vals, node_name) for k, op, vals in fields):
                 return True
         return False
+
+    @staticmethod
+    def _field(key: str, op: str, vals: list, node_name: str) -> bool:
+        """upstream v1.20 NodeSelectorRequirementsAsFieldSelector over {metadata.name: node}: In /
+        NotIn with exactly one value (anything else errors, failing the term); an unknown field
+        reads as ""."""
+        if op not in ("In", "NotIn") or len(vals) != 1:
+            return False
+        eq = vals[0] == (node_name if key == "metadata.name" else "")
+        return eq if op == "In" else not eq

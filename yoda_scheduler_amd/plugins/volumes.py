@@ -461,6 +461,8 @@ class VolumeBinding(_VolumeBase, PreFilterPlugin, FilterPlugin, ReservePlugin, P
 class _LimitsBase(_VolumeBase, FilterPlugin):
     """Counts unique attachable volumes per (driver) on the node plus the pod's new ones."""
 
+    new_only = False   # CSI: skip drivers the pod adds no new volume to (NodeVolumeLimits)
+
     def _pod_ids(self, ns: str, spec: dict) -> dict[str, set[str]]:
         raise NotImplementedError
 
@@ -481,15 +483,21 @@ class _LimitsBase(_VolumeBase, FilterPlugin):
                 attached.setdefault(d, set()).update(ids)
         for d, ids in mine.items():
             lim = limits.get(d)
-            if lim is not None and len(attached.get(d, set()) | ids) > lim:
+            have = attached.get(d, set())
+            if self.new_only and ids <= have:
+                continue      # upstream CSILimits compares only drivers the pod adds volumes to
+            if lim is not None and len(have | ids) > lim:
                 return Status.unschedulable(ERR_MAX_VOLUMES, plugin=self.name)
         return Status.ok()
 
 
 class NodeVolumeLimits(_LimitsBase):
     """CSI attach limits: ``CSINode.spec.drivers[].allocatable.count`` (or node allocatable
-    ``attachable-volumes-csi-<driver>``)."""
+    ``attachable-volumes-csi-<driver>``). As upstream v1.20 CSILimits, a driver whose volumes
+    of the pod are all attached on the node already is not compared (the in-tree limits are:
+    existing + new > limit rejects even with nothing new)."""
     name = "NodeVolumeLimits"
+    new_only = True
     pod_flags = PF_CLAIMS
     claim_inert_ok = True   # the lane's claim table covers it (claim_lane): a no-op or an engine filter
     reads_flags = PF_CLAIMS  # other pods' features this plugin reads (needs_lane_mirror)
