@@ -162,10 +162,11 @@ def main(argv=None) -> int:
                     help="GPUs per synthetic node (BASELINE protocol item 5); default: the config's own")
     ap.add_argument("--nodes", type=int, default=None,
                     help="config 6 only: cluster size (default 4096; the CPU/device crossover end to end)")
-    ap.add_argument("--cluster", choices=["synthetic", "kind"], default="synthetic",
+    ap.add_argument("--cluster", choices=["synthetic", "kind", "cloud"], default="synthetic",
                     help="kind: nodes report 50 images + ephemeral-storage, the cluster has the kubernetes / kube-dns "
                          "Services, 30%% of pods belong to a Service-selected ReplicaSet, 20%% request "
-                         "ephemeral-storage (bench/workloads.py)")
+                         "ephemeral-storage; cloud: kind + zone labels on every node (3 zones) and the hot image "
+                         "on 30%% of nodes at varying sizes (bench/workloads.py)")
     ap.add_argument("--mix-anti", type=int, default=0,
                     help="beyond BASELINE: replace this many pods of the burst (evenly spread) with pods that carry "
                          "required pod anti-affinity (native InterPodAffinity since round 5)")
@@ -414,6 +415,7 @@ def main(argv=None) -> int:
 
         uniq = {id(x): x for x in shards}.values()
         device_cycles = sum(s.sched.engine.device_cycles for s in uniq)
+        device_batches = sum(getattr(s.sched.engine, "device_batches", 0) for s in uniq)
         bound = sum(r.bound for r in results)
         unsched = sum(r.unschedulable for r in results)
         lats = [x for r in results for x in r.latencies_s]
@@ -509,6 +511,7 @@ def main(argv=None) -> int:
             "pods_bound": bound,
             "pods_unschedulable": unsched,
             "device_cycles": device_cycles,
+            "device_batches": device_batches,
             "ranks": per_rank,
             "transport": transport,
             **({"apiserver": a.apiserver, "client": a.client} if transport == "http" else {}),

@@ -410,6 +410,7 @@ PYBIND11_MODULE(_yoda_core, m) {
       .def_property_readonly("device_ctx", &Engine::device_ctx)
       .def_property_readonly("device_cycles", &Engine::device_cycles)
       .def_property_readonly("device_fallbacks", &Engine::device_fallbacks)
+      .def_property_readonly("device_batches", &Engine::device_batches)
       .def("device_last_us", &Engine::device_last_us, py::call_guard<EngineGuard>())
       .def("device_set_timing", &Engine::device_set_timing, py::arg("on"), py::call_guard<EngineGuard>())
       .def("device_eligible", &Engine::device_eligible, py::call_guard<EngineGuard>())

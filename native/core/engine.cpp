@@ -2088,14 +2088,35 @@ CycleResult Engine::schedule(uint64_t pod, const PodReq& req, bool assume, const
 
 std::vector<CycleResult> Engine::schedule_batch(const std::vector<uint64_t>& pods,
                                                 const std::vector<const PodReq*>& reqs) {
+  // Maximal runs of batch-eligible pods go to the device as one k_batch dispatch each; the pods
+  // between them take per-pod cycles (device per-pod cycle or CPU), in creation order, so each
+  // pod still sees every earlier pod's reservation. One pod the device cannot carry no longer
+  // sends the whole batch to per-pod cycles (VERDICT r5 next #3a).
   std::vector<CycleResult> out;
-  if (schedule_batch_device(pods, reqs, &out)) return out;
-  out.clear();
   out.reserve(pods.size());
   static const std::vector<int32_t> none;
   static const std::vector<int64_t> nox;
-  for (size_t i = 0; i < pods.size(); ++i) out.push_back(schedule(pods[i], *reqs[i], true, none, nox));
+  const size_t n = std::min(pods.size(), reqs.size());
+  const bool dev = dev_ctx_ && fn_schedule_batch_ && live_ >= dev_min_nodes_;
+  size_t i = 0;
+  while (i < n) {
+    size_t j = i;
+    if (dev)
+      while (j < n && batch_eligible(*reqs[j])) ++j;
+    if (j - i >= 2 && schedule_batch_device(pods.data() + i, reqs.data() + i, j - i, &out)) {
+      ++dev_batches_;
+      i = j;
+      continue;
+    }
+    // a lone eligible pod, an ineligible one, or a run the device refused: per-pod cycles
+    const size_t end = std::max(j, i + 1);
+    for (; i < end; ++i) out.push_back(schedule(pods[i], *reqs[i], true, none, nox));
+  }
   return out;
+}
+
+bool Engine::batch_eligible(const PodReq& q) const {
+  return device_eligible(q) && !needs_candidates(q) && !(q.has_memory && q.memory > UINT32_MAX);
 }
 
 // ============================================================== device scorer (dlopen)
@@ -2377,13 +2398,11 @@ bool Engine::schedule_device(const PodReq& req, CycleResult* r) {
   return true;
 }
 
-bool Engine::schedule_batch_device(const std::vector<uint64_t>& pods, const std::vector<const PodReq*>& reqs,
+bool Engine::schedule_batch_device(const uint64_t* pods, const PodReq* const* reqs, size_t count,
                                    std::vector<CycleResult>* out) {
-  if (!dev_ctx_ || !fn_schedule_batch_ || live_ < dev_min_nodes_ || pods.size() < 2) return false;
+  if (!dev_ctx_ || !fn_schedule_batch_ || live_ < dev_min_nodes_ || count < 2) return false;
   std::unique_lock<std::mutex> dl(dev_mu_, std::try_to_lock);
   if (!dl.owns_lock()) return false;
-  for (const PodReq* q : reqs)
-    if (!device_eligible(*q) || needs_candidates(*q) || (q->has_memory && q->memory > UINT32_MAX)) return false;
   // the device assumes each winner with its reservation counted as pending (Engine::reserve
   // with is_pending true); that holds for every node whose sample is not from the future
   const double t = now();
@@ -2395,9 +2414,9 @@ bool Engine::schedule_batch_device(const std::vector<uint64_t>& pods, const std:
   }
   // rng draws happen in make_dev_req, in pod order — the same sequence as per-pod cycles
   const std::mt19937_64 rng_before = rng_;
-  std::vector<yoda_dev_req_t> d(reqs.size());
-  for (size_t i = 0; i < reqs.size(); ++i) make_dev_req(*reqs[i], &d[i]);
-  std::vector<yoda_dev_result_t> res(reqs.size());
+  std::vector<yoda_dev_req_t> d(count);
+  for (size_t i = 0; i < count; ++i) make_dev_req(*reqs[i], &d[i]);
+  std::vector<yoda_dev_result_t> res(count);
   using batch_t = int (*)(void*, int, int, const yoda_dev_req_t*, yoda_dev_result_t*);
   void* ctx = dev_ctx_;
   const int n_nodes = (int)nodes_.size();
@@ -2421,12 +2440,10 @@ bool Engine::schedule_batch_device(const std::vector<uint64_t>& pods, const std:
     for (int32_t i = 0; i < (int32_t)nodes_.size(); ++i) mark_dirty(i);
     return false;
   }
-  out->clear();
-  out->reserve(pods.size());
   std::vector<int32_t> diverged;   // device assumed, host refused (duplicate pod, node gone): re-upload
   // rows dirtied while the lock was dropped are before this mark and stay dirty
   const size_t mark = dirty_list_.size();
-  for (size_t i = 0; i < pods.size(); ++i) {
+  for (size_t i = 0; i < count; ++i) {
     ++cycles_;
     ++dev_cycles_;
     CycleResult r;

@@ -611,6 +611,7 @@ class Engine {
   void set_external_lock(std::recursive_mutex* m) { ext_mu_ = m; }
   bool batch_in_flight() const { return batch_in_flight_.load(std::memory_order_acquire); }
   uint64_t device_cycles() const { return dev_cycles_; }
+  uint64_t device_batches() const { return dev_batches_; }   // k_batch dispatches that placed pods
   uint64_t device_fallbacks() const { return dev_fallbacks_; }
   float device_last_us() const;
   void device_set_timing(bool on);   // per-cycle event timing (benchmarks)
@@ -626,8 +627,11 @@ class Engine {
   bool pack_node(int32_t idx, void* row) const;   // row: yoda_dev_node_t*
   bool flush_dirty();
   bool schedule_device(const PodReq& req, CycleResult* r);
-  bool schedule_batch_device(const std::vector<uint64_t>& pods, const std::vector<const PodReq*>& reqs,
+  // one k_batch dispatch for pods[0, count) (all batch_eligible), results appended to *out;
+  // false (nothing appended) when the device refuses or fails
+  bool schedule_batch_device(const uint64_t* pods, const PodReq* const* reqs, size_t count,
                              std::vector<CycleResult>* out);
+  bool batch_eligible(const PodReq& q) const;   // device_eligible and no per-node candidate mask
   void make_dev_req(const PodReq& req, yoda_dev_req_t* out);
   bool needs_candidates(const PodReq& req) const;
   // PodTopologySpread PreFilter state of one pod's DoNotSchedule constraints (upstream
@@ -718,7 +722,7 @@ class Engine {
   void* dev_ctx_ = nullptr;
   int dev_cap_ = 0;
   int dev_min_nodes_ = 256;
-  uint64_t dev_cycles_ = 0, dev_fallbacks_ = 0;
+  uint64_t dev_cycles_ = 0, dev_fallbacks_ = 0, dev_batches_ = 0;
   std::vector<char> dirty_;
   std::vector<int32_t> dirty_list_;
   int32_t hard_taint_nodes_ = 0, prefer_taint_nodes_ = 0;
