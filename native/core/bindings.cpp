@@ -336,6 +336,7 @@ PYBIND11_MODULE(_yoda_core, m) {
       .def_readonly("mem", &PodReq::mem)
       .def_readonly("containers", &PodReq::containers)
       .def_readonly("spread_explicit", &PodReq::spread_explicit)
+      .def_readwrite("pod_priority", &PodReq::pod_priority)
       .def_property_readonly("n_ext", [](const PodReq& r) { return r.ext.size(); })
       .def_property_readonly("n_spread", [](const PodReq& r) { return r.spread.size(); });
 
@@ -717,6 +718,44 @@ PYBIND11_MODULE(_yoda_core, m) {
              for (const auto& x : res) r.push_back(e.intern(x));
              e.set_ext_ignored(std::move(r), groups);
            }, py::call_guard<EngineGuard>())
+      // DefaultPreemption on the ledger: pdbs [(namespace, LabelSelector.native() | None,
+      // disruptionsAllowed)] → (node | -1, [victim ids], [cards], PDB violations, potential
+      // nodes, nodes dry-run, candidates)
+      .def("preempt",
+           [](Engine& e, const PodReq& r, int64_t priority, const py::list& pdbs, int32_t min_pct, int32_t min_abs,
+              int64_t offset) {
+             PreemptArgs a;
+             a.priority = priority;
+             a.min_pct = min_pct;
+             a.min_abs = min_abs;
+             a.offset = offset;
+             for (auto t : pdbs) {
+               auto tup = t.cast<py::tuple>();
+               Pdb d;
+               d.ns = e.intern(tup[0].cast<std::string>());
+               d.sel = lsel_of(e, tup[1]);
+               d.allowed = tup[2].cast<int64_t>();
+               a.pdbs.push_back(std::move(d));
+             }
+             PreemptResult o;
+             e.preempt(r, a, &o);
+             return py::make_tuple(o.node, o.victims, o.cards, o.violations, o.potential, o.evaluated, o.candidates);
+           },
+           py::arg("req"), py::arg("priority"), py::arg("pdbs"), py::arg("min_pct") = 10, py::arg("min_abs") = 100,
+           py::arg("offset") = -1, py::call_guard<EngineGuard>())
+      // nodes where preemption might help (first failing filter in upstream order is not
+      // UnschedulableAndUnresolvable), in node-index order
+      .def("preempt_potential",
+           [](Engine& e, const PodReq& r) { return e.preempt_potential(r); }, py::call_guard<EngineGuard>())
+      .def("detach_pod", &Engine::detach_pod, py::call_guard<EngineGuard>())
+      .def("attach_pod", &Engine::attach_pod, py::call_guard<EngineGuard>())
+      // (node, cards, mb per card, reservation time, spec.priority) or None
+      .def("assignment_info",
+           [](Engine& e, uint64_t pod) -> py::object {
+             const Assignment* a = e.assignment(pod);
+             if (!a) return py::none();
+             return py::make_tuple(a->node, a->cards, a->mb, a->t_res, a->prio);
+           }, py::call_guard<EngineGuard>())
       .def("reserve", &Engine::reserve, py::call_guard<EngineGuard>())
       .def("release", &Engine::release, py::call_guard<EngineGuard>())
       .def("has_pod", &Engine::has_pod, py::call_guard<EngineGuard>())
@@ -931,6 +970,18 @@ PYBIND11_MODULE(_yoda_core, m) {
              return py::make_tuple(py::cast(ev), owned);
            })
       .def("keys", &Lane::keys, py::call_guard<py::gil_scoped_release>())
+      // a lane-owned pod by its engine ledger id: (event, node name) or None
+      .def("lookup_id",
+           [](Lane& l, uint64_t id) -> py::object {
+             std::string node;
+             std::shared_ptr<yk::PodEv> ev;
+             {
+               py::gil_scoped_release nogil;
+               ev = l.lookup_id(id, &node);
+             }
+             if (!ev) return py::none();
+             return py::make_tuple(py::cast(ev), node);
+           })
       .def("__len__", &Lane::store_size, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("scheduled", [](Lane& l) { return l.scheduled_.load(std::memory_order_relaxed); })
       .def("set_watermark", &Lane::set_watermark, "signal the eventfd once this many Bindings are acknowledged")

@@ -513,9 +513,36 @@ bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::ve
   a.mb = req.has_memory ? req.memory : 0;
   a.cards.assign(cards.begin(), cards.end());
   a.t_res = now();
+  a.cpu_m = req.cpu_m;
+  a.mem = req.mem;
+  a.nz_cpu_m = req.nz_cpu_m;
+  a.nz_mem = req.nz_mem;
+  a.has_label_mem = req.has_memory;
+  a.label_mem = req.memory;
+  a.prio = req.pod_priority;
+  a.ns = req.ns;
+  a.labset = labset_acquire(req.ns, req.labels);
+  a.deleting = req.deleting;
+  a.aff.reset();
+  a.aff_hash = 0;
+  if (req.aff && !req.aff->empty()) a.aff = req.aff;
+  a.pvc_claims.assign(req.pvc_claims.begin(), req.pvc_claims.end());
+  a.host_ports.assign(req.host_ports.begin(), req.host_ports.end());
+  a.ext.assign(req.ext.begin(), req.ext.end());
+  attach(si);
+  ledger_.insert(pod, si);
+  return true;
+}
+
+// A ledger entry's effect on its node (card reservations, requests, label index and groups,
+// ports, claims, extended resources) and on the cluster-wide affinity sets. reserve / release
+// attach / detach once; a preemption what-if detaches a node's victims and re-attaches them.
+void Engine::attach(int32_t si) {
+  Assignment& a = slab_[si];
+  Node& n = nodes_[a.node];
   if (!compat_) {
     const bool pend = is_pending(n, a);
-    for (int32_t c : cards) {
+    for (int32_t c : a.cards) {
       n.cards[c].reserved_mb += a.mb;
       if (pend) n.cards[c].pending_mb += a.mb;
       n.cards[c].pods += 1;
@@ -523,68 +550,33 @@ bool Engine::reserve(uint64_t pod, const PodReq& req, int32_t idx, const std::ve
   }
   a.slot = (int32_t)n.pods.size();
   n.pods.push_back(si);
-  a.cpu_m = req.cpu_m;
-  a.mem = req.mem;
-  a.nz_cpu_m = req.nz_cpu_m;
-  a.nz_mem = req.nz_mem;
-  a.has_label_mem = req.has_memory;
-  a.label_mem = req.memory;
   n.req_cpu_m += a.cpu_m;
   n.req_mem += a.mem;
   n.nz_cpu_m += a.nz_cpu_m;
   n.nz_mem += a.nz_mem;
   n.pod_count += 1;
   if (a.has_label_mem) n.label_mem_sum += a.label_mem;
-  a.ns = req.ns;
-  a.labset = labset_acquire(req.ns, req.labels);
-  a.deleting = req.deleting;
-  a.aff.reset();
-  a.aff_hash = 0;
-  if (req.aff && !req.aff->empty()) {
-    a.aff = req.aff;
-    aff_holders_.insert(pod);
-    if (!req.aff->req_anti.empty()) anti_holders_.insert(pod);
+  if (a.aff) {
+    aff_holders_.insert(a.pod);
+    if (!a.aff->req_anti.empty()) anti_holders_.insert(a.pod);
     aff_set_add(a);
   }
   index_pod(n, a, +1);
-  a.pvc_claims.assign(req.pvc_claims.begin(), req.pvc_claims.end());
   for (int32_t c : a.pvc_claims) ++n.claims[c];
-  a.host_ports.assign(req.host_ports.begin(), req.host_ports.end());
   for (const HostPort& h : a.host_ports) {
     ++n.ports[h];
     ++n.ports_any[{h.proto, h.port}];
   }
-  a.ext.assign(req.ext.begin(), req.ext.end());
   for (const auto& r : a.ext) {
     auto it = std::lower_bound(n.ext_used.begin(), n.ext_used.end(), std::make_pair(r.first, INT64_MIN));
     if (it != n.ext_used.end() && it->first == r.first) it->second += r.second;
     else n.ext_used.insert(it, r);
   }
-  ledger_.insert(pod, si);
-  mark_dirty(idx);
-  return true;
+  mark_dirty(a.node);
 }
 
-void Engine::free_entry(int32_t si) {
+void Engine::detach(int32_t si) {
   Assignment& a = slab_[si];
-  ledger_.erase(a.pod);
-  labset_release(a.labset);
-  a.labset = -1;
-  a.live = false;
-  a.node = -1;
-  a.slot = -1;
-  a.aff.reset();
-  a.cards.clear();
-  a.ext.clear();
-  a.host_ports.clear();
-  a.pvc_claims.clear();
-  slab_free_.push_back(si);
-}
-
-bool Engine::release(uint64_t pod) {
-  const int32_t si = ledger_.find(pod);
-  if (si < 0) return false;
-  const Assignment& a = slab_[si];
   if (a.node >= 0 && a.node < (int32_t)nodes_.size() && nodes_[a.node].alive) {
     Node& n = nodes_[a.node];
     if (!compat_) {
@@ -603,6 +595,7 @@ bool Engine::release(uint64_t pod) {
       n.pods.pop_back();
       if (last != si) slab_[last].slot = a.slot;
     }
+    a.slot = -1;
     n.req_cpu_m -= a.cpu_m;
     n.req_mem -= a.mem;
     n.nz_cpu_m -= a.nz_cpu_m;
@@ -627,11 +620,270 @@ bool Engine::release(uint64_t pod) {
     mark_dirty(a.node);
   }
   if (a.aff) {
-    aff_holders_.erase(pod);
-    anti_holders_.erase(pod);
+    aff_holders_.erase(a.pod);
+    anti_holders_.erase(a.pod);
     aff_set_remove(a);
   }
+}
+
+void Engine::free_entry(int32_t si) {
+  Assignment& a = slab_[si];
+  ledger_.erase(a.pod);
+  labset_release(a.labset);
+  a.labset = -1;
+  a.live = false;
+  a.detached = false;
+  a.node = -1;
+  a.slot = -1;
+  a.aff.reset();
+  a.cards.clear();
+  a.ext.clear();
+  a.host_ports.clear();
+  a.pvc_claims.clear();
+  slab_free_.push_back(si);
+}
+
+bool Engine::release(uint64_t pod) {
+  const int32_t si = ledger_.find(pod);
+  if (si < 0) return false;
+  if (!slab_[si].detached) detach(si);
   free_entry(si);
+  return true;
+}
+
+// ============================================================== DefaultPreemption
+static bool tolerates(const Toleration& t, const Taint& x);
+
+bool Engine::preemption_might_help(const PodReq& req, int32_t idx) const {
+  // upstream v1.20 default filter order with each plugin's failure code: Unschedulable and
+  // Unresolvable for NodeUnschedulable, NodeName, NodeAffinity, TaintToleration, VolumeBinding,
+  // VolumeZone, a missing spread topology key and unmet required pod affinity; Unschedulable
+  // (preemption may help) for the rest. yoda (out-of-tree, after the defaults) says Unschedulable
+  // — except for a node without a fresh Scv sample, which no eviction can fix (skipped here).
+  const Node& n = nodes_[idx];
+  if (!n.alive) return false;
+  if ((filters_ & F_NODE_UNSCHEDULABLE) && n.unschedulable) {
+    bool tol = false;
+    Taint t{unsched_key_, 0, kNoSchedule};
+    for (const Toleration& x : req.tolerations)
+      if (tolerates(x, t)) { tol = true; break; }
+    if (!tol) return false;
+  }
+  if (filters_ & F_NODE_RESOURCES_FIT) {
+    if (n.pod_count + 1 > n.alloc_pods) return true;
+    if (req.cpu_m > 0 && n.alloc_cpu_m < req.cpu_m + n.req_cpu_m) return true;
+    if (req.mem > 0 && n.alloc_mem < req.mem + n.req_mem) return true;
+    for (const auto& r : req.ext)
+      if (ext_checked(r.first) && ext_amount(n.ext_used, r.first) + r.second > ext_amount(n.ext_alloc, r.first))
+        return true;
+  }
+  if ((filters_ & F_NODE_NAME) && req.node_name > 0 && strings_[req.node_name] != n.name) return false;
+  if ((filters_ & F_NODE_PORTS) && !req.host_ports.empty() && !ports_free(req, n)) return true;
+  if ((filters_ & F_NODE_AFFINITY) && !affinity_ok(req, n)) return false;
+  if ((filters_ & F_TAINT_TOLERATION) && !taints_ok(req, n)) return false;
+  if (req.count_vols && !req.pvc_claims.empty() && !n.vol_limits.empty() && !vols_fit(req, n)) return true;
+  for (const PodReq::VolTerms& v : req.vol) {
+    bool ok = false;
+    for (const SelTerm& t : *v.terms)
+      if (term_matches(t, n)) { ok = true; break; }
+    if (!ok) return false;
+  }
+  return true;   // PodTopologySpread, InterPodAffinity and yoda: preempt_status goes on
+}
+
+bool Engine::detach_pod(uint64_t pod) {
+  const int32_t si = ledger_.find(pod);
+  if (si < 0 || slab_[si].detached) return false;
+  detach(si);
+  slab_[si].detached = true;
+  return true;
+}
+
+bool Engine::attach_pod(uint64_t pod) {
+  const int32_t si = ledger_.find(pod);
+  if (si < 0 || !slab_[si].detached) return false;
+  const Assignment& a = slab_[si];
+  if (a.node < 0 || a.node >= (int32_t)nodes_.size() || !nodes_[a.node].alive) return false;
+  slab_[si].detached = false;
+  attach(si);
+  return true;
+}
+
+int Engine::preempt_status(const PodReq& req, int32_t idx, const SpreadPF* spf, const InterPodPF* ipf) const {
+  // -1: the first failing filter (upstream order) is Unschedulable and Unresolvable; +1: it is
+  // not (or every filter passes)
+  if (!preemption_might_help(req, idx)) return -1;
+  const Node& n = nodes_[idx];
+  // the early-decided resolvable failures (NodeResourcesFit, NodePorts, NodeVolumeLimits) come
+  // before the checks below in upstream order: preemption_might_help returned true for them
+  // too, so the checks below apply only when those pass
+  const bool early = ((filters_ & F_NODE_RESOURCES_FIT) && [&] {
+                       if (n.pod_count + 1 > n.alloc_pods) return true;
+                       if (req.cpu_m > 0 && n.alloc_cpu_m < req.cpu_m + n.req_cpu_m) return true;
+                       if (req.mem > 0 && n.alloc_mem < req.mem + n.req_mem) return true;
+                       for (const auto& r : req.ext)
+                         if (ext_checked(r.first) &&
+                             ext_amount(n.ext_used, r.first) + r.second > ext_amount(n.ext_alloc, r.first))
+                           return true;
+                       return false;
+                     }()) ||
+                     ((filters_ & F_NODE_PORTS) && !req.host_ports.empty() && !ports_free(req, n)) ||
+                     (req.count_vols && !req.pvc_claims.empty() && !n.vol_limits.empty() && !vols_fit(req, n));
+  if (early) return 1;
+  if (spf && !spf->cons.empty()) {
+    const Reason r = spread_filter(req, n, *spf);
+    if (r == RS_SPREAD_LABEL) return -1;
+    if (r != RS_OK) return 1;
+  }
+  if (ipf && ipf->active) {
+    const Reason r = interpod_filter(req, n, *ipf);
+    if (r == RS_POD_AFFINITY) return -1;
+    if (r != RS_OK) return 1;
+  }
+  // yoda: Unschedulable in the reference, but no eviction gives a node a fresh Scv sample
+  if ((filters_ & F_YODA) && (!n.has_scv || (!compat_ && n.stale))) return -1;
+  return 1;
+}
+
+bool Engine::preempt(const PodReq& req, const PreemptArgs& args, PreemptResult* out) {
+  *out = PreemptResult();
+  const std::vector<int32_t> potential = preempt_potential(req);   // nodesWherePreemptionMightHelp
+  out->potential = (int32_t)potential.size();
+  if (potential.empty()) return false;
+  return preempt_over(req, args, potential, out);
+}
+
+std::vector<int32_t> Engine::preempt_potential(const PodReq& req) const {
+  SpreadPF spf;
+  InterPodPF ipf;
+  const bool sp = wants_spread_filter(req), ia = wants_interpod_filter(req);
+  if (sp) spread_prefilter(req, &spf);
+  if (ia) interpod_prefilter(req, &ipf);
+  std::vector<int32_t> potential;
+  for (int32_t i = 0; i < (int32_t)nodes_.size(); ++i)
+    if (preempt_status(req, i, sp ? &spf : nullptr, ia ? &ipf : nullptr) > 0) potential.push_back(i);
+  return potential;
+}
+
+bool Engine::preempt_over(const PodReq& req, const PreemptArgs& args, const std::vector<int32_t>& potential,
+                          PreemptResult* out) {
+  const bool sp = wants_spread_filter(req), ia = wants_interpod_filter(req);
+  if (potential.empty()) return false;
+  // calculateNumCandidates and a random offset (dryRunPreemption walks from it, wrapping)
+  const int32_t np = (int32_t)potential.size();
+  int32_t want = (int32_t)((int64_t)np * args.min_pct / 100);
+  want = std::min(std::max(want, args.min_abs), np);
+  const int32_t offset = args.offset >= 0 ? (int32_t)(args.offset % np) : (int32_t)(rng_() % (uint64_t)np);
+  // a what-if filter: the pre-filter states follow the detached / re-attached pods as upstream's
+  // RunPreFilterExtensionRemovePod / AddPod do (recomputed: only for spread / affinity pods)
+  auto fits = [&](int32_t idx) {
+    if (sp || ia) return filter_node(req, idx, nullptr, nullptr, nullptr) == RS_OK;
+    return filter_node_pf(req, idx, nullptr, nullptr, nullptr, nullptr, nullptr) == RS_OK;
+  };
+  struct Cand {
+    int32_t node;
+    std::vector<int32_t> victims;   // slab indices, in eviction-decision order
+    int32_t violations;
+  };
+  std::vector<Cand> nonviol, viol;
+  std::vector<int32_t> lower;
+  std::vector<std::pair<int32_t, bool>> order;
+  std::vector<int64_t> budget;
+  for (int32_t k = 0; k < np; ++k) {
+    const int32_t idx = potential[(offset + k) % np];
+    ++out->evaluated;
+    Node& n = nodes_[idx];
+    lower.clear();
+    for (int32_t si : n.pods)
+      if (slab_[si].prio < args.priority) lower.push_back(si);
+    if (!lower.empty()) {
+      for (int32_t si : lower) detach(si);
+      if (!fits(idx)) {
+        for (auto it = lower.rbegin(); it != lower.rend(); ++it) attach(*it);
+      } else {
+        // MoreImportantPod: higher priority first, then the earlier start (reservation)
+        std::sort(lower.begin(), lower.end(), [&](int32_t x, int32_t y) {
+          const Assignment &a = slab_[x], &b = slab_[y];
+          return a.prio != b.prio ? a.prio > b.prio : a.t_res != b.t_res ? a.t_res < b.t_res : a.pod < b.pod;
+        });
+        // filterPodsWithPDBViolation: budgets consumed in that order
+        budget.assign(args.pdbs.size(), 0);
+        for (size_t q = 0; q < args.pdbs.size(); ++q) budget[q] = args.pdbs[q].allowed;
+        order.clear();
+        for (int32_t si : lower) {
+          const Assignment& a = slab_[si];
+          bool bad = false;
+          for (size_t q = 0; q < args.pdbs.size(); ++q) {
+            const Pdb& d = args.pdbs[q];
+            if (d.ns != a.ns || d.sel.nothing || d.sel.reqs.empty() || !d.sel.matches(labsets_[a.labset].labels))
+              continue;
+            if (--budget[q] < 0) bad = true;
+          }
+          order.emplace_back(si, bad);
+        }
+        std::stable_partition(order.begin(), order.end(), [](const std::pair<int32_t, bool>& x) { return x.second; });
+        Cand c{idx, {}, 0};
+        for (const auto& o : order) {   // reprieve: PDB-violating victims first, then the others
+          attach(o.first);
+          if (!fits(idx)) {
+            detach(o.first);
+            c.victims.push_back(o.first);
+            c.violations += o.second;
+          }
+        }
+        for (int32_t si : c.victims) attach(si);   // restore the node
+        if (!c.victims.empty()) (c.violations ? viol : nonviol).push_back(std::move(c));
+      }
+    }
+    if (!nonviol.empty() && (int32_t)(nonviol.size() + viol.size()) >= want) break;
+  }
+  out->candidates = (int32_t)(nonviol.size() + viol.size());
+  if (!out->candidates) return false;
+  // pickOneNodeForPreemption over non-violating then violating candidates
+  std::vector<Cand*> all;
+  for (auto& c : nonviol) all.push_back(&c);
+  for (auto& c : viol) all.push_back(&c);
+  struct Key {
+    int32_t violations;
+    int64_t top;          // highest victim priority
+    __int128 sum;         // Σ (priority + MaxInt32 + 1)
+    size_t count;
+    double earliest;      // earliest start among the highest-priority victims (later wins)
+  };
+  auto key_of = [&](const Cand& c) {
+    Key k{c.violations, INT64_MIN, 0, c.victims.size(), 0};
+    for (int32_t si : c.victims) {
+      k.top = std::max(k.top, slab_[si].prio);
+      k.sum += (__int128)slab_[si].prio + ((__int128)1 << 31);
+    }
+    k.earliest = 1e300;
+    for (int32_t si : c.victims)
+      if (slab_[si].prio == k.top) k.earliest = std::min(k.earliest, slab_[si].t_res);
+    return k;
+  };
+  Cand* best = all[0];
+  Key bk = key_of(*best);
+  for (size_t i = 1; i < all.size(); ++i) {
+    const Key k = key_of(*all[i]);
+    bool better;
+    if (k.violations != bk.violations) better = k.violations < bk.violations;
+    else if (k.top != bk.top) better = k.top < bk.top;
+    else if (k.sum != bk.sum) better = k.sum < bk.sum;
+    else if (k.count != bk.count) better = k.count < bk.count;
+    else better = k.earliest > bk.earliest;
+    if (better) {
+      best = all[i];
+      bk = k;
+    }
+  }
+  out->node = best->node;
+  out->violations = best->violations;
+  for (int32_t si : best->victims) out->victims.push_back(slab_[si].pod);
+  // the GPUs the preemptor would take on the nominated node once the victims are gone
+  for (int32_t si : best->victims) detach(si);
+  int32_t q = 10000;
+  if (filters_ & F_YODA) select_gpus(req, best->node, &out->cards, &q);
+  for (auto it = best->victims.rbegin(); it != best->victims.rend(); ++it) attach(*it);
   return true;
 }
 

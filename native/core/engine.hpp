@@ -286,7 +286,8 @@ struct PodReq {
   // scv labels (Go semantics already applied by the caller's parser)
   bool has_number = false, has_memory = false, has_clock = false;
   uint64_t number = 1, memory = 0, clock = 0, clock_min = 0;
-  int64_t priority = 0;
+  int64_t priority = 0;                  // scv/priority (yoda QueueSort)
+  int64_t pod_priority = 0;              // spec.priority (PriorityClass: DefaultPreemption)
   // k8s spec
   int32_t node_name = -1;                // interned spec.nodeName, -1 = none
   int64_t cpu_m = 0, mem = 0;
@@ -377,6 +378,32 @@ struct Assignment {
   uint64_t aff_hash = 0;                           // its AffSet's bucket (aff_sets_)
   std::vector<HostPort> host_ports;                // NodePorts: the host ports it holds on the node
   std::vector<int32_t> pvc_claims;                 // NodeVolumeLimits: the PVC claims it mounts
+  int64_t prio = 0;                                // spec.priority (DefaultPreemption)
+  bool detached = false;                           // off its node for a what-if (detach_pod)
+};
+
+// DefaultPreemption (upstream v1.20 preemption: FindCandidates → SelectCandidate) on the ledger.
+// A PodDisruptionBudget as selectVictimsOnNode reads it: namespace, selector (empty / nil
+// selects nothing), status.disruptionsAllowed
+struct Pdb {
+  int32_t ns = 0;
+  LSel sel;
+  int64_t allowed = 0;
+};
+struct PreemptArgs {
+  int64_t priority = 0;                 // the preemptor's spec.priority
+  std::vector<Pdb> pdbs;
+  int32_t min_pct = 10, min_abs = 100;  // DefaultPreemptionArgs minCandidateNodes{Percentage,Absolute}
+  int64_t offset = -1;                  // dry-run start in the potential nodes; <0: the engine's rng
+};
+struct PreemptResult {
+  int32_t node = -1;                    // nominated node, -1: no candidate
+  std::vector<uint64_t> victims;        // ledger pod ids to evict
+  std::vector<int32_t> cards;           // the GPUs the preemptor takes once they are gone
+  int32_t violations = 0;               // PDB violations of the chosen victims
+  int32_t potential = 0;                // nodes where preemption might help (resolvable status)
+  int32_t evaluated = 0;                // nodes dry-run before the candidate quota was met
+  int32_t candidates = 0;
 };
 
 struct CycleResult {
@@ -516,6 +543,18 @@ class Engine {
   bool select_gpus_small(const Node& n, const std::vector<int32_t>& E, uint64_t k, uint64_t m,
                          std::vector<int32_t>* out, int32_t* quality) const;
 
+  // ---- DefaultPreemption: the pod failed on every node; find the node where evicting the
+  // fewest / least important lower-priority pods lets it fit. The ledger is restored exactly.
+  bool preempt(const PodReq& req, const PreemptArgs& args, PreemptResult* out);
+  std::vector<int32_t> preempt_potential(const PodReq& req) const;
+  // the node's first failing filter in upstream v1.20 plugin order is not
+  // UnschedulableAndUnresolvable (nodesWherePreemptionMightHelp); a node that passes counts too
+  bool preemption_might_help(const PodReq& req, int32_t idx) const;
+  // what-if helpers for the Python spec of preemption: a ledger entry's effect on its node off /
+  // back on, the entry (and its reservation time) kept; false if the pod is unknown or already so
+  bool detach_pod(uint64_t pod);
+  bool attach_pod(uint64_t pod);
+
   // ---- full native cycle
   // candidates: node indices to consider (empty = all). Python filter/score plugins can
   // pre-restrict candidates and add extra per-node scores (extra_scores aligned with
@@ -647,6 +686,9 @@ class Engine {
   Reason filter_node_pf(const PodReq& req, int32_t idx, uint64_t* n, uint64_t* m, uint64_t* c,
                         const SpreadPF* pf, const InterPodPF* ip = nullptr) const;
   bool wants_spread_filter(const PodReq& req) const;
+  int preempt_status(const PodReq& req, int32_t idx, const SpreadPF* spf, const InterPodPF* ipf) const;
+  bool preempt_over(const PodReq& req, const PreemptArgs& args, const std::vector<int32_t>& potential,
+                    PreemptResult* out);
   bool wants_interpod_filter(const PodReq& req) const;
   // InterPodAffinity is a constant (no filter, equal scores) for this pod: device-eligible
   bool interpod_inert(const PodReq& req) const;
@@ -714,6 +756,8 @@ class Engine {
   void labset_sweep();
   void sweep_lab_index(Node& n);
   void free_entry(int32_t si);
+  void attach(int32_t si);
+  void detach(int32_t si);
   std::mt19937_64 rng_{0x59d4};
   double settle_s_ = 30.0;
   double fixed_now_ = -1.0;

@@ -430,6 +430,14 @@ std::shared_ptr<yk::PodEv> Lane::lookup(const std::string& key, bool* owned) {
   return it->second->ev;
 }
 
+std::shared_ptr<yk::PodEv> Lane::lookup_id(uint64_t id, std::string* node) {
+  std::lock_guard<std::mutex> g(store_mu_);
+  auto it = by_id_.find(id);
+  if (it == by_id_.end()) return nullptr;
+  if (node) *node = it->second->node_name;
+  return it->second->ev;
+}
+
 std::vector<std::string> Lane::keys() {
   std::lock_guard<std::mutex> g(store_mu_);
   std::vector<std::string> out;
@@ -977,6 +985,7 @@ bool Lane::make_req(const yk::PodProj& p, PodReq* r) {
   r->clock = c ? str_to_uint(*c) : 0;
   r->clock_min = cm ? str_to_uint(*cm) : 0;
   r->priority = pr ? atoi_or_zero(*pr) : 0;
+  r->pod_priority = p.priority;
   r->node_name = p.node.empty() ? -1 : eng_->intern(p.node);
   r->cpu_m = p.cpu;
   r->mem = p.mem;

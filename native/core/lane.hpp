@@ -212,6 +212,8 @@ class Lane : public yk::PodSink {
   // lane thread; returns the events Python must see. Blocks until processed.
   std::vector<Fwd> relist(std::vector<std::shared_ptr<yk::PodEv>> items);
   std::shared_ptr<yk::PodEv> lookup(const std::string& key, bool* owned);
+  // a lane-owned pod by its engine ledger id (the event and its node), or null
+  std::shared_ptr<yk::PodEv> lookup_id(uint64_t id, std::string* node);
   std::vector<std::string> keys();
   size_t store_size();
   LaneStats stats();

@@ -58,6 +58,7 @@ int main(int argc, char** argv) {
       r.memory = 1024 * (1 + rng() % 32);
       r.cpu_m = 100;
       r.mem = 1 << 28;
+      r.pod_priority = (int64_t)(rng() % 4);
       CycleResult res = e.schedule(next_pod, r, true, {}, {});
       if (res.node >= 0) live.push_back(next_pod);
       ++next_pod;
@@ -66,6 +67,21 @@ int main(int argc, char** argv) {
       if (!e.release(live[k])) return fail("release of a live pod failed", s);
       live[k] = live.back();
       live.pop_back();
+    } else if (op < 88) {
+      // DefaultPreemption what-if: detaches / re-attaches victims on many nodes; the ledger
+      // invariants below must hold exactly afterwards
+      PodReq r;
+      r.has_number = true;
+      r.number = 1 + rng() % 8;
+      r.has_memory = true;
+      r.memory = 100000 + rng() % 190000;
+      r.pod_priority = 5;
+      PreemptArgs a;
+      a.priority = 5;
+      a.min_abs = 1 + (int32_t)(rng() % 50);
+      PreemptResult out;
+      e.preempt(r, a, &out);
+      if (out.node >= 0 && out.victims.empty()) return fail("preemption without victims", s);
     } else if (op < 95) {
       int idx = (int)(rng() % e.num_nodes());
       if (e.node(idx).alive) e.set_cards(idx, make_cards(8), 8, 0, 8 * 294912, false, (double)s);

@@ -904,8 +904,11 @@ class Scheduler:
             if self.lane is not None and self._lane_held != "held" and pi.priority > self.lane.preempt_above(fw):
                 prev = self._lane_held
                 self._lane_held = "held"
+                # park the lane for the ledger what-ifs; mirror lane pods only for a Python
+                # what-if (the native search reads the ledger, which holds them)
+                sync = any(getattr(p, "needs_mirror", lambda _pod: True)(pi) for p in fw.post_filter)
                 try:
-                    with self.lane.held():        # mirror lane pods, park the lane: ledger what-ifs
+                    with self.lane.held(sync=sync):
                         return self._fail(fw, state, pi, cycle, msg, t0, unschedulable)
                 finally:
                     self._lane_held = prev

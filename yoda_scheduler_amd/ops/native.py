@@ -225,7 +225,7 @@ def pod_req(engine, pi: PodInfo):
     if not (pi.node_name or pi.node_selector or pi.required_terms or pi.preferred_terms or pi.tolerations
             or pi.ext or pi.spread or pi.pod_aff or pi.host_ports or pi.flags & PF_CLAIMS):
         key = (pi.gpu, pi.cpu_m, pi.mem, pi.nz_cpu_m, pi.nz_mem, pi.namespace, tuple(pi.labels.items()),
-               tuple(pi.images), pi.containers, pi.owner, pi.avoid, pi.deleting)
+               tuple(pi.images), pi.containers, pi.owner, pi.avoid, pi.deleting, pi.priority)
         shared = _shared_reqs
         if shared[0] is None or shared[0]() is not engine:   # weak: a shut-down engine is freed
             shared[0], shared[1] = weakref.ref(engine), {}
@@ -240,6 +240,8 @@ def pod_req(engine, pi: PodInfo):
                         pi.tolerations, pi.nz_cpu_m, pi.nz_mem)
     engine.set_req_extras(r, pi.namespace, list(pi.labels.items()), pi.deleting, pi.images, pi.containers,
                           list(pi.ext.items()), pi.owner, pi.avoid, pi.spread, pi.pod_aff)
+    if pi.priority:
+        r.pod_priority = pi.priority      # spec.priority: what DefaultPreemption compares on the ledger
     if pi.host_ports:
         from ..plugins.defaults import host_port_set
         engine.set_req_ports(r, [(port, proto, ip) for ip, proto, port in sorted(host_port_set(pi.host_ports))])

@@ -280,16 +280,6 @@ class DefaultPreemption(PostFilterPlugin):
                         allowed))
         return out
 
-    @staticmethod
-    def _violates(pdbs: list, info, budget: dict) -> bool:
-        """Evicting ``info`` would exceed some PDB's remaining budget (consumes it)."""
-        bad = False
-        for k, (ns, sel, _allowed) in enumerate(pdbs):
-            if ns == info.namespace and sel.matches(info.labels):
-                budget[k] -= 1
-                bad = bad or budget[k] < 0
-        return bad
-
     def _eligible(self, pod) -> bool:
         if (pod.obj.get("spec") or {}).get("preemptionPolicy") == "Never":
             return False
@@ -304,6 +294,49 @@ class DefaultPreemption(PostFilterPlugin):
                 return False
         return True
 
+    def _python_filters(self, pod) -> bool:
+        """A Python filter or PreFilter of the profile applies to the pod: the what-if must
+        re-run them (the Python path below); otherwise the engine's native search decides."""
+        fw = self.framework
+        return fw is not None and (fw.has_active_filter_py(pod) or any(fw._applies(p, pod) for p in fw.pre_filter))
+
+    def needs_mirror(self, pod) -> bool:
+        """The Python what-if walks the cache's pods (lane pods mirrored into it); the native
+        search reads the engine ledger, which holds every pod."""
+        return self._python_filters(pod) or not hasattr(self.handle.engine, "preempt")
+
+    def _native(self, pod, req, pdbs) -> tuple[Optional[PostFilterResult], Status]:
+        """upstream v1.20 preemption in the engine (Engine::preempt): nodesWherePreemptionMightHelp
+        (nodes whose first failing filter is UnschedulableAndUnresolvable are skipped), at most
+        max(minCandidateNodesPercentage % of them, minCandidateNodesAbsolute) candidates dry-run
+        from a random offset, selectVictimsOnNode's reprieve order (PDB-violating first, then by
+        importance) and pickOneNodeForPreemption's ranking — on the ledger, lane pods included."""
+        h = self.handle
+        eng, cache = h.engine, h.cache
+        pct = int(self.args.get("minCandidateNodesPercentage", 10))
+        absolute = int(self.args.get("minCandidateNodesAbsolute", 100))
+        native_pdbs = [(ns, sel.native(), allowed) for ns, sel, allowed in pdbs]
+        node_idx, ids, cards, _viol, *_ = eng.preempt(req, pod.priority, native_pdbs, pct, absolute)
+        if node_idx < 0:
+            return None, Status.unschedulable("preemption: no node can be freed", plugin=self.name)
+        node = eng.node_name(node_idx)
+        want = set(ids)
+        victims = []
+        for uid in cache.node_pods.get(node, ()):        # Python-owned pods on the node
+            ps = cache.pods.get(uid)
+            if ps is not None and ps.info.num_id in want:
+                victims.append(ps.info)
+                want.discard(ps.info.num_id)
+        lane = getattr(cache, "lane", None)
+        if want and lane is not None:                   # lane-owned pods: the lane's store
+            from ..models.pod import PodInfo
+            for lid in sorted(want):
+                got = lane.lookup_id(lid)
+                if got is not None:
+                    victims.append(PodInfo.from_native(got[0]))
+        h.preempt(pod, node, victims)
+        return PostFilterResult(node, list(cards)), Status.ok()
+
     def post_filter(self, state: CycleState, pod, statuses: dict) -> tuple[Optional[PostFilterResult], Status]:
         h = self.handle
         if pod.priority <= 0 and not self.args.get("preemptZeroPriority", False):
@@ -316,61 +349,151 @@ class DefaultPreemption(PostFilterPlugin):
         req = pod_req(eng, pod)
         pdbs = self._pdbs()
         fw = self.framework
-        py = fw is not None and (fw.has_active_filter_py(pod) or
-                                 any(fw._applies(p, pod) for p in fw.pre_filter))
+        py = self._python_filters(pod)
+        if not py and hasattr(eng, "preempt"):
+            return self._native(pod, req, pdbs)
+        pct = int(self.args.get("minCandidateNodesPercentage", 10))
+        absolute = int(self.args.get("minCandidateNodesAbsolute", 100))
 
         def fits(node: str, idx: int) -> bool:
             return eng.filter_node(req, idx) == 0 and (not py or fw.passes_py_filters(pod, node))
 
-        best = None
-        for node, ps_uids in list(cache.node_pods.items()):
-            idx = eng.node_index(node)
-            if idx < 0:
-                continue
-            lower = [cache.pods[u] for u in ps_uids if u in cache.pods and cache.pods[u].info.priority < pod.priority]
-            if not lower:
-                continue
-            for ps in lower:
-                eng.release(ps.info.num_id)
-            if py:
-                cache.hide([ps.info.uid for ps in lower])
-            try:
-                if not fits(node, idx):                     # no candidate: put everything back
-                    for ps in lower:
-                        eng.reserve(ps.info.num_id, pod_req(eng, ps.info), idx, list(ps.cards))
-                    continue
-                victims, violations = [], 0
-                budget = {k: allowed for k, (_ns, _sel, allowed) in enumerate(pdbs)}
-                flagged = [(self._violates(pdbs, ps.info, budget), ps) for ps in lower]
-                # reprieve PDB-violating pods first, then higher priorities first
-                for violating, ps in sorted(flagged, key=lambda t: (not t[0], -t[1].info.priority)):
-                    eng.reserve(ps.info.num_id, pod_req(eng, ps.info), idx, list(ps.cards))
-                    if py:
-                        cache.unhide([ps])
-                    if not fits(node, idx):
-                        eng.release(ps.info.num_id)
-                        if py:
-                            cache.hide([ps.info.uid])
-                        victims.append(ps)
-                        violations += violating
-                # the GPUs the preemptor would take once the victims are gone
-                ok_cards, cards, _q = eng.select_gpus(req, idx)
-                # restore the ledger exactly (victims are still released at this point)
-                for ps in victims:
-                    eng.reserve(ps.info.num_id, pod_req(eng, ps.info), idx, list(ps.cards))
-            finally:
-                if py:
-                    cache.unhide([ps for ps in lower if ps.info.uid not in cache.pods])
-            if victims:
-                prios = [v.info.priority for v in victims]
-                key = (violations, max(prios), sum(prios), len(victims))
-                if best is None or key < best[0]:
-                    best = (key, node, victims, list(cards) if ok_cards else [])
+        best = preempt_spec(eng, cache, pod, req, pdbs, pct, absolute, fits=fits, hide=py)
         if best is None:
             return None, Status.unschedulable("preemption: no node can be freed", plugin=self.name)
-        _, node, victims, cards = best
+        node, victims, cards = best
         h.preempt(pod, node, [v.info for v in victims])
         return PostFilterResult(node, cards), Status.ok()
+
+
+# upstream v1.20 filter order and whether a failure is UnschedulableAndUnresolvable (preemption
+# cannot help): the native engine's plugin bits with the reason names each reports
+_PREEMPT_ORDER = ("F_NODE_UNSCHEDULABLE", "F_NODE_RESOURCES_FIT", "F_NODE_NAME", "F_NODE_PORTS", "F_NODE_AFFINITY",
+                  "F_TAINT_TOLERATION", "F_SPREAD", "F_INTERPOD", "F_YODA")
+_UNRESOLVABLE = frozenset({"NodeUnschedulable", "NodeName", "NodeAffinity", "TaintToleration", "VolumeBinding",
+                           "VolumeZone", "PodTopologySpreadLabel", "InterPodAffinity", "NoScv", "ScvStale", "NodeGone"})
+
+
+def preemption_might_help(eng, req, idx: int) -> bool:
+    """nodesWherePreemptionMightHelp for one node: the first failing filter in upstream order is
+    not UnschedulableAndUnresolvable (a node that passes counts too). The engine evaluates one
+    plugin at a time (its ``filters`` mask), so the order here is upstream's, not the engine's."""
+    from ..ops.native import core
+    C = core()
+    saved = eng.filters
+    try:
+        for name in _PREEMPT_ORDER:
+            bit = getattr(C, name)
+            if not saved & bit:
+                continue
+            eng.filters = bit
+            r = C.REASONS[eng.filter_node(req, idx)]
+            if r != "OK":
+                return r not in _UNRESOLVABLE
+        return True
+    finally:
+        eng.filters = saved
+
+
+def preempt_spec(eng, cache, pod, req, pdbs: list, pct: int = 10, absolute: int = 100, offset: int = -1,
+                 fits=None, hide: bool = False, rng=None):
+    """Python spec of upstream v1.20 preemption over the engine ledger (``Engine::preempt`` is
+    its native twin; tests/test_preemption_native.py pins the two together):
+
+    * potential nodes: ``preemption_might_help``; ``numCandidates`` = max(``pct`` % of them,
+      ``absolute``) capped at their count; dry-run from ``offset`` (random when < 0), wrapping,
+      until a non-violating candidate exists and the candidates reach ``numCandidates``;
+    * selectVictimsOnNode: every lower-priority pod off the node (a what-if); no fit → no
+      candidate. Otherwise the pods by MoreImportantPod (priority, then earlier start = earlier
+      reservation), PDB budgets consumed in that order, PDB-violating ones reprieved first;
+    * pickOneNodeForPreemption: fewest PDB violations, lowest highest victim priority, lowest
+      Σ (priority + 2^31), fewest victims, latest earliest start among the top-priority victims,
+      then the first (non-violating candidates before violating ones).
+
+    Returns (node, victims [PodState], cards) or None."""
+    import random as _random
+    fits = fits or (lambda node, idx: eng.filter_node(req, idx) == 0)
+    names = {}
+    potential = []
+    for node in cache.nodes:
+        idx = eng.node_index(node)
+        if idx >= 0:
+            names[idx] = node
+    for idx in sorted(names):
+        if preemption_might_help(eng, req, idx):
+            potential.append(idx)
+    if not potential:
+        return None
+    np_ = len(potential)
+    want = min(max(np_ * pct // 100, absolute), np_)
+    start = offset % np_ if offset >= 0 else (rng or _random).randrange(np_)
+    nonviol, viol = [], []
+    for k in range(np_):
+        idx = potential[(start + k) % np_]
+        node = names[idx]
+        lower = []
+        for u in cache.node_pods.get(node, ()):
+            ps = cache.pods.get(u)
+            info = eng.assignment_info(ps.info.num_id) if ps is not None else None
+            if info is not None and info[0] == idx and info[4] < pod.priority:
+                lower.append((ps, info[3], info[4]))
+        if lower:
+            for ps, _t, _p in lower:
+                eng.detach_pod(ps.info.num_id)
+            if hide:
+                cache.hide([ps.info.uid for ps, _t, _p in lower])
+            try:
+                if not fits(node, idx):
+                    for ps, _t, _p in lower:
+                        eng.attach_pod(ps.info.num_id)
+                else:
+                    lower.sort(key=lambda x: (-x[2], x[1], x[0].info.num_id))
+                    budget = [allowed for _ns, _sel, allowed in pdbs]
+                    flagged = []
+                    for ps, t, pr in lower:
+                        bad = False
+                        for q, (ns, sel, _a) in enumerate(pdbs):
+                            if ns != ps.info.namespace or sel.empty or not sel.matches(ps.info.labels):
+                                continue
+                            budget[q] -= 1
+                            bad = bad or budget[q] < 0
+                        flagged.append((bad, ps, t, pr))
+                    victims, violations = [], 0
+                    for bad, ps, t, pr in [f for f in flagged if f[0]] + [f for f in flagged if not f[0]]:
+                        eng.attach_pod(ps.info.num_id)
+                        if hide:
+                            cache.unhide([ps])
+                        if not fits(node, idx):
+                            eng.detach_pod(ps.info.num_id)
+                            if hide:
+                                cache.hide([ps.info.uid])
+                            victims.append((ps, t, pr))
+                            violations += bad
+                    for ps, _t, _p in victims:
+                        eng.attach_pod(ps.info.num_id)
+                    if victims:
+                        (viol if violations else nonviol).append((node, idx, victims, violations))
+            finally:
+                if hide:
+                    cache.unhide([ps for ps, _t, _p in lower if ps.info.uid not in cache.pods])
+        if nonviol and len(nonviol) + len(viol) >= want:
+            break
+    cands = nonviol + viol
+    if not cands:
+        return None
+
+    def rank(c):
+        _node, _idx, victims, violations = c
+        top = max(pr for _ps, _t, pr in victims)
+        earliest = min(t for _ps, t, pr in victims if pr == top)
+        return (violations, top, sum(pr + (1 << 31) for _ps, _t, pr in victims), len(victims), -earliest)
+    node, idx, victims, _v = min(cands, key=rank)     # min keeps the first of equal keys
+    for ps, _t, _p in victims:
+        eng.detach_pod(ps.info.num_id)
+    ok_cards, cards, _q = eng.select_gpus(req, idx)
+    for ps, _t, _p in victims:
+        eng.attach_pod(ps.info.num_id)
+    return node, [ps for ps, _t, _p in victims], (list(cards) if ok_cards else [])
 
 
 def register_defaults(registry) -> None:
