@@ -179,6 +179,10 @@ PYBIND11_MODULE(_yoda_kube, m) {
       });
 
   m.def("project", &project_bytes, py::arg("raw"), "Project a pod's JSON (tests / tooling).");
+  // every watch event allocates, fills and frees one PodEv on two threads: its size is a cost of
+  // every pod event (round 5 grew it 984 → 1184 bytes, −8 % on the headline; tests pin it)
+  m.attr("SIZEOF_POD_EV") = (int)sizeof(PodEv);
+  m.attr("SIZEOF_POD_PROJ") = (int)sizeof(PodProj);
   m.def("project_flat_nohash", [](const std::string& raw) {
     auto pe = std::make_shared<PodEv>();
     FlatDoc d;

@@ -624,9 +624,14 @@ def test_bench_headline_reset_stays_small_and_mirror_off():
         assert d["pods_bound"] == 3000 and d["pods_unschedulable"] == 0
         assert d["lane_log_on"] is False
         bursts = sorted(s - rs for s, rs in zip(d["step_ms"], d["reset_ms"]))
-        if d["reset_ms_median"] <= 0.5 * bursts[len(bursts) // 2] or attempt == 1:
+        # absolute: against the host's single-thread calibration loop (a
+        # ratio to the burst let a +55 % reset pass). MI355X boxes: 0.26-0.29x with the fix,
+        # 0.39x at round 5's regression; this container runs ~2x slower per event and noisier
+        calib = d["host"]["calib_loop_ms"]
+        if d["reset_ms_median"] <= 1.0 * calib or attempt == 1:
             break
     assert d["reset_ms_median"] <= 0.5 * bursts[len(bursts) // 2], (d["reset_ms"], d["step_ms"])
+    assert d["reset_ms_median"] <= 1.0 * calib, (d["reset_ms"], calib)
     assert d["burst_only_pods_per_s"] >= d["value"]
     # the engine's share of a lane pod stays a small part of the scheduler's CPU per pod
     assert d["lane_engine_us_per_pod"]["cpu"] <= 0.5 * d["cpu_us_per_pod"]
