@@ -837,9 +837,9 @@ void Lane::apply_gates(std::vector<Fwd>* out) {
 }
 
 bool Lane::claims_in_table(const yk::PodProj& p) const {
-  if (p.claims.empty() || claim_table_.empty()) return false;
+  if (p.cold().claims.empty() || claim_table_.empty()) return false;
   std::string key;
-  for (const std::string& c : p.claims) {
+  for (const std::string& c : p.cold().claims) {
     key.assign(p.ns).append("/").append(c);
     if (!claim_table_.count(key)) return false;
   }
@@ -848,7 +848,7 @@ bool Lane::claims_in_table(const yk::PodProj& p) const {
 
 bool Lane::claim_cons(const yk::PodProj& p, std::vector<ClaimConsP>* out) const {
   std::string key;
-  for (const std::string& c : p.claims) {
+  for (const std::string& c : p.cold().claims) {
     key.assign(p.ns).append("/").append(c);
     auto it = claim_table_.find(key);
     if (it == claim_table_.end()) return false;
@@ -901,7 +901,7 @@ void Lane::apply_claims(std::vector<Fwd>* out) {
     if (e->st != QUEUED && e->st != PARKED && e->st != BACKOFF) continue;
     const yk::PodProj& p = e->ev->full();
     if (!(p.flags & yk::PF_CLAIMS)) continue;
-    for (const std::string& c : p.claims) {
+    for (const std::string& c : p.cold().claims) {
       key.assign(p.ns).append("/").append(c);
       if (removed.count(key)) {
         evict.push_back(e);
@@ -991,7 +991,7 @@ bool Lane::make_req(const yk::PodProj& p, PodReq* r) {
   r->mem = p.mem;
   r->nz_cpu_m = p.nzc;
   r->nz_mem = p.nzm;
-  for (const auto& kv : p.node_selector) r->node_selector.emplace_back(eng_->intern(kv.first), eng_->intern(kv.second));
+  for (const auto& kv : p.cold().node_selector) r->node_selector.emplace_back(eng_->intern(kv.first), eng_->intern(kv.second));
   auto term = [&](const yk::TermP& t, SelTerm* out) {
     for (const auto& q : t) {
       SelReq x;
@@ -1010,18 +1010,18 @@ bool Lane::make_req(const yk::PodProj& p, PodReq* r) {
     }
     return true;
   };
-  for (const auto& t : p.req_terms) {
+  for (const auto& t : p.cold().req_terms) {
     SelTerm st;
     if (!term(t, &st)) return false;
     r->required_terms.push_back(std::move(st));
   }
-  for (const auto& wt : p.pref_terms) {
+  for (const auto& wt : p.cold().pref_terms) {
     PrefTerm pt;
     pt.weight = (int32_t)wt.first;
     if (!term(wt.second, &pt.term)) return false;
     r->preferred_terms.push_back(std::move(pt));
   }
-  for (const auto& t : p.tolerations) {
+  for (const auto& t : p.cold().tolerations) {
     Toleration x;
     x.key = t.has_key ? eng_->intern(t.key) : -1;
     if (x.key == 0) x.key = -1;
@@ -1036,13 +1036,13 @@ bool Lane::make_req(const yk::PodProj& p, PodReq* r) {
   r->deleting = p.deleting;
   for (const auto& im : p.images) r->images.push_back(eng_->intern(im));
   r->containers = p.containers;
-  for (const auto& x : p.ext) r->ext.emplace_back(eng_->intern(x.first), x.second);
+  for (const auto& x : p.cold().ext) r->ext.emplace_back(eng_->intern(x.first), x.second);
   std::sort(r->ext.begin(), r->ext.end());
   HostPort hp;
-  for (const auto& x : p.ports)
+  for (const auto& x : p.cold().ports)
     if (eng_->host_port(x.host_port, x.protocol, x.host_ip, &hp)) r->host_ports.push_back(hp);
-  for (size_t i = 0; i < p.claims.size(); ++i)   // the ledger keeps every pod's PVC claims (NodeVolumeLimits)
-    if (i < p.claim_pvc.size() && p.claim_pvc[i]) r->pvc_claims.push_back(eng_->intern(p.ns + "/" + p.claims[i]));
+  for (size_t i = 0; i < p.cold().claims.size(); ++i)   // the ledger keeps every pod's PVC claims (NodeVolumeLimits)
+    if (i < p.cold().claim_pvc.size() && p.cold().claim_pvc[i]) r->pvc_claims.push_back(eng_->intern(p.ns + "/" + p.cold().claims[i]));
   if (const yk::PodProj::Owners* o = p.owners.get()) {
     if (o->has_owner) {
       r->owner_kind = o->owner_api == "v1" && o->owner_kind == "ReplicationController" ? 1
@@ -1055,8 +1055,8 @@ bool Lane::make_req(const yk::PodProj& p, PodReq* r) {
       r->avoid_uid = eng_->intern(o->avoid_uid);
     }
   }
-  r->spread_explicit = !p.spread.empty();
-  for (const auto& c : p.spread) {
+  r->spread_explicit = !p.cold().spread.empty();
+  for (const auto& c : p.cold().spread) {
     if (c.when == 2) continue;               // neither DoNotSchedule nor ScheduleAnyway: in no list
     SpreadC x;
     x.key = eng_->intern(c.key);
@@ -1073,7 +1073,7 @@ bool Lane::make_req(const yk::PodProj& p, PodReq* r) {
     }
     r->spread.push_back(std::move(x));
   }
-  if (p.has_pod_aff) {
+  if (p.cold().has_pod_aff) {
     auto pa = std::make_shared<PodAffinity>();
     auto conv = [&](const std::vector<yk::PodProj::PodTermP>& src, std::vector<PodTerm>* dst) {
       for (const auto& t : src) {
@@ -1095,8 +1095,8 @@ bool Lane::make_req(const yk::PodProj& p, PodReq* r) {
       }
       return true;
     };
-    if (!conv(p.aff_req, &pa->req_aff) || !conv(p.anti_req, &pa->req_anti) || !conv(p.aff_pref, &pa->pref_aff) ||
-        !conv(p.anti_pref, &pa->pref_anti))
+    if (!conv(p.cold().aff_req, &pa->req_aff) || !conv(p.cold().anti_req, &pa->req_anti) || !conv(p.cold().aff_pref, &pa->pref_aff) ||
+        !conv(p.cold().anti_pref, &pa->pref_anti))
       return false;
     if (!pa->empty()) r->aff = std::move(pa);
   }
@@ -1769,7 +1769,7 @@ std::string Lane::fit_error(const CycleResult& r, const yk::PodProj& p) const {
     if (i == RS_EXT_RESOURCES) {
       // framework/scheduler.py::ext_text: "Insufficient <the pod's resources beyond cpu/memory>"
       std::vector<std::string> names;
-      for (const auto& x : p.ext) names.push_back(x.first);
+      for (const auto& x : p.cold().ext) names.push_back(x.first);
       std::sort(names.begin(), names.end());
       std::string t = "Insufficient ";
       for (size_t k = 0; k < names.size(); ++k) t += (k ? "/" : "") + names[k];

@@ -51,7 +51,7 @@ py::object sel_tuple(bool has, const std::vector<KV>& labels, const std::vector<
 // (required affinity, required anti, preferred affinity, preferred anti) of
 // (topologyKey, namespaces | None, selector | None, weight), or None without pod (anti-)affinity
 py::object pod_aff_tuple(const PodProj& p) {
-  if (!p.has_pod_aff) return py::none();
+  if (!p.cold().has_pod_aff) return py::none();
   auto lst = [](const std::vector<PodProj::PodTermP>& v) {
     py::list out;
     for (const auto& t : v) {
@@ -65,39 +65,39 @@ py::object pod_aff_tuple(const PodProj& p) {
     }
     return out;
   };
-  return py::make_tuple(lst(p.aff_req), lst(p.anti_req), lst(p.aff_pref), lst(p.anti_pref));
+  return py::make_tuple(lst(p.cold().aff_req), lst(p.cold().anti_req), lst(p.cold().aff_pref), lst(p.cold().anti_pref));
 }
 
 py::tuple info_args(const PodProj& p) {
-  py::object ann = p.has_annotations ? kv_dict(p.annotations) : py::none();
-  py::object nsel = p.has_node_selector ? kv_dict(p.node_selector) : py::none();
+  py::object ann = p.cold().has_annotations ? kv_dict(p.cold().annotations) : py::none();
+  py::object nsel = p.cold().has_node_selector ? kv_dict(p.cold().node_selector) : py::none();
   py::object req = py::none(), pref = py::none();
-  if (p.has_affinity) {
+  if (p.cold().has_affinity) {
     py::list r;
-    for (const auto& t : p.req_terms) r.append(term_list(t));
+    for (const auto& t : p.cold().req_terms) r.append(term_list(t));
     py::list pf;
-    for (const auto& wt : p.pref_terms) pf.append(py::make_tuple(wt.first, term_list(wt.second)));
+    for (const auto& wt : p.cold().pref_terms) pf.append(py::make_tuple(wt.first, term_list(wt.second)));
     req = std::move(r);
     pref = std::move(pf);
   }
   py::object tols = py::none();
-  if (!p.tolerations.empty()) {
+  if (!p.cold().tolerations.empty()) {
     py::list t;
-    for (const auto& x : p.tolerations)
+    for (const auto& x : p.cold().tolerations)
       t.append(py::make_tuple(x.has_key ? py::object(py::str(x.key)) : py::object(py::none()), py::str(x.value),
                               py::str(x.op), py::str(x.effect)));
     tols = std::move(t);
   }
   py::object ports = py::none();
-  if (!p.ports.empty()) {
+  if (!p.cold().ports.empty()) {
     py::list t;
-    for (const auto& x : p.ports) t.append(py::make_tuple(x.host_port, py::str(x.protocol), py::str(x.host_ip)));
+    for (const auto& x : p.cold().ports) t.append(py::make_tuple(x.host_port, py::str(x.protocol), py::str(x.host_ip)));
     ports = std::move(t);
   }
   py::object ext = py::none();
-  if (!p.ext.empty()) {
+  if (!p.cold().ext.empty()) {
     py::dict d;
-    for (const auto& e : p.ext) d[py::str(e.first)] = e.second;
+    for (const auto& e : p.cold().ext) d[py::str(e.first)] = e.second;
     ext = std::move(d);
   }
   py::list images;
@@ -109,11 +109,11 @@ py::tuple info_args(const PodProj& p) {
   py::object avoid = o && o->has_avoid ? py::object(py::make_tuple(py::str(o->avoid_kind), py::str(o->avoid_uid)))
                                        : py::object(py::none());
   py::object spread = py::none();
-  if (!p.spread.empty()) {
+  if (!p.cold().spread.empty()) {
     // (topologyKey, maxSkew, whenUnsatisfiable, LabelSelector.native() tuple | None)
     static const char* kWhen[3] = {"DoNotSchedule", "ScheduleAnyway", "?"};
     py::list l;
-    for (const auto& c : p.spread) {
+    for (const auto& c : p.cold().spread) {
       py::object sel = sel_tuple(c.has_sel, c.labels, c.exprs);
       l.append(py::make_tuple(py::str(c.key), c.max_skew, py::str(kWhen[c.when]), sel));
     }
@@ -156,7 +156,7 @@ PYBIND11_MODULE(_yoda_kube, m) {
       .def_property_readonly("deleting", [](const PodEv& e) { return e.p.deleting; })
       .def_property_readonly("hash", [](const PodEv& e) { return e.hash(); })
       .def_property_readonly("flags", [](const PodEv& e) { return e.full().flags; })
-      .def_property_readonly("claims", [](const PodEv& e) { return e.full().claims; })
+      .def_property_readonly("claims", [](const PodEv& e) { return e.full().cold().claims; })
       .def_property_readonly("labels_hash", [](const PodEv& e) { return e.p.labels_hash; })
       // status.conditions' PodScheduled entry: (status, reason, message, lastTransitionTime) or None
       .def_property_readonly("sched_cond", [](const PodEv& e) -> py::object {

@@ -336,6 +336,16 @@ thread_local bool t_skip_hash = false;   // project_pod_nohash
 template <class N>
 void project_generic(N pod, PodProj& p) {
   p = PodProj();
+  // the rarely-present fields go into one record, attached when the projection ends (every
+  // early return included) if any is set
+  struct ColdCommit {
+    PodProj& p;
+    PodProj::Cold c;
+    ~ColdCommit() {
+      if (!c.empty()) p.cold_ = std::make_shared<const PodProj::Cold>(std::move(c));
+    }
+  } commit{p, {}};
+  PodProj::Cold& cx = commit.c;
   N meta = pod.get("metadata");
   N spec = pod.get("spec");
   const N m = meta.obj() ? meta : N{};
@@ -376,8 +386,8 @@ void project_generic(N pod, PodProj& p) {
   // ---- everything below: fall back to Python on any shape the projection does not mirror
   if (!kvs(m.get("labels"), p.labels)) return;
   if (N a = m.get("annotations"); a && a.truthy()) {
-    p.has_annotations = true;
-    if (!kvs(a, p.annotations)) return;
+    cx.has_annotations = true;
+    if (!kvs(a, cx.annotations)) return;
   } else if (a && !a.null_t() && !a.obj()) {
     return;
   }
@@ -454,7 +464,7 @@ void project_generic(N pod, PodProj& p) {
           N ip = pt.get("hostIP");
           if (ip && !ip.str_t()) return false;
           port.host_ip = ip ? std::string(ip.str()) : "";
-          p.ports.push_back(std::move(port));
+          cx.ports.push_back(std::move(port));
           return true;
         });
         if (!pok) return false;
@@ -505,17 +515,17 @@ void project_generic(N pod, PodProj& p) {
   p.nzc = nzc;
   p.nzm = nzm;
   for (auto& e : ext)
-    if (e.second) p.ext.push_back(std::move(e));
-  if (!p.ext.empty()) flags |= PF_EXTENDED;
-  if (!p.ports.empty()) flags |= PF_HOST_PORTS;
+    if (e.second) cx.ext.push_back(std::move(e));
+  if (!cx.ext.empty()) flags |= PF_EXTENDED;
+  if (!cx.ports.empty()) flags |= PF_HOST_PORTS;
 
   if (N ns = sp.get("nodeSelector"); ns && ns.truthy()) {
-    p.has_node_selector = true;
-    if (!kvs(ns, p.node_selector)) return;
+    cx.has_node_selector = true;
+    if (!kvs(ns, cx.node_selector)) return;
   }
   if (N aff = sp.get("affinity"); aff && aff.truthy()) {
     if (!aff.obj()) return;
-    p.has_affinity = true;
+    cx.has_affinity = true;
     N na = aff.get("nodeAffinity");
     if (na && na.truthy()) {
       if (!na.obj()) return;
@@ -527,7 +537,7 @@ void project_generic(N pod, PodProj& p) {
           bool ok = terms.each([&](std::string_view, N t) {
             TermP tp;
             if (!term_of(t, tp)) return false;
-            p.req_terms.push_back(std::move(tp));
+            cx.req_terms.push_back(std::move(tp));
             return true;
           });
           if (!ok) return;
@@ -547,7 +557,7 @@ void project_generic(N pod, PodProj& p) {
           N pref = x.get("preference");
           if (pref && !pref.obj() && !pref.null_t()) return false;
           if (!term_of(pref && pref.truthy() ? pref : N{}, tp)) return false;
-          p.pref_terms.emplace_back(w, std::move(tp));
+          cx.pref_terms.emplace_back(w, std::move(tp));
           return true;
         });
         if (!ok) return;
@@ -594,8 +604,8 @@ void project_generic(N pod, PodProj& p) {
       return true;
     };
     if ((pa && pa.truthy()) || (paa && paa.truthy())) {
-      p.has_pod_aff = true;
-      if (!terms_of(pa, p.aff_req, p.aff_pref) || !terms_of(paa, p.anti_req, p.anti_pref)) return;
+      cx.has_pod_aff = true;
+      if (!terms_of(pa, cx.aff_req, cx.aff_pref) || !terms_of(paa, cx.anti_req, cx.anti_pref)) return;
     }
   }
   if (N tols = sp.get("tolerations"); tols && tols.truthy()) {
@@ -616,7 +626,7 @@ void project_generic(N pod, PodProj& p) {
       N ef = t.get("effect");
       if (ef && !ef.str_t() && !ef.null_t()) return false;
       tp.effect = (ef && ef.str_t()) ? std::string(ef.str()) : "";
-      p.tolerations.push_back(std::move(tp));
+      cx.tolerations.push_back(std::move(tp));
       return true;
     });
     if (!ok) return;
@@ -647,7 +657,7 @@ void project_generic(N pod, PodProj& p) {
         x.has_sel = true;
         if (!label_selector_of(ls, x.labels, x.exprs)) return false;
       }
-      p.spread.push_back(std::move(x));
+      cx.spread.push_back(std::move(x));
       return true;
     });
     if (!ok) return;
@@ -659,13 +669,13 @@ void project_generic(N pod, PodProj& p) {
       if (N pvc = v.get("persistentVolumeClaim")) {
         flags |= PF_CLAIMS;
         N cn = pvc.obj() ? pvc.get("claimName") : N{};
-        p.claims.emplace_back(!cn ? std::string() : cn.str_t() ? std::string(cn.str()) : std::string("\x01"));
-        p.claim_pvc.push_back(1);
+        cx.claims.emplace_back(!cn ? std::string() : cn.str_t() ? std::string(cn.str()) : std::string("\x01"));
+        cx.claim_pvc.push_back(1);
       } else if (v.get("ephemeral")) {
         flags |= PF_CLAIMS;
         N vn = v.get("name");
-        p.claims.emplace_back(vn && !vn.str_t() ? std::string("\x01") : p.name + "-" + std::string(vn ? vn.str() : ""));
-        p.claim_pvc.push_back(0);
+        cx.claims.emplace_back(vn && !vn.str_t() ? std::string("\x01") : p.name + "-" + std::string(vn ? vn.str() : ""));
+        cx.claim_pvc.push_back(0);
       } else {
         for (const char* d : kDisks)
           if (v.get(d)) {
@@ -1062,33 +1072,16 @@ bool scan_watch_identity(std::string_view line, char* type, std::string_view* ob
 
 void merge_non_identity(PodProj& d, PodProj&& s) {
   d.labels = std::move(s.labels);
-  d.has_annotations = s.has_annotations;
-  d.annotations = std::move(s.annotations);
   d.cpu = s.cpu;
   d.mem = s.mem;
   d.nzc = s.nzc;
   d.nzm = s.nzm;
   d.priority = s.priority;
-  d.has_node_selector = s.has_node_selector;
-  d.node_selector = std::move(s.node_selector);
-  d.has_affinity = s.has_affinity;
-  d.req_terms = std::move(s.req_terms);
-  d.pref_terms = std::move(s.pref_terms);
-  d.tolerations = std::move(s.tolerations);
-  d.ports = std::move(s.ports);
   d.images = std::move(s.images);
   d.containers = s.containers;
-  d.ext = std::move(s.ext);
   d.owners = std::move(s.owners);
-  d.spread = std::move(s.spread);
-  d.has_pod_aff = s.has_pod_aff;
-  d.aff_req = std::move(s.aff_req);
-  d.anti_req = std::move(s.anti_req);
-  d.aff_pref = std::move(s.aff_pref);
-  d.anti_pref = std::move(s.anti_pref);
+  d.cold_ = std::move(s.cold_);
   d.flags = s.flags;
-  d.claims = std::move(s.claims);
-  d.claim_pvc = std::move(s.claim_pvc);
   d.spec_meta_hash = s.spec_meta_hash;
   d.ok = s.ok;
   d.sched_cond = std::move(s.sched_cond);

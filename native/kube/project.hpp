@@ -53,22 +53,8 @@ struct PodProj {
   std::string uid, ns, name, rv, sched, node, phase, creation;
   bool deleting = false;            // metadata.deletionTimestamp set
   std::vector<KV> labels;
-  bool has_annotations = false;
-  std::vector<KV> annotations;
   int64_t cpu = 0, mem = 0, nzc = 0, nzm = 0, priority = 0;
-  bool has_node_selector = false;
-  std::vector<KV> node_selector;
-  bool has_affinity = false;        // spec.affinity truthy → terms lists (maybe empty)
-  std::vector<TermP> req_terms;
-  std::vector<std::pair<int64_t, TermP>> pref_terms;
-  std::vector<TolP> tolerations;
-  std::vector<PortP> ports;
   int flags = 0;
-  // the claims of spec.volumes (plugins/volumes.py::_claim_names): a persistentVolumeClaim's
-  // claimName, a generic ephemeral volume's "<pod>-<volume>"; "\x01" for a name that is not a
-  // string (it names no PersistentVolumeClaim the lane could call inert)
-  std::vector<std::string> claims;
-  std::vector<char> claim_pvc;      // per claim: 1 a persistentVolumeClaim volume, 0 an ephemeral one
   uint64_t spec_meta_hash = 0;      // upstream isPodUpdated: spec + metadata minus volatile fields
   // the hash was not computed (a lane-attached ADDED: the lane never compares it); PodEv::hash()
   // computes it from the raw object on first use
@@ -88,13 +74,10 @@ struct PodProj {
     std::string status, reason, msg, ltt;
   };
   std::shared_ptr<const SchedCond> sched_cond;
-  // default-plugin inputs (models/pod.py PodInfo.images / containers / ext / owner / avoid /
-  // spread): normalized images of spec.containers and their count, requests beyond cpu/memory
-  // (non-zero, models/pod.py::ext_requests), the first controller ownerReference, the first
-  // ReplicationController / ReplicaSet controller, spec.topologySpreadConstraints
+  // default-plugin inputs (models/pod.py PodInfo.images / containers): normalized images of
+  // spec.containers and their count
   std::vector<std::string> images;
   int32_t containers = 0;
-  std::vector<std::pair<std::string, int64_t>> ext;
   // the controller references (null: the pod has no controller ownerReference); one record, so
   // a pod without one carries 16 bytes for them
   struct Owners {
@@ -112,7 +95,6 @@ struct PodProj {
     std::vector<KV> labels;
     std::vector<SelReqP> exprs;
   };
-  std::vector<SpreadP> spread;
   // spec.affinity.podAffinity / podAntiAffinity terms (plugins/spread_affinity.py::_terms)
   struct PodTermP {
     std::string key;
@@ -122,8 +104,42 @@ struct PodProj {
     std::vector<SelReqP> exprs;
     int64_t weight = 1;
   };
-  bool has_pod_aff = false;
-  std::vector<PodTermP> aff_req, anti_req, aff_pref, anti_pref;
+  // Everything else a full projection reads — present on few pods, so it lives in one record
+  // behind a pointer (null: all empty). Every watch event carries a PodProj from the I/O
+  // thread to the lane thread; a pod's echo and its deletion only need the identity fields
+  // above, and the bytes of this record would be paid on each (tests/test_engine_alloc.py)
+  struct Cold {
+    bool has_annotations = false;
+    std::vector<KV> annotations;
+    bool has_node_selector = false;
+    std::vector<KV> node_selector;
+    bool has_affinity = false;        // spec.affinity truthy → terms lists (maybe empty)
+    std::vector<TermP> req_terms;
+    std::vector<std::pair<int64_t, TermP>> pref_terms;
+    std::vector<TolP> tolerations;
+    std::vector<PortP> ports;
+    // the claims of spec.volumes (plugins/volumes.py::_claim_names): a persistentVolumeClaim's
+    // claimName, a generic ephemeral volume's "<pod>-<volume>"; "\x01" for a name that is not a
+    // string (it names no PersistentVolumeClaim the lane could call inert)
+    std::vector<std::string> claims;
+    std::vector<char> claim_pvc;      // per claim: 1 a persistentVolumeClaim volume, 0 an ephemeral one
+    // requests beyond cpu/memory (non-zero, models/pod.py::ext_requests)
+    std::vector<std::pair<std::string, int64_t>> ext;
+    std::vector<SpreadP> spread;      // spec.topologySpreadConstraints
+    bool has_pod_aff = false;
+    std::vector<PodTermP> aff_req, anti_req, aff_pref, anti_pref;
+    bool empty() const {
+      return !has_annotations && annotations.empty() && !has_node_selector && node_selector.empty() && !has_affinity &&
+             req_terms.empty() && pref_terms.empty() && tolerations.empty() && ports.empty() && claims.empty() &&
+             claim_pvc.empty() && ext.empty() && spread.empty() && !has_pod_aff && aff_req.empty() &&
+             anti_req.empty() && aff_pref.empty() && anti_pref.empty();
+    }
+  };
+  std::shared_ptr<const Cold> cold_;
+  const Cold& cold() const {
+    static const Cold kNone;
+    return cold_ ? *cold_ : kNone;
+  }
 };
 
 // Quantity → ceil(q × 10^scale) with exact decimal arithmetic (scale 3: CPU millicores,

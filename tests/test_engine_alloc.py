@@ -32,7 +32,7 @@ def test_watch_event_record_stays_small():
     frees it on the lane thread, so each byte of it is paid on every event. Round 5 grew it from
     984 to 1184 bytes (PodScheduled condition strings, owner references by value). On one MI355X
     box that cost 143.5k vs 154.2k pods/s, and the reset grew from 1.46 to 1.94 ms (a same-box
-    bisect, profiles/bench/r6/bisect/). Optional parts now live behind shared records."""
+    bisect, profiles/bench/r6/bisect/). Optional parts now live behind shared records: 528 bytes."""
     from yoda_scheduler_amd.ops.native import load_native
     k = load_native("kube", "yoda_scheduler_amd._native._yoda_kube")
-    assert k.SIZEOF_POD_EV <= 896, k.SIZEOF_POD_EV
+    assert k.SIZEOF_POD_EV <= 576, k.SIZEOF_POD_EV
