@@ -414,7 +414,8 @@ PYBIND11_MODULE(_yoda_core, m) {
       .def_property_readonly("device_batches", &Engine::device_batches)
       .def("device_last_us", &Engine::device_last_us, py::call_guard<EngineGuard>())
       .def("device_set_timing", &Engine::device_set_timing, py::arg("on"), py::call_guard<EngineGuard>())
-      .def("device_eligible", &Engine::device_eligible, py::call_guard<EngineGuard>())
+      .def("device_eligible", &Engine::device_eligible, py::arg("req"), py::arg("slots") = false,
+           py::call_guard<EngineGuard>())
       .def("device_flush", &Engine::device_flush, py::call_guard<EngineGuard>())
       .def("device_cycle",
            [](Engine& e, const PodReq& r) -> py::object {

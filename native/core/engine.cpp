@@ -2350,12 +2350,20 @@ std::vector<CycleResult> Engine::schedule_batch(const std::vector<uint64_t>& pod
   static const std::vector<int64_t> nox;
   const size_t n = std::min(pods.size(), reqs.size());
   const bool dev = dev_ctx_ && fn_schedule_batch_ && live_ >= dev_min_nodes_;
+  BatchCols cols;
   size_t i = 0;
   while (i < n) {
     size_t j = i;
+    cols.spread.clear();
+    cols.image.clear();
+    cols.pods.clear();
+    // a run ends at a pod the device cannot carry, one needing a third column slot, or after
+    // one k_batch chunk when it uses columns (the staged columns are the chunk's start)
     if (dev)
-      while (j < n && batch_eligible(*reqs[j])) ++j;
-    if (j - i >= 2 && schedule_batch_device(pods.data() + i, reqs.data() + i, j - i, &out)) {
+      while (j < n && batch_eligible(*reqs[j]) && (j - i) < 256 && assign_cols(*reqs[j], &cols)) ++j;
+    const bool use_cols = !cols.spread.empty() || !cols.image.empty();
+    if (j - i >= (use_cols ? 1u : 2u) &&
+        schedule_batch_device(pods.data() + i, reqs.data() + i, j - i, &out, use_cols ? &cols : nullptr)) {
       ++dev_batches_;
       i = j;
       continue;
@@ -2368,7 +2376,7 @@ std::vector<CycleResult> Engine::schedule_batch(const std::vector<uint64_t>& pod
 }
 
 bool Engine::batch_eligible(const PodReq& q) const {
-  return device_eligible(q) && !needs_candidates(q) && !(q.has_memory && q.memory > UINT32_MAX);
+  return device_eligible(q, fn_extras_ != nullptr) && !needs_candidates(q) && !(q.has_memory && q.memory > UINT32_MAX);
 }
 
 // ============================================================== device scorer (dlopen)
@@ -2402,6 +2410,7 @@ bool Engine::enable_device(const std::string& lib_path, int device, int capacity
   fn_set_timing_ = dlsym(lib, "yoda_dev_set_timing");
   fn_schedule_batch_ = dlsym(lib, "yoda_dev_schedule_batch");   // optional
   fn_busy_ = dlsym(lib, "yoda_dev_busy");                         // optional
+  fn_extras_ = dlsym(lib, "yoda_dev_batch_extras");               // optional
   if (!create || !fn_destroy_ || !fn_upload_ || !fn_schedule_ || !fn_last_us_) {
     if (err) *err = "libyoda_hip.so lacks the yoda_dev_* entry points";
     dlclose(lib);
@@ -2504,7 +2513,7 @@ bool Engine::flush_dirty() {
   return true;
 }
 
-bool Engine::device_eligible(const PodReq& req) const {
+bool Engine::device_eligible(const PodReq& req, bool slots) const {
   if (!dev_ctx_ || compat_) return false;
   if ((int32_t)nodes_.size() > dev_cap_) return false;
   if (wt_.enum_limit < 70) return false;                       // device search is always exhaustive
@@ -2529,7 +2538,7 @@ bool Engine::device_eligible(const PodReq& req) const {
     for (const auto& r : req.ext)   // the device carries one extended resource dimension
       if (r.first != dev_ext_res_ && ext_checked(r.first)) return false;
   int64_t img;
-  if (!image_score_const(req, &img)) return false;
+  if (!slots && !image_score_const(req, &img)) return false;   // (k_batch: an image slot)
   if (!interpod_inert(req)) return false;
   if (score_w_[S_PREFER_AVOID] && req.avoid_kind && avoid_nodes_ > 0) return false;
   if (wants_spread_filter(req)) {
@@ -2537,12 +2546,126 @@ bool Engine::device_eligible(const PodReq& req) const {
     spread_constraints(req, true, &hard);
     if (!hard.empty()) return false;
   }
-  if (score_w_[S_SPREAD]) {
+  if (score_w_[S_SPREAD] && !slots) {   // (k_batch: a spread slot, assign_cols)
     std::vector<SpreadC> soft;
     spread_constraints(req, false, &soft);
     if (!soft.empty() && !spread_soft_constant(soft)) return false;
   }
   return true;
+}
+
+bool Engine::assign_cols(const PodReq& q, BatchCols* cols) const {
+  BatchCols::PodCols pc;
+  int64_t img_const;
+  if (score_w_[S_IMAGE_LOCALITY] && !image_score_const(q, &img_const)) {
+    int k = 0;
+    while (k < (int)cols->image.size() && !(cols->image[k].first == q.images && cols->image[k].second == q.containers)) ++k;
+    if (k == (int)cols->image.size()) {
+      if (k >= YODA_DEV_IMAGE_SLOTS) return false;
+      cols->image.emplace_back(q.images, q.containers);
+    }
+    pc.image = (int8_t)k;
+  }
+  if (score_w_[S_SPREAD]) {
+    std::vector<SpreadC> soft;
+    spread_constraints(q, false, &soft);
+    if (!soft.empty() && !spread_soft_constant(soft)) {
+      // representable: ≤ 2 constraints of one selector, at most one on kubernetes.io/hostname
+      // and one on another key (the slot's domain key)
+      if (soft.size() > 2) return false;
+      static const std::string kHostname = "kubernetes.io/hostname";
+      auto hit = string_idx_.find(kHostname);
+      const int32_t host_key = hit == string_idx_.end() ? -1 : hit->second;
+      BatchCols::Spread sp;
+      sp.ns = q.ns;
+      sp.sel = soft[0].sel;
+      for (size_t c = 0; c < soft.size(); ++c) {
+        if (!(soft[c].sel == sp.sel)) return false;
+        if (soft[c].key == host_key) {
+          if (sp.host) return false;
+          sp.host = true;
+          pc.ckind[c] = 0;
+        } else {
+          if (sp.dom_key >= 0) return false;
+          sp.dom_key = soft[c].key;
+          pc.ckind[c] = 1;
+        }
+        pc.skew[c] = soft[c].max_skew;
+      }
+      pc.nc = (uint8_t)soft.size();
+      int k = 0;
+      while (k < (int)cols->spread.size()) {
+        const BatchCols::Spread& x = cols->spread[k];
+        if (x.ns == sp.ns && x.host == sp.host && x.dom_key == sp.dom_key && x.sel == sp.sel) break;
+        ++k;
+      }
+      if (k == (int)cols->spread.size()) {
+        if (k >= YODA_DEV_SPREAD_SLOTS) return false;
+        cols->spread.push_back(std::move(sp));
+      }
+      pc.spread = (int8_t)k;
+    }
+  }
+  cols->pods.push_back(pc);
+  return true;
+}
+
+bool Engine::stage_cols(const BatchCols& cols, const PodReq* const* reqs, size_t count) {
+  const int n = (int)nodes_.size();
+  const int ns = (int)cols.spread.size(), ni = (int)cols.image.size();
+  if (!ns && !ni) return true;
+  if (!fn_extras_) return false;
+  std::vector<int32_t> cnt((size_t)ns * n, 0), zc((size_t)ns * YODA_DEV_DOMAINS, 0);
+  std::vector<uint8_t> dom((size_t)ns * n, YODA_DEV_DOM_NONE);
+  static const std::string kHostname = "kubernetes.io/hostname";
+  auto hit = string_idx_.find(kHostname);
+  const int32_t host_key = hit == string_idx_.end() ? -1 : hit->second;
+  for (int k = 0; k < ns; ++k) {
+    const BatchCols::Spread& sp = cols.spread[k];
+    std::unordered_map<int32_t, int32_t> ids;   // domain value → id
+    int64_t total = 0;
+    for (int32_t i = 0; i < n; ++i) {
+      const Node& nd = nodes_[i];
+      if (!nd.alive) continue;
+      if (sp.host && !nd.labels.count(host_key)) continue;
+      int32_t d = 0;
+      if (sp.dom_key >= 0) {
+        auto lab = nd.labels.find(sp.dom_key);
+        if (lab == nd.labels.end()) continue;
+        auto it = ids.find(lab->second);
+        if (it == ids.end()) {
+          if ((int)ids.size() >= YODA_DEV_DOMAINS) return false;   // too many domains: per-pod cycles
+          it = ids.emplace(lab->second, (int32_t)ids.size()).first;
+        }
+        d = it->second;
+      }
+      const int64_t c = nd.pods.empty() ? 0 : count_matching(i, sp.ns, sp.sel);
+      if (c > INT32_MAX / 2) return false;
+      cnt[(size_t)k * n + i] = (int32_t)c;
+      dom[(size_t)k * n + i] = (uint8_t)d;
+      zc[(size_t)k * YODA_DEV_DOMAINS + d] += (int32_t)c;
+      total += c;
+    }
+    // the device keeps a spread raw score in 32 bits: (pods + the batch) × log(n + 2) per
+    // constraint, plus the skews
+    int64_t skew = 0;
+    for (size_t j = 0; j < count; ++j) skew = std::max<int64_t>(skew, cols.pods[j].skew[0] + (int64_t)cols.pods[j].skew[1]);
+    if ((double)(total + (int64_t)count) * std::log((double)n + 2.0) * 2.0 + (double)skew > 1.0e9) return false;
+  }
+  std::vector<int32_t> img((size_t)ni * n, 0);
+  for (int k = 0; k < ni; ++k) {
+    PodReq tmp;
+    tmp.images = cols.image[k].first;
+    tmp.containers = cols.image[k].second;
+    for (int32_t i = 0; i < n; ++i)
+      if (nodes_[i].alive) {
+        const int64_t v = score_w_[S_IMAGE_LOCALITY] * image_score(tmp, nodes_[i]);
+        if (v > INT32_MAX || v < 0) return false;
+        img[(size_t)k * n + i] = (int32_t)v;
+      }
+  }
+  using extras_t = int (*)(void*, int, int, const int32_t*, const uint8_t*, const int32_t*, int, const int32_t*);
+  return ((extras_t)fn_extras_)(dev_ctx_, n, ns, cnt.data(), dom.data(), zc.data(), ni, img.data()) == 0;
 }
 
 Reason Engine::candidate_reason(const PodReq& req, const Node& n) const {
@@ -2552,9 +2675,28 @@ Reason Engine::candidate_reason(const PodReq& req, const Node& n) const {
   return RS_OK;
 }
 
-void Engine::make_dev_req(const PodReq& req, yoda_dev_req_t* out) {
+void Engine::make_dev_req(const PodReq& req, yoda_dev_req_t* out, const BatchCols::PodCols* pc,
+                          const BatchCols* cols) {
   yoda_dev_req_t& d = *out;
   d = yoda_dev_req_t{};
+  d.spread_slot = -1;
+  d.img_slot = -1;
+  if (pc) {
+    d.img_slot = pc->image;
+    d.spread_slot = pc->spread;
+    d.spread_w = (int32_t)score_w_[S_SPREAD];
+    d.spread_nc = pc->nc;
+    for (int c = 0; c < 2; ++c) {
+      d.ckind[c] = pc->ckind[c];
+      d.cskew[c] = pc->skew[c];
+    }
+    // which slots' selectors this pod counts for once assumed (upstream countPodsMatchSelector:
+    // same namespace, not terminating)
+    for (size_t k = 0; k < cols->spread.size(); ++k) {
+      const BatchCols::Spread& sp = cols->spread[k];
+      if (sp.ns == req.ns && !req.deleting && sp.sel.matches(req.labels)) d.match_mask |= (uint8_t)(1u << k);
+    }
+  }
   d.number = req.has_number ? req.number : 1;
   d.memory = req.has_memory ? req.memory : 0;
   d.clock = req.has_clock ? req.clock : 0;
@@ -2578,7 +2720,7 @@ void Engine::make_dev_req(const PodReq& req, yoda_dev_req_t* out) {
   // ImageLocality scores every node alike (image_score_const)
   d.w_const += score_w_[S_PREFER_AVOID] * kMaxNodeScore;
   int64_t img = 0;
-  if (image_score_const(req, &img)) d.w_const += img;
+  if (d.img_slot < 0 && image_score_const(req, &img)) d.w_const += img;   // (a slot: the column)
   d.ext = ((filters_ & F_NODE_RESOURCES_FIT) && ext_checked(dev_ext_res_)) ? ext_amount(req.ext, dev_ext_res_) : 0;
   d.w_link = wt_.w_link;
   d.w_numa = wt_.w_numa;
@@ -2651,8 +2793,8 @@ bool Engine::schedule_device(const PodReq& req, CycleResult* r) {
 }
 
 bool Engine::schedule_batch_device(const uint64_t* pods, const PodReq* const* reqs, size_t count,
-                                   std::vector<CycleResult>* out) {
-  if (!dev_ctx_ || !fn_schedule_batch_ || live_ < dev_min_nodes_ || count < 2) return false;
+                                   std::vector<CycleResult>* out, const BatchCols* cols) {
+  if (!dev_ctx_ || !fn_schedule_batch_ || live_ < dev_min_nodes_ || count < (cols ? 1u : 2u)) return false;
   std::unique_lock<std::mutex> dl(dev_mu_, std::try_to_lock);
   if (!dl.owns_lock()) return false;
   // the device assumes each winner with its reservation counted as pending (Engine::reserve
@@ -2664,10 +2806,12 @@ bool Engine::schedule_batch_device(const uint64_t* pods, const PodReq* const* re
     ++dev_fallbacks_;
     return false;
   }
+  // the run's score columns, staged for this call (false: the device cannot take them)
+  if (cols && !stage_cols(*cols, reqs, count)) return false;
   // rng draws happen in make_dev_req, in pod order — the same sequence as per-pod cycles
   const std::mt19937_64 rng_before = rng_;
   std::vector<yoda_dev_req_t> d(count);
-  for (size_t i = 0; i < count; ++i) make_dev_req(*reqs[i], &d[i]);
+  for (size_t i = 0; i < count; ++i) make_dev_req(*reqs[i], &d[i], cols ? &cols->pods[i] : nullptr, cols);
   std::vector<yoda_dev_result_t> res(count);
   using batch_t = int (*)(void*, int, int, const yoda_dev_req_t*, yoda_dev_result_t*);
   void* ctx = dev_ctx_;

@@ -654,7 +654,9 @@ class Engine {
   uint64_t device_fallbacks() const { return dev_fallbacks_; }
   float device_last_us() const;
   void device_set_timing(bool on);   // per-cycle event timing (benchmarks)
-  bool device_eligible(const PodReq& req) const;
+  // `slots`: for k_batch, whose score columns carry a non-constant ImageLocality term and
+  // PodTopologySpread soft constraints (BatchCols); the per-pod kernels carry neither
+  bool device_eligible(const PodReq& req, bool slots = false) const;
   // parity hook: run one device cycle without reserving; false if not eligible/failed
   bool device_cycle(const PodReq& req, CycleResult* out);
   // push the rows changed since the last device call to the device now (an idle scheduler
@@ -666,12 +668,37 @@ class Engine {
   bool pack_node(int32_t idx, void* row) const;   // row: yoda_dev_node_t*
   bool flush_dirty();
   bool schedule_device(const PodReq& req, CycleResult* r);
+  // k_batch score columns of one device run: up to YODA_DEV_SPREAD_SLOTS spread slots (pods
+  // counted by one selector in one namespace, over one set of topology keys) and
+  // YODA_DEV_IMAGE_SLOTS image slots (one image list); per pod its slots and constraints
+  struct BatchCols {
+    struct Spread {
+      int32_t ns = 0;
+      LSel sel;
+      bool host = false;       // a kubernetes.io/hostname constraint
+      int32_t dom_key = -1;    // the other constraint's key (-1: none)
+    };
+    struct PodCols {
+      int8_t spread = -1, image = -1;
+      uint8_t nc = 0, ckind[2] = {0, 0};
+      int32_t skew[2] = {0, 0};
+    };
+    std::vector<Spread> spread;
+    std::vector<std::pair<std::vector<int32_t>, int32_t>> image;   // (images, containers)
+    std::vector<PodCols> pods;
+  };
   // one k_batch dispatch for pods[0, count) (all batch_eligible), results appended to *out;
   // false (nothing appended) when the device refuses or fails
   bool schedule_batch_device(const uint64_t* pods, const PodReq* const* reqs, size_t count,
-                             std::vector<CycleResult>* out);
-  bool batch_eligible(const PodReq& q) const;   // device_eligible and no per-node candidate mask
-  void make_dev_req(const PodReq& req, yoda_dev_req_t* out);
+                             std::vector<CycleResult>* out, const BatchCols* cols = nullptr);
+  bool batch_eligible(const PodReq& q) const;   // device_eligible (with slots), no per-node candidate mask
+  // the pod's slots in `cols` (adding slots as needed); false when it needs one too many or its
+  // soft constraints are not representable
+  bool assign_cols(const PodReq& q, BatchCols* cols) const;
+  // stage the run's columns on the device (fn_extras_); false: the run takes per-pod cycles
+  bool stage_cols(const BatchCols& cols, const PodReq* const* reqs, size_t count);
+  void make_dev_req(const PodReq& req, yoda_dev_req_t* out, const BatchCols::PodCols* pc = nullptr,
+                    const BatchCols* cols = nullptr);
   bool needs_candidates(const PodReq& req) const;
   // PodTopologySpread PreFilter state of one pod's DoNotSchedule constraints (upstream
   // preFilterState): matching pods per (key, value) over the nodes passing the pod's node
@@ -802,6 +829,7 @@ class Engine {
   void* fn_set_timing_ = nullptr;   // optional entry points
   void* fn_schedule_batch_ = nullptr;
   void* fn_busy_ = nullptr;
+  void* fn_extras_ = nullptr;   // yoda_dev_batch_extras (k_batch score columns); optional
   std::recursive_mutex* ext_mu_ = nullptr;
   std::mutex dev_mu_;                        // device context (stream, staging buffers)
   std::atomic<bool> batch_in_flight_{false};

@@ -28,6 +28,7 @@
 #include <atomic>
 #include <chrono>
 #include <climits>
+#include <cmath>
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
@@ -204,6 +205,7 @@ __device__ __forceinline__ T readlane(T v, int l) {
 struct OpMax { template <typename T> __device__ T operator()(T a, T b) const { return a > b ? a : b; } };
 struct OpMin { template <typename T> __device__ T operator()(T a, T b) const { return a < b ? a : b; } };
 struct OpSum { template <typename T> __device__ T operator()(T a, T b) const { return a + b; } };
+struct OpOr { template <typename T> __device__ T operator()(T a, T b) const { return a | b; } };
 
 template <typename T, typename Op>
 __device__ __forceinline__ T group_reduce(T v, Op op) {   // every lane of the 8 gets the result
@@ -228,6 +230,8 @@ template <typename T>
 __device__ __forceinline__ T wave_min(T v) { return across_groups(group_reduce(v, OpMin{}), OpMin{}); }
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) { return across_groups(group_reduce(v, OpSum{}), OpSum{}); }
+template <typename T>
+__device__ __forceinline__ T wave_or(T v) { return across_groups(group_reduce(v, OpOr{}), OpOr{}); }
 
 // ------------------------------------------------------------------ dirty-row patch
 __global__ void k_patch(PatchArgs a, yoda_dev_node_t* __restrict__ nodes) {
@@ -916,18 +920,31 @@ __global__ __launch_bounds__(kBlock) void k_select(int n, const yoda_dev_req_t r
 //    copies them to mapped host memory and raises `done` with a system-scope release.
 //  * every spin is bounded (abort word + s_memrealtime deadline): a block that never arrives
 //    makes every waiter give up, the host sees `done` missing and falls back.
-constexpr int kMaxNodesPerBlock = 256;    // 256 × 536 B of LDS per block
+constexpr int kMaxNodesPerBlock = 256;    // 256 × 536 B of LDS per block (+ the batch's score columns)
 constexpr int kRecStride = 16;            // granules per record slot
-constexpr int kRec1 = 11;                 // maxima[6], feasible, 8 reason counts packed 2 × u16
-constexpr int kRec2 = 4;                  // raw lo, hi (2 granules each)
-constexpr int kRec3 = 2;                  // best key (2 granules)
+// record 1: maxima[6], feasible, 8 reason counts packed 2 × u16, then PodTopologySpread's
+// feasible non-ignored nodes and the domain mask of those (lo, hi)
+// (a batch without score columns — COLS false — keeps the shorter records: 11 / 4 / 2-3)
+constexpr int kRec1 = 14;
+constexpr int kRec2 = 8;                  // raw lo, hi, spread lo, hi (2 granules each)
+constexpr int kRec3 = 3;                  // best key (2 granules), the block best's mask / flags / domains
 constexpr int kMaxGrid = 256;
-// LDS bytes per node: row + raw + total + quality + 2 × feas + 2 × elig + mask + dirty
+constexpr int kSP = YODA_DEV_SPREAD_SLOTS, kIMG = YODA_DEV_IMAGE_SLOTS, kDOM = YODA_DEV_DOMAINS;
+// LDS bytes per node: row + raw + total + quality + 2 × feas + 2 × elig + mask + dirty; a batch
+// with score columns adds batch_col_bytes (spread raw + per slot count and domain, per image
+// slot its score)
 constexpr size_t kBatchRowBytes = sizeof(yoda_dev_node_t) + 8 + 8 + 4 + 6;
+__host__ __device__ constexpr size_t batch_col_bytes(int n_sp, int n_img) {
+  return (n_sp > 0 ? 4 + 5 * (size_t)n_sp : 0) + 4 * (size_t)n_img;
+}
 constexpr int kMaxGroups = kMaxNodesPerBlock / kNodesPerWave;   // 8-node filter groups per block
 // reason codes the batch path can produce (no candidate reasons: the engine sends no
 // candidates to batches), packed into granules 7..10 of record 1
 constexpr int kNR = 8;                    // reason codes a batch can produce (record 1 packs 2 per granule)
+constexpr int kRsPairs = (kNR + 1) / 2;   // their granules
+// record-1 fields once unpacked: 0..5 maxima (max), 6 feasible (sum), 7.. reasons (sum), then
+// spread's feasible non-ignored nodes (sum) and domain mask (or, two halves)
+constexpr int kFNfi = 7 + kNR, kFDlo = 8 + kNR, kFDhi = 9 + kNR, kNF1 = 10 + kNR;
 __constant__ int c_batch_reasons[kNR] = {RS_UNSCHEDULABLE, RS_RESOURCES, RS_NO_SCV, RS_STALE, RS_GPU_NUMBER,
                                          RS_GPU_FIT, RS_DEAD, RS_EXT_RESOURCES};
 
@@ -948,6 +965,14 @@ struct BatchArgs {
   unsigned int* ticket;
   unsigned int* abort_word;
   unsigned long long* trace;          // optional: block 0's phase stamps, kTracePts per pod
+  // score columns of this batch (yoda_dev_batch_extras; device views of mapped host memory,
+  // read once in the prologue); n_sp / n_img = 0: none
+  const int32_t* sp_cnt;              // [n_sp][n] the slot selector's matching pods per node
+  const uint8_t* sp_dom;              // [n_sp][n] the node's domain, YODA_DEV_DOM_NONE: ignored
+  const int32_t* sp_zc;               // [n_sp][kDOM] matching pods per domain
+  const int32_t* img;                 // [n_img][n] weighted ImageLocality scores
+  const double* logtab;               // log(i + 2) (the host's libm): PodTopologySpread weights
+  int n_sp, n_img;
 };
 constexpr int kResWords = (int)(sizeof(yoda_dev_result_t) / 8);
 static_assert(kResWords == 19 && YODA_DEV_REASONS == 16 && offsetof(yoda_dev_result_t, feasible) == 4 &&
@@ -959,7 +984,7 @@ static_assert(kResWords == 19 && YODA_DEV_REASONS == 16 && offsetof(yoda_dev_res
 // the reason codes of c_batch_reasons, for compile-time indexing
 constexpr int kBatchReasonCodes[kNR] = {RS_UNSCHEDULABLE, RS_RESOURCES, RS_NO_SCV, RS_STALE, RS_GPU_NUMBER,
                                         RS_GPU_FIT, RS_DEAD, RS_EXT_RESOURCES};
-static_assert(7 + (kNR + 1) / 2 == kRec1, "record 1: 7 fields + the reason counts as u16 pairs");
+static_assert(7 + kRsPairs + 3 == kRec1, "record 1: 7 fields + the reason counts as u16 pairs + 3 spread fields");
 constexpr int kTracePts = 24;   // 9 phase stamps per pod (block 0), 9 of the PAIRS fix-up's owner, padded
 constexpr int kReqWords = sizeof(yoda_dev_req_t) / 4;
 static_assert(sizeof(yoda_dev_req_t) % 4 == 0 && kReqWords <= 64, "req fits one wave");
@@ -988,6 +1013,51 @@ __device__ __forceinline__ bool spin_ok(const BatchArgs& a, unsigned& spins, lon
   return true;
 }
 
+// Records are read two granules (16 B) per request: buffer_load_dwordx4 with sc1, the
+// coherence bits of __hip_atomic_load's agent-scope dwordx2. Every granule is still written by
+// one 8-byte atomic store and carries its own tag, so a pair caught between two stores only
+// fails its tag check. A gather is request-bound — each of the G blocks reads G records, and
+// every granule of a record costs G² requests chip-wide (MI355X, 4096 nodes, G = 256 blocks:
+// 3 more granules per record 1 cost ~1 µs per pod) — so halving the requests is what counts.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kSlotBytes = 2u * kMaxGrid * kRecStride * 8u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slot_rsrc(const BatchArgs& a) {
+  return __builtin_amdgcn_make_buffer_rsrc(a.slots, 0, (int)kSlotBytes, 0x00020000);
+}
+__device__ __forceinline__ uint32_t slot_off(uint32_t tag, int blk) {
+  return (((tag & 1u) * kMaxGrid + (uint32_t)blk) * kRecStride) * 8u;
+}
+// granules k, k + 1 of the slot at byte offset `off`; a lane outside the grid reads nothing and
+// sees (0, tag) twice
+__device__ __forceinline__ u32x4 load_pair(__amdgpu_buffer_rsrc_t rs, uint32_t off, int k, bool in, uint32_t tag) {
+  if (!in) return u32x4{0u, tag, 0u, tag};
+  return __builtin_amdgcn_raw_buffer_load_b128(rs, off + 8u * (uint32_t)k, 0, 16 /* sc1 */);
+}
+// granules 2.. of a record (granules 0, 1 were the poll); false if one is not yet from `tag`
+template <int K>
+__device__ __forceinline__ bool read_rest(__amdgpu_buffer_rsrc_t rs, uint32_t off, bool in, uint32_t tag,
+                                          uint32_t (&v)[K]) {
+  bool ok = true;
+#pragma unroll
+  for (int k = 2; k < K; k += 2) {   // (K odd: the pair's second granule lies inside the 16-granule slot)
+    const u32x4 y = load_pair(rs, off, k, in, tag);
+    v[k] = y.x;
+    ok &= y.y == tag;
+    if (k + 1 < K) {
+      v[k + 1] = y.z;
+      ok &= y.w == tag;
+    }
+  }
+  return ok;
+}
+// the poll: granules 0 (and 1) of a record
+template <int K>
+__device__ __forceinline__ bool read_head(const u32x4& x, uint32_t tag, uint32_t (&v)[K]) {
+  v[0] = x.x;
+  if constexpr (K > 1) v[1] = x.z;
+  return x.y == tag && (K < 2 || x.w == tag);
+}
+
 // Thread t < G polls the record of block p_off + t for epoch `tag` (K granules) until every
 // tag matches; returns false (block-uniform) when the wait was abandoned.
 template <int K>
@@ -996,25 +1066,19 @@ __device__ __forceinline__ bool gather(const BatchArgs& a, uint32_t tag, int G, 
   const int t = threadIdx.x;
   bool failed = false;
   if (uniform(t & ~63) < G) {   // waves holding at least one producer
-    const gu64* p = slot_ptr(a, tag, p_off + (t < G ? t : 0));
+    const __amdgpu_buffer_rsrc_t rs = slot_rsrc(a);
+    const bool in = t < G;
+    const uint32_t off = slot_off(tag, p_off + (in ? t : 0));
     const long long t0 = __builtin_amdgcn_s_memrealtime();
     for (unsigned spins = 0;;) {
-      // poll one granule per record until every record's has landed, then read the rest
+      __asm__ volatile("" ::: "memory");   // every round reads the slots again
+      // poll the first pair of every record until each has landed, then read the rest
       // (written in the same instant by the producer's other threads): a waiting block
-      // loads G words per round instead of G·K — with G blocks all polling each other that
-      // is the fabric traffic of the wait
-      const unsigned long long x0 = t < G ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                          : ((unsigned long long)tag << 32);
-      bool ok = (uint32_t)(x0 >> 32) == tag;
+      // loads G requests per round instead of G·K/2 — with G blocks all polling each other
+      // that is the fabric traffic of the wait
+      bool ok = read_head<K>(load_pair(rs, off, 0, in, tag), tag, v);
       if (__all(ok)) {
-        v[0] = (uint32_t)x0;
-#pragma unroll
-        for (int k = 1; k < K; ++k) {
-          const unsigned long long x = t < G ? __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                             : ((unsigned long long)tag << 32);
-          v[k] = (uint32_t)x;
-          ok &= (uint32_t)(x >> 32) == tag;
-        }
+        ok = read_rest<K>(rs, off, in, tag, v);
         if (__all(ok)) break;
       }
       if (!spin_ok(a, spins, t0)) {
@@ -1037,26 +1101,17 @@ __device__ __forceinline__ bool gather_wave0_2(const BatchArgs& a, uint32_t tag,
                                                uint32_t (&v2)[K], int skip) {
   const int t = threadIdx.x & 63, t2 = t + 64;
   const bool in = t < G && t != skip, in2 = t2 < G && t2 != skip;
-  const gu64* p = slot_ptr(a, tag, p_off + (t < G ? t : 0));
-  const gu64* p2 = slot_ptr(a, tag, p_off + (t2 < G ? t2 : 0));
-  const unsigned long long none = (unsigned long long)tag << 32;
+  const __amdgpu_buffer_rsrc_t rs = slot_rsrc(a);
+  const uint32_t off = slot_off(tag, p_off + (t < G ? t : 0)), off2 = slot_off(tag, p_off + (t2 < G ? t2 : 0));
   const long long t0 = __builtin_amdgcn_s_memrealtime();
   for (unsigned spins = 0;;) {
-    const unsigned long long x0 = in ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
-    const unsigned long long y0 = in2 ? __hip_atomic_load(p2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
-    bool ok = (uint32_t)(x0 >> 32) == tag && (uint32_t)(y0 >> 32) == tag;
+    __asm__ volatile("" ::: "memory");
+    bool ok = read_head<K>(load_pair(rs, off, 0, in, tag), tag, v);
+    ok &= read_head<K>(load_pair(rs, off2, 0, in2, tag), tag, v2);
     if (__all(ok)) {
-      v[0] = (uint32_t)x0;
-      v2[0] = (uint32_t)y0;
-#pragma unroll
-      for (int k = 1; k < K; ++k) {
-        const unsigned long long x = in ? __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
-        const unsigned long long y = in2 ? __hip_atomic_load(p2 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : none;
-        v[k] = (uint32_t)x;
-        v2[k] = (uint32_t)y;
-        ok &= (uint32_t)(x >> 32) == tag && (uint32_t)(y >> 32) == tag;
-      }
-      if (__all(ok)) return true;
+      ok = read_rest<K>(rs, off, in, tag, v);
+      ok &= read_rest<K>(rs, off2, in2, tag, v2);
+      if (__all(ok)) return true;   // (a skipped producer's values are 0)
     }
     if (!spin_ok(a, spins, t0)) return false;
   }
@@ -1070,21 +1125,14 @@ __device__ __forceinline__ bool gather_wave0(const BatchArgs& a, uint32_t tag, i
   for (int k = 0; k < K; ++k) v2[k] = 0;
   const int t = threadIdx.x & 63;
   const bool in = t < G && t != skip;
-  const gu64* p = slot_ptr(a, tag, p_off + (t < G ? t : 0));
+  const __amdgpu_buffer_rsrc_t rs = slot_rsrc(a);
+  const uint32_t off = slot_off(tag, p_off + (t < G ? t : 0));
   const long long t0 = __builtin_amdgcn_s_memrealtime();
   for (unsigned spins = 0;;) {
-    const unsigned long long x0 = in ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                        : ((unsigned long long)tag << 32);
-    bool ok = (uint32_t)(x0 >> 32) == tag;
+    __asm__ volatile("" ::: "memory");
+    bool ok = read_head<K>(load_pair(rs, off, 0, in, tag), tag, v);
     if (__all(ok)) {
-      v[0] = (uint32_t)x0;
-#pragma unroll
-      for (int k = 1; k < K; ++k) {
-        const unsigned long long x = in ? __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                           : ((unsigned long long)tag << 32);
-        v[k] = (uint32_t)x;
-        ok &= (uint32_t)(x >> 32) == tag;
-      }
+      ok = read_rest<K>(rs, off, in, tag, v);
       if (__all(ok)) return true;
     }
     if (!spin_ok(a, spins, t0)) return false;
@@ -1111,22 +1159,36 @@ __device__ __forceinline__ bool gather_wave0(const BatchArgs& a, uint32_t tag, i
 // the filter and score A of every block but one group's; results are bit-identical to the
 // serial order (reference: the per-pod cycle of scheduler.go:132-157 / algorithm.go:28-87,
 // run for consecutive pods against the same node table).
-template <int BW, bool PAIRS>
+template <int BW, bool PAIRS, bool COLS>
 __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   constexpr int kBB = 64 * BW;
+  // record sizes of this instantiation: score columns add spread fields to records 1 and 2 and
+  // the winner's domains to record 3
+#ifdef YODA_EXP_SHORT_REC
+  constexpr bool XC = false;
+#else
+  constexpr bool XC = COLS;
+#endif
+  constexpr int REC1 = XC ? kRec1 : kRec1 - 3, REC2 = XC ? kRec2 : kRec2 - 4;
+  constexpr int REC3 = (XC || PAIRS) ? kRec3 : kRec3 - 1, NF1 = XC ? kNF1 : kNF1 - 3;
   extern __shared__ __align__(16) unsigned char s_dyn[];
   __shared__ uint8_t s_masks[256];
   // request ring: pods b (and b−1 in PAIRS mode, for its assume) plus the prefetched next ones
   __shared__ __align__(16) uint32_t s_req[4][sizeof(yoda_dev_req_t) / 4];
   __shared__ int s_fix;   // PAIRS: the other set's last winner's row here, or −1
   __shared__ unsigned long long s_part[BW][16];
-  __shared__ unsigned long long s_glob[16];
+  __shared__ unsigned long long s_glob[kNF1];
   // G ≤ 64: wave 0 holds every record of a gather and reduces it alone; the result reaches the
   // block through these words and one barrier (no per-wave partials, no second barrier)
-  __shared__ unsigned long long s_red[2];
-  __shared__ uint32_t s_rec[7 + kNR][kMaxGrid + 4];   // gather-1 records transposed (+4: bank skew)
-  // filter aggregates per 8-node group: 6 maxima, feasible count, 7 reason counts
-  __shared__ uint32_t s_grp[kMaxGroups][7 + kNR];
+  __shared__ unsigned long long s_red[4];
+  __shared__ uint32_t s_rec[kNF1][kMaxGrid + 4];   // gather-1 records transposed (+4: bank skew)
+  // filter aggregates per 8-node group: 6 maxima, feasible count, the reason counts, spread's
+  // feasible non-ignored count and domain mask halves
+  __shared__ uint32_t s_grp[kMaxGroups][kNF1];
+  // PodTopologySpread: matching pods per domain of each slot (every block keeps the whole table
+  // and applies each winner), the last winner's record-3 granule 2 (its domains)
+  __shared__ int32_t s_zc[kSP][kDOM];
+  __shared__ uint32_t s_wdom;
   __shared__ GangBest s_gang[8 * BW];
   __shared__ int s_fail;
   __shared__ uint32_t s_bfeas;   // this block's feasible nodes for the current pod (record 1)
@@ -1146,10 +1208,15 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   int64_t* s_raw = reinterpret_cast<int64_t*>(s_dyn + (size_t)npb * sizeof(yoda_dev_node_t));
   int64_t* s_total = s_raw + npb;
   int32_t* s_quality = reinterpret_cast<int32_t*>(s_total + npb);
-  uint8_t* s_feas2 = reinterpret_cast<uint8_t*>(s_quality + npb);   // [2][npb] by pod parity
+  // the batch's score columns (sized by a.n_sp / a.n_img: absent without slots)
+  int32_t* s_sp = s_quality + npb;                                    // spread raw score, −1: ignored
+  int32_t* s_cnt = s_sp + (a.n_sp > 0 ? npb : 0);                     // [n_sp][npb] matching pods
+  int32_t* s_img = s_cnt + a.n_sp * npb;                              // [n_img][npb] ImageLocality
+  uint8_t* s_feas2 = reinterpret_cast<uint8_t*>(s_img + a.n_img * npb);   // [2][npb] by pod parity
   uint8_t* s_elig2 = s_feas2 + 2 * npb;                               // [2][npb]
   uint8_t* s_mask = s_elig2 + 2 * npb;
   uint8_t* s_dirty = s_mask + npb;
+  uint8_t* s_dom = s_dirty + npb;                                     // [n_sp][npb] domains
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int grp = lane >> 3, sub = lane & 7;
 
@@ -1169,6 +1236,20 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     reinterpret_cast<uint4*>(a.nodes + a.pa.idx[rec])[tid & 31] = reinterpret_cast<const uint4*>(&a.pa.rows[rec])[tid & 31];
   }
   if (tid < 256) s_masks[tid] = c_subsets.masks[tid];
+  // score columns of the batch (one burst per block from mapped host memory)
+  if constexpr (COLS)
+  for (int t = tid; t < a.n_sp * cnt; t += kBB) {
+    const int sl = t / cnt, row = t - sl * cnt;
+    s_cnt[sl * npb + row] = a.sp_cnt[(size_t)sl * a.n + base + row];
+    s_dom[sl * npb + row] = a.sp_dom[(size_t)sl * a.n + base + row];
+  }
+  if constexpr (COLS)
+  for (int t = tid; t < a.n_img * cnt; t += kBB) {
+    const int sl = t / cnt, row = t - sl * cnt;
+    s_img[sl * npb + row] = a.img[(size_t)sl * a.n + base + row];
+  }
+  if constexpr (COLS)
+    for (int t = tid; t < a.n_sp * kDOM; t += kBB) s_zc[t / kDOM][t % kDOM] = a.sp_zc[t];
   if (tid < kReqWords) {
     s_req[0][tid] = reinterpret_cast<const uint32_t*>(a.reqs)[tid];
     if (PAIRS && a.B > 1) s_req[1][tid] = reinterpret_cast<const uint32_t*>(a.reqs + 1)[tid];
@@ -1197,28 +1278,46 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       uint32_t rc[kNR];
 #pragma unroll
       for (int q = 0; q < kNR; ++q) rc[q] = (uint32_t)__popcll(__ballot(head && reason == c_batch_reasons[q]));
+      // PodTopologySpread (soft): the feasible nodes carrying every key of the pod's slot, and
+      // the domains among them (upstream initPreScoreState's topology sizes)
+      uint32_t nfi = 0, dlo = 0, dhi = 0;
+      if constexpr (COLS) {
+        const int sl = rq.spread_slot;
+        if (sl >= 0) {   // wave-uniform
+          const uint32_t d = valid ? s_dom[sl * npb + j] : (uint32_t)YODA_DEV_DOM_NONE;
+          const bool counted = head && fok && d != YODA_DEV_DOM_NONE;
+          nfi = (uint32_t)__popcll(__ballot(counted));
+          dlo = wave_or(counted && d < 32 ? 1u << d : 0u);
+          dhi = wave_or(counted && d >= 32 ? 1u << (d - 32) : 0u);
+        }
+      }
       if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) s_grp[gq][k] = wmx[k];
         s_grp[gq][6] = nf;
 #pragma unroll
         for (int q = 0; q < kNR; ++q) s_grp[gq][7 + q] = rc[q];
+        if constexpr (COLS) {
+          s_grp[gq][kFNfi] = nfi;
+          s_grp[gq][kFDlo] = dlo;
+          s_grp[gq][kFDhi] = dhi;
+        }
       }
   };
   auto filter_groups = [&](const yoda_dev_req_t& rq, int par) {
     for (int gq = wave; gq * kNodesPerWave < cnt; gq += BW) filter_one(rq, par, gq);
   };
-  // record 1 from the group aggregates: threads 0..kRec1-1 (wave 0), after every group's
+  // record 1 from the group aggregates: threads 0..REC1-1 (wave 0), after every group's
   // s_grp row is visible to them
   auto record1 = [&](uint32_t tag1) -> uint32_t {
     uint32_t v = 0;
-    if (tid < kRec1) {   // block totals over the groups → the record's 11 granules
+    if (tid < REC1) {   // block totals over the groups → the record's 11 granules
       const int ngr = (cnt + kNodesPerWave - 1) / kNodesPerWave;
       if (tid < 7) {
         v = tid < 6 ? 1u : 0u;
         for (int q = 0; q < ngr; ++q) v = tid < 6 ? (s_grp[q][tid] > v ? s_grp[q][tid] : v) : v + s_grp[q][tid];
         if (tid == 6) s_bfeas = v;
-      } else {   // reason counts packed as u16 pairs (≤ npb ≤ 256 per block)
+      } else if (tid < 7 + kRsPairs) {   // reason counts packed as u16 pairs (≤ npb ≤ 256 per block)
         const int r0 = 7 + 2 * (tid - 7);
         uint32_t lo = 0, hi = 0;
         for (int q = 0; q < ngr; ++q) {
@@ -1226,6 +1325,9 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           hi += r0 + 1 < 7 + kNR ? s_grp[q][r0 + 1] : 0u;
         }
         v = lo | (hi << 16);
+      } else if constexpr (COLS) {   // spread: feasible non-ignored nodes (sum), domain mask halves (or)
+        const int f = kFNfi + (tid - 7 - kRsPairs);
+        for (int q = 0; q < ngr; ++q) v = f == kFNfi ? v + s_grp[q][f] : (v | s_grp[q][f]);
       }
       store_granule(slot_ptr(a, tag1, g) + tid, tag1, v);
     }
@@ -1371,6 +1473,8 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     nd->nz_cpu += rq.nz_cpu_m;
     nd->nz_mem += rq.nz_mem;
     s_dirty[j] = 1;
+    if constexpr (COLS)
+      for (int sl = 0; sl < a.n_sp; ++sl) s_cnt[sl * npb + j] += (int32_t)((rq.match_mask >> sl) & 1u);
   };
 
   bool ok = true;
@@ -1428,6 +1532,15 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         auto holds = [&](bool have, unsigned long long mk, unsigned long long key, const uint32_t (&v)[3]) {
           return have && mk == key && ((v[2] >> 9) & 1u) && ((v[2] >> 8) & 1u);
         };
+        // every block of this set counts pod b−1's winner in its spread domain tables (granule 2
+        // of the holder's record: the winner's domains); one thread
+        auto count_winner = [&](uint32_t g2) {
+          const yoda_dev_req_t& rp = *reinterpret_cast<const yoda_dev_req_t*>(s_req[(b - 1) & 3]);
+          for (int sl = 0; sl < a.n_sp; ++sl) {
+            const uint32_t d = (g2 >> (16 + 8 * sl)) & 0xFFu;
+            if (((rp.match_mask >> sl) & 1u) && d != YODA_DEV_DOM_NONE) s_zc[sl][d] += 1;
+          }
+        };
         if (G <= 128) {
           // wave 0 alone (lane t: producers t and t + 64) gathers, reduces and assumes
           if (wave == 0) {
@@ -1438,8 +1551,17 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
               const unsigned long long mk = have ? ((unsigned long long)v[1] << 32 | v[0]) : 0ull;
               const unsigned long long mk2 = have2 ? ((unsigned long long)v2[1] << 32 | v2[0]) : 0ull;
               const unsigned long long key = wave_max(mk > mk2 ? mk : mk2);
-              if (holds(have, mk, key, v)) take_winner(key, v, t_g3);
-              else if (holds(have2, mk2, key, v2)) take_winner(key, v2, t_g3);
+              const bool h1 = holds(have, mk, key, v), h2 = !h1 && holds(have2, mk2, key, v2);
+              if (h1) take_winner(key, v, t_g3);
+              else if (h2) take_winner(key, v2, t_g3);
+              if (COLS && a.n_sp > 0) {
+                const unsigned long long bal = __ballot(h1 || h2);
+                if (bal) {
+                  const int src = __ffsll((long long)bal) - 1;
+                  const uint32_t g2 = (uint32_t)__builtin_amdgcn_readlane((int)(h1 ? v[2] : v2[2]), src);
+                  if (lane == 0) count_winner(g2);
+                }
+              }
             } else if (lane == 0) {
               s_fail = 1;
             }
@@ -1463,7 +1585,10 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           __syncthreads();
           unsigned long long key = 0;
           for (int w = 0; w < BW; ++w) key = s_part[w][0] > key ? s_part[w][0] : key;
-          if (holds(have, mk, key, v)) take_winner(key, v, t_g3);
+          if (holds(have, mk, key, v)) {
+            take_winner(key, v, t_g3);
+            if (COLS && a.n_sp > 0) count_winner(v[2]);   // (every block has one thread reading the holder's record)
+          }
           __syncthreads();
         }
         fix = s_fix;
@@ -1484,8 +1609,8 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         // Its own record goes into the transposed records from wave 0's registers.
         const int gw = nrep + 1 < BW - 1 ? BW - 1 : 0;
         auto gather_early = [&]() {
-          uint32_t v[kRec1], v2[kRec1];
-          if (gather_wave0<kRec1>(a, tag1, G, p0, v, v2, gi)) {
+          uint32_t v[REC1], v2[REC1];
+          if (gather_wave0<REC1>(a, tag1, G, p0, v, v2, gi)) {
             if (a.trace && lane == 0) a.trace[(size_t)b * kTracePts + 18] = __builtin_amdgcn_s_memrealtime();
             const int t2 = lane + 64;
             if (lane < G && lane != gi) {
@@ -1493,12 +1618,20 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
               for (int k = 0; k < 7; ++k) s_rec[k][lane] = v[k];
 #pragma unroll
               for (int q = 0; q < kNR; ++q) s_rec[7 + q][lane] = (q & 1) ? (v[7 + q / 2] >> 16) : (v[7 + q / 2] & 0xFFFFu);
+              if constexpr (COLS) {
+#pragma unroll
+                for (int e = 0; e < 3; ++e) s_rec[kFNfi + e][lane] = v[7 + kRsPairs + e];
+              }
             }
             if (t2 < G && t2 != gi) {
 #pragma unroll
               for (int k = 0; k < 7; ++k) s_rec[k][t2] = v2[k];
 #pragma unroll
               for (int q = 0; q < kNR; ++q) s_rec[7 + q][t2] = (q & 1) ? (v2[7 + q / 2] >> 16) : (v2[7 + q / 2] & 0xFFFFu);
+              if constexpr (COLS) {
+#pragma unroll
+                for (int e = 0; e < 3; ++e) s_rec[kFNfi + e][t2] = v2[7 + kRsPairs + e];
+              }
             }
           } else if (lane == 0) {
             s_fail = 1;
@@ -1508,13 +1641,15 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           filter_one(r, par, fg);
           __builtin_amdgcn_wave_barrier();
           const uint32_t own = record1(tag1);
-          if (early1 && tid < kRec1) {   // this block's column of the transposed records
+          if (early1 && tid < REC1) {   // this block's column of the transposed records
             if (tid < 7) {
               s_rec[tid][gi] = own;
-            } else {
+            } else if (tid < 7 + kRsPairs) {
               const int q0 = 2 * (tid - 7);
               s_rec[7 + q0][gi] = own & 0xFFFFu;
               if (q0 + 1 < kNR) s_rec[8 + q0][gi] = own >> 16;
+            } else if constexpr (COLS) {
+              s_rec[kFNfi + (tid - 7 - kRsPairs)][gi] = own;
             }
           }
           if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 10] = __builtin_amdgcn_s_memrealtime();
@@ -1543,41 +1678,58 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     // ================= gather 1: global maxima, feasible and reason counts
     {
       if (!early1) {
-        uint32_t v[kRec1];
-        if (!gather<kRec1>(a, tag1, G, p0, v, &s_fail)) {
+        uint32_t v[REC1];
+        if (!gather<REC1>(a, tag1, G, p0, v, &s_fail)) {
           ok = false;
           break;
         }
+        if (PAIRS && fix >= 0 && a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 19] = __builtin_amdgcn_s_memrealtime();
         // transpose through LDS (7 + kNR fields × G), then 16 threads per field reduce it
         if (tid < G) {
 #pragma unroll
           for (int k = 0; k < 7; ++k) s_rec[k][tid] = v[k];
 #pragma unroll
           for (int q = 0; q < kNR; ++q) s_rec[7 + q][tid] = (q & 1) ? (v[7 + q / 2] >> 16) : (v[7 + q / 2] & 0xFFFFu);
+          if constexpr (COLS) {
+#pragma unroll
+            for (int e = 0; e < 3; ++e) s_rec[kFNfi + e][tid] = v[7 + kRsPairs + e];
+          }
         }
         __syncthreads();
+        if (PAIRS && fix >= 0 && a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 20] = __builtin_amdgcn_s_memrealtime();
       } else if (s_fail) {   // (PAIRS owner: wave 0 gathered before the fix-up barrier)
         ok = false;
         break;
       }
-      const int f = tid >> 4, seg = tid & 15;
-      if (f < 7 + kNR) {   // waves 0..3 cover fields 0..15; f is uniform per 16 lanes
-        const bool is_max = f < 6;
+      const int seg = tid & 15;
+      for (int f = tid >> 4; f < NF1; f += kBB >> 4) {   // 16 lanes per field; f is uniform per 16 lanes
+        const bool is_max = f < 6, is_or = f == kFDlo || f == kFDhi;
+        // a lane's ≤ kMaxGrid / 16 records of the field in one LDS round trip (a loop carried
+        // through acc waited out every load: ~1 µs per pass at G = 256), past G masked (every
+        // field's identity is 0: the maxima start at 1)
+        uint32_t x[kMaxGrid / 16];
+#pragma unroll
+        for (int i = 0; i < kMaxGrid / 16; ++i) x[i] = s_rec[f][seg + 16 * i];
         uint32_t acc = is_max ? 1u : 0u;
-        for (int t = seg; t < G; t += 16) {
-          const uint32_t x = s_rec[f][t];
-          acc = is_max ? (x > acc ? x : acc) : acc + x;
+#pragma unroll
+        for (int i = 0; i < kMaxGrid / 16; ++i) {
+          const uint32_t y = seg + 16 * i < G ? x[i] : 0u;
+          acc = is_max ? (y > acc ? y : acc) : is_or ? (acc | y) : acc + y;
         }
         // the 16 lanes of a field are one DPP row (f is row-uniform)
         if (is_max) {
           acc = group_reduce(acc, OpMax{});
           acc = OpMax{}(acc, dpp<kDppRowMirror>(acc));
+        } else if (is_or) {
+          acc = group_reduce(acc, OpOr{});
+          acc |= dpp<kDppRowMirror>(acc);
         } else {
           acc = group_reduce(acc, OpSum{});
           acc += dpp<kDppRowMirror>(acc);
         }
         if (seg == 0) s_glob[f] = acc;
       }
+      if (PAIRS && fix >= 0 && a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 21] = __builtin_amdgcn_s_memrealtime();
       // (also orders a PAIRS owner's gang merge before phase B)
       __syncthreads();
     }
@@ -1588,6 +1740,10 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     const int nf = (int)s_glob[6];
     const uint64_t gmx[6] = {s_glob[0], s_glob[1], s_glob[2], s_glob[3], s_glob[4], s_glob[5]};
     score_consts_maxima(sc, gmx);
+    // PodTopologySpread weights log(size + 2) (engine.cpp spread_scores): the hostname
+    // constraint's size is the feasible non-ignored nodes, the domain constraint's the domains
+    // among them; the logarithms come from the host's libm (a table), as the CPU engine's
+    const int spl = r.spread_slot;
     // request b+1 (prefetched at the start of this pod) to LDS; the barriers of the
     // remaining phases order it before the next pod reads it
     if (tid < kReqWords) {
@@ -1599,7 +1755,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     // ================= phase B: maxima-normalised card metrics → raw scores, lo/hi → record 2
     unsigned long long glo = ULLONG_MAX, ghi = 0;
     {
-      unsigned long long lo = ULLONG_MAX, hi = 0;
+      unsigned long long lo = ULLONG_MAX, hi = 0, slo = ULLONG_MAX, shi = 0;
       for (int j0 = wave * kNodesPerWave; j0 < cnt; j0 += BW * kNodesPerWave) {
         const int j = j0 + grp;
         const bool act = j < cnt && s_feas[j];
@@ -1607,38 +1763,69 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         const uint64_t rbase = (act && sub == 0) ? (uint64_t)s_raw[j] : 0;
         const int64_t raw_v = score_node_b(s_rows + (j < cnt ? j : 0), act, emask, sc, sub, rbase, lo, hi);
         if (act && sub == 0) s_raw[j] = raw_v;
+        if (COLS && act && sub == 0 && spl >= 0) {
+          // Σ over the constraints, in order, of count × weight + (maxSkew − 1) in float64 with
+          // the CPU's rounding (no contraction), truncated; −1: the node lacks a key (ignored)
+          const uint32_t d = s_dom[spl * npb + j];
+          int32_t sp = -1;
+          if (d != YODA_DEV_DOM_NONE) {
+            const uint32_t ndom = (uint32_t)__popc((uint32_t)s_glob[kFDlo]) + (uint32_t)__popc((uint32_t)s_glob[kFDhi]);
+            double total = 0.0;
+            for (int c = 0; c < (int)r.spread_nc; ++c) {
+              const int32_t cv = r.ckind[c] ? s_zc[spl][d] : s_cnt[spl * npb + j];
+              const double w = a.logtab[r.ckind[c] ? ndom : (uint32_t)s_glob[kFNfi]];
+              total = __dadd_rn(total, __dadd_rn(__dmul_rn((double)cv, w), (double)(r.cskew[c] - 1)));
+            }
+            sp = (int32_t)(int64_t)total;   // the host bounds the columns so that this fits
+            const unsigned long long us = (unsigned long long)sp;
+            slo = us < slo ? us : slo;
+            shi = us > shi ? us : shi;
+          }
+          s_sp[j] = sp;
+        }
       }
       lo = wave_min(lo);
       hi = wave_max(hi);
+      if (COLS && spl >= 0) {
+        slo = wave_min(slo);
+        shi = wave_max(shi);
+      }
       if (lane == 0) {
         s_part[wave][0] = lo;
         s_part[wave][1] = hi;
+        s_part[wave][2] = slo;
+        s_part[wave][3] = shi;
       }
       __syncthreads();
-      if (tid < kRec2) {
+      if (tid < REC2) {
         unsigned long long blo = ULLONG_MAX, bhi = 0;
+        const int q = tid < 4 ? 0 : 2;   // raw lo/hi, then spread lo/hi
         for (int w = 0; w < BW; ++w) {
-          blo = s_part[w][0] < blo ? s_part[w][0] : blo;
-          bhi = s_part[w][1] > bhi ? s_part[w][1] : bhi;
+          blo = s_part[w][q] < blo ? s_part[w][q] : blo;
+          bhi = s_part[w][q + 1] > bhi ? s_part[w][q + 1] : bhi;
         }
-        const unsigned long long x = tid < 2 ? blo : bhi;
+        const unsigned long long x = (tid & 3) < 2 ? blo : bhi;
         store_granule(slot_ptr(a, tag2, g) + tid, tag2, (tid & 1) ? (uint32_t)(x >> 32) : (uint32_t)x);
       }
       TRACE(4);
       if (G <= 128) {
         // wave 0 alone gathers and reduces; one barrier hands lo/hi to the block
         if (wave == 0) {
-          uint32_t v[kRec2], v2[kRec2];
-          if (gather_wave0<kRec2>(a, tag2, G, p0, v, v2)) {
+          uint32_t v[REC2], v2[REC2];
+          if (gather_wave0<REC2>(a, tag2, G, p0, v, v2)) {
             const bool have = tid < G, have2 = tid + 64 < G;
-            const unsigned long long l1 = have ? ((unsigned long long)v[1] << 32 | v[0]) : ULLONG_MAX;
-            const unsigned long long l2 = have2 ? ((unsigned long long)v2[1] << 32 | v2[0]) : ULLONG_MAX;
-            const unsigned long long h1 = have ? ((unsigned long long)v[3] << 32 | v[2]) : 0ull;
-            const unsigned long long h2 = have2 ? ((unsigned long long)v2[3] << 32 | v2[2]) : 0ull;
-            const unsigned long long wlo = wave_min(l1 < l2 ? l1 : l2), whi = wave_max(h1 > h2 ? h1 : h2);
-            if (lane == 0) {
-              s_red[0] = wlo;
-              s_red[1] = whi;
+#pragma unroll
+            for (int q = 0; q < (COLS ? 2 : 1); ++q) {   // raw lo/hi, spread lo/hi
+              const int o = 4 * q;
+              const unsigned long long l1 = have ? ((unsigned long long)v[o + 1] << 32 | v[o]) : ULLONG_MAX;
+              const unsigned long long l2 = have2 ? ((unsigned long long)v2[o + 1] << 32 | v2[o]) : ULLONG_MAX;
+              const unsigned long long h1 = have ? ((unsigned long long)v[o + 3] << 32 | v[o + 2]) : 0ull;
+              const unsigned long long h2 = have2 ? ((unsigned long long)v2[o + 3] << 32 | v2[o + 2]) : 0ull;
+              const unsigned long long wlo = wave_min(l1 < l2 ? l1 : l2), whi = wave_max(h1 > h2 ? h1 : h2);
+              if (lane == 0) {
+                s_red[2 * q] = wlo;
+                s_red[2 * q + 1] = whi;
+              }
             }
           } else if (lane == 0) {
             s_fail = 1;
@@ -1652,24 +1839,37 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         glo = s_red[0];
         ghi = s_red[1];
       } else {
-        uint32_t v[kRec2];
-        if (!gather<kRec2>(a, tag2, G, p0, v, &s_fail)) {
+        uint32_t v[REC2];
+        if (!gather<REC2>(a, tag2, G, p0, v, &s_fail)) {
           ok = false;
           break;
         }
         // (the gather's barrier ordered every read of the record-2 partials before these writes)
         const bool have = tid < G;
-        const unsigned long long mlo = have ? ((unsigned long long)v[1] << 32 | v[0]) : ULLONG_MAX;
-        const unsigned long long mhi = have ? ((unsigned long long)v[3] << 32 | v[2]) : 0ull;
-        const unsigned long long wlo = wave_min(mlo), whi = wave_max(mhi);
-        if (lane == 0) {
-          s_part[wave][0] = wlo;
-          s_part[wave][1] = whi;
+#pragma unroll
+        for (int q = 0; q < (COLS ? 2 : 1); ++q) {
+          const int o = 4 * q;
+          const unsigned long long mlo = have ? ((unsigned long long)v[o + 1] << 32 | v[o]) : ULLONG_MAX;
+          const unsigned long long mhi = have ? ((unsigned long long)v[o + 3] << 32 | v[o + 2]) : 0ull;
+          const unsigned long long wlo = wave_min(mlo), whi = wave_max(mhi);
+          if (lane == 0) {
+            s_part[wave][2 * q] = wlo;
+            s_part[wave][2 * q + 1] = whi;
+          }
         }
         __syncthreads();
         for (int w = 0; w < BW; ++w) {
           glo = s_part[w][0] < glo ? s_part[w][0] : glo;
           ghi = s_part[w][1] > ghi ? s_part[w][1] : ghi;
+        }
+        if (COLS && tid == 0) {   // spread lo / hi: read from LDS where used (fewer live registers)
+          unsigned long long sl = ULLONG_MAX, sh = 0;
+          for (int w = 0; w < BW; ++w) {
+            sl = s_part[w][2] < sl ? s_part[w][2] : sl;
+            sh = s_part[w][3] > sh ? s_part[w][3] : sh;
+          }
+          s_red[2] = sl;
+          s_red[3] = sh;
         }
         __syncthreads();
       }
@@ -1685,10 +1885,20 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       const uint64_t den = (uint64_t)hi - (uint64_t)lo;
       const double rden = rcp64((double)den);
       unsigned long long best = 0;
+      // PodTopologySpread NormalizeScore: ignored nodes 0; MaxNodeScore when the highest is 0;
+      // else 100·(hi + lo − s) / hi (all terms ≥ 0)
+      const int64_t shi = (int64_t)s_red[3], slo = (int64_t)s_red[2];
+      const int img_sl = r.img_slot;
       for (int j = tid; j < cnt; j += kBB) {
         if (!s_feas[j]) continue;
         int64_t f = s_total[j];
         if (sc.yoda_s) f += (int64_t)udiv_r(((uint64_t)s_raw[j] - (uint64_t)lo) * 100ull, den, rden) * r.w_yoda;
+        if (COLS && spl >= 0) {
+          const int64_t sp = s_sp[j];
+          const int64_t norm = sp < 0 ? 0 : shi == 0 ? 100 : (100 * (shi + slo - sp)) / shi;   // (sp: int32)
+          f += norm * (int64_t)r.spread_w;
+        }
+        if (COLS && img_sl >= 0) f += s_img[img_sl * npb + j];
         const uint32_t p = ((uint32_t)(base + j) * r.perm_mul + r.perm_add) & 0xFFFFFFu;
         const unsigned long long k = ((unsigned long long)f << 24) | p;
         best = k > best ? k : best;
@@ -1696,31 +1906,46 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       best = wave_max(best);
       if (lane == 0) s_part[wave][0] = best;
       __syncthreads();
-      if (tid < (PAIRS ? 3 : kRec3)) {
+      if (tid < REC3) {
         unsigned long long bb = 0;
         for (int w = 0; w < BW; ++w) bb = s_part[w][0] > bb ? s_part[w][0] : bb;
         uint32_t x = tid == 0 ? (uint32_t)bb : (uint32_t)(bb >> 32);
-        if (tid == 2) {   // PAIRS: the block best's GPU mask, whether the pod fits anywhere and here
-          uint32_t m = 0;
+        if (tid == 2) {   // the block best's GPU mask (PAIRS), whether the pod fits anywhere and here,
+                          // and the node's domain in each spread slot (every block counts the winner)
+          uint32_t m = 0, dd = 0xFFFF0000u;
           const bool here = s_bfeas > 0;   // (a best key of 0 is a feasible node's when here)
           if (here) {
             const uint32_t pb = (uint32_t)(bb & 0xFFFFFFull);
             const int nb = (int)(((pb - r.perm_add) * r.perm_inv) & 0xFFFFFFu);
-            if (nb >= base && nb < base + cnt) m = s_mask[nb - base];
+            if (nb >= base && nb < base + cnt) {
+              m = s_mask[nb - base];
+              for (int sl = 0; sl < a.n_sp; ++sl)
+                dd = (dd & ~(0xFFu << (16 + 8 * sl))) | ((uint32_t)s_dom[sl * npb + nb - base] << (16 + 8 * sl));
+            }
           }
-          x = m | ((nf > 0 ? 1u : 0u) << 8) | ((here ? 1u : 0u) << 9);
+          x = m | ((nf > 0 ? 1u : 0u) << 8) | ((here ? 1u : 0u) << 9) | dd;
         }
         store_granule(slot_ptr(a, tag3, g) + tid, tag3, x);
       }
       TRACE(6);
       if (G <= 128) {
         if (wave == 0) {
-          uint32_t v[kRec3], v2[kRec3];
-          if (gather_wave0<kRec3>(a, tag3, G, p0, v, v2)) {
+          uint32_t v[REC3], v2[REC3];
+          if (gather_wave0<REC3>(a, tag3, G, p0, v, v2)) {
             const unsigned long long k1 = tid < G ? ((unsigned long long)v[1] << 32 | v[0]) : 0ull;
             const unsigned long long k2 = tid + 64 < G ? ((unsigned long long)v2[1] << 32 | v2[0]) : 0ull;
             const unsigned long long wk = wave_max(k1 > k2 ? k1 : k2);
             if (lane == 0) s_red[0] = wk;
+            if constexpr (COLS) {   // the winning record's granule 2 (its domains)
+              const bool h1 = tid < G && k1 == wk && ((v[2] >> 9) & 1u);
+              const bool h2 = tid + 64 < G && k2 == wk && ((v2[2] >> 9) & 1u);
+              const unsigned long long bal = __ballot(h1 || h2);
+              if (bal) {
+                const int src = __ffsll((long long)bal) - 1;
+                const uint32_t g2 = (uint32_t)__builtin_amdgcn_readlane((int)(h1 ? v[2] : v2[2]), src);
+                if (lane == 0) s_wdom = g2;
+              }
+            }
           } else if (lane == 0) {
             s_fail = 1;
           }
@@ -1732,8 +1957,8 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         }
         key = s_red[0];
       } else {
-        uint32_t v[kRec3];
-        if (!gather<kRec3>(a, tag3, G, p0, v, &s_fail)) {
+        uint32_t v[REC3];
+        if (!gather<REC3>(a, tag3, G, p0, v, &s_fail)) {
           ok = false;
           break;
         }
@@ -1742,6 +1967,10 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         if (lane == 0) s_part[wave][0] = wk;
         __syncthreads();
         for (int w = 0; w < BW; ++w) key = s_part[w][0] > key ? s_part[w][0] : key;
+        if constexpr (COLS) {
+          if (tid < G && mk == key && ((v[2] >> 9) & 1u)) s_wdom = v[2];
+          __syncthreads();
+        }
       }
     }
     TRACE(7);
@@ -1752,6 +1981,12 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       const uint32_t p = (uint32_t)(key & 0xFFFFFFull);
       node = (int)(((p - r.perm_add) * r.perm_inv) & 0xFFFFFFu);
     }
+    // every block counts the winner in its domain tables (the owner its node count: assume_row)
+    if (COLS && nf > 0 && tid == 0)
+      for (int sl = 0; sl < a.n_sp; ++sl) {
+        const uint32_t d = (s_wdom >> (16 + 8 * sl)) & 0xFFu;
+        if (((r.match_mask >> sl) & 1u) && d != YODA_DEV_DOM_NONE) s_zc[sl][d] += 1;
+      }
     const bool owner = nf > 0 ? (node >= base && node < base + cnt) : gi == 0;
     if (owner) {
       const int j = nf > 0 ? node - base : 0;
@@ -1879,6 +2114,8 @@ struct Ctx {
   double wait_us_per_pod = 0;   // k_batch wall µs per pod, smoothed (the host's pre-sleep)
   long long n_presleep = 0;
   int occ_waves = 0, occ_lds = -1, occ_blocks = 0;   // cached k_batch occupancy query
+  bool occ_cols = false;
+  bool force_cols = false;   // YODA_DEV_FORCE_COLS=1: batches without columns on the COLS kernel (A/B)
   yoda_dev_req_t *h_reqs = nullptr, *d_reqs_map = nullptr;
   yoda_dev_result_t* d_bres = nullptr;
   unsigned long long* d_slots = nullptr;
@@ -1890,6 +2127,14 @@ struct Ctx {
   bool last_pairs = false;
   unsigned long long* d_trace = nullptr;   // yoda_dev_batch_trace: block 0's phase stamps
   int trace_pods = 0;
+  // score columns staged by yoda_dev_batch_extras for the next batch (mapped pinned memory the
+  // kernel reads in its prologue) and the log table of PodTopologySpread's weights
+  int32_t *h_sp_cnt = nullptr, *d_sp_cnt = nullptr, *h_sp_zc = nullptr, *d_sp_zc = nullptr;
+  uint8_t *h_sp_dom = nullptr, *d_sp_dom = nullptr;
+  int32_t *h_img = nullptr, *d_img = nullptr;
+  double* d_logtab = nullptr;
+  int x_n = 0, x_sp = 0, x_img = 0;   // staged columns (consumed by the next batch)
+  int lds_static = 0;                 // k_batch's static LDS (the dynamic part gets the rest)
 };
 
 #define CK(x)                               \
@@ -2004,6 +2249,7 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
   if (const char* v = getenv("YODA_DEV_HOST_DEADLINE_US")) c->host_deadline_us = atof(v) > 0 ? atof(v) : 1.0;
   if (const char* v = getenv("YODA_DEV_BWAVES")) c->batch_waves = atoi(v) == 4 ? 4 : atoi(v) == 8 ? 8 : 0;
   if (const char* v = getenv("YODA_DEV_PAIRS")) c->pairs = v[0] != '0';
+  if (const char* v = getenv("YODA_DEV_FORCE_COLS")) c->force_cols = v[0] == '1';
   if (const char* v = getenv("YODA_DEV_DIRECT_ATOMICS")) c->direct_atomics = v[0] == '1' ? 1 : 0;
   if (const char* v = getenv("YODA_DEV_FUSE_MAX")) c->fuse_max = atoi(v);
   const SubsetTable st = make_subsets();
@@ -2055,10 +2301,48 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
   if ((e = hipMemset(c->d_slots, 0, slot_bytes)) != hipSuccess) return fail("slots", e);
   if ((e = hipMalloc(&c->d_words, 64)) != hipSuccess) return fail("words", e);
   if ((e = hipMemset(c->d_words, 0, 64)) != hipSuccess) return fail("words", e);
-  for (const void* kf : {(const void*)k_batch<4, false>, (const void*)k_batch<8, false>, (const void*)k_batch<4, true>,
-                         (const void*)k_batch<8, true>})
-    if ((e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)(kMaxNodesPerBlock * kBatchRowBytes))) != hipSuccess)
+  // score columns (2 slots each) and log(i + 2) for i ≤ capacity from the host's libm (the CPU
+  // engine's std::log), so device and CPU weights are the same doubles
+  if ((e = hipHostMalloc(&c->h_sp_cnt, kSP * N * sizeof(int32_t), hipHostMallocMapped)) != hipSuccess)
+    return fail("spread counts", e);
+  if ((e = hipHostGetDevicePointer((void**)&c->d_sp_cnt, c->h_sp_cnt, 0)) != hipSuccess) return fail("spread map", e);
+  if ((e = hipHostMalloc(&c->h_sp_dom, kSP * N, hipHostMallocMapped)) != hipSuccess) return fail("spread domains", e);
+  if ((e = hipHostGetDevicePointer((void**)&c->d_sp_dom, c->h_sp_dom, 0)) != hipSuccess) return fail("spread map", e);
+  if ((e = hipHostMalloc(&c->h_sp_zc, kSP * kDOM * sizeof(int32_t), hipHostMallocMapped)) != hipSuccess)
+    return fail("spread zones", e);
+  if ((e = hipHostGetDevicePointer((void**)&c->d_sp_zc, c->h_sp_zc, 0)) != hipSuccess) return fail("spread map", e);
+  if ((e = hipHostMalloc(&c->h_img, kIMG * N * sizeof(int32_t), hipHostMallocMapped)) != hipSuccess)
+    return fail("image scores", e);
+  if ((e = hipHostGetDevicePointer((void**)&c->d_img, c->h_img, 0)) != hipSuccess) return fail("image map", e);
+  {
+    double* lt = new double[N + 3];
+    for (size_t i = 0; i < N + 3; ++i) lt[i] = std::log((double)(i + 2));
+    e = hipMalloc(&c->d_logtab, (N + 3) * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpy(c->d_logtab, lt, (N + 3) * sizeof(double), hipMemcpyHostToDevice);
+    delete[] lt;
+    if (e != hipSuccess) return fail("log table", e);
+  }
+  // every byte of LDS the static part leaves goes to the dynamic part (rows + columns)
+  int lds_max = 65536;
+  hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, device);
+  static const void* const kBatchKernels[] = {
+      (const void*)k_batch<4, false, false>, (const void*)k_batch<8, false, false>, (const void*)k_batch<4, true, false>,
+      (const void*)k_batch<8, true, false>,  (const void*)k_batch<4, false, true>,  (const void*)k_batch<8, false, true>,
+      (const void*)k_batch<4, true, true>,   (const void*)k_batch<8, true, true>};
+  for (const void* kf : kBatchKernels) {
+    hipFuncAttributes fa{};
+    if ((e = hipFuncGetAttributes(&fa, kf)) != hipSuccess) return fail("k_batch attributes", e);
+    c->lds_static = (int)fa.sharedSizeBytes > c->lds_static ? (int)fa.sharedSizeBytes : c->lds_static;
+  }
+  const int dyn_max = lds_max - c->lds_static;
+  if (dyn_max < (int)(kMaxNodesPerBlock * kBatchRowBytes)) {
+    snprintf(err, err_len, "k_batch LDS: %d B static + %zu B rows > %d B", c->lds_static,
+             kMaxNodesPerBlock * kBatchRowBytes, lds_max);
+    delete c;
+    return nullptr;
+  }
+  for (const void* kf : kBatchKernels)
+    if ((e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, dyn_max)) != hipSuccess)
       return fail("k_batch LDS", e);
   Globals init;
   globals_reset(&init);
@@ -2075,6 +2359,7 @@ void yoda_dev_destroy(void* p) {
   hipFree(c->d_feas); hipFree(c->d_elig); hipFree(c->d_cand); hipHostFree(c->h_cand); hipFree(c->d_raw);
   hipFree(c->d_total); hipFree(c->d_mask); hipFree(c->d_quality); hipHostFree(c->h_res); hipHostFree(c->h_resb); hipFree(c->d_g);
   hipHostFree(c->h_reqs); hipHostFree(c->h_done); hipFree(c->d_bres); hipFree(c->d_slots); hipFree(c->d_words);
+  hipHostFree(c->h_sp_cnt); hipHostFree(c->h_sp_dom); hipHostFree(c->h_sp_zc); hipHostFree(c->h_img); hipFree(c->d_logtab);
   hipEventDestroy(c->e0); hipEventDestroy(c->e1);
   hipStreamDestroy(c->stream);
   delete c;
@@ -2211,6 +2496,10 @@ int yoda_dev_schedule(void* p, int n, const yoda_dev_req_t* req, const uint8_t* 
 // Persistent path: one k_batch dispatch per chunk of ≤ kBatchCap pods. Returns 1 when the
 // cluster does not fit the LDS-resident layout (the caller then uses the launch chain).
 static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yoda_dev_result_t* out) {
+  // staged score columns belong to this call's nodes and first chunk only (in-batch counts are
+  // the kernel's own; a second chunk would restart from the staged ones)
+  const bool cols = c->x_sp > 0 || c->x_img > 0 || c->force_cols;
+  if ((c->x_sp > 0 || c->x_img > 0) && (c->x_n != n || B > kBatchCap)) return -3;
   int npb = (n + c->cus - 1) / c->cus;
   // 4 waves while one pass of 8 nodes per wave covers a block's share (a wave per SIMD is
   // fastest then); beyond, 8 waves: two per SIMD hide each other's latency and halve the
@@ -2222,26 +2511,29 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
   // blocks lose, profiles/device/r3/geometry/)
   const int npb_min = c->npb_min > 0 ? c->npb_min : (n <= 1024 ? kNodesPerWave : waves * kNodesPerWave);
   npb = npb < npb_min ? npb_min : npb;
-  if (npb > kMaxNodesPerBlock) return 1;
+  if (npb > kMaxNodesPerBlock) return cols ? -3 : 1;
   const int G = (n + npb - 1) / npb;
-  if (G > kMaxGrid) return 1;
-  const size_t lds = (size_t)npb * kBatchRowBytes;
+  if (G > kMaxGrid) return cols ? -3 : 1;
+  const size_t lds = (size_t)npb * (kBatchRowBytes + batch_col_bytes(c->x_sp, c->x_img));
   // every block spins on the others' records: all G must be resident at once. The device's
   // capacity for this geometry (blocks per CU × CUs) must cover G, or the batch takes the
   // launch chain (no cross-block waits). A tenant kernel holding CUs at run time is the
   // host deadline's job (abandon + CPU path), not this check's.
-  if (c->occ_waves != waves || c->occ_lds != (int)lds) {
+  if (c->occ_waves != waves || c->occ_lds != (int)lds || c->occ_cols != cols) {
     int nb = 0, np = 0;
-    const hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &nb, waves == 8 ? (const void*)k_batch<8, false> : (const void*)k_batch<4, false>, waves * 64, lds);
-    const hipError_t op = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &np, waves == 8 ? (const void*)k_batch<8, true> : (const void*)k_batch<4, true>, waves * 64, lds);
+    const void* k1 = cols ? (waves == 8 ? (const void*)k_batch<8, false, true> : (const void*)k_batch<4, false, true>)
+                          : (waves == 8 ? (const void*)k_batch<8, false, false> : (const void*)k_batch<4, false, false>);
+    const void* k2 = cols ? (waves == 8 ? (const void*)k_batch<8, true, true> : (const void*)k_batch<4, true, true>)
+                          : (waves == 8 ? (const void*)k_batch<8, true, false> : (const void*)k_batch<4, true, false>);
+    const hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k1, waves * 64, lds);
+    const hipError_t op = hipOccupancyMaxActiveBlocksPerMultiprocessor(&np, k2, waves * 64, lds);
     c->occ_waves = waves;
     c->occ_lds = (int)lds;
+    c->occ_cols = cols;
     c->occ_blocks = oe == hipSuccess ? nb : 0;
     c->occ_blocks_pairs = op == hipSuccess ? np : 0;
   }
-  if ((long long)c->occ_blocks * c->cus_total < G) return 1;
+  if ((long long)c->occ_blocks * c->cus_total < G) return cols ? -3 : 1;
   // two sets of G blocks: every one resident, and within the slot table
   const bool pairs = c->pairs && 2 * G <= kMaxGrid && (long long)c->occ_blocks_pairs * c->cus_total >= 2 * G;
   c->last_grid = G;
@@ -2274,14 +2566,31 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
     a.ticket = c->d_words;
     a.abort_word = c->d_words + 1;
     a.trace = c->d_trace;
+    a.sp_cnt = c->d_sp_cnt;
+    a.sp_dom = c->d_sp_dom;
+    a.sp_zc = c->d_sp_zc;
+    a.img = c->d_img;
+    a.logtab = c->d_logtab;
+    a.n_sp = c->x_sp;
+    a.n_img = c->x_img;
     __atomic_store_n(c->h_done, 0, __ATOMIC_RELEASE);
     if (c->timing) CK(hipEventRecord(c->e0, c->stream));
     if (pairs && m >= 2) {
-      if (waves == 8) hipLaunchKernelGGL((k_batch<8, true>), dim3(2 * G), dim3(512), lds, c->stream, a);
-      else hipLaunchKernelGGL((k_batch<4, true>), dim3(2 * G), dim3(256), lds, c->stream, a);
+      if (cols) {
+        if (waves == 8) hipLaunchKernelGGL((k_batch<8, true, true>), dim3(2 * G), dim3(512), lds, c->stream, a);
+        else hipLaunchKernelGGL((k_batch<4, true, true>), dim3(2 * G), dim3(256), lds, c->stream, a);
+      } else {
+        if (waves == 8) hipLaunchKernelGGL((k_batch<8, true, false>), dim3(2 * G), dim3(512), lds, c->stream, a);
+        else hipLaunchKernelGGL((k_batch<4, true, false>), dim3(2 * G), dim3(256), lds, c->stream, a);
+      }
     } else {
-      if (waves == 8) hipLaunchKernelGGL((k_batch<8, false>), dim3(G), dim3(512), lds, c->stream, a);
-      else hipLaunchKernelGGL((k_batch<4, false>), dim3(G), dim3(256), lds, c->stream, a);
+      if (cols) {
+        if (waves == 8) hipLaunchKernelGGL((k_batch<8, false, true>), dim3(G), dim3(512), lds, c->stream, a);
+        else hipLaunchKernelGGL((k_batch<4, false, true>), dim3(G), dim3(256), lds, c->stream, a);
+      } else {
+        if (waves == 8) hipLaunchKernelGGL((k_batch<8, false, false>), dim3(G), dim3(512), lds, c->stream, a);
+        else hipLaunchKernelGGL((k_batch<4, false, false>), dim3(G), dim3(256), lds, c->stream, a);
+      }
     }
     c->last_pairs = pairs && m >= 2;
     c->pend.n = 0;
@@ -2356,6 +2665,23 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
   return 0;
 }
 
+int yoda_dev_batch_extras(void* p, int n, int n_spread, const int32_t* cnt, const uint8_t* dom, const int32_t* zc,
+                          int n_img, const int32_t* img) {
+  Ctx* c = (Ctx*)p;
+  if (!c || n <= 0 || n > c->cap || n_spread < 0 || n_spread > kSP || n_img < 0 || n_img > kIMG) return -1;
+  // the previous batch is complete (calls are synchronous): the staging memory is free
+  if (n_spread) {
+    memcpy(c->h_sp_cnt, cnt, (size_t)n_spread * n * sizeof(int32_t));
+    memcpy(c->h_sp_dom, dom, (size_t)n_spread * n);
+    memcpy(c->h_sp_zc, zc, (size_t)n_spread * kDOM * sizeof(int32_t));
+  }
+  if (n_img) memcpy(c->h_img, img, (size_t)n_img * n * sizeof(int32_t));
+  c->x_n = n;
+  c->x_sp = n_spread;
+  c->x_img = n_img;
+  return 0;
+}
+
 // B consecutive cycles enqueued back to back: each cycle's winner is assumed on the
 // device (its node row updated in place by the publishing block), so cycle b+1 sees cycle
 // b's reservation exactly as sequential host cycles would — no host round trip between
@@ -2364,11 +2690,18 @@ int yoda_dev_schedule_batch(void* p, int n, int B, const yoda_dev_req_t* reqs, y
   Ctx* c = (Ctx*)p;
   if (n <= 0 || n > c->cap || B < 0) return -1;
   CK(hipSetDevice(c->device));
-  if (const int b = busy_check(c)) return b;
+  const bool cols = c->x_sp > 0 || c->x_img > 0;
+  if (const int b = busy_check(c)) {
+    c->x_sp = c->x_img = 0;
+    return b;
+  }
   if (c->persist && B > 0) {
     const int rc = batch_persistent(c, n, B, reqs, out);
+    c->x_sp = c->x_img = 0;   // the staged columns were this call's
     if (rc <= 0) return rc;
   }
+  c->x_sp = c->x_img = 0;
+  if (cols) return -3;        // the launch chain has no score columns
   for (int base = 0; base < B; base += kBatchCap) {
     const int m = B - base < kBatchCap ? B - base : kBatchCap;
     for (int j = 0; j < m; ++j) {

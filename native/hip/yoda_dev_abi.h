@@ -13,6 +13,12 @@ extern "C" {
 
 #define YODA_DEV_CARDS 8
 #define YODA_DEV_REASONS 16
+// k_batch per-batch score columns (yoda_dev_batch_extras): up to 2 PodTopologySpread soft
+// constraint sets ("spread slots") and 2 ImageLocality image sets ("image slots") per batch
+#define YODA_DEV_SPREAD_SLOTS 2
+#define YODA_DEV_IMAGE_SLOTS 2
+#define YODA_DEV_DOMAINS 64          // distinct values of a spread slot's non-hostname key
+#define YODA_DEV_DOM_NONE 0xFF       // the node lacks one of the slot's topology keys (ignored)
 
 enum {
   YODA_DEV_ALIVE = 1,
@@ -61,6 +67,17 @@ typedef struct {
   uint32_t perm_mul, perm_add, perm_inv;   // random tie-break: p(i) = (i*mul + add) mod 2^24
   uint32_t dev_flags;     // set by the device context, not the engine
   int64_t ext;            // request of the device's extended resource (0: none)
+  // k_batch only (the per-pod launch chain has no score columns: the engine never sends it a
+  // pod with a slot). PodTopologySpread soft constraints of slot `spread_slot` (-1: none), in
+  // the engine's constraint order: ckind 0 = kubernetes.io/hostname (the node's own count),
+  // 1 = the slot's domain key (its domain's count); maxSkew per constraint; the score weight
+  int32_t spread_w;
+  int8_t spread_slot, img_slot;   // img_slot: ImageLocality column (weighted), -1: none
+  uint8_t spread_nc;              // constraints (1..2)
+  uint8_t match_mask;             // bit s: once assumed, this pod counts for slot s's selector
+  uint8_t ckind[2];
+  uint8_t pad2[2];
+  int32_t cskew[2];
 } yoda_dev_req_t;
 
 typedef struct {
@@ -88,6 +105,13 @@ int yoda_dev_schedule(void* ctx, int n_nodes, const yoda_dev_req_t* req, const u
 int yoda_dev_schedule_batch(void* ctx, int n_nodes, int B, const yoda_dev_req_t* reqs, yoda_dev_result_t* out);
 int yoda_dev_debug(void* ctx, int n_nodes, uint8_t* feas, int64_t* raw, int64_t* total, uint32_t* mask,
                    int32_t* quality);
+// Score columns for the next yoda_dev_schedule_batch call (consumed by it): for each of
+// n_spread slots, per node the slot selector's matching pods (`cnt`, [slot][n]) and the node's
+// domain id (`dom`, [slot][n], YODA_DEV_DOM_NONE: a key is missing), and per domain the
+// matching pods over the nodes with every key (`zc`, [slot][YODA_DEV_DOMAINS]); for each of
+// n_img slots, per node the weighted ImageLocality score (`img`, [slot][n]). 0 = accepted.
+int yoda_dev_batch_extras(void* ctx, int n, int n_spread, const int32_t* cnt, const uint8_t* dom, const int32_t* zc,
+                          int n_img, const int32_t* img);
 // last kernel time of yoda_dev_schedule in microseconds (device events)
 float yoda_dev_last_us(void* ctx);
 // per-cycle event timing (yoda_dev_last_us); off by default — it adds a stream sync

@@ -606,3 +606,43 @@ def test_kind_cluster_batches_pairs_and_single_cycles_agree(require_gpu, n):
     assert any(r[5][13] for r in res_a)
     for i in range(0, n, max(1, n // 97)):
         assert a.node_cards(i) == b.node_cards(i) and a.node_usage(i) == b.node_usage(i)
+
+
+def _cloud_engine(n, seed, device=True):
+    """A zoned cloud pool (``device_scorer.cloud_cluster``): every node carries
+    topology.kubernetes.io/zone (3 zones), the hot image sits on ~30 % of the nodes at varying
+    sizes, and a third of the nodes already hold trainer pods (so the System default spreading —
+    hostname maxSkew 3, zone maxSkew 5 — is a real per-node term)."""
+    from yoda_scheduler_amd.ops import device_scorer as ds
+    from yoda_scheduler_amd.ops.native import core
+    eng = core().Engine(False, 1)
+    ds.cloud_cluster(eng, n, seed)
+    if device:
+        ds.enable(eng, 0, capacity=max(2048, n), min_nodes=1)
+    return eng
+
+
+def _cloud_pod(eng, rng, uid):
+    from yoda_scheduler_amd.ops import device_scorer as ds
+    return ds.cloud_pod(eng, rng, uid)
+
+
+@pytest.mark.parametrize("n", [600, 4096])
+def test_cloud_cluster_spread_and_image_columns_match_the_cpu(require_gpu, n):
+    """on a zoned pool, ReplicaSet pods under the System default spreading
+    and pods whose image only some nodes hold stay on k_batch (score columns: per-node and
+    per-zone matching-pod counts, per-node ImageLocality), including in-batch spread updates; every
+    cycle equals the CPU engine's replay (node among the argmax, score, feasible count, reasons,
+    GPU set)."""
+    from yoda_scheduler_amd.ops import device_scorer as ds
+    from yoda_scheduler_amd.ops.native import pod_req
+    dev, ref = _cloud_engine(n, 31), _cloud_engine(n, 31, device=False)
+    rng = random.Random(n + 7)
+    for rnd in range(3):
+        pods = [_cloud_pod(dev, rng, f"cl-{n}-{rnd}-{k}") for k in range(200)]
+        c0 = ds.counters(dev)
+        diffs = ds.compare_batch(dev, ref, pods, [pod_req(dev, p) for p in pods], [pod_req(ref, p) for p in pods])
+        c1 = ds.counters(dev)
+        assert not diffs, diffs[:3]
+        assert c1["kbatch_pods"] - c0["kbatch_pods"] == len(pods), (c0, c1)   # every pod on k_batch
+    assert dev.device_fallbacks == 0

@@ -47,7 +47,10 @@ OWNER_PHASES = (("own_winner", 13, 9), ("own_filter_rec1", 9, 10), ("own_score_a
                 # inside wave 1's score A: node tables loaded, GPU set chosen, default scores
                 ("own_sa_tables", 14, 16), ("own_sa_gang", 16, 17), ("own_sa_defaults", 17, 15),
                 # wave 0's early gather 1: record 1 sent → every record 1 of the set in hand
-                ("own_early_g1", 10, 18))
+                ("own_early_g1", 10, 18),
+                # the block-wide gather 1 (G > 128): records in hand, transposed, reduced
+                ("own_g1_load", 11, 19), ("own_g1_transpose", 19, 20), ("own_g1_reduce", 20, 21),
+                ("own_g1_barrier", 21, 12))
 
 
 def batch_trace(engine, on: bool = True) -> None:
@@ -78,7 +81,7 @@ def read_batch_trace(engine, max_pods: int = 256) -> list[dict]:
         t = [buf[b * W + k] for k in range(W)]
         d = {ph: (t[k + 1] - t[k]) / 100.0 for k, ph in enumerate(TRACE_PHASES)}
         if t[13] and t[9] and t[12]:   # PAIRS: the fix-up owner's stamps (a pod with one)
-            d.update({ph: (t[hi] - t[lo]) / 100.0 for ph, lo, hi in OWNER_PHASES})
+            d.update({ph: (t[hi] - t[lo]) / 100.0 for ph, lo, hi in OWNER_PHASES if t[lo] and t[hi]})
         out.append(d)
     return out
 
@@ -108,8 +111,10 @@ def enable(engine, device: int = 0, capacity: int = 65536, min_nodes: int = 256)
         raise RuntimeError(f"device scorer unavailable: {err}")
 
 
-def synthetic_cluster(engine, n_nodes: int, seed: int = 0, compat: bool = False, busy: float = 0.5):
-    """Populate ``engine`` with ``n_nodes`` random MI355X/MI350X nodes (8 GPUs each)."""
+def synthetic_cluster(engine, n_nodes: int, seed: int = 0, compat: bool = False, busy: float = 0.5,
+                      labels_fn=None):
+    """Populate ``engine`` with ``n_nodes`` random MI355X/MI350X nodes (8 GPUs each);
+    ``labels_fn(i)``: extra node labels (e.g. a zone)."""
     from ..models.device import MI350X, MI355X, make_node
     from ..models.pod import NodeInfo
     from ..models.scv import Card, Scv, ScvStatus, XgmiLink
@@ -118,7 +123,8 @@ def synthetic_cluster(engine, n_nodes: int, seed: int = 0, compat: bool = False,
     for i in range(n_nodes):
         spec = MI355X if rng.random() < 0.75 else MI350X
         info = NodeInfo.from_obj(make_node(f"node-{i}", cpu=str(rng.choice([96, 192])),
-                                           memory=rng.choice(["1Ti", "2Ti"])))
+                                           memory=rng.choice(["1Ti", "2Ti"]),
+                                           labels=labels_fn(i) if labels_fn else None))
         idx = push_node(engine, info)
         cards = []
         for g in range(8):
@@ -154,6 +160,58 @@ def random_request(engine, rng: random.Random, uid: str):
     return pi, pod_req(engine, pi)
 
 
+def cloud_cluster(engine, n_nodes: int, seed: int = 0) -> None:
+    """A zoned cloud pool on ``engine``: ``synthetic_cluster`` nodes with
+    topology.kubernetes.io/zone (3 zones), the hot image on ~30 % of the nodes at varying sizes, a
+    Service + ReplicaSet selecting app=trainer, the System default spreading, and trainer pods
+    already running on a third of the nodes (so spreading is a real per-node term)."""
+    from ..framework.scheduler import push_spread_source
+    from ..models.pod import PodInfo
+    from ..plugins.spread_affinity import PodTopologySpread
+    from .native import core, pod_req
+    C = core()
+    engine.set_percentage_of_nodes_to_score(100)
+    synthetic_cluster(engine, n_nodes, seed=seed, labels_fn=lambda i: {"topology.kubernetes.io/zone": f"zone-{i % 3}"})
+    rng = random.Random(seed)
+    gi = 1 << 30
+    for i in range(n_nodes):
+        imgs = [("registry.k8s.io/pause:3.9", 1 << 20)]
+        if rng.random() < 0.3:
+            imgs.append(("docker.io/rocm/vllm:v0.6.4", (600 + 250 * rng.randrange(5)) << 20))
+        engine.set_node_extras(i, imgs, [("ephemeral-storage", rng.choice([2, 5, 100]) * gi)], [])
+    engine.filters = engine.filters | C.F_SPREAD
+    engine.set_score_weight(C.S_IMAGE_LOCALITY, 1)
+    engine.set_score_weight(C.S_PREFER_AVOID, 10000)
+    engine.set_score_weight(C.S_SPREAD, 2)
+    engine.set_spread_defaults(PodTopologySpread({}, None).engine_defaults())
+    push_spread_source(engine, "services", {"metadata": {"name": "trainer", "namespace": "default"},
+                                            "spec": {"selector": {"app": "trainer"}}}, False)
+    push_spread_source(engine, "replicasets", {"metadata": {"name": "trainer-rs", "namespace": "default"},
+                                               "spec": {"selector": {"matchLabels": {"app": "trainer"}}}}, False)
+    for k in range(n_nodes // 3):        # trainer pods already running (no GPU reservation)
+        pi = PodInfo.from_obj({"metadata": {"name": f"old-{k}", "uid": f"old-{seed}-{k}", "namespace": "default",
+                                            "labels": {"app": "trainer"}}, "spec": {}})
+        engine.reserve(pi.num_id, pod_req(engine, pi), rng.randrange(n_nodes), [])
+
+
+def cloud_pod(engine, rng: random.Random, uid: str, image: str | None = None, trainer: float = 0.3):
+    """A pod for ``cloud_cluster``: ``random_request``'s GPU labels, an image (the hot one the
+    nodes partly hold, or one none holds; ``image`` fixes it), sometimes ephemeral storage, and
+    with probability ``trainer`` a trainer ReplicaSet pod (System default spreading applies)."""
+    from ..models.pod import PodInfo
+    base, _ = random_request(engine, rng, uid)
+    obj = {"metadata": {"name": uid, "uid": uid, "namespace": "default", "labels": dict(base.labels)},
+           "spec": {"containers": [{"name": "c", "image": image or rng.choice(["docker.io/rocm/vllm:v0.6.4", "rocm/pytorch"]),
+                                    "resources": {"requests": {"cpu": "1", "memory": "16Gi"}}}]}}
+    if rng.random() < 0.2:
+        obj["spec"]["containers"][0]["resources"]["requests"]["ephemeral-storage"] = rng.choice(["1Gi", "3Gi"])
+    if rng.random() < trainer:
+        obj["metadata"]["labels"]["app"] = "trainer"
+        obj["metadata"]["ownerReferences"] = [{"apiVersion": "apps/v1", "kind": "ReplicaSet", "name": "trainer-rs",
+                                               "uid": "rs-1", "controller": True}]
+    return PodInfo.from_obj(obj)
+
+
 def compare_cycle(engine, req) -> dict:
     """Run one device cycle and the CPU reference on the same state; return a diff dict
     (empty = bit-exact). Ties may pick different nodes; the device's node must be one of
@@ -183,6 +241,46 @@ def compare_cycle(engine, req) -> dict:
             diffs["cards"] = (list(dev[3]), list(cards), dev[6], q)
     elif dev[0] != -1:
         diffs["node"] = (dev[0], -1)
+    return diffs
+
+
+def compare_batch(dev, ref, pods, reqs_dev, reqs_ref) -> list:
+    """One k_batch run on ``dev`` against a CPU replay on ``ref`` (same cluster, no device):
+    for each pod in order, the device's node must be in the CPU's argmax set with the CPU's best
+    score, feasible count and reason histogram, and its GPU set the CPU's choice on that node;
+    the replay then reserves the device's choice, so every later pod is compared on the same
+    state. Returns the diffs (empty: bit-exact up to tie-breaks) — the PodTopologySpread and
+    ImageLocality score columns included."""
+    res = dev.schedule_batch([p.num_id for p in pods], reqs_dev)
+    diffs = []
+    for k, (p, r) in enumerate(zip(pods, res)):
+        req = reqs_ref[k]
+        feas, reasons = ref.feasible_nodes(req, [])
+        d = {}
+        if r[1] != len(feas):
+            d["feasible"] = (r[1], len(feas))
+        if list(r[5]) != list(reasons):
+            d["reasons"] = (list(r[5]), list(reasons))
+        if feas:
+            if len(feas) == 1:
+                best, arg = 0, {feas[0]}
+            else:
+                sc = ref.score_nodes(req, feas)
+                best = max(sc)
+                arg = {n for n, s in zip(feas, sc) if s == best}
+            if r[4] != best:
+                d["score"] = (r[4], best)
+            if r[0] not in arg:
+                d["node"] = (r[0], sorted(arg)[:5])
+            ok, cards, _q = ref.select_gpus(req, r[0] if r[0] >= 0 else 0)
+            if r[0] >= 0 and list(r[3]) != list(cards):
+                d["cards"] = (list(r[3]), list(cards))
+        elif r[0] != -1:
+            d["node"] = (r[0], -1)
+        if d:
+            diffs.append((k, d))
+        if r[0] >= 0:
+            ref.reserve(p.num_id, req, r[0], list(r[3]))
     return diffs
 
 
