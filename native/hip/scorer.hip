@@ -922,11 +922,12 @@ __global__ __launch_bounds__(kBlock) void k_select(int n, const yoda_dev_req_t r
 //    makes every waiter give up, the host sees `done` missing and falls back.
 constexpr int kMaxNodesPerBlock = 256;    // 256 × 536 B of LDS per block (+ the batch's score columns)
 constexpr int kRecStride = 16;            // granules per record slot
-// record 1: maxima[6], feasible, 8 reason counts packed 2 × u16, then PodTopologySpread's
-// feasible non-ignored nodes and the domain mask of those (lo, hi)
+// record 1: maxima[6], feasible, 8 reason counts packed 2 × u16; with score columns (COLS) the
+// feasible granule carries PodTopologySpread's feasible non-ignored nodes in its high half, and
+// the domain mask of those follows (lo, hi)
 // (a batch without score columns — COLS false — keeps the shorter records: 11 / 4 / 2-3)
-constexpr int kRec1 = 14;
-constexpr int kRec2 = 8;                  // raw lo, hi, spread lo, hi (2 granules each)
+constexpr int kRec1 = 13;
+constexpr int kRec2 = 6;                  // raw lo, hi (2 granules each), spread lo, hi (1 each: int32 ≥ 0)
 constexpr int kRec3 = 3;                  // best key (2 granules), the block best's mask / flags / domains
 constexpr int kMaxGrid = 256;
 constexpr int kSP = YODA_DEV_SPREAD_SLOTS, kIMG = YODA_DEV_IMAGE_SLOTS, kDOM = YODA_DEV_DOMAINS;
@@ -942,9 +943,17 @@ constexpr int kMaxGroups = kMaxNodesPerBlock / kNodesPerWave;   // 8-node filter
 // candidates to batches), packed into granules 7..10 of record 1
 constexpr int kNR = 8;                    // reason codes a batch can produce (record 1 packs 2 per granule)
 constexpr int kRsPairs = (kNR + 1) / 2;   // their granules
-// record-1 fields once unpacked: 0..5 maxima (max), 6 feasible (sum), 7.. reasons (sum), then
+// per-group aggregates (s_grp): 0..5 maxima (max), 6 feasible (sum), 7.. reasons (sum), then
 // spread's feasible non-ignored nodes (sum) and domain mask (or, two halves)
 constexpr int kFNfi = 7 + kNR, kFDlo = 8 + kNR, kFDhi = 9 + kNR, kNF1 = 10 + kNR;
+// record 1 transposed for the reduction (s_rec / s_glob fields). Without columns the reason
+// pairs are unpacked: 0..5 maxima, 6 feasible, 7..14 reasons (15 fields). With columns the
+// granules are reduced as they are — feasible | non-ignored << 16 and the reason pairs summed as
+// u16 halves (the host keeps such batches below 65536 nodes), the domain halves or-ed — so the
+// 13 fields fit one 16-lane pass of a 4-wave block (18 unpacked fields took a second pass:
+// ~1.1 µs per pod on the PAIRS fix-up owner's critical path, profiles/device/r6/)
+constexpr int kGDlo = 7 + kRsPairs, kGDhi = 8 + kRsPairs;   // record-1 granules of the domain mask
+constexpr int kNF1T = 7 + kNR;                              // the most transposed fields (no columns)
 __constant__ int c_batch_reasons[kNR] = {RS_UNSCHEDULABLE, RS_RESOURCES, RS_NO_SCV, RS_STALE, RS_GPU_NUMBER,
                                          RS_GPU_FIT, RS_DEAD, RS_EXT_RESOURCES};
 
@@ -984,7 +993,8 @@ static_assert(kResWords == 19 && YODA_DEV_REASONS == 16 && offsetof(yoda_dev_res
 // the reason codes of c_batch_reasons, for compile-time indexing
 constexpr int kBatchReasonCodes[kNR] = {RS_UNSCHEDULABLE, RS_RESOURCES, RS_NO_SCV, RS_STALE, RS_GPU_NUMBER,
                                         RS_GPU_FIT, RS_DEAD, RS_EXT_RESOURCES};
-static_assert(7 + kRsPairs + 3 == kRec1, "record 1: 7 fields + the reason counts as u16 pairs + 3 spread fields");
+static_assert(7 + kRsPairs + 2 == kRec1 && kRec1 <= kNF1T && kRec1 <= 16,
+              "record 1: 7 fields + the reason counts as u16 pairs + 2 domain-mask granules, one reduction pass");
 constexpr int kTracePts = 24;   // 9 phase stamps per pod (block 0), 9 of the PAIRS fix-up's owner, padded
 constexpr int kReqWords = sizeof(yoda_dev_req_t) / 4;
 static_assert(sizeof(yoda_dev_req_t) % 4 == 0 && kReqWords <= 64, "req fits one wave");
@@ -1164,24 +1174,19 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   constexpr int kBB = 64 * BW;
   // record sizes of this instantiation: score columns add spread fields to records 1 and 2 and
   // the winner's domains to record 3
-#ifdef YODA_EXP_SHORT_REC
-  constexpr bool XC = false;
-#else
-  constexpr bool XC = COLS;
-#endif
-  constexpr int REC1 = XC ? kRec1 : kRec1 - 3, REC2 = XC ? kRec2 : kRec2 - 4;
-  constexpr int REC3 = (XC || PAIRS) ? kRec3 : kRec3 - 1, NF1 = XC ? kNF1 : kNF1 - 3;
+  constexpr int REC1 = COLS ? kRec1 : kRec1 - 2, REC2 = COLS ? kRec2 : kRec2 - 2;
+  constexpr int REC3 = (COLS || PAIRS) ? kRec3 : kRec3 - 1, NF1 = COLS ? kRec1 : kNF1T;
   extern __shared__ __align__(16) unsigned char s_dyn[];
   __shared__ uint8_t s_masks[256];
   // request ring: pods b (and b−1 in PAIRS mode, for its assume) plus the prefetched next ones
   __shared__ __align__(16) uint32_t s_req[4][sizeof(yoda_dev_req_t) / 4];
   __shared__ int s_fix;   // PAIRS: the other set's last winner's row here, or −1
   __shared__ unsigned long long s_part[BW][16];
-  __shared__ unsigned long long s_glob[kNF1];
+  __shared__ unsigned long long s_glob[kNF1T];
   // G ≤ 64: wave 0 holds every record of a gather and reduces it alone; the result reaches the
   // block through these words and one barrier (no per-wave partials, no second barrier)
   __shared__ unsigned long long s_red[4];
-  __shared__ uint32_t s_rec[kNF1][kMaxGrid + 4];   // gather-1 records transposed (+4: bank skew)
+  __shared__ uint32_t s_rec[kNF1T][kMaxGrid + 4];   // gather-1 records transposed (+4: bank skew)
   // filter aggregates per 8-node group: 6 maxima, feasible count, the reason counts, spread's
   // feasible non-ignored count and domain mask halves
   __shared__ uint32_t s_grp[kMaxGroups][kNF1];
@@ -1304,6 +1309,19 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         }
       }
   };
+  // a gathered record 1 into column t of the transposed fields (without columns the reason
+  // pairs are unpacked; with columns every granule is a field as it is)
+  auto transpose1 = [&](const uint32_t (&v)[REC1], int t) {
+    if constexpr (COLS) {
+#pragma unroll
+      for (int k = 0; k < REC1; ++k) s_rec[k][t] = v[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) s_rec[k][t] = v[k];
+#pragma unroll
+      for (int q = 0; q < kNR; ++q) s_rec[7 + q][t] = (q & 1) ? (v[7 + q / 2] >> 16) : (v[7 + q / 2] & 0xFFFFu);
+    }
+  };
   auto filter_groups = [&](const yoda_dev_req_t& rq, int par) {
     for (int gq = wave; gq * kNodesPerWave < cnt; gq += BW) filter_one(rq, par, gq);
   };
@@ -1316,7 +1334,14 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       if (tid < 7) {
         v = tid < 6 ? 1u : 0u;
         for (int q = 0; q < ngr; ++q) v = tid < 6 ? (s_grp[q][tid] > v ? s_grp[q][tid] : v) : v + s_grp[q][tid];
-        if (tid == 6) s_bfeas = v;
+        if (tid == 6) {
+          s_bfeas = v;
+          if constexpr (COLS) {   // + the feasible non-ignored nodes (≤ npb ≤ 256 each)
+            uint32_t nfi = 0;
+            for (int q = 0; q < ngr; ++q) nfi += s_grp[q][kFNfi];
+            v |= nfi << 16;
+          }
+        }
       } else if (tid < 7 + kRsPairs) {   // reason counts packed as u16 pairs (≤ npb ≤ 256 per block)
         const int r0 = 7 + 2 * (tid - 7);
         uint32_t lo = 0, hi = 0;
@@ -1325,9 +1350,9 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           hi += r0 + 1 < 7 + kNR ? s_grp[q][r0 + 1] : 0u;
         }
         v = lo | (hi << 16);
-      } else if constexpr (COLS) {   // spread: feasible non-ignored nodes (sum), domain mask halves (or)
-        const int f = kFNfi + (tid - 7 - kRsPairs);
-        for (int q = 0; q < ngr; ++q) v = f == kFNfi ? v + s_grp[q][f] : (v | s_grp[q][f]);
+      } else if constexpr (COLS) {   // spread: the domain mask halves (or)
+        const int f = tid == kGDlo ? kFDlo : kFDhi;
+        for (int q = 0; q < ngr; ++q) v |= s_grp[q][f];
       }
       store_granule(slot_ptr(a, tag1, g) + tid, tag1, v);
     }
@@ -1613,26 +1638,8 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           if (gather_wave0<REC1>(a, tag1, G, p0, v, v2, gi)) {
             if (a.trace && lane == 0) a.trace[(size_t)b * kTracePts + 18] = __builtin_amdgcn_s_memrealtime();
             const int t2 = lane + 64;
-            if (lane < G && lane != gi) {
-#pragma unroll
-              for (int k = 0; k < 7; ++k) s_rec[k][lane] = v[k];
-#pragma unroll
-              for (int q = 0; q < kNR; ++q) s_rec[7 + q][lane] = (q & 1) ? (v[7 + q / 2] >> 16) : (v[7 + q / 2] & 0xFFFFu);
-              if constexpr (COLS) {
-#pragma unroll
-                for (int e = 0; e < 3; ++e) s_rec[kFNfi + e][lane] = v[7 + kRsPairs + e];
-              }
-            }
-            if (t2 < G && t2 != gi) {
-#pragma unroll
-              for (int k = 0; k < 7; ++k) s_rec[k][t2] = v2[k];
-#pragma unroll
-              for (int q = 0; q < kNR; ++q) s_rec[7 + q][t2] = (q & 1) ? (v2[7 + q / 2] >> 16) : (v2[7 + q / 2] & 0xFFFFu);
-              if constexpr (COLS) {
-#pragma unroll
-                for (int e = 0; e < 3; ++e) s_rec[kFNfi + e][t2] = v2[7 + kRsPairs + e];
-              }
-            }
+            if (lane < G && lane != gi) transpose1(v, lane);
+            if (t2 < G && t2 != gi) transpose1(v2, t2);
           } else if (lane == 0) {
             s_fail = 1;
           }
@@ -1642,14 +1649,12 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           __builtin_amdgcn_wave_barrier();
           const uint32_t own = record1(tag1);
           if (early1 && tid < REC1) {   // this block's column of the transposed records
-            if (tid < 7) {
+            if (COLS || tid < 7) {
               s_rec[tid][gi] = own;
-            } else if (tid < 7 + kRsPairs) {
+            } else {
               const int q0 = 2 * (tid - 7);
               s_rec[7 + q0][gi] = own & 0xFFFFu;
               if (q0 + 1 < kNR) s_rec[8 + q0][gi] = own >> 16;
-            } else if constexpr (COLS) {
-              s_rec[kFNfi + (tid - 7 - kRsPairs)][gi] = own;
             }
           }
           if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 10] = __builtin_amdgcn_s_memrealtime();
@@ -1685,16 +1690,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         }
         if (PAIRS && fix >= 0 && a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 19] = __builtin_amdgcn_s_memrealtime();
         // transpose through LDS (7 + kNR fields × G), then 16 threads per field reduce it
-        if (tid < G) {
-#pragma unroll
-          for (int k = 0; k < 7; ++k) s_rec[k][tid] = v[k];
-#pragma unroll
-          for (int q = 0; q < kNR; ++q) s_rec[7 + q][tid] = (q & 1) ? (v[7 + q / 2] >> 16) : (v[7 + q / 2] & 0xFFFFu);
-          if constexpr (COLS) {
-#pragma unroll
-            for (int e = 0; e < 3; ++e) s_rec[kFNfi + e][tid] = v[7 + kRsPairs + e];
-          }
-        }
+        if (tid < G) transpose1(v, tid);
         __syncthreads();
         if (PAIRS && fix >= 0 && a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 20] = __builtin_amdgcn_s_memrealtime();
       } else if (s_fail) {   // (PAIRS owner: wave 0 gathered before the fix-up barrier)
@@ -1703,7 +1699,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       }
       const int seg = tid & 15;
       for (int f = tid >> 4; f < NF1; f += kBB >> 4) {   // 16 lanes per field; f is uniform per 16 lanes
-        const bool is_max = f < 6, is_or = f == kFDlo || f == kFDhi;
+        const bool is_max = f < 6, is_or = COLS && f >= kGDlo;
         // a lane's ≤ kMaxGrid / 16 records of the field in one LDS round trip (a loop carried
         // through acc waited out every load: ~1 µs per pass at G = 256), past G masked (every
         // field's identity is 0: the maxima start at 1)
@@ -1736,8 +1732,9 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     if (PAIRS && fix >= 0 && a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 12] = __builtin_amdgcn_s_memrealtime();
     int reasons7[kNR];
 #pragma unroll
-    for (int q = 0; q < kNR; ++q) reasons7[q] = (int)s_glob[7 + q];
-    const int nf = (int)s_glob[6];
+    for (int q = 0; q < kNR; ++q)
+      reasons7[q] = COLS ? (int)((s_glob[7 + q / 2] >> (16 * (q & 1))) & 0xFFFFu) : (int)s_glob[7 + q];
+    const int nf = COLS ? (int)(s_glob[6] & 0xFFFFu) : (int)s_glob[6];
     const uint64_t gmx[6] = {s_glob[0], s_glob[1], s_glob[2], s_glob[3], s_glob[4], s_glob[5]};
     score_consts_maxima(sc, gmx);
     // PodTopologySpread weights log(size + 2) (engine.cpp spread_scores): the hostname
@@ -1756,6 +1753,13 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     unsigned long long glo = ULLONG_MAX, ghi = 0;
     {
       unsigned long long lo = ULLONG_MAX, hi = 0, slo = ULLONG_MAX, shi = 0;
+      double w0 = 0.0, w1 = 0.0;   // the constraints' weights (pod-uniform)
+      if (COLS && spl >= 0) {
+        const uint32_t ndom = (uint32_t)__popc((uint32_t)s_glob[kGDlo]) + (uint32_t)__popc((uint32_t)s_glob[kGDhi]);
+        const uint32_t nfi = (uint32_t)(s_glob[6] >> 16);
+        w0 = a.logtab[r.ckind[0] ? ndom : nfi];
+        if (r.spread_nc > 1) w1 = a.logtab[r.ckind[1] ? ndom : nfi];
+      }
       for (int j0 = wave * kNodesPerWave; j0 < cnt; j0 += BW * kNodesPerWave) {
         const int j = j0 + grp;
         const bool act = j < cnt && s_feas[j];
@@ -1769,12 +1773,10 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           const uint32_t d = s_dom[spl * npb + j];
           int32_t sp = -1;
           if (d != YODA_DEV_DOM_NONE) {
-            const uint32_t ndom = (uint32_t)__popc((uint32_t)s_glob[kFDlo]) + (uint32_t)__popc((uint32_t)s_glob[kFDhi]);
             double total = 0.0;
             for (int c = 0; c < (int)r.spread_nc; ++c) {
               const int32_t cv = r.ckind[c] ? s_zc[spl][d] : s_cnt[spl * npb + j];
-              const double w = a.logtab[r.ckind[c] ? ndom : (uint32_t)s_glob[kFNfi]];
-              total = __dadd_rn(total, __dadd_rn(__dmul_rn((double)cv, w), (double)(r.cskew[c] - 1)));
+              total = __dadd_rn(total, __dadd_rn(__dmul_rn((double)cv, c ? w1 : w0), (double)(r.cskew[c] - 1)));
             }
             sp = (int32_t)(int64_t)total;   // the host bounds the columns so that this fits
             const unsigned long long us = (unsigned long long)sp;
@@ -1804,8 +1806,11 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           blo = s_part[w][q] < blo ? s_part[w][q] : blo;
           bhi = s_part[w][q + 1] > bhi ? s_part[w][q + 1] : bhi;
         }
-        const unsigned long long x = (tid & 3) < 2 ? blo : bhi;
-        store_granule(slot_ptr(a, tag2, g) + tid, tag2, (tid & 1) ? (uint32_t)(x >> 32) : (uint32_t)x);
+        const unsigned long long x = (tid < 4 ? (tid & 3) < 2 : tid == 4) ? blo : bhi;
+        // (spread lo / hi: one granule each, no spread node → lo 0xFFFFFFFF)
+        const uint32_t g32 = tid < 4 ? ((tid & 1) ? (uint32_t)(x >> 32) : (uint32_t)x)
+                                     : (uint32_t)(x < 0xFFFFFFFFull ? x : 0xFFFFFFFFull);
+        store_granule(slot_ptr(a, tag2, g) + tid, tag2, g32);
       }
       TRACE(4);
       if (G <= 128) {
@@ -1814,17 +1819,24 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           uint32_t v[REC2], v2[REC2];
           if (gather_wave0<REC2>(a, tag2, G, p0, v, v2)) {
             const bool have = tid < G, have2 = tid + 64 < G;
-#pragma unroll
-            for (int q = 0; q < (COLS ? 2 : 1); ++q) {   // raw lo/hi, spread lo/hi
-              const int o = 4 * q;
-              const unsigned long long l1 = have ? ((unsigned long long)v[o + 1] << 32 | v[o]) : ULLONG_MAX;
-              const unsigned long long l2 = have2 ? ((unsigned long long)v2[o + 1] << 32 | v2[o]) : ULLONG_MAX;
-              const unsigned long long h1 = have ? ((unsigned long long)v[o + 3] << 32 | v[o + 2]) : 0ull;
-              const unsigned long long h2 = have2 ? ((unsigned long long)v2[o + 3] << 32 | v2[o + 2]) : 0ull;
+            {   // raw lo/hi
+              const unsigned long long l1 = have ? ((unsigned long long)v[1] << 32 | v[0]) : ULLONG_MAX;
+              const unsigned long long l2 = have2 ? ((unsigned long long)v2[1] << 32 | v2[0]) : ULLONG_MAX;
+              const unsigned long long h1 = have ? ((unsigned long long)v[3] << 32 | v[2]) : 0ull;
+              const unsigned long long h2 = have2 ? ((unsigned long long)v2[3] << 32 | v2[2]) : 0ull;
               const unsigned long long wlo = wave_min(l1 < l2 ? l1 : l2), whi = wave_max(h1 > h2 ? h1 : h2);
               if (lane == 0) {
-                s_red[2 * q] = wlo;
-                s_red[2 * q + 1] = whi;
+                s_red[0] = wlo;
+                s_red[1] = whi;
+              }
+            }
+            if constexpr (COLS) {   // spread lo/hi (32-bit)
+              const uint32_t l1 = have ? v[4] : 0xFFFFFFFFu, l2 = have2 ? v2[4] : 0xFFFFFFFFu;
+              const uint32_t h1 = have ? v[5] : 0u, h2 = have2 ? v2[5] : 0u;
+              const uint32_t wlo = wave_min(l1 < l2 ? l1 : l2), whi = wave_max(h1 > h2 ? h1 : h2);
+              if (lane == 0) {
+                s_red[2] = wlo == 0xFFFFFFFFu ? ULLONG_MAX : wlo;
+                s_red[3] = whi;
               }
             }
           } else if (lane == 0) {
@@ -1846,15 +1858,20 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         }
         // (the gather's barrier ordered every read of the record-2 partials before these writes)
         const bool have = tid < G;
-#pragma unroll
-        for (int q = 0; q < (COLS ? 2 : 1); ++q) {
-          const int o = 4 * q;
-          const unsigned long long mlo = have ? ((unsigned long long)v[o + 1] << 32 | v[o]) : ULLONG_MAX;
-          const unsigned long long mhi = have ? ((unsigned long long)v[o + 3] << 32 | v[o + 2]) : 0ull;
+        {
+          const unsigned long long mlo = have ? ((unsigned long long)v[1] << 32 | v[0]) : ULLONG_MAX;
+          const unsigned long long mhi = have ? ((unsigned long long)v[3] << 32 | v[2]) : 0ull;
           const unsigned long long wlo = wave_min(mlo), whi = wave_max(mhi);
           if (lane == 0) {
-            s_part[wave][2 * q] = wlo;
-            s_part[wave][2 * q + 1] = whi;
+            s_part[wave][0] = wlo;
+            s_part[wave][1] = whi;
+          }
+        }
+        if constexpr (COLS) {   // spread lo/hi (32-bit)
+          const uint32_t wlo = wave_min(have ? v[4] : 0xFFFFFFFFu), whi = wave_max(have ? v[5] : 0u);
+          if (lane == 0) {
+            s_part[wave][2] = wlo == 0xFFFFFFFFu ? ULLONG_MAX : wlo;
+            s_part[wave][3] = whi;
           }
         }
         __syncthreads();
@@ -2498,8 +2515,9 @@ int yoda_dev_schedule(void* p, int n, const yoda_dev_req_t* req, const uint8_t* 
 static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yoda_dev_result_t* out) {
   // staged score columns belong to this call's nodes and first chunk only (in-batch counts are
   // the kernel's own; a second chunk would restart from the staged ones)
-  const bool cols = c->x_sp > 0 || c->x_img > 0 || c->force_cols;
-  if ((c->x_sp > 0 || c->x_img > 0) && (c->x_n != n || B > kBatchCap)) return -3;
+  const bool cols = c->x_sp > 0 || c->x_img > 0 || (c->force_cols && n <= 65535);
+  // (a COLS batch sums record-1 counts as u16 halves: below 65536 nodes)
+  if ((c->x_sp > 0 || c->x_img > 0) && (c->x_n != n || B > kBatchCap || n > 65535)) return -3;
   int npb = (n + c->cus - 1) / c->cus;
   // 4 waves while one pass of 8 nodes per wave covers a block's share (a wave per SIMD is
   // fastest then); beyond, 8 waves: two per SIMD hide each other's latency and halve the
