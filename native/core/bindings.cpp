@@ -799,6 +799,15 @@ PYBIND11_MODULE(_yoda_core, m) {
            py::arg("req"), py::arg("candidates"), py::arg("exhaustive") = false, py::call_guard<EngineGuard>())
       .def("num_feasible_to_find", &Engine::num_feasible_to_find, py::call_guard<EngineGuard>())
       .def("score_nodes", &Engine::score_nodes, py::call_guard<EngineGuard>())
+      // the six per-metric maxima (bandwidth, clock, core, free, power, total) over `nodes` —
+      // what k_batch's record 1 exchanges (scripts/record1_reuse.py)
+      .def("maxima",
+           [](const Engine& e, const PodReq& r, const std::vector<int32_t>& nodes) {
+             uint64_t mx[6];
+             e.collect_max(r, nodes, mx);
+             return std::vector<uint64_t>(mx, mx + 6);
+           },
+           py::call_guard<EngineGuard>())
       .def("schedule",
            [](Engine& e, uint64_t pod, const PodReq& r, bool assume, const std::vector<int32_t>& cand,
               const std::vector<int64_t>& extra) { return cycle_tuple(e.schedule(pod, r, assume, cand, extra)); },
