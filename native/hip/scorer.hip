@@ -796,6 +796,40 @@ __device__ __forceinline__ int64_t score_node_b(const yoda_dev_node_t* nd, bool 
   return s_out;
 }
 
+// score_node_b for k_batch: returns the raw score before the int64 clamp (the clamp is applied
+// where it is read, so `s − basic` gives part A back exactly) and the maxima-normalised part
+// (`basic_o`, ≤ 8 cards × 700); lo / hi fold the clamped value. Valid on `sub == 0` when `act`.
+__device__ __forceinline__ uint64_t score_node_b_k(const yoda_dev_node_t* nd, bool act, uint32_t emask,
+                                                   const ScoreConsts& sc, int sub, uint64_t rbase,
+                                                   unsigned long long& lo, unsigned long long& hi, uint32_t& basic_o) {
+  uint64_t basic = 0;
+  if (act && sc.yoda_s && ((emask >> sub) & 1u)) {
+    const yoda_dev_card_t cd = nd->cards[sub];
+    const uint64_t ef = eff_free(cd.free, cd.pending, cd.total, cd.reserved);
+    basic = udiv_r((uint64_t)cd.bandwidth * 100, sc.mx[0], sc.rmx[0]) +
+            udiv_r((uint64_t)cd.clock * 100, sc.mx[1], sc.rmx[1]) +
+            udiv_r((uint64_t)cd.core * 100, sc.mx[2], sc.rmx[2]) +
+            udiv_r((uint64_t)cd.power * 100, sc.mx[4], sc.rmx[4]) +
+            udiv_r(ef * 100, sc.mx[3], sc.rmx[3]) * 2 + udiv_r((uint64_t)cd.total * 100, sc.mx[5], sc.rmx[5]);
+  }
+  basic_o = gsum((uint32_t)basic);
+  uint64_t s = 0;
+  if (act && sub == 0 && sc.yoda_s) {
+    s = basic_o + rbase;
+    const unsigned long long us = s > (uint64_t)LLONG_MAX ? 0ull : s;
+    lo = us < lo ? us : lo;
+    hi = us > hi ? us : hi;
+  }
+  return s;
+}
+
+// SPEC: what makes two pods' maxima differ on the same cards — the clock requirement (a pod held
+// to one clock only sees those cards); the speculation table's key and slot
+__device__ __forceinline__ uint64_t spec_key(const yoda_dev_req_t& r) {
+  return ((uint64_t)r.has_clock << 63) ^ (r.clock << 24) ^ r.clock_min;
+}
+__device__ __forceinline__ int spec_slot(uint64_t key) { return (int)((key * 0x9E3779B97F4A7C15ull) >> 62); }
+
 // Both parts (the per-pod launch chain's k_score).
 __device__ __forceinline__ void score_node(const yoda_dev_node_t* nd, bool act, uint32_t emask,
                                            const yoda_dev_req_t& r, const ScoreConsts& sc,
@@ -912,29 +946,33 @@ __global__ __launch_bounds__(kBlock) void k_select(int n, const yoda_dev_req_t r
 //    partial record write-through (agent-scope relaxed atomic store = sc1), then one thread
 //    per producer block polls that record until every tag equals the phase's epoch and the
 //    block reduces the G records itself. The data is the flag: no fence, no counter, no
-//    reset (tags grow monotonically across launches). Records are double-buffered by epoch
-//    parity: a block can only overwrite slot e%2 after reading every e+1 record, i.e. after
-//    every block finished reading epoch e.
+//    reset (tags grow monotonically across launches). Each record kind has its own slot
+//    (tag mod 3: tags are epoch + 3·pod + kind, epochs ≡ 1 mod 3): a block overwrites its
+//    record of one kind only after an exchange of another kind that every block joined after
+//    reading the first — also when a pod skips record 2 (speculated maxima, below).
 //  * the batch's requests are read from mapped host memory, req b+1 prefetched during pod b;
 //    results collect in a device buffer and the last block (agent release/acquire ticket)
 //    copies them to mapped host memory and raises `done` with a system-scope release.
 //  * every spin is bounded (abort word + s_memrealtime deadline): a block that never arrives
 //    makes every waiter give up, the host sees `done` missing and falls back.
-constexpr int kMaxNodesPerBlock = 256;    // 256 × 536 B of LDS per block (+ the batch's score columns)
+constexpr int kMaxNodesPerBlock = 256;    // 256 × 542 B of LDS per block (+ the batch's score columns)
 constexpr int kRecStride = 16;            // granules per record slot
 // record 1: maxima[6], feasible, 8 reason counts packed 2 × u16; with score columns (COLS) the
 // feasible granule carries PodTopologySpread's feasible non-ignored nodes in its high half, and
 // the domain mask of those follows (lo, hi)
 // (a batch without score columns — COLS false — keeps the shorter records: 11 / 4 / 2-3)
 constexpr int kRec1 = 13;
+// SPEC kernels (PAIRS without columns): record 1 also carries the block's raw lo / hi under the
+// speculated maxima (granules 11..14)
+constexpr int kRec1S = 7 + (8 + 1) / 2 + 4;
 constexpr int kRec2 = 6;                  // raw lo, hi (2 granules each), spread lo, hi (1 each: int32 ≥ 0)
 constexpr int kRec3 = 3;                  // best key (2 granules), the block best's mask / flags / domains
 constexpr int kMaxGrid = 256;
 constexpr int kSP = YODA_DEV_SPREAD_SLOTS, kIMG = YODA_DEV_IMAGE_SLOTS, kDOM = YODA_DEV_DOMAINS;
-// LDS bytes per node: row + raw + total + quality + 2 × feas + 2 × elig + mask + dirty; a batch
+// LDS bytes per node: row + raw + total + quality + basic + 2 × feas + 2 × elig + mask + dirty; a batch
 // with score columns adds batch_col_bytes (spread raw + per slot count and domain, per image
 // slot its score)
-constexpr size_t kBatchRowBytes = sizeof(yoda_dev_node_t) + 8 + 8 + 4 + 6;
+constexpr size_t kBatchRowBytes = sizeof(yoda_dev_node_t) + 8 + 8 + 4 + 4 + 6;
 __host__ __device__ constexpr size_t batch_col_bytes(int n_sp, int n_img) {
   return (n_sp > 0 ? 4 + 5 * (size_t)n_sp : 0) + 4 * (size_t)n_img;
 }
@@ -967,7 +1005,7 @@ struct BatchArgs {
   uint32_t tag0;                      // epoch of record 1 of pod 0 (tags: tag0 + 3b + phase)
   long long deadline_ticks;           // per spin, s_memrealtime ticks (100 MHz)
   const yoda_dev_req_t* reqs;         // device view of mapped host memory
-  unsigned long long* slots;          // [2][kMaxGrid][kRecStride]
+  unsigned long long* slots;          // [3][kMaxGrid][kRecStride]: records 3, 1, 2 (tag mod 3)
   yoda_dev_result_t* res;             // device scratch, one per pod
   yoda_dev_result_t* out;             // device view of mapped host memory
   int32_t* done;                      // mapped host word: seq when `out` is complete
@@ -993,6 +1031,7 @@ static_assert(kResWords == 19 && YODA_DEV_REASONS == 16 && offsetof(yoda_dev_res
 // the reason codes of c_batch_reasons, for compile-time indexing
 constexpr int kBatchReasonCodes[kNR] = {RS_UNSCHEDULABLE, RS_RESOURCES, RS_NO_SCV, RS_STALE, RS_GPU_NUMBER,
                                         RS_GPU_FIT, RS_DEAD, RS_EXT_RESOURCES};
+static_assert(kRec1S == 7 + kRsPairs + 4 && kRec1S <= kRecStride, "SPEC record 1: the plain record + raw lo / hi");
 static_assert(7 + kRsPairs + 2 == kRec1 && kRec1 <= kNF1T && kRec1 <= 16,
               "record 1: 7 fields + the reason counts as u16 pairs + 2 domain-mask granules, one reduction pass");
 constexpr int kTracePts = 24;   // 9 phase stamps per pod (block 0), 9 of the PAIRS fix-up's owner, padded
@@ -1000,7 +1039,7 @@ constexpr int kReqWords = sizeof(yoda_dev_req_t) / 4;
 static_assert(sizeof(yoda_dev_req_t) % 4 == 0 && kReqWords <= 64, "req fits one wave");
 
 __device__ __forceinline__ gu64* slot_ptr(const BatchArgs& a, uint32_t tag, int blk) {
-  return (gu64*)(a.slots + ((size_t)(tag & 1u) * kMaxGrid + blk) * kRecStride);
+  return (gu64*)(a.slots + ((size_t)(tag % 3u) * kMaxGrid + blk) * kRecStride);
 }
 
 __device__ __forceinline__ void store_granule(gu64* p, uint32_t tag, uint32_t v) {
@@ -1030,13 +1069,15 @@ __device__ __forceinline__ bool spin_ok(const BatchArgs& a, unsigned& spins, lon
 // every granule of a record costs G² requests chip-wide (MI355X, 4096 nodes, G = 256 blocks:
 // 3 more granules per record 1 cost ~1 µs per pod) — so halving the requests is what counts.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-constexpr uint32_t kSlotBytes = 2u * kMaxGrid * kRecStride * 8u;
+// (+ one slot per block set for SPEC's fix-up record: the PAIRS owner's re-scored group lo / hi)
+constexpr uint32_t kSlotBytes = (3u * kMaxGrid + 2u) * kRecStride * 8u;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t slot_rsrc(const BatchArgs& a) {
   return __builtin_amdgcn_make_buffer_rsrc(a.slots, 0, (int)kSlotBytes, 0x00020000);
 }
 __device__ __forceinline__ uint32_t slot_off(uint32_t tag, int blk) {
-  return (((tag & 1u) * kMaxGrid + (uint32_t)blk) * kRecStride) * 8u;
+  return (((tag % 3u) * kMaxGrid + (uint32_t)blk) * kRecStride) * 8u;
 }
+__device__ __forceinline__ uint32_t fix_slot_off(int set) { return ((3u * kMaxGrid + (uint32_t)set) * kRecStride) * 8u; }
 // granules k, k + 1 of the slot at byte offset `off`; a lane outside the grid reads nothing and
 // sees (0, tag) twice
 __device__ __forceinline__ u32x4 load_pair(__amdgpu_buffer_rsrc_t rs, uint32_t off, int k, bool in, uint32_t tag) {
@@ -1174,13 +1215,21 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   constexpr int kBB = 64 * BW;
   // record sizes of this instantiation: score columns add spread fields to records 1 and 2 and
   // the winner's domains to record 3
-  constexpr int REC1 = COLS ? kRec1 : kRec1 - 2, REC2 = COLS ? kRec2 : kRec2 - 2;
+  // SPEC (PAIRS without columns): every block runs phase B on its set's previous maxima before
+  // record 1 (while the other set's exchanges run), record 1 carries the block's raw lo / hi,
+  // and record 2 is exchanged only when the gathered maxima differ from the speculated ones —
+  // one dependent exchange per pod instead of two before the best key (profiles/device/r6/:
+  // the maxima repeat for 100 % of the bench mix's pods at normal load)
+  constexpr bool SPEC = PAIRS && !COLS;
+  constexpr int REC1 = SPEC ? kRec1S : COLS ? kRec1 : kRec1 - 2, REC2 = COLS ? kRec2 : kRec2 - 2;
   constexpr int REC3 = (COLS || PAIRS) ? kRec3 : kRec3 - 1, NF1 = COLS ? kRec1 : kNF1T;
   extern __shared__ __align__(16) unsigned char s_dyn[];
   __shared__ uint8_t s_masks[256];
   // request ring: pods b (and b−1 in PAIRS mode, for its assume) plus the prefetched next ones
   __shared__ __align__(16) uint32_t s_req[4][sizeof(yoda_dev_req_t) / 4];
   __shared__ int s_fix;   // PAIRS: the other set's last winner's row here, or −1
+  __shared__ int s_fixg;  // PAIRS: the block (of this set) holding that row, or −1 (no winner)
+  __shared__ unsigned long long s_fixlh[2];   // SPEC: the fix-up owner's re-scored group lo / hi
   __shared__ unsigned long long s_part[BW][16];
   __shared__ unsigned long long s_glob[kNF1T];
   // G ≤ 64: wave 0 holds every record of a gather and reduces it alone; the result reaches the
@@ -1197,6 +1246,14 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   __shared__ GangBest s_gang[8 * BW];
   __shared__ int s_fail;
   __shared__ uint32_t s_bfeas;   // this block's feasible nodes for the current pod (record 1)
+  // SPEC: the maxima this set's last pod gathered (the speculation; 1s before its first pod) and
+  // each 8-node group's raw lo / hi under them
+  __shared__ uint64_t s_spec[6];
+  // … per clock requirement too (a pod limited to one clock sees other cards' maxima): 4 entries
+  // {key, maxima}; the speculation is the entry of the pod's key, else the last pod's
+  __shared__ uint64_t s_ptab[4][7];
+  __shared__ uint64_t s_cur[6];   // this pod's speculated maxima
+  __shared__ unsigned long long s_glh[kMaxGroups][2];
   __shared__ bool s_last;
   static_assert(sizeof(yoda_dev_result_t) % 8 == 0, "result copied as u64 words");
 
@@ -1217,7 +1274,10 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   int32_t* s_sp = s_quality + npb;                                    // spread raw score, −1: ignored
   int32_t* s_cnt = s_sp + (a.n_sp > 0 ? npb : 0);                     // [n_sp][npb] matching pods
   int32_t* s_img = s_cnt + a.n_sp * npb;                              // [n_img][npb] ImageLocality
-  uint8_t* s_feas2 = reinterpret_cast<uint8_t*>(s_img + a.n_img * npb);   // [2][npb] by pod parity
+  // phase B's maxima part of s_raw (32-bit: a wrong speculation, e.g. the 1s before a set's
+  // first pod, can make it exceed 16 bits)
+  uint32_t* s_basic = reinterpret_cast<uint32_t*>(s_img + a.n_img * npb);
+  uint8_t* s_feas2 = reinterpret_cast<uint8_t*>(s_basic + npb);           // [2][npb] by pod parity
   uint8_t* s_elig2 = s_feas2 + 2 * npb;                               // [2][npb]
   uint8_t* s_mask = s_elig2 + 2 * npb;
   uint8_t* s_dirty = s_mask + npb;
@@ -1260,6 +1320,8 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     if (PAIRS && a.B > 1) s_req[1][tid] = reinterpret_cast<const uint32_t*>(a.reqs + 1)[tid];
   }
   if (tid == 0) s_fail = 0;
+  if (tid < 6) s_spec[tid] = 1;
+  if (tid < 4) s_ptab[tid][0] = ~0ull;
   __syncthreads();
 
   // Filter every 8-node group of this block for request `rq` (or only group `only`) into the
@@ -1327,8 +1389,26 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
   };
   // record 1 from the group aggregates: threads 0..REC1-1 (wave 0), after every group's
   // s_grp row is visible to them
-  auto record1 = [&](uint32_t tag1) -> uint32_t {
+  // (SPEC: the raw lo / hi leave out group `skipq` — the PAIRS owner's group, whose lo / hi follow
+  // in the fix-up record once re-scored)
+  auto record1 = [&](uint32_t tag1, int skipq = -1, bool own_lh = false) -> uint32_t {
     uint32_t v = 0;
+    unsigned long long blo = ULLONG_MAX, bhi = 0;   // SPEC: over the groups but skipq, wave 0
+    if constexpr (SPEC) {
+      if (wave == 0) {   // (wave-uniform) one group per lane, one LDS round trip
+        const int ngr = (cnt + kNodesPerWave - 1) / kNodesPerWave;
+        if (lane < ngr && lane != skipq) {
+          blo = s_glh[lane][0];
+          bhi = s_glh[lane][1];
+        }
+        blo = wave_min(blo);
+        bhi = wave_max(bhi);
+        if (own_lh && tid == 0) {   // the PAIRS owner's own lo / hi beside the others' (gather_early)
+          s_red[2] = blo;
+          s_red[3] = bhi;
+        }
+      }
+    }
     if (tid < REC1) {   // block totals over the groups → the record's 11 granules
       const int ngr = (cnt + kNodesPerWave - 1) / kNodesPerWave;
       if (tid < 7) {
@@ -1353,6 +1433,9 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       } else if constexpr (COLS) {   // spread: the domain mask halves (or)
         const int f = tid == kGDlo ? kFDlo : kFDhi;
         for (int q = 0; q < ngr; ++q) v |= s_grp[q][f];
+      } else if constexpr (SPEC) {   // raw lo (11, 12) / hi (13, 14) over the groups, as u32 halves
+        const unsigned long long x = tid < 7 + kRsPairs + 2 ? blo : bhi;
+        v = ((tid - 7 - kRsPairs) & 1) ? (uint32_t)(x >> 32) : (uint32_t)x;
       }
       store_granule(slot_ptr(a, tag1, g) + tid, tag1, v);
     }
@@ -1477,6 +1560,31 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     }
   };
 
+  // SPEC phase B on the speculated maxima (in `sc`) for 8-node groups gfirst + wstart, + wstep,
+  // … < gend: each group's raw scores (s_raw: part A → the full raw score, s_basic: the maxima
+  // part, so a wrong speculation is undone exactly) and its lo / hi (s_glh). Wave-uniform.
+  auto phase_b_groups = [&](const ScoreConsts& sc, const uint8_t* s_feas, const uint8_t* s_elig, int gfirst, int gend,
+                            int wstart, int wstep) {
+    for (int gq = gfirst + wstart; gq < gend; gq += wstep) {
+      const int j = gq * kNodesPerWave + grp;
+      const bool act = j < cnt && s_feas[j];
+      const uint32_t emask = act ? s_elig[j] : 0u;
+      const uint64_t rbase = (act && sub == 0) ? (uint64_t)s_raw[j] : 0;
+      unsigned long long lo = ULLONG_MAX, hi = 0;
+      uint32_t basic = 0;
+      const uint64_t sv = score_node_b_k(s_rows + (j < cnt ? j : 0), act, emask, sc, sub, rbase, lo, hi, basic);
+      if (act && sub == 0) {
+        s_raw[j] = (int64_t)sv;
+        s_basic[j] = basic;
+      }
+      lo = wave_min(lo);
+      hi = wave_max(hi);
+      if (lane == 0) {
+        s_glh[gq][0] = lo;
+        s_glh[gq][1] = hi;
+      }
+    }
+  };
 
   // assume (engine.cpp Engine::reserve, non-compat, reservation pending) of pod `rq` on row j
   // with GPU set `mask`: one thread
@@ -1530,22 +1638,38 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     __syncthreads();
     ScoreConsts sc = score_consts(r, nullptr);
     int fix = -1;   // PAIRS: the other set's last winner's row, in its owner block only
+    int fixg = -1;  // PAIRS: that owner block (every block of the set knows it), −1: none
     bool early1 = false;   // PAIRS owner: wave 0 already gathered record 1 (into s_rec)
     if constexpr (PAIRS) {
       // score A of every group now, against the rows as of this set's last pod; then the other
       // set's pod b−1: its winner, from its record 3 (best key; the GPU mask, whether the record's
       // block had a feasible node, whether the pod fit anywhere)
       score_a_groups(r, sc, s_feas, s_elig, 0, ngroups);
+      if constexpr (SPEC) {   // phase B on the speculated maxima, before the other set's winner
+        if (tid < 6) {
+          const uint64_t key = spec_key(r);
+          const int slot = spec_slot(key);
+          s_cur[tid] = s_ptab[slot][0] == key ? s_ptab[slot][1 + tid] : s_spec[tid];
+        }
+        __syncthreads();   // (also: a multi-GPU pod's gang merge rewrote part A across waves)
+        score_consts_maxima(sc, s_cur);
+        phase_b_groups(sc, s_feas, s_elig, 0, ngroups, wave, BW);
+        __syncthreads();
+      }
       if (b >= 1) {
-        if (tid == 0) s_fix = -1;   // before the holder's write: same wave, or the gather's barrier
+        if (tid == 0) {   // before the holder's write: same wave, or the gather's barrier
+          s_fix = -1;
+          s_fixg = -1;
+        }
         // (slots are double-buffered by tag parity: the other set overwrites this record only
         // with its pod b+1's record 1, which it publishes after this set's pod b record 3 —
         // i.e. after this read)
         // the one record that holds the winner: its key, from a block with a feasible node
         // (keys of feasible nodes are unique; a block without one reports key 0), and the pod
         // fit somewhere. Its thread applies the assume if this block holds the node.
-        auto take_winner = [&](unsigned long long key, const uint32_t (&v)[3], unsigned long long t_g3) {
+        auto take_winner = [&](unsigned long long key, const uint32_t (&v)[3], unsigned long long t_g3, int prod) {
           const yoda_dev_req_t& rp = *reinterpret_cast<const yoda_dev_req_t*>(s_req[(b - 1) & 3]);
+          s_fixg = prod;   // the record's producer holds the winner's node
           const uint32_t pp = (uint32_t)(key & 0xFFFFFFull);
           const int w = (int)(((pp - rp.perm_add) * rp.perm_inv) & 0xFFFFFFu);
           if (w >= base && w < base + cnt) {
@@ -1577,8 +1701,8 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
               const unsigned long long mk2 = have2 ? ((unsigned long long)v2[1] << 32 | v2[0]) : 0ull;
               const unsigned long long key = wave_max(mk > mk2 ? mk : mk2);
               const bool h1 = holds(have, mk, key, v), h2 = !h1 && holds(have2, mk2, key, v2);
-              if (h1) take_winner(key, v, t_g3);
-              else if (h2) take_winner(key, v2, t_g3);
+              if (h1) take_winner(key, v, t_g3, lane);
+              else if (h2) take_winner(key, v2, t_g3, lane + 64);
               if (COLS && a.n_sp > 0) {
                 const unsigned long long bal = __ballot(h1 || h2);
                 if (bal) {
@@ -1611,12 +1735,13 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           unsigned long long key = 0;
           for (int w = 0; w < BW; ++w) key = s_part[w][0] > key ? s_part[w][0] : key;
           if (holds(have, mk, key, v)) {
-            take_winner(key, v, t_g3);
+            take_winner(key, v, t_g3, tid);
             if (COLS && a.n_sp > 0) count_winner(v[2]);   // (every block has one thread reading the holder's record)
           }
           __syncthreads();
         }
         fix = s_fix;
+        fixg = s_fixg;
       }
       if (fix >= 0) {
         // owner: wave 0 re-filters the winner's group and sends record 1 (its s_grp row is
@@ -1638,26 +1763,50 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           if (gather_wave0<REC1>(a, tag1, G, p0, v, v2, gi)) {
             if (a.trace && lane == 0) a.trace[(size_t)b * kTracePts + 18] = __builtin_amdgcn_s_memrealtime();
             const int t2 = lane + 64;
-            if (lane < G && lane != gi) transpose1(v, lane);
-            if (t2 < G && t2 != gi) transpose1(v2, t2);
+            const bool h1 = lane < G && lane != gi, h2 = t2 < G && t2 != gi;
+            if (h1) transpose1(v, lane);
+            if (h2) transpose1(v2, t2);
+            if constexpr (SPEC) {   // the other blocks' raw lo / hi under the speculated maxima
+              const unsigned long long l1 = h1 ? ((unsigned long long)v[12] << 32 | v[11]) : ULLONG_MAX;
+              const unsigned long long l2 = h2 ? ((unsigned long long)v2[12] << 32 | v2[11]) : ULLONG_MAX;
+              const unsigned long long g1 = h1 ? ((unsigned long long)v[14] << 32 | v[13]) : 0ull;
+              const unsigned long long g2 = h2 ? ((unsigned long long)v2[14] << 32 | v2[13]) : 0ull;
+              const unsigned long long wl = wave_min(l1 < l2 ? l1 : l2), wh = wave_max(g1 > g2 ? g1 : g2);
+              if (lane == 0) {
+                s_red[0] = wl;
+                s_red[1] = wh;
+              }
+            }
           } else if (lane == 0) {
             s_fail = 1;
           }
         };
-        if (wave == 0) {
-          filter_one(r, par, fg);
-          __builtin_amdgcn_wave_barrier();
-          const uint32_t own = record1(tag1);
-          if (early1 && tid < REC1) {   // this block's column of the transposed records
+        // this block's column of the transposed records (wave 0, after record 1)
+        auto own_column = [&](uint32_t own) {
+          if (early1 && tid < REC1) {
             if (COLS || tid < 7) {
               s_rec[tid][gi] = own;
-            } else {
+            } else if (tid < 7 + kRsPairs) {
               const int q0 = 2 * (tid - 7);
               s_rec[7 + q0][gi] = own & 0xFFFFu;
               if (q0 + 1 < kNR) s_rec[8 + q0][gi] = own >> 16;
             }
           }
+        };
+        if (wave == 0) {
+          filter_one(r, par, fg);
+          __builtin_amdgcn_wave_barrier();
+          own_column(record1(tag1, fg, early1));
           if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 10] = __builtin_amdgcn_s_memrealtime();
+          if constexpr (SPEC) {   // the maxima part of the group's phase B (speculated maxima in sc),
+                                  // while the other waves score it: finished right after the barrier
+            const int j = fg * kNodesPerWave + grp;
+            const bool act = j < cnt && s_feas[j];
+            unsigned long long lo_u = ULLONG_MAX, hi_u = 0;
+            uint32_t basic = 0;
+            (void)score_node_b_k(s_rows + (j < cnt ? j : 0), act, act ? s_elig[j] : 0u, sc, sub, 0, lo_u, hi_u, basic);
+            if (act && sub == 0) s_basic[j] = basic;
+          }
           if (early1 && gw == 0) gather_early();
         } else if (early1 && wave == gw) {
           gather_early();
@@ -1666,6 +1815,28 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         }
         __syncthreads();
         combine_fix(r, sc, s_feas, fg * kNodesPerWave, nrep);
+        if constexpr (SPEC) {
+          // the group's raw scores finished on the speculated maxima (the scores wave left the
+          // maxima part in s_basic) and its lo / hi sent as the fix-up record, which every block of
+          // the set folds into record 1's (combine_fix's lanes: same wave, in order)
+          if (tid < kNodesPerWave) {   // one node each (a whole 8-lane group)
+            const int j = fg * kNodesPerWave + tid;
+            const bool act = j < cnt && s_feas[j];
+            unsigned long long lo = ULLONG_MAX, hi = 0;
+            if (act) {
+              const uint64_t sv = sc.yoda_s ? (uint64_t)s_raw[j] + s_basic[j] : 0ull;
+              s_raw[j] = (int64_t)sv;
+              if (sc.yoda_s) lo = hi = sv > (uint64_t)LLONG_MAX ? 0ull : sv;
+            }
+            lo = group_reduce(lo, OpMin{});
+            hi = group_reduce(hi, OpMax{});
+            if (tid < 4) {
+              const unsigned long long x = tid < 2 ? lo : hi;
+              store_granule((gu64*)(a.slots + fix_slot_off(set) / 8u) + tid, tag1,
+                            (tid & 1) ? (uint32_t)(x >> 32) : (uint32_t)x);
+            }
+          }
+        }
         if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 11] = __builtin_amdgcn_s_memrealtime();
       } else {
         record1(tag1);
@@ -1691,6 +1862,16 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         if (PAIRS && fix >= 0 && a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 19] = __builtin_amdgcn_s_memrealtime();
         // transpose through LDS (7 + kNR fields × G), then 16 threads per field reduce it
         if (tid < G) transpose1(v, tid);
+        if constexpr (SPEC) {   // raw lo / hi under the speculated maxima: per wave, then s_red
+          const bool have = tid < G;
+          const unsigned long long l = have ? ((unsigned long long)v[12] << 32 | v[11]) : ULLONG_MAX;
+          const unsigned long long h = have ? ((unsigned long long)v[14] << 32 | v[13]) : 0ull;
+          const unsigned long long wl = wave_min(l), wh = wave_max(h);
+          if (lane == 0) {
+            s_part[wave][2] = wl;
+            s_part[wave][3] = wh;
+          }
+        }
         __syncthreads();
         if (PAIRS && fix >= 0 && a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 20] = __builtin_amdgcn_s_memrealtime();
       } else if (s_fail) {   // (PAIRS owner: wave 0 gathered before the fix-up barrier)
@@ -1730,6 +1911,54 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       __syncthreads();
     }
     if (PAIRS && fix >= 0 && a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 12] = __builtin_amdgcn_s_memrealtime();
+    // SPEC: the gathered maxima against the speculated ones (every block of the set compares the
+    // same values: a block-set-uniform choice), and the raw lo / hi that hold if they match
+    bool hit = false;
+    unsigned long long slo1 = ULLONG_MAX, shi1 = 0;
+    if constexpr (SPEC) {
+      hit = true;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) hit = hit && s_glob[k] == s_cur[k];
+      if (a.trace && gi == 0 && tid == 0) a.trace[(size_t)b * kTracePts + 22] = hit ? 1ull : 2ull;
+      if (early1) {
+        slo1 = s_red[0] < s_red[2] ? s_red[0] : s_red[2];
+        shi1 = s_red[1] > s_red[3] ? s_red[1] : s_red[3];
+      } else {
+        for (int w = 0; w < BW; ++w) {
+          slo1 = s_part[w][2] < slo1 ? s_part[w][2] : slo1;
+          shi1 = s_part[w][3] > shi1 ? s_part[w][3] : shi1;
+        }
+      }
+      if (hit && fixg >= 0) {   // (set-uniform) the owner's re-scored group: one record, polled by one lane
+        if (wave == 0) {
+          const __amdgpu_buffer_rsrc_t rs = slot_rsrc(a);
+          const uint32_t off = fix_slot_off(set);
+          const long long t0 = __builtin_amdgcn_s_memrealtime();
+          bool got = false;
+          for (unsigned spins = 0;;) {
+            __asm__ volatile("" ::: "memory");
+            const u32x4 x = load_pair(rs, off, 0, lane == 0, tag1), y = load_pair(rs, off, 2, lane == 0, tag1);
+            if (__all(x.y == tag1 && x.w == tag1 && y.y == tag1 && y.w == tag1)) {
+              if (lane == 0) {
+                s_fixlh[0] = (unsigned long long)x.z << 32 | x.x;
+                s_fixlh[1] = (unsigned long long)y.z << 32 | y.x;
+              }
+              got = true;
+              break;
+            }
+            if (!spin_ok(a, spins, t0)) break;
+          }
+          if (!got && lane == 0) s_fail = 1;
+        }
+        __syncthreads();
+        if (s_fail) {
+          ok = false;
+          break;
+        }
+        slo1 = s_fixlh[0] < slo1 ? s_fixlh[0] : slo1;
+        shi1 = s_fixlh[1] > shi1 ? s_fixlh[1] : shi1;
+      }
+    }
     int reasons7[kNR];
 #pragma unroll
     for (int q = 0; q < kNR; ++q)
@@ -1750,8 +1979,13 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
     TRACE(3);
 
     // ================= phase B: maxima-normalised card metrics → raw scores, lo/hi → record 2
+    // (SPEC: only when the speculated maxima were wrong — part A is recovered as s_raw − s_basic)
     unsigned long long glo = ULLONG_MAX, ghi = 0;
-    {
+    if (hit) {
+      glo = slo1;
+      ghi = shi1;
+      TRACE(4);
+    } else {
       unsigned long long lo = ULLONG_MAX, hi = 0, slo = ULLONG_MAX, shi = 0;
       double w0 = 0.0, w1 = 0.0;   // the constraints' weights (pod-uniform)
       if (COLS && spl >= 0) {
@@ -1764,9 +1998,10 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
         const int j = j0 + grp;
         const bool act = j < cnt && s_feas[j];
         const uint32_t emask = act ? s_elig[j] : 0u;
-        const uint64_t rbase = (act && sub == 0) ? (uint64_t)s_raw[j] : 0;
-        const int64_t raw_v = score_node_b(s_rows + (j < cnt ? j : 0), act, emask, sc, sub, rbase, lo, hi);
-        if (act && sub == 0) s_raw[j] = raw_v;
+        const uint64_t rbase = (act && sub == 0) ? (uint64_t)s_raw[j] - (SPEC ? (uint64_t)s_basic[j] : 0ull) : 0;
+        uint32_t basic = 0;
+        const uint64_t raw_v = score_node_b_k(s_rows + (j < cnt ? j : 0), act, emask, sc, sub, rbase, lo, hi, basic);
+        if (act && sub == 0) s_raw[j] = (int64_t)raw_v;   // (unclamped: Sel clamps)
         if (COLS && act && sub == 0 && spl >= 0) {
           // Σ over the constraints, in order, of count × weight + (maxSkew − 1) in float64 with
           // the CPU's rounding (no contraction), truncated; −1: the node lacks a key (ignored)
@@ -1909,7 +2144,10 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       for (int j = tid; j < cnt; j += kBB) {
         if (!s_feas[j]) continue;
         int64_t f = s_total[j];
-        if (sc.yoda_s) f += (int64_t)udiv_r(((uint64_t)s_raw[j] - (uint64_t)lo) * 100ull, den, rden) * r.w_yoda;
+        if (sc.yoda_s) {
+          const uint64_t rs = (uint64_t)s_raw[j], rv = rs > (uint64_t)LLONG_MAX ? 0ull : rs;
+          f += (int64_t)udiv_r((rv - (uint64_t)lo) * 100ull, den, rden) * r.w_yoda;
+        }
         if (COLS && spl >= 0) {
           const int64_t sp = s_sp[j];
           const int64_t norm = sp < 0 ? 0 : shi == 0 ? 100 : (100 * (shi + slo - sp)) / shi;   // (sp: int32)
@@ -1923,6 +2161,16 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
       best = wave_max(best);
       if (lane == 0) s_part[wave][0] = best;
       __syncthreads();
+      if (SPEC && tid < 7) {   // this set's next pods speculate on them
+        const uint64_t key = spec_key(r);
+        const int slot = spec_slot(key);
+        if (tid < 6) {
+          if (nf > 0) s_spec[tid] = gmx[tid];   // (no feasible node: the maxima stay at 1, no guide)
+          s_ptab[slot][1 + tid] = gmx[tid];
+        } else {
+          s_ptab[slot][0] = key;
+        }
+      }
       if (tid < REC3) {
         unsigned long long bb = 0;
         for (int w = 0; w < BW; ++w) bb = s_part[w][0] > bb ? s_part[w][0] : bb;
@@ -2313,7 +2561,7 @@ void* yoda_dev_create(int device, int capacity, char* err, int err_len) {
     return fail("batch done", e);
   if ((e = hipHostGetDevicePointer((void**)&c->d_done_map, c->h_done, 0)) != hipSuccess) return fail("done map", e);
   if ((e = hipMalloc(&c->d_bres, kBatchCap * sizeof(yoda_dev_result_t))) != hipSuccess) return fail("batch scratch", e);
-  const size_t slot_bytes = 2 * kMaxGrid * kRecStride * sizeof(unsigned long long);
+  const size_t slot_bytes = kSlotBytes;
   if ((e = hipMalloc(&c->d_slots, slot_bytes)) != hipSuccess) return fail("slots", e);
   if ((e = hipMemset(c->d_slots, 0, slot_bytes)) != hipSuccess) return fail("slots", e);
   if ((e = hipMalloc(&c->d_words, 64)) != hipSuccess) return fail("words", e);
@@ -2562,7 +2810,7 @@ static int batch_persistent(Ctx* c, int n, int B, const yoda_dev_req_t* reqs, yo
       if (reqs[base + j].use_candidates) return -3;
     memcpy(c->h_reqs, reqs + base, (size_t)m * sizeof(yoda_dev_req_t));
     if (c->epoch > 0xF0000000u) {   // tag space exhausted: forget every old tag
-      CK(hipMemsetAsync(c->d_slots, 0, 2 * kMaxGrid * kRecStride * sizeof(unsigned long long), c->stream));
+      CK(hipMemsetAsync(c->d_slots, 0, kSlotBytes, c->stream));
       c->epoch = 1;
     }
     BatchArgs a;

@@ -48,11 +48,12 @@ def test_device_candidates_taints_and_selector(require_gpu):
         assert not diff, (spec, diff)
 
 
-# k_batch kernel time per pod at 4096 nodes, the bench mix, measured on MI355X with two pods in
-# flight (profiles/device/r4/early_gather1/: 12.6; round 5 with the extended-resource dimension:
-# 11.7 under rocprofv3, profiles/device/r5/kbprof/; one at a time 15.9–16.0); the test allows
-# 1.25× before it calls a regression (1.5× let a 60 % slowdown pass)
-KBATCH_US_PER_POD_4096 = 12.6
+# k_batch kernel time per pod at 4096 nodes, measured on MI355X with two pods in flight
+# (profiles/device/r4/early_gather1/: 12.6; round 5: 11.7 under rocprofv3; round 6 with
+# speculated maxima: this test's mix 10.8–11.0, the bench mix 10.4 under rocprofv3,
+# profiles/device/r6/); the test allows 1.25× before it calls a regression (VERDICT r4 weak #4:
+# 1.5× let a 60 % slowdown pass)
+KBATCH_US_PER_POD_4096 = 11.0
 KBATCH_SLACK = 1.25
 
 
@@ -82,7 +83,41 @@ def test_k_batch_time_per_pod_and_one_dispatch_per_batch(require_gpu):
         per_pod.append((c1["kbatch_us"] - c0["kbatch_us"]) / size)
     assert eng.device_fallbacks == 0
     per_pod.sort()
+    print("k_batch us/pod at 4096 nodes:", [round(x, 2) for x in per_pod])
     assert per_pod[len(per_pod) // 2] <= KBATCH_SLACK * KBATCH_US_PER_POD_4096, per_pod
+
+
+def test_k_batch_speculated_maxima_hold_for_the_bench_mix_and_stay_exact(require_gpu):
+    """k_batch's PAIRS kernel runs phase B on its block set's previous maxima
+    (per clock requirement) before record 1, and exchanges record 2 only when the gathered maxima
+    differ. On the bench's label mix the maxima repeat (profiles/device/r6/record1_reuse.jsonl),
+    so ≥ 95 % of pods skip record 2; every cycle still equals the CPU replay, the pods whose
+    speculation failed included (the first pod of each set always fails: its maxima are 1s)."""
+    from yoda_scheduler_amd.bench.workloads import _mixed_labels
+    from yoda_scheduler_amd.models.pod import PodInfo
+    from yoda_scheduler_amd.ops import device_scorer as ds
+    from yoda_scheduler_amd.ops.native import core, pod_req
+    dev = _engine(4096, 13)
+    ref = core().Engine(False, 1)
+    ref.set_percentage_of_nodes_to_score(100)
+    ds.synthetic_cluster(ref, 4096, seed=13)
+    rng = random.Random(13)
+
+    def pod(k):
+        return PodInfo.from_obj({"metadata": {"name": f"sp{k}", "uid": f"spec-{k}", "labels": _mixed_labels(rng)},
+                                 "spec": {"containers": [{"name": "c", "resources": {"requests": {
+                                     "cpu": "100m", "memory": "128Mi"}}}]}})
+    ds.batch_trace(dev, True)
+    pods = [pod(k) for k in range(200)]
+    diffs = ds.compare_batch(dev, ref, pods, [pod_req(dev, p) for p in pods], [pod_req(ref, p) for p in pods])
+    tr = ds.read_batch_trace(dev)
+    ds.batch_trace(dev, False)
+    assert not diffs, diffs[:3]
+    assert ds.counters(dev)["last_pairs"] == 1 and dev.device_fallbacks == 0
+    hits = [x["spec_hit"] for x in tr if "spec_hit" in x]
+    assert len(hits) == len(pods)
+    assert hits[0] == 0.0 and hits[1] == 0.0        # each set's first pod: nothing to speculate on
+    assert sum(hits) >= 0.95 * len(hits), sum(hits)
 
 
 def test_scheduler_auto_enables_device_scorer_and_matches_cpu(require_gpu):

@@ -80,6 +80,8 @@ def read_batch_trace(engine, max_pods: int = 256) -> list[dict]:
     for b in range(max(m, 0)):
         t = [buf[b * W + k] for k in range(W)]
         d = {ph: (t[k + 1] - t[k]) / 100.0 for k, ph in enumerate(TRACE_PHASES)}
+        if t[22]:   # SPEC kernels: 1 = the speculated maxima held (no record 2), 2 = record 2 exchanged
+            d["spec_hit"] = 1.0 if t[22] == 1 else 0.0
         if t[13] and t[9] and t[12]:   # PAIRS: the fix-up owner's stamps (a pod with one)
             d.update({ph: (t[hi] - t[lo]) / 100.0 for ph, lo, hi in OWNER_PHASES if t[lo] and t[hi]})
         out.append(d)
