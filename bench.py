@@ -173,6 +173,10 @@ def main(argv=None) -> int:
     ap.add_argument("--mix-spread", type=int, default=0,
                     help="beyond BASELINE: give this many pods of the burst (evenly spread; 1000 = all) a hostname "
                          "DoNotSchedule topologySpreadConstraint (native PodTopologySpread since round 5)")
+    ap.add_argument("--mix-preempt", type=int, default=0,
+                    help="beyond BASELINE: fill every GPU with bound low-priority pods, then burst this many "
+                         "priority-100 pods that must preempt (DefaultPreemption); use with --transport inproc "
+                         "(a fresh cluster every step)")
     ap.add_argument("--mix-hostports", type=int, default=0,
                     help="beyond BASELINE: this many pods of the burst (evenly spread; 1000 = all) request a distinct "
                          "host port (native NodePorts since round 5)")
@@ -203,6 +207,8 @@ def main(argv=None) -> int:
     a = ap.parse_args(argv)
     if a.reference_qps:
         a.qps, a.burst = 50.0, 100
+    if a.mix_preempt and a.transport != "inproc":
+        ap.error("--mix-preempt needs --transport inproc (every step on a freshly filled cluster)")
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -262,6 +268,7 @@ def main(argv=None) -> int:
     from yoda_scheduler_amd.bench.workloads import make_workload
     w = make_workload(a.config, seed=rank, node_gpus=a.node_gpus, nodes=a.nodes, mix_anti=a.mix_anti,
                       mix_spread=a.mix_spread, mix_volumes=a.mix_volumes, mix_hostports=a.mix_hostports,
+                      mix_preempt=a.mix_preempt,
                       cluster=a.cluster)
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
@@ -553,6 +560,15 @@ def main(argv=None) -> int:
             "telemetry": tels[0],
             "host": dict(host_info(), pinned_cpus=pinned),
         }
+        if a.mix_preempt:
+            # the preemptors' PostFilter (DefaultPreemption) over every step, warmup included: calls,
+            # nominations, victims deleted, ms per call (native search + victim deletion + hold).
+            # A preemptor binds after its first retry, upstream's podInitialBackoffSeconds (1 s here)
+            from yoda_scheduler_amd.plugins.defaults import DefaultPreemption
+            S = DefaultPreemption.stats
+            out["preemption"] = {"calls": S["calls"], "nominated": S["nominated"], "victims": S["victims"],
+                                 "ms_per_call": round(S["seconds"] / S["calls"] * 1e3, 3) if S["calls"] else None,
+                                 "backoff_s": 1}
         if alt is not None:
             out["alt"] = alt      # the other transport, measured after the headline's timed region
         print(json.dumps(out), flush=True)

@@ -104,7 +104,7 @@ class Shard:
         while True:
             if len(srv.bind_log) >= n:
                 break
-            if not q._active_entries and self.sched.pending_binds == 0 and \
+            if not w.wait_bound and not q._active_entries and self.sched.pending_binds == 0 and \
                     len(srv.bind_log) + len(q._unsched) + len(q._backoff_pods) >= n:
                 break
             if time.perf_counter() > deadline:

@@ -49,6 +49,8 @@ class Workload:
     metas: dict = field(default_factory=dict)        # pod index → extra metadata fields (ownerReferences)
     objects: list = field(default_factory=list)      # (resource, object) created with the cluster (PVCs, PVs)
     cluster: str = "synthetic"                       # "kind": realistic node/cluster objects (populate)
+    wait_bound: bool = False                         # a burst ends when every pod is bound (preemptors
+                                                     # park in backoff while their victims go)
 
     @property
     def n_pods(self) -> int:
@@ -71,7 +73,7 @@ def _mixed_labels(rng: random.Random) -> dict:
 def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None,
                   node_gpus: Optional[int] = None, nodes: Optional[int] = None, mix_anti: int = 0,
                   cluster: str = "synthetic", mix_spread: int = 0, mix_volumes: int = 0,
-                  mix_hostports: int = 0) -> Workload:
+                  mix_hostports: int = 0, mix_preempt: int = 0) -> Workload:
     """``node_gpus`` overrides the GPUs per node (BASELINE.md protocol item 5: every
     config at 1, 2, 4 and 8 GPUs per node); pods keep their labels, so e.g. ``scv/number: 8``
     pods are unschedulable on smaller nodes and are reported as such. ``nodes`` resizes
@@ -122,6 +124,8 @@ def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None,
             spec["containers"] = [c]
             w.specs[i] = spec
         w.name += f" + {count} host-port pods"
+    if mix_preempt:
+        _preempt_burst(w, mix_preempt, seed)
     if nodes is not None:
         if cfg != 6 or nodes < 1:
             raise ValueError("nodes: config 6 only, >= 1")
@@ -169,6 +173,44 @@ def _make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None) -> 
     else:
         raise ValueError(f"unknown config {cfg}")
     return w
+
+
+# ---------------------------------------------------------------- preemption (--mix-preempt)
+def _preempt_burst(w: Workload, count: int, seed: int) -> None:
+    """Beyond BASELINE: a full cluster — every GPU of every node held by a
+    bound low-priority pod (priorities 0-5, one full card each, as ``scripts/preempt_bench.py``) —
+    and a burst of ``count`` priority-100 pods that each need one whole card. Each of them fails
+    the filters, DefaultPreemption (the native search, upstream v1.20 candidate pruning) picks a
+    node and victims, the victims are deleted through the API, and the pod binds once they are
+    gone. The fillers are cluster objects (``w.objects``): with ``--transport inproc`` every step
+    runs on a freshly populated shard, so every step preempts."""
+    rng = random.Random(seed * 104729 + count)
+    fillers = []
+    k = 0
+    for name, spec, gpus in w.nodes:
+        for g in range(gpus):
+            mb = spec.hbm_mb
+            fillers.append(("pods", {
+                "apiVersion": "v1", "kind": "Pod",
+                "metadata": {"name": f"filler-{k}", "namespace": "default",
+                             "labels": {"app": f"job-{k % 17}", "scv/memory": str(mb)},
+                             "annotations": {"scv.amd.com/gpus": str(g), "scv.amd.com/reserved-mb": str(mb)}},
+                "spec": {"schedulerName": w.scheduler_name, "nodeName": name, "priority": rng.randint(0, 5),
+                         "containers": [{"name": "main", "image": "rocm/pytorch:latest",
+                                         "resources": {"requests": {"cpu": "100m", "memory": "128Mi"}}}]},
+                "status": {"phase": "Running"}}))
+            k += 1
+    count = min(count, k)
+    # three quarters of a card: the card's Scv telemetry (jittered, or a real amd-smi sample with
+    # the driver's own use) never reports it entirely free, so a whole-card request would fit
+    # only the few cards that happen to report full; any evicted filler's card fits this
+    mb = w.nodes[0][1].hbm_mb * 3 // 4
+    w.objects.extend(fillers)
+    w.pods = [{"scv/memory": str(mb)} for _ in range(count)]
+    w.specs = {i: {"priority": 100} for i in range(count)}
+    w.wait_bound = True
+    w.metas = {}
+    w.name += f" + full cluster ({k} low-priority pods), burst of {count} preemptors"
 
 
 # ---------------------------------------------------------------- PVC pods (--mix-volumes)
