@@ -177,6 +177,9 @@ def main(argv=None) -> int:
                     help="beyond BASELINE: fill every GPU with bound low-priority pods, then burst this many "
                          "priority-100 pods that must preempt (DefaultPreemption); use with --transport inproc "
                          "(a fresh cluster every step)")
+    ap.add_argument("--prefill", type=float, default=0.0,
+                    help="beyond BASELINE: this fraction of all cards is held whole by bound pods before the "
+                         "first step (a populated cluster: ledger, label index and device rows full of pods)")
     ap.add_argument("--mix-hostports", type=int, default=0,
                     help="beyond BASELINE: this many pods of the burst (evenly spread; 1000 = all) request a distinct "
                          "host port (native NodePorts since round 5)")
@@ -268,7 +271,7 @@ def main(argv=None) -> int:
     from yoda_scheduler_amd.bench.workloads import make_workload
     w = make_workload(a.config, seed=rank, node_gpus=a.node_gpus, nodes=a.nodes, mix_anti=a.mix_anti,
                       mix_spread=a.mix_spread, mix_volumes=a.mix_volumes, mix_hostports=a.mix_hostports,
-                      mix_preempt=a.mix_preempt,
+                      mix_preempt=a.mix_preempt, prefill=a.prefill,
                       cluster=a.cluster)
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)

@@ -775,6 +775,9 @@ class Server {
     std::vector<std::string> keys;
   };
   std::deque<BenchJob> jobs_;
+  // pods the bench bursts created: what a reset deletes (pods created through the API — a
+  // populated cluster's bound pods, `bench.py --prefill` — stay)
+  std::vector<std::string> bench_keys_;
   void handle_list(Conn* c, ResState& rs, const std::string& ns, const Request& req);
   void start_watch(Conn* c, ResState& rs, const std::string& ns, const Request& req);
   void finish_watch(Conn* c);
@@ -1113,7 +1116,9 @@ void Server::handle_bench(Conn* c, Request& req) {
   if (p == "/debug/bench/reset") {
     BenchJob job;
     job.del = true;
-    for (const auto& kv : pods.objs) job.keys.push_back(kv.first);
+    for (auto& k : bench_keys_)
+      if (pods.objs.count(k)) job.keys.push_back(std::move(k));
+    bench_keys_.clear();
     const size_t n = job.keys.size();
     jobs_.push_back(std::move(job));
     respond(c, 200, "{\"deleted\":" + std::to_string(n) + "}");
@@ -1165,11 +1170,14 @@ void Server::step_jobs() {
       SP s = make_stored_text(std::move(text), last_rv_, tt.ns, nullptr, {}, rv_at);
       pods.objs[key] = s;
       create_log_[key] = mono();
+      bench_keys_.push_back(key);
       emit(pods, 'A', s, nullptr);
     } else {
       Value o = templates_[i];
       o.at("metadata").at("name") = Value::str(name);
+      const std::string ns = o.at("metadata").get("namespace") ? o.at("metadata").at("namespace").s : "default";
       create(pods, std::move(o), "", &err);
+      bench_keys_.push_back(ns + "/" + name);
     }
   }
   job.next = end;

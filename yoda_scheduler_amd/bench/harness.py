@@ -302,7 +302,10 @@ class HttpShard:
             # on and charge a Python copy of every lane pod to each timed step)
             # (YODA_BENCH_RESET_SYNC=1 restores round 3's sync in this loop: same-box A/B only)
             old_sync = os.environ.get("YODA_BENCH_RESET_SYNC") == "1"
-            while ((old_sync and sched.cache.sync_lane() >= 0 and sched.cache.pods) or sched.cache.python_pods()
+            # (a populated cluster's bound pods — `--prefill` — stay: they are not the burst's)
+            keep = sum(1 for res, _o in self.w.objects if res == "pods")
+            while ((old_sync and sched.cache.sync_lane() >= 0 and len(sched.cache.pods) > keep)
+                   or sched.cache.python_pods() > keep
                    or q._active_entries or sched.pending_binds or sched.lane_owned()):
                 if trace is not None:
                     trace.append((round((time.perf_counter() - tr) * 1e3, 3), sched.lane_owned(), len(sched.cache.pods),

@@ -73,7 +73,7 @@ def _mixed_labels(rng: random.Random) -> dict:
 def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None,
                   node_gpus: Optional[int] = None, nodes: Optional[int] = None, mix_anti: int = 0,
                   cluster: str = "synthetic", mix_spread: int = 0, mix_volumes: int = 0,
-                  mix_hostports: int = 0, mix_preempt: int = 0) -> Workload:
+                  mix_hostports: int = 0, mix_preempt: int = 0, prefill: float = 0.0) -> Workload:
     """``node_gpus`` overrides the GPUs per node (BASELINE.md protocol item 5: every
     config at 1, 2, 4 and 8 GPUs per node); pods keep their labels, so e.g. ``scv/number: 8``
     pods are unschedulable on smaller nodes and are reported as such. ``nodes`` resizes
@@ -126,6 +126,8 @@ def make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None,
         w.name += f" + {count} host-port pods"
     if mix_preempt:
         _preempt_burst(w, mix_preempt, seed)
+    elif prefill > 0:
+        _prefill(w, prefill, seed)
     if nodes is not None:
         if cfg != 6 or nodes < 1:
             raise ValueError("nodes: config 6 only, >= 1")
@@ -175,6 +177,36 @@ def _make_workload(cfg: int, seed: int = 0, template: Optional[Card] = None) -> 
     return w
 
 
+# ---------------------------------------------------------------- populated cluster (--prefill)
+def _filler(w: Workload, k: int, node: str, g: int, mb: int, prio: int) -> tuple:
+    """A bound pod holding card ``g`` of ``node`` whole (its GPU annotation, as the scheduler
+    writes it at bind time), of one of 17 jobs."""
+    return ("pods", {
+        "apiVersion": "v1", "kind": "Pod",
+        "metadata": {"name": f"filler-{k}", "namespace": "default",
+                     "labels": {"app": f"job-{k % 17}", "scv/memory": str(mb)},
+                     "annotations": {"scv.amd.com/gpus": str(g), "scv.amd.com/reserved-mb": str(mb)}},
+        "spec": {"schedulerName": w.scheduler_name, "nodeName": node, "priority": prio,
+                 "containers": [{"name": "main", "image": "rocm/pytorch:latest",
+                                 "resources": {"requests": {"cpu": "100m", "memory": "128Mi"}}}]},
+        "status": {"phase": "Running"}})
+
+
+def _prefill(w: Workload, frac: float, seed: int) -> None:
+    """Beyond BASELINE: the burst lands on a populated cluster — a fraction
+    ``frac`` of all cards (a seeded choice) is held whole by bound pods, so the ledger, the label
+    index and the device rows start full of other pods, and the burst's pods fit only on the
+    free cards (the 8-GPU ones on wholly free nodes)."""
+    rng = random.Random(seed * 7717 + int(frac * 1000))
+    k = 0
+    for name, spec, gpus in w.nodes:
+        for g in range(gpus):
+            if rng.random() < frac:
+                w.objects.append(_filler(w, k, name, g, spec.hbm_mb, 0))
+                k += 1
+    w.name += f" + {k} pods already bound ({frac:.0%} of the cards)"
+
+
 # ---------------------------------------------------------------- preemption (--mix-preempt)
 def _preempt_burst(w: Workload, count: int, seed: int) -> None:
     """Beyond BASELINE: a full cluster — every GPU of every node held by a
@@ -189,16 +221,7 @@ def _preempt_burst(w: Workload, count: int, seed: int) -> None:
     k = 0
     for name, spec, gpus in w.nodes:
         for g in range(gpus):
-            mb = spec.hbm_mb
-            fillers.append(("pods", {
-                "apiVersion": "v1", "kind": "Pod",
-                "metadata": {"name": f"filler-{k}", "namespace": "default",
-                             "labels": {"app": f"job-{k % 17}", "scv/memory": str(mb)},
-                             "annotations": {"scv.amd.com/gpus": str(g), "scv.amd.com/reserved-mb": str(mb)}},
-                "spec": {"schedulerName": w.scheduler_name, "nodeName": name, "priority": rng.randint(0, 5),
-                         "containers": [{"name": "main", "image": "rocm/pytorch:latest",
-                                         "resources": {"requests": {"cpu": "100m", "memory": "128Mi"}}}]},
-                "status": {"phase": "Running"}}))
+            fillers.append(_filler(w, k, name, g, spec.hbm_mb, rng.randint(0, 5)))
             k += 1
     count = min(count, k)
     # three quarters of a card: the card's Scv telemetry (jittered, or a real amd-smi sample with

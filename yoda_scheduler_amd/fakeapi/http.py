@@ -63,6 +63,7 @@ class FakeApiHttp:
             self.app.router.add_get("/debug/bench/status", self._bench_status)
             self.app.router.add_post("/debug/bench/reset", self._bench_reset)
             self.bench_workload = None
+            self.bench_keys: list = []
         self.app.router.add_route("*", "/{tail:.*}", self.dispatch)
 
     @property
@@ -84,7 +85,8 @@ class FakeApiHttp:
         tag = body.get("tag", "b")
         self.server.reset_logs()
         for i, lab in enumerate(w.pods):
-            self.server.create("pods", pod_object(i, lab, w.scheduler_name, prefix=tag))
+            o = self.server.create("pods", pod_object(i, lab, w.scheduler_name, prefix=tag))
+            self.bench_keys.append((o["metadata"]["name"], o["metadata"].get("namespace", "default")))
             if i % 64 == 63:
                 await asyncio.sleep(0)
         return web.json_response({"n": len(w.pods)})
@@ -99,12 +101,17 @@ class FakeApiHttp:
         return web.json_response(out)
 
     async def _bench_reset(self, _req: web.Request) -> web.Response:
-        items, _ = self.server.list("pods")
-        for o in items:
-            m = o["metadata"]
-            self.server.delete("pods", m["name"], m.get("namespace", "default"))
+        # the bursts' pods only: pods created through the API (a populated cluster) stay
+        n = 0
+        for name, ns in self.bench_keys:
+            try:
+                self.server.delete("pods", name, ns)
+                n += 1
+            except Exception:  # noqa: BLE001 - already gone (e.g. preempted)
+                pass
+        self.bench_keys.clear()
         self.server.reset_logs()
-        return web.json_response({"deleted": len(items)})
+        return web.json_response({"deleted": n})
 
     async def stop(self) -> None:
         self.server.close_watches()
