@@ -1617,7 +1617,7 @@ void Engine::interpod_prefilter(const PodReq& req, InterPodPF* pf) const {
         all = term_count(n, aff[0]);
       } else {                                  // a pod must match every term: per label-set group
         for (const auto& g : n.lab_groups) {
-          if (g.second.first <= 0) continue;
+          if (g.second.all <= 0) continue;
           const LabSetRec& ls = labsets_[g.first];
           bool m = true;
           for (const PodTerm& t : aff)
@@ -1625,7 +1625,7 @@ void Engine::interpod_prefilter(const PodReq& req, InterPodPF* pf) const {
               m = false;
               break;
             }
-          if (m) all += g.second.first;
+          if (m) all += g.second.all;
         }
       }
       if (all > 0) {
@@ -1946,22 +1946,33 @@ bool Engine::set_pod_meta(uint64_t pod, Labels labels, bool deleting) {
 
 void Engine::index_pod(Node& n, const Assignment& a, int sign) {
   // counts that reach 0 keep their entry (the next pod of the template bumps it without
-  // allocating); a node sweeps them once they outnumber the live entries
+  // allocating); a node sweeps them once they outnumber the live entries. A pod's label-index
+  // entries are found once per (node, label set) — one hash lookup per reserve / release, not
+  // one per label
   const int live = a.deleting ? 0 : sign;
-  auto count = [&](std::pair<int32_t, int32_t>& c, bool fresh, int32_t& zeros) {
-    if (c.first <= 0 && !fresh) --zeros;
-    c.first += sign;
-    c.second += live;
-    if (c.first <= 0) ++zeros;
-  };
-  auto bump = [&](LKey k) {
-    auto r = n.lab_idx.try_emplace(k, 0, 0);
-    count(r.first->second, r.second, n.lab_idx_zero);
-  };
-  bump(LKey{a.ns, -1, -1});
-  for (const auto& kv : labsets_[a.labset].labels) bump(LKey{a.ns, kv.first, kv.second});
-  auto g = n.lab_groups.try_emplace(a.labset, 0, 0);
-  count(g.first->second, g.second, n.lab_groups_zero);
+  auto gr = n.lab_groups.try_emplace(a.labset);
+  Node::LabGroup& g = gr.first->second;
+  if (gr.second) ++n.lab_groups_zero;   // a fresh group counts as a zero one until bumped
+  if (g.all <= 0) {
+    g.idx.clear();
+    auto bind = [&](LKey k) {
+      auto r = n.lab_idx.try_emplace(k, 0, 0);
+      if (r.second) ++n.lab_idx_zero;
+      g.idx.push_back(&r.first->second);
+    };
+    bind(LKey{a.ns, -1, -1});
+    for (const auto& kv : labsets_[a.labset].labels) bind(LKey{a.ns, kv.first, kv.second});
+  }
+  for (std::pair<int32_t, int32_t>* c : g.idx) {
+    if (c->first <= 0) --n.lab_idx_zero;
+    c->first += sign;
+    c->second += live;
+    if (c->first <= 0) ++n.lab_idx_zero;
+  }
+  if (g.all <= 0) --n.lab_groups_zero;
+  g.all += sign;
+  g.live += live;
+  if (g.all <= 0) ++n.lab_groups_zero;
   if (sign < 0 && (n.lab_idx_zero > 64 || n.lab_groups_zero > 64)) sweep_lab_index(n);
 }
 
@@ -1973,7 +1984,7 @@ void Engine::sweep_lab_index(Node& n) {
   }
   if (n.lab_groups_zero * 2 > (int32_t)n.lab_groups.size()) {
     for (auto it = n.lab_groups.begin(); it != n.lab_groups.end();)
-      it = it->second.first <= 0 ? n.lab_groups.erase(it) : std::next(it);
+      it = it->second.all <= 0 ? n.lab_groups.erase(it) : std::next(it);
     n.lab_groups_zero = 0;
   }
 }
@@ -1982,9 +1993,9 @@ int64_t Engine::group_count(const Node& n, int32_t ns, const LSel& sel, bool ski
   if (sel.nothing) return 0;
   int64_t c = 0;
   for (const auto& g : n.lab_groups) {
-    if (g.second.first <= 0) continue;
+    if (g.second.all <= 0) continue;
     const LabSetRec& ls = labsets_[g.first];
-    if (ls.ns == ns && sel.matches(ls.labels)) c += skip_deleting ? g.second.second : g.second.first;
+    if (ls.ns == ns && sel.matches(ls.labels)) c += skip_deleting ? g.second.live : g.second.all;
   }
   return c;
 }

@@ -268,7 +268,14 @@ struct Node {
   // the same pods grouped by their exact (namespace, label set) — an interned label-set id — with
   // (all, not terminating) counts: any other selector is matched once per group instead of once
   // per pod (a node's pods come from few templates)
-  std::unordered_map<int32_t, std::pair<int32_t, int32_t>> lab_groups;
+  struct LabGroup {
+    int32_t all = 0, live = 0;
+    // the group's label-index entries (its namespace's, then one per label): bumped through these
+    // pointers (unordered_map references are stable), rebound when the group's count is 0 — a
+    // fresh group, or an id the label-set table recycled for another set
+    std::vector<std::pair<int32_t, int32_t>*> idx;
+  };
+  std::unordered_map<int32_t, LabGroup> lab_groups;
   // entries of lab_idx / lab_groups whose count dropped to 0: kept, so a pod of the same template
   // arriving again allocates nothing; swept once they outnumber the live entries
   int32_t lab_idx_zero = 0, lab_groups_zero = 0;
