@@ -1814,6 +1814,7 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           score_a_fix(r, sc, fg, nrep, b);
         }
         __syncthreads();
+        if (a.trace && tid == 0) a.trace[(size_t)b * kTracePts + 23] = __builtin_amdgcn_s_memrealtime();
         combine_fix(r, sc, s_feas, fg * kNodesPerWave, nrep);
         if constexpr (SPEC) {
           // the group's raw scores finished on the speculated maxima (the scores wave left the

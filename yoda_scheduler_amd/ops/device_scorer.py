@@ -50,7 +50,10 @@ OWNER_PHASES = (("own_winner", 13, 9), ("own_filter_rec1", 9, 10), ("own_score_a
                 ("own_early_g1", 10, 18),
                 # the block-wide gather 1 (G > 128): records in hand, transposed, reduced
                 ("own_g1_load", 11, 19), ("own_g1_transpose", 19, 20), ("own_g1_reduce", 20, 21),
-                ("own_g1_barrier", 21, 12))
+                ("own_g1_barrier", 21, 12),
+                # the fix-up's block barrier: the scoring wave done → every wave there → the group finished
+                ("own_to_barrier", 15, 23), ("own_finish", 23, 11), ("own_w0_to_barrier", 10, 23),
+                ("own_barrier_at", 9, 23))
 
 
 def batch_trace(engine, on: bool = True) -> None:
