@@ -1661,9 +1661,9 @@ __global__ __launch_bounds__(64 * BW) void k_batch(const BatchArgs a) {
           s_fix = -1;
           s_fixg = -1;
         }
-        // (slots are double-buffered by tag parity: the other set overwrites this record only
-        // with its pod b+1's record 1, which it publishes after this set's pod b record 3 —
-        // i.e. after this read)
+        // (each record kind has its own slot: the other set overwrites this record 3 only with
+        // its pod b+1's, which needs pod b's winner from this set — and every block of this set
+        // publishes its part of that after this read)
         // the one record that holds the winner: its key, from a block with a feasible node
         // (keys of feasible nodes are unique; a block without one reports key 0), and the pod
         // fit somewhere. Its thread applies the assume if this block holds the node.
