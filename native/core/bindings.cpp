@@ -292,7 +292,16 @@ MatchTerm match_term(const py::handle& h) {
   return m;
 }
 
+namespace yoda_sampler {
+void start(const std::vector<int>& tids, int period_us, bool stacks);
+std::pair<std::vector<std::tuple<uintptr_t, int, std::vector<uintptr_t>>>, size_t> stop();
+}  // namespace yoda_sampler
+
 PYBIND11_MODULE(_yoda_core, m) {
+  m.def("sampler_start", &yoda_sampler::start, py::arg("tids"), py::arg("period_us") = 200,
+        py::arg("stacks") = false,
+        "sample the program counter of these threads every period_us of their own CPU time (sampler.cpp)");
+  m.def("sampler_stop", &yoda_sampler::stop, "stop sampling: ([(pc, tid | overrun << 24, [return addresses])], dropped)");
   m.def("build_id", [] { return std::string(YODA_BUILD_ID); }, "hash of the sources this module was built from");
   m.doc() = "Native placement / scheduling-cycle engine (C++17)";
   m.def("engine_lock_stats", [] {

@@ -44,6 +44,8 @@ def main() -> int:
     from yoda_scheduler_amd.bench import harness as H
     if os.environ.get("YODA_PROF_SAMPLE"):
         return _sample(args, out, bench, H)
+    if os.environ.get("YODA_NATIVE_PROF"):
+        return _native(args, out, bench, H)
     # YODA_PROF_CPU=1: the interpreter thread's CPU time (waits on locks and the GIL excluded)
     pr = cProfile.Profile(__import__("time").thread_time) if os.environ.get("YODA_PROF_CPU") else cProfile.Profile()
     for cls in (H.Shard, H.HttpShard):
@@ -155,6 +157,35 @@ def _sample(args, out, bench, H) -> int:
     if out:
         with open(out, "w") as f:
             f.write(text)
+    return 0
+
+
+def _native(args, out, bench, H) -> int:
+    """YODA_NATIVE_PROF=<period us>: flat profile of the native threads (yoda-io, yoda-lane,
+    yoda-engine) over the timed bursts (native/core/sampler.cpp, utils/native_prof.py)."""
+    from yoda_scheduler_amd.utils.native_prof import maybe_sampler
+    smp = maybe_sampler()
+    for cls in (H.Shard, H.HttpShard):
+        orig = cls.burst
+
+        def wrap(orig):
+            async def burst(self, tag="b", timeout=600.0):
+                on = tag.startswith("s")
+                if on:
+                    smp.start()
+                try:
+                    return await orig(self, tag, timeout)
+                finally:
+                    if on:
+                        smp.stop()
+            return burst
+        cls.burst = wrap(orig)
+    bench.main(args)
+    text = smp.report(top=int(os.environ.get("YODA_PROF_TOP", "35")))
+    print(text)
+    if out:
+        with open(out, "w") as f:
+            f.write(text + "\n")
     return 0
 
 

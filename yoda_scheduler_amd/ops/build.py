@@ -42,7 +42,7 @@ ARCH = os.environ.get("YODA_HIP_ARCH", "gfx950")
 
 # Per artefact: output name, the sources compiled, every file whose contents define the
 # artefact (sources + headers), and a recipe tag (bump it when the compile flags change).
-CORE_SRCS = ["core/engine.cpp", "core/lane.cpp", "core/bindings.cpp"]
+CORE_SRCS = ["core/engine.cpp", "core/lane.cpp", "core/bindings.cpp", "core/sampler.cpp"]
 KUBE_COMMON = ["kube/json.cpp", "kube/flatjson.cpp", "kube/project.cpp"]
 ARTEFACTS: dict[str, dict] = {
     "core": {"out": f"_yoda_core{EXT}", "srcs": CORE_SRCS,
@@ -151,7 +151,7 @@ def build_core(force: bool = False) -> Path:
         _run([cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-Wall",
               "-Wno-unused-function", _bid_flag(bid), *_pybind_includes(), f"-I{NATIVE / 'core'}",
               f"-I{NATIVE / 'hip'}", f"-I{NATIVE / 'kube'}", f"-I{NATIVE / 'common'}", *_srcs("core"),
-              "-o", str(out), "-lpthread", "-ldl"], "core")
+              "-o", str(out), "-lpthread", "-ldl", "-lrt"], "core")
         _record("core", bid)
     return out
 
