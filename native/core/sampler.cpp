@@ -17,6 +17,7 @@
 #include <ucontext.h>
 #include <unistd.h>
 
+#include <cstdio>
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
@@ -118,6 +119,32 @@ std::pair<std::vector<std::tuple<uintptr_t, int, std::vector<uintptr_t>>>, size_
     out.emplace_back(g_pc[i], g_tid[i], std::move(st));
   }
   return {std::move(out), g_dropped.load()};
+}
+
+// Stop and write the samples to `path` (one "pc tid_w ret1 ret2 ..." hex line per sample)
+// and this process's executable mappings to `path`.maps: for a process without Python
+// (the fake apiserver), symbolised by utils/native_prof.py::load_dump.
+bool dump(const std::string& path) {
+  auto r = stop();
+  FILE* f = fopen(path.c_str(), "w");
+  if (!f) return false;
+  fprintf(f, "# dropped %zu\n", r.second);
+  for (auto& [pc, tw, st] : r.first) {
+    fprintf(f, "%lx %x", (unsigned long)pc, (unsigned)tw);
+    for (uintptr_t a : st) fprintf(f, " %lx", (unsigned long)a);
+    fputc('\n', f);
+  }
+  fclose(f);
+  FILE* in = fopen("/proc/self/maps", "r");
+  FILE* out = fopen((path + ".maps").c_str(), "w");
+  if (in && out) {
+    char buf[4096];
+    size_t n;
+    while ((n = fread(buf, 1, sizeof buf, in)) > 0) fwrite(buf, 1, n, out);
+  }
+  if (in) fclose(in);
+  if (out) fclose(out);
+  return true;
 }
 
 }  // namespace yoda_sampler

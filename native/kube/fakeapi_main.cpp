@@ -4,8 +4,20 @@
 #include <cstring>
 #include <string>
 
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <tuple>
+#include <utility>
+#include <vector>
+
 #include "build_id.h"
 #include "fakeapi.hpp"
+
+namespace yoda_sampler {   // native/core/sampler.cpp
+void start(const std::vector<int>& tids, int period_us, bool stacks);
+bool dump(const std::string& path);
+}  // namespace yoda_sampler
 
 int main(int argc, char** argv) {
   yk::FakeApiOptions o;
@@ -36,5 +48,15 @@ int main(int argc, char** argv) {
       return 2;
     }
   }
-  return yk::run_fake_apiserver(o);
+  // YODA_APISERVER_PROF=<file>: sample this (single-threaded) server's CPU for its whole life
+  // and write the samples at exit (utils/native_prof.py::load_dump)
+  const char* prof = getenv("YODA_APISERVER_PROF");
+  if (prof && *prof) {
+    const char* us = getenv("YODA_NATIVE_PROF");
+    yoda_sampler::start({(int)syscall(SYS_gettid)}, us && atoi(us) > 1 ? atoi(us) : 200,
+                        getenv("YODA_NATIVE_PROF_STACKS") != nullptr);
+  }
+  const int rc = yk::run_fake_apiserver(o);
+  if (prof && *prof) yoda_sampler::dump(prof);
+  return rc;
 }

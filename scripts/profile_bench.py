@@ -163,8 +163,12 @@ def _sample(args, out, bench, H) -> int:
 def _native(args, out, bench, H) -> int:
     """YODA_NATIVE_PROF=<period us>: flat profile of the native threads (yoda-io, yoda-lane,
     yoda-engine) over the timed bursts (native/core/sampler.cpp, utils/native_prof.py)."""
-    from yoda_scheduler_amd.utils.native_prof import maybe_sampler
+    import tempfile
+    from yoda_scheduler_amd.utils.native_prof import load_dump, maybe_sampler
     smp = maybe_sampler()
+    # the native fake apiserver (http transport) samples itself for its whole life
+    api_dump = os.path.join(tempfile.mkdtemp(prefix="yoda-apiprof-"), "apiserver.samples")
+    os.environ["YODA_APISERVER_PROF"] = api_dump
     for cls in (H.Shard, H.HttpShard):
         orig = cls.burst
 
@@ -181,7 +185,11 @@ def _native(args, out, bench, H) -> int:
             return burst
         cls.burst = wrap(orig)
     bench.main(args)
-    text = smp.report(top=int(os.environ.get("YODA_PROF_TOP", "35")))
+    top = int(os.environ.get("YODA_PROF_TOP", "35"))
+    text = smp.report(top=top)
+    if os.path.exists(api_dump):
+        text += "\n\nfake apiserver process, whole life (start-up and warmup included):\n" + \
+            load_dump(api_dump, period_us=smp.period_us).report(top=top)
     print(text)
     if out:
         with open(out, "w") as f:

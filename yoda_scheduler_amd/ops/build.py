@@ -54,8 +54,8 @@ ARTEFACTS: dict[str, dict] = {
                                     "kube/project.hpp", "kube/flatjson.hpp", "kube/transport.hpp", "kube/lane_port.hpp",
                                     "common/build_id.h"],
              "recipe": "g++ -O3 -std=c++17 -fPIC -shared -fvisibility=hidden -lssl -lcrypto v2"},
-    "fakeapi": {"out": "yoda-fake-apiserver-native", "srcs": KUBE_COMMON + ["kube/fakeapi.cpp", "kube/fakeapi_main.cpp"],
-                "deps": KUBE_COMMON + ["kube/fakeapi.cpp", "kube/fakeapi_main.cpp", "kube/fakeapi.hpp",
+    "fakeapi": {"out": "yoda-fake-apiserver-native", "srcs": KUBE_COMMON + ["kube/fakeapi.cpp", "kube/fakeapi_main.cpp", "core/sampler.cpp"],
+                "deps": KUBE_COMMON + ["kube/fakeapi.cpp", "kube/fakeapi_main.cpp", "core/sampler.cpp", "kube/fakeapi.hpp",
                                        "kube/json.hpp", "kube/flatjson.hpp", "kube/project.hpp", "kube/http.hpp",
                                        "common/build_id.h"],
                 "recipe": "g++ -O3 -std=c++17 v2"},
@@ -174,7 +174,7 @@ def build_kube(force: bool = False) -> list[Path]:
         if force or _stale("fakeapi"):
             bid = source_hash("fakeapi")
             _run([os.environ.get("CXX", "g++"), *flags, _bid_flag(bid), *_srcs("fakeapi"), "-o", str(exe),
-                  "-lpthread"], "native fake apiserver")
+                  "-lpthread", "-lrt"], "native fake apiserver")
             _record("fakeapi", bid)
         outs.append(exe)
     return outs

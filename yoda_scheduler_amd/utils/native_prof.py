@@ -34,13 +34,13 @@ def threads_by_name(names: Iterable[str]) -> dict[int, str]:
     return out
 
 
-def _maps() -> list[tuple[int, int, int, str]]:
+def _maps(path: str = "/proc/self/maps") -> list[tuple[int, int, int, str]]:
     """Executable mappings: (start, end, file offset, path)."""
     out = []
-    with open("/proc/self/maps") as f:
+    with open(path) as f:
         for ln in f:
             parts = ln.split()
-            if len(parts) < 6 or "x" not in parts[1] or not parts[5].startswith("/"):
+            if len(parts) < 6 or "x" not in parts[1] or not parts[5].startswith(("/", "[vdso]")):
                 continue
             a, b = (int(x, 16) for x in parts[0].split("-"))
             out.append((a, b, int(parts[2], 16), parts[5]))
@@ -69,6 +69,7 @@ class NativeSampler:
         self.samples: list[tuple[int, int, list]] = []
         self.dropped = 0
         self.tids: dict[int, str] = {}
+        self.maps_file = "/proc/self/maps"
 
     def start(self) -> None:
         self.tids.update(threads_by_name(self.names))
@@ -93,7 +94,7 @@ class NativeSampler:
 
     def symbolise(self) -> list[tuple[str, int, list[tuple[str, str]]]]:
         """(thread, weight in periods, [(module basename, function), leaf first]) per sample."""
-        maps = _maps()
+        maps = _maps(self.maps_file)
         where: dict[int, tuple[str, int]] = {}
         per_file: dict[str, set[int]] = collections.defaultdict(set)
         frames = [self._frames(pc, st) for pc, _tw, st in self.samples]
@@ -111,6 +112,8 @@ class NativeSampler:
                     where[pc] = ("?", pc)
         names: dict[tuple[str, int], str] = {}
         for path, offs in per_file.items():
+            if not path.startswith("/"):
+                continue                     # [vdso]: clock_gettime & co
             srt = sorted(offs)
             for i in range(0, len(srt), 2000):
                 for o, fn in _addr2line(path, srt[i:i + 2000]).items():
@@ -172,7 +175,26 @@ def _is_std(fn: str) -> bool:
     return f.startswith(("std::", "__gnu_cxx::", "operator new", "operator delete"))
 
 
-_RUNTIME = ("libc.so", "libstdc++.so", "libgcc_s.so", "ld-linux", "libm.so", "?")
+_RUNTIME = ("libc.so", "libstdc++.so", "libgcc_s.so", "ld-linux", "libm.so", "[vdso]", "?")
+
+
+def load_dump(path: str, thread: str = "apiserver", period_us: int = 200) -> NativeSampler:
+    """The samples another process wrote with ``yoda_sampler::dump`` (the native fake
+    apiserver under ``YODA_APISERVER_PROF``), ready for ``report()``."""
+    s = NativeSampler.__new__(NativeSampler)
+    s.names, s.period_us, s.stacks, s.dropped = (thread,), period_us, False, 0
+    s.samples, s.tids, s.maps_file = [], {}, path + ".maps"
+    with open(path) as f:
+        for ln in f:
+            if ln.startswith("#"):
+                s.dropped = int(ln.split()[-1])
+                continue
+            v = [int(x, 16) for x in ln.split()]
+            if len(v) >= 2:
+                s.samples.append((v[0], v[1], v[2:]))
+                s.tids[v[1] & 0xFFFFFF] = thread
+    s.stacks = any(st for _, _, st in s.samples)
+    return s
 
 
 def maybe_sampler() -> Optional[NativeSampler]:
