@@ -1111,23 +1111,50 @@ Labels Lane::intern_labels(const std::vector<std::pair<std::string, std::string>
   return l;
 }
 
+namespace {
+// a JSON string literal (the kube module's dump_string is not linked into this module)
+void json_quoted(std::string_view v, std::string& o) {
+  static const char hx[] = "0123456789abcdef";
+  o.push_back('"');
+  for (unsigned char c : v) {
+    if (c == '"' || c == '\\') {
+      o.push_back('\\');
+      o.push_back(char(c));
+    } else if (c < 0x20) {
+      o.append("\\u00");
+      o.push_back(hx[c >> 4]);
+      o.push_back(hx[c & 15]);
+    } else {
+      o.push_back(char(c));
+    }
+  }
+  o.push_back('"');
+}
+}  // namespace
+
 void Lane::annotations(const Profile& pr, const Entry& e, const PodReq& req, const CycleResult& r,
-                       std::vector<yk::KV>* out) {
-  // plugins/defaults.py::bind_annotations
+                       std::string* out) {
+  // plugins/defaults.py::bind_annotations, written as JSON object members
   if (!pr.annotate) return;
-  std::string gpus, vis, uu;
+  thread_local std::string vis, uu;
+  vis.clear();
+  uu.clear();
   size_t nu = 0;
+  char num[24];
+  std::string& o = *out;
+  o.append("\"scv.amd.com/gpus\":\"");
   {
     std::lock_guard<std::mutex> g(vis_mu_);
     auto it = vis_.find(e.node_name);
     const std::vector<std::pair<std::string, std::string>>* per = it == vis_.end() ? nullptr : &it->second;
     for (size_t i = 0; i < r.cards.size(); ++i) {
       const int32_t c = r.cards[i];
+      const int nn = snprintf(num, sizeof num, "%d", c);
       if (i) {
-        gpus.push_back(',');
+        o.push_back(',');
         vis.push_back(',');
       }
-      gpus += std::to_string(c);
+      o.append(num, size_t(nn));
       if (per && c >= 0 && c < (int32_t)per->size()) {
         vis += (*per)[c].first;
         if (!(*per)[c].second.empty()) {
@@ -1136,14 +1163,20 @@ void Lane::annotations(const Profile& pr, const Entry& e, const PodReq& req, con
           ++nu;
         }
       } else {
-        vis += std::to_string(c);
+        vis.append(num, size_t(nn));
       }
     }
   }
-  out->emplace_back("scv.amd.com/gpus", std::move(gpus));
-  out->emplace_back("scv.amd.com/visible-devices", std::move(vis));
-  if (nu && nu == r.cards.size()) out->emplace_back("scv.amd.com/gpu-uuids", std::move(uu));
-  if (req.has_memory) out->emplace_back("scv.amd.com/reserved-mb", std::to_string(req.memory));
+  o.append("\",\"scv.amd.com/visible-devices\":");
+  json_quoted(vis, o);
+  if (nu && nu == r.cards.size()) {
+    o.append(",\"scv.amd.com/gpu-uuids\":");
+    json_quoted(uu, o);
+  }
+  if (req.has_memory) {
+    const int nn = snprintf(num, sizeof num, "%lld", (long long)req.memory);
+    o.append(",\"scv.amd.com/reserved-mb\":\"").append(num, size_t(nn)).push_back('"');
+  }
 }
 
 // The engine's part of a run: requests from the pods' projections, the batch cycle under the
@@ -1296,7 +1329,7 @@ void Lane::finish_run(Run& r, std::vector<yk::BindSpec>* binds, std::vector<uint
     b.name = e->ev->p.name;
     b.uid = e->ev->p.uid;
     b.node = e->node_name;
-    annotations(pr, *e, r.reqs[k], res, &b.annotations);
+    annotations(pr, *e, r.reqs[k], res, &b.ann_json);
     binds->push_back(std::move(b));
     tags->push_back(e->id);
     e->bind_out = true;

@@ -349,7 +349,7 @@ class Lane : public yk::PodSink {
   bool make_req(const yk::PodProj& p, PodReq* r);
   Labels intern_labels(const std::vector<std::pair<std::string, std::string>>& kv);   // engine lock held
   void annotations(const Profile& pr, const Entry& e, const PodReq& req, const CycleResult& r,
-                   std::vector<yk::KV>* out);
+                   std::string* out);
   void record_scheduled(const Entry& e);
   // native unschedulable path
   void fail_native(Entry* e, const Profile& pr, const CycleResult& res, bool hinted);

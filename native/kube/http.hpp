@@ -338,9 +338,8 @@ inline std::string url_decode(std::string_view s) {
   return out;
 }
 
-inline std::string url_encode(std::string_view s) {
+inline void url_encode_into(std::string_view s, std::string& out) {
   static const char hx[] = "0123456789ABCDEF";
-  std::string out;
   for (unsigned char c : s) {
     if ((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '-' || c == '_' ||
         c == '.' || c == '~') {
@@ -351,6 +350,11 @@ inline std::string url_encode(std::string_view s) {
       out.push_back(hx[c & 15]);
     }
   }
+}
+
+inline std::string url_encode(std::string_view s) {
+  std::string out;
+  url_encode_into(s, out);
   return out;
 }
 

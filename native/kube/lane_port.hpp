@@ -62,6 +62,9 @@ struct WatchEvent {
 struct BindSpec {
   std::string ns, name, uid, node;
   std::vector<KV> annotations;
+  // the annotations as serialised JSON object members (`"k":"v",...`), used instead of
+  // `annotations` when set: the lane writes them in one buffer (no per-key allocations)
+  std::string ann_json;
 };
 
 class PodSink {

@@ -228,6 +228,13 @@ std::string Transport::bind_body(const std::string& ns, const std::string& name,
                                  const std::string& node, const std::vector<KV>& annotations) {
   std::string b;
   b.reserve(256);
+  append_bind_body(b, ns, name, uid, node, annotations);
+  return b;
+}
+
+void Transport::append_bind_body(std::string& b, const std::string& ns, const std::string& name,
+                                 const std::string& uid, const std::string& node,
+                                 const std::vector<KV>& annotations, std::string_view ann_json) {
   b.append("{\"apiVersion\":\"v1\",\"kind\":\"Binding\",\"metadata\":{\"name\":");
   dump_string(name, b);
   b.append(",\"namespace\":");
@@ -235,7 +242,8 @@ std::string Transport::bind_body(const std::string& ns, const std::string& name,
   b.append(",\"uid\":");
   dump_string(uid, b);
   b.append(",\"annotations\":{");
-  for (size_t i = 0; i < annotations.size(); ++i) {
+  b.append(ann_json);
+  for (size_t i = 0; ann_json.empty() && i < annotations.size(); ++i) {
     if (i) b.push_back(',');
     dump_string(annotations[i].first, b);
     b.push_back(':');
@@ -244,7 +252,40 @@ std::string Transport::bind_body(const std::string& ns, const std::string& name,
   b.append("}},\"target\":{\"apiVersion\":\"v1\",\"kind\":\"Node\",\"name\":");
   dump_string(node, b);
   b.append("}}");
-  return b;
+}
+
+// A Binding POST in one buffer: request line, headers, body. The body goes into a per-thread
+// scratch first (its length is a header); the header lines that do not change between
+// requests (head()'s, for a POST of application/json) are built once per token.
+void Transport::bind_wire(const BindSpec& s, std::string& wire) {
+  thread_local std::string body;
+  body.clear();
+  append_bind_body(body, s.ns, s.name, s.uid, s.node, s.annotations, s.ann_json);
+  char len[24];
+  const int nl = snprintf(len, sizeof len, "%zu\r\n\r\n", body.size());
+  wire.reserve(320 + cfg_.prefix.size() + s.ns.size() + s.name.size() + body.size());
+  wire.append("POST ").append(cfg_.prefix).append("/api/v1/namespaces/");
+  url_encode_into(s.ns, wire);
+  wire.append("/pods/");
+  url_encode_into(s.name, wire);
+  wire.append("/binding HTTP/1.1\r\n");
+  {
+    std::lock_guard<std::mutex> g(in_mu_);
+    if (bind_hdr_.empty() || bind_hdr_token_ != token_) {
+      std::string& h = bind_hdr_;
+      h.clear();
+      h.append("Host: ");
+      if (cfg_.host.find(':') != std::string::npos) h.append("[").append(cfg_.host).append("]");
+      else h.append(cfg_.host);
+      h.append(":").append(std::to_string(cfg_.port)).append("\r\nUser-Agent: ").append(cfg_.user_agent);
+      h.append("\r\nAccept: application/json\r\n");
+      if (!token_.empty()) h.append("Authorization: Bearer ").append(token_).append("\r\n");
+      h.append("Content-Type: application/json\r\nContent-Length: ");
+      bind_hdr_token_ = token_;
+    }
+    wire.append(bind_hdr_);
+  }
+  wire.append(len, size_t(nl)).append(body);
 }
 
 uint64_t Transport::bind(const std::string& ns, const std::string& name, const std::string& uid,
@@ -262,12 +303,9 @@ uint64_t Transport::bind_many(const std::vector<BindSpec>& binds, double timeout
   rs.reserve(binds.size());
   for (size_t k = 0; k < binds.size(); ++k) {
     const BindSpec& s = binds[k];
-    std::string b = bind_body(s.ns, s.name, s.uid, s.node, s.annotations);
     auto r = std::make_unique<Req>();
     r->id = first + k;
-    r->wire = head("POST", "/api/v1/namespaces/" + url_encode(s.ns) + "/pods/" + url_encode(s.name) + "/binding",
-                   b.size(), "application/json");
-    r->wire.append(b);
+    bind_wire(s, r->wire);
     r->limited = true;
     r->deadline = deadline;
     rs.push_back(std::move(r));
@@ -291,12 +329,9 @@ void Transport::bind_native(std::vector<BindSpec>&& binds, const std::vector<uin
   rs.reserve(binds.size());
   for (size_t k = 0; k < binds.size(); ++k) {
     const BindSpec& s = binds[k];
-    std::string b = bind_body(s.ns, s.name, s.uid, s.node, s.annotations);
     auto r = std::make_unique<Req>();
     r->id = next_id_++;
-    r->wire = head("POST", "/api/v1/namespaces/" + url_encode(s.ns) + "/pods/" + url_encode(s.name) + "/binding",
-                   b.size(), "application/json");
-    r->wire.append(b);
+    bind_wire(s, r->wire);
     r->limited = true;
     r->deadline = deadline;
     r->sink = sink;

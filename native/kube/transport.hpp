@@ -113,6 +113,10 @@ class Transport : public PodPort {
  private:
   void run();
   void submit(std::unique_ptr<Req> r);
+  void append_bind_body(std::string& b, const std::string& ns, const std::string& name, const std::string& uid,
+                        const std::string& node, const std::vector<KV>& annotations,
+                        std::string_view ann_json = {});
+  void bind_wire(const BindSpec& s, std::string& wire);
   std::string bind_body(const std::string& ns, const std::string& name, const std::string& uid,
                         const std::string& node, const std::vector<KV>& annotations);
   std::string head(const std::string& method, const std::string& path, size_t body_len,
@@ -147,6 +151,7 @@ class Transport : public PodPort {
   std::mutex in_mu_;
   std::vector<std::unique_ptr<Req>> incoming_;
   std::vector<uint64_t> cancels_;
+  std::string bind_hdr_, bind_hdr_token_;   // bind_wire's constant header lines (in_mu_)
   std::string token_;
 
   std::mutex out_mu_;
