@@ -1243,6 +1243,8 @@ bool Engine::select_gpus(const PodReq& req, int32_t idx, std::vector<int32_t>* o
   uint64_t cl = req.has_clock ? req.clock : 0;
   if (k == 0) return true;
   std::vector<int32_t> E;
+  E.reserve(n.cards.size());             // one allocation, not a growth chain per pod
+  out->reserve(k);
   for (int32_t i = 0; i < (int32_t)n.cards.size(); ++i) {
     const Card& c = n.cards[i];
     bool ok = compat_ ? (c.healthy && c.free_mb >= m && (!req.has_clock || c.clock == cl))
@@ -1413,6 +1415,7 @@ std::vector<int32_t> Engine::feasible_nodes(const PodReq& req, const std::vector
   if (reasons) reasons->assign(RS_NUM, 0);
   if (N == 0) return feasible;
   const int32_t want = exhaustive ? N : num_feasible_to_find(N);
+  feasible.reserve(std::min(want, N));
   const int32_t start = next_start_ % N;
   SpreadPF pf_store;
   const SpreadPF* pf = nullptr;

@@ -6,6 +6,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <charconv>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -153,7 +154,13 @@ std::string rfc3339(double ts) {
   return buf;
 }
 
-std::string key_of(const yk::PodProj& p) { return p.ns + "/" + p.name; }
+std::string key_of(const yk::PodProj& p) {
+  std::string k;                          // one allocation (ns + "/" + name builds a temporary)
+  k.reserve(p.ns.size() + 1 + p.name.size());
+  k.append(p.ns).push_back('/');
+  k.append(p.name);
+  return k;
+}
 
 bool terminal(const yk::PodProj& p) { return p.phase == "Succeeded" || p.phase == "Failed"; }
 
@@ -551,7 +558,7 @@ bool uninteresting(const yk::PodProj& p, const std::vector<Lane::Profile>& lp) {
 // store mutations: lane thread, store_mu_ held by the caller
 void Lane::handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::vector<Fwd>* out) {
   const yk::PodProj& p = ev->p;
-  const std::string key = key_of(p);
+  std::string key = key_of(p);
   auto it = by_key_.find(key);
   if (it != by_key_.end() && it->second->ev->p.uid != p.uid && type != 'D') {
     // the key now names another pod (deleted + recreated while we were not watching)
@@ -594,7 +601,7 @@ void Lane::handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::ve
     } else if (!uninteresting(p, lp_)) {
       forward('A', ev, nullptr, out);
     }
-    by_key_.emplace(key, std::move(e));
+    by_key_.emplace(std::move(key), std::move(e));
     return;
   }
   Entry* e = it->second.get();
@@ -1149,7 +1156,7 @@ void Lane::annotations(const Profile& pr, const Entry& e, const PodReq& req, con
     const std::vector<std::pair<std::string, std::string>>* per = it == vis_.end() ? nullptr : &it->second;
     for (size_t i = 0; i < r.cards.size(); ++i) {
       const int32_t c = r.cards[i];
-      const int nn = snprintf(num, sizeof num, "%d", c);
+      const int nn = int(std::to_chars(num, num + sizeof num, c).ptr - num);   // snprintf: ~10x dearer
       if (i) {
         o.push_back(',');
         vis.push_back(',');
@@ -1174,7 +1181,7 @@ void Lane::annotations(const Profile& pr, const Entry& e, const PodReq& req, con
     json_quoted(uu, o);
   }
   if (req.has_memory) {
-    const int nn = snprintf(num, sizeof num, "%lld", (long long)req.memory);
+    const int nn = int(std::to_chars(num, num + sizeof num, (long long)req.memory).ptr - num);
     o.append(",\"scv.amd.com/reserved-mb\":\"").append(num, size_t(nn)).push_back('"');
   }
 }

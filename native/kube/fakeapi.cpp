@@ -358,13 +358,20 @@ void chunk(std::string& out, std::string_view data) {
   out.append("\r\n");
 }
 
+// one watch event as an HTTP chunk, appended straight to `out` (a connection's write buffer)
+void append_frame(std::string& out, char type, const std::string& obj_text) {
+  static constexpr std::string_view pre = "{\"type\":\"", mid = "\",\"object\":", post = "}\n";
+  const std::string_view tn = type_name(type);
+  const size_t n = pre.size() + tn.size() + mid.size() + obj_text.size() + post.size();
+  char hdr[24];
+  const int hn = snprintf(hdr, sizeof(hdr), "%zx\r\n", n);
+  out.reserve(out.size() + size_t(hn) + n + 2);
+  out.append(hdr, size_t(hn)).append(pre).append(tn).append(mid).append(obj_text).append(post).append("\r\n");
+}
+
 std::string frame(char type, const std::string& obj_text) {
-  std::string line;
-  line.reserve(obj_text.size() + 32);
-  line.append("{\"type\":\"").append(type_name(type)).append("\",\"object\":").append(obj_text).append("}\n");
   std::string out;
-  out.reserve(line.size() + 16);
-  chunk(out, line);
+  append_frame(out, type, obj_text);
   return out;
 }
 
@@ -471,16 +478,13 @@ class Server {
       rs.hist.pop_front();
     }
     if (rs.watchers.empty()) return;
-    std::string frames[3];
     const std::string& ns = obj->ns;
     for (Watcher* w : rs.watchers) {
       if (w->dead) continue;
       if (!w->ns.empty() && ns != w->ns) continue;
       char t = w->sel.empty() ? type : filter_event(w->sel, type, *obj, old.get());
       if (!t) continue;
-      int fi = t == 'A' ? 0 : t == 'M' ? 1 : 2;
-      if (frames[fi].empty()) frames[fi] = frame(t, obj->text);
-      w->conn->wbuf.append(frames[fi]);
+      append_frame(w->conn->wbuf, t, obj->text);      // no intermediate frame string
       mark_out(w->conn);
     }
   }
@@ -994,7 +998,7 @@ void Server::start_watch(Conn* c, ResState& rs, const std::string& ns, const Req
       if (!w->ns.empty() && h.obj->ns != w->ns) continue;
       char t = w->sel.empty() ? h.type : filter_event(w->sel, h.type, *h.obj, h.old.get());
       if (!t) continue;
-      c->wbuf.append(frame(t, h.obj->text));
+      append_frame(c->wbuf, t, h.obj->text);
     }
   }
   rs.watchers.push_back(w.get());

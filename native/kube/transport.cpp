@@ -16,6 +16,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <charconv>
 #include <cerrno>
 #include <chrono>
 #include <cstring>
@@ -261,8 +262,10 @@ void Transport::bind_wire(const BindSpec& s, std::string& wire) {
   thread_local std::string body;
   body.clear();
   append_bind_body(body, s.ns, s.name, s.uid, s.node, s.annotations, s.ann_json);
-  char len[24];
-  const int nl = snprintf(len, sizeof len, "%zu\r\n\r\n", body.size());
+  char len[32];
+  char* le = std::to_chars(len, len + 20, body.size()).ptr;
+  memcpy(le, "\r\n\r\n", 4);
+  const int nl = int(le + 4 - len);
   wire.reserve(320 + cfg_.prefix.size() + s.ns.size() + s.name.size() + body.size());
   wire.append("POST ").append(cfg_.prefix).append("/api/v1/namespaces/");
   url_encode_into(s.ns, wire);
