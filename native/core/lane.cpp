@@ -519,6 +519,7 @@ void Lane::publish(std::vector<Fwd>&& fwd, std::vector<Handoff>&& hand) {
 }
 
 void Lane::forward(char type, std::shared_ptr<yk::PodEv> ev, std::shared_ptr<yk::PodEv> old, std::vector<Fwd>* out) {
+  ev->materialize();                      // Python may read it from another thread
   out->push_back(Fwd{type, std::move(ev), std::move(old)});
   std::lock_guard<std::mutex> g(stat_mu_);
   st_.forwarded++;

@@ -171,7 +171,10 @@ PYBIND11_MODULE(_yoda_kube, m) {
         return py::make_tuple(py::str(p.ns + "/" + p.name), py::str(p.uid), py::str(p.node),
                               py::str(p.sched), py::str(p.phase), e.hash());
       })
-      .def("raw", [](const PodEv& e) { return py::bytes(e.raw); })
+      .def("raw", [](const PodEv& e) {
+        const std::string_view r = e.raw_view();
+        return py::bytes(r.data(), r.size());
+      })
       .def("info_args", [](const PodEv& e) -> py::object {
         const PodProj& p = e.full();
         if (!p.ok) return py::none();
@@ -359,6 +362,7 @@ PYBIND11_MODULE(_yoda_kube, m) {
         d["watch_bytes"] = s.watch_bytes;
         d["parse_errors"] = s.parse_errors;
         d["watch_cpu_s"] = s.watch_cpu_s;
+        d["slab_deletions"] = s.slab_deletions;
         d["sink_sent"] = s.sink_sent;
         d["sink_answered"] = s.sink_answered;
         d["sink_queue_s"] = s.sink_queue_s;

@@ -24,6 +24,21 @@ namespace yk {
 struct PodEv {
   PodProj p;
   std::string raw;             // the pod object's JSON text
+  // A deletion's text stays in the watch read buffer it arrived in (shared by the deletions
+  // of that read) instead of being copied out: the lane drops a lane-owned pod's deletion
+  // unread. materialize() copies it into `raw` — the lane does before handing the event to
+  // Python, and complete() (full()) does before projecting. Lane thread / under `once` only.
+  std::shared_ptr<const std::string> slab;
+  uint32_t slab_off = 0, slab_len = 0;
+  void materialize() {
+    if (slab) {
+      raw.assign(slab->data() + slab_off, slab_len);
+      slab.reset();
+    }
+  }
+  std::string_view raw_view() const {
+    return slab ? std::string_view(slab->data() + slab_off, slab_len) : std::string_view(raw);
+  }
   // A "light" event carries only the identity fields (ns, name, uid, rv, node, scheduler,
   // phase, deletion, creation) — what the lane reads of a Binding's echo or a deletion. The
   // rest (labels, requests, selectors, flags, spec/metadata hash, ok) is projected from `raw`

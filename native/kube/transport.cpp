@@ -374,6 +374,7 @@ void Transport::set_pod_sink(PodSink* sink) {
 }
 
 void complete_pod_ev(PodEv* e) {
+  e->materialize();
   PodProj full;
   FlatDoc d;
   if (d.parse(e->raw)) project_pod(d.root(), full);
@@ -665,12 +666,16 @@ void Transport::watch_lines(Conn* c) {
   // pods are projected from the same document (project.hpp)
   const double cpu0 = decode_clock_s();
   size_t start = 0;
-  uint64_t nev = 0, nerr = 0;
+  uint64_t nev = 0, nerr = 0, nslab = 0;
   FlatDoc doc;
+  // the read buffer as a view: deletions may take the buffer itself over as their shared slab
+  // (PodEv::slab), after which the unconsumed tail is copied back into c->lines
+  std::string_view buf(c->lines);
+  std::shared_ptr<const std::string> slab;
   while (true) {
-    size_t nl = c->lines.find('\n', start);
+    size_t nl = buf.find('\n', start);
     if (nl == std::string::npos) break;
-    std::string_view line(c->lines.data() + start, nl - start);
+    std::string_view line(buf.data() + start, nl - start);
     start = nl + 1;
     bool blank = true;
     for (char ch : line)
@@ -687,13 +692,27 @@ void Transport::watch_lines(Conn* c) {
       std::string_view obj;
       pe = std::make_shared<PodEv>();
       static const bool scan_all = getenv("YODA_WATCH_SCAN_ALL") != nullptr;   // A/B: the old full scan
+      static const bool copy_del = getenv("YODA_WATCH_COPY_DELETIONS") != nullptr;   // A/B: copy every text
       if (scan_watch_identity(line, &t, &obj, pe->p, !scan_all) && (t == 'M' || t == 'D')) {
         WatchEvent ev;
         ev.type = t;
         ev.rv = pe->p.rv;
         pe->light = true;
         pe->complete = &complete_pod_ev;
-        pe->raw.assign(obj.data(), obj.size());
+        if (t == 'D' && !copy_del && (slab || c->lines.size() >= 4096)) {
+          if (!slab) {
+            // moving a heap-held string keeps its buffer: `buf` and `line` stay valid
+            auto own = std::make_shared<std::string>(std::move(c->lines));
+            c->lines.clear();
+            slab = std::move(own);
+          }
+          pe->slab = slab;
+          pe->slab_off = uint32_t(obj.data() - slab->data());
+          pe->slab_len = uint32_t(obj.size());
+          nslab++;
+        } else {
+          pe->raw.assign(obj.data(), obj.size());
+        }
         ev.pod = std::move(pe);
         c->evs.push_back(std::move(ev));
         nev++;
@@ -745,11 +764,13 @@ void Transport::watch_lines(Conn* c) {
     c->evs.push_back(std::move(ev));
     nev++;
   }
-  if (start) c->lines.erase(0, start);
+  if (slab) c->lines.assign(buf.data() + start, buf.size() - start);
+  else if (start) c->lines.erase(0, start);
   if (nev || nerr) {
     const double dc = decode_clock_s() - cpu0;
     std::lock_guard<std::mutex> g(stats_mu_);
     stats_.watch_events += nev;
+    stats_.slab_deletions += nslab;
     stats_.parse_errors += nerr;
     stats_.watch_cpu_s += dc;
   }

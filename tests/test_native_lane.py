@@ -1270,3 +1270,44 @@ def test_claim_table_reset_with_unchanged_constraints_keeps_waiting_lane_pods():
             return nl.lane.stats()["parked"], nl.owned()
     parked, owned = run(go())
     assert parked == 1 and owned == 1
+
+
+def test_deletions_kept_in_the_read_buffer_reach_python_whole(monkeypatch):
+    """A deletion's text stays in the watch read buffer it arrived in (PodEv::slab, reads of
+    >= 4 KiB): lane-owned pods are released without copying it, and a deletion the lane
+    forwards (a pod bound by someone else) reaches Python with its full object text."""
+    seen = []
+    orig = Scheduler.on_pod_native
+
+    def rec(self, typ, ev, idt, old):
+        if typ == "DELETED":
+            seen.append((idt[0], ev.raw()))
+        return orig(self, typ, ev, idt, old)
+    monkeypatch.setattr(Scheduler, "on_pod_native", rec)
+    big = "x" * 5000                     # each event alone fills a read past the slab threshold
+
+    async def go():
+        async with Env() as e:
+            for i in range(12):
+                await e.create(pod(f"own{i}", {"scv/memory": "1024"}, ))
+                await e.create({"metadata": {"name": f"ext{i}", "annotations": {"big": big}},
+                                "spec": {"schedulerName": "other", "nodeName": "n1", "tolerations": TOL}})
+            assert await e.wait(lambda: e.sched.scheduled == 12)
+            lane = e.sched.lane.lane
+            assert await e.wait(lambda: lane.stats()["confirmed"] == 12)
+            for i in range(12):
+                await e.cl.patch("pods", f"own{i}", {"metadata": {"annotations": {"big": big}}}, "default")
+            for i in range(12):
+                await e.cl.delete("pods", f"own{i}", "default")
+                await e.cl.delete("pods", f"ext{i}", "default")
+            assert await e.wait(lambda: e.sched.engine.ledger_size == 0 and lane.stats()["owned"] == 0)
+            assert await e.wait(lambda: len(seen) >= 12)
+            assert not e.sched.cache.pods
+            assert e.cl.native.stats()["slab_deletions"] >= 24
+    run(go())
+    import json as _json
+    got = {k: _json.loads(raw) for k, raw in seen}
+    assert set(got) == {f"default/ext{i}" for i in range(12)}
+    for k, obj in got.items():
+        assert obj["metadata"]["name"] == k.split("/")[1]
+        assert obj["metadata"]["annotations"]["big"] == big
