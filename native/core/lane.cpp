@@ -580,6 +580,7 @@ void Lane::handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::ve
         out_moves_pending_++;
       }
     }
+    grave_.push_back(std::move(it->second->ev));   // freed on the I/O thread (recycle)
     by_key_.erase(it);
     return;
   }
@@ -665,6 +666,7 @@ void Lane::handle_event(char type, const std::shared_ptr<yk::PodEv>& ev, std::ve
       meta_pending_.push_back({e->id, ev});
     }
     if (e->crow >= 0) census_[e->crow].deleting = p.deleting;
+    if (e->ev != e->lab_ev) grave_.push_back(std::move(e->ev));
     e->ev = ev;
     if (!e->confirmed) {
       e->confirmed = true;
@@ -710,7 +712,7 @@ void Lane::drop_owned(Entry* e, bool release) {
   if (e->st == PARKED) parked_.erase(e->id);      // a BACKOFF heap item goes stale by itself
   e->req.reset();
   if (e->crow >= 0) census_remove(e);
-  e->lab_ev.reset();
+  if (e->lab_ev) grave_.push_back(std::move(e->lab_ev));
   if (release && e->id) {
     to_release_.push_back(e->id);
     log_remove(e->id);
@@ -2193,7 +2195,10 @@ void Lane::run() {
           case Item::kRunDone:
             for (auto& r : *it.runs) done.push_back(r);
             break;
-          case Item::kEvent: handle_event(it.type, it.ev, &fwd); break;
+          case Item::kEvent:
+            handle_event(it.type, it.ev, &fwd);
+            grave_.push_back(std::move(it.ev));
+            break;
           case Item::kAnswer: handle_answer(it.tag, it.status, it.body, it.t); break;
           case Item::kProfiles: apply_profiles(&fwd); break;
           case Item::kGates: apply_gates(&fwd); break;
@@ -2209,6 +2214,13 @@ void Lane::run() {
       }
     }
     work.clear();
+    if (!grave_.empty()) {
+      // the I/O thread allocated these events: freed there, their memory goes back to its
+      // malloc cache instead of both threads contending for its arena (native profile of the
+      // reset: a third of the lane's time in those frees, profiles/bench/r6/natprof/)
+      if (yk::PodPort* port = port_.load()) port->recycle(std::move(grave_));
+      grave_.clear();
+    }
     // a lane release is a move request for the lane's own waiting pods too (AssignedPodDelete);
     // moves apply before this turn's runs complete (upstream's moveRequestCycle rule)
     if (out_moves_pending_ && !parked_.empty()) pending_moves_.push_back(-1);

@@ -475,6 +475,7 @@ class Lane : public yk::PodSink {
   bool active_admission_ = false;                    // some profile hands pods to the lane
 
   // lane-thread scratch, flushed once per loop turn
+  std::vector<std::shared_ptr<yk::PodEv>> grave_;   // lane thread: events to drop on the I/O thread
   std::vector<uint64_t> to_release_;                 // engine ledger releases (one lock per turn)
   // reserved pods whose labels / deletionTimestamp changed: the engine ledger's copy follows
   std::vector<std::pair<uint64_t, std::shared_ptr<yk::PodEv>>> meta_pending_;

@@ -112,6 +112,10 @@ class PodPort {
   virtual void request_native(const std::string& method, const std::string& path, std::string&& body,
                               bool limited, double timeout_s, uint64_t tag, PodSink* sink,
                               const char* content_type = nullptr) = 0;
+  // Pod events the sink is done with, handed back so that their last reference drops on the
+  // thread that allocated them (the I/O thread): freed there, their memory returns to that
+  // thread's malloc cache instead of contending for its arena from the sink's thread.
+  virtual void recycle(std::vector<std::shared_ptr<PodEv>>&& dead) { dead.clear(); }
 };
 
 }  // namespace yk

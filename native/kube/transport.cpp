@@ -323,6 +323,23 @@ uint64_t Transport::bind_many(const std::vector<BindSpec>& binds, double timeout
   return first;
 }
 
+void Transport::recycle(std::vector<std::shared_ptr<PodEv>>&& dead) {
+  if (dead.empty()) return;
+  bool wake;
+  {
+    std::lock_guard<std::mutex> g(recycle_mu_);
+    if (recycle_.empty()) {
+      recycle_.swap(dead);
+    } else {
+      recycle_.reserve(recycle_.size() + dead.size());
+      for (auto& d : dead) recycle_.push_back(std::move(d));
+    }
+    wake = recycle_.size() >= 16384;      // an idle I/O thread would otherwise hold them a while
+  }
+  dead.clear();
+  if (wake) efd_signal(wake_efd_);
+}
+
 void Transport::bind_native(std::vector<BindSpec>&& binds, const std::vector<uint64_t>& tags, double timeout_s,
                             PodSink* sink) {
   if (binds.empty()) return;
@@ -1035,6 +1052,14 @@ void Transport::run() {
     if (!local_out_.empty()) timeout_ms = 0;
     int n = epoll_wait(ep_, evs, 128, timeout_ms);
     if (n < 0 && errno != EINTR) break;
+    {
+      // pod events the lane finished with: freed here, before this turn decodes new ones
+      std::vector<std::shared_ptr<PodEv>> dead;
+      {
+        std::lock_guard<std::mutex> g(recycle_mu_);
+        dead.swap(recycle_);
+      }
+    }
     bool woke = false;
     for (int i = 0; i < n; ++i) {
       if (evs[i].data.ptr == nullptr) {

@@ -97,6 +97,7 @@ class Transport : public PodPort {
   // detaches it (waits for a sink call in progress). Answers of requests submitted for a
   // sink that is no longer attached are dropped.
   void set_pod_sink(PodSink* sink);
+  void recycle(std::vector<std::shared_ptr<PodEv>>&& dead) override;
   void bind_native(std::vector<BindSpec>&& binds, const std::vector<uint64_t>& tags, double timeout_s,
                    PodSink* sink) override;
   void request_native(const std::string& method, const std::string& path, std::string&& body, bool limited,
@@ -152,6 +153,8 @@ class Transport : public PodPort {
   std::mutex in_mu_;
   std::vector<std::unique_ptr<Req>> incoming_;
   std::vector<uint64_t> cancels_;
+  std::mutex recycle_mu_;
+  std::vector<std::shared_ptr<PodEv>> recycle_;   // dropped on the I/O thread (recycle())
   std::string bind_hdr_, bind_hdr_token_;   // bind_wire's constant header lines (in_mu_)
   std::string token_;
 

@@ -169,12 +169,17 @@ def _native(args, out, bench, H) -> int:
     # the native fake apiserver (http transport) samples itself for its whole life
     api_dump = os.path.join(tempfile.mkdtemp(prefix="yoda-apiprof-"), "apiserver.samples")
     os.environ["YODA_APISERVER_PROF"] = api_dump
+    # YODA_NATIVE_PROF_PHASE=reset: sample only while the previous burst is being deleted
+    reset_only = os.environ.get("YODA_NATIVE_PROF_PHASE") == "reset"
     for cls in (H.Shard, H.HttpShard):
         orig = cls.burst
 
         def wrap(orig):
             async def burst(self, tag="b", timeout=600.0):
                 on = tag.startswith("s")
+                if reset_only:
+                    self.phase_hook = (lambda ph, started: (smp.start() if started else smp.stop())) if on else None
+                    return await orig(self, tag, timeout)
                 if on:
                     smp.start()
                 try:

@@ -260,8 +260,11 @@ class HttpShard:
         sched = self.sched
         q = sched.queue
         self.last_reset_s = 0.0
+        hook = getattr(self, "phase_hook", None)   # profilers: hook("reset" | "burst", started)
         if self._bursts:
             tr = time.perf_counter()
+            if hook:
+                hook("reset", True)
             await self._call("POST", "/debug/bench/reset")
             self.last_reset_post_s = time.perf_counter() - tr
             trace = [] if os.environ.get("YODA_BENCH_RUNLOG") else None
@@ -317,6 +320,8 @@ class HttpShard:
             if os.environ.get("YODA_BENCH_LOOPDEBUG"):
                 asyncio.get_event_loop().set_debug(False)
             self.last_reset_s = time.perf_counter() - tr
+            if hook:
+                hook("reset", False)
         self._bursts += 1
         sched.take_lane_samples()
         sched.e2e_samples.clear()
