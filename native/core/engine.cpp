@@ -1242,8 +1242,8 @@ bool Engine::select_gpus(const PodReq& req, int32_t idx, std::vector<int32_t>* o
   uint64_t m = req.has_memory ? req.memory : 0;
   uint64_t cl = req.has_clock ? req.clock : 0;
   if (k == 0) return true;
-  std::vector<int32_t> E;
-  E.reserve(n.cards.size());             // one allocation, not a growth chain per pod
+  thread_local std::vector<int32_t> E;   // reused: no allocation per node per pod
+  E.clear();
   out->reserve(k);
   for (int32_t i = 0; i < (int32_t)n.cards.size(); ++i) {
     const Card& c = n.cards[i];
