@@ -363,6 +363,7 @@ PYBIND11_MODULE(_yoda_kube, m) {
         d["parse_errors"] = s.parse_errors;
         d["watch_cpu_s"] = s.watch_cpu_s;
         d["slab_deletions"] = s.slab_deletions;
+        d["recycled"] = s.recycled;
         d["sink_sent"] = s.sink_sent;
         d["sink_answered"] = s.sink_answered;
         d["sink_queue_s"] = s.sink_queue_s;

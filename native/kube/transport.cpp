@@ -1059,6 +1059,10 @@ void Transport::run() {
         std::lock_guard<std::mutex> g(recycle_mu_);
         dead.swap(recycle_);
       }
+      if (!dead.empty()) {
+        std::lock_guard<std::mutex> g(stats_mu_);
+        stats_.recycled += dead.size();
+      }
     }
     bool woke = false;
     for (int i = 0; i < n; ++i) {

@@ -61,7 +61,8 @@ struct TransportStats {
   uint64_t requests = 0, responses = 0, errors = 0, timeouts = 0, connects = 0;
   uint64_t watch_events = 0, watch_bytes = 0, parse_errors = 0, bytes_out = 0, bytes_in = 0;
   uint64_t throttled = 0;
-  uint64_t slab_deletions = 0;   // deletions left in their read buffer (PodEv::slab), not copied
+  uint64_t slab_deletions = 0;
+  uint64_t recycled = 0;         // pod events a sink handed back, freed on this (I/O) thread   // deletions left in their read buffer (PodEv::slab), not copied
   double watch_cpu_s = 0;     // I/O thread time decoding watch lines (parse + projection; monotonic clock, the decoder does not block)
   // lane Bindings: hand-off → written to a connection (queue), written → answer read (rtt)
   uint64_t sink_sent = 0, sink_answered = 0;

@@ -139,6 +139,9 @@ def test_lane_burst_confirms_echoes_and_releases_on_delete():
             assert await e.wait(lambda: e.sched.engine.ledger_size == 0 and lane.stats()["owned"] == 0)
             assert sum(g["reserved"] for g in e.sched.cache.node_gpu_state("n1")) == 0
             assert e.sched.lane.forwarded == 0 and not e.sched.cache.pods
+            # the events the lane dropped went back to the I/O thread to be freed there
+            # (PodPort::recycle): at least one per creation, echo and deletion it handled
+            assert await e.wait(lambda: e.cl.native.stats()["recycled"] >= 3 * 60)
     run(go())
 
 
