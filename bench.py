@@ -518,6 +518,13 @@ def main(argv=None) -> int:
             **({"apiserver_loop_us_per_pod": {k: round((v[0] - ap0.get(k, [0, 0])[0]) / my_bound * 1e6, 2)
                                               for k, v in ap1.items() if v[0] > ap0.get(k, [0, 0])[0]}}
                if ap1 and my_bound else {}),
+            # share of the bursts' wall time (resets excluded) the single-threaded fake apiserver's
+            # loop was busy with burst work (everything but the resets' deletions): near 1.0, the
+            # harness — not the scheduler — bounds pods/s (rank 0)
+            **({"apiserver_busy_share_of_bursts": round(
+                sum(v[0] - ap0.get(k, [0, 0])[0] for k, v in ap1.items() if k != "job_delete")
+                / max(1e-9, elapsed - sum(reset_s)), 3)}
+               if ap1 and transport == "http" and world == 1 else {}),
             "pods_bound": bound,
             "pods_unschedulable": unsched,
             "device_cycles": device_cycles,
