@@ -42,16 +42,15 @@ ARCH = os.environ.get("YODA_HIP_ARCH", "gfx950")
 
 # Per artefact: output name, the sources compiled, every file whose contents define the
 # artefact (sources + headers), and a recipe tag (bump it when the compile flags change).
-CORE_SRCS = ["core/engine.cpp", "core/lane.cpp", "core/bindings.cpp", "core/sampler.cpp", "common/fastalloc.cpp"]
+CORE_SRCS = ["core/engine.cpp", "core/lane.cpp", "core/bindings.cpp", "core/sampler.cpp"]
 KUBE_COMMON = ["kube/json.cpp", "kube/flatjson.cpp", "kube/project.cpp"]
 ARTEFACTS: dict[str, dict] = {
     "core": {"out": f"_yoda_core{EXT}", "srcs": CORE_SRCS,
              "deps": CORE_SRCS + ["core/engine.hpp", "core/lane.hpp", "hip/yoda_dev_abi.h", "kube/project.hpp",
                                   "kube/json.hpp", "kube/flatjson.hpp", "kube/lane_port.hpp", "common/build_id.h"],
              "recipe": "g++ -O3 -std=c++17 -fPIC -shared -fvisibility=hidden v2"},
-    "kube": {"out": f"_yoda_kube{EXT}", "srcs": KUBE_COMMON + ["kube/transport.cpp", "kube/bindings.cpp",
-                                                                "common/fastalloc.cpp"],
-             "deps": KUBE_COMMON + ["kube/transport.cpp", "kube/bindings.cpp", "common/fastalloc.cpp", "kube/json.hpp", "kube/http.hpp",
+    "kube": {"out": f"_yoda_kube{EXT}", "srcs": KUBE_COMMON + ["kube/transport.cpp", "kube/bindings.cpp"],
+             "deps": KUBE_COMMON + ["kube/transport.cpp", "kube/bindings.cpp", "kube/json.hpp", "kube/http.hpp",
                                     "kube/project.hpp", "kube/flatjson.hpp", "kube/transport.hpp", "kube/lane_port.hpp",
                                     "common/build_id.h"],
              "recipe": "g++ -O3 -std=c++17 -fPIC -shared -fvisibility=hidden -lssl -lcrypto v2"},
@@ -152,7 +151,7 @@ def build_core(force: bool = False) -> Path:
         _run([cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-Wall",
               "-Wno-unused-function", _bid_flag(bid), *_pybind_includes(), f"-I{NATIVE / 'core'}",
               f"-I{NATIVE / 'hip'}", f"-I{NATIVE / 'kube'}", f"-I{NATIVE / 'common'}", *_srcs("core"),
-              "-o", str(out), "-lpthread", "-ldl", "-lrt", "-Wl,-Bsymbolic-functions"], "core")
+              "-o", str(out), "-lpthread", "-ldl", "-lrt"], "core")
         _record("core", bid)
     return out
 
@@ -166,8 +165,7 @@ def build_kube(force: bool = False) -> list[Path]:
     if force or _stale("kube"):
         bid = source_hash("kube")
         _run([os.environ.get("CXX", "g++"), *flags, _bid_flag(bid), "-fPIC", "-shared", "-fvisibility=hidden",
-              *_pybind_includes(), *_srcs("kube"), "-o", str(mod), "-lssl", "-lcrypto", "-lpthread",
-              "-Wl,-Bsymbolic-functions"],
+              *_pybind_includes(), *_srcs("kube"), "-o", str(mod), "-lssl", "-lcrypto", "-lpthread"],
              "kube transport")
         _record("kube", bid)
     outs.append(mod)
