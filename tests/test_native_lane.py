@@ -454,8 +454,11 @@ def test_finish_cycle_refuses_a_result_whose_node_slot_was_reused():
         assert s.engine.node_index("new") == res[0]           # the slot was reused
         fw = next(iter(s.frameworks.values()))
         s._finish_cycle(fw, CycleState(), pi, res, s.queue.scheduling_cycle, time.perf_counter())
+        # requeued by the cycle itself (read now: on a loaded host the scheduling loop may pop it
+        # again during the sleep below)
+        queued_now = s.queue.contains(pi.uid)
         await asyncio.sleep(0.05)
-        out = (s.pending_binds, pi.uid in s.cache.pods, s.queue.contains(pi.uid), s.engine.has_pod(pi.num_id))
+        out = (s.pending_binds, pi.uid in s.cache.pods, queued_now, s.engine.has_pod(pi.num_id))
         await c.stop()
         return out
     pending, cached, queued, reserved = run(go())
