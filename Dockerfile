@@ -10,4 +10,6 @@ COPY native ./native
 RUN pip3 install --no-cache-dir pyyaml aiohttp prometheus_client pybind11 \
  && python3 -m yoda_scheduler_amd.ops.build \
  && pip3 install --no-cache-dir --no-deps .
+# glibc malloc tcache for the scheduler's native threads (deploy/yoda-scheduler.yaml sets it too)
+ENV GLIBC_TUNABLES=glibc.malloc.tcache_count=2048
 CMD ["yoda-scheduler"]

@@ -569,6 +569,8 @@ def main(argv=None) -> int:
                              "reference run; with --reference-qps this scheduler is bound the same way (~55 pods/s)",
             "telemetry": tels[0],
             "host": dict(host_info(), pinned_cpus=pinned),
+            # the scheduler process's glibc malloc tunables (see _with_scheduler_malloc)
+            "malloc": os.environ.get("GLIBC_TUNABLES") or "glibc defaults",
         }
         if a.mix_preempt:
             # the preemptors' PostFilter (DefaultPreemption) over every step, warmup included: calls,
@@ -589,5 +591,27 @@ def main(argv=None) -> int:
     return 0
 
 
+# The scheduler's glibc malloc setting (deploy/yoda-scheduler.yaml sets the same env on the
+# scheduler container): a 2048-entry tcache per size class instead of 7. The native threads
+# hand pod events and Bindings to each other, and with 7 entries nearly every hand-off fell
+# into the malloc arena (profiles/bench/r6/tcache_ab/: config 3 +5.6 % pods/s, p99 1.01 ->
+# 0.67 ms). Tunables are read at process start, so the bench re-executes itself once with it,
+# before anything has touched the GPU. The fake apiserver child keeps the environment the
+# bench was started with (harness.py). YODA_BENCH_MALLOC=default keeps glibc's defaults.
+MALLOC_TUNABLES = "glibc.malloc.tcache_count=2048"
+
+
+def _with_scheduler_malloc() -> None:
+    if os.environ.get("YODA_BENCH_MALLOC") == "default" or "GLIBC_TUNABLES" in os.environ:
+        return
+    os.environ["YODA_BENCH_ORIG_GLIBC_TUNABLES"] = ""          # unset before: the child gets none
+    os.environ["GLIBC_TUNABLES"] = MALLOC_TUNABLES
+    try:
+        os.execv(sys.executable, list(getattr(sys, "orig_argv", None) or [sys.executable, *sys.argv]))
+    except OSError:
+        os.environ.pop("GLIBC_TUNABLES", None)                  # carry on with the defaults
+
+
 if __name__ == "__main__":
+    _with_scheduler_malloc()
     sys.exit(main())

@@ -189,6 +189,12 @@ class HttpShard:
                 raise RuntimeError(f"{exe} is not built (python -m yoda_scheduler_amd.ops.build)")
             cmd = [exe, "--port", "0", "--port-file", self.port_file]
             env = None
+            if "YODA_BENCH_ORIG_GLIBC_TUNABLES" in os.environ:
+                # bench.py set the scheduler's malloc tunable for its own process: the fake
+                # apiserver (the test double of kube-apiserver) runs as it was started
+                env = {k: v for k, v in os.environ.items() if k != "GLIBC_TUNABLES"}
+                if os.environ["YODA_BENCH_ORIG_GLIBC_TUNABLES"]:
+                    env["GLIBC_TUNABLES"] = os.environ["YODA_BENCH_ORIG_GLIBC_TUNABLES"]
         else:
             cmd = [sys.executable, "-m", "yoda_scheduler_amd.cmd.fakeapi", "--port", "0", "--bench-config",
                    str(w.id), "--seed", str(seed), "--port-file", self.port_file]
