@@ -63,6 +63,13 @@ class FakePort : public yk::PodPort {
     events.push_back({tag, sink});
     cv.notify_one();
   }
+  // as the transport: the events the lane is done with are dropped on the I/O thread
+  void recycle(std::vector<std::shared_ptr<yk::PodEv>>&& d) override {
+    std::lock_guard<std::mutex> g(mu);
+    for (auto& x : d) dead.push_back(std::move(x));
+    d.clear();
+  }
+  std::vector<std::shared_ptr<yk::PodEv>> dead;
   struct B {
     uint64_t tag;
     yk::PodSink* sink;
@@ -134,6 +141,7 @@ int run_mode(int bursts, int per, int batch, int async_mode, int spin_us) {
         if (stop.load() && port.q.empty()) return;
         q.swap(port.q);
         evs.swap(port.events);
+        port.dead.clear();                 // freed here, off the lane thread
       }
       std::vector<yk::PodSink::Answer> ans;
       for (auto& x : evs) ans.push_back({x.first, 201, std::string()});
