@@ -516,6 +516,21 @@ def test_bench_http_transport_contract():
     d = json.loads(line)
     assert d["transport"] == "http" and d["pods_bound"] == 200 and d["pods_unschedulable"] == 0
     assert d["value"] > 0 and d["p99_latency_ms"] > 0 and d["e2e_scheduling_p99_ms"] is not None
+    # the harness's own bound is reported, and the scheduler process ran with its malloc
+    # tunable (bench.py re-executed itself; the environment here did not set one)
+    assert 0.0 < d["apiserver_busy_share_of_bursts"] <= 1.5
+    if "GLIBC_TUNABLES" not in os.environ:
+        assert d["malloc"] == "glibc.malloc.tcache_count=2048"
+
+
+def test_bench_malloc_opt_out_keeps_glibc_defaults():
+    env = dict(os.environ, PYTHONPATH=ROOT, YODA_BENCH_MALLOC="default")
+    env.pop("GLIBC_TUNABLES", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "1", "--steps", "1",
+                        "--warmup", "0", "--alt", "none"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["malloc"] == "glibc defaults"
 
 
 def test_fastbind_pipelining_errors_chunked_and_reconnect():

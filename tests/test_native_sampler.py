@@ -43,3 +43,22 @@ def test_sampler_samples_a_named_busy_thread_and_symbolises_it():
     finally:
         stop.set()
         th.join()
+
+
+def test_load_dump_symbolises_another_process_samples(tmp_path):
+    """The fake apiserver writes its samples with yoda_sampler::dump (pc, tid|overrun<<24,
+    callers; plus its maps); load_dump reads them back for report()."""
+    from yoda_scheduler_amd.utils.native_prof import load_dump
+    import ctypes
+    # a PC inside this process's libc (its maps double as the other process's)
+    pc = ctypes.cast(ctypes.CDLL(None).malloc, ctypes.c_void_p).value
+    dump = tmp_path / "apiserver.samples"
+    dump.write_text(f"# dropped 3\n{pc:x} {(2 << 24) | 4242:x}\n{pc + 1:x} {4242:x} {pc:x}\n")
+    with open("/proc/self/maps") as f:
+        (tmp_path / "apiserver.samples.maps").write_text(f.read())
+    s = load_dump(str(dump), period_us=1000)
+    assert s.dropped == 3 and len(s.samples) == 2 and s.stacks
+    rows = s.symbolise()
+    assert [w for _, w, _ in rows] == [3, 1]
+    assert all(t == "apiserver" and syms[0][0].startswith("libc") for t, _, syms in rows)
+    assert "[apiserver] 4 periods" in s.report()
