@@ -601,9 +601,31 @@ def main(argv=None) -> int:
 MALLOC_TUNABLES = "glibc.malloc.tcache_count=2048"
 
 
+def _gpu_touched() -> bool:
+    """Whether anything in this process may already have initialised the GPU: an open KFD or
+    DRM render node (a profiler's preloaded library initialises the runtime before the program
+    starts), or a profiler / HSA tool in the environment. Then the bench never re-executes."""
+    if any(k.startswith(("ROCPROF", "ROCP_", "HSA_TOOLS")) for k in os.environ) or \
+            "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        return True
+    try:
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                t = os.readlink(f"/proc/self/fd/{fd}")
+            except OSError:
+                continue
+            if t == "/dev/kfd" or t.startswith("/dev/dri/"):
+                return True
+    except OSError:
+        return True
+    return False
+
+
 def _with_scheduler_malloc() -> None:
     if os.environ.get("YODA_BENCH_MALLOC") == "default" or "GLIBC_TUNABLES" in os.environ:
         return
+    if _gpu_touched():
+        return                                                  # no exec once the GPU may be up
     os.environ["YODA_BENCH_ORIG_GLIBC_TUNABLES"] = ""          # unset before: the child gets none
     os.environ["GLIBC_TUNABLES"] = MALLOC_TUNABLES
     try:
